@@ -1,0 +1,202 @@
+"""Weight sets for the PreGAN+ decision model (host side).
+
+Two sources, both yielding the reference's own parameter names and shapes
+(``recovery/PreGANSrc/src/models.py:314-416`` Transformer_16, ``:118-151``
+Gen_16/Disc_16, ``:258-291`` Gen_50/Disc_50; checkpoint dict format
+``recovery/PreGANSrc/src/utils.py:53-58``):
+
+* :func:`load_reference_checkpoints` reads the shipped ``.ckpt`` files with
+  ``torch.load(weights_only=True)`` (no code from the file runs);
+* :func:`synth_weights` builds seeded random weights of the H-generic
+  architecture (H=50 has no shipped checkpoint).  numpy's PCG64
+  stream is platform-independent, so the same seed gives bit-identical weights
+  on the build container and on the GPU box (the golden fixtures rely on it).
+
+The packed blob handed to the C-ABI (``pgp_load_weights``) is the
+concatenation, in :func:`blob_layout` order, of these arrays as float64.
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+
+PROTO_DIM = 2
+
+
+def transformer_shapes(H, W=3, ff=64, layers=2, feats=3):
+    d = H
+    shp = {
+        "gat.layer1.heads.0.fc.weight": (d, feats),
+        "gat.layer1.heads.0.attn_fc.weight": (1, 2 * d),
+        "time_encoder.weight": (d, d),
+        "time_encoder.bias": (d,),
+        "pos_encoder.pe": (W, 1, d),
+    }
+    for li in range(layers):
+        p = f"transformer_encoder.layers.{li}."
+        shp.update({
+            p + "self_attn.in_proj_weight": (3 * d, d),
+            p + "self_attn.in_proj_bias": (3 * d,),
+            p + "self_attn.out_proj.weight": (d, d),
+            p + "self_attn.out_proj.bias": (d,),
+            p + "linear1.weight": (ff, d),
+            p + "linear1.bias": (ff,),
+            p + "linear2.weight": (d, ff),
+            p + "linear2.bias": (d,),
+            p + "norm1.weight": (d,),
+            p + "norm1.bias": (d,),
+            p + "norm2.weight": (d,),
+            p + "norm2.bias": (d,),
+        })
+    lat = H * d * W
+    shp.update({
+        "anomaly_decoder.0.weight": (2 * H, lat),
+        "anomaly_decoder.0.bias": (2 * H,),
+        "prototype_decoder.0.weight": (PROTO_DIM * H, lat),
+        "prototype_decoder.0.bias": (PROTO_DIM * H,),
+    })
+    return shp
+
+
+def gen_shapes(H, hidden=64):
+    n = H * PROTO_DIM + H * H
+    return {"delta.0.weight": (hidden, n), "delta.0.bias": (hidden,),
+            "delta.2.weight": (H * H, hidden), "delta.2.bias": (H * H,)}
+
+
+def disc_shapes(H, hidden=64):
+    n = 2 * H * H
+    return {"probs.0.weight": (hidden, n), "probs.0.bias": (hidden,),
+            "probs.2.weight": (2, hidden), "probs.2.bias": (2,)}
+
+
+def blob_layout(H, n_protos=None):
+    """Ordered (section, name, shape) list of the C-ABI weight blob."""
+    K = H if n_protos is None else n_protos
+    out = [("transformer", k, s) for k, s in transformer_shapes(H).items()]
+    out += [("gen", k, s) for k, s in gen_shapes(H).items()]
+    out += [("disc", k, s) for k, s in disc_shapes(H).items()]
+    out += [("prototypes", "prototypes", (K, PROTO_DIM))]
+    return out
+
+
+def pack_blob(weights, H):
+    """Concatenate a weight set into the float64 blob of ``pgp_load_weights``."""
+    K = np.asarray(weights["prototypes"]).shape[0]
+    parts = []
+    for sec, name, shp in blob_layout(H, K):
+        a = np.asarray(weights[sec] if sec == "prototypes" else weights[sec][name],
+                       dtype=np.float64)
+        if a.shape != tuple(shp):
+            raise ValueError(f"{sec}/{name}: shape {a.shape} != {shp}")
+        parts.append(a.reshape(-1))
+    return np.ascontiguousarray(np.concatenate(parts))
+
+
+def blob_size(H, n_protos=None):
+    return sum(int(np.prod(s)) for _, _, s in blob_layout(H, n_protos))
+
+
+def positional_encoding(d_model, max_len=3):
+    """``models.py:297-307`` buffer, computed in fp32 as the reference does."""
+    position = np.arange(0, max_len, dtype=np.float32)[:, None]
+    div = np.exp(np.arange(0, d_model, 2, dtype=np.float32)
+                 * np.float32(-np.log(10000.0) / d_model)).astype(np.float32)
+    pe = np.zeros((max_len, d_model), dtype=np.float32)
+    pe[:, 0::2] = np.sin(position * div)
+    pe[:, 1::2] = np.cos(position * div)
+    return pe.astype(np.float64)[:, None, :]
+
+
+def synth_weights(H, seed=0):
+    """Seeded weights for the H-generic model (uniform +-1/sqrt(fan_in), like
+    torch's Linear default; LayerNorm gamma around 1; prototypes U(0,1) as
+    ``models.py:373-374``).  Values are rounded to fp32-representable doubles so
+    an fp32 kernel and an fp64 reference start from the same numbers."""
+    if H % 2:
+        raise ValueError("H must be even (d_model = H is split over 2 heads)")
+    rng = np.random.Generator(np.random.PCG64(seed))
+
+    def fill(shapes, sec):
+        out = {}
+        for name, shp in shapes.items():
+            if name == "pos_encoder.pe":
+                out[name] = positional_encoding(H, shp[0])
+                continue
+            if name.endswith("norm1.weight") or name.endswith("norm2.weight"):
+                a = 1.0 + 0.1 * rng.uniform(-1, 1, size=shp)
+            elif name.endswith("norm1.bias") or name.endswith("norm2.bias"):
+                a = 0.1 * rng.uniform(-1, 1, size=shp)
+            else:
+                fan_in = shp[1] if len(shp) == 2 else shapes[name.replace("bias", "weight")][1]
+                bound = 1.0 / np.sqrt(fan_in)
+                a = rng.uniform(-bound, bound, size=shp)
+            out[name] = a.astype(np.float32).astype(np.float64)
+        return out
+
+    w = {
+        "transformer": fill(transformer_shapes(H), "t"),
+        "gen": fill(gen_shapes(H), "g"),
+        "disc": fill(disc_shapes(H), "d"),
+    }
+    w["prototypes"] = rng.uniform(0, 1, size=(H, PROTO_DIM)).astype(np.float32).astype(np.float64)
+    return w
+
+
+def weights_checksum(weights):
+    h = 0.0
+    for sec in ("transformer", "gen", "disc"):
+        for k in sorted(weights[sec]):
+            a = np.asarray(weights[sec][k], dtype=np.float64).reshape(-1)
+            h += float(np.dot(a, np.cos(np.arange(a.size) * 0.001)))
+    return h + float(np.asarray(weights["prototypes"]).sum())
+
+
+def load_reference_checkpoints(model_dir, env_name="simulator", H=16):
+    """Read ``{env}_Transformer_{H}.ckpt``/``Gen``/``Disc`` from a COSCO tree
+    (``checkpointsplus/``; format ``utils.py:53-58``) with the safe loader."""
+    import torch
+    sg = [(np._core.multiarray.scalar, "numpy.core.multiarray.scalar"), np.dtype,
+          np.dtypes.Float64DType]
+
+    def ld(name):
+        with torch.serialization.safe_globals(sg):
+            return torch.load(os.path.join(model_dir, f"{env_name}_{name}_{H}.ckpt"),
+                              weights_only=True)
+
+    t, g, d = ld("Transformer"), ld("Gen"), ld("Disc")
+    conv = lambda sd: {k: v.detach().cpu().numpy().astype(np.float64) for k, v in sd.items()}
+    return {
+        "transformer": conv(t["model_state_dict"]),
+        "gen": conv(g["model_state_dict"]),
+        "disc": conv(d["model_state_dict"]),
+        "prototypes": np.stack([p.detach().cpu().numpy() for p in t["model_prototypes"]]),
+        "meta": {"epoch": t["epoch"], "gan_epoch": g["epoch"]},
+    }
+
+
+def save_npz(path, weights, extra=None):
+    flat = {}
+    for sec in ("transformer", "gen", "disc"):
+        for k, v in weights[sec].items():
+            flat[f"{sec}/{k}"] = np.asarray(v, dtype=np.float64)
+    flat["prototypes"] = np.asarray(weights["prototypes"], dtype=np.float64)
+    for k, v in (extra or {}).items():
+        flat[k] = v
+    np.savez_compressed(path, **flat)
+
+
+def load_npz(path):
+    z = np.load(path, allow_pickle=False)
+    w = {"transformer": {}, "gen": {}, "disc": {}}
+    extra = {}
+    for k in z.files:
+        if "/" in k:
+            sec, name = k.split("/", 1)
+            w[sec][name] = z[k]
+        elif k == "prototypes":
+            w["prototypes"] = z[k]
+        else:
+            extra[k] = z[k]
+    return w, extra

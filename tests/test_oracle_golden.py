@@ -1,0 +1,76 @@
+"""Pin the numpy oracle against fixtures produced by the reference itself
+(tests/golden/make_golden.py: reference modules, eval mode, fp64)."""
+import numpy as np
+import pytest
+
+from oracle import pregan_oracle as O
+from preganplus_amd import weights as W
+
+GOLD = "tests/golden"
+
+
+def _weights(H, z):
+    if H == 16:
+        w, _ = W.load_npz("preganplus_amd/data/simulator_16.npz")
+    else:
+        w = W.synth_weights(H, int(z["weights_seed"]))
+        assert W.weights_checksum(w) == float(z["weights_checksum"])
+    return w
+
+
+@pytest.mark.parametrize("H", [16, 50])
+def test_oracle_fp64_matches_reference(H):
+    z = np.load(f"{GOLD}/fwd_h{H}.npz")
+    w = _weights(H, z)
+    out = O.forward(w, z["windows"], z["sched"])
+    n = z["latent"].shape[0]
+    np.testing.assert_allclose(out["latent"][:n], z["latent"], rtol=0, atol=1e-12)
+    for k in ["logits", "protos", "emb", "new_sched", "probs"]:
+        np.testing.assert_allclose(out[k], z[k], rtol=0, atol=1e-12, err_msg=k)
+    for k in ["cls", "any", "keep", "final_target", "gen_target"]:
+        np.testing.assert_array_equal(out[k], z[k], err_msg=k)
+
+
+@pytest.mark.parametrize("H", [16, 50])
+def test_oracle_fp32_within_north_star_tolerance(H):
+    """fp32 restatement vs the fp64 reference: logits within rtol 1e-4 (+ a small
+    atol for logits near 0) and identical decisions on these fixtures."""
+    z = np.load(f"{GOLD}/fwd_h{H}.npz")
+    w = _weights(H, z)
+    out = O.forward(w, z["windows"], z["sched"], dtype=np.float32)
+    np.testing.assert_allclose(out["logits"], z["logits"], rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(out["protos"], z["protos"], rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(out["probs"], z["probs"], rtol=1e-4, atol=1e-6)
+    for k in ["cls", "any", "keep", "final_target", "gen_target"]:
+        np.testing.assert_array_equal(out[k], z[k], err_msg=k)
+
+
+def test_inference_window_drops_newest_row():
+    """PreGANPlus.py:107-112: window = rows [t-2, t-2, t-1] of the normalised series."""
+    ts = np.arange(5 * 6, dtype=np.float64).reshape(5, 6) + 1.0
+    train = np.ones((3, 6)) * 100.0
+    win = O.inference_window(ts, train)
+    norm = ts / (100.0 + 1e-8)
+    np.testing.assert_allclose(win, np.stack([norm[2], norm[2], norm[3]]))
+
+
+def test_real_fixture_windows_follow_run_encoder():
+    z = np.load(f"{GOLD}/fwd_h16.npz")
+    _, extra = W.load_npz("preganplus_amd/data/simulator_16.npz")
+    series = extra["train_time_data"]
+    for i in (0, 10, 198):
+        tt = i + 3
+        np.testing.assert_allclose(z["windows"][i], O.inference_window(series[:tt], series),
+                                   rtol=0, atol=0)
+
+
+def test_ties_break_to_first_index():
+    logits = np.array([[[1.0, 1.0], [0.0, 2.0]]])
+    protos = np.array([[[0.5, 0.5], [0.25, 0.75]]])
+    P = np.array([[0.25, 0.75], [0.25, 0.75], [0.0, 0.0]])
+    anom, emb, cls, anyb = O.classify(logits, protos, P)
+    assert anom.tolist() == [[False, True]]
+    assert cls.tolist() == [[-1, 0]]
+    assert anyb.tolist() == [True]
+    s = np.array([[[0.5, 0.5, 0.1]]])
+    assert O.first_argmax_rows(s).tolist() == [[0]]
