@@ -1,0 +1,190 @@
+"""Benchmark of the PreGAN+ decision path (BASELINE.json config 2).
+
+One step = detect + diagnose + generate over one batch of synthetic windows
+already resident in HBM: K1 GAT aggregation -> K2 encoder+decoders+classify ->
+K3 Gen+Disc+decisions (libpreganplus.so).  Multi-GPU: one process per GPU
+(torchrun); every rank processes its own batch of independent windows (weak
+scaling, no data-path collective); timing is max over ranks.
+
+Prints ONE JSON line (rank 0).  The roofline object is for the dominant kernel
+(K2, fp32 MFMA-bound); its kernel time is measured live with HIP events on the
+stream the kernels run on.  cpu_baseline times the numpy oracle (a CPU port of
+the reference math) on a bounded sample, rank 0 at N=1 only.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from preganplus_amd import roofline as R  # noqa: E402
+from preganplus_amd import weights as W  # noqa: E402
+from preganplus_amd.model import DecisionModel  # noqa: E402
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def synth_inputs(B, H, device, seed):
+    """load U(0,0.6), 2% spikes U(0.9,1.3); one-hot schedule."""
+    g = torch.Generator(device=device).manual_seed(seed)
+    x = torch.rand((B, 3, 3 * H), generator=g, device=device) * 0.6
+    spike = torch.rand((B, 3, 3 * H), generator=g, device=device) < 0.02
+    x = torch.where(spike, 0.9 + 0.4 * torch.rand((B, 3, 3 * H), generator=g, device=device), x)
+    idx = torch.randint(0, H, (B, H), generator=g, device=device)
+    s = torch.zeros((B, H, H), device=device)
+    s.scatter_(2, idx.unsqueeze(-1), 1.0)
+    return x.contiguous(), s.contiguous()
+
+
+def cpu_baseline(H, weights, budget_s=12.0, max_threads=16):
+    """numpy fp64 oracle (batched restatement of the reference math) on the
+    host cores, on a bounded sample of the same synthetic workload."""
+    from threadpoolctl import threadpool_limits
+    from oracle import pregan_oracle as O  # CPU baseline leg only
+    threads = min(max_threads, os.cpu_count() or 1)
+    rng = np.random.Generator(np.random.PCG64(99))
+    nb = 64
+    x = rng.uniform(0, 0.6, size=(nb, 3, 3 * H))
+    s = np.zeros((nb, H, H))
+    s[np.arange(nb)[:, None], np.arange(H)[None, :], rng.integers(0, H, size=(nb, H))] = 1.0
+    done, t0 = 0, time.perf_counter()
+    with threadpool_limits(limits=threads):
+        O.forward(weights, x[:8], s[:8])  # warm-up
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < budget_s:
+            O.forward(weights, x, s)
+            done += nb
+    dt = time.perf_counter() - t0
+    return {"value": done * H / dt, "unit": "host-windows/s", "cores": threads, "kind": "port",
+            "sample": f"{done} windows (H={H}, batches of {nb}), numpy fp64 oracle, {dt:.1f}s"}
+
+
+def load_traffic(H, B):
+    p = os.path.join(ROOT, "profiles", f"pmc_encdec_h{H}.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        d = json.load(open(p))
+        if int(d.get("batch", -1)) != B:
+            return None
+        return d.get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--hosts", type=int, default=50)
+    ap.add_argument("--batch", type=int, default=65536, help="windows per GPU per step")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+    H, B = args.hosts, args.batch
+
+    weights = W.synth_weights(H, seed=0)
+    model = DecisionModel(H, weights, device=device)
+    model.reserve(B)
+    x, s = synth_inputs(B, H, device, 1234 + rank)
+    out = model.alloc_outputs(B)
+    torch.cuda.synchronize()
+
+    def step(evs=None):
+        if evs is None:
+            model.forward(x, s, out=out, stage=-1)
+            return
+        evs[0].record()
+        model.forward(x, s, out=out, stage=0)
+        evs[1].record()
+        model.forward(x, s, out=out, stage=1)
+        evs[2].record()
+        model.forward(x, s, out=out, stage=2)
+        evs[3].record()
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(evs[i])
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    t1 = time.perf_counter()
+    el = torch.tensor([t1 - t0], dtype=torch.float64, device=device)
+    if world > 1:
+        torch.distributed.all_reduce(el, op=torch.distributed.ReduceOp.MAX)
+    elapsed = float(el.item())
+    k_ms = np.array([[e[k].elapsed_time(e[k + 1]) for k in range(3)] for e in evs])  # [steps, 3]
+    k_mean = k_ms.mean(axis=0)
+
+    if rank == 0:
+        ms = elapsed / args.steps * 1e3
+        hw = B * world * H * args.steps / elapsed
+        k2_flops = R.encdec_flops_per_window(H) * B
+        achieved = k2_flops / (k_mean[1] * 1e-3) / 1e12
+        traffic = load_traffic(H, B)
+        res = {
+            "metric": "host-windows/sec (detect+diagnose+generate)",
+            "value": hw,
+            "unit": "host-windows/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic (SURVEY §8d C2 distribution; seeded random-init weights of the H=50 architecture)",
+            "config": {"workload": f"C2: PreGAN+ batched inference, {H} hosts x W=3 x 3 resources, "
+                                   f"{B} windows per GPU, fp32",
+                       "hosts": H, "windows_per_gpu": B, "parallelism": f"dp{world} (independent windows)"},
+            "kernel_ms": {"gat_agg": k_mean[0], "encdec": k_mean[1], "gan": k_mean[2]},
+            "roofline": {"kernel": "encdec_kernel (K2)", "bound": "mfma", "achieved": achieved,
+                         "peak": R.PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+                         "frac": achieved / R.PEAK_FP32_TFLOPS, "traffic": traffic,
+                         "flops_per_window": R.encdec_flops_per_window(H)},
+            "path_roofline": {
+                "flops_per_window": R.total_flops_per_window(H),
+                "achieved_tflops": R.total_flops_per_window(H) * B * world * args.steps / elapsed / 1e12,
+                "hbm_algorithmic_gbs": R.path_bytes_per_window(H) * B * world * args.steps / elapsed / 1e9,
+                "hbm_frac": R.path_bytes_per_window(H) * B * world * args.steps / elapsed / 1e9 / R.PEAK_HBM_GBS,
+            },
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            log("timing CPU baseline ...")
+            res["cpu_baseline"] = cpu_baseline(H, weights, args.cpu_budget)
+        else:
+            res["cpu_baseline"] = None
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

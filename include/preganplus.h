@@ -1,0 +1,125 @@
+/*
+ * preganplus.h — C-ABI of the MI355X-native PreGAN+ decision model.
+ *
+ * The drop-in boundary.  The reference's "FFI" for this path is Python calling
+ * torch modules; the binding a maintainer adds is a ctypes stub
+ * (INTEGRATION.md).  Plain pointers and sizes only: no torch types.
+ *
+ * Entry points and the reference interface each replaces (paths relative to
+ * the reference repo root):
+ *
+ *   pgp_create / pgp_load_weights
+ *       load_model / load_gan  recovery/PreGANSrc/src/utils.py:60-84
+ *       (model construction models.py:314-374, 118-151, 258-291; checkpoint
+ *        dict utils.py:53-58).  The blob is the reference's own tensors, fp64,
+ *       concatenated in the order documented at pgp_load_weights.
+ *   pgp_forward
+ *       one batched call of the per-window path of run_model
+ *       recovery/PreGANPlus.py:115-136 without its training side effects:
+ *         Transformer_16.forward       models.py:376-416  (logits, protos)
+ *         detect + embed               PreGANPlus.py:119-131 (any_anom, emb)
+ *         get_classes                  utils.py:102-109   (cls)
+ *         Gen_*.forward / Disc_*.forward models.py:131-151 (probs)
+ *         recover_decision gate+targets PreGANPlus.py:84-105
+ *             keep_orig    = probs[0] > probs[1]           (:87)
+ *             final_target = first-argmax(sched[c,:])      (:99)
+ *         generator proposal (GAN label input)  stats/Stats.py:162-166
+ *             gen_target   = first-argmax(new_sched[c,:])
+ *   pgp_destroy
+ *       (object lifetime; no reference counterpart)
+ *
+ * Conventions: every call returns 0 on success or a negative PGP_ERR_*;
+ * pgp_last_error() gives a message (thread-local).  Device pointers, fp32
+ * activations, int32 indices, row-major arrays; the stream is a hipStream_t
+ * passed as void* (NULL = default stream).  pgp_forward allocates nothing when
+ * batch <= the size passed to pgp_reserve (required before graph capture).
+ */
+#ifndef PREGANPLUS_H
+#define PREGANPLUS_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PGP_ABI_VERSION 1
+
+#define PGP_OK 0
+#define PGP_ERR_ARG (-1)         /* bad argument (null pointer, size, H) */
+#define PGP_ERR_UNSUPPORTED (-2) /* host count not compiled in */
+#define PGP_ERR_HIP (-3)         /* HIP runtime error */
+#define PGP_ERR_STATE (-4)       /* weights not loaded / workspace missing */
+
+typedef struct pgp_model pgp_model;
+
+int pgp_abi_version(void);
+const char* pgp_last_error(void);
+
+/* Host counts compiled into this library (H must be even: d_model = H is split
+ * over 2 heads, models.py:323-324).  Writes up to cap values; returns count. */
+int pgp_supported_hosts(int* out, int cap);
+
+/* A model for H hosts (= C containers, main.py:80) with K prototypes
+ * (K = H for PreGAN+, models.py:373-374). */
+int pgp_create(int n_hosts, int n_protos, pgp_model** out);
+int pgp_destroy(pgp_model* m);
+
+/* Number of doubles pgp_load_weights expects for (H, K). */
+size_t pgp_weight_blob_len(int n_hosts, int n_protos);
+
+/* Load the reference's tensors (host memory, fp64), concatenated row-major in
+ * this order (names as in the reference state_dicts):
+ *   Transformer: gat.layer1.heads.0.fc.weight [H,3], ...attn_fc.weight [1,2H],
+ *     time_encoder.weight [H,H], time_encoder.bias [H], pos_encoder.pe [3,1,H],
+ *     for layer l in 0,1: self_attn.in_proj_weight [3H,H], in_proj_bias [3H],
+ *       out_proj.weight [H,H], out_proj.bias [H], linear1.weight [64,H],
+ *       linear1.bias [64], linear2.weight [H,64], linear2.bias [H],
+ *       norm1.weight [H], norm1.bias [H], norm2.weight [H], norm2.bias [H],
+ *     anomaly_decoder.0.weight [2H,3H^2], .bias [2H],
+ *     prototype_decoder.0.weight [2H,3H^2], .bias [2H]
+ *   Gen: delta.0.weight [64,2H+H^2], delta.0.bias [64], delta.2.weight [H^2,64],
+ *     delta.2.bias [H^2]
+ *   Disc: probs.0.weight [64,2H^2], probs.0.bias [64], probs.2.weight [2,64],
+ *     probs.2.bias [2]
+ *   prototypes [K,2]   (model.prototype list, utils.py:70)
+ * Packs them (fp64 host arithmetic, then fp32) into the device layouts and
+ * uploads synchronously. */
+int pgp_load_weights(pgp_model* m, const double* blob, size_t len);
+
+/* Pre-allocate the device workspace for batches up to max_batch windows. */
+int pgp_reserve(pgp_model* m, int max_batch);
+
+/* detect + diagnose + generate for `batch` windows, all pointers on device:
+ *   in  windows      [B,3,3H] normalised rows (run_encoder's window,
+ *                    PreGANPlus.py:107-112; columns host-major cpu/ram/disk)
+ *   in  sched        [B,C,H]  schedule (GOBI result_cache, PreGANPlus.py:117)
+ *   out logits       [B,H,2]  anomaly decoder outputs (raw: LeakyReLU(True)=id)
+ *   out protos       [B,H,2]  sigmoid prototype embeddings
+ *   out cls          [B,H]    diagnosed class, -1 where no anomaly
+ *   out any_anom     [B]      1 if any host is anomalous (else run_model
+ *                             returns the original decision, :119-127)
+ *   out probs        [B,2]    discriminator softmax
+ *   out keep_orig    [B]      probs[0] > probs[1]
+ *   out final_target [B,C]    first-argmax of sched rows
+ *   out gen_target   [B,C]    first-argmax of the generator's rows
+ * latent (may be NULL) receives the encoder output [B,3H^2] in the reference's
+ * (host, step, channel) order (models.py:399) — a debug/test tap. */
+int pgp_forward(pgp_model* m, int batch, const float* windows, const float* sched,
+                float* logits, float* protos, int* cls, int* any_anom,
+                float* probs, int* keep_orig, int* final_target, int* gen_target,
+                float* latent, void* stream);
+
+/* Per-kernel launches of pgp_forward, for profiling and kernel-level tests.
+ * stage 0: GAT aggregation, 1: encoder+decoder+classify, 2: GAN+decide.
+ * Uses the workspace/outputs of the last pgp_forward-compatible arguments. */
+int pgp_forward_stage(pgp_model* m, int stage, int batch, const float* windows,
+                      const float* sched, float* logits, float* protos, int* cls,
+                      int* any_anom, float* probs, int* keep_orig, int* final_target,
+                      int* gen_target, float* latent, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PREGANPLUS_H */

@@ -1,0 +1,128 @@
+// pgp_layout.hpp — compile-time geometry of the PreGAN+ kernels for H hosts,
+// shared by the host-side packer (pgp_pack.cpp) and the gfx950 kernels.
+//
+// Execution layout: every kernel runs "windows on lanes".
+// One wave owns 16 windows.  Activations are kept as the accumulators of
+// v_mfma_f32_16x16x4_f32 with the TOKEN (window) on the lane column j = lane&15
+// and FEATURES on the rows: lane group g = lane>>4, register r hold row
+// 16*t + 4*g + r of tile t.  Such an accumulator register is directly the B
+// operand of the next GEMM's k-step (t, r): lane group g supplies k-row
+// 16t+4g+r.  Weights are the A operand, pre-packed into per-lane fragments.
+//
+// Row <-> feature maps (all chosen so padding sits in whole k-steps):
+//   d-space (X, residual stream), feature c:  X row (t,g,r)  <-> c = 16t+4r+g
+//     consumed as B: k-step s, group g  <-> c = 4s+g   (KS_D = ceil(H/4) steps)
+//   head space, HP >= 16 (per head block of HP rows): same formula with the
+//     head dim e in place of c; P8 mode (head dim <= 8, H <= 16): one tile holds
+//     both heads, row (g,r) <-> head g>>1, dim 4(g&1)+r.
+//   FFN hidden (64) and GAN hidden (64): natural rows u = 16t+4g+r.
+//   decoder outputs: row n = 4*host + q, q = {logit0, logit1, proto0, proto1}.
+#pragma once
+
+namespace pgp {
+
+constexpr int round_up(int x, int m) { return (x + m - 1) / m * m; }
+constexpr int cdiv(int x, int m) { return (x + m - 1) / m; }
+
+constexpr int kWindow = 3;     // models.py:320
+constexpr int kFeat = 3;       // models.py:321
+constexpr int kFF = 64;        // models.py:325
+constexpr int kLayers = 2;     // models.py:326
+constexpr int kGanHidden = 64; // models.py:124,142
+constexpr int kProtoDim = 2;   // constants.py:12
+constexpr int kFrag = 64;      // floats per MFMA A fragment (one per lane)
+
+template <int H>
+struct Geo {
+  static_assert(H % 2 == 0, "H must be even (2 heads)");
+  static constexpr int D = H;                 // d_model
+  static constexpr int DP = round_up(H, 16);  // padded d rows
+  static constexpr int MT_D = DP / 16;        // d-space M tiles
+  static constexpr int KS_D = cdiv(H, 4);     // k-steps over d-space
+  static constexpr int KQ_D = cdiv(KS_D, 4);  // float4 groups of k-steps
+  static constexpr int HD = H / 2;            // head dim
+  static constexpr bool P8 = HD <= 8;
+  static constexpr int HP = P8 ? 8 : round_up(HD, 16);
+  static constexpr int NPASS = P8 ? 1 : 2;    // attention passes (heads per pass: 2 or 1)
+  static constexpr int TP = P8 ? 1 : HP / 16; // tiles per Q/K/V per pass
+  static constexpr int KS_O = P8 ? 4 : cdiv(HD, 4);
+  static constexpr int KQ_O = cdiv(KS_O, 4);
+  static constexpr int MT_F = kFF / 16;       // 4
+  static constexpr int KQ_F = kFF / 16;       // 16 k-steps -> 4 groups
+  static constexpr int MT_O = cdiv(H, 4);     // decoder output tiles (4H rows)
+  static constexpr int LAT = H * kWindow * H; // latent length 3H^2
+  // GAN
+  static constexpr int C = H;                 // containers (main.py:80)
+  static constexpr int H2 = H * H;
+  static constexpr int EP = round_up(2 * H, 16);  // padded embedding row
+  static constexpr int EQ = EP / 16;
+  static constexpr int SQ = cdiv(H2, 16);
+  static constexpr int MT_G = kGanHidden / 16;    // 4
+  static constexpr int MT_N = cdiv(H, 16);        // Gen2 tiles per container row
+
+  // ---------------- device weight buffer (floats) ----------------
+  // fragments are stored [..][q][lane][4]: one 16-B load gives 4 k-steps
+  static constexpr int FQ = kFrag * 4;                         // floats per float4-fragment group
+  static constexpr int SZ_TE = MT_D * kFrag;                   // K=4 (3 feats + 0), single k-step
+  static constexpr int SZ_QKV = NPASS * 3 * TP * KQ_D * FQ;
+  static constexpr int SZ_O = NPASS * MT_D * KQ_O * FQ;
+  static constexpr int SZ_F1 = MT_F * KQ_D * FQ;
+  static constexpr int SZ_F2 = MT_D * KQ_F * FQ;
+  static constexpr int SZ_LAYER = SZ_QKV + SZ_O + SZ_F1 + SZ_F2;
+  static constexpr int SZ_DEC_HW = MT_O * KQ_D * FQ;           // per (host, step)
+  static constexpr int SZ_DEC = H * kWindow * SZ_DEC_HW;
+  static constexpr int SZ_G1E = MT_G * EQ * FQ;
+  static constexpr int SZ_G1S = MT_G * SQ * FQ;
+  static constexpr int SZ_D1S = MT_G * SQ * FQ;
+  static constexpr int SZ_G2_C = MT_N * 4 * FQ;                // per container: MT_N tiles x 16 k-steps
+  static constexpr int SZ_G2 = C * SZ_G2_C;
+  static constexpr int SZ_D1N_C = MT_G * round_up(MT_N * 4, 4) / 4 * FQ;  // per container
+  static constexpr int SZ_D1N = C * SZ_D1N_C;
+
+  static constexpr long OFF_TE = 0;
+  static constexpr long OFF_L0 = OFF_TE + SZ_TE;
+  static constexpr long OFF_DEC = OFF_L0 + kLayers * SZ_LAYER;
+  static constexpr long OFF_G1E = OFF_DEC + SZ_DEC;
+  static constexpr long OFF_G1S = OFF_G1E + SZ_G1E;
+  static constexpr long OFF_D1S = OFF_G1S + SZ_G1S;
+  static constexpr long OFF_G2 = OFF_D1S + SZ_D1S;
+  static constexpr long OFF_D1N = OFF_G2 + SZ_G2;
+  static constexpr long SZ_FRAGS = OFF_D1N + SZ_D1N;
+  // within a layer
+  static constexpr int LO_QKV = 0;
+  static constexpr int LO_O = SZ_QKV;
+  static constexpr int LO_F1 = LO_O + SZ_O;
+  static constexpr int LO_F2 = LO_F1 + SZ_F1;
+
+  // ---------------- encoder tables (staged into LDS) ----------------
+  static constexpr int T_TE = 0;                    // [3][DP] time-encoder bias + pe[w]
+  static constexpr int T_L0 = T_TE + kWindow * DP;
+  static constexpr int TL_QKV = 0;                  // [NPASS][3][TP*16]
+  static constexpr int TL_BO = NPASS * 3 * TP * 16;
+  static constexpr int TL_LN1G = TL_BO + DP;
+  static constexpr int TL_LN1B = TL_LN1G + DP;
+  static constexpr int TL_B1 = TL_LN1B + DP;
+  static constexpr int TL_B2 = TL_B1 + kFF;
+  static constexpr int TL_LN2G = TL_B2 + DP;
+  static constexpr int TL_LN2B = TL_LN2G + DP;
+  static constexpr int TL_SIZE = TL_LN2B + DP;
+  static constexpr int T_DEC = T_L0 + kLayers * TL_SIZE;  // [MT_O*16] decoder bias
+  static constexpr int T_PROTO = T_DEC + MT_O * 16;         // [K][2]
+  static constexpr int t_size(int K) { return T_PROTO + round_up(2 * K, 4); }
+
+  // ---------------- GAN tables (global) ----------------
+  static constexpr int G_B1 = 0;                  // [64] gen hidden bias
+  static constexpr int G_BD1 = G_B1 + 64;         // [64] disc hidden bias
+  static constexpr int G_WD2 = G_BD1 + 64;        // [2][64]
+  static constexpr int G_BD2 = G_WD2 + 128;       // [4] (2 used)
+  static constexpr int G_B2 = G_BD2 + 4;          // [C][MT_N*16] gen output bias
+  static constexpr int G_SIZE = G_B2 + C * MT_N * 16;
+};
+
+// GAT constants passed by value: u = Wfc^T a_src, v = Wfc^T a_dst (fp64-composed)
+struct GatConst {
+  float u[4];
+  float v[4];
+};
+
+}  // namespace pgp

@@ -1,0 +1,320 @@
+// pgp_pack.cpp — pack the reference's fp64 tensors into the kernels' layouts.
+//
+// Source tensors and their reference definitions:
+//   GAT fc / attn_fc            dlutils.py:301-302 (no bias)
+//   time_encoder, pos_encoder   models.py:344-347, 297-311
+//   encoder layers              models.py:350-356 (torch TransformerEncoderLayer)
+//   anomaly/prototype decoders  models.py:359-370
+//   Gen / Disc                  models.py:118-151, 258-291
+//   prototypes                  models.py:373-374, utils.py:70
+// Algebraic folds done here in fp64 (results then rounded once to fp32):
+//   GAT + time encoder: the GAT aggregates z_i = Wfc x_i linearly, so
+//     te(h_j) = Wte (Wfc sum_i a_ij x_i) + b = (Wte Wfc) agg_j + b
+//   edge scores: a . [z_i || z_j] = (Wfc^T a_src) . x_i + (Wfc^T a_dst) . x_j
+//   attention scale 1/sqrt(head_dim) folded into Wq, bq.
+#include "pgp_pack.hpp"
+
+#include <cmath>
+#include <cstring>
+
+namespace pgp {
+namespace {
+
+struct Reader {
+  const double* p;
+  size_t len, off = 0;
+  const double* take(size_t n) {
+    const double* r = p + off;
+    off += n;
+    return r;
+  }
+};
+
+// feature of d-space row R (see pgp_layout.hpp): R = 16t+4g+r <-> c = 16t+4r+g
+inline int featX(int R) { return 16 * (R / 16) + 4 * (R % 4) + (R % 16) / 4; }
+
+template <int H>
+size_t blob_len_t(int K) {
+  const size_t d = H, L = 3 * H * H;
+  size_t n = d * 3 + 2 * d + d * d + d + 3 * d;
+  n += 2 * (3 * d * d + 3 * d + d * d + d + 64 * d + 64 + d * 64 + d + 4 * d);
+  n += 2 * (2 * d * L + 2 * d);
+  n += 64 * (2 * d + d * d) + 64 + d * d * 64 + d * d;
+  n += 64 * 2 * d * d + 64 + 2 * 64 + 2;
+  n += (size_t)K * 2;
+  return n;
+}
+
+template <int H>
+std::string pack_t(int K, const double* blob, size_t len, Packed* P) {
+  using G = Geo<H>;
+  if (len != blob_len_t<H>(K)) return "weight blob length mismatch";
+  Reader rd{blob, len};
+  const int d = H, L = 3 * H * H;
+  const double* fcW = rd.take(d * 3);
+  const double* attn = rd.take(2 * d);
+  const double* teW = rd.take(d * d);
+  const double* teB = rd.take(d);
+  const double* pe = rd.take(3 * d);
+  struct LayerSrc {
+    const double *inW, *inB, *outW, *outB, *l1W, *l1B, *l2W, *l2B, *n1w, *n1b, *n2w, *n2b;
+  } ly[kLayers];
+  for (int l = 0; l < kLayers; ++l) {
+    ly[l].inW = rd.take(3 * d * d);
+    ly[l].inB = rd.take(3 * d);
+    ly[l].outW = rd.take(d * d);
+    ly[l].outB = rd.take(d);
+    ly[l].l1W = rd.take(64 * d);
+    ly[l].l1B = rd.take(64);
+    ly[l].l2W = rd.take(d * 64);
+    ly[l].l2B = rd.take(d);
+    ly[l].n1w = rd.take(d);
+    ly[l].n1b = rd.take(d);
+    ly[l].n2w = rd.take(d);
+    ly[l].n2b = rd.take(d);
+  }
+  const double* anW = rd.take((size_t)2 * d * L);
+  const double* anB = rd.take(2 * d);
+  const double* prW = rd.take((size_t)2 * d * L);
+  const double* prB = rd.take(2 * d);
+  const int GIN = 2 * d + d * d;
+  const double* g0W = rd.take((size_t)64 * GIN);
+  const double* g0B = rd.take(64);
+  const double* g2W = rd.take((size_t)d * d * 64);
+  const double* g2B = rd.take(d * d);
+  const double* d0W = rd.take((size_t)64 * 2 * d * d);
+  const double* d0B = rd.take(64);
+  const double* d2W = rd.take(2 * 64);
+  const double* d2B = rd.take(2);
+  const double* protos = rd.take(2 * K);
+  if (rd.off != len) return "weight blob parse error";
+
+  P->frags.assign(G::SZ_FRAGS, 0.0f);
+  P->enc_tab.assign(G::t_size(K), 0.0f);
+  P->gan_tab.assign(G::G_SIZE, 0.0f);
+  float* F = P->frags.data();
+  float* T = P->enc_tab.data();
+  float* GT = P->gan_tab.data();
+
+  // ---- GAT constants ----
+  for (int f = 0; f < 3; ++f) {
+    double u = 0, v = 0;
+    for (int c = 0; c < d; ++c) {
+      u += fcW[c * 3 + f] * attn[c];
+      v += fcW[c * 3 + f] * attn[d + c];
+    }
+    P->gat.u[f] = (float)u;
+    P->gat.v[f] = (float)v;
+  }
+  P->gat.u[3] = P->gat.v[3] = 0.f;
+
+  // ---- time encoder (folded with GAT fc) ----
+  for (int mt = 0; mt < G::MT_D; ++mt)
+    for (int lane = 0; lane < 64; ++lane) {
+      const int i = lane & 15, g = lane >> 4;
+      const int c = featX(16 * mt + i);
+      if (c >= d || g >= 3) continue;
+      double acc = 0;
+      for (int k = 0; k < d; ++k) acc += teW[c * d + k] * fcW[k * 3 + g];
+      F[G::OFF_TE + mt * 64 + lane] = (float)acc;
+    }
+  for (int w = 0; w < 3; ++w)
+    for (int R = 0; R < G::DP; ++R) {
+      const int c = featX(R);
+      if (c < d) T[G::T_TE + w * G::DP + R] = (float)(teB[c] + pe[w * d + c]);
+    }
+
+  // ---- encoder layers ----
+  const double scale = 1.0 / std::sqrt((double)G::HD);
+  for (int l = 0; l < kLayers; ++l) {
+    const LayerSrc& S = ly[l];
+    float* FL = F + G::OFF_L0 + (long)l * G::SZ_LAYER;
+    float* TL = T + G::T_L0 + l * G::TL_SIZE;
+    // head-space row R within a pass block -> (head, dim), valid?
+    auto head_row = [&](int p, int R, int* hh, int* e) -> bool {
+      if (G::P8) {
+        const int g = (R % 16) / 4, r = R % 4;
+        *hh = g >> 1;
+        *e = 4 * (g & 1) + r;
+      } else {
+        *hh = p;
+        *e = featX(R);
+      }
+      return *e < G::HD;
+    };
+    for (int p = 0; p < G::NPASS; ++p)
+      for (int m = 0; m < 3; ++m)
+        for (int tp = 0; tp < G::TP; ++tp) {
+          for (int q4 = 0; q4 < G::KQ_D; ++q4)
+            for (int lane = 0; lane < 64; ++lane)
+              for (int e4 = 0; e4 < 4; ++e4) {
+                const int i = lane & 15, g = lane >> 4, s = 4 * q4 + e4;
+                const int c = 4 * s + g;
+                int hh, e;
+                if (s >= G::KS_D || c >= d || !head_row(p, 16 * tp + i, &hh, &e)) continue;
+                const int src = m * d + hh * G::HD + e;
+                const double v = S.inW[src * d + c] * (m == 0 ? scale : 1.0);
+                FL[G::LO_QKV + ((((p * 3 + m) * G::TP + tp) * G::KQ_D + q4) * 64 + lane) * 4 + e4] = (float)v;
+              }
+          for (int i = 0; i < 16; ++i) {
+            int hh, e;
+            if (!head_row(p, 16 * tp + i, &hh, &e)) continue;
+            const int src = m * d + hh * G::HD + e;
+            TL[G::TL_QKV + (p * 3 + m) * G::TP * 16 + 16 * tp + i] =
+                (float)(S.inB[src] * (m == 0 ? scale : 1.0));
+          }
+        }
+    // out_proj
+    for (int p = 0; p < G::NPASS; ++p)
+      for (int mt = 0; mt < G::MT_D; ++mt)
+        for (int q4 = 0; q4 < G::KQ_O; ++q4)
+          for (int lane = 0; lane < 64; ++lane)
+            for (int e4 = 0; e4 < 4; ++e4) {
+              const int i = lane & 15, g = lane >> 4, s = 4 * q4 + e4;
+              const int co = featX(16 * mt + i);
+              if (s >= G::KS_O || co >= d) continue;
+              int hh, e;
+              if (G::P8) {
+                hh = g >> 1;
+                e = 4 * (g & 1) + s;
+              } else {
+                hh = p;
+                e = 4 * s + g;
+              }
+              if (e >= G::HD) continue;
+              FL[G::LO_O + (((p * G::MT_D + mt) * G::KQ_O + q4) * 64 + lane) * 4 + e4] =
+                  (float)S.outW[co * d + hh * G::HD + e];
+            }
+    // FFN
+    for (int mt = 0; mt < G::MT_F; ++mt)
+      for (int q4 = 0; q4 < G::KQ_D; ++q4)
+        for (int lane = 0; lane < 64; ++lane)
+          for (int e4 = 0; e4 < 4; ++e4) {
+            const int i = lane & 15, g = lane >> 4, s = 4 * q4 + e4, c = 4 * s + g;
+            if (s >= G::KS_D || c >= d) continue;
+            FL[G::LO_F1 + ((mt * G::KQ_D + q4) * 64 + lane) * 4 + e4] = (float)S.l1W[(16 * mt + i) * d + c];
+          }
+    for (int mt = 0; mt < G::MT_D; ++mt)
+      for (int q4 = 0; q4 < G::KQ_F; ++q4)
+        for (int lane = 0; lane < 64; ++lane)
+          for (int e4 = 0; e4 < 4; ++e4) {
+            const int i = lane & 15, g = lane >> 4, u = 16 * q4 + 4 * g + e4;
+            const int co = featX(16 * mt + i);
+            if (co >= d) continue;
+            FL[G::LO_F2 + ((mt * G::KQ_F + q4) * 64 + lane) * 4 + e4] = (float)S.l2W[co * 64 + u];
+          }
+    for (int R = 0; R < G::DP; ++R) {
+      const int c = featX(R);
+      if (c >= d) continue;
+      TL[G::TL_BO + R] = (float)S.outB[c];
+      TL[G::TL_LN1G + R] = (float)S.n1w[c];
+      TL[G::TL_LN1B + R] = (float)S.n1b[c];
+      TL[G::TL_B2 + R] = (float)S.l2B[c];
+      TL[G::TL_LN2G + R] = (float)S.n2w[c];
+      TL[G::TL_LN2B + R] = (float)S.n2b[c];
+    }
+    for (int u = 0; u < 64; ++u) TL[G::TL_B1 + u] = (float)S.l1B[u];
+  }
+
+  // ---- decoders: rows n = 4*host + {l0, l1, p0, p1} ----
+  for (int h = 0; h < d; ++h)
+    for (int w = 0; w < 3; ++w)
+      for (int mt = 0; mt < G::MT_O; ++mt)
+        for (int q4 = 0; q4 < G::KQ_D; ++q4)
+          for (int lane = 0; lane < 64; ++lane)
+            for (int e4 = 0; e4 < 4; ++e4) {
+              const int i = lane & 15, g = lane >> 4, s = 4 * q4 + e4, c = 4 * s + g;
+              const int n = 16 * mt + i, host = n / 4, q = n % 4;
+              if (s >= G::KS_D || c >= d || host >= d) continue;
+              const size_t col = (size_t)h * 3 * d + w * d + c;
+              const double v = q < 2 ? anW[(size_t)(2 * host + q) * L + col]
+                                     : prW[(size_t)(2 * host + q - 2) * L + col];
+              F[G::OFF_DEC + ((((long)(h * 3 + w) * G::MT_O + mt) * G::KQ_D + q4) * 64 + lane) * 4 + e4] =
+                  (float)v;
+            }
+  for (int n = 0; n < G::MT_O * 16; ++n) {
+    const int host = n / 4, q = n % 4;
+    if (host >= d) continue;
+    T[G::T_DEC + n] = (float)(q < 2 ? anB[2 * host + q] : prB[2 * host + q - 2]);
+  }
+  for (int k = 0; k < 2 * K; ++k) T[G::T_PROTO + k] = (float)protos[k];
+
+  // ---- GAN ----
+  for (int mt = 0; mt < G::MT_G; ++mt)
+    for (int lane = 0; lane < 64; ++lane)
+      for (int e4 = 0; e4 < 4; ++e4) {
+        const int i = lane & 15, g = lane >> 4, row = 16 * mt + i;
+        for (int q = 0; q < G::EQ; ++q) {
+          const int k = 16 * q + 4 * g + e4;
+          if (k < 2 * d)
+            F[G::OFF_G1E + ((mt * G::EQ + q) * 64 + lane) * 4 + e4] = (float)g0W[(size_t)row * GIN + k];
+        }
+        for (int q = 0; q < G::SQ; ++q) {
+          const int k = 16 * q + 4 * g + e4;
+          if (k >= d * d) continue;
+          F[G::OFF_G1S + ((long)(mt * G::SQ + q) * 64 + lane) * 4 + e4] =
+              (float)g0W[(size_t)row * GIN + 2 * d + k];
+          F[G::OFF_D1S + ((long)(mt * G::SQ + q) * 64 + lane) * 4 + e4] =
+              (float)d0W[(size_t)row * 2 * d * d + k];
+        }
+      }
+  for (int c = 0; c < d; ++c) {
+    for (int t = 0; t < G::MT_N; ++t)
+      for (int q4 = 0; q4 < 4; ++q4)
+        for (int lane = 0; lane < 64; ++lane)
+          for (int e4 = 0; e4 < 4; ++e4) {
+            const int i = lane & 15, g = lane >> 4, u = 16 * q4 + 4 * g + e4, hh = 16 * t + i;
+            if (hh >= d) continue;
+            F[G::OFF_G2 + ((((long)c * G::MT_N + t) * 4 + q4) * 64 + lane) * 4 + e4] =
+                (float)g2W[(size_t)(c * d + hh) * 64 + u];
+          }
+    for (int mt = 0; mt < G::MT_G; ++mt)
+      for (int q4 = 0; q4 < G::MT_N; ++q4)
+        for (int lane = 0; lane < 64; ++lane)
+          for (int e4 = 0; e4 < 4; ++e4) {
+            const int i = lane & 15, g = lane >> 4, hh = 16 * q4 + 4 * g + e4;
+            if (hh >= d) continue;
+            F[G::OFF_D1N + ((((long)c * G::MT_G + mt) * G::MT_N + q4) * 64 + lane) * 4 + e4] =
+                (float)d0W[(size_t)(16 * mt + i) * 2 * d * d + d * d + c * d + hh];
+          }
+    for (int R = 0; R < G::MT_N * 16; ++R)
+      if (R < d) GT[G::G_B2 + c * G::MT_N * 16 + R] = (float)g2B[c * d + R];
+  }
+  for (int u = 0; u < 64; ++u) {
+    GT[G::G_B1 + u] = (float)g0B[u];
+    GT[G::G_BD1 + u] = (float)d0B[u];
+    GT[G::G_WD2 + u] = (float)d2W[u];
+    GT[G::G_WD2 + 64 + u] = (float)d2W[64 + u];
+  }
+  GT[G::G_BD2 + 0] = (float)d2B[0];
+  GT[G::G_BD2 + 1] = (float)d2B[1];
+  return "";
+}
+
+}  // namespace
+
+#define PGP_FOR_EACH_H(X) X(8) X(16) X(32) X(50) X(64)
+
+size_t blob_len(int H, int K) {
+  switch (H) {
+#define CASE(h) \
+  case h:       \
+    return blob_len_t<h>(K);
+    PGP_FOR_EACH_H(CASE)
+#undef CASE
+  }
+  return 0;
+}
+
+std::string pack_weights(int H, int K, const double* blob, size_t len, Packed* out) {
+  switch (H) {
+#define CASE(h) \
+  case h:       \
+    return pack_t<h>(K, blob, len, out);
+    PGP_FOR_EACH_H(CASE)
+#undef CASE
+  }
+  return "unsupported host count";
+}
+
+}  // namespace pgp

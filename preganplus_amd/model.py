@@ -1,0 +1,120 @@
+"""Batched PreGAN+ decision model on MI355X (host side of the C-ABI).
+
+``DecisionModel.forward`` is one launch sequence of ``pgp_forward``: the
+per-window part of ``PreGANPlusRecovery.run_model``
+(``recovery/PreGANPlus.py:115-136``) for a whole batch of windows — encoder
+(``models.py:376-416``), detect/embed (``PreGANPlus.py:119-131``),
+``get_classes`` (``utils.py:102-109``), Gen/Disc (``models.py:118-151``) and the
+decision tensors of ``recover_decision`` (``PreGANPlus.py:84-105``).
+
+torch is only plumbing here (device memory, the stream); every FLOP runs in
+``libpreganplus.so``.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _native
+from . import weights as W
+
+
+class DecisionModel:
+    def __init__(self, n_hosts: int, weights: dict, device: str | torch.device = "cuda"):
+        self.H = int(n_hosts)
+        self.K = int(np.asarray(weights["prototypes"]).shape[0])
+        self.device = torch.device(device)
+        if self.device.type == "cuda" and self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
+        if self.device.type != "cuda":
+            raise ValueError("DecisionModel runs on the GPU only (no CPU fallback)")
+        L = _native.lib()
+        if self.H not in _native.supported_hosts():
+            raise ValueError(f"H={self.H} not compiled in; supported {_native.supported_hosts()}")
+        self._L = L
+        h = ctypes.c_void_p()
+        _native.check(L.pgp_create(self.H, self.K, ctypes.byref(h)), "pgp_create")
+        self._h = h
+        self.load_weights(weights)
+
+    def load_weights(self, weights: dict):
+        blob = W.pack_blob(weights, self.H)
+        n = self._L.pgp_weight_blob_len(self.H, self.K)
+        if n != blob.size:
+            raise ValueError(f"blob length {blob.size} != {n}")
+        torch.cuda.set_device(self.device)
+        _native.check(self._L.pgp_load_weights(
+            self._h, blob.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), blob.size),
+            "pgp_load_weights")
+        self.prototypes = np.asarray(weights["prototypes"], dtype=np.float64)
+
+    def reserve(self, max_batch: int):
+        _native.check(self._L.pgp_reserve(self._h, int(max_batch)), "pgp_reserve")
+
+    def alloc_outputs(self, B: int, latent: bool = False):
+        dev, H = self.device, self.H
+        f32, i32 = torch.float32, torch.int32
+        out = dict(
+            logits=torch.empty((B, H, 2), dtype=f32, device=dev),
+            protos=torch.empty((B, H, 2), dtype=f32, device=dev),
+            cls=torch.empty((B, H), dtype=i32, device=dev),
+            any=torch.empty((B,), dtype=i32, device=dev),
+            probs=torch.empty((B, 2), dtype=f32, device=dev),
+            keep=torch.empty((B,), dtype=i32, device=dev),
+            final_target=torch.empty((B, H), dtype=i32, device=dev),
+            gen_target=torch.empty((B, H), dtype=i32, device=dev),
+        )
+        out["latent"] = torch.empty((B, 3 * H * H), dtype=f32, device=dev) if latent else None
+        return out
+
+    def _check_inputs(self, windows, sched):
+        H = self.H
+        B = windows.shape[0]
+        if tuple(windows.shape) != (B, 3, 3 * H) or windows.dtype != torch.float32:
+            raise ValueError(f"windows must be float32 [B,3,{3 * H}], got {tuple(windows.shape)} {windows.dtype}")
+        if sched is not None and (tuple(sched.shape) != (B, H, H) or sched.dtype != torch.float32):
+            raise ValueError(f"sched must be float32 [B,{H},{H}], got {tuple(sched.shape)} {sched.dtype}")
+        for t in (windows, sched):
+            if t is not None and (t.device != self.device or not t.is_contiguous()):
+                raise ValueError("inputs must be contiguous tensors on the model's device")
+        return B
+
+    def forward(self, windows: torch.Tensor, sched: torch.Tensor, out: dict | None = None,
+                latent: bool = False, stage: int = -1, stream=None) -> dict:
+        """windows [B,3,3H] f32 (normalised), sched [B,H,H] f32, both on device."""
+        B = self._check_inputs(windows, sched)
+        if out is None:
+            out = self.alloc_outputs(B, latent)
+        st = stream if stream is not None else torch.cuda.current_stream(self.device)
+        p = lambda t: None if t is None else t.data_ptr()
+        _native.check(self._L.pgp_forward_stage(
+            self._h, int(stage), B, p(windows), p(sched), p(out["logits"]), p(out["protos"]),
+            p(out["cls"]), p(out["any"]), p(out["probs"]), p(out["keep"]),
+            p(out["final_target"]), p(out["gen_target"]), p(out.get("latent")),
+            ctypes.c_void_p(st.cuda_stream)), "pgp_forward")
+        return out
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self._L.pgp_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def to_numpy(out: dict) -> dict:
+    res = {}
+    for k, v in out.items():
+        if v is None:
+            continue
+        a = v.detach().cpu().numpy()
+        if k in ("any", "keep"):
+            a = a.astype(bool)
+        res[k] = a
+    return res

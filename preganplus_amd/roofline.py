@@ -1,0 +1,53 @@
+"""Algorithmic work of the decision path, per window.
+
+FLOPs are 2 x the multiply-accumulates of the model's dense products, counted
+on the reference's formulation (unfused, unpadded: what the math requires, not
+what a kernel executes).  Bytes are the compulsory HBM I/O of the path
+(window + dense schedule in; logits, protos, class, target,
+probs out).
+"""
+from __future__ import annotations
+
+PEAK_FP32_TFLOPS = 157.3   # MI355X dense fp32 (VALU = f32 MFMA), MI355X_MICROARCH.md
+PEAK_HBM_GBS = 8000.0      # MI355X HBM3E spec
+
+W = 3
+FF = 64
+GAN_HIDDEN = 64
+
+
+def macs_per_window(H: int) -> dict:
+    d = H
+    tokens = W * H
+    hd = d // 2
+    gat = tokens * 3 * d + 2 * tokens * d + W * H * H * d     # fc, decomposed scores, aggregation
+    te = tokens * d * d
+    per_token_layer = 3 * d * d + d * d + 2 * (W * hd) * 2 + 2 * FF * d  # qkv, out, q.k + p.v (2 heads), ffn
+    layers = 2 * tokens * per_token_layer
+    dec = (W * H * d) * (4 * H)                                 # anomaly + prototype decoders
+    gan = GAN_HIDDEN * (2 * H + H * H) + (H * H) * GAN_HIDDEN + GAN_HIDDEN * 2 * H * H + 2 * GAN_HIDDEN
+    return dict(gat=gat, time_encoder=te, encoder_layers=layers, decoders=dec, gan=gan)
+
+
+def flops_per_window(H: int) -> dict:
+    return {k: 2 * v for k, v in macs_per_window(H).items()}
+
+
+def total_flops_per_window(H: int) -> int:
+    return sum(flops_per_window(H).values())
+
+
+def encdec_flops_per_window(H: int) -> int:
+    """K2 (encdec_kernel): time encoder + 2 encoder layers + both decoders."""
+    f = flops_per_window(H)
+    return f["time_encoder"] + f["encoder_layers"] + f["decoders"]
+
+
+def gan_flops_per_window(H: int) -> int:
+    return flops_per_window(H)["gan"]
+
+
+def path_bytes_per_window(H: int) -> int:
+    """in 36H (window) + 4H^2 (dense schedule); out logits 8H,
+    protos 8H, class 4H, final target 4H, probs 8."""
+    return 36 * H + 4 * H * H + 8 * H + 8 * H + 4 * H + 4 * H + 8

@@ -1,0 +1,60 @@
+"""CPU checks of the C-ABI library: it loads, exports every symbol declared in
+include/preganplus.h, and its host-side logic (blob length, argument checks)
+behaves — no compute calls (no GPU here)."""
+import ctypes
+import re
+
+import numpy as np
+import pytest
+
+from preganplus_amd import _native
+from preganplus_amd import weights as W
+
+
+def declared_symbols():
+    txt = open("include/preganplus.h").read()
+    return sorted(set(re.findall(r"\b(pgp_[a-z_]+)\s*\(", txt)))
+
+
+def test_library_exports_every_declared_symbol():
+    L = _native.lib()
+    syms = declared_symbols()
+    assert len(syms) >= 10
+    for s in syms:
+        assert hasattr(L, s), f"missing export {s}"
+
+
+def test_abi_version_and_hosts():
+    L = _native.lib()
+    assert L.pgp_abi_version() == 1
+    hs = _native.supported_hosts()
+    assert 16 in hs and 50 in hs
+    assert all(h % 2 == 0 for h in hs)
+
+
+@pytest.mark.parametrize("H", [8, 16, 32, 50, 64])
+def test_blob_length_matches_python_layout(H):
+    L = _native.lib()
+    assert L.pgp_weight_blob_len(H, H) == W.blob_size(H)
+    assert L.pgp_weight_blob_len(H, 3) == W.blob_size(H, 3)
+
+
+def test_shipped_weights_blob_length():
+    w, _ = W.load_npz("preganplus_amd/data/simulator_16.npz")
+    assert W.pack_blob(w, 16).size == _native.lib().pgp_weight_blob_len(16, 16)
+
+
+def test_argument_errors():
+    L = _native.lib()
+    h = ctypes.c_void_p()
+    assert L.pgp_create(15, 15, ctypes.byref(h)) == -2        # odd / not compiled
+    assert L.pgp_create(16, 0, ctypes.byref(h)) == -1
+    assert L.pgp_create(16, 16, ctypes.byref(h)) == 0
+    blob = np.zeros(10)
+    rc = L.pgp_load_weights(h, blob.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), 10)
+    assert rc == -1 and b"length" in L.pgp_last_error()
+    # forward before weights -> state error, no device work
+    rc = L.pgp_forward(h, 4, *([None] * 11), None)
+    assert rc == -4
+    assert L.pgp_destroy(h) == 0
+    assert L.pgp_weight_blob_len(7, 7) == 0
