@@ -4,21 +4,27 @@ ARCH ?= gfx950
 LIBDIR := preganplus_amd/_lib
 LIB := $(LIBDIR)/libpreganplus.so
 CSRC := preganplus_amd/csrc
-SRCS := $(CSRC)/pgp_kernels.hip $(CSRC)/pgp_pack.cpp
-HDRS := include/preganplus.h $(CSRC)/pgp_layout.hpp $(CSRC)/pgp_pack.hpp
+KSRCS := $(CSRC)/pgp_gat.hip $(CSRC)/pgp_encoder.hip $(CSRC)/pgp_decoder.hip $(CSRC)/pgp_gan.hip $(CSRC)/pgp_capi.hip
+SRCS := $(KSRCS) $(CSRC)/pgp_pack.cpp
+OBJDIR := build/obj
+OBJS := $(patsubst $(CSRC)/%,$(OBJDIR)/%.o,$(SRCS))
+HDRS := include/preganplus.h $(CSRC)/pgp_layout.hpp $(CSRC)/pgp_pack.hpp $(CSRC)/pgp_device.hpp
 CXXFLAGS := -O3 -std=c++17 -fPIC -Wall -Wno-unused-function
 
 .PHONY: all clean resource-usage
 all: $(LIB)
 
-$(LIB): $(SRCS) $(HDRS)
+$(OBJDIR)/%.o: $(CSRC)/% $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) -c -o $@ $<
+
+$(LIB): $(OBJS)
 	@mkdir -p $(LIBDIR)
-	$(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) -shared -o $@ $(SRCS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS)
 
 # per-kernel VGPR / spill / occupancy report
 resource-usage:
-	$(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) -c -o /tmp/pgp_k.o $(CSRC)/pgp_kernels.hip \
-	  -Rpass-analysis=kernel-resource-usage 2>&1 | grep -E "Function Name|VGPRs:|AGPRs|Spill|Occupancy|LDS Size|SGPRs:" 
+	python3 tools/resource_usage.py
 
 clean:
-	rm -f $(LIB)
+	rm -f $(LIB) $(OBJS)

@@ -68,7 +68,7 @@ def cpu_baseline(H, weights, budget_s=12.0, max_threads=16):
 
 
 def load_traffic(H, B):
-    p = os.path.join(ROOT, "profiles", f"pmc_encdec_h{H}.json")
+    p = os.path.join(ROOT, "profiles", f"pmc_encoder_h{H}.json")
     if not os.path.exists(p):
         return None
     try:
@@ -109,22 +109,21 @@ def main():
     out = model.alloc_outputs(B)
     torch.cuda.synchronize()
 
+    NK = 4  # K1 gat, K2 encoder, K2b decoder, K3 gan
+
     def step(evs=None):
         if evs is None:
             model.forward(x, s, out=out, stage=-1)
             return
-        evs[0].record()
-        model.forward(x, s, out=out, stage=0)
-        evs[1].record()
-        model.forward(x, s, out=out, stage=1)
-        evs[2].record()
-        model.forward(x, s, out=out, stage=2)
-        evs[3].record()
+        for k in range(NK):
+            evs[k].record()
+            model.forward(x, s, out=out, stage=k)
+        evs[NK].record()
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(NK + 1)] for _ in range(args.steps)]
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
@@ -139,13 +138,13 @@ def main():
     if world > 1:
         torch.distributed.all_reduce(el, op=torch.distributed.ReduceOp.MAX)
     elapsed = float(el.item())
-    k_ms = np.array([[e[k].elapsed_time(e[k + 1]) for k in range(3)] for e in evs])  # [steps, 3]
+    k_ms = np.array([[e[k].elapsed_time(e[k + 1]) for k in range(NK)] for e in evs])  # [steps, NK]
     k_mean = k_ms.mean(axis=0)
 
     if rank == 0:
         ms = elapsed / args.steps * 1e3
         hw = B * world * H * args.steps / elapsed
-        k2_flops = R.encdec_flops_per_window(H) * B
+        k2_flops = R.encoder_flops_per_window(H) * B
         achieved = k2_flops / (k_mean[1] * 1e-3) / 1e12
         traffic = load_traffic(H, B)
         res = {
@@ -164,11 +163,15 @@ def main():
             "config": {"workload": f"C2: PreGAN+ batched inference, {H} hosts x W=3 x 3 resources, "
                                    f"{B} windows per GPU, fp32",
                        "hosts": H, "windows_per_gpu": B, "parallelism": f"dp{world} (independent windows)"},
-            "kernel_ms": {"gat_agg": k_mean[0], "encdec": k_mean[1], "gan": k_mean[2]},
-            "roofline": {"kernel": "encdec_kernel (K2)", "bound": "mfma", "achieved": achieved,
+            "kernel_ms": {"gat_agg": k_mean[0], "encoder": k_mean[1], "decoder": k_mean[2], "gan": k_mean[3]},
+            "kernel_tflops": {
+                "encoder": achieved,
+                "decoder": R.decoder_flops_per_window(H) * B / (k_mean[2] * 1e-3) / 1e12,
+                "gan": R.gan_flops_per_window(H) * B / (k_mean[3] * 1e-3) / 1e12},
+            "roofline": {"kernel": "encoder_kernel (K2)", "bound": "mfma", "achieved": achieved,
                          "peak": R.PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                          "frac": achieved / R.PEAK_FP32_TFLOPS, "traffic": traffic,
-                         "flops_per_window": R.encdec_flops_per_window(H)},
+                         "flops_per_window": R.encoder_flops_per_window(H)},
             "path_roofline": {
                 "flops_per_window": R.total_flops_per_window(H),
                 "achieved_tflops": R.total_flops_per_window(H) * B * world * args.steps / elapsed / 1e12,

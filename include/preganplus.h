@@ -111,8 +111,10 @@ int pgp_forward(pgp_model* m, int batch, const float* windows, const float* sche
                 float* latent, void* stream);
 
 /* Per-kernel launches of pgp_forward, for profiling and kernel-level tests.
- * stage 0: GAT aggregation, 1: encoder+decoder+classify, 2: GAN+decide.
- * Uses the workspace/outputs of the last pgp_forward-compatible arguments. */
+ * stage 0: GAT aggregation (K1), 1: encoder layers (K2), 2: decoders + detect
+ * + classify (K2b), 3: GAN + decisions (K3); -1 = all, as pgp_forward.
+ * Stages communicate through the model's workspace, so they must run in order
+ * on one stream with the same batch. */
 int pgp_forward_stage(pgp_model* m, int stage, int batch, const float* windows,
                       const float* sched, float* logits, float* protos, int* cls,
                       int* any_anom, float* probs, int* keep_orig, int* final_target,

@@ -1,0 +1,145 @@
+// pgp_decoder.hip — K2b: anomaly + prototype decoders (models.py:359-370) as
+// one GEMM [B x 3H^2] . [3H^2 x 4H], fused with detect/embed
+// (PreGANPlus.py:119-131) and get_classes (utils.py:102-109).
+//
+// One workgroup = 16 waves = 256 windows (16 per wave, on lanes).  The K loop
+// runs over (host, step) chunks of the latent; each chunk's weight fragments
+// (MT_O x KQ_D groups) are streamed into a 2-slot LDS ring by global_load_lds
+// and shared by all 16 waves; each wave's latent B operands for the next chunk
+// are prefetched into registers while the current chunk computes.
+// Output rows n = 4*host + {logit0, logit1, proto0, proto1} put a host's four
+// values in one lane's accumulator, so the epilogue is lane-local.
+#include "pgp_device.hpp"
+
+namespace pgp {
+namespace {
+
+constexpr int kDecWaves = 16;
+
+template <int H>
+struct DecLds {
+  static constexpr int SLOT = Geo<H>::DEC_G * Geo<H>::FQ;
+  static constexpr int TAB = Geo<H>::t_size(kMaxProtos);
+  static constexpr int TOTAL = 2 * SLOT + TAB;
+};
+
+template <int H>
+__global__ __launch_bounds__(kDecWaves * 64) void decoder_kernel(FwdArgs a) {
+  using G = Geo<H>;
+  using L = DecLds<H>;
+  __shared__ __attribute__((aligned(16))) float smem[L::TOTAL];
+  float* tab = smem + 2 * L::SLOT;
+  const int tsz = G::t_size(a.K);
+  for (int i = threadIdx.x; i < tsz; i += blockDim.x) tab[i] = a.tab[i];
+
+  const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const long blk = (long)blockIdx.x * kDecWaves + wv;
+  const long nblk = (a.B + 15) / 16;
+  const bool active = blk < nblk;
+  const float* wdec = a.frags + G::OFF_DEC;
+  const float* lat = a.lat + (active ? blk : 0) * G::LAT_BLK;
+  constexpr int NCH = H * kWindow;
+
+  float* cur = smem;
+  float* nxt = smem + L::SLOT;
+  dma_groups(wdec, cur, G::DEC_G, wv, kDecWaves, lane);
+  float b[G::KS_D];
+#pragma unroll
+  for (int s = 0; s < G::KS_D; ++s) b[s] = active ? lat[s * 64 + lane] : 0.f;
+  __syncthreads();
+  dma_groups(wdec + (long)G::DEC_G * G::FQ, nxt, G::DEC_G, wv, kDecWaves, lane);
+
+  f32x4 acc[G::MT_O];
+#pragma unroll
+  for (int mt = 0; mt < G::MT_O; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int c = 0; c < NCH; ++c) {
+    float bn[G::KS_D];
+    const bool pre = active && (c + 1 < NCH);
+#pragma unroll
+    for (int s = 0; s < G::KS_D; ++s) bn[s] = pre ? lat[((c + 1) * G::KS_D + s) * 64 + lane] : 0.f;
+#pragma unroll
+    for (int mt = 0; mt < G::MT_O; ++mt)
+#pragma unroll
+      for (int q4 = 0; q4 < G::KQ_D; ++q4) {
+        const f32x4 av = ld4(cur + (mt * G::KQ_D + q4) * 256 + lane * 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (4 * q4 + e < G::KS_D) acc[mt] = mfma(av[e], b[4 * q4 + e], acc[mt]);
+      }
+    __syncthreads();
+    float* t = cur;
+    cur = nxt;
+    nxt = t;
+    if (c + 2 < NCH) dma_groups(wdec + (long)(c + 2) * G::DEC_G * G::FQ, nxt, G::DEC_G, wv, kDecWaves, lane);
+#pragma unroll
+    for (int s = 0; s < G::KS_D; ++s) b[s] = bn[s];
+  }
+
+  // ---- epilogue: bias, sigmoid, detect, embed, classify ----
+  const long bw = blk * 16 + j;
+  const bool valid = active && bw < a.B;
+  int anyf = 0;
+  const float* P = tab + G::T_PROTO;
+#pragma unroll
+  for (int mt = 0; mt < G::MT_O; ++mt) {
+    const int host = 4 * mt + g;
+    const f32x4 v = acc[mt] + ld4(tab + G::T_DEC + 16 * mt + 4 * g);
+    if (host < H) {
+      const float l0 = v[0], l1 = v[1];
+      const float p0 = 1.0f / (1.0f + expf(-v[2])), p1 = 1.0f / (1.0f + expf(-v[3]));
+      const bool an = l1 > l0;  // torch.argmax: ties -> index 0
+      const float e0 = an ? p0 : 0.f, e1 = an ? p1 : 0.f;
+      int cl = -1;
+      if (!(e0 == 0.f && e1 == 0.f)) {
+        float best = INFINITY;
+        for (int k = 0; k < a.K; ++k) {
+          const float d0 = e0 - P[2 * k], d1 = e1 - P[2 * k + 1];
+          const float dist = (d0 * d0 + d1 * d1) * 0.5f;  // torch.mean over PROTO_DIM = 2
+          if (dist < best) {                              // np.argmin: first minimum
+            best = dist;
+            cl = k;
+          }
+        }
+      }
+      anyf |= an ? 1 : 0;
+      if (valid) {
+        const long o = (bw * H + host) * 2;
+        a.logits[o] = l0;
+        a.logits[o + 1] = l1;
+        a.protos[o] = p0;
+        a.protos[o + 1] = p1;
+        a.cls[bw * H + host] = cl;
+        a.emb[bw * G::EP + 2 * host] = e0;
+        a.emb[bw * G::EP + 2 * host + 1] = e1;
+      }
+    }
+  }
+  anyf |= __shfl_xor(anyf, 16);
+  anyf |= __shfl_xor(anyf, 32);
+  if (valid && g == 0) a.any_anom[bw] = anyf;
+}
+
+template <int H>
+hipError_t launch(const FwdArgs& a, hipStream_t st) {
+  const long nblk = (a.B + 15) / 16;
+  const int grid = (int)((nblk + kDecWaves - 1) / kDecWaves);
+  decoder_kernel<H><<<grid, kDecWaves * 64, 0, st>>>(a);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t launch_decoder(const FwdArgs& a, hipStream_t st) {
+  switch (a.H) {
+#define CASE(h) \
+  case h:       \
+    return launch<h>(a, st);
+    PGP_FOR_EACH_H(CASE)
+#undef CASE
+  }
+  return hipErrorInvalidValue;
+}
+
+}  // namespace pgp

@@ -1,0 +1,68 @@
+// pgp_device.hpp — device helpers shared by the gfx950 kernels, and the host
+// launch entry points each kernel file exports (pgp_capi.hip calls them).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "pgp_layout.hpp"
+
+namespace pgp {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kMaxProtos = 64;
+
+// Kernel arguments shared by the launches of one forward call.
+struct FwdArgs {
+  int B, H, K;
+  const float* windows;  // [B,3,3H]
+  const float* sched;    // [B,H,H]
+  float* agg;            // workspace: GAT output, [blk][H][3][48]
+  float* lat;            // workspace: encoder output tiles, [blk][H][3][KS_D][64]
+  float* emb;            // workspace: masked embeddings [B][EP]
+  const float* frags;    // device weight fragments (Geo<H> offsets)
+  const float* tab;      // encoder/decoder tables (LDS-staged)
+  const float* gtab;     // GAN tables
+  GatConst gat;
+  float* logits;
+  float* protos;
+  int* cls;
+  int* any_anom;
+  float* probs;
+  int* keep;
+  int* final_t;
+  int* gen_t;
+  float* latent;  // optional debug tap [B, 3H^2] (reference order)
+};
+
+hipError_t launch_gat(const FwdArgs& a, hipStream_t st);
+hipError_t launch_encoder(const FwdArgs& a, hipStream_t st);
+hipError_t launch_decoder(const FwdArgs& a, hipStream_t st);
+hipError_t launch_gan(const FwdArgs& a, hipStream_t st);
+
+#ifdef __HIP_DEVICE_COMPILE__
+#define PGP_DEV __device__ __forceinline__
+#else
+#define PGP_DEV __device__ __forceinline__
+#endif
+
+PGP_DEV f32x4 mfma(float a, float b, f32x4 c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
+PGP_DEV f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+PGP_DEV float xsum(float v, bool both) {
+  v += __shfl_xor(v, 16);
+  if (both) v += __shfl_xor(v, 32);
+  return v;
+}
+
+// Async copy of `ngroups` 1-KiB fragment groups global -> LDS, spread over the
+// workgroup's waves (group g by wave g % nwaves).  LDS destination is the
+// wave-uniform base + lane*16 (global_load_lds_dwordx4), so a group's 64
+// lane-consecutive float4 land contiguously, exactly as packed.
+PGP_DEV void dma_groups(const float* __restrict__ src, float* dst, int ngroups, int wv, int nwaves, int lane) {
+  for (int g = wv; g < ngroups; g += nwaves) {
+    __builtin_amdgcn_global_load_lds(
+        (const __attribute__((address_space(1))) void*)(src + (long)g * 256 + lane * 4),
+        (__attribute__((address_space(3))) void*)(dst + g * 256), 16, 0, 0);
+  }
+}
+
+}  // namespace pgp

@@ -1,0 +1,89 @@
+// pgp_gat.hip — K1: GAT edge softmax + aggregation (dlutils.py:304-348).
+//
+// One wave per (window, step); lane = destination host j (H <= 64).
+//   s_i = u.x_i, t_j = v.x_j           (attn_fc split, folded through fc: pgp_pack.cpp)
+//   e_ij = leaky_relu_0.01(s_i + t_j)  (dlutils.py:329)
+//   a_ij = exp(e_ij - M) / sum_{i,j} exp(e_ij - M)   graph-wise over all H^2 edges
+//                                      (dgl.softmax_edges, dlutils.py:335)
+//   agg_j = sum_i a_ij x_i             (update_all src_mul_edge/sum, dlutils.py:338-342,
+//                                       taken before the linear fc)
+// Output = the B operand of the encoder's time-encoder MFMA:
+//   agg[((blk*H + j)*3 + w)*48 + f*16 + (b & 15)]
+#include "pgp_device.hpp"
+
+namespace pgp {
+namespace {
+
+__device__ __forceinline__ float lrelu001(float e) { return e > 0.f ? e : 0.01f * e; }
+
+template <int H>
+__global__ __launch_bounds__(256) void gat_agg_kernel(int B, const float* __restrict__ win,
+                                                      float* __restrict__ agg, GatConst gc) {
+  static_assert(H <= 64, "GAT kernel maps hosts to lanes");
+  __shared__ f32x4 sx[4][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const long item = (long)blockIdx.x * 4 + wv;
+  const bool active = item < (long)B * 3;
+  const long b = active ? item / 3 : 0;
+  const int w = active ? (int)(item % 3) : 0;
+  float x0 = 0.f, x1 = 0.f, x2 = 0.f;
+  if (active && lane < H) {
+    const float* p = win + (b * 3 + w) * 3 * H + 3 * lane;
+    x0 = p[0];
+    x1 = p[1];
+    x2 = p[2];
+  }
+  const float s = gc.u[0] * x0 + gc.u[1] * x1 + gc.u[2] * x2;
+  const float t = gc.v[0] * x0 + gc.v[1] * x1 + gc.v[2] * x2;
+  float smax = lane < H ? s : -INFINITY, tmax = lane < H ? t : -INFINITY;
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    smax = fmaxf(smax, __shfl_xor(smax, off));
+    tmax = fmaxf(tmax, __shfl_xor(tmax, off));
+  }
+  const float M = lrelu001(smax + tmax);  // = max_ij e_ij (lrelu and rounding are monotone)
+  sx[wv][lane] = f32x4{s, x0, x1, x2};
+  __syncthreads();
+  float S = 0.f, a0 = 0.f, a1 = 0.f, a2 = 0.f;
+#pragma unroll 5
+  for (int i = 0; i < H; ++i) {
+    const f32x4 v = sx[wv][i];
+    const float p = expf(lrelu001(v.x + t) - M);
+    S += p;
+    a0 += p * v.y;
+    a1 += p * v.z;
+    a2 += p * v.w;
+  }
+  float St = lane < H ? S : 0.f;
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) St += __shfl_xor(St, off);
+  if (active && lane < H) {
+    const float inv = 1.0f / St;
+    float* o = agg + (((b >> 4) * H + lane) * 3 + w) * 48 + (b & 15);
+    o[0] = a0 * inv;
+    o[16] = a1 * inv;
+    o[32] = a2 * inv;
+  }
+}
+
+template <int H>
+hipError_t launch(const FwdArgs& a, hipStream_t st) {
+  const long items = (long)a.B * 3;
+  gat_agg_kernel<H><<<(int)((items + 3) / 4), 256, 0, st>>>(a.B, a.windows, a.agg, a.gat);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t launch_gat(const FwdArgs& a, hipStream_t st) {
+  switch (a.H) {
+#define CASE(h) \
+  case h:       \
+    return launch<h>(a, st);
+    PGP_FOR_EACH_H(CASE)
+#undef CASE
+  }
+  return hipErrorInvalidValue;
+}
+
+}  // namespace pgp

@@ -19,6 +19,9 @@
 //   decoder outputs: row n = 4*host + q, q = {logit0, logit1, proto0, proto1}.
 #pragma once
 
+// host counts compiled into the library (d_model = H split over 2 heads: H even)
+#define PGP_FOR_EACH_H(X) X(8) X(16) X(32) X(50) X(64)
+
 namespace pgp {
 
 constexpr int round_up(int x, int m) { return (x + m - 1) / m * m; }
@@ -60,42 +63,59 @@ struct Geo {
   static constexpr int MT_G = kGanHidden / 16;    // 4
   static constexpr int MT_N = cdiv(H, 16);        // Gen2 tiles per container row
 
-  // ---------------- device weight buffer (floats) ----------------
-  // fragments are stored [..][q][lane][4]: one 16-B load gives 4 k-steps
-  static constexpr int FQ = kFrag * 4;                         // floats per float4-fragment group
-  static constexpr int SZ_TE = MT_D * kFrag;                   // K=4 (3 feats + 0), single k-step
-  static constexpr int SZ_QKV = NPASS * 3 * TP * KQ_D * FQ;
-  static constexpr int SZ_O = NPASS * MT_D * KQ_O * FQ;
-  static constexpr int SZ_F1 = MT_F * KQ_D * FQ;
-  static constexpr int SZ_F2 = MT_D * KQ_F * FQ;
-  static constexpr int SZ_LAYER = SZ_QKV + SZ_O + SZ_F1 + SZ_F2;
-  static constexpr int SZ_DEC_HW = MT_O * KQ_D * FQ;           // per (host, step)
-  static constexpr int SZ_DEC = H * kWindow * SZ_DEC_HW;
+  // ---------------- device weight buffer ----------------
+  // Fragments are stored as 1-KiB "groups" [..][q][lane][4]: 64 lanes x one
+  // float4 = 4 consecutive k-steps of one 16-row tile; a group is one
+  // global_load_lds_dwordx4 wave-instruction and one ds_read_b128 per lane.
+  static constexpr int FQ = kFrag * 4;  // floats per group
+  // encoder stream of one layer, in consumption order:
+  //   for p: qkv(p) [m][tp][q4], o(p) [mt][q4];  f1 [mt][q4];  f2 [mt][q4]
+  static constexpr int G_QKV = 3 * TP * KQ_D;
+  static constexpr int G_O = MT_D * KQ_O;
+  static constexpr int G_F1 = MT_F * KQ_D;
+  static constexpr int G_F2 = MT_D * KQ_F;
+  static constexpr int P_QKV(int p) { return p * (G_QKV + G_O); }
+  static constexpr int P_O(int p) { return p * (G_QKV + G_O) + G_QKV; }
+  static constexpr int P_F1 = NPASS * (G_QKV + G_O);
+  static constexpr int P_F2 = P_F1 + G_F1;
+  static constexpr int LAYER_G = P_F2 + G_F2;
+  // LDS stages of a layer: NPASS=2: [qkv0] [o0 qkv1] [o1 f1] [f2]
+  //                        NPASS=1: [qkv0] [o0 f1] [f2]
+  static constexpr int NST = NPASS + 2;
+  static constexpr int st_begin(int k) {
+    return NPASS == 2 ? (k == 0 ? 0 : k == 1 ? P_O(0) : k == 2 ? P_O(1) : P_F2)
+                      : (k == 0 ? 0 : k == 1 ? P_O(0) : P_F2);
+  }
+  static constexpr int st_end(int k) { return k + 1 < NST ? st_begin(k + 1) : LAYER_G; }
+  static constexpr int max_stage() {
+    int m = 0;
+    for (int k = 0; k < NST; ++k) m = st_end(k) - st_begin(k) > m ? st_end(k) - st_begin(k) : m;
+    return m;
+  }
+  static constexpr int SLOT_G = max_stage();      // groups per LDS slot (encoder)
+  // decoder chunk per (host, step): [mt][q4]
+  static constexpr int DEC_G = MT_O * KQ_D;
+
+  static constexpr long OFF_ENC = 0;                                   // [layer][LAYER_G groups]
+  static constexpr long OFF_DEC = OFF_ENC + (long)kLayers * LAYER_G * FQ;  // [h][w][DEC_G]
+  static constexpr long OFF_G1E = OFF_DEC + (long)H * kWindow * DEC_G * FQ;
   static constexpr int SZ_G1E = MT_G * EQ * FQ;
   static constexpr int SZ_G1S = MT_G * SQ * FQ;
-  static constexpr int SZ_D1S = MT_G * SQ * FQ;
-  static constexpr int SZ_G2_C = MT_N * 4 * FQ;                // per container: MT_N tiles x 16 k-steps
-  static constexpr int SZ_G2 = C * SZ_G2_C;
-  static constexpr int SZ_D1N_C = MT_G * round_up(MT_N * 4, 4) / 4 * FQ;  // per container
-  static constexpr int SZ_D1N = C * SZ_D1N_C;
-
-  static constexpr long OFF_TE = 0;
-  static constexpr long OFF_L0 = OFF_TE + SZ_TE;
-  static constexpr long OFF_DEC = OFF_L0 + kLayers * SZ_LAYER;
-  static constexpr long OFF_G1E = OFF_DEC + SZ_DEC;
   static constexpr long OFF_G1S = OFF_G1E + SZ_G1E;
   static constexpr long OFF_D1S = OFF_G1S + SZ_G1S;
-  static constexpr long OFF_G2 = OFF_D1S + SZ_D1S;
-  static constexpr long OFF_D1N = OFF_G2 + SZ_G2;
-  static constexpr long SZ_FRAGS = OFF_D1N + SZ_D1N;
-  // within a layer
-  static constexpr int LO_QKV = 0;
-  static constexpr int LO_O = SZ_QKV;
-  static constexpr int LO_F1 = LO_O + SZ_O;
-  static constexpr int LO_F2 = LO_F1 + SZ_F1;
+  static constexpr int SZ_G2_C = MT_N * 4 * FQ;                // per container: MT_N tiles x 16 k-steps
+  static constexpr int SZ_D1N_C = MT_G * MT_N * FQ;            // per container
+  static constexpr long OFF_G2 = OFF_D1S + SZ_G1S;
+  static constexpr long OFF_D1N = OFF_G2 + (long)C * SZ_G2_C;
+  static constexpr long SZ_FRAGS = OFF_D1N + (long)C * SZ_D1N_C;
 
-  // ---------------- encoder tables (staged into LDS) ----------------
-  static constexpr int T_TE = 0;                    // [3][DP] time-encoder bias + pe[w]
+  // latent workspace (encoder -> decoder): per 16-window block
+  //   [H][3][KS_D][64]: X tile registers as the decoder's B operand
+  static constexpr long LAT_BLK = (long)H * kWindow * KS_D * 64;
+
+  // ---------------- encoder/decoder tables (staged into LDS) ----------------
+  static constexpr int T_TEW = 0;                   // [MT_D][64] time-encoder A fragments (K=4)
+  static constexpr int T_TE = T_TEW + MT_D * 64;    // [3][DP] time-encoder bias + pe[w]
   static constexpr int T_L0 = T_TE + kWindow * DP;
   static constexpr int TL_QKV = 0;                  // [NPASS][3][TP*16]
   static constexpr int TL_BO = NPASS * 3 * TP * 16;

@@ -116,7 +116,7 @@ std::string pack_t(int K, const double* blob, size_t len, Packed* P) {
       if (c >= d || g >= 3) continue;
       double acc = 0;
       for (int k = 0; k < d; ++k) acc += teW[c * d + k] * fcW[k * 3 + g];
-      F[G::OFF_TE + mt * 64 + lane] = (float)acc;
+      T[G::T_TEW + mt * 64 + lane] = (float)acc;
     }
   for (int w = 0; w < 3; ++w)
     for (int R = 0; R < G::DP; ++R) {
@@ -128,7 +128,7 @@ std::string pack_t(int K, const double* blob, size_t len, Packed* P) {
   const double scale = 1.0 / std::sqrt((double)G::HD);
   for (int l = 0; l < kLayers; ++l) {
     const LayerSrc& S = ly[l];
-    float* FL = F + G::OFF_L0 + (long)l * G::SZ_LAYER;
+    float* FL = F + G::OFF_ENC + (long)l * G::LAYER_G * G::FQ;
     float* TL = T + G::T_L0 + l * G::TL_SIZE;
     // head-space row R within a pass block -> (head, dim), valid?
     auto head_row = [&](int p, int R, int* hh, int* e) -> bool {
@@ -154,7 +154,7 @@ std::string pack_t(int K, const double* blob, size_t len, Packed* P) {
                 if (s >= G::KS_D || c >= d || !head_row(p, 16 * tp + i, &hh, &e)) continue;
                 const int src = m * d + hh * G::HD + e;
                 const double v = S.inW[src * d + c] * (m == 0 ? scale : 1.0);
-                FL[G::LO_QKV + ((((p * 3 + m) * G::TP + tp) * G::KQ_D + q4) * 64 + lane) * 4 + e4] = (float)v;
+                FL[(G::P_QKV(p) + (m * G::TP + tp) * G::KQ_D + q4) * G::FQ + lane * 4 + e4] = (float)v;
               }
           for (int i = 0; i < 16; ++i) {
             int hh, e;
@@ -182,7 +182,7 @@ std::string pack_t(int K, const double* blob, size_t len, Packed* P) {
                 e = 4 * s + g;
               }
               if (e >= G::HD) continue;
-              FL[G::LO_O + (((p * G::MT_D + mt) * G::KQ_O + q4) * 64 + lane) * 4 + e4] =
+              FL[(G::P_O(p) + mt * G::KQ_O + q4) * G::FQ + lane * 4 + e4] =
                   (float)S.outW[co * d + hh * G::HD + e];
             }
     // FFN
@@ -192,7 +192,7 @@ std::string pack_t(int K, const double* blob, size_t len, Packed* P) {
           for (int e4 = 0; e4 < 4; ++e4) {
             const int i = lane & 15, g = lane >> 4, s = 4 * q4 + e4, c = 4 * s + g;
             if (s >= G::KS_D || c >= d) continue;
-            FL[G::LO_F1 + ((mt * G::KQ_D + q4) * 64 + lane) * 4 + e4] = (float)S.l1W[(16 * mt + i) * d + c];
+            FL[(G::P_F1 + mt * G::KQ_D + q4) * G::FQ + lane * 4 + e4] = (float)S.l1W[(16 * mt + i) * d + c];
           }
     for (int mt = 0; mt < G::MT_D; ++mt)
       for (int q4 = 0; q4 < G::KQ_F; ++q4)
@@ -201,7 +201,7 @@ std::string pack_t(int K, const double* blob, size_t len, Packed* P) {
             const int i = lane & 15, g = lane >> 4, u = 16 * q4 + 4 * g + e4;
             const int co = featX(16 * mt + i);
             if (co >= d) continue;
-            FL[G::LO_F2 + ((mt * G::KQ_F + q4) * 64 + lane) * 4 + e4] = (float)S.l2W[co * 64 + u];
+            FL[(G::P_F2 + mt * G::KQ_F + q4) * G::FQ + lane * 4 + e4] = (float)S.l2W[co * 64 + u];
           }
     for (int R = 0; R < G::DP; ++R) {
       const int c = featX(R);
@@ -229,7 +229,7 @@ std::string pack_t(int K, const double* blob, size_t len, Packed* P) {
               const size_t col = (size_t)h * 3 * d + w * d + c;
               const double v = q < 2 ? anW[(size_t)(2 * host + q) * L + col]
                                      : prW[(size_t)(2 * host + q - 2) * L + col];
-              F[G::OFF_DEC + ((((long)(h * 3 + w) * G::MT_O + mt) * G::KQ_D + q4) * 64 + lane) * 4 + e4] =
+              F[G::OFF_DEC + ((long)(h * 3 + w) * G::DEC_G + mt * G::KQ_D + q4) * G::FQ + lane * 4 + e4] =
                   (float)v;
             }
   for (int n = 0; n < G::MT_O * 16; ++n) {
@@ -292,8 +292,6 @@ std::string pack_t(int K, const double* blob, size_t len, Packed* P) {
 }
 
 }  // namespace
-
-#define PGP_FOR_EACH_H(X) X(8) X(16) X(32) X(50) X(64)
 
 size_t blob_len(int H, int K) {
   switch (H) {

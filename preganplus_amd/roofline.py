@@ -43,6 +43,17 @@ def encdec_flops_per_window(H: int) -> int:
     return f["time_encoder"] + f["encoder_layers"] + f["decoders"]
 
 
+def encoder_flops_per_window(H: int) -> int:
+    """K2 (encoder_kernel): time encoder + 2 encoder layers."""
+    f = flops_per_window(H)
+    return f["time_encoder"] + f["encoder_layers"]
+
+
+def decoder_flops_per_window(H: int) -> int:
+    """K2b (decoder_kernel): anomaly + prototype decoders."""
+    return flops_per_window(H)["decoders"]
+
+
 def gan_flops_per_window(H: int) -> int:
     return flops_per_window(H)["gan"]
 

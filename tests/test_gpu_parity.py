@@ -27,7 +27,7 @@ def run(model, windows, sched, latent=False, stage_split=False):
     st = torch.tensor(np.asarray(sched, dtype=np.float32), device="cuda")
     if stage_split:
         out = model.alloc_outputs(wt.shape[0], latent)
-        for s in (0, 1, 2):
+        for s in (0, 1, 2, 3):
             model.forward(wt, st, out=out, stage=s)
     else:
         out = model.forward(wt, st, latent=latent)

@@ -1,8 +1,12 @@
 """Summarise hipcc -Rpass-analysis=kernel-resource-usage output per kernel."""
 import re, subprocess, sys
-cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-c", "-o", "/tmp/pgp_k.o",
-       "preganplus_amd/csrc/pgp_kernels.hip", "-Rpass-analysis=kernel-resource-usage"] + sys.argv[1:]
-out = subprocess.run(cmd, capture_output=True, text=True).stderr
+import glob
+out = ""
+files = sys.argv[1:] or sorted(glob.glob("preganplus_amd/csrc/*.hip"))
+for f in files:
+    cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-c", "-o", "/tmp/pgp_k.o",
+           f, "-Rpass-analysis=kernel-resource-usage"]
+    out += subprocess.run(cmd, capture_output=True, text=True).stderr
 rows, cur = [], None
 for line in out.splitlines():
     m = re.search(r"remark:\s*(.+?): (.+?) \[", line)
