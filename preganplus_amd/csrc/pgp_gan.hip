@@ -1,38 +1,89 @@
 // pgp_gan.hip — K3: generator + discriminator + decision argmaxes
 // (models.py:118-151, 258-291; PreGANPlus.py:84-105; stats/Stats.py:162-166).
 //
-// One wave = 16 windows on lanes.  Gen1 [64 x (2H+H^2)] and the schedule half
-// of Disc1 [64 x H^2] share one pass over the schedule (shared B operand);
-// Gen2 is produced one container row at a time, tanh'd, added to the schedule,
-// arg-maxed, and immediately consumed as B operand by the new-schedule half of
-// Disc1 — the new schedule never leaves registers.
+// One workgroup = 16 waves = 256 windows (16 per wave, on lanes).  The weights
+// (3 MB at H=50) stream once per workgroup through a 2-slot LDS ring
+// (global_load_lds), shared by all 16 waves, in three phases:
+//   1. Gen1, embedding columns        hg  = W1[:, :2H] . vec(emb)
+//   2. one pass over the schedule     hg += W1[:, 2H:] . vec(s);  hd = Wd1[:, :H^2] . vec(s)
+//      (Gen1 and the schedule half of Disc1 share the B operand)
+//   3. per container row c            ns_c = s_c + 4 tanh(W2[c] . hg + b2[c])   (Gen2)
+//                                      gen_target[c] = first-argmax(ns_c), final_target[c] = first-argmax(s_c)
+//                                      hd += Wd1[:, H^2 + cH : H^2 + (c+1)H] . ns_c  (Disc1, new-schedule half)
+// so the new schedule never leaves registers.  Then Disc2 + softmax + gate.
+// LeakyReLU(True) in Gen/Disc has slope 1.0 (identity), so no activation is applied.
 #include "pgp_device.hpp"
 
 namespace pgp {
 namespace {
 
-constexpr int kGanWaves = 4;
+constexpr int kGanWaves = 16;
+constexpr int kQC = 4;  // schedule k-blocks (16 columns each) per chunk
+
+template <int H>
+struct GanGeo {
+  using G = Geo<H>;
+  static constexpr int NQC = cdiv(G::SQ, kQC);
+  static constexpr int NCHUNK = 1 + NQC + G::C;
+  static constexpr int mx(int x, int y) { return x > y ? x : y; }
+  static constexpr int SLOT_G = mx(G::GE_G, mx(kQC * G::GS_G, G::GC_G));
+  static constexpr int SLOT = SLOT_G * G::FQ;
+  // chunk k -> (global source, groups)
+  PGP_DEV static void chunk(int k, const float* frags, const float** src, int* ng) {
+    if (k == 0) {
+      *src = frags + G::OFF_GE;
+      *ng = G::GE_G;
+    } else if (k <= NQC) {
+      const int q0 = (k - 1) * kQC;
+      *src = frags + G::OFF_GS + (long)q0 * G::GS_G * G::FQ;
+      *ng = (G::SQ - q0 < kQC ? G::SQ - q0 : kQC) * G::GS_G;
+    } else {
+      *src = frags + G::OFF_GC + (long)(k - 1 - NQC) * G::GC_G * G::FQ;
+      *ng = G::GC_G;
+    }
+  }
+};
 
 template <int H>
 __global__ __launch_bounds__(kGanWaves * 64) void gan_kernel(FwdArgs a) {
-  const int B = a.B;
-  const float* __restrict__ emb = a.emb;
-  const float* __restrict__ sched = a.sched;
-  const float* __restrict__ frags = a.frags;
-  const float* __restrict__ gt = a.gtab;
-  float* __restrict__ probs = a.probs;
-  int* __restrict__ keep = a.keep;
-  int* __restrict__ final_t = a.final_t;
-  int* __restrict__ gen_t = a.gen_t;
   using G = Geo<H>;
+  using GG = GanGeo<H>;
+  __shared__ __attribute__((aligned(16))) float smem[2 * GG::SLOT];
   const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
-  const long blk = (long)blockIdx.x * kGanWaves + (threadIdx.x >> 6);
-  const long nblk = (B + 15) / 16;
-  if (blk >= nblk) return;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const long blk = (long)blockIdx.x * kGanWaves + wv;
+  const long nblk = (a.B + 15) / 16;
   const long b = blk * 16 + j;
-  const bool valid = b < B;
-  const float* sw = sched + (valid ? b : 0) * G::H2;
-  const float* ew = emb + (valid ? b : 0) * G::EP;
+  const bool valid = blk < nblk && b < a.B;
+  const float* sw = a.sched + (valid ? b : 0) * G::H2;
+  const float* ew = a.emb + (valid ? b : 0) * G::EP;
+  const float* gt = a.gtab;
+
+  float* cur = smem;
+  float* nxt = smem + GG::SLOT;
+  int next = 1;
+  {
+    const float* src;
+    int ng;
+    GG::chunk(0, a.frags, &src, &ng);
+    dma_groups(src, cur, ng, wv, kGanWaves, lane);
+  }
+  auto issue = [&]() {
+    if (next < GG::NCHUNK) {
+      const float* src;
+      int ng;
+      GG::chunk(next, a.frags, &src, &ng);
+      dma_groups(src, nxt, ng, wv, kGanWaves, lane);
+    }
+  };
+  auto advance = [&]() {
+    __syncthreads();
+    float* t = cur;
+    cur = nxt;
+    nxt = t;
+    ++next;
+    issue();
+  };
 
   f32x4 hg[G::MT_G], hd[G::MT_G];
 #pragma unroll
@@ -41,70 +92,104 @@ __global__ __launch_bounds__(kGanWaves * 64) void gan_kernel(FwdArgs a) {
     hd[mt] = ld4(gt + G::G_BD1 + 16 * mt + 4 * g);
   }
   const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
-  // ---- Gen1, embedding half ----
-  const f32x4* A1e = reinterpret_cast<const f32x4*>(frags + G::OFF_G1E);
+  f32x4 be[G::EQ];
 #pragma unroll
-  for (int q = 0; q < G::EQ; ++q) {
-    const f32x4 bv = valid ? ld4(ew + 16 * q + 4 * g) : zero4;
+  for (int q = 0; q < G::EQ; ++q) be[q] = valid ? ld4(ew + 16 * q + 4 * g) : zero4;
+  __syncthreads();
+  issue();
+
+  // ---- phase 1: Gen1, embedding columns ----
+#pragma unroll
+  for (int q = 0; q < G::EQ; ++q)
 #pragma unroll
     for (int mt = 0; mt < G::MT_G; ++mt) {
-      const f32x4 a = A1e[(mt * G::EQ + q) * 64 + lane];
+      const f32x4 w = ld4(cur + (mt * G::EQ + q) * 256 + lane * 4);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) hg[mt] = mfma(a[e], bv[e], hg[mt]);
+      for (int e = 0; e < 4; ++e) hg[mt] = mfma(w[e], be[q][e], hg[mt]);
     }
+
+  // ---- phase 2: schedule pass (Gen1 + Disc1 schedule half) ----
+  f32x4 bq[kQC];
+#pragma unroll
+  for (int i = 0; i < kQC; ++i) {
+    const int idx = 16 * i + 4 * g;
+    bq[i] = (valid && idx < G::H2) ? ld4(sw + idx) : zero4;
   }
-  // ---- Gen1 schedule half + Disc1 schedule half (shared B operand) ----
-  const f32x4* A1s = reinterpret_cast<const f32x4*>(frags + G::OFF_G1S);
-  const f32x4* Ad1s = reinterpret_cast<const f32x4*>(frags + G::OFF_D1S);
-#pragma unroll 2
-  for (int q = 0; q < G::SQ; ++q) {
-    const int idx = 16 * q + 4 * g;
-    const f32x4 bv = (valid && idx < G::H2) ? ld4(sw + idx) : zero4;
+  advance();
+  for (int qc = 0; qc < GG::NQC; ++qc) {
+    f32x4 bn[kQC];
 #pragma unroll
-    for (int mt = 0; mt < G::MT_G; ++mt) {
-      const f32x4 a = A1s[(mt * G::SQ + q) * 64 + lane];
-      const f32x4 ad = Ad1s[(mt * G::SQ + q) * 64 + lane];
+    for (int i = 0; i < kQC; ++i) {
+      const int idx = 16 * ((qc + 1) * kQC + i) + 4 * g;
+      bn[i] = (valid && idx < G::H2) ? ld4(sw + idx) : zero4;
+    }
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        hg[mt] = mfma(a[e], bv[e], hg[mt]);
-        hd[mt] = mfma(ad[e], bv[e], hd[mt]);
+    for (int i = 0; i < kQC; ++i) {
+      if (qc * kQC + i < G::SQ) {
+#pragma unroll
+        for (int mt = 0; mt < G::MT_G; ++mt) {
+          const f32x4 wg = ld4(cur + (i * G::GS_G + mt) * 256 + lane * 4);
+          const f32x4 wd = ld4(cur + (i * G::GS_G + G::MT_G + mt) * 256 + lane * 4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            hg[mt] = mfma(wg[e], bq[i][e], hg[mt]);
+            hd[mt] = mfma(wd[e], bq[i][e], hd[mt]);
+          }
+        }
       }
     }
+    advance();
+#pragma unroll
+    for (int i = 0; i < kQC; ++i) bq[i] = bn[i];
   }
-  // (LeakyReLU(True) is the identity: hg is the hidden layer as is)
-  // ---- per container row: Gen2 -> tanh -> ns -> argmaxes -> Disc1 ns half ----
-  const f32x4* A2 = reinterpret_cast<const f32x4*>(frags + G::OFF_G2);
-  const f32x4* Ad1n = reinterpret_cast<const f32x4*>(frags + G::OFF_D1N);
+
+  // ---- phase 3: per container row ----
+  float sv[G::MT_N][4];
+#pragma unroll
+  for (int t = 0; t < G::MT_N; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int hh = 16 * t + 4 * g + r;
+      sv[t][r] = (valid && hh < H) ? sw[hh] : 0.f;
+    }
   for (int c = 0; c < G::C; ++c) {
+    float svn[G::MT_N][4];
+#pragma unroll
+    for (int t = 0; t < G::MT_N; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int hh = 16 * t + 4 * g + r;
+        svn[t][r] = (valid && hh < H && c + 1 < G::C) ? sw[(c + 1) * H + hh] : 0.f;
+      }
     f32x4 ns[G::MT_N];
 #pragma unroll
     for (int t = 0; t < G::MT_N; ++t) {
       ns[t] = ld4(gt + G::G_B2 + c * G::MT_N * 16 + 16 * t + 4 * g);
 #pragma unroll
       for (int q4 = 0; q4 < 4; ++q4) {
-        const f32x4 a = A2[(((long)c * G::MT_N + t) * 4 + q4) * 64 + lane];
+        const f32x4 w = ld4(cur + (t * 4 + q4) * 256 + lane * 4);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) ns[t] = mfma(a[e], hg[q4][e], ns[t]);
+        for (int e = 0; e < 4; ++e) ns[t] = mfma(w[e], hg[q4][e], ns[t]);
       }
     }
-    float bn = -INFINITY, bs = -INFINITY;
-    int bni = 0, bsi = 0;
+    float bn_v = -INFINITY, bs_v = -INFINITY;
+    int bn_i = 0, bs_i = 0;
 #pragma unroll
     for (int t = 0; t < G::MT_N; ++t)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int hh = 16 * t + 4 * g + r;
         if (hh < H) {
-          const float sv = valid ? sw[c * H + hh] : 0.f;
-          const float nv = sv + 4.0f * tanhf(ns[t][r]);
+          const float s0 = sv[t][r];
+          const float nv = s0 + 4.0f * tanhf(ns[t][r]);
           ns[t][r] = nv;
-          if (nv > bn) {
-            bn = nv;
-            bni = hh;
+          if (nv > bn_v) {  // strict: first maximum wins (list.index(max(...)))
+            bn_v = nv;
+            bn_i = hh;
           }
-          if (sv > bs) {
-            bs = sv;
-            bsi = hh;
+          if (s0 > bs_v) {
+            bs_v = s0;
+            bs_i = hh;
           }
         } else {
           ns[t][r] = 0.f;
@@ -114,29 +199,35 @@ __global__ __launch_bounds__(kGanWaves * 64) void gan_kernel(FwdArgs a) {
     for (int mt = 0; mt < G::MT_G; ++mt)
 #pragma unroll
       for (int q4 = 0; q4 < G::MT_N; ++q4) {
-        const f32x4 a = Ad1n[(((long)c * G::MT_G + mt) * G::MT_N + q4) * 64 + lane];
+        const f32x4 w = ld4(cur + (G::GC_G2 + mt * G::MT_N + q4) * 256 + lane * 4);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) hd[mt] = mfma(a[e], ns[q4][e], hd[mt]);
+        for (int e = 0; e < 4; ++e) hd[mt] = mfma(w[e], ns[q4][e], hd[mt]);
       }
 #pragma unroll
     for (int off = 16; off <= 32; off <<= 1) {
-      const float ov = __shfl_xor(bn, off), os = __shfl_xor(bs, off);
-      const int oi = __shfl_xor(bni, off), osi = __shfl_xor(bsi, off);
-      if (ov > bn || (ov == bn && oi < bni)) {
-        bn = ov;
-        bni = oi;
+      const float ov = __shfl_xor(bn_v, off), os = __shfl_xor(bs_v, off);
+      const int oi = __shfl_xor(bn_i, off), osi = __shfl_xor(bs_i, off);
+      if (ov > bn_v || (ov == bn_v && oi < bn_i)) {
+        bn_v = ov;
+        bn_i = oi;
       }
-      if (os > bs || (os == bs && osi < bsi)) {
-        bs = os;
-        bsi = osi;
+      if (os > bs_v || (os == bs_v && osi < bs_i)) {
+        bs_v = os;
+        bs_i = osi;
       }
     }
     if (valid && g == 0) {
-      gen_t[b * G::C + c] = bni;
-      final_t[b * G::C + c] = bsi;
+      a.gen_t[b * G::C + c] = bn_i;
+      a.final_t[b * G::C + c] = bs_i;
     }
+    advance();
+#pragma unroll
+    for (int t = 0; t < G::MT_N; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) sv[t][r] = svn[t][r];
   }
-  // ---- Disc2 + softmax + gate ----
+
+  // ---- Disc2 + softmax + gate (PreGANPlus.py:87) ----
   float z0 = 0.f, z1 = 0.f;
 #pragma unroll
   for (int mt = 0; mt < G::MT_G; ++mt) {
@@ -154,12 +245,11 @@ __global__ __launch_bounds__(kGanWaves * 64) void gan_kernel(FwdArgs a) {
   const float inv = 1.0f / (e0 + e1);
   const float p0 = e0 * inv, p1 = e1 * inv;
   if (valid && g == 0) {
-    probs[2 * b] = p0;
-    probs[2 * b + 1] = p1;
-    keep[b] = p0 > p1 ? 1 : 0;
+    a.probs[2 * b] = p0;
+    a.probs[2 * b + 1] = p1;
+    a.keep[b] = p0 > p1 ? 1 : 0;
   }
 }
-
 
 template <int H>
 hipError_t launch(const FwdArgs& a, hipStream_t st) {

@@ -98,16 +98,18 @@ struct Geo {
 
   static constexpr long OFF_ENC = 0;                                   // [layer][LAYER_G groups]
   static constexpr long OFF_DEC = OFF_ENC + (long)kLayers * LAYER_G * FQ;  // [h][w][DEC_G]
-  static constexpr long OFF_G1E = OFF_DEC + (long)H * kWindow * DEC_G * FQ;
-  static constexpr int SZ_G1E = MT_G * EQ * FQ;
-  static constexpr int SZ_G1S = MT_G * SQ * FQ;
-  static constexpr long OFF_G1S = OFF_G1E + SZ_G1E;
-  static constexpr long OFF_D1S = OFF_G1S + SZ_G1S;
-  static constexpr int SZ_G2_C = MT_N * 4 * FQ;                // per container: MT_N tiles x 16 k-steps
-  static constexpr int SZ_D1N_C = MT_G * MT_N * FQ;            // per container
-  static constexpr long OFF_G2 = OFF_D1S + SZ_G1S;
-  static constexpr long OFF_D1N = OFF_G2 + (long)C * SZ_G2_C;
-  static constexpr long SZ_FRAGS = OFF_D1N + (long)C * SZ_D1N_C;
+  // GAN (K3) chunks, each contiguous:
+  //   emb chunk   [mt][q]  MT_G x EQ groups           (Gen1, embedding columns)
+  //   sched q     [q][8]   Gen1 mt0..3 | Disc1 mt0..3 (schedule columns 16q..16q+15)
+  //   container c [G2: t][q4] (MT_N x 4) | [D1N: mt][q4] (MT_G x MT_N)
+  static constexpr int GE_G = MT_G * EQ;
+  static constexpr int GS_G = 2 * MT_G;                       // per schedule q
+  static constexpr int GC_G2 = MT_N * 4;
+  static constexpr int GC_G = GC_G2 + MT_G * MT_N;            // per container
+  static constexpr long OFF_GE = OFF_DEC + (long)H * kWindow * DEC_G * FQ;
+  static constexpr long OFF_GS = OFF_GE + (long)GE_G * FQ;
+  static constexpr long OFF_GC = OFF_GS + (long)SQ * GS_G * FQ;
+  static constexpr long SZ_FRAGS = OFF_GC + (long)C * GC_G * FQ;
 
   // latent workspace (encoder -> decoder): per 16-window block
   //   [H][3][KS_D][64]: X tile registers as the decoder's B operand

@@ -247,26 +247,26 @@ std::string pack_t(int K, const double* blob, size_t len, Packed* P) {
         for (int q = 0; q < G::EQ; ++q) {
           const int k = 16 * q + 4 * g + e4;
           if (k < 2 * d)
-            F[G::OFF_G1E + ((mt * G::EQ + q) * 64 + lane) * 4 + e4] = (float)g0W[(size_t)row * GIN + k];
+            F[G::OFF_GE + (long)(mt * G::EQ + q) * G::FQ + lane * 4 + e4] = (float)g0W[(size_t)row * GIN + k];
         }
         for (int q = 0; q < G::SQ; ++q) {
           const int k = 16 * q + 4 * g + e4;
           if (k >= d * d) continue;
-          F[G::OFF_G1S + ((long)(mt * G::SQ + q) * 64 + lane) * 4 + e4] =
+          F[G::OFF_GS + ((long)q * G::GS_G + mt) * G::FQ + lane * 4 + e4] =
               (float)g0W[(size_t)row * GIN + 2 * d + k];
-          F[G::OFF_D1S + ((long)(mt * G::SQ + q) * 64 + lane) * 4 + e4] =
+          F[G::OFF_GS + ((long)q * G::GS_G + G::MT_G + mt) * G::FQ + lane * 4 + e4] =
               (float)d0W[(size_t)row * 2 * d * d + k];
         }
       }
   for (int c = 0; c < d; ++c) {
+    float* FC = F + G::OFF_GC + (long)c * G::GC_G * G::FQ;
     for (int t = 0; t < G::MT_N; ++t)
       for (int q4 = 0; q4 < 4; ++q4)
         for (int lane = 0; lane < 64; ++lane)
           for (int e4 = 0; e4 < 4; ++e4) {
             const int i = lane & 15, g = lane >> 4, u = 16 * q4 + 4 * g + e4, hh = 16 * t + i;
             if (hh >= d) continue;
-            F[G::OFF_G2 + ((((long)c * G::MT_N + t) * 4 + q4) * 64 + lane) * 4 + e4] =
-                (float)g2W[(size_t)(c * d + hh) * 64 + u];
+            FC[(t * 4 + q4) * G::FQ + lane * 4 + e4] = (float)g2W[(size_t)(c * d + hh) * 64 + u];
           }
     for (int mt = 0; mt < G::MT_G; ++mt)
       for (int q4 = 0; q4 < G::MT_N; ++q4)
@@ -274,7 +274,7 @@ std::string pack_t(int K, const double* blob, size_t len, Packed* P) {
           for (int e4 = 0; e4 < 4; ++e4) {
             const int i = lane & 15, g = lane >> 4, hh = 16 * q4 + 4 * g + e4;
             if (hh >= d) continue;
-            F[G::OFF_D1N + ((((long)c * G::MT_G + mt) * G::MT_N + q4) * 64 + lane) * 4 + e4] =
+            FC[(G::GC_G2 + mt * G::MT_N + q4) * G::FQ + lane * 4 + e4] =
                 (float)d0W[(size_t)(16 * mt + i) * 2 * d * d + d * d + c * d + hh];
           }
     for (int R = 0; R < G::MT_N * 16; ++R)
