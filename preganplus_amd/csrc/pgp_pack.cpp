@@ -103,8 +103,10 @@ std::string pack_t(int K, const double* blob, size_t len, Packed* P) {
       u += fcW[c * 3 + f] * attn[c];
       v += fcW[c * 3 + f] * attn[d + c];
     }
-    P->gat.u[f] = (float)u;
-    P->gat.v[f] = (float)v;
+    // pre-scaled by log2(e): leaky_relu is positively homogeneous, so the kernel
+    // evaluates exp(e - M) as exp2(e' - M') with one v_exp_f32
+    P->gat.u[f] = (float)(u * 1.4426950408889634);
+    P->gat.v[f] = (float)(v * 1.4426950408889634);
   }
   P->gat.u[3] = P->gat.v[3] = 0.f;
 
