@@ -192,9 +192,9 @@ def load_npz(path):
     w = {"transformer": {}, "gen": {}, "disc": {}}
     extra = {}
     for k in z.files:
-        if "/" in k:
-            sec, name = k.split("/", 1)
-            w[sec][name] = z[k]
+        sec = k.split("/", 1)[0]
+        if sec in w:
+            w[sec][k.split("/", 1)[1]] = z[k]
         elif k == "prototypes":
             w["prototypes"] = z[k]
         else:
