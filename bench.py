@@ -89,7 +89,15 @@ def main():
     ap.add_argument("--batch", type=int, default=65536, help="windows per GPU per step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--config", choices=["c2", "fleet", "tune"], default="c2",
+                    help="c2: BASELINE config 2 (default, the headline line); fleet: config 5 "
+                         "(1024-host fleet = 64 cells of 16 hosts, shipped weights); tune: config 3 "
+                         "(tuning step fwd+bwd+AdamW, data-parallel with an RCCL all-reduce)")
     args = ap.parse_args()
+    if args.config == "fleet":
+        return bench_fleet(args)
+    if args.config == "tune":
+        return bench_tune(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -185,6 +193,105 @@ def main():
         else:
             res["cpu_baseline"] = None
         print(json.dumps(res), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+def _dist_setup():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+    return world, rank, device
+
+
+def _timed(world, device, fn, steps):
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=device)
+    if world > 1:
+        torch.distributed.all_reduce(el, op=torch.distributed.ReduceOp.MAX)
+    return float(el.item())
+
+
+def bench_fleet(args):
+    """BASELINE config 5: a 1024-host fleet as 64 independent 16-host cells
+    (SURVEY §8d), 1M windows per cell = 64M cell-windows sharded over the GPUs.
+    One step = one launch sequence over a chunk of cell-windows resident in HBM;
+    the per-GPU share is covered in ceil(share / chunk) steps."""
+    world, rank, device = _dist_setup()
+    w, _ = W.load_npz(os.path.join(ROOT, "preganplus_amd/data/simulator_16.npz"))
+    H, B = 16, args.batch if args.batch != 65536 else 262144
+    model = DecisionModel(H, w, device=device)
+    model.reserve(B)
+    x, s = synth_inputs(B, H, device, 77 + rank)
+    out = model.alloc_outputs(B)
+    total = 64 * 1_000_000
+    share = total // world
+    steps = -(-share // B) if args.steps <= 0 else args.steps
+    for _ in range(args.warmup):
+        model.forward(x, s, out=out)
+    el = _timed(world, device, lambda: model.forward(x, s, out=out), steps)
+    if rank == 0:
+        cw = B * steps * world
+        print(json.dumps({
+            "metric": "host-windows/sec (detect+diagnose+generate), fleet", "value": cw * H / el,
+            "unit": "host-windows/s", "n_gpus": world, "steps": steps, "warmup": args.warmup,
+            "ms_per_step": el / steps * 1e3, "higher_is_better": True, "scaling": "strong" if args.steps <= 0 else "weak",
+            "vs_baseline": None, "dtype": "fp32", "data": "synthetic (C2 distribution), shipped H=16 weights",
+            "config": {"workload": "C5: 1024-host fleet = 64 x 16-host cells, cell-windows sharded over GPUs",
+                       "hosts_per_cell": H, "cells": 64, "cell_windows_per_step_per_gpu": B,
+                       "cell_windows_total": cw, "parallelism": f"dp{world}"}}), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+def bench_tune(args):
+    """BASELINE config 3: one semi-supervised tuning step per iteration on a
+    local batch of windows per GPU: HIP forward with saved activations, loss
+    gradient, backward, one flat RCCL all-reduce of the gradients, AdamW.
+    Labels/targets are synthetic (fixed) so the timed region is device work."""
+    from preganplus_amd import train as TR
+    world, rank, device = _dist_setup()
+    H = args.hosts
+    B = args.batch if args.batch != 65536 else 1024
+    w = W.synth_weights(H, seed=0)
+    tr = TR.Trainer(H, w, device=device, max_batch=B)
+    x, _ = synth_inputs(B, H, device, 5 + rank)
+    g = torch.Generator(device=device).manual_seed(17 + rank)
+    y = (torch.rand((B, H), generator=g, device=device) < 0.1).to(torch.int32)
+    mult = torch.ones((B, H), device=device)
+    tgt = torch.rand((B, H, 2), generator=g, device=device)
+
+    def step():
+        tr.tune_forward(x)
+        tr.tune_backward(B, y, mult, tgt)
+        tr.all_reduce_grads("transformer")
+        tr.adam_step("transformer")
+
+    for _ in range(args.warmup):
+        step()
+    el = _timed(world, device, step, args.steps)
+    if rank == 0:
+        print(json.dumps({
+            "metric": "tuning windows/sec (fwd+bwd+all-reduce+AdamW)", "value": B * world * args.steps / el,
+            "unit": "windows/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": el / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "fp32", "data": "synthetic windows, labels and targets",
+            "config": {"workload": f"C3: tuning step, {H} hosts, {B} windows per GPU", "hosts": H,
+                       "windows_per_gpu": B, "parallelism": f"dp{world} + RCCL all-reduce"}}), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
 

@@ -120,6 +120,60 @@ int pgp_forward_stage(pgp_model* m, int stage, int batch, const float* windows,
                       int* any_anom, float* probs, int* keep_orig, int* final_target,
                       int* gen_target, float* latent, void* stream);
 
+/* ------------------------------------------------------------------------
+ * Online training ops (stateless; buffers owned by the caller, device memory).
+ * Master weights `P` are fp32 in the NATURAL blob order of pgp_load_weights
+ * (transformer | gen | disc, prototypes excluded); grads `G` share the layout.
+ * Replace, per window (or summed over a batch of windows):
+ *   pgp_tune_forward   Transformer forward in train mode (dropout p=0),
+ *                      models.py:376-416, saving activations in `scratch`
+ *   pgp_tune_backward  custom_loss / triplet_loss gradients (train.py:13-40;
+ *                      the sequential prototype/counter logic stays on the host
+ *                      and arrives as y, mult, tgt) + backward into G
+ *                      (loss.backward(), train.py:53)
+ *   pgp_gan_forward    Gen + Disc forward (PreGANPlus.py:62-63)
+ *   pgp_gan_disc_backward  BCE(probs, target) backward into the Disc grads (:66-67)
+ *   pgp_gan_gen_backward   Disc forward with the updated Disc, BCE toward [0,1],
+ *                      backward into the Gen grads (:69-74)
+ *   pgp_adamw          torch.optim.AdamW.step (utils.py:65)
+ * ---------------------------------------------------------------------- */
+size_t pgp_master_len(int n_hosts);               /* floats in P / G            */
+size_t pgp_tune_scratch_len(int n_hosts);         /* floats per window          */
+size_t pgp_gan_scratch_len(int n_hosts);          /* floats per window          */
+size_t pgp_master_offset(int n_hosts, int section); /* 0 transformer, 1 gen, 2 disc */
+
+/* windows [B,3,3H]; outputs latent [B,3H^2] (reference order), logits [B,H,2],
+ * protos [B,H,2] (sigmoid); scratch [B, pgp_tune_scratch_len]. */
+int pgp_tune_forward(int n_hosts, int batch, const float* windows, const float* P, float* scratch,
+                     float* latent, float* logits, float* protos, void* stream);
+/* y [B,H] int labels, mult [B,H] CE weights, tgt [B,H,2] positive prototypes
+ * (only rows with y>0 used); dpre [B,4H] workspace.  Accumulates into G
+ * (the caller zeroes G before the step). */
+int pgp_tune_backward(int n_hosts, int batch, const float* P, float* G, float* scratch, const float* latent,
+                      const float* logits, const float* protos, const int* y, const float* mult,
+                      const float* tgt, float* dpre, void* stream);
+/* emb [B,2H] (masked prototype embeddings), sched [B,H,H]; outputs the new
+ * schedule ns [B,H,H] and probs [B,2]; gscratch [B, pgp_gan_scratch_len]. */
+int pgp_gan_forward(int n_hosts, int batch, const float* emb, const float* sched, const float* P, float* gscratch,
+                    float* ns, float* probs, void* stream);
+int pgp_gan_disc_backward(int n_hosts, int batch, const float* target, const float* P, float* G, float* gscratch,
+                          void* stream);
+int pgp_gan_gen_backward(int n_hosts, int batch, const float* P, float* G, float* gscratch, void* stream);
+
+typedef struct {
+  long long offset;  /* first element of the tensor in P/G/m/v */
+  int n;             /* elements */
+  int active;        /* 0: the tensor got no gradient (torch skips it) */
+  float step_size;   /* lr / (1 - beta1^step) for this tensor's new step */
+  float bc2_sqrt;    /* sqrt(1 - beta2^step) */
+} pgp_adam_tensor;
+int pgp_adamw(float* P, const float* G, float* exp_avg, float* exp_avg_sq, float lr, float weight_decay,
+              float beta1, float beta2, float eps, const pgp_adam_tensor* tensors, int ntensors, void* stream);
+
+/* Rebuild the inference layouts from device master weights P (natural fp32)
+ * and prototypes [K,2] (host, fp64): the sync after an optimizer step. */
+int pgp_load_weights_master(pgp_model* m, const float* P_device, const double* prototypes);
+
 #ifdef __cplusplus
 }
 #endif

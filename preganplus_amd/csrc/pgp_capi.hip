@@ -9,6 +9,9 @@
 #include "../../include/preganplus.h"
 #include "pgp_device.hpp"
 #include "pgp_pack.hpp"
+#include "pgp_train.hpp"
+
+#include <vector>
 
 using namespace pgp;
 
@@ -194,6 +197,133 @@ int pgp_forward(pgp_model* m, int batch, const float* windows, const float* sche
                 float* latent, void* stream) {
   return pgp_forward_stage(m, -1, batch, windows, sched, logits, protos, cls, any_anom, probs, keep_orig,
                            final_target, gen_target, latent, stream);
+}
+
+// ---------------------------------------------------------------------------
+// training ops
+// ---------------------------------------------------------------------------
+namespace {
+bool master_offsets(int H, long* tr, long* gen, long* disc, long* all) {
+  switch (H) {
+#define CASE(h)                     \
+  case h:                           \
+    *tr = 0;                        \
+    *gen = TGeo<h>::OFF_GEN;        \
+    *disc = TGeo<h>::OFF_DISC;      \
+    *all = TGeo<h>::ALL;            \
+    return true;
+    PGP_FOR_EACH_H(CASE)
+#undef CASE
+  }
+  return false;
+}
+}  // namespace
+
+size_t pgp_master_len(int n_hosts) {
+  long a, b, c, d;
+  return master_offsets(n_hosts, &a, &b, &c, &d) ? (size_t)d : 0;
+}
+size_t pgp_master_offset(int n_hosts, int section) {
+  long a, b, c, d;
+  if (!master_offsets(n_hosts, &a, &b, &c, &d)) return 0;
+  return section == 0 ? a : section == 1 ? b : section == 2 ? c : d;
+}
+size_t pgp_tune_scratch_len(int n_hosts) { return supported(n_hosts) ? (size_t)train_scratch_floats(n_hosts) : 0; }
+size_t pgp_gan_scratch_len(int n_hosts) { return supported(n_hosts) ? (size_t)gan_scratch_floats(n_hosts) : 0; }
+
+int pgp_tune_forward(int n_hosts, int batch, const float* windows, const float* P, float* scratch, float* latent,
+                     float* logits, float* protos, void* stream) {
+  if (!supported(n_hosts)) return fail(PGP_ERR_UNSUPPORTED, "host count");
+  if (batch < 0 || (batch > 0 && (!windows || !P || !scratch || !latent || !logits || !protos)))
+    return fail(PGP_ERR_ARG, "bad tune_forward arguments");
+  if (batch == 0) return PGP_OK;
+  HIPCHK(launch_tune_fwd(n_hosts, batch, windows, P, scratch, latent, logits, protos,
+                         reinterpret_cast<hipStream_t>(stream)));
+  return PGP_OK;
+}
+
+int pgp_tune_backward(int n_hosts, int batch, const float* P, float* G, float* scratch, const float* latent,
+                      const float* logits, const float* protos, const int* y, const float* mult, const float* tgt,
+                      float* dpre, void* stream) {
+  if (!supported(n_hosts)) return fail(PGP_ERR_UNSUPPORTED, "host count");
+  if (batch < 0 ||
+      (batch > 0 && (!P || !G || !scratch || !latent || !logits || !protos || !y || !mult || !tgt || !dpre)))
+    return fail(PGP_ERR_ARG, "bad tune_backward arguments");
+  if (batch == 0) return PGP_OK;
+  HIPCHK(launch_tune_bwd(n_hosts, batch, P, G, scratch, latent, logits, protos, y, mult, tgt, dpre,
+                         reinterpret_cast<hipStream_t>(stream)));
+  return PGP_OK;
+}
+
+int pgp_gan_forward(int n_hosts, int batch, const float* emb, const float* sched, const float* P, float* gscratch,
+                    float* ns, float* probs, void* stream) {
+  long tr, go, dof, all;
+  if (!master_offsets(n_hosts, &tr, &go, &dof, &all)) return fail(PGP_ERR_UNSUPPORTED, "host count");
+  if (batch < 0 || (batch > 0 && (!emb || !sched || !P || !gscratch || !ns || !probs)))
+    return fail(PGP_ERR_ARG, "bad gan_forward arguments");
+  if (batch == 0) return PGP_OK;
+  HIPCHK(launch_gan_fwd(n_hosts, batch, emb, sched, P + go, P + dof, gscratch, ns, probs,
+                        reinterpret_cast<hipStream_t>(stream)));
+  return PGP_OK;
+}
+
+int pgp_gan_disc_backward(int n_hosts, int batch, const float* target, const float* P, float* G, float* gscratch,
+                          void* stream) {
+  long tr, go, dof, all;
+  if (!master_offsets(n_hosts, &tr, &go, &dof, &all)) return fail(PGP_ERR_UNSUPPORTED, "host count");
+  if (batch < 0 || (batch > 0 && (!target || !P || !G || !gscratch))) return fail(PGP_ERR_ARG, "bad arguments");
+  if (batch == 0) return PGP_OK;
+  HIPCHK(launch_gan_disc_bwd(n_hosts, batch, target, P + dof, G + dof, gscratch,
+                             reinterpret_cast<hipStream_t>(stream)));
+  return PGP_OK;
+}
+
+int pgp_gan_gen_backward(int n_hosts, int batch, const float* P, float* G, float* gscratch, void* stream) {
+  long tr, go, dof, all;
+  if (!master_offsets(n_hosts, &tr, &go, &dof, &all)) return fail(PGP_ERR_UNSUPPORTED, "host count");
+  if (batch < 0 || (batch > 0 && (!P || !G || !gscratch))) return fail(PGP_ERR_ARG, "bad arguments");
+  if (batch == 0) return PGP_OK;
+  HIPCHK(launch_gan_gen_bwd(n_hosts, batch, P + go, P + dof, G + go, gscratch,
+                            reinterpret_cast<hipStream_t>(stream)));
+  return PGP_OK;
+}
+
+int pgp_adamw(float* P, const float* G, float* exp_avg, float* exp_avg_sq, float lr, float weight_decay,
+              float beta1, float beta2, float eps, const pgp_adam_tensor* tensors, int ntensors, void* stream) {
+  if (!P || !G || !exp_avg || !exp_avg_sq || !tensors || ntensors < 0 || ntensors > kMaxTensors)
+    return fail(PGP_ERR_ARG, "bad adamw arguments");
+  if (ntensors == 0) return PGP_OK;
+  AdamArgs a{};
+  a.param = P;
+  a.grad = const_cast<float*>(G);
+  a.m = exp_avg;
+  a.v = exp_avg_sq;
+  a.lr_wd = lr * weight_decay;
+  a.b1 = beta1;
+  a.b2 = beta2;
+  a.eps = eps;
+  a.ntensors = ntensors;
+  for (int i = 0; i < ntensors; ++i) {
+    a.t[i].off = (long)tensors[i].offset;
+    a.t[i].n = tensors[i].n;
+    a.t[i].active = tensors[i].active;
+    a.t[i].step_size = tensors[i].step_size;
+    a.t[i].bc2_sqrt = tensors[i].bc2_sqrt;
+  }
+  HIPCHK(launch_adamw(a, reinterpret_cast<hipStream_t>(stream)));
+  return PGP_OK;
+}
+
+int pgp_load_weights_master(pgp_model* m, const float* P_device, const double* prototypes) {
+  if (!m || !P_device || !prototypes) return fail(PGP_ERR_ARG, "NULL argument");
+  long tr, go, dof, all;
+  if (!master_offsets(m->H, &tr, &go, &dof, &all)) return fail(PGP_ERR_UNSUPPORTED, "host count");
+  std::vector<float> host((size_t)all);
+  HIPCHK(hipMemcpy(host.data(), P_device, host.size() * sizeof(float), hipMemcpyDeviceToHost));
+  std::vector<double> blob(host.size() + 2 * (size_t)m->K);
+  for (size_t i = 0; i < host.size(); ++i) blob[i] = host[i];
+  for (int k = 0; k < 2 * m->K; ++k) blob[host.size() + k] = prototypes[k];
+  return pgp_load_weights(m, blob.data(), blob.size());
 }
 
 }  // extern "C"

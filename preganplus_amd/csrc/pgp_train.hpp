@@ -1,0 +1,111 @@
+// pgp_train.hpp — geometry of the training (tuning / GAN) kernels.
+//
+// Training runs on fp32 master weights in the reference's NATURAL layout (the
+// blob order of pgp_load_weights): the inference kernels' packed layouts fold
+// several parameters together (GAT fc into the time encoder, the attention
+// scale into Wq), so they cannot be trained in place; after an optimizer step
+// the packed copies are rebuilt from the master weights.
+//
+// Per-window activations saved by the tuning forward for the backward, tokens
+// ordered [w][h] like the reference's [S=W, N=H, d] (models.py:387-396).
+#pragma once
+#include <cstddef>
+
+namespace pgp {
+
+template <int H>
+struct TGeo {
+  static constexpr int D = H, W = 3, T = 3 * H, FF = 64, HD = H / 2, L = 3 * H * H;
+  // natural weight blob offsets (transformer section)
+  static constexpr long W_FC = 0;                   // [d][3]
+  static constexpr long W_ATT = W_FC + 3 * D;       // [2d]
+  static constexpr long W_TE = W_ATT + 2 * D;       // [d][d]
+  static constexpr long B_TE = W_TE + D * D;        // [d]
+  static constexpr long PE = B_TE + D;              // [3][d]
+  static constexpr long LAY0 = PE + 3 * D;
+  // within a layer
+  static constexpr long L_IN = 0, L_INB = 3 * D * D, L_OUT = L_INB + 3 * D, L_OUTB = L_OUT + D * D,
+                        L_W1 = L_OUTB + D, L_B1 = L_W1 + FF * D, L_W2 = L_B1 + FF, L_B2 = L_W2 + D * FF,
+                        L_N1W = L_B2 + D, L_N1B = L_N1W + D, L_N2W = L_N1B + D, L_N2B = L_N2W + D,
+                        L_SIZE = L_N2B + D;
+  static constexpr long W_AN = LAY0 + 2 * L_SIZE;   // [2H][L]
+  static constexpr long B_AN = W_AN + 2L * H * L;
+  static constexpr long W_PR = B_AN + 2 * H;
+  static constexpr long B_PR = W_PR + 2L * H * L;
+  static constexpr long TR_SIZE = B_PR + 2 * H;     // transformer section length
+  // gen / disc sections (relative to their own start)
+  static constexpr int GIN = 2 * H + H * H;
+  static constexpr long G_W1 = 0, G_B1 = 64L * GIN, G_W2 = G_B1 + 64, G_B2 = G_W2 + (long)H * H * 64,
+                        G_SIZE = G_B2 + H * H;
+  static constexpr int DIN = 2 * H * H;
+  static constexpr long D_W1 = 0, D_B1 = 64L * DIN, D_W2 = D_B1 + 64, D_B2 = D_W2 + 128, D_SIZE = D_B2 + 2;
+  static constexpr long OFF_GEN = TR_SIZE, OFF_DISC = TR_SIZE + G_SIZE, ALL = TR_SIZE + G_SIZE + D_SIZE;
+
+  // ---- tuning scratch per window (floats) ----
+  static constexpr long S_X = 0;                         // [3][H][3] input window
+  static constexpr long S_Z = S_X + 9 * H;               // [3][H][d] fc(x)
+  static constexpr long S_SS = S_Z + T * D;              // [3][H] src score
+  static constexpr long S_TT = S_SS + T;                 // [3][H] dst score
+  static constexpr long S_A = S_TT + T;                  // [3][H][H] edge softmax a[w][i][j]
+  static constexpr long S_G = S_A + 3L * H * H;          // [3][H][d] GAT output
+  static constexpr long S_LAY = S_G + T * D;             // per layer:
+  static constexpr long LS_X = 0;                        //   [T][d] layer input
+  static constexpr long LS_QKV = LS_X + T * D;           //   [T][3d]
+  static constexpr long LS_P = LS_QKV + 3L * T * D;      //   [H][2][3][3] attention probs
+  static constexpr long LS_O = LS_P + 18L * H;           //   [T][d] attention output (pre out_proj)
+  static constexpr long LS_R1 = LS_O + T * D;            //   [T][d] LN1 input
+  static constexpr long LS_M1 = LS_R1 + T * D;           //   [T] LN1 mean
+  static constexpr long LS_S1 = LS_M1 + T;               //   [T] LN1 rstd
+  static constexpr long LS_Y1 = LS_S1 + T;               //   [T][d] LN1 output
+  static constexpr long LS_F = LS_Y1 + T * D;            //   [T][64] FFN pre-activation
+  static constexpr long LS_R2 = LS_F + (long)T * FF;     //   [T][d] LN2 input
+  static constexpr long LS_M2 = LS_R2 + T * D;           //   [T] LN2 mean
+  static constexpr long LS_S2 = LS_M2 + T;               //   [T] LN2 rstd
+  static constexpr long LS_SIZE = LS_S2 + T;
+  static constexpr long S_XL = S_LAY + 2 * LS_SIZE;      // [T][d] encoder output
+  // backward temporaries
+  static constexpr long S_DX = S_XL + T * D;             // [T][d]
+  static constexpr long S_DY = S_DX + T * D;             // [T][d]
+  static constexpr long S_DF = S_DY + T * D;             // [T][64]
+  static constexpr long S_DQKV = S_DF + (long)T * FF;    // [T][3d]
+  static constexpr long S_DO = S_DQKV + 3L * T * D;      // [T][d]
+  static constexpr long S_DA = S_DO + T * D;             // [3][H][H]
+  static constexpr long S_DS = S_DA + 3L * H * H;        // [3][H] d(src score)
+  static constexpr long S_DT = S_DS + T;                 // [3][H] d(dst score)
+  static constexpr long S_SIZE = S_DT + T;
+
+  // ---- GAN scratch per window (floats) ----
+  static constexpr long GS_X = 0;                        // [GIN] gen input [emb; s]
+  static constexpr long GS_Z = GS_X + GIN;               // [2H^2] disc input [s; ns]
+  static constexpr long GS_H = GS_Z + DIN;               // [64] gen hidden
+  static constexpr long GS_T = GS_H + 64;                // [H^2] tanh
+  static constexpr long GS_DD = GS_T + H * H;            // [64] disc hidden
+  static constexpr long GS_P = GS_DD + 64;               // [2] (pad 4) probs
+  static constexpr long GS_DO = GS_P + 4;                // [2] (pad 4) d logits
+  static constexpr long GS_DDD = GS_DO + 4;              // [64] d disc hidden
+  static constexpr long GS_DY = GS_DDD + 64;             // [H^2] d gen pre-tanh
+  static constexpr long GS_DH = GS_DY + H * H;           // [64] d gen hidden
+  static constexpr long GS_SIZE = GS_DH + 64;
+};
+
+// AdamW descriptor: one per parameter tensor in the natural blob
+constexpr int kMaxTensors = 48;
+struct AdamTensor {
+  long off;       // offset in the master buffer (floats)
+  int n;          // elements
+  int active;     // got a gradient this step (torch skips params whose grad is None)
+  float step_size;  // lr / (1 - b1^step)
+  float bc2_sqrt;   // sqrt(1 - b2^step)
+};
+struct AdamArgs {
+  float* param;
+  float* grad;
+  float* m;
+  float* v;
+  float lr_wd;  // lr * weight_decay
+  float b1, b2, eps;
+  int ntensors;
+  AdamTensor t[kMaxTensors];
+};
+
+}  // namespace pgp

@@ -50,6 +50,18 @@ class DecisionModel:
             "pgp_load_weights")
         self.prototypes = np.asarray(weights["prototypes"], dtype=np.float64)
 
+    def load_master(self, P: torch.Tensor, prototypes):
+        """Rebuild the packed inference weights from device master weights
+        (natural fp32 layout, preganplus_amd.train.Trainer.P)."""
+        pr = np.ascontiguousarray(np.asarray(prototypes, dtype=np.float64))
+        L = self._L
+        L.pgp_load_weights_master.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_double)]
+        torch.cuda.synchronize(self.device)
+        _native.check(L.pgp_load_weights_master(self._h, ctypes.c_void_p(P.data_ptr()),
+                                                pr.ctypes.data_as(ctypes.POINTER(ctypes.c_double))),
+                      "pgp_load_weights_master")
+        self.prototypes = pr.copy()
+
     def reserve(self, max_batch: int):
         _native.check(self._L.pgp_reserve(self._h, int(max_batch)), "pgp_reserve")
 

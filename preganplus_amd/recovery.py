@@ -1,0 +1,194 @@
+"""Drop-in ``PreGANPlusRecovery`` for the COSCO framework/simulator on MI355X.
+
+Same constructor and ``run_model(time_series, original_decision)`` contract as
+``recovery/PreGANPlus.py:11-136`` (plugin base ``recovery/Recovery.py:3-14``):
+``setEnvironment(env)`` then one ``run_model`` per scheduling interval
+(``main.py:157``), reading ``env.stats.time_series`` / ``schedule_series`` /
+``runSimulation``, ``env.scheduler.result_cache``, ``env.hostlist`` and
+``env.containerlist`` by reference, returning a new decision list.
+
+Per call, as the reference:
+  1. detect + diagnose on the newest window (HIP inference kernels K1-K2b);
+     no anomaly -> the original decision (PreGANPlus.py:119-127);
+  2. ``train_gan`` (PreGANPlus.py:60-81): Gen/Disc forward, two simulator
+     scores, Disc step then Gen step (HIP training kernels + AdamW);
+  3. ``tune_model`` (PreGANPlus.py:51-58): 10 sequential tuning steps on the
+     latest window set (HIP);
+  4. ``recover_decision`` (PreGANPlus.py:83-105) with the updated GAN.
+Deliberate deviations: dropout is off (the reference runs its
+modules in train mode with p=0.1, so its own decisions are stochastic); no
+plotting; checkpoints are written only when ``save_folder`` is set.
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import torch
+
+from . import train as TR
+from . import weights as W
+from .model import DecisionModel, to_numpy
+
+COEFF_ENERGY, COEFF_LATENCY = 0.8, 0.2  # constants.py:19-20
+_DATA = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data")
+
+
+class Recovery:
+    """recovery/Recovery.py:3-14."""
+
+    def __init__(self):
+        self.env = None
+        self.env_name = ""
+        self.model = None
+        self.latent = None
+
+    def setEnvironment(self, env):
+        self.env = env
+
+    def run_model(self, time_series, original_decision):
+        return original_decision
+
+
+class PreGANPlusRecovery(Recovery):
+    def __init__(self, hosts, env, training=False, device=None, model_folder=None, save_folder=None,
+                 weights=None, extra=None):
+        super().__init__()
+        self.model_name = f"Transformer_{hosts}"
+        self.gen_name = f"Gen_{hosts}"
+        self.disc_name = f"Disc_{hosts}"
+        self.hosts = hosts
+        self.env_name = "simulator" if env == "" else "framework"
+        self.training = training
+        self.save_gan = save_folder is not None
+        self.save_folder = save_folder
+        self.device = torch.device(device or "cuda")
+        self.load_models(model_folder, weights, extra)
+
+    # -- PreGANPlus.py:23-37 --
+    def load_models(self, model_folder=None, weights=None, extra=None):
+        if weights is None:
+            folder = model_folder or "recovery/PreGANSrc/checkpointsplus"
+            ck = os.path.join(folder, f"{self.env_name}_{self.model_name}.ckpt")
+            if os.path.exists(ck):
+                weights = W.load_reference_checkpoints(folder, self.env_name, self.hosts)
+                extra = extra or {}
+            else:
+                packaged = os.path.join(_DATA, f"{self.env_name}_{self.hosts}.npz")
+                if not os.path.exists(packaged):
+                    raise FileNotFoundError(f"no checkpoint for {self.model_name} in {folder} or {packaged}")
+                weights, extra = W.load_npz(packaged)
+        self.extra = extra or {}
+        self.prototypes = np.asarray(weights["prototypes"], dtype=np.float64)
+        self.infer = DecisionModel(self.hosts, weights, device=self.device)
+        self.trainer = TR.Trainer(self.hosts, weights, self.extra, device=self.device)
+        self.tune_state = TR.TuneState(self.prototypes)
+        self.epoch = int(self.extra.get(f"meta/gen/epoch", 0))
+        self.accuracy_list = []
+        if "train_time_data" in self.extra:
+            self.train_time_data = np.asarray(self.extra["train_time_data"], dtype=np.float64)
+        else:
+            self.train_time_data = np.load(os.path.join("recovery/PreGANSrc/data", self.env_name, "time_series.npy"))
+
+    # -- PreGANPlus.py:107-113 --
+    def input_window(self):
+        td = TR.normalize_test_time_data(self.env.stats.time_series, self.train_time_data)
+        if td.shape[0] >= 3:
+            td = td[-3:]
+        return TR.convert_to_windows(td)[-1]
+
+    def _score(self, schedule):
+        e, r = self.env.stats.runSimulation(torch.tensor(schedule))  # utils.py:97-100
+        return COEFF_ENERGY * e + COEFF_LATENCY * r
+
+    # -- PreGANPlus.py:60-81 --
+    def train_gan(self, embedding, schedule_data):
+        ns, new_score, orig_score = TR.train_gan(self.trainer, embedding, schedule_data, self._score)
+        self.epoch += 1
+        return ns
+
+    # -- PreGANPlus.py:51-58 --
+    def tune_model(self):
+        wins, _, anom, cls = TR.on_the_fly_dataset(self.env.stats.time_series, self.env.stats.schedule_series,
+                                                   self.train_time_data)
+        losses = TR.backprop(self.trainer, self.tune_state, wins, anom, cls)
+        self.accuracy_list.append((float(np.mean([a for a, _ in losses]) + np.mean([t for _, t in losses])),
+                                   self.tune_state.factor + TR.PROTO_UPDATE_MIN))
+        return losses
+
+    def sync_inference_weights(self):
+        """Rebuild the inference kernels' packed weights from the trained master."""
+        self.infer.load_master(self.trainer.P, self.tune_state.protos)
+        self.prototypes = self.tune_state.protos.copy()
+
+    # -- PreGANPlus.py:83-105 --
+    def recover_decision(self, embedding, schedule_data, original_decision):
+        _, probs = self.trainer.gan_forward(np.asarray(embedding)[None], np.asarray(schedule_data)[None])
+        p = probs[0].cpu().numpy()
+        if p[0] > p[1]:
+            return original_decision
+        host_alloc = [[] for _ in range(len(self.env.hostlist))]
+        container_alloc = [-1] * len(self.env.hostlist)
+        for c in self.env.containerlist:
+            if c and c.getHostID() != -1:
+                host_alloc[c.getHostID()].append(c.id)
+                container_alloc[c.id] = c.getHostID()
+        decision = dict(original_decision)
+        self.hosts_from = [0] * self.hosts
+        s = np.asarray(schedule_data)
+        for cids in host_alloc:
+            for cid in cids:
+                row = s[int(cid)].tolist()
+                new_host = row.index(max(row))
+                if container_alloc[cid] != new_host:
+                    decision[cid] = new_host
+                    self.hosts_from[container_alloc[cid]] = 1
+        return list(decision.items())
+
+    # -- PreGANPlus.py:115-136 --
+    def run_model(self, time_series, original_decision):
+        schedule_data = np.asarray(self.env.scheduler.result_cache, dtype=np.float64)
+        win = self.input_window()
+        dev = self.infer.device
+        out = to_numpy(self.infer.forward(torch.tensor(win[None], dtype=torch.float32, device=dev),
+                                          torch.tensor(schedule_data[None], dtype=torch.float32, device=dev)))
+        if not out["any"][0]:
+            return original_decision
+        anom = out["logits"][0, :, 1] > out["logits"][0, :, 0]
+        embedding = np.where(anom[:, None], out["protos"][0], 0.0)
+        self.classes = out["cls"][0].tolist()
+        self.train_gan(embedding, schedule_data)
+        self.tune_model()
+        self.sync_inference_weights()
+        if self.save_gan:
+            self.save_checkpoints(self.save_folder)
+        return self.recover_decision(embedding, schedule_data, original_decision)
+
+    # -- utils.py:49-58 (checkpoint dict), written with torch.save --
+    def save_checkpoints(self, folder):
+        os.makedirs(folder, exist_ok=True)
+        w = self.trainer.weights_numpy()
+        p = self.trainer.P.detach().cpu().numpy()
+        mm, vv = self.trainer.m.cpu().numpy(), self.trainer.v.cpu().numpy()
+        for sec, name, proto in (("transformer", self.model_name, self.tune_state.protos),
+                                 ("gen", self.gen_name, None), ("disc", self.disc_name, None)):
+            state, idx = {}, 0
+            for t in self.trainer.tensors:
+                if t["section"] != sec or not t["trainable"]:
+                    continue
+                sl = slice(t["offset"], t["offset"] + t["n"])
+                shp = w[sec][t["name"]].shape
+                state[idx] = {"step": torch.tensor(float(t["step"])),
+                              "exp_avg": torch.tensor(mm[sl].astype(np.float64).reshape(shp)),
+                              "exp_avg_sq": torch.tensor(vv[sl].astype(np.float64).reshape(shp))}
+                idx += 1
+            ck = {"epoch": self.epoch,
+                  "model_state_dict": {k: torch.tensor(v) for k, v in w[sec].items()},
+                  "model_prototypes": [torch.tensor(x) for x in proto] if proto is not None else {},
+                  "optimizer_state_dict": {"state": state, "param_groups": [{
+                      "lr": self.trainer.lrs[sec], "betas": (self.trainer.b1, self.trainer.b2),
+                      "eps": self.trainer.eps, "weight_decay": self.trainer.wd, "amsgrad": False,
+                      "params": list(range(idx))}]},
+                  "accuracy_list": list(self.accuracy_list)}
+            torch.save(ck, os.path.join(folder, f"{self.env_name}_{name}.ckpt"))
+        del p

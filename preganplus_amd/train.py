@@ -1,0 +1,340 @@
+"""Online training on MI355X: host side of the tuning and GAN steps.
+
+Mirrors the reference's training code (recovery/PreGANSrc/src/train.py:13-57,
+recovery/PreGANPlus.py:51-81, utils.py:65) with every tensor operation in the
+HIP library (``pgp_tune_*``, ``pgp_gan_*``, ``pgp_adamw``).  What stays on the
+host is the reference's own scalar, sequential bookkeeping — the per-host loop
+of ``custom_loss`` that decides CE weights (num_zero/num_ones) and the
+prototype EMA of ``triplet_loss`` (it depends on the forward's outputs and must
+run host-by-host in order) — exactly as the reference runs it in Python.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+
+import numpy as np
+import torch
+
+from . import _native
+from . import weights as W
+
+PROTO_UPDATE_FACTOR = 0.2   # constants.py:13
+PROTO_UPDATE_MIN = 0.02     # constants.py:14
+PROTO_FACTOR_DECAY = 0.995  # constants.py:15
+LATEST_WINDOW_SIZE = 10     # constants.py:16
+PERCENTILES = 98            # constants.py:11
+
+
+class _AdamTensor(ctypes.Structure):
+    _fields_ = [("offset", ctypes.c_longlong), ("n", ctypes.c_int), ("active", ctypes.c_int),
+                ("step_size", ctypes.c_float), ("bc2_sqrt", ctypes.c_float)]
+
+
+def default_lrs(H):
+    """Model lr attributes: Transformer_16.lr = 1e-4 (models.py:318); Gen/Disc
+    5e-5 at 16 hosts (:122, :140), 3e-5 at 50 (:262, :280)."""
+    g = 5e-5 if H <= 16 else 3e-5
+    return {"transformer": 1e-4, "gen": g, "disc": g}
+
+
+class Trainer:
+    """fp32 master weights in the natural blob order (prototypes excluded),
+    gradients and AdamW moments, all on the device."""
+
+    SECTIONS = ("transformer", "gen", "disc")
+
+    def __init__(self, H: int, weights: dict, extra: dict | None = None, lrs: dict | None = None,
+                 device="cuda", max_batch: int = 16, weight_decay=1e-5, betas=(0.9, 0.999), eps=1e-8):
+        self.H = int(H)
+        self.device = torch.device(device)
+        if self.device.type == "cuda" and self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
+        L = _native.lib()
+        self._L = L
+        self._bind()
+        n = L.pgp_master_len(self.H)
+        if n == 0:
+            raise ValueError(f"H={H} not compiled in")
+        blob = W.pack_blob(weights, self.H)[:n]
+        dev = self.device
+        self.P = torch.tensor(blob, dtype=torch.float32, device=dev)
+        self.G = torch.zeros_like(self.P)
+        self.m = torch.zeros_like(self.P)
+        self.v = torch.zeros_like(self.P)
+        self.lrs = dict(default_lrs(self.H), **(lrs or {}))
+        self.wd, self.b1, self.b2, self.eps = weight_decay, betas[0], betas[1], eps
+        # tensor table in blob order
+        self.tensors = []
+        off = 0
+        for sec, name, shp in W.blob_layout(self.H)[:-1]:
+            cnt = int(np.prod(shp))
+            self.tensors.append({"section": sec, "name": name, "offset": off, "n": cnt, "step": 0.0,
+                                 "trainable": name != "pos_encoder.pe"})
+            off += cnt
+        assert off == n
+        if extra:
+            m = self.m.cpu().numpy()
+            v = self.v.cpu().numpy()
+            for t in self.tensors:
+                key = f"opt/{t['section']}/{t['name']}"
+                if f"{key}/exp_avg" in extra:
+                    m[t["offset"]:t["offset"] + t["n"]] = np.asarray(extra[f"{key}/exp_avg"]).reshape(-1)
+                    v[t["offset"]:t["offset"] + t["n"]] = np.asarray(extra[f"{key}/exp_avg_sq"]).reshape(-1)
+                    t["step"] = float(extra[f"{key}/step"])
+            self.m.copy_(torch.tensor(m))
+            self.v.copy_(torch.tensor(v))
+        self.sec_off = {s: int(L.pgp_master_offset(self.H, i)) for i, s in enumerate(self.SECTIONS)}
+        self.sec_end = {"transformer": self.sec_off["gen"], "gen": self.sec_off["disc"], "disc": n}
+        self._alloc(max_batch)
+
+    def _bind(self):
+        L = self._L
+        if getattr(L, "_pgp_train_bound", False):
+            return
+        vp, i32, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
+        L.pgp_master_len.argtypes = [i32]
+        L.pgp_master_len.restype = sz
+        L.pgp_master_offset.argtypes = [i32, i32]
+        L.pgp_master_offset.restype = sz
+        L.pgp_tune_scratch_len.argtypes = [i32]
+        L.pgp_tune_scratch_len.restype = sz
+        L.pgp_gan_scratch_len.argtypes = [i32]
+        L.pgp_gan_scratch_len.restype = sz
+        L.pgp_tune_forward.argtypes = [i32, i32] + [vp] * 6 + [vp]
+        L.pgp_tune_backward.argtypes = [i32, i32] + [vp] * 10 + [vp]
+        L.pgp_gan_forward.argtypes = [i32, i32] + [vp] * 6 + [vp]
+        L.pgp_gan_disc_backward.argtypes = [i32, i32] + [vp] * 4 + [vp]
+        L.pgp_gan_gen_backward.argtypes = [i32, i32] + [vp] * 3 + [vp]
+        L.pgp_adamw.argtypes = [vp] * 4 + [ctypes.c_float] * 5 + [ctypes.POINTER(_AdamTensor), i32, vp]
+        L.pgp_load_weights_master.argtypes = [vp, vp, ctypes.POINTER(ctypes.c_double)]
+        for f in ("pgp_tune_forward", "pgp_tune_backward", "pgp_gan_forward", "pgp_gan_disc_backward",
+                  "pgp_gan_gen_backward", "pgp_adamw", "pgp_load_weights_master"):
+            getattr(L, f).restype = i32
+        L._pgp_train_bound = True
+
+    def _alloc(self, B):
+        H, dev, L = self.H, self.device, self._L
+        f32 = torch.float32
+        self.cap = B
+        self.scr = torch.zeros((B, L.pgp_tune_scratch_len(H)), dtype=f32, device=dev)
+        self.gscr = torch.zeros((B, L.pgp_gan_scratch_len(H)), dtype=f32, device=dev)
+        self.lat = torch.zeros((B, 3 * H * H), dtype=f32, device=dev)
+        self.logits = torch.zeros((B, H, 2), dtype=f32, device=dev)
+        self.protos = torch.zeros((B, H, 2), dtype=f32, device=dev)
+        self.dpre = torch.zeros((B, 4 * H), dtype=f32, device=dev)
+        self.ns = torch.zeros((B, H, H), dtype=f32, device=dev)
+        self.probs = torch.zeros((B, 2), dtype=f32, device=dev)
+
+    def _ensure(self, B):
+        if B > self.cap:
+            self._alloc(B)
+
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    # ---------------- ops ----------------
+    def zero_grad(self, section: str):
+        self.G[self.sec_off[section]:self.sec_end[section]].zero_()
+
+    def tune_forward(self, windows: torch.Tensor):
+        B = windows.shape[0]
+        self._ensure(B)
+        windows = windows.to(self.device, torch.float32).contiguous()
+        _native.check(self._L.pgp_tune_forward(
+            self.H, B, windows.data_ptr(), self.P.data_ptr(), self.scr.data_ptr(), self.lat.data_ptr(),
+            self.logits.data_ptr(), self.protos.data_ptr(), self._stream()), "pgp_tune_forward")
+        return self.logits[:B], self.protos[:B]
+
+    def tune_backward(self, B, y, mult, tgt):
+        """y [B,H] int, mult [B,H], tgt [B,H,2] (host arrays or tensors)."""
+        dev = self.device
+        y = torch.as_tensor(np.asarray(y), dtype=torch.int32).to(dev).contiguous()
+        mult = torch.as_tensor(np.asarray(mult), dtype=torch.float32).to(dev).contiguous()
+        tgt = torch.as_tensor(np.asarray(tgt), dtype=torch.float32).to(dev).contiguous()
+        self.zero_grad("transformer")
+        _native.check(self._L.pgp_tune_backward(
+            self.H, B, self.P.data_ptr(), self.G.data_ptr(), self.scr.data_ptr(), self.lat.data_ptr(),
+            self.logits.data_ptr(), self.protos.data_ptr(), y.data_ptr(), mult.data_ptr(), tgt.data_ptr(),
+            self.dpre.data_ptr(), self._stream()), "pgp_tune_backward")
+
+    def gan_forward(self, emb, sched):
+        emb = torch.as_tensor(np.asarray(emb) if not torch.is_tensor(emb) else emb, dtype=torch.float32)
+        sched = torch.as_tensor(np.asarray(sched) if not torch.is_tensor(sched) else sched, dtype=torch.float32)
+        emb = emb.to(self.device).reshape(emb.shape[0], -1).contiguous()
+        sched = sched.to(self.device).contiguous()
+        B = sched.shape[0]
+        self._ensure(B)
+        self._gan_in = (emb, sched)
+        _native.check(self._L.pgp_gan_forward(
+            self.H, B, emb.data_ptr(), sched.data_ptr(), self.P.data_ptr(), self.gscr.data_ptr(),
+            self.ns.data_ptr(), self.probs.data_ptr(), self._stream()), "pgp_gan_forward")
+        return self.ns[:B], self.probs[:B]
+
+    def gan_disc_backward(self, target):
+        target = torch.as_tensor(np.asarray(target), dtype=torch.float32).to(self.device).contiguous()
+        B = target.shape[0]
+        self.zero_grad("disc")
+        _native.check(self._L.pgp_gan_disc_backward(
+            self.H, B, target.data_ptr(), self.P.data_ptr(), self.G.data_ptr(), self.gscr.data_ptr(),
+            self._stream()), "pgp_gan_disc_backward")
+
+    def gan_gen_backward(self, B):
+        self.zero_grad("gen")
+        _native.check(self._L.pgp_gan_gen_backward(
+            self.H, B, self.P.data_ptr(), self.G.data_ptr(), self.gscr.data_ptr(), self._stream()),
+            "pgp_gan_gen_backward")
+
+    def adam_step(self, section: str, inactive: tuple = ()):
+        """torch.optim.AdamW.step for the tensors of `section` (utils.py:65);
+        tensors named in `inactive` had no gradient and are skipped, as torch
+        skips params whose .grad is None."""
+        lr = self.lrs[section]
+        arr = []
+        for t in self.tensors:
+            if t["section"] != section or not t["trainable"]:
+                continue
+            active = t["name"] not in inactive
+            if active:
+                t["step"] += 1
+            st = max(t["step"], 1.0)
+            arr.append(_AdamTensor(t["offset"], t["n"], int(active), lr / (1 - self.b1 ** st),
+                                   math.sqrt(1 - self.b2 ** st)))
+        desc = (_AdamTensor * len(arr))(*arr)
+        _native.check(self._L.pgp_adamw(
+            ctypes.c_void_p(self.P.data_ptr()), ctypes.c_void_p(self.G.data_ptr()),
+            ctypes.c_void_p(self.m.data_ptr()), ctypes.c_void_p(self.v.data_ptr()),
+            lr, self.wd, self.b1, self.b2, self.eps, desc, len(arr), self._stream()), "pgp_adamw")
+
+    def all_reduce_grads(self, section: str, group=None):
+        """Data-parallel tuning: sum the section's gradients over
+        ranks with one flat RCCL all-reduce before the identical AdamW step."""
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            dist.all_reduce(self.G[self.sec_off[section]:self.sec_end[section]], group=group)
+
+    def weights_numpy(self) -> dict:
+        """Master weights as reference-named float64 arrays."""
+        p = self.P.detach().cpu().numpy().astype(np.float64)
+        out = {s: {} for s in self.SECTIONS}
+        shapes = {(sec, name): shp for sec, name, shp in W.blob_layout(self.H)[:-1]}
+        for t in self.tensors:
+            out[t["section"]][t["name"]] = p[t["offset"]:t["offset"] + t["n"]].reshape(
+                shapes[(t["section"], t["name"])])
+        return out
+
+
+# ---------------------------------------------------------------------------
+# host-side sequential logic of custom_loss / triplet_loss (train.py:13-40)
+# ---------------------------------------------------------------------------
+class TuneState:
+    """train.py's module globals (PROTO_UPDATE_FACTOR, num_zero, num_ones) and
+    model.prototype, per model instance."""
+
+    def __init__(self, prototypes, factor=PROTO_UPDATE_FACTOR):
+        self.protos = np.array(prototypes, dtype=np.float64)
+        self.factor = float(factor)
+        self.num_zero, self.num_ones = 1, 1
+
+
+def loss_targets(logits, protos, y, c, st: TuneState):
+    """One window: CE weights, positive prototype targets, loss values; updates
+    the prototype EMA and counters in reference order (train.py:27-40)."""
+    H = logits.shape[0]
+    mult = np.ones(H)
+    tgt = np.zeros((H, 2))
+    nz = no = 0
+    aloss = 0.0
+    for i in range(H):
+        mult[i] = 1.0 if y[i] == 0 else st.num_zero / st.num_ones
+        nz += 1
+        no += 1 if y[i] == 1 else 0
+        l = logits[i].astype(np.float64)
+        m = l.max()
+        aloss += (np.log(np.exp(l - m).sum()) + m - l[int(y[i])]) * mult[i]
+    tloss = 0.0
+    for i in range(H):
+        if y[i] > 0:
+            cc = int(c[i])
+            a = protos[i].astype(np.float64)
+            tgt[i] = st.protos[cc]
+            pos = float(np.mean((a - st.protos[cc]) ** 2))
+            negs = [float(np.mean((a - st.protos[nc]) ** 2)) for nc in (0, 1, 2) if nc != cc]
+            tloss += pos - sum(negs)
+            if pos <= negs[0] and pos <= negs[1]:
+                f = st.factor + PROTO_UPDATE_MIN
+                st.protos[cc] = f * a + (1 - f) * st.protos[cc]
+    st.factor *= PROTO_FACTOR_DECAY
+    st.num_zero += nz
+    st.num_ones += no
+    return mult, tgt, aloss, tloss
+
+
+def normalize_test_time_data(time_data, train_time_data):
+    """utils.py:94-95."""
+    return np.asarray(time_data, dtype=np.float64) / (np.max(train_time_data, axis=0) + 1e-8)
+
+
+def convert_to_windows(data, n_window=3):
+    """utils.py:7-14."""
+    data = np.asarray(data, dtype=np.float64)
+    out = []
+    for i in range(data.shape[0]):
+        if i >= n_window:
+            out.append(data[i - n_window:i])
+        else:
+            out.append(np.concatenate([np.repeat(data[0:1], n_window - i, axis=0), data[0:i]]))
+    return np.stack(out)
+
+
+def form_test_dataset(data):
+    """utils.py:16-24."""
+    anomaly_per_dim = data > np.percentile(data, PERCENTILES, axis=0)
+    which, anydim = [], []
+    for i in range(0, data.shape[1], 3):
+        which.append(np.argmax(data[:, i:i + 3] + 0, axis=1))
+        anydim.append(np.logical_or.reduce(anomaly_per_dim[:, i:i + 3], axis=1))
+    return np.stack(anydim, axis=1) + 0, np.stack(which, axis=1)
+
+
+def on_the_fly_dataset(time_series, schedule_series, train_time_data):
+    """utils.py:40-47: the last 10 rows, normalised; windows and labels."""
+    td = normalize_test_time_data(np.asarray(time_series)[-LATEST_WINDOW_SIZE:], train_time_data)
+    sched = np.asarray(schedule_series)[-LATEST_WINDOW_SIZE:]
+    anom, cls = form_test_dataset(td)
+    return convert_to_windows(td), sched, anom, cls
+
+
+def backprop(tr: Trainer, st: TuneState, wins, anom, cls):
+    """train.py:42-57: sequential batch-1 steps (forward, custom_loss, backward,
+    AdamW).  Returns the per-window (aloss, tloss)."""
+    st.num_zero, st.num_ones = 1, 1
+    losses = []
+    for i in range(wins.shape[0]):
+        logits, protos = tr.tune_forward(torch.as_tensor(wins[i:i + 1], dtype=torch.float32))
+        lg = logits[0].cpu().numpy()
+        pr = protos[0].cpu().numpy()
+        mult, tgt, aloss, tloss = loss_targets(lg, pr, anom[i], cls[i], st)
+        tr.tune_backward(1, anom[i][None], mult[None], tgt[None])
+        inactive = () if np.any(anom[i] > 0) else ("prototype_decoder.0.weight", "prototype_decoder.0.bias")
+        tr.adam_step("transformer", inactive)
+        losses.append((aloss, tloss))
+    return losses
+
+
+def bce_target(new_score, orig_score):
+    """PreGANPlus.py:65-66: label [0,1] if the generator's schedule scores no
+    worse than the original, else [1,0]."""
+    return [0.0, 1.0] if new_score <= orig_score else [1.0, 0.0]
+
+
+def train_gan(tr: Trainer, emb, sched, simulate):
+    """PreGANPlus.py:60-75 (one window).  simulate(schedule ndarray) -> score."""
+    ns, probs = tr.gan_forward(np.asarray(emb)[None], np.asarray(sched)[None])
+    ns_h = ns[0].cpu().numpy().astype(np.float64)
+    new_score, orig_score = simulate(ns_h), simulate(np.asarray(sched, dtype=np.float64))
+    tr.gan_disc_backward(np.array([bce_target(new_score, orig_score)]))
+    tr.adam_step("disc")
+    tr.gan_gen_backward(1)
+    tr.adam_step("gen")
+    return ns_h, new_score, orig_score
