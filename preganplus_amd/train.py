@@ -130,6 +130,10 @@ class Trainer:
         if B > self.cap:
             self._alloc(B)
 
+    def _dev(self, a, dtype):
+        t = a if torch.is_tensor(a) else torch.as_tensor(np.asarray(a))
+        return t.to(self.device, dtype).contiguous()
+
     def _stream(self):
         return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
 
@@ -148,10 +152,9 @@ class Trainer:
 
     def tune_backward(self, B, y, mult, tgt):
         """y [B,H] int, mult [B,H], tgt [B,H,2] (host arrays or tensors)."""
-        dev = self.device
-        y = torch.as_tensor(np.asarray(y), dtype=torch.int32).to(dev).contiguous()
-        mult = torch.as_tensor(np.asarray(mult), dtype=torch.float32).to(dev).contiguous()
-        tgt = torch.as_tensor(np.asarray(tgt), dtype=torch.float32).to(dev).contiguous()
+        y = self._dev(y, torch.int32)
+        mult = self._dev(mult, torch.float32)
+        tgt = self._dev(tgt, torch.float32)
         self.zero_grad("transformer")
         _native.check(self._L.pgp_tune_backward(
             self.H, B, self.P.data_ptr(), self.G.data_ptr(), self.scr.data_ptr(), self.lat.data_ptr(),
@@ -159,10 +162,9 @@ class Trainer:
             self.dpre.data_ptr(), self._stream()), "pgp_tune_backward")
 
     def gan_forward(self, emb, sched):
-        emb = torch.as_tensor(np.asarray(emb) if not torch.is_tensor(emb) else emb, dtype=torch.float32)
-        sched = torch.as_tensor(np.asarray(sched) if not torch.is_tensor(sched) else sched, dtype=torch.float32)
-        emb = emb.to(self.device).reshape(emb.shape[0], -1).contiguous()
-        sched = sched.to(self.device).contiguous()
+        emb = self._dev(emb, torch.float32)
+        emb = emb.reshape(emb.shape[0], -1).contiguous()
+        sched = self._dev(sched, torch.float32)
         B = sched.shape[0]
         self._ensure(B)
         self._gan_in = (emb, sched)
@@ -172,7 +174,7 @@ class Trainer:
         return self.ns[:B], self.probs[:B]
 
     def gan_disc_backward(self, target):
-        target = torch.as_tensor(np.asarray(target), dtype=torch.float32).to(self.device).contiguous()
+        target = self._dev(target, torch.float32)
         B = target.shape[0]
         self.zero_grad("disc")
         _native.check(self._L.pgp_gan_disc_backward(
