@@ -89,15 +89,18 @@ def main():
     ap.add_argument("--batch", type=int, default=65536, help="windows per GPU per step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
-    ap.add_argument("--config", choices=["c2", "fleet", "tune"], default="c2",
+    ap.add_argument("--config", choices=["c2", "fleet", "tune", "fpe"], default="c2",
                     help="c2: BASELINE config 2 (default, the headline line); fleet: config 5 "
                          "(1024-host fleet = 64 cells of 16 hosts, shipped weights); tune: config 3 "
-                         "(tuning step fwd+bwd+AdamW, data-parallel with an RCCL all-reduce)")
+                         "(tuning step fwd+bwd+AdamW, data-parallel with an RCCL all-reduce); fpe: config 4 "
+                         "(PreGAN FPE_16 encoder + K=3 classifier + PreGAN's Gen/Disc, shipped weights)")
     args = ap.parse_args()
     if args.config == "fleet":
         return bench_fleet(args)
     if args.config == "tune":
         return bench_tune(args)
+    if args.config == "fpe":
+        return bench_fpe(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -292,6 +295,103 @@ def bench_tune(args):
             "vs_baseline": None, "dtype": "fp32", "data": "synthetic windows, labels and targets",
             "config": {"workload": f"C3: tuning step, {H} hosts, {B} windows per GPU", "hosts": H,
                        "windows_per_gpu": B, "parallelism": f"dp{world} + RCCL all-reduce"}}), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+
+def fpe_cpu_baseline(weights, budget_s=12.0, max_threads=16):
+    """numpy fp64 FPE oracle on the host cores, bounded sample (C4)."""
+    from threadpoolctl import threadpool_limits
+    from oracle import pregan_oracle as O  # CPU baseline leg only
+    threads = min(max_threads, os.cpu_count() or 1)
+    rng = np.random.Generator(np.random.PCG64(98))
+    nb, H = 256, 16
+    x = rng.uniform(0, 0.6, size=(nb, 3, 3 * H))
+    h0 = rng.standard_normal((nb, 3))
+    s = np.zeros((nb, H, H))
+    s[np.arange(nb)[:, None], np.arange(H)[None, :], rng.integers(0, H, size=(nb, H))] = 1.0
+    done = 0
+    with threadpool_limits(limits=threads):
+        O.forward_fpe(weights, x[:8], h0[:8], s[:8])
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < budget_s:
+            O.forward_fpe(weights, x, h0, s)
+            done += nb
+    dt = time.perf_counter() - t0
+    return {"value": done * H / dt, "unit": "host-windows/s", "cores": threads, "kind": "port",
+            "sample": f"{done} windows (H=16, batches of {nb}), numpy fp64 FPE oracle, {dt:.1f}s"}
+
+
+def bench_fpe(args):
+    """BASELINE config 4: PreGAN's FPE_16 path (K4 + K3), shipped checkpoints/
+    weights, 64k synthetic windows per GPU (C2 distribution at H=16), GRU h0
+    ~ N(0,1) as an input.  H=16: the reference defines FPE_16 only."""
+    from preganplus_amd.model import FPEDecisionModel
+    world, rank, device = _dist_setup()
+    H, B = 16, args.batch
+    w, _ = W.load_npz(os.path.join(ROOT, "preganplus_amd", "data", "pregan_simulator_16.npz"))
+    model = FPEDecisionModel(H, w, device=device)
+    model.reserve(B)
+    x, s = synth_inputs(B, H, device, 4321 + rank)
+    g = torch.Generator(device=device).manual_seed(77 + rank)
+    h0 = torch.randn((B, 3), generator=g, device=device).contiguous()
+    out = model.alloc_outputs(B)
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    it = iter(range(args.steps))
+
+    def step(timed=False):
+        if not timed:
+            model.forward(x, h0, s, out=out)
+            return
+        e = evs[next(it)]
+        e[0].record()
+        model.forward(x, h0, s, out=out, stage=0)
+        e[1].record()
+        model.forward(x, h0, s, out=out, stage=1)
+        e[2].record()
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    elapsed = _timed(world, device, lambda: step(True), args.steps)
+    k = np.array([[e[0].elapsed_time(e[1]), e[1].elapsed_time(e[2])] for e in evs]).mean(axis=0)
+    if rank == 0:
+        fpe_bytes = R.fpe_bytes_per_window(H) * B
+        gan_fl = R.gan_flops_per_window(H) * B
+        dom_fpe = k[0] >= k[1]
+        if dom_fpe:
+            ach = fpe_bytes / (k[0] * 1e-3) / 1e9
+            roof = {"kernel": "fpe_kernel (K4)", "bound": "hbm", "achieved": ach, "peak": R.PEAK_HBM_GBS,
+                    "unit": "GB/s", "frac": ach / R.PEAK_HBM_GBS, "traffic": None,
+                    "bytes_per_window": R.fpe_bytes_per_window(H)}
+        else:
+            ach = gan_fl / (k[1] * 1e-3) / 1e12
+            roof = {"kernel": "gan_kernel (K3)", "bound": "mfma", "achieved": ach, "peak": R.PEAK_FP32_TFLOPS,
+                    "unit": "TFLOP/s", "frac": ach / R.PEAK_FP32_TFLOPS, "traffic": None,
+                    "flops_per_window": R.gan_flops_per_window(H)}
+        res = {
+            "metric": "host-windows/sec (detect+diagnose+generate)",
+            "value": B * world * H * args.steps / elapsed, "unit": "host-windows/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "fp32",
+            "data": "synthetic windows (SURVEY §8d C2 distribution at H=16), h0 ~ N(0,1); "
+                    "shipped checkpoints/ FPE_16, Gen_16, Disc_16 weights",
+            "config": {"workload": f"C4: PreGAN FPE_16 encoder + K=3 classifier + GAN, {B} windows per GPU, fp32",
+                       "hosts": H, "windows_per_gpu": B, "parallelism": f"dp{world} (independent windows)"},
+            "kernel_ms": {"fpe": k[0], "gan": k[1]},
+            "kernel_rates": {"fpe_gbs": fpe_bytes / (k[0] * 1e-3) / 1e9,
+                             "fpe_gflops": R.fpe_flops_per_window(H) * B / (k[0] * 1e-3) / 1e9,
+                             "gan_tflops": gan_fl / (k[1] * 1e-3) / 1e12},
+            "roofline": roof,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            log("timing CPU baseline ...")
+            res["cpu_baseline"] = fpe_cpu_baseline(w, args.cpu_budget)
+        else:
+            res["cpu_baseline"] = None
+        print(json.dumps(res), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
 

@@ -121,6 +121,40 @@ int pgp_forward_stage(pgp_model* m, int stage, int batch, const float* windows,
                       int* gen_target, float* latent, void* stream);
 
 /* ------------------------------------------------------------------------
+ * PreGAN (FPE) variant — BASELINE config C4, SURVEY.md §8 a14.
+ * Replaces PreGANRecovery.run_encoder + the GAN half of run_model
+ * (recovery/PreGAN.py:97-126): FPE_16.forward (models.py:65-115), detect
+ * (argmax of each host's softmax, :110-111), embedding + get_classes over the
+ * K = 3 prototypes (:119-120), Gen_16/Disc_16 (recover_decision, :74-77).
+ * ---------------------------------------------------------------------- */
+/* A PreGAN model for H hosts (H = 16 only: the reference defines FPE_16 alone). */
+int pgp_create_fpe(int n_hosts, pgp_model** out);
+/* Doubles pgp_load_weights expects for an FPE model, row-major in this order:
+ *   FPE: gru.weight_ih_l0 [9,3H], gru.weight_hh_l0 [9,3], gru.bias_ih_l0 [9],
+ *     gru.bias_hh_l0 [9], gat.layer1.heads.0.fc.weight [H,3],
+ *     ...attn_fc.weight [1,2H], mha.in_proj_weight [3E,E], mha.in_proj_bias [3E],
+ *     mha.out_proj.weight [E,E], mha.out_proj.bias [E] (E = H+3),
+ *     encoder.0.weight [10H,3E], encoder.0.bias [10H],
+ *     anomaly_decoder.0.weight [2,10], .bias [2],
+ *     prototype_decoder.0.weight [2,10], .bias [2]
+ *   Gen, Disc: as pgp_load_weights;  prototypes [3,2]. */
+size_t pgp_fpe_weight_blob_len(int n_hosts);
+/* Device pointers:
+ *   in  windows [B,3,3H], h0 [B,3] (the GRU state the reference draws with
+ *       torch.randn, models.py:70), sched [B,C,H]
+ *   out scores [B,H,2] anomaly softmax, protos [B,H,2], cls [B,H] (-1: none),
+ *       any_anom [B], probs [B,2], keep_orig [B], final_target [B,C],
+ *       gen_target [B,C]  (as pgp_forward) */
+int pgp_forward_fpe(pgp_model* m, int batch, const float* windows, const float* h0, const float* sched,
+                    float* scores, float* protos, int* cls, int* any_anom, float* probs, int* keep_orig,
+                    int* final_target, int* gen_target, void* stream);
+/* Per-kernel launches of pgp_forward_fpe: stage 0 = K4 (FPE encoder, decoders,
+ * detect, classify), 1 = K3 (GAN + decisions), -1 = both; in order, one stream. */
+int pgp_forward_fpe_stage(pgp_model* m, int stage, int batch, const float* windows, const float* h0,
+                          const float* sched, float* scores, float* protos, int* cls, int* any_anom, float* probs,
+                          int* keep_orig, int* final_target, int* gen_target, void* stream);
+
+/* ------------------------------------------------------------------------
  * Online training ops (stateless; buffers owned by the caller, device memory).
  * Master weights `P` are fp32 in the NATURAL blob order of pgp_load_weights
  * (transformer | gen | disc, prototypes excluded); grads `G` share the layout.

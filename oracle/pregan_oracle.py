@@ -326,3 +326,73 @@ def positional_encoding(d_model, max_len=N_WINDOW):
     pe[:, 0::2] = np.sin(position * div)
     pe[:, 1::2] = np.cos(position * div)
     return pe.astype(np.float64)[:, None, :]
+
+
+# ----------------------------------------------------------------------------
+# PreGAN's FPE_16 encoder (models.py:10-115) — BASELINE config 4
+# ----------------------------------------------------------------------------
+def _sigmoid(x):
+    return 1.0 / (1.0 + np.exp(-x))
+
+
+def fpe_forward(fw, win_flat, h0, dtype=np.float64):
+    """``FPE_16.forward`` (models.py:65-115), batched.
+
+    win_flat [B,3,3H] normalised windows; h0 [B,3] GRU initial state (the
+    reference draws it with torch.randn inside encode, models.py:70, so it is an
+    explicit input here).  Returns per-host anomaly softmax probs [B,H,2] and
+    sigmoid prototypes [B,H,2].
+      GRU(3H -> 3) over the 3 window rows (torch gate order r, z, n)
+      GAT over [1,3,H,3] (dlutils.py:304-348), mean over nodes -> [3, H]
+      concat -> [3,1,3+H] -> MultiheadAttention(3+H, 1 head), seq 3, batch 1
+      flatten [3*(3+H)] -> Linear -> H x 10 latent (LeakyReLU(True) = id)
+      per host: Softmax(Linear(10,2)) and Sigmoid(Linear(10,2)).
+    """
+    fw = {k: np.asarray(v, dtype=dtype) for k, v in fw.items()}
+    x = np.asarray(win_flat, dtype=dtype)
+    B, Wn, F = x.shape
+    H = F // 3
+    h = np.asarray(h0, dtype=dtype).reshape(B, 3)
+    Wih, Whh, bih, bhh = fw["gru.weight_ih_l0"], fw["gru.weight_hh_l0"], fw["gru.bias_ih_l0"], fw["gru.bias_hh_l0"]
+    gru = []
+    for w in range(Wn):
+        gi = x[:, w] @ Wih.T + bih
+        gh = h @ Whh.T + bhh
+        r = _sigmoid(gi[:, 0:3] + gh[:, 0:3])
+        z = _sigmoid(gi[:, 3:6] + gh[:, 3:6])
+        n = np.tanh(gi[:, 6:9] + r * gh[:, 6:9])
+        h = (1 - z) * n + z * h
+        gru.append(h)
+    gru = np.stack(gru, axis=1)                                                   # [B,3,3]
+    g = gat(x.reshape(B, Wn, H, 3), fw["gat.layer1.heads.0.fc.weight"],
+            fw["gat.layer1.heads.0.attn_fc.weight"]).mean(axis=2)                 # [B,3,H]
+    c = np.concatenate([gru, g], axis=2)                                          # [B,3,E]
+    E = c.shape[2]
+    qkv = c @ fw["mha.in_proj_weight"].T + fw["mha.in_proj_bias"]
+    q, k, v = qkv[..., :E], qkv[..., E:2 * E], qkv[..., 2 * E:]
+    sc = np.einsum("bse,bte->bst", q, k) / np.sqrt(E)
+    sc = sc - sc.max(-1, keepdims=True)
+    p = np.exp(sc)
+    p = p / p.sum(-1, keepdims=True)
+    o = np.einsum("bst,bte->bse", p, v) @ fw["mha.out_proj.weight"].T + fw["mha.out_proj.bias"]
+    lat = (o.reshape(B, -1) @ fw["encoder.0.weight"].T + fw["encoder.0.bias"]).reshape(B, H, -1)
+    a = lat @ fw["anomaly_decoder.0.weight"].T + fw["anomaly_decoder.0.bias"]
+    a = a - a.max(-1, keepdims=True)
+    a = np.exp(a)
+    probs = a / a.sum(-1, keepdims=True)
+    protos = _sigmoid(lat @ fw["prototype_decoder.0.weight"].T + fw["prototype_decoder.0.bias"])
+    return probs, protos
+
+
+def forward_fpe(weights, windows, h0, sched, dtype=np.float64):
+    """PreGAN (``recovery/PreGAN.py:97-126``) per-window path: FPE encoder,
+    detect (argmax of the softmax == 1), embed, classes over K=3 prototypes,
+    Gen/Disc and the decision tensors."""
+    probs, protos = fpe_forward(weights["fpe"], windows, h0, dtype)
+    anom, emb, cls, anyb = classify(probs, protos, weights["prototypes"])
+    sched = np.asarray(sched, dtype=dtype)
+    ns = generator(weights["gen"], emb, sched, dtype)
+    gp = discriminator(weights["disc"], sched, ns, dtype)
+    keep, final_t, gen_t = decide(sched, ns, gp)
+    return dict(probs=probs, protos=protos, anom=anom, emb=emb, cls=cls, any=anyb, new_sched=ns,
+                gprobs=gp, keep=keep, final_target=final_t, gen_target=gen_t)

@@ -53,6 +53,14 @@ def lib():
     L.pgp_forward.restype = c_int
     L.pgp_forward_stage.argtypes = [vp, c_int, c_int] + [fp] * 11 + [vp]
     L.pgp_forward_stage.restype = c_int
+    L.pgp_create_fpe.argtypes = [c_int, ctypes.POINTER(vp)]
+    L.pgp_create_fpe.restype = c_int
+    L.pgp_fpe_weight_blob_len.argtypes = [c_int]
+    L.pgp_fpe_weight_blob_len.restype = c_size
+    L.pgp_forward_fpe.argtypes = [vp, c_int] + [fp] * 11 + [vp]
+    L.pgp_forward_fpe.restype = c_int
+    L.pgp_forward_fpe_stage.argtypes = [vp, c_int, c_int] + [fp] * 11 + [vp]
+    L.pgp_forward_fpe_stage.restype = c_int
     _lib = L
     return L
 

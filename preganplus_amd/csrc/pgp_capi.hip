@@ -2,6 +2,7 @@
 // upload, workspace, and the launch sequence of one forward call:
 //   K1 gat (pgp_gat.hip) -> K2 encoder (pgp_encoder.hip) ->
 //   K2b decoders+classify (pgp_decoder.hip) -> K3 GAN+decisions (pgp_gan.hip)
+// and of the PreGAN (FPE) variant: K4 FPE encoder+classify (pgp_fpe.hip) -> K3
 #include <hip/hip_runtime.h>
 
 #include <string>
@@ -17,6 +18,7 @@ using namespace pgp;
 
 struct pgp_model {
   int H = 0, K = 0;
+  bool fpe = false;  // PreGAN FPE_16 variant (pgp_create_fpe)
   bool loaded = false;
   float* d_frags = nullptr;
   float* d_tab = nullptr;
@@ -70,8 +72,8 @@ int reserve(pgp_model* m, int n) {
     }
   m->cap = 0;
   const size_t nblk = (size_t)(n + 15) / 16;
-  const size_t agg_f = nblk * m->H * 3 * 48;
-  const size_t lat_f = nblk * (size_t)lat_blk(m->H);
+  const size_t agg_f = m->fpe ? 4 : nblk * m->H * 3 * 48;  // the FPE variant needs only emb
+  const size_t lat_f = m->fpe ? 4 : nblk * (size_t)lat_blk(m->H);
   const size_t emb_f = nblk * 16 * round_up(2 * m->H, 16);
   HIPCHK(hipMalloc(&m->d_agg, agg_f * sizeof(float)));
   HIPCHK(hipMalloc(&m->d_lat, lat_f * sizeof(float)));
@@ -116,6 +118,21 @@ int pgp_create(int n_hosts, int n_protos, pgp_model** out) {
   return PGP_OK;
 }
 
+size_t pgp_fpe_weight_blob_len(int n_hosts) { return fpe_blob_len(n_hosts); }
+
+int pgp_create_fpe(int n_hosts, pgp_model** out) {
+  if (!out) return fail(PGP_ERR_ARG, "out is NULL");
+  *out = nullptr;
+  if (fpe_blob_len(n_hosts) == 0)
+    return fail(PGP_ERR_UNSUPPORTED, "FPE variant: host count not compiled in: " + std::to_string(n_hosts));
+  pgp_model* m = new pgp_model();
+  m->H = n_hosts;
+  m->K = 3;
+  m->fpe = true;
+  *out = m;
+  return PGP_OK;
+}
+
 int pgp_destroy(pgp_model* m) {
   if (!m) return PGP_OK;
   for (float* p : {m->d_frags, m->d_tab, m->d_gtab, m->d_agg, m->d_lat, m->d_emb})
@@ -127,7 +144,7 @@ int pgp_destroy(pgp_model* m) {
 int pgp_load_weights(pgp_model* m, const double* blob, size_t len) {
   if (!m || !blob) return fail(PGP_ERR_ARG, "NULL model or blob");
   Packed P;
-  const std::string err = pack_weights(m->H, m->K, blob, len, &P);
+  const std::string err = m->fpe ? pack_fpe_weights(m->H, blob, len, &P) : pack_weights(m->H, m->K, blob, len, &P);
   if (!err.empty()) return fail(PGP_ERR_ARG, err);
   if (!m->d_frags) HIPCHK(hipMalloc(&m->d_frags, P.frags.size() * sizeof(float)));
   if (!m->d_tab) HIPCHK(hipMalloc(&m->d_tab, P.enc_tab.size() * sizeof(float)));
@@ -150,14 +167,15 @@ int pgp_forward_stage(pgp_model* m, int stage, int batch, const float* windows, 
                       int* gen_target, float* latent, void* stream) {
   if (!m) return fail(PGP_ERR_ARG, "NULL model");
   if (!m->loaded) return fail(PGP_ERR_STATE, "weights not loaded");
+  if (m->fpe) return fail(PGP_ERR_STATE, "FPE model: use pgp_forward_fpe");
   if (batch < 0) return fail(PGP_ERR_ARG, "negative batch");
   if (stage < -1 || stage > 3) return fail(PGP_ERR_ARG, "bad stage");
+  if (batch == 0) return PGP_OK;  // empty batch: nothing to read or write (pointers may be NULL)
   const bool all = stage == -1;
   if (((all || stage == 0) && !windows) ||
       ((all || stage == 2) && (!logits || !protos || !cls || !any_anom)) ||
       ((all || stage == 3) && (!sched || !probs || !keep_orig || !final_target || !gen_target)))
     return fail(PGP_ERR_ARG, "NULL input/output pointer");
-  if (batch == 0) return PGP_OK;
   if (batch > m->cap) {
     const int rc = reserve(m, batch);
     if (rc) return rc;
@@ -197,6 +215,58 @@ int pgp_forward(pgp_model* m, int batch, const float* windows, const float* sche
                 float* latent, void* stream) {
   return pgp_forward_stage(m, -1, batch, windows, sched, logits, protos, cls, any_anom, probs, keep_orig,
                            final_target, gen_target, latent, stream);
+}
+
+int pgp_forward_fpe_stage(pgp_model* m, int stage, int batch, const float* windows, const float* h0,
+                          const float* sched, float* scores, float* protos, int* cls, int* any_anom, float* probs,
+                          int* keep_orig, int* final_target, int* gen_target, void* stream) {
+  if (!m) return fail(PGP_ERR_ARG, "NULL model");
+  if (!m->loaded) return fail(PGP_ERR_STATE, "weights not loaded");
+  if (!m->fpe) return fail(PGP_ERR_STATE, "not an FPE model: use pgp_forward");
+  if (batch < 0) return fail(PGP_ERR_ARG, "negative batch");
+  if (stage < -1 || stage > 1) return fail(PGP_ERR_ARG, "bad stage");
+  if (batch == 0) return PGP_OK;  // empty batch: nothing to read or write (pointers may be NULL)
+  const bool all = stage == -1;
+  if (((all || stage == 0) && (!windows || !h0 || !scores || !protos || !cls || !any_anom)) ||
+      ((all || stage == 1) && (!sched || !probs || !keep_orig || !final_target || !gen_target)))
+    return fail(PGP_ERR_ARG, "NULL input/output pointer");
+  if (batch > m->cap) {
+    const int rc = reserve(m, batch);
+    if (rc) return rc;
+  }
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  FpeArgs f{};
+  f.B = batch;
+  f.windows = windows;
+  f.h0 = h0;
+  f.tab = m->d_tab;
+  f.scores = scores;
+  f.protos = protos;
+  f.cls = cls;
+  f.any_anom = any_anom;
+  f.emb = m->d_emb;
+  if (all || stage == 0) HIPCHK(launch_fpe(m->H, f, st));
+  FwdArgs a{};
+  a.B = batch;
+  a.H = m->H;
+  a.K = m->K;
+  a.sched = sched;
+  a.emb = m->d_emb;
+  a.frags = m->d_frags;
+  a.gtab = m->d_gtab;
+  a.probs = probs;
+  a.keep = keep_orig;
+  a.final_t = final_target;
+  a.gen_t = gen_target;
+  if (all || stage == 1) HIPCHK(launch_gan(a, st));
+  return PGP_OK;
+}
+
+int pgp_forward_fpe(pgp_model* m, int batch, const float* windows, const float* h0, const float* sched,
+                    float* scores, float* protos, int* cls, int* any_anom, float* probs, int* keep_orig,
+                    int* final_target, int* gen_target, void* stream) {
+  return pgp_forward_fpe_stage(m, -1, batch, windows, h0, sched, scores, protos, cls, any_anom, probs, keep_orig,
+                               final_target, gen_target, stream);
 }
 
 // ---------------------------------------------------------------------------
@@ -316,6 +386,7 @@ int pgp_adamw(float* P, const float* G, float* exp_avg, float* exp_avg_sq, float
 
 int pgp_load_weights_master(pgp_model* m, const float* P_device, const double* prototypes) {
   if (!m || !P_device || !prototypes) return fail(PGP_ERR_ARG, "NULL argument");
+  if (m->fpe) return fail(PGP_ERR_STATE, "FPE model: master-layout reload covers the PreGAN+ model only");
   long tr, go, dof, all;
   if (!master_offsets(m->H, &tr, &go, &dof, &all)) return fail(PGP_ERR_UNSUPPORTED, "host count");
   std::vector<float> host((size_t)all);

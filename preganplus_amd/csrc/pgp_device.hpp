@@ -34,6 +34,20 @@ struct FwdArgs {
   float* latent;  // optional debug tap [B, 3H^2] (reference order)
 };
 
+// PreGAN FPE encoder + detect/diagnose (pgp_fpe.hip)
+struct FpeArgs {
+  int B;
+  const float* windows;  // [B,3,3H]
+  const float* h0;       // [B,3] GRU initial state
+  const float* tab;      // FpeGeo<H> table
+  float* scores;         // [B,H,2] anomaly softmax
+  float* protos;         // [B,H,2]
+  int* cls;              // [B,H]
+  int* any_anom;         // [B]
+  float* emb;            // workspace [B][EP] -> K3
+};
+hipError_t launch_fpe(int H, const FpeArgs& a, hipStream_t st);
+
 hipError_t launch_gat(const FwdArgs& a, hipStream_t st);
 hipError_t launch_encoder(const FwdArgs& a, hipStream_t st);
 hipError_t launch_decoder(const FwdArgs& a, hipStream_t st);

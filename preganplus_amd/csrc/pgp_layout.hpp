@@ -141,6 +141,37 @@ struct Geo {
   static constexpr int G_SIZE = G_B2 + C * MT_N * 16;
 };
 
+// PreGAN's FPE_16 encoder (models.py:10-115), folded table of K4 (pgp_fpe.hip).
+// Only H = 16 is instantiated: the reference defines FPE_16 alone
+// (FPE_50 is not constructible there).
+#define PGP_FOR_EACH_FPE_H(X) X(16)
+template <int H>
+struct FpeGeo {
+  static constexpr int W = 3;          // window rows = GRU steps = GRU state size
+  static constexpr int NIN = 3 * H;    // features per window row
+  static constexpr int E = W + H;      // MHA embedding: GRU state ++ GAT node-mean
+  static constexpr int KC = W * E;     // flattened attention output (encoder input)
+  static constexpr int NO = 4 * H;     // outputs per window: per host {a0, a1, p0, p1}
+  static constexpr int K = 3;          // prototypes (models.py:62)
+  static constexpr int F_WIH = 0;                                 // [9][NIN] GRU input weights (r,z,n)
+  static constexpr int F_WHH = F_WIH + round_up(9 * NIN, 4);      // [9][3]
+  static constexpr int F_BRZ = F_WHH + round_up(27, 4);           // [6] b_ih + b_hh for r, z
+  static constexpr int F_BIN = F_BRZ + 8;                         // [3] b_ih of n
+  static constexpr int F_BHN = F_BIN + 4;                         // [3] b_hh of n
+  static constexpr int F_UV = F_BHN + 4;                          // u[3] (+pad), v[3] (+pad), log2e-scaled
+  static constexpr int F_FC = F_UV + 8;                           // [H][3] GAT fc / H (node mean)
+  static constexpr int F_M = F_FC + round_up(3 * H, 4);           // [E][E] log2e Wq^T Wk / sqrt(E)
+  static constexpr int F_BETA = F_M + round_up(E * E, 4);         // [E]    log2e Wk^T bq / sqrt(E)
+  static constexpr int F_W2 = F_BETA + round_up(E, 4);            // [NO][KC] Dec . Wenc . Wout . Wv
+  static constexpr int F_B2 = F_W2 + round_up(NO * KC, 4);        // [NO]
+  static constexpr int F_PROTO = F_B2 + round_up(NO, 4);          // [K][2]
+  static constexpr int F_SIZE = F_PROTO + round_up(2 * K, 4);
+  static constexpr size_t blob_len() {
+    return 9 * NIN + 27 + 9 + 9 + 3 * H + 2 * H + 3 * E * E + 3 * E + E * E + E + (size_t)10 * H * KC + 10 * H +
+           20 + 2 + 20 + 2;
+  }
+};
+
 // GAT constants passed by value: u = Wfc^T a_src, v = Wfc^T a_dst (fp64-composed)
 struct GatConst {
   float u[4];

@@ -16,6 +16,7 @@
 
 #include <cmath>
 #include <cstring>
+#include <vector>
 
 namespace pgp {
 namespace {
@@ -32,6 +33,62 @@ struct Reader {
 
 // feature of d-space row R (see pgp_layout.hpp): R = 16t+4g+r <-> c = 16t+4r+g
 inline int featX(int R) { return 16 * (R / 16) + 4 * (R % 4) + (R % 16) / 4; }
+
+// Gen / Disc (models.py:118-151) into the K3 chunk layout (pgp_gan.hip).
+template <int H>
+void pack_gan(const double* g0W, const double* g0B, const double* g2W, const double* g2B, const double* d0W,
+              const double* d0B, const double* d2W, const double* d2B, float* F, float* GT) {
+  using G = Geo<H>;
+  const int d = H, GIN = 2 * d + d * d;
+  for (int mt = 0; mt < G::MT_G; ++mt)
+    for (int lane = 0; lane < 64; ++lane)
+      for (int e4 = 0; e4 < 4; ++e4) {
+        const int i = lane & 15, g = lane >> 4, row = 16 * mt + i;
+        for (int q = 0; q < G::EQ; ++q) {
+          const int k = 16 * q + 4 * g + e4;
+          if (k < 2 * d)
+            F[G::OFF_GE + (long)(mt * G::EQ + q) * G::FQ + lane * 4 + e4] = (float)g0W[(size_t)row * GIN + k];
+        }
+        for (int q = 0; q < G::SQ; ++q) {
+          const int k = 16 * q + 4 * g + e4;
+          if (k >= d * d) continue;
+          F[G::OFF_GS + ((long)q * G::GS_G + mt) * G::FQ + lane * 4 + e4] =
+              (float)g0W[(size_t)row * GIN + 2 * d + k];
+          F[G::OFF_GS + ((long)q * G::GS_G + G::MT_G + mt) * G::FQ + lane * 4 + e4] =
+              (float)d0W[(size_t)row * 2 * d * d + k];
+        }
+      }
+  for (int c = 0; c < d; ++c) {
+    float* FC = F + G::OFF_GC + (long)c * G::GC_G * G::FQ;
+    for (int t = 0; t < G::MT_N; ++t)
+      for (int q4 = 0; q4 < 4; ++q4)
+        for (int lane = 0; lane < 64; ++lane)
+          for (int e4 = 0; e4 < 4; ++e4) {
+            const int i = lane & 15, g = lane >> 4, u = 16 * q4 + 4 * g + e4, hh = 16 * t + i;
+            if (hh >= d) continue;
+            FC[(t * 4 + q4) * G::FQ + lane * 4 + e4] = (float)g2W[(size_t)(c * d + hh) * 64 + u];
+          }
+    for (int mt = 0; mt < G::MT_G; ++mt)
+      for (int q4 = 0; q4 < G::MT_N; ++q4)
+        for (int lane = 0; lane < 64; ++lane)
+          for (int e4 = 0; e4 < 4; ++e4) {
+            const int i = lane & 15, g = lane >> 4, hh = 16 * q4 + 4 * g + e4;
+            if (hh >= d) continue;
+            FC[(G::GC_G2 + mt * G::MT_N + q4) * G::FQ + lane * 4 + e4] =
+                (float)d0W[(size_t)(16 * mt + i) * 2 * d * d + d * d + c * d + hh];
+          }
+    for (int R = 0; R < G::MT_N * 16; ++R)
+      if (R < d) GT[G::G_B2 + c * G::MT_N * 16 + R] = (float)g2B[c * d + R];
+  }
+  for (int u = 0; u < 64; ++u) {
+    GT[G::G_B1 + u] = (float)g0B[u];
+    GT[G::G_BD1 + u] = (float)d0B[u];
+    GT[G::G_WD2 + u] = (float)d2W[u];
+    GT[G::G_WD2 + 64 + u] = (float)d2W[64 + u];
+  }
+  GT[G::G_BD2 + 0] = (float)d2B[0];
+  GT[G::G_BD2 + 1] = (float)d2B[1];
+}
 
 template <int H>
 size_t blob_len_t(int K) {
@@ -88,6 +145,7 @@ std::string pack_t(int K, const double* blob, size_t len, Packed* P) {
   const double* d2B = rd.take(2);
   const double* protos = rd.take(2 * K);
   if (rd.off != len) return "weight blob parse error";
+  (void)GIN;
 
   P->frags.assign(G::SZ_FRAGS, 0.0f);
   P->enc_tab.assign(G::t_size(K), 0.0f);
@@ -241,55 +299,137 @@ std::string pack_t(int K, const double* blob, size_t len, Packed* P) {
   }
   for (int k = 0; k < 2 * K; ++k) T[G::T_PROTO + k] = (float)protos[k];
 
-  // ---- GAN ----
-  for (int mt = 0; mt < G::MT_G; ++mt)
-    for (int lane = 0; lane < 64; ++lane)
-      for (int e4 = 0; e4 < 4; ++e4) {
-        const int i = lane & 15, g = lane >> 4, row = 16 * mt + i;
-        for (int q = 0; q < G::EQ; ++q) {
-          const int k = 16 * q + 4 * g + e4;
-          if (k < 2 * d)
-            F[G::OFF_GE + (long)(mt * G::EQ + q) * G::FQ + lane * 4 + e4] = (float)g0W[(size_t)row * GIN + k];
-        }
-        for (int q = 0; q < G::SQ; ++q) {
-          const int k = 16 * q + 4 * g + e4;
-          if (k >= d * d) continue;
-          F[G::OFF_GS + ((long)q * G::GS_G + mt) * G::FQ + lane * 4 + e4] =
-              (float)g0W[(size_t)row * GIN + 2 * d + k];
-          F[G::OFF_GS + ((long)q * G::GS_G + G::MT_G + mt) * G::FQ + lane * 4 + e4] =
-              (float)d0W[(size_t)row * 2 * d * d + k];
-        }
+  pack_gan<H>(g0W, g0B, g2W, g2B, d0W, d0B, d2W, d2B, F, GT);
+  return "";
+}
+
+
+// ---------------------------------------------------------------------------
+// PreGAN FPE_16 variant (models.py:10-115).  Folds, all in fp64:
+//   GAT node mean: mean_j sum_i a_ij Wfc x_i = (Wfc / H) sum_i r_i x_i, r_i = sum_j a_ij
+//   edge scores as above (u, v), pre-scaled by log2(e)
+//   MHA scores: q_s.k_t = c_s^T (Wq^T Wk) c_t + (Wk^T bq).c_t + (terms constant in t,
+//     which cancel in the softmax over t); 1/sqrt(E) and log2(e) folded in
+//   V, out_proj, encoder Linear (identity LeakyReLU(True)) and both decoders are
+//     affine maps applied after a convex combination (sum_t p_st = 1), so
+//     [a0 a1 p0 p1]_host = W2 . [sum_t p_st c_t]_s + b2 with
+//     W2 = Dec . Wenc . blockdiag_s(Wout Wv), b2 = Dec (Wenc (Wout bv + bout)_s + benc) + bdec
+// ---------------------------------------------------------------------------
+template <int H>
+std::string pack_fpe_t(const double* blob, size_t len, Packed* P) {
+  using FG = FpeGeo<H>;
+  using G = Geo<H>;
+  const int d = H, E = FG::E, KC = FG::KC, L = 10;
+  const size_t gan_len = (size_t)64 * (2 * d + d * d) + 64 + (size_t)d * d * 64 + d * d + 64 * 2 * d * d + 64 +
+                         2 * 64 + 2;
+  if (len != FG::blob_len() + gan_len + 2 * FG::K) return "FPE weight blob length mismatch";
+  Reader rd{blob, len};
+  const double* Wih = rd.take(9 * FG::NIN);
+  const double* Whh = rd.take(27);
+  const double* bih = rd.take(9);
+  const double* bhh = rd.take(9);
+  const double* fcW = rd.take(d * 3);
+  const double* attn = rd.take(2 * d);
+  const double* inW = rd.take(3 * E * E);
+  const double* inB = rd.take(3 * E);
+  const double* outW = rd.take(E * E);
+  const double* outB = rd.take(E);
+  const double* encW = rd.take((size_t)L * d * KC);
+  const double* encB = rd.take(L * d);
+  const double* anW = rd.take(2 * L);
+  const double* anB = rd.take(2);
+  const double* prW = rd.take(2 * L);
+  const double* prB = rd.take(2);
+  const int GIN = 2 * d + d * d;
+  const double* g0W = rd.take((size_t)64 * GIN);
+  const double* g0B = rd.take(64);
+  const double* g2W = rd.take((size_t)d * d * 64);
+  const double* g2B = rd.take(d * d);
+  const double* d0W = rd.take((size_t)64 * 2 * d * d);
+  const double* d0B = rd.take(64);
+  const double* d2W = rd.take(2 * 64);
+  const double* d2B = rd.take(2);
+  const double* protos = rd.take(2 * FG::K);
+  if (rd.off != len) return "FPE weight blob parse error";
+
+  P->frags.assign(G::SZ_FRAGS, 0.0f);
+  P->enc_tab.assign(FG::F_SIZE, 0.0f);
+  P->gan_tab.assign(G::G_SIZE, 0.0f);
+  float* T = P->enc_tab.data();
+  const double log2e = 1.4426950408889634;
+  for (int i = 0; i < 9 * FG::NIN; ++i) T[FG::F_WIH + i] = (float)Wih[i];
+  for (int i = 0; i < 27; ++i) T[FG::F_WHH + i] = (float)Whh[i];
+  for (int i = 0; i < 6; ++i) T[FG::F_BRZ + i] = (float)(bih[i] + bhh[i]);
+  for (int i = 0; i < 3; ++i) {
+    T[FG::F_BIN + i] = (float)bih[6 + i];
+    T[FG::F_BHN + i] = (float)bhh[6 + i];
+  }
+  for (int f = 0; f < 3; ++f) {
+    double u = 0, v = 0;
+    for (int k = 0; k < d; ++k) {
+      u += fcW[k * 3 + f] * attn[k];
+      v += fcW[k * 3 + f] * attn[d + k];
+    }
+    T[FG::F_UV + f] = (float)(u * log2e);
+    T[FG::F_UV + 4 + f] = (float)(v * log2e);
+  }
+  for (int i = 0; i < 3 * d; ++i) T[FG::F_FC + i] = (float)(fcW[i] / d);
+  const double* Wq = inW;
+  const double* Wk = inW + E * E;
+  const double* Wv = inW + 2 * E * E;
+  const double* bq = inB;
+  const double* bv = inB + 2 * E;
+  const double sc = log2e / std::sqrt((double)E);
+  for (int a = 0; a < E; ++a) {
+    for (int b = 0; b < E; ++b) {
+      double m = 0;
+      for (int e = 0; e < E; ++e) m += Wq[e * E + a] * Wk[e * E + b];
+      T[FG::F_M + a * E + b] = (float)(m * sc);
+    }
+    double beta = 0;
+    for (int e = 0; e < E; ++e) beta += Wk[e * E + a] * bq[e];
+    T[FG::F_BETA + a] = (float)(beta * sc);
+  }
+  std::vector<double> A((size_t)E * E), a0(E);  // A = Wout Wv, a0 = Wout bv + bout
+  for (int f = 0; f < E; ++f) {
+    double acc0 = outB[f];
+    for (int g = 0; g < E; ++g) acc0 += outW[f * E + g] * bv[g];
+    a0[f] = acc0;
+    for (int e = 0; e < E; ++e) {
+      double acc = 0;
+      for (int g = 0; g < E; ++g) acc += outW[f * E + g] * Wv[g * E + e];
+      A[(size_t)f * E + e] = acc;
+    }
+  }
+  // encoder rows composed with A:  WA[row][s*E+e] = sum_f Wenc[row][s*E+f] A[f][e]
+  std::vector<double> WA((size_t)L * d * KC), bA((size_t)L * d);
+  for (int row = 0; row < L * d; ++row) {
+    double bb = encB[row];
+    for (int s = 0; s < 3; ++s) {
+      for (int f = 0; f < E; ++f) bb += encW[(size_t)row * KC + s * E + f] * a0[f];
+      for (int e = 0; e < E; ++e) {
+        double acc = 0;
+        for (int f = 0; f < E; ++f) acc += encW[(size_t)row * KC + s * E + f] * A[(size_t)f * E + e];
+        WA[(size_t)row * KC + s * E + e] = acc;
       }
-  for (int c = 0; c < d; ++c) {
-    float* FC = F + G::OFF_GC + (long)c * G::GC_G * G::FQ;
-    for (int t = 0; t < G::MT_N; ++t)
-      for (int q4 = 0; q4 < 4; ++q4)
-        for (int lane = 0; lane < 64; ++lane)
-          for (int e4 = 0; e4 < 4; ++e4) {
-            const int i = lane & 15, g = lane >> 4, u = 16 * q4 + 4 * g + e4, hh = 16 * t + i;
-            if (hh >= d) continue;
-            FC[(t * 4 + q4) * G::FQ + lane * 4 + e4] = (float)g2W[(size_t)(c * d + hh) * 64 + u];
-          }
-    for (int mt = 0; mt < G::MT_G; ++mt)
-      for (int q4 = 0; q4 < G::MT_N; ++q4)
-        for (int lane = 0; lane < 64; ++lane)
-          for (int e4 = 0; e4 < 4; ++e4) {
-            const int i = lane & 15, g = lane >> 4, hh = 16 * q4 + 4 * g + e4;
-            if (hh >= d) continue;
-            FC[(G::GC_G2 + mt * G::MT_N + q4) * G::FQ + lane * 4 + e4] =
-                (float)d0W[(size_t)(16 * mt + i) * 2 * d * d + d * d + c * d + hh];
-          }
-    for (int R = 0; R < G::MT_N * 16; ++R)
-      if (R < d) GT[G::G_B2 + c * G::MT_N * 16 + R] = (float)g2B[c * d + R];
+    }
+    bA[row] = bb;
   }
-  for (int u = 0; u < 64; ++u) {
-    GT[G::G_B1 + u] = (float)g0B[u];
-    GT[G::G_BD1 + u] = (float)d0B[u];
-    GT[G::G_WD2 + u] = (float)d2W[u];
-    GT[G::G_WD2 + 64 + u] = (float)d2W[64 + u];
-  }
-  GT[G::G_BD2 + 0] = (float)d2B[0];
-  GT[G::G_BD2 + 1] = (float)d2B[1];
+  for (int h = 0; h < d; ++h)
+    for (int q = 0; q < 4; ++q) {
+      const double* dw = q < 2 ? anW + q * L : prW + (q - 2) * L;
+      double bb = q < 2 ? anB[q] : prB[q - 2];
+      for (int l = 0; l < L; ++l) bb += dw[l] * bA[h * L + l];
+      T[FG::F_B2 + 4 * h + q] = (float)bb;
+      for (int k = 0; k < KC; ++k) {
+        double acc = 0;
+        for (int l = 0; l < L; ++l) acc += dw[l] * WA[(size_t)(h * L + l) * KC + k];
+        T[FG::F_W2 + (4 * h + q) * KC + k] = (float)acc;
+      }
+    }
+  for (int k = 0; k < 2 * FG::K; ++k) T[FG::F_PROTO + k] = (float)protos[k];
+  pack_gan<H>(g0W, g0B, g2W, g2B, d0W, d0B, d2W, d2B, P->frags.data(), P->gan_tab.data());
+  P->gat = GatConst{};
   return "";
 }
 
@@ -315,6 +455,29 @@ std::string pack_weights(int H, int K, const double* blob, size_t len, Packed* o
 #undef CASE
   }
   return "unsupported host count";
+}
+
+size_t fpe_blob_len(int H) {
+  switch (H) {
+#define CASE(h) \
+  case h:       \
+    return FpeGeo<h>::blob_len() + (size_t)64 * (2 * h + h * h) + 64 + (size_t)h * h * 64 + h * h + \
+           64 * 2 * h * h + 64 + 2 * 64 + 2 + 2 * FpeGeo<h>::K;
+    PGP_FOR_EACH_FPE_H(CASE)
+#undef CASE
+  }
+  return 0;
+}
+
+std::string pack_fpe_weights(int H, const double* blob, size_t len, Packed* out) {
+  switch (H) {
+#define CASE(h) \
+  case h:       \
+    return pack_fpe_t<h>(blob, len, out);
+    PGP_FOR_EACH_FPE_H(CASE)
+#undef CASE
+  }
+  return "FPE variant: unsupported host count";
 }
 
 }  // namespace pgp

@@ -11,7 +11,7 @@ namespace pgp {
 
 struct Packed {
   std::vector<float> frags;    // Geo<H>::SZ_FRAGS
-  std::vector<float> enc_tab;  // Geo<H>::t_size(K)
+  std::vector<float> enc_tab;  // Geo<H>::t_size(K), or FpeGeo<H>::F_SIZE for the FPE variant
   std::vector<float> gan_tab;  // Geo<H>::G_SIZE
   GatConst gat;
 };
@@ -21,5 +21,9 @@ size_t blob_len(int H, int K);
 
 // Pack; returns "" on success or an error message.
 std::string pack_weights(int H, int K, const double* blob, size_t len, Packed* out);
+
+// PreGAN FPE variant (FpeGeo<H>): FPE table in enc_tab, GAN chunks in frags.
+size_t fpe_blob_len(int H);
+std::string pack_fpe_weights(int H, const double* blob, size_t len, Packed* out);
 
 }  // namespace pgp

@@ -120,6 +120,68 @@ class DecisionModel:
             pass
 
 
+class FPEDecisionModel(DecisionModel):
+    """PreGAN's decision model (BASELINE config C4): ``FPE_16`` encoder
+    (``models.py:10-115``) + detect/embed/``get_classes`` over K = 3 prototypes
+    (``recovery/PreGAN.py:105-120``) + PreGAN's own Gen/Disc
+    (``recover_decision``, ``PreGAN.py:73-77``), one ``pgp_forward_fpe`` call
+    (K4 then K3).  The GRU initial state ``h0`` [B,3] is an input: the reference
+    draws it with ``torch.randn`` inside ``encode`` (``models.py:70``)."""
+
+    def __init__(self, n_hosts: int, weights: dict, device: str | torch.device = "cuda"):
+        self.H = int(n_hosts)
+        self.K = W.FPE_PROTOS
+        self.device = torch.device(device)
+        if self.device.type == "cuda" and self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
+        if self.device.type != "cuda":
+            raise ValueError("FPEDecisionModel runs on the GPU only (no CPU fallback)")
+        L = _native.lib()
+        self._L = L
+        h = ctypes.c_void_p()
+        _native.check(L.pgp_create_fpe(self.H, ctypes.byref(h)), "pgp_create_fpe")
+        self._h = h
+        self.load_weights(weights)
+
+    def load_weights(self, weights: dict):
+        if "fpe" not in weights:
+            raise ValueError("FPE weights need an 'fpe' section (PreGAN FPE_16 state_dict)")
+        blob = W.pack_blob(weights, self.H)
+        n = self._L.pgp_fpe_weight_blob_len(self.H)
+        if n != blob.size:
+            raise ValueError(f"blob length {blob.size} != {n}")
+        torch.cuda.set_device(self.device)
+        _native.check(self._L.pgp_load_weights(
+            self._h, blob.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), blob.size), "pgp_load_weights")
+        self.prototypes = np.asarray(weights["prototypes"], dtype=np.float64)
+
+    def load_master(self, P, prototypes):
+        raise NotImplementedError("the PreGAN encoder is frozen (PreGAN.py:29); reload GAN weights with load_weights")
+
+    def alloc_outputs(self, B: int, latent: bool = False):
+        out = super().alloc_outputs(B, False)
+        out["scores"] = out.pop("logits")
+        return out
+
+    def forward(self, windows: torch.Tensor, h0: torch.Tensor, sched: torch.Tensor, out: dict | None = None,
+                stage: int = -1, stream=None) -> dict:
+        """windows [B,3,3H], h0 [B,3], sched [B,H,H]; float32, contiguous, on device.
+        stage: -1 both kernels, 0 K4 only, 1 K3 only (after a stage-0 call)."""
+        B = self._check_inputs(windows, sched)
+        if tuple(h0.shape) != (B, 3) or h0.dtype != torch.float32 or h0.device != self.device \
+                or not h0.is_contiguous():
+            raise ValueError(f"h0 must be contiguous float32 [B,3] on {self.device}")
+        if out is None:
+            out = self.alloc_outputs(B)
+        st = stream if stream is not None else torch.cuda.current_stream(self.device)
+        p = lambda t: t.data_ptr()
+        _native.check(self._L.pgp_forward_fpe_stage(
+            self._h, int(stage), B, p(windows), p(h0), p(sched), p(out["scores"]), p(out["protos"]), p(out["cls"]),
+            p(out["any"]), p(out["probs"]), p(out["keep"]), p(out["final_target"]), p(out["gen_target"]),
+            ctypes.c_void_p(st.cuda_stream)), "pgp_forward_fpe")
+        return out
+
+
 def to_numpy(out: dict) -> dict:
     res = {}
     for k, v in out.items():

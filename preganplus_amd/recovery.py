@@ -1,4 +1,5 @@
-"""Drop-in ``PreGANPlusRecovery`` for the COSCO framework/simulator on MI355X.
+"""Drop-in ``PreGANPlusRecovery`` (and PreGAN's ``PreGANRecovery``) for the
+COSCO framework/simulator on MI355X.
 
 Same constructor and ``run_model(time_series, original_decision)`` contract as
 ``recovery/PreGANPlus.py:11-136`` (plugin base ``recovery/Recovery.py:3-14``):
@@ -18,6 +19,12 @@ Per call, as the reference:
 Deliberate deviations: dropout is off (the reference runs its
 modules in train mode with p=0.1, so its own decisions are stochastic); no
 plotting; checkpoints are written only when ``save_folder`` is set.
+
+``PreGANRecovery`` (``recovery/PreGAN.py:11-126``, BASELINE config C4): frozen
+FPE_16 encoder + K = 3 prototypes (HIP kernel K4), PreGAN's own Gen/Disc (K3),
+GAN-only online training when ``training``.  The GRU state is drawn exactly as
+the reference draws it (``torch.randn(1, 1, 3, dtype=double)`` on the CPU
+generator, ``models.py:70``), so a seeded run reproduces the reference's h0.
 """
 from __future__ import annotations
 
@@ -28,7 +35,7 @@ import torch
 
 from . import train as TR
 from . import weights as W
-from .model import DecisionModel, to_numpy
+from .model import DecisionModel, FPEDecisionModel, to_numpy
 
 COEFF_ENERGY, COEFF_LATENCY = 0.8, 0.2  # constants.py:19-20
 _DATA = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data")
@@ -125,25 +132,10 @@ class PreGANPlusRecovery(Recovery):
     def recover_decision(self, embedding, schedule_data, original_decision):
         _, probs = self.trainer.gan_forward(np.asarray(embedding)[None], np.asarray(schedule_data)[None])
         p = probs[0].cpu().numpy()
-        if p[0] > p[1]:
-            return original_decision
-        host_alloc = [[] for _ in range(len(self.env.hostlist))]
-        container_alloc = [-1] * len(self.env.hostlist)
-        for c in self.env.containerlist:
-            if c and c.getHostID() != -1:
-                host_alloc[c.getHostID()].append(c.id)
-                container_alloc[c.id] = c.getHostID()
-        decision = dict(original_decision)
-        self.hosts_from = [0] * self.hosts
-        s = np.asarray(schedule_data)
-        for cids in host_alloc:
-            for cid in cids:
-                row = s[int(cid)].tolist()
-                new_host = row.index(max(row))
-                if container_alloc[cid] != new_host:
-                    decision[cid] = new_host
-                    self.hosts_from[container_alloc[cid]] = 1
-        return list(decision.items())
+        res = _recover(self.env, self.hosts, schedule_data, original_decision, bool(p[0] > p[1]))
+        if isinstance(res, tuple):
+            res, self.hosts_from = res
+        return res
 
     # -- PreGANPlus.py:115-136 --
     def run_model(self, time_series, original_decision):
@@ -166,29 +158,159 @@ class PreGANPlusRecovery(Recovery):
 
     # -- utils.py:49-58 (checkpoint dict), written with torch.save --
     def save_checkpoints(self, folder):
-        os.makedirs(folder, exist_ok=True)
+        save_checkpoints(self.trainer, folder, self.env_name, self.epoch, self.accuracy_list,
+                         [("transformer", self.model_name, self.tune_state.protos),
+                          ("gen", self.gen_name, None), ("disc", self.disc_name, None)])
+
+
+def save_checkpoints(trainer, folder, env_name, epoch, accuracy_list, entries):
+    """Write ``{env}_{name}.ckpt`` per (section, name, prototypes) in the
+    reference's checkpoint format (utils.py:49-58, AdamW state per parameter)."""
+    os.makedirs(folder, exist_ok=True)
+    w = trainer.weights_numpy()
+    mm, vv = trainer.m.cpu().numpy(), trainer.v.cpu().numpy()
+    for sec, name, proto in entries:
+        state, idx = {}, 0
+        for t in trainer.tensors:
+            if t["section"] != sec or not t["trainable"]:
+                continue
+            sl = slice(t["offset"], t["offset"] + t["n"])
+            shp = w[sec][t["name"]].shape
+            state[idx] = {"step": torch.tensor(float(t["step"])),
+                          "exp_avg": torch.tensor(mm[sl].astype(np.float64).reshape(shp)),
+                          "exp_avg_sq": torch.tensor(vv[sl].astype(np.float64).reshape(shp))}
+            idx += 1
+        ck = {"epoch": epoch,
+              "model_state_dict": {k: torch.tensor(v) for k, v in w[sec].items()},
+              "model_prototypes": [torch.tensor(x) for x in proto] if proto is not None else {},
+              "optimizer_state_dict": {"state": state, "param_groups": [{
+                  "lr": trainer.lrs[sec], "betas": (trainer.b1, trainer.b2),
+                  "eps": trainer.eps, "weight_decay": trainer.wd, "amsgrad": False,
+                  "params": list(range(idx))}]},
+              "accuracy_list": list(accuracy_list)}
+        torch.save(ck, os.path.join(folder, f"{env_name}_{name}.ckpt"))
+
+
+def _recover(env, hosts, schedule_data, original_decision, keep_original):
+    """recover_decision's decision loop (PreGAN.py:77-95 == PreGANPlus.py:84-105):
+    move every placed container to the first argmax of its ORIGINAL schedule row."""
+    if keep_original:
+        return original_decision
+    host_alloc = [[] for _ in range(len(env.hostlist))]
+    container_alloc = [-1] * len(env.hostlist)
+    for c in env.containerlist:
+        if c and c.getHostID() != -1:
+            host_alloc[c.getHostID()].append(c.id)
+            container_alloc[c.id] = c.getHostID()
+    decision = dict(original_decision)
+    hosts_from = [0] * hosts
+    s = np.asarray(schedule_data)
+    for cids in host_alloc:
+        for cid in cids:
+            row = s[int(cid)].tolist()
+            new_host = row.index(max(row))
+            if container_alloc[cid] != new_host:
+                decision[cid] = new_host
+                hosts_from[container_alloc[cid]] = 1
+    return list(decision.items()), hosts_from
+
+
+class PreGANRecovery(Recovery):
+    """recovery/PreGAN.py:11-126 on MI355X."""
+
+    def __init__(self, hosts, env, training=False, device=None, model_folder=None, save_folder=None,
+                 weights=None, extra=None):
+        super().__init__()
+        self.model_name = f"FPE_{hosts}"
+        self.gen_name = f"Gen_{hosts}"
+        self.disc_name = f"Disc_{hosts}"
+        self.hosts = hosts
+        self.env_name = "simulator" if env == "" else "framework"
+        self.training = training
+        self.save_folder = save_folder
+        self.device = torch.device(device or "cuda")
+        self.load_models(model_folder, weights, extra)
+
+    # -- PreGAN.py:22-37 (the encoder is frozen; no encoder training path: a
+    #    missing FPE checkpoint is an error, not a 30-epoch training run) --
+    def load_models(self, model_folder=None, weights=None, extra=None):
+        if weights is None:
+            folder = model_folder or "recovery/PreGANSrc/checkpoints"
+            ck = os.path.join(folder, f"{self.env_name}_{self.model_name}.ckpt")
+            if os.path.exists(ck):
+                weights = W.load_reference_checkpoints(folder, self.env_name, self.hosts, encoder="FPE")
+                extra = extra or {}
+            else:
+                packaged = os.path.join(_DATA, f"pregan_{self.env_name}_{self.hosts}.npz")
+                if not os.path.exists(packaged):
+                    raise FileNotFoundError(f"no checkpoint for {self.model_name} in {folder} or {packaged}")
+                weights, extra = W.load_npz(packaged)
+        self.weights = weights
+        self.extra = extra or {}
+        self.model = FPEDecisionModel(self.hosts, weights, device=self.device)
+        self.epoch = int(self.extra.get("meta/gen/epoch", 0))
+        self.accuracy_list = []
+        self.trainer = None
+        if self.training:
+            gan_only = {"transformer": {k: np.zeros(s) for k, s in W.transformer_shapes(self.hosts).items()},
+                        "gen": weights["gen"], "disc": weights["disc"],
+                        "prototypes": np.zeros((self.hosts, W.PROTO_DIM))}
+            self.trainer = TR.Trainer(self.hosts, gan_only, self.extra, device=self.device)
+        if "train_time_data" in self.extra:
+            self.train_time_data = np.asarray(self.extra["train_time_data"], dtype=np.float64)
+        else:
+            self.train_time_data = np.load(os.path.join("recovery/PreGANSrc/data", self.env_name, "time_series.npy"))
+
+    def _score(self, schedule):
+        e, r = self.env.stats.runSimulation(torch.tensor(schedule))  # utils.py:97-100
+        return COEFF_ENERGY * e + COEFF_LATENCY * r
+
+    # -- PreGAN.py:97-103 --
+    def run_encoder(self, schedule_data):
+        td = TR.normalize_test_time_data(self.env.stats.time_series, self.train_time_data)
+        if td.shape[0] >= 3:
+            td = td[-3:]
+        win = TR.convert_to_windows(td)[-1]
+        h0 = torch.randn(1, 1, 3, dtype=torch.double)                     # models.py:70
+        dev = self.model.device
+        f32 = lambda a: torch.as_tensor(np.asarray(a), dtype=torch.float32, device=dev).contiguous()
+        return to_numpy(self.model.forward(f32(win[None]), f32(h0.reshape(1, 3)),
+                                           f32(np.asarray(schedule_data)[None])))
+
+    # -- PreGAN.py:51-71 --
+    def train_gan(self, embedding, schedule_data):
+        TR.train_gan(self.trainer, embedding, schedule_data, self._score)
+        self.epoch += 1
         w = self.trainer.weights_numpy()
-        p = self.trainer.P.detach().cpu().numpy()
-        mm, vv = self.trainer.m.cpu().numpy(), self.trainer.v.cpu().numpy()
-        for sec, name, proto in (("transformer", self.model_name, self.tune_state.protos),
-                                 ("gen", self.gen_name, None), ("disc", self.disc_name, None)):
-            state, idx = {}, 0
-            for t in self.trainer.tensors:
-                if t["section"] != sec or not t["trainable"]:
-                    continue
-                sl = slice(t["offset"], t["offset"] + t["n"])
-                shp = w[sec][t["name"]].shape
-                state[idx] = {"step": torch.tensor(float(t["step"])),
-                              "exp_avg": torch.tensor(mm[sl].astype(np.float64).reshape(shp)),
-                              "exp_avg_sq": torch.tensor(vv[sl].astype(np.float64).reshape(shp))}
-                idx += 1
-            ck = {"epoch": self.epoch,
-                  "model_state_dict": {k: torch.tensor(v) for k, v in w[sec].items()},
-                  "model_prototypes": [torch.tensor(x) for x in proto] if proto is not None else {},
-                  "optimizer_state_dict": {"state": state, "param_groups": [{
-                      "lr": self.trainer.lrs[sec], "betas": (self.trainer.b1, self.trainer.b2),
-                      "eps": self.trainer.eps, "weight_decay": self.trainer.wd, "amsgrad": False,
-                      "params": list(range(idx))}]},
-                  "accuracy_list": list(self.accuracy_list)}
-            torch.save(ck, os.path.join(folder, f"{self.env_name}_{name}.ckpt"))
-        del p
+        self.weights = dict(self.weights, gen=w["gen"], disc=w["disc"])
+        self.model.load_weights(self.weights)     # keep K3's packed GAN in step with the master
+        if self.save_folder is not None:
+            save_checkpoints(self.trainer, self.save_folder, self.env_name, self.epoch, self.accuracy_list,
+                             [("gen", self.gen_name, None), ("disc", self.disc_name, None)])
+
+    # -- PreGAN.py:73-95 --
+    def recover_decision(self, embedding, schedule_data, original_decision):
+        if self.trainer is not None:
+            _, probs = self.trainer.gan_forward(np.asarray(embedding)[None], np.asarray(schedule_data)[None])
+            p = probs[0].cpu().numpy()
+        else:
+            p = self._probs
+        res = _recover(self.env, self.hosts, schedule_data, original_decision, bool(p[0] > p[1]))
+        if isinstance(res, tuple):
+            res, self.hosts_from = res
+        return res
+
+    # -- PreGAN.py:105-126 --
+    def run_model(self, time_series, original_decision):
+        schedule_data = np.asarray(self.env.scheduler.result_cache, dtype=np.float64)
+        out = self.run_encoder(schedule_data)
+        if not out["any"][0]:
+            return original_decision
+        sc = out["scores"][0]
+        anom = sc[:, 1] > sc[:, 0]
+        embedding = np.where(anom[:, None], out["protos"][0], 0.0)
+        self.classes = out["cls"][0].tolist()
+        self._probs = out["probs"][0]
+        if self.training:
+            self.train_gan(embedding, schedule_data)
+        return self.recover_decision(embedding, schedule_data, original_decision)

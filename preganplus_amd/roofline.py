@@ -62,3 +62,26 @@ def path_bytes_per_window(H: int) -> int:
     """in 36H (window) + 4H^2 (dense schedule); out logits 8H,
     protos 8H, class 4H, final target 4H, probs 8."""
     return 36 * H + 4 * H * H + 8 * H + 8 * H + 4 * H + 4 * H + 8
+
+
+def fpe_macs_per_window(H: int = 16) -> int:
+    """PreGAN FPE_16 (models.py:65-115) on the reference's formulation: GRU,
+    GAT (fc, decomposed scores, aggregation), MHA(E = H+3, 1 head), encoder,
+    per-host decoders."""
+    E, L = H + 3, 10
+    gru = W * (9 * 3 * H + 9 * 3)
+    gat = W * (H * 3 * H + 2 * H * H + H * H * H)
+    mha = W * 3 * E * E + 2 * W * W * E + W * E * E
+    enc = W * E * L * H
+    dec = H * (2 * L + 2 * L)
+    return gru + gat + mha + enc + dec
+
+
+def fpe_flops_per_window(H: int = 16) -> int:
+    return 2 * fpe_macs_per_window(H)
+
+
+def fpe_bytes_per_window(H: int = 16) -> int:
+    """K4's compulsory HBM I/O: window 36H + h0 12 in; scores 8H, protos 8H,
+    class 4H, any 4, masked embedding 8H (to K3) out."""
+    return 36 * H + 12 + 8 * H + 8 * H + 4 * H + 4 + 8 * H

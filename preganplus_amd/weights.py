@@ -71,6 +71,52 @@ def disc_shapes(H, hidden=64):
             "probs.2.weight": (2, hidden), "probs.2.bias": (2,)}
 
 
+def fpe_shapes(H=16, window=3, latent=10, feats=3):
+    """PreGAN's ``FPE_16`` parameters in ``state_dict`` order (models.py:10-64)."""
+    E = window + H                    # GRU state (3) + GAT node-mean (H)
+    return {
+        "gru.weight_ih_l0": (3 * window, feats * H), "gru.weight_hh_l0": (3 * window, window),
+        "gru.bias_ih_l0": (3 * window,), "gru.bias_hh_l0": (3 * window,),
+        "gat.layer1.heads.0.fc.weight": (H, feats), "gat.layer1.heads.0.attn_fc.weight": (1, 2 * H),
+        "mha.in_proj_weight": (3 * E, E), "mha.in_proj_bias": (3 * E,),
+        "mha.out_proj.weight": (E, E), "mha.out_proj.bias": (E,),
+        "encoder.0.weight": (H * latent, window * E), "encoder.0.bias": (H * latent,),
+        "anomaly_decoder.0.weight": (2, latent), "anomaly_decoder.0.bias": (2,),
+        "prototype_decoder.0.weight": (PROTO_DIM, latent), "prototype_decoder.0.bias": (PROTO_DIM,),
+    }
+
+
+FPE_PROTOS = 3   # models.py:62
+
+
+def fpe_blob_layout(H=16):
+    """(section, name, shape) list of the PreGAN (FPE) variant's weight blob."""
+    out = [("fpe", k, s) for k, s in fpe_shapes(H).items()]
+    out += [("gen", k, s) for k, s in gen_shapes(H).items()]
+    out += [("disc", k, s) for k, s in disc_shapes(H).items()]
+    out += [("prototypes", "prototypes", (FPE_PROTOS, PROTO_DIM))]
+    return out
+
+
+def synth_fpe_weights(H=16, seed=0):
+    """Seeded FPE + GAN weights (uniform +-1/sqrt(fan_in), fp32-representable)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    w = {}
+    for sec, shapes in (("fpe", fpe_shapes(H)), ("gen", gen_shapes(H)), ("disc", disc_shapes(H))):
+        w[sec] = {}
+        for name, shp in shapes.items():
+            if name.startswith("gru."):
+                fan_in = 3
+            elif len(shp) == 2:
+                fan_in = shp[1]
+            else:
+                fan_in = shapes[name.replace("bias", "weight")][1]
+            a = rng.uniform(-1, 1, size=shp) / np.sqrt(fan_in)
+            w[sec][name] = a.astype(np.float32).astype(np.float64)
+    w["prototypes"] = rng.uniform(0, 1, size=(FPE_PROTOS, PROTO_DIM)).astype(np.float32).astype(np.float64)
+    return w
+
+
 def blob_layout(H, n_protos=None):
     """Ordered (section, name, shape) list of the C-ABI weight blob."""
     K = H if n_protos is None else n_protos
@@ -82,10 +128,12 @@ def blob_layout(H, n_protos=None):
 
 
 def pack_blob(weights, H):
-    """Concatenate a weight set into the float64 blob of ``pgp_load_weights``."""
+    """Concatenate a weight set into the float64 blob of ``pgp_load_weights``
+    (PreGAN+ Transformer set, or PreGAN FPE set when ``weights`` has ``fpe``)."""
     K = np.asarray(weights["prototypes"]).shape[0]
     parts = []
-    for sec, name, shp in blob_layout(H, K):
+    layout = fpe_blob_layout(H) if "fpe" in weights else blob_layout(H, K)
+    for sec, name, shp in layout:
         a = np.asarray(weights[sec] if sec == "prototypes" else weights[sec][name],
                        dtype=np.float64)
         if a.shape != tuple(shp):
@@ -153,7 +201,7 @@ def weights_checksum(weights):
     return h + float(np.asarray(weights["prototypes"]).sum())
 
 
-def load_reference_checkpoints(model_dir, env_name="simulator", H=16):
+def load_reference_checkpoints(model_dir, env_name="simulator", H=16, encoder="Transformer"):
     """Read ``{env}_Transformer_{H}.ckpt``/``Gen``/``Disc`` from a COSCO tree
     (``checkpointsplus/``; format ``utils.py:53-58``) with the safe loader."""
     import torch
@@ -165,10 +213,10 @@ def load_reference_checkpoints(model_dir, env_name="simulator", H=16):
             return torch.load(os.path.join(model_dir, f"{env_name}_{name}_{H}.ckpt"),
                               weights_only=True)
 
-    t, g, d = ld("Transformer"), ld("Gen"), ld("Disc")
+    t, g, d = ld(encoder), ld("Gen"), ld("Disc")
     conv = lambda sd: {k: v.detach().cpu().numpy().astype(np.float64) for k, v in sd.items()}
     return {
-        "transformer": conv(t["model_state_dict"]),
+        ("fpe" if encoder == "FPE" else "transformer"): conv(t["model_state_dict"]),
         "gen": conv(g["model_state_dict"]),
         "disc": conv(d["model_state_dict"]),
         "prototypes": np.stack([p.detach().cpu().numpy() for p in t["model_prototypes"]]),
@@ -178,8 +226,8 @@ def load_reference_checkpoints(model_dir, env_name="simulator", H=16):
 
 def save_npz(path, weights, extra=None):
     flat = {}
-    for sec in ("transformer", "gen", "disc"):
-        for k, v in weights[sec].items():
+    for sec in ("transformer", "fpe", "gen", "disc"):
+        for k, v in weights.get(sec, {}).items():
             flat[f"{sec}/{k}"] = np.asarray(v, dtype=np.float64)
     flat["prototypes"] = np.asarray(weights["prototypes"], dtype=np.float64)
     for k, v in (extra or {}).items():
@@ -189,7 +237,7 @@ def save_npz(path, weights, extra=None):
 
 def load_npz(path):
     z = np.load(path, allow_pickle=False)
-    w = {"transformer": {}, "gen": {}, "disc": {}}
+    w = {"transformer": {}, "fpe": {}, "gen": {}, "disc": {}}
     extra = {}
     for k in z.files:
         sec = k.split("/", 1)[0]
@@ -199,4 +247,7 @@ def load_npz(path):
             w["prototypes"] = z[k]
         else:
             extra[k] = z[k]
+    for sec in ("transformer", "fpe"):
+        if not w[sec]:
+            del w[sec]
     return w, extra

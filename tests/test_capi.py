@@ -58,3 +58,20 @@ def test_argument_errors():
     assert rc == -4
     assert L.pgp_destroy(h) == 0
     assert L.pgp_weight_blob_len(7, 7) == 0
+
+
+def test_fpe_variant_abi():
+    """PreGAN FPE variant: blob length agrees with the Python layout, host
+    count and argument errors surface before any device work."""
+    L = _native.lib()
+    w, _ = W.load_npz("preganplus_amd/data/pregan_simulator_16.npz")
+    assert W.pack_blob(w, 16).size == L.pgp_fpe_weight_blob_len(16)
+    assert L.pgp_fpe_weight_blob_len(50) == 0           # FPE_50 not defined by the reference
+    h = ctypes.c_void_p()
+    assert L.pgp_create_fpe(50, ctypes.byref(h)) == -2
+    assert L.pgp_create_fpe(16, ctypes.byref(h)) == 0
+    blob = np.zeros(10)
+    assert L.pgp_load_weights(h, blob.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), 10) == -1
+    assert b"FPE" in L.pgp_last_error()
+    assert L.pgp_forward_fpe(h, 4, *([None] * 11), None) == -4   # weights not loaded
+    assert L.pgp_destroy(h) == 0

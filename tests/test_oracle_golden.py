@@ -74,3 +74,27 @@ def test_ties_break_to_first_index():
     assert anyb.tolist() == [True]
     s = np.array([[[0.5, 0.5, 0.1]]])
     assert O.first_argmax_rows(s).tolist() == [[0]]
+
+
+def test_fpe_oracle_matches_reference():
+    """PreGAN's FPE_16 path (config C4) vs the reference modules (make_golden_fpe.py),
+    shipped checkpoints/ weights, GRU h0 injected from the recorded draw."""
+    z = np.load(f"{GOLD}/fpe_h16.npz")
+    w, _ = W.load_npz("preganplus_amd/data/pregan_simulator_16.npz")
+    assert "fpe" in w and w["prototypes"].shape == (W.FPE_PROTOS, 2)
+    out = O.forward_fpe(w, z["windows"], z["h0"], z["sched"])
+    for k in ["probs", "protos", "emb", "new_sched", "gprobs"]:
+        np.testing.assert_allclose(out[k], z[k], rtol=0, atol=1e-12, err_msg=k)
+    for k in ["cls", "any", "keep", "final_target", "gen_target"]:
+        np.testing.assert_array_equal(out[k], z[k], err_msg=k)
+    out32 = O.forward_fpe(w, z["windows"], z["h0"], z["sched"], dtype=np.float32)
+    np.testing.assert_allclose(out32["probs"], z["probs"], rtol=1e-4, atol=1e-6)
+    np.testing.assert_array_equal(out32["cls"], z["cls"])
+
+
+def test_fpe_blob_layout():
+    w, _ = W.load_npz("preganplus_amd/data/pregan_simulator_16.npz")
+    blob = W.pack_blob(w, 16)
+    assert blob.size == sum(int(np.prod(s)) for _, _, s in W.fpe_blob_layout(16))
+    ws = W.synth_fpe_weights(16, 1)
+    assert W.pack_blob(ws, 16).size == blob.size

@@ -74,7 +74,7 @@ def fake_env(z, step, train_time, ss_all_rows):
     env.hostlist = list(range(16))
     placement = z[f"s{step}/placement"]
     cl = [FakeContainer(c, int(placement[c])) for c in range(16)]
-    cl[3] = None
+    cl[int(z["container_none"]) if "container_none" in z.files else 3] = None
     env.containerlist = cl
     env.scheduler = _Obj()
     env.scheduler.result_cache = z[f"s{step}/sched"]

@@ -46,6 +46,17 @@ for st in $STEPS; do
           -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline >"$OUT/pmc_$C.log" 2>&1
         ok_or_stop $? "pmc_$C"
       done;;
+    fpetest)
+      timeout -k 10 600 python -m pytest tests/test_gpu_fpe.py -x -q -p no:cacheprovider >"$OUT/gpu_fpe_tests.log" 2>&1
+      ok_or_stop $? fpetest; tail -15 "$OUT/gpu_fpe_tests.log";;
+    fpebench)
+      timeout -k 10 600 python bench.py --config fpe >"$OUT/bench_fpe.json" 2>"$OUT/bench_fpe.err"
+      ok_or_stop $? fpebench; cat "$OUT/bench_fpe.json";;
+    fpeprof)
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_fpe" -o run --output-format csv \
+        -- python3 "$ROOT/bench.py" --config fpe --steps 10 --warmup 2 --no-cpu-baseline >"$OUT/prof_fpe.log" 2>&1
+      ok_or_stop $? fpeprof
+      find "$OUT/prof_fpe" -name "*kernel_stats.csv" -exec cat {} \; | head -20;;
     *) echo "unknown step $st";;
   esac
 done
