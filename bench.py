@@ -1,8 +1,9 @@
 """Benchmark of the PreGAN+ decision path (BASELINE.json config 2).
 
 One step = detect + diagnose + generate over one batch of synthetic windows
-already resident in HBM: K1 GAT aggregation -> K2 encoder+decoders+classify ->
-K3 Gen+Disc+decisions (libpreganplus.so).  Multi-GPU: one process per GPU
+already resident in HBM: K1 GAT aggregation -> K2 encoder -> K2b decoders +
+classify -> K3 Gen+Disc+decision tensors -> K5 per-container moves
+(libpreganplus.so).  Multi-GPU: one process per GPU
 (torchrun); every rank processes its own batch of independent windows (weak
 scaling, no data-path collective); timing is max over ranks.
 
@@ -25,7 +26,7 @@ sys.path.insert(0, ROOT)
 
 from preganplus_amd import roofline as R  # noqa: E402
 from preganplus_amd import weights as W  # noqa: E402
-from preganplus_amd.model import DecisionModel  # noqa: E402
+from preganplus_amd.model import DecisionModel, migrations  # noqa: E402
 
 
 def log(*a):
@@ -117,18 +118,25 @@ def main():
     model = DecisionModel(H, weights, device=device)
     model.reserve(B)
     x, s = synth_inputs(B, H, device, 1234 + rank)
+    g = torch.Generator(device=device).manual_seed(4242 + rank)
+    cur = torch.randint(-1, H, (B, H), generator=g, device=device, dtype=torch.int32)  # -1: unplaced
     out = model.alloc_outputs(B)
+    mv_out = (torch.empty((B, H), dtype=torch.int32, device=device),
+              torch.empty((B, H), dtype=torch.int32, device=device))
     torch.cuda.synchronize()
 
-    NK = 4  # K1 gat, K2 encoder, K2b decoder, K3 gan
+    NK = 5  # K1 gat, K2 encoder, K2b decoder, K3 gan, K5 container moves
 
     def step(evs=None):
         if evs is None:
             model.forward(x, s, out=out, stage=-1)
+            migrations(out["keep"], out["final_target"], cur, out=mv_out)
             return
-        for k in range(NK):
+        for k in range(4):
             evs[k].record()
             model.forward(x, s, out=out, stage=k)
+        evs[4].record()
+        migrations(out["keep"], out["final_target"], cur, out=mv_out)
         evs[NK].record()
 
     for _ in range(args.warmup):
@@ -174,7 +182,8 @@ def main():
             "config": {"workload": f"C2: PreGAN+ batched inference, {H} hosts x W=3 x 3 resources, "
                                    f"{B} windows per GPU, fp32",
                        "hosts": H, "windows_per_gpu": B, "parallelism": f"dp{world} (independent windows)"},
-            "kernel_ms": {"gat_agg": k_mean[0], "encoder": k_mean[1], "decoder": k_mean[2], "gan": k_mean[3]},
+            "kernel_ms": {"gat_agg": k_mean[0], "encoder": k_mean[1], "decoder": k_mean[2], "gan": k_mean[3],
+                          "moves": k_mean[4]},
             "kernel_tflops": {
                 "encoder": achieved,
                 "decoder": R.decoder_flops_per_window(H) * B / (k_mean[2] * 1e-3) / 1e12,

@@ -120,6 +120,19 @@ int pgp_forward_stage(pgp_model* m, int stage, int batch, const float* windows,
                       int* any_anom, float* probs, int* keep_orig, int* final_target,
                       int* gen_target, float* latent, void* stream);
 
+/* recover_decision's container moves (PreGANPlus.py:87-105, PreGAN.py:77-95)
+ * for a batch, from pgp_forward's keep_orig / final_target (device pointers):
+ *   in  cur_host  [B,C] current host of container c, -1 = unplaced or None
+ *                       (the containerlist filter, PreGANPlus.py:92-95)
+ *   out moves     [B,C] new host where final_target != cur_host and the
+ *                       discriminator did not keep the original, else -1
+ *   out hosts_from[B,H] 1 for every host a container moves away from
+ * C = H (Gen reshapes to H x H, models.py:133).  The decision list is
+ * dict(original_decision) with moves[c] >= 0 overriding / appending key c in
+ * host-ascending, then container order. */
+int pgp_migrations(int n_hosts, int batch, const int* keep_orig, const int* final_target, const int* cur_host,
+                   int* moves, int* hosts_from, void* stream);
+
 /* ------------------------------------------------------------------------
  * PreGAN (FPE) variant — BASELINE config C4, SURVEY.md §8 a14.
  * Replaces PreGANRecovery.run_encoder + the GAN half of run_model

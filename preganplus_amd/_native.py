@@ -61,6 +61,8 @@ def lib():
     L.pgp_forward_fpe.restype = c_int
     L.pgp_forward_fpe_stage.argtypes = [vp, c_int, c_int] + [fp] * 11 + [vp]
     L.pgp_forward_fpe_stage.restype = c_int
+    L.pgp_migrations.argtypes = [c_int, c_int] + [fp] * 5 + [vp]
+    L.pgp_migrations.restype = c_int
     _lib = L
     return L
 

@@ -269,6 +269,17 @@ int pgp_forward_fpe(pgp_model* m, int batch, const float* windows, const float* 
                                final_target, gen_target, stream);
 }
 
+int pgp_migrations(int n_hosts, int batch, const int* keep_orig, const int* final_target, const int* cur_host,
+                   int* moves, int* hosts_from, void* stream) {
+  if (n_hosts < 1 || batch < 0) return fail(PGP_ERR_ARG, "bad migrations arguments");
+  if (batch == 0) return PGP_OK;
+  if (!keep_orig || !final_target || !cur_host || !moves || !hosts_from)
+    return fail(PGP_ERR_ARG, "NULL input/output pointer");
+  HIPCHK(launch_decide(batch, n_hosts, keep_orig, final_target, cur_host, moves, hosts_from,
+                       reinterpret_cast<hipStream_t>(stream)));
+  return PGP_OK;
+}
+
 // ---------------------------------------------------------------------------
 // training ops
 // ---------------------------------------------------------------------------

@@ -1,0 +1,44 @@
+// pgp_decide.hip — K5: the per-container decision of recover_decision
+// (recovery/PreGANPlus.py:87-105, recovery/PreGAN.py:77-95) for a batch of
+// windows, from K3's keep_orig / final_target and the current placement.
+//   keep_orig[b]          -> no change (the original decision stands)
+//   cur_host[b,c] == -1   -> unplaced / None container: not considered
+//   final_target != cur   -> moves[b,c] = final_target, hosts_from[b,cur] = 1
+// Integer work over C = H containers per window: one lane per (window,
+// container); hosts_from is a per-window OR, formed with a 64-bit ballot per
+// host inside the wave and one atomicOr per set bit.
+#include "pgp_device.hpp"
+
+namespace pgp {
+namespace {
+
+__global__ __launch_bounds__(256) void decide_kernel(int B, int C, const int* __restrict__ keep,
+                                                     const int* __restrict__ target, const int* __restrict__ cur,
+                                                     int* __restrict__ moves, int* __restrict__ hosts_from) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)B * C) return;
+  const long b = i / C;
+  const int h = cur[i];
+  const int t = target[i];
+  const bool mv = !keep[b] && h >= 0 && t != h;
+  moves[i] = mv ? t : -1;
+  if (mv) atomicOr(hosts_from + b * C + h, 1);
+}
+
+__global__ __launch_bounds__(256) void zero_kernel(long n, int* __restrict__ p) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = 0;
+}
+
+}  // namespace
+
+hipError_t launch_decide(int B, int C, const int* keep, const int* target, const int* cur, int* moves,
+                         int* hosts_from, hipStream_t st) {
+  const long n = (long)B * C;
+  const int grid = (int)((n + 255) / 256);
+  zero_kernel<<<grid, 256, 0, st>>>(n, hosts_from);
+  decide_kernel<<<grid, 256, 0, st>>>(B, C, keep, target, cur, moves, hosts_from);
+  return hipGetLastError();
+}
+
+}  // namespace pgp

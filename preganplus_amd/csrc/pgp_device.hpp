@@ -48,6 +48,10 @@ struct FpeArgs {
 };
 hipError_t launch_fpe(int H, const FpeArgs& a, hipStream_t st);
 
+// recover_decision's per-container moves (pgp_decide.hip)
+hipError_t launch_decide(int B, int C, const int* keep, const int* target, const int* cur, int* moves,
+                         int* hosts_from, hipStream_t st);
+
 hipError_t launch_gat(const FwdArgs& a, hipStream_t st);
 hipError_t launch_encoder(const FwdArgs& a, hipStream_t st);
 hipError_t launch_decoder(const FwdArgs& a, hipStream_t st);

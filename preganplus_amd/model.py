@@ -182,6 +182,37 @@ class FPEDecisionModel(DecisionModel):
         return out
 
 
+def migrations(keep_orig: torch.Tensor, final_target: torch.Tensor, cur_host: torch.Tensor, stream=None,
+               out=None):
+    """recover_decision's per-container moves for a batch (K5, ``pgp_migrations``):
+    int32 device tensors keep_orig [B], final_target [B,C], cur_host [B,C]
+    (-1 = unplaced / None) -> (moves [B,C], hosts_from [B,C])."""
+    B, C = final_target.shape
+    for t, shp in ((keep_orig, (B,)), (final_target, (B, C)), (cur_host, (B, C))):
+        if tuple(t.shape) != shp or t.dtype != torch.int32 or not t.is_cuda or not t.is_contiguous():
+            raise ValueError("migrations: int32 contiguous device tensors keep [B], final_target/cur_host [B,C]")
+    moves, hosts_from = out if out is not None else (torch.empty_like(final_target), torch.empty_like(final_target))
+    st = stream if stream is not None else torch.cuda.current_stream(final_target.device)
+    _native.check(_native.lib().pgp_migrations(
+        C, B, keep_orig.data_ptr(), final_target.data_ptr(), cur_host.data_ptr(), moves.data_ptr(),
+        hosts_from.data_ptr(), ctypes.c_void_p(st.cuda_stream)), "pgp_migrations")
+    return moves, hosts_from
+
+
+def assemble_decision(original_decision, moves_row, cur_host_row):
+    """The returned list of recover_decision (PreGANPlus.py:96-105): the original
+    decision's order, then overridden / new container keys in host-ascending,
+    then container order (``np.concatenate(host_alloc)``)."""
+    decision = dict(original_decision)
+    moves_row = [int(v) for v in moves_row]
+    cur = [int(v) for v in cur_host_row]
+    order = sorted((h, c) for c, h in enumerate(cur) if h >= 0)
+    for _, c in order:
+        if moves_row[c] >= 0:
+            decision[c] = moves_row[c]
+    return list(decision.items())
+
+
 def to_numpy(out: dict) -> dict:
     res = {}
     for k, v in out.items():

@@ -35,7 +35,7 @@ import torch
 
 from . import train as TR
 from . import weights as W
-from .model import DecisionModel, FPEDecisionModel, to_numpy
+from .model import DecisionModel, FPEDecisionModel, assemble_decision, migrations, to_numpy
 
 COEFF_ENERGY, COEFF_LATENCY = 0.8, 0.2  # constants.py:19-20
 _DATA = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data")
@@ -132,9 +132,10 @@ class PreGANPlusRecovery(Recovery):
     def recover_decision(self, embedding, schedule_data, original_decision):
         _, probs = self.trainer.gan_forward(np.asarray(embedding)[None], np.asarray(schedule_data)[None])
         p = probs[0].cpu().numpy()
-        res = _recover(self.env, self.hosts, schedule_data, original_decision, bool(p[0] > p[1]))
-        if isinstance(res, tuple):
-            res, self.hosts_from = res
+        res, hf = _recover(self.env, self.hosts, schedule_data, original_decision, bool(p[0] > p[1]),
+                           self.infer.device, getattr(self, "_final_target", None))
+        if hf is not None:
+            self.hosts_from = hf
         return res
 
     # -- PreGANPlus.py:115-136 --
@@ -149,6 +150,7 @@ class PreGANPlusRecovery(Recovery):
         anom = out["logits"][0, :, 1] > out["logits"][0, :, 0]
         embedding = np.where(anom[:, None], out["protos"][0], 0.0)
         self.classes = out["cls"][0].tolist()
+        self._final_target = out["final_target"][0].tolist()
         self.train_gan(embedding, schedule_data)
         self.tune_model()
         self.sync_inference_weights()
@@ -191,28 +193,23 @@ def save_checkpoints(trainer, folder, env_name, epoch, accuracy_list, entries):
         torch.save(ck, os.path.join(folder, f"{env_name}_{name}.ckpt"))
 
 
-def _recover(env, hosts, schedule_data, original_decision, keep_original):
-    """recover_decision's decision loop (PreGAN.py:77-95 == PreGANPlus.py:84-105):
-    move every placed container to the first argmax of its ORIGINAL schedule row."""
+def _recover(env, hosts, schedule_data, original_decision, keep_original, device, final_target=None):
+    """recover_decision's decision loop (PreGAN.py:77-95 == PreGANPlus.py:84-105)
+    on the device (K5, pgp_migrations): every placed container moves to the first
+    argmax of its ORIGINAL schedule row.  Returns (decision list, hosts_from)."""
     if keep_original:
-        return original_decision
-    host_alloc = [[] for _ in range(len(env.hostlist))]
-    container_alloc = [-1] * len(env.hostlist)
+        return original_decision, None
+    cur = [-1] * hosts
     for c in env.containerlist:
         if c and c.getHostID() != -1:
-            host_alloc[c.getHostID()].append(c.id)
-            container_alloc[c.id] = c.getHostID()
-    decision = dict(original_decision)
-    hosts_from = [0] * hosts
-    s = np.asarray(schedule_data)
-    for cids in host_alloc:
-        for cid in cids:
-            row = s[int(cid)].tolist()
-            new_host = row.index(max(row))
-            if container_alloc[cid] != new_host:
-                decision[cid] = new_host
-                hosts_from[container_alloc[cid]] = 1
-    return list(decision.items()), hosts_from
+            cur[c.id] = c.getHostID()
+    if final_target is None:
+        s = np.asarray(schedule_data)
+        final_target = [row.index(max(row)) for row in s.tolist()]
+    i32 = lambda a: torch.tensor(np.asarray(a, dtype=np.int32).reshape(1, -1), device=device)
+    moves, hosts_from = migrations(torch.zeros(1, dtype=torch.int32, device=device), i32(final_target), i32(cur))
+    moves, hosts_from = moves[0].cpu().numpy(), hosts_from[0].cpu().numpy()
+    return assemble_decision(original_decision, moves, cur), [int(v) for v in hosts_from]
 
 
 class PreGANRecovery(Recovery):
@@ -295,9 +292,10 @@ class PreGANRecovery(Recovery):
             p = probs[0].cpu().numpy()
         else:
             p = self._probs
-        res = _recover(self.env, self.hosts, schedule_data, original_decision, bool(p[0] > p[1]))
-        if isinstance(res, tuple):
-            res, self.hosts_from = res
+        res, hf = _recover(self.env, self.hosts, schedule_data, original_decision, bool(p[0] > p[1]),
+                           self.model.device, getattr(self, "_final_target", None))
+        if hf is not None:
+            self.hosts_from = hf
         return res
 
     # -- PreGAN.py:105-126 --
@@ -311,6 +309,7 @@ class PreGANRecovery(Recovery):
         embedding = np.where(anom[:, None], out["protos"][0], 0.0)
         self.classes = out["cls"][0].tolist()
         self._probs = out["probs"][0]
+        self._final_target = out["final_target"][0].tolist()
         if self.training:
             self.train_gan(embedding, schedule_data)
         return self.recover_decision(embedding, schedule_data, original_decision)
