@@ -24,9 +24,11 @@ struct EncLds {
   static constexpr int TOTAL = 2 * SLOT + TAB;
 };
 
-// acc[m][w] += A[m] . B, A = NM tiles x KQ groups in LDS, B k-step s = Bx[s/4][w][s%4]
-template <int NM, int KQ, int KS, int NB>
-PGP_DEV void gemm3(f32x4 (&acc)[NM][3], const float* A, const f32x4 (&Bx)[NB][3], int lane) {
+// acc[m][w] += A[m] . B for the first NM of NMA accumulator tiles, A = NM tiles
+// x KQ groups in LDS, B k-step s = Bx[s/4][w][s%4]
+template <int NM, int KQ, int KS, int NB, int NMA = NM>
+PGP_DEV void gemm3(f32x4 (&acc)[NMA][3], const float* A, const f32x4 (&Bx)[NB][3], int lane) {
+  static_assert(NM <= NMA, "accumulator tiles");
 #pragma unroll
   for (int m = 0; m < NM; ++m)
 #pragma unroll
@@ -39,6 +41,46 @@ PGP_DEV void gemm3(f32x4 (&acc)[NM][3], const float* A, const f32x4 (&Bx)[NB][3]
           for (int w = 0; w < 3; ++w) acc[m][w] = mfma(a[e], Bx[q4][w][e], acc[m][w]);
         }
     }
+}
+
+// VALU rows (tail mode): out[n][w] = sum_k W[n][k] B[k][w] for the NR rows with
+// no MFMA tile.  Lane group g holds k-steps' rows 4s+g of B, so each lane sums
+// its quarter of k (weights [n][q4][g][4] in LDS, one float4 per 4 k-steps,
+// the same address for the 16 lanes of a group) and two cross-group shuffles
+// complete the dot product in every lane.
+template <int NR, int KQ, int KS, int NB>
+PGP_DEV void rows_gemv(float (&out)[NR][3], const float* W, const f32x4 (&B)[NB][3], int g) {
+  float acc[NR][3];
+#pragma unroll
+  for (int n = 0; n < NR; ++n)
+#pragma unroll
+    for (int w = 0; w < 3; ++w) acc[n][w] = 0.f;
+#pragma unroll
+  for (int n = 0; n < NR; ++n)
+#pragma unroll
+    for (int q4 = 0; q4 < KQ; ++q4) {
+      const f32x4 wv = ld4(W + ((n * KQ + q4) * 4 + g) * 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (4 * q4 + e < KS) {
+#pragma unroll
+          for (int w = 0; w < 3; ++w) acc[n][w] = fmaf(wv[e], B[(4 * q4 + e) / 4][w][e], acc[n][w]);
+        }
+    }
+#pragma unroll
+  for (int n = 0; n < NR; ++n)
+#pragma unroll
+    for (int w = 0; w < 3; ++w) out[n][w] = xsum(acc[n][w], true);
+}
+
+// value of VALU row n = g in lane group g (0 elsewhere): the B-operand slot of
+// d-rows 16*MT_X + g (X tile MT_X, register 0)
+template <int NR>
+PGP_DEV float pick_row(const float (&v)[NR][3], int w, int g) {
+  float r = 0.f;
+#pragma unroll
+  for (int n = 0; n < NR; ++n) r = g == n ? v[n][w] : r;
+  return r;
 }
 
 template <int H>
@@ -143,6 +185,155 @@ PGP_DEV void qkv_gemm(f32x4 (&QKV)[3 * Geo<H>::TP][3], const float* A, const flo
   gemm3<3 * G::TP, G::KQ_D, G::KS_D, G::MT_D>(QKV, A, X, lane);
 }
 
+// Tail-mode layer (Geo<H>::TAIL, H = 50): stages [qk] [v o] [f1 f2].
+template <int H>
+PGP_DEV void encoder_layer_tail(f32x4 (&X)[Geo<H>::MT_D][3], Ring<H>& ring, const float* TL, int lane) {
+  using G = Geo<H>;
+  constexpr int TQ = G::TQ, SR = G::SR, HF = G::HF;
+  const int g = lane >> 4;
+  // [S0] q and k of both heads
+  f32x4 QK[2 * TQ][3];
+#pragma unroll
+  for (int m = 0; m < 2 * TQ; ++m) {
+    const f32x4 bias = ld4(TL + G::TL_QKV + m * 16 + 4 * g);
+#pragma unroll
+    for (int w = 0; w < 3; ++w) QK[m][w] = bias;
+  }
+  gemm3<2 * TQ, G::KQ_D, G::KS_D, G::MT_D>(QK, ring.cur, X, lane);
+  float qr[SR][3], kr[SR][3];
+  rows_gemv<SR, G::KQ_D, G::KS_D, G::MT_D>(qr, TL + G::TL_RQ, X, g);
+  rows_gemv<SR, G::KQ_D, G::KS_D, G::MT_D>(kr, TL + G::TL_RQ + SR * G::KQ_D * 16, X, g);
+#pragma unroll
+  for (int n = 0; n < SR; ++n)
+#pragma unroll
+    for (int w = 0; w < 3; ++w) {
+      qr[n][w] += TL[G::TL_RQB + n];
+      kr[n][w] += TL[G::TL_RQB + SR + n];
+    }
+  ring.advance();
+  // scores of both heads; the shared tile's slot 4r+g belongs to head 0 below HT
+  float P0[3][3], P1[3][3];
+#pragma unroll
+  for (int w = 0; w < 3; ++w) {
+    float s0[3], s1[3];
+#pragma unroll
+    for (int w2 = 0; w2 < 3; ++w2) {
+      float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+      for (int t = 0; t < HF; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          a0 = fmaf(QK[t][w][r], QK[TQ + t][w2][r], a0);
+          a1 = fmaf(QK[HF + t][w][r], QK[TQ + HF + t][w2][r], a1);
+        }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float pr = QK[2 * HF][w][r] * QK[TQ + 2 * HF][w2][r];
+        if (4 * r + g < G::HT)
+          a0 += pr;
+        else
+          a1 += pr;
+      }
+      s0[w2] = xsum(a0, true);
+      float t1 = xsum(a1, true);
+#pragma unroll
+      for (int n = 0; n < SR; ++n) t1 = fmaf(qr[n][w], kr[n][w2], t1);
+      s1[w2] = t1;
+    }
+    const float m0 = fmaxf(s0[0], fmaxf(s0[1], s0[2])), m1 = fmaxf(s1[0], fmaxf(s1[1], s1[2]));
+    const float e00 = expf(s0[0] - m0), e01 = expf(s0[1] - m0), e02 = expf(s0[2] - m0);
+    const float e10 = expf(s1[0] - m1), e11 = expf(s1[1] - m1), e12 = expf(s1[2] - m1);
+    const float i0 = 1.0f / (e00 + e01 + e02), i1 = 1.0f / (e10 + e11 + e12);
+    P0[w][0] = e00 * i0;
+    P0[w][1] = e01 * i0;
+    P0[w][2] = e02 * i0;
+    P1[w][0] = e10 * i1;
+    P1[w][1] = e11 * i1;
+    P1[w][2] = e12 * i1;
+  }
+  // [S1] v, P.v, out_proj (+ residual), norm1
+  f32x4 V[TQ][3];
+#pragma unroll
+  for (int t = 0; t < TQ; ++t) {
+    const f32x4 bias = ld4(TL + G::TL_QKV + (2 * TQ + t) * 16 + 4 * g);
+#pragma unroll
+    for (int w = 0; w < 3; ++w) V[t][w] = bias;
+  }
+  gemm3<TQ, G::KQ_D, G::KS_D, G::MT_D>(V, ring.cur, X, lane);
+  float vr[SR][3];
+  rows_gemv<SR, G::KQ_D, G::KS_D, G::MT_D>(vr, TL + G::TL_RQ + 2 * SR * G::KQ_D * 16, X, g);
+  f32x4 O[TQ + 1][3];
+#pragma unroll
+  for (int w = 0; w < 3; ++w) {
+#pragma unroll
+    for (int t = 0; t < 2 * HF; ++t) {
+      const float(&Pw)[3][3] = t < HF ? P0 : P1;
+      O[t][w] = Pw[w][0] * V[t][0] + Pw[w][1] * V[t][1] + Pw[w][2] * V[t][2];
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const bool h0 = 4 * r + g < G::HT;
+      const float c0 = h0 ? P0[w][0] : P1[w][0], c1 = h0 ? P0[w][1] : P1[w][1], c2 = h0 ? P0[w][2] : P1[w][2];
+      O[2 * HF][w][r] = c0 * V[2 * HF][0][r] + c1 * V[2 * HF][1][r] + c2 * V[2 * HF][2][r];
+    }
+    float orr[SR][1];
+#pragma unroll
+    for (int n = 0; n < SR; ++n) orr[n][0] = P1[w][0] * (vr[n][0] + TL[G::TL_RQB + 2 * SR + n]) +
+                                             P1[w][1] * (vr[n][1] + TL[G::TL_RQB + 2 * SR + n]) +
+                                             P1[w][2] * (vr[n][2] + TL[G::TL_RQB + 2 * SR + n]);
+    float o3 = 0.f;
+#pragma unroll
+    for (int n = 0; n < SR; ++n) o3 = g == n ? orr[n][0] : o3;
+    O[TQ][w] = f32x4{o3, 0.f, 0.f, 0.f};
+  }
+  f32x4 acc[G::MT_D][3];
+#pragma unroll
+  for (int mt = 0; mt < G::MT_D; ++mt) {
+    const f32x4 bo = ld4(TL + G::TL_BO + 16 * mt + 4 * g);
+#pragma unroll
+    for (int w = 0; w < 3; ++w) acc[mt][w] = bo + X[mt][w];
+  }
+  gemm3<G::MT_X, G::KQ_OT, G::KS_OT, TQ + 1, G::MT_D>(acc, ring.cur + G::G_V * G::FQ, O, lane);
+  {
+    float ro[G::XR][3];
+    rows_gemv<G::XR, G::KQ_OT, G::KS_OT, TQ + 1>(ro, TL + G::TL_RO, O, g);
+#pragma unroll
+    for (int w = 0; w < 3; ++w) acc[G::MT_X][w][0] += pick_row<G::XR>(ro, w, g);
+  }
+  layer_norm_tiles<H>(acc, X, TL + G::TL_LN1G, TL + G::TL_LN1B, g);
+  ring.advance();
+  // [S2] relu(W1 x + b1), W2 . h + b2 + x, norm2
+  f32x4 F1[G::MT_F][3];
+#pragma unroll
+  for (int mt = 0; mt < G::MT_F; ++mt) {
+    const f32x4 b1 = ld4(TL + G::TL_B1 + 16 * mt + 4 * g);
+#pragma unroll
+    for (int w = 0; w < 3; ++w) F1[mt][w] = b1;
+  }
+  gemm3<G::MT_F, G::KQ_D, G::KS_D, G::MT_D>(F1, ring.cur, X, lane);
+#pragma unroll
+  for (int mt = 0; mt < G::MT_F; ++mt)
+#pragma unroll
+    for (int w = 0; w < 3; ++w)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) F1[mt][w][r] = fmaxf(F1[mt][w][r], 0.f);
+#pragma unroll
+  for (int mt = 0; mt < G::MT_D; ++mt) {
+    const f32x4 b2 = ld4(TL + G::TL_B2 + 16 * mt + 4 * g);
+#pragma unroll
+    for (int w = 0; w < 3; ++w) acc[mt][w] = b2 + X[mt][w];
+  }
+  gemm3<G::MT_X, G::KQ_F, 16, G::MT_F, G::MT_D>(acc, ring.cur + G::G_F1 * G::FQ, F1, lane);
+  {
+    float rf[G::XR][3];
+    rows_gemv<G::XR, G::KQ_F, 16, G::MT_F>(rf, TL + G::TL_RF, F1, g);
+#pragma unroll
+    for (int w = 0; w < 3; ++w) acc[G::MT_X][w][0] += pick_row<G::XR>(rf, w, g);
+  }
+  ring.advance();
+  layer_norm_tiles<H>(acc, X, TL + G::TL_LN2G, TL + G::TL_LN2B, g);
+}
+
 // One encoder layer; weights arrive stage by stage through the ring.
 template <int H>
 PGP_DEV void encoder_layer(f32x4 (&X)[Geo<H>::MT_D][3], Ring<H>& ring, const float* TL, int lane) {
@@ -237,7 +428,12 @@ __global__ __launch_bounds__(kEncWaves * 64, 2) void encoder_kernel(FwdArgs a) {
       for (int w = 0; w < 3; ++w) X[mt][w] = mfma(aw, ba[w], ld4(tab + G::T_TE + w * G::DP + 16 * mt + 4 * g));
     }
 #pragma unroll 1
-    for (int l = 0; l < kLayers; ++l) encoder_layer<H>(X, ring, tab + G::T_L0 + l * G::TL_SIZE, lane);
+    for (int l = 0; l < kLayers; ++l) {
+      if constexpr (G::TAIL)
+        encoder_layer_tail<H>(X, ring, tab + G::T_L0 + l * G::TL_SIZE, lane);
+      else
+        encoder_layer<H>(X, ring, tab + G::T_L0 + l * G::TL_SIZE, lane);
+    }
 
     if (active) {
 #pragma unroll

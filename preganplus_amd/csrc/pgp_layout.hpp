@@ -18,6 +18,7 @@
 //   FFN hidden (64) and GAN hidden (64): natural rows u = 16t+4g+r.
 //   decoder outputs: row n = 4*host + q, q = {logit0, logit1, proto0, proto1}.
 #pragma once
+#include <cstddef>
 
 // host counts compiled into the library (d_model = H split over 2 heads: H even)
 #define PGP_FOR_EACH_H(X) X(8) X(16) X(32) X(50) X(64)
@@ -68,23 +69,47 @@ struct Geo {
   // float4 = 4 consecutive k-steps of one 16-row tile; a group is one
   // global_load_lds_dwordx4 wave-instruction and one ds_read_b128 per lane.
   static constexpr int FQ = kFrag * 4;  // floats per group
+  // ---- tail mode (H = 50): no padded 16-row output tile ----
+  // d = 16*MT_X + XR with XR <= 4 and head dim = 16*HF + HT with 16 < 2*HT <= 20.
+  // The XR last d-rows (X tile MT_X, register 0, lane groups < XR) are produced
+  // by a VALU GEMV + cross-group sum instead of a 16-row MFMA tile; q/k/v of
+  // both heads share TQ = 2*HF+1 tiles per pass (head-0 full tiles, head-1 full
+  // tiles, one tile holding both tails) and the SR head-1 tail rows that do
+  // not fit are VALU rows too.
+  static constexpr int HF = HD / 16, HT = HD % 16;
+  static constexpr bool TAIL = !P8 && (H % 16) != 0 && (H % 16) <= 4 && 2 * HT > 16 && 2 * HT - 16 <= 4;
+  static constexpr int MT_X = TAIL ? H / 16 : MT_D;   // MFMA output tiles of d-space GEMMs
+  static constexpr int XR = TAIL ? H % 16 : 0;        // VALU d-rows
+  static constexpr int TQ = 2 * HF + 1;               // q (k, v) tiles, tail mode
+  static constexpr int SR = TAIL ? 2 * HT - 16 : 0;   // VALU q/k/v rows (head 1)
+  static constexpr int KS_OT = 4 * TQ + (SR > 0 ? 1 : 0);
+  static constexpr int KQ_OT = cdiv(KS_OT, 4);
+
   // encoder stream of one layer, in consumption order:
   //   for p: qkv(p) [m][tp][q4], o(p) [mt][q4];  f1 [mt][q4];  f2 [mt][q4]
+  //   tail mode: qk [m][t][q4] | v [t][q4], o [mt][q4] | f1 [mt][q4], f2 [mt][q4]
   static constexpr int G_QKV = 3 * TP * KQ_D;
   static constexpr int G_O = MT_D * KQ_O;
   static constexpr int G_F1 = MT_F * KQ_D;
-  static constexpr int G_F2 = MT_D * KQ_F;
+  static constexpr int G_F2 = MT_X * KQ_F;
+  static constexpr int G_QK = 2 * TQ * KQ_D;          // tail mode
+  static constexpr int G_V = TQ * KQ_D;
+  static constexpr int G_OT = MT_X * KQ_OT;
   static constexpr int P_QKV(int p) { return p * (G_QKV + G_O); }
   static constexpr int P_O(int p) { return p * (G_QKV + G_O) + G_QKV; }
-  static constexpr int P_F1 = NPASS * (G_QKV + G_O);
+  static constexpr int P_V = G_QK;                    // tail mode
+  static constexpr int P_OT = G_QK + G_V;
+  static constexpr int P_F1 = TAIL ? P_OT + G_OT : NPASS * (G_QKV + G_O);
   static constexpr int P_F2 = P_F1 + G_F1;
   static constexpr int LAYER_G = P_F2 + G_F2;
   // LDS stages of a layer: NPASS=2: [qkv0] [o0 qkv1] [o1 f1] [f2]
   //                        NPASS=1: [qkv0] [o0 f1] [f2]
-  static constexpr int NST = NPASS + 2;
+  //                        tail:    [qk] [v o] [f1 f2]
+  static constexpr int NST = TAIL ? 3 : NPASS + 2;
   static constexpr int st_begin(int k) {
-    return NPASS == 2 ? (k == 0 ? 0 : k == 1 ? P_O(0) : k == 2 ? P_O(1) : P_F2)
-                      : (k == 0 ? 0 : k == 1 ? P_O(0) : P_F2);
+    return TAIL ? (k == 0 ? 0 : k == 1 ? P_V : P_F1)
+                : NPASS == 2 ? (k == 0 ? 0 : k == 1 ? P_O(0) : k == 2 ? P_O(1) : P_F2)
+                             : (k == 0 ? 0 : k == 1 ? P_O(0) : P_F2);
   }
   static constexpr int st_end(int k) { return k + 1 < NST ? st_begin(k + 1) : LAYER_G; }
   static constexpr int max_stage() {
@@ -119,15 +144,20 @@ struct Geo {
   static constexpr int T_TEW = 0;                   // [MT_D][64] time-encoder A fragments (K=4)
   static constexpr int T_TE = T_TEW + MT_D * 64;    // [3][DP] time-encoder bias + pe[w]
   static constexpr int T_L0 = T_TE + kWindow * DP;
-  static constexpr int TL_QKV = 0;                  // [NPASS][3][TP*16]
-  static constexpr int TL_BO = NPASS * 3 * TP * 16;
+  static constexpr int TL_QKV = 0;                  // [NPASS][3][TP*16]; tail: [3][TQ*16]
+  static constexpr int TL_BO = TAIL ? 3 * TQ * 16 : NPASS * 3 * TP * 16;
   static constexpr int TL_LN1G = TL_BO + DP;
   static constexpr int TL_LN1B = TL_LN1G + DP;
   static constexpr int TL_B1 = TL_LN1B + DP;
   static constexpr int TL_B2 = TL_B1 + kFF;
   static constexpr int TL_LN2G = TL_B2 + DP;
   static constexpr int TL_LN2B = TL_LN2G + DP;
-  static constexpr int TL_SIZE = TL_LN2B + DP;
+  // tail-mode VALU rows: weights [.][n][q4][g][4] (k-step 4*q4+e, lane group g)
+  static constexpr int TL_RQ = TL_LN2B + DP;                 // [3][SR][KQ_D][4][4] q/k/v rows
+  static constexpr int TL_RQB = TL_RQ + 3 * SR * KQ_D * 16;  // [3*SR] (pad 8) their biases
+  static constexpr int TL_RO = TL_RQB + (TAIL ? 8 : 0);      // [XR][KQ_OT][4][4] out_proj rows
+  static constexpr int TL_RF = TL_RO + XR * KQ_OT * 16;      // [XR][KQ_F][4][4] linear2 rows
+  static constexpr int TL_SIZE = TL_RF + XR * KQ_F * 16;
   static constexpr int T_DEC = T_L0 + kLayers * TL_SIZE;  // [MT_O*16] decoder bias
   static constexpr int T_PROTO = T_DEC + MT_O * 16;         // [K][2]
   static constexpr int t_size(int K) { return T_PROTO + round_up(2 * K, 4); }

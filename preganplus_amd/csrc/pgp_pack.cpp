@@ -90,6 +90,103 @@ void pack_gan(const double* g0W, const double* g0B, const double* g2W, const dou
   GT[G::G_BD2 + 1] = (float)d2B[1];
 }
 
+// Tail mode (Geo<H>::TAIL): q/k/v tile t, C-row i -> (head, dim).  Slot
+// sigma = 4*(i%4) + i/4 (the B-operand order of the row); tiles [0,HF) head 0,
+// [HF,2HF) head 1, tile 2HF: sigma < HT head 0's tail, else head 1's tail.
+// Head 1's last SR tail dims are VALU rows n: dim 16*HF + 16 - HT + n.
+template <int H>
+bool tail_slot(int t, int i, int* hh, int* e) {
+  using G = Geo<H>;
+  const int sg = 4 * (i % 4) + i / 4;
+  if (t < G::HF) {
+    *hh = 0;
+    *e = 16 * t + sg;
+  } else if (t < 2 * G::HF) {
+    *hh = 1;
+    *e = 16 * (t - G::HF) + sg;
+  } else if (sg < G::HT) {
+    *hh = 0;
+    *e = 16 * G::HF + sg;
+  } else {
+    *hh = 1;
+    *e = 16 * G::HF + sg - G::HT;
+  }
+  return *e < G::HD;
+}
+
+// out_proj k-step s, lane group g -> the (head, dim) of the O slot it reads
+template <int H>
+bool tail_oslot(int s, int g, int* hh, int* e) {
+  using G = Geo<H>;
+  if (s < 4 * G::TQ) return tail_slot<H>(s / 4, 4 * g + s % 4, hh, e);
+  if (s == 4 * G::TQ && g < G::SR) {
+    *hh = 1;
+    *e = 16 * G::HF + 16 - G::HT + g;
+    return true;
+  }
+  return false;
+}
+
+template <int H>
+void pack_tail_attention(const double* inW, const double* inB, const double* outW, double scale, float* FL,
+                         float* TL) {
+  using G = Geo<H>;
+  const int d = H;
+  // q, k tiles (stage 0) and v tiles (stage 1): [m][t][q4] groups over X k-steps
+  for (int m = 0; m < 3; ++m)
+    for (int t = 0; t < G::TQ; ++t) {
+      const long base = m < 2 ? (long)(m * G::TQ + t) * G::KQ_D : G::P_V + (long)t * G::KQ_D;
+      for (int q4 = 0; q4 < G::KQ_D; ++q4)
+        for (int lane = 0; lane < 64; ++lane)
+          for (int e4 = 0; e4 < 4; ++e4) {
+            const int i = lane & 15, g = lane >> 4, s = 4 * q4 + e4, c = 4 * s + g;
+            int hh, e;
+            if (s >= G::KS_D || c >= d || !tail_slot<H>(t, i, &hh, &e)) continue;
+            const int src = m * d + hh * G::HD + e;
+            FL[(base + q4) * G::FQ + lane * 4 + e4] = (float)(inW[src * d + c] * (m == 0 ? scale : 1.0));
+          }
+      for (int i = 0; i < 16; ++i) {
+        int hh, e;
+        if (!tail_slot<H>(t, i, &hh, &e)) continue;
+        TL[G::TL_QKV + (m * G::TQ + t) * 16 + i] = (float)(inB[m * d + hh * G::HD + e] * (m == 0 ? scale : 1.0));
+      }
+      // VALU rows of head 1's tail
+      if (t == 0)
+        for (int n = 0; n < G::SR; ++n) {
+          const int src = m * d + G::HD + 16 * G::HF + 16 - G::HT + n;
+          for (int q4 = 0; q4 < G::KQ_D; ++q4)
+            for (int g = 0; g < 4; ++g)
+              for (int e4 = 0; e4 < 4; ++e4) {
+                const int s = 4 * q4 + e4, c = 4 * s + g;
+                if (s >= G::KS_D || c >= d) continue;
+                TL[G::TL_RQ + (((m * G::SR + n) * G::KQ_D + q4) * 4 + g) * 4 + e4] =
+                    (float)(inW[src * d + c] * (m == 0 ? scale : 1.0));
+              }
+          TL[G::TL_RQB + m * G::SR + n] = (float)(inB[src] * (m == 0 ? scale : 1.0));
+        }
+    }
+  // out_proj: MT_X output tiles over the O slots (+ VALU rows 16*MT_X + n)
+  for (int mt = 0; mt < G::MT_X; ++mt)
+    for (int q4 = 0; q4 < G::KQ_OT; ++q4)
+      for (int lane = 0; lane < 64; ++lane)
+        for (int e4 = 0; e4 < 4; ++e4) {
+          const int i = lane & 15, g = lane >> 4, s = 4 * q4 + e4;
+          const int co = featX(16 * mt + i);
+          int hh, e;
+          if (co >= d || !tail_oslot<H>(s, g, &hh, &e)) continue;
+          FL[(G::P_OT + mt * G::KQ_OT + q4) * G::FQ + lane * 4 + e4] = (float)outW[co * d + hh * G::HD + e];
+        }
+  for (int n = 0; n < G::XR; ++n)
+    for (int q4 = 0; q4 < G::KQ_OT; ++q4)
+      for (int g = 0; g < 4; ++g)
+        for (int e4 = 0; e4 < 4; ++e4) {
+          int hh, e;
+          if (!tail_oslot<H>(4 * q4 + e4, g, &hh, &e)) continue;
+          TL[G::TL_RO + ((n * G::KQ_OT + q4) * 4 + g) * 4 + e4] =
+              (float)outW[(16 * G::MT_X + n) * d + hh * G::HD + e];
+        }
+}
+
 template <int H>
 size_t blob_len_t(int K) {
   const size_t d = H, L = 3 * H * H;
@@ -190,61 +287,65 @@ std::string pack_t(int K, const double* blob, size_t len, Packed* P) {
     const LayerSrc& S = ly[l];
     float* FL = F + G::OFF_ENC + (long)l * G::LAYER_G * G::FQ;
     float* TL = T + G::T_L0 + l * G::TL_SIZE;
-    // head-space row R within a pass block -> (head, dim), valid?
-    auto head_row = [&](int p, int R, int* hh, int* e) -> bool {
-      if (G::P8) {
-        const int g = (R % 16) / 4, r = R % 4;
-        *hh = g >> 1;
-        *e = 4 * (g & 1) + r;
-      } else {
-        *hh = p;
-        *e = featX(R);
-      }
-      return *e < G::HD;
-    };
-    for (int p = 0; p < G::NPASS; ++p)
-      for (int m = 0; m < 3; ++m)
-        for (int tp = 0; tp < G::TP; ++tp) {
-          for (int q4 = 0; q4 < G::KQ_D; ++q4)
+    if constexpr (G::TAIL) {
+      pack_tail_attention<H>(S.inW, S.inB, S.outW, scale, FL, TL);
+    } else {
+      // head-space row R within a pass block -> (head, dim), valid?
+      auto head_row = [&](int p, int R, int* hh, int* e) -> bool {
+        if (G::P8) {
+          const int g = (R % 16) / 4, r = R % 4;
+          *hh = g >> 1;
+          *e = 4 * (g & 1) + r;
+        } else {
+          *hh = p;
+          *e = featX(R);
+        }
+        return *e < G::HD;
+      };
+      for (int p = 0; p < G::NPASS; ++p)
+        for (int m = 0; m < 3; ++m)
+          for (int tp = 0; tp < G::TP; ++tp) {
+            for (int q4 = 0; q4 < G::KQ_D; ++q4)
+              for (int lane = 0; lane < 64; ++lane)
+                for (int e4 = 0; e4 < 4; ++e4) {
+                  const int i = lane & 15, g = lane >> 4, s = 4 * q4 + e4;
+                  const int c = 4 * s + g;
+                  int hh, e;
+                  if (s >= G::KS_D || c >= d || !head_row(p, 16 * tp + i, &hh, &e)) continue;
+                  const int src = m * d + hh * G::HD + e;
+                  const double v = S.inW[src * d + c] * (m == 0 ? scale : 1.0);
+                  FL[(G::P_QKV(p) + (m * G::TP + tp) * G::KQ_D + q4) * G::FQ + lane * 4 + e4] = (float)v;
+                }
+            for (int i = 0; i < 16; ++i) {
+              int hh, e;
+              if (!head_row(p, 16 * tp + i, &hh, &e)) continue;
+              const int src = m * d + hh * G::HD + e;
+              TL[G::TL_QKV + (p * 3 + m) * G::TP * 16 + 16 * tp + i] =
+                  (float)(S.inB[src] * (m == 0 ? scale : 1.0));
+            }
+          }
+      // out_proj
+      for (int p = 0; p < G::NPASS; ++p)
+        for (int mt = 0; mt < G::MT_D; ++mt)
+          for (int q4 = 0; q4 < G::KQ_O; ++q4)
             for (int lane = 0; lane < 64; ++lane)
               for (int e4 = 0; e4 < 4; ++e4) {
                 const int i = lane & 15, g = lane >> 4, s = 4 * q4 + e4;
-                const int c = 4 * s + g;
+                const int co = featX(16 * mt + i);
+                if (s >= G::KS_O || co >= d) continue;
                 int hh, e;
-                if (s >= G::KS_D || c >= d || !head_row(p, 16 * tp + i, &hh, &e)) continue;
-                const int src = m * d + hh * G::HD + e;
-                const double v = S.inW[src * d + c] * (m == 0 ? scale : 1.0);
-                FL[(G::P_QKV(p) + (m * G::TP + tp) * G::KQ_D + q4) * G::FQ + lane * 4 + e4] = (float)v;
+                if (G::P8) {
+                  hh = g >> 1;
+                  e = 4 * (g & 1) + s;
+                } else {
+                  hh = p;
+                  e = 4 * s + g;
+                }
+                if (e >= G::HD) continue;
+                FL[(G::P_O(p) + mt * G::KQ_O + q4) * G::FQ + lane * 4 + e4] =
+                    (float)S.outW[co * d + hh * G::HD + e];
               }
-          for (int i = 0; i < 16; ++i) {
-            int hh, e;
-            if (!head_row(p, 16 * tp + i, &hh, &e)) continue;
-            const int src = m * d + hh * G::HD + e;
-            TL[G::TL_QKV + (p * 3 + m) * G::TP * 16 + 16 * tp + i] =
-                (float)(S.inB[src] * (m == 0 ? scale : 1.0));
-          }
-        }
-    // out_proj
-    for (int p = 0; p < G::NPASS; ++p)
-      for (int mt = 0; mt < G::MT_D; ++mt)
-        for (int q4 = 0; q4 < G::KQ_O; ++q4)
-          for (int lane = 0; lane < 64; ++lane)
-            for (int e4 = 0; e4 < 4; ++e4) {
-              const int i = lane & 15, g = lane >> 4, s = 4 * q4 + e4;
-              const int co = featX(16 * mt + i);
-              if (s >= G::KS_O || co >= d) continue;
-              int hh, e;
-              if (G::P8) {
-                hh = g >> 1;
-                e = 4 * (g & 1) + s;
-              } else {
-                hh = p;
-                e = 4 * s + g;
-              }
-              if (e >= G::HD) continue;
-              FL[(G::P_O(p) + mt * G::KQ_O + q4) * G::FQ + lane * 4 + e4] =
-                  (float)S.outW[co * d + hh * G::HD + e];
-            }
+    }
     // FFN
     for (int mt = 0; mt < G::MT_F; ++mt)
       for (int q4 = 0; q4 < G::KQ_D; ++q4)
@@ -254,7 +355,7 @@ std::string pack_t(int K, const double* blob, size_t len, Packed* P) {
             if (s >= G::KS_D || c >= d) continue;
             FL[(G::P_F1 + mt * G::KQ_D + q4) * G::FQ + lane * 4 + e4] = (float)S.l1W[(16 * mt + i) * d + c];
           }
-    for (int mt = 0; mt < G::MT_D; ++mt)
+    for (int mt = 0; mt < G::MT_X; ++mt)
       for (int q4 = 0; q4 < G::KQ_F; ++q4)
         for (int lane = 0; lane < 64; ++lane)
           for (int e4 = 0; e4 < 4; ++e4) {
@@ -274,6 +375,13 @@ std::string pack_t(int K, const double* blob, size_t len, Packed* P) {
       TL[G::TL_LN2B + R] = (float)S.n2b[c];
     }
     for (int u = 0; u < 64; ++u) TL[G::TL_B1 + u] = (float)S.l1B[u];
+    // tail mode: linear2 rows of the VALU d-rows (feature 16*MT_X + n)
+    for (int n = 0; n < G::XR; ++n)
+      for (int q4 = 0; q4 < G::KQ_F; ++q4)
+        for (int g = 0; g < 4; ++g)
+          for (int e = 0; e < 4; ++e)
+            TL[G::TL_RF + ((n * G::KQ_F + q4) * 4 + g) * 4 + e] =
+                (float)S.l2W[(16 * G::MT_X + n) * 64 + 16 * q4 + 4 * g + e];
   }
 
   // ---- decoders: rows n = 4*host + {l0, l1, p0, p1} ----
