@@ -82,9 +82,20 @@ hipError_t launch_gan_gen_bwd(int H, int B, const float* Pg, const float* Pd, fl
 
 PGP_DEV f32x4 mfma(float a, float b, f32x4 c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
 PGP_DEV f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+// Sum over lane groups: v + v[lane ^ 16] (+ the same across lane ^ 32), with
+// the gfx950 half-row swaps instead of ds_bpermute round trips.
+// permlane16_swap(v, v) returns (rows 0,0,2,2 | rows 1,1,3,3) of v and
+// permlane32_swap(v, v) returns (halves 0,0 | 1,1): the element-wise sum of the
+// pair is the xor-16 / xor-32 sum, bit-identical to v + shfl_xor (a+b == b+a).
 PGP_DEV float xsum(float v, bool both) {
-  v += __shfl_xor(v, 16);
-  if (both) v += __shfl_xor(v, 32);
+  const unsigned u = __float_as_uint(v);
+  const auto r = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+  v = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  if (both) {
+    const unsigned u2 = __float_as_uint(v);
+    const auto q = __builtin_amdgcn_permlane32_swap(u2, u2, false, false);
+    v = __uint_as_float(q[0]) + __uint_as_float(q[1]);
+  }
   return v;
 }
 

@@ -43,34 +43,53 @@ PGP_DEV void gemm3(f32x4 (&acc)[NMA][3], const float* A, const f32x4 (&Bx)[NB][3
     }
 }
 
-// VALU rows (tail mode): out[n][w] = sum_k W[n][k] B[k][w] for the NR rows with
-// no MFMA tile.  Lane group g holds k-steps' rows 4s+g of B, so each lane sums
-// its quarter of k (weights [n][q4][g][4] in LDS, one float4 per 4 k-steps,
-// the same address for the 16 lanes of a group) and two cross-group shuffles
-// complete the dot product in every lane.
-template <int NR, int KQ, int KS, int NB>
-PGP_DEV void rows_gemv(float (&out)[NR][3], const float* W, const f32x4 (&B)[NB][3], int g) {
-  float acc[NR][3];
+// gemm3 with NR VALU rows folded into the first tile's pass: the rows' FMAs
+// (same B operands, k-step by k-step) sit between that pass's MFMAs, where
+// they issue in the matrix pipe's shadow.  racc must start at zero; the
+// cross-group sum is done by rows_finish.
+template <int NM, int KQ, int KS, int NB, int NMA, int NR>
+PGP_DEV void gemm3_rows(f32x4 (&acc)[NMA][3], const float* A, const f32x4 (&Bx)[NB][3], int lane,
+                        float (&racc)[NR][3], const float* RW, int g) {
+  static_assert(NM <= NMA, "accumulator tiles");
 #pragma unroll
-  for (int n = 0; n < NR; ++n)
-#pragma unroll
-    for (int w = 0; w < 3; ++w) acc[n][w] = 0.f;
-#pragma unroll
-  for (int n = 0; n < NR; ++n)
+  for (int m = 0; m < NM; ++m)
 #pragma unroll
     for (int q4 = 0; q4 < KQ; ++q4) {
-      const f32x4 wv = ld4(W + ((n * KQ + q4) * 4 + g) * 4);
+      const f32x4 a = ld4(A + (m * KQ + q4) * 256 + lane * 4);
+      f32x4 rw[NR];
+      if (m == 0) {
+#pragma unroll
+        for (int n = 0; n < NR; ++n) rw[n] = ld4(RW + ((n * KQ + q4) * 4 + g) * 4);
+      }
 #pragma unroll
       for (int e = 0; e < 4; ++e)
         if (4 * q4 + e < KS) {
 #pragma unroll
-          for (int w = 0; w < 3; ++w) acc[n][w] = fmaf(wv[e], B[(4 * q4 + e) / 4][w][e], acc[n][w]);
+          for (int w = 0; w < 3; ++w) {
+            acc[m][w] = mfma(a[e], Bx[q4][w][e], acc[m][w]);
+            if (m == 0) {
+#pragma unroll
+              for (int n = 0; n < NR; ++n) racc[n][w] = fmaf(rw[n][e], Bx[q4][w][e], racc[n][w]);
+            }
+          }
         }
     }
+}
+
+template <int NR>
+PGP_DEV void rows_finish(float (&r)[NR][3]) {
 #pragma unroll
   for (int n = 0; n < NR; ++n)
 #pragma unroll
-    for (int w = 0; w < 3; ++w) out[n][w] = xsum(acc[n][w], true);
+    for (int w = 0; w < 3; ++w) r[n][w] = xsum(r[n][w], true);
+}
+
+template <int NR>
+PGP_DEV void zero_rows(float (&r)[NR][3]) {
+#pragma unroll
+  for (int n = 0; n < NR; ++n)
+#pragma unroll
+    for (int w = 0; w < 3; ++w) r[n][w] = 0.f;
 }
 
 // value of VALU row n = g in lane group g (0 elsewhere): the B-operand slot of
@@ -199,16 +218,17 @@ PGP_DEV void encoder_layer_tail(f32x4 (&X)[Geo<H>::MT_D][3], Ring<H>& ring, cons
 #pragma unroll
     for (int w = 0; w < 3; ++w) QK[m][w] = bias;
   }
-  gemm3<2 * TQ, G::KQ_D, G::KS_D, G::MT_D>(QK, ring.cur, X, lane);
+  float qkr[2 * SR][3];
+  zero_rows(qkr);
+  gemm3_rows<2 * TQ, G::KQ_D, G::KS_D, G::MT_D, 2 * TQ, 2 * SR>(QK, ring.cur, X, lane, qkr, TL + G::TL_RQ, g);
+  rows_finish(qkr);
   float qr[SR][3], kr[SR][3];
-  rows_gemv<SR, G::KQ_D, G::KS_D, G::MT_D>(qr, TL + G::TL_RQ, X, g);
-  rows_gemv<SR, G::KQ_D, G::KS_D, G::MT_D>(kr, TL + G::TL_RQ + SR * G::KQ_D * 16, X, g);
 #pragma unroll
   for (int n = 0; n < SR; ++n)
 #pragma unroll
     for (int w = 0; w < 3; ++w) {
-      qr[n][w] += TL[G::TL_RQB + n];
-      kr[n][w] += TL[G::TL_RQB + SR + n];
+      qr[n][w] = qkr[n][w] + TL[G::TL_RQB + n];
+      kr[n][w] = qkr[SR + n][w] + TL[G::TL_RQB + SR + n];
     }
   ring.advance();
   // scores of both heads; the shared tile's slot 4r+g belongs to head 0 below HT
@@ -259,9 +279,11 @@ PGP_DEV void encoder_layer_tail(f32x4 (&X)[Geo<H>::MT_D][3], Ring<H>& ring, cons
 #pragma unroll
     for (int w = 0; w < 3; ++w) V[t][w] = bias;
   }
-  gemm3<TQ, G::KQ_D, G::KS_D, G::MT_D>(V, ring.cur, X, lane);
   float vr[SR][3];
-  rows_gemv<SR, G::KQ_D, G::KS_D, G::MT_D>(vr, TL + G::TL_RQ + 2 * SR * G::KQ_D * 16, X, g);
+  zero_rows(vr);
+  gemm3_rows<TQ, G::KQ_D, G::KS_D, G::MT_D, TQ, SR>(V, ring.cur, X, lane, vr,
+                                                         TL + G::TL_RQ + 2 * SR * G::KQ_D * 16, g);
+  rows_finish(vr);
   f32x4 O[TQ + 1][3];
 #pragma unroll
   for (int w = 0; w < 3; ++w) {
@@ -293,10 +315,12 @@ PGP_DEV void encoder_layer_tail(f32x4 (&X)[Geo<H>::MT_D][3], Ring<H>& ring, cons
 #pragma unroll
     for (int w = 0; w < 3; ++w) acc[mt][w] = bo + X[mt][w];
   }
-  gemm3<G::MT_X, G::KQ_OT, G::KS_OT, TQ + 1, G::MT_D>(acc, ring.cur + G::G_V * G::FQ, O, lane);
   {
     float ro[G::XR][3];
-    rows_gemv<G::XR, G::KQ_OT, G::KS_OT, TQ + 1>(ro, TL + G::TL_RO, O, g);
+    zero_rows(ro);
+    gemm3_rows<G::MT_X, G::KQ_OT, G::KS_OT, TQ + 1, G::MT_D, G::XR>(acc, ring.cur + G::G_V * G::FQ, O, lane, ro,
+                                                                   TL + G::TL_RO, g);
+    rows_finish(ro);
 #pragma unroll
     for (int w = 0; w < 3; ++w) acc[G::MT_X][w][0] += pick_row<G::XR>(ro, w, g);
   }
@@ -323,10 +347,12 @@ PGP_DEV void encoder_layer_tail(f32x4 (&X)[Geo<H>::MT_D][3], Ring<H>& ring, cons
 #pragma unroll
     for (int w = 0; w < 3; ++w) acc[mt][w] = b2 + X[mt][w];
   }
-  gemm3<G::MT_X, G::KQ_F, 16, G::MT_F, G::MT_D>(acc, ring.cur + G::G_F1 * G::FQ, F1, lane);
   {
     float rf[G::XR][3];
-    rows_gemv<G::XR, G::KQ_F, 16, G::MT_F>(rf, TL + G::TL_RF, F1, g);
+    zero_rows(rf);
+    gemm3_rows<G::MT_X, G::KQ_F, 16, G::MT_F, G::MT_D, G::XR>(acc, ring.cur + G::G_F1 * G::FQ, F1, lane, rf,
+                                                             TL + G::TL_RF, g);
+    rows_finish(rf);
 #pragma unroll
     for (int w = 0; w < 3; ++w) acc[G::MT_X][w][0] += pick_row<G::XR>(rf, w, g);
   }
