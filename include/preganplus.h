@@ -25,6 +25,14 @@
  *             final_target = first-argmax(sched[c,:])      (:99)
  *         generator proposal (GAN label input)  stats/Stats.py:162-166
  *             gen_target   = first-argmax(new_sched[c,:])
+ *   pgp_migrations
+ *       recover_decision's container loop PreGANPlus.py:90-105 (PreGAN.py:80-95)
+ *   pgp_create_fpe / pgp_forward_fpe
+ *       PreGAN: PreGANRecovery.run_encoder + detect/embed/get_classes + the
+ *       GAN gate, recovery/PreGAN.py:97-126 over FPE_16.forward models.py:65-115
+ *   pgp_tune_* / pgp_gan_* / pgp_adamw / pgp_load_weights_master
+ *       online training: tune_model PreGANPlus.py:51-58 (train.py:13-57),
+ *       train_gan PreGANPlus.py:60-81 / PreGAN.py:51-71, AdamW utils.py:65
  *   pgp_destroy
  *       (object lifetime; no reference counterpart)
  *
