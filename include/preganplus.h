@@ -193,20 +193,24 @@ int pgp_forward_fpe_stage(pgp_model* m, int stage, int batch, const float* windo
  *   pgp_adamw          torch.optim.AdamW.step (utils.py:65)
  * ---------------------------------------------------------------------- */
 size_t pgp_master_len(int n_hosts);               /* floats in P / G            */
-size_t pgp_tune_scratch_len(int n_hosts);         /* floats per window          */
 size_t pgp_gan_scratch_len(int n_hosts);          /* floats per window          */
+/* floats of tuning workspace for a batch (activations saved by the forward for
+ * the backward, token-major, plus split-K / weight-gradient partial slabs).
+ * Sizes grow with batch: a workspace for B_max serves every batch <= B_max. */
+size_t pgp_tune_workspace_len(int n_hosts, int batch);
 size_t pgp_master_offset(int n_hosts, int section); /* 0 transformer, 1 gen, 2 disc */
 
-/* windows [B,3,3H]; outputs latent [B,3H^2] (reference order), logits [B,H,2],
- * protos [B,H,2] (sigmoid); scratch [B, pgp_tune_scratch_len]. */
-int pgp_tune_forward(int n_hosts, int batch, const float* windows, const float* P, float* scratch,
+/* windows [B,3,3H]; outputs logits [B,H,2], protos [B,H,2] (sigmoid) and, if
+ * latent != NULL, the encoder output [B,3H^2] in the reference's order;
+ * workspace: pgp_tune_workspace_len(H, >= B) floats, kept for the backward. */
+int pgp_tune_forward(int n_hosts, int batch, const float* windows, const float* P, float* workspace,
                      float* latent, float* logits, float* protos, void* stream);
-/* y [B,H] int labels, mult [B,H] CE weights, tgt [B,H,2] positive prototypes
- * (only rows with y>0 used); dpre [B,4H] workspace.  Accumulates into G
- * (the caller zeroes G before the step). */
-int pgp_tune_backward(int n_hosts, int batch, const float* P, float* G, float* scratch, const float* latent,
-                      const float* logits, const float* protos, const int* y, const float* mult,
-                      const float* tgt, float* dpre, void* stream);
+/* After pgp_tune_forward with the same batch and workspace: y [B,H] int
+ * labels, mult [B,H] CE weights, tgt [B,H,2] positive prototypes (only rows
+ * with y>0 used).  Accumulates the gradient of the summed per-window losses
+ * into G (the caller zeroes G before the step). */
+int pgp_tune_backward(int n_hosts, int batch, const float* P, float* G, float* workspace, const float* logits,
+                      const float* protos, const int* y, const float* mult, const float* tgt, void* stream);
 /* emb [B,2H] (masked prototype embeddings), sched [B,H,H]; outputs the new
  * schedule ns [B,H,H] and probs [B,2]; gscratch [B, pgp_gan_scratch_len]. */
 int pgp_gan_forward(int n_hosts, int batch, const float* emb, const float* sched, const float* P, float* gscratch,

@@ -11,6 +11,7 @@
 #include "pgp_device.hpp"
 #include "pgp_pack.hpp"
 #include "pgp_train.hpp"
+#include "pgp_tune.hpp"
 
 #include <vector>
 
@@ -309,30 +310,34 @@ size_t pgp_master_offset(int n_hosts, int section) {
   if (!master_offsets(n_hosts, &a, &b, &c, &d)) return 0;
   return section == 0 ? a : section == 1 ? b : section == 2 ? c : d;
 }
-size_t pgp_tune_scratch_len(int n_hosts) { return supported(n_hosts) ? (size_t)train_scratch_floats(n_hosts) : 0; }
+size_t pgp_tune_workspace_len(int n_hosts, int batch) {
+  TunePlan p;
+  return (supported(n_hosts) && tune_plan(n_hosts, batch, &p)) ? (size_t)p.total : 0;
+}
 size_t pgp_gan_scratch_len(int n_hosts) { return supported(n_hosts) ? (size_t)gan_scratch_floats(n_hosts) : 0; }
 
-int pgp_tune_forward(int n_hosts, int batch, const float* windows, const float* P, float* scratch, float* latent,
+int pgp_tune_forward(int n_hosts, int batch, const float* windows, const float* P, float* workspace, float* latent,
                      float* logits, float* protos, void* stream) {
   if (!supported(n_hosts)) return fail(PGP_ERR_UNSUPPORTED, "host count");
-  if (batch < 0 || (batch > 0 && (!windows || !P || !scratch || !latent || !logits || !protos)))
+  if (batch < 0 || (batch > 0 && (!windows || !P || !workspace || !logits || !protos)))
     return fail(PGP_ERR_ARG, "bad tune_forward arguments");
   if (batch == 0) return PGP_OK;
-  HIPCHK(launch_tune_fwd(n_hosts, batch, windows, P, scratch, latent, logits, protos,
-                         reinterpret_cast<hipStream_t>(stream)));
+  TunePlan p;
+  tune_plan(n_hosts, batch, &p);
+  HIPCHK(launch_tune_forward(p, windows, P, workspace, latent, logits, protos, reinterpret_cast<hipStream_t>(stream)));
   return PGP_OK;
 }
 
-int pgp_tune_backward(int n_hosts, int batch, const float* P, float* G, float* scratch, const float* latent,
-                      const float* logits, const float* protos, const int* y, const float* mult, const float* tgt,
-                      float* dpre, void* stream) {
+int pgp_tune_backward(int n_hosts, int batch, const float* P, float* G, float* workspace, const float* logits,
+                      const float* protos, const int* y, const float* mult, const float* tgt, void* stream) {
   if (!supported(n_hosts)) return fail(PGP_ERR_UNSUPPORTED, "host count");
-  if (batch < 0 ||
-      (batch > 0 && (!P || !G || !scratch || !latent || !logits || !protos || !y || !mult || !tgt || !dpre)))
+  if (batch < 0 || (batch > 0 && (!P || !G || !workspace || !logits || !protos || !y || !mult || !tgt)))
     return fail(PGP_ERR_ARG, "bad tune_backward arguments");
   if (batch == 0) return PGP_OK;
-  HIPCHK(launch_tune_bwd(n_hosts, batch, P, G, scratch, latent, logits, protos, y, mult, tgt, dpre,
-                         reinterpret_cast<hipStream_t>(stream)));
+  TunePlan p;
+  tune_plan(n_hosts, batch, &p);
+  HIPCHK(launch_tune_backward(p, P, G, workspace, logits, protos, y, mult, tgt,
+                              reinterpret_cast<hipStream_t>(stream)));
   return PGP_OK;
 }
 

@@ -59,13 +59,7 @@ hipError_t launch_gan(const FwdArgs& a, hipStream_t st);
 
 // training ops (pgp_train.hip)
 struct AdamArgs;
-long train_scratch_floats(int H);
 long gan_scratch_floats(int H);
-hipError_t launch_tune_fwd(int H, int B, const float* win, const float* P, float* scr, float* lat, float* logits,
-                           float* protos, hipStream_t st);
-hipError_t launch_tune_bwd(int H, int B, const float* P, float* Gd, float* scr, const float* lat, const float* logits,
-                           const float* protos, const int* y, const float* mult, const float* tgt, float* dpre,
-                           hipStream_t st);
 hipError_t launch_adamw(const AdamArgs& a, hipStream_t st);
 hipError_t launch_gan_fwd(int H, int B, const float* emb, const float* sched, const float* Pg, const float* Pd,
                           float* scr, float* ns_out, float* probs, hipStream_t st);

@@ -6,8 +6,7 @@
 // scale into Wq), so they cannot be trained in place; after an optimizer step
 // the packed copies are rebuilt from the master weights.
 //
-// Per-window activations saved by the tuning forward for the backward, tokens
-// ordered [w][h] like the reference's [S=W, N=H, d] (models.py:387-396).
+// The tuning step's activation workspace is planned in pgp_tune.hpp.
 #pragma once
 #include <cstddef>
 
@@ -40,39 +39,6 @@ struct TGeo {
   static constexpr int DIN = 2 * H * H;
   static constexpr long D_W1 = 0, D_B1 = 64L * DIN, D_W2 = D_B1 + 64, D_B2 = D_W2 + 128, D_SIZE = D_B2 + 2;
   static constexpr long OFF_GEN = TR_SIZE, OFF_DISC = TR_SIZE + G_SIZE, ALL = TR_SIZE + G_SIZE + D_SIZE;
-
-  // ---- tuning scratch per window (floats) ----
-  static constexpr long S_X = 0;                         // [3][H][3] input window
-  static constexpr long S_Z = S_X + 9 * H;               // [3][H][d] fc(x)
-  static constexpr long S_SS = S_Z + T * D;              // [3][H] src score
-  static constexpr long S_TT = S_SS + T;                 // [3][H] dst score
-  static constexpr long S_A = S_TT + T;                  // [3][H][H] edge softmax a[w][i][j]
-  static constexpr long S_G = S_A + 3L * H * H;          // [3][H][d] GAT output
-  static constexpr long S_LAY = S_G + T * D;             // per layer:
-  static constexpr long LS_X = 0;                        //   [T][d] layer input
-  static constexpr long LS_QKV = LS_X + T * D;           //   [T][3d]
-  static constexpr long LS_P = LS_QKV + 3L * T * D;      //   [H][2][3][3] attention probs
-  static constexpr long LS_O = LS_P + 18L * H;           //   [T][d] attention output (pre out_proj)
-  static constexpr long LS_R1 = LS_O + T * D;            //   [T][d] LN1 input
-  static constexpr long LS_M1 = LS_R1 + T * D;           //   [T] LN1 mean
-  static constexpr long LS_S1 = LS_M1 + T;               //   [T] LN1 rstd
-  static constexpr long LS_Y1 = LS_S1 + T;               //   [T][d] LN1 output
-  static constexpr long LS_F = LS_Y1 + T * D;            //   [T][64] FFN pre-activation
-  static constexpr long LS_R2 = LS_F + (long)T * FF;     //   [T][d] LN2 input
-  static constexpr long LS_M2 = LS_R2 + T * D;           //   [T] LN2 mean
-  static constexpr long LS_S2 = LS_M2 + T;               //   [T] LN2 rstd
-  static constexpr long LS_SIZE = LS_S2 + T;
-  static constexpr long S_XL = S_LAY + 2 * LS_SIZE;      // [T][d] encoder output
-  // backward temporaries
-  static constexpr long S_DX = S_XL + T * D;             // [T][d]
-  static constexpr long S_DY = S_DX + T * D;             // [T][d]
-  static constexpr long S_DF = S_DY + T * D;             // [T][64]
-  static constexpr long S_DQKV = S_DF + (long)T * FF;    // [T][3d]
-  static constexpr long S_DO = S_DQKV + 3L * T * D;      // [T][d]
-  static constexpr long S_DA = S_DO + T * D;             // [3][H][H]
-  static constexpr long S_DS = S_DA + 3L * H * H;        // [3][H] d(src score)
-  static constexpr long S_DT = S_DS + T;                 // [3][H] d(dst score)
-  static constexpr long S_SIZE = S_DT + T;
 
   // ---- GAN scratch per window (floats) ----
   static constexpr long GS_X = 0;                        // [GIN] gen input [emb; s]

@@ -1,0 +1,53 @@
+// pgp_tune.hpp — geometry and workspace plan of the tuning step (train.py:42-57)
+// as token-major fp32 MFMA GEMMs (pgp_tune.hip).
+//
+// Every activation of the Transformer forward is a row-major [M][ld] array over
+// the batch's M = B * 3H tokens, token row m = b*3H + w*H + h (the reference's
+// [S=W, N=H, d] order per window, models.py:387-396).  Feature widths are padded
+// to multiples of 16 with zeros (d = H -> DP, 3d -> Q3P), so every GEMM k-block
+// is a whole float4 per lane and pads contribute exact zeros.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+
+#include "pgp_layout.hpp"
+
+namespace pgp {
+
+template <int H>
+struct TuneGeo {
+  static constexpr int D = H, DP = round_up(H, 16), T = 3 * H, HD = H / 2;
+  static constexpr int Q3 = 3 * H, Q3P = round_up(3 * H, 16), FF = 64;
+  static constexpr int NO = 4 * H, NOP = round_up(4 * H, 16);  // decoder outputs: anomaly 2H | prototype 2H
+  static constexpr long KD = (long)T * DP;                     // decoder contraction in token layout
+  static constexpr int XBP = 16;                               // GAT aggregated raw features, padded
+};
+
+// Workspace regions (float offsets) for one (H, B); region-major, so the same
+// (H, B) must be used by the forward and the backward of one step.
+struct TunePlan {
+  int H = 0, B = 0;
+  long M = 0;  // tokens
+  int DP = 0, Q3P = 0, NOP = 0;
+  long KD = 0;
+  long win = 0;                                          // [B][9H] copy of the input windows
+  long g = 0, xb = 0, gs = 0;                            // GAT out [M][DP], x-bar [M][16], (max, Z) [3B][4]
+  long x[3] = {0, 0, 0};                                 // layer inputs; x[2] = encoder output [M][DP]
+  long qkv[2] = {0, 0}, o[2] = {0, 0}, pr[2] = {0, 0};   // [M][Q3P], [M][DP], probs [M][8]
+  long xh1[2] = {0, 0}, rs1[2] = {0, 0}, y1[2] = {0, 0}; // LN1 x-hat [M][DP], rstd [M], output [M][DP]
+  long f[2] = {0, 0}, xh2[2] = {0, 0}, rs2[2] = {0, 0};  // FFN pre-activation [M][64], LN2 x-hat, rstd
+  long da = 0, db = 0, dq = 0, df = 0;                   // backward temporaries
+  long gsx = 0, dpre = 0, wp = 0, wpt = 0, part = 0, red2 = 0, total = 0;
+  int lin_grid = 0, dw_grid = 0, dec_s = 0, dec_bg = 0, dec_dxg = 0;
+};
+
+bool tune_plan(int H, int B, TunePlan* p);
+
+hipError_t launch_tune_forward(const TunePlan& p, const float* windows, const float* P, float* ws, float* latent,
+                               float* logits, float* protos, hipStream_t st);
+hipError_t launch_tune_backward(const TunePlan& p, const float* P, float* G, float* ws, const float* logits,
+                                const float* protos, const int* y, const float* mult, const float* tgt,
+                                hipStream_t st);
+
+}  // namespace pgp

@@ -97,12 +97,12 @@ class Trainer:
         L.pgp_master_len.restype = sz
         L.pgp_master_offset.argtypes = [i32, i32]
         L.pgp_master_offset.restype = sz
-        L.pgp_tune_scratch_len.argtypes = [i32]
-        L.pgp_tune_scratch_len.restype = sz
+        L.pgp_tune_workspace_len.argtypes = [i32, i32]
+        L.pgp_tune_workspace_len.restype = sz
         L.pgp_gan_scratch_len.argtypes = [i32]
         L.pgp_gan_scratch_len.restype = sz
         L.pgp_tune_forward.argtypes = [i32, i32] + [vp] * 6 + [vp]
-        L.pgp_tune_backward.argtypes = [i32, i32] + [vp] * 10 + [vp]
+        L.pgp_tune_backward.argtypes = [i32, i32] + [vp] * 8 + [vp]
         L.pgp_gan_forward.argtypes = [i32, i32] + [vp] * 6 + [vp]
         L.pgp_gan_disc_backward.argtypes = [i32, i32] + [vp] * 4 + [vp]
         L.pgp_gan_gen_backward.argtypes = [i32, i32] + [vp] * 3 + [vp]
@@ -117,12 +117,13 @@ class Trainer:
         H, dev, L = self.H, self.device, self._L
         f32 = torch.float32
         self.cap = B
-        self.scr = torch.zeros((B, L.pgp_tune_scratch_len(H)), dtype=f32, device=dev)
+        # token-major activations of the tuning forward (kept for the backward);
+        # zero-filled once: feature pads must stay 0 (pgp_tune.hpp)
+        self.ws = torch.zeros((L.pgp_tune_workspace_len(H, B),), dtype=f32, device=dev)
         self.gscr = torch.zeros((B, L.pgp_gan_scratch_len(H)), dtype=f32, device=dev)
-        self.lat = torch.zeros((B, 3 * H * H), dtype=f32, device=dev)
         self.logits = torch.zeros((B, H, 2), dtype=f32, device=dev)
         self.protos = torch.zeros((B, H, 2), dtype=f32, device=dev)
-        self.dpre = torch.zeros((B, 4 * H), dtype=f32, device=dev)
+        self._fwd_batch = 0
         self.ns = torch.zeros((B, H, H), dtype=f32, device=dev)
         self.probs = torch.zeros((B, 2), dtype=f32, device=dev)
 
@@ -141,25 +142,32 @@ class Trainer:
     def zero_grad(self, section: str):
         self.G[self.sec_off[section]:self.sec_end[section]].zero_()
 
-    def tune_forward(self, windows: torch.Tensor):
+    def tune_forward(self, windows: torch.Tensor, latent: torch.Tensor | None = None):
+        """Transformer forward of a batch of windows [B,3,3H], activations kept
+        in the workspace for tune_backward; optional latent tap [B,3H^2]."""
         B = windows.shape[0]
         self._ensure(B)
         windows = windows.to(self.device, torch.float32).contiguous()
         _native.check(self._L.pgp_tune_forward(
-            self.H, B, windows.data_ptr(), self.P.data_ptr(), self.scr.data_ptr(), self.lat.data_ptr(),
+            self.H, B, windows.data_ptr(), self.P.data_ptr(), self.ws.data_ptr(),
+            None if latent is None else latent.data_ptr(),
             self.logits.data_ptr(), self.protos.data_ptr(), self._stream()), "pgp_tune_forward")
+        self._fwd_batch = B
         return self.logits[:B], self.protos[:B]
 
     def tune_backward(self, B, y, mult, tgt):
-        """y [B,H] int, mult [B,H], tgt [B,H,2] (host arrays or tensors)."""
+        """y [B,H] int, mult [B,H], tgt [B,H,2] (host arrays or tensors); B must
+        be the batch of the preceding tune_forward."""
+        if B != self._fwd_batch:
+            raise ValueError(f"tune_backward batch {B} != tune_forward batch {self._fwd_batch}")
         y = self._dev(y, torch.int32)
         mult = self._dev(mult, torch.float32)
         tgt = self._dev(tgt, torch.float32)
         self.zero_grad("transformer")
         _native.check(self._L.pgp_tune_backward(
-            self.H, B, self.P.data_ptr(), self.G.data_ptr(), self.scr.data_ptr(), self.lat.data_ptr(),
+            self.H, B, self.P.data_ptr(), self.G.data_ptr(), self.ws.data_ptr(),
             self.logits.data_ptr(), self.protos.data_ptr(), y.data_ptr(), mult.data_ptr(), tgt.data_ptr(),
-            self.dpre.data_ptr(), self._stream()), "pgp_tune_backward")
+            self._stream()), "pgp_tune_backward")
 
     def gan_forward(self, emb, sched):
         emb = self._dev(emb, torch.float32)
