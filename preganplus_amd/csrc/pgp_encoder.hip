@@ -204,32 +204,74 @@ PGP_DEV void qkv_gemm(f32x4 (&QKV)[3 * Geo<H>::TP][3], const float* A, const flo
   gemm3<3 * G::TP, G::KQ_D, G::KS_D, G::MT_D>(QKV, A, X, lane);
 }
 
-// Tail-mode layer (Geo<H>::TAIL, H = 50): stages [qk] [v o] [f1 f2].
+// Layer 0's q/k/v tiles [T0, T0 + n) from the aggregated raw features: X0 is
+// affine in them, so each tile is ONE K=4 MFMA (raw feature k = lane group,
+// ba[w] zero in group 3) onto its per-step bias (pgp_pack.cpp, T_F0*).
+template <int H, int NM>
+PGP_DEV void qkv_fold(f32x4 (&acc)[NM][3], int T0, int n, const float* tab, const float (&ba)[3], int lane, int g) {
+  using G = Geo<H>;
+#pragma unroll
+  for (int m = 0; m < NM; ++m)
+    if (m < n) {
+      const float a = tab[G::T_F0 + (T0 + m) * 64 + lane];
+#pragma unroll
+      for (int w = 0; w < 3; ++w)
+        acc[m][w] = mfma(a, ba[w], ld4(tab + G::T_F0B + (w * 3 * G::NQT + T0 + m) * 16 + 4 * g));
+    }
+}
+// tail-mode VALU rows of layer 0 (q/k/v m, head-1 tail row n), without bias
 template <int H>
-PGP_DEV void encoder_layer_tail(f32x4 (&X)[Geo<H>::MT_D][3], Ring<H>& ring, const float* TL, int lane) {
+PGP_DEV float row_fold(int m, int n, int w, const float* tab, const float (&ba)[3], int g) {
+  using G = Geo<H>;
+  const float wg = g < 3 ? tab[G::T_F0R + (m * G::SR + n) * 4 + g] : 0.f;
+  return xsum(wg * ba[w], true);
+}
+template <int H>
+PGP_DEV float row_fold_bias(int m, int n, int w, const float* tab) {
+  using G = Geo<H>;
+  return tab[G::T_F0RB + w * 3 * G::SR + m * G::SR + n];
+}
+
+// Tail-mode layer (Geo<H>::TAIL, H = 50): stages [qk] [v o] [f1 f2].
+// F0: layer 0, q/k/v from the folded raw-feature product (the ring's q/k/v
+// stages are then unused).
+template <int H, bool F0>
+PGP_DEV void encoder_layer_tail(f32x4 (&X)[Geo<H>::MT_D][3], Ring<H>& ring, const float* TL, int lane,
+                                const float* tab, const float (&ba)[3]) {
   using G = Geo<H>;
   constexpr int TQ = G::TQ, SR = G::SR, HF = G::HF;
   const int g = lane >> 4;
   // [S0] q and k of both heads
   f32x4 QK[2 * TQ][3];
-#pragma unroll
-  for (int m = 0; m < 2 * TQ; ++m) {
-    const f32x4 bias = ld4(TL + G::TL_QKV + m * 16 + 4 * g);
-#pragma unroll
-    for (int w = 0; w < 3; ++w) QK[m][w] = bias;
-  }
-  float qkr[2 * SR][3];
-  zero_rows(qkr);
-  gemm3_rows<2 * TQ, G::KQ_D, G::KS_D, G::MT_D, 2 * TQ, 2 * SR>(QK, ring.cur, X, lane, qkr, TL + G::TL_RQ, g);
-  rows_finish(qkr);
   float qr[SR][3], kr[SR][3];
+  if constexpr (F0) {
+    qkv_fold<H, 2 * TQ>(QK, 0, 2 * TQ, tab, ba, lane, g);
 #pragma unroll
-  for (int n = 0; n < SR; ++n)
+    for (int n = 0; n < SR; ++n)
 #pragma unroll
-    for (int w = 0; w < 3; ++w) {
-      qr[n][w] = qkr[n][w] + TL[G::TL_RQB + n];
-      kr[n][w] = qkr[SR + n][w] + TL[G::TL_RQB + SR + n];
+      for (int w = 0; w < 3; ++w) {
+        qr[n][w] = row_fold<H>(0, n, w, tab, ba, g) + row_fold_bias<H>(0, n, w, tab);
+        kr[n][w] = row_fold<H>(1, n, w, tab, ba, g) + row_fold_bias<H>(1, n, w, tab);
+      }
+  } else {
+#pragma unroll
+    for (int m = 0; m < 2 * TQ; ++m) {
+      const f32x4 bias = ld4(TL + G::TL_QKV + m * 16 + 4 * g);
+#pragma unroll
+      for (int w = 0; w < 3; ++w) QK[m][w] = bias;
     }
+    float qkr[2 * SR][3];
+    zero_rows(qkr);
+    gemm3_rows<2 * TQ, G::KQ_D, G::KS_D, G::MT_D, 2 * TQ, 2 * SR>(QK, ring.cur, X, lane, qkr, TL + G::TL_RQ, g);
+    rows_finish(qkr);
+#pragma unroll
+    for (int n = 0; n < SR; ++n)
+#pragma unroll
+      for (int w = 0; w < 3; ++w) {
+        qr[n][w] = qkr[n][w] + TL[G::TL_RQB + n];
+        kr[n][w] = qkr[SR + n][w] + TL[G::TL_RQB + SR + n];
+      }
+  }
   ring.advance();
   // scores of both heads; the shared tile's slot 4r+g belongs to head 0 below HT
   float P0[3][3], P1[3][3];
@@ -273,17 +315,29 @@ PGP_DEV void encoder_layer_tail(f32x4 (&X)[Geo<H>::MT_D][3], Ring<H>& ring, cons
   }
   // [S1] v, P.v, out_proj (+ residual), norm1
   f32x4 V[TQ][3];
+  float vr[SR][3];  // VALU v rows including their bias
+  if constexpr (F0) {
+    qkv_fold<H, TQ>(V, 2 * TQ, TQ, tab, ba, lane, g);
 #pragma unroll
-  for (int t = 0; t < TQ; ++t) {
-    const f32x4 bias = ld4(TL + G::TL_QKV + (2 * TQ + t) * 16 + 4 * g);
+    for (int n = 0; n < SR; ++n)
 #pragma unroll
-    for (int w = 0; w < 3; ++w) V[t][w] = bias;
+      for (int w = 0; w < 3; ++w) vr[n][w] = row_fold<H>(2, n, w, tab, ba, g) + row_fold_bias<H>(2, n, w, tab);
+  } else {
+#pragma unroll
+    for (int t = 0; t < TQ; ++t) {
+      const f32x4 bias = ld4(TL + G::TL_QKV + (2 * TQ + t) * 16 + 4 * g);
+#pragma unroll
+      for (int w = 0; w < 3; ++w) V[t][w] = bias;
+    }
+    zero_rows(vr);
+    gemm3_rows<TQ, G::KQ_D, G::KS_D, G::MT_D, TQ, SR>(V, ring.cur, X, lane, vr,
+                                                           TL + G::TL_RQ + 2 * SR * G::KQ_D * 16, g);
+    rows_finish(vr);
+#pragma unroll
+    for (int n = 0; n < SR; ++n)
+#pragma unroll
+      for (int w = 0; w < 3; ++w) vr[n][w] += TL[G::TL_RQB + 2 * SR + n];
   }
-  float vr[SR][3];
-  zero_rows(vr);
-  gemm3_rows<TQ, G::KQ_D, G::KS_D, G::MT_D, TQ, SR>(V, ring.cur, X, lane, vr,
-                                                         TL + G::TL_RQ + 2 * SR * G::KQ_D * 16, g);
-  rows_finish(vr);
   f32x4 O[TQ + 1][3];
 #pragma unroll
   for (int w = 0; w < 3; ++w) {
@@ -300,9 +354,7 @@ PGP_DEV void encoder_layer_tail(f32x4 (&X)[Geo<H>::MT_D][3], Ring<H>& ring, cons
     }
     float orr[SR][1];
 #pragma unroll
-    for (int n = 0; n < SR; ++n) orr[n][0] = P1[w][0] * (vr[n][0] + TL[G::TL_RQB + 2 * SR + n]) +
-                                             P1[w][1] * (vr[n][1] + TL[G::TL_RQB + 2 * SR + n]) +
-                                             P1[w][2] * (vr[n][2] + TL[G::TL_RQB + 2 * SR + n]);
+    for (int n = 0; n < SR; ++n) orr[n][0] = P1[w][0] * vr[n][0] + P1[w][1] * vr[n][1] + P1[w][2] * vr[n][2];
     float o3 = 0.f;
 #pragma unroll
     for (int n = 0; n < SR; ++n) o3 = g == n ? orr[n][0] : o3;
@@ -360,16 +412,21 @@ PGP_DEV void encoder_layer_tail(f32x4 (&X)[Geo<H>::MT_D][3], Ring<H>& ring, cons
   layer_norm_tiles<H>(acc, X, TL + G::TL_LN2G, TL + G::TL_LN2B, g);
 }
 
-// One encoder layer; weights arrive stage by stage through the ring.
-template <int H>
-PGP_DEV void encoder_layer(f32x4 (&X)[Geo<H>::MT_D][3], Ring<H>& ring, const float* TL, int lane) {
+// One encoder layer; weights arrive stage by stage through the ring.  F0:
+// layer 0, q/k/v from the folded raw-feature product.
+template <int H, bool F0>
+PGP_DEV void encoder_layer(f32x4 (&X)[Geo<H>::MT_D][3], Ring<H>& ring, const float* TL, int lane,
+                           const float* tab, const float (&ba)[3]) {
   using G = Geo<H>;
   const int g = lane >> 4;
   f32x4 acc[G::MT_D][3];
   f32x4 QKV[3 * G::TP][3];
   f32x4 O[G::TP][3];
   // [S0] qkv pass 0
-  qkv_gemm<H>(QKV, ring.cur, TL + G::TL_QKV, X, lane, g);
+  if constexpr (F0)
+    qkv_fold<H, 3 * G::TP>(QKV, 0, 3 * G::TP, tab, ba, lane, g);
+  else
+    qkv_gemm<H>(QKV, ring.cur, TL + G::TL_QKV, X, lane, g);
   ring.advance();
   attention<H>(QKV, O);
   // [S1] out_proj pass 0 (+ qkv pass 1)
@@ -381,7 +438,10 @@ PGP_DEV void encoder_layer(f32x4 (&X)[Geo<H>::MT_D][3], Ring<H>& ring, const flo
   }
   gemm3<G::MT_D, G::KQ_O, G::KS_O, G::TP>(acc, ring.cur, O, lane);
   if constexpr (G::NPASS == 2) {
-    qkv_gemm<H>(QKV, ring.cur + G::G_O * G::FQ, TL + G::TL_QKV + 3 * G::TP * 16, X, lane, g);
+    if constexpr (F0)
+      qkv_fold<H, 3 * G::TP>(QKV, 3 * G::TP, 3 * G::TP, tab, ba, lane, g);
+    else
+      qkv_gemm<H>(QKV, ring.cur + G::G_O * G::FQ, TL + G::TL_QKV + 3 * G::TP * 16, X, lane, g);
     ring.advance();
     attention<H>(QKV, O);
     // [S2] out_proj pass 1 (+ f1)
@@ -453,12 +513,13 @@ __global__ __launch_bounds__(kEncWaves * 64, 2) void encoder_kernel(FwdArgs a) {
 #pragma unroll
       for (int w = 0; w < 3; ++w) X[mt][w] = mfma(aw, ba[w], ld4(tab + G::T_TE + w * G::DP + 16 * mt + 4 * g));
     }
-#pragma unroll 1
-    for (int l = 0; l < kLayers; ++l) {
-      if constexpr (G::TAIL)
-        encoder_layer_tail<H>(X, ring, tab + G::T_L0 + l * G::TL_SIZE, lane);
-      else
-        encoder_layer<H>(X, ring, tab + G::T_L0 + l * G::TL_SIZE, lane);
+    static_assert(kLayers == 2, "layer 0 (folded q/k/v) + layer 1");
+    if constexpr (G::TAIL) {
+      encoder_layer_tail<H, true>(X, ring, tab + G::T_L0, lane, tab, ba);
+      encoder_layer_tail<H, false>(X, ring, tab + G::T_L0 + G::TL_SIZE, lane, tab, ba);
+    } else {
+      encoder_layer<H, true>(X, ring, tab + G::T_L0, lane, tab, ba);
+      encoder_layer<H, false>(X, ring, tab + G::T_L0 + G::TL_SIZE, lane, tab, ba);
     }
 
     if (active) {

@@ -158,7 +158,15 @@ struct Geo {
   static constexpr int TL_RO = TL_RQB + (TAIL ? 8 : 0);      // [XR][KQ_OT][4][4] out_proj rows
   static constexpr int TL_RF = TL_RO + XR * KQ_OT * 16;      // [XR][KQ_F][4][4] linear2 rows
   static constexpr int TL_SIZE = TL_RF + XR * KQ_F * 16;
-  static constexpr int T_DEC = T_L0 + kLayers * TL_SIZE;  // [MT_O*16] decoder bias
+  // layer 0's q/k/v folded onto the aggregated raw features (X0 is affine in
+  // them): one K=4 A fragment per q/k/v output tile (k = raw feature, lane
+  // groups 0..2) and per-step biases; tail-mode VALU rows likewise
+  static constexpr int NQT = TAIL ? TQ : NPASS * TP;       // tiles per q / k / v
+  static constexpr int T_F0 = T_L0 + kLayers * TL_SIZE;    // [3*NQT][64] A fragments
+  static constexpr int T_F0B = T_F0 + 3 * NQT * 64;        // [3 steps][3*NQT*16] biases
+  static constexpr int T_F0R = T_F0B + 9 * NQT * 16;       // [3][SR][4] VALU-row weights
+  static constexpr int T_F0RB = T_F0R + 3 * SR * 4;        // [3 steps][3*SR] VALU-row biases
+  static constexpr int T_DEC = T_F0RB + round_up(9 * SR, 4);  // [MT_O*16] decoder bias
   static constexpr int T_PROTO = T_DEC + MT_O * 16;         // [K][2]
   static constexpr int t_size(int K) { return T_PROTO + round_up(2 * K, 4); }
 

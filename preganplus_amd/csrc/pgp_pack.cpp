@@ -12,6 +12,9 @@
 //     te(h_j) = Wte (Wfc sum_i a_ij x_i) + b = (Wte Wfc) agg_j + b
 //   edge scores: a . [z_i || z_j] = (Wfc^T a_src) . x_i + (Wfc^T a_dst) . x_j
 //   attention scale 1/sqrt(head_dim) folded into Wq, bq.
+//   layer 0's q/k/v: X0 is affine in the aggregated raw features, so
+//     Win X0 + bin = (Win Wte Wfc) agg + (Win (bte + pe[w]) + bin), one K=3
+//     product per output row and per-step biases.
 #include "pgp_pack.hpp"
 
 #include <cmath>
@@ -382,6 +385,69 @@ std::string pack_t(int K, const double* blob, size_t len, Packed* P) {
           for (int e = 0; e < 4; ++e)
             TL[G::TL_RF + ((n * G::KQ_F + q4) * 4 + g) * 4 + e] =
                 (float)S.l2W[(16 * G::MT_X + n) * 64 + 16 * q4 + 4 * g + e];
+  }
+
+  // ---- layer 0's q/k/v folded onto the aggregated raw features ----
+  // X0[c] = sum_f A[c][f] agg[f] + teB[c] + pe[w][c], A = Wte Wfc, so
+  // qkv[src] = sum_f (Win A)[src][f] agg[f] + (inB + Win (teB + pe[w]))[src]
+  {
+    const LayerSrc& S = ly[0];
+    std::vector<double> A((size_t)d * 3, 0.0);
+    for (int c = 0; c < d; ++c)
+      for (int f = 0; f < 3; ++f)
+        for (int k = 0; k < d; ++k) A[c * 3 + f] += teW[c * d + k] * fcW[k * 3 + f];
+    auto fold = [&](int src, double* wf, double* bw) {  // wf[3], bw[3 steps]
+      const double sc = src < d ? scale : 1.0;
+      for (int f = 0; f < 3; ++f) {
+        double acc = 0;
+        for (int c = 0; c < d; ++c) acc += S.inW[(size_t)src * d + c] * A[c * 3 + f];
+        wf[f] = acc * sc;
+      }
+      for (int w = 0; w < 3; ++w) {
+        double acc = S.inB[src];
+        for (int c = 0; c < d; ++c) acc += S.inW[(size_t)src * d + c] * (teB[c] + pe[w * d + c]);
+        bw[w] = acc * sc;
+      }
+    };
+    // (tile, C-row) -> source row of in_proj, or -1
+    auto tile_src = [&](int T, int i) -> int {
+      int hh, e, m;
+      if constexpr (G::TAIL) {
+        m = T / G::TQ;
+        if (!tail_slot<H>(T % G::TQ, i, &hh, &e)) return -1;
+      } else {
+        const int p = T / (3 * G::TP), r = T % (3 * G::TP), tp = r % G::TP;
+        m = r / G::TP;
+        const int R = 16 * tp + i;
+        if (G::P8) {
+          const int g = (R % 16) / 4, rr = R % 4;
+          hh = g >> 1;
+          e = 4 * (g & 1) + rr;
+        } else {
+          hh = p;
+          e = featX(R);
+        }
+        if (e >= G::HD) return -1;
+      }
+      return m * d + hh * G::HD + e;
+    };
+    for (int T0 = 0; T0 < 3 * G::NQT; ++T0)
+      for (int i = 0; i < 16; ++i) {
+        const int src = tile_src(T0, i);
+        if (src < 0) continue;
+        double wf[3], bw[3];
+        fold(src, wf, bw);
+        for (int g = 0; g < 3; ++g) T[G::T_F0 + T0 * 64 + 16 * g + i] = (float)wf[g];
+        for (int w = 0; w < 3; ++w) T[G::T_F0B + (w * 3 * G::NQT + T0) * 16 + i] = (float)bw[w];
+      }
+    for (int m = 0; m < 3; ++m)
+      for (int n = 0; n < G::SR; ++n) {
+        const int src = m * d + G::HD + 16 * G::HF + 16 - G::HT + n;
+        double wf[3], bw[3];
+        fold(src, wf, bw);
+        for (int g = 0; g < 3; ++g) T[G::T_F0R + (m * G::SR + n) * 4 + g] = (float)wf[g];
+        for (int w = 0; w < 3; ++w) T[G::T_F0RB + w * 3 * G::SR + m * G::SR + n] = (float)bw[w];
+      }
   }
 
   // ---- decoders: rows n = 4*host + {l0, l1, p0, p1} ----
