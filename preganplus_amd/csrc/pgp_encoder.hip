@@ -313,31 +313,61 @@ PGP_DEV void encoder_layer_tail(f32x4 (&X)[Geo<H>::MT_D][3], Ring<H>& ring, cons
     P1[w][1] = e11 * i1;
     P1[w][2] = e12 * i1;
   }
+  f32x4 acc[G::MT_D][3];
+#pragma unroll
+  for (int mt = 0; mt < G::MT_D; ++mt) {
+    const f32x4 bo = ld4(TL + G::TL_BO + 16 * mt + 4 * g);
+#pragma unroll
+    for (int w = 0; w < 3; ++w) acc[mt][w] = bo + X[mt][w];
+  }
+  if constexpr (F0) {
+    // [S1] layer 0: out_proj through the attention, folded (no v, no P.v):
+    // B operands per window, raw-feature / key-step slot g < 3:
+    //   y_hh[w] = sum_w' P_hh[w][w'] agg_w'[g],  p_hh[w] = P_hh[w][g]
+#pragma unroll
+    for (int w = 0; w < 3; ++w) {
+      const float y0 = P0[w][0] * ba[0] + P0[w][1] * ba[1] + P0[w][2] * ba[2];
+      const float y1 = P1[w][0] * ba[0] + P1[w][1] * ba[1] + P1[w][2] * ba[2];
+      const float p0 = g == 0 ? P0[w][0] : g == 1 ? P0[w][1] : g == 2 ? P0[w][2] : 0.f;
+      const float p1 = g == 0 ? P1[w][0] : g == 1 ? P1[w][1] : g == 2 ? P1[w][2] : 0.f;
+#pragma unroll
+      for (int mt = 0; mt < G::MT_X; ++mt) {
+        acc[mt][w] = mfma(tab[G::T_F0O + (0 * G::MT_X + mt) * 64 + lane], y0, acc[mt][w]);
+        acc[mt][w] = mfma(tab[G::T_F0O + (1 * G::MT_X + mt) * 64 + lane], p0, acc[mt][w]);
+        acc[mt][w] = mfma(tab[G::T_F0O + (2 * G::MT_X + mt) * 64 + lane], y1, acc[mt][w]);
+        acc[mt][w] = mfma(tab[G::T_F0O + (3 * G::MT_X + mt) * 64 + lane], p1, acc[mt][w]);
+      }
+      float ro[G::XR];
+#pragma unroll
+      for (int n = 0; n < G::XR; ++n) {
+        const float* rw = tab + G::T_F0OR + n * 16;
+        const float part = g < 3 ? rw[g] * y0 + rw[4 + g] * p0 + rw[8 + g] * y1 + rw[12 + g] * p1 : 0.f;
+        ro[n] = xsum(part, true);
+      }
+      float rsel = 0.f;
+#pragma unroll
+      for (int n = 0; n < G::XR; ++n) rsel = g == n ? ro[n] : rsel;
+      acc[G::MT_X][w][0] += rsel;
+    }
+    layer_norm_tiles<H>(acc, X, TL + G::TL_LN1G, TL + G::TL_LN1B, g);
+  } else {
   // [S1] v, P.v, out_proj (+ residual), norm1
   f32x4 V[TQ][3];
   float vr[SR][3];  // VALU v rows including their bias
-  if constexpr (F0) {
-    qkv_fold<H, TQ>(V, 2 * TQ, TQ, tab, ba, lane, g);
 #pragma unroll
-    for (int n = 0; n < SR; ++n)
+  for (int t = 0; t < TQ; ++t) {
+    const f32x4 bias = ld4(TL + G::TL_QKV + (2 * TQ + t) * 16 + 4 * g);
 #pragma unroll
-      for (int w = 0; w < 3; ++w) vr[n][w] = row_fold<H>(2, n, w, tab, ba, g) + row_fold_bias<H>(2, n, w, tab);
-  } else {
-#pragma unroll
-    for (int t = 0; t < TQ; ++t) {
-      const f32x4 bias = ld4(TL + G::TL_QKV + (2 * TQ + t) * 16 + 4 * g);
-#pragma unroll
-      for (int w = 0; w < 3; ++w) V[t][w] = bias;
-    }
-    zero_rows(vr);
-    gemm3_rows<TQ, G::KQ_D, G::KS_D, G::MT_D, TQ, SR>(V, ring.cur, X, lane, vr,
-                                                           TL + G::TL_RQ + 2 * SR * G::KQ_D * 16, g);
-    rows_finish(vr);
-#pragma unroll
-    for (int n = 0; n < SR; ++n)
-#pragma unroll
-      for (int w = 0; w < 3; ++w) vr[n][w] += TL[G::TL_RQB + 2 * SR + n];
+    for (int w = 0; w < 3; ++w) V[t][w] = bias;
   }
+  zero_rows(vr);
+  gemm3_rows<TQ, G::KQ_D, G::KS_D, G::MT_D, TQ, SR>(V, ring.cur, X, lane, vr, TL + G::TL_RQ + 2 * SR * G::KQ_D * 16,
+                                                         g);
+  rows_finish(vr);
+#pragma unroll
+  for (int n = 0; n < SR; ++n)
+#pragma unroll
+    for (int w = 0; w < 3; ++w) vr[n][w] += TL[G::TL_RQB + 2 * SR + n];
   f32x4 O[TQ + 1][3];
 #pragma unroll
   for (int w = 0; w < 3; ++w) {
@@ -360,13 +390,6 @@ PGP_DEV void encoder_layer_tail(f32x4 (&X)[Geo<H>::MT_D][3], Ring<H>& ring, cons
     for (int n = 0; n < SR; ++n) o3 = g == n ? orr[n][0] : o3;
     O[TQ][w] = f32x4{o3, 0.f, 0.f, 0.f};
   }
-  f32x4 acc[G::MT_D][3];
-#pragma unroll
-  for (int mt = 0; mt < G::MT_D; ++mt) {
-    const f32x4 bo = ld4(TL + G::TL_BO + 16 * mt + 4 * g);
-#pragma unroll
-    for (int w = 0; w < 3; ++w) acc[mt][w] = bo + X[mt][w];
-  }
   {
     float ro[G::XR][3];
     zero_rows(ro);
@@ -377,6 +400,7 @@ PGP_DEV void encoder_layer_tail(f32x4 (&X)[Geo<H>::MT_D][3], Ring<H>& ring, cons
     for (int w = 0; w < 3; ++w) acc[G::MT_X][w][0] += pick_row<G::XR>(ro, w, g);
   }
   layer_norm_tiles<H>(acc, X, TL + G::TL_LN1G, TL + G::TL_LN1B, g);
+  }  // F0
   ring.advance();
   // [S2] relu(W1 x + b1), W2 . h + b2 + x, norm2
   f32x4 F1[G::MT_F][3];

@@ -166,7 +166,12 @@ struct Geo {
   static constexpr int T_F0B = T_F0 + 3 * NQT * 64;        // [3 steps][3*NQT*16] biases
   static constexpr int T_F0R = T_F0B + 9 * NQT * 16;       // [3][SR][4] VALU-row weights
   static constexpr int T_F0RB = T_F0R + 3 * SR * 4;        // [3 steps][3*SR] VALU-row biases
-  static constexpr int T_DEC = T_F0RB + round_up(9 * SR, 4);  // [MT_O*16] decoder bias
+  // tail mode, layer 0's out_proj folded through the attention (v affine in the
+  // raw features too): out = sum_head (Wo Fv) (P x-bar) + (Wo bv_w') P + bo, as
+  // K=4 A fragments [head][G|C][MT_X][64] and VALU rows [XR][head][G|C][4]
+  static constexpr int T_F0O = T_F0RB + round_up(9 * SR, 4);
+  static constexpr int T_F0OR = T_F0O + (TAIL ? 4 * MT_X * 64 : 0);
+  static constexpr int T_DEC = T_F0OR + (TAIL ? XR * 16 : 0);  // [MT_O*16] decoder bias
   static constexpr int T_PROTO = T_DEC + MT_O * 16;         // [K][2]
   static constexpr int t_size(int K) { return T_PROTO + round_up(2 * K, 4); }
 

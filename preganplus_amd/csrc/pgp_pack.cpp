@@ -14,7 +14,8 @@
 //   attention scale 1/sqrt(head_dim) folded into Wq, bq.
 //   layer 0's q/k/v: X0 is affine in the aggregated raw features, so
 //     Win X0 + bin = (Win Wte Wfc) agg + (Win (bte + pe[w]) + bin), one K=3
-//     product per output row and per-step biases.
+//     product per output row and per-step biases; in tail mode its out_proj
+//     too: Wo P V = sum_head (Wo Fv)(P agg) + (Wo bv_w') P (v affine in agg).
 #include "pgp_pack.hpp"
 
 #include <cmath>
@@ -440,6 +441,40 @@ std::string pack_t(int K, const double* blob, size_t len, Packed* P) {
         for (int g = 0; g < 3; ++g) T[G::T_F0 + T0 * 64 + 16 * g + i] = (float)wf[g];
         for (int w = 0; w < 3; ++w) T[G::T_F0B + (w * 3 * G::NQT + T0) * 16 + i] = (float)bw[w];
       }
+    if constexpr (G::TAIL) {  // out_proj through the attention: per head hh and output c
+      // Gh[c][f] = sum_e Wo[c][hh*HD+e] Fv[e][f], Ch[c][w'] = sum_e Wo[c][hh*HD+e] bv_w'[e]
+      std::vector<double> Gm((size_t)2 * d * 3, 0.0), Cm((size_t)2 * d * 3, 0.0);
+      for (int hh = 0; hh < 2; ++hh)
+        for (int e = 0; e < G::HD; ++e) {
+          double wf[3], bw[3];
+          fold(2 * d + hh * G::HD + e, wf, bw);
+          for (int c = 0; c < d; ++c) {
+            const double wo = S.outW[(size_t)c * d + hh * G::HD + e];
+            for (int f = 0; f < 3; ++f) {
+              Gm[((size_t)hh * d + c) * 3 + f] += wo * wf[f];
+              Cm[((size_t)hh * d + c) * 3 + f] += wo * bw[f];
+            }
+          }
+        }
+      for (int hh = 0; hh < 2; ++hh)
+        for (int mt = 0; mt < G::MT_X; ++mt)
+          for (int i = 0; i < 16; ++i) {
+            const int c = featX(16 * mt + i);
+            if (c >= d) continue;
+            for (int g = 0; g < 3; ++g) {
+              T[G::T_F0O + ((hh * 2 + 0) * G::MT_X + mt) * 64 + 16 * g + i] = (float)Gm[((size_t)hh * d + c) * 3 + g];
+              T[G::T_F0O + ((hh * 2 + 1) * G::MT_X + mt) * 64 + 16 * g + i] = (float)Cm[((size_t)hh * d + c) * 3 + g];
+            }
+          }
+      for (int n = 0; n < G::XR; ++n) {
+        const int c = 16 * G::MT_X + n;
+        for (int hh = 0; hh < 2; ++hh)
+          for (int g = 0; g < 3; ++g) {
+            T[G::T_F0OR + n * 16 + (hh * 2 + 0) * 4 + g] = (float)Gm[((size_t)hh * d + c) * 3 + g];
+            T[G::T_F0OR + n * 16 + (hh * 2 + 1) * 4 + g] = (float)Cm[((size_t)hh * d + c) * 3 + g];
+          }
+      }
+    }
     for (int m = 0; m < 3; ++m)
       for (int n = 0; n < G::SR; ++n) {
         const int src = m * d + G::HD + 16 * G::HF + 16 - G::HT + n;
