@@ -90,6 +90,7 @@ def main():
     ap.add_argument("--batch", type=int, default=65536, help="windows per GPU per step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--no-gan", action="store_true", help="tune config: Transformer tuning step only")
     ap.add_argument("--config", choices=["c2", "fleet", "tune", "fpe"], default="c2",
                     help="c2: BASELINE config 2 (default, the headline line); fleet: config 5 "
                          "(1024-host fleet = 64 cells of 16 hosts, shipped weights); tune: config 3 "
@@ -272,26 +273,43 @@ def bench_fleet(args):
 
 def bench_tune(args):
     """BASELINE config 3: one semi-supervised tuning step per iteration on a
-    local batch of windows per GPU: HIP forward with saved activations, loss
-    gradient, backward, one flat RCCL all-reduce of the gradients, AdamW.
-    Labels/targets are synthetic (fixed) so the timed region is device work."""
+    local batch of windows per GPU: the Transformer's forward with
+    saved activations, loss gradient and backward (pgp_tune.hip), then the GAN
+    step of the same windows (Gen + Disc forward, Disc BCE backward, Gen BCE
+    backward through the updated Disc), each section's gradients summed over
+    ranks by one flat RCCL all-reduce before its AdamW step, in the reference's
+    order (PreGANPlus.py:60-81 Disc then Gen; train.py:42-57).  Labels, CE
+    weights, prototype targets and GAN labels are synthetic and fixed, so the
+    timed region is device work."""
     from preganplus_amd import train as TR
     world, rank, device = _dist_setup()
     H = args.hosts
     B = args.batch if args.batch != 65536 else 1024
     w = W.synth_weights(H, seed=0)
     tr = TR.Trainer(H, w, device=device, max_batch=B)
-    x, _ = synth_inputs(B, H, device, 5 + rank)
+    x, s = synth_inputs(B, H, device, 5 + rank)
     g = torch.Generator(device=device).manual_seed(17 + rank)
     y = (torch.rand((B, H), generator=g, device=device) < 0.1).to(torch.int32)
     mult = torch.ones((B, H), device=device)
     tgt = torch.rand((B, H, 2), generator=g, device=device)
+    emb = torch.where(y[..., None] > 0, torch.rand((B, H, 2), generator=g, device=device), 0.0).contiguous()
+    lab = (torch.rand((B,), generator=g, device=device) < 0.5).to(torch.float32)
+    gan_target = torch.stack([1.0 - lab, lab], dim=1).contiguous()
+    gan = not args.no_gan
 
     def step():
         tr.tune_forward(x)
         tr.tune_backward(B, y, mult, tgt)
         tr.all_reduce_grads("transformer")
         tr.adam_step("transformer")
+        if gan:
+            tr.gan_forward(emb, s)
+            tr.gan_disc_backward(gan_target)
+            tr.all_reduce_grads("disc")
+            tr.adam_step("disc")
+            tr.gan_gen_backward(B)
+            tr.all_reduce_grads("gen")
+            tr.adam_step("gen")
 
     for _ in range(args.warmup):
         step()
@@ -302,7 +320,8 @@ def bench_tune(args):
             "unit": "windows/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": el / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "fp32", "data": "synthetic windows, labels and targets",
-            "config": {"workload": f"C3: tuning step, {H} hosts, {B} windows per GPU", "hosts": H,
+            "config": {"workload": f"C3: tuning step ({'Transformer + GAN' if gan else 'Transformer only'}), "
+                                   f"{H} hosts, {B} windows per GPU", "hosts": H,
                        "windows_per_gpu": B, "parallelism": f"dp{world} + RCCL all-reduce"}}), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
