@@ -193,11 +193,13 @@ int pgp_forward_fpe_stage(pgp_model* m, int stage, int batch, const float* windo
  *   pgp_adamw          torch.optim.AdamW.step (utils.py:65)
  * ---------------------------------------------------------------------- */
 size_t pgp_master_len(int n_hosts);               /* floats in P / G            */
-size_t pgp_gan_scratch_len(int n_hosts);          /* floats per window          */
 /* floats of tuning workspace for a batch (activations saved by the forward for
  * the backward, token-major, plus split-K / weight-gradient partial slabs).
  * Sizes grow with batch: a workspace for B_max serves every batch <= B_max. */
 size_t pgp_tune_workspace_len(int n_hosts, int batch);
+/* floats of GAN-step workspace for a batch (per-window activation rows, split-K
+ * partials, weight transposes); grows with batch like the tuning workspace. */
+size_t pgp_gan_workspace_len(int n_hosts, int batch);
 size_t pgp_master_offset(int n_hosts, int section); /* 0 transformer, 1 gen, 2 disc */
 
 /* windows [B,3,3H]; outputs logits [B,H,2], protos [B,H,2] (sigmoid) and, if
@@ -212,12 +214,15 @@ int pgp_tune_forward(int n_hosts, int batch, const float* windows, const float* 
 int pgp_tune_backward(int n_hosts, int batch, const float* P, float* G, float* workspace, const float* logits,
                       const float* protos, const int* y, const float* mult, const float* tgt, void* stream);
 /* emb [B,2H] (masked prototype embeddings), sched [B,H,H]; outputs the new
- * schedule ns [B,H,H] and probs [B,2]; gscratch [B, pgp_gan_scratch_len]. */
-int pgp_gan_forward(int n_hosts, int batch, const float* emb, const float* sched, const float* P, float* gscratch,
+ * schedule ns [B,H,H] and probs [B,2]; workspace pgp_gan_workspace_len(H, >= B)
+ * floats, shared by the three calls of one step (same batch).  The backward
+ * calls accumulate the gradient summed over the batch's windows into G. */
+int pgp_gan_forward(int n_hosts, int batch, const float* emb, const float* sched, const float* P, float* workspace,
                     float* ns, float* probs, void* stream);
-int pgp_gan_disc_backward(int n_hosts, int batch, const float* target, const float* P, float* G, float* gscratch,
+/* target [B,2]: the BCE label (PreGANPlus.py:65-66) */
+int pgp_gan_disc_backward(int n_hosts, int batch, const float* target, const float* P, float* G, float* workspace,
                           void* stream);
-int pgp_gan_gen_backward(int n_hosts, int batch, const float* P, float* G, float* gscratch, void* stream);
+int pgp_gan_gen_backward(int n_hosts, int batch, const float* P, float* G, float* workspace, void* stream);
 
 typedef struct {
   long long offset;  /* first element of the tensor in P/G/m/v */

@@ -314,7 +314,9 @@ size_t pgp_tune_workspace_len(int n_hosts, int batch) {
   TunePlan p;
   return (supported(n_hosts) && tune_plan(n_hosts, batch, &p)) ? (size_t)p.total : 0;
 }
-size_t pgp_gan_scratch_len(int n_hosts) { return supported(n_hosts) ? (size_t)gan_scratch_floats(n_hosts) : 0; }
+size_t pgp_gan_workspace_len(int n_hosts, int batch) {
+  return supported(n_hosts) ? (size_t)gan_workspace_floats(n_hosts, batch) : 0;
+}
 
 int pgp_tune_forward(int n_hosts, int batch, const float* windows, const float* P, float* workspace, float* latent,
                      float* logits, float* protos, void* stream) {
@@ -341,35 +343,35 @@ int pgp_tune_backward(int n_hosts, int batch, const float* P, float* G, float* w
   return PGP_OK;
 }
 
-int pgp_gan_forward(int n_hosts, int batch, const float* emb, const float* sched, const float* P, float* gscratch,
+int pgp_gan_forward(int n_hosts, int batch, const float* emb, const float* sched, const float* P, float* workspace,
                     float* ns, float* probs, void* stream) {
   long tr, go, dof, all;
   if (!master_offsets(n_hosts, &tr, &go, &dof, &all)) return fail(PGP_ERR_UNSUPPORTED, "host count");
-  if (batch < 0 || (batch > 0 && (!emb || !sched || !P || !gscratch || !ns || !probs)))
+  if (batch < 0 || (batch > 0 && (!emb || !sched || !P || !workspace || !ns || !probs)))
     return fail(PGP_ERR_ARG, "bad gan_forward arguments");
   if (batch == 0) return PGP_OK;
-  HIPCHK(launch_gan_fwd(n_hosts, batch, emb, sched, P + go, P + dof, gscratch, ns, probs,
+  HIPCHK(launch_gan_fwd(n_hosts, batch, emb, sched, P + go, P + dof, workspace, ns, probs,
                         reinterpret_cast<hipStream_t>(stream)));
   return PGP_OK;
 }
 
-int pgp_gan_disc_backward(int n_hosts, int batch, const float* target, const float* P, float* G, float* gscratch,
+int pgp_gan_disc_backward(int n_hosts, int batch, const float* target, const float* P, float* G, float* workspace,
                           void* stream) {
   long tr, go, dof, all;
   if (!master_offsets(n_hosts, &tr, &go, &dof, &all)) return fail(PGP_ERR_UNSUPPORTED, "host count");
-  if (batch < 0 || (batch > 0 && (!target || !P || !G || !gscratch))) return fail(PGP_ERR_ARG, "bad arguments");
+  if (batch < 0 || (batch > 0 && (!target || !P || !G || !workspace))) return fail(PGP_ERR_ARG, "bad arguments");
   if (batch == 0) return PGP_OK;
-  HIPCHK(launch_gan_disc_bwd(n_hosts, batch, target, P + dof, G + dof, gscratch,
+  HIPCHK(launch_gan_disc_bwd(n_hosts, batch, target, P + dof, G + dof, workspace,
                              reinterpret_cast<hipStream_t>(stream)));
   return PGP_OK;
 }
 
-int pgp_gan_gen_backward(int n_hosts, int batch, const float* P, float* G, float* gscratch, void* stream) {
+int pgp_gan_gen_backward(int n_hosts, int batch, const float* P, float* G, float* workspace, void* stream) {
   long tr, go, dof, all;
   if (!master_offsets(n_hosts, &tr, &go, &dof, &all)) return fail(PGP_ERR_UNSUPPORTED, "host count");
-  if (batch < 0 || (batch > 0 && (!P || !G || !gscratch))) return fail(PGP_ERR_ARG, "bad arguments");
+  if (batch < 0 || (batch > 0 && (!P || !G || !workspace))) return fail(PGP_ERR_ARG, "bad arguments");
   if (batch == 0) return PGP_OK;
-  HIPCHK(launch_gan_gen_bwd(n_hosts, batch, P + go, P + dof, G + go, gscratch,
+  HIPCHK(launch_gan_gen_bwd(n_hosts, batch, P + go, P + dof, G + go, workspace,
                             reinterpret_cast<hipStream_t>(stream)));
   return PGP_OK;
 }

@@ -59,13 +59,14 @@ hipError_t launch_gan(const FwdArgs& a, hipStream_t st);
 
 // training ops (pgp_train.hip)
 struct AdamArgs;
-long gan_scratch_floats(int H);
+long gan_workspace_floats(int H, int B);
 hipError_t launch_adamw(const AdamArgs& a, hipStream_t st);
+// GAN step (pgp_gantrain.hip); ws = gan_workspace_floats(H, B) floats
 hipError_t launch_gan_fwd(int H, int B, const float* emb, const float* sched, const float* Pg, const float* Pd,
-                          float* scr, float* ns_out, float* probs, hipStream_t st);
-hipError_t launch_gan_disc_bwd(int H, int B, const float* target, const float* Pd, float* Gdd, float* scr,
+                          float* ws, float* ns_out, float* probs, hipStream_t st);
+hipError_t launch_gan_disc_bwd(int H, int B, const float* target, const float* Pd, float* Gdd, float* ws,
                                hipStream_t st);
-hipError_t launch_gan_gen_bwd(int H, int B, const float* Pg, const float* Pd, float* Gdg, float* scr,
+hipError_t launch_gan_gen_bwd(int H, int B, const float* Pg, const float* Pd, float* Gdg, float* ws,
                               hipStream_t st);
 
 #ifdef __HIP_DEVICE_COMPILE__

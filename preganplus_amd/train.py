@@ -99,8 +99,8 @@ class Trainer:
         L.pgp_master_offset.restype = sz
         L.pgp_tune_workspace_len.argtypes = [i32, i32]
         L.pgp_tune_workspace_len.restype = sz
-        L.pgp_gan_scratch_len.argtypes = [i32]
-        L.pgp_gan_scratch_len.restype = sz
+        L.pgp_gan_workspace_len.argtypes = [i32, i32]
+        L.pgp_gan_workspace_len.restype = sz
         L.pgp_tune_forward.argtypes = [i32, i32] + [vp] * 6 + [vp]
         L.pgp_tune_backward.argtypes = [i32, i32] + [vp] * 8 + [vp]
         L.pgp_gan_forward.argtypes = [i32, i32] + [vp] * 6 + [vp]
@@ -120,7 +120,7 @@ class Trainer:
         # token-major activations of the tuning forward (kept for the backward);
         # zero-filled once: feature pads must stay 0 (pgp_tune.hpp)
         self.ws = torch.zeros((L.pgp_tune_workspace_len(H, B),), dtype=f32, device=dev)
-        self.gscr = torch.zeros((B, L.pgp_gan_scratch_len(H)), dtype=f32, device=dev)
+        self.gscr = torch.zeros((L.pgp_gan_workspace_len(H, B),), dtype=f32, device=dev)
         self.logits = torch.zeros((B, H, 2), dtype=f32, device=dev)
         self.protos = torch.zeros((B, H, 2), dtype=f32, device=dev)
         self._fwd_batch = 0

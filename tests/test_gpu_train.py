@@ -181,3 +181,46 @@ def test_batched_tuning_step_is_deterministic():
         tr.tune_backward(B, y, mult, tgt)
         gs.append(tr.G.cpu().numpy().copy())
     assert np.array_equal(gs[0], gs[1])
+
+
+@pytest.mark.parametrize("H,B", [(8, 3), (16, 37), (50, 21), (64, 5), (16, 300)])
+def test_batched_gan_step_matches_autograd(H, B):
+    """GAN step over a ragged batch (pgp_gantrain.hip): new schedule and Disc
+    probabilities within fp32 tolerance of the fp64 forward; Disc gradients of
+    the summed BCE toward per-window targets, and Gen gradients of the summed
+    BCE toward [0,1] through the (unchanged) Disc == autograd (PreGANPlus.py:60-74)."""
+    from preganplus_amd import train as TR
+    w = W.synth_weights(H, seed=4)
+    rng = np.random.Generator(np.random.PCG64(21 + H + B))
+    emb = np.where(rng.uniform(size=(B, H, 1)) < 0.3, rng.uniform(size=(B, H, 2)), 0.0)
+    sched = np.zeros((B, H, H))
+    sched[np.arange(B)[:, None], np.arange(H)[None, :], rng.integers(0, H, size=(B, H))] = 1.0
+    lab = rng.uniform(size=B) < 0.5
+    target = np.stack([1.0 - lab, lab], axis=1).astype(np.float64)
+    tr = TR.Trainer(H, w, max_batch=B)
+    ns, probs = tr.gan_forward(emb, sched)
+    ns, probs = ns.cpu().numpy(), probs.cpu().numpy()
+    tr.gan_disc_backward(target)
+    tr.gan_gen_backward(B)
+    g = tr.G.cpu().numpy()
+    gw = TO.leaf_params(w["gen"])
+    dw = TO.leaf_params(w["disc"])
+    e_t, s_t = torch.tensor(emb), torch.tensor(sched)
+    ns_r = TO.gen_t(gw, e_t, s_t)
+    p_r = TO.disc_t(dw, s_t, ns_r.detach())
+    close(ns, ns_r.detach().numpy(), rel=1e-4, abs_scale=1e-5, what="ns")
+    close(probs, p_r.detach().numpy(), rel=1e-4, abs_scale=1e-5, what="probs")
+    bce = torch.nn.functional.binary_cross_entropy
+    torch.stack([bce(p_r[i], torch.tensor(target[i])) for i in range(B)]).sum().backward()
+    for t in tr.tensors:
+        if t["section"] == "disc":
+            close(g[t["offset"]:t["offset"] + t["n"]], dw[t["name"]].grad.numpy().reshape(-1), rel=1e-3,
+                  abs_scale=1e-4, what="disc " + t["name"])
+    for p in dw.values():
+        p.grad = None
+    p2 = TO.disc_t(dw, s_t, ns_r)
+    torch.stack([bce(p2[i], torch.tensor([0.0, 1.0], dtype=torch.float64)) for i in range(B)]).sum().backward()
+    for t in tr.tensors:
+        if t["section"] == "gen":
+            close(g[t["offset"]:t["offset"] + t["n"]], gw[t["name"]].grad.numpy().reshape(-1), rel=1e-3,
+                  abs_scale=1e-4, what="gen " + t["name"])
