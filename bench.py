@@ -91,11 +91,13 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-gan", action="store_true", help="tune config: Transformer tuning step only")
-    ap.add_argument("--config", choices=["c2", "fleet", "tune", "fpe"], default="c2",
+    ap.add_argument("--config", choices=["c2", "fleet", "tune", "fpe", "gobi"], default="c2",
                     help="c2: BASELINE config 2 (default, the headline line); fleet: config 5 "
                          "(1024-host fleet = 64 cells of 16 hosts, shipped weights); tune: config 3 "
                          "(tuning step fwd+bwd+AdamW, data-parallel with an RCCL all-reduce); fpe: config 4 "
-                         "(PreGAN FPE_16 encoder + K=3 classifier + PreGAN's Gen/Disc, shipped weights)")
+                         "(PreGAN FPE_16 encoder + K=3 classifier + PreGAN's Gen/Disc, shipped weights); "
+                         "gobi: SURVEY 8f row f3, the schedule producer (GOBI's opt() over the "
+                         "energy_latency_16 surrogate, a batch of independent environments)")
     args = ap.parse_args()
     if args.config == "fleet":
         return bench_fleet(args)
@@ -103,6 +105,8 @@ def main():
         return bench_tune(args)
     if args.config == "fpe":
         return bench_fpe(args)
+    if args.config == "gobi":
+        return bench_gobi(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -419,6 +423,53 @@ def bench_fpe(args):
             res["cpu_baseline"] = fpe_cpu_baseline(w, args.cpu_budget)
         else:
             res["cpu_baseline"] = None
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+def bench_gobi(args):
+    """GOBI (scheduler/GOBI.py:19-42, BaGTI/src/opt.py:17-33)
+    over a batch of independent 16-host environments per GPU (the fleet's
+    cells), one pgp_gobi_optimize launch per step, inits drawn from the
+    reference's own scheduling dataset rows (tests/golden/gobi_h16.npz)."""
+    from preganplus_amd.gobi import GOBIOptimizer
+    world, rank, device = _dist_setup()
+    E = args.batch if args.batch != 65536 else 1024
+    z = np.load(os.path.join(ROOT, "tests", "golden", "gobi_h16.npz"))
+    reps = -(-E // z["inits"].shape[0])
+    inits = torch.tensor(np.concatenate([z["inits"]] * reps)[:E], device=device)
+    g = GOBIOptimizer(device=device)
+    out = (torch.empty_like(inits), torch.empty(E, dtype=torch.int32, device=device),
+           torch.empty(E, dtype=torch.float32, device=device))
+    for _ in range(args.warmup):
+        g.optimize(inits, out=out)
+    el = _timed(world, device, lambda: g.optimize(inits, out=out), args.steps)
+    its = out[1].float().mean().item()
+    if rank == 0:
+        macs_it = 2 * (288 * 128 + 128 * 128 + 128 * 64 + 64 * 2)  # forward + input gradient
+        res = {
+            "metric": "GOBI schedules/sec (opt() over energy_latency_16)", "value": E * world * args.steps / el,
+            "unit": "schedules/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": el / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "fp32",
+            "data": "inits = the reference's scheduling dataset rows + synthetic (tests/golden/gobi_h16.npz)",
+            "config": {"workload": f"f3: GOBI, {E} independent 16-host environments per GPU", "hosts": 16,
+                       "environments_per_gpu": E, "mean_iterations": its, "parallelism": f"dp{world}"},
+            "achieved_tflops": 2 * macs_it * (its + 2) * E / (el / args.steps) / 1e12,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            from oracle import gobi_oracle as GO  # CPU baseline leg only
+            sd, _ = GO.load(os.path.join(ROOT, "preganplus_amd", "data", "gobi_energy_latency_16.npz"))
+            torch.set_num_threads(1)
+            t0, n = time.perf_counter(), 0
+            while time.perf_counter() - t0 < args.cpu_budget:
+                GO.opt(sd, z["inits"][n % z["inits"].shape[0]])
+                n += 1
+            dt = time.perf_counter() - t0
+            res["cpu_baseline"] = {"value": n / dt, "unit": "schedules/s", "cores": 1, "kind": "port",
+                                   "sample": f"{n} opt() runs of the torch-CPU restatement (bit-identical to the "
+                                             f"reference's), 1 thread, {dt:.1f}s"}
         print(json.dumps(res), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()

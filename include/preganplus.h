@@ -33,6 +33,9 @@
  *   pgp_tune_* / pgp_gan_* / pgp_adamw / pgp_load_weights_master
  *       online training: tune_model PreGANPlus.py:51-58 (train.py:13-57),
  *       train_gan PreGANPlus.py:60-81 / PreGAN.py:51-71, AdamW utils.py:65
+ *   pgp_gobi_*
+ *       the schedule producer upstream of the path: GOBIScheduler.run_GOBI's
+ *       opt() (scheduler/GOBI.py:19-42, scheduler/BaGTI/src/opt.py:17-33)
  *   pgp_destroy
  *       (object lifetime; no reference counterpart)
  *
@@ -237,6 +240,30 @@ int pgp_adamw(float* P, const float* G, float* exp_avg, float* exp_avg_sq, float
 /* Rebuild the inference layouts from device master weights P (natural fp32)
  * and prototypes [K,2] (host, fp64): the sync after an optimizer step. */
 int pgp_load_weights_master(pgp_model* m, const float* P_device, const double* prototypes);
+
+/* ------------------------------------------------------------------------
+ * GOBI, the schedule producer: replaces
+ * GOBIScheduler.run_GOBI's optimiser (scheduler/GOBI.py:19-42) =
+ * opt() in scheduler/BaGTI/src/opt.py:17-33 over the energy_latency_16
+ * surrogate (scheduler/BaGTI/src/models.py:8-27), for a batch of independent
+ * environments.  Its result's allocation columns are run_model's schedule input
+ * (env.scheduler.result_cache, PreGANPlus.py:117).
+ * ---------------------------------------------------------------------- */
+typedef struct pgp_gobi pgp_gobi;
+/* floats of the surrogate's state dict (find.0.weight [128,288], find.0.bias,
+ * find.2.weight [128,128], find.2.bias, find.4.weight [64,128], find.4.bias,
+ * find.6.weight [2,64], find.6.bias), fp32 row-major; 0 if H is not 16 */
+size_t pgp_gobi_weight_len(int n_hosts);
+int pgp_gobi_create(int n_hosts, const float* weights, size_t len, pgp_gobi** out);
+int pgp_gobi_destroy(pgp_gobi* g);
+const char* pgp_gobi_last_error(void);
+/* device pointers: init / result [E,16,18] (per container: host cpu, container
+ * ips, one-hot host), iterations [E] (opt()'s returned count), fitness [E]
+ * (surrogate value of the result).  max_iters <= 0: the reference's 200.
+ * pre (may be NULL) [E,16,16]: the last step's allocation values before the
+ * one-hot projection (a test tap). */
+int pgp_gobi_optimize(pgp_gobi* g, int n_env, const float* init, float* result, int* iterations,
+                      float* fitness, int max_iters, float* pre, void* stream);
 
 #ifdef __cplusplus
 }

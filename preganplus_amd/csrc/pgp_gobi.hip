@@ -1,0 +1,323 @@
+// pgp_gobi.hip — GOBI, the schedule producer of the decision path (SURVEY §8f
+// row f3): scheduler/GOBI.py:19-42 -> scheduler/BaGTI/src/opt.py:17-33 over
+// the energy_latency_16 surrogate (scheduler/BaGTI/src/models.py:8-27), for a
+// batch of independent environments.
+//
+// One 256-thread workgroup per environment runs the whole optimisation
+// in-kernel (the reference's loop: up to 200 AdamW steps on the input matrix,
+// one-hot projection after each, stop after 31 unchanged steps).  Thread t owns
+// allocation entry t = (container t/16, host t%16): its AdamW moments live in
+// registers, and a row's first-argmax is a 16-lane reduction inside one wave.
+// The MLP (288-128-128-64-2) and its input gradient are VALU dot products over
+// L2-resident weights, read coalesced: forward from transposed copies [K][N],
+// backward from the natural [N][K] rows.  Elementwise semantics follow torch's
+// CPU kernels (softplus threshold 20, tanhshrink = x - tanh x composite,
+// sigmoid backward g(1-y)y, AdamW single-tensor op order); per-iteration AdamW
+// scalars (cosine lr) are computed on the host in double, as torch does.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <string>
+#include <vector>
+
+#include "../../include/preganplus.h"
+#include "pgp_device.hpp"
+
+namespace pgp {
+namespace {
+
+constexpr int kH = 16, kF = 2 + kH, kIn = kH * kF;  // 16 containers x [cpu, ips, one-hot 16] = 288
+constexpr int kN1 = 128, kN2 = 128, kN3 = 64;
+constexpr int kMaxIt = 200, kPatience = 30;
+
+struct GobiW {  // device offsets (floats) into one buffer
+  static constexpr int W1T = 0;                    // [288][128]
+  static constexpr int W1 = W1T + kIn * kN1;       // [128][288]
+  static constexpr int B1 = W1 + kN1 * kIn;        // [128]
+  static constexpr int W2T = B1 + kN1;             // [128][128]
+  static constexpr int W2 = W2T + kN1 * kN2;       // [128][128]
+  static constexpr int B2 = W2 + kN2 * kN1;
+  static constexpr int W3T = B2 + kN2;             // [128][64]
+  static constexpr int W3 = W3T + kN2 * kN3;       // [64][128]
+  static constexpr int B3 = W3 + kN3 * kN2;
+  static constexpr int W4 = B3 + kN3;              // [2][64]
+  static constexpr int B4 = W4 + 2 * kN3;
+  static constexpr int ADAM = B4 + 4;              // [200][4]: decay, step size, sqrt(bc2), lr
+  static constexpr int SIZE = ADAM + kMaxIt * 4;
+};
+
+__device__ __forceinline__ float softplus_f(float x) { return x > 20.f ? x : log1pf(expf(x)); }
+__device__ __forceinline__ float softplus_b(float g, float x) {
+  if (x > 20.f) return g;
+  const float z = expf(x);
+  return g * z / (z + 1.f);
+}
+__device__ __forceinline__ float sigmoid_f(float x) { return 1.f / (1.f + expf(-x)); }
+
+struct GobiLds {
+  float x[kIn];
+  float a1[kN1], h1[kN1], a2[kN2], h2[kN2], a3[kN3], h3[kN3];
+  float g1[kN1], g2[kN2], g3[kN3];
+  float part[256];
+  float o[4];
+  int flag[2];
+};
+
+// forward of the surrogate on L.x (all 256 threads); returns z in L.o[2]
+__device__ void surrogate_fwd(const float* __restrict__ W, GobiLds& L) {
+  const int t = threadIdx.x;
+  {  // layer 1: 128 outputs x 2 halves of K = 288
+    const int o = t & 127, hf = t >> 7;
+    float acc = 0.f;
+    for (int k = hf * 144; k < hf * 144 + 144; ++k) acc = fmaf(W[GobiW::W1T + k * kN1 + o], L.x[k], acc);
+    L.part[t] = acc;
+    __syncthreads();
+    if (t < kN1) {
+      const float a = (L.part[t] + L.part[t + 128]) + W[GobiW::B1 + t];
+      L.a1[t] = a;
+      L.h1[t] = softplus_f(a);
+    }
+    __syncthreads();
+  }
+  {  // layer 2: 128 outputs x 2 halves of K = 128
+    const int o = t & 127, hf = t >> 7;
+    float acc = 0.f;
+    for (int k = hf * 64; k < hf * 64 + 64; ++k) acc = fmaf(W[GobiW::W2T + k * kN2 + o], L.h1[k], acc);
+    L.part[t] = acc;
+    __syncthreads();
+    if (t < kN2) {
+      const float a = (L.part[t] + L.part[t + 128]) + W[GobiW::B2 + t];
+      L.a2[t] = a;
+      L.h2[t] = softplus_f(a);
+    }
+    __syncthreads();
+  }
+  {  // layer 3: 64 outputs x 4 quarters of K = 128
+    const int o = t & 63, q = t >> 6;
+    float acc = 0.f;
+    for (int k = q * 32; k < q * 32 + 32; ++k) acc = fmaf(W[GobiW::W3T + k * kN3 + o], L.h2[k], acc);
+    L.part[t] = acc;
+    __syncthreads();
+    if (t < kN3) {
+      const float a = ((L.part[t] + L.part[t + 64]) + (L.part[t + 128] + L.part[t + 192])) + W[GobiW::B3 + t];
+      L.a3[t] = a;
+      L.h3[t] = a - tanhf(a);  // Tanhshrink
+    }
+    __syncthreads();
+  }
+  if (t < 64) {  // layer 4 (2 outputs) in wave 0, sigmoid, z = 0.8 e + 0.2 l
+    float p0 = W[GobiW::W4 + t] * L.h3[t], p1 = W[GobiW::W4 + kN3 + t] * L.h3[t];
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      p0 += __shfl_xor(p0, off);
+      p1 += __shfl_xor(p1, off);
+    }
+    if (t == 0) {
+      const float o0 = sigmoid_f(p0 + W[GobiW::B4]), o1 = sigmoid_f(p1 + W[GobiW::B4 + 1]);
+      L.o[0] = o0;
+      L.o[1] = o1;
+      L.o[2] = 0.8f * o0 + 0.2f * o1;
+    }
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(256) void gobi_kernel(int E, const float* __restrict__ W, const float* __restrict__ init,
+                                                   float* __restrict__ result, int* __restrict__ iterations,
+                                                   float* __restrict__ fitness, int max_it, float* __restrict__ pre) {
+#pragma clang fp contract(off)  // elementwise steps as torch's separate mul/add
+  __shared__ GobiLds L;
+  const int e = blockIdx.x;
+  if (e >= E) return;  // whole workgroup
+  const int t = threadIdx.x, c = t >> 4, hcol = t & 15;
+  const int xi = c * kF + 2 + hcol;  // this thread's allocation entry in the flattened input
+  for (int k = t; k < kIn; k += 256) L.x[k] = init[(long)e * kIn + k];
+  __syncthreads();
+  float m = 0.f, v = 0.f;
+  int equal = 0, it = 0;
+  while (it < max_it) {
+    surrogate_fwd(W, L);
+    // ---- backward to the input (autograd of z) ----
+    if (t < 64) {  // dz/do = (0.8, 0.2) through the sigmoids; dh3 = W4^T do; through Tanhshrink
+      const float o0 = L.o[0], o1 = L.o[1];
+      const float d0 = 0.8f * (1.f - o0) * o0, d1 = 0.2f * (1.f - o1) * o1;
+      const float gh = W[GobiW::W4 + t] * d0 + W[GobiW::W4 + kN3 + t] * d1;
+      const float th = tanhf(L.a3[t]);
+      L.g3[t] = gh - gh * (1.f - th * th);
+    }
+    __syncthreads();
+    {  // dh2 = W3^T g3 (128 x K=64, 2 halves), through softplus
+      const int o = t & 127, hf = t >> 7;
+      float acc = 0.f;
+      for (int k = hf * 32; k < hf * 32 + 32; ++k) acc = fmaf(W[GobiW::W3 + k * kN2 + o], L.g3[k], acc);
+      L.part[t] = acc;
+      __syncthreads();
+      if (t < kN2) L.g2[t] = softplus_b(L.part[t] + L.part[t + 128], L.a2[t]);
+      __syncthreads();
+    }
+    {  // dh1 = W2^T g2 (128 x K=128), through softplus
+      const int o = t & 127, hf = t >> 7;
+      float acc = 0.f;
+      for (int k = hf * 64; k < hf * 64 + 64; ++k) acc = fmaf(W[GobiW::W2 + k * kN1 + o], L.g2[k], acc);
+      L.part[t] = acc;
+      __syncthreads();
+      if (t < kN1) L.g1[t] = softplus_b(L.part[t] + L.part[t + 128], L.a1[t]);
+      __syncthreads();
+    }
+    // dx for this thread's allocation entry: W1[:, xi] . g1
+    float gx = 0.f;
+    for (int o = 0; o < kN1; ++o) gx = fmaf(W[GobiW::W1 + o * kIn + xi], L.g1[o], gx);
+    // ---- AdamW (torch single-tensor, opt.py:18 defaults) on the entry ----
+    const float* ad = W + GobiW::ADAM + it * 4;
+    const float xold = L.x[xi];
+    float xv = xold * ad[0];
+    m = m + 0.1f * (gx - m);              // exp_avg.lerp_(grad, 1 - beta1)
+    v = v * 0.999f + 0.001f * gx * gx;    // exp_avg_sq.mul_(beta2).addcmul_(grad, grad, 1 - beta2)
+    const float denom = sqrtf(v) / ad[2] + 1e-8f;
+    xv = xv + (-ad[1]) * m / denom;       // addcdiv_: self + value * t1 / t2 (ATen's order)
+    // ---- one-hot of the row's first argmax (opt.py:9-15) ----
+    float best = xv;
+    int bi = hcol;
+#pragma unroll
+    for (int off = 8; off >= 1; off >>= 1) {
+      const float ov = __shfl_xor(best, off);
+      const int oi = __shfl_xor(bi, off);
+      if (ov > best || (ov == best && oi < bi)) {
+        best = ov;
+        bi = oi;
+      }
+    }
+    if (pre) pre[(long)e * kH * kH + t] = xv;  // test tap: the step's values before the projection
+    const float nv = bi == hcol ? 1.f : 0.f;
+    const int changed = nv != xold;
+    if (t == 0) L.flag[0] = 0;
+    __syncthreads();
+    if (changed) L.flag[0] = 1;  // benign race: every writer stores 1
+    L.x[xi] = nv;
+    __syncthreads();
+    equal = L.flag[0] ? 0 : equal + 1;
+    if (equal > kPatience) break;
+    ++it;
+  }
+  surrogate_fwd(W, L);
+  for (int k = t; k < kIn; k += 256) result[(long)e * kIn + k] = L.x[k];
+  if (t == 0) {
+    iterations[e] = it;
+    fitness[e] = L.o[2];
+  }
+}
+
+}  // namespace
+}  // namespace pgp
+
+using namespace pgp;
+
+struct pgp_gobi {
+  int H = 0;
+  float* d_w = nullptr;
+};
+
+namespace {
+thread_local std::string g_gerr;
+int gfail(int code, const std::string& msg) {
+  g_gerr = msg;
+  return code;
+}
+}  // namespace
+
+extern "C" {
+
+size_t pgp_gobi_weight_len(int n_hosts) {
+  if (n_hosts != kH) return 0;
+  return (size_t)kN1 * kIn + kN1 + kN2 * kN1 + kN2 + kN3 * kN2 + kN3 + 2 * kN3 + 2;
+}
+
+int pgp_gobi_create(int n_hosts, const float* weights, size_t len, pgp_gobi** out) {
+  if (!out) return gfail(PGP_ERR_ARG, "out is NULL");
+  *out = nullptr;
+  if (n_hosts != kH) return gfail(PGP_ERR_UNSUPPORTED, "GOBI surrogate: only energy_latency_16 exists (16 hosts)");
+  if (!weights || len != pgp_gobi_weight_len(n_hosts)) return gfail(PGP_ERR_ARG, "GOBI weight length mismatch");
+  // state-dict order: find.0.weight [128,288], find.0.bias, find.2.weight [128,128], find.2.bias,
+  //                   find.4.weight [64,128], find.4.bias, find.6.weight [2,64], find.6.bias
+  const float* w1 = weights;
+  const float* b1 = w1 + kN1 * kIn;
+  const float* w2 = b1 + kN1;
+  const float* b2 = w2 + kN2 * kN1;
+  const float* w3 = b2 + kN2;
+  const float* b3 = w3 + kN3 * kN2;
+  const float* w4 = b3 + kN3;
+  const float* b4 = w4 + 2 * kN3;
+  std::vector<float> h(GobiW::SIZE, 0.f);
+  for (int o = 0; o < kN1; ++o)
+    for (int k = 0; k < kIn; ++k) {
+      h[GobiW::W1 + o * kIn + k] = w1[o * kIn + k];
+      h[GobiW::W1T + k * kN1 + o] = w1[o * kIn + k];
+    }
+  for (int o = 0; o < kN2; ++o)
+    for (int k = 0; k < kN1; ++k) {
+      h[GobiW::W2 + o * kN1 + k] = w2[o * kN1 + k];
+      h[GobiW::W2T + k * kN2 + o] = w2[o * kN1 + k];
+    }
+  for (int o = 0; o < kN3; ++o)
+    for (int k = 0; k < kN2; ++k) {
+      h[GobiW::W3 + o * kN2 + k] = w3[o * kN2 + k];
+      h[GobiW::W3T + k * kN3 + o] = w3[o * kN2 + k];
+    }
+  for (int i = 0; i < kN1; ++i) h[GobiW::B1 + i] = b1[i];
+  for (int i = 0; i < kN2; ++i) h[GobiW::B2 + i] = b2[i];
+  for (int i = 0; i < kN3; ++i) h[GobiW::B3 + i] = b3[i];
+  for (int i = 0; i < 2 * kN3; ++i) h[GobiW::W4 + i] = w4[i];
+  h[GobiW::B4] = b4[0];
+  h[GobiW::B4 + 1] = b4[1];
+  // AdamW(lr=0.8, betas (0.9, 0.999), eps 1e-8, weight_decay 1e-2) under
+  // CosineAnnealingLR(T_max=10), torch's recursive update, in double as torch does
+  const double base = 0.8, wd = 1e-2, T = 10.0;
+  double lr = base;
+  for (int i = 0; i < kMaxIt; ++i) {
+    const int step = i + 1;
+    h[GobiW::ADAM + i * 4 + 0] = (float)(1.0 - lr * wd);
+    h[GobiW::ADAM + i * 4 + 1] = (float)(lr / (1.0 - std::pow(0.9, step)));
+    h[GobiW::ADAM + i * 4 + 2] = (float)std::sqrt(1.0 - std::pow(0.999, step));
+    h[GobiW::ADAM + i * 4 + 3] = (float)lr;
+    const int ep = i + 1;
+    if ((ep - 1 - 10) % 20 == 0)
+      lr = lr + base * (1 - std::cos(M_PI / T)) / 2;
+    else
+      lr = (1 + std::cos(M_PI * ep / T)) / (1 + std::cos(M_PI * (ep - 1) / T)) * lr;
+  }
+  pgp_gobi* g = new pgp_gobi();
+  g->H = n_hosts;
+  if (hipMalloc(&g->d_w, h.size() * sizeof(float)) != hipSuccess ||
+      hipMemcpy(g->d_w, h.data(), h.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess) {
+    if (g->d_w) (void)hipFree(g->d_w);
+    delete g;
+    return gfail(PGP_ERR_HIP, "GOBI weight upload failed");
+  }
+  *out = g;
+  return PGP_OK;
+}
+
+int pgp_gobi_destroy(pgp_gobi* g) {
+  if (!g) return PGP_OK;
+  if (g->d_w) (void)hipFree(g->d_w);
+  delete g;
+  return PGP_OK;
+}
+
+const char* pgp_gobi_last_error(void) { return g_gerr.c_str(); }
+
+int pgp_gobi_optimize(pgp_gobi* g, int n_env, const float* init, float* result, int* iterations, float* fitness,
+                      int max_iters, float* pre, void* stream) {
+  if (!g) return gfail(PGP_ERR_ARG, "NULL optimiser");
+  if (n_env < 0) return gfail(PGP_ERR_ARG, "negative batch");
+  if (n_env == 0) return PGP_OK;
+  if (!init || !result || !iterations || !fitness) return gfail(PGP_ERR_ARG, "NULL input/output pointer");
+  const int mi = (max_iters <= 0 || max_iters > kMaxIt) ? kMaxIt : max_iters;
+  gobi_kernel<<<n_env, 256, 0, reinterpret_cast<hipStream_t>(stream)>>>(n_env, g->d_w, init, result, iterations,
+                                                                       fitness, mi, pre);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return gfail(PGP_ERR_HIP, std::string("gobi_kernel: ") + hipGetErrorString(e));
+  return PGP_OK;
+}
+
+}  // extern "C"
