@@ -166,10 +166,12 @@ __global__ __launch_bounds__(256) void transpose_kernel(int R, int C, const floa
 }
 
 // dW[n][k] += sum_b Y[b][n] X[b][k] for the 64x64 block (blockIdx.y, blockIdx.x);
-// db[n] += sum_b Y[b][n] by the blockIdx.x == 0 blocks
+// db[n] += sum_b Y[b][n] by the blockIdx.x == 0 blocks.  With gridDim.z > 1 the
+// batch is split: split z sums its rows into part[z] ([N][K] then [N]) and
+// dw_part_reduce adds the splits in order.
 __global__ __launch_bounds__(256) void dw_block_kernel(int B, int N, int K, const float* __restrict__ Y, long ldy,
                                                        const float* __restrict__ X, long ldx, float* __restrict__ dW,
-                                                       float* __restrict__ db) {
+                                                       float* __restrict__ db, float* __restrict__ part) {
   constexpr int NP = 64, KP = 64, KT = 4, NTW = 1;
   __shared__ __attribute__((aligned(16))) float ys[kDwRows * lds_stride(NP)];
   __shared__ __attribute__((aligned(16))) float xs[kDwRows * lds_stride(KP)];
@@ -179,20 +181,51 @@ __global__ __launch_bounds__(256) void dw_block_kernel(int B, int N, int K, cons
   float pb[NTW] = {0.f};
 #pragma unroll
   for (int u = 0; u < KT; ++u) acc[0][u] = zero4();
-  dw_accumulate<NP, KP, NTW>(0, B, Y + n0, ldy, X + k0, ldx, 0, 0, 4, ys, xs, acc, pb, std::min(NP, N - n0),
+  const int S = gridDim.z, z = blockIdx.z;
+  const long nch = (B + kDwRows - 1) / kDwRows;
+  const long r0 = nch * z / S * kDwRows, r1 = std::min<long>(B, nch * (z + 1) / S * kDwRows);
+  dw_accumulate<NP, KP, NTW>(r0, r1, Y + n0, ldy, X + k0, ldx, 0, 0, 4, ys, xs, acc, pb, std::min(NP, N - n0),
                              std::min(KP, K - k0));
+  float* oW = S > 1 ? part + (long)z * ((long)N * K + N) : dW;
+  float* ob = S > 1 ? part + (long)z * ((long)N * K + N) + (long)N * K : db;
   const int t = wv;  // n-tile of this wave
 #pragma unroll
   for (int u = 0; u < KT; ++u)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int n = n0 + 16 * t + 4 * g + r, k = k0 + 16 * u + i;
-      if (n < N && k < K) dW[(long)n * K + k] += acc[0][u][r];
+      if (n < N && k < K) {
+        if (S > 1)
+          oW[(long)n * K + k] = acc[0][u][r];
+        else
+          oW[(long)n * K + k] += acc[0][u][r];
+      }
     }
   if (db && blockIdx.x == 0) {
     const float s = xsum(pb[0], true);
     const int n = n0 + 16 * t + i;
-    if (g == 0 && n < N) db[n] += s;
+    if (g == 0 && n < N) {
+      if (S > 1)
+        ob[n] = s;
+      else
+        ob[n] += s;
+    }
+  }
+}
+
+// dW[o] += sum_z part[z][o] (o < N*K), db[n] += sum_z part[z][N*K + n], z ascending
+__global__ __launch_bounds__(256) void dw_part_reduce(int S, int N, int K, const float* __restrict__ part,
+                                                      float* __restrict__ dW, float* __restrict__ db) {
+  const long o = (long)blockIdx.x * 256 + threadIdx.x;
+  const long nk = (long)N * K, stride = nk + N;
+  if (o < nk) {
+    float s = 0.f;
+    for (int z = 0; z < S; ++z) s += part[z * stride + o];
+    dW[o] += s;
+  } else if (db && o < nk + N) {
+    float s = 0.f;
+    for (int z = 0; z < S; ++z) s += part[z * stride + o];
+    db[o - nk] += s;
   }
 }
 
@@ -225,7 +258,9 @@ GanPlan gan_plan_h(int B) {
   };
   p.rows = take((long)B * G::GS_SIZE);
   const long wide = (long)B * round_up(H * H, 64);  // S = 1 GEMMs over H^2 outputs
-  p.part = take(std::max(256L * 64 * 64, wide));  // split GEMMs: S * ceil(B/64)*64 <= 256*64 rows x 64
+  // split GEMMs: S * ceil(B/64)*64 <= 256*64 rows x 64; weight-gradient splits <= 8 x the largest [N][K] + [N]
+  const long dwmax = 8L * (std::max({64L * G::DIN, (long)H * H * 64, 64L * G::GIN}) + (long)H * H);
+  p.part = take(std::max({256L * 64 * 64, wide, dwmax}));
   p.tr = take(2L * H * H * 64);
   p.total = off;
   return p;
@@ -249,8 +284,15 @@ hipError_t gemm(int M, int N, int K, const float* X, long ldx, const float* W, l
 }
 
 hipError_t dw_blocks(int B, int N, int K, const float* Y, long ldy, const float* X, long ldx, float* dW, float* db,
-                     hipStream_t st) {
-  GCK((dw_block_kernel<<<dim3((K + 63) / 64, (N + 63) / 64), 256, 0, st>>>(B, N, K, Y, ldy, X, ldx, dW, db)));
+                     float* part, hipStream_t st) {
+  const int nb = ((K + 63) / 64) * ((N + 63) / 64);
+  const int S = std::max(1, std::min({8, 256 / nb, (B + kDwRows - 1) / kDwRows}));
+  GCK((dw_block_kernel<<<dim3((K + 63) / 64, (N + 63) / 64, S), 256, 0, st>>>(B, N, K, Y, ldy, X, ldx, dW, db,
+                                                                                part)));
+  if (S > 1) {
+    const long n = (long)N * K + N;
+    GCK((dw_part_reduce<<<(int)((n + 255) / 256), 256, 0, st>>>(S, N, K, part, dW, db)));
+  }
   return hipSuccess;
 }
 
@@ -292,10 +334,10 @@ hipError_t gan_disc_bwd_h(int B, const float* target, const float* Pd, float* Gd
   hipError_t e;
   GCK((disc_head_kernel<H><<<(B + 3) / 4, 256, 0, st>>>(B, 1, Pd, R, target, nullptr)));
   if ((e = dw_blocks(B, 2, 64, R + G::GS_DO, G::GS_SIZE, R + G::GS_DD, G::GS_SIZE, Gdd + G::D_W2, Gdd + G::D_B2,
-                     st)) != hipSuccess)
+                     ws + gp.part, st)) != hipSuccess)
     return e;
   return dw_blocks(B, 64, G::DIN, R + G::GS_DDD, G::GS_SIZE, R + G::GS_Z, G::GS_SIZE, Gdd + G::D_W1, Gdd + G::D_B1,
-                   st);
+                   ws + gp.part, st);
 }
 
 template <int H>
@@ -316,7 +358,7 @@ hipError_t gan_gen_bwd_h(int B, const float* Pg, const float* Pd, float* Gdg, fl
                 G::GS_SIZE, R + G::GS_T, nullptr, nullptr, st)) != hipSuccess)
     return e;
   if ((e = dw_blocks(B, HH, 64, R + G::GS_DY, G::GS_SIZE, R + G::GS_H, G::GS_SIZE, Gdg + G::G_W2, Gdg + G::G_B2,
-                     st)) != hipSuccess)
+                     ws + gp.part, st)) != hipSuccess)
     return e;
   // dHg = W2^T dY, then Gen1's gradients
   GCK((transpose_kernel<<<(int)((64L * HH + 255) / 256), 256, 0, st>>>(HH, 64, Pg + G::G_W2, 64, W2T)));
@@ -324,7 +366,7 @@ hipError_t gan_gen_bwd_h(int B, const float* Pg, const float* Pd, float* Gdg, fl
                 R + G::GS_DH, G::GS_SIZE, nullptr, nullptr, nullptr, st)) != hipSuccess)
     return e;
   return dw_blocks(B, 64, G::GIN, R + G::GS_DH, G::GS_SIZE, R + G::GS_X, G::GS_SIZE, Gdg + G::G_W1, Gdg + G::G_B1,
-                   st);
+                   ws + gp.part, st);
 }
 
 }  // namespace
