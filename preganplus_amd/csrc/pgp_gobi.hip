@@ -3,14 +3,17 @@
 // the energy_latency_16 surrogate (scheduler/BaGTI/src/models.py:8-27), for a
 // batch of independent environments.
 //
-// One 256-thread workgroup per environment runs the whole optimisation
+// One 1024-thread workgroup per environment runs the whole optimisation
 // in-kernel (the reference's loop: up to 200 AdamW steps on the input matrix,
-// one-hot projection after each, stop after 31 unchanged steps).  Thread t owns
-// allocation entry t = (container t/16, host t%16): its AdamW moments live in
-// registers, and a row's first-argmax is a 16-lane reduction inside one wave.
-// The MLP (288-128-128-64-2) and its input gradient are VALU dot products over
-// L2-resident weights, read coalesced: forward from transposed copies [K][N],
-// backward from the natural [N][K] rows.  Elementwise semantics follow torch's
+// one-hot projection after each, stop after 31 unchanged steps).  Thread t < 256
+// owns allocation entry t = (container t/16, host t%16): its AdamW moments live
+// in registers, and a row's first-argmax is a 16-lane reduction inside one wave.
+// The MLP (288-128-128-64-2) and its input gradient are VALU dot products split
+// 4-16 ways over the threads; layer 1 (60% of the work, used in both
+// directions) sits in LDS as one copy with a 289-float row stride, so row reads
+// (forward) and column reads (input gradient) are both bank-conflict-free;
+// layers 2-3 are read from L2, forward from transposed copies, backward from
+// the natural rows, both coalesced.  Elementwise semantics follow torch's
 // CPU kernels (softplus threshold 20, tanhshrink = x - tanh x composite,
 // sigmoid backward g(1-y)y, AdamW single-tensor op order); per-iteration AdamW
 // scalars (cosine lr) are computed on the host in double, as torch does.
@@ -54,52 +57,88 @@ __device__ __forceinline__ float softplus_b(float g, float x) {
 }
 __device__ __forceinline__ float sigmoid_f(float x) { return 1.f / (1.f + expf(-x)); }
 
+constexpr int kT = 1024;          // threads per environment
+constexpr int kW1S = kIn + 1;      // LDS row stride of W1: 289 = 33 (mod 64) banks -> row and column reads conflict-free
+
 struct GobiLds {
+  float w1[kN1 * kW1S];  // layer-1 weights, natural [128][288] rows padded to 289 (147,968 B)
   float x[kIn];
   float a1[kN1], h1[kN1], a2[kN2], h2[kN2], a3[kN3], h3[kN3];
   float g1[kN1], g2[kN2], g3[kN3];
-  float part[256];
+  float part[1024];
   float o[4];
   int flag[2];
 };
 
-// forward of the surrogate on L.x (all 256 threads); returns z in L.o[2]
-__device__ void surrogate_fwd(const float* __restrict__ W, GobiLds& L) {
+// this thread's slices of layers 2-3, loaded once and kept in registers for
+// every iteration (forward: W2^T/W3^T column blocks; backward: W2/W3 row blocks)
+struct GobiRegs {
+  float w2f[16], w3f[8], w3b[8], w2b[16];
+};
+
+__device__ void load_regs(const float* __restrict__ W, GobiRegs& R) {
+  const int t = threadIdx.x, o = t & 127, sp = t >> 7, o3 = t & 63, sp3 = t >> 6;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) R.w2f[j] = W[GobiW::W2T + (sp * 16 + j) * kN2 + o];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) R.w3f[j] = W[GobiW::W3T + (sp3 * 8 + j) * kN3 + o3];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) R.w3b[j] = W[GobiW::W3 + (sp * 8 + j) * kN2 + o];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) R.w2b[j] = W[GobiW::W2 + (sp * 16 + j) * kN1 + o];
+}
+
+// forward of the surrogate on L.x (all 1024 threads); z in L.o[2]
+__device__ void surrogate_fwd(const float* __restrict__ W, const GobiRegs& R, GobiLds& L) {
   const int t = threadIdx.x;
-  {  // layer 1: 128 outputs x 2 halves of K = 288
-    const int o = t & 127, hf = t >> 7;
+  {  // layer 1: 128 outputs x 8 splits of K = 288 (36 each), W1 rows from LDS
+    const int o = t & 127, sp = t >> 7;
     float acc = 0.f;
-    for (int k = hf * 144; k < hf * 144 + 144; ++k) acc = fmaf(W[GobiW::W1T + k * kN1 + o], L.x[k], acc);
+    const float* wr = L.w1 + o * kW1S + sp * 36;
+    const float* xr = L.x + sp * 36;
+#pragma unroll 6
+    for (int k = 0; k < 36; ++k) acc = fmaf(wr[k], xr[k], acc);
     L.part[t] = acc;
     __syncthreads();
     if (t < kN1) {
-      const float a = (L.part[t] + L.part[t + 128]) + W[GobiW::B1 + t];
+      float a = 0.f;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) a += L.part[q * 128 + t];
+      a += W[GobiW::B1 + t];
       L.a1[t] = a;
       L.h1[t] = softplus_f(a);
     }
     __syncthreads();
   }
-  {  // layer 2: 128 outputs x 2 halves of K = 128
-    const int o = t & 127, hf = t >> 7;
+  {  // layer 2: 128 outputs x 8 splits of K = 128 (16 each)
+    const int sp = t >> 7;
     float acc = 0.f;
-    for (int k = hf * 64; k < hf * 64 + 64; ++k) acc = fmaf(W[GobiW::W2T + k * kN2 + o], L.h1[k], acc);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc = fmaf(R.w2f[j], L.h1[sp * 16 + j], acc);
     L.part[t] = acc;
     __syncthreads();
     if (t < kN2) {
-      const float a = (L.part[t] + L.part[t + 128]) + W[GobiW::B2 + t];
+      float a = 0.f;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) a += L.part[q * 128 + t];
+      a += W[GobiW::B2 + t];
       L.a2[t] = a;
       L.h2[t] = softplus_f(a);
     }
     __syncthreads();
   }
-  {  // layer 3: 64 outputs x 4 quarters of K = 128
-    const int o = t & 63, q = t >> 6;
+  {  // layer 3: 64 outputs x 16 splits of K = 128 (8 each)
+    const int sp = t >> 6;
     float acc = 0.f;
-    for (int k = q * 32; k < q * 32 + 32; ++k) acc = fmaf(W[GobiW::W3T + k * kN3 + o], L.h2[k], acc);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc = fmaf(R.w3f[j], L.h2[sp * 8 + j], acc);
     L.part[t] = acc;
     __syncthreads();
     if (t < kN3) {
-      const float a = ((L.part[t] + L.part[t + 64]) + (L.part[t + 128] + L.part[t + 192])) + W[GobiW::B3 + t];
+      float a = 0.f;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) a += L.part[q * 64 + t];
+      a += W[GobiW::B3 + t];
       L.a3[t] = a;
       L.h3[t] = a - tanhf(a);  // Tanhshrink
     }
@@ -122,21 +161,28 @@ __device__ void surrogate_fwd(const float* __restrict__ W, GobiLds& L) {
   __syncthreads();
 }
 
-__global__ __launch_bounds__(256) void gobi_kernel(int E, const float* __restrict__ W, const float* __restrict__ init,
-                                                   float* __restrict__ result, int* __restrict__ iterations,
-                                                   float* __restrict__ fitness, int max_it, float* __restrict__ pre) {
+__global__ __launch_bounds__(kT) void gobi_kernel(int E, const float* __restrict__ W, const float* __restrict__ init,
+                                                  float* __restrict__ result, int* __restrict__ iterations,
+                                                  float* __restrict__ fitness, int max_it, float* __restrict__ pre) {
 #pragma clang fp contract(off)  // elementwise steps as torch's separate mul/add
-  __shared__ GobiLds L;
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+  GobiLds& L = *reinterpret_cast<GobiLds*>(lds_raw);
   const int e = blockIdx.x;
   if (e >= E) return;  // whole workgroup
-  const int t = threadIdx.x, c = t >> 4, hcol = t & 15;
-  const int xi = c * kF + 2 + hcol;  // this thread's allocation entry in the flattened input
-  for (int k = t; k < kIn; k += 256) L.x[k] = init[(long)e * kIn + k];
+  const int t = threadIdx.x, c = (t & 255) >> 4, hcol = t & 15;
+  const int xi = c * kF + 2 + hcol;  // threads < 256: this thread's allocation entry in the flattened input
+  for (int k = t; k < kN1 * kIn; k += kT) {
+    const int o = k / kIn, j = k - o * kIn;
+    L.w1[o * kW1S + j] = W[GobiW::W1 + k];
+  }
+  for (int k = t; k < kIn; k += kT) L.x[k] = init[(long)e * kIn + k];
+  GobiRegs R;
+  load_regs(W, R);
   __syncthreads();
   float m = 0.f, v = 0.f;
   int equal = 0, it = 0;
   while (it < max_it) {
-    surrogate_fwd(W, L);
+    surrogate_fwd(W, R, L);
     // ---- backward to the input (autograd of z) ----
     if (t < 64) {  // dz/do = (0.8, 0.2) through the sigmoids; dh3 = W4^T do; through Tanhshrink
       const float o0 = L.o[0], o1 = L.o[1];
@@ -146,61 +192,82 @@ __global__ __launch_bounds__(256) void gobi_kernel(int E, const float* __restric
       L.g3[t] = gh - gh * (1.f - th * th);
     }
     __syncthreads();
-    {  // dh2 = W3^T g3 (128 x K=64, 2 halves), through softplus
-      const int o = t & 127, hf = t >> 7;
+    {  // dh2 = W3^T g3 (128 x K=64, 8 splits of 8), through softplus
+      const int sp = t >> 7;
       float acc = 0.f;
-      for (int k = hf * 32; k < hf * 32 + 32; ++k) acc = fmaf(W[GobiW::W3 + k * kN2 + o], L.g3[k], acc);
-      L.part[t] = acc;
-      __syncthreads();
-      if (t < kN2) L.g2[t] = softplus_b(L.part[t] + L.part[t + 128], L.a2[t]);
-      __syncthreads();
-    }
-    {  // dh1 = W2^T g2 (128 x K=128), through softplus
-      const int o = t & 127, hf = t >> 7;
-      float acc = 0.f;
-      for (int k = hf * 64; k < hf * 64 + 64; ++k) acc = fmaf(W[GobiW::W2 + k * kN1 + o], L.g2[k], acc);
-      L.part[t] = acc;
-      __syncthreads();
-      if (t < kN1) L.g1[t] = softplus_b(L.part[t] + L.part[t + 128], L.a1[t]);
-      __syncthreads();
-    }
-    // dx for this thread's allocation entry: W1[:, xi] . g1
-    float gx = 0.f;
-    for (int o = 0; o < kN1; ++o) gx = fmaf(W[GobiW::W1 + o * kIn + xi], L.g1[o], gx);
-    // ---- AdamW (torch single-tensor, opt.py:18 defaults) on the entry ----
-    const float* ad = W + GobiW::ADAM + it * 4;
-    const float xold = L.x[xi];
-    float xv = xold * ad[0];
-    m = m + 0.1f * (gx - m);              // exp_avg.lerp_(grad, 1 - beta1)
-    v = v * 0.999f + 0.001f * gx * gx;    // exp_avg_sq.mul_(beta2).addcmul_(grad, grad, 1 - beta2)
-    const float denom = sqrtf(v) / ad[2] + 1e-8f;
-    xv = xv + (-ad[1]) * m / denom;       // addcdiv_: self + value * t1 / t2 (ATen's order)
-    // ---- one-hot of the row's first argmax (opt.py:9-15) ----
-    float best = xv;
-    int bi = hcol;
 #pragma unroll
-    for (int off = 8; off >= 1; off >>= 1) {
-      const float ov = __shfl_xor(best, off);
-      const int oi = __shfl_xor(bi, off);
-      if (ov > best || (ov == best && oi < bi)) {
-        best = ov;
-        bi = oi;
+      for (int j = 0; j < 8; ++j) acc = fmaf(R.w3b[j], L.g3[sp * 8 + j], acc);
+      L.part[t] = acc;
+      __syncthreads();
+      if (t < kN2) {
+        float a = 0.f;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) a += L.part[q * 128 + t];
+        L.g2[t] = softplus_b(a, L.a2[t]);
       }
+      __syncthreads();
     }
-    if (pre) pre[(long)e * kH * kH + t] = xv;  // test tap: the step's values before the projection
-    const float nv = bi == hcol ? 1.f : 0.f;
-    const int changed = nv != xold;
+    {  // dh1 = W2^T g2 (128 x K=128, 8 splits of 16), through softplus
+      const int sp = t >> 7;
+      float acc = 0.f;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) acc = fmaf(R.w2b[j], L.g2[sp * 16 + j], acc);
+      L.part[t] = acc;
+      __syncthreads();
+      if (t < kN1) {
+        float a = 0.f;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) a += L.part[q * 128 + t];
+        L.g1[t] = softplus_b(a, L.a1[t]);
+      }
+      __syncthreads();
+    }
+    {  // dx for the 256 allocation entries: W1[:, xi] . g1, 4 splits of 32 over the LDS copy
+      const int sp = t >> 8;
+      float acc = 0.f;
+#pragma unroll 8
+      for (int o = sp * 32; o < sp * 32 + 32; ++o) acc = fmaf(L.w1[o * kW1S + xi], L.g1[o], acc);
+      L.part[t] = acc;
+      __syncthreads();
+    }
+    int changed = 0;
+    if (t < 256) {
+      const float gx = (L.part[t] + L.part[t + 256]) + (L.part[t + 512] + L.part[t + 768]);
+      // ---- AdamW (torch single-tensor, opt.py:18 defaults) on the entry ----
+      const float* ad = W + GobiW::ADAM + it * 4;
+      const float xold = L.x[xi];
+      float xv = xold * ad[0];
+      m = m + 0.1f * (gx - m);            // exp_avg.lerp_(grad, 1 - beta1)
+      v = v * 0.999f + 0.001f * gx * gx;  // exp_avg_sq.mul_(beta2).addcmul_(grad, grad, 1 - beta2)
+      const float denom = sqrtf(v) / ad[2] + 1e-8f;
+      xv = xv + (-ad[1]) * m / denom;     // addcdiv_: self + value * t1 / t2 (ATen's order)
+      // ---- one-hot of the row's first argmax (opt.py:9-15) ----
+      float best = xv;
+      int bi = hcol;
+#pragma unroll
+      for (int off = 8; off >= 1; off >>= 1) {
+        const float ov = __shfl_xor(best, off);
+        const int oi = __shfl_xor(bi, off);
+        if (ov > best || (ov == best && oi < bi)) {
+          best = ov;
+          bi = oi;
+        }
+      }
+      if (pre) pre[(long)e * kH * kH + t] = xv;  // test tap: the step's values before the projection
+      const float nv = bi == hcol ? 1.f : 0.f;
+      changed = nv != xold;
+      L.x[xi] = nv;
+    }
     if (t == 0) L.flag[0] = 0;
     __syncthreads();
     if (changed) L.flag[0] = 1;  // benign race: every writer stores 1
-    L.x[xi] = nv;
     __syncthreads();
     equal = L.flag[0] ? 0 : equal + 1;
     if (equal > kPatience) break;
     ++it;
   }
-  surrogate_fwd(W, L);
-  for (int k = t; k < kIn; k += 256) result[(long)e * kIn + k] = L.x[k];
+  surrogate_fwd(W, R, L);
+  for (int k = t; k < kIn; k += kT) result[(long)e * kIn + k] = L.x[k];
   if (t == 0) {
     iterations[e] = it;
     fitness[e] = L.o[2];
@@ -287,6 +354,11 @@ int pgp_gobi_create(int n_hosts, const float* weights, size_t len, pgp_gobi** ou
   }
   pgp_gobi* g = new pgp_gobi();
   g->H = n_hosts;
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&gobi_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)sizeof(GobiLds)) != hipSuccess) {
+    delete g;
+    return gfail(PGP_ERR_HIP, "GOBI: cannot reserve LDS");
+  }
   if (hipMalloc(&g->d_w, h.size() * sizeof(float)) != hipSuccess ||
       hipMemcpy(g->d_w, h.data(), h.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess) {
     if (g->d_w) (void)hipFree(g->d_w);
@@ -313,8 +385,8 @@ int pgp_gobi_optimize(pgp_gobi* g, int n_env, const float* init, float* result, 
   if (n_env == 0) return PGP_OK;
   if (!init || !result || !iterations || !fitness) return gfail(PGP_ERR_ARG, "NULL input/output pointer");
   const int mi = (max_iters <= 0 || max_iters > kMaxIt) ? kMaxIt : max_iters;
-  gobi_kernel<<<n_env, 256, 0, reinterpret_cast<hipStream_t>(stream)>>>(n_env, g->d_w, init, result, iterations,
-                                                                       fitness, mi, pre);
+  gobi_kernel<<<n_env, kT, sizeof(GobiLds), reinterpret_cast<hipStream_t>(stream)>>>(n_env, g->d_w, init, result,
+                                                                                     iterations, fitness, mi, pre);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return gfail(PGP_ERR_HIP, std::string("gobi_kernel: ") + hipGetErrorString(e));
   return PGP_OK;
