@@ -91,7 +91,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-gan", action="store_true", help="tune config: Transformer tuning step only")
-    ap.add_argument("--config", choices=["c2", "fleet", "tune", "fpe", "gobi"], default="c2",
+    ap.add_argument("--config", choices=["c2", "fleet", "tune", "fpe", "gobi", "sim"], default="c2",
                     help="c2: BASELINE config 2 (default, the headline line); fleet: config 5 "
                          "(1024-host fleet = 64 cells of 16 hosts, shipped weights); tune: config 3 "
                          "(tuning step fwd+bwd+AdamW, data-parallel with an RCCL all-reduce); fpe: config 4 "
@@ -107,6 +107,8 @@ def main():
         return bench_fpe(args)
     if args.config == "gobi":
         return bench_gobi(args)
+    if args.config == "sim":
+        return bench_sim(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -282,9 +284,13 @@ def bench_tune(args):
     step of the same windows (Gen + Disc forward, Disc BCE backward, Gen BCE
     backward through the updated Disc), each section's gradients summed over
     ranks by one flat RCCL all-reduce before its AdamW step, in the reference's
-    order (PreGANPlus.py:60-81 Disc then Gen; train.py:42-57).  Labels, CE
-    weights, prototype targets and GAN labels are synthetic and fixed, so the
-    timed region is device work."""
+    order (PreGANPlus.py:60-81 Disc then Gen; train.py:42-57).  The GAN label
+    of each window is simulated on the device from the generator's output
+    (pgp_simulate: Stats.runSimulation of the new and the original schedule on
+    a synthetic environment record per window).  Tuning labels,
+    CE weights and prototype targets are synthetic and fixed, so the timed
+    region is device work."""
+    from preganplus_amd import simulate as SIM
     from preganplus_amd import train as TR
     world, rank, device = _dist_setup()
     H = args.hosts
@@ -297,8 +303,10 @@ def bench_tune(args):
     mult = torch.ones((B, H), device=device)
     tgt = torch.rand((B, H, 2), generator=g, device=device)
     emb = torch.where(y[..., None] > 0, torch.rand((B, H, 2), generator=g, device=device), 0.0).contiguous()
-    lab = (torch.rand((B,), generator=g, device=device) < 0.5).to(torch.float32)
-    gan_target = torch.stack([1.0 - lab, lab], dim=1).contiguous()
+    envs = torch.tensor(SIM.synth_envs(B, H, seed=5 + rank), device=device)
+    sim = SIM.Simulation(H, device=device)
+    sim_out = torch.empty((B, 4), dtype=torch.float64, device=device)
+    gan_target = torch.empty((B, 2), dtype=torch.float32, device=device)
     gan = not args.no_gan
 
     def step():
@@ -307,7 +315,8 @@ def bench_tune(args):
         tr.all_reduce_grads("transformer")
         tr.adam_step("transformer")
         if gan:
-            tr.gan_forward(emb, s)
+            ns, _ = tr.gan_forward(emb, s)
+            sim.score(envs, ns, s, out=sim_out, target=gan_target)  # PreGANPlus.py:65-66 on the device
             tr.gan_disc_backward(gan_target)
             tr.all_reduce_grads("disc")
             tr.adam_step("disc")
@@ -323,7 +332,8 @@ def bench_tune(args):
             "metric": "tuning windows/sec (fwd+bwd+all-reduce+AdamW)", "value": B * world * args.steps / el,
             "unit": "windows/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": el / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "fp32", "data": "synthetic windows, labels and targets",
+            "vs_baseline": None, "dtype": "fp32",
+            "data": "synthetic windows, tuning labels/targets and environment records; GAN labels simulated",
             "config": {"workload": f"C3: tuning step ({'Transformer + GAN' if gan else 'Transformer only'}), "
                                    f"{H} hosts, {B} windows per GPU", "hosts": H,
                        "windows_per_gpu": B, "parallelism": f"dp{world} + RCCL all-reduce"}}), flush=True)
@@ -470,6 +480,62 @@ def bench_gobi(args):
             res["cpu_baseline"] = {"value": n / dt, "unit": "schedules/s", "cores": 1, "kind": "port",
                                    "sample": f"{n} opt() runs of the torch-CPU restatement (bit-identical to the "
                                              f"reference's), 1 thread, {dt:.1f}s"}
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+def bench_sim(args):
+    """the GAN label's two Stats.runSimulation calls
+    (PreGANPlus.py:65, Stats.py:154-177) for a batch of environments per GPU,
+    one pgp_simulate launch per step (generator-like and original schedule per
+    environment, synthetic records of simulate.synth_envs)."""
+    from preganplus_amd import simulate as SIM
+    world, rank, device = _dist_setup()
+    H = args.hosts
+    E = args.batch if args.batch != 65536 else 4096
+    rng = np.random.Generator(np.random.PCG64(9 + rank))
+    envs_h = SIM.synth_envs(E, H, seed=3 + rank)
+    new_h = rng.uniform(size=(E, H, H)).astype(np.float32)
+    orig_h = np.zeros((E, H, H), np.float32)
+    orig_h[np.arange(E)[:, None], np.arange(H)[None, :], rng.integers(0, H, (E, H))] = 1.0
+    envs, new, orig = (torch.tensor(a, device=device) for a in (envs_h, new_h, orig_h))
+    sim = SIM.Simulation(H, device=device)
+    out = torch.empty((E, 4), dtype=torch.float64, device=device)
+    target = torch.empty((E, 2), dtype=torch.float32, device=device)
+
+    def step():
+        sim.score(envs, new, orig, out=out, target=target)
+
+    for _ in range(args.warmup):
+        step()
+    el = _timed(world, device, step, args.steps)
+    if rank == 0:
+        t = el / args.steps
+        byt = E * (8 * SIM.env_len(H) + 2 * 4 * H * H + 8 * 4 + 4 * 2)  # record + 2 schedules in; out + target
+        res = {
+            "metric": "GAN-label simulations/sec (2 x runSimulation per environment)", "value": E * world / t,
+            "unit": "environments/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": t * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "fp64 (scores), fp32 (schedules)",
+            "data": "synthetic environment records (simulate.synth_envs), random generator-like and one-hot schedules",
+            "config": {"workload": f"f4: runSimulation label, {E} environments x {H} hosts per GPU", "hosts": H,
+                       "environments_per_gpu": E, "parallelism": f"dp{world}"},
+            "roofline": {"kernel": "simulate_kernel", "bound": "hbm", "achieved": byt / t / 1e9,
+                         "peak": R.PEAK_HBM_GBS, "unit": "GB/s", "frac": byt / t / 1e9 / R.PEAK_HBM_GBS,
+                         "traffic": None, "bytes_per_environment": byt / E},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            from oracle import sim_oracle as SO  # CPU baseline leg only
+            t0, n = time.perf_counter(), 0
+            while time.perf_counter() - t0 < args.cpu_budget:
+                i = n % E
+                SO.simulate_batch(envs_h[i:i + 1], new_h[i:i + 1], orig_h[i:i + 1], H)
+                n += 1
+            dt = time.perf_counter() - t0
+            res["cpu_baseline"] = {"value": n / dt, "unit": "environments/s", "cores": 1, "kind": "port",
+                                   "sample": f"{n} environments through the Python restatement (bit-identical to "
+                                             f"the reference's runSimulation), 1 thread, {dt:.1f}s"}
         print(json.dumps(res), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()

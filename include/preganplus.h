@@ -36,6 +36,9 @@
  *   pgp_gobi_*
  *       the schedule producer upstream of the path: GOBIScheduler.run_GOBI's
  *       opt() (scheduler/GOBI.py:19-42, scheduler/BaGTI/src/opt.py:17-33)
+ *   pgp_sim_env_len / pgp_simulate
+ *       the GAN label: run_simulation (PreGANSrc/src/utils.py:97-100) ->
+ *       Stats.runSimulation (stats/Stats.py:154-177), PreGANPlus.py:65-66
  *   pgp_destroy
  *       (object lifetime; no reference counterpart)
  *
@@ -264,6 +267,24 @@ const char* pgp_gobi_last_error(void);
  * one-hot projection (a test tap). */
 int pgp_gobi_optimize(pgp_gobi* g, int n_env, const float* init, float* result, int* iterations,
                       float* fitness, int max_iters, float* pre, void* stream);
+
+/* ---- GAN-label simulation ----
+ * Replaces the two env.stats.runSimulation calls of train_gan
+ * (PreGANPlus.py:65 -> utils.py:97-100 -> Stats.py:154-177) for a batch of
+ * environments.  Each environment is one fp64 record of pgp_sim_env_len(H) =
+ * 2 + 20H doubles (C = H containers; layout in preganplus_amd/simulate.py):
+ *   interval time, latency term max(0, mean(avgresponsetime[-5:])),
+ *   host[C] (-1: none/unplaced), base_ips[C], ram_size[C], disk_size[C],
+ *   apparent_ips[C], ips_available[H], ram_available[H], disk_available[H],
+ *   ips_cap[H], power_list[H][11]  (the values the reference's getters return).
+ * new_sched / orig_sched [E,C,H] fp32 (generator output, original schedule).
+ * out [E,4] fp64 = (energy·interval, 0.8·energy + 0.2·latency) of the new,
+ * then of the original schedule, bit-identical to the reference's Python;
+ * target [E,2] fp32 = [0,1] if new <= orig else [1,0] (PreGANPlus.py:66), the
+ * target argument of pgp_gan_disc_backward.  1 <= H <= 64. */
+size_t pgp_sim_env_len(int n_hosts);
+int pgp_simulate(int n_hosts, int n_env, const double* envs, const float* new_sched, const float* orig_sched,
+                 double* out, float* target, void* stream);
 
 #ifdef __cplusplus
 }

@@ -87,6 +87,8 @@ int reserve(pgp_model* m, int n) {
 }
 }  // namespace
 
+int pgp::set_error(int code, const std::string& msg) { return fail(code, msg); }
+
 extern "C" {
 
 int pgp_abi_version(void) { return PGP_ABI_VERSION; }

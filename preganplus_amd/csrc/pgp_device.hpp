@@ -3,6 +3,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <string>
+
 #include "pgp_layout.hpp"
 
 namespace pgp {
@@ -105,5 +107,8 @@ PGP_DEV void dma_groups(const float* __restrict__ src, float* dst, int ngroups, 
         (__attribute__((address_space(3))) void*)(dst + g * 256), 16, 0, 0);
   }
 }
+
+// Record an error for pgp_last_error() (pgp_capi.hip) and return `code`.
+int set_error(int code, const std::string& msg);
 
 }  // namespace pgp

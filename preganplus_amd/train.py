@@ -348,3 +348,24 @@ def train_gan(tr: Trainer, emb, sched, simulate):
     tr.gan_gen_backward(1)
     tr.adam_step("gen")
     return ns_h, new_score, orig_score
+
+
+def train_gan_batched(tr: Trainer, sim, envs, emb, sched, out=None, target=None, all_reduce=False, group=None):
+    """PreGANPlus.py:60-75 for a batch of environments with the label simulated
+    on the device (``simulate.Simulation`` -> ``pgp_simulate``):
+    Gen + Disc forward, both schedules scored, Disc BCE step on the label, Gen
+    BCE step toward [0, 1] — no host round trip.  envs [B, env_len(H)] fp64
+    records (``simulate.pack_env``).  With ``all_reduce`` each section's
+    gradients are summed over ranks before its AdamW step (data parallel).
+    Returns (out [B,4] energy/score of new and original, target [B,2])."""
+    ns, _ = tr.gan_forward(emb, sched)
+    out, target = sim.score(envs, ns, tr._gan_in[1], out=out, target=target)
+    tr.gan_disc_backward(target)
+    if all_reduce:
+        tr.all_reduce_grads("disc", group)
+    tr.adam_step("disc")
+    tr.gan_gen_backward(ns.shape[0])
+    if all_reduce:
+        tr.all_reduce_grads("gen", group)
+    tr.adam_step("gen")
+    return out, target
