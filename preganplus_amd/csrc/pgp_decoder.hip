@@ -59,14 +59,25 @@ __global__ __launch_bounds__(kDecWaves * 64) void decoder_kernel(FwdArgs a) {
     const bool pre = active && (c + 1 < NCH);
 #pragma unroll
     for (int s = 0; s < G::KS_D; ++s) bn[s] = pre ? lat[((c + 1) * G::KS_D + s) * 64 + lane] : 0.f;
+    // consecutive MFMAs go to different accumulators (dependent-accumulator
+    // latency 40 cyc > 32 cyc issue): A fragments of half the output tiles at a time
+    constexpr int AMAX = G::MT_O >= 16 ? 4 : 7;          // A fragments live (VGPR budget at 4 waves/SIMD)
+    constexpr int NGRP = (G::MT_O + AMAX - 1) / AMAX;
+    constexpr int MH = (G::MT_O + NGRP - 1) / NGRP;
 #pragma unroll
-    for (int mt = 0; mt < G::MT_O; ++mt)
+    for (int q4 = 0; q4 < G::KQ_D; ++q4)
 #pragma unroll
-      for (int q4 = 0; q4 < G::KQ_D; ++q4) {
-        const f32x4 av = ld4(cur + (mt * G::KQ_D + q4) * 256 + lane * 4);
+      for (int m0 = 0; m0 < G::MT_O; m0 += MH) {
+        f32x4 av[MH];
+#pragma unroll
+        for (int i = 0; i < MH; ++i)
+          if (m0 + i < G::MT_O) av[i] = ld4(cur + ((m0 + i) * G::KQ_D + q4) * 256 + lane * 4);
 #pragma unroll
         for (int e = 0; e < 4; ++e)
-          if (4 * q4 + e < G::KS_D) acc[mt] = mfma(av[e], b[4 * q4 + e], acc[mt]);
+          if (4 * q4 + e < G::KS_D)
+#pragma unroll
+            for (int i = 0; i < MH; ++i)
+              if (m0 + i < G::MT_O) acc[m0 + i] = mfma(av[i][e], b[4 * q4 + e], acc[m0 + i]);
       }
     __syncthreads();
     float* t = cur;

@@ -330,13 +330,12 @@ PGP_DEV void encoder_layer_tail(f32x4 (&X)[Geo<H>::MT_D][3], Ring<H>& ring, cons
       const float y1 = P1[w][0] * ba[0] + P1[w][1] * ba[1] + P1[w][2] * ba[2];
       const float p0 = g == 0 ? P0[w][0] : g == 1 ? P0[w][1] : g == 2 ? P0[w][2] : 0.f;
       const float p1 = g == 0 ? P1[w][0] : g == 1 ? P1[w][1] : g == 2 ? P1[w][2] : 0.f;
+      const float bops[4] = {y0, p0, y1, p1};
 #pragma unroll
-      for (int mt = 0; mt < G::MT_X; ++mt) {
-        acc[mt][w] = mfma(tab[G::T_F0O + (0 * G::MT_X + mt) * 64 + lane], y0, acc[mt][w]);
-        acc[mt][w] = mfma(tab[G::T_F0O + (1 * G::MT_X + mt) * 64 + lane], p0, acc[mt][w]);
-        acc[mt][w] = mfma(tab[G::T_F0O + (2 * G::MT_X + mt) * 64 + lane], y1, acc[mt][w]);
-        acc[mt][w] = mfma(tab[G::T_F0O + (3 * G::MT_X + mt) * 64 + lane], p1, acc[mt][w]);
-      }
+      for (int k = 0; k < 4; ++k)  // tiles alternate: no dependent-accumulator issue stall
+#pragma unroll
+        for (int mt = 0; mt < G::MT_X; ++mt)
+          acc[mt][w] = mfma(tab[G::T_F0O + (k * G::MT_X + mt) * 64 + lane], bops[k], acc[mt][w]);
       float ro[G::XR];
 #pragma unroll
       for (int n = 0; n < G::XR; ++n) {

@@ -99,13 +99,18 @@ __global__ __launch_bounds__(kGanWaves * 64) void gan_kernel(FwdArgs a) {
   issue();
 
   // ---- phase 1: Gen1, embedding columns ----
+  // (MFMA order: consecutive ones on different accumulators — dependent latency 40 > 32 issue)
 #pragma unroll
   for (int q = 0; q < G::EQ; ++q)
 #pragma unroll
-    for (int mt = 0; mt < G::MT_G; ++mt) {
-      const f32x4 w = ld4(cur + (mt * G::EQ + q) * 256 + lane * 4);
+    for (int m0 = 0; m0 < G::MT_G; m0 += 2) {
+      f32x4 w[2];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) hg[mt] = mfma(w[e], be[q][e], hg[mt]);
+      for (int i = 0; i < 2; ++i) w[i] = ld4(cur + ((m0 + i) * G::EQ + q) * 256 + lane * 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) hg[m0 + i] = mfma(w[i][e], be[q][e], hg[m0 + i]);
     }
 
   // ---- phase 2: schedule pass (Gen1 + Disc1 schedule half) ----
@@ -163,15 +168,21 @@ __global__ __launch_bounds__(kGanWaves * 64) void gan_kernel(FwdArgs a) {
       }
     f32x4 ns[G::MT_N];
 #pragma unroll
-    for (int t = 0; t < G::MT_N; ++t) {
-      ns[t] = ld4(gt + G::G_B2 + c * G::MT_N * 16 + 16 * t + 4 * g);
+    for (int t = 0; t < G::MT_N; ++t) ns[t] = ld4(gt + G::G_B2 + c * G::MT_N * 16 + 16 * t + 4 * g);
 #pragma unroll
-      for (int q4 = 0; q4 < 4; ++q4) {
-        const f32x4 w = ld4(cur + (t * 4 + q4) * 256 + lane * 4);
+    for (int q4 = 0; q4 < 4; ++q4)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) ns[t] = mfma(w[e], hg[q4][e], ns[t]);
+      for (int t0 = 0; t0 < G::MT_N; t0 += 2) {  // two accumulators alternate: no dependent-issue stall
+        f32x4 w[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+          if (t0 + i < G::MT_N) w[i] = ld4(cur + ((t0 + i) * 4 + q4) * 256 + lane * 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+            if (t0 + i < G::MT_N) ns[t0 + i] = mfma(w[i][e], hg[q4][e], ns[t0 + i]);
       }
-    }
     float bn_v = -INFINITY, bs_v = -INFINITY;
     int bn_i = 0, bs_i = 0;
 #pragma unroll
@@ -196,12 +207,16 @@ __global__ __launch_bounds__(kGanWaves * 64) void gan_kernel(FwdArgs a) {
         }
       }
 #pragma unroll
-    for (int mt = 0; mt < G::MT_G; ++mt)
+    for (int q4 = 0; q4 < G::MT_N; ++q4)
 #pragma unroll
-      for (int q4 = 0; q4 < G::MT_N; ++q4) {
-        const f32x4 w = ld4(cur + (G::GC_G2 + mt * G::MT_N + q4) * 256 + lane * 4);
+      for (int m0 = 0; m0 < G::MT_G; m0 += 2) {
+        f32x4 w[2];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) hd[mt] = mfma(w[e], ns[q4][e], hd[mt]);
+        for (int i = 0; i < 2; ++i) w[i] = ld4(cur + (G::GC_G2 + (m0 + i) * G::MT_N + q4) * 256 + lane * 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int i = 0; i < 2; ++i) hd[m0 + i] = mfma(w[i][e], ns[q4][e], hd[m0 + i]);
       }
 #pragma unroll
     for (int off = 16; off <= 32; off <<= 1) {
