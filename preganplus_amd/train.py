@@ -280,6 +280,113 @@ def loss_targets(logits, protos, y, c, st: TuneState):
     return mult, tgt, aloss, tloss
 
 
+class TuneIncrements:
+    """One rank's contribution to a data-parallel tuning step's host state
+    (SURVEY §8e): prototype EMA deltas and counts per class, counter
+    increments, windows seen.  Summed over ranks by ``dp_state_update``."""
+
+    def __init__(self, K):
+        self.delta = np.zeros((K, 2))
+        self.count = np.zeros(K)
+        self.num_zero = 0.0
+        self.num_ones = 0.0
+        self.windows = 0.0
+
+    def flat(self):
+        return np.concatenate([self.delta.reshape(-1), self.count, [self.num_zero, self.num_ones, self.windows]])
+
+    @classmethod
+    def from_flat(cls, v, K):
+        t = cls(K)
+        t.delta = v[:2 * K].reshape(K, 2).copy()
+        t.count = v[2 * K:3 * K].copy()
+        t.num_zero, t.num_ones, t.windows = (float(x) for x in v[3 * K:3 * K + 3])
+        return t
+
+
+def loss_targets_dp(logits, protos, y, c, st: TuneState):
+    """Data-parallel form of loss_targets (train.py:27-40) for a local batch
+    [B,H,...]: every window is scored against the step-START state (counters,
+    prototypes, factor) instead of the state left by the previous window, and
+    the state changes are returned as increments instead of applied:
+    a qualifying (window, host) contributes f·(a − P[c]) to class c's delta
+    (f = factor + PROTO_UPDATE_MIN), each window adds H to num_zero and its
+    positives to num_ones.  With one window on one rank this is the reference's
+    update exactly.  Returns (mult [B,H], tgt [B,H,2], aloss [B], tloss [B],
+    TuneIncrements)."""
+    B, H = logits.shape[0], logits.shape[1]
+    K = st.protos.shape[0]
+    inc = TuneIncrements(K)
+    mult = np.where(np.asarray(y) == 0, 1.0, st.num_zero / st.num_ones)
+    tgt = np.zeros((B, H, 2))
+    aloss = np.zeros(B)
+    tloss = np.zeros(B)
+    f = st.factor + PROTO_UPDATE_MIN
+    for b in range(B):
+        for i in range(H):
+            l = logits[b, i].astype(np.float64)
+            m = l.max()
+            aloss[b] += (np.log(np.exp(l - m).sum()) + m - l[int(y[b, i])]) * mult[b, i]
+            if y[b, i] > 0:
+                cc = int(c[b, i])
+                a = protos[b, i].astype(np.float64)
+                tgt[b, i] = st.protos[cc]
+                pos = float(np.mean((a - st.protos[cc]) ** 2))
+                negs = [float(np.mean((a - st.protos[nc]) ** 2)) for nc in (0, 1, 2) if nc != cc]
+                tloss[b] += pos - sum(negs)
+                if pos <= negs[0] and pos <= negs[1]:
+                    inc.delta[cc] += f * (a - st.protos[cc])
+                    inc.count[cc] += 1
+        inc.num_zero += H
+        inc.num_ones += float(np.sum(np.asarray(y[b]) == 1))
+        inc.windows += 1
+    return mult, tgt, aloss, tloss, inc
+
+
+def dp_state_update(st: TuneState, inc: TuneIncrements, group=None):
+    """Sum the increments over ranks (one all-reduce of 3K+3 doubles; a no-op
+    without a process group) and apply them identically everywhere: counters
+    += sums; each prototype moves by the MEAN of its qualifying deltas (so one
+    update reproduces the reference's f·a + (1−f)·P); the factor decays once
+    per window of the global batch (train.py:39)."""
+    import torch.distributed as dist
+    K = st.protos.shape[0]
+    v = inc.flat()
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        t = torch.tensor(v, dtype=torch.float64)
+        if dist.get_backend(group) == "nccl":
+            t = t.cuda()
+        dist.all_reduce(t, group=group)
+        v = t.cpu().numpy()
+    tot = TuneIncrements.from_flat(v, K)
+    upd = tot.count > 0
+    st.protos[upd] += tot.delta[upd] / tot.count[upd][:, None]
+    st.num_zero += tot.num_zero
+    st.num_ones += tot.num_ones
+    st.factor *= PROTO_FACTOR_DECAY ** tot.windows
+    return tot
+
+
+def dp_tune_step(tr: "Trainer", st: TuneState, wins, anom, cls, group=None):
+    """One data-parallel tuning step on this rank's windows:
+    forward, targets against the step-start state, backward, ONE gradient
+    all-reduce, the host state reduced over ranks, AdamW.  The loss is the
+    sum over the global batch.  Returns (aloss [B], tloss [B])."""
+    wins = torch.as_tensor(np.asarray(wins), dtype=torch.float32)
+    B = wins.shape[0]
+    logits, protos = tr.tune_forward(wins)
+    mult, tgt, aloss, tloss, inc = loss_targets_dp(logits[:B].cpu().numpy(), protos[:B].cpu().numpy(),
+                                                   np.asarray(anom), np.asarray(cls), st)
+    tr.tune_backward(B, np.asarray(anom), mult, tgt)
+    tr.all_reduce_grads("transformer", group)
+    tot = dp_state_update(st, inc, group)
+    # no positive label in the whole global batch: the prototype decoder got no
+    # gradient and torch's AdamW skips it (as backprop does per window)
+    inactive = () if tot.num_ones > 0 else ("prototype_decoder.0.weight", "prototype_decoder.0.bias")
+    tr.adam_step("transformer", inactive)
+    return aloss, tloss
+
+
 def normalize_test_time_data(time_data, train_time_data):
     """utils.py:94-95."""
     return np.asarray(time_data, dtype=np.float64) / (np.max(train_time_data, axis=0) + 1e-8)

@@ -80,3 +80,78 @@ def test_trainer_allreduce_is_noop_without_process_group():
     tr.sec_off, tr.sec_end = {"transformer": 0}, {"transformer": 10}
     tr.all_reduce_grads("transformer")
     assert tr.G.tolist() == list(range(10))
+
+
+# ---- DP tuning host state (prototype EMA deltas, counters) ----
+def _state_inputs(Bt=6, Hh=5):
+    rng = np.random.Generator(np.random.PCG64(11))
+    logits = rng.normal(size=(Bt, Hh, 2))
+    protos = rng.uniform(size=(Bt, Hh, 2))
+    y = (rng.uniform(size=(Bt, Hh)) < 0.5).astype(np.int64)
+    c = rng.integers(0, 3, size=(Bt, Hh))
+    return logits, protos, y, c
+
+
+def _state_worker(rank, world, port, q):
+    from preganplus_amd import train as TR
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    lg, pr, y, c = _state_inputs()
+    n = lg.shape[0]
+    sl = slice(rank * n // world, (rank + 1) * n // world)
+    st = TR.TuneState(np.array([[0.2, 0.3], [0.6, 0.1], [0.5, 0.9]]))
+    st.num_zero, st.num_ones = 7, 3
+    mult, tgt, _, _, inc = TR.loss_targets_dp(lg[sl], pr[sl], y[sl], c[sl], st)
+    TR.dp_state_update(st, inc)
+    if rank == 0:
+        q.put((st.protos.copy(), st.num_zero, st.num_ones, st.factor, mult, tgt))
+    dist.destroy_process_group()
+
+
+def test_dp_tuning_state_equals_full_batch():
+    """Prototype EMA / counters / factor after a 2-rank DP step == the same
+    update computed on the concatenated batch in one process."""
+    from preganplus_amd import train as TR
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 30500 + os.getpid() % 1000
+    procs = [ctx.Process(target=_state_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    protos, nz, no, fac, mult0, tgt0 = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    lg, pr, y, c = _state_inputs()
+    st = TR.TuneState(np.array([[0.2, 0.3], [0.6, 0.1], [0.5, 0.9]]))
+    st.num_zero, st.num_ones = 7, 3
+    mult, tgt, _, _, inc = TR.loss_targets_dp(lg, pr, y, c, st)
+    TR.dp_state_update(st, inc)
+    np.testing.assert_allclose(protos, st.protos, rtol=1e-13, atol=1e-15)
+    assert (nz, no) == (st.num_zero, st.num_ones) and fac == pytest.approx(st.factor, rel=1e-15)
+    np.testing.assert_array_equal(mult0, mult[:3])
+    np.testing.assert_array_equal(tgt0, tgt[:3])
+
+
+def test_dp_state_single_window_is_reference_update():
+    """One window with one positive host on one rank: loss_targets_dp +
+    dp_state_update == the reference-order loss_targets (train.py:27-40)
+    exactly (with several positives the reference compounds within the window;
+    the DP form scores them all against the step-start state)."""
+    from preganplus_amd import train as TR
+    lg, pr, y, c = _state_inputs(Bt=1, Hh=3)
+    base = np.array([[0.2, 0.3], [0.6, 0.1], [0.5, 0.9]])
+    y[0] = [0, 1, 0]
+    c[0] = [0, 1, 2]
+    pr[0, 1] = base[1] + [0.01, -0.02]  # closest to its own class: the EMA update fires
+    st1, st2 = TR.TuneState(base.copy()), TR.TuneState(base.copy())
+    m1, t1, a1, l1 = TR.loss_targets(lg[0], pr[0], y[0], c[0], st1)
+    m2, t2, a2, l2, inc = TR.loss_targets_dp(lg, pr, y, c, st2)
+    TR.dp_state_update(st2, inc)
+    np.testing.assert_allclose(st2.protos, st1.protos, rtol=1e-14, atol=1e-15)
+    np.testing.assert_allclose(m2[0], m1)
+    np.testing.assert_allclose(t2[0], t1)
+    assert not np.array_equal(st2.protos, base)
+    assert a2[0] == pytest.approx(a1, rel=1e-14) and l2[0] == pytest.approx(l1, rel=1e-14, abs=1e-15)
+    assert st2.factor == pytest.approx(st1.factor) and (st2.num_zero, st2.num_ones) == (st1.num_zero, st1.num_ones)

@@ -224,3 +224,29 @@ def test_batched_gan_step_matches_autograd(H, B):
         if t["section"] == "gen":
             close(g[t["offset"]:t["offset"] + t["n"]], gw[t["name"]].grad.numpy().reshape(-1), rel=1e-3,
                   abs_scale=1e-4, what="gen " + t["name"])
+
+
+def test_dp_tune_step_single_rank():
+    """dp_tune_step on one rank == its pieces run by hand:
+    forward, loss_targets_dp on the step-start state, backward, AdamW, state
+    update; parameters bit-identical, state updated."""
+    from preganplus_amd import train as TR
+    H, B = 16, 12
+    w = W.synth_weights(H, seed=6)
+    rng = np.random.Generator(np.random.PCG64(5))
+    wins = rng.uniform(0, 0.8, size=(B, 3, 3 * H)).astype(np.float32)
+    anom = (rng.uniform(size=(B, H)) < 0.3).astype(np.int32)
+    cls = rng.integers(0, 3, size=(B, H))
+    p0 = np.array([[0.2, 0.3], [0.6, 0.1], [0.5, 0.9]])
+    t1, s1 = TR.Trainer(H, w, max_batch=B), TR.TuneState(p0.copy())
+    TR.dp_tune_step(t1, s1, wins, anom, cls)
+    t2, s2 = TR.Trainer(H, w, max_batch=B), TR.TuneState(p0.copy())
+    lg, pr = t2.tune_forward(torch.tensor(wins))
+    mult, tgt, _, _, inc = TR.loss_targets_dp(lg.cpu().numpy(), pr.cpu().numpy(), anom, cls, s2)
+    t2.tune_backward(B, anom, mult, tgt)
+    t2.adam_step("transformer")
+    TR.dp_state_update(s2, inc)
+    torch.cuda.synchronize()
+    assert torch.equal(t1.P, t2.P)
+    np.testing.assert_array_equal(s1.protos, s2.protos)
+    assert not np.array_equal(s1.protos, p0) and s1.num_ones > 1
