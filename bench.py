@@ -91,7 +91,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-gan", action="store_true", help="tune config: Transformer tuning step only")
-    ap.add_argument("--config", choices=["c2", "fleet", "tune", "fpe", "gobi", "sim"], default="c2",
+    ap.add_argument("--config", choices=["c2", "fleet", "tune", "fpe", "gobi", "sim", "loop"], default="c2",
                     help="c2: BASELINE config 2 (default, the headline line); fleet: config 5 "
                          "(1024-host fleet = 64 cells of 16 hosts, shipped weights); tune: config 3 "
                          "(tuning step fwd+bwd+AdamW, data-parallel with an RCCL all-reduce); fpe: config 4 "
@@ -109,6 +109,8 @@ def main():
         return bench_gobi(args)
     if args.config == "sim":
         return bench_sim(args)
+    if args.config == "loop":
+        return bench_loop(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -539,6 +541,149 @@ def bench_sim(args):
         print(json.dumps(res), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
+
+
+def bench_loop(args):
+    """One online interval of PreGAN+ for a fleet of independent 16-host cells,
+    every stage on the device (f3 -> path -> f4 -> a11/a12):
+      GOBI schedules (pgp_gobi_optimize)  -> result_cache [E,16,16]
+      K1/K2/K2b encode + detect/classify  (run_model up to the embedding)
+      GAN step, labels simulated           (train_gan, pgp_simulate)
+      tuning step                          (tune_model; synthetic labels, as C3)
+      inference weight sync                (load_master: master -> packed layouts)
+      K3 + K5 with the updated GAN         (recover_decision)
+    in the reference's order (PreGANPlus.py:115-136).  All cells train as one
+    data-parallel batch (sum of their losses).  Shipped H=16 weights (PreGAN+
+    and the GOBI surrogate); GOBI inits from the reference's scheduling dataset;
+    synthetic windows and environment records."""
+    from preganplus_amd import simulate as SIM
+    from preganplus_amd import train as TR
+    from preganplus_amd.gobi import GOBIOptimizer
+    world, rank, device = _dist_setup()
+    H = 16
+    E = args.batch if args.batch != 65536 else 1024
+    w, extra = W.load_npz(os.path.join(ROOT, "preganplus_amd/data/simulator_16.npz"))
+    model = DecisionModel(H, w, device=device)
+    model.reserve(E)
+    tr = TR.Trainer(H, w, device=device, max_batch=E)
+    gobi = GOBIOptimizer(device=device)
+    sim = SIM.Simulation(H, device=device)
+    z = np.load(os.path.join(ROOT, "tests", "golden", "gobi_h16.npz"))
+    reps = -(-E // z["inits"].shape[0])
+    inits_h = np.concatenate([z["inits"]] * reps)[:E]
+    inits = torch.tensor(inits_h, device=device)
+    cur_h = inits_h[:, :, 2:].argmax(-1).astype(np.int32)
+    cur_host = torch.tensor(cur_h, device=device)
+    envs_h = SIM.synth_envs(E, H, seed=13 + rank)
+    envs_h[:, 2:2 + H] = cur_h  # the records' placement = GOBI's current allocation
+    envs = torch.tensor(envs_h, device=device)
+    x, _ = synth_inputs(E, H, device, 31 + rank)
+    g = torch.Generator(device=device).manual_seed(19 + rank)
+    y = (torch.rand((E, H), generator=g, device=device) < 0.1).to(torch.int32)
+    mult = torch.ones((E, H), device=device)
+    tgt = torch.rand((E, H, 2), generator=g, device=device)
+    protos = np.asarray(model.prototypes, dtype=np.float64)
+    gout = (torch.empty_like(inits), torch.empty(E, dtype=torch.int32, device=device),
+            torch.empty(E, dtype=torch.float32, device=device))
+    out = model.alloc_outputs(E)
+    sim_out = torch.empty((E, 4), dtype=torch.float64, device=device)
+    gan_target = torch.empty((E, 2), dtype=torch.float32, device=device)
+    sched = torch.empty((E, H, H), device=device)
+    names = ("gobi", "encode_classify", "gan_step", "tune_step", "weight_sync", "gan_decide_moves")
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(len(names) + 1)]
+    acc = np.zeros(len(names))
+
+    def interval(timed=False):
+        if timed:
+            ev[0].record()
+        res, _, _ = gobi.optimize(inits, out=gout)
+        sched.copy_(res[:, :, 2:])
+        if timed:
+            ev[1].record()
+        for st in (0, 1, 2):
+            model.forward(x, sched, out=out, stage=st)
+        emb = torch.where(out["logits"][..., 1:2] > out["logits"][..., 0:1], out["protos"], 0.0)
+        if timed:
+            ev[2].record()
+        TR.train_gan_batched(tr, sim, envs, emb, sched, out=sim_out, target=gan_target)
+        if timed:
+            ev[3].record()
+        tr.tune_forward(x)
+        tr.tune_backward(E, y, mult, tgt)
+        tr.adam_step("transformer")
+        if timed:
+            ev[4].record()
+        model.load_master(tr.P, protos)
+        if timed:
+            ev[5].record()
+        model.forward(x, sched, out=out, stage=3)
+        migrations(out["keep"], out["final_target"], cur_host)
+        if timed:
+            ev[6].record()
+
+    for _ in range(args.warmup):
+        interval()
+    steps = args.steps
+
+    def timed_interval():
+        interval(True)
+        torch.cuda.synchronize()
+        for k in range(len(names)):
+            acc[k] += ev[k].elapsed_time(ev[k + 1])
+
+    el = _timed(world, device, timed_interval, steps)
+    if rank == 0:
+        res = {
+            "metric": "fleet cell-intervals/sec (GOBI + decision + GAN/tuning steps + decisions)",
+            "value": E * world * steps / el, "unit": "cell-intervals/s", "n_gpus": world, "steps": steps,
+            "warmup": args.warmup, "ms_per_step": el / steps * 1e3, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "fp32 (fp64 simulation scores)",
+            "data": "GOBI inits from the reference's scheduling dataset; synthetic windows, environment records "
+                    "and tuning labels; shipped H=16 weights",
+            "config": {"workload": f"online interval, {E} independent 16-host cells per GPU", "hosts": H,
+                       "cells_per_gpu": E, "parallelism": f"dp{world}"},
+            "stage_ms": {n: float(acc[k] / steps) for k, n in enumerate(names)}}
+        if world == 1 and not args.no_cpu_baseline:
+            res["cpu_baseline"] = loop_cpu_baseline(w, extra, inits_h, x.cpu().numpy(), envs_h,
+                                                    y.cpu().numpy(), args.cpu_budget)
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+def loop_cpu_baseline(w, extra, inits, wins, envs, y, budget_s):
+    """The same per-cell interval on the host from the pinned restatements
+    (CPU baseline leg only): GOBI opt() (bit-identical to the reference's),
+    encode + classify (torch fp64), train_gan with runSimulation labels
+    (bit-identical restatement), one tuning step on the cell's window
+    (train.py backprop), recover_decision's Gen/Disc forward.  1 thread."""
+    from oracle import gobi_oracle as GO
+    from oracle import pregan_train_oracle as TO
+    from oracle import sim_oracle as SO
+    sd, _ = GO.load(os.path.join(ROOT, "preganplus_amd", "data", "gobi_energy_latency_16.npz"))
+    P = TO.PluginOracle(w, extra, np.ones((1, 48)))
+    torch.set_num_threads(1)
+    H = 16
+    t0, n = time.perf_counter(), 0
+    while time.perf_counter() - t0 < budget_s:
+        i = n % len(inits)
+        res, _, _ = GO.opt(sd, inits[i])
+        s = torch.tensor(np.asarray(res)[:, 2:], dtype=torch.float64)
+        with torch.no_grad():
+            logits, protos = TO.decode_t(P.tw, TO.encode_t(P.tw, torch.tensor(wins[i:i + 1], dtype=torch.float64)))
+        anom = logits[0, :, 1] > logits[0, :, 0]
+        emb = torch.where(anom[:, None], protos[0], torch.zeros_like(protos[0]))
+        TO.train_gan(P.gw, P.dw, P.gopt, P.dopt, emb, s, lambda sch: SO.score(envs[i], sch, H)[1])
+        TO.backprop(P.tw, P.topt, P.st, wins[i:i + 1].astype(np.float64), s.numpy()[None], y[i:i + 1],
+                    np.zeros_like(y[i:i + 1]))
+        with torch.no_grad():
+            ns = TO.gen_t(P.gw, emb[None], s[None])
+            TO.disc_t(P.dw, s[None], ns)
+        n += 1
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "cell-intervals/s", "cores": 1, "kind": "port",
+            "sample": f"{n} cell-intervals through the CPU restatements (GOBI opt, encode/classify, train_gan with "
+                      f"runSimulation labels, one tuning window, Gen/Disc), 1 thread, {dt:.1f}s"}
 
 
 if __name__ == "__main__":
