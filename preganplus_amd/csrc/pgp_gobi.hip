@@ -66,6 +66,7 @@ struct GobiLds {
   float a1[kN1], h1[kN1], a2[kN2], h2[kN2], a3[kN3], h3[kN3];
   float g1[kN1], g2[kN2], g3[kN3];
   float part[1024];
+  float adam[kMaxIt * 4];  // per-iteration AdamW scalars (GobiW::ADAM)
   float o[4];
   int flag[2];
 };
@@ -74,6 +75,7 @@ struct GobiLds {
 // every iteration (forward: W2^T/W3^T column blocks; backward: W2/W3 row blocks)
 struct GobiRegs {
   float w2f[16], w3f[8], w3b[8], w2b[16];
+  float b1, b2, b3, w40, w41, b40, b41;  // biases (threads < 128 / < 64) and the head, off the critical path
 };
 
 __device__ void load_regs(const float* __restrict__ W, GobiRegs& R) {
@@ -86,6 +88,13 @@ __device__ void load_regs(const float* __restrict__ W, GobiRegs& R) {
   for (int j = 0; j < 8; ++j) R.w3b[j] = W[GobiW::W3 + (sp * 8 + j) * kN2 + o];
 #pragma unroll
   for (int j = 0; j < 16; ++j) R.w2b[j] = W[GobiW::W2 + (sp * 16 + j) * kN1 + o];
+  R.b1 = W[GobiW::B1 + o];
+  R.b2 = W[GobiW::B2 + o];
+  R.b3 = W[GobiW::B3 + o3];
+  R.w40 = W[GobiW::W4 + o3];
+  R.w41 = W[GobiW::W4 + kN3 + o3];
+  R.b40 = W[GobiW::B4];
+  R.b41 = W[GobiW::B4 + 1];
 }
 
 // forward of the surrogate on L.x (all 1024 threads); z in L.o[2]
@@ -104,7 +113,7 @@ __device__ void surrogate_fwd(const float* __restrict__ W, const GobiRegs& R, Go
       float a = 0.f;
 #pragma unroll
       for (int q = 0; q < 8; ++q) a += L.part[q * 128 + t];
-      a += W[GobiW::B1 + t];
+      a += R.b1;
       L.a1[t] = a;
       L.h1[t] = softplus_f(a);
     }
@@ -121,7 +130,7 @@ __device__ void surrogate_fwd(const float* __restrict__ W, const GobiRegs& R, Go
       float a = 0.f;
 #pragma unroll
       for (int q = 0; q < 8; ++q) a += L.part[q * 128 + t];
-      a += W[GobiW::B2 + t];
+      a += R.b2;
       L.a2[t] = a;
       L.h2[t] = softplus_f(a);
     }
@@ -138,21 +147,21 @@ __device__ void surrogate_fwd(const float* __restrict__ W, const GobiRegs& R, Go
       float a = 0.f;
 #pragma unroll
       for (int q = 0; q < 16; ++q) a += L.part[q * 64 + t];
-      a += W[GobiW::B3 + t];
+      a += R.b3;
       L.a3[t] = a;
       L.h3[t] = a - tanhf(a);  // Tanhshrink
     }
     __syncthreads();
   }
   if (t < 64) {  // layer 4 (2 outputs) in wave 0, sigmoid, z = 0.8 e + 0.2 l
-    float p0 = W[GobiW::W4 + t] * L.h3[t], p1 = W[GobiW::W4 + kN3 + t] * L.h3[t];
+    float p0 = R.w40 * L.h3[t], p1 = R.w41 * L.h3[t];
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {
       p0 += __shfl_xor(p0, off);
       p1 += __shfl_xor(p1, off);
     }
     if (t == 0) {
-      const float o0 = sigmoid_f(p0 + W[GobiW::B4]), o1 = sigmoid_f(p1 + W[GobiW::B4 + 1]);
+      const float o0 = sigmoid_f(p0 + R.b40), o1 = sigmoid_f(p1 + R.b41);
       L.o[0] = o0;
       L.o[1] = o1;
       L.o[2] = 0.8f * o0 + 0.2f * o1;
@@ -176,6 +185,8 @@ __global__ __launch_bounds__(kT) void gobi_kernel(int E, const float* __restrict
     L.w1[o * kW1S + j] = W[GobiW::W1 + k];
   }
   for (int k = t; k < kIn; k += kT) L.x[k] = init[(long)e * kIn + k];
+  for (int k = t; k < kMaxIt * 4; k += kT) L.adam[k] = W[GobiW::ADAM + k];
+  if (t < 2) L.flag[t] = 0;
   GobiRegs R;
   load_regs(W, R);
   __syncthreads();
@@ -187,9 +198,10 @@ __global__ __launch_bounds__(kT) void gobi_kernel(int E, const float* __restrict
     if (t < 64) {  // dz/do = (0.8, 0.2) through the sigmoids; dh3 = W4^T do; through Tanhshrink
       const float o0 = L.o[0], o1 = L.o[1];
       const float d0 = 0.8f * (1.f - o0) * o0, d1 = 0.2f * (1.f - o1) * o1;
-      const float gh = W[GobiW::W4 + t] * d0 + W[GobiW::W4 + kN3 + t] * d1;
+      const float gh = R.w40 * d0 + R.w41 * d1;
       const float th = tanhf(L.a3[t]);
       L.g3[t] = gh - gh * (1.f - th * th);
+      if (t == 0) L.flag[(it + 1) & 1] = 0;  // next iteration's flag; this one's readers passed a barrier since
     }
     __syncthreads();
     {  // dh2 = W3^T g3 (128 x K=64, 8 splits of 8), through softplus
@@ -234,7 +246,7 @@ __global__ __launch_bounds__(kT) void gobi_kernel(int E, const float* __restrict
     if (t < 256) {
       const float gx = (L.part[t] + L.part[t + 256]) + (L.part[t + 512] + L.part[t + 768]);
       // ---- AdamW (torch single-tensor, opt.py:18 defaults) on the entry ----
-      const float* ad = W + GobiW::ADAM + it * 4;
+      const float* ad = L.adam + it * 4;
       const float xold = L.x[xi];
       float xv = xold * ad[0];
       m = m + 0.1f * (gx - m);            // exp_avg.lerp_(grad, 1 - beta1)
@@ -258,11 +270,9 @@ __global__ __launch_bounds__(kT) void gobi_kernel(int E, const float* __restrict
       changed = nv != xold;
       L.x[xi] = nv;
     }
-    if (t == 0) L.flag[0] = 0;
+    if (changed) L.flag[it & 1] = 1;  // benign race: every writer stores 1
     __syncthreads();
-    if (changed) L.flag[0] = 1;  // benign race: every writer stores 1
-    __syncthreads();
-    equal = L.flag[0] ? 0 : equal + 1;
+    equal = L.flag[it & 1] ? 0 : equal + 1;
     if (equal > kPatience) break;
     ++it;
   }
