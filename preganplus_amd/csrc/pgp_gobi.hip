@@ -49,12 +49,6 @@ struct GobiW {  // device offsets (floats) into one buffer
   static constexpr int SIZE = ADAM + kMaxIt * 4;
 };
 
-__device__ __forceinline__ float softplus_f(float x) { return x > 20.f ? x : log1pf(expf(x)); }
-__device__ __forceinline__ float softplus_b(float g, float x) {
-  if (x > 20.f) return g;
-  const float z = expf(x);
-  return g * z / (z + 1.f);
-}
 __device__ __forceinline__ float sigmoid_f(float x) { return 1.f / (1.f + expf(-x)); }
 
 constexpr int kT = 1024;          // threads per environment
@@ -63,10 +57,12 @@ constexpr int kW1S = kIn + 1;      // LDS row stride of W1: 289 = 33 (mod 64) ba
 struct GobiLds {
   float w1[kN1 * kW1S];  // layer-1 weights, natural [128][288] rows padded to 289 (147,968 B)
   float x[kIn];
-  float a1[kN1], h1[kN1], a2[kN2], h2[kN2], a3[kN3], h3[kN3];
+  float h1[kN1], h2[kN2];
   float g1[kN1], g2[kN2], g3[kN3];
   float part[1024];
   float adam[kMaxIt * 4];  // per-iteration AdamW scalars (GobiW::ADAM)
+  int hs[kH];              // each container's host (the one-hot column of its allocation row)
+  int dense;               // 1 while the allocation may not be one-hot (a non-one-hot init, iteration 0)
   float o[4];
   int flag[2];
 };
@@ -97,10 +93,24 @@ __device__ void load_regs(const float* __restrict__ W, GobiRegs& R) {
   R.b41 = W[GobiW::B4 + 1];
 }
 
+// pre-activations and their exp / tanh, kept in the registers of the threads
+// that own them in both directions (t < 128 for layers 1-2, t < 64 for layer 3),
+// so the backward's derivatives need no transcendental
+struct FwdKeep {
+  float a1, z1, a2, z2, th3;
+};
+__device__ __forceinline__ float softplus_keep(float a, float& z) {  // softplus (threshold 20), z = exp(a)
+  z = expf(a);
+  return a > 20.f ? a : log1pf(z);
+}
+__device__ __forceinline__ float softplus_grad(float g, float a, float z) {  // torch: g * z / (z + 1)
+  return a > 20.f ? g : g * z / (z + 1.f);
+}
+
 // forward of the surrogate on L.x (all 1024 threads); z in L.o[2]
-__device__ void surrogate_fwd(const float* __restrict__ W, const GobiRegs& R, GobiLds& L) {
+__device__ void surrogate_fwd(const float* __restrict__ W, const GobiRegs& R, GobiLds& L, FwdKeep& K, bool grad) {
   const int t = threadIdx.x;
-  {  // layer 1: 128 outputs x 8 splits of K = 288 (36 each), W1 rows from LDS
+  if (L.dense) {  // layer 1, dense: 128 outputs x 8 splits of K = 288 (36 each), W1 rows from LDS
     const int o = t & 127, sp = t >> 7;
     float acc = 0.f;
     const float* wr = L.w1 + o * kW1S + sp * 36;
@@ -114,8 +124,23 @@ __device__ void surrogate_fwd(const float* __restrict__ W, const GobiRegs& R, Go
 #pragma unroll
       for (int q = 0; q < 8; ++q) a += L.part[q * 128 + t];
       a += R.b1;
-      L.a1[t] = a;
-      L.h1[t] = softplus_f(a);
+      K.a1 = a;
+      L.h1[t] = softplus_keep(a, K.z1);
+    }
+    __syncthreads();
+  } else {  // layer 1 on a one-hot allocation: per container 2 FMAs (cpu, ips) + its host's column
+    if (t < kN1) {
+      const float* wr = L.w1 + t * kW1S;
+      float a = 0.f;
+#pragma unroll
+      for (int c = 0; c < kH; ++c) {
+        a = fmaf(wr[c * kF], L.x[c * kF], a);
+        a = fmaf(wr[c * kF + 1], L.x[c * kF + 1], a);
+        a = a + wr[c * kF + 2 + L.hs[c]];  // w * 1.0; the other 15 columns multiply 0
+      }
+      a += R.b1;
+      K.a1 = a;
+      L.h1[t] = softplus_keep(a, K.z1);
     }
     __syncthreads();
   }
@@ -131,8 +156,8 @@ __device__ void surrogate_fwd(const float* __restrict__ W, const GobiRegs& R, Go
 #pragma unroll
       for (int q = 0; q < 8; ++q) a += L.part[q * 128 + t];
       a += R.b2;
-      L.a2[t] = a;
-      L.h2[t] = softplus_f(a);
+      K.a2 = a;
+      L.h2[t] = softplus_keep(a, K.z2);
     }
     __syncthreads();
   }
@@ -148,23 +173,28 @@ __device__ void surrogate_fwd(const float* __restrict__ W, const GobiRegs& R, Go
 #pragma unroll
       for (int q = 0; q < 16; ++q) a += L.part[q * 64 + t];
       a += R.b3;
-      L.a3[t] = a;
-      L.h3[t] = a - tanhf(a);  // Tanhshrink
-    }
-    __syncthreads();
-  }
-  if (t < 64) {  // layer 4 (2 outputs) in wave 0, sigmoid, z = 0.8 e + 0.2 l
-    float p0 = R.w40 * L.h3[t], p1 = R.w41 * L.h3[t];
+      K.th3 = tanhf(a);
+      const float h3 = a - K.th3;  // Tanhshrink
+      // layer 4 (2 outputs) in the same wave 0 (no barrier), sigmoid, z = 0.8 e + 0.2 l
+      float p0 = R.w40 * h3, p1 = R.w41 * h3;
 #pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-      p0 += __shfl_xor(p0, off);
-      p1 += __shfl_xor(p1, off);
-    }
-    if (t == 0) {
+      for (int off = 32; off >= 1; off >>= 1) {
+        p0 += __shfl_xor(p0, off);
+        p1 += __shfl_xor(p1, off);
+      }
+      // every lane holds the same sums (the butterfly adds commute exactly)
       const float o0 = sigmoid_f(p0 + R.b40), o1 = sigmoid_f(p1 + R.b41);
-      L.o[0] = o0;
-      L.o[1] = o1;
-      L.o[2] = 0.8f * o0 + 0.2f * o1;
+      if (t == 0) {
+        L.o[0] = o0;
+        L.o[1] = o1;
+        L.o[2] = 0.8f * o0 + 0.2f * o1;
+      }
+      if (grad) {  // backward start in the same wave: dz/do = (0.8, 0.2) through the sigmoids,
+                   // dh3 = W4^T do, through Tanhshrink
+        const float d0 = 0.8f * (1.f - o0) * o0, d1 = 0.2f * (1.f - o1) * o1;
+        const float gh = R.w40 * d0 + R.w41 * d1;
+        L.g3[t] = gh - gh * (1.f - K.th3 * K.th3);
+      }
     }
   }
   __syncthreads();
@@ -187,23 +217,31 @@ __global__ __launch_bounds__(kT) void gobi_kernel(int E, const float* __restrict
   for (int k = t; k < kIn; k += kT) L.x[k] = init[(long)e * kIn + k];
   for (int k = t; k < kMaxIt * 4; k += kT) L.adam[k] = W[GobiW::ADAM + k];
   if (t < 2) L.flag[t] = 0;
+  if (t == 0) L.dense = 0;
   GobiRegs R;
   load_regs(W, R);
   __syncthreads();
+  if (t < kH) {  // is the init's allocation one-hot?  (then layer 1 is a column gather)
+    int ones = 0, other = 0, h = 0;
+    for (int j = 0; j < kH; ++j) {
+      const float xv = L.x[t * kF + 2 + j];
+      if (xv == 1.f) {
+        ++ones;
+        h = j;
+      } else if (xv != 0.f) {
+        ++other;
+      }
+    }
+    L.hs[t] = h;
+    if (ones != 1 || other) L.dense = 1;
+  }
+  __syncthreads();
   float m = 0.f, v = 0.f;
+  FwdKeep K{0.f, 0.f, 0.f, 0.f, 0.f};
   int equal = 0, it = 0;
   while (it < max_it) {
-    surrogate_fwd(W, R, L);
-    // ---- backward to the input (autograd of z) ----
-    if (t < 64) {  // dz/do = (0.8, 0.2) through the sigmoids; dh3 = W4^T do; through Tanhshrink
-      const float o0 = L.o[0], o1 = L.o[1];
-      const float d0 = 0.8f * (1.f - o0) * o0, d1 = 0.2f * (1.f - o1) * o1;
-      const float gh = R.w40 * d0 + R.w41 * d1;
-      const float th = tanhf(L.a3[t]);
-      L.g3[t] = gh - gh * (1.f - th * th);
-      if (t == 0) L.flag[(it + 1) & 1] = 0;  // next iteration's flag; this one's readers passed a barrier since
-    }
-    __syncthreads();
+    surrogate_fwd(W, R, L, K, true);
+    // ---- backward to the input (autograd of z; g3 came with the forward) ----
     {  // dh2 = W3^T g3 (128 x K=64, 8 splits of 8), through softplus
       const int sp = t >> 7;
       float acc = 0.f;
@@ -211,11 +249,12 @@ __global__ __launch_bounds__(kT) void gobi_kernel(int E, const float* __restrict
       for (int j = 0; j < 8; ++j) acc = fmaf(R.w3b[j], L.g3[sp * 8 + j], acc);
       L.part[t] = acc;
       __syncthreads();
+      if (t == 0) L.flag[(it + 1) & 1] = 0;  // next iteration's flag; its last readers passed barriers since
       if (t < kN2) {
         float a = 0.f;
 #pragma unroll
         for (int q = 0; q < 8; ++q) a += L.part[q * 128 + t];
-        L.g2[t] = softplus_b(a, L.a2[t]);
+        L.g2[t] = softplus_grad(a, K.a2, K.z2);
       }
       __syncthreads();
     }
@@ -230,7 +269,7 @@ __global__ __launch_bounds__(kT) void gobi_kernel(int E, const float* __restrict
         float a = 0.f;
 #pragma unroll
         for (int q = 0; q < 8; ++q) a += L.part[q * 128 + t];
-        L.g1[t] = softplus_b(a, L.a1[t]);
+        L.g1[t] = softplus_grad(a, K.a1, K.z1);
       }
       __syncthreads();
     }
@@ -269,6 +308,8 @@ __global__ __launch_bounds__(kT) void gobi_kernel(int E, const float* __restrict
       const float nv = bi == hcol ? 1.f : 0.f;
       changed = nv != xold;
       L.x[xi] = nv;
+      if (bi == hcol) L.hs[c] = hcol;
+      if (t == 0) L.dense = 0;  // one-hot from here on
     }
     if (changed) L.flag[it & 1] = 1;  // benign race: every writer stores 1
     __syncthreads();
@@ -276,7 +317,7 @@ __global__ __launch_bounds__(kT) void gobi_kernel(int E, const float* __restrict
     if (equal > kPatience) break;
     ++it;
   }
-  surrogate_fwd(W, R, L);
+  surrogate_fwd(W, R, L, K, false);
   for (int k = t; k < kIn; k += kT) result[(long)e * kIn + k] = L.x[k];
   if (t == 0) {
     iterations[e] = it;
