@@ -82,6 +82,14 @@ PGP_DEV f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 // Sum over lane groups: v + v[lane ^ 16] (+ the same across lane ^ 32), with
 // the gfx950 half-row swaps instead of ds_bpermute round trips.
 // permlane16_swap(v, v) returns (rows 0,0,2,2 | rows 1,1,3,3) of v and
+// tanh as 1 - 2 / (exp(2x) + 1) on the hardware exp2 / rcp (5 VALU ops vs ~26
+// for tanhf): absolute error ~1e-7 (cancellation near 0), saturates to +-1.
+// For inference outputs compared at fp32 tolerance; training kernels keep tanhf.
+PGP_DEV float tanh_fast(float x) {
+  const float e = __expf(2.f * x);
+  return 1.f - 2.f * __builtin_amdgcn_rcpf(e + 1.f);
+}
+
 // permlane32_swap(v, v) returns (halves 0,0 | 1,1): the element-wise sum of the
 // pair is the xor-16 / xor-32 sum, bit-identical to v + shfl_xor (a+b == b+a).
 PGP_DEV float xsum(float v, bool both) {

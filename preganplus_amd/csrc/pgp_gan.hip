@@ -192,7 +192,7 @@ __global__ __launch_bounds__(kGanWaves * 64) void gan_kernel(FwdArgs a) {
         const int hh = 16 * t + 4 * g + r;
         if (hh < H) {
           const float s0 = sv[t][r];
-          const float nv = s0 + 4.0f * tanhf(ns[t][r]);
+          const float nv = s0 + 4.0f * tanh_fast(ns[t][r]);
           ns[t][r] = nv;
           if (nv > bn_v) {  // strict: first maximum wins (list.index(max(...)))
             bn_v = nv;
