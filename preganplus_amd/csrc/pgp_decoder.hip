@@ -99,7 +99,7 @@ __global__ __launch_bounds__(kDecWaves * 64) void decoder_kernel(FwdArgs a) {
     const f32x4 v = acc[mt] + ld4(tab + G::T_DEC + 16 * mt + 4 * g);
     if (host < H) {
       const float l0 = v[0], l1 = v[1];
-      const float p0 = 1.0f / (1.0f + expf(-v[2])), p1 = 1.0f / (1.0f + expf(-v[3]));
+      const float p0 = __builtin_amdgcn_rcpf(1.0f + __expf(-v[2])), p1 = __builtin_amdgcn_rcpf(1.0f + __expf(-v[3]));
       const bool an = l1 > l0;  // torch.argmax: ties -> index 0
       const float e0 = an ? p0 : 0.f, e1 = an ? p1 : 0.f;
       int cl = -1;

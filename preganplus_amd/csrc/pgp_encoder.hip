@@ -123,7 +123,7 @@ PGP_DEV void layer_norm_tiles(f32x4 (&acc)[Geo<H>::MT_D][3], f32x4 (&X)[Geo<H>::
         var += dv * dv;
       }
     var = xsum(var, true);
-    const float rstd = 1.0f / sqrtf(var * invH + 1e-5f);
+    const float rstd = __builtin_amdgcn_rsqf(var * invH + 1e-5f);  // v_rsq_f32 (1 ulp)
 #pragma unroll
     for (int mt = 0; mt < G::MT_D; ++mt) {
       const f32x4 ga = ld4(gam + 16 * mt + 4 * g), be = ld4(bet + 16 * mt + 4 * g);
@@ -177,8 +177,8 @@ PGP_DEV void attention(const f32x4 (&QKV)[3 * Geo<H>::TP][3], f32x4 (&O)[Geo<H>:
       sc[w2] = xsum(part, !G::P8);  // P8: lane groups {0,1} = head 0, {2,3} = head 1
     }
     const float m = fmaxf(sc[0], fmaxf(sc[1], sc[2]));
-    const float e0 = expf(sc[0] - m), e1 = expf(sc[1] - m), e2 = expf(sc[2] - m);
-    const float inv = 1.0f / (e0 + e1 + e2);
+    const float e0 = __expf(sc[0] - m), e1 = __expf(sc[1] - m), e2 = __expf(sc[2] - m);  // v_exp_f32
+    const float inv = __builtin_amdgcn_rcpf(e0 + e1 + e2);
     pr[w][0] = e0 * inv;
     pr[w][1] = e1 * inv;
     pr[w][2] = e2 * inv;
@@ -303,9 +303,11 @@ PGP_DEV void encoder_layer_tail(f32x4 (&X)[Geo<H>::MT_D][3], Ring<H>& ring, cons
       s1[w2] = t1;
     }
     const float m0 = fmaxf(s0[0], fmaxf(s0[1], s0[2])), m1 = fmaxf(s1[0], fmaxf(s1[1], s1[2]));
-    const float e00 = expf(s0[0] - m0), e01 = expf(s0[1] - m0), e02 = expf(s0[2] - m0);
-    const float e10 = expf(s1[0] - m1), e11 = expf(s1[1] - m1), e12 = expf(s1[2] - m1);
-    const float i0 = 1.0f / (e00 + e01 + e02), i1 = 1.0f / (e10 + e11 + e12);
+    // hardware exp2 / rcp (a few ulp; logits are compared at rtol 1e-4): the softmax is the
+    // VALU-heaviest phase beside the MFMAs at 2 waves per SIMD
+    const float e00 = __expf(s0[0] - m0), e01 = __expf(s0[1] - m0), e02 = __expf(s0[2] - m0);
+    const float e10 = __expf(s1[0] - m1), e11 = __expf(s1[1] - m1), e12 = __expf(s1[2] - m1);
+    const float i0 = __builtin_amdgcn_rcpf(e00 + e01 + e02), i1 = __builtin_amdgcn_rcpf(e10 + e11 + e12);
     P0[w][0] = e00 * i0;
     P0[w][1] = e01 * i0;
     P0[w][2] = e02 * i0;
