@@ -112,15 +112,7 @@ def main():
     if args.config == "loop":
         return bench_loop(args)
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    device = torch.device("cuda", local)
-    torch.cuda.set_device(device)
+    world, rank, device = _dist_setup()
     H, B = args.hosts, args.batch
 
     weights = W.synth_weights(H, seed=0)
@@ -219,13 +211,20 @@ def main():
 
 
 def _dist_setup():
+    """One process per GPU (torchrun env).  Rehearsal knobs for a 1-GPU box:
+    PGP_DIST_BACKEND=gloo and PGP_DEVICE=0 put every rank on that GPU
+    (RCCL refuses two ranks on one device); the driver's runs use neither."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = int(os.environ.get("PGP_DEVICE", os.environ.get("LOCAL_RANK", "0")))
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = os.environ.get("PGP_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
     return world, rank, device
