@@ -91,7 +91,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-gan", action="store_true", help="tune config: Transformer tuning step only")
-    ap.add_argument("--config", choices=["c2", "fleet", "tune", "fpe", "gobi", "sim", "loop"], default="c2",
+    ap.add_argument("--config", choices=["c2", "fleet", "tune", "fpe", "gobi", "sim", "loop", "plugin"], default="c2",
                     help="c2: BASELINE config 2 (default, the headline line); fleet: config 5 "
                          "(1024-host fleet = 64 cells of 16 hosts, shipped weights); tune: config 3 "
                          "(tuning step fwd+bwd+AdamW, data-parallel with an RCCL all-reduce); fpe: config 4 "
@@ -111,6 +111,8 @@ def main():
         return bench_sim(args)
     if args.config == "loop":
         return bench_loop(args)
+    if args.config == "plugin":
+        return bench_plugin(args)
 
     world, rank, device = _dist_setup()
     H, B = args.hosts, args.batch
@@ -683,6 +685,108 @@ def loop_cpu_baseline(w, extra, inits, wins, envs, y, budget_s):
     return {"value": n / dt, "unit": "cell-intervals/s", "cores": 1, "kind": "port",
             "sample": f"{n} cell-intervals through the CPU restatements (GOBI opt, encode/classify, train_gan with "
                       f"runSimulation labels, one tuning window, Gen/Disc), 1 thread, {dt:.1f}s"}
+
+
+class _Obj:
+    pass
+
+
+class _Container:
+    def __init__(self, cid, hid):
+        self.id, self._h = cid, hid
+
+    def getHostID(self):
+        return self._h
+
+
+def _plugin_env(z, step, train_time):
+    """A COSCO-shaped environment for one interval of the plugin fixture
+    (tests/golden/plugin_h16.npz): placement, GOBI schedule, time series, and
+    runSimulation returning that interval's recorded scores."""
+    env = _Obj()
+    env.hostlist = list(range(16))
+    placement = z[f"s{step}/placement"]
+    cl = [_Container(c, int(placement[c])) for c in range(16)]
+    cl[int(z["container_none"]) if "container_none" in z.files else 3] = None
+    env.containerlist = cl
+    env.scheduler = _Obj()
+    env.scheduler.result_cache = z[f"s{step}/sched"]
+    env.stats = _Obj()
+    tt = int(z["T0"]) + step
+    env.stats.time_series = train_time[:tt + 1]
+    env.stats.schedule_series = z["schedule_series"][:tt + 1]
+    sc = [tuple(x) for x in z[f"s{step}/scores"]]
+    env.stats.runSimulation = lambda sched: sc.pop(0)
+    return env
+
+
+def bench_plugin(args):
+    """BASELINE config 1: one PreGANPlusRecovery.run_model call (PreGANPlus.py:115-136)
+    as COSCO makes it each interval, H=16 shipped weights: encoder, detect,
+    train_gan, tune_model (10 sequential windows), recover_decision.  The
+    environment replays the reference-recorded intervals of
+    tests/golden/plugin_h16.npz (runSimulation returns the recorded scores).
+    Checkpoint writes and plotting are off on both sides.  The CPU baseline is
+    the torch-fp64 restatement of the same call (oracle/pregan_train_oracle.py
+    PluginOracle, pinned to the reference's own outputs)."""
+    from preganplus_amd.recovery import PreGANPlusRecovery
+    world, rank, device = _dist_setup()
+    w, extra = W.load_npz(os.path.join(ROOT, "preganplus_amd/data/simulator_16.npz"))
+    z = np.load(os.path.join(ROOT, "tests", "golden", "plugin_h16.npz"))
+    tr_time = extra["train_time_data"]
+    rec = PreGANPlusRecovery(16, "", training=True, weights=w, extra=extra, device=device)
+
+    def call(k):
+        step = k % 4
+        rec.setEnvironment(_plugin_env(z, step, tr_time))
+        return rec.run_model(None, [tuple(x) for x in z[f"s{step}/decision_in"]])
+
+    for k in range(args.warmup):
+        call(k)
+    lat = []
+    for k in range(args.steps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        call(k)
+        torch.cuda.synchronize()
+        lat.append(time.perf_counter() - t0)
+    # batch-1 inference latency (the encoder + classify + GAN gate of one window)
+    model = rec.infer
+    x1 = torch.tensor(rec.input_window()[None], dtype=torch.float32, device=device)
+    s1 = torch.tensor(np.asarray(z["s0/sched"])[None], dtype=torch.float32, device=device)
+    out = model.alloc_outputs(1)
+    for _ in range(5):
+        model.forward(x1, s1, out=out)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(50):
+        model.forward(x1, s1, out=out)
+    torch.cuda.synchronize()
+    fwd_ms = (time.perf_counter() - t0) / 50 * 1e3
+    ms = float(np.median(lat) * 1e3)
+    if rank == 0:
+        res = {"metric": "plugin run_model calls/sec (H=16, train_gan + tune_model + decision)", "value": 1e3 / ms,
+               "unit": "calls/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
+               "higher_is_better": True, "scaling": "replicas only", "vs_baseline": None, "dtype": "fp32",
+               "data": "reference-recorded intervals (tests/golden/plugin_h16.npz), shipped H=16 weights",
+               "config": {"workload": "C1: PreGANPlusRecovery.run_model, one COSCO interval, 16 hosts",
+                          "hosts": 16, "tuning_windows": 10},
+               "latency_ms": {"run_model_median": ms, "run_model_p90": float(np.percentile(lat, 90) * 1e3),
+                              "forward_batch1": fwd_ms}}
+        if not args.no_cpu_baseline:
+            from oracle import pregan_train_oracle as TO  # CPU baseline leg only
+            torch.set_num_threads(1)
+            po = TO.PluginOracle(w, extra, tr_time)
+            t0, n = time.perf_counter(), 0
+            while time.perf_counter() - t0 < args.cpu_budget:
+                step = n % 4
+                po.run_model(_plugin_env(z, step, tr_time), [tuple(x) for x in z[f"s{step}/decision_in"]])
+                n += 1
+            dt = time.perf_counter() - t0
+            res["cpu_baseline"] = {"value": n / dt, "unit": "calls/s", "cores": 1, "kind": "port",
+                                   "sample": f"{n} run_model calls of the torch-fp64 plugin restatement "
+                                             f"(pinned to the reference's outputs), 1 thread, {dt:.1f}s"}
+        print(json.dumps(res), flush=True)
 
 
 if __name__ == "__main__":
