@@ -325,11 +325,11 @@ struct RedArgs {
   float* outB;
   float* lvl2;
 };
-__global__ __launch_bounds__(256) void reduce_kernel(RedArgs a) {
+PGP_DEV void reduce_block(const RedArgs& a, int bx, int by) {
   __shared__ float red[4][65];
   const int jl = threadIdx.x & 63, pg = threadIdx.x >> 6;
   const long na = (long)a.rows * a.cols, nout = na + a.nb;
-  const long o = (long)blockIdx.x * 64 + jl;
+  const long o = (long)bx * 64 + jl;
   const bool ok = o < nout;
   long src = 0;
   if (ok) {
@@ -340,7 +340,7 @@ __global__ __launch_bounds__(256) void reduce_kernel(RedArgs a) {
       src = a.srcb + (o - na);
     }
   }
-  const int p0 = blockIdx.y * a.pc, p1 = min(a.nparts, p0 + a.pc);
+  const int p0 = by * a.pc, p1 = min(a.nparts, p0 + a.pc);
   const float* sp = a.part + src;
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
   if (ok) {
@@ -358,7 +358,7 @@ __global__ __launch_bounds__(256) void reduce_kernel(RedArgs a) {
   if (pg == 0 && ok) {
     const float t = (red[0][jl] + red[1][jl]) + (red[2][jl] + red[3][jl]);
     if (a.lvl2) {
-      a.lvl2[blockIdx.y * nout + o] = t;
+      a.lvl2[by * nout + o] = t;
     } else if (o < na) {
       const int i = (int)(o / a.cols), j = (int)(o - (long)i * a.cols);
       a.outA[(long)i * a.ldo + j] += t;
@@ -367,6 +367,27 @@ __global__ __launch_bounds__(256) void reduce_kernel(RedArgs a) {
     }
   }
 }
+__global__ __launch_bounds__(256) void reduce_kernel(RedArgs a) { reduce_block(a, blockIdx.x, blockIdx.y); }
+
+// Up to kMaxRedSeg reductions in one launch (the backward defers every weight-
+// gradient reduction to its end): block x -> (segment, local block) by the
+// prefix table, y = split; a segment's blocks run reduce_block exactly as its own
+// reduce_kernel launch would, so the sums are bit-identical.
+constexpr int kMaxRedSeg = 16;
+struct RedTable {
+  int n;
+  int bx0[kMaxRedSeg + 1];
+  int nsplit[kMaxRedSeg];
+  RedArgs seg[kMaxRedSeg];
+};
+__global__ __launch_bounds__(256) void reduce_multi_kernel(RedTable t) {
+  const int bx = blockIdx.x;
+  int s = 0;
+  while (s + 1 < t.n && bx >= t.bx0[s + 1]) ++s;
+  if ((int)blockIdx.y >= t.nsplit[s]) return;  // whole block
+  reduce_block(t.seg[s], bx - t.bx0[s], blockIdx.y);
+}
+
 
 // ============================================================================
 // GAT (dlutils.py:296-369), one wave per (window, step), lane = host.
@@ -862,40 +883,71 @@ hipError_t lin(const TunePlan& p, const LinArgs& a, hipStream_t st) {
   return hipSuccess;
 }
 
-// Reduce partial slabs into segment A (rows x cols matrix) and B (nb vector).
-hipError_t reduce_into(const TunePlan& p, float* ws, int nparts, long pstride, const float* part, int rows, int cols,
-                       int ldp, float* outA, int ldo, int nb, long srcb, float* outB, hipStream_t st) {
-  RedArgs a{nparts, nparts, pstride, part, rows, cols, ldp, ldo, nb, srcb, outA, outB, nullptr};
-  const long nout = (long)rows * cols + nb;
-  const int gx = (int)((nout + 63) / 64);
-  const int nsplit = (nparts + kRedChunk - 1) / kRedChunk;
-  if (nsplit <= 1) {
-    TCK((reduce_kernel<<<gx, 256, 0, st>>>(a)));
+// The backward's weight-gradient reductions, deferred to one pair of launches at
+// its end (nothing in the backward reads a weight gradient).  Each deferred
+// reduction gets its own partial and level-2 regions from the plan's pool.
+struct RedBatch {
+  float* pool;
+  long cap;
+  long used = 0;
+  RedTable l1{}, l2{};
+  int gx1 = 0, gx2 = 0, ny1 = 1;
+  float* take(long n) {
+    float* r = pool + used;
+    used += (n + 63) / 64 * 64;
+    return r;
+  }
+  bool add(int nparts, long pstride, const float* part, int rows, int cols, int ldp, float* outA, int ldo, int nb,
+           long srcb, float* outB) {
+    if (l1.n >= kMaxRedSeg) return false;
+    const long nout = (long)rows * cols + nb;
+    const int gx = (int)((nout + 63) / 64);
+    const int nsplit = (nparts + kRedChunk - 1) / kRedChunk;
+    RedArgs a{nparts, nparts, pstride, part, rows, cols, ldp, ldo, nb, srcb, outA, outB, nullptr};
+    if (nsplit > 1) {
+      a.pc = kRedChunk;
+      a.lvl2 = take((long)nsplit * nout);
+      l2.seg[l2.n] = RedArgs{nsplit, nsplit, nout, a.lvl2, rows, cols, cols, ldo, nb, (long)rows * cols,
+                             outA, outB, nullptr};
+      l2.nsplit[l2.n] = 1;
+      l2.bx0[l2.n] = gx2;
+      gx2 += gx;
+      ++l2.n;
+    }
+    l1.seg[l1.n] = a;
+    l1.nsplit[l1.n] = nsplit;
+    l1.bx0[l1.n] = gx1;
+    gx1 += gx;
+    ny1 = std::max(ny1, nsplit);
+    ++l1.n;
+    return used <= cap;
+  }
+  hipError_t flush(hipStream_t st) {
+    if (used > cap) return hipErrorInvalidValue;  // the plan's pool is too small (a bug): fail loudly
+    l1.bx0[l1.n] = gx1;
+    l2.bx0[l2.n] = gx2;
+    if (l1.n) TCK((reduce_multi_kernel<<<dim3(gx1, ny1), 256, 0, st>>>(l1)));
+    if (l2.n) TCK((reduce_multi_kernel<<<gx2, 256, 0, st>>>(l2)));
     return hipSuccess;
   }
-  a.pc = kRedChunk;
-  a.lvl2 = ws + p.red2;
-  TCK((reduce_kernel<<<dim3(gx, nsplit), 256, 0, st>>>(a)));
-  // second pass over the splits: the level-2 slab is [nsplit][nout] in output order
-  RedArgs b{nsplit, nsplit, nout, ws + p.red2, rows, cols, cols, ldo, nb, (long)rows * cols, outA, outB, nullptr};
-  TCK((reduce_kernel<<<gx, 256, 0, st>>>(b)));
-  return hipSuccess;
-}
+};
 
 // dW[N][K] (row stride K) += sum_m Y[m][n] X[m][k];  db[N] += sum_m Y[m][n]
+// (partial slabs from the pool; the reduction is deferred to rb.flush)
 template <int NP, int KP>
-hipError_t dw(const TunePlan& p, float* ws, const float* Y, int ldy, const float* X, int ldx, int relu, int N, int K,
-              float* gW, float* gb, hipStream_t st) {
-  DwArgs a{p.M, Y, ldy, X, ldx, relu, ws + p.part};
+hipError_t dw(const TunePlan& p, RedBatch& rb, const float* Y, int ldy, const float* X, int ldx, int relu, int N,
+              int K, float* gW, float* gb, hipStream_t st) {
+  const long pstride = (long)NP * KP + NP;
+  float* part = rb.take((long)p.dw_grid * pstride);
+  DwArgs a{p.M, Y, ldy, X, ldx, relu, part};
   TCK((dw_kernel<NP, KP><<<p.dw_grid, 256, 0, st>>>(a)));
-  return reduce_into(p, ws, p.dw_grid, (long)NP * KP + NP, ws + p.part, N, K, KP, gW, K, gb ? N : 0,
-                     (long)NP * KP, gb, st);
+  return rb.add(p.dw_grid, pstride, part, N, K, KP, gW, K, gb ? N : 0, (long)NP * KP, gb) ? hipSuccess
+                                                                                          : hipErrorInvalidValue;
 }
 
-// gamma / beta gradients from LNB partials [nparts][2][DP]
-hipError_t ln_grads(const TunePlan& p, float* ws, int nparts, const float* part, int N, float* gw, float* gb,
-                    hipStream_t st) {
-  return reduce_into(p, ws, nparts, 2L * p.DP, part, 1, N, 0, gw, 0, N, p.DP, gb, st);
+// gamma / beta gradients from LNB partials [nparts][2][DP] (deferred)
+hipError_t ln_grads(const TunePlan& p, RedBatch& rb, int nparts, const float* part, int N, float* gw, float* gb) {
+  return rb.add(nparts, 2L * p.DP, part, 1, N, 0, gw, 0, N, p.DP, gb) ? hipSuccess : hipErrorInvalidValue;
 }
 
 template <int H>
@@ -954,9 +1006,32 @@ bool plan_h(int B, TunePlan* out) {
   part = std::max(part, std::max(512L, (long)q.dec_bg) * 64 * Q::NOP);    // decoder split-K
   part = std::max(part, (long)Q::T * 8 * 2 * Q::DP);                      // decoder dX LNB (<= 8 x T groups)
   q.part = take(part);
-  // second-level reduction: <= ceil(max partials / 64) splits x the largest slab
-  const long max_parts = std::max<long>(512, (long)Q::T * 8);
-  q.red2 = take((max_parts + 255) / 256 * (np_max * 64 + np_max));
+  // the backward's deferred reductions (RedBatch): each dW / LN-gradient partial
+  // region plus its level-2 region, in the order tune_bwd_h takes them
+  {
+    long pool = 0;
+    auto r64 = [](long n) { return (n + 63) / 64 * 64; };
+    auto red = [&](long nparts, long slab, long nout) {
+      pool += r64(nparts * slab);
+      const long ns = (nparts + 255) / 256;
+      if (ns > 1) pool += r64(ns * nout);
+    };
+    auto dwr = [&](long np, long kp, long n, long k, bool bias) { red(q.dw_grid, np * kp + np, n * k + (bias ? n : 0)); };
+    const long DPl = Q::DP, FFl = Q::FF, Q3Pl = Q::Q3P, Hl = H;
+    red((long)q.dec_dxg * Q::T, 2 * DPl, 2 * Hl);  // decoder dX through layer 1's norm2
+    for (int l = 1; l >= 0; --l) {
+      dwr(DPl, FFl, Hl, FFl, true);        // W2
+      dwr(FFl, DPl, FFl, Hl, true);        // W1
+      red(q.lin_grid, 2 * DPl, 2 * Hl);    // norm1
+      dwr(DPl, DPl, Hl, Hl, true);         // out_proj
+      dwr(Q3Pl, DPl, 3 * Hl, Hl, true);    // in_proj
+      if (l == 1) red(q.lin_grid, 2 * DPl, 2 * Hl);  // layer 0's norm2
+    }
+    dwr(DPl, DPl, Hl, Hl, true);           // time encoder
+    dwr(DPl, Q::XBP, Hl, 3, false);        // GAT fc
+    q.pool = take(pool);
+    q.pool_len = pool;
+  }
   q.total = off;
   *out = q;
   return true;
@@ -1023,6 +1098,7 @@ hipError_t tune_bwd_h(const TunePlan& p, const float* P, float* Gd, float* ws, c
   const int B = p.B;
   const long M = p.M;
   hipError_t e;
+  RedBatch rb{ws + p.pool, p.pool_len};
   TCK((tune_loss_kernel<<<(int)(((long)B * H + 255) / 256), 256, 0, st>>>(B, H, Q::NOP, logits, protos, y, mult,
                                                                            tgt, ws + p.dpre)));
   TCK((dec_dw_kernel<H><<<dim3(Q::T, 2), 256, 0, st>>>(B, ws + p.dpre, ws + p.x[2], Gd)));
@@ -1036,27 +1112,26 @@ hipError_t tune_bwd_h(const TunePlan& p, const float* P, float* Gd, float* ws, c
     a.RS = ws + p.rs2[1];
     a.rss = Q::T;
     a.lnw = L1 + G::L_N2W;
-    a.part = ws + p.part;
+    a.part = rb.take((long)p.dec_dxg * Q::T * 2 * DP);
     a.bw = (long)DP * Q::NOP;
     a.by = a.bxh = DP;
     a.brs = 1;
     TCK((linear_kernel<DP, Q::NOP, EPI_LNB><<<dim3(p.dec_dxg, Q::T), 256, 0, st>>>(a)));
-    if ((e = ln_grads(p, ws, p.dec_dxg * Q::T, ws + p.part, H, L1g + G::L_N2W, L1g + G::L_N2B, st)) != hipSuccess)
-      return e;
+    if ((e = ln_grads(p, rb, p.dec_dxg * Q::T, a.part, H, L1g + G::L_N2W, L1g + G::L_N2B)) != hipSuccess) return e;
   }
   const int lnb_parts = p.lin_grid;
   for (int l = 1; l >= 0; --l) {
     const float* Lp = P + G::LAY0 + l * G::L_SIZE;
     float* Lg = Gd + G::LAY0 + l * G::L_SIZE;
     // da = grad of R2 = Y1 + relu(F) W2^T + b2
-    if ((e = dw<DP, FF>(p, ws, ws + p.da, DP, ws + p.f[l], FF, 1, H, FF, Lg + G::L_W2, Lg + G::L_B2, st)) !=
+    if ((e = dw<DP, FF>(p, rb, ws + p.da, DP, ws + p.f[l], FF, 1, H, FF, Lg + G::L_W2, Lg + G::L_B2, st)) !=
         hipSuccess)
       return e;
     LinArgs a = lin_args(M, ws + p.da, DP, Lp + G::L_W2, FF, FF, H, 1, nullptr, ws + p.df, FF);
     a.R = ws + p.f[l];
     a.ldr = FF;
     if ((e = lin<FF, DP, EPI_MASK>(p, a, st)) != hipSuccess) return e;
-    if ((e = dw<FF, DP>(p, ws, ws + p.df, FF, ws + p.y1[l], DP, 0, FF, H, Lg + G::L_W1, Lg + G::L_B1, st)) !=
+    if ((e = dw<FF, DP>(p, rb, ws + p.df, FF, ws + p.y1[l], DP, 0, FF, H, Lg + G::L_W1, Lg + G::L_B1, st)) !=
         hipSuccess)
       return e;
     // db = grad of R1: (dF W1 + dR2) through norm1
@@ -1066,10 +1141,10 @@ hipError_t tune_bwd_h(const TunePlan& p, const float* P, float* Gd, float* ws, c
     a.XH = ws + p.xh1[l];
     a.RS = ws + p.rs1[l];
     a.lnw = Lp + G::L_N1W;
-    a.part = ws + p.part;
+    a.part = rb.take((long)lnb_parts * 2 * DP);
     if ((e = lin<DP, FF, EPI_LNB>(p, a, st)) != hipSuccess) return e;
-    if ((e = ln_grads(p, ws, lnb_parts, ws + p.part, H, Lg + G::L_N1W, Lg + G::L_N1B, st)) != hipSuccess) return e;
-    if ((e = dw<DP, DP>(p, ws, ws + p.db, DP, ws + p.o[l], DP, 0, H, H, Lg + G::L_OUT, Lg + G::L_OUTB, st)) !=
+    if ((e = ln_grads(p, rb, lnb_parts, a.part, H, Lg + G::L_N1W, Lg + G::L_N1B)) != hipSuccess) return e;
+    if ((e = dw<DP, DP>(p, rb, ws + p.db, DP, ws + p.o[l], DP, 0, H, H, Lg + G::L_OUT, Lg + G::L_OUTB, st)) !=
         hipSuccess)
       return e;
     // da = grad of the attention output
@@ -1077,7 +1152,7 @@ hipError_t tune_bwd_h(const TunePlan& p, const float* P, float* Gd, float* ws, c
     if ((e = lin<DP, DP, EPI_STORE>(p, a, st)) != hipSuccess) return e;
     TCK((attn_bwd_kernel<H><<<(int)(((long)B * H * 32 + 255) / 256), 256, 0, st>>>(B, ws + p.qkv[l], ws + p.pr[l],
                                                                                        ws + p.da, ws + p.dq)));
-    if ((e = dw<Q3P, DP>(p, ws, ws + p.dq, Q3P, ws + p.x[l], DP, 0, 3 * H, H, Lg + G::L_IN, Lg + G::L_INB, st)) !=
+    if ((e = dw<Q3P, DP>(p, rb, ws + p.dq, Q3P, ws + p.x[l], DP, 0, 3 * H, H, Lg + G::L_IN, Lg + G::L_INB, st)) !=
         hipSuccess)
       return e;
     // grad of the layer input: dQKV Win + dR1 (residual); for l = 1 through layer 0's norm2
@@ -1090,15 +1165,15 @@ hipError_t tune_bwd_h(const TunePlan& p, const float* P, float* Gd, float* ws, c
       a.XH = ws + p.xh2[0];
       a.RS = ws + p.rs2[0];
       a.lnw = L0 + G::L_N2W;
-      a.part = ws + p.part;
+      a.part = rb.take((long)lnb_parts * 2 * DP);
       if ((e = lin<DP, Q3P, EPI_LNB>(p, a, st)) != hipSuccess) return e;
-      if ((e = ln_grads(p, ws, lnb_parts, ws + p.part, H, L0g + G::L_N2W, L0g + G::L_N2B, st)) != hipSuccess) return e;
+      if ((e = ln_grads(p, rb, lnb_parts, a.part, H, L0g + G::L_N2W, L0g + G::L_N2B)) != hipSuccess) return e;
     } else {
       if ((e = lin<DP, Q3P, EPI_RES>(p, a, st)) != hipSuccess) return e;
     }
   }
   // time encoder: da = grad of X0
-  if ((e = dw<DP, DP>(p, ws, ws + p.da, DP, ws + p.g, DP, 0, H, H, Gd + G::W_TE, Gd + G::B_TE, st)) != hipSuccess)
+  if ((e = dw<DP, DP>(p, rb, ws + p.da, DP, ws + p.g, DP, 0, H, H, Gd + G::W_TE, Gd + G::B_TE, st)) != hipSuccess)
     return e;
   {
     LinArgs a = lin_args(M, ws + p.da, DP, P + G::W_TE, H, H, H, 1, nullptr, ws + p.db, DP);
@@ -1106,11 +1181,11 @@ hipError_t tune_bwd_h(const TunePlan& p, const float* P, float* Gd, float* ws, c
   }
   // GAT: db = grad of the GAT output
   TCK((gat_bwd_kernel<H><<<(3 * B + 3) / 4, 256, 0, st>>>(B, ws + p.win, P, ws + p.db, ws + p.gs, ws + p.gsx)));
-  if ((e = dw<DP, Q::XBP>(p, ws, ws + p.db, DP, ws + p.xb, Q::XBP, 0, H, 3, Gd + G::W_FC, nullptr, st)) !=
+  if ((e = dw<DP, Q::XBP>(p, rb, ws + p.db, DP, ws + p.xb, Q::XBP, 0, H, 3, Gd + G::W_FC, nullptr, st)) !=
       hipSuccess)
     return e;
   TCK((gat_param_kernel<H><<<1, 256, 0, st>>>(3 * B, ws + p.gsx, P, Gd)));
-  return hipSuccess;
+  return rb.flush(st);  // every deferred weight-gradient reduction: 2 launches
 }
 
 }  // namespace

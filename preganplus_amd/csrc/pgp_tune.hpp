@@ -38,7 +38,8 @@ struct TunePlan {
   long xh1[2] = {0, 0}, rs1[2] = {0, 0}, y1[2] = {0, 0}; // LN1 x-hat [M][DP], rstd [M], output [M][DP]
   long f[2] = {0, 0}, xh2[2] = {0, 0}, rs2[2] = {0, 0};  // FFN pre-activation [M][64], LN2 x-hat, rstd
   long da = 0, db = 0, dq = 0, df = 0;                   // backward temporaries
-  long gsx = 0, dpre = 0, wp = 0, wpt = 0, part = 0, red2 = 0, total = 0;
+  long gsx = 0, dpre = 0, wp = 0, wpt = 0, part = 0, total = 0;
+  long pool = 0, pool_len = 0;  // the backward's deferred-reduction regions (RedBatch)
   int lin_grid = 0, dw_grid = 0, dec_s = 0, dec_bg = 0, dec_dxg = 0;
 };
 
