@@ -149,23 +149,26 @@ __global__ __launch_bounds__(kGanWaves * 64) void gan_kernel(FwdArgs a) {
   }
 
   // ---- phase 3: per container row ----
-  float sv[G::MT_N][4];
-#pragma unroll
-  for (int t = 0; t < G::MT_N; ++t)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int hh = 16 * t + 4 * g + r;
-      sv[t][r] = (valid && hh < H) ? sw[hh] : 0.f;
-    }
-  for (int c = 0; c < G::C; ++c) {
-    float svn[G::MT_N][4];
+  // a lane's 4 row values 16t+4g+{0..3} as two 8-byte loads (H even: every pair is
+  // aligned and lies wholly inside or wholly past the row)
+  static_assert(H % 2 == 0, "row pairs");
+  auto load_row = [&](int c, float (&v)[G::MT_N][4]) {
 #pragma unroll
     for (int t = 0; t < G::MT_N; ++t)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
+      for (int r = 0; r < 4; r += 2) {
         const int hh = 16 * t + 4 * g + r;
-        svn[t][r] = (valid && hh < H && c + 1 < G::C) ? sw[(c + 1) * H + hh] : 0.f;
+        float2 p = make_float2(0.f, 0.f);
+        if (valid && hh < H && c < G::C) p = *reinterpret_cast<const float2*>(sw + c * H + hh);
+        v[t][r] = p.x;
+        v[t][r + 1] = p.y;
       }
+  };
+  float sv[G::MT_N][4];
+  load_row(0, sv);
+  for (int c = 0; c < G::C; ++c) {
+    float svn[G::MT_N][4];
+    load_row(c + 1, svn);
     f32x4 ns[G::MT_N];
 #pragma unroll
     for (int t = 0; t < G::MT_N; ++t) ns[t] = ld4(gt + G::G_B2 + c * G::MT_N * 16 + 16 * t + 4 * g);
