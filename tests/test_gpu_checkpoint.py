@@ -1,0 +1,54 @@
+"""Checkpoint round trip: recovery.save_checkpoints
+writes the reference's checkpoint dict (utils.py:49-58) from the device master
+weights and AdamW moments; weights.load_reference_checkpoints reads it back with
+the safe loader (torch.load weights_only=True), and torch's AdamW accepts the
+optimizer state exactly as the reference's load_model does (utils.py:60-79)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from preganplus_amd import simulate as SIM
+from preganplus_amd import train as TR
+from preganplus_amd import weights as W
+from preganplus_amd.recovery import save_checkpoints
+
+pytestmark = pytest.mark.gpu
+
+
+def test_checkpoint_round_trip(tmp_path):
+    H, B = 16, 8
+    w, _ = W.load_npz("preganplus_amd/data/simulator_16.npz")
+    tr = TR.Trainer(H, w, max_batch=B)
+    rng = np.random.Generator(np.random.PCG64(2))
+    emb = np.where(rng.uniform(size=(B, H, 1)) < 0.3, rng.uniform(size=(B, H, 2)), 0.0)
+    sched = np.zeros((B, H, H))
+    sched[np.arange(B)[:, None], np.arange(H)[None, :], rng.integers(0, H, (B, H))] = 1.0
+    TR.train_gan_batched(tr, SIM.Simulation(H), SIM.synth_envs(B, H), emb, sched)  # moments != 0
+    protos = np.asarray(w["prototypes"])
+    save_checkpoints(tr, str(tmp_path), "simulator", 7, [(0.5, 0.25)],
+                     [("transformer", f"Transformer_{H}", protos), ("gen", f"Gen_{H}", None),
+                      ("disc", f"Disc_{H}", None)])
+    for name in ("Transformer", "Gen", "Disc"):
+        assert os.path.exists(tmp_path / f"simulator_{name}_{H}.ckpt")
+    back = W.load_reference_checkpoints(str(tmp_path), "simulator", H)
+    cur = tr.weights_numpy()
+    for sec in ("transformer", "gen", "disc"):
+        for k, v in cur[sec].items():
+            assert np.array_equal(back[sec][k], v), (sec, k)
+    assert np.array_equal(back["prototypes"], protos)
+    assert back["meta"]["epoch"] == 7
+
+    # the optimizer state loads into torch.optim.AdamW over the same parameters
+    ck = torch.load(tmp_path / f"simulator_Gen_{H}.ckpt", weights_only=True)
+    names = [t["name"] for t in tr.tensors if t["section"] == "gen" and t["trainable"]]
+    params = [torch.nn.Parameter(torch.tensor(cur["gen"][n])) for n in names]
+    opt = torch.optim.AdamW(params, lr=tr.lrs["gen"], weight_decay=tr.wd)
+    opt.load_state_dict(ck["optimizer_state_dict"])
+    m = tr.m.cpu().numpy()
+    for p, t in zip(params, [t for t in tr.tensors if t["section"] == "gen" and t["trainable"]]):
+        st = opt.state[p]
+        assert float(st["step"]) == t["step"] == 1.0
+        want = m[t["offset"]:t["offset"] + t["n"]].reshape(p.shape)
+        assert np.array_equal(st["exp_avg"].numpy(), want.astype(np.float64))
