@@ -7,6 +7,14 @@
 //                                      (dgl.softmax_edges, dlutils.py:335)
 //   agg_j = sum_i a_ij x_i             (update_all src_mul_edge/sum, dlutils.py:338-342,
 //                                       taken before the linear fc)
+// The H^2 exponentials factorise: exp is monotone, so exp(lrelu(e) - M) =
+// max(exp(e - M), exp(0.01 e - M)), and each branch is a product of a source
+// factor and a destination factor:
+//   exp(s_i + t_j - M)        = A_i  * B_j,   A_i  = exp(s_i - smax),         B_j  = exp(t_j + smax - M)
+//   exp(0.01 (s_i + t_j) - M) = A'_i * B'_j,  A'_i = exp(0.01 (s_i - smax)),  B'_j = exp(0.01 (t_j + smax) - M)
+// Every factor is <= 1 (M = lrelu(smax + tmax)), so nothing overflows, and the
+// edge loop is 2 multiplies and a max instead of an add, lrelu and v_exp_f32
+// (4H exponentials per graph instead of H^2).
 // Output = the B operand of the encoder's time-encoder MFMA:
 //   agg[((blk*H + j)*3 + w)*48 + f*16 + (b & 15)]
 #include "pgp_device.hpp"
@@ -26,7 +34,8 @@ __global__ __launch_bounds__(256) void gat_agg_kernel(int B, const float* __rest
   static_assert(H <= 64, "GAT kernel maps hosts to lanes");
   constexpr int BLK = H * 3 * 48;  // floats per 16-window block
   __shared__ __attribute__((aligned(16))) float out_lds[BLK];
-  __shared__ f32x4 sx[4][64];
+  __shared__ f32x4 sx[4][64];  // {A_i, x_i}
+  __shared__ float sa[4][64];  // A'_i
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const long blk = blockIdx.x;
   for (int i = threadIdx.x; i < BLK; i += 256) out_lds[i] = 0.f;
@@ -51,14 +60,19 @@ __global__ __launch_bounds__(256) void gat_agg_kernel(int B, const float* __rest
       tmax = fmaxf(tmax, __shfl_xor(tmax, off));
     }
     const float M = lrelu001(smax + tmax);  // = max_ij e_ij (lrelu and rounding are monotone)
-    sx[wv][lane] = f32x4{s, x0, x1, x2};
+    // u,v are pre-scaled by log2(e): the factors are v_exp_f32 (2^x) of the scaled terms
+    const float ds = s - smax;
+    sx[wv][lane] = f32x4{__builtin_amdgcn_exp2f(ds), x0, x1, x2};
+    sa[wv][lane] = __builtin_amdgcn_exp2f(0.01f * ds);
+    const float Bp = __builtin_amdgcn_exp2f(t + smax - M);
+    const float Bn = __builtin_amdgcn_exp2f(0.01f * (t + smax) - M);
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes landed
     __builtin_amdgcn_wave_barrier();
     float S = 0.f, a0 = 0.f, a1 = 0.f, a2 = 0.f;
 #pragma unroll 5
     for (int i = 0; i < H; ++i) {
       const f32x4 v = sx[wv][i];
-      const float p = __builtin_amdgcn_exp2f(lrelu001(v.x + t) - M);  // u,v pre-scaled by log2(e)
+      const float p = fmaxf(v.x * Bp, sa[wv][i] * Bn);  // exp2(lrelu(s_i + t_j) - M)
       S += p;
       a0 += p * v.y;
       a1 += p * v.z;
