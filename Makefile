@@ -11,7 +11,7 @@ OBJS := $(patsubst $(CSRC)/%,$(OBJDIR)/%.o,$(SRCS))
 HDRS := include/preganplus.h $(CSRC)/pgp_layout.hpp $(CSRC)/pgp_pack.hpp $(CSRC)/pgp_device.hpp $(CSRC)/pgp_train.hpp $(CSRC)/pgp_tune.hpp $(CSRC)/pgp_gemm.hpp
 CXXFLAGS := -O3 -std=c++17 -fPIC -Wall -Wno-unused-function
 
-.PHONY: all clean resource-usage
+.PHONY: all clean resource-usage variant
 all: $(LIB)
 
 $(OBJDIR)/%.o: $(CSRC)/% $(HDRS)
@@ -21,6 +21,15 @@ $(OBJDIR)/%.o: $(CSRC)/% $(HDRS)
 $(LIB): $(OBJS)
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS)
+
+# experiment builds: make variant NAME=w8 VFLAGS=-DPGP_GAN_WAVES=8
+# -> preganplus_amd/_lib/var/libpreganplus_w8.so (select with PGP_LIB=...)
+VOBJDIR := build/var_$(NAME)
+variant:
+	@mkdir -p $(VOBJDIR) $(LIBDIR)/var
+	@for f in $(SRCS); do b=$$(basename $$f); \
+	  $(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) $(VFLAGS) -c -o $(VOBJDIR)/$$b.o $$f & done; wait
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(LIBDIR)/var/libpreganplus_$(NAME).so $(VOBJDIR)/*.o
 
 # per-kernel VGPR / spill / occupancy report
 resource-usage:

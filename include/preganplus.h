@@ -219,6 +219,19 @@ int pgp_tune_forward(int n_hosts, int batch, const float* windows, const float* 
  * into G (the caller zeroes G before the step). */
 int pgp_tune_backward(int n_hosts, int batch, const float* P, float* G, float* workspace, const float* logits,
                       const float* protos, const int* y, const float* mult, const float* tgt, void* stream);
+/* custom_loss / triplet_loss bookkeeping of ONE window (train.py:13-40,
+ * replaces the host loop between `model(...)` and `loss.backward()` in
+ * backprop, train.py:47-53), on the stream: reads the batch-1 forward's logits
+ * [H,2] / protos [H,2], labels y [H] and classes cls [H] (int32, 0-2 where
+ * y>0); updates state [2K+3] fp64 = prototypes [K][2] (model.prototype,
+ * K = n_protos >= 3; triplet_loss uses rows 0-2), PROTO_UPDATE_FACTOR,
+ * num_zero, num_ones in place in the reference's order; writes mult [H], tgt [H,2] (the inputs of
+ * pgp_tune_backward) and loss [2] fp64 = (aloss, tloss).  update_min / decay =
+ * constants.py PROTO_UPDATE_MIN / PROTO_FACTOR_DECAY.  Lets a backprop loop of
+ * sequential batch-1 steps run without a host round trip. */
+int pgp_tune_targets(int n_hosts, int n_protos, const float* logits, const float* protos, const int* y, const int* cls,
+                     double* state, double update_min, double decay, float* mult, float* tgt, double* loss,
+                     void* stream);
 /* emb [B,2H] (masked prototype embeddings), sched [B,H,H]; outputs the new
  * schedule ns [B,H,H] and probs [B,2]; workspace pgp_gan_workspace_len(H, >= B)
  * floats, shared by the three calls of one step (same batch).  The backward

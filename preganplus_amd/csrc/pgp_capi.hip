@@ -345,6 +345,18 @@ int pgp_tune_backward(int n_hosts, int batch, const float* P, float* G, float* w
   return PGP_OK;
 }
 
+int pgp_tune_targets(int n_hosts, int n_protos, const float* logits, const float* protos, const int* y, const int* cls,
+                     double* state, double update_min, double decay, float* mult, float* tgt, double* loss,
+                     void* stream) {
+  if (n_hosts <= 0 || n_hosts > 64) return fail(PGP_ERR_UNSUPPORTED, "host count");
+  if (n_protos < 3) return fail(PGP_ERR_ARG, "triplet_loss needs prototypes 0-2");
+  if (!logits || !protos || !y || !cls || !state || !mult || !tgt || !loss)
+    return fail(PGP_ERR_ARG, "bad tune_targets arguments");
+  HIPCHK(launch_tune_targets(n_hosts, n_protos, logits, protos, y, cls, state, update_min, decay, mult, tgt, loss,
+                             reinterpret_cast<hipStream_t>(stream)));
+  return PGP_OK;
+}
+
 int pgp_gan_forward(int n_hosts, int batch, const float* emb, const float* sched, const float* P, float* workspace,
                     float* ns, float* probs, void* stream) {
   long tr, go, dof, all;

@@ -17,7 +17,10 @@
 namespace pgp {
 namespace {
 
-constexpr int kGanWaves = 16;
+#ifndef PGP_GAN_WAVES
+#define PGP_GAN_WAVES 16
+#endif
+constexpr int kGanWaves = PGP_GAN_WAVES;  // waves per workgroup (16 windows each)
 constexpr int kQC = 4;  // schedule k-blocks (16 columns each) per chunk
 
 template <int H>

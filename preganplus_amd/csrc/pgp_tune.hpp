@@ -50,5 +50,8 @@ hipError_t launch_tune_forward(const TunePlan& p, const float* windows, const fl
 hipError_t launch_tune_backward(const TunePlan& p, const float* P, float* G, float* ws, const float* logits,
                                 const float* protos, const int* y, const float* mult, const float* tgt,
                                 hipStream_t st);
+hipError_t launch_tune_targets(int H, int K, const float* logits, const float* protos, const int* y, const int* cls,
+                               double* state, double update_min, double decay, float* mult, float* tgt, double* loss,
+                               hipStream_t st);
 
 }  // namespace pgp

@@ -2,11 +2,15 @@
 
 Mirrors the reference's training code (recovery/PreGANSrc/src/train.py:13-57,
 recovery/PreGANPlus.py:51-81, utils.py:65) with every tensor operation in the
-HIP library (``pgp_tune_*``, ``pgp_gan_*``, ``pgp_adamw``).  What stays on the
-host is the reference's own scalar, sequential bookkeeping — the per-host loop
-of ``custom_loss`` that decides CE weights (num_zero/num_ones) and the
-prototype EMA of ``triplet_loss`` (it depends on the forward's outputs and must
-run host-by-host in order) — exactly as the reference runs it in Python.
+HIP library (``pgp_tune_*``, ``pgp_gan_*``, ``pgp_adamw``).  The reference's
+scalar, sequential bookkeeping — the per-host loop of ``custom_loss`` that
+decides CE weights (num_zero/num_ones) and the prototype EMA of
+``triplet_loss`` (it depends on the forward's outputs and must run host-by-host
+in order) — runs on the device in the single-model ``backprop`` loop
+(``pgp_tune_targets``, fp64, the reference's operation order), so the ten
+sequential steps of one interval need no host round trip.  ``loss_targets`` is
+the same bookkeeping in numpy; the data-parallel step keeps it on the host,
+where the ranks' increments are reduced.
 """
 from __future__ import annotations
 
@@ -108,8 +112,9 @@ class Trainer:
         L.pgp_gan_gen_backward.argtypes = [i32, i32] + [vp] * 3 + [vp]
         L.pgp_adamw.argtypes = [vp] * 4 + [ctypes.c_float] * 5 + [ctypes.POINTER(_AdamTensor), i32, vp]
         L.pgp_load_weights_master.argtypes = [vp, vp, ctypes.POINTER(ctypes.c_double)]
+        L.pgp_tune_targets.argtypes = [i32, i32] + [vp] * 5 + [ctypes.c_double] * 2 + [vp] * 3 + [vp]
         for f in ("pgp_tune_forward", "pgp_tune_backward", "pgp_gan_forward", "pgp_gan_disc_backward",
-                  "pgp_gan_gen_backward", "pgp_adamw", "pgp_load_weights_master"):
+                  "pgp_gan_gen_backward", "pgp_adamw", "pgp_load_weights_master", "pgp_tune_targets"):
             getattr(L, f).restype = i32
         L._pgp_train_bound = True
 
@@ -168,6 +173,19 @@ class Trainer:
             self.H, B, self.P.data_ptr(), self.G.data_ptr(), self.ws.data_ptr(),
             self.logits.data_ptr(), self.protos.data_ptr(), y.data_ptr(), mult.data_ptr(), tgt.data_ptr(),
             self._stream()), "pgp_tune_backward")
+
+    def tune_targets(self, y, cls, state, mult, tgt, loss):
+        """custom_loss / triplet_loss bookkeeping of the preceding batch-1
+        tune_forward on the device (``pgp_tune_targets``): y, cls [H] int32,
+        state [9] fp64 (``TuneState.to_device``) updated in place; writes
+        mult [H], tgt [H,2] (fp32) and loss [2] fp64.  All device tensors."""
+        K = (state.numel() - 3) // 2
+        if self._fwd_batch != 1:
+            raise ValueError("tune_targets follows a batch-1 tune_forward (train.py:47-53)")
+        _native.check(self._L.pgp_tune_targets(
+            self.H, K, self.logits.data_ptr(), self.protos.data_ptr(), y.data_ptr(), cls.data_ptr(),
+            state.data_ptr(), PROTO_UPDATE_MIN, PROTO_FACTOR_DECAY, mult.data_ptr(), tgt.data_ptr(),
+            loss.data_ptr(), self._stream()), "pgp_tune_targets")
 
     def gan_forward(self, emb, sched):
         emb = self._dev(emb, torch.float32)
@@ -245,6 +263,19 @@ class TuneState:
         self.protos = np.array(prototypes, dtype=np.float64)
         self.factor = float(factor)
         self.num_zero, self.num_ones = 1, 1
+
+    def to_device(self, device):
+        """[2K+3] fp64 = prototypes [K][2], factor, num_zero, num_ones (the
+        layout pgp_tune_targets updates)."""
+        v = np.concatenate([self.protos.reshape(-1), [self.factor, self.num_zero, self.num_ones]])
+        return torch.tensor(v, dtype=torch.float64, device=device)
+
+    def from_device(self, t):
+        v = t.cpu().numpy()
+        K = (v.size - 3) // 2
+        self.protos = v[:2 * K].reshape(K, 2).copy()
+        self.factor = float(v[2 * K])
+        self.num_zero, self.num_ones = int(v[2 * K + 1]), int(v[2 * K + 2])
 
 
 def loss_targets(logits, protos, y, c, st: TuneState):
@@ -424,19 +455,37 @@ def on_the_fly_dataset(time_series, schedule_series, train_time_data):
 
 def backprop(tr: Trainer, st: TuneState, wins, anom, cls):
     """train.py:42-57: sequential batch-1 steps (forward, custom_loss, backward,
-    AdamW).  Returns the per-window (aloss, tloss)."""
+    AdamW).  Returns the per-window (aloss, tloss).
+
+    Every step stays on the stream: the windows, labels and classes go up once,
+    custom_loss's sequential bookkeeping runs on the device (``tune_targets``,
+    state in fp64), and the host reads back only the final state and the loss
+    values, once per call.  ``loss_targets`` is the same bookkeeping in numpy
+    (used by the data-parallel step and as the tests' restatement)."""
     st.num_zero, st.num_ones = 1, 1
-    losses = []
-    for i in range(wins.shape[0]):
-        logits, protos = tr.tune_forward(torch.as_tensor(wins[i:i + 1], dtype=torch.float32))
-        lg = logits[0].cpu().numpy()
-        pr = protos[0].cpu().numpy()
-        mult, tgt, aloss, tloss = loss_targets(lg, pr, anom[i], cls[i], st)
-        tr.tune_backward(1, anom[i][None], mult[None], tgt[None])
+    n, H, dev = wins.shape[0], tr.H, tr.device
+    if n == 0:
+        return []
+    anom = np.asarray(anom).reshape(n, H)
+    cls = np.asarray(cls).reshape(n, H)
+    bad = (anom > 0) & ((cls < 0) | (cls > 2))
+    if bad.any():
+        raise ValueError("anomalous host with a class outside 0..2 (triplet_loss, train.py:15-17)")
+    W_d = torch.as_tensor(np.asarray(wins), dtype=torch.float32).to(dev)
+    Y_d = torch.as_tensor(anom.astype(np.int32)).to(dev)
+    C_d = torch.as_tensor(cls.astype(np.int32)).to(dev)
+    state = st.to_device(dev)
+    mult = torch.empty((1, H), dtype=torch.float32, device=dev)
+    tgt = torch.empty((1, H, 2), dtype=torch.float32, device=dev)
+    losses = torch.empty((n, 2), dtype=torch.float64, device=dev)
+    for i in range(n):
+        tr.tune_forward(W_d[i:i + 1])
+        tr.tune_targets(Y_d[i], C_d[i], state, mult, tgt, losses[i])
+        tr.tune_backward(1, Y_d[i:i + 1], mult, tgt)
         inactive = () if np.any(anom[i] > 0) else ("prototype_decoder.0.weight", "prototype_decoder.0.bias")
         tr.adam_step("transformer", inactive)
-        losses.append((aloss, tloss))
-    return losses
+    st.from_device(state)
+    return [tuple(r) for r in losses.cpu().numpy().tolist()]
 
 
 def bce_target(new_score, orig_score):

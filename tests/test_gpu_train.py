@@ -250,3 +250,64 @@ def test_dp_tune_step_single_rank():
     assert torch.equal(t1.P, t2.P)
     np.testing.assert_array_equal(s1.protos, s2.protos)
     assert not np.array_equal(s1.protos, p0) and s1.num_ones > 1
+
+
+def test_backprop_device_bookkeeping_matches_reference():
+    """TR.backprop (custom_loss bookkeeping on the device, no host round trip
+    between steps) against the same reference fixture as the host-loop test."""
+    from preganplus_amd import train as TR
+    w, extra = load16()
+    z = np.load(f"{GOLD}/tune_h16.npz")
+    tr = TR.Trainer(16, w, extra)
+    st = TR.TuneState(z["protos0"], float(z["factor0"]))
+    losses = TR.backprop(tr, st, z["windows"], z["anom"], z["cls"])
+    np.testing.assert_allclose(np.array(losses), z["losses"], rtol=1e-4, atol=1e-5)
+    pw = tr.weights_numpy()["transformer"]
+    for k, v in pw.items():
+        if k != "pos_encoder.pe":
+            close_params(v, z[f"p10/{k}"], k, 10, rel=1e-4, abs_scale=2e-5, what="p10 " + k)
+    np.testing.assert_allclose(st.protos, z["protos_steps"][-1], atol=1e-5)
+    assert abs(st.factor - float(z["factor_end"])) < 1e-12
+    assert st.num_zero == z["num_zero"] and st.num_ones == z["num_ones"]
+
+
+@pytest.mark.parametrize("H", [16, 50])
+def test_tune_targets_bit_exact_vs_host_bookkeeping(H):
+    """pgp_tune_targets vs train.loss_targets (the numpy restatement of
+    train.py:13-40) over 40 consecutive windows of random forward outputs:
+    mult, tgt and the fp64 state (prototype EMA, factor, counters) bit-exact,
+    loss values to fp64 rounding.  Anchors are drawn near the class prototypes
+    so both outcomes of the EMA condition occur."""
+    from preganplus_amd import train as TR
+    rng = np.random.default_rng(7 + H)
+    w = W.synth_weights(H, seed=3) if H != 16 else load16()[0]
+    tr = TR.Trainer(H, w, None)
+    protos0 = rng.uniform(0.1, 0.9, (H, 2))  # K = n_hosts prototypes (models.py:373)
+    st_h = TR.TuneState(protos0, 0.2)
+    st_d = TR.TuneState(protos0, 0.2)
+    dev = tr.device
+    state = st_d.to_device(dev)
+    mult = torch.empty((1, H), dtype=torch.float32, device=dev)
+    tgt = torch.empty((1, H, 2), dtype=torch.float32, device=dev)
+    loss = torch.empty(2, dtype=torch.float64, device=dev)
+    ema_hits = 0
+    for it in range(40):
+        y = (rng.random(H) < 0.4).astype(np.int32)
+        c = rng.integers(0, 3, H).astype(np.int32)
+        lg = rng.normal(0, 2, (H, 2)).astype(np.float32)
+        pr = np.clip(protos0[c] + rng.normal(0, 0.15, (H, 2)), 0, 1).astype(np.float32)
+        tr.logits[0].copy_(torch.from_numpy(lg))
+        tr.protos[0].copy_(torch.from_numpy(pr))
+        tr._fwd_batch = 1
+        before = st_h.protos.copy()
+        m_h, t_h, a_h, l_h = TR.loss_targets(lg, pr, y, c, st_h)
+        ema_hits += int(np.any(before != st_h.protos))
+        tr.tune_targets(torch.from_numpy(y).to(dev), torch.from_numpy(c).to(dev), state, mult, tgt, loss)
+        np.testing.assert_array_equal(mult[0].cpu().numpy(), m_h.astype(np.float32))
+        np.testing.assert_array_equal(tgt[0].cpu().numpy(), t_h.astype(np.float32))
+        st_d.from_device(state)
+        np.testing.assert_array_equal(st_d.protos, st_h.protos)
+        assert st_d.factor == st_h.factor
+        assert (st_d.num_zero, st_d.num_ones) == (st_h.num_zero, st_h.num_ones)
+        np.testing.assert_allclose(loss.cpu().numpy(), [a_h, l_h], rtol=1e-12, atol=1e-12)
+    assert ema_hits > 5
