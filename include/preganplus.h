@@ -252,6 +252,14 @@ typedef struct {
 } pgp_adam_tensor;
 int pgp_adamw(float* P, const float* G, float* exp_avg, float* exp_avg_sq, float lr, float weight_decay,
               float beta1, float beta2, float eps, const pgp_adam_tensor* tensors, int ntensors, void* stream);
+/* pgp_adamw with the per-step scalars read from the device: sched [ntensors][3]
+ * fp32 = (active, step_size, bc2_sqrt) replaces the fields of `tensors` (only
+ * offset / n are used from it).  The kernel's arguments then do not change
+ * from step to step, so a loop of optimizer steps can be captured once in a
+ * HIP graph and replayed with a new table (backprop, train.py:42-57). */
+int pgp_adamw_table(float* P, const float* G, float* exp_avg, float* exp_avg_sq, float lr, float weight_decay,
+                    float beta1, float beta2, float eps, const pgp_adam_tensor* tensors, int ntensors,
+                    const float* sched, void* stream);
 
 /* Rebuild the inference layouts from device master weights P (natural fp32)
  * and prototypes [K,2] (host, fp64): the sync after an optimizer step. */

@@ -416,6 +416,34 @@ int pgp_adamw(float* P, const float* G, float* exp_avg, float* exp_avg_sq, float
   return PGP_OK;
 }
 
+int pgp_adamw_table(float* P, const float* G, float* exp_avg, float* exp_avg_sq, float lr, float weight_decay,
+                    float beta1, float beta2, float eps, const pgp_adam_tensor* tensors, int ntensors,
+                    const float* sched, void* stream) {
+  if (!P || !G || !exp_avg || !exp_avg_sq || !tensors || !sched || ntensors < 0 || ntensors > kMaxTensors)
+    return fail(PGP_ERR_ARG, "bad adamw arguments");
+  if (ntensors == 0) return PGP_OK;
+  AdamArgs a{};
+  a.param = P;
+  a.grad = const_cast<float*>(G);
+  a.m = exp_avg;
+  a.v = exp_avg_sq;
+  a.lr_wd = lr * weight_decay;
+  a.b1 = beta1;
+  a.b2 = beta2;
+  a.eps = eps;
+  a.ntensors = ntensors;
+  a.sched = sched;
+  for (int i = 0; i < ntensors; ++i) {
+    a.t[i].off = (long)tensors[i].offset;
+    a.t[i].n = tensors[i].n;
+    a.t[i].active = tensors[i].active;
+    a.t[i].step_size = tensors[i].step_size;
+    a.t[i].bc2_sqrt = tensors[i].bc2_sqrt;
+  }
+  HIPCHK(launch_adamw(a, reinterpret_cast<hipStream_t>(stream)));
+  return PGP_OK;
+}
+
 int pgp_load_weights_master(pgp_model* m, const float* P_device, const double* prototypes) {
   if (!m || !P_device || !prototypes) return fail(PGP_ERR_ARG, "NULL argument");
   if (m->fpe) return fail(PGP_ERR_STATE, "FPE model: master-layout reload covers the PreGAN+ model only");

@@ -13,14 +13,22 @@ namespace {
 // m = lerp(m, g, 1-b1); v = b2 v + (1-b2) g^2; p -= lr/bc1 * m / (sqrt(v)/sqrt(bc2) + eps)
 __global__ __launch_bounds__(256) void adamw_kernel(AdamArgs a) {
   const AdamTensor& t = a.t[blockIdx.y];
-  if (!t.active) return;
+  float step_size = t.step_size, bc2_sqrt = t.bc2_sqrt;
+  if (a.sched) {  // per-step scalars from the device (graph-captured loops)
+    const float* r = a.sched + 3 * blockIdx.y;
+    if (r[0] == 0.f) return;
+    step_size = r[1];
+    bc2_sqrt = r[2];
+  } else if (!t.active) {
+    return;
+  }
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < t.n; i += (long)gridDim.x * 256) {
     const long o = t.off + i;
     const float g = a.grad[o];
     float p = a.param[o] * (1.0f - a.lr_wd);
     const float m = a.m[o] + (1.0f - a.b1) * (g - a.m[o]);
     const float v = a.b2 * a.v[o] + (1.0f - a.b2) * g * g;
-    p -= t.step_size * m / (sqrtf(v) / t.bc2_sqrt + a.eps);
+    p -= step_size * m / (sqrtf(v) / bc2_sqrt + a.eps);
     a.param[o] = p;
     a.m[o] = m;
     a.v[o] = v;

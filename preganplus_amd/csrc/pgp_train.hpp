@@ -71,6 +71,7 @@ struct AdamArgs {
   float lr_wd;  // lr * weight_decay
   float b1, b2, eps;
   int ntensors;
+  const float* sched;  // optional device table [ntensors][3] = (active, step_size, bc2_sqrt), overrides t[]
   AdamTensor t[kMaxTensors];
 };
 

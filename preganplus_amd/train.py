@@ -113,8 +113,11 @@ class Trainer:
         L.pgp_adamw.argtypes = [vp] * 4 + [ctypes.c_float] * 5 + [ctypes.POINTER(_AdamTensor), i32, vp]
         L.pgp_load_weights_master.argtypes = [vp, vp, ctypes.POINTER(ctypes.c_double)]
         L.pgp_tune_targets.argtypes = [i32, i32] + [vp] * 5 + [ctypes.c_double] * 2 + [vp] * 3 + [vp]
+        L.pgp_adamw_table.argtypes = ([vp] * 4 + [ctypes.c_float] * 5 + [ctypes.POINTER(_AdamTensor), i32, vp]
+                                      + [vp])
         for f in ("pgp_tune_forward", "pgp_tune_backward", "pgp_gan_forward", "pgp_gan_disc_backward",
-                  "pgp_gan_gen_backward", "pgp_adamw", "pgp_load_weights_master", "pgp_tune_targets"):
+                  "pgp_gan_gen_backward", "pgp_adamw", "pgp_load_weights_master", "pgp_tune_targets",
+                  "pgp_adamw_table"):
             getattr(L, f).restype = i32
         L._pgp_train_bound = True
 
@@ -122,6 +125,8 @@ class Trainer:
         H, dev, L = self.H, self.device, self._L
         f32 = torch.float32
         self.cap = B
+        self.generation = getattr(self, "generation", 0) + 1  # captured graphs hold these buffers
+        self._graphs = {}
         # token-major activations of the tuning forward (kept for the backward);
         # zero-filled once: feature pads must stay 0 (pgp_tune.hpp)
         self.ws = torch.zeros((L.pgp_tune_workspace_len(H, B),), dtype=f32, device=dev)
@@ -233,6 +238,33 @@ class Trainer:
             ctypes.c_void_p(self.P.data_ptr()), ctypes.c_void_p(self.G.data_ptr()),
             ctypes.c_void_p(self.m.data_ptr()), ctypes.c_void_p(self.v.data_ptr()),
             lr, self.wd, self.b1, self.b2, self.eps, desc, len(arr), self._stream()), "pgp_adamw")
+
+    def adam_schedule(self, section: str, inactive_per_step):
+        """adam_step's host bookkeeping for a sequence of steps, done ahead:
+        returns the section's trainable tensors and a [steps, T, 3] fp32 table
+        of (active, step_size, bc2_sqrt) — the values adam_step would pass —
+        and advances the tensors' step counts as those steps would."""
+        lr = self.lrs[section]
+        sel = [t for t in self.tensors if t["section"] == section and t["trainable"]]
+        tab = np.zeros((len(inactive_per_step), len(sel), 3), dtype=np.float32)
+        for s, inactive in enumerate(inactive_per_step):
+            for k, t in enumerate(sel):
+                active = t["name"] not in inactive
+                if active:
+                    t["step"] += 1
+                st = max(t["step"], 1.0)
+                tab[s, k] = (float(active), lr / (1 - self.b1 ** st), math.sqrt(1 - self.b2 ** st))
+        return sel, tab
+
+    def adam_step_table(self, section: str, sel, sched):
+        """AdamW over `sel` with the per-step scalars in the device row `sched`
+        [T,3] (``pgp_adamw_table``): fixed kernel arguments, graph-capturable."""
+        desc = (_AdamTensor * len(sel))(*[_AdamTensor(t["offset"], t["n"], 1, 0.0, 0.0) for t in sel])
+        _native.check(self._L.pgp_adamw_table(
+            ctypes.c_void_p(self.P.data_ptr()), ctypes.c_void_p(self.G.data_ptr()),
+            ctypes.c_void_p(self.m.data_ptr()), ctypes.c_void_p(self.v.data_ptr()),
+            self.lrs[section], self.wd, self.b1, self.b2, self.eps, desc, len(sel), sched.data_ptr(),
+            self._stream()), "pgp_adamw_table")
 
     def all_reduce_grads(self, section: str, group=None):
         """Data-parallel tuning: sum the section's gradients over
@@ -453,16 +485,48 @@ def on_the_fly_dataset(time_series, schedule_series, train_time_data):
     return convert_to_windows(td), sched, anom, cls
 
 
+class _TuneGraph:
+    """One backprop() call of n sequential batch-1 steps captured as a HIP
+    graph: per step tune_forward -> tune_targets -> tune_backward (zero_grad +
+    kernels) -> AdamW from a device table.  Inputs live in fixed device buffers
+    that each call refills; a replay issues the ~20 launches per step with one
+    host call."""
+
+    def __init__(self, tr: Trainer, n: int, win_shape, K: int):
+        H, dev = tr.H, tr.device
+        self.n, self.generation = n, tr.generation
+        self.W = torch.zeros((n,) + tuple(win_shape), dtype=torch.float32, device=dev)
+        self.Y = torch.zeros((n, H), dtype=torch.int32, device=dev)
+        self.C = torch.zeros((n, H), dtype=torch.int32, device=dev)
+        self.state = torch.zeros(2 * K + 3, dtype=torch.float64, device=dev)
+        self.mult = torch.zeros((1, H), dtype=torch.float32, device=dev)
+        self.tgt = torch.zeros((1, H, 2), dtype=torch.float32, device=dev)
+        self.loss = torch.zeros((n, 2), dtype=torch.float64, device=dev)
+        self.sel = [t for t in tr.tensors if t["section"] == "transformer" and t["trainable"]]
+        self.sched = torch.zeros((n, len(self.sel), 3), dtype=torch.float32, device=dev)
+        self.graph = torch.cuda.CUDAGraph()
+        torch.cuda.synchronize(dev)
+        with torch.cuda.graph(self.graph):
+            for i in range(n):
+                tr.tune_forward(self.W[i:i + 1])
+                tr.tune_targets(self.Y[i], self.C[i], self.state, self.mult, self.tgt, self.loss[i])
+                tr.tune_backward(1, self.Y[i:i + 1], self.mult, self.tgt)
+                tr.adam_step_table("transformer", self.sel, self.sched[i])
+
+
 def backprop(tr: Trainer, st: TuneState, wins, anom, cls):
     """train.py:42-57: sequential batch-1 steps (forward, custom_loss, backward,
     AdamW).  Returns the per-window (aloss, tloss).
 
-    Every step stays on the stream: the windows, labels and classes go up once,
-    custom_loss's sequential bookkeeping runs on the device (``tune_targets``,
-    state in fp64), and the host reads back only the final state and the loss
-    values, once per call.  ``loss_targets`` is the same bookkeeping in numpy
-    (used by the data-parallel step and as the tests' restatement)."""
+    Every step stays on the device: custom_loss's sequential bookkeeping runs
+    in a kernel (``tune_targets``, state in fp64), AdamW's per-step scalars come
+    from a table computed ahead on the host (``Trainer.adam_schedule``), and the
+    n steps replay as one captured HIP graph (``_TuneGraph``, cached per n).
+    The host uploads the inputs and reads back the final state and the loss
+    values once per call.  ``loss_targets`` is the same bookkeeping in numpy
+    (the data-parallel step keeps it on the host; the tests restate with it)."""
     st.num_zero, st.num_ones = 1, 1
+    wins = np.asarray(wins)
     n, H, dev = wins.shape[0], tr.H, tr.device
     if n == 0:
         return []
@@ -471,21 +535,23 @@ def backprop(tr: Trainer, st: TuneState, wins, anom, cls):
     bad = (anom > 0) & ((cls < 0) | (cls > 2))
     if bad.any():
         raise ValueError("anomalous host with a class outside 0..2 (triplet_loss, train.py:15-17)")
-    W_d = torch.as_tensor(np.asarray(wins), dtype=torch.float32).to(dev)
-    Y_d = torch.as_tensor(anom.astype(np.int32)).to(dev)
-    C_d = torch.as_tensor(cls.astype(np.int32)).to(dev)
-    state = st.to_device(dev)
-    mult = torch.empty((1, H), dtype=torch.float32, device=dev)
-    tgt = torch.empty((1, H, 2), dtype=torch.float32, device=dev)
-    losses = torch.empty((n, 2), dtype=torch.float64, device=dev)
-    for i in range(n):
-        tr.tune_forward(W_d[i:i + 1])
-        tr.tune_targets(Y_d[i], C_d[i], state, mult, tgt, losses[i])
-        tr.tune_backward(1, Y_d[i:i + 1], mult, tgt)
-        inactive = () if np.any(anom[i] > 0) else ("prototype_decoder.0.weight", "prototype_decoder.0.bias")
-        tr.adam_step("transformer", inactive)
-    st.from_device(state)
-    return [tuple(r) for r in losses.cpu().numpy().tolist()]
+    K = st.protos.shape[0]
+    key = (n, wins.shape[1:], K)
+    g = tr._graphs.get(key)
+    if g is None or g.generation != tr.generation:
+        tr._ensure(1)
+        g = tr._graphs[key] = _TuneGraph(tr, n, wins.shape[1:], K)
+    inactive = [() if np.any(anom[i] > 0) else ("prototype_decoder.0.weight", "prototype_decoder.0.bias")
+                for i in range(n)]
+    _, tab = tr.adam_schedule("transformer", inactive)
+    g.W.copy_(torch.from_numpy(wins.astype(np.float32)))
+    g.Y.copy_(torch.from_numpy(anom.astype(np.int32)))
+    g.C.copy_(torch.from_numpy(cls.astype(np.int32)))
+    g.state.copy_(st.to_device("cpu"))
+    g.sched.copy_(torch.from_numpy(tab))
+    g.graph.replay()
+    st.from_device(g.state)
+    return [tuple(r) for r in g.loss.cpu().numpy().tolist()]
 
 
 def bce_target(new_score, orig_score):

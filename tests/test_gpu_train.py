@@ -311,3 +311,47 @@ def test_tune_targets_bit_exact_vs_host_bookkeeping(H):
         assert (st_d.num_zero, st_d.num_ones) == (st_h.num_zero, st_h.num_ones)
         np.testing.assert_allclose(loss.cpu().numpy(), [a_h, l_h], rtol=1e-12, atol=1e-12)
     assert ema_hits > 5
+
+
+def _host_loop_backprop(tr, st, wins, anom, cls):
+    """backprop as a plain host loop: numpy bookkeeping (loss_targets) and one
+    adam_step launch per step, synchronising every step."""
+    from preganplus_amd import train as TR
+    st.num_zero, st.num_ones = 1, 1
+    out = []
+    for i in range(wins.shape[0]):
+        logits, protos = tr.tune_forward(torch.as_tensor(wins[i:i + 1], dtype=torch.float32))
+        mult, tgt, aloss, tloss = TR.loss_targets(logits[0].cpu().numpy(), protos[0].cpu().numpy(),
+                                                  anom[i], cls[i], st)
+        tr.tune_backward(1, anom[i][None], mult[None], tgt[None])
+        inactive = () if np.any(anom[i] > 0) else ("prototype_decoder.0.weight", "prototype_decoder.0.bias")
+        tr.adam_step("transformer", inactive)
+        out.append((aloss, tloss))
+    return out
+
+
+def test_backprop_graph_bit_identical_to_host_loop():
+    """The graph-replayed backprop (device bookkeeping, AdamW table) produces the
+    same bits as the host loop over three consecutive calls (capture, then two
+    replays with new inputs), including a window with no anomaly (inactive
+    prototype decoder) and a shorter call (a second cached graph)."""
+    from preganplus_amd import train as TR
+    w, extra = load16()
+    z = np.load(f"{GOLD}/tune_h16.npz")
+    wins, anom, cls = z["windows"], z["anom"].copy(), z["cls"]
+    anom[3] = 0
+    a, b = TR.Trainer(16, w, extra), TR.Trainer(16, w, extra)
+    sa, sb = TR.TuneState(z["protos0"], float(z["factor0"])), TR.TuneState(z["protos0"], float(z["factor0"]))
+    rng = np.random.default_rng(0)
+    for call, n in enumerate([10, 10, 6]):
+        idx = rng.permutation(wins.shape[0])[:n] if call else np.arange(n)
+        la = _host_loop_backprop(a, sa, wins[idx], anom[idx], cls[idx])
+        lb = TR.backprop(b, sb, wins[idx], anom[idx], cls[idx])
+        np.testing.assert_array_equal(a.P.cpu().numpy(), b.P.cpu().numpy())
+        np.testing.assert_array_equal(a.m.cpu().numpy(), b.m.cpu().numpy())
+        np.testing.assert_array_equal(a.v.cpu().numpy(), b.v.cpu().numpy())
+        np.testing.assert_array_equal(sa.protos, sb.protos)
+        assert (sa.factor, sa.num_zero, sa.num_ones) == (sb.factor, sb.num_zero, sb.num_ones)
+        assert [t["step"] for t in a.tensors] == [t["step"] for t in b.tensors]
+        np.testing.assert_allclose(np.array(lb), np.array(la), rtol=1e-12, atol=1e-12)
+    assert len(b._graphs) == 2
