@@ -28,6 +28,14 @@
 #include "pgp_train.hpp"
 #include "pgp_tune.hpp"
 
+// workgroups of the token-major GEMMs / weight-gradient kernels (grid-stride loops)
+#ifndef PGP_LIN_CAP
+#define PGP_LIN_CAP 512
+#endif
+#ifndef PGP_DW_CAP
+#define PGP_DW_CAP 512
+#endif
+
 namespace pgp {
 namespace {
 
@@ -993,8 +1001,8 @@ bool plan_h(int B, TunePlan* out) {
   q.wp = take((long)Q::NOP * Q::KD);
   q.wpt = take((long)Q::NOP * Q::KD);
   const long nrb = (M + 15) / 16;
-  q.lin_grid = (int)std::min<long>(512, std::max<long>(1, (nrb + 3) / 4));
-  q.dw_grid = (int)std::min<long>(512, std::max<long>(1, (nrb + 7) / 8));
+  q.lin_grid = (int)std::min<long>(PGP_LIN_CAP, std::max<long>(1, (nrb + 3) / 4));
+  q.dw_grid = (int)std::min<long>(PGP_DW_CAP, std::max<long>(1, (nrb + 7) / 8));
   q.dec_bg = (B + 63) / 64;
   q.dec_dxg = (int)std::min<long>(4, (B + 63) / 64);
   const long kbt = Q::KD / 16;
