@@ -24,71 +24,89 @@ namespace {
 
 __device__ __forceinline__ float lrelu001(float e) { return fmaxf(e, 0.01f * e); }  // slope 0.01 < 1
 
-// One workgroup per 16-window block: 4 waves x 12 (window, step) items, lane =
-// destination host.  The block's aggregation [H][3][48] is assembled in LDS and
-// written out with contiguous 16-B stores (scattered 4-B stores amplified the
-// HBM writes 6x: profiles/r01/pmc_r01pmc2_summary.txt).
+// One workgroup per 16-window block: 4 waves over the block's 48 (window, step)
+// items, lane = destination host.  For H <= 32 a wave holds P = 64 / S items at
+// once, one per S-lane segment (S = the power of two >= H): at H = 16 a
+// one-item wave left 3/4 of its lanes idle.  Segment reductions are xor shuffles
+// below S; the per-item source tables in LDS are padded by one entry per segment
+// so the P segments' broadcast reads fall in different banks.  The block's
+// aggregation [H][3][48] is assembled in LDS and written out with contiguous
+// 16-B stores (scattered 4-B stores amplified the HBM writes 6x:
+// profiles/r01/pmc_r01pmc2_summary.txt).
+constexpr int seg_lanes(int h) { return h <= 8 ? 8 : h <= 16 ? 16 : h <= 32 ? 32 : 64; }
+
 template <int H>
 __global__ __launch_bounds__(256) void gat_agg_kernel(int B, const float* __restrict__ win,
                                                       float* __restrict__ agg, GatConst gc) {
   static_assert(H <= 64, "GAT kernel maps hosts to lanes");
+  constexpr int S = seg_lanes(H), P = 64 / S, SS = P > 1 ? S + 1 : S;
   constexpr int BLK = H * 3 * 48;  // floats per 16-window block
   __shared__ __attribute__((aligned(16))) float out_lds[BLK];
-  __shared__ f32x4 sx[4][64];  // {A_i, x_i}
-  __shared__ float sa[4][64];  // A'_i
+  __shared__ f32x4 sx[4][P * SS];  // {A_i, x_i}
+  __shared__ float sa[4][P * SS];  // A'_i
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int seg = lane / S, hl = lane % S;  // item slot, destination host
   const long blk = blockIdx.x;
   for (int i = threadIdx.x; i < BLK; i += 256) out_lds[i] = 0.f;
   __syncthreads();
-  for (int it = wv; it < 48; it += 4) {
+  for (int i0 = wv * P; i0 < 48; i0 += 4 * P) {
+    const int it = i0 + seg;
     const int j = it / 3, w = it % 3;
     const long b = blk * 16 + j;
-    const bool active = b < B;
+    const bool active = it < 48 && b < B;
+    const bool host = hl < H;
     float x0 = 0.f, x1 = 0.f, x2 = 0.f;
-    if (active && lane < H) {
-      const float* p = win + (b * 3 + w) * 3 * H + 3 * lane;
+    if (active && host) {
+      const float* p = win + (b * 3 + w) * 3 * H + 3 * hl;
       x0 = p[0];
       x1 = p[1];
       x2 = p[2];
     }
     const float s = gc.u[0] * x0 + gc.u[1] * x1 + gc.u[2] * x2;
     const float t = gc.v[0] * x0 + gc.v[1] * x1 + gc.v[2] * x2;
-    float smax = lane < H ? s : -INFINITY, tmax = lane < H ? t : -INFINITY;
+    float smax = host ? s : -INFINITY, tmax = host ? t : -INFINITY;
 #pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
+    for (int off = S / 2; off >= 1; off >>= 1) {
       smax = fmaxf(smax, __shfl_xor(smax, off));
       tmax = fmaxf(tmax, __shfl_xor(tmax, off));
     }
     const float M = lrelu001(smax + tmax);  // = max_ij e_ij (lrelu and rounding are monotone)
     // u,v are pre-scaled by log2(e): the factors are v_exp_f32 (2^x) of the scaled terms
     const float ds = s - smax;
-    sx[wv][lane] = f32x4{__builtin_amdgcn_exp2f(ds), x0, x1, x2};
-    sa[wv][lane] = __builtin_amdgcn_exp2f(0.01f * ds);
+    const int base = seg * SS;
+    sx[wv][base + hl] = f32x4{__builtin_amdgcn_exp2f(ds), x0, x1, x2};
+    sa[wv][base + hl] = __builtin_amdgcn_exp2f(0.01f * ds);
     const float Bp = __builtin_amdgcn_exp2f(t + smax - M);
     const float Bn = __builtin_amdgcn_exp2f(0.01f * (t + smax) - M);
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes landed
     __builtin_amdgcn_wave_barrier();
-    float S = 0.f, a0 = 0.f, a1 = 0.f, a2 = 0.f;
-#pragma unroll 5
-    for (int i = 0; i < H; ++i) {
-      const f32x4 v = sx[wv][i];
-      const float p = fmaxf(v.x * Bp, sa[wv][i] * Bn);  // exp2(lrelu(s_i + t_j) - M)
-      S += p;
+    float S_ = 0.f, a0 = 0.f, a1 = 0.f, a2 = 0.f;
+    auto edge = [&](int i) {
+      const f32x4 v = sx[wv][base + i];
+      const float p = fmaxf(v.x * Bp, sa[wv][base + i] * Bn);  // exp2(lrelu(s_i + t_j) - M)
+      S_ += p;
       a0 += p * v.y;
       a1 += p * v.z;
       a2 += p * v.w;
+    };
+    if constexpr (H % 5 == 0) {
+#pragma unroll 5
+      for (int i = 0; i < H; ++i) edge(i);
+    } else {
+#pragma unroll 4
+      for (int i = 0; i < H; ++i) edge(i);
     }
-    float St = lane < H ? S : 0.f;
+    float St = host ? S_ : 0.f;
 #pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) St += __shfl_xor(St, off);
-    if (active && lane < H) {
+    for (int off = S / 2; off >= 1; off >>= 1) St += __shfl_xor(St, off);
+    if (active && host) {
       const float inv = 1.0f / St;
-      float* o = out_lds + (lane * 3 + w) * 48 + j;
+      float* o = out_lds + (hl * 3 + w) * 48 + j;
       o[0] = a0 * inv;
       o[16] = a1 * inv;
       o[32] = a2 * inv;
     }
-    __builtin_amdgcn_wave_barrier();  // sx is reused by this wave's next item
+    __builtin_amdgcn_wave_barrier();  // sx is reused by this wave's next items
   }
   __syncthreads();
   f32x4* dst = reinterpret_cast<f32x4*>(agg + blk * BLK);
