@@ -16,15 +16,28 @@ namespace {
 
 constexpr int kDecWaves = 16;
 
+// CPS (host, step) chunks per ring slot: at small H one chunk is only a few
+// groups (4 KB, 16 MFMAs per wave at H = 16), so a barrier per chunk dominated;
+// chunks are grouped up to 16 groups per slot (CPS divides the chunk count;
+// the latent B registers of one slot are prefetched a slot ahead).
+template <int H>
+constexpr int dec_cps() {
+  int best = 1;
+  for (int c = 1; c * Geo<H>::DEC_G <= 16; ++c)
+    if ((H * kWindow) % c == 0) best = c;
+  return best;
+}
+
 template <int H>
 struct DecLds {
-  static constexpr int SLOT = Geo<H>::DEC_G * Geo<H>::FQ;
+  static constexpr int CPS = dec_cps<H>();
+  static constexpr int SLOT = CPS * Geo<H>::DEC_G * Geo<H>::FQ;
   static constexpr int TAB = Geo<H>::t_size(kMaxProtos);
   static constexpr int TOTAL = 2 * SLOT + TAB;
 };
 
 template <int H>
-__global__ __launch_bounds__(kDecWaves * 64) void decoder_kernel(FwdArgs a) {
+__global__ __launch_bounds__(kDecWaves * 64, H <= 16 ? 8 : 1) void decoder_kernel(FwdArgs a) {
   using G = Geo<H>;
   using L = DecLds<H>;
   __shared__ __attribute__((aligned(16))) float smem[L::TOTAL];
@@ -41,51 +54,65 @@ __global__ __launch_bounds__(kDecWaves * 64) void decoder_kernel(FwdArgs a) {
   const float* lat = a.lat + (active ? blk : 0) * G::LAT_BLK;
   constexpr int NCH = H * kWindow;
 
+  constexpr int CPS = L::CPS, SG = CPS * G::DEC_G;  // chunks, groups per slot
   float* cur = smem;
   float* nxt = smem + L::SLOT;
-  dma_groups(wdec, cur, G::DEC_G, wv, kDecWaves, lane);
-  float b[G::KS_D];
+  dma_groups(wdec, cur, SG, wv, kDecWaves, lane);
+  // latent B operands one slot (CPS chunks) ahead: at small H a single chunk is
+  // too little work to cover the HBM latency of the next one
+  float b[CPS][G::KS_D];
 #pragma unroll
-  for (int s = 0; s < G::KS_D; ++s) b[s] = active ? lat[s * 64 + lane] : 0.f;
+  for (int u = 0; u < CPS; ++u)
+#pragma unroll
+    for (int s = 0; s < G::KS_D; ++s) b[u][s] = active ? lat[(u * G::KS_D + s) * 64 + lane] : 0.f;
   __syncthreads();
-  dma_groups(wdec + (long)G::DEC_G * G::FQ, nxt, G::DEC_G, wv, kDecWaves, lane);
+  if (CPS < NCH) dma_groups(wdec + (long)SG * G::FQ, nxt, SG, wv, kDecWaves, lane);
 
   f32x4 acc[G::MT_O];
 #pragma unroll
   for (int mt = 0; mt < G::MT_O; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  for (int c = 0; c < NCH; ++c) {
-    float bn[G::KS_D];
-    const bool pre = active && (c + 1 < NCH);
+#pragma unroll 1
+  for (int c0 = 0; c0 < NCH; c0 += CPS) {
+    float bn[CPS][G::KS_D];
+    const bool pre = active && (c0 + CPS < NCH);
 #pragma unroll
-    for (int s = 0; s < G::KS_D; ++s) bn[s] = pre ? lat[((c + 1) * G::KS_D + s) * 64 + lane] : 0.f;
-    // consecutive MFMAs go to different accumulators (dependent-accumulator
-    // latency 40 cyc > 32 cyc issue): A fragments of half the output tiles at a time
-    constexpr int AMAX = G::MT_O >= 16 ? 4 : 7;          // A fragments live (VGPR budget at 4 waves/SIMD)
-    constexpr int NGRP = (G::MT_O + AMAX - 1) / AMAX;
-    constexpr int MH = (G::MT_O + NGRP - 1) / NGRP;
+    for (int u = 0; u < CPS; ++u)
 #pragma unroll
-    for (int q4 = 0; q4 < G::KQ_D; ++q4)
+      for (int s = 0; s < G::KS_D; ++s) bn[u][s] = pre ? lat[((c0 + CPS + u) * G::KS_D + s) * 64 + lane] : 0.f;
 #pragma unroll
-      for (int m0 = 0; m0 < G::MT_O; m0 += MH) {
-        f32x4 av[MH];
+    for (int sub = 0; sub < CPS; ++sub) {
+      const float* A = cur + sub * G::DEC_G * G::FQ;
+      // consecutive MFMAs go to different accumulators (dependent-accumulator
+      // latency 40 cyc > 32 cyc issue): A fragments of half the output tiles at a time
+      constexpr int AMAX = G::MT_O >= 16 ? 4 : H <= 16 ? 2 : 7;  // A fragments live (VGPR budget)
+      constexpr int NGRP = (G::MT_O + AMAX - 1) / AMAX;
+      constexpr int MH = (G::MT_O + NGRP - 1) / NGRP;
 #pragma unroll
-        for (int i = 0; i < MH; ++i)
-          if (m0 + i < G::MT_O) av[i] = ld4(cur + ((m0 + i) * G::KQ_D + q4) * 256 + lane * 4);
+      for (int q4 = 0; q4 < G::KQ_D; ++q4)
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if (4 * q4 + e < G::KS_D)
+        for (int m0 = 0; m0 < G::MT_O; m0 += MH) {
+          f32x4 av[MH];
 #pragma unroll
-            for (int i = 0; i < MH; ++i)
-              if (m0 + i < G::MT_O) acc[m0 + i] = mfma(av[i][e], b[4 * q4 + e], acc[m0 + i]);
-      }
+          for (int i = 0; i < MH; ++i)
+            if (m0 + i < G::MT_O) av[i] = ld4(A + ((m0 + i) * G::KQ_D + q4) * 256 + lane * 4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (4 * q4 + e < G::KS_D)
+#pragma unroll
+              for (int i = 0; i < MH; ++i)
+                if (m0 + i < G::MT_O) acc[m0 + i] = mfma(av[i][e], b[sub][4 * q4 + e], acc[m0 + i]);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < CPS; ++u)
+#pragma unroll
+      for (int s = 0; s < G::KS_D; ++s) b[u][s] = bn[u][s];
     __syncthreads();
     float* t = cur;
     cur = nxt;
     nxt = t;
-    if (c + 2 < NCH) dma_groups(wdec + (long)(c + 2) * G::DEC_G * G::FQ, nxt, G::DEC_G, wv, kDecWaves, lane);
-#pragma unroll
-    for (int s = 0; s < G::KS_D; ++s) b[s] = bn[s];
+    if (c0 + 2 * CPS < NCH) dma_groups(wdec + (long)(c0 + 2 * CPS) * G::DEC_G * G::FQ, nxt, SG, wv, kDecWaves, lane);
   }
 
   // ---- epilogue: bias, sigmoid, detect, embed, classify ----

@@ -17,11 +17,15 @@ namespace {
 
 constexpr int kEncWaves = 4;
 
+// RESIDENT (H <= 16): both layers' weights (24 KB at H = 16) are loaded into LDS
+// once per workgroup; the host loop then runs with no ring barriers or DMAs.
 template <int H>
 struct EncLds {
-  static constexpr int SLOT = Geo<H>::SLOT_G * Geo<H>::FQ;  // floats
+  static constexpr int STREAM = kLayers * Geo<H>::LAYER_G * Geo<H>::FQ;  // floats
+  static constexpr bool RESIDENT = STREAM * 4 <= 32 * 1024;
+  static constexpr int SLOT = Geo<H>::SLOT_G * Geo<H>::FQ;
   static constexpr int TAB = Geo<H>::t_size(kMaxProtos);
-  static constexpr int TOTAL = 2 * SLOT + TAB;
+  static constexpr int TOTAL = (RESIDENT ? STREAM : 2 * SLOT) + TAB;
 };
 
 // acc[m][w] += A[m] . B for the first NM of NMA accumulator tiles, A = NM tiles
@@ -133,9 +137,12 @@ PGP_DEV void layer_norm_tiles(f32x4 (&acc)[Geo<H>::MT_D][3], f32x4 (&X)[Geo<H>::
 }
 
 // Ring state: `cur` holds the stage being computed, `nxt` is being filled.
+// Resident mode: `nxt` is the LDS copy of the whole stream and advance() only
+// moves `cur` to the next stage.
 template <int H>
 struct Ring {
   using G = Geo<H>;
+  static constexpr bool RES = EncLds<H>::RESIDENT;
   float* cur;
   float* nxt;
   const float* enc;  // global encoder stream [layer][LAYER_G groups]
@@ -143,6 +150,7 @@ struct Ring {
   int last;          // number of stages in the launch
   int wv, lane;
   PGP_DEV void issue() {
+    if constexpr (RES) return;
     if (next < last) {
       const int si = next % (kLayers * G::NST), l = si / G::NST, k = si % G::NST;
       dma_groups(enc + (long)(l * G::LAYER_G + G::st_begin(k)) * G::FQ, nxt, G::st_end(k) - G::st_begin(k), wv,
@@ -150,6 +158,13 @@ struct Ring {
     }
   }
   PGP_DEV void advance() {
+    if constexpr (RES) {
+      const int si = next % (kLayers * G::NST), l = si / G::NST, k = si % G::NST;
+      cur = nxt + (l * G::LAYER_G + G::st_begin(k)) * G::FQ;
+      ++next;
+      __builtin_amdgcn_sched_barrier(0);  // keep stages apart (no hoisting of later stages' LDS reads)
+      return;
+    }
     __syncthreads();  // drains this wave's DMAs (vmcnt(0)) and orders all waves
     float* t = cur;
     cur = nxt;
@@ -507,7 +522,7 @@ __global__ __launch_bounds__(kEncWaves * 64, 2) void encoder_kernel(FwdArgs a) {
   using G = Geo<H>;
   using L = EncLds<H>;
   __shared__ __attribute__((aligned(16))) float smem[L::TOTAL];
-  float* tab = smem + 2 * L::SLOT;
+  float* tab = smem + (L::RESIDENT ? L::STREAM : 2 * L::SLOT);
   const int tsz = G::t_size(a.K);
   for (int i = threadIdx.x; i < tsz; i += blockDim.x) tab[i] = a.tab[i];
 
@@ -518,15 +533,23 @@ __global__ __launch_bounds__(kEncWaves * 64, 2) void encoder_kernel(FwdArgs a) {
   const bool active = blk < nblk;  // inactive waves still take part in the ring and barriers
 
   Ring<H> ring{smem, smem + L::SLOT, a.frags + G::OFF_ENC, 0, H * kLayers * G::NST, wv, lane};
-  ring.nxt = smem;  // prologue: stage 0 -> slot 0
-  ring.issue();
-  ring.nxt = smem + L::SLOT;
-  ring.next = 1;
-  __syncthreads();
-  ring.issue();  // stage 1 -> slot 1
+  if constexpr (L::RESIDENT) {
+    dma_groups(a.frags + G::OFF_ENC, smem, kLayers * G::LAYER_G, wv, kEncWaves, lane);
+    ring.nxt = smem;
+    ring.next = 1;
+    __syncthreads();
+  } else {
+    ring.nxt = smem;  // prologue: stage 0 -> slot 0
+    ring.issue();
+    ring.nxt = smem + L::SLOT;
+    ring.next = 1;
+    __syncthreads();
+    ring.issue();  // stage 1 -> slot 1
+  }
 
   const float* agg = a.agg + (active ? blk : 0) * H * 3 * 48;
   float* lat = a.lat + (active ? blk : 0) * G::LAT_BLK;
+#pragma unroll 1
   for (int h = 0; h < H; ++h) {
     float ba[3];
 #pragma unroll

@@ -27,9 +27,18 @@ template <int H>
 struct GanGeo {
   using G = Geo<H>;
   static constexpr int NQC = cdiv(G::SQ, kQC);
-  static constexpr int NCHUNK = 1 + NQC + G::C;
+  // CPC containers per ring chunk (up to 32 groups; CPC divides C): at H = 16 a
+  // container's chunk is 8 groups, 32 MFMAs per wave per barrier
+  static constexpr int cpc() {
+    int best = 1;
+    for (int c = 1; c * G::GC_G <= 32; ++c)
+      if (G::C % c == 0) best = c;
+    return best;
+  }
+  static constexpr int CPC = cpc();
+  static constexpr int NCHUNK = 1 + NQC + G::C / CPC;
   static constexpr int mx(int x, int y) { return x > y ? x : y; }
-  static constexpr int SLOT_G = mx(G::GE_G, mx(kQC * G::GS_G, G::GC_G));
+  static constexpr int SLOT_G = mx(G::GE_G, mx(kQC * G::GS_G, CPC * G::GC_G));
   static constexpr int SLOT = SLOT_G * G::FQ;
   // chunk k -> (global source, groups)
   PGP_DEV static void chunk(int k, const float* frags, const float** src, int* ng) {
@@ -41,8 +50,8 @@ struct GanGeo {
       *src = frags + G::OFF_GS + (long)q0 * G::GS_G * G::FQ;
       *ng = (G::SQ - q0 < kQC ? G::SQ - q0 : kQC) * G::GS_G;
     } else {
-      *src = frags + G::OFF_GC + (long)(k - 1 - NQC) * G::GC_G * G::FQ;
-      *ng = G::GC_G;
+      *src = frags + G::OFF_GC + (long)(k - 1 - NQC) * CPC * G::GC_G * G::FQ;
+      *ng = CPC * G::GC_G;
     }
   }
 };
@@ -170,6 +179,7 @@ __global__ __launch_bounds__(kGanWaves * 64) void gan_kernel(FwdArgs a) {
   float sv[G::MT_N][4];
   load_row(0, sv);
   for (int c = 0; c < G::C; ++c) {
+    const float* cw = cur + (c % GG::CPC) * G::GC_G * G::FQ;  // this container's groups
     float svn[G::MT_N][4];
     load_row(c + 1, svn);
     f32x4 ns[G::MT_N];
@@ -182,7 +192,7 @@ __global__ __launch_bounds__(kGanWaves * 64) void gan_kernel(FwdArgs a) {
         f32x4 w[2];
 #pragma unroll
         for (int i = 0; i < 2; ++i)
-          if (t0 + i < G::MT_N) w[i] = ld4(cur + ((t0 + i) * 4 + q4) * 256 + lane * 4);
+          if (t0 + i < G::MT_N) w[i] = ld4(cw + ((t0 + i) * 4 + q4) * 256 + lane * 4);
 #pragma unroll
         for (int e = 0; e < 4; ++e)
 #pragma unroll
@@ -218,7 +228,7 @@ __global__ __launch_bounds__(kGanWaves * 64) void gan_kernel(FwdArgs a) {
       for (int m0 = 0; m0 < G::MT_G; m0 += 2) {
         f32x4 w[2];
 #pragma unroll
-        for (int i = 0; i < 2; ++i) w[i] = ld4(cur + (G::GC_G2 + (m0 + i) * G::MT_N + q4) * 256 + lane * 4);
+        for (int i = 0; i < 2; ++i) w[i] = ld4(cw + (G::GC_G2 + (m0 + i) * G::MT_N + q4) * 256 + lane * 4);
 #pragma unroll
         for (int e = 0; e < 4; ++e)
 #pragma unroll
@@ -241,7 +251,7 @@ __global__ __launch_bounds__(kGanWaves * 64) void gan_kernel(FwdArgs a) {
       a.gen_t[b * G::C + c] = bn_i;
       a.final_t[b * G::C + c] = bs_i;
     }
-    advance();
+    if ((c + 1) % GG::CPC == 0) advance();
 #pragma unroll
     for (int t = 0; t < G::MT_N; ++t)
 #pragma unroll
