@@ -139,3 +139,53 @@ def test_large_batch_properties_h50():
     sub = {k: v[idx] for k, v in full.items()}
     assert_parity(sub, ref, w["prototypes"], check_latent=False)
     assert np.array_equal(full["final_target"], O.first_argmax_rows(s.astype(np.float32)))
+
+
+def _c2_torch(n, H, seed, device="cuda"):
+    """The C2 input distribution generated on the device (full sizes would take
+    minutes to build and copy from numpy)."""
+    g = torch.Generator(device=device).manual_seed(seed)
+    x = torch.rand((n, 3, 3 * H), generator=g, device=device) * 0.6
+    spike = torch.rand(x.shape, generator=g, device=device) < 0.02
+    x = torch.where(spike, 0.9 + 0.4 * torch.rand(x.shape, generator=g, device=device), x)
+    s = torch.zeros((n, H, H), device=device)
+    s.scatter_(2, torch.randint(0, H, (n, H, 1), generator=g, device=device), 1.0)
+    return x.contiguous(), s
+
+
+@pytest.mark.parametrize("H,B", [(50, 65536), (16, 262144)])
+def test_full_size_properties(H, B):
+    """BASELINE sizes: C2 (H=50, 65,536 windows) and one C5 launch (H=16, 262,144
+    cell-windows).  Size-independent checks: windows at the start, middle and
+    ragged tail give bitwise the same results when run alone; final targets are
+    the schedule rows' first argmax; the detect / gate / probability outputs are
+    consistent with the logits and probabilities; a random sample matches the
+    fp64 oracle."""
+    from preganplus_amd.model import to_numpy
+    if H == 16:
+        w, _ = W.load_npz("preganplus_amd/data/simulator_16.npz")
+    else:
+        w = W.synth_weights(H, seed=0)
+    m = get_model(H, w, f"full{H}")
+    x, s = _c2_torch(B, H, seed=31 + H)
+    full = to_numpy(m.forward(x, s))
+    torch.cuda.synchronize()
+    for lo, hi in ((0, 64), (B // 2 - 7, B // 2 + 50), (B - 45, B)):
+        part = to_numpy(m.forward(x[lo:hi].contiguous(), s[lo:hi].contiguous()))
+        torch.cuda.synchronize()
+        for k in part:
+            assert np.array_equal(full[k][lo:hi], part[k]), (k, lo, hi)
+    assert np.isfinite(full["logits"]).all() and np.isfinite(full["probs"]).all()
+    np.testing.assert_allclose(full["probs"].sum(axis=1), 1.0, rtol=0, atol=2e-6)
+    assert np.array_equal(full["keep"], full["probs"][:, 0] > full["probs"][:, 1])
+    anom = full["logits"][..., 1] > full["logits"][..., 0]
+    assert np.array_equal(full["any"], anom.any(axis=1))
+    assert np.array_equal(full["cls"] < 0, ~anom)  # a class exactly where a host is flagged
+    s_np = s.cpu().numpy()
+    assert np.array_equal(full["final_target"], O.first_argmax_rows(s_np))
+    rng = np.random.Generator(np.random.PCG64(H))
+    idx = np.sort(rng.choice(B, size=64, replace=False))
+    xs = x[torch.as_tensor(idx, device=x.device)].cpu().numpy().astype(np.float64)
+    ref = O.forward(w, xs, s_np[idx].astype(np.float64))
+    ref["sched32"] = s_np[idx]
+    assert_parity({k: v[idx] for k, v in full.items()}, ref, w["prototypes"], check_latent=False)
