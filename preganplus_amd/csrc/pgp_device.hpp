@@ -104,6 +104,47 @@ PGP_DEV float xsum(float v, bool both) {
   return v;
 }
 
+// Paired / transposed forms of xsum.  v_permlane16_swap(d, s) exchanges the
+// odd 16-lane rows of d with the even rows of s; v_permlane32_swap(d, s) the
+// upper half of d with the lower half of s.  Two different values in one swap
+// reduce both at once; every sum keeps xsum's association
+// (v0 + v1) + (v2 + v3) over lane groups, so results are bitwise equal to xsum.
+PGP_DEV float pl_sum16(float a, float b) {  // rows [a0+a1, b0+b1, a2+a3, b2+b3]
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+PGP_DEV float pl_sum32(float a, float b) {  // rows [a0+a2, a1+a3, b0+b2, b1+b3]
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+// a, b <- xsum(a, true), xsum(b, true): 3 swaps + 2 adds instead of 4 + 4
+PGP_DEV void xsum2(float& a, float& b) {
+  const float s = pl_sum16(a, b);                       // [a01, b01, a23, b23]
+  const unsigned su = __float_as_uint(s);
+  const auto q = __builtin_amdgcn_permlane32_swap(su, su, false, false);
+  const float t = __uint_as_float(q[0]) + __uint_as_float(q[1]);  // [a, b, a, b]
+  const unsigned tu = __float_as_uint(t);
+  const auto p = __builtin_amdgcn_permlane16_swap(tu, tu, false, false);
+  a = __uint_as_float(p[0]);
+  b = __uint_as_float(p[1]);
+}
+// a, b <- xsum(a, false), xsum(b, false) (sums within lane-group pairs {0,1}, {2,3})
+PGP_DEV void xsum2_half(float& a, float& b) {
+  const unsigned su = __float_as_uint(pl_sum16(a, b));  // [a01, b01, a23, b23]
+  const auto p = __builtin_amdgcn_permlane16_swap(su, su, false, false);
+  a = __uint_as_float(p[0]);
+  b = __uint_as_float(p[1]);
+}
+// Transposed reduction of up to 4 values: lane group n gets xsum(v[n], true),
+// groups n >= NR get 0 (the per-group row pick of the VALU-row GEMVs).
+template <int NR>
+PGP_DEV float xsum_rows(const float (&v)[NR]) {
+  static_assert(NR >= 1 && NR <= 4, "at most 4 rows");
+  const float s01 = pl_sum16(v[0], NR > 1 ? v[1] : 0.f);
+  const float s23 = NR > 2 ? pl_sum16(v[2], NR > 3 ? v[3] : 0.f) : 0.f;
+  return pl_sum32(s01, s23);
+}
+
 // Async copy of `ngroups` 1-KiB fragment groups global -> LDS, spread over the
 // workgroup's waves (group g by wave g % nwaves).  LDS destination is the
 // wave-uniform base + lane*16 (global_load_lds_dwordx4), so a group's 64

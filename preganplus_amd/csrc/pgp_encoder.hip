@@ -28,6 +28,19 @@ struct EncLds {
   static constexpr int TOTAL = (RESIDENT ? STREAM : 2 * SLOT) + TAB;
 };
 
+// ReLU as one integer max on the bit pattern (negative floats have negative
+// int patterns): fmaxf on an MFMA result costs a NaN-canonicalising v_max first,
+// so 2 VALU ops per element; this is 1 (-0.0 -> +0.0, the same value).  H = 32
+// keeps fmaxf: there the integer form scheduled into 16 more VGPRs (one wave
+// of occupancy).
+template <int H>
+PGP_DEV float relu_enc(float x) {
+  if constexpr (Geo<H>::P8 || Geo<H>::TAIL)
+    return __int_as_float(max(__float_as_int(x), 0));
+  else
+    return fmaxf(x, 0.f);
+}
+
 // acc[m][w] += A[m] . B for the first NM of NMA accumulator tiles, A = NM tiles
 // x KQ groups in LDS, B k-step s = Bx[s/4][w][s%4]
 template <int NM, int KQ, int KS, int NB, int NMA = NM>
@@ -80,12 +93,24 @@ PGP_DEV void gemm3_rows(f32x4 (&acc)[NMA][3], const float* A, const f32x4 (&Bx)[
     }
 }
 
+// cross-group sums of all NR x 3 row partials (broadcast), two at a time
 template <int NR>
 PGP_DEV void rows_finish(float (&r)[NR][3]) {
+  float* f = &r[0][0];
 #pragma unroll
-  for (int n = 0; n < NR; ++n)
+  for (int i = 0; i + 1 < 3 * NR; i += 2) xsum2(f[i], f[i + 1]);
+  if constexpr ((3 * NR) % 2) f[3 * NR - 1] = xsum(f[3 * NR - 1], true);
+}
+
+// per-group row sums: lane group n gets the sum of row n for step w (0 in
+// groups >= NR): the B-operand slot of d-rows 16*MT_X + n (X tile MT_X,
+// register 0) in one transposed reduction
+template <int NR>
+PGP_DEV float rows_pick(const float (&r)[NR][3], int w) {
+  float v[NR];
 #pragma unroll
-    for (int w = 0; w < 3; ++w) r[n][w] = xsum(r[n][w], true);
+  for (int n = 0; n < NR; ++n) v[n] = r[n][w];
+  return xsum_rows<NR>(v);
 }
 
 template <int NR>
@@ -96,42 +121,42 @@ PGP_DEV void zero_rows(float (&r)[NR][3]) {
     for (int w = 0; w < 3; ++w) r[n][w] = 0.f;
 }
 
-// value of VALU row n = g in lane group g (0 elsewhere): the B-operand slot of
-// d-rows 16*MT_X + g (X tile MT_X, register 0)
-template <int NR>
-PGP_DEV float pick_row(const float (&v)[NR][3], int w, int g) {
-  float r = 0.f;
-#pragma unroll
-  for (int n = 0; n < NR; ++n) r = g == n ? v[n][w] : r;
-  return r;
-}
-
 template <int H>
 PGP_DEV void layer_norm_tiles(f32x4 (&acc)[Geo<H>::MT_D][3], f32x4 (&X)[Geo<H>::MT_D][3], const float* gam,
                               const float* bet, int g) {
   using G = Geo<H>;
   constexpr float invH = 1.0f / (float)H;
+  // the three steps' statistics are reduced across lane groups in pairs (xsum2)
+  float sum[3], mean[3], var[3];
 #pragma unroll
   for (int w = 0; w < 3; ++w) {
-    float sum = 0.f;
+    sum[w] = 0.f;
 #pragma unroll
-    for (int mt = 0; mt < G::MT_D; ++mt) sum += (acc[mt][w][0] + acc[mt][w][1]) + (acc[mt][w][2] + acc[mt][w][3]);
-    sum = xsum(sum, true);
-    const float mean = sum * invH;
-    float var = 0.f;
+    for (int mt = 0; mt < G::MT_D; ++mt) sum[w] += (acc[mt][w][0] + acc[mt][w][1]) + (acc[mt][w][2] + acc[mt][w][3]);
+  }
+  xsum2(sum[0], sum[1]);
+  sum[2] = xsum(sum[2], true);
+#pragma unroll
+  for (int w = 0; w < 3; ++w) {
+    mean[w] = sum[w] * invH;
+    var[w] = 0.f;
 #pragma unroll
     for (int mt = 0; mt < G::MT_D; ++mt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float dv = (16 * mt + 4 * r + g < H) ? acc[mt][w][r] - mean : 0.f;
-        var += dv * dv;
+        const float dv = (16 * mt + 4 * r + g < H) ? acc[mt][w][r] - mean[w] : 0.f;
+        var[w] += dv * dv;
       }
-    var = xsum(var, true);
-    const float rstd = __builtin_amdgcn_rsqf(var * invH + 1e-5f);  // v_rsq_f32 (1 ulp)
+  }
+  xsum2(var[0], var[1]);
+  var[2] = xsum(var[2], true);
+#pragma unroll
+  for (int w = 0; w < 3; ++w) {
+    const float rstd = __builtin_amdgcn_rsqf(var[w] * invH + 1e-5f);  // v_rsq_f32 (1 ulp)
 #pragma unroll
     for (int mt = 0; mt < G::MT_D; ++mt) {
       const f32x4 ga = ld4(gam + 16 * mt + 4 * g), be = ld4(bet + 16 * mt + 4 * g);
-      X[mt][w] = (acc[mt][w] - mean) * rstd * ga + be;
+      X[mt][w] = (acc[mt][w] - mean[w]) * rstd * ga + be;
     }
   }
 }
@@ -179,18 +204,30 @@ template <int H>
 PGP_DEV void attention(const f32x4 (&QKV)[3 * Geo<H>::TP][3], f32x4 (&O)[Geo<H>::TP][3]) {
   using G = Geo<H>;
   float pr[3][3];
+  // P8: lane groups {0,1} = head 0, {2,3} = head 1 (half sums), reduced in
+  // pairs; otherwise one at a time (pairs cost H = 32 a wave of occupancy)
+  float sc9[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    const int w = i / 3, w2 = i % 3;
+    float part = 0.f;
+#pragma unroll
+    for (int tp = 0; tp < G::TP; ++tp)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) part += QKV[tp][w][r] * QKV[G::TP + tp][w2][r];
+    if constexpr (G::P8)
+      sc9[i] = part;
+    else
+      sc9[i] = xsum(part, true);
+  }
+  if constexpr (G::P8) {
+#pragma unroll
+    for (int i = 0; i < 8; i += 2) xsum2_half(sc9[i], sc9[i + 1]);
+    sc9[8] = xsum(sc9[8], false);
+  }
 #pragma unroll
   for (int w = 0; w < 3; ++w) {
-    float sc[3];
-#pragma unroll
-    for (int w2 = 0; w2 < 3; ++w2) {
-      float part = 0.f;
-#pragma unroll
-      for (int tp = 0; tp < G::TP; ++tp)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) part += QKV[tp][w][r] * QKV[G::TP + tp][w2][r];
-      sc[w2] = xsum(part, !G::P8);  // P8: lane groups {0,1} = head 0, {2,3} = head 1
-    }
+    const float* sc = sc9 + 3 * w;
     const float m = fmaxf(sc[0], fmaxf(sc[1], sc[2]));
     const float e0 = __expf(sc[0] - m), e1 = __expf(sc[1] - m), e2 = __expf(sc[2] - m);  // v_exp_f32
     const float inv = __builtin_amdgcn_rcpf(e0 + e1 + e2);
@@ -234,12 +271,13 @@ PGP_DEV void qkv_fold(f32x4 (&acc)[NM][3], int T0, int n, const float* tab, cons
         acc[m][w] = mfma(a, ba[w], ld4(tab + G::T_F0B + (w * 3 * G::NQT + T0 + m) * 16 + 4 * g));
     }
 }
-// tail-mode VALU rows of layer 0 (q/k/v m, head-1 tail row n), without bias
+// tail-mode VALU rows of layer 0 (q/k/v m, head-1 tail row n), without bias:
+// this lane group's term (the caller sums over groups)
 template <int H>
-PGP_DEV float row_fold(int m, int n, int w, const float* tab, const float (&ba)[3], int g) {
+PGP_DEV float row_fold_part(int m, int n, int w, const float* tab, const float (&ba)[3], int g) {
   using G = Geo<H>;
-  const float wg = g < 3 ? tab[G::T_F0R + (m * G::SR + n) * 4 + g] : 0.f;
-  return xsum(wg * ba[w], true);
+  const float t = tab[G::T_F0R + (m * G::SR + n) * 4 + g];  // slot 3 exists ([.][4] rows)
+  return (g < 3 ? t : 0.f) * ba[w];
 }
 template <int H>
 PGP_DEV float row_fold_bias(int m, int n, int w, const float* tab) {
@@ -265,8 +303,10 @@ PGP_DEV void encoder_layer_tail(f32x4 (&X)[Geo<H>::MT_D][3], Ring<H>& ring, cons
     for (int n = 0; n < SR; ++n)
 #pragma unroll
       for (int w = 0; w < 3; ++w) {
-        qr[n][w] = row_fold<H>(0, n, w, tab, ba, g) + row_fold_bias<H>(0, n, w, tab);
-        kr[n][w] = row_fold<H>(1, n, w, tab, ba, g) + row_fold_bias<H>(1, n, w, tab);
+        float q = row_fold_part<H>(0, n, w, tab, ba, g), k = row_fold_part<H>(1, n, w, tab, ba, g);
+        xsum2(q, k);
+        qr[n][w] = q + row_fold_bias<H>(0, n, w, tab);
+        kr[n][w] = k + row_fold_bias<H>(1, n, w, tab);
       }
   } else {
 #pragma unroll
@@ -311,8 +351,9 @@ PGP_DEV void encoder_layer_tail(f32x4 (&X)[Geo<H>::MT_D][3], Ring<H>& ring, cons
         else
           a1 += pr;
       }
-      s0[w2] = xsum(a0, true);
-      float t1 = xsum(a1, true);
+      xsum2(a0, a1);
+      s0[w2] = a0;
+      float t1 = a1;
 #pragma unroll
       for (int n = 0; n < SR; ++n) t1 = fmaf(qr[n][w], kr[n][w2], t1);
       s1[w2] = t1;
@@ -357,13 +398,9 @@ PGP_DEV void encoder_layer_tail(f32x4 (&X)[Geo<H>::MT_D][3], Ring<H>& ring, cons
 #pragma unroll
       for (int n = 0; n < G::XR; ++n) {
         const float* rw = tab + G::T_F0OR + n * 16;
-        const float part = g < 3 ? rw[g] * y0 + rw[4 + g] * p0 + rw[8 + g] * y1 + rw[12 + g] * p1 : 0.f;
-        ro[n] = xsum(part, true);
+        ro[n] = g < 3 ? rw[g] * y0 + rw[4 + g] * p0 + rw[8 + g] * y1 + rw[12 + g] * p1 : 0.f;
       }
-      float rsel = 0.f;
-#pragma unroll
-      for (int n = 0; n < G::XR; ++n) rsel = g == n ? ro[n] : rsel;
-      acc[G::MT_X][w][0] += rsel;
+      acc[G::MT_X][w][0] += xsum_rows<G::XR>(ro);  // row n's sum in lane group n
     }
     layer_norm_tiles<H>(acc, X, TL + G::TL_LN1G, TL + G::TL_LN1B, g);
   } else {
@@ -379,11 +416,14 @@ PGP_DEV void encoder_layer_tail(f32x4 (&X)[Geo<H>::MT_D][3], Ring<H>& ring, cons
   zero_rows(vr);
   gemm3_rows<TQ, G::KQ_D, G::KS_D, G::MT_D, TQ, SR>(V, ring.cur, X, lane, vr, TL + G::TL_RQ + 2 * SR * G::KQ_D * 16,
                                                          g);
-  rows_finish(vr);
+  // v row n (+ its bias) in lane group n, 0 in groups >= SR (the bias table is
+  // padded to 8 entries, so slot 2*SR + g is in bounds)
+  float vd[3];
+  {
+    const float vb = TL[G::TL_RQB + 2 * SR + g];
 #pragma unroll
-  for (int n = 0; n < SR; ++n)
-#pragma unroll
-    for (int w = 0; w < 3; ++w) vr[n][w] += TL[G::TL_RQB + 2 * SR + n];
+    for (int w = 0; w < 3; ++w) vd[w] = rows_pick<SR>(vr, w) + (g < SR ? vb : 0.f);
+  }
   f32x4 O[TQ + 1][3];
 #pragma unroll
   for (int w = 0; w < 3; ++w) {
@@ -398,12 +438,7 @@ PGP_DEV void encoder_layer_tail(f32x4 (&X)[Geo<H>::MT_D][3], Ring<H>& ring, cons
       const float c0 = h0 ? P0[w][0] : P1[w][0], c1 = h0 ? P0[w][1] : P1[w][1], c2 = h0 ? P0[w][2] : P1[w][2];
       O[2 * HF][w][r] = c0 * V[2 * HF][0][r] + c1 * V[2 * HF][1][r] + c2 * V[2 * HF][2][r];
     }
-    float orr[SR][1];
-#pragma unroll
-    for (int n = 0; n < SR; ++n) orr[n][0] = P1[w][0] * vr[n][0] + P1[w][1] * vr[n][1] + P1[w][2] * vr[n][2];
-    float o3 = 0.f;
-#pragma unroll
-    for (int n = 0; n < SR; ++n) o3 = g == n ? orr[n][0] : o3;
+    const float o3 = P1[w][0] * vd[0] + P1[w][1] * vd[1] + P1[w][2] * vd[2];  // 0 in groups >= SR
     O[TQ][w] = f32x4{o3, 0.f, 0.f, 0.f};
   }
   {
@@ -411,9 +446,8 @@ PGP_DEV void encoder_layer_tail(f32x4 (&X)[Geo<H>::MT_D][3], Ring<H>& ring, cons
     zero_rows(ro);
     gemm3_rows<G::MT_X, G::KQ_OT, G::KS_OT, TQ + 1, G::MT_D, G::XR>(acc, ring.cur + G::G_V * G::FQ, O, lane, ro,
                                                                    TL + G::TL_RO, g);
-    rows_finish(ro);
 #pragma unroll
-    for (int w = 0; w < 3; ++w) acc[G::MT_X][w][0] += pick_row<G::XR>(ro, w, g);
+    for (int w = 0; w < 3; ++w) acc[G::MT_X][w][0] += rows_pick<G::XR>(ro, w);
   }
   layer_norm_tiles<H>(acc, X, TL + G::TL_LN1G, TL + G::TL_LN1B, g);
   }  // F0
@@ -432,7 +466,7 @@ PGP_DEV void encoder_layer_tail(f32x4 (&X)[Geo<H>::MT_D][3], Ring<H>& ring, cons
 #pragma unroll
     for (int w = 0; w < 3; ++w)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) F1[mt][w][r] = fmaxf(F1[mt][w][r], 0.f);
+      for (int r = 0; r < 4; ++r) F1[mt][w][r] = relu_enc<H>(F1[mt][w][r]);
 #pragma unroll
   for (int mt = 0; mt < G::MT_D; ++mt) {
     const f32x4 b2 = ld4(TL + G::TL_B2 + 16 * mt + 4 * g);
@@ -444,9 +478,8 @@ PGP_DEV void encoder_layer_tail(f32x4 (&X)[Geo<H>::MT_D][3], Ring<H>& ring, cons
     zero_rows(rf);
     gemm3_rows<G::MT_X, G::KQ_F, 16, G::MT_F, G::MT_D, G::XR>(acc, ring.cur + G::G_F1 * G::FQ, F1, lane, rf,
                                                              TL + G::TL_RF, g);
-    rows_finish(rf);
 #pragma unroll
-    for (int w = 0; w < 3; ++w) acc[G::MT_X][w][0] += pick_row<G::XR>(rf, w, g);
+    for (int w = 0; w < 3; ++w) acc[G::MT_X][w][0] += rows_pick<G::XR>(rf, w);
   }
   ring.advance();
   layer_norm_tiles<H>(acc, X, TL + G::TL_LN2G, TL + G::TL_LN2B, g);
@@ -503,7 +536,7 @@ PGP_DEV void encoder_layer(f32x4 (&X)[Geo<H>::MT_D][3], Ring<H>& ring, const flo
 #pragma unroll
     for (int w = 0; w < 3; ++w)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) F1[mt][w][r] = fmaxf(F1[mt][w][r], 0.f);
+      for (int r = 0; r < 4; ++r) F1[mt][w][r] = relu_enc<H>(F1[mt][w][r]);
   ring.advance();
   // [S3] W2 . h + b2 + x, norm2
 #pragma unroll
