@@ -41,11 +41,25 @@ PGP_DEV float relu_enc(float x) {
     return fmaxf(x, 0.f);
 }
 
+// MFMA phases run at wave priority 1, VALU phases (softmax, LayerNorm) at 0: the
+// co-resident wave of the other workgroup on the SIMD then gets its MFMA issue
+// slots ahead of a VALU stream (PGP_ENC_PRIO=0 disables)
+#ifndef PGP_ENC_PRIO
+#define PGP_ENC_PRIO 1
+#endif
+PGP_DEV void prio_mfma() {
+  if (PGP_ENC_PRIO) __builtin_amdgcn_s_setprio(1);
+}
+PGP_DEV void prio_valu() {
+  if (PGP_ENC_PRIO) __builtin_amdgcn_s_setprio(0);
+}
+
 // acc[m][w] += A[m] . B for the first NM of NMA accumulator tiles, A = NM tiles
 // x KQ groups in LDS, B k-step s = Bx[s/4][w][s%4]
 template <int NM, int KQ, int KS, int NB, int NMA = NM>
 PGP_DEV void gemm3(f32x4 (&acc)[NMA][3], const float* A, const f32x4 (&Bx)[NB][3], int lane) {
   static_assert(NM <= NMA, "accumulator tiles");
+  prio_mfma();
 #pragma unroll
   for (int m = 0; m < NM; ++m)
 #pragma unroll
@@ -58,6 +72,7 @@ PGP_DEV void gemm3(f32x4 (&acc)[NMA][3], const float* A, const f32x4 (&Bx)[NB][3
           for (int w = 0; w < 3; ++w) acc[m][w] = mfma(a[e], Bx[q4][w][e], acc[m][w]);
         }
     }
+  prio_valu();
 }
 
 // gemm3 with NR VALU rows folded into the first tile's pass: the rows' FMAs
@@ -68,6 +83,7 @@ template <int NM, int KQ, int KS, int NB, int NMA, int NR>
 PGP_DEV void gemm3_rows(f32x4 (&acc)[NMA][3], const float* A, const f32x4 (&Bx)[NB][3], int lane,
                         float (&racc)[NR][3], const float* RW, int g) {
   static_assert(NM <= NMA, "accumulator tiles");
+  prio_mfma();
 #pragma unroll
   for (int m = 0; m < NM; ++m)
 #pragma unroll
@@ -91,6 +107,7 @@ PGP_DEV void gemm3_rows(f32x4 (&acc)[NMA][3], const float* A, const f32x4 (&Bx)[
           }
         }
     }
+  prio_valu();
 }
 
 // cross-group sums of all NR x 3 row partials (broadcast), two at a time
