@@ -22,6 +22,14 @@ namespace {
 #endif
 constexpr int kGanWaves = PGP_GAN_WAVES;  // waves per workgroup (16 windows each)
 constexpr int kQC = 4;  // schedule k-blocks (16 columns each) per chunk
+// per-container MFMA loops at wave priority 1, the tanh / argmax VALU at 0
+#ifndef PGP_GAN_PRIO
+#define PGP_GAN_PRIO 1
+#endif
+template <int P>
+__device__ __forceinline__ void gan_prio() {
+  if (PGP_GAN_PRIO) __builtin_amdgcn_s_setprio(P);
+}
 
 template <int H>
 struct GanGeo {
@@ -185,6 +193,7 @@ __global__ __launch_bounds__(kGanWaves * 64) void gan_kernel(FwdArgs a) {
     f32x4 ns[G::MT_N];
 #pragma unroll
     for (int t = 0; t < G::MT_N; ++t) ns[t] = ld4(gt + G::G_B2 + c * G::MT_N * 16 + 16 * t + 4 * g);
+    gan_prio<1>();
 #pragma unroll
     for (int q4 = 0; q4 < 4; ++q4)
 #pragma unroll
@@ -199,6 +208,7 @@ __global__ __launch_bounds__(kGanWaves * 64) void gan_kernel(FwdArgs a) {
           for (int i = 0; i < 2; ++i)
             if (t0 + i < G::MT_N) ns[t0 + i] = mfma(w[i][e], hg[q4][e], ns[t0 + i]);
       }
+    gan_prio<0>();
     float bn_v = -INFINITY, bs_v = -INFINITY;
     int bn_i = 0, bs_i = 0;
 #pragma unroll
@@ -222,6 +232,7 @@ __global__ __launch_bounds__(kGanWaves * 64) void gan_kernel(FwdArgs a) {
           ns[t][r] = 0.f;
         }
       }
+    gan_prio<1>();
 #pragma unroll
     for (int q4 = 0; q4 < G::MT_N; ++q4)
 #pragma unroll
@@ -234,6 +245,7 @@ __global__ __launch_bounds__(kGanWaves * 64) void gan_kernel(FwdArgs a) {
 #pragma unroll
           for (int i = 0; i < 2; ++i) hd[m0 + i] = mfma(w[i][e], ns[q4][e], hd[m0 + i]);
       }
+    gan_prio<0>();
 #pragma unroll
     for (int off = 16; off <= 32; off <<= 1) {
       const float ov = __shfl_xor(bn_v, off), os = __shfl_xor(bs_v, off);
