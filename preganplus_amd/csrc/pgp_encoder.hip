@@ -16,6 +16,16 @@ namespace pgp {
 namespace {
 
 constexpr int kEncWaves = 4;
+// H <= 16 (weights LDS-resident): ENC16_WAVES waves per workgroup share one LDS
+// copy, and ENC16_EU waves per SIMD are requested from the register allocator
+#ifndef PGP_ENC16_WAVES
+#define PGP_ENC16_WAVES 4
+#endif
+#ifndef PGP_ENC16_EU
+#define PGP_ENC16_EU 2
+#endif
+template <int H>
+constexpr int enc_waves() { return H <= 16 ? PGP_ENC16_WAVES : kEncWaves; }
 
 // RESIDENT (H <= 16): both layers' weights (24 KB at H = 16) are loaded into LDS
 // once per workgroup; the host loop then runs with no ring barriers or DMAs.
@@ -196,7 +206,7 @@ struct Ring {
     if (next < last) {
       const int si = next % (kLayers * G::NST), l = si / G::NST, k = si % G::NST;
       dma_groups(enc + (long)(l * G::LAYER_G + G::st_begin(k)) * G::FQ, nxt, G::st_end(k) - G::st_begin(k), wv,
-                 kEncWaves, lane);
+                 enc_waves<H>(), lane);
     }
   }
   PGP_DEV void advance() {
@@ -568,7 +578,7 @@ PGP_DEV void encoder_layer(f32x4 (&X)[Geo<H>::MT_D][3], Ring<H>& ring, const flo
 }
 
 template <int H>
-__global__ __launch_bounds__(kEncWaves * 64, 2) void encoder_kernel(FwdArgs a) {
+__global__ __launch_bounds__(enc_waves<H>() * 64, H <= 16 ? PGP_ENC16_EU : 2) void encoder_kernel(FwdArgs a) {
   using G = Geo<H>;
   using L = EncLds<H>;
   __shared__ __attribute__((aligned(16))) float smem[L::TOTAL];
@@ -578,13 +588,14 @@ __global__ __launch_bounds__(kEncWaves * 64, 2) void encoder_kernel(FwdArgs a) {
 
   const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const long blk = (long)blockIdx.x * kEncWaves + wv;
+  constexpr int NW = enc_waves<H>();
+  const long blk = (long)blockIdx.x * NW + wv;
   const long nblk = (a.B + 15) / 16;
   const bool active = blk < nblk;  // inactive waves still take part in the ring and barriers
 
   Ring<H> ring{smem, smem + L::SLOT, a.frags + G::OFF_ENC, 0, H * kLayers * G::NST, wv, lane};
   if constexpr (L::RESIDENT) {
-    dma_groups(a.frags + G::OFF_ENC, smem, kLayers * G::LAYER_G, wv, kEncWaves, lane);
+    dma_groups(a.frags + G::OFF_ENC, smem, kLayers * G::LAYER_G, wv, NW, lane);
     ring.nxt = smem;
     ring.next = 1;
     __syncthreads();
@@ -646,8 +657,9 @@ __global__ __launch_bounds__(kEncWaves * 64, 2) void encoder_kernel(FwdArgs a) {
 template <int H>
 hipError_t launch(const FwdArgs& a, hipStream_t st) {
   const long nblk = (a.B + 15) / 16;
-  const int grid = (int)((nblk + kEncWaves - 1) / kEncWaves);
-  encoder_kernel<H><<<grid, kEncWaves * 64, 0, st>>>(a);
+  constexpr int NW = enc_waves<H>();
+  const int grid = (int)((nblk + NW - 1) / NW);
+  encoder_kernel<H><<<grid, NW * 64, 0, st>>>(a);
   return hipGetLastError();
 }
 
