@@ -148,6 +148,9 @@ PGP_DEV void zero_rows(float (&r)[NR][3]) {
     for (int w = 0; w < 3; ++w) r[n][w] = 0.f;
 }
 
+#ifndef PGP_LN_FMA
+#define PGP_LN_FMA 1
+#endif
 template <int H>
 PGP_DEV void layer_norm_tiles(f32x4 (&acc)[Geo<H>::MT_D][3], f32x4 (&X)[Geo<H>::MT_D][3], const float* gam,
                               const float* bet, int g) {
@@ -180,10 +183,21 @@ PGP_DEV void layer_norm_tiles(f32x4 (&acc)[Geo<H>::MT_D][3], f32x4 (&X)[Geo<H>::
 #pragma unroll
   for (int w = 0; w < 3; ++w) {
     const float rstd = __builtin_amdgcn_rsqf(var[w] * invH + 1e-5f);  // v_rsq_f32 (1 ulp)
+#if PGP_LN_FMA
+    // (x - mean) * rstd as one fma per element: x * rstd + (-mean * rstd)
+    const float nm = -mean[w] * rstd;
+#endif
 #pragma unroll
     for (int mt = 0; mt < G::MT_D; ++mt) {
       const f32x4 ga = ld4(gam + 16 * mt + 4 * g), be = ld4(bet + 16 * mt + 4 * g);
+#if PGP_LN_FMA
+      f32x4 xn;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) xn[r] = fmaf(acc[mt][w][r], rstd, nm);
+      X[mt][w] = xn * ga + be;
+#else
       X[mt][w] = (acc[mt][w] - mean[w]) * rstd * ga + be;
+#endif
     }
   }
 }
