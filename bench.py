@@ -194,7 +194,12 @@ def main():
             "roofline": {"kernel": "encoder_kernel (K2)", "bound": "mfma", "achieved": achieved,
                          "peak": R.PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                          "frac": achieved / R.PEAK_FP32_TFLOPS, "traffic": traffic,
-                         "flops_per_window": R.encoder_flops_per_window(H)},
+                         "flops_per_window": R.encoder_flops_per_window(H),
+                         # what the kernel actually issues (MFMA count from its ISA)
+                         "executed_flops_per_window": R.encoder_executed_flops_per_window(H),
+                         "executed_frac": (None if R.encoder_executed_flops_per_window(H) is None else
+                                           R.encoder_executed_flops_per_window(H) * B / (k_mean[1] * 1e-3)
+                                           / 1e12 / R.PEAK_FP32_TFLOPS)},
             "path_roofline": {
                 "flops_per_window": R.total_flops_per_window(H),
                 "achieved_tflops": R.total_flops_per_window(H) * B * world * args.steps / elapsed / 1e12,

@@ -49,6 +49,18 @@ def encoder_flops_per_window(H: int) -> int:
     return f["time_encoder"] + f["encoder_layers"]
 
 
+# MFMA instructions (v_mfma_f32_16x16x4_f32, 2,048 flops each, 16 windows) per
+# host and wave in the encoder kernel's ISA (tools/isa_count.py).  K2 executes
+# fewer MFMA flops than the reference's algorithm (layer-0 folds), so
+# its algorithmic rate can exceed the peak; the executed rate cannot.
+ENC_MFMA_PER_HOST = {16: 264, 50: 1134}
+
+
+def encoder_executed_flops_per_window(H: int):
+    n = ENC_MFMA_PER_HOST.get(H)
+    return None if n is None else n * 2048 * H / 16
+
+
 def decoder_flops_per_window(H: int) -> int:
     """K2b (decoder_kernel): anomaly + prototype decoders."""
     return flops_per_window(H)["decoders"]
