@@ -151,7 +151,9 @@ PGP_DEV void zero_rows(float (&r)[NR][3]) {
 #ifndef PGP_LN_FMA
 #define PGP_LN_FMA 1
 #endif
-template <int H>
+// AFFINE = false (norm1): X = x-hat; gamma / beta are folded into linear1 and
+// linear2's bias by the packer, and the residual is formed as x-hat*gamma + b2'
+template <int H, bool AFFINE = true>
 PGP_DEV void layer_norm_tiles(f32x4 (&acc)[Geo<H>::MT_D][3], f32x4 (&X)[Geo<H>::MT_D][3], const float* gam,
                               const float* bet, int g) {
   using G = Geo<H>;
@@ -189,15 +191,19 @@ PGP_DEV void layer_norm_tiles(f32x4 (&acc)[Geo<H>::MT_D][3], f32x4 (&X)[Geo<H>::
 #endif
 #pragma unroll
     for (int mt = 0; mt < G::MT_D; ++mt) {
-      const f32x4 ga = ld4(gam + 16 * mt + 4 * g), be = ld4(bet + 16 * mt + 4 * g);
 #if PGP_LN_FMA
       f32x4 xn;
 #pragma unroll
       for (int r = 0; r < 4; ++r) xn[r] = fmaf(acc[mt][w][r], rstd, nm);
-      X[mt][w] = xn * ga + be;
 #else
-      X[mt][w] = (acc[mt][w] - mean[w]) * rstd * ga + be;
+      const f32x4 xn = (acc[mt][w] - mean[w]) * rstd;
 #endif
+      if constexpr (AFFINE) {
+        const f32x4 ga = ld4(gam + 16 * mt + 4 * g), be = ld4(bet + 16 * mt + 4 * g);
+        X[mt][w] = xn * ga + be;
+      } else {
+        X[mt][w] = xn;
+      }
     }
   }
 }
@@ -443,7 +449,7 @@ PGP_DEV void encoder_layer_tail(f32x4 (&X)[Geo<H>::MT_D][3], Ring<H>& ring, cons
       }
       acc[G::MT_X][w][0] += xsum_rows<G::XR>(ro);  // row n's sum in lane group n
     }
-    layer_norm_tiles<H>(acc, X, TL + G::TL_LN1G, TL + G::TL_LN1B, g);
+    layer_norm_tiles<H, false>(acc, X, TL + G::TL_LN1G, TL + G::TL_LN1B, g);
   } else {
   // [S1] v, P.v, out_proj (+ residual), norm1
   f32x4 V[TQ][3];
@@ -490,7 +496,7 @@ PGP_DEV void encoder_layer_tail(f32x4 (&X)[Geo<H>::MT_D][3], Ring<H>& ring, cons
 #pragma unroll
     for (int w = 0; w < 3; ++w) acc[G::MT_X][w][0] += rows_pick<G::XR>(ro, w);
   }
-  layer_norm_tiles<H>(acc, X, TL + G::TL_LN1G, TL + G::TL_LN1B, g);
+  layer_norm_tiles<H, false>(acc, X, TL + G::TL_LN1G, TL + G::TL_LN1B, g);
   }  // F0
   ring.advance();
   // [S2] relu(W1 x + b1), W2 . h + b2 + x, norm2
@@ -510,9 +516,9 @@ PGP_DEV void encoder_layer_tail(f32x4 (&X)[Geo<H>::MT_D][3], Ring<H>& ring, cons
       for (int r = 0; r < 4; ++r) F1[mt][w][r] = relu_enc<H>(F1[mt][w][r]);
 #pragma unroll
   for (int mt = 0; mt < G::MT_D; ++mt) {
-    const f32x4 b2 = ld4(TL + G::TL_B2 + 16 * mt + 4 * g);
+    const f32x4 b2 = ld4(TL + G::TL_B2 + 16 * mt + 4 * g), g1 = ld4(TL + G::TL_LN1G + 16 * mt + 4 * g);
 #pragma unroll
-    for (int w = 0; w < 3; ++w) acc[mt][w] = b2 + X[mt][w];
+    for (int w = 0; w < 3; ++w) acc[mt][w] = X[mt][w] * g1 + b2;  // residual gamma*x-hat + beta, + b2
   }
   {
     float rf[G::XR][3];
@@ -562,7 +568,7 @@ PGP_DEV void encoder_layer(f32x4 (&X)[Geo<H>::MT_D][3], Ring<H>& ring, const flo
     gemm3<G::MT_D, G::KQ_O, G::KS_O, G::TP>(acc, ring.cur, O, lane);
   }
   // x = norm1(x + sa)
-  layer_norm_tiles<H>(acc, X, TL + G::TL_LN1G, TL + G::TL_LN1B, g);
+  layer_norm_tiles<H, false>(acc, X, TL + G::TL_LN1G, TL + G::TL_LN1B, g);
   // feed-forward: relu(W1 x + b1) in the same stage as the last out_proj
   f32x4 F1[G::MT_F][3];
 #pragma unroll
@@ -582,9 +588,9 @@ PGP_DEV void encoder_layer(f32x4 (&X)[Geo<H>::MT_D][3], Ring<H>& ring, const flo
   // [S3] W2 . h + b2 + x, norm2
 #pragma unroll
   for (int mt = 0; mt < G::MT_D; ++mt) {
-    const f32x4 b2 = ld4(TL + G::TL_B2 + 16 * mt + 4 * g);
+    const f32x4 b2 = ld4(TL + G::TL_B2 + 16 * mt + 4 * g), g1 = ld4(TL + G::TL_LN1G + 16 * mt + 4 * g);
 #pragma unroll
-    for (int w = 0; w < 3; ++w) acc[mt][w] = b2 + X[mt][w];
+    for (int w = 0; w < 3; ++w) acc[mt][w] = X[mt][w] * g1 + b2;  // residual gamma*x-hat + beta, + b2
   }
   gemm3<G::MT_D, G::KQ_F, 16, G::MT_F>(acc, ring.cur, F1, lane);
   ring.advance();

@@ -357,7 +357,9 @@ std::string pack_t(int K, const double* blob, size_t len, Packed* P) {
           for (int e4 = 0; e4 < 4; ++e4) {
             const int i = lane & 15, g = lane >> 4, s = 4 * q4 + e4, c = 4 * s + g;
             if (s >= G::KS_D || c >= d) continue;
-            FL[(G::P_F1 + mt * G::KQ_D + q4) * G::FQ + lane * 4 + e4] = (float)S.l1W[(16 * mt + i) * d + c];
+            // norm1's gamma folded into linear1 (the kernel feeds it the un-scaled x-hat)
+            FL[(G::P_F1 + mt * G::KQ_D + q4) * G::FQ + lane * 4 + e4] =
+                (float)(S.l1W[(16 * mt + i) * d + c] * S.n1w[c]);
           }
     for (int mt = 0; mt < G::MT_X; ++mt)
       for (int q4 = 0; q4 < G::KQ_F; ++q4)
@@ -374,11 +376,15 @@ std::string pack_t(int K, const double* blob, size_t len, Packed* P) {
       TL[G::TL_BO + R] = (float)S.outB[c];
       TL[G::TL_LN1G + R] = (float)S.n1w[c];
       TL[G::TL_LN1B + R] = (float)S.n1b[c];
-      TL[G::TL_B2 + R] = (float)S.l2B[c];
+      TL[G::TL_B2 + R] = (float)(S.l2B[c] + S.n1b[c]);  // + norm1's beta: the residual is gamma*x-hat + beta
       TL[G::TL_LN2G + R] = (float)S.n2w[c];
       TL[G::TL_LN2B + R] = (float)S.n2b[c];
     }
-    for (int u = 0; u < 64; ++u) TL[G::TL_B1 + u] = (float)S.l1B[u];
+    for (int u = 0; u < 64; ++u) {  // linear1 bias + linear1 . norm1's beta
+      double b = S.l1B[u];
+      for (int c = 0; c < d; ++c) b += S.l1W[u * d + c] * S.n1b[c];
+      TL[G::TL_B1 + u] = (float)b;
+    }
     // tail mode: linear2 rows of the VALU d-rows (feature 16*MT_X + n)
     for (int n = 0; n < G::XR; ++n)
       for (int q4 = 0; q4 < G::KQ_F; ++q4)
