@@ -151,6 +151,9 @@ PGP_DEV void zero_rows(float (&r)[NR][3]) {
 #ifndef PGP_LN_FMA
 #define PGP_LN_FMA 1
 #endif
+#ifndef PGP_LN_ONEPASS
+#define PGP_LN_ONEPASS 1
+#endif
 // AFFINE = false (norm1): X = x-hat; gamma / beta are folded into linear1 and
 // linear2's bias by the packer, and the residual is formed as x-hat*gamma + b2'
 template <int H, bool AFFINE = true>
@@ -158,6 +161,26 @@ PGP_DEV void layer_norm_tiles(f32x4 (&acc)[Geo<H>::MT_D][3], f32x4 (&X)[Geo<H>::
                               const float* bet, int g) {
   using G = Geo<H>;
   constexpr float invH = 1.0f / (float)H;
+#if PGP_LN_ONEPASS
+  // one pass: sum and sum of squares of each step reduced together (xsum2).
+  // Padded feature rows hold exact zeros here, so no mask is needed.
+  // var = E[x^2] - mean^2 (LN inputs are a residual stream whose mean is O(std))
+  float sum[3], mean[3], var[3];
+#pragma unroll
+  for (int w = 0; w < 3; ++w) {
+    sum[w] = 0.f;
+    float sq = 0.f;
+#pragma unroll
+    for (int mt = 0; mt < G::MT_D; ++mt) {
+      sum[w] += (acc[mt][w][0] + acc[mt][w][1]) + (acc[mt][w][2] + acc[mt][w][3]);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) sq = fmaf(acc[mt][w][r], acc[mt][w][r], sq);
+    }
+    xsum2(sum[w], sq);
+    mean[w] = sum[w] * invH;
+    var[w] = fmaxf(fmaf(-mean[w], mean[w], sq * invH), 0.f);  // the variance itself
+  }
+#else
   // the three steps' statistics are reduced across lane groups in pairs (xsum2)
   float sum[3], mean[3], var[3];
 #pragma unroll
@@ -182,9 +205,14 @@ PGP_DEV void layer_norm_tiles(f32x4 (&acc)[Geo<H>::MT_D][3], f32x4 (&X)[Geo<H>::
   }
   xsum2(var[0], var[1]);
   var[2] = xsum(var[2], true);
+#endif
 #pragma unroll
   for (int w = 0; w < 3; ++w) {
-    const float rstd = __builtin_amdgcn_rsqf(var[w] * invH + 1e-5f);  // v_rsq_f32 (1 ulp)
+#if PGP_LN_ONEPASS
+    const float rstd = __builtin_amdgcn_rsqf(var[w] + 1e-5f);  // v_rsq_f32 (1 ulp)
+#else
+    const float rstd = __builtin_amdgcn_rsqf(var[w] * invH + 1e-5f);
+#endif
 #if PGP_LN_FMA
     // (x - mean) * rstd as one fma per element: x * rstd + (-mean * rstd)
     const float nm = -mean[w] * rstd;
