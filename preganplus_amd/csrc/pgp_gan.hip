@@ -26,6 +26,11 @@ constexpr int kQC = 4;  // schedule k-blocks (16 columns each) per chunk
 #ifndef PGP_GAN_PRIO
 #define PGP_GAN_PRIO 1
 #endif
+// Disc1's new-schedule half: skip the MFMAs whose whole k slice is padding rows
+// (at H = 50 the last tile's e = 2, 3 steps: 8 of 128 MFMAs per container)
+#ifndef PGP_GAN_KSKIP
+#define PGP_GAN_KSKIP 1
+#endif
 template <int P>
 __device__ __forceinline__ void gan_prio() {
   if (PGP_GAN_PRIO) __builtin_amdgcn_s_setprio(P);
@@ -242,8 +247,9 @@ __global__ __launch_bounds__(kGanWaves * 64) void gan_kernel(FwdArgs a) {
         for (int i = 0; i < 2; ++i) w[i] = ld4(cw + (G::GC_G2 + (m0 + i) * G::MT_N + q4) * 256 + lane * 4);
 #pragma unroll
         for (int e = 0; e < 4; ++e)
+          if (!PGP_GAN_KSKIP || 16 * q4 + e < H)  // k = 16 q4 + 4g + e: all lanes' rows >= H are zero
 #pragma unroll
-          for (int i = 0; i < 2; ++i) hd[m0 + i] = mfma(w[i][e], ns[q4][e], hd[m0 + i]);
+            for (int i = 0; i < 2; ++i) hd[m0 + i] = mfma(w[i][e], ns[q4][e], hd[m0 + i]);
       }
     gan_prio<0>();
 #pragma unroll
