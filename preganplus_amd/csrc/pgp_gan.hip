@@ -31,6 +31,11 @@ constexpr int kQC = 4;  // schedule k-blocks (16 columns each) per chunk
 #ifndef PGP_GAN_KSKIP
 #define PGP_GAN_KSKIP 1
 #endif
+// Gen2 tail rows: a last row tile with at most kTailMax real rows runs on VALU
+#ifndef PGP_GAN_TAIL
+#define PGP_GAN_TAIL 1
+#endif
+constexpr int kTailMax = 2;
 template <int P>
 __device__ __forceinline__ void gan_prio() {
   if (PGP_GAN_PRIO) __builtin_amdgcn_s_setprio(P);
@@ -189,6 +194,12 @@ __global__ __launch_bounds__(kGanWaves * 64) void gan_kernel(FwdArgs a) {
         v[t][r + 1] = p.y;
       }
   };
+  // Gen2's last row tile at H = 50 holds 2 real rows of 16: those rows are VALU
+  // dot products (k split over the lane groups, summed across them) issued in
+  // the shadow of the other tiles' MFMAs, instead of 16 MFMAs per container
+  constexpr int NTR = H - 16 * (G::MT_N - 1);
+  constexpr bool TAIL = PGP_GAN_TAIL && G::MT_N > 1 && NTR <= kTailMax;
+  constexpr int MTM = TAIL ? G::MT_N - 1 : G::MT_N;  // Gen2 tiles on MFMA
   float sv[G::MT_N][4];
   load_row(0, sv);
   for (int c = 0; c < G::C; ++c) {
@@ -198,22 +209,36 @@ __global__ __launch_bounds__(kGanWaves * 64) void gan_kernel(FwdArgs a) {
     f32x4 ns[G::MT_N];
 #pragma unroll
     for (int t = 0; t < G::MT_N; ++t) ns[t] = ld4(gt + G::G_B2 + c * G::MT_N * 16 + 16 * t + 4 * g);
+    float racc[kTailMax] = {};
     gan_prio<1>();
 #pragma unroll
-    for (int q4 = 0; q4 < 4; ++q4)
+    for (int q4 = 0; q4 < 4; ++q4) {
 #pragma unroll
-      for (int t0 = 0; t0 < G::MT_N; t0 += 2) {  // two accumulators alternate: no dependent-issue stall
+      for (int t0 = 0; t0 < MTM; t0 += 2) {  // two accumulators alternate: no dependent-issue stall
         f32x4 w[2];
 #pragma unroll
         for (int i = 0; i < 2; ++i)
-          if (t0 + i < G::MT_N) w[i] = ld4(cw + ((t0 + i) * 4 + q4) * 256 + lane * 4);
+          if (t0 + i < MTM) w[i] = ld4(cw + ((t0 + i) * 4 + q4) * 256 + lane * 4);
 #pragma unroll
         for (int e = 0; e < 4; ++e)
 #pragma unroll
           for (int i = 0; i < 2; ++i)
-            if (t0 + i < G::MT_N) ns[t0 + i] = mfma(w[i][e], hg[q4][e], ns[t0 + i]);
+            if (t0 + i < MTM) ns[t0 + i] = mfma(w[i][e], hg[q4][e], ns[t0 + i]);
       }
+      if (TAIL) {  // row r of the last tile: its A fragment column sits on lane 16g + r
+#pragma unroll
+        for (int r = 0; r < NTR; ++r) {
+          const f32x4 rw = ld4(cw + (MTM * 4 + q4) * 256 + (16 * g + r) * 4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) racc[r] = fmaf(rw[e], hg[q4][e], racc[r]);
+        }
+      }
+    }
     gan_prio<0>();
+    if (TAIL) {  // lanes g = 0 hold rows 16 MTM + r; the other groups' rows are >= H
+#pragma unroll
+      for (int r = 0; r < NTR; ++r) ns[MTM][r] += xsum(racc[r], true);
+    }
     float bn_v = -INFINITY, bs_v = -INFINITY;
     int bn_i = 0, bs_i = 0;
 #pragma unroll
