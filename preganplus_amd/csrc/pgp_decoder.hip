@@ -15,6 +15,9 @@ namespace pgp {
 namespace {
 
 constexpr int kDecWaves = 16;
+#ifndef PGP_DEC_TAIL
+#define PGP_DEC_TAIL 0
+#endif
 
 // CPS (host, step) chunks per ring slot: at small H one chunk is only a few
 // groups (4 KB, 16 MFMAs per wave at H = 16), so a barrier per chunk dominated;
@@ -71,6 +74,13 @@ __global__ __launch_bounds__(kDecWaves * 64, H <= 16 ? 8 : 1) void decoder_kerne
   f32x4 acc[G::MT_O];
 #pragma unroll
   for (int mt = 0; mt < G::MT_O; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // tail rows: a last output tile with NTR <= 8 real rows (H = 50: hosts 48, 49)
+  // as VALU dot products over each lane group's k-steps, summed across groups once
+  // after the K loop, instead of one MFMA per k-step
+  constexpr int NTR = 4 * (H - 4 * (G::MT_O - 1));
+  constexpr bool TAIL = PGP_DEC_TAIL && G::MT_O > 1 && NTR <= 8;
+  constexpr int MTM = TAIL ? G::MT_O - 1 : G::MT_O;  // output tiles on MFMA
+  float racc[8] = {};
 
 #pragma unroll 1
   for (int c0 = 0; c0 < NCH; c0 += CPS) {
@@ -86,23 +96,33 @@ __global__ __launch_bounds__(kDecWaves * 64, H <= 16 ? 8 : 1) void decoder_kerne
       // consecutive MFMAs go to different accumulators (dependent-accumulator
       // latency 40 cyc > 32 cyc issue): A fragments of half the output tiles at a time
       constexpr int AMAX = G::MT_O >= 16 ? 4 : H <= 16 ? 2 : 7;  // A fragments live (VGPR budget)
-      constexpr int NGRP = (G::MT_O + AMAX - 1) / AMAX;
-      constexpr int MH = (G::MT_O + NGRP - 1) / NGRP;
+      constexpr int NGRP = (MTM + AMAX - 1) / AMAX;
+      constexpr int MH = (MTM + NGRP - 1) / NGRP;
 #pragma unroll
-      for (int q4 = 0; q4 < G::KQ_D; ++q4)
+      for (int q4 = 0; q4 < G::KQ_D; ++q4) {
 #pragma unroll
-        for (int m0 = 0; m0 < G::MT_O; m0 += MH) {
+        for (int m0 = 0; m0 < MTM; m0 += MH) {
           f32x4 av[MH];
 #pragma unroll
           for (int i = 0; i < MH; ++i)
-            if (m0 + i < G::MT_O) av[i] = ld4(A + ((m0 + i) * G::KQ_D + q4) * 256 + lane * 4);
+            if (m0 + i < MTM) av[i] = ld4(A + ((m0 + i) * G::KQ_D + q4) * 256 + lane * 4);
 #pragma unroll
           for (int e = 0; e < 4; ++e)
             if (4 * q4 + e < G::KS_D)
 #pragma unroll
               for (int i = 0; i < MH; ++i)
-                if (m0 + i < G::MT_O) acc[m0 + i] = mfma(av[i][e], b[sub][4 * q4 + e], acc[m0 + i]);
+                if (m0 + i < MTM) acc[m0 + i] = mfma(av[i][e], b[sub][4 * q4 + e], acc[m0 + i]);
         }
+        if (TAIL) {  // row r of the last tile: its A fragment column sits on lane 16g + r
+#pragma unroll
+          for (int r = 0; r < NTR; ++r) {
+            const f32x4 rw = ld4(A + (MTM * G::KQ_D + q4) * 256 + (16 * g + r) * 4);
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              if (4 * q4 + e < G::KS_D) racc[r] = fmaf(rw[e], b[sub][4 * q4 + e], racc[r]);
+          }
+        }
+      }
     }
 #pragma unroll
     for (int u = 0; u < CPS; ++u)
@@ -113,6 +133,19 @@ __global__ __launch_bounds__(kDecWaves * 64, H <= 16 ? 8 : 1) void decoder_kerne
     cur = nxt;
     nxt = t;
     if (c0 + 2 * CPS < NCH) dma_groups(wdec + (long)(c0 + 2 * CPS) * G::DEC_G * G::FQ, nxt, SG, wv, kDecWaves, lane);
+  }
+
+  if (TAIL) {  // lane group g takes rows 4g + {0..3} of the summed tail rows
+    float tv[8];
+#pragma unroll
+    for (int r = 0; r < NTR; ++r) tv[r] = xsum(racc[r], true);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float v = 0.f;
+#pragma unroll
+      for (int q = 0; q * 4 + r < NTR; ++q) v = (g == q) ? tv[4 * q + r] : v;
+      acc[MTM][r] = v;
+    }
   }
 
   // ---- epilogue: bias, sigmoid, detect, embed, classify ----
