@@ -45,31 +45,20 @@ def synth_inputs(B, H, device, seed):
     return x.contiguous(), s.contiguous()
 
 
-def cpu_baseline(H, weights, budget_s=12.0, max_threads=16):
-    """numpy fp64 oracle (batched restatement of the reference math) on the
-    host cores, on a bounded sample of the same synthetic workload."""
-    from threadpoolctl import threadpool_limits
-    from oracle import pregan_oracle as O  # CPU baseline leg only
-    threads = min(max_threads, os.cpu_count() or 1)
-    rng = np.random.Generator(np.random.PCG64(99))
-    nb = 64
-    x = rng.uniform(0, 0.6, size=(nb, 3, 3 * H))
-    s = np.zeros((nb, H, H))
-    s[np.arange(nb)[:, None], np.arange(H)[None, :], rng.integers(0, H, size=(nb, H))] = 1.0
-    done, t0 = 0, time.perf_counter()
-    with threadpool_limits(limits=threads):
-        O.forward(weights, x[:8], s[:8])  # warm-up
-        t0 = time.perf_counter()
-        while time.perf_counter() - t0 < budget_s:
-            O.forward(weights, x, s)
-            done += nb
-    dt = time.perf_counter() - t0
-    return {"value": done * H / dt, "unit": "host-windows/s", "cores": threads, "kind": "port",
-            "sample": f"{done} windows (H={H}, batches of {nb}), numpy fp64 oracle, {dt:.1f}s"}
+def cpu_baseline(weights, x, s, per_window_n=32, batch_n=1024):
+    """the CPU restatement timed on this box's host cores, on the
+    GPU run's own first windows (same C2 inputs, spikes included), in two modes
+    (reference-faithful per-window fp64; batched fp32 torch-CPU), median of 5."""
+    from oracle import cpu_baseline as CB  # CPU baseline leg only
+    n = max(per_window_n, batch_n)
+    return CB.measure(weights, x[:n].cpu().numpy(), s[:n].cpu().numpy(), per_window_n, batch_n)
 
 
-def load_traffic(H, B):
-    p = os.path.join(ROOT, "profiles", f"pmc_encoder_h{H}.json")
+def load_traffic(H, B, kernel="encoder"):
+    """HBM bytes per launch of one kernel from the committed rocprofv3 --pmc
+    FETCH_SIZE / WRITE_SIZE passes (profiles/pmc_<kernel>_h<H>.json, corrected
+    per MI355X_MICROARCH.md §HBM), or None when absent / another batch."""
+    p = os.path.join(ROOT, "profiles", f"pmc_{kernel}_h{H}.json")
     if not os.path.exists(p):
         return None
     try:
@@ -84,7 +73,7 @@ def load_traffic(H, B):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=300)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--hosts", type=int, default=50)
     ap.add_argument("--batch", type=int, default=65536, help="windows per GPU per step")
@@ -166,9 +155,15 @@ def main():
     if rank == 0:
         ms = elapsed / args.steps * 1e3
         hw = B * world * H * args.steps / elapsed
-        k2_flops = R.encoder_flops_per_window(H) * B
-        achieved = k2_flops / (k_mean[1] * 1e-3) / 1e12
+        k2_s = k_mean[1] * 1e-3
+        # executed work: the MFMAs K2 issues (ISA count); the reference formulation's
+        # flops are reported beside it (the layer-0 folds issue 0.67x of them)
+        exe = R.encoder_executed_flops_per_window(H)
+        alg = R.encoder_flops_per_window(H)
+        achieved = (exe if exe is not None else alg) * B / k2_s / 1e12
         traffic = load_traffic(H, B)
+        k_traffic = {k: load_traffic(H, B, k) for k in ("gat_agg", "encoder", "decoder", "gan")}
+        path_bytes = R.path_bytes_per_window(H) * B
         res = {
             "metric": "host-windows/sec (detect+diagnose+generate)",
             "value": hw,
@@ -193,23 +188,29 @@ def main():
                 "gan": R.gan_flops_per_window(H) * B / (k_mean[3] * 1e-3) / 1e12},
             "roofline": {"kernel": "encoder_kernel (K2)", "bound": "mfma", "achieved": achieved,
                          "peak": R.PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved / R.PEAK_FP32_TFLOPS, "traffic": traffic,
-                         "flops_per_window": R.encoder_flops_per_window(H),
-                         # what the kernel actually issues (MFMA count from its ISA)
-                         "executed_flops_per_window": R.encoder_executed_flops_per_window(H),
-                         "executed_frac": (None if R.encoder_executed_flops_per_window(H) is None else
-                                           R.encoder_executed_flops_per_window(H) * B / (k_mean[1] * 1e-3)
-                                           / 1e12 / R.PEAK_FP32_TFLOPS)},
+                         "frac": achieved / R.PEAK_FP32_TFLOPS,
+                         "basis": "executed MFMA flops per launch (ISA count, tools/isa_count.py) / HIP-event "
+                                  "kernel time",
+                         "executed_flops_per_window": exe,
+                         "algorithmic_flops_per_window": alg,
+                         "algorithmic_rate": alg * B / k2_s / 1e12,
+                         "traffic": traffic,
+                         "traffic_ratio": (None if traffic is None else
+                                           traffic / (R.encoder_io_bytes_per_window(H) * B)),
+                         "io_bytes_per_window": R.encoder_io_bytes_per_window(H)},
             "path_roofline": {
                 "flops_per_window": R.total_flops_per_window(H),
                 "achieved_tflops": R.total_flops_per_window(H) * B * world * args.steps / elapsed / 1e12,
-                "hbm_algorithmic_gbs": R.path_bytes_per_window(H) * B * world * args.steps / elapsed / 1e9,
-                "hbm_frac": R.path_bytes_per_window(H) * B * world * args.steps / elapsed / 1e9 / R.PEAK_HBM_GBS,
+                "hbm_algorithmic_gbs": path_bytes * world * args.steps / elapsed / 1e9,
+                "hbm_frac": path_bytes * world * args.steps / elapsed / 1e9 / R.PEAK_HBM_GBS,
+                "traffic_per_step": (None if None in k_traffic.values() else sum(k_traffic.values())),
+                "traffic_ratio": (None if None in k_traffic.values() else sum(k_traffic.values()) / path_bytes),
+                "traffic_by_kernel": k_traffic,
             },
         }
         if world == 1 and not args.no_cpu_baseline:
             log("timing CPU baseline ...")
-            res["cpu_baseline"] = cpu_baseline(H, weights, args.cpu_budget)
+            res["cpu_baseline"] = cpu_baseline(weights, x, s)
         else:
             res["cpu_baseline"] = None
         print(json.dumps(res), flush=True)
@@ -273,14 +274,18 @@ def bench_fleet(args):
     el = _timed(world, device, lambda: model.forward(x, s, out=out), steps)
     if rank == 0:
         cw = B * steps * world
-        print(json.dumps({
+        res = {
             "metric": "host-windows/sec (detect+diagnose+generate), fleet", "value": cw * H / el,
             "unit": "host-windows/s", "n_gpus": world, "steps": steps, "warmup": args.warmup,
             "ms_per_step": el / steps * 1e3, "higher_is_better": True, "scaling": "strong" if args.steps <= 0 else "weak",
             "vs_baseline": None, "dtype": "fp32", "data": "synthetic (C2 distribution), shipped H=16 weights",
             "config": {"workload": "C5: 1024-host fleet = 64 x 16-host cells, cell-windows sharded over GPUs",
                        "hosts_per_cell": H, "cells": 64, "cell_windows_per_step_per_gpu": B,
-                       "cell_windows_total": cw, "parallelism": f"dp{world}"}}), flush=True)
+                       "cell_windows_total": cw, "parallelism": f"dp{world}"}}
+        if world == 1 and not args.no_cpu_baseline:
+            log("timing CPU baseline ...")
+            res["cpu_baseline"] = cpu_baseline(w, x, s, per_window_n=64, batch_n=4096)
+        print(json.dumps(res), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
 

@@ -94,7 +94,8 @@ def form_test_dataset(data):
 # model pieces
 # ----------------------------------------------------------------------------
 def _lin(x, w, b=None):
-    y = x @ w.T
+    # one 2-D GEMM over all leading axes (a stacked matmul calls BLAS per slice)
+    y = (x.reshape(-1, x.shape[-1]) @ w.T).reshape(x.shape[:-1] + (w.shape[0],))
     if b is not None:
         y = y + b
     return y
@@ -122,7 +123,7 @@ def gat(win, fc_w, attn_w):
     ef = ef - ef.max(axis=-1, keepdims=True)
     p = np.exp(ef)
     p = (p / p.sum(axis=-1, keepdims=True)).reshape(B, W, H, H)
-    return np.einsum("bwij,bwid->bwjd", p, z)
+    return np.matmul(p.transpose(0, 1, 3, 2), z)       # sum_i p_ij z_i (einsum bwij,bwid->bwjd)
 
 
 def layer_norm(x, g, b, eps=LN_EPS):

@@ -61,6 +61,12 @@ def encoder_executed_flops_per_window(H: int):
     return None if n is None else n * 2048 * H / 16
 
 
+def encoder_io_bytes_per_window(H: int) -> int:
+    """K2's own compulsory HBM I/O: the GAT output it reads (W x H x 3 aggregated
+    raw features, fp32) and the latent it writes (3H^2 fp32) for K2b."""
+    return 4 * (W * H * 3) + 4 * (W * H * H)
+
+
 def decoder_flops_per_window(H: int) -> int:
     """K2b (decoder_kernel): anomaly + prototype decoders."""
     return flops_per_window(H)["decoders"]

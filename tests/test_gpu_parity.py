@@ -52,9 +52,8 @@ def test_reference_fixtures(H):
     w, ref = fixture(H)
     m = get_model(H, w, f"fix{H}")
     got = run(m, ref["windows"], ref["sched"], latent=True)
-    stats = assert_parity(got, ref, w["prototypes"])
     # on the committed fixtures every decision must match exactly
-    assert all(v == 0 for v in stats.values()), stats
+    assert_parity(got, ref, w, ref["sched"], exact=True)
     assert np.array_equal(got["cls"], ref["cls"])
     assert np.array_equal(got["gen_target"], ref["gen_target"])
     assert np.array_equal(got["keep"], ref["keep"])
@@ -91,7 +90,7 @@ def test_synthetic_vs_oracle_ragged_batch(H):
     ref["sched32"] = s.astype(np.float32)
     m = get_model(H, w, f"syn{H}")
     got = run(m, x, s, latent=True)
-    assert_parity(got, ref, w["prototypes"])
+    assert_parity(got, ref, w, s)
 
 
 def test_edge_inputs_h16():
@@ -115,7 +114,7 @@ def test_edge_inputs_h16():
     ref["sched32"] = s.astype(np.float32)
     m = get_model(H, w, "fix16b")
     got = run(m, x, s)
-    assert_parity(got, ref, w["prototypes"])
+    assert_parity(got, ref, w, s)
     assert got["final_target"][0].tolist() == [0] * H
     assert got["final_target"][1].tolist() == [3] * H
     assert np.isfinite(got["logits"]).all() and np.isfinite(got["probs"]).all()
@@ -137,7 +136,7 @@ def test_large_batch_properties_h50():
     ref = O.forward(w, x[idx], s[idx])
     ref["sched32"] = s[idx].astype(np.float32)
     sub = {k: v[idx] for k, v in full.items()}
-    assert_parity(sub, ref, w["prototypes"], check_latent=False)
+    assert_parity(sub, ref, w, s[idx], check_latent=False)
     assert np.array_equal(full["final_target"], O.first_argmax_rows(s.astype(np.float32)))
 
 
@@ -153,15 +152,28 @@ def _c2_torch(n, H, seed, device="cuda"):
     return x.contiguous(), s
 
 
+@pytest.mark.timeout(900)
 @pytest.mark.parametrize("H,B", [(50, 65536), (16, 262144)])
-def test_full_size_properties(H, B):
-    """BASELINE sizes: C2 (H=50, 65,536 windows) and one C5 launch (H=16, 262,144
-    cell-windows).  Size-independent checks: windows at the start, middle and
-    ragged tail give bitwise the same results when run alone; final targets are
-    the schedule rows' first argmax; the detect / gate / probability outputs are
-    consistent with the logits and probabilities; a random sample matches the
-    fp64 oracle."""
+def test_full_size_census(H, B):
+    """BASELINE sizes: C2 (H=50, 65,536 windows) and one whole C5 launch (H=16,
+    262,144 cell-windows), every window compared with the fp64 oracle
+    (tests/census.py over a CPU worker pool).
+
+    - continuous outputs within the north-star tolerance for every window
+      (logits / protos rtol 1e-4; probs wherever the anomaly flags agree);
+    - every decision (anomaly flag, any, class, keep, final target, generator
+      target) equal to the oracle's unless its fp64 margin lies inside its
+      derived fp32 error bound (tests/decision_bounds.py): mismatches outside
+      the bound must be 0; in-band counts and mismatches are printed and written
+      to gpurun_out/census_h{H}_b{B}.json;
+    - windows at the start, middle and ragged tail give bitwise the same results
+      when run alone; keep / any / class consistent with probs and logits."""
+    import json
+    import os
+
     from preganplus_amd.model import to_numpy
+    from tests import census as CE
+    from tests import decision_bounds as DB
     if H == 16:
         w, _ = W.load_npz("preganplus_amd/data/simulator_16.npz")
     else:
@@ -177,15 +189,21 @@ def test_full_size_properties(H, B):
             assert np.array_equal(full[k][lo:hi], part[k]), (k, lo, hi)
     assert np.isfinite(full["logits"]).all() and np.isfinite(full["probs"]).all()
     np.testing.assert_allclose(full["probs"].sum(axis=1), 1.0, rtol=0, atol=2e-6)
-    assert np.array_equal(full["keep"], full["probs"][:, 0] > full["probs"][:, 1])
     anom = full["logits"][..., 1] > full["logits"][..., 0]
     assert np.array_equal(full["any"], anom.any(axis=1))
     assert np.array_equal(full["cls"] < 0, ~anom)  # a class exactly where a host is flagged
-    s_np = s.cpu().numpy()
-    assert np.array_equal(full["final_target"], O.first_argmax_rows(s_np))
-    rng = np.random.Generator(np.random.PCG64(H))
-    idx = np.sort(rng.choice(B, size=64, replace=False))
-    xs = x[torch.as_tensor(idx, device=x.device)].cpu().numpy().astype(np.float64)
-    ref = O.forward(w, xs, s_np[idx].astype(np.float64))
-    ref["sched32"] = s_np[idx]
-    assert_parity({k: v[idx] for k, v in full.items()}, ref, w["prototypes"], check_latent=False)
+    x32 = x.cpu().numpy()
+    sidx = s.argmax(dim=-1).cpu().numpy()
+    del x, s
+    st, worst = CE.run(w, x32, sidx, full, log=print)
+    res = {"H": H, "windows": B, "census": st, "worst_error_over_tolerance": worst}
+    print("CENSUS", json.dumps(res))
+    os.makedirs("gpurun_out", exist_ok=True)
+    with open(f"gpurun_out/census_h{H}_b{B}.json", "w") as f:
+        json.dump(res, f, indent=1)
+    assert worst["logits"] <= 1.0 and worst["protos"] <= 1.0 and worst["probs"] <= 1.0, worst
+    assert not DB.violations(st), st
+    assert st["windows"] == B
+    # the rigorous bounds leave a small unverifiable fraction: keep it < 0.1 %
+    for kind in ("anomaly", "class", "keep", "gen"):
+        assert st[kind]["in_band"] <= 1e-3 * max(st[kind]["n"], 1), (kind, st[kind])
