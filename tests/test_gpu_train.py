@@ -355,3 +355,156 @@ def test_backprop_graph_bit_identical_to_host_loop():
         assert [t["step"] for t in a.tensors] == [t["step"] for t in b.tensors]
         np.testing.assert_allclose(np.array(lb), np.array(la), rtol=1e-12, atol=1e-12)
     assert len(b._graphs) == 2
+
+
+# ---------------------------------------------------------------------------
+# H = 50 against the reference's own modules (tests/golden/make_golden_train50.py)
+# ---------------------------------------------------------------------------
+def _dclose(rel, abs_scale, H=50, steps=None):
+    """close() on a digest part; full in_proj_bias parts get the key-bias
+    treatment (identically-zero gradient, see key_bias_mask)."""
+    def f(got, want, what):
+        if steps is not None and what.endswith("self_attn.in_proj_bias/full"):
+            kb = key_bias_mask("self_attn.in_proj_bias", want.size, d=H)
+            close(got[~kb], want[~kb], rel=rel, abs_scale=abs_scale, what=what)
+            assert np.all(np.abs(got[kb] - want[kb]) <= 2e-4 * steps), what + " (key bias)"
+        else:
+            close(got, want, rel=rel, abs_scale=abs_scale, what=what)
+    return f
+
+
+def _param_close(z, k, steps, rel, abs_scale, lr=1e-4, H=50):
+    """Parameters after `steps` fresh-AdamW steps.  AdamW's first step moves
+    every entry by ~lr * g / |g|, so an entry whose fp64 gradient is below the
+    fp32 gradient's own absolute accuracy (1e-4 of the tensor's largest
+    gradient, as the gradient check allows) takes a step whose sign is rounding
+    noise on both sides: those entries (and the key bias, see key_bias_mask) are
+    held to 2 lr per step; all others to rel / abs_scale."""
+    from tests.golden import digest as D
+    g = D.parts(z, f"g0/{k}")
+
+    def cmp(got, want, what):
+        part = what.rsplit("/", 1)[1]
+        gr = g[part].reshape(-1)
+        noise = np.abs(gr) <= 1e-4 * np.abs(gr).max()
+        if part == "full" and k.endswith("self_attn.in_proj_bias"):
+            noise |= key_bias_mask(k, want.size, d=H)
+        got, want = got.reshape(-1), want.reshape(-1)
+        close(got[~noise], want[~noise], rel=rel, abs_scale=abs_scale, what=what)
+        assert np.all(np.abs(got[noise] - want[noise]) <= 2 * lr * steps), what + " (noise-level gradients)"
+    return cmp
+
+
+def test_tuning_step_matches_reference_h50():
+    """backprop (train.py:42-57) at H=50 vs the reference's own modules: step-0
+    gradients, parameters after steps 1 and 10, prototypes and counters."""
+    from preganplus_amd import train as TR
+    from tests.golden import digest as D
+    H = 50
+    w = W.synth_weights(H, 0)
+    z = np.load(f"{GOLD}/tune_h50.npz")
+    tr = TR.Trainer(H, w)
+    st = TR.TuneState(w["prototypes"], float(z["factor0"]))
+    wins, anom, cls = z["windows"], z["anom"], z["cls"]
+    st.num_zero, st.num_ones = 1, 1
+    losses = []
+    for i in range(wins.shape[0]):
+        logits, protos = tr.tune_forward(torch.tensor(wins[i:i + 1], dtype=torch.float32))
+        mult, tgt, aloss, tloss = TR.loss_targets(logits[0].cpu().numpy(), protos[0].cpu().numpy(),
+                                                  anom[i], cls[i], st)
+        tr.tune_backward(1, anom[i][None], mult[None], tgt[None])
+        if i == 0:
+            g = tr.G.cpu().numpy()
+            for t in tr.tensors:
+                if t["section"] == "transformer" and t["trainable"]:
+                    D.check(z, f"g0/{t['name']}", g[t["offset"]:t["offset"] + t["n"]].reshape(
+                        w["transformer"][t["name"]].shape), _dclose(1e-3, 1e-4), sum_rel=1e-4, key=t["name"])
+        inactive = () if np.any(anom[i] > 0) else ("prototype_decoder.0.weight", "prototype_decoder.0.bias")
+        tr.adam_step("transformer", inactive)
+        if i == 0:
+            for k, v in tr.weights_numpy()["transformer"].items():
+                if k != "pos_encoder.pe":
+                    D.check(z, f"p1/{k}", v, _param_close(z, k, 1, 1e-5, 1e-6), key=k)
+        losses.append((aloss, tloss))
+    np.testing.assert_allclose(np.array(losses), z["losses"], rtol=1e-4, atol=1e-5)
+    for k, v in tr.weights_numpy()["transformer"].items():
+        if k != "pos_encoder.pe":
+            D.check(z, f"p10/{k}", v, _param_close(z, k, 10, 1e-4, 2e-5), key=k)
+    np.testing.assert_allclose(st.protos[:3], z["protos_steps"][-1], atol=1e-5)
+    assert abs(st.factor - float(z["factor_end"])) < 1e-12
+    assert st.num_zero == z["num_zero"] and st.num_ones == z["num_ones"]
+
+
+@pytest.mark.parametrize("tag,scores", [("better", [1.0, 2.0]), ("worse", [3.0, 1.0])])
+def test_gan_step_matches_reference_h50(tag, scores):
+    from preganplus_amd import train as TR
+    from tests.golden import digest as D
+    w = W.synth_weights(50, 0)
+    z = np.load(f"{GOLD}/gan_h50.npz")
+    tr = TR.Trainer(50, w)
+    it = iter(scores)
+    ns, _, _ = TR.train_gan(tr, z["emb"], z["sched"], lambda s: next(it))
+    np.testing.assert_allclose(ns, z[f"{tag}/sim_new"], rtol=1e-4, atol=1e-5)
+    pw = tr.weights_numpy()
+    for k, v in pw["gen"].items():
+        D.check(z, f"{tag}/gen/{k}", v, _dclose(1e-5, 1e-6), sum_rel=1e-5, key=k)
+    for k, v in pw["disc"].items():
+        D.check(z, f"{tag}/disc/{k}", v, _dclose(1e-5, 1e-6), sum_rel=1e-5, key=k)
+
+
+def test_dp_step_b1024_h50_matches_reference():
+    """C3's local batch: the product's data-parallel step (train.dp_tune_step)
+    on 1,024 windows at H=50 vs the reference modules under the DP loss
+    (dp_h50_b1024.npz): per-window losses, every transformer gradient, and the
+    state after the step (prototype EMA increments, counters, factor)."""
+    from preganplus_amd import train as TR
+    from tests.golden import digest as D
+    from tests.test_train_oracle_golden import dp_inputs
+    H = 50
+    w = W.synth_weights(H, 0)
+    z = np.load(f"{GOLD}/dp_h50_b1024.npz")
+    x, y, c = dp_inputs(z), z["y"], z["c"]
+    B = y.shape[0]
+    tr = TR.Trainer(H, w, max_batch=B)
+    st = TR.TuneState(w["prototypes"], float(z["factor"]))
+    st.num_zero, st.num_ones = float(z["num_zero"]), float(z["num_ones"])
+    p0 = st.protos.copy()
+    aloss, tloss = TR.dp_tune_step(tr, st, x.astype(np.float32), y, c)
+    np.testing.assert_allclose(np.stack([aloss, tloss], 1), z["losses"], rtol=1e-4, atol=2e-3)
+    g = tr.G.cpu().numpy()
+    for t in tr.tensors:
+        if t["section"] == "transformer" and t["trainable"]:
+            D.check(z, f"grad/{t['name']}", g[t["offset"]:t["offset"] + t["n"]].reshape(
+                w["transformer"][t["name"]].shape), _dclose(1e-3, 1e-4), sum_rel=1e-4, key=t["name"])
+    cnt = z["count"]
+    want = p0.copy()
+    want[:3] += z["delta"] / np.maximum(cnt, 1)[:, None]
+    np.testing.assert_allclose(st.protos, want, atol=1e-5)
+    assert st.num_zero == z["num_zero"] + B * H and st.num_ones == z["num_ones"] + y.sum()
+    assert abs(st.factor - float(z["factor"]) * 0.995 ** B) < 1e-12
+
+
+def test_gan_step_b1024_h50_matches_reference():
+    """The batched GAN step at C3's local batch vs the reference Gen_50/Disc_50
+    over the same 1,024 windows: new schedules, Disc gradients (per-window BCE
+    targets) and Gen gradients (BCE toward [0, 1] through the Disc)."""
+    from preganplus_amd import train as TR
+    from tests.golden import digest as D
+    H = 50
+    w = W.synth_weights(H, 0)
+    z = np.load(f"{GOLD}/dp_h50_b1024.npz")
+    emb, sidx, target = z["gan/emb"], z["gan/sidx"], z["gan/target"]
+    B = emb.shape[0]
+    s = np.zeros((B, H, H), np.float32)
+    s[np.arange(B)[:, None], np.arange(H)[None, :], sidx] = 1.0
+    tr = TR.Trainer(H, w, max_batch=B)
+    ns, _ = tr.gan_forward(emb, s)
+    D.check(z, "gan/ns", ns.cpu().numpy(), _dclose(1e-4, 1e-5), sum_rel=1e-5)
+    tr.gan_disc_backward(target)
+    tr.gan_gen_backward(B)
+    g = tr.G.cpu().numpy()
+    for t in tr.tensors:
+        sec = {"disc": "gan/dgrad", "gen": "gan/ggrad"}.get(t["section"])
+        if sec:
+            D.check(z, f"{sec}/{t['name']}", g[t["offset"]:t["offset"] + t["n"]].reshape(
+                w[t["section"]][t["name"]].shape), _dclose(1e-3, 1e-4), sum_rel=1e-4, key=t["name"])
