@@ -232,6 +232,40 @@ int pgp_tune_backward(int n_hosts, int batch, const float* P, float* G, float* w
 int pgp_tune_targets(int n_hosts, int n_protos, const float* logits, const float* protos, const int* y, const int* cls,
                      double* state, double update_min, double decay, float* mult, float* tgt, double* loss,
                      void* stream);
+/* ---- data-parallel tuning step on the device ----
+ * pgp_tune_dataset replaces load_on_the_fly_dataset (utils.py:40-47) for a
+ * batch of E environments: series [E,R,3H] fp64 = each environment's last R
+ * rows of stats.time_series (R = LATEST_WINDOW_SIZE = 10, 3 <= R <= 16),
+ * train_max [3H] fp64 = np.max(train_time_data, axis=0); normalises
+ * (utils.py:94-95), writes the R windows per environment (convert_to_windows,
+ * utils.py:7-14) windows [E*R,3,3H] fp32, the labels of form_test_dataset
+ * (utils.py:16-24; bit-exact numpy 'linear' 98th percentile) y [E*R,H] and
+ * cls [E*R,H] int32, and, if infer != NULL, run_encoder's window of the same
+ * rows (PreGANPlus.py:107-112: [R-3, R-3, R-2]) infer [E,3,3H]. */
+int pgp_tune_dataset(int n_hosts, int n_env, int n_rows, const double* series, const double* train_max,
+                     float* windows, int* y, int* cls, float* infer, void* stream);
+/* doubles of workspace pgp_tune_targets_dp needs for a batch */
+size_t pgp_tune_targets_dp_workspace_len(int batch);
+/* custom_loss / triplet_loss (train.py:13-40) for a batch in the data-parallel
+ * form (train.loss_targets_dp; replaces its B x H host loop): every window is
+ * scored against the step-start state [2K+3] (read only); writes mult [B,H],
+ * tgt [B,H,2] (pgp_tune_backward's inputs), loss [B,2] fp64 (aloss, tloss) and
+ * the rank's state increments inc [3K+3] fp64 = prototype-EMA deltas [K][2]
+ * (f (a - P[c]) per qualifying host, f = factor + update_min), their counts [K],
+ * num_zero, num_ones, windows — the buffer the ranks all-reduce (sum). */
+int pgp_tune_targets_dp(int n_hosts, int n_protos, int batch, const float* logits, const float* protos, const int* y,
+                        const int* cls, const double* state, double update_min, float* mult, float* tgt, double* loss,
+                        double* inc, double* workspace, void* stream);
+/* train.dp_state_update after the all-reduce, on the device: state [2K+3] +=
+ * the summed increments (each prototype moves by the mean of its deltas, the
+ * factor decays by decay^windows).  AdamW activity of the n_cond tensors that
+ * torch skips when no window of the global batch has a positive label (the
+ * prototype decoder, train.py:51-54 -> torch.optim.AdamW): their step counts
+ * cond_steps [n_cond] fp64 live on the device; rows cond_rows[i] of the
+ * pgp_adamw_table table [T,3] get (active, lr/(1-beta1^step), sqrt(1-beta2^step)). */
+int pgp_tune_state_apply(int n_protos, double* state, const double* inc, double decay, int n_cond,
+                         const int* cond_rows, double* cond_steps, float* adam_table, double lr, double beta1,
+                         double beta2, void* stream);
 /* emb [B,2H] (masked prototype embeddings), sched [B,H,H]; outputs the new
  * schedule ns [B,H,H] and probs [B,2]; workspace pgp_gan_workspace_len(H, >= B)
  * floats, shared by the three calls of one step (same batch).  The backward

@@ -12,6 +12,7 @@
 #include "pgp_pack.hpp"
 #include "pgp_train.hpp"
 #include "pgp_tune.hpp"
+#include "pgp_tunedp.hpp"
 
 #include <vector>
 
@@ -354,6 +355,50 @@ int pgp_tune_targets(int n_hosts, int n_protos, const float* logits, const float
     return fail(PGP_ERR_ARG, "bad tune_targets arguments");
   HIPCHK(launch_tune_targets(n_hosts, n_protos, logits, protos, y, cls, state, update_min, decay, mult, tgt, loss,
                              reinterpret_cast<hipStream_t>(stream)));
+  return PGP_OK;
+}
+
+int pgp_tune_dataset(int n_hosts, int n_env, int n_rows, const double* series, const double* train_max,
+                     float* windows, int* y, int* cls, float* infer, void* stream) {
+  if (n_hosts <= 0 || n_hosts > 64) return fail(PGP_ERR_UNSUPPORTED, "host count");
+  if (n_env < 0 || n_rows < 3 || n_rows > kMaxTuneRows) return fail(PGP_ERR_ARG, "n_env >= 0, 3 <= n_rows <= 16");
+  if (n_env == 0) return PGP_OK;
+  if (!series || !train_max || !windows || !y || !cls) return fail(PGP_ERR_ARG, "bad tune_dataset arguments");
+  HIPCHK(launch_tune_dataset(n_hosts, n_env, n_rows, series, train_max, windows, y, cls, infer,
+                             reinterpret_cast<hipStream_t>(stream)));
+  return PGP_OK;
+}
+
+size_t pgp_tune_targets_dp_workspace_len(int batch) {
+  return batch > 0 ? (size_t)tune_dp_workspace_doubles(batch) : 0;
+}
+
+int pgp_tune_targets_dp(int n_hosts, int n_protos, int batch, const float* logits, const float* protos, const int* y,
+                        const int* cls, const double* state, double update_min, float* mult, float* tgt, double* loss,
+                        double* inc, double* workspace, void* stream) {
+  if (n_hosts <= 0 || n_hosts > 64) return fail(PGP_ERR_UNSUPPORTED, "host count");
+  if (n_protos < 3 || n_protos > kMaxProtos) return fail(PGP_ERR_ARG, "triplet_loss needs prototypes 0-2");
+  if (batch <= 0 || !logits || !protos || !y || !cls || !state || !mult || !tgt || !loss || !inc || !workspace)
+    return fail(PGP_ERR_ARG, "bad tune_targets_dp arguments");
+  HIPCHK(launch_tune_targets_dp(n_hosts, n_protos, batch, logits, protos, y, cls, state, update_min, mult, tgt, loss,
+                                inc, workspace, reinterpret_cast<hipStream_t>(stream)));
+  return PGP_OK;
+}
+
+int pgp_tune_state_apply(int n_protos, double* state, const double* inc, double decay, int n_cond,
+                         const int* cond_rows, double* cond_steps, float* adam_table, double lr, double beta1,
+                         double beta2, void* stream) {
+  if (n_protos < 3 || n_protos > kMaxProtos || !state || !inc) return fail(PGP_ERR_ARG, "bad state arguments");
+  if (n_cond < 0 || n_cond > kMaxCond || (n_cond > 0 && (!cond_rows || !cond_steps || !adam_table)))
+    return fail(PGP_ERR_ARG, "bad AdamW condition arguments");
+  CondRows cr{};
+  cr.n = n_cond;
+  for (int i = 0; i < n_cond; ++i) {
+    if (cond_rows[i] < 0 || cond_rows[i] >= kMaxTensors) return fail(PGP_ERR_ARG, "AdamW table row out of range");
+    cr.row[i] = cond_rows[i];
+  }
+  HIPCHK(launch_tune_state_apply(n_protos, state, inc, decay, cr, cond_steps, adam_table, lr, beta1, beta2,
+                                 reinterpret_cast<hipStream_t>(stream)));
   return PGP_OK;
 }
 

@@ -1,0 +1,238 @@
+// pgp_tunedp.hip — the data-parallel tuning step's bookkeeping on the device
+// (BASELINE config C3), so that one step of the semi-supervised
+// tuning (tune_model, PreGANPlus.py:51-58) over a batch of environments needs
+// no host round trip:
+//
+//   tune_dataset_kernel     load_on_the_fly_dataset (utils.py:40-47): the last
+//                           n rows of each environment's series, normalised by
+//                           the training series' column max (utils.py:94-95),
+//                           cut into windows (convert_to_windows, utils.py:7-14)
+//                           and labelled by form_test_dataset (utils.py:16-24:
+//                           98th percentile per column, numpy 'linear'
+//                           interpolation; class = first argmax of the host's 3
+//                           columns); plus run_encoder's inference window of the
+//                           same rows (PreGANPlus.py:107-112)
+//   tune_targets_dp_kernel  custom_loss / triplet_loss (train.py:13-40) in the
+//                           data-parallel form of train.loss_targets_dp: every
+//                           window scored against the step-START state; CE
+//                           weights, positive targets, per-window losses and the
+//                           state increments (prototype-EMA deltas f(a - P[c]) and
+//                           counts, num_zero / num_ones, windows)
+//   tune_dp_finish_kernel   the increments summed over the batch in a fixed order
+//                           (deterministic; the rank's buffer for the all-reduce)
+//   tune_state_apply_kernel train.dp_state_update after the all-reduce: each
+//                           prototype moves by the mean of its deltas, counters
+//                           add, the factor decays once per window; and the AdamW
+//                           table rows of the prototype decoder, which torch skips
+//                           when no window of the global batch has a positive
+//                           label (their step counts live on the device)
+//
+// All fp64 with FMA contraction off, in the numpy restatement's operation order
+// per value (labels and CE weights bit-identical to it; sums over the batch are
+// tree-ordered, equal to fp64 rounding).
+#include <hip/hip_runtime.h>
+
+#include "pgp_device.hpp"
+#include "pgp_tunedp.hpp"
+
+namespace pgp {
+namespace {
+
+constexpr int kWin = 3;  // models.py:320 n_window
+
+// ---------------------------------------------------------------------------
+// dataset: one thread per (environment, host)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void tune_dataset_kernel(int H, int E, int R, const double* __restrict__ series,
+                                                           const double* __restrict__ train_max,
+                                                           float* __restrict__ windows, int* __restrict__ y,
+                                                           int* __restrict__ cls, float* __restrict__ infer) {
+#pragma clang fp contract(off)
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (long)E * H) return;
+  const int e = (int)(t / H), h = (int)(t % H);
+  const int F = 3 * H;
+  double v[kMaxTuneRows][3];  // normalised rows x the host's 3 columns
+  for (int c = 0; c < 3; ++c) {
+    const double den = train_max[3 * h + c] + 1e-8;  // np.max(train, axis=0) + 1e-8
+    for (int r = 0; r < R; ++r) v[r][c] = series[((long)e * R + r) * F + 3 * h + c] / den;
+  }
+  // 98th percentile per column, numpy 'linear': virtual index (R-1)*0.98,
+  // gamma = frac, lerp(a, b, g) = g >= 0.5 ? b - (b-a)(1-g) : a + (b-a) g
+  const double vi = (double)(R - 1) * (98.0 / 100.0);
+  const double lo = floor(vi);
+  const double gm = vi - lo;
+  const int ilo = (int)lo, ihi = ilo + 1 < R ? ilo + 1 : R - 1;
+  double thr[3];
+  for (int c = 0; c < 3; ++c) {
+    double s[kMaxTuneRows];
+    for (int r = 0; r < R; ++r) {  // insertion sort (R <= 16)
+      double x = v[r][c];
+      int k = r;
+      while (k > 0 && s[k - 1] > x) {
+        s[k] = s[k - 1];
+        --k;
+      }
+      s[k] = x;
+    }
+    const double a = s[ilo], b = s[ihi], d = b - a;
+    thr[c] = gm >= 0.5 ? b - d * (1.0 - gm) : a + d * gm;
+  }
+  for (int r = 0; r < R; ++r) {
+    const bool an = v[r][0] > thr[0] || v[r][1] > thr[1] || v[r][2] > thr[2];
+    int am = 0;  // np.argmax: first maximum
+    if (v[r][1] > v[r][am]) am = 1;
+    if (v[r][2] > v[r][am]) am = 2;
+    y[((long)e * R + r) * H + h] = an ? 1 : 0;
+    cls[((long)e * R + r) * H + h] = am;
+    // convert_to_windows: window r = rows r-3..r-1, row 0 repeated for r < 3
+    for (int w = 0; w < kWin; ++w) {
+      const int src = r >= kWin ? r - kWin + w : (w < kWin - r ? 0 : w - (kWin - r));
+      float* o = windows + (((long)e * R + r) * kWin + w) * F + 3 * h;
+      for (int c = 0; c < 3; ++c) o[c] = (float)v[src][c];
+    }
+  }
+  if (infer) {  // run_encoder: last 3 rows -> convert_to_windows(...)[-1] = [R-3, R-3, R-2]
+    const int rows[kWin] = {R - 3, R - 3, R - 2};
+    for (int w = 0; w < kWin; ++w)
+      for (int c = 0; c < 3; ++c) infer[((long)e * kWin + w) * F + 3 * h + c] = (float)v[rows[w]][c];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// targets: one thread per window, block partials of the increments
+// ---------------------------------------------------------------------------
+constexpr int kTB = 256;
+__global__ __launch_bounds__(kTB) void tune_targets_dp_kernel(int H, int B, const float* __restrict__ logits,
+                                                              const float* __restrict__ protos,
+                                                              const int* __restrict__ y, const int* __restrict__ cls,
+                                                              const double* __restrict__ state, int K, double update_min,
+                                                              float* __restrict__ mult, float* __restrict__ tgt,
+                                                              double* __restrict__ loss, double* __restrict__ part) {
+#pragma clang fp contract(off)
+  __shared__ double red[kDpInc][kTB];
+  const int b = blockIdx.x * kTB + threadIdx.x;
+  double acc[kDpInc] = {};  // delta[3][2], count[3], ones
+  if (b < B) {
+    const double* P = state;
+    const double ratio = state[2 * K + 1] / state[2 * K + 2];  // num_zero / num_ones at the step start
+    const double f = state[2 * K] + update_min;               // PROTO_UPDATE_FACTOR + PROTO_UPDATE_MIN
+    double aloss = 0.0, tloss = 0.0;
+    for (int i = 0; i < H; ++i) {
+      const long o = (long)b * H + i;
+      const int yi = y[o];
+      const double mu = yi == 0 ? 1.0 : ratio;
+      mult[o] = (float)mu;
+      const double l0 = logits[2 * o], l1 = logits[2 * o + 1];
+      const double m = fmax(l0, l1);
+      aloss += (log(exp(l0 - m) + exp(l1 - m)) + m - (yi ? l1 : l0)) * mu;
+      acc[9] += yi == 1 ? 1.0 : 0.0;
+      if (yi > 0) {
+        const int cc = cls[o];
+        const double a0 = protos[2 * o], a1 = protos[2 * o + 1];
+        tgt[2 * o] = (float)P[2 * cc];
+        tgt[2 * o + 1] = (float)P[2 * cc + 1];
+        double mse[3];
+        for (int k = 0; k < 3; ++k) {
+          const double d0 = a0 - P[2 * k], d1 = a1 - P[2 * k + 1];
+          mse[k] = (d0 * d0 + d1 * d1) / 2.0;
+        }
+        const double pos = mse[cc];
+        const double n0 = mse[cc == 0 ? 1 : 0], n1 = mse[cc == 2 ? 1 : 2];
+        tloss += pos - (n0 + n1);
+        if (pos <= n0 && pos <= n1) {
+          acc[2 * cc] += f * (a0 - P[2 * cc]);
+          acc[2 * cc + 1] += f * (a1 - P[2 * cc + 1]);
+          acc[6 + cc] += 1.0;
+        }
+      } else {
+        tgt[2 * o] = 0.f;
+        tgt[2 * o + 1] = 0.f;
+      }
+    }
+    loss[2 * b] = aloss;
+    loss[2 * b + 1] = tloss;
+  }
+  for (int k = 0; k < kDpInc; ++k) red[k][threadIdx.x] = acc[k];
+  __syncthreads();
+  for (int s = kTB / 2; s > 0; s >>= 1) {  // fixed tree order
+    if (threadIdx.x < s)
+      for (int k = 0; k < kDpInc; ++k) red[k][threadIdx.x] += red[k][threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x < kDpInc) part[(long)blockIdx.x * kDpInc + threadIdx.x] = red[threadIdx.x][0];
+}
+
+// increments [3K+3] = delta [K][2], count [K], num_zero, num_ones, windows
+__global__ void tune_dp_finish_kernel(int H, int B, int K, int nblk, const double* __restrict__ part,
+                                      double* __restrict__ inc) {
+#pragma clang fp contract(off)
+  const int k = threadIdx.x;
+  if (k >= 3 * K + 3) return;
+  double v = 0.0;
+  int src = -1;
+  if (k < 6) src = k;                              // delta rows 0-2 (triplet classes)
+  else if (k >= 2 * K && k < 2 * K + 3) src = 6 + (k - 2 * K);  // counts 0-2
+  else if (k == 3 * K + 1) src = 9;                // num_ones
+  if (src >= 0)
+    for (int i = 0; i < nblk; ++i) v += part[(long)i * kDpInc + src];
+  if (k == 3 * K) v = (double)H * (double)B;       // num_zero: every host counts (train.py:31)
+  if (k == 3 * K + 2) v = (double)B;               // windows
+  inc[k] = v;
+}
+
+__global__ void tune_state_apply_kernel(int K, double* __restrict__ state, const double* __restrict__ inc, double decay,
+                                        CondRows cr, double* __restrict__ dsteps, float* __restrict__ table, double lr,
+                                        double b1, double b2) {
+#pragma clang fp contract(off)
+  if (threadIdx.x != 0) return;
+  for (int c = 0; c < K; ++c) {
+    const double n = inc[2 * K + c];
+    if (n > 0) {
+      state[2 * c] += inc[2 * c] / n;
+      state[2 * c + 1] += inc[2 * c + 1] / n;
+    }
+  }
+  state[2 * K + 1] += inc[3 * K];
+  state[2 * K + 2] += inc[3 * K + 1];
+  state[2 * K] *= pow(decay, inc[3 * K + 2]);
+  const bool active = inc[3 * K + 1] > 0;  // a positive label somewhere in the global batch
+  for (int i = 0; i < cr.n; ++i) {
+    if (active) dsteps[i] += 1.0;
+    const double s = dsteps[i] > 1.0 ? dsteps[i] : 1.0;
+    float* r = table + 3 * cr.row[i];
+    r[0] = active ? 1.f : 0.f;
+    r[1] = (float)(lr / (1.0 - pow(b1, s)));
+    r[2] = (float)sqrt(1.0 - pow(b2, s));
+  }
+}
+
+}  // namespace
+
+hipError_t launch_tune_dataset(int H, int E, int R, const double* series, const double* train_max, float* windows,
+                               int* y, int* cls, float* infer, hipStream_t st) {
+  const long n = (long)E * H;
+  tune_dataset_kernel<<<(int)((n + 255) / 256), 256, 0, st>>>(H, E, R, series, train_max, windows, y, cls, infer);
+  return hipGetLastError();
+}
+
+long tune_dp_workspace_doubles(int B) { return (long)((B + kTB - 1) / kTB) * kDpInc; }
+
+hipError_t launch_tune_targets_dp(int H, int K, int B, const float* logits, const float* protos, const int* y,
+                                  const int* cls, const double* state, double update_min, float* mult, float* tgt,
+                                  double* loss, double* inc, double* ws, hipStream_t st) {
+  const int nblk = (B + kTB - 1) / kTB;
+  tune_targets_dp_kernel<<<nblk, kTB, 0, st>>>(H, B, logits, protos, y, cls, state, K, update_min, mult, tgt, loss, ws);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  tune_dp_finish_kernel<<<1, 64 * ((3 * K + 3 + 63) / 64), 0, st>>>(H, B, K, nblk, ws, inc);
+  return hipGetLastError();
+}
+
+hipError_t launch_tune_state_apply(int K, double* state, const double* inc, double decay, const CondRows& cr,
+                                   double* dsteps, float* table, double lr, double b1, double b2, hipStream_t st) {
+  tune_state_apply_kernel<<<1, 64, 0, st>>>(K, state, inc, decay, cr, dsteps, table, lr, b1, b2);
+  return hipGetLastError();
+}
+
+}  // namespace pgp

@@ -115,9 +115,16 @@ class Trainer:
         L.pgp_tune_targets.argtypes = [i32, i32] + [vp] * 5 + [ctypes.c_double] * 2 + [vp] * 3 + [vp]
         L.pgp_adamw_table.argtypes = ([vp] * 4 + [ctypes.c_float] * 5 + [ctypes.POINTER(_AdamTensor), i32, vp]
                                       + [vp])
+        dbl = ctypes.c_double
+        L.pgp_tune_dataset.argtypes = [i32, i32, i32] + [vp] * 6 + [vp]
+        L.pgp_tune_targets_dp_workspace_len.argtypes = [i32]
+        L.pgp_tune_targets_dp_workspace_len.restype = sz
+        L.pgp_tune_targets_dp.argtypes = [i32, i32, i32] + [vp] * 5 + [dbl] + [vp] * 5 + [vp]
+        L.pgp_tune_state_apply.argtypes = [i32, vp, vp, dbl, i32, ctypes.POINTER(ctypes.c_int), vp, vp,
+                                           dbl, dbl, dbl, vp]
         for f in ("pgp_tune_forward", "pgp_tune_backward", "pgp_gan_forward", "pgp_gan_disc_backward",
                   "pgp_gan_gen_backward", "pgp_adamw", "pgp_load_weights_master", "pgp_tune_targets",
-                  "pgp_adamw_table"):
+                  "pgp_adamw_table", "pgp_tune_dataset", "pgp_tune_targets_dp", "pgp_tune_state_apply"):
             getattr(L, f).restype = i32
         L._pgp_train_bound = True
 
@@ -430,24 +437,140 @@ def dp_state_update(st: TuneState, inc: TuneIncrements, group=None):
     return tot
 
 
+def dataset_buffers(tr: "Trainer", E: int, R: int = LATEST_WINDOW_SIZE):
+    """Preallocated outputs of tune_dataset for E environments of R rows."""
+    H, dev = tr.H, tr.device
+    return (torch.empty((E * R, 3, 3 * H), dtype=torch.float32, device=dev),
+            torch.empty((E * R, H), dtype=torch.int32, device=dev),
+            torch.empty((E * R, H), dtype=torch.int32, device=dev),
+            torch.empty((E, 3, 3 * H), dtype=torch.float32, device=dev))
+
+
+def tune_dataset(tr: "Trainer", series, train_max, infer: bool = True, out=None):
+    """load_on_the_fly_dataset (utils.py:40-47) for a batch of environments on
+    the device (``pgp_tune_dataset``): series [E,R,3H] fp64 (each environment's
+    last R rows of stats.time_series), train_max [3H] fp64 = the training
+    series' column max.  Returns windows [E*R,3,3H] fp32, y / cls [E*R,H] int32
+    (form_test_dataset, utils.py:16-24) and run_encoder's window [E,3,3H] of the
+    same rows (PreGANPlus.py:107-112) or None."""
+    series = tr._dev(series, torch.float64)
+    train_max = tr._dev(train_max, torch.float64)
+    E, R, F = series.shape
+    H = tr.H
+    if F != 3 * H:
+        raise ValueError(f"series must be [E,R,{3 * H}]")
+    wins, y, cls, inf = out if out is not None else dataset_buffers(tr, E, R)
+    if tuple(wins.shape) != (E * R, 3, F) or tuple(y.shape) != (E * R, H) or tuple(inf.shape) != (E, 3, F):
+        raise ValueError("tune_dataset: output buffers do not match the series")
+    inf = inf if infer else None
+    _native.check(tr._L.pgp_tune_dataset(H, E, R, series.data_ptr(), train_max.data_ptr(), wins.data_ptr(),
+                                         y.data_ptr(), cls.data_ptr(), None if inf is None else inf.data_ptr(),
+                                         tr._stream()), "pgp_tune_dataset")
+    return wins, y, cls, inf
+
+
+class DPTuner:
+    """The data-parallel tuning step with its state on the device (SURVEY §8e,
+    config C3): forward, custom_loss / triplet_loss bookkeeping against the
+    step-start state (``pgp_tune_targets_dp``), backward, ONE gradient
+    all-reduce and ONE all-reduce of the 3K+3 fp64 state increments (device
+    buffers, RCCL), the state update and AdamW from a device table
+    (``pgp_tune_state_apply`` decides the prototype decoder's activity there).
+    No host round trip: the step is launch-only.  ``loss_targets_dp`` /
+    ``dp_state_update`` are the same semantics in numpy (the tests restate with
+    them).  ``sync(st)`` copies the state back to a host ``TuneState`` and the
+    AdamW step counts back to the Trainer."""
+
+    COND = ("prototype_decoder.0.weight", "prototype_decoder.0.bias")
+    CHUNK = 64   # AdamW table rows precomputed per upload
+
+    def __init__(self, tr: "Trainer", st: TuneState, max_batch: int, group=None):
+        self.tr, self.group = tr, group
+        H, dev, L = tr.H, tr.device, tr._L
+        self.K = st.protos.shape[0]
+        tr._ensure(max_batch)
+        self.cap = max_batch
+        self.state = st.to_device(dev)
+        self.mult = torch.zeros((max_batch, H), dtype=torch.float32, device=dev)
+        self.tgt = torch.zeros((max_batch, H, 2), dtype=torch.float32, device=dev)
+        self.loss = torch.zeros((max_batch, 2), dtype=torch.float64, device=dev)
+        self.inc = torch.zeros(3 * self.K + 3, dtype=torch.float64, device=dev)
+        self.ws = torch.zeros(max(int(L.pgp_tune_targets_dp_workspace_len(max_batch)), 1), dtype=torch.float64,
+                              device=dev)
+        self.sel = [t for t in tr.tensors if t["section"] == "transformer" and t["trainable"]]
+        self.cond = [k for k, t in enumerate(self.sel) if t["name"] in self.COND]
+        self.cond_rows = (ctypes.c_int * len(self.cond))(*self.cond)
+        self.cond_steps = torch.tensor([self.sel[k]["step"] for k in self.cond], dtype=torch.float64, device=dev)
+        self.base = [t["step"] for t in self.sel]
+        self.n = 0
+        self.table = torch.zeros((self.CHUNK, len(self.sel), 3), dtype=torch.float32, device=dev)
+
+    def _fill_table(self):
+        """Rows (active, lr/(1-b1^step), sqrt(1-b2^step)) of the next CHUNK
+        steps for the always-active tensors (their step counts are known ahead);
+        the prototype decoder's rows are written per step on the device."""
+        tr = self.tr
+        lr = tr.lrs["transformer"]
+        tab = np.zeros((self.CHUNK, len(self.sel), 3), dtype=np.float32)
+        for i in range(self.CHUNK):
+            for k, b in enumerate(self.base):
+                stp = max(b + self.n + i + 1, 1.0)
+                tab[i, k] = (1.0, lr / (1 - tr.b1 ** stp), math.sqrt(1 - tr.b2 ** stp))
+        self.table.copy_(torch.from_numpy(tab).pin_memory(), non_blocking=True)
+
+    def step(self, wins: torch.Tensor, y: torch.Tensor, cls: torch.Tensor):
+        """wins [B,3,3H] fp32, y / cls [B,H] int32, all on the device.
+        Returns the per-window (aloss, tloss) [B,2] fp64 device view."""
+        import torch.distributed as dist
+        tr, L = self.tr, self.tr._L
+        B = wins.shape[0]
+        if B > self.cap:
+            raise ValueError(f"batch {B} > DPTuner capacity {self.cap}")
+        if y.dtype != torch.int32 or cls.dtype != torch.int32 or y.device != tr.device or cls.device != tr.device:
+            raise ValueError("y / cls must be int32 device tensors")
+        i = self.n % self.CHUNK
+        if i == 0:
+            self._fill_table()
+        s = tr._stream()
+        tr.tune_forward(wins)
+        _native.check(L.pgp_tune_targets_dp(
+            tr.H, self.K, B, tr.logits.data_ptr(), tr.protos.data_ptr(), y.data_ptr(), cls.data_ptr(),
+            self.state.data_ptr(), PROTO_UPDATE_MIN, self.mult.data_ptr(), self.tgt.data_ptr(), self.loss.data_ptr(),
+            self.inc.data_ptr(), self.ws.data_ptr(), s), "pgp_tune_targets_dp")
+        tr.tune_backward(B, y, self.mult[:B], self.tgt[:B])
+        tr.all_reduce_grads("transformer", self.group)
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            dist.all_reduce(self.inc, group=self.group)
+        row = self.table[i]
+        _native.check(L.pgp_tune_state_apply(
+            self.K, self.state.data_ptr(), self.inc.data_ptr(), PROTO_FACTOR_DECAY, len(self.cond), self.cond_rows,
+            self.cond_steps.data_ptr(), row.data_ptr(), tr.lrs["transformer"], tr.b1, tr.b2, s),
+            "pgp_tune_state_apply")
+        tr.adam_step_table("transformer", self.sel, row)
+        self.n += 1
+        return self.loss[:B]
+
+    def sync(self, st: TuneState):
+        """State and AdamW step counts back to the host (one device sync)."""
+        st.from_device(self.state)
+        cs = self.cond_steps.cpu().numpy()
+        for k, t in enumerate(self.sel):
+            t["step"] = float(cs[self.cond.index(k)]) if k in self.cond else self.base[k] + self.n
+
+
 def dp_tune_step(tr: "Trainer", st: TuneState, wins, anom, cls, group=None):
-    """One data-parallel tuning step on this rank's windows:
-    forward, targets against the step-start state, backward, ONE gradient
-    all-reduce, the host state reduced over ranks, AdamW.  The loss is the
-    sum over the global batch.  Returns (aloss [B], tloss [B])."""
-    wins = torch.as_tensor(np.asarray(wins), dtype=torch.float32)
+    """One data-parallel tuning step on this rank's windows,
+    through ``DPTuner`` (device bookkeeping, device state): forward, targets
+    against the step-start state, backward, one gradient all-reduce, the state
+    increments all-reduced, AdamW.  The loss is the sum over the global batch.
+    ``st`` is updated from the device afterwards.  Returns (aloss [B], tloss [B])."""
+    wins = tr._dev(wins, torch.float32)
     B = wins.shape[0]
-    logits, protos = tr.tune_forward(wins)
-    mult, tgt, aloss, tloss, inc = loss_targets_dp(logits[:B].cpu().numpy(), protos[:B].cpu().numpy(),
-                                                   np.asarray(anom), np.asarray(cls), st)
-    tr.tune_backward(B, np.asarray(anom), mult, tgt)
-    tr.all_reduce_grads("transformer", group)
-    tot = dp_state_update(st, inc, group)
-    # no positive label in the whole global batch: the prototype decoder got no
-    # gradient and torch's AdamW skips it (as backprop does per window)
-    inactive = () if tot.num_ones > 0 else ("prototype_decoder.0.weight", "prototype_decoder.0.bias")
-    tr.adam_step("transformer", inactive)
-    return aloss, tloss
+    tun = DPTuner(tr, st, B, group)
+    loss = tun.step(wins, tr._dev(anom, torch.int32), tr._dev(cls, torch.int32))
+    tun.sync(st)
+    out = loss.cpu().numpy()
+    return out[:, 0].copy(), out[:, 1].copy()
 
 
 def normalize_test_time_data(time_data, train_time_data):

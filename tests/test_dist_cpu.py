@@ -1,10 +1,11 @@
 """Multi-process (gloo, world_size 2, CPU) checks of the data-parallel paths.
 
 * Tuning: each rank computes the gradients of its shard of
-  windows; one flat all-reduce (sum) of the gradient buffer — the exact call
-  Trainer.all_reduce_grads makes (RCCL on the GPU box, gloo here) — equals the
-  gradient of the concatenated batch.  Gradients come from the torch training
-  oracle (no GPU here).
+  windows; Trainer.all_reduce_grads (the product's call: one flat all-reduce,
+  RCCL on the GPU box, gloo here) over a Trainer whose buffer holds them
+  equals the gradient of the concatenated batch.  Gradients come from the
+  torch training oracle (no GPU here); tests/test_gpu_dist.py runs the whole
+  product step (train.dp_tune_step) with two ranks on the GPU.
 * Inference sharding: bench.py gives every rank its own independent windows;
   the per-rank seeds differ and no collective touches the data path.
 """
@@ -42,6 +43,17 @@ def _inputs():
     return x, y, mult, tgt
 
 
+def _stub_trainer(g):
+    """A Trainer whose gradient buffer is `g` (the oracle's gradients; no GPU
+    here), with a gen section after the transformer one that must stay local."""
+    from preganplus_amd import train as TR
+    tr = TR.Trainer.__new__(TR.Trainer)
+    n = g.numel()
+    tr.G = torch.cat([g, torch.full((5,), 7.0, dtype=g.dtype)])
+    tr.sec_off, tr.sec_end = {"transformer": 0, "gen": n}, {"transformer": n, "gen": n + 5}
+    return tr
+
+
 def _worker(rank, world, port, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -50,9 +62,10 @@ def _worker(rank, world, port, q):
     x, y, mult, tgt = _inputs()
     sl = slice(rank * B // world, (rank + 1) * B // world)
     g = _batch_grads(w, x[sl], y[sl], mult[sl], tgt[sl])
-    dist.all_reduce(g)  # Trainer.all_reduce_grads: one flat SUM all-reduce
+    tr = _stub_trainer(g)
+    tr.all_reduce_grads("transformer")  # the product's call: one flat SUM all-reduce
     if rank == 0:
-        q.put(g.numpy())
+        q.put(tr.G.numpy())
     dist.destroy_process_group()
 
 
@@ -69,7 +82,8 @@ def test_dp_gradient_allreduce_equals_full_batch():
         assert p.exitcode == 0
     w = W.synth_weights(H, seed=1)
     g_full = _batch_grads(w, *_inputs()).numpy()
-    np.testing.assert_allclose(g_dp, g_full, rtol=1e-10, atol=1e-12)
+    np.testing.assert_allclose(g_dp[:-5], g_full, rtol=1e-10, atol=1e-12)
+    assert np.all(g_dp[-5:] == 7.0)  # only the named section is reduced
 
 
 def test_trainer_allreduce_is_noop_without_process_group():

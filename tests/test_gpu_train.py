@@ -229,7 +229,8 @@ def test_batched_gan_step_matches_autograd(H, B):
 def test_dp_tune_step_single_rank():
     """dp_tune_step on one rank == its pieces run by hand:
     forward, loss_targets_dp on the step-start state, backward, AdamW, state
-    update; parameters bit-identical, state updated."""
+    update; parameters bit-identical, state updated (device bookkeeping,
+    DPTuner, vs the numpy restatement)."""
     from preganplus_amd import train as TR
     H, B = 16, 12
     w = W.synth_weights(H, seed=6)
@@ -248,7 +249,8 @@ def test_dp_tune_step_single_rank():
     TR.dp_state_update(s2, inc)
     torch.cuda.synchronize()
     assert torch.equal(t1.P, t2.P)
-    np.testing.assert_array_equal(s1.protos, s2.protos)
+    # the device sums the batch's EMA deltas in a tree order, numpy sequentially
+    np.testing.assert_allclose(s1.protos, s2.protos, rtol=1e-13, atol=1e-15)
     assert not np.array_equal(s1.protos, p0) and s1.num_ones > 1
 
 
