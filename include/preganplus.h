@@ -137,7 +137,8 @@ int pgp_forward_stage(pgp_model* m, int stage, int batch, const float* windows,
 /* recover_decision's container moves (PreGANPlus.py:87-105, PreGAN.py:77-95)
  * for a batch, from pgp_forward's keep_orig / final_target (device pointers):
  *   in  cur_host  [B,C] current host of container c, -1 = unplaced or None
- *                       (the containerlist filter, PreGANPlus.py:92-95)
+ *                       (the containerlist filter, PreGANPlus.py:92-95); any
+ *                       value outside [0, C) is treated as unplaced
  *   out moves     [B,C] new host where final_target != cur_host and the
  *                       discriminator did not keep the original, else -1
  *   out hosts_from[B,H] 1 for every host a container moves away from
@@ -276,6 +277,11 @@ int pgp_gan_forward(int n_hosts, int batch, const float* emb, const float* sched
 int pgp_gan_disc_backward(int n_hosts, int batch, const float* target, const float* P, float* G, float* workspace,
                           void* stream);
 int pgp_gan_gen_backward(int n_hosts, int batch, const float* P, float* G, float* workspace, void* stream);
+/* probs [B,2] of the last Disc head evaluated in the workspace: after
+ * pgp_gan_gen_backward, the updated Disc's probabilities of the generator's
+ * schedule, whose BCE toward [0,1] is gen_loss (PreGANPlus.py:69-73; the
+ * reference appends (gen_loss, disc_loss) to accuracy_list, :77). */
+int pgp_gan_probs(int n_hosts, int batch, const float* workspace, float* probs, void* stream);
 
 typedef struct {
   long long offset;  /* first element of the tensor in P/G/m/v */

@@ -435,6 +435,14 @@ int pgp_gan_gen_backward(int n_hosts, int batch, const float* P, float* G, float
   return PGP_OK;
 }
 
+int pgp_gan_probs(int n_hosts, int batch, const float* workspace, float* probs, void* stream) {
+  if (!supported(n_hosts)) return fail(PGP_ERR_UNSUPPORTED, "host count");
+  if (batch < 0 || (batch > 0 && (!workspace || !probs))) return fail(PGP_ERR_ARG, "bad arguments");
+  if (batch == 0) return PGP_OK;
+  HIPCHK(launch_gan_probs(n_hosts, batch, workspace, probs, reinterpret_cast<hipStream_t>(stream)));
+  return PGP_OK;
+}
+
 int pgp_adamw(float* P, const float* G, float* exp_avg, float* exp_avg_sq, float lr, float weight_decay,
               float beta1, float beta2, float eps, const pgp_adam_tensor* tensors, int ntensors, void* stream) {
   if (!P || !G || !exp_avg || !exp_avg_sq || !tensors || ntensors < 0 || ntensors > kMaxTensors)

@@ -2,11 +2,12 @@
 // (recovery/PreGANPlus.py:87-105, recovery/PreGAN.py:77-95) for a batch of
 // windows, from K3's keep_orig / final_target and the current placement.
 //   keep_orig[b]          -> no change (the original decision stands)
-//   cur_host[b,c] == -1   -> unplaced / None container: not considered
+//   cur_host[b,c] == -1   -> unplaced / None container: not considered (so is any
+//                            host index outside [0, C): it is never written through)
 //   final_target != cur   -> moves[b,c] = final_target, hosts_from[b,cur] = 1
 // Integer work over C = H containers per window: one lane per (window,
-// container); hosts_from is a per-window OR, formed with a 64-bit ballot per
-// host inside the wave and one atomicOr per set bit.
+// container); hosts_from is a per-window OR, one atomicOr per moving container
+// (after a zeroing pass).
 #include "pgp_device.hpp"
 
 namespace pgp {
@@ -20,7 +21,7 @@ __global__ __launch_bounds__(256) void decide_kernel(int B, int C, const int* __
   const long b = i / C;
   const int h = cur[i];
   const int t = target[i];
-  const bool mv = !keep[b] && h >= 0 && t != h;
+  const bool mv = !keep[b] && h >= 0 && h < C && t != h;
   moves[i] = mv ? t : -1;
   if (mv) atomicOr(hosts_from + b * C + h, 1);
 }

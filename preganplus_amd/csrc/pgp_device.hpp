@@ -70,6 +70,7 @@ hipError_t launch_gan_disc_bwd(int H, int B, const float* target, const float* P
                                hipStream_t st);
 hipError_t launch_gan_gen_bwd(int H, int B, const float* Pg, const float* Pd, float* Gdg, float* ws,
                               hipStream_t st);
+hipError_t launch_gan_probs(int H, int B, const float* ws, float* probs, hipStream_t st);
 
 #ifdef __HIP_DEVICE_COMPILE__
 #define PGP_DEV __device__ __forceinline__

@@ -369,7 +369,36 @@ hipError_t gan_gen_bwd_h(int B, const float* Pg, const float* Pd, float* Gdg, fl
                    ws + gp.part, st);
 }
 
+// the Disc probabilities the last disc_head_kernel left in the window rows (after
+// pgp_gan_gen_backward: the updated Disc's, i.e. gen_loss's, PreGANPlus.py:71-73)
+template <int H>
+__global__ void gan_probs_kernel(int B, const float* __restrict__ scr, float* __restrict__ probs) {
+  using G = TGeo<H>;
+  const long b = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  probs[2 * b] = scr[b * G::GS_SIZE + G::GS_P];
+  probs[2 * b + 1] = scr[b * G::GS_SIZE + G::GS_P + 1];
+}
+
+template <int H>
+hipError_t gan_probs_h(int B, const float* ws, float* probs, hipStream_t st) {
+  const GanPlan gp = gan_plan_h<H>(B);
+  GCK((gan_probs_kernel<H><<<(B + 255) / 256, 256, 0, st>>>(B, ws + gp.rows, probs)));
+  return hipSuccess;
+}
+
 }  // namespace
+
+hipError_t launch_gan_probs(int H, int B, const float* ws, float* probs, hipStream_t st) {
+  switch (H) {
+#define CASE(h) \
+  case h:       \
+    return gan_probs_h<h>(B, ws, probs, st);
+    PGP_FOR_EACH_H(CASE)
+#undef CASE
+  }
+  return hipErrorInvalidValue;
+}
 
 long gan_workspace_floats(int H, int B) {
   if (B < 1) return 0;

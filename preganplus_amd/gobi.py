@@ -92,21 +92,57 @@ class GOBIOptimizer:
             pass
 
 
-class GOBIScheduler:
-    """The placement step of scheduler/GOBI.py:19-42 on the COSCO env interface
-    (hostlist[i].getCPU(), containerlist[c].getApparentIPS() / getHostID() / id)."""
+class Scheduler:
+    """The scheduler plugin interface COSCO drives (scheduler/Scheduler.py:9-38):
+    main.py:154-155 calls ``selection()``, ``placement(ids)`` and
+    ``filter_placement(decision)``; Simulator.py:118, 173-174 call
+    ``getMigrationFromHost`` / ``getMigrationToHost``.  Only these plugin methods
+    are restated; the base class's host-selection heuristics (LR / MAD / IQR
+    ..., :40-185) belong to the other schedulers, which are out of scope."""
 
-    def __init__(self, data_type="energy_latency_16", device="cuda"):
-        if data_type != "energy_latency_16":
-            raise ValueError("only the energy_latency_16 surrogate ships with the reference")
-        self.opt = GOBIOptimizer(device=device)
-        self.max_container_ips = self.opt.max_ips
-        self.hosts = H
-        self.result_cache = None
+    def __init__(self):
         self.env = None
 
     def setEnvironment(self, env):
         self.env = env
+
+    def selection(self):
+        return None
+
+    def placement(self, containerlist):
+        return None
+
+    def filter_placement(self, decision):
+        """Scheduler.py:20-25: drop decisions that keep a container in place."""
+        return [(cid, hid) for cid, hid in decision if self.env.getContainerByID(cid).getHostID() != hid]
+
+    def getMigrationFromHost(self, hostID, decision):
+        """Scheduler.py:27-32."""
+        return [cid for cid, _ in decision if self.env.getContainerByID(cid).getHostID() == hostID]
+
+    def getMigrationToHost(self, hostID, decision):
+        """Scheduler.py:34-38."""
+        return [cid for cid, hid in decision if hid == hostID]
+
+
+class GOBIScheduler(Scheduler):
+    """The placement step of scheduler/GOBI.py:19-48 on the COSCO env interface
+    (hostlist[i].getCPU(), containerlist[c].getApparentIPS() / getHostID() / id),
+    a drop-in for the scheduler main.py builds (``GOBIScheduler('energy_latency_16')``)."""
+
+    def __init__(self, data_type="energy_latency_16", device="cuda"):
+        super().__init__()
+        if data_type != "energy_latency_16":
+            raise ValueError("only the energy_latency_16 surrogate ships with the reference")
+        self.opt = GOBIOptimizer(device=device)
+        self.max_container_ips = self.opt.max_ips
+        self.data_type = data_type
+        self.hosts = H
+        self.result_cache = None
+
+    def selection(self):
+        """GOBI.py:44-45: GOBI re-places every container, it selects none."""
+        return []
 
     def init_matrix(self, rng=np.random):
         """GOBI.py:20-32: [host cpu / 100, container ips / max, one-hot host];

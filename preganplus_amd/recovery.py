@@ -77,9 +77,9 @@ class PreGANPlusRecovery(Recovery):
         if weights is None:
             folder = model_folder or "recovery/PreGANSrc/checkpointsplus"
             ck = os.path.join(folder, f"{self.env_name}_{self.model_name}.ckpt")
-            if os.path.exists(ck):
-                weights = W.load_reference_checkpoints(folder, self.env_name, self.hosts)
-                extra = extra or {}
+            if os.path.exists(ck):   # load_model + load_gan (utils.py:60-84): weights AND training state
+                weights, state = W.load_reference_checkpoints(folder, self.env_name, self.hosts, with_state=True)
+                extra = dict(state, **(extra or {}))
             else:
                 packaged = os.path.join(_DATA, f"{self.env_name}_{self.hosts}.npz")
                 if not os.path.exists(packaged):
@@ -90,8 +90,9 @@ class PreGANPlusRecovery(Recovery):
         self.infer = DecisionModel(self.hosts, weights, device=self.device)
         self.trainer = TR.Trainer(self.hosts, weights, self.extra, device=self.device)
         self.tune_state = TR.TuneState(self.prototypes)
-        self.epoch = int(self.extra.get(f"meta/gen/epoch", 0))
-        self.accuracy_list = []
+        # load_gan's epoch and accuracy_list are the ones the plugin keeps (PreGANPlus.py:32-34)
+        self.epoch = int(self.extra.get("meta/gen/epoch", 0))
+        self.accuracy_list = W.accuracy_list_from_arrays(self.extra, "meta/gen/accuracy_list")
         if "train_time_data" in self.extra:
             self.train_time_data = np.asarray(self.extra["train_time_data"], dtype=np.float64)
         else:
@@ -110,8 +111,14 @@ class PreGANPlusRecovery(Recovery):
 
     # -- PreGANPlus.py:60-81 --
     def train_gan(self, embedding, schedule_data):
-        ns, new_score, orig_score = TR.train_gan(self.trainer, embedding, schedule_data, self._score)
+        ns, new_score, orig_score, gen_loss, disc_loss = TR.train_gan(self.trainer, embedding, schedule_data,
+                                                                      self._score)
+        # the reference's save_gan is always on: epoch += 1, (gen_loss, disc_loss)
+        # appended, Gen / Disc checkpoints rewritten (PreGANPlus.py:76-81)
         self.epoch += 1
+        self.accuracy_list.append((gen_loss, disc_loss))
+        if self.save_gan:
+            self.save_gan_checkpoints(self.save_folder)
         return ns
 
     # -- PreGANPlus.py:51-58 --
@@ -119,8 +126,10 @@ class PreGANPlusRecovery(Recovery):
         wins, _, anom, cls = TR.on_the_fly_dataset(self.env.stats.time_series, self.env.stats.schedule_series,
                                                    self.train_time_data)
         losses = TR.backprop(self.trainer, self.tune_state, wins, anom, cls)
-        self.accuracy_list.append((float(np.mean([a for a, _ in losses]) + np.mean([t for _, t in losses])),
-                                   self.tune_state.factor + TR.PROTO_UPDATE_MIN))
+        loss = float(np.mean([a for a, _ in losses]) + np.mean([t for _, t in losses]))   # train.py:56-57
+        factor = self.tune_state.factor + TR.PROTO_UPDATE_MIN
+        anomaly_score, class_score = TR.accuracy(self.trainer, self.tune_state, wins, anom, cls)  # :56
+        self.accuracy_list.append((loss, factor, anomaly_score, class_score))                  # :58
         return losses
 
     def sync_inference_weights(self):
@@ -154,15 +163,21 @@ class PreGANPlusRecovery(Recovery):
         self.train_gan(embedding, schedule_data)
         self.tune_model()
         self.sync_inference_weights()
-        if self.save_gan:
-            self.save_checkpoints(self.save_folder)
         return self.recover_decision(embedding, schedule_data, original_decision)
 
-    # -- utils.py:49-58 (checkpoint dict), written with torch.save --
+    # -- utils.py:86-88 save_gan: Gen with (epoch, accuracy_list), Disc with (0, []) --
+    def save_gan_checkpoints(self, folder):
+        save_checkpoints(self.trainer, folder, self.env_name, self.epoch, self.accuracy_list,
+                         [("gen", self.gen_name, None)])
+        save_checkpoints(self.trainer, folder, self.env_name, 0, [], [("disc", self.disc_name, None)])
+
+    # -- utils.py:49-58 (checkpoint dict), written with torch.save: all three
+    #    models (the reference rewrites only the GAN per call; this is the
+    #    explicit full save, e.g. at shutdown) --
     def save_checkpoints(self, folder):
         save_checkpoints(self.trainer, folder, self.env_name, self.epoch, self.accuracy_list,
-                         [("transformer", self.model_name, self.tune_state.protos),
-                          ("gen", self.gen_name, None), ("disc", self.disc_name, None)])
+                         [("transformer", self.model_name, self.tune_state.protos)])
+        self.save_gan_checkpoints(folder)
 
 
 def save_checkpoints(trainer, folder, env_name, epoch, accuracy_list, entries):
@@ -235,8 +250,9 @@ class PreGANRecovery(Recovery):
             folder = model_folder or "recovery/PreGANSrc/checkpoints"
             ck = os.path.join(folder, f"{self.env_name}_{self.model_name}.ckpt")
             if os.path.exists(ck):
-                weights = W.load_reference_checkpoints(folder, self.env_name, self.hosts, encoder="FPE")
-                extra = extra or {}
+                weights, state = W.load_reference_checkpoints(folder, self.env_name, self.hosts, encoder="FPE",
+                                                              with_state=True)
+                extra = dict(state, **(extra or {}))
             else:
                 packaged = os.path.join(_DATA, f"pregan_{self.env_name}_{self.hosts}.npz")
                 if not os.path.exists(packaged):
@@ -246,7 +262,7 @@ class PreGANRecovery(Recovery):
         self.extra = extra or {}
         self.model = FPEDecisionModel(self.hosts, weights, device=self.device)
         self.epoch = int(self.extra.get("meta/gen/epoch", 0))
-        self.accuracy_list = []
+        self.accuracy_list = W.accuracy_list_from_arrays(self.extra, "meta/gen/accuracy_list")
         self.trainer = None
         if self.training:
             gan_only = {"transformer": {k: np.zeros(s) for k, s in W.transformer_shapes(self.hosts).items()},
@@ -276,14 +292,16 @@ class PreGANRecovery(Recovery):
 
     # -- PreGAN.py:51-71 --
     def train_gan(self, embedding, schedule_data):
-        TR.train_gan(self.trainer, embedding, schedule_data, self._score)
+        _, _, _, gen_loss, disc_loss = TR.train_gan(self.trainer, embedding, schedule_data, self._score)
         self.epoch += 1
+        self.accuracy_list.append((gen_loss, disc_loss))                          # PreGAN.py:67
         w = self.trainer.weights_numpy()
         self.weights = dict(self.weights, gen=w["gen"], disc=w["disc"])
         self.model.load_weights(self.weights)     # keep K3's packed GAN in step with the master
-        if self.save_folder is not None:
+        if self.save_folder is not None:           # save_gan (utils.py:86-88): Disc with epoch 0, []
             save_checkpoints(self.trainer, self.save_folder, self.env_name, self.epoch, self.accuracy_list,
-                             [("gen", self.gen_name, None), ("disc", self.disc_name, None)])
+                             [("gen", self.gen_name, None)])
+            save_checkpoints(self.trainer, self.save_folder, self.env_name, 0, [], [("disc", self.disc_name, None)])
 
     # -- PreGAN.py:73-95 --
     def recover_decision(self, embedding, schedule_data, original_decision):

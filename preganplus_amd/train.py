@@ -110,6 +110,7 @@ class Trainer:
         L.pgp_gan_forward.argtypes = [i32, i32] + [vp] * 6 + [vp]
         L.pgp_gan_disc_backward.argtypes = [i32, i32] + [vp] * 4 + [vp]
         L.pgp_gan_gen_backward.argtypes = [i32, i32] + [vp] * 3 + [vp]
+        L.pgp_gan_probs.argtypes = [i32, i32, vp, vp, vp]
         L.pgp_adamw.argtypes = [vp] * 4 + [ctypes.c_float] * 5 + [ctypes.POINTER(_AdamTensor), i32, vp]
         L.pgp_load_weights_master.argtypes = [vp, vp, ctypes.POINTER(ctypes.c_double)]
         L.pgp_tune_targets.argtypes = [i32, i32] + [vp] * 5 + [ctypes.c_double] * 2 + [vp] * 3 + [vp]
@@ -124,7 +125,8 @@ class Trainer:
                                            dbl, dbl, dbl, vp]
         for f in ("pgp_tune_forward", "pgp_tune_backward", "pgp_gan_forward", "pgp_gan_disc_backward",
                   "pgp_gan_gen_backward", "pgp_adamw", "pgp_load_weights_master", "pgp_tune_targets",
-                  "pgp_adamw_table", "pgp_tune_dataset", "pgp_tune_targets_dp", "pgp_tune_state_apply"):
+                  "pgp_adamw_table", "pgp_tune_dataset", "pgp_tune_targets_dp", "pgp_tune_state_apply",
+                  "pgp_gan_probs"):
             getattr(L, f).restype = i32
         L._pgp_train_bound = True
 
@@ -224,6 +226,14 @@ class Trainer:
         _native.check(self._L.pgp_gan_gen_backward(
             self.H, B, self.P.data_ptr(), self.G.data_ptr(), self.gscr.data_ptr(), self._stream()),
             "pgp_gan_gen_backward")
+
+    def gan_probs(self, B):
+        """The Disc probabilities of the last Disc head in the GAN workspace
+        [B,2] (after gan_gen_backward: gen_loss's, PreGANPlus.py:71-73)."""
+        out = torch.empty((B, 2), dtype=torch.float32, device=self.device)
+        _native.check(self._L.pgp_gan_probs(self.H, B, self.gscr.data_ptr(), out.data_ptr(), self._stream()),
+                      "pgp_gan_probs")
+        return out
 
     def adam_step(self, section: str, inactive: tuple = ()):
         """torch.optim.AdamW.step for the tensors of `section` (utils.py:65);
@@ -683,16 +693,65 @@ def bce_target(new_score, orig_score):
     return [0.0, 1.0] if new_score <= orig_score else [1.0, 0.0]
 
 
+def bce(p, target):
+    """nn.BCELoss (mean over the 2 probabilities, log clamped at -100), fp64."""
+    p = np.asarray(p, dtype=np.float64)
+    t = np.asarray(target, dtype=np.float64)
+    lp = np.maximum(np.log(p), -100.0)
+    l1p = np.maximum(np.log(1.0 - p), -100.0)
+    return float(-np.mean(t * lp + (1 - t) * l1p))
+
+
 def train_gan(tr: Trainer, emb, sched, simulate):
-    """PreGANPlus.py:60-75 (one window).  simulate(schedule ndarray) -> score."""
+    """PreGANPlus.py:60-75 (one window).  simulate(schedule ndarray) -> score.
+    Returns (ns, new_score, orig_score, gen_loss, disc_loss)."""
     ns, probs = tr.gan_forward(np.asarray(emb)[None], np.asarray(sched)[None])
     ns_h = ns[0].cpu().numpy().astype(np.float64)
+    p_d = probs[0].cpu().numpy()
     new_score, orig_score = simulate(ns_h), simulate(np.asarray(sched, dtype=np.float64))
-    tr.gan_disc_backward(np.array([bce_target(new_score, orig_score)]))
+    target = bce_target(new_score, orig_score)
+    tr.gan_disc_backward(np.array([target]))
     tr.adam_step("disc")
     tr.gan_gen_backward(1)
+    p_g = tr.gan_probs(1)[0].cpu().numpy()
     tr.adam_step("gen")
-    return ns_h, new_score, orig_score
+    return ns_h, new_score, orig_score, bce(p_g, [0.0, 1.0]), bce(p_d, target)
+
+
+def accuracy(tr: Trainer, st: TuneState, wins, anom, cls):
+    """train.py:94-109 after a tuning call (PreGANPlus.py:56): the updated model
+    on the same windows (one batched forward, pgp_tune_forward), then the
+    reference's per-window scores in its order — anomaly_accuracy (:60-73, the
+    fraction of hosts whose argmax matches the label) and class_accuracy
+    (:75-92, positives closer to their class prototype than to both others,
+    over 1e-4 + positives).  Returns (AScore, CScore).  Like the reference it
+    raises ZeroDivisionError when no window of the set has a positive label
+    (class_total = 0, train.py:109)."""
+    wins = np.asarray(wins)
+    n = wins.shape[0]
+    logits, protos = tr.tune_forward(torch.as_tensor(wins, dtype=torch.float32))
+    lg = logits[:n].cpu().numpy().astype(np.float64)
+    pr = protos[:n].cpu().numpy().astype(np.float64)
+    anom = np.asarray(anom).reshape(n, tr.H)
+    cls = np.asarray(cls).reshape(n, tr.H)
+    P = st.protos
+    anomaly_correct, class_correct, class_total = 0, 0, 0
+    for i in range(n):
+        res = (lg[i, :, 1] > lg[i, :, 0]).astype(np.int64)   # torch.argmax, ties -> 0
+        anomaly_correct += int(np.sum(res == anom[i])) / tr.H
+        if np.sum(anom[i]) > 0:
+            class_total += 1
+            correct, total = 0, 1e-4
+            for h in range(tr.H):
+                if anom[i, h] > 0:
+                    total += 1
+                    c = int(cls[i, h])
+                    pos = float(np.mean((pr[i, h] - P[c]) ** 2))
+                    negs = [float(np.mean((pr[i, h] - P[nc]) ** 2)) for nc in (0, 1, 2) if nc != c]
+                    if pos <= negs[0] and pos <= negs[1]:
+                        correct += 1
+            class_correct += correct / total
+    return anomaly_correct / n, class_correct / class_total
 
 
 def train_gan_batched(tr: Trainer, sim, envs, emb, sched, out=None, target=None, all_reduce=False, group=None):

@@ -201,9 +201,21 @@ def weights_checksum(weights):
     return h + float(np.asarray(weights["prototypes"]).sum())
 
 
-def load_reference_checkpoints(model_dir, env_name="simulator", H=16, encoder="Transformer"):
+_BUFFERS = {"transformer": ("pos_encoder.pe",), "fpe": (), "gen": (), "disc": ()}   # state_dict entries that are not parameters
+
+
+def load_reference_checkpoints(model_dir, env_name="simulator", H=16, encoder="Transformer", with_state=False):
     """Read ``{env}_Transformer_{H}.ckpt``/``Gen``/``Disc`` from a COSCO tree
-    (``checkpointsplus/``; format ``utils.py:53-58``) with the safe loader."""
+    (``checkpointsplus/``; format ``utils.py:53-58``) with the safe loader.
+
+    with_state=True also returns ``extra``, the training state ``load_model`` /
+    ``load_gan`` restore (``utils.py:60-84``) in the packaged-npz key format the
+    Trainer reads: AdamW ``opt/{sec}/{name}/exp_avg|exp_avg_sq|step`` (the
+    optimizer state is keyed by parameter index, i.e. ``named_parameters``
+    order = the state_dict order without buffers), ``meta/{sec}/epoch`` and the
+    Gen checkpoint's ``accuracy_list`` (the one PreGANPlusRecovery keeps,
+    ``PreGANPlus.py:32-34``) as ``meta/gen/accuracy_list`` (flat) +
+    ``meta/gen/accuracy_list_lens``."""
     import torch
     sg = [(np._core.multiarray.scalar, "numpy.core.multiarray.scalar"), np.dtype,
           np.dtypes.Float64DType]
@@ -215,13 +227,51 @@ def load_reference_checkpoints(model_dir, env_name="simulator", H=16, encoder="T
 
     t, g, d = ld(encoder), ld("Gen"), ld("Disc")
     conv = lambda sd: {k: v.detach().cpu().numpy().astype(np.float64) for k, v in sd.items()}
-    return {
-        ("fpe" if encoder == "FPE" else "transformer"): conv(t["model_state_dict"]),
+    tsec = "fpe" if encoder == "FPE" else "transformer"
+    weights = {
+        tsec: conv(t["model_state_dict"]),
         "gen": conv(g["model_state_dict"]),
         "disc": conv(d["model_state_dict"]),
         "prototypes": np.stack([p.detach().cpu().numpy() for p in t["model_prototypes"]]),
         "meta": {"epoch": t["epoch"], "gan_epoch": g["epoch"]},
     }
+    if not with_state:
+        return weights
+    extra = {}
+    for sec, ck in ((tsec, t), ("gen", g), ("disc", d)):
+        names = [k for k in ck["model_state_dict"] if k not in _BUFFERS[sec]]
+        osd = ck["optimizer_state_dict"]
+        idx = [i for grp in osd["param_groups"] for i in grp["params"]]
+        if len(idx) != len(names):
+            raise ValueError(f"{sec}: {len(idx)} optimizer params vs {len(names)} state_dict parameters")
+        for i, name in zip(idx, names):
+            s = osd["state"].get(i)
+            if not s:
+                continue
+            extra[f"opt/{sec}/{name}/exp_avg"] = s["exp_avg"].detach().cpu().numpy().astype(np.float64)
+            extra[f"opt/{sec}/{name}/exp_avg_sq"] = s["exp_avg_sq"].detach().cpu().numpy().astype(np.float64)
+            extra[f"opt/{sec}/{name}/step"] = np.float64(float(s["step"]))
+        extra[f"meta/{sec}/epoch"] = np.int64(ck["epoch"])
+    extra.update(accuracy_list_to_arrays(g["accuracy_list"], "meta/gen/accuracy_list"))
+    return weights, extra
+
+
+def accuracy_list_to_arrays(acc, key):
+    """A checkpoint accuracy_list (tuples of 2 or 4 numbers) as npz arrays."""
+    vals = [np.asarray([float(v) for v in (e if isinstance(e, (tuple, list)) else (e,))]) for e in acc]
+    flat = np.concatenate(vals) if vals else np.zeros(0)
+    return {key: flat, key + "_lens": np.array([len(v) for v in vals], dtype=np.int64)}
+
+
+def accuracy_list_from_arrays(extra, key):
+    if key not in extra:
+        return []
+    flat, lens = np.asarray(extra[key], np.float64), np.asarray(extra[key + "_lens"], np.int64)
+    out, o = [], 0
+    for n in lens:
+        out.append(tuple(float(v) for v in flat[o:o + n]))
+        o += n
+    return out
 
 
 def save_npz(path, weights, extra=None):

@@ -103,6 +103,8 @@ def make_plugin_golden(train_time):
     rec.update({f"end/d/{k}": v for k, v in params(d).items()})
     rec["T0"] = np.int64(T0)
     rec["container_none"] = np.int64(5)
+    rec["end/epoch"] = np.int64(obj.epoch)
+    rec["end/accuracy_list"] = np.array(obj.accuracy_list, dtype=np.float64)   # 4 x (gen_loss, disc_loss)
     rec["schedule_series"] = ss_all[:T0 + 4]
     np.savez_compressed(os.path.join(HERE, "pregan_plugin_h16.npz"), **rec)
 
@@ -125,11 +127,16 @@ def main():
     flat.update({f"disc/{k}": v for k, v in wts["disc"].items()})
     flat["prototypes"] = wts["prototypes"]
     flat["train_time_data"] = np.load(refshim.ckpt_path("data/simulator/time_series.npy"))
+    # the FPE_16 training curve (AScore per epoch): the only reference-held
+    # evidence on DGL's softmax_edges semantics (tests/test_gat_semantics.py)
+    flat.update(W.accuracy_list_to_arrays(ck["FPE"]["accuracy_list"], "meta/fpe/accuracy_list"))
     ms = load_pregan()
     for name, pre in (("Gen", "gen"), ("Disc", "disc")):
         m, opt, ckk = ms[name]
         flat.update(opt_state_arrays(m, opt, pre))
         flat[f"meta/{pre}/epoch"] = np.int64(ckk["epoch"])
+        if name == "Gen":   # load_gan's accuracy_list, kept by the plugin (PreGAN.py:31-32)
+            flat.update(W.accuracy_list_to_arrays(ckk["accuracy_list"], "meta/gen/accuracy_list"))
     np.savez_compressed(os.path.join(REPO, "preganplus_amd", "data", "pregan_simulator_16.npz"), **flat)
 
     train_time = np.load(refshim.ckpt_path("data/simulator/time_series.npy"))

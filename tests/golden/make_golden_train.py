@@ -193,7 +193,11 @@ def make_plugin_golden(train_time):
     obj.gan_plotter = sys.modules["recovery.PreGANSrc.src.plotter"].GAN_Plotter()
     obj.ganloss = nn.BCELoss()
     obj.train_time_data = train_time
-    obj.hosts, obj.env_name, obj.training, obj.save_gan = H, "simulator", True, False
+    # save_gan is always True in the reference (PreGANPlus.py:20): train_gan
+    # appends (gen_loss, disc_loss) and counts the epoch; the checkpoint write
+    # itself is replaced by a no-op so nothing is written
+    obj.hosts, obj.env_name, obj.training, obj.save_gan = H, "simulator", True, True
+    plugin_mod.save_gan = lambda *a, **k: None
     obj.model_name, obj.gen_name, obj.disc_name = "Transformer_16", "Gen_16", "Disc_16"
     env = Obj()
     env.hostlist = list(range(H))
@@ -226,6 +230,12 @@ def make_plugin_golden(train_time):
     rec.update({f"end/g/{k}": v for k, v in params(g).items()})
     rec.update({f"end/d/{k}": v for k, v in params(d).items()})
     rec["end/protos"] = np.stack([p.detach().numpy() for p in t.prototype])
+    # per interval: (gen_loss, disc_loss) from train_gan, then (loss, factor,
+    # AScore, CScore) from tune_model's accuracy() (PreGANPlus.py:56-58, 77)
+    rec["end/accuracy_list"] = np.concatenate([np.asarray(x, dtype=np.float64) for x in obj.accuracy_list])
+    rec["end/accuracy_list_lens"] = np.array([len(x) for x in obj.accuracy_list], dtype=np.int64)
+    rec["end/epoch"] = np.int64(obj.epoch)
+    rec["start/epoch"] = np.int64(gck["epoch"])
     rec["end/factor"] = np.float64(train.PROTO_UPDATE_FACTOR)
     rec["T0"] = np.int64(T0)
     rec["schedule_series"] = ss_all[:T0 + 4]
@@ -242,6 +252,8 @@ def main():
         m, opt, ck = ms[name]
         extra.update(opt_state_arrays(m, opt, pre))
         extra[f"meta/{pre}/epoch"] = np.int64(ck["epoch"])
+        if name == "Gen":   # load_gan's accuracy_list, kept by the plugin (PreGANPlus.py:32-34)
+            extra.update(W.accuracy_list_to_arrays(ck["accuracy_list"], "meta/gen/accuracy_list"))
     W.save_npz(wpath, w, extra=extra)
     make_tune_golden(ms, train_time)
     z = np.load(os.path.join(HERE, "fwd_h16.npz"))

@@ -52,3 +52,30 @@ def test_checkpoint_round_trip(tmp_path):
         assert float(st["step"]) == t["step"] == 1.0
         want = m[t["offset"]:t["offset"] + t["n"]].reshape(p.shape)
         assert np.array_equal(st["exp_avg"].numpy(), want.astype(np.float64))
+
+
+def test_plugin_checkpoint_resume(tmp_path):
+    """A plugin that ran two intervals saves its checkpoints; a new plugin
+    constructed on that folder (the checkpoint path of load_models) resumes
+    with the same weights, AdamW moments and step counts, epoch and
+    accuracy_list (the checkpoint path used to drop them)."""
+    from preganplus_amd.recovery import PreGANPlusRecovery
+    from tests.test_train_oracle_golden import fake_env
+    w, extra = W.load_npz("preganplus_amd/data/simulator_16.npz")
+    z = np.load("tests/golden/plugin_h16.npz")
+    a = PreGANPlusRecovery(16, "", training=True, weights=w, extra=extra)
+    for step in range(2):
+        a.setEnvironment(fake_env(z, step, extra["train_time_data"], z["schedule_series"]))
+        a.run_model(None, [tuple(x) for x in z[f"s{step}/decision_in"]])
+    a.save_checkpoints(str(tmp_path))
+    b = PreGANPlusRecovery(16, "", training=True, model_folder=str(tmp_path),
+                           extra={"train_time_data": extra["train_time_data"]})
+    assert b.epoch == a.epoch and b.accuracy_list == a.accuracy_list
+    torch.cuda.synchronize()
+    assert torch.equal(a.trainer.P, b.trainer.P)
+    assert torch.equal(a.trainer.m, b.trainer.m) and torch.equal(a.trainer.v, b.trainer.v)
+    assert [t["step"] for t in a.trainer.tensors] == [t["step"] for t in b.trainer.tensors]
+    np.testing.assert_array_equal(b.prototypes, a.tune_state.protos)
+    # the Disc checkpoint carries epoch 0 and an empty accuracy_list (utils.py:86-88)
+    ck = torch.load(tmp_path / "simulator_Disc_16.ckpt", weights_only=True)
+    assert ck["epoch"] == 0 and ck["accuracy_list"] == []

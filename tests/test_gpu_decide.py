@@ -42,3 +42,19 @@ def test_migrations_empty_batch():
     z = torch.zeros((0, 16), dtype=torch.int32, device="cuda")
     mv, hf = migrations(torch.zeros(0, dtype=torch.int32, device="cuda"), z, z)
     assert mv.shape == (0, 16) and hf.shape == (0, 16)
+
+
+def test_migrations_out_of_range_host_is_unplaced():
+    """A current-host index outside [0, C) never writes through: the
+    container is treated as unplaced, exactly like -1."""
+    from preganplus_amd.model import migrations
+    H = 16
+    d = lambda a: torch.tensor(np.asarray(a, dtype=np.int32), device="cuda")
+    cur = np.array([[3, 16, 1000, -7, 5] + [2] * (H - 5), [-1] * H])
+    tgt = np.zeros((2, H), dtype=np.int32)
+    ref = cur.copy()
+    ref[(ref < 0) | (ref >= H)] = -1
+    mv, hf = migrations(d([0, 0]), d(tgt), d(cur))
+    mv2, hf2 = migrations(d([0, 0]), d(tgt), d(ref))
+    assert torch.equal(mv, mv2) and torch.equal(hf, hf2)
+    assert mv[0, 1].item() == -1 and mv[0, 2].item() == -1 and int(hf[0].sum().item()) == 3

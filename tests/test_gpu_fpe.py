@@ -139,6 +139,8 @@ def test_pregan_plugin_run_model_matches_reference():
         close(v, z[f"end/g/{k}"], rel=1e-4, abs_scale=1e-5, what="g " + k)
     for k, v in pw["disc"].items():
         close(v, z[f"end/d/{k}"], rel=1e-4, abs_scale=1e-5, what="d " + k)
+    np.testing.assert_allclose(np.array(rec.accuracy_list[-4:]), z["end/accuracy_list"], rtol=1e-4, atol=1e-6)
+    assert rec.epoch == int(extra["meta/gen/epoch"]) + 4
 
 
 def test_pregan_plugin_inference_only():

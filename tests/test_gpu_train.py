@@ -88,7 +88,7 @@ def test_gan_step_matches_reference(tag, scores):
     z = np.load(f"{GOLD}/gan_h16.npz")
     tr = TR.Trainer(16, w, extra)
     it = iter(scores)
-    ns, _, _ = TR.train_gan(tr, z["emb"], z["sched"], lambda s: next(it))
+    ns, _, _, _, _ = TR.train_gan(tr, z["emb"], z["sched"], lambda s: next(it))
     np.testing.assert_allclose(ns, z[f"{tag}/sim_new"], rtol=1e-4, atol=1e-5)
     pw = tr.weights_numpy()
     for k, v in pw["gen"].items():
@@ -116,6 +116,27 @@ def test_plugin_run_model_matches_reference():
     for k, v in pw["gen"].items():
         close(v, z[f"end/g/{k}"], rel=1e-4, abs_scale=1e-5, what="g " + k)
     np.testing.assert_allclose(rec.tune_state.protos, z["end/protos"], atol=1e-4)
+    check_accuracy_list(rec.accuracy_list, z)
+    assert rec.epoch == int(extra["meta/gen/epoch"]) + 4     # one GAN epoch per call (PreGANPlus.py:77)
+
+
+def check_accuracy_list(got, z):
+    """accuracy_list entries appended by run_model (PreGANPlus.py:58, 77): per
+    call (gen_loss, disc_loss), then (loss, factor, AScore, CScore) — the
+    scores are ratios of counts and must be exact."""
+    lens = z["end/accuracy_list_lens"].tolist()
+    assert [len(e) for e in got[-len(lens):]] == lens
+    flat = np.concatenate([np.asarray(e, dtype=np.float64) for e in got[-len(lens):]])
+    want = z["end/accuracy_list"]
+    o = 0
+    for n in lens:
+        g, w = flat[o:o + n], want[o:o + n]
+        if n == 2:
+            np.testing.assert_allclose(g, w, rtol=1e-4, atol=1e-6, err_msg="(gen_loss, disc_loss)")
+        else:
+            np.testing.assert_allclose(g[:2], w[:2], rtol=1e-4, atol=1e-5, err_msg="(loss, factor)")
+            np.testing.assert_array_equal(g[2:], w[2:], err_msg="(AScore, CScore)")
+        o += n
 
 
 def _batched_case(H, B, seed):
@@ -445,7 +466,7 @@ def test_gan_step_matches_reference_h50(tag, scores):
     z = np.load(f"{GOLD}/gan_h50.npz")
     tr = TR.Trainer(50, w)
     it = iter(scores)
-    ns, _, _ = TR.train_gan(tr, z["emb"], z["sched"], lambda s: next(it))
+    ns, _, _, _, _ = TR.train_gan(tr, z["emb"], z["sched"], lambda s: next(it))
     np.testing.assert_allclose(ns, z[f"{tag}/sim_new"], rtol=1e-4, atol=1e-5)
     pw = tr.weights_numpy()
     for k, v in pw["gen"].items():
