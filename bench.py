@@ -488,10 +488,15 @@ def bench_fpe(args):
         gan_fl = R.gan_flops_per_window(H) * B
         dom_fpe = k[0] >= k[1]
         if dom_fpe:
-            ach = fpe_bytes / (k[0] * 1e-3) / 1e9
-            roof = {"kernel": "fpe_kernel (K4)", "bound": "hbm", "achieved": ach, "peak": R.PEAK_HBM_GBS,
-                    "unit": "GB/s", "frac": ach / R.PEAK_HBM_GBS, "traffic": None,
-                    "bytes_per_window": R.fpe_bytes_per_window(H)}
+            # K4 is one window per lane on the VALU (too little work per window for MFMA
+            # operand shuffles): its roofline is the fp32 vector peak (= the f32 MFMA rate);
+            # its HBM rate is reported beside it
+            ach = R.fpe_flops_per_window(H) * B / (k[0] * 1e-3) / 1e12
+            roof = {"kernel": "fpe_kernel (K4)", "bound": "valu", "achieved": ach, "peak": R.PEAK_FP32_TFLOPS,
+                    "unit": "TFLOP/s", "frac": ach / R.PEAK_FP32_TFLOPS, "traffic": None,
+                    "flops_per_window": R.fpe_flops_per_window(H),
+                    "hbm_gbs": fpe_bytes / (k[0] * 1e-3) / 1e9,
+                    "hbm_frac": fpe_bytes / (k[0] * 1e-3) / 1e9 / R.PEAK_HBM_GBS}
         else:
             ach = gan_fl / (k[1] * 1e-3) / 1e12
             roof = {"kernel": "gan_kernel (K3)", "bound": "mfma", "achieved": ach, "peak": R.PEAK_FP32_TFLOPS,
