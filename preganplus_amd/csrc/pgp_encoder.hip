@@ -15,6 +15,25 @@
 namespace pgp {
 namespace {
 
+// Timing-study switches (default 0; they change the numerics and exist only to
+// measure how much of K2's time each VALU phase costs): PGP_EXP_NO_LN
+// skips the LayerNorms, PGP_EXP_NO_SOFTMAX the tail-mode scores + softmax
+// (P = 1/3), PGP_EXP_NO_ROWS the tail-mode VALU rows.
+// Tail mode, layer 0: attention scores as bilinear forms of the 3 raw features
+// per step (q, k affine in them; pgp_pack.cpp T_F0S): lane-local FMAs instead of
+// q / k tiles, partial dot products and cross-lane sums
+#ifndef PGP_ENC_BILIN
+#define PGP_ENC_BILIN 1
+#endif
+#ifndef PGP_EXP_NO_LN
+#define PGP_EXP_NO_LN 0
+#endif
+#ifndef PGP_EXP_NO_SOFTMAX
+#define PGP_EXP_NO_SOFTMAX 0
+#endif
+#ifndef PGP_EXP_NO_ROWS
+#define PGP_EXP_NO_ROWS 0
+#endif
 constexpr int kEncWaves = 4;
 // H <= 16 (weights LDS-resident): ENC16_WAVES waves per workgroup share one LDS
 // copy, and ENC16_EU waves per SIMD are requested from the register allocator
@@ -110,7 +129,7 @@ PGP_DEV void gemm3_rows(f32x4 (&acc)[NMA][3], const float* A, const f32x4 (&Bx)[
 #pragma unroll
           for (int w = 0; w < 3; ++w) {
             acc[m][w] = mfma(a[e], Bx[q4][w][e], acc[m][w]);
-            if (m == 0) {
+            if (m == 0 && !PGP_EXP_NO_ROWS) {
 #pragma unroll
               for (int n = 0; n < NR; ++n) racc[n][w] = fmaf(rw[n][e], Bx[q4][w][e], racc[n][w]);
             }
@@ -161,6 +180,13 @@ PGP_DEV void layer_norm_tiles(f32x4 (&acc)[Geo<H>::MT_D][3], f32x4 (&X)[Geo<H>::
                               const float* bet, int g) {
   using G = Geo<H>;
   constexpr float invH = 1.0f / (float)H;
+  if constexpr (PGP_EXP_NO_LN) {
+#pragma unroll
+    for (int mt = 0; mt < G::MT_D; ++mt)
+#pragma unroll
+      for (int w = 0; w < 3; ++w) X[mt][w] = acc[mt][w];
+    return;
+  }
 #if PGP_LN_ONEPASS
   // one pass: sum and sum of squares of each step reduced together (xsum2).
   // Padded feature rows hold exact zeros here, so no mask is needed.
@@ -365,14 +391,16 @@ PGP_DEV float row_fold_bias(int m, int n, int w, const float* tab) {
 // stages are then unused).
 template <int H, bool F0>
 PGP_DEV void encoder_layer_tail(f32x4 (&X)[Geo<H>::MT_D][3], Ring<H>& ring, const float* TL, int lane,
-                                const float* tab, const float (&ba)[3]) {
+                                const float* tab, const float (&ba)[3], const float (&xv)[3][3]) {
   using G = Geo<H>;
   constexpr int TQ = G::TQ, SR = G::SR, HF = G::HF;
   const int g = lane >> 4;
   // [S0] q and k of both heads
-  f32x4 QK[2 * TQ][3];
+  constexpr bool BIL = F0 && PGP_ENC_BILIN;
+  f32x4 QK[BIL ? 1 : 2 * TQ][3];
   float qr[SR][3], kr[SR][3];
-  if constexpr (F0) {
+  if constexpr (BIL) {
+  } else if constexpr (F0) {
     qkv_fold<H, 2 * TQ>(QK, 0, 2 * TQ, tab, ba, lane, g);
 #pragma unroll
     for (int n = 0; n < SR; ++n)
@@ -405,6 +433,42 @@ PGP_DEV void encoder_layer_tail(f32x4 (&X)[Geo<H>::MT_D][3], Ring<H>& ring, cons
   ring.advance();
   // scores of both heads; the shared tile's slot 4r+g belongs to head 0 below HT
   float P0[3][3], P1[3][3];
+  if constexpr (BIL) {
+    // score(w, w2) = x_w^T M x_w2 + x_w . U[:, w2] + V[w] . x_w2 + S[w][w2]
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      const float* SB = tab + G::T_F0S + hh * 36;
+      float tk[3][3], vk[3][3];  // [key step][f]: M x_w2 + U[:, w2];  [query][key]: V[w] . x_w2
+#pragma unroll
+      for (int w2 = 0; w2 < 3; ++w2) {
+#pragma unroll
+        for (int f = 0; f < 3; ++f)
+          tk[w2][f] = fmaf(SB[3 * f + 2], xv[w2][2], fmaf(SB[3 * f + 1], xv[w2][1], fmaf(SB[3 * f], xv[w2][0], SB[9 + 3 * f + w2])));
+#pragma unroll
+        for (int w = 0; w < 3; ++w)
+          vk[w][w2] = fmaf(SB[18 + 3 * w + 2], xv[w2][2], fmaf(SB[18 + 3 * w + 1], xv[w2][1], fmaf(SB[18 + 3 * w], xv[w2][0], SB[27 + 3 * w + w2])));
+      }
+#pragma unroll
+      for (int w = 0; w < 3; ++w) {
+        float s[3];
+#pragma unroll
+        for (int w2 = 0; w2 < 3; ++w2)
+          s[w2] = fmaf(xv[w][2], tk[w2][2], fmaf(xv[w][1], tk[w2][1], fmaf(xv[w][0], tk[w2][0], vk[w][w2])));
+        const float m = fmaxf(s[0], fmaxf(s[1], s[2]));
+        const float e0 = __expf(s[0] - m), e1 = __expf(s[1] - m), e2 = __expf(s[2] - m);
+        const float iv = __builtin_amdgcn_rcpf(e0 + e1 + e2);
+        float(&Pw)[3][3] = hh == 0 ? P0 : P1;
+        Pw[w][0] = e0 * iv;
+        Pw[w][1] = e1 * iv;
+        Pw[w][2] = e2 * iv;
+      }
+    }
+  } else if constexpr (PGP_EXP_NO_SOFTMAX) {
+#pragma unroll
+    for (int w = 0; w < 3; ++w)
+#pragma unroll
+      for (int w2 = 0; w2 < 3; ++w2) P0[w][w2] = P1[w][w2] = 1.f / 3.f + 0.f * QK[0][w][0] * qr[0][w] * kr[0][w2];
+  } else
 #pragma unroll
   for (int w = 0; w < 3; ++w) {
     float s0[3], s1[3];
@@ -663,6 +727,13 @@ __global__ __launch_bounds__(enc_waves<H>() * 64, H <= 16 ? PGP_ENC16_EU : 2) vo
     float ba[3];
 #pragma unroll
     for (int w = 0; w < 3; ++w) ba[w] = (active && g < 3) ? agg[(h * 3 + w) * 48 + lane] : 0.f;
+    // all 3 raw features of every step of this lane's window (layer 0's bilinear scores)
+    float xv[3][3];
+#pragma unroll
+    for (int w = 0; w < 3; ++w)
+#pragma unroll
+      for (int f = 0; f < 3; ++f)
+        xv[w][f] = (G::TAIL && PGP_ENC_BILIN && active) ? agg[(h * 3 + w) * 48 + 16 * f + j] : 0.f;
     f32x4 X[G::MT_D][3];
 #pragma unroll
     for (int mt = 0; mt < G::MT_D; ++mt) {
@@ -672,8 +743,8 @@ __global__ __launch_bounds__(enc_waves<H>() * 64, H <= 16 ? PGP_ENC16_EU : 2) vo
     }
     static_assert(kLayers == 2, "layer 0 (folded q/k/v) + layer 1");
     if constexpr (G::TAIL) {
-      encoder_layer_tail<H, true>(X, ring, tab + G::T_L0, lane, tab, ba);
-      encoder_layer_tail<H, false>(X, ring, tab + G::T_L0 + G::TL_SIZE, lane, tab, ba);
+      encoder_layer_tail<H, true>(X, ring, tab + G::T_L0, lane, tab, ba, xv);
+      encoder_layer_tail<H, false>(X, ring, tab + G::T_L0 + G::TL_SIZE, lane, tab, ba, xv);
     } else {
       encoder_layer<H, true>(X, ring, tab + G::T_L0, lane, tab, ba);
       encoder_layer<H, false>(X, ring, tab + G::T_L0 + G::TL_SIZE, lane, tab, ba);

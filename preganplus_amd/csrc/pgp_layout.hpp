@@ -171,7 +171,12 @@ struct Geo {
   // K=4 A fragments [head][G|C][MT_X][64] and VALU rows [XR][head][G|C][4]
   static constexpr int T_F0O = T_F0RB + round_up(9 * SR, 4);
   static constexpr int T_F0OR = T_F0O + (TAIL ? 4 * MT_X * 64 : 0);
-  static constexpr int T_DEC = T_F0OR + (TAIL ? XR * 16 : 0);  // [MT_O*16] decoder bias
+  // tail mode, layer 0's attention scores as bilinear forms of the raw features
+  // (q and k are affine in them): per head [M 3x3 | U 3x3 (f, key step) | V 3x3
+  // (query step, f) | S 3x3 (query, key step)], score(w, w2) = x_w^T M x_w2 +
+  // x_w . U[:, w2] + V[w] . x_w2 + S[w][w2]
+  static constexpr int T_F0S = T_F0OR + (TAIL ? XR * 16 : 0);
+  static constexpr int T_DEC = T_F0S + (TAIL ? 72 : 0);     // [MT_O*16] decoder bias
   static constexpr int T_PROTO = T_DEC + MT_O * 16;         // [K][2]
   static constexpr int t_size(int K) { return T_PROTO + round_up(2 * K, 4); }
 

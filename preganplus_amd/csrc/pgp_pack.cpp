@@ -481,6 +481,29 @@ std::string pack_t(int K, const double* blob, size_t len, Packed* P) {
           }
       }
     }
+    if constexpr (G::TAIL) {  // layer 0's scores per head as bilinear forms of the raw features
+      for (int hh = 0; hh < 2; ++hh) {
+        double M[9] = {}, U[9] = {}, V[9] = {}, Sc[9] = {};
+        for (int e = 0; e < G::HD; ++e) {
+          double qf[3], qb[3], kf[3], kb[3];
+          fold(hh * G::HD + e, qf, qb);      // q (attention scale folded in)
+          fold(d + hh * G::HD + e, kf, kb);  // k
+          for (int a = 0; a < 3; ++a)
+            for (int b = 0; b < 3; ++b) {
+              M[a * 3 + b] += qf[a] * kf[b];
+              U[a * 3 + b] += qf[a] * kb[b];   // (f, key step)
+              V[a * 3 + b] += qb[a] * kf[b];   // (query step, f)
+              Sc[a * 3 + b] += qb[a] * kb[b];  // (query step, key step)
+            }
+        }
+        for (int i = 0; i < 9; ++i) {
+          T[G::T_F0S + hh * 36 + i] = (float)M[i];
+          T[G::T_F0S + hh * 36 + 9 + i] = (float)U[i];
+          T[G::T_F0S + hh * 36 + 18 + i] = (float)V[i];
+          T[G::T_F0S + hh * 36 + 27 + i] = (float)Sc[i];
+        }
+      }
+    }
     for (int m = 0; m < 3; ++m)
       for (int n = 0; n < G::SR; ++n) {
         const int src = m * d + G::HD + 16 * G::HF + 16 - G::HT + n;

@@ -53,7 +53,7 @@ def encoder_flops_per_window(H: int) -> int:
 # host and wave in the encoder kernel's ISA (tools/isa_count.py).  K2 executes
 # fewer MFMA flops than the reference's algorithm (layer-0 folds), so
 # its algorithmic rate can exceed the peak; the executed rate cannot.
-ENC_MFMA_PER_HOST = {16: 264, 50: 1134}
+ENC_MFMA_PER_HOST = {16: 264, 50: 1116}
 
 
 def encoder_executed_flops_per_window(H: int):
