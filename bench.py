@@ -837,6 +837,34 @@ def bench_plugin(args):
         call(k)
         torch.cuda.synchronize()
         lat.append(time.perf_counter() - t0)
+    # per-stage wall time (a separate pass: each stage bracketed by synchronize)
+    stages = {}
+
+    def timed(name, fn):
+        def wrapper(*a, **k):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            r = fn(*a, **k)
+            torch.cuda.synchronize()
+            stages.setdefault(name, []).append(time.perf_counter() - t0)
+            return r
+        return wrapper
+
+    for name in ("train_gan", "tune_model", "sync_inference_weights", "recover_decision"):
+        setattr(rec, name, timed(name, getattr(rec, name)))
+    rec.infer.forward = timed("detect_forward", rec.infer.forward)
+    import preganplus_amd.train as TRm
+    bp, acc = TRm.backprop, TRm.accuracy
+    TRm.backprop, TRm.accuracy = timed("tune_backprop", bp), timed("tune_accuracy", acc)
+    try:
+        for k in range(min(args.steps, 20)):
+            call(k)
+    finally:
+        TRm.backprop, TRm.accuracy = bp, acc
+        for name in ("train_gan", "tune_model", "sync_inference_weights", "recover_decision"):
+            delattr(rec, name)
+        del rec.infer.forward
+    stage_ms = {k: float(np.median(v) * 1e3) for k, v in stages.items()}
     # batch-1 inference latency (the encoder + classify + GAN gate of one window)
     model = rec.infer
     x1 = torch.tensor(rec.input_window()[None], dtype=torch.float32, device=device)
@@ -859,7 +887,8 @@ def bench_plugin(args):
                "config": {"workload": "C1: PreGANPlusRecovery.run_model, one COSCO interval, 16 hosts",
                           "hosts": 16, "tuning_windows": 10},
                "latency_ms": {"run_model_median": ms, "run_model_p90": float(np.percentile(lat, 90) * 1e3),
-                              "forward_batch1": fwd_ms}}
+                              "forward_batch1": fwd_ms},
+               "stages_ms": stage_ms}
         if not args.no_cpu_baseline:
             from oracle import pregan_train_oracle as TO  # CPU baseline leg only
             torch.set_num_threads(1)

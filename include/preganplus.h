@@ -233,6 +233,16 @@ int pgp_tune_backward(int n_hosts, int batch, const float* P, float* G, float* w
 int pgp_tune_targets(int n_hosts, int n_protos, const float* logits, const float* protos, const int* y, const int* cls,
                      double* state, double update_min, double decay, float* mult, float* tgt, double* loss,
                      void* stream);
+/* ONE whole batch-1 tuning step of backprop (train.py:46-53: model(window),
+ * custom_loss, loss.backward()) in a single launch, for n_hosts 8 or 16:
+ * pgp_tune_forward + pgp_tune_targets + pgp_tune_backward with batch 1 fused.
+ * window [3,3H], y / cls [H] int32, state as pgp_tune_targets (updated in
+ * place); writes logits [H,2], protos [H,2], loss [2] fp64 and the whole
+ * transformer section of G (overwritten, no zeroing needed; the gen / disc
+ * sections are untouched).  The AdamW step stays a separate launch. */
+int pgp_tune_step1(int n_hosts, int n_protos, const float* window, const int* y, const int* cls, const float* P,
+                   float* G, double* state, double update_min, double decay, float* logits, float* protos,
+                   double* loss, void* stream);
 /* ---- data-parallel tuning step on the device ----
  * pgp_tune_dataset replaces load_on_the_fly_dataset (utils.py:40-47) for a
  * batch of E environments: series [E,R,3H] fp64 = each environment's last R

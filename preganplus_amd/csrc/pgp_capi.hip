@@ -358,6 +358,18 @@ int pgp_tune_targets(int n_hosts, int n_protos, const float* logits, const float
   return PGP_OK;
 }
 
+int pgp_tune_step1(int n_hosts, int n_protos, const float* window, const int* y, const int* cls, const float* P,
+                   float* G, double* state, double update_min, double decay, float* logits, float* protos,
+                   double* loss, void* stream) {
+  if (!tune1_supported(n_hosts)) return fail(PGP_ERR_UNSUPPORTED, "host count (fused step: 8 or 16)");
+  if (n_protos < 3) return fail(PGP_ERR_ARG, "triplet_loss needs prototypes 0-2");
+  if (!window || !y || !cls || !P || !G || !state || !logits || !protos || !loss)
+    return fail(PGP_ERR_ARG, "bad tune_step1 arguments");
+  HIPCHK(launch_tune1(n_hosts, n_protos, window, y, cls, P, G, state, update_min, decay, logits, protos, loss,
+                      reinterpret_cast<hipStream_t>(stream)));
+  return PGP_OK;
+}
+
 int pgp_tune_dataset(int n_hosts, int n_env, int n_rows, const double* series, const double* train_max,
                      float* windows, int* y, int* cls, float* infer, void* stream) {
   if (n_hosts <= 0 || n_hosts > 64) return fail(PGP_ERR_UNSUPPORTED, "host count");

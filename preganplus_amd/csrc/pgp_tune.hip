@@ -27,6 +27,7 @@
 #include "pgp_gemm.hpp"
 #include "pgp_train.hpp"
 #include "pgp_tune.hpp"
+#include "pgp_tunetargets.hpp"
 
 // workgroups of the token-major GEMMs / weight-gradient kernels (grid-stride loops)
 #ifndef PGP_LIN_CAP
@@ -1255,53 +1256,8 @@ __global__ __launch_bounds__(64) void tune_targets_kernel(int H, int K, const fl
                                                           const int* __restrict__ cls, double* __restrict__ state,
                                                           double update_min, double decay, float* __restrict__ mult,
                                                           float* __restrict__ tgt, double* __restrict__ loss) {
-#pragma clang fp contract(off)
   if (threadIdx.x != 0) return;
-  double* pr = state;  // [K][2]
-  double* sc = state + 2 * K;  // factor, num_zero, num_ones
-  const double ratio = sc[1] / sc[2];  // num_zero / num_ones (exact integers in fp64)
-  double aloss = 0.0;
-  long ones = 0;
-  for (int i = 0; i < H; ++i) {  // train.py:28-32
-    const int yi = y[i];
-    const double mu = yi == 0 ? 1.0 : ratio;
-    mult[i] = (float)mu;
-    ones += yi == 1 ? 1 : 0;
-    const double l0 = logits[2 * i], l1 = logits[2 * i + 1];
-    const double m = fmax(l0, l1);
-    const double lse = log(exp(l0 - m) + exp(l1 - m)) + m;  // CrossEntropyLoss of one row
-    aloss += (lse - (yi ? l1 : l0)) * mu;
-  }
-  double tloss = 0.0;
-  for (int i = 0; i < H; ++i) {  // train.py:33-35 -> triplet_loss (:13-24)
-    if (y[i] > 0) {
-      const int cc = cls[i];
-      const double a0 = protos[2 * i], a1 = protos[2 * i + 1];
-      tgt[2 * i] = (float)pr[2 * cc];
-      tgt[2 * i + 1] = (float)pr[2 * cc + 1];
-      double mse[3];
-      for (int k = 0; k < 3; ++k) {
-        const double d0 = a0 - pr[2 * k], d1 = a1 - pr[2 * k + 1];
-        mse[k] = (d0 * d0 + d1 * d1) / 2.0;  // MSELoss(reduction='mean') over 2 values
-      }
-      const double pos = mse[cc];
-      const double n0 = mse[cc == 0 ? 1 : 0], n1 = mse[cc == 2 ? 1 : 2];  // negatives in class order
-      tloss += pos - (n0 + n1);
-      if (pos <= n0 && pos <= n1) {
-        const double f = sc[0] + update_min;
-        pr[2 * cc] = f * a0 + (1.0 - f) * pr[2 * cc];
-        pr[2 * cc + 1] = f * a1 + (1.0 - f) * pr[2 * cc + 1];
-      }
-    } else {
-      tgt[2 * i] = 0.f;
-      tgt[2 * i + 1] = 0.f;
-    }
-  }
-  sc[0] *= decay;  // PROTO_UPDATE_FACTOR *= PROTO_FACTOR_DECAY
-  sc[1] += (double)H;  // nz counts every host (train.py:31)
-  sc[2] += (double)ones;
-  loss[0] = aloss;
-  loss[1] = tloss;
+  tune_targets_one(H, K, logits, protos, y, cls, state, update_min, decay, mult, tgt, loss);
 }
 
 hipError_t launch_tune_targets(int H, int K, const float* logits, const float* protos, const int* y, const int* cls,

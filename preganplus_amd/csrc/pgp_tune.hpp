@@ -54,4 +54,11 @@ hipError_t launch_tune_targets(int H, int K, const float* logits, const float* p
                                double* state, double update_min, double decay, float* mult, float* tgt, double* loss,
                                hipStream_t st);
 
+// one fused batch-1 tuning step (pgp_tune1.hip): forward + targets + backward
+// writing the transformer section of G; H in {8, 16}
+bool tune1_supported(int H);
+hipError_t launch_tune1(int H, int K, const float* win, const int* y, const int* cls, const float* P, float* G,
+                        double* state, double update_min, double decay, float* logits, float* protos, double* loss,
+                        hipStream_t st);
+
 }  // namespace pgp

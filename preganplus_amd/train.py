@@ -117,6 +117,7 @@ class Trainer:
         L.pgp_adamw_table.argtypes = ([vp] * 4 + [ctypes.c_float] * 5 + [ctypes.POINTER(_AdamTensor), i32, vp]
                                       + [vp])
         dbl = ctypes.c_double
+        L.pgp_tune_step1.argtypes = [i32, i32] + [vp] * 6 + [dbl, dbl] + [vp] * 3 + [vp]
         L.pgp_tune_dataset.argtypes = [i32, i32, i32] + [vp] * 6 + [vp]
         L.pgp_tune_targets_dp_workspace_len.argtypes = [i32]
         L.pgp_tune_targets_dp_workspace_len.restype = sz
@@ -126,7 +127,7 @@ class Trainer:
         for f in ("pgp_tune_forward", "pgp_tune_backward", "pgp_gan_forward", "pgp_gan_disc_backward",
                   "pgp_gan_gen_backward", "pgp_adamw", "pgp_load_weights_master", "pgp_tune_targets",
                   "pgp_adamw_table", "pgp_tune_dataset", "pgp_tune_targets_dp", "pgp_tune_state_apply",
-                  "pgp_gan_probs"):
+                  "pgp_gan_probs", "pgp_tune_step1"):
             getattr(L, f).restype = i32
         L._pgp_train_bound = True
 
@@ -200,6 +201,19 @@ class Trainer:
             self.H, K, self.logits.data_ptr(), self.protos.data_ptr(), y.data_ptr(), cls.data_ptr(),
             state.data_ptr(), PROTO_UPDATE_MIN, PROTO_FACTOR_DECAY, mult.data_ptr(), tgt.data_ptr(),
             loss.data_ptr(), self._stream()), "pgp_tune_targets")
+
+    def tune_step1(self, window, y, cls, state, loss):
+        """tune_forward + tune_targets + tune_backward of ONE window as a single
+        launch (``pgp_tune_step1``, n_hosts 8 or 16): window [1,3,3H] (or
+        [3,3H]), y, cls [H] int32, state as tune_targets; writes logits /
+        protos, loss [2] fp64 and the transformer section of G.  Device
+        tensors."""
+        K = (state.numel() - 3) // 2
+        _native.check(self._L.pgp_tune_step1(
+            self.H, K, window.data_ptr(), y.data_ptr(), cls.data_ptr(), self.P.data_ptr(), self.G.data_ptr(),
+            state.data_ptr(), PROTO_UPDATE_MIN, PROTO_FACTOR_DECAY, self.logits.data_ptr(),
+            self.protos.data_ptr(), loss.data_ptr(), self._stream()), "pgp_tune_step1")
+        self._fwd_batch = 0   # the fused step keeps no activations for tune_backward
 
     def gan_forward(self, emb, sched):
         emb = self._dev(emb, torch.float32)
@@ -618,16 +632,23 @@ def on_the_fly_dataset(time_series, schedule_series, train_time_data):
     return convert_to_windows(td), sched, anom, cls
 
 
+FUSED_STEP_HOSTS = (8, 16)   # pgp_tune_step1's compiled host counts
+
+
 class _TuneGraph:
     """One backprop() call of n sequential batch-1 steps captured as a HIP
-    graph: per step tune_forward -> tune_targets -> tune_backward (zero_grad +
-    kernels) -> AdamW from a device table.  Inputs live in fixed device buffers
-    that each call refills; a replay issues the ~20 launches per step with one
-    host call."""
+    graph.  Per step, at 8 / 16 hosts: the fused step (``tune_step1``: forward,
+    bookkeeping and backward in one workgroup) -> AdamW from a device table —
+    2 launches; otherwise tune_forward -> tune_targets -> tune_backward
+    (zero_grad + kernels) -> AdamW, ~45 launches.  Inputs live in fixed device
+    buffers that each call refills; a replay issues every launch of the n
+    steps with one host call."""
 
-    def __init__(self, tr: Trainer, n: int, win_shape, K: int):
+    def __init__(self, tr: Trainer, n: int, win_shape, K: int, fused: bool | None = None):
         H, dev = tr.H, tr.device
-        self.n, self.generation = n, tr.generation
+        if fused is None:
+            fused = H in FUSED_STEP_HOSTS
+        self.n, self.generation, self.fused = n, tr.generation, fused
         self.W = torch.zeros((n,) + tuple(win_shape), dtype=torch.float32, device=dev)
         self.Y = torch.zeros((n, H), dtype=torch.int32, device=dev)
         self.C = torch.zeros((n, H), dtype=torch.int32, device=dev)
@@ -641,13 +662,16 @@ class _TuneGraph:
         torch.cuda.synchronize(dev)
         with torch.cuda.graph(self.graph):
             for i in range(n):
-                tr.tune_forward(self.W[i:i + 1])
-                tr.tune_targets(self.Y[i], self.C[i], self.state, self.mult, self.tgt, self.loss[i])
-                tr.tune_backward(1, self.Y[i:i + 1], self.mult, self.tgt)
+                if fused:
+                    tr.tune_step1(self.W[i], self.Y[i], self.C[i], self.state, self.loss[i])
+                else:
+                    tr.tune_forward(self.W[i:i + 1])
+                    tr.tune_targets(self.Y[i], self.C[i], self.state, self.mult, self.tgt, self.loss[i])
+                    tr.tune_backward(1, self.Y[i:i + 1], self.mult, self.tgt)
                 tr.adam_step_table("transformer", self.sel, self.sched[i])
 
 
-def backprop(tr: Trainer, st: TuneState, wins, anom, cls):
+def backprop(tr: Trainer, st: TuneState, wins, anom, cls, fused: bool | None = None):
     """train.py:42-57: sequential batch-1 steps (forward, custom_loss, backward,
     AdamW).  Returns the per-window (aloss, tloss).
 
@@ -669,11 +693,13 @@ def backprop(tr: Trainer, st: TuneState, wins, anom, cls):
     if bad.any():
         raise ValueError("anomalous host with a class outside 0..2 (triplet_loss, train.py:15-17)")
     K = st.protos.shape[0]
-    key = (n, wins.shape[1:], K)
+    if fused is None:
+        fused = H in FUSED_STEP_HOSTS
+    key = (n, wins.shape[1:], K, bool(fused))
     g = tr._graphs.get(key)
     if g is None or g.generation != tr.generation:
         tr._ensure(1)
-        g = tr._graphs[key] = _TuneGraph(tr, n, wins.shape[1:], K)
+        g = tr._graphs[key] = _TuneGraph(tr, n, wins.shape[1:], K, fused)
     inactive = [() if np.any(anom[i] > 0) else ("prototype_decoder.0.weight", "prototype_decoder.0.bias")
                 for i in range(n)]
     _, tab = tr.adam_schedule("transformer", inactive)
