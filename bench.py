@@ -854,13 +854,13 @@ def bench_plugin(args):
         setattr(rec, name, timed(name, getattr(rec, name)))
     rec.infer.forward = timed("detect_forward", rec.infer.forward)
     import preganplus_amd.train as TRm
-    bp, acc = TRm.backprop, TRm.accuracy
-    TRm.backprop, TRm.accuracy = timed("tune_backprop", bp), timed("tune_accuracy", acc)
+    bp, ds = TRm.backprop, TRm.on_the_fly_dataset
+    TRm.backprop, TRm.on_the_fly_dataset = timed("tune_backprop", bp), timed("tune_dataset", ds)
     try:
         for k in range(min(args.steps, 20)):
             call(k)
     finally:
-        TRm.backprop, TRm.accuracy = bp, acc
+        TRm.backprop, TRm.on_the_fly_dataset = bp, ds
         for name in ("train_gan", "tune_model", "sync_inference_weights", "recover_decision"):
             delattr(rec, name)
         del rec.infer.forward

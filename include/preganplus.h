@@ -312,8 +312,18 @@ int pgp_adamw_table(float* P, const float* G, float* exp_avg, float* exp_avg_sq,
                     const float* sched, void* stream);
 
 /* Rebuild the inference layouts from device master weights P (natural fp32)
- * and prototypes [K,2] (host, fp64): the sync after an optimizer step. */
+ * and prototypes [K,2] (host, fp64): the sync after an optimizer step, via the
+ * host packer (a device-to-host copy of P, pack, upload; synchronous). */
 int pgp_load_weights_master(pgp_model* m, const float* P_device, const double* prototypes);
+/* The same rebuild ON THE DEVICE, asynchronous on `stream`: P natural fp32 and
+ * prototypes_device [K,2] fp64 (e.g. the head of the tuning state vector) are
+ * read by three repack launches that write the model's packed buffers in
+ * place — the same bits as pgp_load_weights_master (shared packing code,
+ * fp64, no contraction).  Replaces the host round trip after an optimizer step
+ * (the reference's AdamW updates the modules in place, utils.py:64-65;
+ * PreGANPlus.py:115-136 runs the next interval on the updated model).  The
+ * model must have been loaded once (pgp_load_weights). */
+int pgp_repack_master(pgp_model* m, const float* P_device, const double* prototypes_device, void* stream);
 
 /* ------------------------------------------------------------------------
  * GOBI, the schedule producer: replaces

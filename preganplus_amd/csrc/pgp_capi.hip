@@ -10,6 +10,7 @@
 #include "../../include/preganplus.h"
 #include "pgp_device.hpp"
 #include "pgp_pack.hpp"
+#include "pgp_repack.hpp"
 #include "pgp_train.hpp"
 #include "pgp_tune.hpp"
 #include "pgp_tunedp.hpp"
@@ -25,7 +26,8 @@ struct pgp_model {
   float* d_frags = nullptr;
   float* d_tab = nullptr;
   float* d_gtab = nullptr;
-  GatConst gat{};
+  float* d_gat = nullptr;    // GAT constants u[4] | v[4] (K1 reads them on the device)
+  double* d_pscr = nullptr;  // device repack scratch (pgp_repack_master)
   int cap = 0;  // workspace capacity in windows
   float* d_agg = nullptr;
   float* d_lat = nullptr;
@@ -139,8 +141,9 @@ int pgp_create_fpe(int n_hosts, pgp_model** out) {
 
 int pgp_destroy(pgp_model* m) {
   if (!m) return PGP_OK;
-  for (float* p : {m->d_frags, m->d_tab, m->d_gtab, m->d_agg, m->d_lat, m->d_emb})
+  for (float* p : {m->d_frags, m->d_tab, m->d_gtab, m->d_agg, m->d_lat, m->d_emb, m->d_gat})
     if (p) (void)hipFree(p);
+  if (m->d_pscr) (void)hipFree(m->d_pscr);
   delete m;
   return PGP_OK;
 }
@@ -156,7 +159,8 @@ int pgp_load_weights(pgp_model* m, const double* blob, size_t len) {
   HIPCHK(hipMemcpy(m->d_frags, P.frags.data(), P.frags.size() * sizeof(float), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(m->d_tab, P.enc_tab.data(), P.enc_tab.size() * sizeof(float), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(m->d_gtab, P.gan_tab.data(), P.gan_tab.size() * sizeof(float), hipMemcpyHostToDevice));
-  m->gat = P.gat;
+  if (!m->d_gat) HIPCHK(hipMalloc(&m->d_gat, sizeof(GatConst)));
+  HIPCHK(hipMemcpy(m->d_gat, &P.gat, sizeof(GatConst), hipMemcpyHostToDevice));
   m->loaded = true;
   return PGP_OK;
 }
@@ -196,7 +200,7 @@ int pgp_forward_stage(pgp_model* m, int stage, int batch, const float* windows, 
   a.frags = m->d_frags;
   a.tab = m->d_tab;
   a.gtab = m->d_gtab;
-  a.gat = m->gat;
+  a.gat = m->d_gat;
   a.logits = logits;
   a.protos = protos;
   a.cls = cls;
@@ -506,6 +510,19 @@ int pgp_adamw_table(float* P, const float* G, float* exp_avg, float* exp_avg_sq,
     a.t[i].bc2_sqrt = tensors[i].bc2_sqrt;
   }
   HIPCHK(launch_adamw(a, reinterpret_cast<hipStream_t>(stream)));
+  return PGP_OK;
+}
+
+int pgp_repack_master(pgp_model* m, const float* P_device, const double* prototypes_device, void* stream) {
+  if (!m || !P_device || !prototypes_device) return fail(PGP_ERR_ARG, "NULL argument");
+  if (m->fpe) return fail(PGP_ERR_STATE, "FPE model: master-layout reload covers the PreGAN+ model only");
+  if (!m->loaded) return fail(PGP_ERR_STATE, "weights not loaded (the first load packs on the host)");
+  long tr, go, dof, all;
+  if (!master_offsets(m->H, &tr, &go, &dof, &all)) return fail(PGP_ERR_UNSUPPORTED, "host count");
+  if (repack_blob_protos_offset(m->H, m->K) != all) return fail(PGP_ERR_STATE, "master / blob layout mismatch");
+  if (!m->d_pscr) HIPCHK(hipMalloc(&m->d_pscr, repack_scratch_len(m->H) * sizeof(double)));
+  RepackArgs a{m->K, P_device, all, prototypes_device, m->d_pscr, m->d_frags, m->d_tab, m->d_gtab, m->d_gat};
+  HIPCHK(launch_repack(m->H, a, reinterpret_cast<hipStream_t>(stream)));
   return PGP_OK;
 }
 

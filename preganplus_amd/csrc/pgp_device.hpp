@@ -24,7 +24,7 @@ struct FwdArgs {
   const float* frags;    // device weight fragments (Geo<H> offsets)
   const float* tab;      // encoder/decoder tables (LDS-staged)
   const float* gtab;     // GAN tables
-  GatConst gat;
+  const float* gat;      // GAT constants u[4] | v[4] (device)
   float* logits;
   float* protos;
   int* cls;

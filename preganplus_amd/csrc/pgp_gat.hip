@@ -37,7 +37,7 @@ constexpr int seg_lanes(int h) { return h <= 8 ? 8 : h <= 16 ? 16 : h <= 32 ? 32
 
 template <int H>
 __global__ __launch_bounds__(256) void gat_agg_kernel(int B, const float* __restrict__ win,
-                                                      float* __restrict__ agg, GatConst gc) {
+                                                      float* __restrict__ agg, const float* __restrict__ gcp) {
   static_assert(H <= 64, "GAT kernel maps hosts to lanes");
   constexpr int S = seg_lanes(H), P = 64 / S, SS = P > 1 ? S + 1 : S;
   constexpr int BLK = H * 3 * 48;  // floats per 16-window block
@@ -47,6 +47,7 @@ __global__ __launch_bounds__(256) void gat_agg_kernel(int B, const float* __rest
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int seg = lane / S, hl = lane % S;  // item slot, destination host
   const long blk = blockIdx.x;
+  const float gu0 = gcp[0], gu1 = gcp[1], gu2 = gcp[2], gv0 = gcp[4], gv1 = gcp[5], gv2 = gcp[6];
   for (int i = threadIdx.x; i < BLK; i += 256) out_lds[i] = 0.f;
   __syncthreads();
   for (int i0 = wv * P; i0 < 48; i0 += 4 * P) {
@@ -62,8 +63,8 @@ __global__ __launch_bounds__(256) void gat_agg_kernel(int B, const float* __rest
       x1 = p[1];
       x2 = p[2];
     }
-    const float s = gc.u[0] * x0 + gc.u[1] * x1 + gc.u[2] * x2;
-    const float t = gc.v[0] * x0 + gc.v[1] * x1 + gc.v[2] * x2;
+    const float s = gu0 * x0 + gu1 * x1 + gu2 * x2;
+    const float t = gv0 * x0 + gv1 * x1 + gv2 * x2;
     float smax = host ? s : -INFINITY, tmax = host ? t : -INFINITY;
 #pragma unroll
     for (int off = S / 2; off >= 1; off >>= 1) {

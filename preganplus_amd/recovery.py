@@ -125,16 +125,23 @@ class PreGANPlusRecovery(Recovery):
     def tune_model(self):
         wins, _, anom, cls = TR.on_the_fly_dataset(self.env.stats.time_series, self.env.stats.schedule_series,
                                                    self.train_time_data)
-        losses = TR.backprop(self.trainer, self.tune_state, wins, anom, cls)
+        # backprop + accuracy (PreGANPlus.py:55-56) in one device graph
+        losses, (anomaly_score, class_score) = TR.backprop(self.trainer, self.tune_state, wins, anom, cls,
+                                                           score=True)
         loss = float(np.mean([a for a, _ in losses]) + np.mean([t for _, t in losses]))   # train.py:56-57
         factor = self.tune_state.factor + TR.PROTO_UPDATE_MIN
-        anomaly_score, class_score = TR.accuracy(self.trainer, self.tune_state, wins, anom, cls)  # :56
         self.accuracy_list.append((loss, factor, anomaly_score, class_score))                  # :58
         return losses
 
     def sync_inference_weights(self):
-        """Rebuild the inference kernels' packed weights from the trained master."""
-        self.infer.load_master(self.trainer.P, self.tune_state.protos)
+        """Rebuild the inference kernels' packed weights from the trained master
+        on the device (pgp_repack_master): P and the prototypes of the tuning
+        state never leave the GPU."""
+        K = self.tune_state.protos.shape[0]
+        dev_state = getattr(self.trainer, "tune_state_dev", None)
+        if dev_state is None:
+            dev_state = torch.tensor(self.tune_state.vector(), dtype=torch.float64, device=self.trainer.device)
+        self.infer.repack_master(self.trainer.P, dev_state[:2 * K], self.tune_state.protos)
         self.prototypes = self.tune_state.protos.copy()
 
     # -- PreGANPlus.py:83-105 --

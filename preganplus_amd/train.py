@@ -287,6 +287,27 @@ class Trainer:
                 tab[s, k] = (float(active), lr / (1 - self.b1 ** st), math.sqrt(1 - self.b2 ** st))
         return sel, tab
 
+    def adam_schedule_np(self, section: str, positive, cond_names):
+        """adam_schedule for the tuning loop's pattern, vectorised: step s of a
+        call skips the tensors named in cond_names unless positive[s] (the
+        prototype decoder gets no gradient from a window without a positive
+        label).  Same values as adam_schedule, same step-count advance."""
+        lr = self.lrs[section]
+        sel = [t for t in self.tensors if t["section"] == section and t["trainable"]]
+        positive = np.asarray(positive, dtype=bool)
+        cond = np.array([t["name"] in cond_names for t in sel])
+        active = np.where(cond[None, :], positive[:, None], True)                # [steps, T]
+        step0 = np.array([t["step"] for t in sel], dtype=np.float64)
+        steps = step0[None, :] + np.cumsum(active, axis=0)
+        st = np.maximum(steps, 1.0)
+        tab = np.empty(active.shape + (3,), dtype=np.float32)
+        tab[..., 0] = active
+        tab[..., 1] = lr / (1 - self.b1 ** st)
+        tab[..., 2] = np.sqrt(1 - self.b2 ** st)
+        for k, t in enumerate(sel):
+            t["step"] = float(steps[-1, k])
+        return tab
+
     def adam_step_table(self, section: str, sel, sched):
         """AdamW over `sel` with the per-step scalars in the device row `sched`
         [T,3] (``pgp_adamw_table``): fixed kernel arguments, graph-capturable."""
@@ -332,6 +353,16 @@ class TuneState:
         layout pgp_tune_targets updates)."""
         v = np.concatenate([self.protos.reshape(-1), [self.factor, self.num_zero, self.num_ones]])
         return torch.tensor(v, dtype=torch.float64, device=device)
+
+    def vector(self):
+        """[2K+3] fp64 = prototypes [K][2], factor, num_zero, num_ones."""
+        return np.concatenate([self.protos.reshape(-1), [self.factor, self.num_zero, self.num_ones]])
+
+    def from_vector(self, v):
+        K = (v.size - 3) // 2
+        self.protos = np.array(v[:2 * K], dtype=np.float64).reshape(K, 2)
+        self.factor = float(v[2 * K])
+        self.num_zero, self.num_ones = int(v[2 * K + 1]), int(v[2 * K + 2])
 
     def from_device(self, t):
         v = t.cpu().numpy()
@@ -640,24 +671,51 @@ class _TuneGraph:
     graph.  Per step, at 8 / 16 hosts: the fused step (``tune_step1``: forward,
     bookkeeping and backward in one workgroup) -> AdamW from a device table —
     2 launches; otherwise tune_forward -> tune_targets -> tune_backward
-    (zero_grad + kernels) -> AdamW, ~45 launches.  Inputs live in fixed device
-    buffers that each call refills; a replay issues every launch of the n
-    steps with one host call."""
+    (zero_grad + kernels) -> AdamW, ~45 launches.  With ``score``, the graph
+    ends with the batched forward of accuracy() (train.py:94-109) on the
+    updated weights.
 
-    def __init__(self, tr: Trainer, n: int, win_shape, K: int, fused: bool | None = None):
+    Host traffic per call: ONE upload of every input (windows, labels,
+    classes, state, AdamW table) from a pinned staging buffer into the device
+    buffer the graph reads, and ONE download of every output (losses, state,
+    accuracy logits / prototypes, gathered into one fp64 buffer inside the
+    graph)."""
+
+    def __init__(self, tr: Trainer, n: int, win_shape, K: int, fused: bool | None = None, score: bool = False):
         H, dev = tr.H, tr.device
         if fused is None:
             fused = H in FUSED_STEP_HOSTS
-        self.n, self.generation, self.fused = n, tr.generation, fused
-        self.W = torch.zeros((n,) + tuple(win_shape), dtype=torch.float32, device=dev)
-        self.Y = torch.zeros((n, H), dtype=torch.int32, device=dev)
-        self.C = torch.zeros((n, H), dtype=torch.int32, device=dev)
-        self.state = torch.zeros(2 * K + 3, dtype=torch.float64, device=dev)
+        self.n, self.fused, self.score, self.K = n, fused, score, K
+        self.sel = [t for t in tr.tensors if t["section"] == "transformer" and t["trainable"]]
+        nw = int(np.prod(win_shape))
+        # input staging: windows f32 | y i32 | cls i32 | AdamW table f32 | state f64 (8-byte aligned)
+        parts = [("W", torch.float32, (n,) + tuple(win_shape)), ("Y", torch.int32, (n, H)),
+                 ("C", torch.int32, (n, H)), ("sched", torch.float32, (n, len(self.sel), 3)),
+                 ("state", torch.float64, (2 * K + 3,))]
+        off, lay = 0, []
+        for name, dt, shp in parts:
+            nb = int(np.prod(shp)) * torch.tensor([], dtype=dt).element_size()
+            off = (off + 7) // 8 * 8
+            lay.append((name, dt, shp, off, nb))
+            off += nb
+        self.din = torch.zeros(off, dtype=torch.uint8, device=dev)
+        self.hin = torch.zeros(off, dtype=torch.uint8).pin_memory()
+        self.hviews = {}
+        for name, dt, shp, o, nb in lay:
+            setattr(self, name, self.din[o:o + nb].view(dt).view(shp))
+            self.hviews[name] = self.hin[o:o + nb].view(dt).view(shp).numpy()
+        # output gather: loss [n,2] | state [2K+3] | logits [n,H,2] | protos [n,H,2] (fp64)
+        nout = 2 * n + 2 * K + 3 + (4 * n * H if score else 0)
+        self.dout = torch.zeros(nout, dtype=torch.float64, device=dev)
+        self.hout = torch.zeros(nout, dtype=torch.float64).pin_memory()
+        self.loss = self.dout[:2 * n].view(n, 2)
         self.mult = torch.zeros((1, H), dtype=torch.float32, device=dev)
         self.tgt = torch.zeros((1, H, 2), dtype=torch.float32, device=dev)
-        self.loss = torch.zeros((n, 2), dtype=torch.float64, device=dev)
-        self.sel = [t for t in tr.tensors if t["section"] == "transformer" and t["trainable"]]
-        self.sched = torch.zeros((n, len(self.sel), 3), dtype=torch.float32, device=dev)
+        if score:
+            tr._ensure(n)
+        else:
+            tr._ensure(1)
+        self.generation = tr.generation
         self.graph = torch.cuda.CUDAGraph()
         torch.cuda.synchronize(dev)
         with torch.cuda.graph(self.graph):
@@ -669,24 +727,47 @@ class _TuneGraph:
                     tr.tune_targets(self.Y[i], self.C[i], self.state, self.mult, self.tgt, self.loss[i])
                     tr.tune_backward(1, self.Y[i:i + 1], self.mult, self.tgt)
                 tr.adam_step_table("transformer", self.sel, self.sched[i])
+            o = 2 * n
+            self.dout[o:o + 2 * K + 3].copy_(self.state)
+            if score:
+                o += 2 * K + 3
+                lg, pr = tr.tune_forward(self.W)
+                self.dout[o:o + 2 * n * H].copy_(lg.reshape(-1))
+                self.dout[o + 2 * n * H:o + 4 * n * H].copy_(pr.reshape(-1))
+
+    def run(self, tr, wins, anom, cls, state_vec, tab):
+        hv = self.hviews
+        hv["W"][...] = wins
+        hv["Y"][...] = anom
+        hv["C"][...] = cls
+        hv["sched"][...] = tab
+        hv["state"][...] = state_vec
+        self.din.copy_(self.hin, non_blocking=True)
+        self.graph.replay()
+        self.hout.copy_(self.dout, non_blocking=True)
+        torch.cuda.current_stream(tr.device).synchronize()
+        return self.hout.numpy()
 
 
-def backprop(tr: Trainer, st: TuneState, wins, anom, cls, fused: bool | None = None):
+def backprop(tr: Trainer, st: TuneState, wins, anom, cls, fused: bool | None = None, score: bool = False):
     """train.py:42-57: sequential batch-1 steps (forward, custom_loss, backward,
-    AdamW).  Returns the per-window (aloss, tloss).
+    AdamW).  Returns the per-window (aloss, tloss); with ``score`` also
+    accuracy()'s (AScore, CScore) of the updated model on the same windows
+    (train.py:94-109, as tune_model calls it, PreGANPlus.py:56), computed in
+    the same graph.
 
     Every step stays on the device: custom_loss's sequential bookkeeping runs
-    in a kernel (``tune_targets``, state in fp64), AdamW's per-step scalars come
-    from a table computed ahead on the host (``Trainer.adam_schedule``), and the
-    n steps replay as one captured HIP graph (``_TuneGraph``, cached per n).
-    The host uploads the inputs and reads back the final state and the loss
-    values once per call.  ``loss_targets`` is the same bookkeeping in numpy
-    (the data-parallel step keeps it on the host; the tests restate with it)."""
+    in a kernel (state in fp64), AdamW's per-step scalars come from a table
+    computed ahead on the host (``Trainer.adam_schedule``), and the n steps
+    replay as one captured HIP graph (``_TuneGraph``, cached per shape).  The
+    host uploads the inputs and reads back the results once per call.
+    ``loss_targets`` is the same bookkeeping in numpy (the tests restate with
+    it)."""
     st.num_zero, st.num_ones = 1, 1
     wins = np.asarray(wins)
-    n, H, dev = wins.shape[0], tr.H, tr.device
+    n, H = wins.shape[0], tr.H
     if n == 0:
-        return []
+        return ([], None) if score else []
     anom = np.asarray(anom).reshape(n, H)
     cls = np.asarray(cls).reshape(n, H)
     bad = (anom > 0) & ((cls < 0) | (cls > 2))
@@ -695,22 +776,23 @@ def backprop(tr: Trainer, st: TuneState, wins, anom, cls, fused: bool | None = N
     K = st.protos.shape[0]
     if fused is None:
         fused = H in FUSED_STEP_HOSTS
-    key = (n, wins.shape[1:], K, bool(fused))
+    key = (n, wins.shape[1:], K, bool(fused), bool(score))
     g = tr._graphs.get(key)
     if g is None or g.generation != tr.generation:
-        tr._ensure(1)
-        g = tr._graphs[key] = _TuneGraph(tr, n, wins.shape[1:], K, fused)
-    inactive = [() if np.any(anom[i] > 0) else ("prototype_decoder.0.weight", "prototype_decoder.0.bias")
-                for i in range(n)]
-    _, tab = tr.adam_schedule("transformer", inactive)
-    g.W.copy_(torch.from_numpy(wins.astype(np.float32)))
-    g.Y.copy_(torch.from_numpy(anom.astype(np.int32)))
-    g.C.copy_(torch.from_numpy(cls.astype(np.int32)))
-    g.state.copy_(st.to_device("cpu"))
-    g.sched.copy_(torch.from_numpy(tab))
-    g.graph.replay()
-    st.from_device(g.state)
-    return [tuple(r) for r in g.loss.cpu().numpy().tolist()]
+        g = _TuneGraph(tr, n, wins.shape[1:], K, fused, score)
+        tr._graphs[key] = g
+    positive = np.any(anom > 0, axis=1)
+    tab = tr.adam_schedule_np("transformer", positive, ("prototype_decoder.0.weight", "prototype_decoder.0.bias"))
+    out = g.run(tr, wins, anom, cls, st.vector(), tab)
+    tr.tune_state_dev = g.state     # the updated state, on the device (prototypes first: the device repack)
+    st.from_vector(out[2 * n:2 * n + 2 * K + 3])
+    losses = [tuple(r) for r in out[:2 * n].reshape(n, 2).tolist()]
+    if not score:
+        return losses
+    o = 2 * n + 2 * K + 3
+    lg = out[o:o + 2 * n * H].reshape(n, H, 2)
+    pr = out[o + 2 * n * H:o + 4 * n * H].reshape(n, H, 2)
+    return losses, accuracy_scores(lg, pr, anom, cls, st.protos)
 
 
 def bce_target(new_score, orig_score):
@@ -747,28 +829,36 @@ def train_gan(tr: Trainer, emb, sched, simulate):
 def accuracy(tr: Trainer, st: TuneState, wins, anom, cls):
     """train.py:94-109 after a tuning call (PreGANPlus.py:56): the updated model
     on the same windows (one batched forward, pgp_tune_forward), then the
-    reference's per-window scores in its order — anomaly_accuracy (:60-73, the
-    fraction of hosts whose argmax matches the label) and class_accuracy
-    (:75-92, positives closer to their class prototype than to both others,
-    over 1e-4 + positives).  Returns (AScore, CScore).  Like the reference it
-    raises ZeroDivisionError when no window of the set has a positive label
-    (class_total = 0, train.py:109)."""
+    reference's per-window scores (``accuracy_scores``).  Returns (AScore,
+    CScore).  ``backprop(..., score=True)`` computes the same inside the tuning
+    graph."""
     wins = np.asarray(wins)
     n = wins.shape[0]
     logits, protos = tr.tune_forward(torch.as_tensor(wins, dtype=torch.float32))
     lg = logits[:n].cpu().numpy().astype(np.float64)
     pr = protos[:n].cpu().numpy().astype(np.float64)
-    anom = np.asarray(anom).reshape(n, tr.H)
-    cls = np.asarray(cls).reshape(n, tr.H)
-    P = st.protos
+    return accuracy_scores(lg, pr, anom, cls, st.protos)
+
+
+def accuracy_scores(lg, pr, anom, cls, P):
+    """The reference's per-window scores in its order — anomaly_accuracy
+    (train.py:60-73, the fraction of hosts whose argmax matches the label) and
+    class_accuracy (:75-92, positives closer to their class prototype than to
+    both others, over 1e-4 + positives) — from the forward's logits / protos
+    [n,H,2] and prototypes P.  Like the reference it raises ZeroDivisionError
+    when no window of the set has a positive label (class_total = 0,
+    train.py:109)."""
+    n, H = lg.shape[0], lg.shape[1]
+    anom = np.asarray(anom).reshape(n, H)
+    cls = np.asarray(cls).reshape(n, H)
     anomaly_correct, class_correct, class_total = 0, 0, 0
     for i in range(n):
         res = (lg[i, :, 1] > lg[i, :, 0]).astype(np.int64)   # torch.argmax, ties -> 0
-        anomaly_correct += int(np.sum(res == anom[i])) / tr.H
+        anomaly_correct += int(np.sum(res == anom[i])) / H
         if np.sum(anom[i]) > 0:
             class_total += 1
             correct, total = 0, 1e-4
-            for h in range(tr.H):
+            for h in range(H):
                 if anom[i, h] > 0:
                     total += 1
                     c = int(cls[i, h])

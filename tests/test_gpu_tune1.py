@@ -139,3 +139,21 @@ def test_fused_step_rejects_unsupported_hosts():
     loss = torch.zeros(2, dtype=torch.float64, device=dev)
     with pytest.raises(_native.NativeError):
         tr.tune_step1(z, yi, yi, state, loss)
+
+
+def test_backprop_score_equals_separate_accuracy():
+    """backprop(score=True) — accuracy()'s forward inside the tuning graph —
+    gives the same losses, parameters and (AScore, CScore) as backprop followed
+    by a separate accuracy() call."""
+    from preganplus_amd import train as TR
+    w, extra = load16()
+    z = np.load(f"{GOLD}/tune_h16.npz")
+    a, b = TR.Trainer(16, w, extra), TR.Trainer(16, w, extra)
+    sa, sb = TR.TuneState(z["protos0"], float(z["factor0"])), TR.TuneState(z["protos0"], float(z["factor0"]))
+    for _ in range(2):
+        la = TR.backprop(a, sa, z["windows"], z["anom"], z["cls"])
+        acc_a = TR.accuracy(a, sa, z["windows"], z["anom"], z["cls"])
+        lb, acc_b = TR.backprop(b, sb, z["windows"], z["anom"], z["cls"], score=True)
+        assert la == lb and acc_a == acc_b
+        assert torch.equal(a.P, b.P)
+        np.testing.assert_array_equal(sa.protos, sb.protos)
