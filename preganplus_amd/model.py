@@ -81,19 +81,28 @@ class DecisionModel:
     def reserve(self, max_batch: int):
         _native.check(self._L.pgp_reserve(self._h, int(max_batch)), "pgp_reserve")
 
-    def alloc_outputs(self, B: int, latent: bool = False):
+    def alloc_outputs(self, B: int, latent: bool = False, packed: bool = False):
+        """Output tensors of forward().  packed=True places them all in one
+        device buffer (every output is 4-byte) with a pinned host twin, so
+        to_numpy() reads the whole result with ONE device-to-host copy (the
+        batch-1 plugin path)."""
         dev, H = self.device, self.H
         f32, i32 = torch.float32, torch.int32
-        out = dict(
-            logits=torch.empty((B, H, 2), dtype=f32, device=dev),
-            protos=torch.empty((B, H, 2), dtype=f32, device=dev),
-            cls=torch.empty((B, H), dtype=i32, device=dev),
-            any=torch.empty((B,), dtype=i32, device=dev),
-            probs=torch.empty((B, 2), dtype=f32, device=dev),
-            keep=torch.empty((B,), dtype=i32, device=dev),
-            final_target=torch.empty((B, H), dtype=i32, device=dev),
-            gen_target=torch.empty((B, H), dtype=i32, device=dev),
-        )
+        spec = [("logits", f32, (B, H, 2)), ("protos", f32, (B, H, 2)), ("cls", i32, (B, H)), ("any", i32, (B,)),
+                ("probs", f32, (B, 2)), ("keep", i32, (B,)), ("final_target", i32, (B, H)),
+                ("gen_target", i32, (B, H))]
+        if packed:
+            n = sum(int(np.prod(s)) for _, _, s in spec)
+            buf = torch.zeros(n, dtype=i32, device=dev)
+            out, o = {}, 0
+            for name, dt, shp in spec:
+                k = int(np.prod(shp))
+                out[name] = buf[o:o + k].view(dt).view(shp)
+                o += k
+            out["_buf"] = buf
+            out["_hbuf"] = torch.zeros(n, dtype=i32).pin_memory()
+        else:
+            out = {name: torch.empty(shp, dtype=dt, device=dev) for name, dt, shp in spec}
         out["latent"] = torch.empty((B, 3 * H * H), dtype=f32, device=dev) if latent else None
         return out
 
@@ -231,8 +240,23 @@ def assemble_decision(original_decision, moves_row, cur_host_row):
 
 def to_numpy(out: dict) -> dict:
     res = {}
+    if "_buf" in out:   # packed outputs: one device-to-host copy, numpy views of the pinned twin
+        hb = out["_hbuf"]
+        hb.copy_(out["_buf"], non_blocking=True)
+        torch.cuda.current_stream(out["_buf"].device).synchronize()
+        a, o = hb.numpy(), 0
+        for k, v in out.items():
+            if k.startswith("_") or v is None or k == "latent":
+                continue
+            n = v.numel()
+            x = a[o:o + n].view(np.float32 if v.dtype == torch.float32 else np.int32).reshape(tuple(v.shape)).copy()
+            res[k] = x.astype(bool) if k in ("any", "keep") else x
+            o += n
+        if out.get("latent") is not None:
+            res["latent"] = out["latent"].detach().cpu().numpy()
+        return res
     for k, v in out.items():
-        if v is None:
+        if v is None or k.startswith("_"):
             continue
         a = v.detach().cpu().numpy()
         if k in ("any", "keep"):

@@ -146,21 +146,44 @@ class PreGANPlusRecovery(Recovery):
 
     # -- PreGANPlus.py:83-105 --
     def recover_decision(self, embedding, schedule_data, original_decision):
-        _, probs = self.trainer.gan_forward(np.asarray(embedding)[None], np.asarray(schedule_data)[None])
-        p = probs[0].cpu().numpy()
+        # the updated GAN's gate on (embedding, schedule_data): computed at the end of
+        # train_gan's graph (tr.gan_probs_after, same kernels and inputs), else here
+        p = self.trainer.__dict__.pop("gan_probs_after", None)
+        if p is None:
+            _, probs = self.trainer.gan_forward(np.asarray(embedding)[None], np.asarray(schedule_data)[None])
+            p = probs[0].cpu().numpy()
         res, hf = _recover(self.env, self.hosts, schedule_data, original_decision, bool(p[0] > p[1]),
-                           self.infer.device, getattr(self, "_final_target", None))
+                           self.infer.device, getattr(self, "_final_target", None), io=self._recover_io())
         if hf is not None:
             self.hosts_from = hf
         return res
+
+    def _recover_io(self):
+        if getattr(self, "_rio", None) is None:
+            self._rio = _RecoverIO(self.hosts, self.infer.device)
+        return self._rio
+
+    def _detect(self, win, schedule_data):
+        """The batch-1 forward of run_model (K1-K3) from pinned staging buffers:
+        one host-to-device copy in, one device-to-host copy out (to_numpy)."""
+        H, dev = self.hosts, self.infer.device
+        if getattr(self, "_io", None) is None:
+            nin = 9 * H + H * H
+            self._io = (torch.zeros(nin, dtype=torch.float32).pin_memory(),
+                        torch.zeros(nin, dtype=torch.float32, device=dev),
+                        self.infer.alloc_outputs(1, packed=True))
+        hin, din, out = self._io
+        h = hin.numpy()
+        h[:9 * H] = np.asarray(win, dtype=np.float32).reshape(-1)
+        h[9 * H:] = np.asarray(schedule_data, dtype=np.float32).reshape(-1)
+        din.copy_(hin, non_blocking=True)
+        return self.infer.forward(din[:9 * H].view(1, 3, 3 * H), din[9 * H:].view(1, H, H), out=out)
 
     # -- PreGANPlus.py:115-136 --
     def run_model(self, time_series, original_decision):
         schedule_data = np.asarray(self.env.scheduler.result_cache, dtype=np.float64)
         win = self.input_window()
-        dev = self.infer.device
-        out = to_numpy(self.infer.forward(torch.tensor(win[None], dtype=torch.float32, device=dev),
-                                          torch.tensor(schedule_data[None], dtype=torch.float32, device=dev)))
+        out = to_numpy(self._detect(win, schedule_data))
         if not out["any"][0]:
             return original_decision
         anom = out["logits"][0, :, 1] > out["logits"][0, :, 0]
@@ -215,7 +238,33 @@ def save_checkpoints(trainer, folder, env_name, epoch, accuracy_list, entries):
         torch.save(ck, os.path.join(folder, f"{env_name}_{name}.ckpt"))
 
 
-def _recover(env, hosts, schedule_data, original_decision, keep_original, device, final_target=None):
+class _RecoverIO:
+    """Pinned / device staging of one K5 call: keep | final_target | cur_host in
+    one upload, moves | hosts_from in one download."""
+
+    def __init__(self, C, device):
+        self.C = C
+        self.hin = torch.zeros(1 + 2 * C, dtype=torch.int32).pin_memory()
+        self.din = torch.zeros(1 + 2 * C, dtype=torch.int32, device=device)
+        self.dout = torch.zeros((2, 1, C), dtype=torch.int32, device=device)
+        self.hout = torch.zeros((2, 1, C), dtype=torch.int32).pin_memory()
+
+    def run(self, final_target, cur):
+        C = self.C
+        h = self.hin.numpy()
+        h[0] = 0
+        h[1:1 + C] = final_target
+        h[1 + C:] = cur
+        self.din.copy_(self.hin, non_blocking=True)
+        migrations(self.din[:1], self.din[1:1 + C].view(1, C), self.din[1 + C:].view(1, C),
+                   out=(self.dout[0], self.dout[1]))
+        self.hout.copy_(self.dout, non_blocking=True)
+        torch.cuda.current_stream(self.din.device).synchronize()
+        o = self.hout.numpy()
+        return o[0, 0].copy(), o[1, 0].copy()
+
+
+def _recover(env, hosts, schedule_data, original_decision, keep_original, device, final_target=None, io=None):
     """recover_decision's decision loop (PreGAN.py:77-95 == PreGANPlus.py:84-105)
     on the device (K5, pgp_migrations): every placed container moves to the first
     argmax of its ORIGINAL schedule row.  Returns (decision list, hosts_from)."""
@@ -228,9 +277,9 @@ def _recover(env, hosts, schedule_data, original_decision, keep_original, device
     if final_target is None:
         s = np.asarray(schedule_data)
         final_target = [row.index(max(row)) for row in s.tolist()]
-    i32 = lambda a: torch.tensor(np.asarray(a, dtype=np.int32).reshape(1, -1), device=device)
-    moves, hosts_from = migrations(torch.zeros(1, dtype=torch.int32, device=device), i32(final_target), i32(cur))
-    moves, hosts_from = moves[0].cpu().numpy(), hosts_from[0].cpu().numpy()
+    if io is None:
+        io = _RecoverIO(hosts, device)
+    moves, hosts_from = io.run(np.asarray(final_target, dtype=np.int32), np.asarray(cur, dtype=np.int32))
     return assemble_decision(original_decision, moves, cur), [int(v) for v in hosts_from]
 
 

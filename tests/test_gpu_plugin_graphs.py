@@ -1,0 +1,47 @@
+"""The plugin's batch-1 latency plumbing against the eager path it replaces:
+train_gan's two captured graphs (``_GanGraph``) vs ``train_gan_eager``
+(individual launches, PreGANPlus.py:60-75), bit for bit, including the
+post-training Disc gate recover_decision reads; and the packed single-copy
+detect outputs vs the per-tensor outputs."""
+import numpy as np
+import pytest
+import torch
+
+from preganplus_amd import weights as W
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("scores", [(1.0, 2.0), (3.0, 1.0)])
+def test_gan_graph_equals_eager(scores):
+    from preganplus_amd import train as TR
+    w, extra = W.load_npz("preganplus_amd/data/simulator_16.npz")
+    z = np.load("tests/golden/gan_h16.npz")
+    a, b = TR.Trainer(16, w, extra), TR.Trainer(16, w, extra)
+    for call in range(3):      # capture, then replays with new inputs
+        emb = z["emb"] * (1 + 0.1 * call)
+        sched = np.roll(z["sched"], call, axis=1)
+        ia, ib = iter(scores), iter(scores)
+        ra = TR.train_gan_eager(a, emb, sched, lambda s: next(ia))
+        rb = TR.train_gan(b, emb, sched, lambda s: next(ib))
+        np.testing.assert_array_equal(ra[0], rb[0])
+        assert ra[1:] == rb[1:]
+        for t in ("P", "m", "v"):
+            assert torch.equal(getattr(a, t), getattr(b, t)), t
+        assert [t["step"] for t in a.tensors] == [t["step"] for t in b.tensors]
+        _, probs = a.gan_forward(np.asarray(emb)[None], np.asarray(sched)[None])
+        np.testing.assert_array_equal(probs[0].cpu().numpy(), b.gan_probs_after)
+
+
+def test_packed_outputs_equal_plain():
+    from preganplus_amd.model import DecisionModel, to_numpy
+    w, _ = W.load_npz("preganplus_amd/data/simulator_16.npz")
+    m = DecisionModel(16, w)
+    rng = np.random.default_rng(1)
+    x = torch.tensor(rng.uniform(0, 1, (3, 3, 48)), dtype=torch.float32, device=m.device)
+    s = torch.tensor(rng.uniform(0, 1, (3, 16, 16)), dtype=torch.float32, device=m.device)
+    a = to_numpy(m.forward(x, s))
+    b = to_numpy(m.forward(x, s, out=m.alloc_outputs(3, packed=True)))
+    assert a.keys() == b.keys()
+    for k in a:
+        assert a[k].dtype == b[k].dtype and np.array_equal(a[k], b[k]), k
