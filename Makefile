@@ -11,7 +11,7 @@ OBJS := $(patsubst $(CSRC)/%,$(OBJDIR)/%.o,$(SRCS))
 HDRS := include/preganplus.h $(CSRC)/pgp_layout.hpp $(CSRC)/pgp_pack.hpp $(CSRC)/pgp_device.hpp $(CSRC)/pgp_train.hpp $(CSRC)/pgp_tune.hpp $(CSRC)/pgp_tunedp.hpp $(CSRC)/pgp_tunetargets.hpp $(CSRC)/pgp_gemm.hpp $(CSRC)/pgp_packcore.hpp $(CSRC)/pgp_repack.hpp
 CXXFLAGS := -O3 -std=c++17 -fPIC -Wall -Wno-unused-function
 
-.PHONY: all clean resource-usage variant
+.PHONY: all clean resource-usage variant asan
 all: $(LIB)
 
 $(OBJDIR)/%.o: $(CSRC)/% $(HDRS)
@@ -30,6 +30,15 @@ variant:
 	@for f in $(SRCS); do b=$$(basename $$f); \
 	  $(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) $(VFLAGS) -c -o $(VOBJDIR)/$$b.o $$f & done; wait
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(LIBDIR)/var/libpreganplus_$(NAME).so $(VOBJDIR)/*.o
+
+# host-only sanitizer build of the weight packer (AddressSanitizer + UBSan):
+# build/asan/pack_check packs every compiled host count and the FPE variant
+asan: build/asan/pack_check
+	./build/asan/pack_check
+build/asan/pack_check: tools/pack_check.cpp $(CSRC)/pgp_pack.cpp $(CSRC)/pgp_packcore.hpp $(CSRC)/pgp_pack.hpp $(CSRC)/pgp_layout.hpp
+	@mkdir -p build/asan
+	g++ -std=c++17 -O1 -g -fno-omit-frame-pointer -fsanitize=address,undefined -fno-sanitize-recover=all \
+	  -o $@ tools/pack_check.cpp $(CSRC)/pgp_pack.cpp
 
 # per-kernel VGPR / spill / occupancy report
 resource-usage:
