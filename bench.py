@@ -637,8 +637,10 @@ def bench_loop(args):
       GOBI schedules (pgp_gobi_optimize)  -> result_cache [E,16,16]
       K1/K2/K2b encode + detect/classify  (run_model up to the embedding)
       GAN step, labels simulated           (train_gan, pgp_simulate)
-      tuning step                          (tune_model; synthetic labels, as C3)
-      inference weight sync                (load_master: master -> packed layouts)
+      tuning step                          (tune_model's DP form with its device bookkeeping,
+                                            DPTuner; synthetic labels / classes, as C3)
+      inference weight sync                (pgp_repack_master on the device: master +
+                                            the tuning state's prototypes -> packed layouts)
       K3 + K5 with the updated GAN         (recover_decision)
     in the reference's order (PreGANPlus.py:115-136).  All cells train as one
     data-parallel batch (sum of their losses).  Shipped H=16 weights (PreGAN+
@@ -668,9 +670,9 @@ def bench_loop(args):
     x, _ = synth_inputs(E, H, device, 31 + rank)
     g = torch.Generator(device=device).manual_seed(19 + rank)
     y = (torch.rand((E, H), generator=g, device=device) < 0.1).to(torch.int32)
-    mult = torch.ones((E, H), device=device)
-    tgt = torch.rand((E, H, 2), generator=g, device=device)
-    protos = np.asarray(model.prototypes, dtype=np.float64)
+    cls = torch.randint(0, 3, (E, H), generator=g, device=device, dtype=torch.int32)
+    tun = TR.DPTuner(tr, TR.TuneState(np.asarray(model.prototypes, dtype=np.float64)), E)
+    K = model.K
     gout = (torch.empty_like(inits), torch.empty(E, dtype=torch.int32, device=device),
             torch.empty(E, dtype=torch.float32, device=device))
     out = model.alloc_outputs(E)
@@ -696,12 +698,10 @@ def bench_loop(args):
         TR.train_gan_batched(tr, sim, envs, emb, sched, out=sim_out, target=gan_target)
         if timed:
             ev[3].record()
-        tr.tune_forward(x)
-        tr.tune_backward(E, y, mult, tgt)
-        tr.adam_step("transformer")
+        tun.step(x, y, cls)
         if timed:
             ev[4].record()
-        model.load_master(tr.P, protos)
+        model.repack_master(tr.P, tun.state[:2 * K])
         if timed:
             ev[5].record()
         model.forward(x, sched, out=out, stage=3)
