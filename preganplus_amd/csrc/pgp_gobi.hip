@@ -51,53 +51,98 @@ struct GobiW {  // device offsets (floats) into one buffer
 
 __device__ __forceinline__ float sigmoid_f(float x) { return 1.f / (1.f + expf(-x)); }
 
-constexpr int kT = 1024;          // threads per environment
-constexpr int kW1S = kIn + 1;      // LDS row stride of W1: 289 = 33 (mod 64) banks -> row and column reads conflict-free
+constexpr int kT = 512;  // threads per workgroup (8 waves, 2 per SIMD: 256 VGPRs for the weight slices)
+constexpr int kNE = 4;   // environments per workgroup: they share the weight registers and every barrier
 
+// phase timing study (variant builds only): -DPGP_GOBI_PROF accumulates, in
+// workgroup 0, the wall clock of each barrier-delimited phase over the run;
+// pgp_gobi_prof_read copies the sums out
+#ifdef PGP_GOBI_PROF
+__device__ unsigned long long g_gobi_prof[16];
+#define GMARK(i)                                                        \
+  do {                                                                  \
+    if (blockIdx.x == 0 && threadIdx.x == 0) {                          \
+      const unsigned long long now_ = wall_clock64();                   \
+      g_gobi_prof[i] += now_ - gmark_t_;                                \
+      gmark_t_ = now_;                                                  \
+    }                                                                   \
+  } while (0)
+#else
+#define GMARK(i) \
+  do {           \
+  } while (0)
+#endif
+
+constexpr int kA = kH * kH;  // allocation entries
+constexpr int kSA = kA + 1;  // LDS row stride of layer 1's allocation columns (257 = 1 mod 64)
+
+// Layer 1's allocation columns (the forward's one-hot column gather) and the
+// per-environment activations; the other weights are in registers.
 struct GobiLds {
-  float w1[kN1 * kW1S];  // layer-1 weights, natural [128][288] rows padded to 289 (147,968 B)
-  float x[kIn];
-  float h1[kN1], h2[kN2];
-  float g1[kN1], g2[kN2], g3[kN3];
-  float part[1024];
-  float adam[kMaxIt * 4];  // per-iteration AdamW scalars (GobiW::ADAM)
-  int hs[kH];              // each container's host (the one-hot column of its allocation row)
-  int dense;               // 1 while the allocation may not be one-hot (a non-one-hot init, iteration 0)
-  float o[4];
-  int flag[2];
+  float w1a[kN1 * kSA];  // W1[o][c*18 + 2 + h] at [o][c*16 + h]
+  float x[kNE][kIn];
+  float h1[kNE][kN1], h2[kNE][kN2], h3[kNE][kN3], th3[kNE][kN3];
+  float g1[kNE][kN1], g2[kNE][kN2], g3[kNE][kN3];
+  float o[kNE][4];
+  int hs[kNE][kH];   // each container's host (the one-hot column of its allocation row)
+  int dense[kNE];    // the init's allocation is not one-hot (iteration 0 takes the dense layer 1)
+  int flag[2][kNE];  // "some entry changed" of the current / next iteration
 };
 
-// this thread's slices of layers 2-3, loaded once and kept in registers for
-// every iteration (forward: W2^T/W3^T column blocks; backward: W2/W3 row blocks)
+// Thread roles (fixed for the whole run; every weight slice is loaded once):
+//   128-output layers (1, 2 and the backward's dh2, dh1): o = t >> 2, k-chunk
+//     sp = t & 3; an xor butterfly over the 4 lanes sums the chunks (every
+//     lane holds the same bits) and lane sp == e owns env e's activation and
+//     keeps its pre-activation for the backward;
+//   layer 3 (64 outputs): o3 = t >> 3, k-chunk sp3 = t & 7, owner lane 2e;
+//   the head: wave e (t < 256), lane = o3;
+//   allocation entries: entry = t >> 1 (a container row = 32 lanes), k-chunk
+//     sq = t & 1 of the input gradient; lane sq owns the entry of envs
+//     e = sq, sq + 2 (their AdamW moments).
 struct GobiRegs {
-  float w2f[16], w3f[8], w3b[8], w2b[16];
-  float b1, b2, b3, w40, w41, b40, b41;  // biases (threads < 128 / < 64) and the head, off the critical path
+  float w2f[32], w2b[32], w3f[16], w3b[16], w1c[64];
+  float w1x[8];  // layer 1's cpu / ips weights of this lane's 4 containers
+  float b1, b2, b3, w40, w41, b40, b41;
 };
 
 __device__ void load_regs(const float* __restrict__ W, GobiRegs& R) {
-  const int t = threadIdx.x, o = t & 127, sp = t >> 7, o3 = t & 63, sp3 = t >> 6;
+  const int t = threadIdx.x, o = t >> 2, sp = t & 3, o3 = t >> 3, sp3 = t & 7;
+  const int entry = t >> 1, sq = t & 1, xi = (entry >> 4) * kF + 2 + (entry & 15);
 #pragma unroll
-  for (int j = 0; j < 16; ++j) R.w2f[j] = W[GobiW::W2T + (sp * 16 + j) * kN2 + o];
+  for (int j = 0; j < 64; ++j) R.w1c[j] = W[GobiW::W1T + xi * kN1 + sq * 64 + j];  // W1[k][xi]
 #pragma unroll
-  for (int j = 0; j < 8; ++j) R.w3f[j] = W[GobiW::W3T + (sp3 * 8 + j) * kN3 + o3];
+  for (int j = 0; j < 32; ++j) R.w2f[j] = W[GobiW::W2 + o * kN1 + sp * 32 + j];   // W2[o][k]
 #pragma unroll
-  for (int j = 0; j < 8; ++j) R.w3b[j] = W[GobiW::W3 + (sp * 8 + j) * kN2 + o];
+  for (int j = 0; j < 32; ++j) R.w2b[j] = W[GobiW::W2T + o * kN2 + sp * 32 + j];  // W2[k][o]
 #pragma unroll
-  for (int j = 0; j < 16; ++j) R.w2b[j] = W[GobiW::W2 + (sp * 16 + j) * kN1 + o];
+  for (int j = 0; j < 16; ++j) R.w3f[j] = W[GobiW::W3 + o3 * kN2 + sp3 * 16 + j];  // W3[o3][k]
+#pragma unroll
+  for (int j = 0; j < 16; ++j) R.w3b[j] = W[GobiW::W3T + o * kN3 + sp * 16 + j];   // W3[k][o]
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int c = 4 * sp + q;
+    R.w1x[2 * q] = W[GobiW::W1 + o * kIn + c * kF];
+    R.w1x[2 * q + 1] = W[GobiW::W1 + o * kIn + c * kF + 1];
+  }
   R.b1 = W[GobiW::B1 + o];
   R.b2 = W[GobiW::B2 + o];
   R.b3 = W[GobiW::B3 + o3];
-  R.w40 = W[GobiW::W4 + o3];
-  R.w41 = W[GobiW::W4 + kN3 + o3];
+  R.w40 = W[GobiW::W4 + (t & 63)];
+  R.w41 = W[GobiW::W4 + kN3 + (t & 63)];
   R.b40 = W[GobiW::B4];
   R.b41 = W[GobiW::B4 + 1];
 }
 
-// pre-activations and their exp / tanh, kept in the registers of the threads
-// that own them in both directions (t < 128 for layers 1-2, t < 64 for layer 3),
-// so the backward's derivatives need no transcendental
+template <int N>
+__device__ __forceinline__ float lane_sum(float v) {  // xor butterfly over N adjacent lanes (same bits in all)
+#pragma unroll
+  for (int off = 1; off < N; off <<= 1) v += __shfl_xor(v, off);
+  return v;
+}
+
+// pre-activations (and their exp) of the activations this lane owns
 struct FwdKeep {
-  float a1, z1, a2, z2, th3;
+  float a1, z1, a2, z2;
 };
 __device__ __forceinline__ float softplus_keep(float a, float& z) {  // softplus (threshold 20), z = exp(a)
   z = expf(a);
@@ -107,97 +152,104 @@ __device__ __forceinline__ float softplus_grad(float g, float a, float z) {  // 
   return a > 20.f ? g : g * z / (z + 1.f);
 }
 
-// forward of the surrogate on L.x (all 1024 threads); z in L.o[2]
-__device__ void surrogate_fwd(const float* __restrict__ W, const GobiRegs& R, GobiLds& L, FwdKeep& K, bool grad) {
-  const int t = threadIdx.x;
-  if (L.dense) {  // layer 1, dense: 128 outputs x 8 splits of K = 288 (36 each), W1 rows from LDS
-    const int o = t & 127, sp = t >> 7;
+// forward of the surrogate for the environments in act (all threads);
+// z = 0.8 o0 + 0.2 o1 in L.o[e][2]; with grad, g3 = dz/dh3 through Tanhshrink.
+// act / dense are wave-uniform (the same in every thread).
+__device__ void surrogate_fwd(const float* __restrict__ W, const GobiRegs& R, GobiLds& L, FwdKeep& K, bool grad,
+                              const bool (&act)[kNE], const bool (&dense)[kNE], unsigned long long& gmark_t_) {
+  (void)gmark_t_;
+  const int t = threadIdx.x, o = t >> 2, sp = t & 3, o3 = t >> 3, sp3 = t & 7;
+  // layer 1 (288 -> 128)
+#pragma unroll
+  for (int e = 0; e < kNE; ++e) {
+    if (!act[e]) continue;
     float acc = 0.f;
-    const float* wr = L.w1 + o * kW1S + sp * 36;
-    const float* xr = L.x + sp * 36;
-#pragma unroll 6
-    for (int k = 0; k < 36; ++k) acc = fmaf(wr[k], xr[k], acc);
-    L.part[t] = acc;
-    __syncthreads();
-    if (t < kN1) {
-      float a = 0.f;
+    if (dense[e]) {  // any allocation: k-chunk sp of 72
+      const float* wr = W + GobiW::W1 + o * kIn + sp * 72;
+      const float* xr = L.x[e] + sp * 72;
+#pragma unroll 8
+      for (int k = 0; k < 72; ++k) acc = fmaf(wr[k], xr[k], acc);
+    } else {  // one-hot allocation: containers 4sp..4sp+3: cpu, ips FMAs + their host's column (LDS)
 #pragma unroll
-      for (int q = 0; q < 8; ++q) a += L.part[q * 128 + t];
-      a += R.b1;
-      K.a1 = a;
-      L.h1[t] = softplus_keep(a, K.z1);
-    }
-    __syncthreads();
-  } else {  // layer 1 on a one-hot allocation: per container 2 FMAs (cpu, ips) + its host's column
-    if (t < kN1) {
-      const float* wr = L.w1 + t * kW1S;
-      float a = 0.f;
-#pragma unroll
-      for (int c = 0; c < kH; ++c) {
-        a = fmaf(wr[c * kF], L.x[c * kF], a);
-        a = fmaf(wr[c * kF + 1], L.x[c * kF + 1], a);
-        a = a + wr[c * kF + 2 + L.hs[c]];  // w * 1.0; the other 15 columns multiply 0
+      for (int q = 0; q < 4; ++q) {
+        const int c = 4 * sp + q;
+        acc = fmaf(R.w1x[2 * q], L.x[e][c * kF], acc);
+        acc = fmaf(R.w1x[2 * q + 1], L.x[e][c * kF + 1], acc);
+        acc = acc + L.w1a[o * kSA + c * kH + L.hs[e][c]];  // w * 1.0; the other columns multiply 0
       }
-      a += R.b1;
+    }
+    acc = lane_sum<4>(acc);
+    if (sp == e) {
+      const float a = acc + R.b1;
       K.a1 = a;
-      L.h1[t] = softplus_keep(a, K.z1);
+      L.h1[e][o] = softplus_keep(a, K.z1);
     }
-    __syncthreads();
   }
-  {  // layer 2: 128 outputs x 8 splits of K = 128 (16 each)
-    const int sp = t >> 7;
+  __syncthreads();
+  GMARK(0);
+  // layer 2 (128 -> 128): W2 row o, k-chunk sp
+#pragma unroll
+  for (int e = 0; e < kNE; ++e) {
+    if (!act[e]) continue;
     float acc = 0.f;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) acc = fmaf(R.w2f[j], L.h1[sp * 16 + j], acc);
-    L.part[t] = acc;
-    __syncthreads();
-    if (t < kN2) {
-      float a = 0.f;
-#pragma unroll
-      for (int q = 0; q < 8; ++q) a += L.part[q * 128 + t];
-      a += R.b2;
+    for (int j = 0; j < 32; ++j) acc = fmaf(R.w2f[j], L.h1[e][sp * 32 + j], acc);
+    acc = lane_sum<4>(acc);
+    if (sp == e) {
+      const float a = acc + R.b2;
       K.a2 = a;
-      L.h2[t] = softplus_keep(a, K.z2);
+      L.h2[e][o] = softplus_keep(a, K.z2);
     }
-    __syncthreads();
   }
-  {  // layer 3: 64 outputs x 16 splits of K = 128 (8 each)
-    const int sp = t >> 6;
+  __syncthreads();
+  GMARK(1);
+  // layer 3 (128 -> 64), Tanhshrink: W3 row o3, k-chunk sp3
+#pragma unroll
+  for (int e = 0; e < kNE; ++e) {
+    if (!act[e]) continue;
     float acc = 0.f;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc = fmaf(R.w3f[j], L.h2[sp * 8 + j], acc);
-    L.part[t] = acc;
-    __syncthreads();
-    if (t < kN3) {
-      float a = 0.f;
+    for (int j = 0; j < 16; ++j) acc = fmaf(R.w3f[j], L.h2[e][sp3 * 16 + j], acc);
+    acc = lane_sum<8>(acc);
+    if (sp3 == 2 * e) {
+      const float a = acc + R.b3;
+      const float th = tanhf(a);
+      L.th3[e][o3] = th;
+      L.h3[e][o3] = a - th;
+    }
+  }
+  __syncthreads();
+  GMARK(2);
+  // layer 4 (64 -> 2), sigmoid, z; wave e, lane = o3
+  if (t < 64 * kNE) {
+    const int e = t >> 6, l = t & 63;
+    bool on = false;
 #pragma unroll
-      for (int q = 0; q < 16; ++q) a += L.part[q * 64 + t];
-      a += R.b3;
-      K.th3 = tanhf(a);
-      const float h3 = a - K.th3;  // Tanhshrink
-      // layer 4 (2 outputs) in the same wave 0 (no barrier), sigmoid, z = 0.8 e + 0.2 l
+    for (int q = 0; q < kNE; ++q) on = e == q ? act[q] : on;
+    if (on) {
+      const float h3 = L.h3[e][l];
       float p0 = R.w40 * h3, p1 = R.w41 * h3;
 #pragma unroll
       for (int off = 32; off >= 1; off >>= 1) {
         p0 += __shfl_xor(p0, off);
         p1 += __shfl_xor(p1, off);
       }
-      // every lane holds the same sums (the butterfly adds commute exactly)
       const float o0 = sigmoid_f(p0 + R.b40), o1 = sigmoid_f(p1 + R.b41);
-      if (t == 0) {
-        L.o[0] = o0;
-        L.o[1] = o1;
-        L.o[2] = 0.8f * o0 + 0.2f * o1;
+      if (l == 0) {
+        L.o[e][0] = o0;
+        L.o[e][1] = o1;
+        L.o[e][2] = 0.8f * o0 + 0.2f * o1;
       }
-      if (grad) {  // backward start in the same wave: dz/do = (0.8, 0.2) through the sigmoids,
-                   // dh3 = W4^T do, through Tanhshrink
+      if (grad) {  // dz/do = (0.8, 0.2) through the sigmoids, dh3 = W4^T do, through Tanhshrink
         const float d0 = 0.8f * (1.f - o0) * o0, d1 = 0.2f * (1.f - o1) * o1;
         const float gh = R.w40 * d0 + R.w41 * d1;
-        L.g3[t] = gh - gh * (1.f - K.th3 * K.th3);
+        const float th = L.th3[e][l];
+        L.g3[e][l] = gh - gh * (1.f - th * th);
       }
     }
   }
   __syncthreads();
+  GMARK(3);
 }
 
 __global__ __launch_bounds__(kT) void gobi_kernel(int E, const float* __restrict__ W, const float* __restrict__ init,
@@ -206,25 +258,34 @@ __global__ __launch_bounds__(kT) void gobi_kernel(int E, const float* __restrict
 #pragma clang fp contract(off)  // elementwise steps as torch's separate mul/add
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   GobiLds& L = *reinterpret_cast<GobiLds*>(lds_raw);
-  const int e = blockIdx.x;
-  if (e >= E) return;  // whole workgroup
-  const int t = threadIdx.x, c = (t & 255) >> 4, hcol = t & 15;
-  const int xi = c * kF + 2 + hcol;  // threads < 256: this thread's allocation entry in the flattened input
-  for (int k = t; k < kN1 * kIn; k += kT) {
-    const int o = k / kIn, j = k - o * kIn;
-    L.w1[o * kW1S + j] = W[GobiW::W1 + k];
+  unsigned long long gmark_t_ = 0;
+#ifdef PGP_GOBI_PROF
+  gmark_t_ = wall_clock64();
+#endif
+  const int t = threadIdx.x, o = t >> 2, sp = t & 3;
+  const int entry = t >> 1, sq = t & 1, c = entry >> 4, hcol = entry & 15;
+  const int xi = c * kF + 2 + hcol;  // this thread's allocation entry in the flattened input
+  const long e0 = (long)blockIdx.x * kNE;
+  for (int k = t; k < kN1 * kA; k += kT) {
+    const int oo = k / kA, a = k - oo * kA;
+    L.w1a[oo * kSA + a] = W[GobiW::W1 + oo * kIn + (a >> 4) * kF + 2 + (a & 15)];
   }
-  for (int k = t; k < kIn; k += kT) L.x[k] = init[(long)e * kIn + k];
-  for (int k = t; k < kMaxIt * 4; k += kT) L.adam[k] = W[GobiW::ADAM + k];
-  if (t < 2) L.flag[t] = 0;
-  if (t == 0) L.dense = 0;
+  for (int k = t; k < kNE * kIn; k += kT) {
+    const int e = k / kIn;
+    L.x[e][k - e * kIn] = e0 + e < E ? init[e0 * kIn + k] : 0.f;
+  }
+  if (t < kNE) {
+    L.dense[t] = 0;
+    L.flag[0][t] = L.flag[1][t] = 0;
+  }
   GobiRegs R;
   load_regs(W, R);
   __syncthreads();
-  if (t < kH) {  // is the init's allocation one-hot?  (then layer 1 is a column gather)
+  if (t < kNE * kH) {  // is the init's allocation one-hot?  (then layer 1 is a column gather)
+    const int e = t / kH, cc = t % kH;
     int ones = 0, other = 0, h = 0;
     for (int j = 0; j < kH; ++j) {
-      const float xv = L.x[t * kF + 2 + j];
+      const float xv = L.x[e][cc * kF + 2 + j];
       if (xv == 1.f) {
         ++ones;
         h = j;
@@ -232,71 +293,85 @@ __global__ __launch_bounds__(kT) void gobi_kernel(int E, const float* __restrict
         ++other;
       }
     }
-    L.hs[t] = h;
-    if (ones != 1 || other) L.dense = 1;
+    L.hs[e][cc] = h;
+    if (ones != 1 || other) L.dense[e] = 1;  // benign race: every writer stores 1
   }
   __syncthreads();
-  float m = 0.f, v = 0.f;
-  FwdKeep K{0.f, 0.f, 0.f, 0.f, 0.f};
-  int equal = 0, it = 0;
+  GMARK(7);
+  float m[kNE / 2], v[kNE / 2];  // AdamW moments of this lane's entries (envs sq, sq + 2)
+#pragma unroll
+  for (int k = 0; k < kNE / 2; ++k) m[k] = v[k] = 0.f;
+  FwdKeep K{0.f, 0.f, 0.f, 0.f};
+  bool act[kNE], dense[kNE];
+  int equal[kNE], its[kNE];
+#pragma unroll
+  for (int e = 0; e < kNE; ++e) {
+    act[e] = e0 + e < E;
+    dense[e] = __builtin_amdgcn_readfirstlane(L.dense[e]) != 0;
+    equal[e] = 0;
+    its[e] = max_it;
+  }
+  int it = 0;
   while (it < max_it) {
-    surrogate_fwd(W, R, L, K, true);
+    bool any = false;
+#pragma unroll
+    for (int e = 0; e < kNE; ++e) any |= act[e];
+    if (!any) break;
+    surrogate_fwd(W, R, L, K, true, act, dense, gmark_t_);
     // ---- backward to the input (autograd of z; g3 came with the forward) ----
-    {  // dh2 = W3^T g3 (128 x K=64, 8 splits of 8), through softplus
-      const int sp = t >> 7;
+    // dh2 = W3^T g3 through softplus (W3 column o, k-chunk sp)
+#pragma unroll
+    for (int e = 0; e < kNE; ++e) {
+      if (!act[e]) continue;
       float acc = 0.f;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc = fmaf(R.w3b[j], L.g3[sp * 8 + j], acc);
-      L.part[t] = acc;
-      __syncthreads();
-      if (t == 0) L.flag[(it + 1) & 1] = 0;  // next iteration's flag; its last readers passed barriers since
-      if (t < kN2) {
-        float a = 0.f;
-#pragma unroll
-        for (int q = 0; q < 8; ++q) a += L.part[q * 128 + t];
-        L.g2[t] = softplus_grad(a, K.a2, K.z2);
-      }
-      __syncthreads();
+      for (int j = 0; j < 16; ++j) acc = fmaf(R.w3b[j], L.g3[e][sp * 16 + j], acc);
+      acc = lane_sum<4>(acc);
+      if (sp == e) L.g2[e][o] = softplus_grad(acc, K.a2, K.z2);
     }
-    {  // dh1 = W2^T g2 (128 x K=128, 8 splits of 16), through softplus
-      const int sp = t >> 7;
+    if (t < kNE) L.flag[(it + 1) & 1][t] = 0;  // next iteration's flag; its last readers passed barriers since
+    __syncthreads();
+    GMARK(4);
+    // dh1 = W2^T g2 through softplus (W2 column o, k-chunk sp)
+#pragma unroll
+    for (int e = 0; e < kNE; ++e) {
+      if (!act[e]) continue;
       float acc = 0.f;
 #pragma unroll
-      for (int j = 0; j < 16; ++j) acc = fmaf(R.w2b[j], L.g2[sp * 16 + j], acc);
-      L.part[t] = acc;
-      __syncthreads();
-      if (t < kN1) {
-        float a = 0.f;
+      for (int j = 0; j < 32; ++j) acc = fmaf(R.w2b[j], L.g2[e][sp * 32 + j], acc);
+      acc = lane_sum<4>(acc);
+      if (sp == e) L.g1[e][o] = softplus_grad(acc, K.a1, K.z1);
+    }
+    __syncthreads();
+    GMARK(5);
+    // dx for the 256 allocation entries (W1[:, xi] . g1, 2 k-chunks of 64), AdamW, one-hot
+    const float* ad = W + GobiW::ADAM + it * 4;
+    const float a0 = ad[0], a1 = ad[1], a2 = ad[2];
 #pragma unroll
-        for (int q = 0; q < 8; ++q) a += L.part[q * 128 + t];
-        L.g1[t] = softplus_grad(a, K.a1, K.z1);
-      }
-      __syncthreads();
-    }
-    {  // dx for the 256 allocation entries: W1[:, xi] . g1, 4 splits of 32 over the LDS copy
-      const int sp = t >> 8;
+    for (int e = 0; e < kNE; ++e) {
+      if (!act[e]) continue;
       float acc = 0.f;
-#pragma unroll 8
-      for (int o = sp * 32; o < sp * 32 + 32; ++o) acc = fmaf(L.w1[o * kW1S + xi], L.g1[o], acc);
-      L.part[t] = acc;
-      __syncthreads();
-    }
-    int changed = 0;
-    if (t < 256) {
-      const float gx = (L.part[t] + L.part[t + 256]) + (L.part[t + 512] + L.part[t + 768]);
+#pragma unroll
+      for (int j = 0; j < 64; ++j) acc = fmaf(R.w1c[j], L.g1[e][sq * 64 + j], acc);
+      const float gx = lane_sum<2>(acc);
+      const bool mine = sq == (e & 1);
       // ---- AdamW (torch single-tensor, opt.py:18 defaults) on the entry ----
-      const float* ad = L.adam + it * 4;
-      const float xold = L.x[xi];
-      float xv = xold * ad[0];
-      m = m + 0.1f * (gx - m);            // exp_avg.lerp_(grad, 1 - beta1)
-      v = v * 0.999f + 0.001f * gx * gx;  // exp_avg_sq.mul_(beta2).addcmul_(grad, grad, 1 - beta2)
-      const float denom = sqrtf(v) / ad[2] + 1e-8f;
-      xv = xv + (-ad[1]) * m / denom;     // addcdiv_: self + value * t1 / t2 (ATen's order)
-      // ---- one-hot of the row's first argmax (opt.py:9-15) ----
+      float xv = 0.f;
+      const float xold = L.x[e][xi];
+      if (mine) {
+        float& mm = m[e >> 1];
+        float& vv = v[e >> 1];
+        xv = xold * a0;
+        mm = mm + 0.1f * (gx - mm);           // exp_avg.lerp_(grad, 1 - beta1)
+        vv = vv * 0.999f + 0.001f * gx * gx;  // exp_avg_sq.mul_(beta2).addcmul_(grad, grad, 1 - beta2)
+        const float denom = sqrtf(vv) / a2 + 1e-8f;
+        xv = xv + (-a1) * mm / denom;         // addcdiv_: self + value * t1 / t2 (ATen's order)
+      }
+      // ---- one-hot of the row's first argmax (opt.py:9-15): the row's lanes of this sq ----
       float best = xv;
       int bi = hcol;
 #pragma unroll
-      for (int off = 8; off >= 1; off >>= 1) {
+      for (int off = 2; off <= 16; off <<= 1) {
         const float ov = __shfl_xor(best, off);
         const int oi = __shfl_xor(bi, off);
         if (ov > best || (ov == best && oi < bi)) {
@@ -304,25 +379,47 @@ __global__ __launch_bounds__(kT) void gobi_kernel(int E, const float* __restrict
           bi = oi;
         }
       }
-      if (pre) pre[(long)e * kH * kH + t] = xv;  // test tap: the step's values before the projection
-      const float nv = bi == hcol ? 1.f : 0.f;
-      changed = nv != xold;
-      L.x[xi] = nv;
-      if (bi == hcol) L.hs[c] = hcol;
-      if (t == 0) L.dense = 0;  // one-hot from here on
+      if (mine) {
+        if (pre) pre[(e0 + e) * kH * kH + entry] = xv;  // test tap: the step's values before the projection
+        const float nv = bi == hcol ? 1.f : 0.f;
+        if (nv != xold) L.flag[it & 1][e] = 1;  // benign race: every writer stores 1
+        L.x[e][xi] = nv;
+        if (bi == hcol) L.hs[e][c] = hcol;
+      }
     }
-    if (changed) L.flag[it & 1] = 1;  // benign race: every writer stores 1
     __syncthreads();
-    equal = L.flag[it & 1] ? 0 : equal + 1;
-    if (equal > kPatience) break;
+    GMARK(6);
+    // convergence (opt.py:28-31), per environment, in every thread's registers
+#pragma unroll
+    for (int e = 0; e < kNE; ++e) {
+      dense[e] = false;  // one-hot from here on
+      if (!act[e]) continue;
+      equal[e] = __builtin_amdgcn_readfirstlane(L.flag[it & 1][e]) ? 0 : equal[e] + 1;
+      if (equal[e] > kPatience) {
+        its[e] = it;
+        act[e] = false;
+      }
+    }
     ++it;
   }
-  surrogate_fwd(W, R, L, K, false);
-  for (int k = t; k < kIn; k += kT) result[(long)e * kIn + k] = L.x[k];
-  if (t == 0) {
-    iterations[e] = it;
-    fitness[e] = L.o[2];
+  // final fitness of every real environment
+#pragma unroll
+  for (int e = 0; e < kNE; ++e) act[e] = e0 + e < E;
+  surrogate_fwd(W, R, L, K, false, act, dense, gmark_t_);
+  for (int k = t; k < kNE * kIn; k += kT) {
+    const int e = k / kIn;
+    if (e0 + e < E) result[e0 * kIn + k] = L.x[e][k - e * kIn];
   }
+  if (t < kNE && e0 + t < E) {
+    int n = its[0];
+#pragma unroll
+    for (int e = 1; e < kNE; ++e) n = t == e ? its[e] : n;  // no dynamic register-array index
+    iterations[e0 + t] = n;
+    fitness[e0 + t] = L.o[t][2];
+  }
+#ifdef PGP_GOBI_PROF
+  if (blockIdx.x == 0 && t == 0) g_gobi_prof[15] = (unsigned long long)it;
+#endif
 }
 
 }  // namespace
@@ -429,6 +526,16 @@ int pgp_gobi_destroy(pgp_gobi* g) {
 
 const char* pgp_gobi_last_error(void) { return g_gerr.c_str(); }
 
+#ifdef PGP_GOBI_PROF
+int pgp_gobi_prof_read(unsigned long long* out) {  // phase sums of workgroup 0 (timing variant only)
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_gobi_prof), sizeof(g_gobi_prof)) == hipSuccess ? 0 : -1;
+}
+int pgp_gobi_prof_reset(void) {
+  static const unsigned long long z[16] = {};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_gobi_prof), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif
+
 int pgp_gobi_optimize(pgp_gobi* g, int n_env, const float* init, float* result, int* iterations, float* fitness,
                       int max_iters, float* pre, void* stream) {
   if (!g) return gfail(PGP_ERR_ARG, "NULL optimiser");
@@ -436,8 +543,8 @@ int pgp_gobi_optimize(pgp_gobi* g, int n_env, const float* init, float* result, 
   if (n_env == 0) return PGP_OK;
   if (!init || !result || !iterations || !fitness) return gfail(PGP_ERR_ARG, "NULL input/output pointer");
   const int mi = (max_iters <= 0 || max_iters > kMaxIt) ? kMaxIt : max_iters;
-  gobi_kernel<<<n_env, kT, sizeof(GobiLds), reinterpret_cast<hipStream_t>(stream)>>>(n_env, g->d_w, init, result,
-                                                                                     iterations, fitness, mi, pre);
+  gobi_kernel<<<(n_env + kNE - 1) / kNE, kT, sizeof(GobiLds), reinterpret_cast<hipStream_t>(stream)>>>(n_env, g->d_w, init, result,
+                                                                                          iterations, fitness, mi, pre);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return gfail(PGP_ERR_HIP, std::string("gobi_kernel: ") + hipGetErrorString(e));
   return PGP_OK;
