@@ -865,7 +865,7 @@ def bench_plugin(args):
 
     for name in ("train_gan", "tune_model", "sync_inference_weights", "recover_decision"):
         setattr(rec, name, timed(name, getattr(rec, name)))
-    rec.infer.forward = timed("detect_forward", rec.infer.forward)
+    rec._detect = timed("detect_forward", rec._detect)
     import preganplus_amd.train as TRm
     bp, ds = TRm.backprop, TRm.on_the_fly_dataset
     TRm.backprop, TRm.on_the_fly_dataset = timed("tune_backprop", bp), timed("tune_dataset", ds)
@@ -876,7 +876,7 @@ def bench_plugin(args):
         TRm.backprop, TRm.on_the_fly_dataset = bp, ds
         for name in ("train_gan", "tune_model", "sync_inference_weights", "recover_decision"):
             delattr(rec, name)
-        del rec.infer.forward
+        del rec._detect
     stage_ms = {k: float(np.median(v) * 1e3) for k, v in stages.items()}
     # batch-1 inference latency (the encoder + classify + GAN gate of one window)
     model = rec.infer

@@ -243,6 +243,16 @@ int pgp_tune_targets(int n_hosts, int n_protos, const float* logits, const float
 int pgp_tune_step1(int n_hosts, int n_protos, const float* window, const int* y, const int* cls, const float* P,
                    float* G, double* state, double update_min, double decay, float* logits, float* protos,
                    double* loss, void* stream);
+/* run_model's per-interval forward for ONE window (PreGANPlus.py:115-136:
+ * run_encoder, detect / embed / get_classes, Gen + Disc, the recover_decision
+ * gate and targets), n_hosts 8 or 16, in a single launch, straight from the
+ * training master P (natural fp32, as pgp_tune_*) and prototypes [K,2] fp64
+ * on the device — no packed weights.  window [3,3H], sched [H,H]; outputs as
+ * pgp_forward at batch 1 (logits [H,2], protos [H,2], cls [H], any [1],
+ * probs [2], keep [1], final_target [H], gen_target [H]). */
+int pgp_forward1(int n_hosts, int n_protos, const float* window, const float* sched, const float* P,
+                 const double* prototypes_device, float* logits, float* protos, int* cls, int* any_anom, float* probs,
+                 int* keep_orig, int* final_target, int* gen_target, void* stream);
 /* ---- data-parallel tuning step on the device ----
  * pgp_tune_dataset replaces load_on_the_fly_dataset (utils.py:40-47) for a
  * batch of E environments: series [E,R,3H] fp64 = each environment's last R

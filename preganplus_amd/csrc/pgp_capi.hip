@@ -374,6 +374,19 @@ int pgp_tune_step1(int n_hosts, int n_protos, const float* window, const int* y,
   return PGP_OK;
 }
 
+int pgp_forward1(int n_hosts, int n_protos, const float* window, const float* sched, const float* P,
+                 const double* prototypes_device, float* logits, float* protos, int* cls, int* any_anom, float* probs,
+                 int* keep_orig, int* final_target, int* gen_target, void* stream) {
+  if (!tune1_supported(n_hosts)) return fail(PGP_ERR_UNSUPPORTED, "host count (batch-1 forward: 8 or 16)");
+  if (n_protos < 1 || n_protos > kMaxProtos) return fail(PGP_ERR_ARG, "n_protos out of range");
+  if (!window || !sched || !P || !prototypes_device || !logits || !protos || !cls || !any_anom || !probs ||
+      !keep_orig || !final_target || !gen_target)
+    return fail(PGP_ERR_ARG, "bad forward1 arguments");
+  HIPCHK(launch_infer1(n_hosts, n_protos, window, sched, P, prototypes_device, logits, protos, cls, any_anom, probs,
+                       keep_orig, final_target, gen_target, reinterpret_cast<hipStream_t>(stream)));
+  return PGP_OK;
+}
+
 int pgp_tune_dataset(int n_hosts, int n_env, int n_rows, const double* series, const double* train_max,
                      float* windows, int* y, int* cls, float* infer, void* stream) {
   if (n_hosts <= 0 || n_hosts > 64) return fail(PGP_ERR_UNSUPPORTED, "host count");

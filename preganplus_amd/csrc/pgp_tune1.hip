@@ -211,18 +211,18 @@ PGP_DEV void t1_dx(const float* W, int K, const float* dy, int dys, int T, float
   }
 }
 
+// The forward of one window (GAT, time encoder, 2 layers, decoders) with every
+// activation left in LDS (T1<H> layout) for the backward; the decoder outputs
+// (logits | sigmoid protos) end in sm[S_OUT] and, when given, in global memory.
+// Shared by the tuning step (tune1_kernel) and the batch-1 inference (infer1_kernel).
 template <int H>
-__global__ __launch_bounds__(kT1Threads) void tune1_kernel(int K, const float* __restrict__ win,
-                                                           const int* __restrict__ yv, const int* __restrict__ cv,
-                                                           const float* __restrict__ P, float* __restrict__ Gd,
-                                                           double* __restrict__ state, double update_min,
-                                                           double decay, float* __restrict__ logits_out,
-                                                           float* __restrict__ protos_out, double* __restrict__ loss) {
+PGP_DEV void t1_forward(float* sm, const float* __restrict__ P, const float* __restrict__ win,
+                        float* __restrict__ logits_out, float* __restrict__ protos_out, int& mk_) {
   using S = T1<H>;
   using G = TGeo<H>;
   constexpr int D = S::D, T = S::T, HD = S::HD, FF = S::FF, Q3 = S::Q3, NO = S::NO, L = S::L;
   constexpr int DS = S::DS, QS = S::QS, FS = S::FS;
-  __shared__ __attribute__((aligned(16))) float sm[S::TOTAL];
+  (void)mk_;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   float* win_s = sm + S::S_WIN;
   float* uv = sm + S::S_UV;
@@ -232,23 +232,9 @@ __global__ __launch_bounds__(kT1Threads) void tune1_kernel(int K, const float* _
   float* xb = sm + S::S_XB;
   float* g = sm + S::S_G;
   float* xs = sm + S::S_X0;  // x[l] = xs + l*T*DS
-  float* mult = sm + S::S_MT;
-  float* tgt = sm + S::S_MT + H;
-  int* ys = reinterpret_cast<int*>(sm + S::S_MT + 3 * H);
-  int* cs = reinterpret_cast<int*>(sm + S::S_MT + 4 * H);
-  double* ce = reinterpret_cast<double*>(sm + S::S_CE);
   float* Pw = sm + S::S_PW;
-  int mk_ = 0;
-  (void)mk_;
-  T1MARK();
-
-  // ---------------- forward ----------------
   for (int i = tid; i < S::WN; i += kT1Threads) Pw[i] = P[i];
   for (int i = tid; i < 9 * H; i += kT1Threads) win_s[i] = win[i];
-  for (int i = tid; i < H; i += kT1Threads) {
-    ys[i] = yv[i];
-    cs[i] = cv[i];
-  }
   T1SYNC();
   if (tid < 6) {  // u = fc^T a_src, v = fc^T a_dst (dlutils.py:315-329, algebraically)
     const int k = tid % 3;
@@ -396,16 +382,56 @@ __global__ __launch_bounds__(kT1Threads) void tune1_kernel(int K, const float* _
         float s;
         if (n < 2 * H) {
           s = acc + P[G::B_AN + n];  // LeakyReLU(True) = identity (models.py:361)
-          logits_out[n] = s;
+          if (logits_out) logits_out[n] = s;
         } else {
           s = 1.0f / (1.0f + expf(-(acc + P[G::B_PR + n - 2 * H])));
-          protos_out[n - 2 * H] = s;
+          if (protos_out) protos_out[n - 2 * H] = s;
         }
         out[n] = s;
       }
     }
   }
   T1SYNC();
+}
+
+template <int H>
+__global__ __launch_bounds__(kT1Threads) void tune1_kernel(int K, const float* __restrict__ win,
+                                                           const int* __restrict__ yv, const int* __restrict__ cv,
+                                                           const float* __restrict__ P, float* __restrict__ Gd,
+                                                           double* __restrict__ state, double update_min,
+                                                           double decay, float* __restrict__ logits_out,
+                                                           float* __restrict__ protos_out, double* __restrict__ loss) {
+  using S = T1<H>;
+  using G = TGeo<H>;
+  constexpr int D = S::D, T = S::T, HD = S::HD, FF = S::FF, Q3 = S::Q3, NO = S::NO, L = S::L;
+  constexpr int DS = S::DS, QS = S::QS, FS = S::FS;
+  __shared__ __attribute__((aligned(16))) float sm[S::TOTAL];
+  const int tid = threadIdx.x;
+  float* win_s = sm + S::S_WIN;
+  float* st = sm + S::S_ST;
+  float* gs = sm + S::S_GS;
+  float* xb = sm + S::S_XB;
+  float* g = sm + S::S_G;
+  float* xs = sm + S::S_X0;  // x[l] = xs + l*T*DS
+  float* mult = sm + S::S_MT;
+  float* tgt = sm + S::S_MT + H;
+  int* ys = reinterpret_cast<int*>(sm + S::S_MT + 3 * H);
+  int* cs = reinterpret_cast<int*>(sm + S::S_MT + 4 * H);
+  double* ce = reinterpret_cast<double*>(sm + S::S_CE);
+  float* Pw = sm + S::S_PW;
+  int mk_ = 0;
+  (void)mk_;
+  T1MARK();
+
+  // ---------------- forward ----------------
+  for (int i = tid; i < H; i += kT1Threads) {
+    ys[i] = yv[i];
+    cs[i] = cv[i];
+  }
+  t1_forward<H>(sm, P, win, logits_out, protos_out, mk_);
+  const float* x2 = xs + 2 * T * DS;
+  float* out = sm + S::S_OUT;
+  const float scale = 1.0f / sqrtf((float)HD);
   // custom_loss / triplet_loss bookkeeping (train.py:13-40): the per-host CE
   // terms in parallel, then the sequential part on one lane, fp64
   if (tid < H) ce[tid] = tune_ce_term(out[2 * tid], out[2 * tid + 1], ys[tid]);
@@ -616,6 +642,140 @@ __global__ __launch_bounds__(kT1Threads) void tune1_kernel(int K, const float* _
 #endif
 }
 
+// ---------------------------------------------------------------------------
+// Batch-1 inference of run_model (PreGANPlus.py:115-136: run_encoder, detect /
+// embed / get_classes, Gen + Disc, the recover_decision gate and targets) in ONE
+// workgroup, from the training master weights P (natural layout) and the
+// prototypes (fp64, device) — the plugin's per-interval forward without the
+// batch-tiled K1-K3 (built for 65,536-window batches).  Outputs as pgp_forward
+// at B = 1.  Gen / Disc (models.py:131-151): hg = W1 [emb; s] + b1 (LeakyReLU
+// slope 1 = identity), ns = s + 4 tanh(W2 hg + b2); hd = Wd1 [s; ns] + bd1,
+// probs = softmax(Wd2 hd + bd2).
+// ---------------------------------------------------------------------------
+template <int H>
+__global__ __launch_bounds__(kT1Threads) void infer1_kernel(int K, const float* __restrict__ win,
+                                                            const float* __restrict__ sched,
+                                                            const float* __restrict__ P,
+                                                            const double* __restrict__ protos_dev,
+                                                            float* __restrict__ logits, float* __restrict__ protos,
+                                                            int* __restrict__ cls, int* __restrict__ any_anom,
+                                                            float* __restrict__ probs, int* __restrict__ keep,
+                                                            int* __restrict__ final_t, int* __restrict__ gen_t) {
+  using S = T1<H>;
+  using G = TGeo<H>;
+  constexpr int H2 = H * H, GIN = G::GIN, DIN = G::DIN;
+  __shared__ __attribute__((aligned(16))) float sm[S::TOTAL];
+  const int tid = threadIdx.x, lane = tid & 63;
+  int mk_ = 0;
+  t1_forward<H>(sm, P, win, logits, protos, mk_);  // ends with a barrier; outputs in sm[S_OUT]
+  const float* out = sm + S::S_OUT;
+  // reuse the (now dead) backward scratch regions for the GAN
+  float* xin = sm + S::S_DA;       // [GIN] Gen input [emb; s]
+  float* sd = xin + GIN;           // [DIN] Disc input [s; ns]
+  float* hg = sm + S::S_DF;        // [64]
+  float* hd = hg + 64;             // [64]
+  int* anyf = reinterpret_cast<int*>(hd + 64);
+  const float* Gp = P + G::OFF_GEN;
+  const float* Dp = P + G::OFF_DISC;
+  if (tid == 0) anyf[0] = 0;
+  __syncthreads();
+  // detect + embed + get_classes (as K2b's epilogue): first-argmax of the logits,
+  // embedding = prototype output where anomalous, class = first argmin of the MSE
+  for (int h = tid; h < H; h += kT1Threads) {
+    const float l0 = out[2 * h], l1 = out[2 * h + 1], p0 = out[2 * H + 2 * h], p1 = out[2 * H + 2 * h + 1];
+    const bool an = l1 > l0;  // torch.argmax: ties -> index 0
+    const float e0 = an ? p0 : 0.f, e1 = an ? p1 : 0.f;
+    int cl = -1;
+    if (!(e0 == 0.f && e1 == 0.f)) {
+      float best = INFINITY;
+      for (int k = 0; k < K; ++k) {
+        const float d0 = e0 - (float)protos_dev[2 * k], d1 = e1 - (float)protos_dev[2 * k + 1];
+        const float dist = (d0 * d0 + d1 * d1) * 0.5f;  // torch.mean over PROTO_DIM = 2
+        if (dist < best) {                              // np.argmin: first minimum
+          best = dist;
+          cl = k;
+        }
+      }
+    }
+    cls[h] = cl;
+    xin[2 * h] = e0;
+    xin[2 * h + 1] = e1;
+    if (an) anyf[0] = 1;  // benign race: every writer stores 1
+  }
+  for (int i = tid; i < H2; i += kT1Threads) {
+    xin[2 * H + i] = sched[i];
+    sd[i] = sched[i];
+  }
+  __syncthreads();
+  // Gen1: 64 outputs, 16 lanes each (k-chunks), xor-butterfly sum
+  {
+    const int o = tid >> 4, sp = tid & 15;
+    constexpr int KC = (GIN + 15) / 16;
+    float acc = 0.f;
+    for (int k = sp * KC; k < sp * KC + KC && k < GIN; ++k) acc = fmaf(Gp[G::G_W1 + o * GIN + k], xin[k], acc);
+#pragma unroll
+    for (int off = 1; off < 16; off <<= 1) acc += __shfl_xor(acc, off);
+    if (sp == 0) hg[o] = acc + Gp[G::G_B1 + o];  // LeakyReLU(True): identity
+  }
+  __syncthreads();
+  // Gen2: H^2 outputs, ns = s + 4 tanh(W2 hg + b2)
+  for (int i = tid; i < 4 * H2; i += kT1Threads) {
+    const int o = i >> 2, sp = i & 3;
+    float acc = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) acc = fmaf(Gp[G::G_W2 + o * 64 + sp * 16 + k], hg[sp * 16 + k], acc);
+    acc += __shfl_xor(acc, 1);
+    acc += __shfl_xor(acc, 2);
+    if (sp == 0) sd[H2 + o] = xin[2 * H + o] + 4.0f * tanhf(acc + Gp[G::G_B2 + o]);
+  }
+  __syncthreads();
+  // Disc1: 64 outputs over [s; ns], 16 lanes each
+  {
+    const int o = tid >> 4, sp = tid & 15;
+    constexpr int KC = DIN / 16;
+    float acc = 0.f;
+    for (int k = sp * KC; k < sp * KC + KC; ++k) acc = fmaf(Dp[G::D_W1 + o * DIN + k], sd[k], acc);
+#pragma unroll
+    for (int off = 1; off < 16; off <<= 1) acc += __shfl_xor(acc, off);
+    if (sp == 0) hd[o] = acc + Dp[G::D_B1 + o];
+  }
+  __syncthreads();
+  if (tid < 64) {  // Disc2 + softmax + gate (PreGANPlus.py:87), one wave
+    float z0 = Dp[G::D_W2 + lane] * hd[lane], z1 = Dp[G::D_W2 + 64 + lane] * hd[lane];
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      z0 += __shfl_xor(z0, off);
+      z1 += __shfl_xor(z1, off);
+    }
+    z0 += Dp[G::D_B2];
+    z1 += Dp[G::D_B2 + 1];
+    const float m = fmaxf(z0, z1), e0 = expf(z0 - m), e1 = expf(z1 - m), inv = 1.0f / (e0 + e1);
+    if (lane == 0) {
+      probs[0] = e0 * inv;
+      probs[1] = e1 * inv;
+      keep[0] = e0 * inv > e1 * inv ? 1 : 0;
+      any_anom[0] = anyf[0];
+    }
+  }
+  for (int c = tid; c < H; c += kT1Threads) {  // first-argmax of each schedule row (original / generated)
+    float bs = -INFINITY, bn = -INFINITY;
+    int is = 0, in = 0;
+    for (int h = 0; h < H; ++h) {
+      const float v = sd[c * H + h], w = sd[H2 + c * H + h];
+      if (v > bs) {
+        bs = v;
+        is = h;
+      }
+      if (w > bn) {
+        bn = w;
+        in = h;
+      }
+    }
+    final_t[c] = is;
+    gen_t[c] = in;
+  }
+}
+
 }  // namespace
 
 #ifdef PGP_T1_PROF
@@ -625,6 +785,24 @@ extern "C" int pgp_tune1_prof_read(unsigned long long* out) {
 #endif
 
 bool tune1_supported(int H) { return H == 8 || H == 16; }
+
+hipError_t launch_infer1(int H, int K, const float* win, const float* sched, const float* P, const double* protos,
+                         float* logits, float* protos_out, int* cls, int* any_anom, float* probs, int* keep,
+                         int* final_t, int* gen_t, hipStream_t st) {
+  switch (H) {
+    case 8:
+      infer1_kernel<8><<<1, kT1Threads, 0, st>>>(K, win, sched, P, protos, logits, protos_out, cls, any_anom, probs,
+                                                 keep, final_t, gen_t);
+      break;
+    case 16:
+      infer1_kernel<16><<<1, kT1Threads, 0, st>>>(K, win, sched, P, protos, logits, protos_out, cls, any_anom, probs,
+                                                  keep, final_t, gen_t);
+      break;
+    default:
+      return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
 
 hipError_t launch_tune1(int H, int K, const float* win, const int* y, const int* cls, const float* P, float* G,
                         double* state, double update_min, double decay, float* logits, float* protos, double* loss,

@@ -9,7 +9,9 @@ Same constructor and ``run_model(time_series, original_decision)`` contract as
 ``env.containerlist`` by reference, returning a new decision list.
 
 Per call, as the reference:
-  1. detect + diagnose on the newest window (HIP inference kernels K1-K2b);
+  1. detect + diagnose on the newest window (at 8 / 16 hosts one launch from
+     the training master, ``pgp_forward1``; otherwise the HIP inference
+     kernels K1-K3 on the packed copy, rebuilt on the device after training);
      no anomaly -> the original decision (PreGANPlus.py:119-127);
   2. ``train_gan`` (PreGANPlus.py:60-81): Gen/Disc forward, two simulator
      scores, Disc step then Gen step (HIP training kernels + AdamW);
@@ -87,7 +89,8 @@ class PreGANPlusRecovery(Recovery):
                 weights, extra = W.load_npz(packaged)
         self.extra = extra or {}
         self.prototypes = np.asarray(weights["prototypes"], dtype=np.float64)
-        self.infer = DecisionModel(self.hosts, weights, device=self.device)
+        self._infer = DecisionModel(self.hosts, weights, device=self.device)
+        self._infer_stale = False
         self.trainer = TR.Trainer(self.hosts, weights, self.extra, device=self.device)
         self.tune_state = TR.TuneState(self.prototypes)
         # load_gan's epoch and accuracy_list are the ones the plugin keeps (PreGANPlus.py:32-34)
@@ -133,15 +136,30 @@ class PreGANPlusRecovery(Recovery):
         self.accuracy_list.append((loss, factor, anomaly_score, class_score))                  # :58
         return losses
 
-    def sync_inference_weights(self):
-        """Rebuild the inference kernels' packed weights from the trained master
-        on the device (pgp_repack_master): P and the prototypes of the tuning
-        state never leave the GPU."""
+    @property
+    def infer(self):
+        """The packed inference model (K1-K3), rebuilt from the trained master on
+        first use after an optimizer step (the packed weights are a cache of the
+        master; the 8 / 16-host plugin path reads the master directly)."""
+        if self._infer_stale:
+            self._repack()
+        return self._infer
+
+    def _repack(self):
+        """pgp_repack_master: P and the prototypes of the tuning state never
+        leave the GPU."""
         K = self.tune_state.protos.shape[0]
         dev_state = getattr(self.trainer, "tune_state_dev", None)
         if dev_state is None:
             dev_state = torch.tensor(self.tune_state.vector(), dtype=torch.float64, device=self.trainer.device)
-        self.infer.repack_master(self.trainer.P, dev_state[:2 * K], self.tune_state.protos)
+        self._infer.repack_master(self.trainer.P, dev_state[:2 * K], self.tune_state.protos)
+        self._infer_stale = False
+
+    def sync_inference_weights(self):
+        """After training: the inference model follows the updated master
+        (utils.py:64-65 updates the reference's modules in place).  The packed
+        copy is rebuilt on the device when it is next used (``infer``)."""
+        self._infer_stale = True
         self.prototypes = self.tune_state.protos.copy()
 
     # -- PreGANPlus.py:83-105 --
@@ -153,31 +171,48 @@ class PreGANPlusRecovery(Recovery):
             _, probs = self.trainer.gan_forward(np.asarray(embedding)[None], np.asarray(schedule_data)[None])
             p = probs[0].cpu().numpy()
         res, hf = _recover(self.env, self.hosts, schedule_data, original_decision, bool(p[0] > p[1]),
-                           self.infer.device, getattr(self, "_final_target", None), io=self._recover_io())
+                           self.device_, getattr(self, "_final_target", None), io=self._recover_io())
         if hf is not None:
             self.hosts_from = hf
         return res
 
+    @property
+    def device_(self):
+        return self._infer.device
+
     def _recover_io(self):
         if getattr(self, "_rio", None) is None:
-            self._rio = _RecoverIO(self.hosts, self.infer.device)
+            self._rio = _RecoverIO(self.hosts, self.device_)
         return self._rio
 
     def _detect(self, win, schedule_data):
         """The batch-1 forward of run_model (K1-K3) from pinned staging buffers:
         one host-to-device copy in, one device-to-host copy out (to_numpy)."""
-        H, dev = self.hosts, self.infer.device
+        H, dev = self.hosts, self.device_
         if getattr(self, "_io", None) is None:
             nin = 9 * H + H * H
             self._io = (torch.zeros(nin, dtype=torch.float32).pin_memory(),
                         torch.zeros(nin, dtype=torch.float32, device=dev),
-                        self.infer.alloc_outputs(1, packed=True))
+                        self._infer.alloc_outputs(1, packed=True))
         hin, din, out = self._io
         h = hin.numpy()
         h[:9 * H] = np.asarray(win, dtype=np.float32).reshape(-1)
         h[9 * H:] = np.asarray(schedule_data, dtype=np.float32).reshape(-1)
         din.copy_(hin, non_blocking=True)
+        if H in TR.FUSED_STEP_HOSTS:
+            # one launch from the master weights and the tuning state's prototypes (pgp_forward1):
+            # the same model the packed copy holds after sync_inference_weights
+            return self.trainer.forward1(din[:9 * H], din[9 * H:], self._protos_dev(), out)
         return self.infer.forward(din[:9 * H].view(1, 3, 3 * H), din[9 * H:].view(1, H, H), out=out)
+
+    def _protos_dev(self):
+        K = self.tune_state.protos.shape[0]
+        st = getattr(self.trainer, "tune_state_dev", None)
+        if st is not None:
+            return st[:2 * K]
+        if getattr(self, "_protos0", None) is None:
+            self._protos0 = torch.tensor(self.tune_state.protos, dtype=torch.float64, device=self.trainer.device)
+        return self._protos0
 
     # -- PreGANPlus.py:115-136 --
     def run_model(self, time_series, original_decision):

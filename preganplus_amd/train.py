@@ -118,6 +118,7 @@ class Trainer:
                                       + [vp])
         dbl = ctypes.c_double
         L.pgp_tune_step1.argtypes = [i32, i32] + [vp] * 6 + [dbl, dbl] + [vp] * 3 + [vp]
+        L.pgp_forward1.argtypes = [i32, i32] + [vp] * 12 + [vp]
         L.pgp_tune_dataset.argtypes = [i32, i32, i32] + [vp] * 6 + [vp]
         L.pgp_tune_targets_dp_workspace_len.argtypes = [i32]
         L.pgp_tune_targets_dp_workspace_len.restype = sz
@@ -127,7 +128,7 @@ class Trainer:
         for f in ("pgp_tune_forward", "pgp_tune_backward", "pgp_gan_forward", "pgp_gan_disc_backward",
                   "pgp_gan_gen_backward", "pgp_adamw", "pgp_load_weights_master", "pgp_tune_targets",
                   "pgp_adamw_table", "pgp_tune_dataset", "pgp_tune_targets_dp", "pgp_tune_state_apply",
-                  "pgp_gan_probs", "pgp_tune_step1"):
+                  "pgp_gan_probs", "pgp_tune_step1", "pgp_forward1"):
             getattr(L, f).restype = i32
         L._pgp_train_bound = True
 
@@ -214,6 +215,20 @@ class Trainer:
             state.data_ptr(), PROTO_UPDATE_MIN, PROTO_FACTOR_DECAY, self.logits.data_ptr(),
             self.protos.data_ptr(), loss.data_ptr(), self._stream()), "pgp_tune_step1")
         self._fwd_batch = 0   # the fused step keeps no activations for tune_backward
+
+    def forward1(self, window, sched, protos_dev, out):
+        """run_model's forward of ONE window from the master weights
+        (``pgp_forward1``, n_hosts 8 or 16): window [3,3H], sched [H,H] fp32,
+        protos_dev [K,2] fp64, all device tensors; out: a DecisionModel output
+        dict for batch 1 (logits, protos, cls, any, probs, keep, final_target,
+        gen_target)."""
+        K = protos_dev.numel() // 2
+        p = lambda k: out[k].data_ptr()
+        _native.check(self._L.pgp_forward1(
+            self.H, K, window.data_ptr(), sched.data_ptr(), self.P.data_ptr(), protos_dev.data_ptr(),
+            p("logits"), p("protos"), p("cls"), p("any"), p("probs"), p("keep"), p("final_target"),
+            p("gen_target"), self._stream()), "pgp_forward1")
+        return out
 
     def gan_forward(self, emb, sched):
         emb = self._dev(emb, torch.float32)
