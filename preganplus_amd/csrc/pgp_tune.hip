@@ -765,8 +765,20 @@ __global__ __launch_bounds__(256) void dec_fin_kernel(int B, int S, const float*
   if (idx >= (long)B * 4 * H) return;
   const long b = idx / (4 * H);
   const int n = (int)(idx - b * 4 * H);
+  // the S partials in split order; loads issued 8 at a time so the adds wait
+  // on one batch instead of one round trip per split
+  const float* pp = part + b * Q::NOP + n;
+  const long qs = (long)B * Q::NOP;
   float s = 0.f;
-  for (int q = 0; q < S; ++q) s += part[((long)q * B + b) * Q::NOP + n];
+  int q = 0;
+  for (; q + 8 <= S; q += 8) {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = pp[(q + j) * qs];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += v[j];
+  }
+  for (; q < S; ++q) s += pp[q * qs];
   if (n < 2 * H)
     logits[b * 2 * H + n] = s + P[G::B_AN + n];  // LeakyReLU(True) = identity (models.py:361)
   else

@@ -52,57 +52,84 @@ __global__ __launch_bounds__(256) void tune_dataset_kernel(int H, int E, int R, 
   if (t >= (long)E * H) return;
   const int e = (int)(t / H), h = (int)(t % H);
   const int F = 3 * H;
+  // every loop runs to kMaxTuneRows with an r < R guard, so all indices are
+  // compile-time and the rows stay in registers
   double v[kMaxTuneRows][3];  // normalised rows x the host's 3 columns
+#pragma unroll
   for (int c = 0; c < 3; ++c) {
     const double den = train_max[3 * h + c] + 1e-8;  // np.max(train, axis=0) + 1e-8
-    for (int r = 0; r < R; ++r) v[r][c] = series[((long)e * R + r) * F + 3 * h + c] / den;
+#pragma unroll
+    for (int r = 0; r < kMaxTuneRows; ++r)
+      v[r][c] = r < R ? series[((long)e * R + r) * F + 3 * h + c] / den : 0.0;
   }
   // 98th percentile per column, numpy 'linear': virtual index (R-1)*0.98,
-  // gamma = frac, lerp(a, b, g) = g >= 0.5 ? b - (b-a)(1-g) : a + (b-a) g
+  // gamma = frac, lerp(a, b, g) = g >= 0.5 ? b - (b-a)(1-g) : a + (b-a) g.
+  // The order statistics ilo, ihi are found by stable rank (the element with
+  // rank p is sorted[p]) instead of sorting.
   const double vi = (double)(R - 1) * (98.0 / 100.0);
   const double lo = floor(vi);
   const double gm = vi - lo;
   const int ilo = (int)lo, ihi = ilo + 1 < R ? ilo + 1 : R - 1;
   double thr[3];
+#pragma unroll
   for (int c = 0; c < 3; ++c) {
-    double s[kMaxTuneRows];
-    for (int r = 0; r < R; ++r) {  // insertion sort (R <= 16)
-      double x = v[r][c];
-      int k = r;
-      while (k > 0 && s[k - 1] > x) {
-        s[k] = s[k - 1];
-        --k;
-      }
-      s[k] = x;
+    double a = 0.0, b = 0.0;
+#pragma unroll
+    for (int r = 0; r < kMaxTuneRows; ++r) {
+      int rank = 0;
+#pragma unroll
+      for (int j = 0; j < kMaxTuneRows; ++j)
+        if (j != r && j < R) rank += (v[j][c] < v[r][c] || (j < r && v[j][c] == v[r][c])) ? 1 : 0;
+      if (r < R && rank == ilo) a = v[r][c];
+      if (r < R && rank == ihi) b = v[r][c];
     }
-    const double a = s[ilo], b = s[ihi], d = b - a;
+    const double d = b - a;
     thr[c] = gm >= 0.5 ? b - d * (1.0 - gm) : a + d * gm;
   }
-  for (int r = 0; r < R; ++r) {
-    const bool an = v[r][0] > thr[0] || v[r][1] > thr[1] || v[r][2] > thr[2];
-    int am = 0;  // np.argmax: first maximum
-    if (v[r][1] > v[r][am]) am = 1;
-    if (v[r][2] > v[r][am]) am = 2;
-    y[((long)e * R + r) * H + h] = an ? 1 : 0;
-    cls[((long)e * R + r) * H + h] = am;
-    // convert_to_windows: window r = rows r-3..r-1, row 0 repeated for r < 3
-    for (int w = 0; w < kWin; ++w) {
-      const int src = r >= kWin ? r - kWin + w : (w < kWin - r ? 0 : w - (kWin - r));
-      float* o = windows + (((long)e * R + r) * kWin + w) * F + 3 * h;
-      for (int c = 0; c < 3; ++c) o[c] = (float)v[src][c];
+#pragma unroll
+  for (int r = 0; r < kMaxTuneRows; ++r) {
+    if (r < R) {
+      const bool an = v[r][0] > thr[0] || v[r][1] > thr[1] || v[r][2] > thr[2];
+      int am = 0;  // np.argmax: first maximum
+      if (v[r][1] > v[r][am]) am = 1;
+      if (v[r][2] > v[r][am]) am = 2;
+      y[((long)e * R + r) * H + h] = an ? 1 : 0;
+      cls[((long)e * R + r) * H + h] = am;
+      // convert_to_windows: window r = rows r-3..r-1, row 0 repeated for r < 3
+#pragma unroll
+      for (int w = 0; w < kWin; ++w) {
+        const int src = r >= kWin ? r - kWin + w : (w < kWin - r ? 0 : w - (kWin - r));
+        float* o = windows + (((long)e * R + r) * kWin + w) * F + 3 * h;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) o[c] = (float)v[src][c];
+      }
     }
   }
   if (infer) {  // run_encoder: last 3 rows -> convert_to_windows(...)[-1] = [R-3, R-3, R-2]
-    const int rows[kWin] = {R - 3, R - 3, R - 2};
+    double u[2][3] = {};
+#pragma unroll
+    for (int r = 0; r < kMaxTuneRows; ++r)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        if (r == R - 3) u[0][c] = v[r][c];
+        if (r == R - 2) u[1][c] = v[r][c];
+      }
+#pragma unroll
     for (int w = 0; w < kWin; ++w)
-      for (int c = 0; c < 3; ++c) infer[((long)e * kWin + w) * F + 3 * h + c] = (float)v[rows[w]][c];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) infer[((long)e * kWin + w) * F + 3 * h + c] = (float)u[w < 2 ? 0 : 1][c];
   }
 }
 
 // ---------------------------------------------------------------------------
-// targets: one thread per window, block partials of the increments
+// targets: one wave per window (lane = host), kWpb windows per workgroup.  The
+// per-host terms (the fp64 log-sum-exp of the CE, the triplet MSEs) run across
+// the lanes; lane 0 then folds them in host order, so each window's losses and
+// increments are summed exactly as the one-thread-per-window loop would
+// (train.loss_targets_dp's per-window order); windows are combined in a fixed
+// tree per workgroup and the workgroups in index order by the finish kernel.
 // ---------------------------------------------------------------------------
-constexpr int kTB = 256;
+constexpr int kWpb = 4, kTB = 64 * kWpb;
 __global__ __launch_bounds__(kTB) void tune_targets_dp_kernel(int H, int B, const float* __restrict__ logits,
                                                               const float* __restrict__ protos,
                                                               const int* __restrict__ y, const int* __restrict__ cls,
@@ -110,23 +137,28 @@ __global__ __launch_bounds__(kTB) void tune_targets_dp_kernel(int H, int B, cons
                                                               float* __restrict__ mult, float* __restrict__ tgt,
                                                               double* __restrict__ loss, double* __restrict__ part) {
 #pragma clang fp contract(off)
-  __shared__ double red[kDpInc][kTB];
-  const int b = blockIdx.x * kTB + threadIdx.x;
-  double acc[kDpInc] = {};  // delta[3][2], count[3], ones
-  if (b < B) {
-    const double* P = state;
-    const double ratio = state[2 * K + 1] / state[2 * K + 2];  // num_zero / num_ones at the step start
-    const double f = state[2 * K] + update_min;               // PROTO_UPDATE_FACTOR + PROTO_UPDATE_MIN
-    double aloss = 0.0, tloss = 0.0;
-    for (int i = 0; i < H; ++i) {
+  __shared__ double s_ce[kWpb][64], s_tl[kWpb][64], s_d0[kWpb][64], s_d1[kWpb][64];
+  __shared__ int s_code[kWpb][64];  // -1: negative label; 0-2: class, +4 when the window's prototype moves
+  __shared__ double red[kWpb][kDpInc];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int b = blockIdx.x * kWpb + wv;
+  double acc[kDpInc] = {};  // delta[3][2], count[3], ones (lane 0)
+  const bool live = b < B;
+  const double* P = state;
+  const double ratio = state[2 * K + 1] / state[2 * K + 2];  // num_zero / num_ones at the step start
+  const double f = state[2 * K] + update_min;               // PROTO_UPDATE_FACTOR + PROTO_UPDATE_MIN
+  double aloss = 0.0, tloss = 0.0;
+  for (int i0 = 0; i0 < H; i0 += 64) {  // uniform trip count: every wave reaches the barriers
+    const int i = i0 + lane;
+    if (live && i < H) {
       const long o = (long)b * H + i;
       const int yi = y[o];
       const double mu = yi == 0 ? 1.0 : ratio;
       mult[o] = (float)mu;
       const double l0 = logits[2 * o], l1 = logits[2 * o + 1];
       const double m = fmax(l0, l1);
-      aloss += (log(exp(l0 - m) + exp(l1 - m)) + m - (yi ? l1 : l0)) * mu;
-      acc[9] += yi == 1 ? 1.0 : 0.0;
+      s_ce[wv][lane] = (log(exp(l0 - m) + exp(l1 - m)) + m - (yi ? l1 : l0)) * mu;
+      int code = -1;
       if (yi > 0) {
         const int cc = cls[o];
         const double a0 = protos[2 * o], a1 = protos[2 * o + 1];
@@ -139,46 +171,81 @@ __global__ __launch_bounds__(kTB) void tune_targets_dp_kernel(int H, int B, cons
         }
         const double pos = mse[cc];
         const double n0 = mse[cc == 0 ? 1 : 0], n1 = mse[cc == 2 ? 1 : 2];
-        tloss += pos - (n0 + n1);
+        s_tl[wv][lane] = pos - (n0 + n1);
+        code = cc;
         if (pos <= n0 && pos <= n1) {
-          acc[2 * cc] += f * (a0 - P[2 * cc]);
-          acc[2 * cc + 1] += f * (a1 - P[2 * cc + 1]);
-          acc[6 + cc] += 1.0;
+          s_d0[wv][lane] = f * (a0 - P[2 * cc]);
+          s_d1[wv][lane] = f * (a1 - P[2 * cc + 1]);
+          code += 4;
         }
       } else {
         tgt[2 * o] = 0.f;
         tgt[2 * o + 1] = 0.f;
       }
+      s_code[wv][lane] = code;
     }
+    __syncthreads();
+    if (live && lane == 0) {  // host order, as the per-window loop
+      const int n = H - i0 < 64 ? H - i0 : 64;
+      for (int j = 0; j < n; ++j) {
+        const int code = s_code[wv][j];
+        aloss += s_ce[wv][j];
+        acc[9] += code >= 0 ? 1.0 : 0.0;
+        if (code >= 0) {
+          tloss += s_tl[wv][j];
+          if (code >= 4) {
+            const int cc = code - 4;
+            acc[2 * cc] += s_d0[wv][j];
+            acc[2 * cc + 1] += s_d1[wv][j];
+            acc[6 + cc] += 1.0;
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (live && lane == 0) {
     loss[2 * b] = aloss;
     loss[2 * b + 1] = tloss;
   }
-  for (int k = 0; k < kDpInc; ++k) red[k][threadIdx.x] = acc[k];
+  if (lane == 0)
+    for (int k = 0; k < kDpInc; ++k) red[wv][k] = acc[k];
   __syncthreads();
-  for (int s = kTB / 2; s > 0; s >>= 1) {  // fixed tree order
-    if (threadIdx.x < s)
-      for (int k = 0; k < kDpInc; ++k) red[k][threadIdx.x] += red[k][threadIdx.x + s];
-    __syncthreads();
+  if (threadIdx.x < kDpInc) {  // fixed tree over the workgroup's windows
+    const int k = threadIdx.x;
+    part[(long)blockIdx.x * kDpInc + k] = (red[0][k] + red[1][k]) + (red[2][k] + red[3][k]);
   }
-  if (threadIdx.x < kDpInc) part[(long)blockIdx.x * kDpInc + threadIdx.x] = red[threadIdx.x][0];
 }
 
-// increments [3K+3] = delta [K][2], count [K], num_zero, num_ones, windows
-__global__ void tune_dp_finish_kernel(int H, int B, int K, int nblk, const double* __restrict__ part,
-                                      double* __restrict__ inc) {
+// increments [3K+3] = delta [K][2], count [K], num_zero, num_ones, windows.
+// One workgroup: thread t sums the partials t, t+256, ... in order, then a
+// fixed tree over the threads (deterministic for a given B).
+__global__ __launch_bounds__(kTB) void tune_dp_finish_kernel(int H, int B, int K, int nblk,
+                                                             const double* __restrict__ part,
+                                                             double* __restrict__ inc) {
 #pragma clang fp contract(off)
-  const int k = threadIdx.x;
-  if (k >= 3 * K + 3) return;
-  double v = 0.0;
-  int src = -1;
-  if (k < 6) src = k;                              // delta rows 0-2 (triplet classes)
-  else if (k >= 2 * K && k < 2 * K + 3) src = 6 + (k - 2 * K);  // counts 0-2
-  else if (k == 3 * K + 1) src = 9;                // num_ones
-  if (src >= 0)
-    for (int i = 0; i < nblk; ++i) v += part[(long)i * kDpInc + src];
-  if (k == 3 * K) v = (double)H * (double)B;       // num_zero: every host counts (train.py:31)
-  if (k == 3 * K + 2) v = (double)B;               // windows
-  inc[k] = v;
+  __shared__ double red[kDpInc][kTB];
+  const int t = threadIdx.x;
+  double v[kDpInc] = {};
+  for (int i = t; i < nblk; i += kTB)
+    for (int k = 0; k < kDpInc; ++k) v[k] += part[(long)i * kDpInc + k];
+  for (int k = 0; k < kDpInc; ++k) red[k][t] = v[k];
+  __syncthreads();
+  for (int s = kTB / 2; s > 0; s >>= 1) {
+    if (t < s)
+      for (int k = 0; k < kDpInc; ++k) red[k][t] += red[k][t + s];
+    __syncthreads();
+  }
+  for (int k = t; k < 3 * K + 3; k += kTB) {
+    int src = -1;
+    if (k < 6) src = k;                                           // delta rows 0-2 (triplet classes)
+    else if (k >= 2 * K && k < 2 * K + 3) src = 6 + (k - 2 * K);  // counts 0-2
+    else if (k == 3 * K + 1) src = 9;                             // num_ones
+    double x = src >= 0 ? red[src][0] : 0.0;
+    if (k == 3 * K) x = (double)H * (double)B;  // num_zero: every host counts (train.py:31)
+    if (k == 3 * K + 2) x = (double)B;          // windows
+    inc[k] = x;
+  }
 }
 
 __global__ void tune_state_apply_kernel(int K, double* __restrict__ state, const double* __restrict__ inc, double decay,
@@ -216,16 +283,16 @@ hipError_t launch_tune_dataset(int H, int E, int R, const double* series, const 
   return hipGetLastError();
 }
 
-long tune_dp_workspace_doubles(int B) { return (long)((B + kTB - 1) / kTB) * kDpInc; }
+long tune_dp_workspace_doubles(int B) { return (long)((B + kWpb - 1) / kWpb) * kDpInc; }
 
 hipError_t launch_tune_targets_dp(int H, int K, int B, const float* logits, const float* protos, const int* y,
                                   const int* cls, const double* state, double update_min, float* mult, float* tgt,
                                   double* loss, double* inc, double* ws, hipStream_t st) {
-  const int nblk = (B + kTB - 1) / kTB;
+  const int nblk = (B + kWpb - 1) / kWpb;
   tune_targets_dp_kernel<<<nblk, kTB, 0, st>>>(H, B, logits, protos, y, cls, state, K, update_min, mult, tgt, loss, ws);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  tune_dp_finish_kernel<<<1, 64 * ((3 * K + 3 + 63) / 64), 0, st>>>(H, B, K, nblk, ws, inc);
+  tune_dp_finish_kernel<<<1, kTB, 0, st>>>(H, B, K, nblk, ws, inc);
   return hipGetLastError();
 }
 
