@@ -157,20 +157,31 @@ __global__ __launch_bounds__(256, 2) void linear_kernel(LinArgs a) {
   f32x4 pw[NT], pb[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) pw[t] = pb[t] = zero4();
-  for (long rb = (long)blockIdx.x * 4 + wv; rb < nrb; rb += (long)gridDim.x * 4) {
+  // B-operand k-blocks are prefetched PF ahead (a ring of registers), so a
+  // wave keeps several HBM loads in flight; wide layers (NT > 4) keep the LDS
+  // fragments out of registers with a short unroll.  The next row block's first
+  // PF k-blocks are loaded while the current one computes.
+  constexpr int PF = NT > 4 ? (KB < 2 ? KB : 2) : (KB < 4 ? KB : 4);
+  const long rstep = (long)gridDim.x * 4;
+  f32x4 xq[PF];
+  {
+    const long m0 = ((long)blockIdx.x * 4 + wv) * 16 + mi;
+#pragma unroll
+    for (int j = 0; j < PF; ++j) xq[j] = m0 < a.M ? ld4(a.X + m0 * a.ldx + 4 * g + 16 * j) : zero4();
+  }
+  for (long rb = (long)blockIdx.x * 4 + wv; rb < nrb; rb += rstep) {
     const long m = rb * 16 + mi;
     const bool ok = m < a.M;
     f32x4 acc[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[t] = *reinterpret_cast<const f32x4*>(&cb[16 * t + 4 * g]);
     const float* xr = a.X + m * a.ldx + 4 * g;
-    // B-operand k-blocks are prefetched PF ahead (a ring of registers), so a
-    // wave keeps several HBM loads in flight; wide layers (NT > 4) keep the LDS
-    // fragments out of registers with a short unroll
-    constexpr int PF = NT > 4 ? (KB < 2 ? KB : 2) : (KB < 4 ? KB : 4);
-    f32x4 xq[PF];
+    f32x4 xn[PF];
+    {
+      const long mn = m + rstep * 16;
 #pragma unroll
-    for (int j = 0; j < PF; ++j) xq[j] = ok ? ld4(xr + 16 * j) : zero4();
+      for (int j = 0; j < PF; ++j) xn[j] = mn < a.M ? ld4(a.X + mn * a.ldx + 4 * g + 16 * j) : zero4();
+    }
 #pragma unroll 1
     for (int j0 = 0; j0 < KB; j0 += PF) {
 #pragma unroll
@@ -194,6 +205,8 @@ __global__ __launch_bounds__(256, 2) void linear_kernel(LinArgs a) {
         }
       }
     }
+#pragma unroll
+    for (int j = 0; j < PF; ++j) xq[j] = xn[j];
     float* yr = Yb + m * a.ldy + 4 * g;
     if constexpr (EPI == EPI_PE) {
       const int w = (int)((m % (3L * a.H)) / a.H);
@@ -826,16 +839,22 @@ __global__ __launch_bounds__(256) void tune_loss_kernel(int B, int H, int NOP, c
 // decoder weight / bias gradients straight into G (natural layout): one
 // workgroup per (token, n-half); the contraction runs over the batch's windows
 // (rows: dpre[b], X2 row b*T + tok), staged through LDS like dw_kernel.
+// Decoder weight gradient: for token tok (grid.x) and output-tile half y,
+// sum over windows of dpre[b] (x) X2[b][tok].  The windows are split over
+// grid.z = S parts (latency: one part is a short chain of LDS-staged chunks);
+// S = 1 adds straight into G, otherwise each part writes its [NOP][DP] slab
+// (and tok 0 its bias column) to `part` and dec_dw_sum adds them in part order.
 template <int H>
 __global__ __launch_bounds__(256) void dec_dw_kernel(int B, const float* __restrict__ dpre,
-                                                     const float* __restrict__ X2, float* __restrict__ Gd) {
+                                                     const float* __restrict__ X2, float* __restrict__ Gd,
+                                                     float* __restrict__ part) {
   using Q = TuneGeo<H>;
   using G = TGeo<H>;
   constexpr int NP = Q::NOP, KP = Q::DP, NT = NP / 16, NTW = (NT + 7) / 8, KT = KP / 16;
   __shared__ __attribute__((aligned(16))) float ys[kDwRows * lds_stride(NP)];
   __shared__ __attribute__((aligned(16))) float xs[kDwRows * lds_stride(KP)];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, g = lane >> 4, i = lane & 15;
-  const int tok = blockIdx.x, y = blockIdx.y;
+  const int tok = blockIdx.x, y = blockIdx.y, z = blockIdx.z, S = gridDim.z;
   f32x4 acc[NTW][KT];
   float pb[NTW];
 #pragma unroll
@@ -844,9 +863,13 @@ __global__ __launch_bounds__(256) void dec_dw_kernel(int B, const float* __restr
 #pragma unroll
     for (int u = 0; u < KT; ++u) acc[q][u] = zero4();
   }
-  dw_accumulate<NP, KP, NTW>(0, B, dpre, Q::NOP, X2 + (long)tok * Q::DP, (long)Q::T * Q::DP, 0, 4 * y, 8, ys, xs,
+  const long nch = (B + kDwRows - 1) / kDwRows;
+  const long r0 = nch * z / S * kDwRows, r1 = std::min<long>(B, nch * (z + 1) / S * kDwRows);
+  dw_accumulate<NP, KP, NTW>(r0, r1, dpre, Q::NOP, X2 + (long)tok * Q::DP, (long)Q::T * Q::DP, 0, 4 * y, 8, ys, xs,
                              acc, pb);
   const int w = tok / H, h = tok - w * H;
+  float* ps = part + ((long)z * Q::T + tok) * NP * KP;
+  float* pbias = part + (long)S * Q::T * NP * KP + (long)z * NP;
 #pragma unroll
   for (int q = 0; q < NTW; ++q) {
     const int t = 4 * y + wv + 8 * q;
@@ -856,7 +879,9 @@ __global__ __launch_bounds__(256) void dec_dw_kernel(int B, const float* __restr
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int n = 16 * t + 4 * g + r, c = 16 * u + i;
-          if (n < 4 * H && c < H) {
+          if (S > 1) {
+            ps[n * KP + c] = acc[q][u][r];
+          } else if (n < 4 * H && c < H) {
             const long col = (long)h * 3 * H + w * H + c;
             Gd[(n < 2 * H ? G::W_AN + (long)n * G::L : G::W_PR + (long)(n - 2 * H) * G::L) + col] += acc[q][u][r];
           }
@@ -864,9 +889,40 @@ __global__ __launch_bounds__(256) void dec_dw_kernel(int B, const float* __restr
       if (tok == 0) {
         const float sb = xsum(pb[q], true);
         const int n = 16 * t + i;
-        if (g == 0 && n < 4 * H) Gd[n < 2 * H ? G::B_AN + n : G::B_PR + n - 2 * H] += sb;
+        if (S > 1) {
+          if (g == 0) pbias[n] = sb;
+        } else if (g == 0 && n < 4 * H) {
+          Gd[n < 2 * H ? G::B_AN + n : G::B_PR + n - 2 * H] += sb;
+        }
       }
     }
+  }
+}
+
+// G += the S parts of dec_dw_kernel, summed in part order (one thread per
+// decoder weight in G's own layout, so the adds into G are coalesced)
+template <int H>
+__global__ __launch_bounds__(256) void dec_dw_sum_kernel(int S, const float* __restrict__ part, float* __restrict__ Gd) {
+  using Q = TuneGeo<H>;
+  using G = TGeo<H>;
+  constexpr int NP = Q::NOP, KP = Q::DP;
+  constexpr long NW = 4L * H * G::L;  // anomaly rows then prototype rows, each [2H][L]
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  if (idx < NW) {
+    const int n = (int)(idx / G::L);
+    const long col = idx - (long)n * G::L;  // h*3H + w*H + c
+    const int h = (int)(col / (3 * H)), rem = (int)(col - (long)h * 3 * H), w = rem / H, c = rem - w * H;
+    const int tok = w * H + h;
+    const float* src = part + ((long)tok * NP + n) * KP + c;
+    float v = 0.f;
+    for (int z = 0; z < S; ++z) v += src[(long)z * Q::T * NP * KP];
+    Gd[(n < 2 * H ? G::W_AN + (long)n * G::L : G::W_PR + (long)(n - 2 * H) * G::L) + col] += v;
+  } else if (idx < NW + 4 * H) {
+    const int n = (int)(idx - NW);
+    const float* src = part + (long)S * Q::T * NP * KP + n;
+    float v = 0.f;
+    for (int z = 0; z < S; ++z) v += src[(long)z * NP];
+    Gd[n < 2 * H ? G::B_AN + n : G::B_PR + n - 2 * H] += v;
   }
 }
 
@@ -1022,10 +1078,13 @@ bool plan_h(int B, TunePlan* out) {
   q.dec_s = (int)std::max<long>(1, std::min<long>(kbt, 512 / q.dec_bg));
   // partial slabs; every bound grows with B, so a workspace sized for B_max serves any B <= B_max
   const long np_max = std::max(Q::Q3P, 64);
-  long part = 512L * 2 * Q::DP;                                          // linear LNB, one per workgroup
-  part = std::max(part, 512L * (np_max * 64 + np_max));                   // dW slabs
+  long part = (long)PGP_LIN_CAP * 2 * Q::DP;                             // linear LNB, one per workgroup
+  part = std::max(part, (long)PGP_DW_CAP * (np_max * 64 + np_max));       // dW slabs
   part = std::max(part, std::max(512L, (long)q.dec_bg) * 64 * Q::NOP);    // decoder split-K
   part = std::max(part, (long)Q::T * 8 * 2 * Q::DP);                      // decoder dX LNB (<= 8 x T groups)
+  // decoder weight gradient: windows split over up to 4 parts of >= 8 chunks
+  q.dec_dws = (int)std::max<long>(1, std::min<long>(4, (B + kDwRows - 1) / kDwRows / 8));
+  if (q.dec_dws > 1) part = std::max(part, (long)q.dec_dws * (Q::T * Q::NOP * Q::DP + Q::NOP));
   q.part = take(part);
   // the backward's deferred reductions (RedBatch): each dW / LN-gradient partial
   // region plus its level-2 region, in the order tune_bwd_h takes them
@@ -1122,7 +1181,11 @@ hipError_t tune_bwd_h(const TunePlan& p, const float* P, float* Gd, float* ws, c
   RedBatch rb{ws + p.pool, p.pool_len};
   TCK((tune_loss_kernel<<<(int)(((long)B * H + 255) / 256), 256, 0, st>>>(B, H, Q::NOP, logits, protos, y, mult,
                                                                            tgt, ws + p.dpre)));
-  TCK((dec_dw_kernel<H><<<dim3(Q::T, 2), 256, 0, st>>>(B, ws + p.dpre, ws + p.x[2], Gd)));
+  TCK((dec_dw_kernel<H><<<dim3(Q::T, 2, p.dec_dws), 256, 0, st>>>(B, ws + p.dpre, ws + p.x[2], Gd, ws + p.part)));
+  if (p.dec_dws > 1) {
+    const long nw = 4L * H * G::L + 4 * H;
+    TCK((dec_dw_sum_kernel<H><<<(int)((nw + 255) / 256), 256, 0, st>>>(p.dec_dws, ws + p.part, Gd)));
+  }
   {  // grad of the encoder output = dpre . Wp (token layout), through layer 1's norm2: one
      // linear layer per token (grid.y) with that token's [DP][NOP] slab of Wp^T in LDS
     const float* L1 = P + G::LAY0 + G::L_SIZE;

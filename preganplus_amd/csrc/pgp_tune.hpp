@@ -40,7 +40,7 @@ struct TunePlan {
   long da = 0, db = 0, dq = 0, df = 0;                   // backward temporaries
   long gsx = 0, dpre = 0, wp = 0, wpt = 0, part = 0, total = 0;
   long pool = 0, pool_len = 0;  // the backward's deferred-reduction regions (RedBatch)
-  int lin_grid = 0, dw_grid = 0, dec_s = 0, dec_bg = 0, dec_dxg = 0;
+  int lin_grid = 0, dw_grid = 0, dec_s = 0, dec_bg = 0, dec_dxg = 0, dec_dws = 1;
 };
 
 bool tune_plan(int H, int B, TunePlan* p);
