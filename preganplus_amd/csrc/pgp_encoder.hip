@@ -43,15 +43,28 @@ constexpr int kEncWaves = 4;
 #ifndef PGP_ENC16_EU
 #define PGP_ENC16_EU 2
 #endif
+// Tail mode (H = 50) resident: the weight groups the tail path reads (layer 0's
+// stage 2 — its q/k/v and out_proj are folded onto the raw features — and all
+// of layer 1: 104 KB at H = 50) stay in LDS for the whole launch, one 8-wave
+// workgroup per CU (2 waves per SIMD as before); no ring barriers or DMAs in the
+// host loop, and one copy per workgroup instead of one per host
+#ifndef PGP_ENC_TAIL_RES
+#define PGP_ENC_TAIL_RES 1
+#endif
 template <int H>
-constexpr int enc_waves() { return H <= 16 ? PGP_ENC16_WAVES : kEncWaves; }
+constexpr bool tail_res() { return PGP_ENC_TAIL_RES && Geo<H>::TAIL && PGP_ENC_BILIN; }
+template <int H>
+constexpr int enc_waves() { return H <= 16 ? PGP_ENC16_WAVES : tail_res<H>() ? 8 : kEncWaves; }
 
 // RESIDENT (H <= 16): both layers' weights (24 KB at H = 16) are loaded into LDS
 // once per workgroup; the host loop then runs with no ring barriers or DMAs.
+// Tail-resident: groups [RES0, 2*LAYER_G) of the stream (see tail_res).
 template <int H>
 struct EncLds {
-  static constexpr int STREAM = kLayers * Geo<H>::LAYER_G * Geo<H>::FQ;  // floats
-  static constexpr bool RESIDENT = STREAM * 4 <= 32 * 1024;
+  static constexpr bool TRES = tail_res<H>();
+  static constexpr int RES0 = TRES ? Geo<H>::st_begin(Geo<H>::NST - 1) : 0;  // layer 0 stage 2
+  static constexpr int STREAM = (kLayers * Geo<H>::LAYER_G - RES0) * Geo<H>::FQ;  // floats
+  static constexpr bool RESIDENT = TRES || STREAM * 4 <= 32 * 1024;
   static constexpr int SLOT = Geo<H>::SLOT_G * Geo<H>::FQ;
   static constexpr int TAB = Geo<H>::t_size(kMaxProtos);
   static constexpr int TOTAL = (RESIDENT ? STREAM : 2 * SLOT) + TAB;
@@ -286,7 +299,8 @@ struct Ring {
   PGP_DEV void advance() {
     if constexpr (RES) {
       const int si = next % (kLayers * G::NST), l = si / G::NST, k = si % G::NST;
-      cur = nxt + (l * G::LAYER_G + G::st_begin(k)) * G::FQ;
+      const int gi = l * G::LAYER_G + G::st_begin(k) - EncLds<H>::RES0;  // < 0: a stage tail mode never reads
+      cur = nxt + (gi > 0 ? gi : 0) * G::FQ;
       ++next;
       __builtin_amdgcn_sched_barrier(0);  // keep stages apart (no hoisting of later stages' LDS reads)
       return;
@@ -690,7 +704,8 @@ PGP_DEV void encoder_layer(f32x4 (&X)[Geo<H>::MT_D][3], Ring<H>& ring, const flo
 }
 
 template <int H>
-__global__ __launch_bounds__(enc_waves<H>() * 64, H <= 16 ? PGP_ENC16_EU : 2) void encoder_kernel(FwdArgs a) {
+__global__ __launch_bounds__(enc_waves<H>() * 64, H <= 16 ? PGP_ENC16_EU : tail_res<H>() ? 1 : 2) void encoder_kernel(
+    FwdArgs a) {
   using G = Geo<H>;
   using L = EncLds<H>;
   __shared__ __attribute__((aligned(16))) float smem[L::TOTAL];
@@ -707,7 +722,7 @@ __global__ __launch_bounds__(enc_waves<H>() * 64, H <= 16 ? PGP_ENC16_EU : 2) vo
 
   Ring<H> ring{smem, smem + L::SLOT, a.frags + G::OFF_ENC, 0, H * kLayers * G::NST, wv, lane};
   if constexpr (L::RESIDENT) {
-    dma_groups(a.frags + G::OFF_ENC, smem, kLayers * G::LAYER_G, wv, NW, lane);
+    dma_groups(a.frags + G::OFF_ENC + (long)L::RES0 * G::FQ, smem, kLayers * G::LAYER_G - L::RES0, wv, NW, lane);
     ring.nxt = smem;
     ring.next = 1;
     __syncthreads();
