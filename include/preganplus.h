@@ -243,6 +243,14 @@ int pgp_tune_targets(int n_hosts, int n_protos, const float* logits, const float
 int pgp_tune_step1(int n_hosts, int n_protos, const float* window, const int* y, const int* cls, const float* P,
                    float* G, double* state, double update_min, double decay, float* logits, float* protos,
                    double* loss, void* stream);
+/* n independent batch-1 tuning forwards from the master P (n_hosts 8 or 16;
+ * one workgroup per window, the forward of pgp_tune_step1): the batched
+ * model(windows) that accuracy() scores (train.py:94-109, PreGANPlus.py:56).
+ * windows [n,3,3H] fp32; writes logits [n,H,2] and protos [n,H,2] as fp64
+ * (the values are the fp32 results, widened).  Replaces pgp_tune_forward for
+ * this use at 8 / 16 hosts. */
+int pgp_tune_forward_many(int n_hosts, int n_windows, const float* windows, const float* P, double* logits,
+                          double* protos, void* stream);
 /* run_model's per-interval forward for ONE window (PreGANPlus.py:115-136:
  * run_encoder, detect / embed / get_classes, Gen + Disc, the recover_decision
  * gate and targets), n_hosts 8 or 16, in a single launch, straight from the

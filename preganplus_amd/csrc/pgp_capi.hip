@@ -374,6 +374,16 @@ int pgp_tune_step1(int n_hosts, int n_protos, const float* window, const int* y,
   return PGP_OK;
 }
 
+int pgp_tune_forward_many(int n_hosts, int n_windows, const float* windows, const float* P, double* logits,
+                          double* protos, void* stream) {
+  if (!tune1_supported(n_hosts)) return fail(PGP_ERR_UNSUPPORTED, "host count (fused forward: 8 or 16)");
+  if (n_windows < 0) return fail(PGP_ERR_ARG, "n_windows >= 0");
+  if (n_windows == 0) return PGP_OK;
+  if (!windows || !P || !logits || !protos) return fail(PGP_ERR_ARG, "bad tune_forward_many arguments");
+  HIPCHK(launch_fwd_many(n_hosts, n_windows, windows, P, logits, protos, reinterpret_cast<hipStream_t>(stream)));
+  return PGP_OK;
+}
+
 int pgp_forward1(int n_hosts, int n_protos, const float* window, const float* sched, const float* P,
                  const double* prototypes_device, float* logits, float* protos, int* cls, int* any_anom, float* probs,
                  int* keep_orig, int* final_target, int* gen_target, void* stream) {

@@ -60,6 +60,9 @@ bool tune1_supported(int H);
 hipError_t launch_tune1(int H, int K, const float* win, const int* y, const int* cls, const float* P, float* G,
                         double* state, double update_min, double decay, float* logits, float* protos, double* loss,
                         hipStream_t st);
+// n independent batch-1 forwards (accuracy()'s batch), fp64 logits / protos [n][H][2]
+hipError_t launch_fwd_many(int H, int n, const float* win, const float* P, double* logits, double* protos,
+                           hipStream_t st);
 // batch-1 inference of run_model from the master weights (pgp_tune1.hip)
 hipError_t launch_infer1(int H, int K, const float* win, const float* sched, const float* P, const double* protos,
                          float* logits, float* protos_out, int* cls, int* any_anom, float* probs, int* keep,

@@ -217,7 +217,8 @@ PGP_DEV void t1_dx(const float* W, int K, const float* dy, int dys, int T, float
 // Shared by the tuning step (tune1_kernel) and the batch-1 inference (infer1_kernel).
 template <int H>
 PGP_DEV void t1_forward(float* sm, const float* __restrict__ P, const float* __restrict__ win,
-                        float* __restrict__ logits_out, float* __restrict__ protos_out, int& mk_) {
+                        float* __restrict__ logits_out, float* __restrict__ protos_out, int& mk_,
+                        double* __restrict__ logits64 = nullptr, double* __restrict__ protos64 = nullptr) {
   using S = T1<H>;
   using G = TGeo<H>;
   constexpr int D = S::D, T = S::T, HD = S::HD, FF = S::FF, Q3 = S::Q3, NO = S::NO, L = S::L;
@@ -383,9 +384,11 @@ PGP_DEV void t1_forward(float* sm, const float* __restrict__ P, const float* __r
         if (n < 2 * H) {
           s = acc + P[G::B_AN + n];  // LeakyReLU(True) = identity (models.py:361)
           if (logits_out) logits_out[n] = s;
+          if (logits64) logits64[n] = (double)s;
         } else {
           s = 1.0f / (1.0f + expf(-(acc + P[G::B_PR + n - 2 * H])));
           if (protos_out) protos_out[n - 2 * H] = s;
+          if (protos64) protos64[n - 2 * H] = (double)s;
         }
         out[n] = s;
       }
@@ -778,6 +781,21 @@ __global__ __launch_bounds__(kT1Threads) void infer1_kernel(int K, const float* 
 
 }  // namespace
 
+// n independent batch-1 forwards (one workgroup each, t1_forward): the
+// batched forward accuracy() runs on the tuning windows (train.py:94-109),
+// logits / prototype outputs written as fp64 [n][2H] each
+template <int H>
+__global__ __launch_bounds__(kT1Threads) void fwd_many_kernel(const float* __restrict__ win,
+                                                              const float* __restrict__ P,
+                                                              double* __restrict__ logits,
+                                                              double* __restrict__ protos) {
+  using S = T1<H>;
+  __shared__ __attribute__((aligned(16))) float sm[S::TOTAL];
+  const long b = blockIdx.x;
+  int mk_ = 0;
+  t1_forward<H>(sm, P, win + b * 9 * H, nullptr, nullptr, mk_, logits + b * 2 * H, protos + b * 2 * H);
+}
+
 #ifdef PGP_T1_PROF
 extern "C" int pgp_tune1_prof_read(unsigned long long* out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_t1_prof), sizeof(g_t1_prof)) == hipSuccess ? 0 : -1;
@@ -797,6 +815,22 @@ hipError_t launch_infer1(int H, int K, const float* win, const float* sched, con
     case 16:
       infer1_kernel<16><<<1, kT1Threads, 0, st>>>(K, win, sched, P, protos, logits, protos_out, cls, any_anom, probs,
                                                   keep, final_t, gen_t);
+      break;
+    default:
+      return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_fwd_many(int H, int n, const float* win, const float* P, double* logits, double* protos,
+                           hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  switch (H) {
+    case 8:
+      fwd_many_kernel<8><<<n, kT1Threads, 0, st>>>(win, P, logits, protos);
+      break;
+    case 16:
+      fwd_many_kernel<16><<<n, kT1Threads, 0, st>>>(win, P, logits, protos);
       break;
     default:
       return hipErrorInvalidValue;

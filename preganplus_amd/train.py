@@ -119,6 +119,7 @@ class Trainer:
         dbl = ctypes.c_double
         L.pgp_tune_step1.argtypes = [i32, i32] + [vp] * 6 + [dbl, dbl] + [vp] * 3 + [vp]
         L.pgp_forward1.argtypes = [i32, i32] + [vp] * 12 + [vp]
+        L.pgp_tune_forward_many.argtypes = [i32, i32] + [vp] * 4 + [vp]
         L.pgp_tune_dataset.argtypes = [i32, i32, i32] + [vp] * 6 + [vp]
         L.pgp_tune_targets_dp_workspace_len.argtypes = [i32]
         L.pgp_tune_targets_dp_workspace_len.restype = sz
@@ -128,7 +129,7 @@ class Trainer:
         for f in ("pgp_tune_forward", "pgp_tune_backward", "pgp_gan_forward", "pgp_gan_disc_backward",
                   "pgp_gan_gen_backward", "pgp_adamw", "pgp_load_weights_master", "pgp_tune_targets",
                   "pgp_adamw_table", "pgp_tune_dataset", "pgp_tune_targets_dp", "pgp_tune_state_apply",
-                  "pgp_gan_probs", "pgp_tune_step1", "pgp_forward1"):
+                  "pgp_gan_probs", "pgp_tune_step1", "pgp_forward1", "pgp_tune_forward_many"):
             getattr(L, f).restype = i32
         L._pgp_train_bound = True
 
@@ -215,6 +216,16 @@ class Trainer:
             state.data_ptr(), PROTO_UPDATE_MIN, PROTO_FACTOR_DECAY, self.logits.data_ptr(),
             self.protos.data_ptr(), loss.data_ptr(), self._stream()), "pgp_tune_step1")
         self._fwd_batch = 0   # the fused step keeps no activations for tune_backward
+
+    def tune_forward_many(self, windows, logits64, protos64):
+        """n independent batch-1 forwards from the master (``pgp_tune_forward_many``,
+        n_hosts 8 or 16; the fused step's forward, one workgroup per window):
+        windows [n,3,3H] fp32 -> logits64 / protos64 [n*H*2] fp64 device tensors
+        (accuracy()'s batched forward, train.py:94-109)."""
+        n = windows.shape[0]
+        _native.check(self._L.pgp_tune_forward_many(
+            self.H, n, windows.data_ptr(), self.P.data_ptr(), logits64.data_ptr(), protos64.data_ptr(),
+            self._stream()), "pgp_tune_forward_many")
 
     def forward1(self, window, sched, protos_dev, out):
         """run_model's forward of ONE window from the master weights
@@ -649,25 +660,38 @@ def normalize_test_time_data(time_data, train_time_data):
 
 
 def convert_to_windows(data, n_window=3):
-    """utils.py:7-14."""
+    """utils.py:7-14: window i = rows i-n..i-1, row 0 repeated for i < n (one
+    gather)."""
     data = np.asarray(data, dtype=np.float64)
-    out = []
-    for i in range(data.shape[0]):
-        if i >= n_window:
-            out.append(data[i - n_window:i])
-        else:
-            out.append(np.concatenate([np.repeat(data[0:1], n_window - i, axis=0), data[0:i]]))
-    return np.stack(out)
+    i = np.arange(data.shape[0])[:, None] - n_window + np.arange(n_window)[None, :]
+    return data[np.maximum(i, 0)]
+
+
+def percentile_linear(data, q):
+    """np.percentile(data, q, axis=0) (method 'linear'), from one sort: numpy's
+    virtual index (n-1)*q/100 and its lerp (b - (b-a)(1-g) for g >= 0.5, else
+    a + (b-a) g), so the thresholds are bit-identical to numpy's."""
+    n = data.shape[0]
+    vi = (n - 1) * (q / 100.0)
+    lo = np.floor(vi)
+    gm = vi - lo
+    ilo = int(lo)
+    ihi = min(ilo + 1, n - 1)
+    srt = np.sort(data, axis=0)
+    a, b = srt[ilo], srt[ihi]
+    d = b - a
+    return b - d * (1.0 - gm) if gm >= 0.5 else a + d * gm
 
 
 def form_test_dataset(data):
-    """utils.py:16-24."""
-    anomaly_per_dim = data > np.percentile(data, PERCENTILES, axis=0)
-    which, anydim = [], []
-    for i in range(0, data.shape[1], 3):
-        which.append(np.argmax(data[:, i:i + 3] + 0, axis=1))
-        anydim.append(np.logical_or.reduce(anomaly_per_dim[:, i:i + 3], axis=1))
-    return np.stack(anydim, axis=1) + 0, np.stack(which, axis=1)
+    """utils.py:16-24: per host (3 columns), anomalous if any column exceeds its
+    98th percentile; class = first argmax of the 3 columns (vectorised over hosts)."""
+    data = np.asarray(data)
+    anomaly_per_dim = data > percentile_linear(data, PERCENTILES)
+    R, F = data.shape
+    anydim = anomaly_per_dim.reshape(R, F // 3, 3).any(axis=2)
+    which = np.argmax(data.reshape(R, F // 3, 3), axis=2)
+    return anydim + 0, which
 
 
 def on_the_fly_dataset(time_series, schedule_series, train_time_data):
@@ -726,10 +750,7 @@ class _TuneGraph:
         self.loss = self.dout[:2 * n].view(n, 2)
         self.mult = torch.zeros((1, H), dtype=torch.float32, device=dev)
         self.tgt = torch.zeros((1, H, 2), dtype=torch.float32, device=dev)
-        if score:
-            tr._ensure(n)
-        else:
-            tr._ensure(1)
+        tr._ensure(n if score and not fused else 1)
         self.generation = tr.generation
         self.graph = torch.cuda.CUDAGraph()
         torch.cuda.synchronize(dev)
@@ -746,9 +767,12 @@ class _TuneGraph:
             self.dout[o:o + 2 * K + 3].copy_(self.state)
             if score:
                 o += 2 * K + 3
-                lg, pr = tr.tune_forward(self.W)
-                self.dout[o:o + 2 * n * H].copy_(lg.reshape(-1))
-                self.dout[o + 2 * n * H:o + 4 * n * H].copy_(pr.reshape(-1))
+                if fused:  # one launch, fp64 straight into the gather buffer
+                    tr.tune_forward_many(self.W, self.dout[o:o + 2 * n * H], self.dout[o + 2 * n * H:o + 4 * n * H])
+                else:
+                    lg, pr = tr.tune_forward(self.W)
+                    self.dout[o:o + 2 * n * H].copy_(lg.reshape(-1))
+                    self.dout[o + 2 * n * H:o + 4 * n * H].copy_(pr.reshape(-1))
 
     def run(self, tr, wins, anom, cls, state_vec, tab):
         hv = self.hviews
@@ -940,15 +964,23 @@ def train_gan(tr: Trainer, emb, sched, simulate):
 
 def accuracy(tr: Trainer, st: TuneState, wins, anom, cls):
     """train.py:94-109 after a tuning call (PreGANPlus.py:56): the updated model
-    on the same windows (one batched forward, pgp_tune_forward), then the
+    on the same windows (one batched forward: pgp_tune_forward_many at 8 / 16
+    hosts, else pgp_tune_forward), then the
     reference's per-window scores (``accuracy_scores``).  Returns (AScore,
     CScore).  ``backprop(..., score=True)`` computes the same inside the tuning
     graph."""
     wins = np.asarray(wins)
-    n = wins.shape[0]
-    logits, protos = tr.tune_forward(torch.as_tensor(wins, dtype=torch.float32))
-    lg = logits[:n].cpu().numpy().astype(np.float64)
-    pr = protos[:n].cpu().numpy().astype(np.float64)
+    n, H = wins.shape[0], tr.H
+    if H in FUSED_STEP_HOSTS:  # the fused forward, as backprop(score=True)'s graph runs it
+        w = torch.as_tensor(wins, dtype=torch.float32).to(tr.device).contiguous()
+        out = torch.empty(4 * n * H, dtype=torch.float64, device=tr.device)
+        tr.tune_forward_many(w, out[:2 * n * H], out[2 * n * H:])
+        o = out.cpu().numpy()
+        lg, pr = o[:2 * n * H].reshape(n, H, 2), o[2 * n * H:].reshape(n, H, 2)
+    else:
+        logits, protos = tr.tune_forward(torch.as_tensor(wins, dtype=torch.float32))
+        lg = logits[:n].cpu().numpy().astype(np.float64)
+        pr = protos[:n].cpu().numpy().astype(np.float64)
     return accuracy_scores(lg, pr, anom, cls, st.protos)
 
 
