@@ -329,6 +329,29 @@ int pgp_adamw_table(float* P, const float* G, float* exp_avg, float* exp_avg_sq,
                     float beta1, float beta2, float eps, const pgp_adam_tensor* tensors, int ntensors,
                     const float* sched, void* stream);
 
+/* train_gan (PreGANPlus.py:60-81) for ONE window in two launches, n_hosts 8 or
+ * 16 (the plugin's per-interval call), replacing pgp_gan_forward +
+ * pgp_gan_disc_backward + pgp_adamw_table(disc) + pgp_gan_gen_backward +
+ * pgp_gan_probs + pgp_adamw_table(gen) + pgp_gan_forward at batch 1:
+ * pgp_gan_forward1: emb [2H], sched [H,H] -> ns [H,H] (the generator's
+ * schedule), probs [2] (Disc on it); saves the window's activations in the GAN
+ * workspace (pgp_gan_workspace_len(H, 1) floats).
+ * pgp_gan_step1, after the host simulator's label target [2]: the Disc BCE step
+ * (gradients written into G's disc section, AdamW over disc_tensors with the
+ * device table disc_sched [n_disc,3] as pgp_adamw_table), the Gen step through
+ * the updated Disc (probs_gen [2] = the Disc probabilities it saw, gen_loss's
+ * input) with its AdamW over gen_tensors / gen_sched, then the updated GAN's
+ * Disc probabilities on the same inputs -> probs_after [2] (recover_decision's
+ * gate, PreGANPlus.py:84-87).  Tensor offsets index P / G / m / v and must lie
+ * in the disc / gen sections. */
+int pgp_gan_forward1(int n_hosts, const float* emb, const float* sched, const float* P, float* workspace, float* ns,
+                     float* probs, void* stream);
+int pgp_gan_step1(int n_hosts, const float* target, float* P, float* G, float* exp_avg, float* exp_avg_sq,
+                  float lr_disc, float lr_gen, float weight_decay, float beta1, float beta2, float eps,
+                  const pgp_adam_tensor* disc_tensors, int n_disc, const float* disc_sched,
+                  const pgp_adam_tensor* gen_tensors, int n_gen, const float* gen_sched, float* workspace,
+                  float* probs_gen, float* probs_after, void* stream);
+
 /* Rebuild the inference layouts from device master weights P (natural fp32)
  * and prototypes [K,2] (host, fp64): the sync after an optimizer step, via the
  * host packer (a device-to-host copy of P, pack, upload; synchronous). */

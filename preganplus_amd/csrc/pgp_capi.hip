@@ -474,6 +474,61 @@ int pgp_gan_gen_backward(int n_hosts, int batch, const float* P, float* G, float
   return PGP_OK;
 }
 
+int pgp_gan_forward1(int n_hosts, const float* emb, const float* sched, const float* P, float* workspace, float* ns,
+                     float* probs, void* stream) {
+  long tr, go, dof, all;
+  if (!gan1_supported(n_hosts) || !master_offsets(n_hosts, &tr, &go, &dof, &all))
+    return fail(PGP_ERR_UNSUPPORTED, "host count (fused GAN step: 8 or 16)");
+  if (!emb || !sched || !P || !workspace || !ns || !probs) return fail(PGP_ERR_ARG, "bad gan_forward1 arguments");
+  HIPCHK(launch_gan1_forward(n_hosts, emb, sched, P + go, P + dof, workspace, ns, probs,
+                             reinterpret_cast<hipStream_t>(stream)));
+  return PGP_OK;
+}
+
+static bool adam_args(AdamArgs* a, float* P, float* G, float* m, float* v, float lr, float wd, float b1, float b2,
+                      float eps, const pgp_adam_tensor* t, int n, const float* sched, long lo, long hi) {
+  if (!t || !sched || n < 0 || n > kMaxTensors) return false;
+  *a = AdamArgs{};
+  a->param = P;
+  a->grad = G;
+  a->m = m;
+  a->v = v;
+  a->lr_wd = lr * wd;
+  a->b1 = b1;
+  a->b2 = b2;
+  a->eps = eps;
+  a->ntensors = n;
+  a->sched = sched;
+  for (int i = 0; i < n; ++i) {
+    if (t[i].offset < lo || t[i].n < 0 || (long)t[i].offset + t[i].n > hi) return false;  // inside the section
+    a->t[i].off = (long)t[i].offset;
+    a->t[i].n = t[i].n;
+    a->t[i].active = 1;
+  }
+  return true;
+}
+
+int pgp_gan_step1(int n_hosts, const float* target, float* P, float* G, float* exp_avg, float* exp_avg_sq,
+                  float lr_disc, float lr_gen, float weight_decay, float beta1, float beta2, float eps,
+                  const pgp_adam_tensor* disc_tensors, int n_disc, const float* disc_sched,
+                  const pgp_adam_tensor* gen_tensors, int n_gen, const float* gen_sched, float* workspace,
+                  float* probs_gen, float* probs_after, void* stream) {
+  long tr, go, dof, all;
+  if (!gan1_supported(n_hosts) || !master_offsets(n_hosts, &tr, &go, &dof, &all))
+    return fail(PGP_ERR_UNSUPPORTED, "host count (fused GAN step: 8 or 16)");
+  if (!target || !P || !G || !exp_avg || !exp_avg_sq || !workspace || !probs_gen || !probs_after)
+    return fail(PGP_ERR_ARG, "bad gan_step1 arguments");
+  AdamArgs ad, ag;
+  if (!adam_args(&ad, P, G, exp_avg, exp_avg_sq, lr_disc, weight_decay, beta1, beta2, eps, disc_tensors, n_disc,
+                 disc_sched, dof, all) ||
+      !adam_args(&ag, P, G, exp_avg, exp_avg_sq, lr_gen, weight_decay, beta1, beta2, eps, gen_tensors, n_gen,
+                 gen_sched, go, dof))
+    return fail(PGP_ERR_ARG, "AdamW tensors (disc / gen sections) or tables");
+  HIPCHK(launch_gan1_step(n_hosts, target, P + go, P + dof, G + go, G + dof, workspace, ad, ag, probs_gen, probs_after,
+                          reinterpret_cast<hipStream_t>(stream)));
+  return PGP_OK;
+}
+
 int pgp_gan_probs(int n_hosts, int batch, const float* workspace, float* probs, void* stream) {
   if (!supported(n_hosts)) return fail(PGP_ERR_UNSUPPORTED, "host count");
   if (batch < 0 || (batch > 0 && (!workspace || !probs))) return fail(PGP_ERR_ARG, "bad arguments");

@@ -63,6 +63,14 @@ hipError_t launch_gan(const FwdArgs& a, hipStream_t st);
 struct AdamArgs;
 long gan_workspace_floats(int H, int B);
 hipError_t launch_adamw(const AdamArgs& a, hipStream_t st);
+// fused batch-1 GAN step (pgp_gan1.hip), H in {8, 16}
+bool gan1_supported(int H);
+hipError_t launch_gan1_forward(int H, const float* emb, const float* sched, const float* Pg, const float* Pd,
+                               float* row, float* ns, float* probs, hipStream_t st);
+hipError_t launch_gan1_step(int H, const float* target, float* Pg, float* Pd, float* Gg, float* Gd, float* row,
+                            const AdamArgs& ad, const AdamArgs& ag, float* probs_gen, float* probs_after,
+                            hipStream_t st);
+
 // GAN step (pgp_gantrain.hip); ws = gan_workspace_floats(H, B) floats
 hipError_t launch_gan_fwd(int H, int B, const float* emb, const float* sched, const float* Pg, const float* Pd,
                           float* ws, float* ns_out, float* probs, hipStream_t st);

@@ -9,8 +9,7 @@
 namespace pgp {
 namespace {
 
-// AdamW, torch single-tensor semantics (torch/optim/adamw.py): p *= 1 - lr*wd;
-// m = lerp(m, g, 1-b1); v = b2 v + (1-b2) g^2; p -= lr/bc1 * m / (sqrt(v)/sqrt(bc2) + eps)
+// AdamW (adamw_elem, pgp_train.hpp) over the tensors of a.t, one grid row each
 __global__ __launch_bounds__(256) void adamw_kernel(AdamArgs a) {
   const AdamTensor& t = a.t[blockIdx.y];
   float step_size = t.step_size, bc2_sqrt = t.bc2_sqrt;
@@ -22,17 +21,8 @@ __global__ __launch_bounds__(256) void adamw_kernel(AdamArgs a) {
   } else if (!t.active) {
     return;
   }
-  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < t.n; i += (long)gridDim.x * 256) {
-    const long o = t.off + i;
-    const float g = a.grad[o];
-    float p = a.param[o] * (1.0f - a.lr_wd);
-    const float m = a.m[o] + (1.0f - a.b1) * (g - a.m[o]);
-    const float v = a.b2 * a.v[o] + (1.0f - a.b2) * g * g;
-    p -= step_size * m / (sqrtf(v) / bc2_sqrt + a.eps);
-    a.param[o] = p;
-    a.m[o] = m;
-    a.v[o] = v;
-  }
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < t.n; i += (long)gridDim.x * 256)
+    adamw_elem(a, t.off + i, step_size, bc2_sqrt);
 }
 
 }  // namespace

@@ -75,4 +75,21 @@ struct AdamArgs {
   AdamTensor t[kMaxTensors];
 };
 
+// AdamW, torch single-tensor semantics (torch/optim/adamw.py), element o:
+// p *= 1 - lr*wd; m = lerp(m, g, 1-b1); v = b2 v + (1-b2) g^2;
+// p -= lr/bc1 * m / (sqrt(v)/sqrt(bc2) + eps).  Shared by the batched kernel
+// (pgp_train.hip) and the fused batch-1 GAN step (pgp_gan1.hip).
+#ifdef __HIP__
+__device__ __forceinline__ void adamw_elem(const AdamArgs& a, long o, float step_size, float bc2_sqrt) {
+  const float g = a.grad[o];
+  float p = a.param[o] * (1.0f - a.lr_wd);
+  const float m = a.m[o] + (1.0f - a.b1) * (g - a.m[o]);
+  const float v = a.b2 * a.v[o] + (1.0f - a.b2) * g * g;
+  p -= step_size * m / (sqrtf(v) / bc2_sqrt + a.eps);
+  a.param[o] = p;
+  a.m[o] = m;
+  a.v[o] = v;
+}
+#endif
+
 }  // namespace pgp

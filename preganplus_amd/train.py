@@ -120,6 +120,10 @@ class Trainer:
         L.pgp_tune_step1.argtypes = [i32, i32] + [vp] * 6 + [dbl, dbl] + [vp] * 3 + [vp]
         L.pgp_forward1.argtypes = [i32, i32] + [vp] * 12 + [vp]
         L.pgp_tune_forward_many.argtypes = [i32, i32] + [vp] * 4 + [vp]
+        L.pgp_gan_forward1.argtypes = [i32] + [vp] * 6 + [vp]
+        f32 = ctypes.c_float
+        L.pgp_gan_step1.argtypes = ([i32] + [vp] * 5 + [f32] * 6 + [ctypes.POINTER(_AdamTensor), i32, vp]
+                                    + [ctypes.POINTER(_AdamTensor), i32, vp] + [vp] * 3 + [vp])
         L.pgp_tune_dataset.argtypes = [i32, i32, i32] + [vp] * 6 + [vp]
         L.pgp_tune_targets_dp_workspace_len.argtypes = [i32]
         L.pgp_tune_targets_dp_workspace_len.restype = sz
@@ -129,7 +133,8 @@ class Trainer:
         for f in ("pgp_tune_forward", "pgp_tune_backward", "pgp_gan_forward", "pgp_gan_disc_backward",
                   "pgp_gan_gen_backward", "pgp_adamw", "pgp_load_weights_master", "pgp_tune_targets",
                   "pgp_adamw_table", "pgp_tune_dataset", "pgp_tune_targets_dp", "pgp_tune_state_apply",
-                  "pgp_gan_probs", "pgp_tune_step1", "pgp_forward1", "pgp_tune_forward_many"):
+                  "pgp_gan_probs", "pgp_tune_step1", "pgp_forward1", "pgp_tune_forward_many",
+                  "pgp_gan_forward1", "pgp_gan_step1"):
             getattr(L, f).restype = i32
         L._pgp_train_bound = True
 
@@ -252,6 +257,28 @@ class Trainer:
             self.H, B, emb.data_ptr(), sched.data_ptr(), self.P.data_ptr(), self.gscr.data_ptr(),
             self.ns.data_ptr(), self.probs.data_ptr(), self._stream()), "pgp_gan_forward")
         return self.ns[:B], self.probs[:B]
+
+    def gan_forward1(self, emb, sched, ns_out, probs_out):
+        """Gen + Disc forward of ONE window (``pgp_gan_forward1``, n_hosts 8 or
+        16): emb [2H], sched [H,H] fp32 device tensors -> ns_out [H*H],
+        probs_out [2]; the activations stay in the GAN workspace for
+        ``gan_step1``."""
+        self._ensure(1)
+        _native.check(self._L.pgp_gan_forward1(
+            self.H, emb.data_ptr(), sched.data_ptr(), self.P.data_ptr(), self.gscr.data_ptr(), ns_out.data_ptr(),
+            probs_out.data_ptr(), self._stream()), "pgp_gan_forward1")
+
+    def gan_step1(self, target, selD, tabD, selG, tabG, probs_gen, probs_after):
+        """The rest of train_gan for that window in one launch (``pgp_gan_step1``):
+        Disc BCE step + AdamW (device table tabD [len(selD),3]), Gen step through
+        the updated Disc + AdamW (tabG), the updated GAN's probabilities.
+        target [2] device fp32; probs_gen / probs_after [2] device outputs."""
+        desc = lambda sel: (_AdamTensor * len(sel))(*[_AdamTensor(t["offset"], t["n"], 1, 0.0, 0.0) for t in sel])
+        _native.check(self._L.pgp_gan_step1(
+            self.H, target.data_ptr(), self.P.data_ptr(), self.G.data_ptr(), self.m.data_ptr(), self.v.data_ptr(),
+            self.lrs["disc"], self.lrs["gen"], self.wd, self.b1, self.b2, self.eps,
+            desc(selD), len(selD), tabD.data_ptr(), desc(selG), len(selG), tabG.data_ptr(),
+            self.gscr.data_ptr(), probs_gen.data_ptr(), probs_after.data_ptr(), self._stream()), "pgp_gan_step1")
 
     def gan_disc_backward(self, target):
         target = self._dev(target, torch.float32)
@@ -876,9 +903,11 @@ class _GanGraph:
          saw + AdamW, then the updated GAN's forward on the same inputs (the
          gate recover_decision reads, PreGANPlus.py:84-87: tune_model does not
          touch the GAN, so it is computed here).
-    Each graph has one upload (pinned staging -> device) and one download."""
+    Each graph has one upload (pinned staging -> device) and one download.
+    At 8 / 16 hosts (``fused``, the default there) each graph is ONE launch:
+    ``pgp_gan_forward1`` and ``pgp_gan_step1`` (csrc/pgp_gan1.hip)."""
 
-    def __init__(self, tr: Trainer):
+    def __init__(self, tr: Trainer, fused: bool | None = None):
         H, dev = tr.H, tr.device
         self.generation_in = tr.generation
         tr._ensure(1)
@@ -902,6 +931,14 @@ class _GanGraph:
         HH = H * H
         torch.cuda.synchronize(dev)
         self.gA, self.gB = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        self.fused = (H in FUSED_STEP_HOSTS) if fused is None else fused
+        if self.fused:  # two single-workgroup launches (pgp_gan_forward1 / pgp_gan_step1)
+            with torch.cuda.graph(self.gA):
+                tr.gan_forward1(emb.reshape(-1), sch.reshape(-1), self.dout[:HH], self.dout[HH:HH + 2])
+            with torch.cuda.graph(self.gB):
+                tr.gan_step1(tgt.reshape(-1), self.selD, tabD, self.selG, tabG, self.dout[HH + 2:HH + 4],
+                             self.dout[HH + 4:HH + 6])
+            return
         with torch.cuda.graph(self.gA):
             ns, probs = tr.gan_forward(emb, sch)
             self.dout[:HH].copy_(ns.reshape(-1))
@@ -945,15 +982,16 @@ class _GanGraph:
         return out[HH + 2:HH + 4].copy(), out[HH + 4:HH + 6].copy()
 
 
-def train_gan(tr: Trainer, emb, sched, simulate):
+def train_gan(tr: Trainer, emb, sched, simulate, fused: bool | None = None):
     """PreGANPlus.py:60-75 (one window).  simulate(schedule ndarray) -> score.
     Returns (ns, new_score, orig_score, gen_loss, disc_loss); the updated
     GAN's Disc probabilities on the same (emb, sched) — recover_decision's
     gate — are left in ``tr.gan_probs_after``.  Two graph replays
     (``_GanGraph``) around the two simulator calls."""
     g = getattr(tr, "_gan_graph", None)
-    if g is None or g.generation != tr.generation:
-        g = tr._gan_graph = _GanGraph(tr)
+    want = (tr.H in FUSED_STEP_HOSTS) if fused is None else fused
+    if g is None or g.generation != tr.generation or g.fused != want:
+        g = tr._gan_graph = _GanGraph(tr, want)
     ns_h, p_d = g.forward(tr, emb, sched)
     new_score, orig_score = simulate(ns_h), simulate(np.asarray(sched, dtype=np.float64))
     target = bce_target(new_score, orig_score)
