@@ -80,8 +80,20 @@ __global__ __launch_bounds__(256) void gemm_epi_kernel(int mode, int M, int N, i
   if (idx >= (long)M * N) return;
   const long m = idx / N;
   const int n = (int)(idx - m * N);
+  // the S split partials in split order, loads issued 8 at a time (one
+  // dependent round trip per split made this latency-bound at S = 128)
+  const float* pp = part + m * ldp + n;
+  const long ss = (long)M * ldp;
   float v = 0.f;
-  for (int s = 0; s < S; ++s) v += part[((long)s * M + m) * ldp + n];
+  int s = 0;
+  for (; s + 8 <= S; s += 8) {
+    float q[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) q[j] = pp[(s + j) * ss];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v += q[j];
+  }
+  for (; s < S; ++s) v += pp[s * ss];
   if (bias) v += bias[n];  // LeakyReLU(True) = identity (models.py:127,145)
   if (mode == GE_BIAS) {
     out[m * ldo + n] = v;
