@@ -67,6 +67,38 @@ def test_fused_gan_step_matches_eager(scores):
         np.testing.assert_allclose(b.gan_probs_after, probs[0].cpu().numpy(), rtol=1e-4, atol=1e-6)
 
 
+def test_fused_gan_step_h8_matches_eager():
+    """The same at 8 hosts on seeded weights (one-hot schedules, as GOBI's)."""
+    from preganplus_amd import train as TR
+    H = 8
+    w = W.synth_weights(H, seed=4)
+    a, b = TR.Trainer(H, w), TR.Trainer(H, w)
+    lr = max(a.lrs["gen"], a.lrs["disc"])
+    rng = np.random.default_rng(8)
+    for call in range(3):
+        emb = rng.random(2 * H).astype(np.float32)
+        sched = np.eye(H)[rng.integers(0, H, H)]
+        scores = (1.0, 2.0) if call % 2 else (2.0, 1.0)
+        ia, ib = iter(scores), iter(scores)
+        ra = TR.train_gan_eager(a, emb, sched, lambda s: next(ia))
+        rb = TR.train_gan(b, emb, sched, lambda s: next(ib), fused=True)
+        np.testing.assert_allclose(rb[0], ra[0], rtol=1e-5, atol=1e-5)
+        np.testing.assert_allclose(rb[3:], ra[3:], rtol=1e-4, atol=1e-6)
+        pa, pb = a.P.cpu().numpy(), b.P.cpu().numpy()
+        assert (np.abs(pa - pb) <= 1e-5 * np.abs(pa) + 2.5 * lr * (call + 1)).all()
+        _, probs = a.gan_forward(np.asarray(emb)[None], np.asarray(sched)[None])
+        np.testing.assert_allclose(b.gan_probs_after, probs[0].cpu().numpy(), rtol=1e-4, atol=1e-6)
+
+
+def test_fused_gan_step_rejects_unsupported_hosts():
+    from preganplus_amd import _native
+    from preganplus_amd import train as TR
+    tr = TR.Trainer(50, W.synth_weights(50, seed=1))
+    z = torch.zeros(2600, device="cuda")
+    with pytest.raises(_native.NativeError):
+        tr.gan_forward1(z[:100], z[100:2600], z[:2500], z[:2])
+
+
 def test_packed_outputs_equal_plain():
     from preganplus_amd.model import DecisionModel, to_numpy
     w, _ = W.load_npz("preganplus_amd/data/simulator_16.npz")
