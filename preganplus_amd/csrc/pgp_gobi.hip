@@ -133,10 +133,35 @@ __device__ void load_regs(const float* __restrict__ W, GobiRegs& R) {
   R.b41 = W[GobiW::B4 + 1];
 }
 
+// cross-lane moves inside a 16-lane row as DPP operand modifiers (a few cycles)
+// instead of ds_bpermute round trips (__shfl_xor): quad_perm [1,0,3,2] = xor 1,
+// [2,3,0,1] = xor 2; row_half_mirror (lane i <- 7 - i of its 8) pairs the two
+// quads of an 8-lane group; row_ror 8 = xor 8; row_ror 4 rotates the row.  Every
+// sum keeps the butterfly's association (bitwise as the shuffles)
+constexpr int kDppX1 = 0xB1, kDppX2 = 0x4E, kDppHalfMirror = 0x141, kDppRor4 = 0x124, kDppRor8 = 0x128;
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+template <int CTRL>
+__device__ __forceinline__ int dppi(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+}
+// lane i <- lane i ^ 4 (row_shl 4 into banks 0 / 2, row_shr 4 into banks 1 / 3)
+__device__ __forceinline__ float dppf_xor4(float v) {
+  const int b = __float_as_int(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, b, 0x104, 0xF, 0x5, false);  // row_shl:4, banks 0, 2
+  return __int_as_float(__builtin_amdgcn_update_dpp(lo, b, 0x114, 0xF, 0xA, false));  // row_shr:4, banks 1, 3
+}
+
+// sum over N aligned adjacent lanes (N = 2, 4, 8), the same bits in all of them:
+// xor 1, xor 2, then the two 4-lane halves (whose lanes already agree) exchanged
 template <int N>
-__device__ __forceinline__ float lane_sum(float v) {  // xor butterfly over N adjacent lanes (same bits in all)
-#pragma unroll
-  for (int off = 1; off < N; off <<= 1) v += __shfl_xor(v, off);
+__device__ __forceinline__ float lane_sum(float v) {
+  static_assert(N == 2 || N == 4 || N == 8, "lane groups of 2, 4 or 8");
+  v += dppf<kDppX1>(v);
+  if constexpr (N >= 4) v += dppf<kDppX2>(v);
+  if constexpr (N >= 8) v += dppf<kDppHalfMirror>(v);  // == lane i ^ 4's value: the quads already agree
   return v;
 }
 
@@ -229,11 +254,22 @@ __device__ void surrogate_fwd(const float* __restrict__ W, const GobiRegs& R, Go
     if (on) {
       const float h3 = L.h3[e][l];
       float p0 = R.w40 * h3, p1 = R.w41 * h3;
+      // 64-lane xor butterfly, offsets 32, 16, 8, 4, 2, 1 (the same bits in every
+      // lane): 32 and 16 by ds_bpermute, 8 = row_ror 8, 4 = two bank-masked row
+      // shifts, 2 and 1 = quad_perm
 #pragma unroll
-      for (int off = 32; off >= 1; off >>= 1) {
+      for (int off = 32; off >= 16; off >>= 1) {
         p0 += __shfl_xor(p0, off);
         p1 += __shfl_xor(p1, off);
       }
+      p0 += dppf<kDppRor8>(p0);
+      p1 += dppf<kDppRor8>(p1);
+      p0 += dppf_xor4(p0);
+      p1 += dppf_xor4(p1);
+      p0 += dppf<kDppX2>(p0);
+      p1 += dppf<kDppX2>(p1);
+      p0 += dppf<kDppX1>(p0);
+      p1 += dppf<kDppX1>(p1);
       const float o0 = sigmoid_f(p0 + R.b40), o1 = sigmoid_f(p1 + R.b41);
       if (l == 0) {
         L.o[e][0] = o0;
@@ -368,17 +404,21 @@ __global__ __launch_bounds__(kT) void gobi_kernel(int E, const float* __restrict
         xv = xv + (-a1) * mm / denom;         // addcdiv_: self + value * t1 / t2 (ATen's order)
       }
       // ---- one-hot of the row's first argmax (opt.py:9-15): the row's lanes of this sq ----
+      // (max value, then lowest column) over the 16 lanes of this sq in the row's
+      // 32: xor 2, the row's parity class by rotations of 4 and 8 (each lane then
+      // holds the same winner), then xor 16
       float best = xv;
       int bi = hcol;
-#pragma unroll
-      for (int off = 2; off <= 16; off <<= 1) {
-        const float ov = __shfl_xor(best, off);
-        const int oi = __shfl_xor(bi, off);
+      auto take = [&](float ov, int oi) {
         if (ov > best || (ov == best && oi < bi)) {
           best = ov;
           bi = oi;
         }
-      }
+      };
+      take(dppf<kDppX2>(best), dppi<kDppX2>(bi));
+      take(dppf<kDppRor4>(best), dppi<kDppRor4>(bi));
+      take(dppf<kDppRor8>(best), dppi<kDppRor8>(bi));
+      take(__shfl_xor(best, 16), __shfl_xor(bi, 16));
       if (mine) {
         if (pre) pre[(e0 + e) * kH * kH + entry] = xv;  // test tap: the step's values before the projection
         const float nv = bi == hcol ? 1.f : 0.f;
