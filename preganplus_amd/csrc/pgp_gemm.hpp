@@ -7,27 +7,75 @@
 
 namespace pgp {
 
-PGP_DEV float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+// Cross-lane butterflies without ds_bpermute round trips: xor 1 / 2 as DPP
+// quad_perm, xor 8 as DPP row_ror 8, xor 4 as two bank-masked DPP row shifts,
+// xor 16 / 32 as the gfx950 row / half swaps (v_permlane16/32_swap).  Each
+// step returns own <op> partner exactly as v <op> __shfl_xor(v, o) did, so the
+// butterflies keep their association and results are bitwise unchanged.
+template <int O>
+PGP_DEV float xpartner(float v) {  // the value of lane ^ O, O in {1, 2, 4, 8}
+  const int b = __float_as_int(v);
+  if constexpr (O == 1) return __int_as_float(__builtin_amdgcn_update_dpp(0, b, 0xB1, 0xF, 0xF, false));
+  if constexpr (O == 2) return __int_as_float(__builtin_amdgcn_update_dpp(0, b, 0x4E, 0xF, 0xF, false));
+  if constexpr (O == 8) return __int_as_float(__builtin_amdgcn_update_dpp(0, b, 0x128, 0xF, 0xF, false));
+  if constexpr (O == 4) {
+    const int lo = __builtin_amdgcn_update_dpp(0, b, 0x104, 0xF, 0x5, false);    // row_shl 4 into banks 0, 2
+    return __int_as_float(__builtin_amdgcn_update_dpp(lo, b, 0x114, 0xF, 0xA, false));  // row_shr 4 into 1, 3
+  }
+  static_assert(O == 1 || O == 2 || O == 4 || O == 8, "in-row partner");
   return v;
 }
+// v + v[lane ^ O] for any O in {1, ..., 32}
+template <int O>
+PGP_DEV float xadd(float v) {
+  if constexpr (O == 16 || O == 32) {
+    const unsigned u = __float_as_uint(v);
+    const auto r = O == 16 ? __builtin_amdgcn_permlane16_swap(u, u, false, false)
+                           : __builtin_amdgcn_permlane32_swap(u, u, false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);  // own + partner in either order: a+b == b+a
+  } else {
+    return v + xpartner<O>(v);
+  }
+}
+template <int O>
+PGP_DEV float xmax(float v) {
+  if constexpr (O == 16 || O == 32) {
+    const unsigned u = __float_as_uint(v);
+    const auto r = O == 16 ? __builtin_amdgcn_permlane16_swap(u, u, false, false)
+                           : __builtin_amdgcn_permlane32_swap(u, u, false, false);
+    return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+  } else {
+    return fmaxf(v, xpartner<O>(v));
+  }
+}
+
+PGP_DEV float wave_max(float v) {
+  v = xmax<32>(v);
+  v = xmax<16>(v);
+  v = xmax<8>(v);
+  v = xmax<4>(v);
+  v = xmax<2>(v);
+  return xmax<1>(v);
+}
 PGP_DEV float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
-  return v;
+  v = xadd<32>(v);
+  v = xadd<16>(v);
+  v = xadd<8>(v);
+  v = xadd<4>(v);
+  v = xadd<2>(v);
+  return xadd<1>(v);
 }
 // sum over the 16 lanes of one lane group (the 16 token rows of a tile)
 PGP_DEV float row16_sum(float v) {
-#pragma unroll
-  for (int o = 8; o >= 1; o >>= 1) v += __shfl_xor(v, o);
-  return v;
+  v = xadd<8>(v);
+  v = xadd<4>(v);
+  v = xadd<2>(v);
+  return xadd<1>(v);
 }
-// sum over a 32-lane half wave
+// sum over 32 lanes (lane ^ 16 ... lane ^ 1)
 PGP_DEV float half_sum(float v) {
-#pragma unroll
-  for (int o = 16; o >= 1; o >>= 1) v += __shfl_xor(v, o);
-  return v;
+  v = xadd<16>(v);
+  return row16_sum(v);
 }
 PGP_DEV f32x4 zero4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
 PGP_DEV void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
