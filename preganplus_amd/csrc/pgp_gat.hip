@@ -18,6 +18,7 @@
 // Output = the B operand of the encoder's time-encoder MFMA:
 //   agg[((blk*H + j)*3 + w)*48 + f*16 + (b & 15)]
 #include "pgp_device.hpp"
+#include "pgp_gemm.hpp"
 
 namespace pgp {
 namespace {
@@ -27,8 +28,8 @@ __device__ __forceinline__ float lrelu001(float e) { return fmaxf(e, 0.01f * e);
 // One workgroup per 16-window block: 4 waves over the block's 48 (window, step)
 // items, lane = destination host.  For H <= 32 a wave holds P = 64 / S items at
 // once, one per S-lane segment (S = the power of two >= H): at H = 16 a
-// one-item wave left 3/4 of its lanes idle.  Segment reductions are xor shuffles
-// below S; the per-item source tables in LDS are padded by one entry per segment
+// one-item wave left 3/4 of its lanes idle.  Segment reductions are xor
+// butterflies below S (DPP and row swaps, seg_max / seg_sum); the per-item source tables in LDS are padded by one entry per segment
 // so the P segments' broadcast reads fall in different banks.  The block's
 // aggregation [H][3][48] is assembled in LDS and written out with contiguous
 // 16-B stores (scattered 4-B stores amplified the HBM writes 6x:
@@ -66,11 +67,8 @@ __global__ __launch_bounds__(256) void gat_agg_kernel(int B, const float* __rest
     const float s = gu0 * x0 + gu1 * x1 + gu2 * x2;
     const float t = gv0 * x0 + gv1 * x1 + gv2 * x2;
     float smax = host ? s : -INFINITY, tmax = host ? t : -INFINITY;
-#pragma unroll
-    for (int off = S / 2; off >= 1; off >>= 1) {
-      smax = fmaxf(smax, __shfl_xor(smax, off));
-      tmax = fmaxf(tmax, __shfl_xor(tmax, off));
-    }
+    smax = seg_max<S>(smax);  // DPP / row swaps, no ds_bpermute (pgp_gemm.hpp)
+    tmax = seg_max<S>(tmax);
     const float M = lrelu001(smax + tmax);  // = max_ij e_ij (lrelu and rounding are monotone)
     // u,v are pre-scaled by log2(e): the factors are v_exp_f32 (2^x) of the scaled terms
     const float ds = s - smax;
@@ -98,8 +96,7 @@ __global__ __launch_bounds__(256) void gat_agg_kernel(int B, const float* __rest
       for (int i = 0; i < H; ++i) edge(i);
     }
     float St = host ? S_ : 0.f;
-#pragma unroll
-    for (int off = S / 2; off >= 1; off >>= 1) St += __shfl_xor(St, off);
+    St = seg_sum<S>(St);
     if (active && host) {
       const float inv = 1.0f / St;
       float* o = out_lds + (hl * 3 + w) * 48 + j;

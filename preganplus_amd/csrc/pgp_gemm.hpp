@@ -77,6 +77,27 @@ PGP_DEV float half_sum(float v) {
   v = xadd<16>(v);
   return row16_sum(v);
 }
+// max / sum over aligned S-lane segments (S a power of two <= 64), offsets S/2 .. 1
+template <int S>
+PGP_DEV float seg_max(float v) {
+  if constexpr (S >= 64) v = xmax<32>(v);
+  if constexpr (S >= 32) v = xmax<16>(v);
+  if constexpr (S >= 16) v = xmax<8>(v);
+  if constexpr (S >= 8) v = xmax<4>(v);
+  if constexpr (S >= 4) v = xmax<2>(v);
+  if constexpr (S >= 2) v = xmax<1>(v);
+  return v;
+}
+template <int S>
+PGP_DEV float seg_sum(float v) {
+  if constexpr (S >= 64) v = xadd<32>(v);
+  if constexpr (S >= 32) v = xadd<16>(v);
+  if constexpr (S >= 16) v = xadd<8>(v);
+  if constexpr (S >= 8) v = xadd<4>(v);
+  if constexpr (S >= 4) v = xadd<2>(v);
+  if constexpr (S >= 2) v = xadd<1>(v);
+  return v;
+}
 PGP_DEV f32x4 zero4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
 PGP_DEV void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
 PGP_DEV float lrelu(float x) { return x > 0.f ? x : 0.01f * x; }
