@@ -187,8 +187,12 @@ __global__ __launch_bounds__(kDecWaves * 64, H <= 16 ? 8 : 1) void decoder_kerne
       }
     }
   }
-  anyf |= __shfl_xor(anyf, 16);
-  anyf |= __shfl_xor(anyf, 32);
+  {  // or over the 4 lane groups (the row swaps of xsum)
+    const auto r = __builtin_amdgcn_permlane16_swap((unsigned)anyf, (unsigned)anyf, false, false);
+    const int a16 = (int)(r[0] | r[1]);
+    const auto q = __builtin_amdgcn_permlane32_swap((unsigned)a16, (unsigned)a16, false, false);
+    anyf = (int)(q[0] | q[1]);
+  }
   if (valid && g == 0) a.any_anom[bw] = anyf;
 }
 

@@ -716,8 +716,7 @@ __global__ __launch_bounds__(kT1Threads) void infer1_kernel(int K, const float* 
     constexpr int KC = (GIN + 15) / 16;
     float acc = 0.f;
     for (int k = sp * KC; k < sp * KC + KC && k < GIN; ++k) acc = fmaf(Gp[G::G_W1 + o * GIN + k], xin[k], acc);
-#pragma unroll
-    for (int off = 1; off < 16; off <<= 1) acc += __shfl_xor(acc, off);
+    acc = xadd<8>(xadd<4>(xadd<2>(xadd<1>(acc))));  // xor 1, 2, 4, 8 (DPP, pgp_gemm.hpp)
     if (sp == 0) hg[o] = acc + Gp[G::G_B1 + o];  // LeakyReLU(True): identity
   }
   __syncthreads();
@@ -727,8 +726,7 @@ __global__ __launch_bounds__(kT1Threads) void infer1_kernel(int K, const float* 
     float acc = 0.f;
 #pragma unroll
     for (int k = 0; k < 16; ++k) acc = fmaf(Gp[G::G_W2 + o * 64 + sp * 16 + k], hg[sp * 16 + k], acc);
-    acc += __shfl_xor(acc, 1);
-    acc += __shfl_xor(acc, 2);
+    acc = xadd<2>(xadd<1>(acc));
     if (sp == 0) sd[H2 + o] = xin[2 * H + o] + 4.0f * tanhf(acc + Gp[G::G_B2 + o]);
   }
   __syncthreads();
@@ -738,18 +736,14 @@ __global__ __launch_bounds__(kT1Threads) void infer1_kernel(int K, const float* 
     constexpr int KC = DIN / 16;
     float acc = 0.f;
     for (int k = sp * KC; k < sp * KC + KC; ++k) acc = fmaf(Dp[G::D_W1 + o * DIN + k], sd[k], acc);
-#pragma unroll
-    for (int off = 1; off < 16; off <<= 1) acc += __shfl_xor(acc, off);
+    acc = xadd<8>(xadd<4>(xadd<2>(xadd<1>(acc))));
     if (sp == 0) hd[o] = acc + Dp[G::D_B1 + o];
   }
   __syncthreads();
   if (tid < 64) {  // Disc2 + softmax + gate (PreGANPlus.py:87), one wave
     float z0 = Dp[G::D_W2 + lane] * hd[lane], z1 = Dp[G::D_W2 + 64 + lane] * hd[lane];
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-      z0 += __shfl_xor(z0, off);
-      z1 += __shfl_xor(z1, off);
-    }
+    z0 = wave_sum(z0);  // xor 32 .. 1
+    z1 = wave_sum(z1);
     z0 += Dp[G::D_B2];
     z1 += Dp[G::D_B2 + 1];
     const float m = fmaxf(z0, z1), e0 = expf(z0 - m), e1 = expf(z1 - m), inv = 1.0f / (e0 + e1);
