@@ -13,6 +13,20 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kMaxProtos = 64;
 
+// compute units of the current device (cached per device id): grids of
+// one-workgroup-per-CU kernels
+inline int device_cus() {
+  static int cached[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (cached[dev] == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cached[dev] = n;
+  }
+  return cached[dev];
+}
+
 // Kernel arguments shared by the launches of one forward call.
 struct FwdArgs {
   int B, H, K;

@@ -53,8 +53,19 @@ constexpr int kEncWaves = 4;
 #endif
 template <int H>
 constexpr bool tail_res() { return PGP_ENC_TAIL_RES && Geo<H>::TAIL && PGP_ENC_BILIN; }
+// waves per tail-resident workgroup (one workgroup per CU): 8 = 2 waves per
+// SIMD, 12 = 3 (the register allocator then has 168 VGPRs + AGPRs per wave)
+// tail mode: the feed-forward hidden state formed and consumed 16 rows at a time
+#ifndef PGP_ENC_FFN_CHUNK
+#define PGP_ENC_FFN_CHUNK 1
+#endif
+#ifndef PGP_ENC_TAIL_WAVES
+#define PGP_ENC_TAIL_WAVES 8
+#endif
 template <int H>
-constexpr int enc_waves() { return H <= 16 ? PGP_ENC16_WAVES : tail_res<H>() ? 8 : kEncWaves; }
+constexpr int enc_waves() { return H <= 16 ? PGP_ENC16_WAVES : tail_res<H>() ? PGP_ENC_TAIL_WAVES : kEncWaves; }
+template <int H>
+constexpr int NW_STAGE() { return enc_waves<H>(); }
 
 // RESIDENT (H <= 16): both layers' weights (24 KB at H = 16) are loaded into LDS
 // once per workgroup; the host loop then runs with no ring barriers or DMAs.
@@ -606,6 +617,57 @@ PGP_DEV void encoder_layer_tail(f32x4 (&X)[Geo<H>::MT_D][3], Ring<H>& ring, cons
   }  // F0
   ring.advance();
   // [S2] relu(W1 x + b1), W2 . h + b2 + x, norm2
+#if PGP_ENC_FFN_CHUNK
+  // hidden tile by hidden tile: tile c of relu(W1 x + b1) is k-group c of the
+  // W2 contraction, consumed as soon as it is formed (12 hidden-state VGPRs
+  // live instead of 48; same accumulation order as the unchunked form)
+#pragma unroll
+  for (int mt = 0; mt < G::MT_D; ++mt) {
+    const f32x4 b2 = ld4(TL + G::TL_B2 + 16 * mt + 4 * g), g1 = ld4(TL + G::TL_LN1G + 16 * mt + 4 * g);
+#pragma unroll
+    for (int w = 0; w < 3; ++w) acc[mt][w] = X[mt][w] * g1 + b2;  // residual gamma*x-hat + beta, + b2
+  }
+  {
+    static_assert(G::KQ_F == G::MT_F, "hidden tile c = W2 k-group c");
+    float rf[G::XR][3];
+    zero_rows(rf);
+#pragma unroll
+    for (int c = 0; c < G::MT_F; ++c) {
+      f32x4 Fc[1][3];
+      const f32x4 b1 = ld4(TL + G::TL_B1 + 16 * c + 4 * g);
+#pragma unroll
+      for (int w = 0; w < 3; ++w) Fc[0][w] = b1;
+      gemm3<1, G::KQ_D, G::KS_D, G::MT_D>(Fc, ring.cur + c * G::KQ_D * 256, X, lane);
+#pragma unroll
+      for (int w = 0; w < 3; ++w)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Fc[0][w][r] = relu_enc<H>(Fc[0][w][r]);
+      const float* A2 = ring.cur + G::G_F1 * G::FQ;
+      prio_mfma();
+#pragma unroll
+      for (int m = 0; m < G::MT_X; ++m) {
+        const f32x4 a = ld4(A2 + (m * G::KQ_F + c) * 256 + lane * 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int w = 0; w < 3; ++w) acc[m][w] = mfma(a[e], Fc[0][w][e], acc[m][w]);
+      }
+      prio_valu();
+      if constexpr (!PGP_EXP_NO_ROWS) {
+#pragma unroll
+        for (int n = 0; n < G::XR; ++n) {
+          const f32x4 rw = ld4(TL + G::TL_RF + ((n * G::KQ_F + c) * 4 + g) * 4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int w = 0; w < 3; ++w) rf[n][w] = fmaf(rw[e], Fc[0][w][e], rf[n][w]);
+        }
+      }
+    }
+#pragma unroll
+    for (int w = 0; w < 3; ++w) acc[G::MT_X][w][0] += rows_pick<G::XR>(rf, w);
+  }
+#else
   f32x4 F1[G::MT_F][3];
 #pragma unroll
   for (int mt = 0; mt < G::MT_F; ++mt) {
@@ -634,6 +696,7 @@ PGP_DEV void encoder_layer_tail(f32x4 (&X)[Geo<H>::MT_D][3], Ring<H>& ring, cons
 #pragma unroll
     for (int w = 0; w < 3; ++w) acc[G::MT_X][w][0] += rows_pick<G::XR>(rf, w);
   }
+#endif
   ring.advance();
   layer_norm_tiles<H>(acc, X, TL + G::TL_LN2G, TL + G::TL_LN2B, g);
 }
@@ -709,6 +772,8 @@ __global__ __launch_bounds__(enc_waves<H>() * 64, H <= 16 ? PGP_ENC16_EU : tail_
   using G = Geo<H>;
   using L = EncLds<H>;
   __shared__ __attribute__((aligned(16))) float smem[L::TOTAL];
+  // tail-resident mode: per-wave staging slot of the next unit's raw features
+  __shared__ float xstage[L::TRES ? NW_STAGE<H>() * 144 : 1];
   float* tab = smem + (L::RESIDENT ? L::STREAM : 2 * L::SLOT);
   const int tsz = G::t_size(a.K);
   for (int i = threadIdx.x; i < tsz; i += blockDim.x) tab[i] = a.tab[i];
@@ -716,9 +781,7 @@ __global__ __launch_bounds__(enc_waves<H>() * 64, H <= 16 ? PGP_ENC16_EU : tail_
   const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   constexpr int NW = enc_waves<H>();
-  const long blk = (long)blockIdx.x * NW + wv;
   const long nblk = (a.B + 15) / 16;
-  const bool active = blk < nblk;  // inactive waves still take part in the ring and barriers
 
   Ring<H> ring{smem, smem + L::SLOT, a.frags + G::OFF_ENC, 0, H * kLayers * G::NST, wv, lane};
   if constexpr (L::RESIDENT) {
@@ -735,20 +798,33 @@ __global__ __launch_bounds__(enc_waves<H>() * 64, H <= 16 ? PGP_ENC16_EU : tail_
     ring.issue();  // stage 1 -> slot 1
   }
 
-  const float* agg = a.agg + (active ? blk : 0) * H * 3 * 48;
-  float* lat = a.lat + (active ? blk : 0) * G::LAT_BLK;
-#pragma unroll 1
-  for (int h = 0; h < H; ++h) {
+  // one (16-window block, host) unit: hosts are independent in the encoder
+  // one (16-window block, host) unit: hosts are independent in the encoder.
+  // tail-resident mode: pre = the unit's 144 raw-feature floats ([step][feature]
+  // [window], the agg layout) staged in LDS by the caller; otherwise loaded here
+  auto unit = [&](long blk, int h, bool active, const float* pre) {
+    const float* agg = a.agg + (active ? blk : 0) * H * 3 * 48;
+    float* lat = a.lat + (active ? blk : 0) * G::LAT_BLK;
     float ba[3];
-#pragma unroll
-    for (int w = 0; w < 3; ++w) ba[w] = (active && g < 3) ? agg[(h * 3 + w) * 48 + lane] : 0.f;
     // all 3 raw features of every step of this lane's window (layer 0's bilinear scores)
     float xv[3][3];
+    if constexpr (L::TRES) {
 #pragma unroll
-    for (int w = 0; w < 3; ++w)
+      for (int w = 0; w < 3; ++w) {
 #pragma unroll
-      for (int f = 0; f < 3; ++f)
-        xv[w][f] = (G::TAIL && PGP_ENC_BILIN && active) ? agg[(h * 3 + w) * 48 + 16 * f + j] : 0.f;
+        for (int f = 0; f < 3; ++f) xv[w][f] = pre[w * 48 + 16 * f + j];
+        const float v = pre[w * 48 + (lane < 48 ? lane : 47)];
+        ba[w] = g < 3 ? v : 0.f;  // feature g of window j
+      }
+    } else {
+#pragma unroll
+      for (int w = 0; w < 3; ++w) ba[w] = (active && g < 3) ? agg[(h * 3 + w) * 48 + lane] : 0.f;
+#pragma unroll
+      for (int w = 0; w < 3; ++w)
+#pragma unroll
+        for (int f = 0; f < 3; ++f)
+          xv[w][f] = (G::TAIL && PGP_ENC_BILIN && active) ? agg[(h * 3 + w) * 48 + 16 * f + j] : 0.f;
+    }
     f32x4 X[G::MT_D][3];
 #pragma unroll
     for (int mt = 0; mt < G::MT_D; ++mt) {
@@ -785,6 +861,46 @@ __global__ __launch_bounds__(enc_waves<H>() * 64, H <= 16 ? PGP_ENC16_EU : tail_
         }
       }
     }
+  };
+  if constexpr (L::TRES) {
+    // no barrier in the host loop: each wave takes an equal contiguous range of
+    // the nblk x H units (one workgroup per CU, grid = CU count), so the launch
+    // has no partial last round of workgroups
+    const long U = nblk * H, NWT = (long)gridDim.x * NW, gw = (long)blockIdx.x * NW + wv;
+    const long u1 = (gw + 1) * U / NWT;
+    // unit u's raw features are agg[u * 144 ..] (144 floats).  The next unit's
+    // are loaded while this one computes and staged through a per-wave LDS slot
+    // after this unit's latent stores: no loop-carried registers, so the wait
+    // for them is a counted vmcnt in the body (long satisfied) instead of a
+    // vmcnt(0) at the loop head that would also wait for the stores.
+    float* slot = xstage + wv * 144;
+    const long u0 = gw * U / NWT;
+    float pf[3];
+    auto load_x = [&](long u) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) pf[k] = a.agg[u * 144 + (64 * k + lane < 144 ? 64 * k + lane : 143)];
+    };
+    auto stage_x = [&]() {
+#pragma unroll
+      for (int k = 0; k < 3; ++k)
+        if (64 * k + lane < 144) slot[64 * k + lane] = pf[k];
+    };
+    if (u0 < u1) {
+      load_x(u0);
+      stage_x();
+    }
+#pragma unroll 1
+    for (long u = u0; u < u1; ++u) {
+      load_x(u + 1 < u1 ? u + 1 : u);
+      const long blk = u / H;
+      unit(blk, (int)(u - blk * H), true, slot);
+      stage_x();
+    }
+  } else {
+    const long blk = (long)blockIdx.x * NW + wv;
+    const bool active = blk < nblk;  // inactive waves still take part in the ring and barriers
+#pragma unroll 1
+    for (int h = 0; h < H; ++h) unit(blk, h, active, nullptr);
   }
 }
 
@@ -792,8 +908,9 @@ template <int H>
 hipError_t launch(const FwdArgs& a, hipStream_t st) {
   const long nblk = (a.B + 15) / 16;
   constexpr int NW = enc_waves<H>();
-  const int grid = (int)((nblk + NW - 1) / NW);
-  encoder_kernel<H><<<grid, NW * 64, 0, st>>>(a);
+  long grid = (nblk + NW - 1) / NW;
+  if constexpr (EncLds<H>::TRES) grid = std::min<long>(device_cus(), (nblk * H + NW - 1) / NW);
+  encoder_kernel<H><<<(int)grid, NW * 64, 0, st>>>(a);
   return hipGetLastError();
 }
 
