@@ -698,7 +698,9 @@ PGP_DEV void encoder_layer_tail(f32x4 (&X)[Geo<H>::MT_D][3], Ring<H>& ring, cons
   }
 #endif
   ring.advance();
-  layer_norm_tiles<H>(acc, X, TL + G::TL_LN2G, TL + G::TL_LN2B, g);
+  // the last layer's norm2 emits x-hat: its gamma / beta are folded into the
+  // decoders by the packer (the decoders are linear in the latent)
+  layer_norm_tiles<H, F0>(acc, X, TL + G::TL_LN2G, TL + G::TL_LN2B, g);
 }
 
 // One encoder layer; weights arrive stage by stage through the ring.  F0:
@@ -763,7 +765,7 @@ PGP_DEV void encoder_layer(f32x4 (&X)[Geo<H>::MT_D][3], Ring<H>& ring, const flo
   }
   gemm3<G::MT_D, G::KQ_F, 16, G::MT_F>(acc, ring.cur, F1, lane);
   ring.advance();
-  layer_norm_tiles<H>(acc, X, TL + G::TL_LN2G, TL + G::TL_LN2B, g);
+  layer_norm_tiles<H, F0>(acc, X, TL + G::TL_LN2G, TL + G::TL_LN2B, g);  // layer 1: x-hat (see tail)
 }
 
 template <int H>
@@ -856,7 +858,10 @@ __global__ __launch_bounds__(enc_waves<H>() * 64, H <= 16 ? PGP_ENC16_EU : tail_
 #pragma unroll
               for (int r = 0; r < 4; ++r) {
                 const int c = 16 * mt + 4 * r + g;
-                if (c < H) a.latent[b * G::LAT + (long)h * 3 * H + w * H + c] = X[mt][w][r];
+                const float* TL1 = tab + G::T_L0 + G::TL_SIZE;  // the latent = gamma * x-hat + beta
+                if (c < H)
+                  a.latent[b * G::LAT + (long)h * 3 * H + w * H + c] =
+                      X[mt][w][r] * TL1[G::TL_LN2G + 16 * mt + 4 * g + r] + TL1[G::TL_LN2B + 16 * mt + 4 * g + r];
               }
         }
       }

@@ -519,7 +519,10 @@ PGP_HD void pack_phase2(int K, const Src& src, const Ex& ex, double scale, const
     });
 
   // ---- decoders: rows n = 4*host + {l0, l1, p0, p1} ----
+  // The encoder hands over the last norm2's x-hat: its gamma scales the decoder
+  // columns and W . beta joins the decoder bias (fp64, one rounding)
   const View<Src> anW = V(B.anW), prW = V(B.prW), anB = V(B.anB), prB = V(B.prB);
+  const View<Src> n2wL = V(B.ly[kLayers - 1].n2w), n2bL = V(B.ly[kLayers - 1].n2b);
   ex.par((long)d * 3 * G::MT_O * G::KQ_D * 256, [&](long idx) {
     const int e4 = (int)(idx % 4), lane = (int)(idx / 4 % 64), q4 = (int)(idx / 256 % G::KQ_D);
     long r = idx / (256L * G::KQ_D);
@@ -530,13 +533,17 @@ PGP_HD void pack_phase2(int K, const Src& src, const Ex& ex, double scale, const
     const int n = 16 * mt + i, host = n / 4, q = n % 4;
     if (s >= G::KS_D || c >= d || host >= d) return;
     const long col = (long)h * 3 * d + w * d + c;
-    const double v = q < 2 ? anW[(long)(2 * host + q) * L + col] : prW[(long)(2 * host + q - 2) * L + col];
+    const double v =
+        (q < 2 ? anW[(long)(2 * host + q) * L + col] : prW[(long)(2 * host + q - 2) * L + col]) * n2wL[c];
     F[G::OFF_DEC + ((long)(h * 3 + w) * G::DEC_G + mt * G::KQ_D + q4) * G::FQ + lane * 4 + e4] = (float)v;
   });
   ex.par((long)G::MT_O * 16, [&](long n) {
     const int host = (int)(n / 4), q = (int)(n % 4);
     if (host >= d) return;
-    T[G::T_DEC + n] = (float)(q < 2 ? anB[2 * host + q] : prB[2 * host + q - 2]);
+    double b = q < 2 ? anB[2 * host + q] : prB[2 * host + q - 2];
+    for (long col = 0; col < L; ++col)
+      b += (q < 2 ? anW[(long)(2 * host + q) * L + col] : prW[(long)(2 * host + q - 2) * L + col]) * n2bL[col % d];
+    T[G::T_DEC + n] = (float)b;
   });
   const View<Src> protos = V(B.protos);
   ex.par(2L * K, [&](long k) { T[G::T_PROTO + k] = (float)protos[k]; });
