@@ -539,8 +539,14 @@ PGP_DEV void encoder_layer_tail(f32x4 (&X)[Geo<H>::MT_D][3], Ring<H>& ring, cons
 #pragma unroll
   for (int mt = 0; mt < G::MT_D; ++mt) {
     const f32x4 bo = ld4(TL + G::TL_BO + 16 * mt + 4 * g);
+    if constexpr (F0) {
 #pragma unroll
-    for (int w = 0; w < 3; ++w) acc[mt][w] = bo + X[mt][w];
+      for (int w = 0; w < 3; ++w) acc[mt][w] = bo + X[mt][w];
+    } else {  // X = layer 0's norm2 x-hat: residual gamma0 * x-hat + (bo + beta0) (packer)
+      const f32x4 g0 = ld4(TL - G::TL_SIZE + G::TL_LN2G + 16 * mt + 4 * g);
+#pragma unroll
+      for (int w = 0; w < 3; ++w) acc[mt][w] = X[mt][w] * g0 + bo;
+    }
   }
   if constexpr (F0) {
     // [S1] layer 0: out_proj through the attention, folded (no v, no P.v):
@@ -698,9 +704,10 @@ PGP_DEV void encoder_layer_tail(f32x4 (&X)[Geo<H>::MT_D][3], Ring<H>& ring, cons
   }
 #endif
   ring.advance();
-  // the last layer's norm2 emits x-hat: its gamma / beta are folded into the
-  // decoders by the packer (the decoders are linear in the latent)
-  layer_norm_tiles<H, F0>(acc, X, TL + G::TL_LN2G, TL + G::TL_LN2B, g);
+  // both norm2s emit x-hat: layer 0's gamma / beta are folded into layer 1's
+  // in_proj and residual, the last layer's into the decoders (which are linear
+  // in the latent), by the packer
+  layer_norm_tiles<H, false>(acc, X, TL + G::TL_LN2G, TL + G::TL_LN2B, g);
 }
 
 // One encoder layer; weights arrive stage by stage through the ring.  F0:

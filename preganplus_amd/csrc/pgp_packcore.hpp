@@ -221,9 +221,18 @@ PGP_HD int tile_src(int T0, int i) {
 
 template <int H, class V, class Ex>
 PGP_HD void pack_tail_attention(const V& inW, const V& inB, const V& outW, double scale, const Ex& ex, float* FL,
-                                float* TL) {
+                                float* TL, bool fold, const V& gam, const V& bet) {
   using G = Geo<H>;
   constexpr int d = H;
+  // fold: the layer's input is the previous norm2's x-hat, so in_proj's columns
+  // take that norm's gamma and its rows add in_proj . beta (fp64, one rounding)
+  auto wcol = [&](long src, int c) { return inW[src * d + c] * (fold ? gam[c] : 1.0); };
+  auto brow = [&](long src) {
+    double b = inB[src];
+    if (fold)
+      for (int c = 0; c < d; ++c) b += inW[src * d + c] * bet[c];
+    return b;
+  };
   // q, k tiles (stage 0) and v tiles (stage 1): [m][t][q4] groups over X k-steps
   ex.par(3L * G::TQ * G::KQ_D * 256, [&](long idx) {
     const int e4 = (int)(idx % 4), lane = (int)(idx / 4 % 64), q4 = (int)(idx / 256 % G::KQ_D);
@@ -233,13 +242,13 @@ PGP_HD void pack_tail_attention(const V& inW, const V& inB, const V& outW, doubl
     int hh, e;
     if (s >= G::KS_D || c >= d || !tail_slot<H>(t, i, &hh, &e)) return;
     const int src = m * d + hh * G::HD + e;
-    FL[(base + q4) * G::FQ + lane * 4 + e4] = (float)(inW[(long)src * d + c] * (m == 0 ? scale : 1.0));
+    FL[(base + q4) * G::FQ + lane * 4 + e4] = (float)(wcol(src, c) * (m == 0 ? scale : 1.0));
   });
   ex.par(3L * G::TQ * 16, [&](long idx) {
     const int i = (int)(idx % 16), t = (int)(idx / 16 % G::TQ), m = (int)(idx / (16 * G::TQ));
     int hh, e;
     if (!tail_slot<H>(t, i, &hh, &e)) return;
-    TL[G::TL_QKV + (m * G::TQ + t) * 16 + i] = (float)(inB[m * d + hh * G::HD + e] * (m == 0 ? scale : 1.0));
+    TL[G::TL_QKV + (m * G::TQ + t) * 16 + i] = (float)(brow(m * d + hh * G::HD + e) * (m == 0 ? scale : 1.0));
   });
   // VALU rows of head 1's tail
   ex.par(3L * G::SR * G::KQ_D * 16, [&](long idx) {
@@ -249,12 +258,12 @@ PGP_HD void pack_tail_attention(const V& inW, const V& inB, const V& outW, doubl
     const int s = 4 * q4 + e4, c = 4 * s + g;
     if (s >= G::KS_D || c >= d) return;
     TL[G::TL_RQ + (((m * G::SR + n) * G::KQ_D + q4) * 4 + g) * 4 + e4] =
-        (float)(inW[(long)src * d + c] * (m == 0 ? scale : 1.0));
+        (float)(wcol(src, c) * (m == 0 ? scale : 1.0));
   });
   ex.par(3L * G::SR, [&](long idx) {
     const int n = (int)(idx % G::SR), m = (int)(idx / G::SR);
     const int src = m * d + G::HD + 16 * G::HF + 16 - G::HT + n;
-    TL[G::TL_RQB + m * G::SR + n] = (float)(inB[src] * (m == 0 ? scale : 1.0));
+    TL[G::TL_RQB + m * G::SR + n] = (float)(brow(src) * (m == 0 ? scale : 1.0));
   });
   // out_proj: MT_X output tiles over the O slots (+ VALU rows 16*MT_X + n)
   ex.par((long)G::MT_X * G::KQ_OT * 256, [&](long idx) {
@@ -367,8 +376,12 @@ PGP_HD void pack_phase2(int K, const Src& src, const Ex& ex, double scale, const
                     n2w = V(O.n2w), n2b = V(O.n2b);
     float* FL = F + G::OFF_ENC + (long)l * G::LAYER_G * G::FQ;
     float* TL = T + G::T_L0 + l * G::TL_SIZE;
+    // tail mode: layer 0's norm2 gamma / beta folded into layer 1's in_proj and
+    // residual (the kernel passes layer 1 x-hat; residual = gamma * x-hat + (bo + beta))
+    const bool fold0 = G::TAIL && l > 0;
+    const View<Src> pn2w = V(B.ly[l > 0 ? l - 1 : 0].n2w), pn2b = V(B.ly[l > 0 ? l - 1 : 0].n2b);
     if constexpr (G::TAIL) {
-      pack_tail_attention<H>(inW, inB, outW, scale, ex, FL, TL);
+      pack_tail_attention<H>(inW, inB, outW, scale, ex, FL, TL, fold0, pn2w, pn2b);
     } else {
       ex.par((long)G::NPASS * 3 * G::TP * G::KQ_D * 256, [&](long idx) {
         const int e4 = (int)(idx % 4), lane = (int)(idx / 4 % 64), q4 = (int)(idx / 256 % G::KQ_D);
@@ -430,7 +443,7 @@ PGP_HD void pack_phase2(int K, const Src& src, const Ex& ex, double scale, const
     ex.par((long)G::DP, [&](long R) {
       const int c = featX((int)R);
       if (c >= d) return;
-      TL[G::TL_BO + R] = (float)outB[c];
+      TL[G::TL_BO + R] = (float)(outB[c] + (fold0 ? pn2b[c] : 0.0));
       TL[G::TL_LN1G + R] = (float)n1w[c];
       TL[G::TL_LN1B + R] = (float)n1b[c];
       TL[G::TL_B2 + R] = (float)(l2B[c] + n1b[c]);  // + norm1's beta: the residual is gamma*x-hat + beta
