@@ -10,6 +10,7 @@
 namespace pgp {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int kMaxProtos = 64;
 

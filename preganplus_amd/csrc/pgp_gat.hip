@@ -34,6 +34,10 @@ __device__ __forceinline__ float lrelu001(float e) { return fmaxf(e, 0.01f * e);
 // aggregation [H][3][48] is assembled in LDS and written out with contiguous
 // 16-B stores (scattered 4-B stores amplified the HBM writes 6x:
 // profiles/r01/pmc_r01pmc2_summary.txt).
+// independent accumulation chains of the one-item-per-wave edge loop (H > 32)
+#ifndef PGP_GAT_CHAINS
+#define PGP_GAT_CHAINS 2
+#endif
 constexpr int seg_lanes(int h) { return h <= 8 ? 8 : h <= 16 ? 16 : h <= 32 ? 32 : 64; }
 
 template <int H>
@@ -43,8 +47,9 @@ __global__ __launch_bounds__(256) void gat_agg_kernel(int B, const float* __rest
   constexpr int S = seg_lanes(H), P = 64 / S, SS = P > 1 ? S + 1 : S;
   constexpr int BLK = H * 3 * 48;  // floats per 16-window block
   __shared__ __attribute__((aligned(16))) float out_lds[BLK];
-  __shared__ f32x4 sx[4][P * SS];  // {A_i, x_i}
-  __shared__ float sa[4][P * SS];  // A'_i
+  __shared__ f32x4 sx[4][P * SS];                // P == 1: {A_i, A'_i, x_i0, x_i1}; else {A_i, x_i}
+  __shared__ f32x2 sy[4][P == 1 ? P * SS : 1];    // P == 1: {x_i2, 1}
+  __shared__ float sa[4][P == 1 ? 1 : P * SS];    // P > 1: A'_i
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int seg = lane / S, hl = lane % S;  // item slot, destination host
   const long blk = blockIdx.x;
@@ -73,25 +78,63 @@ __global__ __launch_bounds__(256) void gat_agg_kernel(int B, const float* __rest
     // u,v are pre-scaled by log2(e): the factors are v_exp_f32 (2^x) of the scaled terms
     const float ds = s - smax;
     const int base = seg * SS;
-    sx[wv][base + hl] = f32x4{__builtin_amdgcn_exp2f(ds), x0, x1, x2};
-    sa[wv][base + hl] = __builtin_amdgcn_exp2f(0.01f * ds);
+    const float Ap = __builtin_amdgcn_exp2f(ds), An = __builtin_amdgcn_exp2f(0.01f * ds);
     const float Bp = __builtin_amdgcn_exp2f(t + smax - M);
     const float Bn = __builtin_amdgcn_exp2f(0.01f * (t + smax) - M);
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes landed
-    __builtin_amdgcn_wave_barrier();
-    float S_ = 0.f, a0 = 0.f, a1 = 0.f, a2 = 0.f;
-    auto edge = [&](int i) {
-      const f32x4 v = sx[wv][base + i];
-      const float p = fmaxf(v.x * Bp, sa[wv][base + i] * Bn);  // exp2(lrelu(s_i + t_j) - M)
-      S_ += p;
-      a0 += p * v.y;
-      a1 += p * v.z;
-      a2 += p * v.w;
-    };
-    if constexpr (H % 5 == 0) {
+    float S_, a0, a1, a2;
+    if constexpr (P == 1) {
+      // one item per wave (H > 32): the edge loop is latency-bound on its
+      // accumulation chains, so packed f32 (one v_pk_mul for both branch
+      // products, a max, two v_pk_fma for (a0, a1) and (a2, S)) over PGP_GAT_CHAINS
+      // interleaved chains (source i -> chain i mod NC) summed at the end
+      sx[wv][base + hl] = f32x4{Ap, An, x0, x1};
+      sy[wv][base + hl] = f32x2{x2, 1.f};
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes landed
+      __builtin_amdgcn_wave_barrier();
+      const f32x2 Bpn = {Bp, Bn};
+      constexpr int NC = PGP_GAT_CHAINS;
+      f32x2 a01[NC], a2s[NC];
+#pragma unroll
+      for (int c = 0; c < NC; ++c) a01[c] = a2s[c] = f32x2{0.f, 0.f};
+      auto edge = [&](int i, int c) {
+        const f32x4 v = sx[wv][base + i];
+        const f32x2 q = f32x2{v.x, v.y} * Bpn;
+        const float p = fmaxf(q.x, q.y);  // exp2(lrelu(s_i + t_j) - M)
+        const f32x2 pp = {p, p};
+        a01[c] = __builtin_elementwise_fma(pp, f32x2{v.z, v.w}, a01[c]);
+        a2s[c] = __builtin_elementwise_fma(pp, sy[wv][base + i], a2s[c]);
+      };
 #pragma unroll 5
-      for (int i = 0; i < H; ++i) edge(i);
+      for (int i = 0; i + NC <= H; i += NC)
+#pragma unroll
+        for (int c = 0; c < NC; ++c) edge(i + c, c);
+#pragma unroll
+      for (int c = 0; c < H % NC; ++c) edge(H - H % NC + c, c);
+      f32x2 s01 = a01[0], s2s = a2s[0];
+#pragma unroll
+      for (int c = 1; c < NC; ++c) {
+        s01 += a01[c];
+        s2s += a2s[c];
+      }
+      S_ = s2s.y;
+      a0 = s01.x;
+      a1 = s01.y;
+      a2 = s2s.x;
     } else {
+      // P items per wave already interleave P independent chains
+      sx[wv][base + hl] = f32x4{Ap, x0, x1, x2};
+      sa[wv][base + hl] = An;
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes landed
+      __builtin_amdgcn_wave_barrier();
+      S_ = a0 = a1 = a2 = 0.f;
+      auto edge = [&](int i) {
+        const f32x4 v = sx[wv][base + i];
+        const float p = fmaxf(v.x * Bp, sa[wv][base + i] * Bn);  // exp2(lrelu(s_i + t_j) - M)
+        S_ += p;
+        a0 += p * v.y;
+        a1 += p * v.z;
+        a2 += p * v.w;
+      };
 #pragma unroll 4
       for (int i = 0; i < H; ++i) edge(i);
     }
