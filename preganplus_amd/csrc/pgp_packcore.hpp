@@ -98,7 +98,8 @@ template <int H>
 struct Scratch {
   static constexpr long A = 0;
   static constexpr long FOLD = 3L * H;
-  static constexpr long SIZE = FOLD + 3L * H * 6;
+  static constexpr long DECC = FOLD + 3L * H * 6;  // [dec row][feature]: sum over (host, step) of W
+  static constexpr long SIZE = DECC + (long)Geo<H>::MT_O * 16 * H;
 };
 
 // Gen / Disc (models.py:118-151) into the K3 chunk layout (pgp_gan.hip).
@@ -338,6 +339,22 @@ PGP_HD void pack_phase1(int K, const Src& src, const Ex& ex, double scale, doubl
       FT[s * 6 + 3 + w] = acc * sc;
     }
   });
+  // decoder rows n = 4*host + {l0, l1, p0, p1}: per feature c the sum over the
+  // 3H (host, step) columns of that feature (the last norm2's beta fold, phase 2)
+  using G = Geo<H>;
+  constexpr long L = 3L * H * H;
+  const View<Src> anW{src, B.anW}, prW{src, B.prW};
+  double* DC = scr + Scratch<H>::DECC;
+  ex.par((long)G::MT_O * 16 * d, [&](long idx) {
+    const int n = (int)(idx / d), c = (int)(idx % d), host = n / 4, q = n % 4;
+    double acc = 0;
+    if (host < d)
+      for (int hw = 0; hw < 3 * d; ++hw) {
+        const long col = (long)hw * d + c;
+        acc += q < 2 ? anW[(long)(2 * host + q) * L + col] : prW[(long)(2 * host + q - 2) * L + col];
+      }
+    DC[idx] = acc;
+  });
 }
 
 // phase 2: everything else
@@ -554,8 +571,8 @@ PGP_HD void pack_phase2(int K, const Src& src, const Ex& ex, double scale, const
     const int host = (int)(n / 4), q = (int)(n % 4);
     if (host >= d) return;
     double b = q < 2 ? anB[2 * host + q] : prB[2 * host + q - 2];
-    for (long col = 0; col < L; ++col)
-      b += (q < 2 ? anW[(long)(2 * host + q) * L + col] : prW[(long)(2 * host + q - 2) * L + col]) * n2bL[col % d];
+    const double* DC = scr + Scratch<H>::DECC + n * d;  // phase 1's column sums
+    for (int c = 0; c < d; ++c) b += DC[c] * n2bL[c];
     T[G::T_DEC + n] = (float)b;
   });
   const View<Src> protos = V(B.protos);
