@@ -98,8 +98,8 @@ template <int H>
 struct Scratch {
   static constexpr long A = 0;
   static constexpr long FOLD = 3L * H;
-  static constexpr long DECC = FOLD + 3L * H * 6;  // [dec row][feature]: sum over (host, step) of W
-  static constexpr long SIZE = DECC + (long)Geo<H>::MT_O * 16 * H;
+  static constexpr long DECC = FOLD + 3L * H * 6;  // [dec row][feature][step]: sum over hosts of W
+  static constexpr long SIZE = DECC + (long)Geo<H>::MT_O * 16 * H * 3;
 };
 
 // Gen / Disc (models.py:118-151) into the K3 chunk layout (pgp_gan.hip).
@@ -326,31 +326,34 @@ PGP_HD void pack_phase1(int K, const Src& src, const Ex& ex, double scale, doubl
   const View<Src> teB{src, B.teB}, pe{src, B.pe}, inW{src, B.ly[0].inW}, inB{src, B.ly[0].inB};
   const double* A = scr + Scratch<H>::A;
   double* FT = scr + Scratch<H>::FOLD;
-  ex.par(3L * d, [&](long s) {
+  ex.par(3L * d * 6, [&](long idx) {  // one (row, column) of the fold table per item
+    const long s = idx / 6;
+    const int k = (int)(idx % 6);
     const double sc = s < d ? scale : 1.0;
-    for (int f = 0; f < 3; ++f) {
+    if (k < 3) {
       double acc = 0;
-      for (int c = 0; c < d; ++c) acc += inW[s * d + c] * A[c * 3 + f];
-      FT[s * 6 + f] = acc * sc;
-    }
-    for (int w = 0; w < 3; ++w) {
+      for (int c = 0; c < d; ++c) acc += inW[s * d + c] * A[c * 3 + k];
+      FT[s * 6 + k] = acc * sc;
+    } else {
+      const int w = k - 3;
       double acc = inB[s];
       for (int c = 0; c < d; ++c) acc += inW[s * d + c] * (teB[c] + pe[w * d + c]);
       FT[s * 6 + 3 + w] = acc * sc;
     }
   });
-  // decoder rows n = 4*host + {l0, l1, p0, p1}: per feature c the sum over the
-  // 3H (host, step) columns of that feature (the last norm2's beta fold, phase 2)
+  // decoder rows n = 4*host + {l0, l1, p0, p1}: per (feature c, step w) the sum
+  // over the H host columns (the last norm2's beta fold, phase 2)
   using G = Geo<H>;
   constexpr long L = 3L * H * H;
   const View<Src> anW{src, B.anW}, prW{src, B.prW};
   double* DC = scr + Scratch<H>::DECC;
-  ex.par((long)G::MT_O * 16 * d, [&](long idx) {
-    const int n = (int)(idx / d), c = (int)(idx % d), host = n / 4, q = n % 4;
+  ex.par((long)G::MT_O * 16 * d * 3, [&](long idx) {  // [row][feature][step]: a sum over hosts
+    const int w = (int)(idx % 3), c = (int)(idx / 3 % d), n = (int)(idx / (3L * d)), host = n / 4, q = n % 4;
     double acc = 0;
     if (host < d)
-      for (int hw = 0; hw < 3 * d; ++hw) {
-        const long col = (long)hw * d + c;
+#pragma unroll 8
+      for (int h = 0; h < d; ++h) {
+        const long col = (long)h * 3 * d + w * d + c;
         acc += q < 2 ? anW[(long)(2 * host + q) * L + col] : prW[(long)(2 * host + q - 2) * L + col];
       }
     DC[idx] = acc;
@@ -571,8 +574,9 @@ PGP_HD void pack_phase2(int K, const Src& src, const Ex& ex, double scale, const
     const int host = (int)(n / 4), q = (int)(n % 4);
     if (host >= d) return;
     double b = q < 2 ? anB[2 * host + q] : prB[2 * host + q - 2];
-    const double* DC = scr + Scratch<H>::DECC + n * d;  // phase 1's column sums
-    for (int c = 0; c < d; ++c) b += DC[c] * n2bL[c];
+    const double* DC = scr + Scratch<H>::DECC + n * d * 3;  // phase 1's column sums
+#pragma unroll 4
+    for (int c = 0; c < d; ++c) b += ((DC[3 * c] + DC[3 * c + 1]) + DC[3 * c + 2]) * n2bL[c];
     T[G::T_DEC + n] = (float)b;
   });
   const View<Src> protos = V(B.protos);

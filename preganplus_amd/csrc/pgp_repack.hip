@@ -57,8 +57,8 @@ hipError_t repack_h(const RepackArgs& a, hipStream_t st) {
   const long big = (long)H * 3 * G::DEC_G * 256;
   const int grid2 = (int)std::min<long>(2048, (big + 255) / 256);
   repack_kernel<H><<<1, 256, 0, st>>>(0, a.K, src, scale, a.scr, a.frags, a.tab, a.gtab, a.gat);
-  // phase 1 also sums the decoder weights per (row, feature): MT_O*16*H items
-  const int grid1 = (int)std::min<long>(64, ((long)G::MT_O * 16 * H + 255) / 256);
+  // phase 1 also sums the decoder weights per (row, feature, step): MT_O*16*H*3 items
+  const int grid1 = (int)std::min<long>(256, ((long)G::MT_O * 16 * H * 3 + 255) / 256);
   repack_kernel<H><<<grid1, 256, 0, st>>>(1, a.K, src, scale, a.scr, a.frags, a.tab, a.gtab, a.gat);
   repack_kernel<H><<<grid2, 256, 0, st>>>(2, a.K, src, scale, a.scr, a.frags, a.tab, a.gtab, a.gat);
   return hipGetLastError();
