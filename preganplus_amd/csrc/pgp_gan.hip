@@ -36,6 +36,11 @@ constexpr int kQC = 4;  // schedule k-blocks (16 columns each) per chunk
 #define PGP_GAN_TAIL 1
 #endif
 constexpr int kTailMax = 2;
+// start-of-container delay of the second half of the waves, in s_sleep units of
+// 64 cycles (0: off)
+#ifndef PGP_GAN_SLEEP
+#define PGP_GAN_SLEEP 24
+#endif
 template <int P>
 __device__ __forceinline__ void gan_prio() {
   if (PGP_GAN_PRIO) __builtin_amdgcn_s_setprio(P);
@@ -55,6 +60,7 @@ struct GanGeo {
   }
   static constexpr int CPC = cpc();
   static constexpr int NCHUNK = 1 + NQC + G::C / CPC;
+  static constexpr int NSLOT = 2;
   static constexpr int mx(int x, int y) { return x > y ? x : y; }
   static constexpr int SLOT_G = mx(G::GE_G, mx(kQC * G::GS_G, CPC * G::GC_G));
   static constexpr int SLOT = SLOT_G * G::FQ;
@@ -78,7 +84,7 @@ template <int H>
 __global__ __launch_bounds__(kGanWaves * 64) void gan_kernel(FwdArgs a) {
   using G = Geo<H>;
   using GG = GanGeo<H>;
-  __shared__ __attribute__((aligned(16))) float smem[2 * GG::SLOT];
+  __shared__ __attribute__((aligned(16))) float smem[GG::NSLOT * GG::SLOT];
   const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const long blk = (long)blockIdx.x * kGanWaves + wv;
@@ -89,6 +95,9 @@ __global__ __launch_bounds__(kGanWaves * 64) void gan_kernel(FwdArgs a) {
   const float* ew = a.emb + (valid ? b : 0) * G::EP;
   const float* gt = a.gtab;
 
+  // ring: chunk k lives in slot k % NSLOT; chunk k + 1 is loaded while chunk k
+  // is computed (with 3 slots, chunk k - 1 also stays resident)
+  auto slot = [&](int k) { return smem + (k % GG::NSLOT) * GG::SLOT; };
   float* cur = smem;
   float* nxt = smem + GG::SLOT;
   int next = 1;
@@ -108,10 +117,9 @@ __global__ __launch_bounds__(kGanWaves * 64) void gan_kernel(FwdArgs a) {
   };
   auto advance = [&]() {
     __syncthreads();
-    float* t = cur;
     cur = nxt;
-    nxt = t;
     ++next;
+    nxt = slot(next);
     issue();
   };
 
@@ -202,14 +210,13 @@ __global__ __launch_bounds__(kGanWaves * 64) void gan_kernel(FwdArgs a) {
   constexpr int MTM = TAIL ? G::MT_N - 1 : G::MT_N;  // Gen2 tiles on MFMA
   float sv[G::MT_N][4];
   load_row(0, sv);
-  for (int c = 0; c < G::C; ++c) {
-    const float* cw = cur + (c % GG::CPC) * G::GC_G * G::FQ;  // this container's groups
-    float svn[G::MT_N][4];
-    load_row(c + 1, svn);
-    f32x4 ns[G::MT_N];
+  // Gen2 of container c from its chunk groups cw: ns = b2[c] + W2[c] . hg (the
+  // VALU tail rows into racc)
+  auto gen2 = [&](int c, const float* cw, f32x4 (&ns)[G::MT_N], float (&racc)[kTailMax]) {
 #pragma unroll
     for (int t = 0; t < G::MT_N; ++t) ns[t] = ld4(gt + G::G_B2 + c * G::MT_N * 16 + 16 * t + 4 * g);
-    float racc[kTailMax] = {};
+#pragma unroll
+    for (int r = 0; r < kTailMax; ++r) racc[r] = 0.f;
     gan_prio<1>();
 #pragma unroll
     for (int q4 = 0; q4 < 4; ++q4) {
@@ -235,6 +242,11 @@ __global__ __launch_bounds__(kGanWaves * 64) void gan_kernel(FwdArgs a) {
       }
     }
     gan_prio<0>();
+  };
+  // the rest of container c: tanh / new schedule / both first-argmaxes against
+  // the schedule row sv, Disc1's new-schedule half, the targets
+  auto finish = [&](int c, const float* cw, f32x4 (&ns)[G::MT_N], float (&racc)[kTailMax],
+                    const float (&sv)[G::MT_N][4]) {
     if (TAIL) {  // lanes g = 0 hold rows 16 MTM + r; the other groups' rows are >= H
 #pragma unroll
       for (int r = 0; r < NTR; ++r) ns[MTM][r] += xsum(racc[r], true);
@@ -294,11 +306,28 @@ __global__ __launch_bounds__(kGanWaves * 64) void gan_kernel(FwdArgs a) {
       a.gen_t[b * G::C + c] = bn_i;
       a.final_t[b * G::C + c] = bs_i;
     }
-    if ((c + 1) % GG::CPC == 0) advance();
+  };
+  auto copy_row = [&](float (&d)[G::MT_N][4], const float (&sr)[G::MT_N][4]) {
 #pragma unroll
     for (int t = 0; t < G::MT_N; ++t)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) sv[t][r] = svn[t][r];
+      for (int r = 0; r < 4; ++r) d[t][r] = sr[t][r];
+  };
+  f32x4 ns[G::MT_N];
+  float racc[kTailMax];
+  for (int c = 0; c < G::C; ++c) {
+    const float* cw = cur + (c % GG::CPC) * G::GC_G * G::FQ;  // this container's groups
+    float svn[G::MT_N][4];
+    load_row(c + 1, svn);
+    // stagger: the second half of the waves (two per SIMD) starts each
+    // container interval late, so its tanh / argmax VALU phase meets the
+    // first half's MFMAs instead of every wave reaching it together
+    // (one container per chunk only: at H <= 32 it cost the fleet 0.3 %)
+    if (PGP_GAN_SLEEP > 0 && GG::CPC == 1 && wv >= kGanWaves / 2) __builtin_amdgcn_s_sleep(PGP_GAN_SLEEP);
+    gen2(c, cw, ns, racc);
+    finish(c, cw, ns, racc, sv);
+    if ((c + 1) % GG::CPC == 0) advance();
+    copy_row(sv, svn);
   }
 
   // ---- Disc2 + softmax + gate (PreGANPlus.py:87) ----
