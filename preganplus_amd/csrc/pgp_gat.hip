@@ -35,6 +35,9 @@ __device__ __forceinline__ float lrelu001(float e) { return fmaxf(e, 0.01f * e);
 // 16-B stores (scattered 4-B stores amplified the HBM writes 6x:
 // profiles/r01/pmc_r01pmc2_summary.txt).
 // independent accumulation chains of the one-item-per-wave edge loop (H > 32)
+#ifndef PGP_GAT_PF
+#define PGP_GAT_PF 1
+#endif
 #ifndef PGP_GAT_CHAINS
 #define PGP_GAT_CHAINS 2
 #endif
@@ -56,6 +59,21 @@ __global__ __launch_bounds__(256) void gat_agg_kernel(int B, const float* __rest
   const float gu0 = gcp[0], gu1 = gcp[1], gu2 = gcp[2], gv0 = gcp[4], gv1 = gcp[5], gv2 = gcp[6];
   for (int i = threadIdx.x; i < BLK; i += 256) out_lds[i] = 0.f;
   __syncthreads();
+  // P == 1 (H > 32): the next item's features are loaded one item ahead, from a
+  // clamped address (unconditional loads, zeroed when out of range)
+  constexpr bool PF1 = P == 1 && PGP_GAT_PF;
+  auto ldx = [&](int i0, float& x0, float& x1, float& x2) {
+    const int it = i0 + seg;
+    const long b = blk * 16 + it / 3;
+    const bool ok = it < 48 && b < B && hl < H;
+    const float* p = win + (ok ? (b * 3 + it % 3) * 3 * H + 3 * hl : 0);
+    x0 = p[0];
+    x1 = p[1];
+    x2 = p[2];
+    if (!ok) x0 = x1 = x2 = 0.f;
+  };
+  float nx0 = 0.f, nx1 = 0.f, nx2 = 0.f;
+  if constexpr (PF1) ldx(wv * P, nx0, nx1, nx2);
   for (int i0 = wv * P; i0 < 48; i0 += 4 * P) {
     const int it = i0 + seg;
     const int j = it / 3, w = it % 3;
@@ -63,7 +81,12 @@ __global__ __launch_bounds__(256) void gat_agg_kernel(int B, const float* __rest
     const bool active = it < 48 && b < B;
     const bool host = hl < H;
     float x0 = 0.f, x1 = 0.f, x2 = 0.f;
-    if (active && host) {
+    if constexpr (PF1) {
+      x0 = nx0;
+      x1 = nx1;
+      x2 = nx2;
+      ldx(i0 + 4 * P < 48 ? i0 + 4 * P : i0, nx0, nx1, nx2);
+    } else if (active && host) {
       const float* p = win + (b * 3 + w) * 3 * H + 3 * hl;
       x0 = p[0];
       x1 = p[1];
