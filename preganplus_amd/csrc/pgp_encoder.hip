@@ -3,13 +3,19 @@
 // windows per wave.  Output: the encoder activations ("latent",
 // models.py:399) as MFMA B-operand tiles for the decoder GEMM (K2b).
 //
-// Weights stream through a 2-slot LDS ring, shared by the workgroup's 4 waves:
-// while the waves compute stage k from one slot, global_load_lds fills the
-// other with stage k+1 (the per-host weight stream is identical for every host,
-// so it repeats H times per launch and stays L2-resident).  A-operand fragments
-// are read with ds_read_b128 (lane-linear, conflict-free).  Two workgroups per
-// CU (__launch_bounds__(256, 2)) let one block's VALU phases (softmax, LayerNorm)
-// overlap the other's MFMA phases.
+// Weights live in LDS and are read as A-operand fragments with ds_read_b128
+// (lane-linear, conflict-free).  Three modes:
+// * tail-resident (H = 50): the groups the path reads (layer 0's FFN, all of
+//   layer 1) are loaded once into one 8-wave workgroup per CU; each wave takes
+//   an equal contiguous range of the (16-window block, host) units (hosts are
+//   independent here) and prefetches the next unit's raw features through a
+//   per-wave LDS slot; no barrier in the host loop;
+// * resident (H <= 16): both layers' weights in LDS, one 16-window block per
+//   wave, host loop without barriers;
+// * ring (other H): stages stream through a 2-slot LDS ring by
+//   global_load_lds (stage k computed while k + 1 loads), shared by the
+//   workgroup's 4 waves; two workgroups per CU let one block's VALU phases
+//   overlap the other's MFMA phases.
 #include "pgp_device.hpp"
 
 namespace pgp {
