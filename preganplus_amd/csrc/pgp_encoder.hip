@@ -49,6 +49,9 @@ constexpr int kEncWaves = 4;
 #ifndef PGP_ENC16_EU
 #define PGP_ENC16_EU 2
 #endif
+#ifndef PGP_ENC_UNITS16
+#define PGP_ENC_UNITS16 0
+#endif
 // Tail mode (H = 50) resident: the weight groups the tail path reads (layer 0's
 // stage 2 — its q/k/v and out_proj are folded onto the raw features — and all
 // of layer 1: 104 KB at H = 50) stay in LDS for the whole launch, one 8-wave
@@ -79,12 +82,17 @@ constexpr int NW_STAGE() { return enc_waves<H>(); }
 template <int H>
 struct EncLds {
   static constexpr bool TRES = tail_res<H>();
+  // resident modes have no barrier in the host loop: waves can take (block,
+  // host) unit ranges and prefetch through an LDS slot.  At H <= 16 that
+  // measured slower (fleet 1.97 -> 2.00 ms), so PGP_ENC_UNITS16 defaults to 0
+  // there (one block per wave)
   static constexpr int RES0 = TRES ? Geo<H>::st_begin(Geo<H>::NST - 1) : 0;  // layer 0 stage 2
   static constexpr int STREAM = (kLayers * Geo<H>::LAYER_G - RES0) * Geo<H>::FQ;  // floats
   static constexpr bool RESIDENT = TRES || STREAM * 4 <= 32 * 1024;
   static constexpr int SLOT = Geo<H>::SLOT_G * Geo<H>::FQ;
   static constexpr int TAB = Geo<H>::t_size(kMaxProtos);
   static constexpr int TOTAL = (RESIDENT ? STREAM : 2 * SLOT) + TAB;
+  static constexpr bool UNITS = TRES || (RESIDENT && PGP_ENC_UNITS16);
 };
 
 // ReLU as one integer max on the bit pattern (negative floats have negative
@@ -788,7 +796,7 @@ __global__ __launch_bounds__(enc_waves<H>() * 64, H <= 16 ? PGP_ENC16_EU : tail_
   using L = EncLds<H>;
   __shared__ __attribute__((aligned(16))) float smem[L::TOTAL];
   // tail-resident mode: per-wave staging slot of the next unit's raw features
-  __shared__ float xstage[L::TRES ? NW_STAGE<H>() * 144 : 1];
+  __shared__ float xstage[L::UNITS ? NW_STAGE<H>() * 144 : 1];
   float* tab = smem + (L::RESIDENT ? L::STREAM : 2 * L::SLOT);
   const int tsz = G::t_size(a.K);
   for (int i = threadIdx.x; i < tsz; i += blockDim.x) tab[i] = a.tab[i];
@@ -823,11 +831,11 @@ __global__ __launch_bounds__(enc_waves<H>() * 64, H <= 16 ? PGP_ENC16_EU : tail_
     float ba[3];
     // all 3 raw features of every step of this lane's window (layer 0's bilinear scores)
     float xv[3][3];
-    if constexpr (L::TRES) {
+    if constexpr (L::UNITS) {
 #pragma unroll
       for (int w = 0; w < 3; ++w) {
 #pragma unroll
-        for (int f = 0; f < 3; ++f) xv[w][f] = pre[w * 48 + 16 * f + j];
+        for (int f = 0; f < 3; ++f) xv[w][f] = (G::TAIL && PGP_ENC_BILIN) ? pre[w * 48 + 16 * f + j] : 0.f;
         const float v = pre[w * 48 + (lane < 48 ? lane : 47)];
         ba[w] = g < 3 ? v : 0.f;  // feature g of window j
       }
@@ -880,10 +888,10 @@ __global__ __launch_bounds__(enc_waves<H>() * 64, H <= 16 ? PGP_ENC16_EU : tail_
       }
     }
   };
-  if constexpr (L::TRES) {
+  if constexpr (L::UNITS) {
     // no barrier in the host loop: each wave takes an equal contiguous range of
-    // the nblk x H units (one workgroup per CU, grid = CU count), so the launch
-    // has no partial last round of workgroups
+    // the nblk x H units (grid = the workgroups that fit at once: CU count x
+    // occupancy), so the launch has no partial last round of workgroups
     const long U = nblk * H, NWT = (long)gridDim.x * NW, gw = (long)blockIdx.x * NW + wv;
     const long u1 = (gw + 1) * U / NWT;
     // unit u's raw features are agg[u * 144 ..] (144 floats).  The next unit's
@@ -927,7 +935,13 @@ hipError_t launch(const FwdArgs& a, hipStream_t st) {
   const long nblk = (a.B + 15) / 16;
   constexpr int NW = enc_waves<H>();
   long grid = (nblk + NW - 1) / NW;
-  if constexpr (EncLds<H>::TRES) grid = std::min<long>(device_cus(), (nblk * H + NW - 1) / NW);
+  if constexpr (EncLds<H>::UNITS) {
+    static int occ = 0;  // workgroups resident per CU (registers / LDS), queried once
+    if (occ <= 0 && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, encoder_kernel<H>, NW * 64, 0) != hipSuccess ||
+                     occ <= 0))
+      occ = 1;
+    grid = std::min<long>((long)device_cus() * occ, (nblk * H + NW - 1) / NW);
+  }
   encoder_kernel<H><<<(int)grid, NW * 64, 0, st>>>(a);
   return hipGetLastError();
 }
