@@ -745,8 +745,14 @@ PGP_DEV void encoder_layer(f32x4 (&X)[Geo<H>::MT_D][3], Ring<H>& ring, const flo
 #pragma unroll
   for (int mt = 0; mt < G::MT_D; ++mt) {
     const f32x4 bo = ld4(TL + G::TL_BO + 16 * mt + 4 * g);
+    if constexpr (F0) {
 #pragma unroll
-    for (int w = 0; w < 3; ++w) acc[mt][w] = bo + X[mt][w];  // residual folded into the accumulator
+      for (int w = 0; w < 3; ++w) acc[mt][w] = bo + X[mt][w];  // residual folded into the accumulator
+    } else {  // X = layer 0's norm2 x-hat: residual gamma0 * x-hat + (bo + beta0) (packer)
+      const f32x4 g0 = ld4(TL - G::TL_SIZE + G::TL_LN2G + 16 * mt + 4 * g);
+#pragma unroll
+      for (int w = 0; w < 3; ++w) acc[mt][w] = X[mt][w] * g0 + bo;
+    }
   }
   gemm3<G::MT_D, G::KQ_O, G::KS_O, G::TP>(acc, ring.cur, O, lane);
   if constexpr (G::NPASS == 2) {
@@ -786,7 +792,7 @@ PGP_DEV void encoder_layer(f32x4 (&X)[Geo<H>::MT_D][3], Ring<H>& ring, const flo
   }
   gemm3<G::MT_D, G::KQ_F, 16, G::MT_F>(acc, ring.cur, F1, lane);
   ring.advance();
-  layer_norm_tiles<H, F0>(acc, X, TL + G::TL_LN2G, TL + G::TL_LN2B, g);  // layer 1: x-hat (see tail)
+  layer_norm_tiles<H, false>(acc, X, TL + G::TL_LN2G, TL + G::TL_LN2B, g);  // x-hat: both affines folded (see tail)
 }
 
 template <int H>

@@ -396,9 +396,9 @@ PGP_HD void pack_phase2(int K, const Src& src, const Ex& ex, double scale, const
                     n2w = V(O.n2w), n2b = V(O.n2b);
     float* FL = F + G::OFF_ENC + (long)l * G::LAYER_G * G::FQ;
     float* TL = T + G::T_L0 + l * G::TL_SIZE;
-    // tail mode: layer 0's norm2 gamma / beta folded into layer 1's in_proj and
-    // residual (the kernel passes layer 1 x-hat; residual = gamma * x-hat + (bo + beta))
-    const bool fold0 = G::TAIL && l > 0;
+    // layer 0's norm2 gamma / beta folded into layer 1's in_proj and residual
+    // (the kernel passes layer 1 x-hat; residual = gamma * x-hat + (bo + beta))
+    const bool fold0 = l > 0;
     const View<Src> pn2w = V(B.ly[l > 0 ? l - 1 : 0].n2w), pn2b = V(B.ly[l > 0 ? l - 1 : 0].n2b);
     if constexpr (G::TAIL) {
       pack_tail_attention<H>(inW, inB, outW, scale, ex, FL, TL, fold0, pn2w, pn2b);
@@ -414,7 +414,7 @@ PGP_HD void pack_phase2(int K, const Src& src, const Ex& ex, double scale, const
         int hh, e;
         if (s >= G::KS_D || c >= d || !head_row<H>(p, 16 * tp + i, &hh, &e)) return;
         const int sr = m * d + hh * G::HD + e;
-        const double v = inW[(long)sr * d + c] * (m == 0 ? scale : 1.0);
+        const double v = inW[(long)sr * d + c] * (fold0 ? pn2w[c] : 1.0) * (m == 0 ? scale : 1.0);
         FL[(G::P_QKV(p) + (m * G::TP + tp) * G::KQ_D + q4) * G::FQ + lane * 4 + e4] = (float)v;
       });
       ex.par((long)G::NPASS * 3 * G::TP * 16, [&](long idx) {
@@ -423,7 +423,10 @@ PGP_HD void pack_phase2(int K, const Src& src, const Ex& ex, double scale, const
         int hh, e;
         if (!head_row<H>(p, 16 * tp + i, &hh, &e)) return;
         const int sr = m * d + hh * G::HD + e;
-        TL[G::TL_QKV + (p * 3 + m) * G::TP * 16 + 16 * tp + i] = (float)(inB[sr] * (m == 0 ? scale : 1.0));
+        double bb = inB[sr];
+        if (fold0)
+          for (int c = 0; c < d; ++c) bb += inW[(long)sr * d + c] * pn2b[c];
+        TL[G::TL_QKV + (p * 3 + m) * G::TP * 16 + 16 * tp + i] = (float)(bb * (m == 0 ? scale : 1.0));
       });
       // out_proj
       ex.par((long)G::NPASS * G::MT_D * G::KQ_O * 256, [&](long idx) {
