@@ -60,7 +60,6 @@ struct GanGeo {
   }
   static constexpr int CPC = cpc();
   static constexpr int NCHUNK = 1 + NQC + G::C / CPC;
-  static constexpr int NSLOT = 2;
   static constexpr int mx(int x, int y) { return x > y ? x : y; }
   static constexpr int SLOT_G = mx(G::GE_G, mx(kQC * G::GS_G, CPC * G::GC_G));
   static constexpr int SLOT = SLOT_G * G::FQ;
@@ -84,7 +83,7 @@ template <int H>
 __global__ __launch_bounds__(kGanWaves * 64) void gan_kernel(FwdArgs a) {
   using G = Geo<H>;
   using GG = GanGeo<H>;
-  __shared__ __attribute__((aligned(16))) float smem[GG::NSLOT * GG::SLOT];
+  __shared__ __attribute__((aligned(16))) float smem[2 * GG::SLOT];
   const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const long blk = (long)blockIdx.x * kGanWaves + wv;
@@ -95,9 +94,6 @@ __global__ __launch_bounds__(kGanWaves * 64) void gan_kernel(FwdArgs a) {
   const float* ew = a.emb + (valid ? b : 0) * G::EP;
   const float* gt = a.gtab;
 
-  // ring: chunk k lives in slot k % NSLOT; chunk k + 1 is loaded while chunk k
-  // is computed (with 3 slots, chunk k - 1 also stays resident)
-  auto slot = [&](int k) { return smem + (k % GG::NSLOT) * GG::SLOT; };
   float* cur = smem;
   float* nxt = smem + GG::SLOT;
   int next = 1;
@@ -117,9 +113,10 @@ __global__ __launch_bounds__(kGanWaves * 64) void gan_kernel(FwdArgs a) {
   };
   auto advance = [&]() {
     __syncthreads();
+    float* t = cur;
     cur = nxt;
+    nxt = t;
     ++next;
-    nxt = slot(next);
     issue();
   };
 

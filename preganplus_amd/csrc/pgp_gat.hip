@@ -34,7 +34,8 @@ __device__ __forceinline__ float lrelu001(float e) { return fmaxf(e, 0.01f * e);
 // aggregation [H][3][48] is assembled in LDS and written out with contiguous
 // 16-B stores (scattered 4-B stores amplified the HBM writes 6x:
 // profiles/r01/pmc_r01pmc2_summary.txt).
-// independent accumulation chains of the one-item-per-wave edge loop (H > 32)
+// one-item-per-wave mode (H > 32): load the next item's features one item
+// ahead (PGP_GAT_PF), and the edge loop's independent accumulation chains
 #ifndef PGP_GAT_PF
 #define PGP_GAT_PF 1
 #endif
