@@ -179,7 +179,9 @@ def test_full_size_census(H, B):
     else:
         w = W.synth_weights(H, seed=0)
     m = get_model(H, w, f"full{H}")
-    x, s = _c2_torch(B, H, seed=31 + H)
+    # PGP_CENSUS_SEED: the same census over another seeded input draw (one-off runs)
+    seed = int(os.environ.get("PGP_CENSUS_SEED", 31 + H))
+    x, s = _c2_torch(B, H, seed=seed)
     full = to_numpy(m.forward(x, s))
     torch.cuda.synchronize()
     for lo, hi in ((0, 64), (B // 2 - 7, B // 2 + 50), (B - 45, B)):
@@ -196,10 +198,11 @@ def test_full_size_census(H, B):
     sidx = s.argmax(dim=-1).cpu().numpy()
     del x, s
     st, worst = CE.run(w, x32, sidx, full, log=print)
-    res = {"H": H, "windows": B, "census": st, "worst_error_over_tolerance": worst}
+    res = {"H": H, "windows": B, "seed": seed, "census": st, "worst_error_over_tolerance": worst}
     print("CENSUS", json.dumps(res))
     os.makedirs("gpurun_out", exist_ok=True)
-    with open(f"gpurun_out/census_h{H}_b{B}.json", "w") as f:
+    tag = "" if "PGP_CENSUS_SEED" not in os.environ else f"_s{seed}"
+    with open(f"gpurun_out/census_h{H}_b{B}{tag}.json", "w") as f:
         json.dump(res, f, indent=1)
     assert worst["logits"] <= 1.0 and worst["protos"] <= 1.0 and worst["probs"] <= 1.0, worst
     assert not DB.violations(st), st
