@@ -3,6 +3,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <string>
 
 #include "pgp_layout.hpp"
@@ -17,15 +18,15 @@ constexpr int kMaxProtos = 64;
 // compute units of the current device (cached per device id): grids of
 // one-workgroup-per-CU kernels
 inline int device_cus() {
-  static int cached[64] = {0};
+  static std::atomic<int> cached[64];  // zero-initialised (static storage)
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-  if (cached[dev] == 0) {
-    int n = 0;
+  int n = cached[dev].load(std::memory_order_relaxed);
+  if (n == 0) {
     if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-    cached[dev] = n;
+    cached[dev].store(n, std::memory_order_relaxed);
   }
-  return cached[dev];
+  return n;
 }
 
 // Kernel arguments shared by the launches of one forward call.

@@ -942,10 +942,13 @@ hipError_t launch(const FwdArgs& a, hipStream_t st) {
   constexpr int NW = enc_waves<H>();
   long grid = (nblk + NW - 1) / NW;
   if constexpr (EncLds<H>::UNITS) {
-    static int occ = 0;  // workgroups resident per CU (registers / LDS), queried once
-    if (occ <= 0 && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, encoder_kernel<H>, NW * 64, 0) != hipSuccess ||
-                     occ <= 0))
-      occ = 1;
+    static std::atomic<int> occ_cache{0};  // workgroups resident per CU (registers / LDS), queried once
+    int occ = occ_cache.load(std::memory_order_relaxed);
+    if (occ <= 0) {
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, encoder_kernel<H>, NW * 64, 0) != hipSuccess || occ <= 0)
+        occ = 1;
+      occ_cache.store(occ, std::memory_order_relaxed);
+    }
     grid = std::min<long>((long)device_cus() * occ, (nblk * H + NW - 1) / NW);
   }
   encoder_kernel<H><<<(int)grid, NW * 64, 0, st>>>(a);
