@@ -63,11 +63,22 @@ __global__ __launch_bounds__(kDecWaves * 64, H <= 16 ? 8 : 1) void decoder_kerne
   dma_groups(wdec, cur, SG, wv, kDecWaves, lane);
   // latent B operands one slot (CPS chunks) ahead: at small H a single chunk is
   // too little work to cover the HBM latency of the next one
+  // chunk c's B operands (the latent layout of pgp_layout.hpp LAT_FG: 16-byte
+  // loads for the full groups of 4 k-steps)
+  auto load_b = [&](int c, bool ok, float (&v)[G::KS_D]) {
+    const float* lc = lat + (long)c * G::KS_D * 64;
+#pragma unroll
+    for (int q = 0; q < G::LAT_FG; ++q) {
+      const f32x4 t = ok ? ld4(lc + q * 256 + lane * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[4 * q + e] = t[e];
+    }
+#pragma unroll
+    for (int r = 0; r < G::KS_D % 4; ++r) v[4 * G::LAT_FG + r] = ok ? lc[G::LAT_FG * 256 + r * 64 + lane] : 0.f;
+  };
   float b[CPS][G::KS_D];
 #pragma unroll
-  for (int u = 0; u < CPS; ++u)
-#pragma unroll
-    for (int s = 0; s < G::KS_D; ++s) b[u][s] = active ? lat[(u * G::KS_D + s) * 64 + lane] : 0.f;
+  for (int u = 0; u < CPS; ++u) load_b(u, active, b[u]);
   __syncthreads();
   if (CPS < NCH) dma_groups(wdec + (long)SG * G::FQ, nxt, SG, wv, kDecWaves, lane);
 
@@ -87,9 +98,7 @@ __global__ __launch_bounds__(kDecWaves * 64, H <= 16 ? 8 : 1) void decoder_kerne
     float bn[CPS][G::KS_D];
     const bool pre = active && (c0 + CPS < NCH);
 #pragma unroll
-    for (int u = 0; u < CPS; ++u)
-#pragma unroll
-      for (int s = 0; s < G::KS_D; ++s) bn[u][s] = pre ? lat[((c0 + CPS + u) * G::KS_D + s) * 64 + lane] : 0.f;
+    for (int u = 0; u < CPS; ++u) load_b(c0 + CPS + u, pre, bn[u]);
 #pragma unroll
     for (int sub = 0; sub < CPS; ++sub) {
       const float* A = cur + sub * G::DEC_G * G::FQ;

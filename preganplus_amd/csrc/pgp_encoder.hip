@@ -872,9 +872,17 @@ __global__ __launch_bounds__(enc_waves<H>() * 64, H <= 16 ? PGP_ENC16_EU : tail_
 
     if (active) {
 #pragma unroll
-      for (int w = 0; w < 3; ++w)
+      for (int w = 0; w < 3; ++w) {
+        // chunk (h, w): full groups of 4 k-steps as one 16-byte store per lane,
+        // the remaining k-steps one dword each (pgp_layout.hpp, LAT_FG)
+        float* lc = lat + (long)((h * 3 + w) * G::KS_D) * 64;
 #pragma unroll
-        for (int s = 0; s < G::KS_D; ++s) lat[((h * 3 + w) * G::KS_D + s) * 64 + lane] = X[s / 4][w][s % 4];
+        for (int q = 0; q < G::LAT_FG; ++q) *reinterpret_cast<f32x4*>(lc + q * 256 + lane * 4) = X[q][w];
+        if constexpr (G::KS_D % 4 != 0) {
+#pragma unroll
+          for (int r = 0; r < G::KS_D % 4; ++r) lc[G::LAT_FG * 256 + r * 64 + lane] = X[G::LAT_FG][w][r];
+        }
+      }
       if (a.latent != nullptr) {
         const long b = blk * 16 + j;
         if (b < a.B) {

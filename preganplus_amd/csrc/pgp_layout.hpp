@@ -139,6 +139,10 @@ struct Geo {
   // latent workspace (encoder -> decoder): per 16-window block
   //   [H][3][KS_D][64]: X tile registers as the decoder's B operand
   static constexpr long LAT_BLK = (long)H * kWindow * KS_D * 64;
+  // within a (host, step) chunk of KS_D x 64 floats: LAT_FG full groups of 4
+  // k-steps stored [group][lane][4] (16 B per lane), then the KS_D - 4 LAT_FG
+  // remaining k-steps [k][lane]
+  static constexpr int LAT_FG = KS_D / 4;
 
   // ---------------- encoder/decoder tables (staged into LDS) ----------------
   static constexpr int T_TEW = 0;                   // [MT_D][64] time-encoder A fragments (K=4)
