@@ -4,7 +4,7 @@ One step = detect + diagnose + generate over one batch of synthetic windows
 already resident in HBM: K1 GAT aggregation -> K2 encoder -> K2b decoders +
 classify -> K3 Gen+Disc+decision tensors -> K5 per-container moves
 (libpreganplus.so).  Multi-GPU: one process per GPU
-(torchrun); every rank processes its own batch of independent windows (weak
+(torchrun, or `--gpus N` starting N ranks itself); every rank processes its own batch of independent windows (weak
 scaling, no data-path collective); timing is max over ranks.
 
 Prints ONE JSON line (rank 0).  The roofline object is for the dominant kernel
@@ -70,9 +70,28 @@ def load_traffic(H, B, kernel="encoder"):
         return None
 
 
+def launch_ranks(n, argv=None):
+    """`python bench.py --gpus N` without a torchrun environment: start N ranks,
+    one process per GPU, as a CHILD `torch.distributed.run` (the driver's own
+    launch form; 127.0.0.1 rendezvous on a free port) and return its exit
+    code.  Called before anything touches the GPU (no re-exec of this process:
+    the parent only waits)."""
+    import socket
+    import subprocess
+    argv = sys.argv[1:] if argv is None else list(argv)
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + argv
+    log(f"launching {n} ranks: {' '.join(cmd[1:])}")
+    return subprocess.call(cmd, env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0"))
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1, help="ranks (one process per GPU); without a torchrun "
+                                                          "environment, N > 1 starts N ranks itself")
     ap.add_argument("--steps", type=int, default=300)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--hosts", type=int, default=50)
@@ -80,14 +99,24 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-gan", action="store_true", help="tune config: Transformer tuning step only")
-    ap.add_argument("--config", choices=["c2", "fleet", "tune", "fpe", "gobi", "sim", "loop", "plugin"], default="c2",
+    ap.add_argument("--config", choices=["c2", "fleet", "tune", "fpe", "gobi", "sim", "loop", "plugin", "ranks"],
+                    default="c2",
                     help="c2: BASELINE config 2 (default, the headline line); fleet: config 5 "
                          "(1024-host fleet = 64 cells of 16 hosts, shipped weights); tune: config 3 "
                          "(tuning step fwd+bwd+AdamW, data-parallel with an RCCL all-reduce); fpe: config 4 "
                          "(PreGAN FPE_16 encoder + K=3 classifier + PreGAN's Gen/Disc, shipped weights); "
                          "gobi: SURVEY 8f row f3, the schedule producer (GOBI's opt() over the "
-                         "energy_latency_16 surrogate, a batch of independent environments)")
+                         "energy_latency_16 surrogate, a batch of independent environments); ranks: the "
+                         "launcher / rendezvous check alone (one all-reduce of ones)")
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
+    global _GPUS_REQUESTED
+    _GPUS_REQUESTED = args.gpus
+    if args.config == "ranks":
+        return bench_ranks(args)
     if args.config == "fleet":
         return bench_fleet(args)
     if args.config == "tune":
@@ -200,7 +229,9 @@ def main():
                          "io_bytes_per_window": R.encoder_io_bytes_per_window(H)},
             "path_roofline": {
                 "flops_per_window": R.total_flops_per_window(H),
-                "achieved_tflops": R.total_flops_per_window(H) * B * world * args.steps / elapsed / 1e12,
+                # the reference formulation's flops over the step time: NOT a roofline rate (the
+                # kernels execute fewer flops than this, DESIGN §3 folds; it may exceed the peak)
+                "algorithmic_rate_tflops": R.total_flops_per_window(H) * B * world * args.steps / elapsed / 1e12,
                 "hbm_algorithmic_gbs": path_bytes * world * args.steps / elapsed / 1e9,
                 "hbm_frac": path_bytes * world * args.steps / elapsed / 1e9 / R.PEAK_HBM_GBS,
                 "traffic_per_step": (None if None in k_traffic.values() else sum(k_traffic.values())),
@@ -213,29 +244,63 @@ def main():
             res["cpu_baseline"] = cpu_baseline(weights, x, s)
         else:
             res["cpu_baseline"] = None
-        print(json.dumps(res), flush=True)
+        emit(res)
     if world > 1:
         torch.distributed.destroy_process_group()
 
 
+_RANKS_SEEN = 1
+_GPUS_REQUESTED = 1
+
+
 def _dist_setup():
-    """One process per GPU (torchrun env).  Rehearsal knobs for a 1-GPU box:
-    PGP_DIST_BACKEND=gloo and PGP_DEVICE=0 put every rank on that GPU
-    (RCCL refuses two ranks on one device); the driver's runs use neither."""
+    """One process per GPU (torchrun env, or the ranks launch_ranks started).
+    The world size must equal --gpus (fail loudly otherwise), and every rank
+    takes part in one all-reduce of ones whose sum is reported as
+    `ranks_seen`.  Rehearsal knobs for a 1-GPU box: PGP_DIST_BACKEND=gloo and
+    PGP_DEVICE=0 put every rank on that GPU (RCCL refuses two ranks on one
+    device); PGP_DEVICE=cpu runs the rendezvous check (--config ranks) with no
+    GPU at all.  The driver's runs use neither."""
+    global _RANKS_SEEN
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("PGP_DEVICE", os.environ.get("LOCAL_RANK", "0")))
+    if world != _GPUS_REQUESTED:
+        raise SystemExit(f"bench.py: world size {world} != --gpus {_GPUS_REQUESTED}")
+    dev_env = os.environ.get("PGP_DEVICE", os.environ.get("LOCAL_RANK", "0"))
+    if dev_env == "cpu":
+        device = torch.device("cpu")
+    else:
+        device = torch.device("cuda", int(dev_env))
+        torch.cuda.set_device(device)
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
         backend = os.environ.get("PGP_DIST_BACKEND", "nccl")
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group("nccl", device_id=device)
         else:
             dist.init_process_group(backend)
-    device = torch.device("cuda", local)
-    torch.cuda.set_device(device)
+        ones = torch.ones(1, dtype=torch.float32, device=device)
+        dist.all_reduce(ones)
+        _RANKS_SEEN = int(round(float(ones.item())))
+        if _RANKS_SEEN != world:
+            raise SystemExit(f"bench.py: all-reduce of ones saw {_RANKS_SEEN} ranks, world size {world}")
     return world, rank, device
+
+
+def emit(res):
+    """Rank 0's one JSON line, with the rendezvous count."""
+    res["ranks_seen"] = _RANKS_SEEN
+    print(json.dumps(res), flush=True)
+
+
+def bench_ranks(args):
+    """The launcher / rendezvous alone: N ranks, one all-reduce of ones."""
+    world, rank, device = _dist_setup()
+    if rank == 0:
+        emit({"metric": "ranks", "value": world, "unit": "ranks", "n_gpus": world, "device": str(device),
+              "backend": os.environ.get("PGP_DIST_BACKEND", "nccl") if world > 1 else None})
+    if world > 1:
+        torch.distributed.destroy_process_group()
 
 
 def _timed(world, device, fn, steps):
@@ -285,7 +350,7 @@ def bench_fleet(args):
         if world == 1 and not args.no_cpu_baseline:
             log("timing CPU baseline ...")
             res["cpu_baseline"] = cpu_baseline(w, x, s, per_window_n=64, batch_n=4096)
-        print(json.dumps(res), flush=True)
+        emit(res)
     if world > 1:
         torch.distributed.destroy_process_group()
 
@@ -345,9 +410,11 @@ def bench_tune(args):
     gan_target = torch.empty((E, 2), dtype=torch.float32, device=device)
     bufs = TR.dataset_buffers(tr, E, R)
     names = ("dataset", "detect", "train_gan", "tune_model")
+    subs = TR.DPTuner.SUBSTAGES
     ev = [[torch.cuda.Event(enable_timing=True) for _ in range(len(names) + 1)] for _ in range(max(args.steps, 1))]
+    sev = [[torch.cuda.Event(enable_timing=True) for _ in range(len(subs) + 1)] for _ in range(max(args.steps, 1))]
 
-    def step(e=None):
+    def step(e=None, se=None):
         rec = (lambda k: e[k].record()) if e is not None else (lambda k: None)
         rec(0)
         wins, y, cls, inf = TR.tune_dataset(tr, series, tmax, out=bufs)
@@ -357,14 +424,15 @@ def bench_tune(args):
         rec(2)
         TR.train_gan_batched(tr, sim, envs, emb, s, out=sim_out, target=gan_target, all_reduce=True)
         rec(3)
-        tun.step(wins, y, cls)
+        tun.step(wins, y, cls, mark=(lambda k: se[k].record()) if se is not None else None)
         rec(4)
 
     for _ in range(args.warmup):
         step()
-    it = iter(ev)
-    el = _timed(world, device, lambda: step(next(it)), args.steps)
+    it = iter(zip(ev, sev))
+    el = _timed(world, device, lambda: step(*next(it)), args.steps)
     stage = np.array([[e[k].elapsed_time(e[k + 1]) for k in range(len(names))] for e in ev[:args.steps]]).mean(0)
+    sub = np.array([[e[k].elapsed_time(e[k + 1]) for k in range(len(subs))] for e in sev[:args.steps]]).mean(0)
     if rank == 0:
         res = {
             "metric": "tuning windows/sec (semi-supervised step: dataset + detect + train_gan + DP tune_model)",
@@ -378,11 +446,13 @@ def bench_tune(args):
                                    f"= {B} tuning windows per GPU", "hosts": H, "environments_per_gpu": E,
                        "windows_per_gpu": B, "parallelism": f"dp{world} + RCCL all-reduce (grads, state)"},
             "stage_ms": {n: float(stage[k]) for k, n in enumerate(names)},
+            "tune_model_ms": {n: float(sub[k]) for k, n in enumerate(subs)},
+            "grad_all_reduce_ms": float(sub[subs.index("all_reduce")]),
         }
         if world == 1 and not args.no_cpu_baseline:
             log("timing CPU baseline ...")
             res["cpu_baseline"] = tune_cpu_baseline(w, series_h, tmax_h, s.cpu().numpy(), SIM.synth_envs(4, H, 5), H)
-        print(json.dumps(res), flush=True)
+        emit(res)
     if world > 1:
         torch.distributed.destroy_process_group()
 
@@ -523,7 +593,7 @@ def bench_fpe(args):
             res["cpu_baseline"] = fpe_cpu_baseline(w, args.cpu_budget)
         else:
             res["cpu_baseline"] = None
-        print(json.dumps(res), flush=True)
+        emit(res)
     if world > 1:
         torch.distributed.destroy_process_group()
 
@@ -556,7 +626,7 @@ def bench_gobi(args):
             "data": "inits = the reference's scheduling dataset rows + synthetic (tests/golden/gobi_h16.npz)",
             "config": {"workload": f"f3: GOBI, {E} independent 16-host environments per GPU", "hosts": 16,
                        "environments_per_gpu": E, "mean_iterations": its, "parallelism": f"dp{world}"},
-            "achieved_tflops": 2 * macs_it * (its + 2) * E / (el / args.steps) / 1e12,
+            "algorithmic_rate_tflops": 2 * macs_it * (its + 2) * E / (el / args.steps) / 1e12,
         }
         if world == 1 and not args.no_cpu_baseline:
             from oracle import gobi_oracle as GO  # CPU baseline leg only
@@ -570,7 +640,7 @@ def bench_gobi(args):
             res["cpu_baseline"] = {"value": n / dt, "unit": "schedules/s", "cores": 1, "kind": "port",
                                    "sample": f"{n} opt() runs of the torch-CPU restatement (bit-identical to the "
                                              f"reference's), 1 thread, {dt:.1f}s"}
-        print(json.dumps(res), flush=True)
+        emit(res)
     if world > 1:
         torch.distributed.destroy_process_group()
 
@@ -626,7 +696,7 @@ def bench_sim(args):
             res["cpu_baseline"] = {"value": n / dt, "unit": "environments/s", "cores": 1, "kind": "port",
                                    "sample": f"{n} environments through the Python restatement (bit-identical to "
                                              f"the reference's runSimulation), 1 thread, {dt:.1f}s"}
-        print(json.dumps(res), flush=True)
+        emit(res)
     if world > 1:
         torch.distributed.destroy_process_group()
 
@@ -734,7 +804,7 @@ def bench_loop(args):
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = loop_cpu_baseline(w, extra, inits_h, x.cpu().numpy(), envs_h,
                                                     y.cpu().numpy(), args.cpu_budget)
-        print(json.dumps(res), flush=True)
+        emit(res)
     if world > 1:
         torch.distributed.destroy_process_group()
 
@@ -915,7 +985,7 @@ def bench_plugin(args):
             res["cpu_baseline"] = {"value": n / dt, "unit": "calls/s", "cores": 1, "kind": "port",
                                    "sample": f"{n} run_model calls of the torch-fp64 plugin restatement "
                                              f"(pinned to the reference's outputs), 1 thread, {dt:.1f}s"}
-        print(json.dumps(res), flush=True)
+        emit(res)
 
 
 if __name__ == "__main__":

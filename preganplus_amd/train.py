@@ -626,9 +626,14 @@ class DPTuner:
                 tab[i, k] = (1.0, lr / (1 - tr.b1 ** stp), math.sqrt(1 - tr.b2 ** stp))
         self.table.copy_(torch.from_numpy(tab).pin_memory(), non_blocking=True)
 
-    def step(self, wins: torch.Tensor, y: torch.Tensor, cls: torch.Tensor):
+    SUBSTAGES = ("forward", "targets", "backward", "all_reduce", "apply_adamw")
+
+    def step(self, wins: torch.Tensor, y: torch.Tensor, cls: torch.Tensor, mark=None):
         """wins [B,3,3H] fp32, y / cls [B,H] int32, all on the device.
-        Returns the per-window (aloss, tloss) [B,2] fp64 device view."""
+        Returns the per-window (aloss, tloss) [B,2] fp64 device view.
+        ``mark(k)``, if given, is called before sub-stage k of SUBSTAGES and
+        once more at the end (the bench records HIP events there)."""
+        mark = mark or (lambda k: None)
         import torch.distributed as dist
         tr, L = self.tr, self.tr._L
         B = wins.shape[0]
@@ -640,21 +645,27 @@ class DPTuner:
         if i == 0:
             self._fill_table()
         s = tr._stream()
+        mark(0)
         tr.tune_forward(wins)
+        mark(1)
         _native.check(L.pgp_tune_targets_dp(
             tr.H, self.K, B, tr.logits.data_ptr(), tr.protos.data_ptr(), y.data_ptr(), cls.data_ptr(),
             self.state.data_ptr(), PROTO_UPDATE_MIN, self.mult.data_ptr(), self.tgt.data_ptr(), self.loss.data_ptr(),
             self.inc.data_ptr(), self.ws.data_ptr(), s), "pgp_tune_targets_dp")
+        mark(2)
         tr.tune_backward(B, y, self.mult[:B], self.tgt[:B])
+        mark(3)
         tr.all_reduce_grads("transformer", self.group)
         if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
             dist.all_reduce(self.inc, group=self.group)
+        mark(4)
         row = self.table[i]
         _native.check(L.pgp_tune_state_apply(
             self.K, self.state.data_ptr(), self.inc.data_ptr(), PROTO_FACTOR_DECAY, len(self.cond), self.cond_rows,
             self.cond_steps.data_ptr(), row.data_ptr(), tr.lrs["transformer"], tr.b1, tr.b2, s),
             "pgp_tune_state_apply")
         tr.adam_step_table("transformer", self.sel, row)
+        mark(5)
         self.n += 1
         return self.loss[:B]
 

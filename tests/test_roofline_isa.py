@@ -1,0 +1,33 @@
+"""The executed-work roofline constant must match the BUILT library: the
+v_mfma count per host and wave of encoder_kernel<H> in
+preganplus_amd/_lib/libpreganplus.so (unbundled and disassembled offline by
+tools/isa_count.py) equals roofline.ENC_MFMA_PER_HOST[H], so a K2 change that
+moves the MFMA count fails here instead of silently corrupting bench.py's
+`roofline.frac`."""
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+from preganplus_amd import roofline as R  # noqa: E402
+
+LIB = os.path.join(ROOT, "preganplus_amd", "_lib", "libpreganplus.so")
+
+
+@pytest.mark.skipif(not os.path.exists(LIB) or not os.path.exists("/opt/rocm/lib/llvm/bin/llvm-objdump"),
+                    reason="built library / llvm-objdump absent")
+def test_encoder_mfma_count_matches_built_library():
+    import isa_count
+    counts = isa_count.encoder_counts(tuple(R.ENC_MFMA_PER_HOST))
+    for H, n in R.ENC_MFMA_PER_HOST.items():
+        assert counts[H][0] == n, f"H={H}: built library issues {counts[H][0]} MFMAs per host, roofline says {n}"
+
+
+def test_executed_rate_cannot_exceed_peak_definition():
+    # executed flops per window are what K2 issues; the reference formulation's
+    # count is reported separately as an algorithmic rate
+    for H in R.ENC_MFMA_PER_HOST:
+        assert R.encoder_executed_flops_per_window(H) == R.ENC_MFMA_PER_HOST[H] * 2048 * H / 16
