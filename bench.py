@@ -891,7 +891,8 @@ def bench_plugin(args):
     train_gan, tune_model (10 sequential windows), recover_decision.  The
     environment replays the reference-recorded intervals of
     tests/golden/plugin_h16.npz (runSimulation returns the recorded scores).
-    Checkpoint writes and plotting are off on both sides.  The CPU baseline is
+    The Gen / Disc checkpoints are rewritten every call (save_gan, on a writer
+    thread); plotting is off.  The CPU baseline is
     the torch-fp64 restatement of the same call (oracle/pregan_train_oracle.py
     PluginOracle, pinned to the reference's own outputs)."""
     from preganplus_amd.recovery import PreGANPlusRecovery
@@ -900,7 +901,10 @@ def bench_plugin(args):
     zf = np.load(os.path.join(ROOT, "tests", "golden", "plugin_h16.npz"))
     z = _NpzDict({k: zf[k] for k in zf.files})      # decompressed once: the env is the caller's, not timed
     tr_time = extra["train_time_data"]
-    rec = PreGANPlusRecovery(16, "", training=True, weights=w, extra=extra, device=device)
+    import tempfile
+    ckdir = tempfile.mkdtemp(prefix="pgp_save_gan_")
+    # save_gan on, as in the reference (Gen / Disc checkpoints rewritten every call, PreGANPlus.py:76-81)
+    rec = PreGANPlusRecovery(16, "", training=True, weights=w, extra=extra, device=device, save_folder=ckdir)
 
     def prepare(k):
         step = k % 4
@@ -962,6 +966,7 @@ def bench_plugin(args):
     torch.cuda.synchronize()
     fwd_ms = (time.perf_counter() - t0) / 50 * 1e3
     ms = float(np.median(lat) * 1e3)
+    rec.flush_checkpoints()
     if rank == 0:
         res = {"metric": "plugin run_model calls/sec (H=16, train_gan + tune_model + decision)", "value": 1e3 / ms,
                "unit": "calls/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
@@ -971,7 +976,8 @@ def bench_plugin(args):
                           "hosts": 16, "tuning_windows": 10},
                "latency_ms": {"run_model_median": ms, "run_model_p90": float(np.percentile(lat, 90) * 1e3),
                               "forward_batch1": fwd_ms},
-               "stages_ms": stage_ms}
+               "stages_ms": stage_ms,
+               "save_gan": {"on": rec.save_gan, "files": sorted(os.listdir(ckdir))}}
         if not args.no_cpu_baseline:
             from oracle import pregan_train_oracle as TO  # CPU baseline leg only
             torch.set_num_threads(1)

@@ -15,9 +15,6 @@ namespace pgp {
 namespace {
 
 constexpr int kDecWaves = 16;
-#ifndef PGP_DEC_TAIL
-#define PGP_DEC_TAIL 0
-#endif
 
 // CPS (host, step) chunks per ring slot: at small H one chunk is only a few
 // groups (4 KB, 16 MFMAs per wave at H = 16), so a barrier per chunk dominated;
@@ -85,13 +82,7 @@ __global__ __launch_bounds__(kDecWaves * 64, H <= 16 ? 8 : 1) void decoder_kerne
   f32x4 acc[G::MT_O];
 #pragma unroll
   for (int mt = 0; mt < G::MT_O; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // tail rows: a last output tile with NTR <= 8 real rows (H = 50: hosts 48, 49)
-  // as VALU dot products over each lane group's k-steps, summed across groups once
-  // after the K loop, instead of one MFMA per k-step
-  constexpr int NTR = 4 * (H - 4 * (G::MT_O - 1));
-  constexpr bool TAIL = PGP_DEC_TAIL && G::MT_O > 1 && NTR <= 8;
-  constexpr int MTM = TAIL ? G::MT_O - 1 : G::MT_O;  // output tiles on MFMA
-  float racc[8] = {};
+  constexpr int MTM = G::MT_O;  // output tiles (the VALU tail-row form spilled: DESIGN §12)
 
 #pragma unroll 1
   for (int c0 = 0; c0 < NCH; c0 += CPS) {
@@ -122,15 +113,6 @@ __global__ __launch_bounds__(kDecWaves * 64, H <= 16 ? 8 : 1) void decoder_kerne
               for (int i = 0; i < MH; ++i)
                 if (m0 + i < MTM) acc[m0 + i] = mfma(av[i][e], b[sub][4 * q4 + e], acc[m0 + i]);
         }
-        if (TAIL) {  // row r of the last tile: its A fragment column sits on lane 16g + r
-#pragma unroll
-          for (int r = 0; r < NTR; ++r) {
-            const f32x4 rw = ld4(A + (MTM * G::KQ_D + q4) * 256 + (16 * g + r) * 4);
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-              if (4 * q4 + e < G::KS_D) racc[r] = fmaf(rw[e], b[sub][4 * q4 + e], racc[r]);
-          }
-        }
       }
     }
 #pragma unroll
@@ -142,19 +124,6 @@ __global__ __launch_bounds__(kDecWaves * 64, H <= 16 ? 8 : 1) void decoder_kerne
     cur = nxt;
     nxt = t;
     if (c0 + 2 * CPS < NCH) dma_groups(wdec + (long)(c0 + 2 * CPS) * G::DEC_G * G::FQ, nxt, SG, wv, kDecWaves, lane);
-  }
-
-  if (TAIL) {  // lane group g takes rows 4g + {0..3} of the summed tail rows
-    float tv[8];
-#pragma unroll
-    for (int r = 0; r < NTR; ++r) tv[r] = xsum(racc[r], true);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      float v = 0.f;
-#pragma unroll
-      for (int q = 0; q * 4 + r < NTR; ++q) v = (g == q) ? tv[4 * q + r] : v;
-      acc[MTM][r] = v;
-    }
   }
 
   // ---- epilogue: bias, sigmoid, detect, embed, classify ----

@@ -21,24 +21,11 @@
 namespace pgp {
 namespace {
 
-// Timing-study switches (default 0; they change the numerics and exist only to
-// measure how much of K2's time each VALU phase costs): PGP_EXP_NO_LN
-// skips the LayerNorms, PGP_EXP_NO_SOFTMAX the tail-mode scores + softmax
-// (P = 1/3), PGP_EXP_NO_ROWS the tail-mode VALU rows.
 // Tail mode, layer 0: attention scores as bilinear forms of the 3 raw features
 // per step (q, k affine in them; pgp_pack.cpp T_F0S): lane-local FMAs instead of
 // q / k tiles, partial dot products and cross-lane sums
 #ifndef PGP_ENC_BILIN
 #define PGP_ENC_BILIN 1
-#endif
-#ifndef PGP_EXP_NO_LN
-#define PGP_EXP_NO_LN 0
-#endif
-#ifndef PGP_EXP_NO_SOFTMAX
-#define PGP_EXP_NO_SOFTMAX 0
-#endif
-#ifndef PGP_EXP_NO_ROWS
-#define PGP_EXP_NO_ROWS 0
 #endif
 constexpr int kEncWaves = 4;
 // H <= 16 (weights LDS-resident): ENC16_WAVES waves per workgroup share one LDS
@@ -167,7 +154,7 @@ PGP_DEV void gemm3_rows(f32x4 (&acc)[NMA][3], const float* A, const f32x4 (&Bx)[
 #pragma unroll
           for (int w = 0; w < 3; ++w) {
             acc[m][w] = mfma(a[e], Bx[q4][w][e], acc[m][w]);
-            if (m == 0 && !PGP_EXP_NO_ROWS) {
+            if (m == 0) {
 #pragma unroll
               for (int n = 0; n < NR; ++n) racc[n][w] = fmaf(rw[n][e], Bx[q4][w][e], racc[n][w]);
             }
@@ -205,12 +192,6 @@ PGP_DEV void zero_rows(float (&r)[NR][3]) {
     for (int w = 0; w < 3; ++w) r[n][w] = 0.f;
 }
 
-#ifndef PGP_LN_FMA
-#define PGP_LN_FMA 1
-#endif
-#ifndef PGP_LN_ONEPASS
-#define PGP_LN_ONEPASS 1
-#endif
 // AFFINE = false (norm1): X = x-hat; gamma / beta are folded into linear1 and
 // linear2's bias by the packer, and the residual is formed as x-hat*gamma + b2'
 template <int H, bool AFFINE = true>
@@ -218,14 +199,6 @@ PGP_DEV void layer_norm_tiles(f32x4 (&acc)[Geo<H>::MT_D][3], f32x4 (&X)[Geo<H>::
                               const float* bet, int g) {
   using G = Geo<H>;
   constexpr float invH = 1.0f / (float)H;
-  if constexpr (PGP_EXP_NO_LN) {
-#pragma unroll
-    for (int mt = 0; mt < G::MT_D; ++mt)
-#pragma unroll
-      for (int w = 0; w < 3; ++w) X[mt][w] = acc[mt][w];
-    return;
-  }
-#if PGP_LN_ONEPASS
   // one pass: sum and sum of squares of each step reduced together (xsum2).
   // Padded feature rows hold exact zeros here, so no mask is needed.
   // var = E[x^2] - mean^2 (LN inputs are a residual stream whose mean is O(std))
@@ -244,52 +217,16 @@ PGP_DEV void layer_norm_tiles(f32x4 (&acc)[Geo<H>::MT_D][3], f32x4 (&X)[Geo<H>::
     mean[w] = sum[w] * invH;
     var[w] = fmaxf(fmaf(-mean[w], mean[w], sq * invH), 0.f);  // the variance itself
   }
-#else
-  // the three steps' statistics are reduced across lane groups in pairs (xsum2)
-  float sum[3], mean[3], var[3];
 #pragma unroll
   for (int w = 0; w < 3; ++w) {
-    sum[w] = 0.f;
-#pragma unroll
-    for (int mt = 0; mt < G::MT_D; ++mt) sum[w] += (acc[mt][w][0] + acc[mt][w][1]) + (acc[mt][w][2] + acc[mt][w][3]);
-  }
-  xsum2(sum[0], sum[1]);
-  sum[2] = xsum(sum[2], true);
-#pragma unroll
-  for (int w = 0; w < 3; ++w) {
-    mean[w] = sum[w] * invH;
-    var[w] = 0.f;
-#pragma unroll
-    for (int mt = 0; mt < G::MT_D; ++mt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float dv = (16 * mt + 4 * r + g < H) ? acc[mt][w][r] - mean[w] : 0.f;
-        var[w] += dv * dv;
-      }
-  }
-  xsum2(var[0], var[1]);
-  var[2] = xsum(var[2], true);
-#endif
-#pragma unroll
-  for (int w = 0; w < 3; ++w) {
-#if PGP_LN_ONEPASS
     const float rstd = __builtin_amdgcn_rsqf(var[w] + 1e-5f);  // v_rsq_f32 (1 ulp)
-#else
-    const float rstd = __builtin_amdgcn_rsqf(var[w] * invH + 1e-5f);
-#endif
-#if PGP_LN_FMA
     // (x - mean) * rstd as one fma per element: x * rstd + (-mean * rstd)
     const float nm = -mean[w] * rstd;
-#endif
 #pragma unroll
     for (int mt = 0; mt < G::MT_D; ++mt) {
-#if PGP_LN_FMA
       f32x4 xn;
 #pragma unroll
       for (int r = 0; r < 4; ++r) xn[r] = fmaf(acc[mt][w][r], rstd, nm);
-#else
-      const f32x4 xn = (acc[mt][w] - mean[w]) * rstd;
-#endif
       if constexpr (AFFINE) {
         const f32x4 ga = ld4(gam + 16 * mt + 4 * g), be = ld4(bet + 16 * mt + 4 * g);
         X[mt][w] = xn * ga + be;
@@ -502,11 +439,6 @@ PGP_DEV void encoder_layer_tail(f32x4 (&X)[Geo<H>::MT_D][3], Ring<H>& ring, cons
         Pw[w][2] = e2 * iv;
       }
     }
-  } else if constexpr (PGP_EXP_NO_SOFTMAX) {
-#pragma unroll
-    for (int w = 0; w < 3; ++w)
-#pragma unroll
-      for (int w2 = 0; w2 < 3; ++w2) P0[w][w2] = P1[w][w2] = 1.f / 3.f + 0.f * QK[0][w][0] * qr[0][w] * kr[0][w2];
   } else
 #pragma unroll
   for (int w = 0; w < 3; ++w) {
@@ -673,15 +605,13 @@ PGP_DEV void encoder_layer_tail(f32x4 (&X)[Geo<H>::MT_D][3], Ring<H>& ring, cons
           for (int w = 0; w < 3; ++w) acc[m][w] = mfma(a[e], Fc[0][w][e], acc[m][w]);
       }
       prio_valu();
-      if constexpr (!PGP_EXP_NO_ROWS) {
 #pragma unroll
-        for (int n = 0; n < G::XR; ++n) {
-          const f32x4 rw = ld4(TL + G::TL_RF + ((n * G::KQ_F + c) * 4 + g) * 4);
+      for (int n = 0; n < G::XR; ++n) {
+        const f32x4 rw = ld4(TL + G::TL_RF + ((n * G::KQ_F + c) * 4 + g) * 4);
 #pragma unroll
-          for (int e = 0; e < 4; ++e)
+        for (int e = 0; e < 4; ++e)
 #pragma unroll
-            for (int w = 0; w < 3; ++w) rf[n][w] = fmaf(rw[e], Fc[0][w][e], rf[n][w]);
-        }
+          for (int w = 0; w < 3; ++w) rf[n][w] = fmaf(rw[e], Fc[0][w][e], rf[n][w]);
       }
     }
 #pragma unroll
@@ -949,6 +879,18 @@ hipError_t launch(const FwdArgs& a, hipStream_t st) {
   const long nblk = (a.B + 15) / 16;
   constexpr int NW = enc_waves<H>();
   long grid = (nblk + NW - 1) / NW;
+  // A workgroup whose waves' registers cannot be co-resident never starts: the
+  // round-2 dual-block variant (256 VGPR + 123 AGPR per wave, 8 waves = 2 per
+  // SIMD, i.e. 758 of a SIMD's 512 registers) ended in a launch failure.  Check
+  // the built kernel's limit against the launch once per H and fail loudly.
+  static std::atomic<int> fits{-1};
+  if (fits.load(std::memory_order_relaxed) < 0) {
+    hipFuncAttributes fa{};
+    const bool ok = hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(encoder_kernel<H>)) == hipSuccess &&
+                    fa.maxThreadsPerBlock >= NW * 64;
+    fits.store(ok ? 1 : 0, std::memory_order_relaxed);
+  }
+  if (!fits.load(std::memory_order_relaxed)) return hipErrorLaunchOutOfResources;
   if constexpr (EncLds<H>::UNITS) {
     static std::atomic<int> occ_cache{0};  // workgroups resident per CU (registers / LDS), queried once
     int occ = occ_cache.load(std::memory_order_relaxed);

@@ -18,9 +18,15 @@ Per call, as the reference:
   3. ``tune_model`` (PreGANPlus.py:51-58): 10 sequential tuning steps on the
      latest window set (HIP);
   4. ``recover_decision`` (PreGANPlus.py:83-105) with the updated GAN.
+The Gen / Disc checkpoints are rewritten after every ``train_gan`` as the
+reference's ``save_gan`` does (PreGANPlus.py:76-81, utils.py:86-88), into the
+folder the models were loaded from (default ``recovery/PreGANSrc/checkpointsplus``,
+constants.py:3), off the critical path: a device-to-host copy on a side
+stream and ``torch.save`` on a writer thread (``_GanCheckpointWriter``).
 Deliberate deviations: dropout is off (the reference runs its
 modules in train mode with p=0.1, so its own decisions are stochastic); no
-plotting; checkpoints are written only when ``save_folder`` is set.
+plotting; a plugin built from injected ``weights=`` (tests, benches) writes
+only when ``save_folder`` is given.
 
 ``PreGANRecovery`` (``recovery/PreGAN.py:11-126``, BASELINE config C4): frozen
 FPE_16 encoder + K = 3 prototypes (HIP kernel K4), PreGAN's own Gen/Disc (K3),
@@ -30,7 +36,9 @@ generator, ``models.py:70``), so a seeded run reproduces the reference's h0.
 """
 from __future__ import annotations
 
+import atexit
 import os
+import threading
 
 import numpy as np
 import torch
@@ -40,7 +48,9 @@ from . import weights as W
 from .model import DecisionModel, FPEDecisionModel, assemble_decision, migrations, to_numpy
 
 COEFF_ENERGY, COEFF_LATENCY = 0.8, 0.2  # constants.py:19-20
+MODEL_PLUS_FOLDER = "recovery/PreGANSrc/checkpointsplus"   # constants.py:3
 _DATA = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data")
+_AUTO = object()   # save_folder default: where load_models read the checkpoints
 
 
 class Recovery:
@@ -60,7 +70,7 @@ class Recovery:
 
 
 class PreGANPlusRecovery(Recovery):
-    def __init__(self, hosts, env, training=False, device=None, model_folder=None, save_folder=None,
+    def __init__(self, hosts, env, training=False, device=None, model_folder=None, save_folder=_AUTO,
                  weights=None, extra=None):
         super().__init__()
         self.model_name = f"Transformer_{hosts}"
@@ -69,9 +79,12 @@ class PreGANPlusRecovery(Recovery):
         self.hosts = hosts
         self.env_name = "simulator" if env == "" else "framework"
         self.training = training
+        if save_folder is _AUTO:   # the reference's save_gan = True, into model_plus_folder (PreGANPlus.py:21)
+            save_folder = None if weights is not None else (model_folder or MODEL_PLUS_FOLDER)
         self.save_gan = save_folder is not None
         self.save_folder = save_folder
         self.device = torch.device(device or "cuda")
+        self._writer = None
         self.load_models(model_folder, weights, extra)
 
     # -- PreGANPlus.py:23-37 --
@@ -87,15 +100,25 @@ class PreGANPlusRecovery(Recovery):
                 if not os.path.exists(packaged):
                     raise FileNotFoundError(f"no checkpoint for {self.model_name} in {folder} or {packaged}")
                 weights, extra = W.load_npz(packaged)
+                # the GAN checkpoints save_gan keeps rewriting (load_gan, PreGANPlus.py:32-34)
+                gan = W.load_gan_checkpoints(folder, self.env_name, self.hosts)
+                if gan is not None:
+                    weights = dict(weights, **gan[0])
+                    extra = {k: v for k, v in extra.items()
+                             if not k.startswith(("opt/gen/", "opt/disc/", "meta/gen/", "meta/disc/"))}
+                    extra.update(gan[1])
         self.extra = extra or {}
         self.prototypes = np.asarray(weights["prototypes"], dtype=np.float64)
         self._infer = DecisionModel(self.hosts, weights, device=self.device)
         self._infer_stale = False
         self.trainer = TR.Trainer(self.hosts, weights, self.extra, device=self.device)
         self.tune_state = TR.TuneState(self.prototypes)
-        # load_gan's epoch and accuracy_list are the ones the plugin keeps (PreGANPlus.py:32-34)
+        # load_gan's epoch and accuracy_list are the ones the plugin keeps (PreGANPlus.py:32-34);
+        # the encoder checkpoint's own are kept for an explicit full save
         self.epoch = int(self.extra.get("meta/gen/epoch", 0))
         self.accuracy_list = W.accuracy_list_from_arrays(self.extra, "meta/gen/accuracy_list")
+        self.model_epoch = int(self.extra.get("meta/transformer/epoch", self.epoch))
+        self.model_accuracy_list = W.accuracy_list_from_arrays(self.extra, "meta/transformer/accuracy_list")
         if "train_time_data" in self.extra:
             self.train_time_data = np.asarray(self.extra["train_time_data"], dtype=np.float64)
         else:
@@ -114,6 +137,8 @@ class PreGANPlusRecovery(Recovery):
 
     # -- PreGANPlus.py:60-81 --
     def train_gan(self, embedding, schedule_data):
+        if self._writer is not None:
+            self._writer.fence()   # the previous call's snapshot copy precedes this update
         ns, new_score, orig_score, gen_loss, disc_loss = TR.train_gan(self.trainer, embedding, schedule_data,
                                                                       self._score)
         # the reference's save_gan is always on: epoch += 1, (gen_loss, disc_loss)
@@ -121,8 +146,15 @@ class PreGANPlusRecovery(Recovery):
         self.epoch += 1
         self.accuracy_list.append((gen_loss, disc_loss))
         if self.save_gan:
-            self.save_gan_checkpoints(self.save_folder)
+            if self._writer is None:
+                self._writer = _GanCheckpointWriter(self)
+            self._writer.post()
         return ns
+
+    def flush_checkpoints(self):
+        """Wait until the last posted Gen / Disc checkpoint is on disk."""
+        if self._writer is not None:
+            self._writer.flush()
 
     # -- PreGANPlus.py:51-58 --
     def tune_model(self):
@@ -232,17 +264,50 @@ class PreGANPlusRecovery(Recovery):
 
     # -- utils.py:86-88 save_gan: Gen with (epoch, accuracy_list), Disc with (0, []) --
     def save_gan_checkpoints(self, folder):
+        self.flush_checkpoints()
         save_checkpoints(self.trainer, folder, self.env_name, self.epoch, self.accuracy_list,
                          [("gen", self.gen_name, None)])
         save_checkpoints(self.trainer, folder, self.env_name, 0, [], [("disc", self.disc_name, None)])
 
     # -- utils.py:49-58 (checkpoint dict), written with torch.save: all three
     #    models (the reference rewrites only the GAN per call; this is the
-    #    explicit full save, e.g. at shutdown) --
+    #    explicit full save, e.g. at shutdown).  The encoder checkpoint keeps
+    #    its own epoch and accuracy_list, as load_model read them --
     def save_checkpoints(self, folder):
-        save_checkpoints(self.trainer, folder, self.env_name, self.epoch, self.accuracy_list,
+        self.flush_checkpoints()
+        save_checkpoints(self.trainer, folder, self.env_name, self.model_epoch, self.model_accuracy_list,
                          [("transformer", self.model_name, self.tune_state.protos)])
         self.save_gan_checkpoints(folder)
+
+
+def _ckpt_dict(trainer, sec, weights_sec, m, v, steps, epoch, accuracy_list, proto, base=0):
+    """The reference's checkpoint dict (utils.py:53-58) for one section from host
+    arrays: m / v hold the AdamW moments at blob offsets - base; steps[name] the
+    per-parameter step counts (AdamW state per parameter index)."""
+    state, idx = {}, 0
+    for t in trainer.tensors:
+        if t["section"] != sec or not t["trainable"]:
+            continue
+        sl = slice(t["offset"] - base, t["offset"] - base + t["n"])
+        shp = weights_sec[t["name"]].shape
+        state[idx] = {"step": torch.tensor(float(steps[t["name"]])),
+                      "exp_avg": torch.tensor(m[sl].astype(np.float64).reshape(shp)),
+                      "exp_avg_sq": torch.tensor(v[sl].astype(np.float64).reshape(shp))}
+        idx += 1
+    return {"epoch": epoch,
+            "model_state_dict": {k: torch.tensor(np.asarray(a, dtype=np.float64)) for k, a in weights_sec.items()},
+            "model_prototypes": [torch.tensor(x) for x in proto] if proto is not None else {},
+            "optimizer_state_dict": {"state": state, "param_groups": [{
+                "lr": trainer.lrs[sec], "betas": (trainer.b1, trainer.b2),
+                "eps": trainer.eps, "weight_decay": trainer.wd, "amsgrad": False,
+                "params": list(range(idx))}]},
+            "accuracy_list": list(accuracy_list)}
+
+
+def _save_atomic(ck, path):
+    tmp = path + ".tmp"
+    torch.save(ck, tmp)
+    os.replace(tmp, path)   # a reader never sees a half-written checkpoint
 
 
 def save_checkpoints(trainer, folder, env_name, epoch, accuracy_list, entries):
@@ -252,25 +317,113 @@ def save_checkpoints(trainer, folder, env_name, epoch, accuracy_list, entries):
     w = trainer.weights_numpy()
     mm, vv = trainer.m.cpu().numpy(), trainer.v.cpu().numpy()
     for sec, name, proto in entries:
-        state, idx = {}, 0
-        for t in trainer.tensors:
-            if t["section"] != sec or not t["trainable"]:
-                continue
-            sl = slice(t["offset"], t["offset"] + t["n"])
-            shp = w[sec][t["name"]].shape
-            state[idx] = {"step": torch.tensor(float(t["step"])),
-                          "exp_avg": torch.tensor(mm[sl].astype(np.float64).reshape(shp)),
-                          "exp_avg_sq": torch.tensor(vv[sl].astype(np.float64).reshape(shp))}
-            idx += 1
-        ck = {"epoch": epoch,
-              "model_state_dict": {k: torch.tensor(v) for k, v in w[sec].items()},
-              "model_prototypes": [torch.tensor(x) for x in proto] if proto is not None else {},
-              "optimizer_state_dict": {"state": state, "param_groups": [{
-                  "lr": trainer.lrs[sec], "betas": (trainer.b1, trainer.b2),
-                  "eps": trainer.eps, "weight_decay": trainer.wd, "amsgrad": False,
-                  "params": list(range(idx))}]},
-              "accuracy_list": list(accuracy_list)}
-        torch.save(ck, os.path.join(folder, f"{env_name}_{name}.ckpt"))
+        steps = {t["name"]: t["step"] for t in trainer.tensors if t["section"] == sec}
+        _save_atomic(_ckpt_dict(trainer, sec, w[sec], mm, vv, steps, epoch, accuracy_list, proto),
+                     os.path.join(folder, f"{env_name}_{name}.ckpt"))
+
+
+class _GanCheckpointWriter:
+    """save_gan (utils.py:86-88) after every train_gan, off the critical path.
+    ``post()`` snapshots the Gen / Disc master weights and AdamW moments into a
+    pinned host buffer with a copy on a side stream (ordered after the GAN step
+    on the caller's stream, no host synchronisation) plus the host-side epoch,
+    accuracy_list and step counts; a writer thread waits for that copy and
+    writes the two checkpoints (Gen with (epoch, accuracy_list), Disc with
+    (0, []), atomic renames).  Snapshots still queued when a newer one is posted
+    are superseded (the files on disk always end at the newest call, as the
+    reference's do).  ``fence()`` makes the caller's stream wait for the last
+    snapshot copy before the next GAN update; ``flush()`` waits for the disk."""
+
+    def __init__(self, rec):
+        tr = rec.trainer
+        self.rec, self.tr = rec, tr
+        self.lo, self.hi = tr.sec_off["gen"], tr.sec_end["disc"]
+        n = self.hi - self.lo
+        self.bufs = [torch.empty((3, n), dtype=torch.float32).pin_memory() for _ in range(2)]
+        self.events = [torch.cuda.Event() for _ in range(2)]
+        self.busy = [False, False]
+        self.stream = torch.cuda.Stream(tr.device)
+        self.next = 0
+        self.last_event = None
+        self.cv = threading.Condition()
+        self.job = None
+        self.writing = False
+        self.error = None
+        self.thread = threading.Thread(target=self._run, daemon=True, name="pgp-save-gan")
+        self.thread.start()
+        atexit.register(self.flush)
+
+    def fence(self):
+        if self.last_event is not None:
+            torch.cuda.current_stream(self.tr.device).wait_event(self.last_event)
+
+    def post(self):
+        rec, tr = self.rec, self.tr
+        with self.cv:
+            while self.busy[self.next]:
+                self.cv.wait()
+            k = self.next
+            self.busy[k] = True
+            self.next ^= 1
+        self.stream.wait_stream(torch.cuda.current_stream(tr.device))
+        with torch.cuda.stream(self.stream):
+            b = self.bufs[k]
+            b[0].copy_(tr.P[self.lo:self.hi], non_blocking=True)
+            b[1].copy_(tr.m[self.lo:self.hi], non_blocking=True)
+            b[2].copy_(tr.v[self.lo:self.hi], non_blocking=True)
+            self.events[k].record(self.stream)
+        self.last_event = self.events[k]
+        job = (k, rec.save_folder, rec.env_name, rec.epoch, list(rec.accuracy_list),
+               {t["name"] + "@" + t["section"]: t["step"] for t in tr.tensors if t["section"] in ("gen", "disc")})
+        with self.cv:
+            if self.job is not None:          # superseded, never written
+                self.busy[self.job[0]] = False
+            self.job = job
+            self.cv.notify_all()
+        if self.error is not None:
+            raise RuntimeError("save_gan writer failed") from self.error
+
+    def _run(self):
+        while True:
+            with self.cv:
+                while self.job is None:
+                    self.cv.wait()
+                k, folder, env_name, epoch, acc, steps = self.job
+                self.job = None
+                self.writing = True
+            try:
+                self.events[k].synchronize()
+                host = self.bufs[k].numpy().copy()
+                with self.cv:
+                    self.busy[k] = False
+                    self.cv.notify_all()
+                self._write(host, folder, env_name, epoch, acc, steps)
+            except Exception as e:  # surfaced on the next post()
+                self.error = e
+            finally:
+                with self.cv:
+                    self.busy[k] = False
+                    self.writing = False
+                    self.cv.notify_all()
+
+    def _write(self, host, folder, env_name, epoch, acc, steps):
+        tr, rec = self.tr, self.rec
+        os.makedirs(folder, exist_ok=True)
+        p, m, v = host
+        shapes = {(sec, name): shp for sec, name, shp in W.blob_layout(tr.H)[:-1]}
+        for sec, name, ep, al in (("gen", rec.gen_name, epoch, acc), ("disc", rec.disc_name, 0, [])):
+            wsec = {t["name"]: p[t["offset"] - self.lo:t["offset"] - self.lo + t["n"]].reshape(shapes[(sec, t["name"])])
+                    for t in tr.tensors if t["section"] == sec}
+            st = {t["name"]: steps[t["name"] + "@" + sec] for t in tr.tensors if t["section"] == sec}
+            _save_atomic(_ckpt_dict(tr, sec, wsec, m, v, st, ep, al, None, base=self.lo),
+                         os.path.join(folder, f"{env_name}_{name}.ckpt"))
+
+    def flush(self):
+        with self.cv:
+            while self.job is not None or self.writing:
+                self.cv.wait()
+        if self.error is not None:
+            raise RuntimeError("save_gan writer failed") from self.error
 
 
 class _RecoverIO:

@@ -216,22 +216,15 @@ def load_reference_checkpoints(model_dir, env_name="simulator", H=16, encoder="T
     Gen checkpoint's ``accuracy_list`` (the one PreGANPlusRecovery keeps,
     ``PreGANPlus.py:32-34``) as ``meta/gen/accuracy_list`` (flat) +
     ``meta/gen/accuracy_list_lens``."""
-    import torch
-    sg = [(np._core.multiarray.scalar, "numpy.core.multiarray.scalar"), np.dtype,
-          np.dtypes.Float64DType]
-
     def ld(name):
-        with torch.serialization.safe_globals(sg):
-            return torch.load(os.path.join(model_dir, f"{env_name}_{name}_{H}.ckpt"),
-                              weights_only=True)
+        return _safe_load(os.path.join(model_dir, f"{env_name}_{name}_{H}.ckpt"))
 
     t, g, d = ld(encoder), ld("Gen"), ld("Disc")
-    conv = lambda sd: {k: v.detach().cpu().numpy().astype(np.float64) for k, v in sd.items()}
     tsec = "fpe" if encoder == "FPE" else "transformer"
     weights = {
-        tsec: conv(t["model_state_dict"]),
-        "gen": conv(g["model_state_dict"]),
-        "disc": conv(d["model_state_dict"]),
+        tsec: _conv_sd(t["model_state_dict"]),
+        "gen": _conv_sd(g["model_state_dict"]),
+        "disc": _conv_sd(d["model_state_dict"]),
         "prototypes": np.stack([p.detach().cpu().numpy() for p in t["model_prototypes"]]),
         "meta": {"epoch": t["epoch"], "gan_epoch": g["epoch"]},
     }
@@ -239,19 +232,55 @@ def load_reference_checkpoints(model_dir, env_name="simulator", H=16, encoder="T
         return weights
     extra = {}
     for sec, ck in ((tsec, t), ("gen", g), ("disc", d)):
-        names = [k for k in ck["model_state_dict"] if k not in _BUFFERS[sec]]
-        osd = ck["optimizer_state_dict"]
-        idx = [i for grp in osd["param_groups"] for i in grp["params"]]
-        if len(idx) != len(names):
-            raise ValueError(f"{sec}: {len(idx)} optimizer params vs {len(names)} state_dict parameters")
-        for i, name in zip(idx, names):
-            s = osd["state"].get(i)
-            if not s:
-                continue
-            extra[f"opt/{sec}/{name}/exp_avg"] = s["exp_avg"].detach().cpu().numpy().astype(np.float64)
-            extra[f"opt/{sec}/{name}/exp_avg_sq"] = s["exp_avg_sq"].detach().cpu().numpy().astype(np.float64)
-            extra[f"opt/{sec}/{name}/step"] = np.float64(float(s["step"]))
-        extra[f"meta/{sec}/epoch"] = np.int64(ck["epoch"])
+        extra.update(_ck_state(sec, ck))
+    extra.update(accuracy_list_to_arrays(g["accuracy_list"], "meta/gen/accuracy_list"))
+    # the encoder checkpoint's own accuracy_list (train_model's, PreGANPlus.py:41-49): kept
+    # apart so an explicit full save writes the encoder checkpoint as load_model read it
+    extra.update(accuracy_list_to_arrays(t["accuracy_list"], f"meta/{tsec}/accuracy_list"))
+    return weights, extra
+
+
+def _safe_load(path):
+    import torch
+    sg = [(np._core.multiarray.scalar, "numpy.core.multiarray.scalar"), np.dtype, np.dtypes.Float64DType]
+    with torch.serialization.safe_globals(sg):
+        return torch.load(path, weights_only=True)
+
+
+def _conv_sd(sd):
+    return {k: v.detach().cpu().numpy().astype(np.float64) for k, v in sd.items()}
+
+
+def _ck_state(sec, ck):
+    """load_model's training state of one checkpoint (utils.py:70-77) in the
+    packaged-npz key format: AdamW moments / steps per parameter, epoch."""
+    extra = {}
+    names = [k for k in ck["model_state_dict"] if k not in _BUFFERS[sec]]
+    osd = ck["optimizer_state_dict"]
+    idx = [i for grp in osd["param_groups"] for i in grp["params"]]
+    if len(idx) != len(names):
+        raise ValueError(f"{sec}: {len(idx)} optimizer params vs {len(names)} state_dict parameters")
+    for i, name in zip(idx, names):
+        s = osd["state"].get(i)
+        if not s:
+            continue
+        extra[f"opt/{sec}/{name}/exp_avg"] = s["exp_avg"].detach().cpu().numpy().astype(np.float64)
+        extra[f"opt/{sec}/{name}/exp_avg_sq"] = s["exp_avg_sq"].detach().cpu().numpy().astype(np.float64)
+        extra[f"opt/{sec}/{name}/step"] = np.float64(float(s["step"]))
+    extra[f"meta/{sec}/epoch"] = np.int64(ck["epoch"])
+    return extra
+
+
+def load_gan_checkpoints(model_dir, env_name="simulator", H=16):
+    """load_gan (utils.py:81-84) alone: Gen / Disc weights and their training
+    state from ``{env}_Gen_{H}.ckpt`` / ``{env}_Disc_{H}.ckpt`` (the files
+    save_gan rewrites every call), or None when either is absent."""
+    paths = [os.path.join(model_dir, f"{env_name}_{n}_{H}.ckpt") for n in ("Gen", "Disc")]
+    if not all(os.path.exists(p) for p in paths):
+        return None
+    g, d = (_safe_load(p) for p in paths)
+    weights = {"gen": _conv_sd(g["model_state_dict"]), "disc": _conv_sd(d["model_state_dict"])}
+    extra = dict(_ck_state("gen", g), **_ck_state("disc", d))
     extra.update(accuracy_list_to_arrays(g["accuracy_list"], "meta/gen/accuracy_list"))
     return weights, extra
 

@@ -79,3 +79,42 @@ def test_plugin_checkpoint_resume(tmp_path):
     # the Disc checkpoint carries epoch 0 and an empty accuracy_list (utils.py:86-88)
     ck = torch.load(tmp_path / "simulator_Disc_16.ckpt", weights_only=True)
     assert ck["epoch"] == 0 and ck["accuracy_list"] == []
+
+
+def test_plugin_save_gan_every_call_resumes(tmp_path):
+    """save_gan is on by default (PreGANPlus.py:21, 76-81): a plugin built the
+    drop-in way (no injected weights) rewrites the Gen / Disc checkpoints in
+    its model folder after every train_gan, on a writer thread; a second plugin
+    on the same folder resumes the first's GAN weights, AdamW moments and step
+    counts, epoch and accuracy_list as of its last train_gan (the reference
+    saves inside train_gan, before tune_model appends its entry)."""
+    from preganplus_amd.recovery import PreGANPlusRecovery
+    from tests.test_train_oracle_golden import fake_env
+    _, extra = W.load_npz("preganplus_amd/data/simulator_16.npz")
+    z = np.load("tests/golden/plugin_h16.npz")
+    a = PreGANPlusRecovery(16, "", training=True, model_folder=str(tmp_path))
+    assert a.save_gan and a.save_folder == str(tmp_path)
+    for step in range(3):
+        a.setEnvironment(fake_env(z, step, extra["train_time_data"], z["schedule_series"]))
+        a.run_model(None, [tuple(x) for x in z[f"s{step}/decision_in"]])
+    a.flush_checkpoints()
+    for name in ("Gen", "Disc"):
+        assert os.path.exists(tmp_path / f"simulator_{name}_16.ckpt")
+    assert not os.path.exists(tmp_path / "simulator_Transformer_16.ckpt")   # never rewritten per call
+    b = PreGANPlusRecovery(16, "", training=True, model_folder=str(tmp_path))
+    assert b.epoch == a.epoch
+    assert b.accuracy_list == a.accuracy_list[:-1]          # up to the last train_gan's entry
+    tr_a, tr_b = a.trainer, b.trainer
+    lo, hi = tr_a.sec_off["gen"], tr_a.sec_end["disc"]
+    torch.cuda.synchronize()
+    assert torch.equal(tr_a.P[lo:hi], tr_b.P[lo:hi])
+    assert torch.equal(tr_a.m[lo:hi], tr_b.m[lo:hi]) and torch.equal(tr_a.v[lo:hi], tr_b.v[lo:hi])
+    ga = [t["step"] for t in tr_a.tensors if t["section"] in ("gen", "disc")]
+    assert ga == [t["step"] for t in tr_b.tensors if t["section"] in ("gen", "disc")] and min(ga) >= 3
+    # the transformer comes from the packaged weights, untouched by save_gan
+    t0 = tr_b.sec_off["transformer"]
+    fresh = PreGANPlusRecovery(16, "", training=True, weights=W.load_npz("preganplus_amd/data/simulator_16.npz")[0],
+                               extra=extra)
+    assert torch.equal(tr_b.P[t0:lo], fresh.trainer.P[t0:lo])
+    ck = torch.load(tmp_path / "simulator_Disc_16.ckpt", weights_only=True)
+    assert ck["epoch"] == 0 and ck["accuracy_list"] == []

@@ -153,8 +153,9 @@ def _c2_torch(n, H, seed, device="cuda"):
 
 
 @pytest.mark.timeout(900)
+@pytest.mark.parametrize("seed_off", [0, 970])
 @pytest.mark.parametrize("H,B", [(50, 65536), (16, 262144)])
-def test_full_size_census(H, B):
+def test_full_size_census(H, B, seed_off):
     """BASELINE sizes: C2 (H=50, 65,536 windows) and one whole C5 launch (H=16,
     262,144 cell-windows), every window compared with the fp64 oracle
     (tests/census.py over a CPU worker pool).
@@ -179,8 +180,9 @@ def test_full_size_census(H, B):
     else:
         w = W.synth_weights(H, seed=0)
     m = get_model(H, w, f"full{H}")
-    # PGP_CENSUS_SEED: the same census over another seeded input draw (one-off runs)
-    seed = int(os.environ.get("PGP_CENSUS_SEED", 31 + H))
+    # two input draws per size in the suite (seed_off); PGP_CENSUS_SEED overrides
+    # the first for one-off runs over other draws
+    seed = int(os.environ.get("PGP_CENSUS_SEED", 31 + H)) + seed_off
     x, s = _c2_torch(B, H, seed=seed)
     full = to_numpy(m.forward(x, s))
     torch.cuda.synchronize()
@@ -201,7 +203,7 @@ def test_full_size_census(H, B):
     res = {"H": H, "windows": B, "seed": seed, "census": st, "worst_error_over_tolerance": worst}
     print("CENSUS", json.dumps(res))
     os.makedirs("gpurun_out", exist_ok=True)
-    tag = "" if "PGP_CENSUS_SEED" not in os.environ else f"_s{seed}"
+    tag = "" if "PGP_CENSUS_SEED" not in os.environ and seed_off == 0 else f"_s{seed}"
     with open(f"gpurun_out/census_h{H}_b{B}{tag}.json", "w") as f:
         json.dump(res, f, indent=1)
     assert worst["logits"] <= 1.0 and worst["protos"] <= 1.0 and worst["probs"] <= 1.0, worst
@@ -210,3 +212,9 @@ def test_full_size_census(H, B):
     # the rigorous bounds leave a small unverifiable fraction: keep it < 0.1 %
     for kind in ("anomaly", "class", "keep", "gen"):
         assert st[kind]["in_band"] <= 1e-3 * max(st[kind]["n"], 1), (kind, st[kind])
+    # observed mismatch counts, asserted (PreGANPlus.py:87,99, Stats.py:164-166): every
+    # census launch so far has had 0-2 generator-target near-ties (fp64 margin below
+    # what fp32 resolves, inside the bound) and no other differing decision
+    for kind in ("anomaly", "any", "class", "keep", "final"):
+        assert st[kind]["mismatch"] == 0, (kind, st[kind])
+    assert st["gen"]["mismatch"] <= 8, st["gen"]
