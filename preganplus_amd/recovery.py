@@ -332,9 +332,14 @@ class _GanCheckpointWriter:
     (0, []), atomic renames).  Snapshots still queued when a newer one is posted
     are superseded (the files on disk always end at the newest call, as the
     reference's do).  ``fence()`` makes the caller's stream wait for the last
-    snapshot copy before the next GAN update; ``flush()`` waits for the disk."""
+    snapshot copy before the next GAN update; ``flush()`` waits for the disk.
+    Pickling a checkpoint holds the GIL for milliseconds, so after each write the
+    writer pauses ``min_interval`` seconds (PGP_SAVE_GAN_INTERVAL, default 0.05)
+    before taking the newest snapshot: calls that come faster than that do not
+    wait on the GIL; the files then lag the plugin by at most one pause, and
+    ``flush()`` (also at exit) writes the newest state at once."""
 
-    def __init__(self, rec):
+    def __init__(self, rec, min_interval=None):
         tr = rec.trainer
         self.rec, self.tr = rec, tr
         self.lo, self.hi = tr.sec_off["gen"], tr.sec_end["disc"]
@@ -349,6 +354,9 @@ class _GanCheckpointWriter:
         self.job = None
         self.writing = False
         self.error = None
+        self.urgent = False
+        self.min_interval = float(os.environ.get("PGP_SAVE_GAN_INTERVAL", 0.05) if min_interval is None
+                                  else min_interval)
         self.thread = threading.Thread(target=self._run, daemon=True, name="pgp-save-gan")
         self.thread.start()
         atexit.register(self.flush)
@@ -373,7 +381,8 @@ class _GanCheckpointWriter:
             b[2].copy_(tr.v[self.lo:self.hi], non_blocking=True)
             self.events[k].record(self.stream)
         self.last_event = self.events[k]
-        job = (k, rec.save_folder, rec.env_name, rec.epoch, list(rec.accuracy_list),
+        # accuracy_list only grows (append): the writer slices the first n entries itself
+        job = (k, rec.save_folder, rec.env_name, rec.epoch, (rec.accuracy_list, len(rec.accuracy_list)),
                {t["name"] + "@" + t["section"]: t["step"] for t in tr.tensors if t["section"] in ("gen", "disc")})
         with self.cv:
             if self.job is not None:          # superseded, never written
@@ -405,12 +414,16 @@ class _GanCheckpointWriter:
                     self.busy[k] = False
                     self.writing = False
                     self.cv.notify_all()
+                    # pause before the next write unless a flush is waiting
+                    if self.min_interval > 0 and not self.urgent:
+                        self.cv.wait_for(lambda: self.urgent, timeout=self.min_interval)
 
     def _write(self, host, folder, env_name, epoch, acc, steps):
         tr, rec = self.tr, self.rec
         os.makedirs(folder, exist_ok=True)
         p, m, v = host
         shapes = {(sec, name): shp for sec, name, shp in W.blob_layout(tr.H)[:-1]}
+        acc = acc[0][:acc[1]]
         for sec, name, ep, al in (("gen", rec.gen_name, epoch, acc), ("disc", rec.disc_name, 0, [])):
             wsec = {t["name"]: p[t["offset"] - self.lo:t["offset"] - self.lo + t["n"]].reshape(shapes[(sec, t["name"])])
                     for t in tr.tensors if t["section"] == sec}
@@ -420,8 +433,11 @@ class _GanCheckpointWriter:
 
     def flush(self):
         with self.cv:
+            self.urgent = True
+            self.cv.notify_all()
             while self.job is not None or self.writing:
                 self.cv.wait()
+            self.urgent = False
         if self.error is not None:
             raise RuntimeError("save_gan writer failed") from self.error
 
