@@ -1,19 +1,19 @@
 // pgp_tune.hip — the semi-supervised tuning step (train.py:42-57): forward with
-// saved activations and backward of the PreGAN+ Transformer (models.py:376-416)
-// over a batch of windows, as token-major fp32 MFMA GEMMs.
+// checkpoints and backward of the PreGAN+ Transformer (models.py:376-416) over
+// a batch of windows.
 //
-// Layout (pgp_tune.hpp): activations are [M][ld] over the batch's M = B*3H
-// tokens.  A linear layer runs with one wave per 16 tokens x all N outputs on
-// v_mfma_f32_16x16x4_f32: the weights are the A operand (the whole [N][K]
-// matrix is staged once per workgroup in LDS as per-lane fragments), the 16
-// token rows the B operand (one float4 per lane per 16-deep k-block straight
-// from HBM).  A lane then holds outputs n = 16t + 4g + r of token row
-// (lane & 15), g = lane >> 4 — whole rows per wave, so LayerNorm forward and
-// backward run in the GEMM epilogue with two cross-lane-group sums.  Weight
-// gradients [N][K] = sum over tokens are split over workgroups into partial
-// slabs that one reduction adds up in a fixed order (deterministic).  The
-// decoders contract over a window's whole encoder output (3H x DP, token
-// layout) as split-K GEMMs on a permuted copy of their weights.
+// The encoder layers run as fused per-unit kernels (pgp_tunef.hip: every
+// activation of a layer in MFMA registers, weight gradients contracted in
+// registers / LDS).  Around them, token-major kernels over the batch's M = B*3H
+// tokens ([M][ld] rows, pgp_tune.hpp): the GAT aggregation and its backward
+// (one wave per (window, step)), the time encoder's input gradient (a linear
+// layer on v_mfma_f32_16x16x4_f32, weights as the A operand staged in LDS,
+// 16 token rows per wave as B), the weight-gradient contractions that stay
+// tall (in_proj over dQKV, time encoder, GAT fc: partial slabs over
+// workgroups), and the decoders, which contract over a window's whole encoder
+// output (3H x DP, token layout) as split-K GEMMs on a permuted copy of their
+// weights.  Every weight-gradient reduction is deferred to the end of the
+// backward and runs in a fixed order (deterministic).
 //
 // Deviations from the reference's op order are algebraic only: the GAT
 // aggregates the raw features (sum_i a_ij x_i, then fc) instead of fc(x_i)
@@ -27,6 +27,7 @@
 #include "pgp_gemm.hpp"
 #include "pgp_train.hpp"
 #include "pgp_tune.hpp"
+#include "pgp_tunef.hpp"
 #include "pgp_tunetargets.hpp"
 
 // workgroups of the token-major GEMMs / weight-gradient kernels (grid-stride loops)
@@ -40,62 +41,13 @@
 namespace pgp {
 namespace {
 
-enum : int { EPI_STORE = 0, EPI_PE = 1, EPI_LN = 2, EPI_MASK = 3, EPI_RES = 4, EPI_LNB = 5 };
-
-// LayerNorm (eps 1e-5, biased variance; models.py:350-356 norm1/norm2) of rows
-// held as v[t][r] = feature 16t+4g+r of token (lane & 15); features >= N are 0
-// on entry.  v becomes x-hat (pads 0); returns rstd.
-template <int NT>
-PGP_DEV float ln_rows(f32x4 (&v)[NT], int g, int N) {
-  float s = 0.f;
-#pragma unroll
-  for (int t = 0; t < NT; ++t) s += (v[t][0] + v[t][1]) + (v[t][2] + v[t][3]);
-  const float mu = xsum(s, true) / (float)N;
-  float q = 0.f;
-#pragma unroll
-  for (int t = 0; t < NT; ++t)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float dv = (16 * t + 4 * g + r < N) ? v[t][r] - mu : 0.f;
-      v[t][r] = dv;
-      q += dv * dv;
-    }
-  const float rs = 1.0f / sqrtf(xsum(q, true) / (float)N + 1e-5f);
-#pragma unroll
-  for (int t = 0; t < NT; ++t) v[t] = v[t] * rs;
-  return rs;
-}
-
-// LayerNorm backward: dy (grad of the output) -> grad of the input, from the
-// saved x-hat and rstd and gamma w (pads 0); accumulates dy*xh and dy (the
-// gamma / beta gradients) into pw / pb.
-template <int NT>
-PGP_DEV void ln_bwd_rows(f32x4 (&dy)[NT], const f32x4 (&xh)[NT], const f32x4 (&w)[NT], float rs, int g, int N,
-                         f32x4 (&pw)[NT], f32x4 (&pb)[NT]) {
-  float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-  for (int t = 0; t < NT; ++t)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      pw[t][r] = fmaf(dy[t][r], xh[t][r], pw[t][r]);
-      pb[t][r] += dy[t][r];
-      const float dxh = dy[t][r] * w[t][r];
-      s1 += dxh;
-      s2 = fmaf(dxh, xh[t][r], s2);
-      dy[t][r] = dxh;
-    }
-  s1 = xsum(s1, true) / (float)N;
-  s2 = xsum(s2, true) / (float)N;
-#pragma unroll
-  for (int t = 0; t < NT; ++t)
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-      dy[t][r] = (16 * t + 4 * g + r < N) ? rs * (dy[t][r] - s1 - xh[t][r] * s2) : 0.f;
-}
+enum : int { EPI_STORE = 0 };
 
 // ============================================================================
-// Linear layer over all tokens: Y = epilogue(X . W'^T + bias), W' = W (trans 0,
-// W[n][k] = W[n*ldw+k]) or W^T (trans 1, W'[n][k] = W[k*ldw+n]).
+// Linear layer over all tokens: Y = X . W'^T (+ bias), W' = W (trans 0,
+// W[n][k] = W[n*ldw+k]) or W^T (trans 1, W'[n][k] = W[k*ldw+n]).  Used for the
+// decoders' input gradient (per token, batched over grid.y) and the time
+// encoder's.
 // ============================================================================
 struct LinArgs {
   long M;
@@ -106,33 +58,20 @@ struct LinArgs {
   const float* bias;
   float* Y;
   int ldy;
-  const float* R;  // residual (LN, RES, LNB) or mask source (MASK)
-  int ldr;
-  const float* lnw;
-  const float* lnb;
-  float* XH;  // LN: x-hat out; LNB: saved x-hat in   (row stride ldy)
-  float* RS;  // LN: rstd out;  LNB: saved rstd in
-  const float* pe;  // PE: positional encoding [3][N]
-  int H;
-  float* part;  // LNB: per-workgroup gamma/beta partials [grid.y][grid.x][2][NP]
-  // batched launch (grid.y = batch index): offsets of W, Y, XH and RS per
-  // batch entry; RS is read / written at RS[m * rss]
-  long bw, by, bxh, brs;
-  int rss;
+  // batched launch (grid.y = batch index): offsets of W and Y per batch entry
+  long bw, by;
   int frag;  // W points at W' pre-packed as [NP/16][KP/16][64 lanes][4] fragments
 };
 
 template <int NP, int KP, int EPI>
 __global__ __launch_bounds__(256, 2) void linear_kernel(LinArgs a) {
+  static_assert(EPI == EPI_STORE, "store epilogue only");
   constexpr int NT = NP / 16, KB = KP / 16;
   __shared__ f32x4 wl[NT * KB * 64];
-  __shared__ float cb[NP], cw[NP], cbb[NP];
-  __shared__ float lred[EPI == EPI_LNB ? 8 * NP : 1];
+  __shared__ float cb[NP];
   float* wf_flat = reinterpret_cast<float*>(wl);
   const float* Wb = a.W + blockIdx.y * a.bw;
   float* Yb = a.Y + blockIdx.y * a.by;
-  float* XHb = a.XH ? a.XH + blockIdx.y * a.bxh : nullptr;
-  float* RSb = a.RS ? a.RS + blockIdx.y * a.brs : nullptr;
   if (a.frag) {  // W' already packed in fragment order for this (NP, KP): a straight copy
     const f32x4* src = reinterpret_cast<const f32x4*>(Wb);
     for (int i = threadIdx.x; i < NT * KB * 64; i += 256) wl[i] = src[i];
@@ -146,17 +85,10 @@ __global__ __launch_bounds__(256, 2) void linear_kernel(LinArgs a) {
       wf_flat[i] = v;
     }
   }
-  for (int n = threadIdx.x; n < NP; n += 256) {
-    cb[n] = (a.bias && n < a.N) ? a.bias[n] : 0.f;
-    cw[n] = (a.lnw && n < a.N) ? a.lnw[n] : 0.f;
-    cbb[n] = (a.lnb && n < a.N) ? a.lnb[n] : 0.f;
-  }
+  for (int n = threadIdx.x; n < NP; n += 256) cb[n] = (a.bias && n < a.N) ? a.bias[n] : 0.f;
   __syncthreads();
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, g = lane >> 4, mi = lane & 15;
   const long nrb = (a.M + 15) >> 4;
-  f32x4 pw[NT], pb[NT];
-#pragma unroll
-  for (int t = 0; t < NT; ++t) pw[t] = pb[t] = zero4();
   // B-operand k-blocks are prefetched PF ahead (a ring of registers), so a
   // wave keeps several HBM loads in flight; wide layers (NT > 4) keep the LDS
   // fragments out of registers with a short unroll.  The next row block's first
@@ -208,82 +140,10 @@ __global__ __launch_bounds__(256, 2) void linear_kernel(LinArgs a) {
 #pragma unroll
     for (int j = 0; j < PF; ++j) xq[j] = xn[j];
     float* yr = Yb + m * a.ldy + 4 * g;
-    if constexpr (EPI == EPI_PE) {
-      const int w = (int)((m % (3L * a.H)) / a.H);
+    if (ok) {
 #pragma unroll
-      for (int t = 0; t < NT; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int n = 16 * t + 4 * g + r;
-          if (n < a.N) acc[t][r] += a.pe[w * a.N + n];
-        }
+      for (int t = 0; t < NT; ++t) st4(yr + 16 * t, acc[t]);
     }
-    if (EPI == EPI_LN || EPI == EPI_MASK || EPI == EPI_RES || (EPI == EPI_LNB && a.R)) {
-      const float* rr = a.R + m * a.ldr + 4 * g;
-#pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        const f32x4 rv = ok ? ld4(rr + 16 * t) : zero4();
-        if constexpr (EPI == EPI_MASK) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) acc[t][r] = rv[r] > 0.f ? acc[t][r] : 0.f;
-        } else {
-          acc[t] += rv;
-        }
-      }
-    }
-    if constexpr (EPI == EPI_LN) {
-      const float rs = ln_rows<NT>(acc, g, a.N);
-      if (ok) {
-        float* xh = XHb + m * a.ldy + 4 * g;
-#pragma unroll
-        for (int t = 0; t < NT; ++t) {
-          st4(xh + 16 * t, acc[t]);
-          f32x4 y;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int n = 16 * t + 4 * g + r;
-            y[r] = fmaf(acc[t][r], cw[n], cbb[n]);
-          }
-          st4(yr + 16 * t, y);
-        }
-        if (g == 0) RSb[m * a.rss] = rs;
-      }
-    } else if constexpr (EPI == EPI_LNB) {
-      f32x4 xh[NT], w[NT];
-      const float* xhr = XHb + m * a.ldy + 4 * g;
-#pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        xh[t] = ok ? ld4(xhr + 16 * t) : zero4();
-        w[t] = *reinterpret_cast<const f32x4*>(&cw[16 * t + 4 * g]);
-      }
-      const float rs = ok ? RSb[m * a.rss] : 0.f;
-      ln_bwd_rows<NT>(acc, xh, w, rs, g, a.N, pw, pb);
-      if (ok) {
-#pragma unroll
-        for (int t = 0; t < NT; ++t) st4(yr + 16 * t, acc[t]);
-      }
-    } else {
-      if (ok) {
-#pragma unroll
-        for (int t = 0; t < NT; ++t) st4(yr + 16 * t, acc[t]);
-      }
-    }
-  }
-  if constexpr (EPI == EPI_LNB) {
-#pragma unroll
-    for (int t = 0; t < NT; ++t)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float sw = row16_sum(pw[t][r]), sb = row16_sum(pb[t][r]);
-        if (mi == 0) {
-          lred[wv * 2 * NP + 16 * t + 4 * g + r] = sw;
-          lred[wv * 2 * NP + NP + 16 * t + 4 * g + r] = sb;
-        }
-      }
-    __syncthreads();
-    float* pp = a.part + ((long)blockIdx.y * gridDim.x + blockIdx.x) * 2 * NP;
-    for (int k = threadIdx.x; k < 2 * NP; k += 256)
-      pp[k] = (lred[k] + lred[2 * NP + k]) + (lred[4 * NP + k] + lred[6 * NP + k]);
   }
 }
 
@@ -606,105 +466,6 @@ __global__ __launch_bounds__(256) void gat_param_kernel(int n, const float* __re
 }
 
 // ============================================================================
-// Self-attention over the 3 window steps (models.py:350-356, 2 heads), one
-// 32-lane half wave per (window, host): lane e = head dimension.
-// ============================================================================
-template <int H>
-__global__ __launch_bounds__(256) void attn_fwd_kernel(int B, const float* __restrict__ QKV, float* __restrict__ O,
-                                                       float* __restrict__ PR) {
-  using Q = TuneGeo<H>;
-  constexpr int HD = Q::HD;
-  const long hw = ((long)blockIdx.x * 256 + threadIdx.x) >> 5;
-  const int e = threadIdx.x & 31;
-  const bool okp = hw < (long)B * H;
-  const long b = okp ? hw / H : 0;
-  const int h = okp ? (int)(hw - b * H) : 0;
-  const bool oke = okp && e < HD;
-  const float scale = 1.0f / sqrtf((float)HD);
-  long mr[3];
-#pragma unroll
-  for (int w = 0; w < 3; ++w) mr[w] = b * Q::T + (long)w * H + h;
-  float q[2][3], k[2][3], v[2][3];
-#pragma unroll
-  for (int hh = 0; hh < 2; ++hh)
-#pragma unroll
-    for (int w = 0; w < 3; ++w) {
-      const float* rw = QKV + mr[w] * Q::Q3P + hh * HD + e;
-      q[hh][w] = oke ? rw[0] : 0.f;
-      k[hh][w] = oke ? rw[H] : 0.f;
-      v[hh][w] = oke ? rw[2 * H] : 0.f;
-    }
-#pragma unroll
-  for (int hh = 0; hh < 2; ++hh)
-#pragma unroll
-    for (int w = 0; w < 3; ++w) {
-      float sc[3];
-#pragma unroll
-      for (int w2 = 0; w2 < 3; ++w2) sc[w2] = half_sum(q[hh][w] * k[hh][w2]) * scale;
-      const float mx = fmaxf(sc[0], fmaxf(sc[1], sc[2]));
-      const float e0 = expf(sc[0] - mx), e1 = expf(sc[1] - mx), e2 = expf(sc[2] - mx);
-      const float inv = 1.0f / (e0 + e1 + e2);
-      const float p0 = e0 * inv, p1 = e1 * inv, p2 = e2 * inv;
-      if (oke) O[mr[w] * Q::DP + hh * HD + e] = fmaf(p0, v[hh][0], fmaf(p1, v[hh][1], p2 * v[hh][2]));
-      if (okp && e < 3) PR[mr[w] * 8 + hh * 3 + e] = e == 0 ? p0 : (e == 1 ? p1 : p2);
-    }
-}
-
-template <int H>
-__global__ __launch_bounds__(256) void attn_bwd_kernel(int B, const float* __restrict__ QKV,
-                                                       const float* __restrict__ PR, const float* __restrict__ dO,
-                                                       float* __restrict__ dQKV) {
-  using Q = TuneGeo<H>;
-  constexpr int HD = Q::HD;
-  const long hw = ((long)blockIdx.x * 256 + threadIdx.x) >> 5;
-  const int e = threadIdx.x & 31;
-  const bool okp = hw < (long)B * H;
-  const long b = okp ? hw / H : 0;
-  const int h = okp ? (int)(hw - b * H) : 0;
-  const bool oke = okp && e < HD;
-  const float scale = 1.0f / sqrtf((float)HD);
-  long mr[3];
-#pragma unroll
-  for (int w = 0; w < 3; ++w) mr[w] = b * Q::T + (long)w * H + h;
-#pragma unroll
-  for (int hh = 0; hh < 2; ++hh) {
-    float q[3], k[3], v[3], dov[3], p[3][3];
-#pragma unroll
-    for (int w = 0; w < 3; ++w) {
-      const float* rw = QKV + mr[w] * Q::Q3P + hh * HD + e;
-      q[w] = oke ? rw[0] : 0.f;
-      k[w] = oke ? rw[H] : 0.f;
-      v[w] = oke ? rw[2 * H] : 0.f;
-      dov[w] = oke ? dO[mr[w] * Q::DP + hh * HD + e] : 0.f;
-#pragma unroll
-      for (int w2 = 0; w2 < 3; ++w2) p[w][w2] = okp ? PR[mr[w] * 8 + hh * 3 + w2] : 0.f;
-    }
-    float dS[3][3];
-#pragma unroll
-    for (int w = 0; w < 3; ++w) {
-      float dp[3];
-#pragma unroll
-      for (int w2 = 0; w2 < 3; ++w2) dp[w2] = half_sum(dov[w] * v[w2]);
-      const float sd = p[w][0] * dp[0] + p[w][1] * dp[1] + p[w][2] * dp[2];
-#pragma unroll
-      for (int w2 = 0; w2 < 3; ++w2) dS[w][w2] = p[w][w2] * (dp[w2] - sd) * scale;
-    }
-#pragma unroll
-    for (int w = 0; w < 3; ++w) {
-      const float dq = dS[w][0] * k[0] + dS[w][1] * k[1] + dS[w][2] * k[2];
-      const float dk = dS[0][w] * q[0] + dS[1][w] * q[1] + dS[2][w] * q[2];
-      const float dv = p[0][w] * dov[0] + p[1][w] * dov[1] + p[2][w] * dov[2];
-      if (oke) {
-        float* o = dQKV + mr[w] * Q::Q3P + hh * HD + e;
-        o[0] = dq;
-        o[H] = dk;
-        o[2 * H] = dv;
-      }
-    }
-  }
-}
-
-// ============================================================================
 // Decoders (models.py:359-370, 399) and the loss gradient (train.py:27-40).
 // ============================================================================
 // Decoder weights permuted to the token layout: Wp[n][k'] with k' = tok*DP + c,
@@ -950,7 +711,6 @@ LinArgs lin_args(long M, const float* X, int ldx, const float* W, int ldw, int N
   a.bias = bias;
   a.Y = Y;
   a.ldy = ldy;
-  a.rss = 1;
   return a;
 }
 
@@ -1022,11 +782,6 @@ hipError_t dw(const TunePlan& p, RedBatch& rb, const float* Y, int ldy, const fl
                                                                                           : hipErrorInvalidValue;
 }
 
-// gamma / beta gradients from LNB partials [nparts][2][DP] (deferred)
-hipError_t ln_grads(const TunePlan& p, RedBatch& rb, int nparts, const float* part, int N, float* gw, float* gb) {
-  return rb.add(nparts, 2L * p.DP, part, 1, N, 0, gw, 0, N, p.DP, gb) ? hipSuccess : hipErrorInvalidValue;
-}
-
 template <int H>
 bool plan_h(int B, TunePlan* out) {
   using Q = TuneGeo<H>;
@@ -1051,24 +806,20 @@ bool plan_h(int B, TunePlan* out) {
   q.gs = take(3L * B * 4);
   for (int i = 0; i < 3; ++i) q.x[i] = take(M * Q::DP);
   for (int l = 0; l < 2; ++l) {
-    q.qkv[l] = take(M * Q::Q3P);
-    q.o[l] = take(M * Q::DP);
-    q.pr[l] = take(M * 8);
     q.xh1[l] = take(M * Q::DP);
     q.rs1[l] = take(M);
-    q.y1[l] = take(M * Q::DP);
-    q.f[l] = take(M * Q::FF);
-    q.xh2[l] = take(M * Q::DP);
-    q.rs2[l] = take(M);
   }
   q.da = take(M * Q::DP);
   q.db = take(M * Q::DP);
   q.dq = take(M * Q::Q3P);
-  q.df = take(M * Q::FF);
   q.gsx = take(3L * B * 8);
   q.dpre = take((long)B * Q::NOP);
   q.wp = take((long)Q::NOP * Q::KD);
   q.wpt = take((long)Q::NOP * Q::KD);
+  q.tff = take(tf_frag_floats(H));
+  q.tf_grid = tf_grid();
+  for (int l = 0; l < 2; ++l)
+    for (int k = 0; k < 2; ++k) q.tfs[l][k] = take((long)q.tf_grid * tf_slab_floats(H, 2 + k));
   const long nrb = (M + 15) / 16;
   q.lin_grid = (int)std::min<long>(PGP_LIN_CAP, std::max<long>(1, (nrb + 3) / 4));
   q.dw_grid = (int)std::min<long>(PGP_DW_CAP, std::max<long>(1, (nrb + 7) / 8));
@@ -1078,16 +829,15 @@ bool plan_h(int B, TunePlan* out) {
   q.dec_s = (int)std::max<long>(1, std::min<long>(kbt, 512 / q.dec_bg));
   // partial slabs; every bound grows with B, so a workspace sized for B_max serves any B <= B_max
   const long np_max = std::max(Q::Q3P, 64);
-  long part = (long)PGP_LIN_CAP * 2 * Q::DP;                             // linear LNB, one per workgroup
-  part = std::max(part, (long)PGP_DW_CAP * (np_max * 64 + np_max));       // dW slabs
+  long part = (long)PGP_DW_CAP * (np_max * 64 + np_max);                  // dW slabs
   part = std::max(part, std::max(512L, (long)q.dec_bg) * 64 * Q::NOP);    // decoder split-K
-  part = std::max(part, (long)Q::T * 8 * 2 * Q::DP);                      // decoder dX LNB (<= 8 x T groups)
   // decoder weight gradient: windows split over up to 4 parts of >= 8 chunks
   q.dec_dws = (int)std::max<long>(1, std::min<long>(4, (B + kDwRows - 1) / kDwRows / 8));
   if (q.dec_dws > 1) part = std::max(part, (long)q.dec_dws * (Q::T * Q::NOP * Q::DP + Q::NOP));
   q.part = take(part);
-  // the backward's deferred reductions (RedBatch): each dW / LN-gradient partial
-  // region plus its level-2 region, in the order tune_bwd_h takes them
+  // the backward's deferred reductions (RedBatch): each dW partial region plus
+  // its level-2 region, in the order tune_bwd_h takes them (the fused kernels'
+  // slabs have regions of their own, tfs)
   {
     long pool = 0;
     auto r64 = [](long n) { return (n + 63) / 64 * 64; };
@@ -1097,18 +847,13 @@ bool plan_h(int B, TunePlan* out) {
       if (ns > 1) pool += r64(ns * nout);
     };
     auto dwr = [&](long np, long kp, long n, long k, bool bias) { red(q.dw_grid, np * kp + np, n * k + (bias ? n : 0)); };
-    const long DPl = Q::DP, FFl = Q::FF, Q3Pl = Q::Q3P, Hl = H;
-    red((long)q.dec_dxg * Q::T, 2 * DPl, 2 * Hl);  // decoder dX through layer 1's norm2
-    for (int l = 1; l >= 0; --l) {
-      dwr(DPl, FFl, Hl, FFl, true);        // W2
-      dwr(FFl, DPl, FFl, Hl, true);        // W1
-      red(q.lin_grid, 2 * DPl, 2 * Hl);    // norm1
-      dwr(DPl, DPl, Hl, Hl, true);         // out_proj
-      dwr(Q3Pl, DPl, 3 * Hl, Hl, true);    // in_proj
-      if (l == 1) red(q.lin_grid, 2 * DPl, 2 * Hl);  // layer 0's norm2
-    }
+    const long DPl = Q::DP, Q3Pl = Q::Q3P, Hl = H;
+    for (int l = 1; l >= 0; --l) dwr(Q3Pl, DPl, 3 * Hl, Hl, true);  // in_proj
     dwr(DPl, DPl, Hl, Hl, true);           // time encoder
     dwr(DPl, Q::XBP, Hl, 3, false);        // GAT fc
+    // level-2 regions of the fused slabs (more than 256 workgroups)
+    const long ns = (q.tf_grid + 255) / 256;
+    if (ns > 1) pool += 2 * ns * r64(tf_slab_floats(H, 2) + tf_slab_floats(H, 3)) * 2;
     q.pool = take(pool);
     q.pool_len = pool;
   }
@@ -1121,44 +866,24 @@ template <int H>
 hipError_t tune_fwd_h(const TunePlan& p, const float* win, const float* P, float* ws, float* latent, float* logits,
                       float* protos, hipStream_t st) {
   using Q = TuneGeo<H>;
-  using G = TGeo<H>;
-  constexpr int DP = Q::DP, Q3P = Q::Q3P, FF = Q::FF;
   const int B = p.B;
-  const long M = p.M;
   hipError_t e;
   TCK((dec_pack_kernel<H><<<(int)((Q::NOP * Q::KD + 255) / 256), 256, 0, st>>>(P, ws + p.wp, ws + p.wpt)));
   TCK((gat_fwd_kernel<H><<<(3 * B + 3) / 4, 256, 0, st>>>(B, win, P, ws + p.win, ws + p.g, ws + p.xb, ws + p.gs)));
-  {  // time encoder + positional encoding (models.py:390-393)
-    LinArgs a = lin_args(M, ws + p.g, DP, P + G::W_TE, H, H, H, 0, P + G::B_TE, ws + p.x[0], DP);
-    a.pe = P + G::PE;
-    a.H = H;
-    if ((e = lin<DP, DP, EPI_PE>(p, a, st)) != hipSuccess) return e;
-  }
+  // the encoder: fragments packed from P, then one fused launch per layer
+  TfArgs t{};
+  t.B = B;
+  t.P = P;
+  t.frags = ws + p.tff;
+  if ((e = launch_tf(H, 0, t, st)) != hipSuccess) return e;
   for (int l = 0; l < 2; ++l) {
-    const float* Lp = P + G::LAY0 + l * G::L_SIZE;
-    LinArgs a = lin_args(M, ws + p.x[l], DP, Lp + G::L_IN, H, 3 * H, H, 0, Lp + G::L_INB, ws + p.qkv[l], Q3P);
-    if ((e = lin<Q3P, DP, EPI_STORE>(p, a, st)) != hipSuccess) return e;
-    TCK((attn_fwd_kernel<H><<<(int)(((long)B * H * 32 + 255) / 256), 256, 0, st>>>(B, ws + p.qkv[l], ws + p.o[l],
-                                                                                      ws + p.pr[l])));
-    a = lin_args(M, ws + p.o[l], DP, Lp + G::L_OUT, H, H, H, 0, Lp + G::L_OUTB, ws + p.y1[l], DP);
-    a.R = ws + p.x[l];
-    a.ldr = DP;
-    a.lnw = Lp + G::L_N1W;
-    a.lnb = Lp + G::L_N1B;
-    a.XH = ws + p.xh1[l];
-    a.RS = ws + p.rs1[l];
-    if ((e = lin<DP, DP, EPI_LN>(p, a, st)) != hipSuccess) return e;
-    a = lin_args(M, ws + p.y1[l], DP, Lp + G::L_W1, H, FF, H, 0, Lp + G::L_B1, ws + p.f[l], FF);
-    if ((e = lin<FF, DP, EPI_STORE>(p, a, st)) != hipSuccess) return e;
-    a = lin_args(M, ws + p.f[l], FF, Lp + G::L_W2, FF, H, FF, 0, Lp + G::L_B2, ws + p.x[l + 1], DP);
-    a.relu_x = 1;
-    a.R = ws + p.y1[l];
-    a.ldr = DP;
-    a.lnw = Lp + G::L_N2W;
-    a.lnb = Lp + G::L_N2B;
-    a.XH = ws + p.xh2[l];
-    a.RS = ws + p.rs2[l];
-    if ((e = lin<DP, FF, EPI_LN>(p, a, st)) != hipSuccess) return e;
+    t.layer = l;
+    t.in = ws + (l == 0 ? p.g : p.x[1]);
+    t.out = ws + p.x[l + 1];
+    t.x0 = ws + p.x[0];
+    t.xh1 = ws + p.xh1[l];
+    t.rs1 = ws + p.rs1[l];
+    if ((e = launch_tf(H, 1, t, st)) != hipSuccess) return e;
   }
   TCK((dec_fwd_kernel<H><<<dim3(p.dec_bg, p.dec_s), 256, 0, st>>>(B, p.dec_s, ws + p.x[2], ws + p.wp,
                                                                    ws + p.part)));
@@ -1174,7 +899,7 @@ hipError_t tune_bwd_h(const TunePlan& p, const float* P, float* Gd, float* ws, c
                       const float* protos, const int* y, const float* mult, const float* tgt, hipStream_t st) {
   using Q = TuneGeo<H>;
   using G = TGeo<H>;
-  constexpr int DP = Q::DP, Q3P = Q::Q3P, FF = Q::FF;
+  constexpr int DP = Q::DP, Q3P = Q::Q3P;
   const int B = p.B;
   const long M = p.M;
   hipError_t e;
@@ -1186,77 +911,57 @@ hipError_t tune_bwd_h(const TunePlan& p, const float* P, float* Gd, float* ws, c
     const long nw = 4L * H * G::L + 4 * H;
     TCK((dec_dw_sum_kernel<H><<<(int)((nw + 255) / 256), 256, 0, st>>>(p.dec_dws, ws + p.part, Gd)));
   }
-  {  // grad of the encoder output = dpre . Wp (token layout), through layer 1's norm2: one
-     // linear layer per token (grid.y) with that token's [DP][NOP] slab of Wp^T in LDS
-    const float* L1 = P + G::LAY0 + G::L_SIZE;
-    float* L1g = Gd + G::LAY0 + G::L_SIZE;
+  {  // grad of the encoder output = dpre . Wp (token layout): one linear layer per
+     // token (grid.y) with that token's [DP][NOP] slab of Wp^T in LDS
     LinArgs a = lin_args(B, ws + p.dpre, Q::NOP, ws + p.wpt, Q::NOP, H, 4 * H, 0, nullptr, ws + p.da, Q::T * DP);
     a.frag = 1;
-    a.XH = ws + p.xh2[1];
-    a.RS = ws + p.rs2[1];
-    a.rss = Q::T;
-    a.lnw = L1 + G::L_N2W;
-    a.part = rb.take((long)p.dec_dxg * Q::T * 2 * DP);
     a.bw = (long)DP * Q::NOP;
-    a.by = a.bxh = DP;
-    a.brs = 1;
-    TCK((linear_kernel<DP, Q::NOP, EPI_LNB><<<dim3(p.dec_dxg, Q::T), 256, 0, st>>>(a)));
-    if ((e = ln_grads(p, rb, p.dec_dxg * Q::T, a.part, H, L1g + G::L_N2W, L1g + G::L_N2B)) != hipSuccess) return e;
+    a.by = DP;
+    TCK((linear_kernel<DP, Q::NOP, EPI_STORE><<<dim3(p.dec_dxg, Q::T), 256, 0, st>>>(a)));
   }
-  const int lnb_parts = p.lin_grid;
+  // the encoder layers, fused per unit (pgp_tunef.hip); their weight-gradient
+  // slabs (one per workgroup) join the deferred reductions
+  const int ng = p.tf_grid;
   for (int l = 1; l >= 0; --l) {
-    const float* Lp = P + G::LAY0 + l * G::L_SIZE;
     float* Lg = Gd + G::LAY0 + l * G::L_SIZE;
-    // da = grad of R2 = Y1 + relu(F) W2^T + b2
-    if ((e = dw<DP, FF>(p, rb, ws + p.da, DP, ws + p.f[l], FF, 1, H, FF, Lg + G::L_W2, Lg + G::L_B2, st)) !=
-        hipSuccess)
-      return e;
-    LinArgs a = lin_args(M, ws + p.da, DP, Lp + G::L_W2, FF, FF, H, 1, nullptr, ws + p.df, FF);
-    a.R = ws + p.f[l];
-    a.ldr = FF;
-    if ((e = lin<FF, DP, EPI_MASK>(p, a, st)) != hipSuccess) return e;
-    if ((e = dw<FF, DP>(p, rb, ws + p.df, FF, ws + p.y1[l], DP, 0, FF, H, Lg + G::L_W1, Lg + G::L_B1, st)) !=
-        hipSuccess)
-      return e;
-    // db = grad of R1: (dF W1 + dR2) through norm1
-    a = lin_args(M, ws + p.df, FF, Lp + G::L_W1, H, H, FF, 1, nullptr, ws + p.db, DP);
-    a.R = ws + p.da;
-    a.ldr = DP;
-    a.XH = ws + p.xh1[l];
-    a.RS = ws + p.rs1[l];
-    a.lnw = Lp + G::L_N1W;
-    a.part = rb.take((long)lnb_parts * 2 * DP);
-    if ((e = lin<DP, FF, EPI_LNB>(p, a, st)) != hipSuccess) return e;
-    if ((e = ln_grads(p, rb, lnb_parts, a.part, H, Lg + G::L_N1W, Lg + G::L_N1B)) != hipSuccess) return e;
-    if ((e = dw<DP, DP>(p, rb, ws + p.db, DP, ws + p.o[l], DP, 0, H, H, Lg + G::L_OUT, Lg + G::L_OUTB, st)) !=
-        hipSuccess)
-      return e;
-    // da = grad of the attention output
-    a = lin_args(M, ws + p.db, DP, Lp + G::L_OUT, H, H, H, 1, nullptr, ws + p.da, DP);
-    if ((e = lin<DP, DP, EPI_STORE>(p, a, st)) != hipSuccess) return e;
-    TCK((attn_bwd_kernel<H><<<(int)(((long)B * H * 32 + 255) / 256), 256, 0, st>>>(B, ws + p.qkv[l], ws + p.pr[l],
-                                                                                       ws + p.da, ws + p.dq)));
+    TfArgs t{};
+    t.layer = l;
+    t.B = B;
+    t.P = P;
+    t.frags = ws + p.tff;
+    // feed-forward block: dOut (p.da) -> dR1 (p.db)
+    t.in = ws + p.da;
+    t.out = ws + p.db;
+    t.xh1 = ws + p.xh1[l];
+    t.rs1 = ws + p.rs1[l];
+    t.part = ws + p.tfs[l][0];
+    if ((e = launch_tf(H, 2, t, st)) != hipSuccess) return e;
+    {
+      const long sl = tf_slab_floats(H, 2);
+      const float* s0 = ws + p.tfs[l][0];
+      // slab: dW2 [H][64] | db2 [H] | dW1 [64][H] | db1 [64] | g1 | b1 | g2 | b2 (pgp_tunef.hip BffL)
+      const long oW1 = (long)H * 64 + H, oG1 = oW1 + 64L * H + 64, oG2 = oG1 + 2L * H;
+      bool ok = rb.add(ng, sl, s0, H, 64, 64, Lg + G::L_W2, 64, H, (long)H * 64, Lg + G::L_B2);
+      ok = ok && rb.add(ng, sl, s0 + oW1, 64, H, H, Lg + G::L_W1, H, 64, 64L * H, Lg + G::L_B1);
+      ok = ok && rb.add(ng, sl, s0 + oG1, 1, H, 0, Lg + G::L_N1W, 0, H, H, Lg + G::L_N1B);
+      ok = ok && rb.add(ng, sl, s0 + oG2, 1, H, 0, Lg + G::L_N2W, 0, H, H, Lg + G::L_N2B);
+      if (!ok) return hipErrorInvalidValue;
+    }
+    // attention block: dR1 (p.db), X_l -> dX_l (p.da), dQKV (p.dq)
+    t.in = ws + p.db;
+    t.out = ws + p.da;
+    t.x = ws + p.x[l];
+    t.dqkv = ws + p.dq;
+    t.part = ws + p.tfs[l][1];
+    if ((e = launch_tf(H, 3, t, st)) != hipSuccess) return e;
+    if (!rb.add(ng, tf_slab_floats(H, 3), ws + p.tfs[l][1], H, H, H, Lg + G::L_OUT, H, H, (long)H * H,
+                Lg + G::L_OUTB))
+      return hipErrorInvalidValue;
     if ((e = dw<Q3P, DP>(p, rb, ws + p.dq, Q3P, ws + p.x[l], DP, 0, 3 * H, H, Lg + G::L_IN, Lg + G::L_INB, st)) !=
         hipSuccess)
       return e;
-    // grad of the layer input: dQKV Win + dR1 (residual); for l = 1 through layer 0's norm2
-    a = lin_args(M, ws + p.dq, Q3P, Lp + G::L_IN, H, H, 3 * H, 1, nullptr, ws + p.da, DP);
-    a.R = ws + p.db;
-    a.ldr = DP;
-    if (l == 1) {
-      const float* L0 = P + G::LAY0;
-      float* L0g = Gd + G::LAY0;
-      a.XH = ws + p.xh2[0];
-      a.RS = ws + p.rs2[0];
-      a.lnw = L0 + G::L_N2W;
-      a.part = rb.take((long)lnb_parts * 2 * DP);
-      if ((e = lin<DP, Q3P, EPI_LNB>(p, a, st)) != hipSuccess) return e;
-      if ((e = ln_grads(p, rb, lnb_parts, a.part, H, L0g + G::L_N2W, L0g + G::L_N2B)) != hipSuccess) return e;
-    } else {
-      if ((e = lin<DP, Q3P, EPI_RES>(p, a, st)) != hipSuccess) return e;
-    }
   }
-  // time encoder: da = grad of X0
+  // time encoder: p.da = grad of X0
   if ((e = dw<DP, DP>(p, rb, ws + p.da, DP, ws + p.g, DP, 0, H, H, Gd + G::W_TE, Gd + G::B_TE, st)) != hipSuccess)
     return e;
   {

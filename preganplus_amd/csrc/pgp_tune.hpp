@@ -1,11 +1,12 @@
-// pgp_tune.hpp — geometry and workspace plan of the tuning step (train.py:42-57)
-// as token-major fp32 MFMA GEMMs (pgp_tune.hip).
+// pgp_tune.hpp — geometry and workspace plan of the tuning step (train.py:42-57).
 //
-// Every activation of the Transformer forward is a row-major [M][ld] array over
-// the batch's M = B * 3H tokens, token row m = b*3H + w*H + h (the reference's
-// [S=W, N=H, d] order per window, models.py:387-396).  Feature widths are padded
-// to multiples of 16 with zeros (d = H -> DP, 3d -> Q3P), so every GEMM k-block
-// is a whole float4 per lane and pads contribute exact zeros.
+// The buffers between its kernels are row-major [M][ld] arrays over the batch's
+// M = B * 3H tokens, token row m = b*3H + w*H + h (the reference's [S=W, N=H, d]
+// order per window, models.py:387-396), feature widths zero-padded to multiples
+// of 16 (d = H -> DP, 3d -> Q3P).  The encoder layers themselves run as fused
+// per-unit kernels (pgp_tunef.hip) that keep a layer's activations in registers;
+// only layer inputs, norm1's x-hat / rstd and the gradients between layers
+// cross HBM.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -34,13 +35,13 @@ struct TunePlan {
   long win = 0;                                          // [B][9H] copy of the input windows
   long g = 0, xb = 0, gs = 0;                            // GAT out [M][DP], x-bar [M][16], (max, Z) [3B][4]
   long x[3] = {0, 0, 0};                                 // layer inputs; x[2] = encoder output [M][DP]
-  long qkv[2] = {0, 0}, o[2] = {0, 0}, pr[2] = {0, 0};   // [M][Q3P], [M][DP], probs [M][8]
-  long xh1[2] = {0, 0}, rs1[2] = {0, 0}, y1[2] = {0, 0}; // LN1 x-hat [M][DP], rstd [M], output [M][DP]
-  long f[2] = {0, 0}, xh2[2] = {0, 0}, rs2[2] = {0, 0};  // FFN pre-activation [M][64], LN2 x-hat, rstd
-  long da = 0, db = 0, dq = 0, df = 0;                   // backward temporaries
+  long xh1[2] = {0, 0}, rs1[2] = {0, 0};                 // norm1 x-hat [M][DP], rstd [M] (checkpoints)
+  long da = 0, db = 0, dq = 0;                           // backward temporaries ([M][DP], [M][DP], [M][Q3P])
   long gsx = 0, dpre = 0, wp = 0, wpt = 0, part = 0, total = 0;
+  long tff = 0;                                          // fused-kernel weight fragments (pgp_tunef.hpp)
+  long tfs[2][2] = {{0, 0}, {0, 0}};                     // [layer][ffn | attention] weight-gradient slabs
   long pool = 0, pool_len = 0;  // the backward's deferred-reduction regions (RedBatch)
-  int lin_grid = 0, dw_grid = 0, dec_s = 0, dec_bg = 0, dec_dxg = 0, dec_dws = 1;
+  int lin_grid = 0, dw_grid = 0, dec_s = 0, dec_bg = 0, dec_dxg = 0, dec_dws = 1, tf_grid = 0;
 };
 
 bool tune_plan(int H, int B, TunePlan* p);

@@ -1,0 +1,1046 @@
+// pgp_tunef.hip — the tuning step's Transformer encoder (models.py:344-356,
+// 390-396; train.py:42-57) as fused per-unit kernels, windows on lanes.
+//
+// A unit is 16 (window, host) pairs, p = b*H + h (16u .. 16u+15); lane column
+// j = lane & 15 is pair 16u + j and its 3 window steps are 3 column tiles, so
+// the 3-step attention is lane-local and every activation of a layer lives in
+// v_mfma_f32_16x16x4_f32 accumulators: feature row c = 16t + 4g + r in tile t,
+// lane group g = lane >> 4, register r ("N layout", the natural row order of
+// the token-major buffers, so a tile row group is one 16-byte load).  Weights
+// are A-operand fragments packed from the master P each step (tf_pack_kernel)
+// and held in LDS; an activation register is directly the B operand of the
+// next GEMM.  Per layer:
+//   tf_fwd      X -> q|k|v -> attention -> out_proj + X -> LN1 -> FFN -> LN2,
+//               storing only X, LN1's x-hat / rstd and the layer output;
+//   tf_bwd_ffn  from dOut (grad of the layer output): recompute the FFN from
+//               LN1's x-hat, LN2 / linear2 / linear1 / LN1 backward -> dR1;
+//               dW2, dW1 (+ biases) and both LayerNorms' gamma / beta
+//               gradients accumulated in registers over the wave's units;
+//   tf_bwd_att  from dR1: recompute q|k|v and the attention from X, out_proj /
+//               attention / in_proj backward -> dX; dWo (+ bias) in registers;
+//               dQKV to HBM for in_proj's weight gradient (tall contraction).
+// Weight gradients contract over tokens, which sit on lane columns: each step's
+// 16 tokens are staged through a per-wave LDS scratch ([token][row]) and read
+// back with the token as the MFMA k index (lane group g <-> tokens 4g..4g+3,
+// one k-step per register).  The waves of a workgroup combine their registers
+// in a fixed order at the end, one partial slab per workgroup, reduced in a
+// fixed order by the tuning step's deferred reduction: deterministic.
+#include <hip/hip_runtime.h>
+
+#include "pgp_device.hpp"
+#include "pgp_gemm.hpp"
+#include "pgp_train.hpp"
+#include "pgp_tune.hpp"
+#include "pgp_tunef.hpp"
+
+namespace pgp {
+namespace {
+
+constexpr int kTfWaves = 4;  // one wave per SIMD (the backward needs > 256 registers)
+
+// fragment group of matrix `mat`: float offset ((tile * KG + q) * 64 + lane) * 4 + e
+// holds A[i = lane & 15][k = lane >> 4] of k-step 4q + e of output tile `tile`
+template <int H>
+PGP_DEV float tf_frag_value(const float* __restrict__ P, int layer, int mat, int tile, int ks, int lane) {
+  using F = TF<H>;
+  using G = TGeo<H>;
+  const int i = lane & 15, g = lane >> 4;
+  const float* L = P + G::LAY0 + (long)layer * G::L_SIZE;
+  auto dfeat = [&](int s) { return 16 * (s >> 2) + 4 * g + (s & 3); };  // d-space k-step -> feature
+  switch (mat) {
+    case TFM_TE: {  // out d, in d
+      if (ks >= F::KS) return 0.f;
+      const int n = 16 * tile + i, c = dfeat(ks);
+      return (n < H && c < H) ? P[G::W_TE + n * H + c] : 0.f;
+    }
+    case TFM_IN: {  // out q|k|v tiles, in d
+      if (ks >= F::KS) return 0.f;
+      const int part = tile / F::NT, n = 16 * (tile - part * F::NT) + i, c = dfeat(ks);
+      return (n < H && c < H) ? L[G::L_IN + (long)(part * H + n) * H + c] : 0.f;
+    }
+    case TFM_O: {  // out d, in d
+      if (ks >= F::KS) return 0.f;
+      const int n = 16 * tile + i, c = dfeat(ks);
+      return (n < H && c < H) ? L[G::L_OUT + n * H + c] : 0.f;
+    }
+    case TFM_F1: {  // out hidden, in d
+      if (ks >= F::KS) return 0.f;
+      const int u = 16 * tile + i, c = dfeat(ks);
+      return c < H ? L[G::L_W1 + u * H + c] : 0.f;
+    }
+    case TFM_F2: {  // out d, in hidden
+      const int n = 16 * tile + i, u = dfeat(ks);
+      return n < H ? L[G::L_W2 + n * 64 + u] : 0.f;
+    }
+    case TFM_F2T: {  // out hidden, in d: W2^T
+      if (ks >= F::KS) return 0.f;
+      const int u = 16 * tile + i, n = dfeat(ks);
+      return n < H ? L[G::L_W2 + n * 64 + u] : 0.f;
+    }
+    case TFM_F1T: {  // out d, in hidden: W1^T
+      const int c = 16 * tile + i, u = dfeat(ks);
+      return c < H ? L[G::L_W1 + u * H + c] : 0.f;
+    }
+    case TFM_INT: {  // out d, in q|k|v rows: Win^T
+      if (ks >= F::KSQ) return 0.f;
+      const int part = ks / F::KS, s = ks - part * F::KS, n = dfeat(s), c = 16 * tile + i;
+      return (n < H && c < H) ? L[G::L_IN + (long)(part * H + n) * H + c] : 0.f;
+    }
+    case TFM_OT: {  // out d (attention output feature), in d (dR1 feature): Wo^T
+      if (ks >= F::KS) return 0.f;
+      const int c = 16 * tile + i, n = dfeat(ks);
+      return (n < H && c < H) ? L[G::L_OUT + n * H + c] : 0.f;
+    }
+  }
+  return 0.f;
+}
+
+template <int H>
+__global__ __launch_bounds__(256) void tf_pack_kernel(const float* __restrict__ P, float* __restrict__ frags) {
+  using F = TF<H>;
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= F::TOTAL_FLOATS) return;
+  const int e = (int)(idx & 3), lane = (int)((idx >> 2) & 63);
+  const long grp = idx >> 8;  // 1-KiB group
+  int layer, mat;
+  long gi;
+  F::locate(grp, layer, mat, gi);
+  const int kg = F::mat_kg(mat);
+  const int tile = (int)(gi / kg), q = (int)(gi - (long)tile * kg);
+  frags[idx] = tf_frag_value<H>(P, layer < 0 ? 0 : layer, mat, tile, 4 * q + e, lane);
+}
+
+// ---------------------------------------------------------------------------
+// unit addressing: token-major row of pair p at window step w
+template <int H>
+PGP_DEV long tf_row(long p, int w) {
+  const long b = p / H;
+  return b * 3 * H + (long)w * H + (p - b * H);
+}
+
+// N-layout tiles <-> token-major [M][ld] rows (16-byte row groups)
+template <int NTL>
+PGP_DEV void load_tiles(f32x4 (&v)[NTL][3], const float* __restrict__ base, int ld, const long (&row)[3], bool ok,
+                        int g) {
+#pragma unroll
+  for (int w = 0; w < 3; ++w)
+#pragma unroll
+    for (int t = 0; t < NTL; ++t) v[t][w] = ok ? ld4(base + row[w] * ld + 16 * t + 4 * g) : zero4();
+}
+template <int NTL>
+PGP_DEV void store_tiles(const f32x4 (&v)[NTL][3], float* __restrict__ base, int ld, const long (&row)[3], bool ok,
+                         int g) {
+  if (!ok) return;
+#pragma unroll
+  for (int w = 0; w < 3; ++w)
+#pragma unroll
+    for (int t = 0; t < NTL; ++t) st4(base + row[w] * ld + 16 * t + 4 * g, v[t][w]);
+}
+
+// acc[o][w] += A . B over KSn k-steps; A = NO tiles of fragment groups in LDS
+// (KG groups per tile), B k-step s for step w = bsrc(s, w)
+template <int NO, int KSn, class BF>
+PGP_DEV void tf_gemm(f32x4 (&acc)[NO][3], const float* A, BF bsrc, int lane) {
+  constexpr int KGn = (KSn + 3) / 4;
+#pragma unroll
+  for (int o = 0; o < NO; ++o) {
+#pragma unroll
+    for (int q = 0; q < KGn; ++q) {
+      const f32x4 a = ld4(A + ((o * KGn + q) * 64 + lane) * 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (4 * q + e < KSn) {
+#pragma unroll
+          for (int w = 0; w < 3; ++w) acc[o][w] = mfma(a[e], bsrc(4 * q + e, w), acc[o][w]);
+        }
+    }
+    // one output tile at a time: keeps the scheduler from hoisting every tile's
+    // LDS fragments (register pressure)
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// accumulators initialised with a per-row bias (LDS, natural rows)
+template <int NO>
+PGP_DEV void init_bias(f32x4 (&acc)[NO][3], const float* bias, int g) {
+#pragma unroll
+  for (int o = 0; o < NO; ++o) {
+    const f32x4 b = ld4(bias + 16 * o + 4 * g);
+#pragma unroll
+    for (int w = 0; w < 3; ++w) acc[o][w] = b;
+  }
+}
+
+// LayerNorm (eps 1e-5, biased variance) of each step's feature column, in
+// place: v becomes x-hat (pads 0); rs[w] = rstd.  Two-pass, masked (as
+// pgp_tune.hip's ln_rows).
+template <int H, int NTL>
+PGP_DEV void tf_ln(f32x4 (&v)[NTL][3], float (&rs)[3], int g) {
+  float s[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+  for (int w = 0; w < 3; ++w)
+#pragma unroll
+    for (int t = 0; t < NTL; ++t) s[w] += (v[t][w][0] + v[t][w][1]) + (v[t][w][2] + v[t][w][3]);
+  xsum2(s[0], s[1]);
+  s[2] = xsum(s[2], true);
+  float q[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+  for (int w = 0; w < 3; ++w) {
+    const float mu = s[w] / (float)H;
+#pragma unroll
+    for (int t = 0; t < NTL; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float dv = (16 * t + 4 * g + r < H) ? v[t][w][r] - mu : 0.f;
+        v[t][w][r] = dv;
+        q[w] = fmaf(dv, dv, q[w]);
+      }
+  }
+  xsum2(q[0], q[1]);
+  q[2] = xsum(q[2], true);
+#pragma unroll
+  for (int w = 0; w < 3; ++w) {
+    rs[w] = 1.0f / sqrtf(q[w] / (float)H + 1e-5f);
+#pragma unroll
+    for (int t = 0; t < NTL; ++t) v[t][w] = v[t][w] * rs[w];
+  }
+}
+
+// per-unit token sums of an N-layout quantity, compressed: v[t][r] holds this
+// lane's (one token column's) partial for row 16t+4g+r; the sum over the 16
+// token lanes is added to acc on lane j = 4t + r, so lane (g, j) accumulates row
+// 16(j/4) + 4g + (j%4) (DP <= 64).  One register per gradient vector.
+template <int NTL>
+PGP_DEV void acc_rows(float& acc, const f32x4 (&v)[NTL], int j) {
+  // opaque to the optimiser: otherwise it hoists the loop-invariant lane test
+  // out of the unit loop and keeps 16 accumulators per vector instead of one
+  asm volatile("" : "+v"(j));
+#pragma unroll
+  for (int t = 0; t < NTL; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float sm = row16_sum(v[t][r]);
+      acc += (j == 4 * t + r) ? sm : 0.f;
+    }
+}
+
+// LayerNorm backward in place: dy (grad of the output) -> grad of the input,
+// from x-hat xh, rstd rs and gamma (LDS); the gamma / beta gradients of the
+// unit's tokens are added to the compressed accumulators ag / ab (acc_rows).
+template <int H, int NTL>
+PGP_DEV void tf_ln_bwd(f32x4 (&dy)[NTL][3], const f32x4 (&xh)[NTL][3], const float (&rs)[3], const float* gam, int g,
+                       int j, float& ag, float& ab) {
+  float s1[3] = {0.f, 0.f, 0.f}, s2[3] = {0.f, 0.f, 0.f};
+  asm volatile("" : "+v"(j));
+#pragma unroll
+  for (int t = 0; t < NTL; ++t) {
+    const f32x4 ga = ld4(gam + 16 * t + 4 * g);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float pg = 0.f, pb = 0.f;
+#pragma unroll
+      for (int w = 0; w < 3; ++w) {
+        pg = fmaf(dy[t][w][r], xh[t][w][r], pg);
+        pb += dy[t][w][r];
+        const float d = dy[t][w][r] * ga[r];
+        dy[t][w][r] = d;
+        s1[w] += d;
+        s2[w] = fmaf(d, xh[t][w][r], s2[w]);
+      }
+      // gamma / beta sums of this row over the unit's tokens (acc_rows)
+      pg = row16_sum(pg);
+      pb = row16_sum(pb);
+      ag += (j == 4 * t + r) ? pg : 0.f;
+      ab += (j == 4 * t + r) ? pb : 0.f;
+    }
+  }
+  xsum2(s1[0], s1[1]);
+  xsum2(s1[2], s2[0]);
+  xsum2(s2[1], s2[2]);
+#pragma unroll
+  for (int w = 0; w < 3; ++w) {
+    const float m1 = s1[w] / (float)H, m2 = s2[w] / (float)H;
+#pragma unroll
+    for (int t = 0; t < NTL; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        dy[t][w][r] = (16 * t + 4 * g + r < H) ? rs[w] * (dy[t][w][r] - m1 - xh[t][w][r] * m2) : 0.f;
+  }
+}
+
+// self-attention over the 3 steps (2 heads, scale 1/sqrt(H/2)); QKV tiles
+// [q: 0..NT) [k: NT..2NT) [v: 2NT..3NT); P[head][query w][key w2]
+template <int H>
+PGP_DEV void tf_attn_fwd(const f32x4 (&Q)[3 * TF<H>::NT][3], float (&P)[2][3][3], f32x4 (&O)[TF<H>::NT][3], int g) {
+  using F = TF<H>;
+  constexpr int NT = F::NT;
+  float s[2][3][3];
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+    for (int w = 0; w < 3; ++w)
+#pragma unroll
+      for (int w2 = 0; w2 < 3; ++w2) s[hh][w][w2] = 0.f;
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int c = 16 * t + 4 * g + r;
+      const bool h0 = c < F::HD, h1 = c >= F::HD && c < H;
+#pragma unroll
+      for (int w = 0; w < 3; ++w)
+#pragma unroll
+        for (int w2 = 0; w2 < 3; ++w2) {
+          const float pr = Q[t][w][r] * Q[NT + t][w2][r];
+          s[0][w][w2] += h0 ? pr : 0.f;
+          s[1][w][w2] += h1 ? pr : 0.f;
+        }
+    }
+  float* f = &s[0][0][0];
+#pragma unroll
+  for (int i = 0; i < 18; i += 2) xsum2(f[i], f[i + 1]);
+  const float scale = 1.0f / sqrtf((float)F::HD);
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+    for (int w = 0; w < 3; ++w) {
+      const float a0 = s[hh][w][0] * scale, a1 = s[hh][w][1] * scale, a2 = s[hh][w][2] * scale;
+      const float mx = fmaxf(a0, fmaxf(a1, a2));
+      const float e0 = expf(a0 - mx), e1 = expf(a1 - mx), e2 = expf(a2 - mx);
+      const float inv = 1.0f / (e0 + e1 + e2);
+      P[hh][w][0] = e0 * inv;
+      P[hh][w][1] = e1 * inv;
+      P[hh][w][2] = e2 * inv;
+    }
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int c = 16 * t + 4 * g + r;
+      const int hh = c < F::HD ? 0 : 1;
+#pragma unroll
+      for (int w = 0; w < 3; ++w) {
+        const float p0 = hh ? P[1][w][0] : P[0][w][0], p1 = hh ? P[1][w][1] : P[0][w][1],
+                    p2 = hh ? P[1][w][2] : P[0][w][2];
+        O[t][w][r] = fmaf(p0, Q[2 * NT + t][0][r], fmaf(p1, Q[2 * NT + t][1][r], p2 * Q[2 * NT + t][2][r]));
+      }
+    }
+}
+
+// per-wave LDS scratch for the weight-gradient contractions: one step's 16
+// tokens of an N-layout operand as [token][row] (pitch PITCH floats)
+template <int NTL>
+struct Scr {
+  static constexpr int PITCH = 16 * NTL + 4;
+  static constexpr int SIZE = 16 * PITCH;
+};
+template <int NTL>
+PGP_DEV void stage(const f32x4 (&v)[NTL][3], int w, float* s, int g, int j) {
+#pragma unroll
+  for (int t = 0; t < NTL; ++t) st4(s + j * Scr<NTL>::PITCH + 16 * t + 4 * g, v[t][w]);
+}
+// the same for a value computed per tile (fn(t) -> f32x4)
+template <int NTL, class FN>
+PGP_DEV void stage_fn(FN fn, float* s, int g, int j) {
+#pragma unroll
+  for (int t = 0; t < NTL; ++t) st4(s + j * Scr<NTL>::PITCH + 16 * t + 4 * g, fn(t));
+}
+// acc[T][U] += sum over the step's 16 tokens of A[16T+4g+r][tok] B[16U+j][tok]
+// (k-step e <-> token 4g + e); bsum[T] += the A values read (its token sum)
+template <int NA, int NB>
+PGP_DEV void dw_step(f32x4 (&acc)[NA][NB], float (&bsum)[NA], const float* sa, const float* sb, int g, int i) {
+  float a[NA][4], b[NB][4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+#pragma unroll
+    for (int T = 0; T < NA; ++T) a[T][e] = sa[(4 * g + e) * Scr<NA>::PITCH + 16 * T + i];
+#pragma unroll
+    for (int U = 0; U < NB; ++U) b[U][e] = sb[(4 * g + e) * Scr<NB>::PITCH + 16 * U + i];
+  }
+#pragma unroll
+  for (int T = 0; T < NA; ++T) bsum[T] += (a[T][0] + a[T][1]) + (a[T][2] + a[T][3]);
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+#pragma unroll
+    for (int T = 0; T < NA; ++T)
+#pragma unroll
+      for (int U = 0; U < NB; ++U) acc[T][U] = mfma(a[T][e], b[U][e], acc[T][U]);
+}
+
+// unit range of one wave (contiguous, balanced over all waves of the grid)
+PGP_DEV void unit_range(long nu, long& u0, long& u1) {
+  const long nw = (long)gridDim.x * kTfWaves;
+  const long wv = (long)blockIdx.x * kTfWaves + (threadIdx.x >> 6);
+  u0 = nu * wv / nw;
+  u1 = nu * (wv + 1) / nw;
+}
+
+// LDS parameter block of a layer (natural rows, zero-padded)
+template <int H>
+struct TfPar {
+  using F = TF<H>;
+  static constexpr int BIN = 0;                       // [NQ*16] in_proj bias in q|k|v tiles
+  static constexpr int BO = BIN + F::NQ * 16;         // [DP]
+  static constexpr int N1W = BO + F::DP, N1B = N1W + F::DP;
+  static constexpr int B1 = N1B + F::DP;              // [64]
+  static constexpr int B2 = B1 + 64;                  // [DP]
+  static constexpr int N2W = B2 + F::DP, N2B = N2W + F::DP;
+  static constexpr int BTE = N2B + F::DP;             // [3][DP] time-encoder bias + pe[w]
+  static constexpr int SIZE = BTE + 3 * F::DP;
+};
+template <int H>
+PGP_DEV void load_params(float* sp, const float* __restrict__ P, int layer) {
+  using F = TF<H>;
+  using G = TGeo<H>;
+  using Q = TfPar<H>;
+  const float* L = P + G::LAY0 + (long)layer * G::L_SIZE;
+  for (int k = threadIdx.x; k < Q::SIZE; k += blockDim.x) {
+    float v = 0.f;
+    if (k < Q::BO) {
+      const int part = k / F::DP, n = k - part * F::DP;
+      v = n < H ? L[G::L_INB + part * H + n] : 0.f;
+    } else if (k < Q::BTE) {
+      const int sec = k < Q::N1W ? 0 : k < Q::N1B ? 1 : k < Q::B1 ? 2 : k < Q::B2 ? 3 : k < Q::N2W ? 4 : k < Q::N2B ? 5 : 6;
+      const int base[7] = {Q::BO, Q::N1W, Q::N1B, Q::B1, Q::B2, Q::N2W, Q::N2B};
+      const long src[7] = {G::L_OUTB, G::L_N1W, G::L_N1B, G::L_B1, G::L_B2, G::L_N2W, G::L_N2B};
+      const int n = k - base[sec];
+      const int lim = sec == 3 ? 64 : H;
+      v = n < lim ? L[src[sec] + n] : 0.f;
+    } else {
+      const int w = (k - Q::BTE) / F::DP, n = (k - Q::BTE) - w * F::DP;
+      v = n < H ? P[G::B_TE + n] + P[G::PE + w * H + n] : 0.f;
+    }
+    sp[k] = v;
+  }
+}
+
+// ============================================================================
+// forward of one layer (layer 0 includes the time encoder + PE)
+// ============================================================================
+template <int H>
+struct FwdL {
+  using F = TF<H>;
+  static constexpr int W_TE = 0, W_IN = W_TE + F::G_TE * 256, W_O = W_IN + F::G_IN * 256,
+                       W_F1 = W_O + F::G_O * 256, W_F2 = W_F1 + F::G_F1 * 256, PAR = W_F2 + F::G_F2 * 256,
+                       TOTAL = PAR + TfPar<H>::SIZE;
+};
+
+template <int H>
+__global__ __launch_bounds__(kTfWaves * 64, 1) void tf_fwd_kernel(TfArgs a) {
+  using F = TF<H>;
+  using L = FwdL<H>;
+  using Q = TfPar<H>;
+  constexpr int NT = F::NT;
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, g = lane >> 4, j = lane & 15;
+  const int layer = a.layer;
+  const float* fr = a.frags + F::layer_off(layer);
+  if (layer == 0) dma_groups(a.frags + F::TE_OFF, sm + L::W_TE, F::G_TE, wv, kTfWaves, lane);
+  dma_groups(fr + F::OFF_IN, sm + L::W_IN, F::G_IN + F::G_O + F::G_F1 + F::G_F2, wv, kTfWaves, lane);
+  load_params<H>(sm + L::PAR, a.P, layer);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const float* par = sm + L::PAR;
+  const long npairs = (long)a.B * H, nu = (npairs + 15) / 16;
+  long u0, u1;
+  unit_range(nu, u0, u1);
+#pragma unroll 1
+  for (long u = u0; u < u1; ++u) {
+    const long p = u * 16 + j;
+    const bool ok = p < npairs;
+    long row[3];
+#pragma unroll
+    for (int w = 0; w < 3; ++w) row[w] = ok ? tf_row<H>(p, w) : 0;
+    f32x4 X[NT][3];
+    if (layer == 0) {  // X0 = Wte g + bte + pe[w]  (models.py:390-393)
+      f32x4 Gi[NT][3];
+      load_tiles<NT>(Gi, a.in, F::DP, row, ok, g);
+#pragma unroll
+      for (int o = 0; o < NT; ++o)
+#pragma unroll
+        for (int w = 0; w < 3; ++w) X[o][w] = ld4(par + Q::BTE + w * F::DP + 16 * o + 4 * g);
+      tf_gemm<NT, F::KS>(X, sm + L::W_TE, [&](int s, int w) { return Gi[s >> 2][w][s & 3]; }, lane);
+      store_tiles<NT>(X, a.x0, F::DP, row, ok, g);
+    } else {
+      load_tiles<NT>(X, a.in, F::DP, row, ok, g);
+    }
+    f32x4 QKV[F::NQ][3];
+    init_bias<F::NQ>(QKV, par + Q::BIN, g);
+    tf_gemm<F::NQ, F::KS>(QKV, sm + L::W_IN, [&](int s, int w) { return X[s >> 2][w][s & 3]; }, lane);
+    float Pr[2][3][3];
+    f32x4 O[NT][3];
+    tf_attn_fwd<H>(QKV, Pr, O, g);
+    f32x4 R[NT][3];
+    init_bias<NT>(R, par + Q::BO, g);
+    tf_gemm<NT, F::KS>(R, sm + L::W_O, [&](int s, int w) { return O[s >> 2][w][s & 3]; }, lane);
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int w = 0; w < 3; ++w) R[t][w] += X[t][w];
+    float rs[3];
+    tf_ln<H, NT>(R, rs, g);  // R = x-hat of norm1
+    store_tiles<NT>(R, a.xh1, F::DP, row, ok, g);
+    if (ok && g == 0) {
+#pragma unroll
+      for (int w = 0; w < 3; ++w) a.rs1[row[w]] = rs[w];
+    }
+    // y1 = gamma1 x-hat + beta1 (in place of X: the residual of the FFN)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const f32x4 ga = ld4(par + Q::N1W + 16 * t + 4 * g), be = ld4(par + Q::N1B + 16 * t + 4 * g);
+#pragma unroll
+      for (int w = 0; w < 3; ++w) X[t][w] = R[t][w] * ga + be;
+    }
+    f32x4 Fh[4][3];
+    init_bias<4>(Fh, par + Q::B1, g);
+    tf_gemm<4, F::KS>(Fh, sm + L::W_F1, [&](int s, int w) { return X[s >> 2][w][s & 3]; }, lane);
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int w = 0; w < 3; ++w)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Fh[t][w][r] = fmaxf(Fh[t][w][r], 0.f);
+    init_bias<NT>(R, par + Q::B2, g);
+    tf_gemm<NT, 16>(R, sm + L::W_F2, [&](int s, int w) { return Fh[s >> 2][w][s & 3]; }, lane);
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int w = 0; w < 3; ++w) R[t][w] += X[t][w];
+    tf_ln<H, NT>(R, rs, g);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const f32x4 ga = ld4(par + Q::N2W + 16 * t + 4 * g), be = ld4(par + Q::N2B + 16 * t + 4 * g);
+#pragma unroll
+      for (int w = 0; w < 3; ++w) R[t][w] = R[t][w] * ga + be;
+    }
+    store_tiles<NT>(R, a.out, F::DP, row, ok, g);
+  }
+}
+
+// ============================================================================
+// end-of-kernel combination: each wave adds its register partial into the
+// workgroup's LDS slab in wave order (deterministic), then the slab is written
+// ============================================================================
+PGP_DEV void slab_zero(float* s, int n) {
+  for (int k = threadIdx.x; k < n; k += blockDim.x) s[k] = 0.f;
+}
+PGP_DEV void slab_out(const float* s, float* dst, int n) {
+  for (int k = threadIdx.x; k < n; k += blockDim.x) dst[k] = s[k];
+}
+
+// compressed row accumulator (acc_rows) -> slab[row] for rows < lim
+PGP_DEV void add_rows_c(float* slab, float acc, int lim, int g, int j) {
+  const int n = 16 * (j >> 2) + 4 * g + (j & 3);
+  if (n < lim) slab[n] += acc;
+}
+// bias sums bsum[T] (per lane: row 16T + i, this lane group's tokens) -> slab
+template <int NA>
+PGP_DEV void add_bias(float* slab, const float (&b)[NA], int lim, int g, int i) {
+#pragma unroll
+  for (int T = 0; T < NA; ++T) {
+    const float s = xsum(b[T], true);
+    const int n = 16 * T + i;
+    if (g == 0 && n < lim) slab[n] += s;
+  }
+}
+// dW tile sums acc[T][U] (row 16T+4g+r, column 16U+j) -> slab[row * ld + col]
+template <int NA, int NB>
+PGP_DEV void add_dw(float* slab, const f32x4 (&acc)[NA][NB], int rows, int cols, int ld, int g, int j) {
+#pragma unroll
+  for (int T = 0; T < NA; ++T)
+#pragma unroll
+    for (int U = 0; U < NB; ++U)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = 16 * T + 4 * g + r, c = 16 * U + j;
+        if (n < rows && c < cols) slab[n * ld + c] += acc[T][U][r];
+      }
+}
+
+// ============================================================================
+// backward of a layer's feed-forward block (models.py:356: norm2(y1 + FFN(y1)),
+// y1 = norm1(.)): dOut -> dR1 (grad of norm1's input)
+// ============================================================================
+template <int H>
+struct BffL {
+  using F = TF<H>;
+  static constexpr int W_F1 = 0, W_F2 = W_F1 + F::G_F1 * 256, W_F2T = W_F2 + F::G_F2 * 256,
+                       W_F1T = W_F2T + F::G_F2T * 256, PAR = W_F1T + F::G_F1T * 256,
+                       SCR = PAR + TfPar<H>::SIZE,
+                       SCR_A = Scr<4>::SIZE, SCR_B = Scr<4>::SIZE,  // both operands <= 64 rows
+                       ACC = SCR + kTfWaves * (SCR_A + SCR_B),     // dW2 | dW1 accumulator tiles
+                       NTILE = 2 * F::NT * 4,                     // [NT][4] + [4][NT] tiles of 256 floats
+                       TOTAL = ACC + NTILE * 256;
+  static constexpr int S_W2 = 0, S_B2 = S_W2 + H * 64, S_W1 = S_B2 + H, S_B1 = S_W1 + 64 * H,
+                       S_G1 = S_B1 + 64, S_BT1 = S_G1 + H, S_G2 = S_BT1 + H, S_BT2 = S_G2 + H,
+                       SLAB = S_BT2 + H;
+};
+
+// Add a unit's dW tiles (registers) into the workgroup's LDS accumulators
+// (tile-major, per-lane f32x4) in kTfWaves rounds separated by barriers: in
+// round k wave w adds the tiles of set (w + k) % kTfWaves, so every tile
+// receives the waves' contributions in one fixed order (deterministic) and the
+// waves never write the same tile at once.
+template <int NA, int NB>
+PGP_DEV void lds_acc_add(float* acc, const f32x4 (&d)[NA][NB], int wv, int lane) {
+#pragma unroll
+  for (int k = 0; k < kTfWaves; ++k) {
+    const int set = (wv + k) % kTfWaves;
+#pragma unroll
+    for (int T = 0; T < NA; ++T)
+#pragma unroll
+      for (int U = 0; U < NB; ++U)
+        if ((T * NB + U) % kTfWaves == set) {
+          float* pa = acc + ((T * NB + U) * 64 + lane) * 4;
+          st4(pa, ld4(pa) + d[T][U]);
+        }
+    __syncthreads();
+  }
+}
+// LDS accumulator tile (row 16T+4g+r, column 16U+j per lane) -> slab
+template <int NA, int NB>
+PGP_DEV void add_dw_lds(float* slab, const float* acc, int rows, int cols, int ld, int g, int j, int lane) {
+#pragma unroll
+  for (int T = 0; T < NA; ++T)
+#pragma unroll
+    for (int U = 0; U < NB; ++U) {
+      const f32x4 v = ld4(acc + ((T * NB + U) * 64 + lane) * 4);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = 16 * T + 4 * g + r, c = 16 * U + j;
+        if (n < rows && c < cols) slab[n * ld + c] += v[r];
+      }
+    }
+}
+
+template <int H>
+__global__ __launch_bounds__(kTfWaves * 64, 1) void tf_bwd_ffn_kernel(TfArgs a) {
+  using F = TF<H>;
+  using L = BffL<H>;
+  using Q = TfPar<H>;
+  constexpr int NT = F::NT;
+  static_assert(L::SLAB <= L::SCR, "slab fits the LDS it reuses");
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, g = lane >> 4, j = lane & 15;
+  const int layer = a.layer;
+  dma_groups(a.frags + F::layer_off(layer) + F::OFF_F1, sm + L::W_F1, F::G_F1 + F::G_F2 + F::G_F2T + F::G_F1T, wv,
+             kTfWaves, lane);
+  load_params<H>(sm + L::PAR, a.P, layer);
+  for (int k = threadIdx.x; k < L::NTILE * 256; k += blockDim.x) sm[L::ACC + k] = 0.f;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const float* par = sm + L::PAR;
+  float* sa = sm + L::SCR + wv * (L::SCR_A + L::SCR_B);
+  float* sb = sa + L::SCR_A;
+  float* accW2 = sm + L::ACC;
+  float* accW1 = accW2 + NT * 4 * 256;
+  float b2s[NT], b1s[4];
+  float ag1 = 0.f, ab1 = 0.f, ag2 = 0.f, ab2 = 0.f;  // LayerNorm gamma / beta sums (compressed rows)
+#pragma unroll
+  for (int t = 0; t < NT; ++t) b2s[t] = 0.f;
+#pragma unroll
+  for (int U = 0; U < 4; ++U) b1s[U] = 0.f;
+  // every wave runs the same number of rounds (the LDS accumulation joins
+  // barriers); a wave past its units computes on zeros, which adds exactly 0
+  const long npairs = (long)a.B * H, nu = (npairs + 15) / 16;
+  long u0, u1;
+  unit_range(nu, u0, u1);
+  const long nwav = (long)gridDim.x * kTfWaves, rounds = (nu + nwav - 1) / nwav;
+#pragma unroll 1
+  for (long it = 0; it < rounds; ++it) {
+    // loop-variant view of the LDS base: keeps LICM from hoisting the
+    // loop-invariant parameter / weight reads out of the unit loop (hundreds of
+    // registers held across it)
+    int z = 0;
+    asm volatile("" : "+s"(z));
+    float* smz = sm + z;
+    const float* par = smz + L::PAR;
+    const long u = u0 + it;
+    // y1 = gamma1 x-hat1 + beta1, tile t of step w
+    auto y1 = [&](const f32x4 (&xh)[NT][3], int t, int w) {
+      return xh[t][w] * ld4(par + Q::N1W + 16 * t + 4 * g) + ld4(par + Q::N1B + 16 * t + 4 * g);
+    };
+    const long p = u * 16 + j;
+    const bool ok = u < u1 && p < npairs;
+    long row[3];
+#pragma unroll
+    for (int w = 0; w < 3; ++w) row[w] = ok ? tf_row<H>(p, w) : 0;
+    f32x4 dY[NT][3], Fh[4][3];
+    float rs1[3], rs2[3];
+#pragma unroll
+    for (int w = 0; w < 3; ++w) rs1[w] = ok ? a.rs1[row[w]] : 0.f;
+    {  // recompute the FFN (pre-activation F) and norm2's x-hat
+      f32x4 X2[NT][3];
+      {
+        f32x4 Y1[NT][3];
+        load_tiles<NT>(Y1, a.xh1, F::DP, row, ok, g);
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+          for (int w = 0; w < 3; ++w) Y1[t][w] = y1(Y1, t, w);
+        init_bias<4>(Fh, par + Q::B1, g);
+        tf_gemm<4, F::KS>(Fh, smz + L::W_F1, [&](int s, int w) { return Y1[s >> 2][w][s & 3]; }, lane);
+        init_bias<NT>(X2, par + Q::B2, g);
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+          for (int w = 0; w < 3; ++w) X2[t][w] += Y1[t][w];
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t)  // keep relu(F): its sign is F's for the mask (F = 0 -> 0 either way)
+#pragma unroll
+        for (int w = 0; w < 3; ++w)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) Fh[t][w][r] = fmaxf(Fh[t][w][r], 0.f);
+      tf_gemm<NT, 16>(X2, smz + L::W_F2, [&](int s, int w) { return Fh[s >> 2][w][s & 3]; }, lane);
+      __builtin_amdgcn_sched_barrier(0);
+      tf_ln<H, NT>(X2, rs2, g);
+      load_tiles<NT>(dY, a.in, F::DP, row, ok, g);
+      tf_ln_bwd<H, NT>(dY, X2, rs2, par + Q::N2W, g, j, ag2, ab2);  // dY <- dR2
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    {  // dW2 += dR2 (x) relu(F), db2 += sum dR2
+      f32x4 dW[NT][4];
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int U = 0; U < 4; ++U) dW[t][U] = zero4();
+#pragma unroll
+      for (int w = 0; w < 3; ++w) {
+        stage<NT>(dY, w, sa, g, j);
+        stage<4>(Fh, w, sb, g, j);
+        dw_step<NT, 4>(dW, b2s, sa, sb, g, j);
+      }
+      lds_acc_add<NT, 4>(accW2, dW, wv, lane);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    f32x4 XH1[NT][3];
+    // dF = (W2^T dR2) * (F > 0)
+    {
+      f32x4 dF[4][3];
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int w = 0; w < 3; ++w) dF[t][w] = zero4();
+      tf_gemm<4, F::KS>(dF, smz + L::W_F2T, [&](int s, int w) { return dY[s >> 2][w][s & 3]; }, lane);
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int w = 0; w < 3; ++w)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) dF[t][w][r] = Fh[t][w][r] > 0.f ? dF[t][w][r] : 0.f;
+      __builtin_amdgcn_sched_barrier(0);
+      load_tiles<NT>(XH1, a.xh1, F::DP, row, ok, g);  // reloaded (L2): not held through the phases above
+      {  // dW1 += dF (x) y1, db1 += sum dF
+        f32x4 dW[4][NT];
+#pragma unroll
+        for (int U = 0; U < 4; ++U)
+#pragma unroll
+          for (int t = 0; t < NT; ++t) dW[U][t] = zero4();
+#pragma unroll
+        for (int w = 0; w < 3; ++w) {
+          stage<4>(dF, w, sa, g, j);
+          stage_fn<NT>([&](int t) { return y1(XH1, t, w); }, sb, g, j);
+          dw_step<4, NT>(dW, b1s, sa, sb, g, j);
+        }
+        lds_acc_add<4, NT>(accW1, dW, wv, lane);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      // dy1 = W1^T dF + dR2 (residual)
+      tf_gemm<NT, 16>(dY, smz + L::W_F1T, [&](int s, int w) { return dF[s >> 2][w][s & 3]; }, lane);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    tf_ln_bwd<H, NT>(dY, XH1, rs1, par + Q::N1W, g, j, ag1, ab1);  // -> dR1
+    store_tiles<NT>(dY, a.out, F::DP, row, ok, g);
+  }
+  // one slab per workgroup: the LDS dW tiles, then the waves' vector partials in wave order
+  __syncthreads();
+  float* slab = sm;  // the weight area is free now
+  slab_zero(slab, L::SLAB);
+  __syncthreads();
+  if (wv == 0) {
+    add_dw_lds<NT, 4>(slab + L::S_W2, accW2, H, 64, 64, g, j, lane);
+    add_dw_lds<4, NT>(slab + L::S_W1, accW1, 64, H, H, g, j, lane);
+  }
+  __syncthreads();
+  for (int k = 0; k < kTfWaves; ++k) {
+    if (wv == k) {
+      add_bias<NT>(slab + L::S_B2, b2s, H, g, j);
+      add_bias<4>(slab + L::S_B1, b1s, 64, g, j);
+      add_rows_c(slab + L::S_G1, ag1, H, g, j);
+      add_rows_c(slab + L::S_BT1, ab1, H, g, j);
+      add_rows_c(slab + L::S_G2, ag2, H, g, j);
+      add_rows_c(slab + L::S_BT2, ab2, H, g, j);
+    }
+    __syncthreads();
+  }
+  slab_out(slab, a.part + (long)blockIdx.x * L::SLAB, L::SLAB);
+}
+
+// ============================================================================
+// backward of a layer's attention block (models.py:356: norm1(x + SA(x))):
+// dR1 (grad of norm1's input) -> dX (grad of the layer input) and dQKV
+// ============================================================================
+template <int H>
+struct BatL {
+  using F = TF<H>;
+  static constexpr int W_IN = 0, W_INT = W_IN + F::G_IN * 256, W_OT = W_INT + F::G_INT * 256,
+                       PAR = W_OT + F::G_OT * 256, SCR = PAR + TfPar<H>::SIZE,
+                       SCR_A = Scr<F::NT>::SIZE, SCR_B = Scr<F::NT>::SIZE,
+                       TOTAL = SCR + kTfWaves * (SCR_A + SCR_B);
+  static constexpr int S_WO = 0, S_BO = H * H, SLAB = S_BO + H;
+};
+
+template <int H>
+__global__ __launch_bounds__(kTfWaves * 64, 1) void tf_bwd_att_kernel(TfArgs a) {
+  using F = TF<H>;
+  using L = BatL<H>;
+  using Q = TfPar<H>;
+  constexpr int NT = F::NT;
+  static_assert(L::SLAB <= L::SCR, "slab fits the LDS it reuses");
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, g = lane >> 4, j = lane & 15;
+  const int layer = a.layer;
+  const float* fr = a.frags + F::layer_off(layer);
+  dma_groups(fr + F::OFF_IN, sm + L::W_IN, F::G_IN, wv, kTfWaves, lane);
+  dma_groups(fr + F::OFF_INT, sm + L::W_INT, F::G_INT + F::G_OT, wv, kTfWaves, lane);
+  load_params<H>(sm + L::PAR, a.P, layer);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const float* par = sm + L::PAR;
+  float* sa = sm + L::SCR + wv * (L::SCR_A + L::SCR_B);
+  float* sb = sa + L::SCR_A;
+  f32x4 dWo[NT][NT];
+  float bos[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    bos[t] = 0.f;
+#pragma unroll
+    for (int U = 0; U < NT; ++U) dWo[t][U] = zero4();
+  }
+  const float scale = 1.0f / sqrtf((float)F::HD);
+  const long npairs = (long)a.B * H, nu = (npairs + 15) / 16;
+  long u0, u1;
+  unit_range(nu, u0, u1);
+#pragma unroll 1
+  for (long u = u0; u < u1; ++u) {
+    const long p = u * 16 + j;
+    const bool ok = p < npairs;
+    long row[3];
+#pragma unroll
+    for (int w = 0; w < 3; ++w) row[w] = ok ? tf_row<H>(p, w) : 0;
+    f32x4 QKV[F::NQ][3];
+    {
+      f32x4 X[NT][3];
+      load_tiles<NT>(X, a.x, F::DP, row, ok, g);
+      init_bias<F::NQ>(QKV, par + Q::BIN, g);
+      tf_gemm<F::NQ, F::KS>(QKV, sm + L::W_IN, [&](int s, int w) { return X[s >> 2][w][s & 3]; }, lane);
+    }
+    float Pr[2][3][3];
+    f32x4 O[NT][3], dR1[NT][3];
+    tf_attn_fwd<H>(QKV, Pr, O, g);
+    load_tiles<NT>(dR1, a.in, F::DP, row, ok, g);
+    // dWo += dR1 (x) attention output, dbo += sum dR1
+#pragma unroll
+    for (int w = 0; w < 3; ++w) {
+      stage<NT>(dR1, w, sa, g, j);
+      stage<NT>(O, w, sb, g, j);
+      dw_step<NT, NT>(dWo, bos, sa, sb, g, j);
+    }
+    // dO = Wo^T dR1
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int w = 0; w < 3; ++w) O[t][w] = zero4();
+    tf_gemm<NT, F::KS>(O, sm + L::W_OT, [&](int s, int w) { return dR1[s >> 2][w][s & 3]; }, lane);
+    // attention backward (pgp_tune.hip attn_bwd_kernel, per lane)
+    float dS[2][3][3];
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+      for (int w = 0; w < 3; ++w)
+#pragma unroll
+        for (int w2 = 0; w2 < 3; ++w2) dS[hh][w][w2] = 0.f;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int c = 16 * t + 4 * g + r;
+        const bool h0 = c < F::HD, h1 = c >= F::HD && c < H;
+#pragma unroll
+        for (int w = 0; w < 3; ++w)
+#pragma unroll
+          for (int w2 = 0; w2 < 3; ++w2) {
+            const float pr = O[t][w][r] * QKV[2 * NT + t][w2][r];  // dO[w] . v[w2]
+            dS[0][w][w2] += h0 ? pr : 0.f;
+            dS[1][w][w2] += h1 ? pr : 0.f;
+          }
+      }
+    {
+      float* f = &dS[0][0][0];
+#pragma unroll
+      for (int i = 0; i < 18; i += 2) xsum2(f[i], f[i + 1]);
+    }
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+      for (int w = 0; w < 3; ++w) {
+        const float sd = Pr[hh][w][0] * dS[hh][w][0] + Pr[hh][w][1] * dS[hh][w][1] + Pr[hh][w][2] * dS[hh][w][2];
+#pragma unroll
+        for (int w2 = 0; w2 < 3; ++w2) dS[hh][w][w2] = Pr[hh][w][w2] * (dS[hh][w][w2] - sd) * scale;
+      }
+    // dv (in place of v), dq (temporary), dk (in place of k), then q <- dq
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int hh = (16 * t + 4 * g + r) < F::HD ? 0 : 1;
+        float dq[3], dk[3], dv[3];
+#pragma unroll
+        for (int w = 0; w < 3; ++w) {
+          const float d0 = hh ? dS[1][w][0] : dS[0][w][0], d1 = hh ? dS[1][w][1] : dS[0][w][1],
+                      d2 = hh ? dS[1][w][2] : dS[0][w][2];
+          dq[w] = d0 * QKV[NT + t][0][r] + d1 * QKV[NT + t][1][r] + d2 * QKV[NT + t][2][r];
+          const float e0 = hh ? dS[1][0][w] : dS[0][0][w], e1 = hh ? dS[1][1][w] : dS[0][1][w],
+                      e2 = hh ? dS[1][2][w] : dS[0][2][w];
+          dk[w] = e0 * QKV[t][0][r] + e1 * QKV[t][1][r] + e2 * QKV[t][2][r];
+          const float p0 = hh ? Pr[1][0][w] : Pr[0][0][w], p1 = hh ? Pr[1][1][w] : Pr[0][1][w],
+                      p2 = hh ? Pr[1][2][w] : Pr[0][2][w];
+          dv[w] = p0 * O[t][0][r] + p1 * O[t][1][r] + p2 * O[t][2][r];
+        }
+#pragma unroll
+        for (int w = 0; w < 3; ++w) {
+          QKV[t][w][r] = dq[w];
+          QKV[NT + t][w][r] = dk[w];
+          QKV[2 * NT + t][w][r] = dv[w];
+        }
+      }
+    // dQKV rows to HBM ([M][Q3P], q | k | v natural) for in_proj's weight gradient
+    if (ok) {
+#pragma unroll
+      for (int part = 0; part < 3; ++part)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          const int c0 = 16 * t + 4 * g;
+#pragma unroll
+          for (int w = 0; w < 3; ++w) {
+            float* dst = a.dqkv + row[w] * F::Q3P + part * H + c0;
+            const f32x4 v = QKV[part * NT + t][w];
+            if (c0 + 3 < H) {
+              *reinterpret_cast<f32x2*>(dst) = f32x2{v[0], v[1]};
+              *reinterpret_cast<f32x2*>(dst + 2) = f32x2{v[2], v[3]};
+            } else {
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                if (c0 + r < H) dst[r] = v[r];
+            }
+          }
+        }
+    }
+    // dX = Win^T dQKV + dR1 (the residual)
+    tf_gemm<NT, F::KSQ>(dR1, sm + L::W_INT, [&](int s, int w) {
+      const int part = s / F::KS, sl = s - part * F::KS;
+      return QKV[part * NT + (sl >> 2)][w][sl & 3];
+    }, lane);
+    store_tiles<NT>(dR1, a.out, F::DP, row, ok, g);
+  }
+  __syncthreads();
+  float* slab = sm;
+  slab_zero(slab, L::SLAB);
+  __syncthreads();
+  for (int k = 0; k < kTfWaves; ++k) {
+    if (wv == k) {
+      add_dw<NT, NT>(slab + L::S_WO, dWo, H, H, H, g, j);
+      add_bias<NT>(slab + L::S_BO, bos, H, g, j);
+    }
+    __syncthreads();
+  }
+  slab_out(slab, a.part + (long)blockIdx.x * L::SLAB, L::SLAB);
+}
+
+template <int H>
+hipError_t tf_launch(int kind, const TfArgs& a, int grid, hipStream_t st) {
+  using F = TF<H>;
+  switch (kind) {
+    case 0: {
+      const long n = F::TOTAL_FLOATS;
+      tf_pack_kernel<H><<<(int)((n + 255) / 256), 256, 0, st>>>(a.P, a.frags);
+      return hipGetLastError();
+    }
+    case 1: {
+      const size_t lds = (size_t)FwdL<H>::TOTAL * 4;
+      tf_fwd_kernel<H><<<grid, kTfWaves * 64, lds, st>>>(a);
+      return hipGetLastError();
+    }
+    case 2: {
+      const size_t lds = (size_t)BffL<H>::TOTAL * 4;
+      tf_bwd_ffn_kernel<H><<<grid, kTfWaves * 64, lds, st>>>(a);
+      return hipGetLastError();
+    }
+    case 3: {
+      const size_t lds = (size_t)BatL<H>::TOTAL * 4;
+      tf_bwd_att_kernel<H><<<grid, kTfWaves * 64, lds, st>>>(a);
+      return hipGetLastError();
+    }
+  }
+  return hipErrorInvalidValue;
+}
+
+template <int H>
+bool tf_lds_ok() {
+  return FwdL<H>::TOTAL * 4 <= 160 * 1024 && BffL<H>::TOTAL * 4 <= 160 * 1024 && BatL<H>::TOTAL * 4 <= 160 * 1024;
+}
+
+}  // namespace
+
+long tf_frag_floats(int H) {
+  switch (H) {
+#define CASE(h) \
+  case h:       \
+    return TF<h>::TOTAL_FLOATS;
+    PGP_FOR_EACH_H(CASE)
+#undef CASE
+  }
+  return 0;
+}
+
+long tf_slab_floats(int H, int kind) {
+  switch (H) {
+#define CASE(h) \
+  case h:       \
+    return kind == 2 ? BffL<h>::SLAB : BatL<h>::SLAB;
+    PGP_FOR_EACH_H(CASE)
+#undef CASE
+  }
+  return 0;
+}
+
+int tf_grid() { return device_cus(); }
+
+hipError_t launch_tf(int H, int kind, const TfArgs& a, hipStream_t st) {
+  const int grid = tf_grid();
+  switch (H) {
+#define CASE(h)                                                                          \
+  case h: {                                                                              \
+    static_assert(FwdL<h>::TOTAL * 4 <= 160 * 1024, "forward LDS");                      \
+    static_assert(BffL<h>::TOTAL * 4 <= 160 * 1024, "ffn backward LDS");                 \
+    static_assert(BatL<h>::TOTAL * 4 <= 160 * 1024, "attention backward LDS");           \
+    static bool attr = [] {                                                              \
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(tf_fwd_kernel<h>),         \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, FwdL<h>::TOTAL * 4); \
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(tf_bwd_ffn_kernel<h>),     \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, BffL<h>::TOTAL * 4); \
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(tf_bwd_att_kernel<h>),     \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, BatL<h>::TOTAL * 4); \
+      return true;                                                                       \
+    }();                                                                                 \
+    (void)attr;                                                                          \
+    return tf_launch<h>(kind, a, grid, st);                                              \
+  }
+    PGP_FOR_EACH_H(CASE)
+#undef CASE
+  }
+  return hipErrorInvalidValue;
+}
+
+}  // namespace pgp

@@ -1,0 +1,78 @@
+// pgp_tunef.hpp — geometry and launch interface of the fused tuning-encoder
+// kernels (pgp_tunef.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "pgp_layout.hpp"
+
+namespace pgp {
+
+// weight fragment matrices (A operands; "T" = transposed for the backward)
+enum TfMat : int { TFM_TE = 0, TFM_IN, TFM_O, TFM_F1, TFM_F2, TFM_F2T, TFM_F1T, TFM_INT, TFM_OT };
+
+template <int H>
+struct TF {
+  static constexpr int D = H, DP = round_up(H, 16), NT = DP / 16, HD = H / 2;
+  // k-steps over d in the natural row map (feature 16t + 4g + r of k-step (t, r))
+  static constexpr int KS = 4 * (H / 16) + ((H % 16) == 0 ? 0 : ((H % 16) < 4 ? (H % 16) : 4));
+  static constexpr int KG = (KS + 3) / 4;
+  static constexpr int NQ = 3 * NT;          // q | k | v output tiles
+  static constexpr int KSQ = 3 * KS, KGQ = (KSQ + 3) / 4;
+  static constexpr int KGF = 4;              // 16 k-steps over the FFN hidden (64)
+  static constexpr int Q3P = round_up(3 * H, 16);
+  // fragment groups (1 KiB = 64 lanes x 4 k-steps) per matrix
+  static constexpr int G_TE = NT * KG, G_IN = NQ * KG, G_O = NT * KG, G_F1 = 4 * KG, G_F2 = NT * KGF,
+                       G_F2T = 4 * KG, G_F1T = NT * KGF, G_INT = NT * KGQ, G_OT = NT * KG;
+  // per-layer block order: IN O F1 F2 F2T F1T INT OT (forward | ffn backward | attention backward)
+  static constexpr int LG = G_IN + G_O + G_F1 + G_F2 + G_F2T + G_F1T + G_INT + G_OT;
+  static constexpr long OFF_IN = 0, OFF_O = OFF_IN + G_IN * 256L, OFF_F1 = OFF_O + G_O * 256L,
+                        OFF_F2 = OFF_F1 + G_F1 * 256L, OFF_F2T = OFF_F2 + G_F2 * 256L,
+                        OFF_F1T = OFF_F2T + G_F2T * 256L, OFF_INT = OFF_F1T + G_F1T * 256L,
+                        OFF_OT = OFF_INT + G_INT * 256L;
+  static constexpr long TE_OFF = 0;
+  static constexpr long layer_off(int l) { return (G_TE + (long)l * LG) * 256L; }
+  static constexpr long TOTAL_FLOATS = (G_TE + 2L * LG) * 256L;
+  static constexpr int mat_kg(int m) {
+    return m == TFM_F2 || m == TFM_F1T ? KGF : m == TFM_INT ? KGQ : KG;
+  }
+  __host__ __device__ static void locate(long grp, int& layer, int& mat, long& gi) {
+    if (grp < G_TE) {
+      layer = -1;
+      mat = TFM_TE;
+      gi = grp;
+      return;
+    }
+    long r = grp - G_TE;
+    layer = (int)(r / LG);
+    r -= (long)layer * LG;
+    const int cnt[8] = {G_IN, G_O, G_F1, G_F2, G_F2T, G_F1T, G_INT, G_OT};
+    const int ids[8] = {TFM_IN, TFM_O, TFM_F1, TFM_F2, TFM_F2T, TFM_F1T, TFM_INT, TFM_OT};
+    int k = 0;
+    while (k < 7 && r >= cnt[k]) r -= cnt[k++];
+    mat = ids[k];
+    gi = r;
+  }
+};
+
+// arguments of the fused kernels (unused pointers may be null)
+struct TfArgs {
+  int layer, B;
+  const float* P;      // master weights (natural blob)
+  float* frags;        // packed fragments [TE][layer 0][layer 1] (tf_frag_floats)
+  const float* in;     // fwd: layer input (layer 0: GAT output); ffn bwd: dOut; att bwd: dR1   [M][DP]
+  float* out;          // fwd: layer output; ffn bwd: dR1; att bwd: dX                          [M][DP]
+  float* x0;           // fwd layer 0: X0 (time-encoder output)                                  [M][DP]
+  const float* x;      // att bwd: the layer input X                                             [M][DP]
+  float* xh1;          // norm1 x-hat [M][DP] (fwd writes, ffn bwd reads)
+  float* rs1;          // norm1 rstd [M]
+  float* dqkv;         // att bwd: dQKV [M][Q3P] (q | k | v natural)
+  float* part;         // bwd: one weight-gradient slab per workgroup
+};
+
+long tf_frag_floats(int H);
+long tf_slab_floats(int H, int kind);  // kind 2: ffn backward, 3: attention backward
+int tf_grid();                          // workgroups per fused launch (one per CU)
+// kind 0: pack fragments from P; 1: forward of a.layer; 2: ffn backward; 3: attention backward
+hipError_t launch_tf(int H, int kind, const TfArgs& a, hipStream_t st);
+
+}  // namespace pgp
