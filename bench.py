@@ -26,7 +26,7 @@ sys.path.insert(0, ROOT)
 
 from preganplus_amd import roofline as R  # noqa: E402
 from preganplus_amd import weights as W  # noqa: E402
-from preganplus_amd.model import DecisionModel, migrations  # noqa: E402
+from preganplus_amd.model import DecisionModel, embedding, migrations  # noqa: E402
 
 
 def log(*a):
@@ -409,6 +409,7 @@ def bench_tune(args):
     sim_out = torch.empty((E, 4), dtype=torch.float64, device=device)
     gan_target = torch.empty((E, 2), dtype=torch.float32, device=device)
     bufs = TR.dataset_buffers(tr, E, R)
+    emb_buf = torch.empty((E, H, 2), dtype=torch.float32, device=device)
     names = ("dataset", "detect", "train_gan", "tune_model")
     subs = TR.DPTuner.SUBSTAGES
     ev = [[torch.cuda.Event(enable_timing=True) for _ in range(len(names) + 1)] for _ in range(max(args.steps, 1))]
@@ -420,7 +421,7 @@ def bench_tune(args):
         wins, y, cls, inf = TR.tune_dataset(tr, series, tmax, out=bufs)
         rec(1)
         logits, protos = tr.tune_forward(inf)
-        emb = torch.where(logits[..., 1:2] > logits[..., 0:1], protos, 0.0)   # PreGANPlus.py:129
+        emb = embedding(logits, protos, out=emb_buf)   # PreGANPlus.py:129
         rec(2)
         TR.train_gan_batched(tr, sim, envs, emb, s, out=sim_out, target=gan_target, all_reduce=True)
         rec(3)
@@ -749,6 +750,7 @@ def bench_loop(args):
     sim_out = torch.empty((E, 4), dtype=torch.float64, device=device)
     gan_target = torch.empty((E, 2), dtype=torch.float32, device=device)
     sched = torch.empty((E, H, H), device=device)
+    emb_buf = torch.empty((E, H, 2), dtype=torch.float32, device=device)
     names = ("gobi", "encode_classify", "gan_step", "tune_step", "weight_sync", "gan_decide_moves")
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(len(names) + 1)]
     acc = np.zeros(len(names))
@@ -762,7 +764,7 @@ def bench_loop(args):
             ev[1].record()
         for st in (0, 1, 2):
             model.forward(x, sched, out=out, stage=st)
-        emb = torch.where(out["logits"][..., 1:2] > out["logits"][..., 0:1], out["protos"], 0.0)
+        emb = embedding(out["logits"], out["protos"], out=emb_buf)   # PreGANPlus.py:129
         if timed:
             ev[2].record()
         TR.train_gan_batched(tr, sim, envs, emb, sched, out=sim_out, target=gan_target)

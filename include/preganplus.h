@@ -27,6 +27,8 @@
  *             gen_target   = first-argmax(new_sched[c,:])
  *   pgp_migrations
  *       recover_decision's container loop PreGANPlus.py:90-105 (PreGAN.py:80-95)
+ *   pgp_embedding
+ *       run_model's masked prototype embedding PreGANPlus.py:129
  *   pgp_create_fpe / pgp_forward_fpe
  *       PreGAN: PreGANRecovery.run_encoder + detect/embed/get_classes + the
  *       GAN gate, recovery/PreGAN.py:97-126 over FPE_16.forward models.py:65-115
@@ -147,6 +149,9 @@ int pgp_forward_stage(pgp_model* m, int stage, int batch, const float* windows,
  * host-ascending, then container order. */
 int pgp_migrations(int n_hosts, int batch, const int* keep_orig, const int* final_target, const int* cur_host,
                    int* moves, int* hosts_from, void* stream);
+/* run_model's embedding (PreGANPlus.py:129): emb[b,h,:] = protos[b,h,:] where
+ * argmax(logits[b,h,:]) == 1 (ties -> 0), else 0.  fp32 device [B,H,2] each. */
+int pgp_embedding(int n_hosts, int batch, const float* logits, const float* protos, float* emb, void* stream);
 
 /* ------------------------------------------------------------------------
  * PreGAN (FPE) variant — BASELINE config C4, SURVEY.md §8 a14.

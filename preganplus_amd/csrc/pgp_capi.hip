@@ -288,6 +288,14 @@ int pgp_migrations(int n_hosts, int batch, const int* keep_orig, const int* fina
   return PGP_OK;
 }
 
+int pgp_embedding(int n_hosts, int batch, const float* logits, const float* protos, float* emb, void* stream) {
+  if (n_hosts < 1 || batch < 0) return fail(PGP_ERR_ARG, "bad embedding arguments");
+  if (batch == 0) return PGP_OK;
+  if (!logits || !protos || !emb) return fail(PGP_ERR_ARG, "NULL input/output pointer");
+  HIPCHK(launch_embed((long)batch * n_hosts, logits, protos, emb, reinterpret_cast<hipStream_t>(stream)));
+  return PGP_OK;
+}
+
 // ---------------------------------------------------------------------------
 // training ops
 // ---------------------------------------------------------------------------

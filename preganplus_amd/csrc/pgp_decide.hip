@@ -26,6 +26,17 @@ __global__ __launch_bounds__(256) void decide_kernel(int B, int C, const int* __
   if (mv) atomicOr(hosts_from + b * C + h, 1);
 }
 
+// run_model's embedding (PreGANPlus.py:129): emb[b,h] = protos[b,h] where the
+// host is flagged (argmax of its logits = 1, ties -> 0) else 0
+__global__ __launch_bounds__(256) void embed_kernel(long n, const float* __restrict__ logits,
+                                                    const float* __restrict__ protos, float* __restrict__ emb) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const f32x2 l = *reinterpret_cast<const f32x2*>(logits + 2 * i);
+  const f32x2 p = *reinterpret_cast<const f32x2*>(protos + 2 * i);
+  *reinterpret_cast<f32x2*>(emb + 2 * i) = l[1] > l[0] ? p : f32x2{0.f, 0.f};
+}
+
 __global__ __launch_bounds__(256) void zero_kernel(long n, int* __restrict__ p) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) p[i] = 0;
@@ -39,6 +50,11 @@ hipError_t launch_decide(int B, int C, const int* keep, const int* target, const
   const int grid = (int)((n + 255) / 256);
   zero_kernel<<<grid, 256, 0, st>>>(n, hosts_from);
   decide_kernel<<<grid, 256, 0, st>>>(B, C, keep, target, cur, moves, hosts_from);
+  return hipGetLastError();
+}
+
+hipError_t launch_embed(long n, const float* logits, const float* protos, float* emb, hipStream_t st) {
+  if (n > 0) embed_kernel<<<(int)((n + 255) / 256), 256, 0, st>>>(n, logits, protos, emb);
   return hipGetLastError();
 }
 

@@ -69,6 +69,8 @@ hipError_t launch_fpe(int H, const FpeArgs& a, hipStream_t st);
 // recover_decision's per-container moves (pgp_decide.hip)
 hipError_t launch_decide(int B, int C, const int* keep, const int* target, const int* cur, int* moves,
                          int* hosts_from, hipStream_t st);
+// run_model's masked embedding over n (window, host) pairs (pgp_decide.hip)
+hipError_t launch_embed(long n, const float* logits, const float* protos, float* emb, hipStream_t st);
 
 hipError_t launch_gat(const FwdArgs& a, hipStream_t st);
 hipError_t launch_encoder(const FwdArgs& a, hipStream_t st);

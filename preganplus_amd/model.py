@@ -224,6 +224,21 @@ def migrations(keep_orig: torch.Tensor, final_target: torch.Tensor, cur_host: to
     return moves, hosts_from
 
 
+def embedding(logits: torch.Tensor, protos: torch.Tensor, out: torch.Tensor | None = None, stream=None):
+    """run_model's embedding (PreGANPlus.py:129) for a batch (``pgp_embedding``):
+    fp32 device [B,H,2] logits / protos -> protos where the host is flagged
+    (argmax = 1, ties -> 0), else 0."""
+    B, H = logits.shape[0], logits.shape[1]
+    for t in (logits, protos):
+        if tuple(t.shape) != (B, H, 2) or t.dtype != torch.float32 or not t.is_cuda or not t.is_contiguous():
+            raise ValueError("embedding: fp32 contiguous device tensors logits / protos [B,H,2]")
+    out = torch.empty_like(protos) if out is None else out
+    st = stream if stream is not None else torch.cuda.current_stream(logits.device)
+    _native.check(_native.lib().pgp_embedding(H, B, logits.data_ptr(), protos.data_ptr(), out.data_ptr(),
+                                              ctypes.c_void_p(st.cuda_stream)), "pgp_embedding")
+    return out
+
+
 def assemble_decision(original_decision, moves_row, cur_host_row):
     """The returned list of recover_decision (PreGANPlus.py:96-105): the original
     decision's order, then overridden / new container keys in host-ascending,

@@ -58,3 +58,19 @@ def test_migrations_out_of_range_host_is_unplaced():
     mv2, hf2 = migrations(d([0, 0]), d(tgt), d(ref))
     assert torch.equal(mv, mv2) and torch.equal(hf, hf2)
     assert mv[0, 1].item() == -1 and mv[0, 2].item() == -1 and int(hf[0].sum().item()) == 3
+
+
+def test_embedding_matches_reference_rule():
+    """pgp_embedding = run_model's embedding line (PreGANPlus.py:129): the host's
+    prototype where argmax(logits) == 1 (torch.argmax: ties -> 0), else zeros;
+    bit-exact, ties and ragged batches included."""
+    import torch
+    from preganplus_amd.model import embedding
+    rng = np.random.Generator(np.random.PCG64(5))
+    for B, H in ((1, 16), (77, 50), (1000, 8)):
+        lg = rng.standard_normal((B, H, 2)).astype(np.float32)
+        lg[::3, ::2, 1] = lg[::3, ::2, 0]                      # ties
+        pr = rng.uniform(size=(B, H, 2)).astype(np.float32)
+        want = np.where((lg[..., 1] > lg[..., 0])[..., None], pr, 0.0).astype(np.float32)
+        got = embedding(torch.tensor(lg, device="cuda"), torch.tensor(pr, device="cuda")).cpu().numpy()
+        assert np.array_equal(got, want)
