@@ -269,7 +269,7 @@ int pgp_forward1(int n_hosts, int n_protos, const float* window, const float* sc
 /* ---- data-parallel tuning step on the device ----
  * pgp_tune_dataset replaces load_on_the_fly_dataset (utils.py:40-47) for a
  * batch of E environments: series [E,R,3H] fp64 = each environment's last R
- * rows of stats.time_series (R = LATEST_WINDOW_SIZE = 10, 3 <= R <= 16),
+ * rows of stats.time_series (R = LATEST_WINDOW_SIZE = 10, 1 <= R <= 16),
  * train_max [3H] fp64 = np.max(train_time_data, axis=0); normalises
  * (utils.py:94-95), writes the R windows per environment (convert_to_windows,
  * utils.py:7-14) windows [E*R,3,3H] fp32, the labels of form_test_dataset

@@ -408,7 +408,7 @@ int pgp_forward1(int n_hosts, int n_protos, const float* window, const float* sc
 int pgp_tune_dataset(int n_hosts, int n_env, int n_rows, const double* series, const double* train_max,
                      float* windows, int* y, int* cls, float* infer, void* stream) {
   if (n_hosts <= 0 || n_hosts > 64) return fail(PGP_ERR_UNSUPPORTED, "host count");
-  if (n_env < 0 || n_rows < 3 || n_rows > kMaxTuneRows) return fail(PGP_ERR_ARG, "n_env >= 0, 3 <= n_rows <= 16");
+  if (n_env < 0 || n_rows < 1 || n_rows > kMaxTuneRows) return fail(PGP_ERR_ARG, "n_env >= 0, 1 <= n_rows <= 16");
   if (n_env == 0) return PGP_OK;
   if (!series || !train_max || !windows || !y || !cls) return fail(PGP_ERR_ARG, "bad tune_dataset arguments");
   HIPCHK(launch_tune_dataset(n_hosts, n_env, n_rows, series, train_max, windows, y, cls, infer,

@@ -105,14 +105,17 @@ __global__ __launch_bounds__(256) void tune_dataset_kernel(int H, int E, int R, 
       }
     }
   }
-  if (infer) {  // run_encoder: last 3 rows -> convert_to_windows(...)[-1] = [R-3, R-3, R-2]
+  if (infer) {  // run_encoder: last 3 rows -> convert_to_windows(...)[-1] = [R-3, R-3, R-2];
+                // a shorter series (R = 1, 2: the first intervals) keeps all its rows and
+                // its last window is row 0 three times
+    const int ra = R >= kWin ? R - 3 : 0, rb = R >= kWin ? R - 2 : 0;
     double u[2][3] = {};
 #pragma unroll
     for (int r = 0; r < kMaxTuneRows; ++r)
 #pragma unroll
       for (int c = 0; c < 3; ++c) {
-        if (r == R - 3) u[0][c] = v[r][c];
-        if (r == R - 2) u[1][c] = v[r][c];
+        if (r == ra) u[0][c] = v[r][c];
+        if (r == rb) u[1][c] = v[r][c];
       }
 #pragma unroll
     for (int w = 0; w < kWin; ++w)

@@ -180,19 +180,26 @@ class PreGANPlusRecovery(Recovery):
     def _repack(self):
         """pgp_repack_master: P and the prototypes of the tuning state never
         leave the GPU."""
-        K = self.tune_state.protos.shape[0]
-        dev_state = getattr(self.trainer, "tune_state_dev", None)
-        if dev_state is None:
-            dev_state = torch.tensor(self.tune_state.vector(), dtype=torch.float64, device=self.trainer.device)
-        self._infer.repack_master(self.trainer.P, dev_state[:2 * K], self.tune_state.protos)
+        self._infer.repack_master(self.trainer.P, self._protos_dev(), self.tune_state.protos)
         self._infer_stale = False
 
     def sync_inference_weights(self):
         """After training: the inference model follows the updated master
         (utils.py:64-65 updates the reference's modules in place).  The packed
-        copy is rebuilt on the device when it is next used (``infer``)."""
+        copy is rebuilt on the device when it is next used (``infer``); the
+        device prototypes the detect path and the repack read are refreshed
+        here, from the tuning graph's device state when the last backprop left
+        one, else from the host TuneState (DPTuner.sync, a reload, ...)."""
         self._infer_stale = True
         self.prototypes = self.tune_state.protos.copy()
+        K = self.tune_state.protos.shape[0]
+        if getattr(self, "_protos_buf", None) is None or self._protos_buf.numel() != 2 * K:
+            self._protos_buf = torch.zeros(2 * K, dtype=torch.float64, device=self.trainer.device)
+        st = self.trainer.__dict__.pop("tune_state_dev", None)
+        if st is not None:
+            self._protos_buf.copy_(st[:2 * K])
+        else:
+            self._protos_buf.copy_(torch.from_numpy(np.ascontiguousarray(self.tune_state.protos.reshape(-1))))
 
     # -- PreGANPlus.py:83-105 --
     def recover_decision(self, embedding, schedule_data, original_decision):
@@ -238,13 +245,12 @@ class PreGANPlusRecovery(Recovery):
         return self.infer.forward(din[:9 * H].view(1, 3, 3 * H), din[9 * H:].view(1, H, H), out=out)
 
     def _protos_dev(self):
-        K = self.tune_state.protos.shape[0]
-        st = getattr(self.trainer, "tune_state_dev", None)
-        if st is not None:
-            return st[:2 * K]
-        if getattr(self, "_protos0", None) is None:
-            self._protos0 = torch.tensor(self.tune_state.protos, dtype=torch.float64, device=self.trainer.device)
-        return self._protos0
+        """The prototypes of the inference model on the device: the plugin's own
+        buffer, refreshed by sync_inference_weights after every change."""
+        if getattr(self, "_protos_buf", None) is None:
+            self.sync_inference_weights()
+            self._infer_stale = False   # nothing was trained yet: the packed copy is current
+        return self._protos_buf
 
     # -- PreGANPlus.py:115-136 --
     def run_model(self, time_series, original_decision):
@@ -257,9 +263,13 @@ class PreGANPlusRecovery(Recovery):
         embedding = np.where(anom[:, None], out["protos"][0], 0.0)
         self.classes = out["cls"][0].tolist()
         self._final_target = out["final_target"][0].tolist()
-        self.train_gan(embedding, schedule_data)
-        self.tune_model()
-        self.sync_inference_weights()
+        try:
+            self.train_gan(embedding, schedule_data)
+            self.tune_model()
+        finally:
+            # the master moved even if tune_model raised (accuracy() divides by zero
+            # without a positive label, as the reference's does): K1-K3 follow it
+            self.sync_inference_weights()
         return self.recover_decision(embedding, schedule_data, original_decision)
 
     # -- utils.py:86-88 save_gan: Gen with (epoch, accuracy_list), Disc with (0, []) --

@@ -22,13 +22,14 @@ def _series(rng, E, R, H, ties=True):
     s = np.where(spike, rng.uniform(0.8, 1.0, size=s.shape) * scale, s)
     if ties:
         s[0] = s[0, :1]                               # constant rows: every percentile == the value
-        s[1, -1] = s[1, -2]                           # the two largest rows equal in every column
+        if R >= 2:
+            s[1, -1] = s[1, -2]                       # the two largest rows equal in every column
         s[2, :, ::3] = np.round(s[2, :, ::3] / 10) * 10  # many exact ties
     train = rng.uniform(0.1, 1.0, size=(40, 3 * H)) * scale
     return s, train
 
 
-@pytest.mark.parametrize("H,E,R", [(16, 37, 10), (50, 9, 10), (8, 5, 3), (16, 4, 16)])
+@pytest.mark.parametrize("H,E,R", [(16, 37, 10), (50, 9, 10), (8, 5, 3), (16, 4, 16), (16, 6, 1), (50, 6, 2)])
 def test_tune_dataset_bit_exact(H, E, R):
     from preganplus_amd import train as TR
     rng = np.random.default_rng(H * 100 + R)
@@ -43,7 +44,7 @@ def test_tune_dataset_bit_exact(H, E, R):
         np.testing.assert_array_equal(cls[e * R:(e + 1) * R], wh)
         np.testing.assert_array_equal(wins[e * R:(e + 1) * R], TR.convert_to_windows(td).astype(np.float32))
         np.testing.assert_array_equal(inf[e], O.inference_window(series[e], train).astype(np.float32))
-    assert y.sum() > 0 and (y == 0).any()
+    assert (y == 0).any() and (y.sum() > 0 or R < 3)   # one or two rows: nothing exceeds its own percentile
 
 
 def _host_state(P, factor, nz, no):
