@@ -35,7 +35,11 @@ def lib():
     L = ctypes.CDLL(LIB_PATH)
     c_int, c_size, vp = ctypes.c_int, ctypes.c_size_t, ctypes.c_void_p
     fp = ctypes.c_void_p  # device pointers passed as integers
+    # every entry point gets argtypes: without them ctypes passes Python ints as
+    # 32-bit C ints and silently truncates device pointers
+    L.pgp_abi_version.argtypes = []
     L.pgp_abi_version.restype = c_int
+    L.pgp_last_error.argtypes = []
     L.pgp_last_error.restype = ctypes.c_char_p
     L.pgp_supported_hosts.argtypes = [ctypes.POINTER(c_int), c_int]
     L.pgp_supported_hosts.restype = c_int
@@ -63,6 +67,8 @@ def lib():
     L.pgp_forward_fpe_stage.restype = c_int
     L.pgp_migrations.argtypes = [c_int, c_int] + [fp] * 5 + [vp]
     L.pgp_migrations.restype = c_int
+    L.pgp_embedding.argtypes = [c_int, c_int] + [fp] * 3 + [vp]
+    L.pgp_embedding.restype = c_int
     _lib = L
     return L
 

@@ -341,6 +341,9 @@ __global__ __launch_bounds__(256) void gat_fwd_kernel(int B, const float* __rest
     float* gr = Gout + m * Q::DP;
     for (int c = 0; c < H; ++c)
       gr[c] = fmaf(P[G::W_FC + c * 3], xb[0], fmaf(P[G::W_FC + c * 3 + 1], xb[1], P[G::W_FC + c * 3 + 2] * xb[2]));
+    // feature pads written too: the fused encoder reads whole DP rows, and the
+    // workspace regions move with B (a smaller batch lands on a larger one's data)
+    for (int c = H; c < Q::DP; ++c) gr[c] = 0.f;
 #pragma unroll
     for (int k = 0; k < 3; ++k) XB[m * Q::XBP + k] = xb[k];
   }

@@ -49,6 +49,7 @@ class GOBIOptimizer:
         L.pgp_gobi_create.argtypes = [ctypes.c_int, vp, ctypes.c_size_t, ctypes.POINTER(vp)]
         L.pgp_gobi_optimize.argtypes = [vp, ctypes.c_int, vp, vp, vp, vp, ctypes.c_int, vp, vp]
         L.pgp_gobi_destroy.argtypes = [vp]
+        L.pgp_gobi_last_error.argtypes = []
         L.pgp_gobi_last_error.restype = ctypes.c_char_p
         self._L = L
         blob = np.ascontiguousarray(np.concatenate([np.asarray(weights[k], np.float32).reshape(-1) for k in _ORDER]))

@@ -24,6 +24,22 @@ def test_library_exports_every_declared_symbol():
         assert hasattr(L, s), f"missing export {s}"
 
 
+def test_every_ctypes_call_declares_argtypes():
+    """Every pgp_* entry point called through ctypes has argtypes set somewhere
+    in the package: without them ctypes passes Python ints as 32-bit C ints and
+    silently truncates device pointers (a GPU memory fault, not an error)."""
+    import glob
+    files = glob.glob("preganplus_amd/*.py") + glob.glob("tools/*.py") + glob.glob("tests/*.py") + ["bench.py"]
+    calls, decl = {}, set()
+    for f in files:
+        s = open(f).read()
+        for name in re.findall(r"\.(pgp_\w+)\(", s):
+            calls.setdefault(name, f)
+        decl |= set(re.findall(r"\.(pgp_\w+)\.argtypes", s))
+    missing = {k: v for k, v in calls.items() if k not in decl}
+    assert not missing, missing
+
+
 def test_abi_version_and_hosts():
     L = _native.lib()
     assert L.pgp_abi_version() == 1

@@ -204,6 +204,27 @@ def test_batched_tuning_step_is_deterministic():
     assert np.array_equal(gs[0], gs[1])
 
 
+@pytest.mark.parametrize("H", [16, 50])
+def test_smaller_batch_after_larger_is_unchanged(H):
+    """The workspace regions move with B, so a batch smaller than the previous
+    one lands on that batch's data (run_model's detect window after a tune
+    step): its forward + backward equal a fresh trainer's bit for bit."""
+    from preganplus_amd import train as TR
+    Bbig, B = 300, 23
+    w, xb, yb, mb, tb = _batched_case(H, Bbig, seed=11)
+    _, x, y, mult, tgt = _batched_case(H, B, seed=12)
+    a, b = TR.Trainer(H, w, max_batch=Bbig), TR.Trainer(H, w, max_batch=Bbig)
+    a.tune_forward(torch.tensor(xb, dtype=torch.float32))
+    a.tune_backward(Bbig, yb, mb, tb)
+    out = []
+    for tr in (a, b):
+        lg, pr = tr.tune_forward(torch.tensor(x, dtype=torch.float32))
+        tr.tune_backward(B, y, mult, tgt)
+        out.append((lg.cpu().numpy().copy(), pr.cpu().numpy().copy(), tr.G.cpu().numpy().copy()))
+    for u, v in zip(*out):
+        assert np.array_equal(u, v)
+
+
 @pytest.mark.parametrize("H,B", [(8, 3), (16, 37), (50, 21), (64, 5), (16, 300)])
 def test_batched_gan_step_matches_autograd(H, B):
     """GAN step over a ragged batch (pgp_gantrain.hip): new schedule and Disc

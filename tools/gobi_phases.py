@@ -31,6 +31,7 @@ def main():
     for _ in range(3):
         g.optimize(x)
     torch.cuda.synchronize()
+    L.pgp_gobi_prof_reset.argtypes = []
     L.pgp_gobi_prof_reset()
     n = 10
     for _ in range(n):

@@ -3,9 +3,12 @@ library (PGP_LIB), on the same seeded inputs: `dump OUT H B` writes logits,
 protos, latent and the transformer gradient; `compare A B` prints the largest
 relative difference per parameter tensor.  A debugging aid for kernel
 rewrites (the parity tests proper compare against the reference fixtures)."""
+import os
 import sys
 
 import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def dump(out, H, B):
