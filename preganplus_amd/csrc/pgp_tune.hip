@@ -255,7 +255,7 @@ __global__ __launch_bounds__(256) void reduce_kernel(RedArgs a) { reduce_block(a
 // gradient reduction to its end): block x -> (segment, local block) by the
 // prefix table, y = split; a segment's blocks run reduce_block exactly as its own
 // reduce_kernel launch would, so the sums are bit-identical.
-constexpr int kMaxRedSeg = 16;
+constexpr int kMaxRedSeg = 20;
 struct RedTable {
   int n;
   int bx0[kMaxRedSeg + 1];
@@ -300,7 +300,7 @@ __global__ __launch_bounds__(256) void gat_fwd_kernel(int B, const float* __rest
                                                       float* __restrict__ GS) {
   using Q = TuneGeo<H>;
   using G = TGeo<H>;
-  __shared__ float ss[4][64], sx[4][64][3];
+  __shared__ float ss[4][64], sx[4][64][3], sxb[4][64][4];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const long pw = (long)blockIdx.x * 4 + wv;  // (window, step)
   const bool okw = pw < 3L * B;
@@ -334,18 +334,35 @@ __global__ __launch_bounds__(256) void gat_fwd_kernel(int B, const float* __rest
     }
   const float Z = wave_sum(sum);
   const float iz = 1.0f / Z;
+  const long m0 = b * Q::T + (long)w * H;  // token row of host 0
   if (okj) {
 #pragma unroll
     for (int k = 0; k < 3; ++k) xb[k] *= iz;
-    const long m = b * Q::T + (long)w * H + j;
-    float* gr = Gout + m * Q::DP;
-    for (int c = 0; c < H; ++c)
-      gr[c] = fmaf(P[G::W_FC + c * 3], xb[0], fmaf(P[G::W_FC + c * 3 + 1], xb[1], P[G::W_FC + c * 3 + 2] * xb[2]));
-    // feature pads written too: the fused encoder reads whole DP rows, and the
-    // workspace regions move with B (a smaller batch lands on a larger one's data)
-    for (int c = H; c < Q::DP; ++c) gr[c] = 0.f;
 #pragma unroll
-    for (int k = 0; k < 3; ++k) XB[m * Q::XBP + k] = xb[k];
+    for (int k = 0; k < 3; ++k) XB[(m0 + j) * Q::XBP + k] = xb[k];
+  }
+#pragma unroll
+  for (int k = 0; k < 3; ++k) sxb[wv][j][k] = xb[k];
+  __syncthreads();
+  // G rows = fc x-bar, written row-coalesced: lane (rr, q) computes features
+  // 4q .. 4q+3 of rows rr, rr+4, ...; the feature pads come out 0 (fc is 0
+  // there) and are written too (the fused encoder reads whole DP rows)
+  if (okw) {
+    const int q = lane & 15, rr = lane >> 4;
+    if (4 * q < Q::DP) {
+      float fc[4][3];
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) fc[e][k] = 4 * q + e < H ? P[G::W_FC + (4 * q + e) * 3 + k] : 0.f;
+      for (int r = rr; r < H; r += 4) {
+        const float x0 = sxb[wv][r][0], x1 = sxb[wv][r][1], x2 = sxb[wv][r][2];
+        f32x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = fmaf(fc[e][0], x0, fmaf(fc[e][1], x1, fc[e][2] * x2));
+        st4(Gout + (m0 + r) * Q::DP + 4 * q, v);
+      }
+    }
   }
   if (okw && lane == 0) {
     GS[pw * 4] = mx;
@@ -379,40 +396,56 @@ __global__ __launch_bounds__(256) void gat_bwd_kernel(int B, const float* __rest
   const float s = fo.u[0] * x[0] + fo.u[1] * x[1] + fo.u[2] * x[2];
   const float t = fo.v[0] * x[0] + fo.v[1] * x[1] + fo.v[2] * x[2];
   const float mx = okw ? GS[pw * 4] : 0.f, iz = okw ? 1.0f / GS[pw * 4 + 1] : 0.f;
-  float dxb[3] = {0.f, 0.f, 0.f};  // grad of x-bar_j = fc^T dG_j
-  if (okj) {
-    const float* gr = dG + (b * Q::T + (long)w * H + j) * Q::DP;
-    for (int c = 0; c < H; ++c) {
-      const float gv = gr[c];
-#pragma unroll
-      for (int k = 0; k < 3; ++k) dxb[k] = fmaf(P[G::W_FC + c * 3 + k], gv, dxb[k]);
-    }
-  }
   ss[wv][j] = s;
   st[wv][j] = t;
 #pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    sx[wv][j][k] = x[k];
-    sdx[wv][j][k] = dxb[k];
+  for (int k = 0; k < 3; ++k) sx[wv][j][k] = x[k];
+  // grad of x-bar_j = fc^T dG_j, the dG rows read coalesced: lane (rr, q) takes
+  // features 4q .. 4q+3 of rows rr, rr+4, ...; the 16 lanes of a row are summed
+  {
+    const int q = lane & 15, rr = lane >> 4;
+    float fc[4][3];
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int k = 0; k < 3; ++k) fc[e][k] = 4 * q + e < H ? P[G::W_FC + (4 * q + e) * 3 + k] : 0.f;
+    const float* g0 = dG + (b * Q::T + (long)w * H) * Q::DP + 4 * q;
+    for (int r0 = 0; r0 < H; r0 += 4) {  // uniform trip count: the row sums are cross-lane
+      const int r = r0 + rr;
+      const bool okr = okw && r < H && 4 * q < Q::DP;
+      const f32x4 v = okr ? ld4(g0 + (long)r * Q::DP) : zero4();
+      float d[3];
+#pragma unroll
+      for (int k = 0; k < 3; ++k)
+        d[k] = row16_sum(fmaf(fc[0][k], v[0], fmaf(fc[1][k], v[1], fmaf(fc[2][k], v[2], fc[3][k] * v[3]))));
+      if (okr && q == 0) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) sdx[wv][r][k] = d[k];
+      }
+    }
   }
   __syncthreads();
-  // softmax backward: da_ij = dxb_j . x_i ; dot = sum_ij a_ij da_ij
-  float part = 0.f;
+  float dxb[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) dxb[k] = okj ? sdx[wv][j][k] : 0.f;
+  // softmax backward: da_ij = dxb_j . x_i ; dot = sum_ij a_ij da_ij; with this
+  // lane as destination dt = sum_i a_ij (da_ij - dot) lrelu'(pre_ij), gathered
+  // in the same pass as sum a da lrelu' - dot * sum a lrelu'
+  float part = 0.f, s1 = 0.f, s2 = 0.f;
   if (okj)
     for (int i = 0; i < H; ++i) {
-      const float a = expf(lrelu(ss[wv][i] + t) - mx) * iz;
+      const float pre = ss[wv][i] + t;
+      const float a = expf(lrelu(pre) - mx) * iz;
       const float da = dxb[0] * sx[wv][i][0] + dxb[1] * sx[wv][i][1] + dxb[2] * sx[wv][i][2];
+      const float sl = pre > 0.f ? a : 0.01f * a;
       part = fmaf(a, da, part);
+      s1 = fmaf(sl, da, s1);
+      s2 += sl;
     }
   const float dot = wave_sum(part);
   float dt = 0.f, ds = 0.f;
   if (okj) {
-    for (int i = 0; i < H; ++i) {  // this lane as destination
-      const float pre = ss[wv][i] + t;
-      const float a = expf(lrelu(pre) - mx) * iz;
-      const float da = dxb[0] * sx[wv][i][0] + dxb[1] * sx[wv][i][1] + dxb[2] * sx[wv][i][2];
-      dt = fmaf(a * (da - dot), pre > 0.f ? 1.f : 0.01f, dt);
-    }
+    dt = fmaf(-dot, s2, s1);
     for (int jj = 0; jj < H; ++jj) {  // this lane as source
       const float pre = s + st[wv][jj];
       const float a = expf(lrelu(pre) - mx) * iz;
@@ -473,15 +506,14 @@ __global__ __launch_bounds__(256) void gat_param_kernel(int n, const float* __re
 // ============================================================================
 // Decoder weights permuted to the token layout: Wp[n][k'] with k' = tok*DP + c,
 // tok = w*H + h, natural column h*3H + w*H + c (the latent order, models.py:399);
-// rows n: anomaly 0..2H-1, prototype 2H..4H-1, zero pads.  WpF holds, per token,
-// the transposed slab W'[c][n] = Wp[n][tok*DP + c] as linear_kernel<DP, NOP>
-// fragments (the decoder backward into the encoder output).
+// rows n: anomaly 0..2H-1, prototype 2H..4H-1, zero pads.  WpT holds, per token,
+// the transposed slab WpT[tok][c][n] = Wp[n][tok*DP + c] (the decoder backward
+// into the encoder output, pgp_dec.hip).
 template <int H>
 __global__ __launch_bounds__(256) void dec_pack_kernel(const float* __restrict__ P, float* __restrict__ Wp,
-                                                       float* __restrict__ WpF) {
+                                                       float* __restrict__ WpT) {
   using Q = TuneGeo<H>;
   using G = TGeo<H>;
-  constexpr int KB = Q::NOP / 16;
   const long idx = (long)blockIdx.x * 256 + threadIdx.x;
   if (idx >= (long)Q::NOP * Q::KD) return;
   const int n = (int)(idx / Q::KD);
@@ -494,42 +526,7 @@ __global__ __launch_bounds__(256) void dec_pack_kernel(const float* __restrict__
     v = n < 2 * H ? P[G::W_AN + (long)n * G::L + col] : P[G::W_PR + (long)(n - 2 * H) * G::L + col];
   }
   Wp[idx] = v;
-  const int f = (c >> 4) * KB + (n >> 4), l = (c & 15) + 16 * ((n & 15) >> 2);
-  WpF[(long)tok * Q::DP * Q::NOP + ((long)f * 64 + l) * 4 + (n & 3)] = v;
-}
-
-// split-K decoder GEMM: part[s][b][n] = sum over k-blocks of split s of X2[b] . Wp[n]
-template <int H>
-__global__ __launch_bounds__(256) void dec_fwd_kernel(int B, int S, const float* __restrict__ X2,
-                                                      const float* __restrict__ Wp, float* __restrict__ part) {
-  using Q = TuneGeo<H>;
-  constexpr int NT = Q::NOP / 16;
-  constexpr long KBT = Q::KD / 16;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, g = lane >> 4, i = lane & 15;
-  const long b = ((long)blockIdx.x * 4 + wv) * 16 + i;
-  const bool ok = b < B;
-  const int s = blockIdx.y;
-  const long kb0 = KBT * s / S, kb1 = KBT * (s + 1) / S;
-  f32x4 acc[NT];
-#pragma unroll
-  for (int t = 0; t < NT; ++t) acc[t] = zero4();
-  const float* xr = X2 + b * Q::KD + 4 * g;
-  const float* wr = Wp + (long)i * Q::KD + 4 * g;
-  for (long kb = kb0; kb < kb1; ++kb) {
-    const f32x4 xv = ok ? ld4(xr + 16 * kb) : zero4();
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      const f32x4 wf = ld4(wr + (long)16 * t * Q::KD + 16 * kb);
-      acc[t] = mfma(wf[0], xv[0], acc[t]);
-      acc[t] = mfma(wf[1], xv[1], acc[t]);
-      acc[t] = mfma(wf[2], xv[2], acc[t]);
-      acc[t] = mfma(wf[3], xv[3], acc[t]);
-    }
-  }
-  if (ok) {
-#pragma unroll
-    for (int t = 0; t < NT; ++t) st4(part + ((long)s * B + b) * Q::NOP + 16 * t + 4 * g, acc[t]);
-  }
+  WpT[((long)tok * Q::DP + c) * Q::NOP + n] = v;
 }
 
 template <int H>
@@ -807,14 +804,16 @@ bool plan_h(int B, TunePlan* out) {
   q.g = take(M * Q::DP);
   q.xb = take(M * Q::XBP);
   q.gs = take(3L * B * 4);
-  for (int i = 0; i < 3; ++i) q.x[i] = take(M * Q::DP);
+  // buffers the fused encoder kernels write carry a spare row M (pgp_tunef.hpp)
+  const long M1 = M + 1;
+  for (int i = 0; i < 3; ++i) q.x[i] = take(M1 * Q::DP);
   for (int l = 0; l < 2; ++l) {
-    q.xh1[l] = take(M * Q::DP);
-    q.rs1[l] = take(M);
+    q.xh1[l] = take(M1 * Q::DP);
+    q.rs1[l] = take(M1);
   }
-  q.da = take(M * Q::DP);
-  q.db = take(M * Q::DP);
-  q.dq = take(M * Q::Q3P);
+  q.da = take(M1 * Q::DP);
+  q.db = take(M1 * Q::DP);
+  q.dq = take(M1 * 3 * Q::DP);
   q.gsx = take(3L * B * 8);
   q.dpre = take((long)B * Q::NOP);
   q.wp = take((long)Q::NOP * Q::KD);
@@ -826,14 +825,11 @@ bool plan_h(int B, TunePlan* out) {
   const long nrb = (M + 15) / 16;
   q.lin_grid = (int)std::min<long>(PGP_LIN_CAP, std::max<long>(1, (nrb + 3) / 4));
   q.dw_grid = (int)std::min<long>(PGP_DW_CAP, std::max<long>(1, (nrb + 7) / 8));
-  q.dec_bg = (B + 63) / 64;
-  q.dec_dxg = (int)std::min<long>(4, (B + 63) / 64);
-  const long kbt = Q::KD / 16;
-  q.dec_s = (int)std::max<long>(1, std::min<long>(kbt, 512 / q.dec_bg));
+  q.dec_s = dec_fwd_splits(H, B);
   // partial slabs; every bound grows with B, so a workspace sized for B_max serves any B <= B_max
   const long np_max = std::max(Q::Q3P, 64);
   long part = (long)PGP_DW_CAP * (np_max * 64 + np_max);                  // dW slabs
-  part = std::max(part, std::max(512L, (long)q.dec_bg) * 64 * Q::NOP);    // decoder split-K
+  part = std::max(part, (long)q.dec_s * B * Q::NOP);                    // decoder split-K
   // decoder weight gradient: windows split over up to 4 parts of >= 8 chunks
   q.dec_dws = (int)std::max<long>(1, std::min<long>(4, (B + kDwRows - 1) / kDwRows / 8));
   if (q.dec_dws > 1) part = std::max(part, (long)q.dec_dws * (Q::T * Q::NOP * Q::DP + Q::NOP));
@@ -850,8 +846,12 @@ bool plan_h(int B, TunePlan* out) {
       if (ns > 1) pool += r64(ns * nout);
     };
     auto dwr = [&](long np, long kp, long n, long k, bool bias) { red(q.dw_grid, np * kp + np, n * k + (bias ? n : 0)); };
-    const long DPl = Q::DP, Q3Pl = Q::Q3P, Hl = H;
-    for (int l = 1; l >= 0; --l) dwr(Q3Pl, DPl, 3 * Hl, Hl, true);  // in_proj
+    const long DPl = Q::DP, Hl = H;
+    for (int l = 1; l >= 0; --l) {  // in_proj: one dW launch over [q|k|v] x DP rows, three reductions
+      pool += r64((long)q.dw_grid * (3 * DPl * DPl + 3 * DPl));
+      const long ns2 = (q.dw_grid + 255) / 256;
+      if (ns2 > 1) pool += 3 * r64(ns2 * (Hl * Hl + Hl));
+    }
     dwr(DPl, DPl, Hl, Hl, true);           // time encoder
     dwr(DPl, Q::XBP, Hl, 3, false);        // GAT fc
     // level-2 regions of the fused slabs (more than 256 workgroups)
@@ -888,8 +888,7 @@ hipError_t tune_fwd_h(const TunePlan& p, const float* win, const float* P, float
     t.rs1 = ws + p.rs1[l];
     if ((e = launch_tf(H, 1, t, st)) != hipSuccess) return e;
   }
-  TCK((dec_fwd_kernel<H><<<dim3(p.dec_bg, p.dec_s), 256, 0, st>>>(B, p.dec_s, ws + p.x[2], ws + p.wp,
-                                                                   ws + p.part)));
+  if ((e = launch_dec_fwd(H, B, p.dec_s, ws + p.x[2], ws + p.wp, ws + p.part, st)) != hipSuccess) return e;
   TCK((dec_fin_kernel<H><<<(int)(((long)B * 4 * H + 255) / 256), 256, 0, st>>>(B, p.dec_s, ws + p.part, P, logits,
                                                                                 protos)));
   if (latent)
@@ -902,7 +901,7 @@ hipError_t tune_bwd_h(const TunePlan& p, const float* P, float* Gd, float* ws, c
                       const float* protos, const int* y, const float* mult, const float* tgt, hipStream_t st) {
   using Q = TuneGeo<H>;
   using G = TGeo<H>;
-  constexpr int DP = Q::DP, Q3P = Q::Q3P;
+  constexpr int DP = Q::DP;
   const int B = p.B;
   const long M = p.M;
   hipError_t e;
@@ -914,14 +913,8 @@ hipError_t tune_bwd_h(const TunePlan& p, const float* P, float* Gd, float* ws, c
     const long nw = 4L * H * G::L + 4 * H;
     TCK((dec_dw_sum_kernel<H><<<(int)((nw + 255) / 256), 256, 0, st>>>(p.dec_dws, ws + p.part, Gd)));
   }
-  {  // grad of the encoder output = dpre . Wp (token layout): one linear layer per
-     // token (grid.y) with that token's [DP][NOP] slab of Wp^T in LDS
-    LinArgs a = lin_args(B, ws + p.dpre, Q::NOP, ws + p.wpt, Q::NOP, H, 4 * H, 0, nullptr, ws + p.da, Q::T * DP);
-    a.frag = 1;
-    a.bw = (long)DP * Q::NOP;
-    a.by = DP;
-    TCK((linear_kernel<DP, Q::NOP, EPI_STORE><<<dim3(p.dec_dxg, Q::T), 256, 0, st>>>(a)));
-  }
+  // grad of the encoder output = dpre . Wp (token layout, pgp_dec.hip)
+  if ((e = launch_dec_dx(H, B, ws + p.dpre, ws + p.wpt, ws + p.da, st)) != hipSuccess) return e;
   // the encoder layers, fused per unit (pgp_tunef.hip); their weight-gradient
   // slabs (one per workgroup) join the deferred reductions
   const int ng = p.tf_grid;
@@ -960,9 +953,17 @@ hipError_t tune_bwd_h(const TunePlan& p, const float* P, float* Gd, float* ws, c
     if (!rb.add(ng, tf_slab_floats(H, 3), ws + p.tfs[l][1], H, H, H, Lg + G::L_OUT, H, H, (long)H * H,
                 Lg + G::L_OUTB))
       return hipErrorInvalidValue;
-    if ((e = dw<Q3P, DP>(p, rb, ws + p.dq, Q3P, ws + p.x[l], DP, 0, 3 * H, H, Lg + G::L_IN, Lg + G::L_INB, st)) !=
-        hipSuccess)
-      return e;
+    {  // in_proj: dQKV [M][3][DP] (x) X -> three [H][H] blocks of L_IN (+ bias)
+      constexpr int NP = 3 * DP;
+      const long pstride = (long)NP * DP + NP;
+      float* part = rb.take((long)p.dw_grid * pstride);
+      DwArgs a{M, ws + p.dq, NP, ws + p.x[l], DP, 0, part};
+      TCK((dw_kernel<NP, DP><<<p.dw_grid, 256, 0, st>>>(a)));
+      for (int q = 0; q < 3; ++q)
+        if (!rb.add(p.dw_grid, pstride, part + (long)q * DP * DP, H, H, DP, Lg + G::L_IN + (long)q * H * H, H, H,
+                    (long)NP * DP + q * DP - (long)q * DP * DP, Lg + G::L_INB + q * H))
+          return hipErrorInvalidValue;
+    }
   }
   // time encoder: p.da = grad of X0
   if ((e = dw<DP, DP>(p, rb, ws + p.da, DP, ws + p.g, DP, 0, H, H, Gd + G::W_TE, Gd + G::B_TE, st)) != hipSuccess)

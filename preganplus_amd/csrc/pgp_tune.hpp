@@ -37,14 +37,20 @@ struct TunePlan {
   long x[3] = {0, 0, 0};                                 // layer inputs; x[2] = encoder output [M][DP]
   long xh1[2] = {0, 0}, rs1[2] = {0, 0};                 // norm1 x-hat [M][DP], rstd [M] (checkpoints)
   long da = 0, db = 0, dq = 0;                           // backward temporaries ([M][DP], [M][DP], [M][Q3P])
-  long gsx = 0, dpre = 0, wp = 0, wpt = 0, part = 0, total = 0;
+  long gsx = 0, dpre = 0, wp = 0, wpt = 0, part = 0, total = 0;  // wp: Wp [NOP][KD], wpt: WpT [T][DP][NOP]
   long tff = 0;                                          // fused-kernel weight fragments (pgp_tunef.hpp)
   long tfs[2][2] = {{0, 0}, {0, 0}};                     // [layer][ffn | attention] weight-gradient slabs
   long pool = 0, pool_len = 0;  // the backward's deferred-reduction regions (RedBatch)
-  int lin_grid = 0, dw_grid = 0, dec_s = 0, dec_bg = 0, dec_dxg = 0, dec_dws = 1, tf_grid = 0;
+  int lin_grid = 0, dw_grid = 0, dec_s = 0, dec_dws = 1, tf_grid = 0;
 };
 
 bool tune_plan(int H, int B, TunePlan* p);
+
+// decoder GEMMs (pgp_dec.hip): split-K forward into part[S][B][NOP] and the
+// backward into the encoder output's gradient [M][DP]
+int dec_fwd_splits(int H, int B);
+hipError_t launch_dec_fwd(int H, int B, int S, const float* X2, const float* Wp, float* part, hipStream_t st);
+hipError_t launch_dec_dx(int H, int B, const float* dpre, const float* WpT, float* dX, hipStream_t st);
 
 hipError_t launch_tune_forward(const TunePlan& p, const float* windows, const float* P, float* ws, float* latent,
                                float* logits, float* protos, hipStream_t st);

@@ -38,6 +38,43 @@ namespace {
 
 constexpr int kTfWaves = 4;  // one wave per SIMD (the backward needs > 256 registers)
 
+// Phase attribution (profiling builds only: make variant NAME=st
+// VFLAGS=-DPGP_TF_STAMPS, read by tools/tf_stamps.py): each wave adds the
+// shader-clock cycles between consecutive TF_ST(k) marks to phase k of its slot
+// in tf_stamps[kind][wave] (vector stores by lane 0; one writer per slot).
+#ifdef PGP_TF_STAMPS
+constexpr int kStPhases = 16, kStWaves = 1024;
+__device__ unsigned long long tf_stamps[4][kStWaves][kStPhases];
+#define TF_ST_INIT()                                              \
+  unsigned long long st_acc[kStPhases];                           \
+  for (int _k = 0; _k < kStPhases; ++_k) st_acc[_k] = 0;          \
+  unsigned long long st_t = __builtin_amdgcn_s_memtime()
+#define TF_ST(k)                                                  \
+  do {                                                            \
+    __builtin_amdgcn_sched_barrier(0);                            \
+    const unsigned long long _n = __builtin_amdgcn_s_memtime();   \
+    st_acc[k] += _n - st_t;                                       \
+    st_t = _n;                                                    \
+    __builtin_amdgcn_sched_barrier(0);                            \
+  } while (0)
+#define TF_ST_END(kind)                                                                    \
+  do {                                                                                     \
+    const int _w = (int)blockIdx.x * kTfWaves + (int)(threadIdx.x >> 6);                   \
+    if ((threadIdx.x & 63) == 0 && _w < kStWaves)                                          \
+      for (int _k = 0; _k < kStPhases; ++_k) tf_stamps[kind][_w][_k] += st_acc[_k];         \
+  } while (0)
+#else
+#define TF_ST_INIT() \
+  do {               \
+  } while (0)
+#define TF_ST(k) \
+  do {           \
+  } while (0)
+#define TF_ST_END(kind) \
+  do {                  \
+  } while (0)
+#endif
+
 // fragment group of matrix `mat`: float offset ((tile * KG + q) * 64 + lane) * 4 + e
 // holds A[i = lane & 15][k = lane >> 4] of k-step 4q + e of output tile `tile`
 template <int H>
@@ -118,29 +155,48 @@ PGP_DEV long tf_row(long p, int w) {
   return b * 3 * H + (long)w * H + (p - b * H);
 }
 
-// N-layout tiles <-> token-major [M][ld] rows (16-byte row groups)
+// N-layout tiles <-> token-major [M][ld] rows (16-byte row groups).  Loads and
+// stores are unconditional (no branches, so the compiler's memory-counter waits
+// stay exact and a load issued a unit ahead is not waited for together with the
+// stores after it): a lane outside the batch reads row 0 (row[] is 0 there) and
+// selects zeros, and writes the spare row M of the destination (plan: M + 1 rows).
 template <int NTL>
 PGP_DEV void load_tiles(f32x4 (&v)[NTL][3], const float* __restrict__ base, int ld, const long (&row)[3], bool ok,
                         int g) {
 #pragma unroll
   for (int w = 0; w < 3; ++w)
 #pragma unroll
-    for (int t = 0; t < NTL; ++t) v[t][w] = ok ? ld4(base + row[w] * ld + 16 * t + 4 * g) : zero4();
+    for (int t = 0; t < NTL; ++t) {
+      const f32x4 x = ld4(base + row[w] * ld + 16 * t + 4 * g);
+      v[t][w] = ok ? x : zero4();
+    }
 }
 template <int NTL>
 PGP_DEV void store_tiles(const f32x4 (&v)[NTL][3], float* __restrict__ base, int ld, const long (&row)[3], bool ok,
-                         int g) {
-  if (!ok) return;
+                         long spare, int g) {
 #pragma unroll
-  for (int w = 0; w < 3; ++w)
+  for (int w = 0; w < 3; ++w) {
+    const long r = ok ? row[w] : spare;
 #pragma unroll
-    for (int t = 0; t < NTL; ++t) st4(base + row[w] * ld + 16 * t + 4 * g, v[t][w]);
+    for (int t = 0; t < NTL; ++t) st4(base + r * ld + 16 * t + 4 * g, v[t][w]);
+  }
+}
+
+// one tile (c: tile c / 3 of step c % 3) of load_tiles, for tf_gemm_side work
+template <int NTL>
+PGP_DEV void load_tile(f32x4 (&v)[NTL][3], const float* __restrict__ base, int ld, const long (&row)[3], bool ok,
+                       int g, int c) {
+  const f32x4 x = ld4(base + row[c % 3] * ld + 16 * (c / 3) + 4 * g);
+  v[c / 3][c % 3] = ok ? x : zero4();
 }
 
 // acc[o][w] += A . B over KSn k-steps; A = NO tiles of fragment groups in LDS
-// (KG groups per tile), B k-step s for step w = bsrc(s, w)
-template <int NO, int KSn, class BF>
-PGP_DEV void tf_gemm(f32x4 (&acc)[NO][3], const float* A, BF bsrc, int lane) {
+// (KG groups per tile), B k-step s for step w = bsrc(s, w).  side(i) runs after
+// the i-th of the NO * KG fragment groups (its 12 MFMAs): memory instructions
+// placed there are spread over the GEMM instead of bursting between phases
+// (every CU reaches a phase at about the same time).
+template <int NO, int KSn, class BF, class SIDE>
+PGP_DEV void tf_gemm_side(f32x4 (&acc)[NO][3], const float* A, BF bsrc, int lane, SIDE side) {
   constexpr int KGn = (KSn + 3) / 4;
 #pragma unroll
   for (int o = 0; o < NO; ++o) {
@@ -153,11 +209,16 @@ PGP_DEV void tf_gemm(f32x4 (&acc)[NO][3], const float* A, BF bsrc, int lane) {
 #pragma unroll
           for (int w = 0; w < 3; ++w) acc[o][w] = mfma(a[e], bsrc(4 * q + e, w), acc[o][w]);
         }
+      side(o * KGn + q);
     }
     // one output tile at a time: keeps the scheduler from hoisting every tile's
     // LDS fragments (register pressure)
     __builtin_amdgcn_sched_barrier(0);
   }
+}
+template <int NO, int KSn, class BF>
+PGP_DEV void tf_gemm(f32x4 (&acc)[NO][3], const float* A, BF bsrc, int lane) {
+  tf_gemm_side<NO, KSn>(acc, A, bsrc, lane, [](int) {});
 }
 
 // accumulators initialised with a per-row bias (LDS, natural rows)
@@ -367,6 +428,17 @@ PGP_DEV void dw_step(f32x4 (&acc)[NA][NB], float (&bsum)[NA], const float* sa, c
       for (int U = 0; U < NB; ++U) acc[T][U] = mfma(a[T][e], b[U][e], acc[T][U]);
 }
 
+// rows of unit u's pairs at the 3 window steps; false for a lane past the
+// wave's units or the batch
+template <int H>
+PGP_DEV bool unit_rows(long u, long u1, long npairs, int j, long (&row)[3]) {
+  const long p = u * 16 + j;
+  const bool ok = u < u1 && p < npairs;
+#pragma unroll
+  for (int w = 0; w < 3; ++w) row[w] = ok ? tf_row<H>(p, w) : 0;
+  return ok;
+}
+
 // unit range of one wave (contiguous, balanced over all waves of the grid)
 PGP_DEV void unit_range(long nu, long& u0, long& u1) {
   const long nw = (long)gridDim.x * kTfWaves;
@@ -438,38 +510,77 @@ __global__ __launch_bounds__(kTfWaves * 64, 1) void tf_fwd_kernel(TfArgs a) {
   if (layer == 0) dma_groups(a.frags + F::TE_OFF, sm + L::W_TE, F::G_TE, wv, kTfWaves, lane);
   dma_groups(fr + F::OFF_IN, sm + L::W_IN, F::G_IN + F::G_O + F::G_F1 + F::G_F2, wv, kTfWaves, lane);
   load_params<H>(sm + L::PAR, a.P, layer);
+  TF_ST_INIT();
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  TF_ST(0);
   const float* par = sm + L::PAR;
-  const long npairs = (long)a.B * H, nu = (npairs + 15) / 16;
+  const long npairs = (long)a.B * H, nu = (npairs + 15) / 16, spare = 3 * npairs;
   long u0, u1;
   unit_range(nu, u0, u1);
+  // Memory traffic rides on the GEMMs (tf_gemm_side), one instruction per
+  // fragment group: the unit's input (layer 0: the GAT output) is loaded one
+  // unit ahead during the previous unit's linear2; x0 is stored during q|k|v,
+  // norm1's x-hat / rstd during linear1, and the layer output during the next
+  // unit's q|k|v (the last one after the loop).
+  f32x4 Xn[NT][3], Rp[NT][3];
+  long prow[3] = {spare, spare, spare};  // rows of the output held in Rp
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int w = 0; w < 3; ++w) Rp[t][w] = zero4();
+  {
+    long rn[3];
+    const bool okn = unit_rows<H>(u0, u1, npairs, j, rn);
+    load_tiles<NT>(Xn, a.in, F::DP, rn, okn, g);
+  }
+  auto tile_at = [&](float* base, long r) { return base + r * F::DP + 4 * g; };
 #pragma unroll 1
   for (long u = u0; u < u1; ++u) {
-    const long p = u * 16 + j;
-    const bool ok = p < npairs;
     long row[3];
+    const bool ok = unit_rows<H>(u, u1, npairs, j, row);
+    long srow[3];
 #pragma unroll
-    for (int w = 0; w < 3; ++w) row[w] = ok ? tf_row<H>(p, w) : 0;
+    for (int w = 0; w < 3; ++w) srow[w] = ok ? row[w] : spare;
     f32x4 X[NT][3];
     if (layer == 0) {  // X0 = Wte g + bte + pe[w]  (models.py:390-393)
-      f32x4 Gi[NT][3];
-      load_tiles<NT>(Gi, a.in, F::DP, row, ok, g);
+      TF_ST(1);
 #pragma unroll
       for (int o = 0; o < NT; ++o)
 #pragma unroll
         for (int w = 0; w < 3; ++w) X[o][w] = ld4(par + Q::BTE + w * F::DP + 16 * o + 4 * g);
-      tf_gemm<NT, F::KS>(X, sm + L::W_TE, [&](int s, int w) { return Gi[s >> 2][w][s & 3]; }, lane);
-      store_tiles<NT>(X, a.x0, F::DP, row, ok, g);
+      tf_gemm<NT, F::KS>(X, sm + L::W_TE, [&](int s, int w) { return Xn[s >> 2][w][s & 3]; }, lane);
+      TF_ST(2);
     } else {
-      load_tiles<NT>(X, a.in, F::DP, row, ok, g);
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int w = 0; w < 3; ++w) X[t][w] = Xn[t][w];
+      TF_ST(1);
     }
     f32x4 QKV[F::NQ][3];
     init_bias<F::NQ>(QKV, par + Q::BIN, g);
-    tf_gemm<F::NQ, F::KS>(QKV, sm + L::W_IN, [&](int s, int w) { return X[s >> 2][w][s & 3]; }, lane);
+    {  // side work: the previous unit's output, then (layer 0) this unit's x0
+      constexpr int NS = 3 * NT, NG = F::NQ * F::KG, PER = (2 * NS + NG - 1) / NG;
+      tf_gemm_side<F::NQ, F::KS>(QKV, sm + L::W_IN, [&](int s, int w) { return X[s >> 2][w][s & 3]; }, lane,
+                                 [&](int i) {
+#pragma unroll
+                                   for (int k = 0; k < PER; ++k) {
+                                     const int c = i * PER + k;
+                                     if (c < NS) {
+                                       st4(tile_at(a.out, prow[c % 3]) + 16 * (c / 3), Rp[c / 3][c % 3]);
+                                     } else if (c < 2 * NS && layer == 0) {
+                                       const int d = c - NS;
+                                       st4(tile_at(a.x0, srow[d % 3]) + 16 * (d / 3), X[d / 3][d % 3]);
+                                     }
+                                   }
+                                 });
+    }
+    TF_ST(3);
     float Pr[2][3][3];
     f32x4 O[NT][3];
     tf_attn_fwd<H>(QKV, Pr, O, g);
+    TF_ST(4);
     f32x4 R[NT][3];
     init_bias<NT>(R, par + Q::BO, g);
     tf_gemm<NT, F::KS>(R, sm + L::W_O, [&](int s, int w) { return O[s >> 2][w][s & 3]; }, lane);
@@ -477,13 +588,10 @@ __global__ __launch_bounds__(kTfWaves * 64, 1) void tf_fwd_kernel(TfArgs a) {
     for (int t = 0; t < NT; ++t)
 #pragma unroll
       for (int w = 0; w < 3; ++w) R[t][w] += X[t][w];
+    TF_ST(5);
     float rs[3];
     tf_ln<H, NT>(R, rs, g);  // R = x-hat of norm1
-    store_tiles<NT>(R, a.xh1, F::DP, row, ok, g);
-    if (ok && g == 0) {
-#pragma unroll
-      for (int w = 0; w < 3; ++w) a.rs1[row[w]] = rs[w];
-    }
+    TF_ST(6);
     // y1 = gamma1 x-hat + beta1 (in place of X: the residual of the FFN)
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
@@ -493,59 +601,92 @@ __global__ __launch_bounds__(kTfWaves * 64, 1) void tf_fwd_kernel(TfArgs a) {
     }
     f32x4 Fh[4][3];
     init_bias<4>(Fh, par + Q::B1, g);
-    tf_gemm<4, F::KS>(Fh, sm + L::W_F1, [&](int s, int w) { return X[s >> 2][w][s & 3]; }, lane);
+    {  // side work: norm1's x-hat tiles and rstd (every lane group: the same value)
+      constexpr int NS = 3 * NT + 3, NG = 4 * F::KG, PER = (NS + NG - 1) / NG;
+      tf_gemm_side<4, F::KS>(Fh, sm + L::W_F1, [&](int s, int w) { return X[s >> 2][w][s & 3]; }, lane,
+                             [&](int i) {
+#pragma unroll
+                               for (int k = 0; k < PER; ++k) {
+                                 const int c = i * PER + k;
+                                 if (c < 3 * NT)
+                                   st4(tile_at(a.xh1, srow[c % 3]) + 16 * (c / 3), R[c / 3][c % 3]);
+                                 else if (c < NS)
+                                   a.rs1[srow[c - 3 * NT]] = rs[c - 3 * NT];
+                               }
+                             });
+    }
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
       for (int w = 0; w < 3; ++w)
 #pragma unroll
         for (int r = 0; r < 4; ++r) Fh[t][w][r] = fmaxf(Fh[t][w][r], 0.f);
+    TF_ST(7);
     init_bias<NT>(R, par + Q::B2, g);
-    tf_gemm<NT, 16>(R, sm + L::W_F2, [&](int s, int w) { return Fh[s >> 2][w][s & 3]; }, lane);
+    {  // side work: the next unit's input
+      long rn[3];
+      const bool okn = unit_rows<H>(u + 1, u1, npairs, j, rn);
+      constexpr int NS = 3 * NT, NG = NT * F::KGF, PER = (NS + NG - 1) / NG;
+      tf_gemm_side<NT, 16>(R, sm + L::W_F2, [&](int s, int w) { return Fh[s >> 2][w][s & 3]; }, lane,
+                           [&](int i) {
+#pragma unroll
+                             for (int k = 0; k < PER; ++k) {
+                               const int c = i * PER + k;
+                               if (c < NS) {
+                                 const f32x4 v = ld4(tile_at(const_cast<float*>(a.in), rn[c % 3]) + 16 * (c / 3));
+                                 Xn[c / 3][c % 3] = okn ? v : zero4();
+                               }
+                             }
+                           });
+    }
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
       for (int w = 0; w < 3; ++w) R[t][w] += X[t][w];
+    TF_ST(8);
     tf_ln<H, NT>(R, rs, g);
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       const f32x4 ga = ld4(par + Q::N2W + 16 * t + 4 * g), be = ld4(par + Q::N2B + 16 * t + 4 * g);
 #pragma unroll
-      for (int w = 0; w < 3; ++w) R[t][w] = R[t][w] * ga + be;
+      for (int w = 0; w < 3; ++w) Rp[t][w] = R[t][w] * ga + be;
     }
-    store_tiles<NT>(R, a.out, F::DP, row, ok, g);
+#pragma unroll
+    for (int w = 0; w < 3; ++w) prow[w] = srow[w];
+    TF_ST(9);
   }
+  // the last unit's output
+#pragma unroll
+  for (int w = 0; w < 3; ++w)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) st4(tile_at(a.out, prow[w]) + 16 * t, Rp[t][w]);
+  TF_ST(10);
+  TF_ST_END(layer);
 }
 
 // ============================================================================
-// end-of-kernel combination: each wave adds its register partial into the
-// workgroup's LDS slab in wave order (deterministic), then the slab is written
+// end-of-kernel combination: each wave stores its register partials into a
+// region of its own (plain stores, all waves at once), then the workgroup sums
+// the regions in wave order (deterministic) straight into its global slab
 // ============================================================================
-PGP_DEV void slab_zero(float* s, int n) {
-  for (int k = threadIdx.x; k < n; k += blockDim.x) s[k] = 0.f;
-}
-PGP_DEV void slab_out(const float* s, float* dst, int n) {
-  for (int k = threadIdx.x; k < n; k += blockDim.x) dst[k] = s[k];
-}
-
-// compressed row accumulator (acc_rows) -> slab[row] for rows < lim
-PGP_DEV void add_rows_c(float* slab, float acc, int lim, int g, int j) {
+// compressed row accumulator (acc_rows) -> dst[row] for rows < lim
+PGP_DEV void put_rows_c(float* dst, float acc, int lim, int g, int j) {
   const int n = 16 * (j >> 2) + 4 * g + (j & 3);
-  if (n < lim) slab[n] += acc;
+  if (n < lim) dst[n] = acc;
 }
-// bias sums bsum[T] (per lane: row 16T + i, this lane group's tokens) -> slab
+// bias sums bsum[T] (per lane: row 16T + i, this lane group's tokens) -> dst
 template <int NA>
-PGP_DEV void add_bias(float* slab, const float (&b)[NA], int lim, int g, int i) {
+PGP_DEV void put_bias(float* dst, const float (&b)[NA], int lim, int g, int i) {
 #pragma unroll
   for (int T = 0; T < NA; ++T) {
     const float s = xsum(b[T], true);
     const int n = 16 * T + i;
-    if (g == 0 && n < lim) slab[n] += s;
+    if (g == 0 && n < lim) dst[n] = s;
   }
 }
-// dW tile sums acc[T][U] (row 16T+4g+r, column 16U+j) -> slab[row * ld + col]
+// dW tile sums acc[T][U] (row 16T+4g+r, column 16U+j) -> dst[row * ld + col]
 template <int NA, int NB>
-PGP_DEV void add_dw(float* slab, const f32x4 (&acc)[NA][NB], int rows, int cols, int ld, int g, int j) {
+PGP_DEV void put_dw(float* dst, const f32x4 (&acc)[NA][NB], int rows, int cols, int ld, int g, int j) {
 #pragma unroll
   for (int T = 0; T < NA; ++T)
 #pragma unroll
@@ -553,8 +694,17 @@ PGP_DEV void add_dw(float* slab, const f32x4 (&acc)[NA][NB], int rows, int cols,
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int n = 16 * T + 4 * g + r, c = 16 * U + j;
-        if (n < rows && c < cols) slab[n * ld + c] += acc[T][U][r];
+        if (n < rows && c < cols) dst[n * ld + c] = acc[T][U][r];
       }
+}
+// dst[k] = sum over the kTfWaves regions (pitch `pitch`) in wave order, k < n
+PGP_DEV void sum_regions(float* __restrict__ dst, const float* src, int pitch, int n) {
+  for (int k = threadIdx.x; k < n; k += blockDim.x) {
+    float v = src[k];
+#pragma unroll
+    for (int w = 1; w < kTfWaves; ++w) v += src[w * pitch + k];
+    dst[k] = v;
+  }
 }
 
 // ============================================================================
@@ -574,6 +724,7 @@ struct BffL {
   static constexpr int S_W2 = 0, S_B2 = S_W2 + H * 64, S_W1 = S_B2 + H, S_B1 = S_W1 + 64 * H,
                        S_G1 = S_B1 + 64, S_BT1 = S_G1 + H, S_G2 = S_BT1 + H, S_BT2 = S_G2 + H,
                        SLAB = S_BT2 + H;
+  static constexpr int NV = 5 * H + 64;  // per-wave vector partials in the epilogue
 };
 
 // Add a unit's dW tiles (registers) into the workgroup's LDS accumulators
@@ -597,9 +748,9 @@ PGP_DEV void lds_acc_add(float* acc, const f32x4 (&d)[NA][NB], int wv, int lane)
     __syncthreads();
   }
 }
-// LDS accumulator tile (row 16T+4g+r, column 16U+j per lane) -> slab
+// LDS accumulator tile (row 16T+4g+r, column 16U+j per lane) -> dst (global)
 template <int NA, int NB>
-PGP_DEV void add_dw_lds(float* slab, const float* acc, int rows, int cols, int ld, int g, int j, int lane) {
+PGP_DEV void put_dw_lds(float* dst, const float* acc, int rows, int cols, int ld, int g, int j, int lane) {
 #pragma unroll
   for (int T = 0; T < NA; ++T)
 #pragma unroll
@@ -608,7 +759,7 @@ PGP_DEV void add_dw_lds(float* slab, const float* acc, int rows, int cols, int l
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int n = 16 * T + 4 * g + r, c = 16 * U + j;
-        if (n < rows && c < cols) slab[n * ld + c] += v[r];
+        if (n < rows && c < cols) dst[n * ld + c] = v[r];
       }
     }
 }
@@ -619,7 +770,7 @@ __global__ __launch_bounds__(kTfWaves * 64, 1) void tf_bwd_ffn_kernel(TfArgs a) 
   using L = BffL<H>;
   using Q = TfPar<H>;
   constexpr int NT = F::NT;
-  static_assert(L::SLAB <= L::SCR, "slab fits the LDS it reuses");
+  static_assert(kTfWaves * L::NV <= L::SCR, "epilogue partials fit the LDS they reuse");
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, g = lane >> 4, j = lane & 15;
   const int layer = a.layer;
@@ -627,9 +778,10 @@ __global__ __launch_bounds__(kTfWaves * 64, 1) void tf_bwd_ffn_kernel(TfArgs a) 
              kTfWaves, lane);
   load_params<H>(sm + L::PAR, a.P, layer);
   for (int k = threadIdx.x; k < L::NTILE * 256; k += blockDim.x) sm[L::ACC + k] = 0.f;
+  TF_ST_INIT();
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  const float* par = sm + L::PAR;
+  TF_ST(0);
   float* sa = sm + L::SCR + wv * (L::SCR_A + L::SCR_B);
   float* sb = sa + L::SCR_A;
   float* accW2 = sm + L::ACC;
@@ -642,10 +794,23 @@ __global__ __launch_bounds__(kTfWaves * 64, 1) void tf_bwd_ffn_kernel(TfArgs a) 
   for (int U = 0; U < 4; ++U) b1s[U] = 0.f;
   // every wave runs the same number of rounds (the LDS accumulation joins
   // barriers); a wave past its units computes on zeros, which adds exactly 0
-  const long npairs = (long)a.B * H, nu = (npairs + 15) / 16;
+  const long npairs = (long)a.B * H, nu = (npairs + 15) / 16, spare = 3 * npairs;
   long u0, u1;
   unit_range(nu, u0, u1);
   const long nwav = (long)gridDim.x * kTfWaves, rounds = (nu + nwav - 1) / nwav;
+  // LN1's x-hat and rstd of the unit are loaded one unit ahead (see tf_fwd_kernel)
+  f32x4 Yn[NT][3];
+  float rsn[3];
+  {
+    long rn[3];
+    const bool okn = unit_rows<H>(u0, u1, npairs, j, rn);
+    load_tiles<NT>(Yn, a.xh1, F::DP, rn, okn, g);
+#pragma unroll
+    for (int w = 0; w < 3; ++w) {
+      const float r = a.rs1[rn[w]];
+      rsn[w] = okn ? r : 0.f;
+    }
+  }
 #pragma unroll 1
   for (long it = 0; it < rounds; ++it) {
     // loop-variant view of the LDS base: keeps LICM from hoisting the
@@ -660,20 +825,21 @@ __global__ __launch_bounds__(kTfWaves * 64, 1) void tf_bwd_ffn_kernel(TfArgs a) 
     auto y1 = [&](const f32x4 (&xh)[NT][3], int t, int w) {
       return xh[t][w] * ld4(par + Q::N1W + 16 * t + 4 * g) + ld4(par + Q::N1B + 16 * t + 4 * g);
     };
-    const long p = u * 16 + j;
-    const bool ok = u < u1 && p < npairs;
     long row[3];
-#pragma unroll
-    for (int w = 0; w < 3; ++w) row[w] = ok ? tf_row<H>(p, w) : 0;
+    const bool ok = unit_rows<H>(u, u1, npairs, j, row);
     f32x4 dY[NT][3], Fh[4][3];
     float rs1[3], rs2[3];
 #pragma unroll
-    for (int w = 0; w < 3; ++w) rs1[w] = ok ? a.rs1[row[w]] : 0.f;
+    for (int w = 0; w < 3; ++w) rs1[w] = rsn[w];
     {  // recompute the FFN (pre-activation F) and norm2's x-hat
       f32x4 X2[NT][3];
       {
         f32x4 Y1[NT][3];
-        load_tiles<NT>(Y1, a.xh1, F::DP, row, ok, g);
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+          for (int w = 0; w < 3; ++w) Y1[t][w] = Yn[t][w];
+        TF_ST(1);
 #pragma unroll
         for (int t = 0; t < NT; ++t)
 #pragma unroll
@@ -692,12 +858,22 @@ __global__ __launch_bounds__(kTfWaves * 64, 1) void tf_bwd_ffn_kernel(TfArgs a) 
         for (int w = 0; w < 3; ++w)
 #pragma unroll
           for (int r = 0; r < 4; ++r) Fh[t][w][r] = fmaxf(Fh[t][w][r], 0.f);
-      tf_gemm<NT, 16>(X2, smz + L::W_F2, [&](int s, int w) { return Fh[s >> 2][w][s & 3]; }, lane);
+      TF_ST(2);
+      {  // side work: dOut of the unit
+        constexpr int NS = 3 * NT, NG = NT * F::KGF, PER = (NS + NG - 1) / NG;
+        tf_gemm_side<NT, 16>(X2, smz + L::W_F2, [&](int s, int w) { return Fh[s >> 2][w][s & 3]; }, lane,
+                             [&](int i) {
+#pragma unroll
+                               for (int k = 0; k < PER; ++k)
+                                 if (i * PER + k < NS) load_tile<NT>(dY, a.in, F::DP, row, ok, g, i * PER + k);
+                             });
+      }
       __builtin_amdgcn_sched_barrier(0);
+      TF_ST(3);
       tf_ln<H, NT>(X2, rs2, g);
-      load_tiles<NT>(dY, a.in, F::DP, row, ok, g);
       tf_ln_bwd<H, NT>(dY, X2, rs2, par + Q::N2W, g, j, ag2, ab2);  // dY <- dR2
     }
+    TF_ST(4);
     __builtin_amdgcn_sched_barrier(0);
     {  // dW2 += dR2 (x) relu(F), db2 += sum dR2
       f32x4 dW[NT][4];
@@ -711,7 +887,9 @@ __global__ __launch_bounds__(kTfWaves * 64, 1) void tf_bwd_ffn_kernel(TfArgs a) 
         stage<4>(Fh, w, sb, g, j);
         dw_step<NT, 4>(dW, b2s, sa, sb, g, j);
       }
+      TF_ST(5);
       lds_acc_add<NT, 4>(accW2, dW, wv, lane);
+      TF_ST(6);
     }
     __builtin_amdgcn_sched_barrier(0);
     f32x4 XH1[NT][3];
@@ -722,7 +900,15 @@ __global__ __launch_bounds__(kTfWaves * 64, 1) void tf_bwd_ffn_kernel(TfArgs a) 
       for (int t = 0; t < 4; ++t)
 #pragma unroll
         for (int w = 0; w < 3; ++w) dF[t][w] = zero4();
-      tf_gemm<4, F::KS>(dF, smz + L::W_F2T, [&](int s, int w) { return dY[s >> 2][w][s & 3]; }, lane);
+      {  // side work: norm1's x-hat, reloaded (L2): not held through the phases above
+        constexpr int NS = 3 * NT, NG = 4 * F::KG, PER = (NS + NG - 1) / NG;
+        tf_gemm_side<4, F::KS>(dF, smz + L::W_F2T, [&](int s, int w) { return dY[s >> 2][w][s & 3]; }, lane,
+                               [&](int i) {
+#pragma unroll
+                                 for (int k = 0; k < PER; ++k)
+                                   if (i * PER + k < NS) load_tile<NT>(XH1, a.xh1, F::DP, row, ok, g, i * PER + k);
+                               });
+      }
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
@@ -730,7 +916,7 @@ __global__ __launch_bounds__(kTfWaves * 64, 1) void tf_bwd_ffn_kernel(TfArgs a) 
 #pragma unroll
           for (int r = 0; r < 4; ++r) dF[t][w][r] = Fh[t][w][r] > 0.f ? dF[t][w][r] : 0.f;
       __builtin_amdgcn_sched_barrier(0);
-      load_tiles<NT>(XH1, a.xh1, F::DP, row, ok, g);  // reloaded (L2): not held through the phases above
+      TF_ST(7);
       {  // dW1 += dF (x) y1, db1 += sum dF
         f32x4 dW[4][NT];
 #pragma unroll
@@ -743,38 +929,59 @@ __global__ __launch_bounds__(kTfWaves * 64, 1) void tf_bwd_ffn_kernel(TfArgs a) 
           stage_fn<NT>([&](int t) { return y1(XH1, t, w); }, sb, g, j);
           dw_step<4, NT>(dW, b1s, sa, sb, g, j);
         }
+        TF_ST(8);
         lds_acc_add<4, NT>(accW1, dW, wv, lane);
+        TF_ST(9);
       }
       __builtin_amdgcn_sched_barrier(0);
       // dy1 = W1^T dF + dR2 (residual)
-      tf_gemm<NT, 16>(dY, smz + L::W_F1T, [&](int s, int w) { return dF[s >> 2][w][s & 3]; }, lane);
+      {  // side work: the next unit's norm1 x-hat and rstd
+        long rn[3];
+        const bool okn = unit_rows<H>(u + 1, u1, npairs, j, rn);
+        constexpr int NS = 3 * NT + 3, NG = NT * F::KGF, PER = (NS + NG - 1) / NG;
+        tf_gemm_side<NT, 16>(dY, smz + L::W_F1T, [&](int s, int w) { return dF[s >> 2][w][s & 3]; }, lane,
+                             [&](int i) {
+#pragma unroll
+                               for (int k = 0; k < PER; ++k) {
+                                 const int c = i * PER + k;
+                                 if (c < 3 * NT) {
+                                   load_tile<NT>(Yn, a.xh1, F::DP, rn, okn, g, c);
+                                 } else if (c < NS) {
+                                   const float r = a.rs1[rn[c - 3 * NT]];
+                                   rsn[c - 3 * NT] = okn ? r : 0.f;
+                                 }
+                               }
+                             });
+      }
     }
     __builtin_amdgcn_sched_barrier(0);
+    TF_ST(10);
     tf_ln_bwd<H, NT>(dY, XH1, rs1, par + Q::N1W, g, j, ag1, ab1);  // -> dR1
-    store_tiles<NT>(dY, a.out, F::DP, row, ok, g);
+    store_tiles<NT>(dY, a.out, F::DP, row, ok, spare, g);
+    TF_ST(11);
   }
-  // one slab per workgroup: the LDS dW tiles, then the waves' vector partials in wave order
-  __syncthreads();
-  float* slab = sm;  // the weight area is free now
-  slab_zero(slab, L::SLAB);
-  __syncthreads();
+  TF_ST(12);
+  // one slab per workgroup: the LDS dW tiles (already summed over the waves in
+  // a fixed order), then the waves' vector partials summed in wave order
+  float* slab = a.part + (long)blockIdx.x * L::SLAB;
   if (wv == 0) {
-    add_dw_lds<NT, 4>(slab + L::S_W2, accW2, H, 64, 64, g, j, lane);
-    add_dw_lds<4, NT>(slab + L::S_W1, accW1, 64, H, H, g, j, lane);
+    put_dw_lds<NT, 4>(slab + L::S_W2, accW2, H, 64, 64, g, j, lane);
+    put_dw_lds<4, NT>(slab + L::S_W1, accW1, 64, H, H, g, j, lane);
   }
+  __syncthreads();   // every wave is past its units: the weight area is free
+  float* vr = sm + wv * L::NV;  // this wave's vector partials: b2 | b1 | g1 | bt1 | g2 | bt2
+  put_bias<NT>(vr, b2s, H, g, j);
+  put_bias<4>(vr + H, b1s, 64, g, j);
+  put_rows_c(vr + H + 64, ag1, H, g, j);
+  put_rows_c(vr + 2 * H + 64, ab1, H, g, j);
+  put_rows_c(vr + 3 * H + 64, ag2, H, g, j);
+  put_rows_c(vr + 4 * H + 64, ab2, H, g, j);
   __syncthreads();
-  for (int k = 0; k < kTfWaves; ++k) {
-    if (wv == k) {
-      add_bias<NT>(slab + L::S_B2, b2s, H, g, j);
-      add_bias<4>(slab + L::S_B1, b1s, 64, g, j);
-      add_rows_c(slab + L::S_G1, ag1, H, g, j);
-      add_rows_c(slab + L::S_BT1, ab1, H, g, j);
-      add_rows_c(slab + L::S_G2, ag2, H, g, j);
-      add_rows_c(slab + L::S_BT2, ab2, H, g, j);
-    }
-    __syncthreads();
-  }
-  slab_out(slab, a.part + (long)blockIdx.x * L::SLAB, L::SLAB);
+  sum_regions(slab + L::S_B2, sm, L::NV, H);
+  sum_regions(slab + L::S_B1, sm + H, L::NV, 64);
+  sum_regions(slab + L::S_G1, sm + H + 64, L::NV, 4 * H);  // g1 bt1 g2 bt2 are contiguous in the slab too
+  TF_ST(13);
+  TF_ST_END(2);
 }
 
 // ============================================================================
@@ -797,7 +1004,7 @@ __global__ __launch_bounds__(kTfWaves * 64, 1) void tf_bwd_att_kernel(TfArgs a) 
   using L = BatL<H>;
   using Q = TfPar<H>;
   constexpr int NT = F::NT;
-  static_assert(L::SLAB <= L::SCR, "slab fits the LDS it reuses");
+  static_assert(kTfWaves * L::SLAB <= L::SCR, "epilogue partials fit the LDS they reuse");
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, g = lane >> 4, j = lane & 15;
   const int layer = a.layer;
@@ -805,8 +1012,10 @@ __global__ __launch_bounds__(kTfWaves * 64, 1) void tf_bwd_att_kernel(TfArgs a) 
   dma_groups(fr + F::OFF_IN, sm + L::W_IN, F::G_IN, wv, kTfWaves, lane);
   dma_groups(fr + F::OFF_INT, sm + L::W_INT, F::G_INT + F::G_OT, wv, kTfWaves, lane);
   load_params<H>(sm + L::PAR, a.P, layer);
+  TF_ST_INIT();
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  TF_ST(0);
   const float* par = sm + L::PAR;
   float* sa = sm + L::SCR + wv * (L::SCR_A + L::SCR_B);
   float* sb = sa + L::SCR_A;
@@ -819,27 +1028,32 @@ __global__ __launch_bounds__(kTfWaves * 64, 1) void tf_bwd_att_kernel(TfArgs a) 
     for (int U = 0; U < NT; ++U) dWo[t][U] = zero4();
   }
   const float scale = 1.0f / sqrtf((float)F::HD);
-  const long npairs = (long)a.B * H, nu = (npairs + 15) / 16;
+  const long npairs = (long)a.B * H, nu = (npairs + 15) / 16, spare = 3 * npairs;
   long u0, u1;
   unit_range(nu, u0, u1);
+  // the layer input X is loaded one unit ahead (see tf_fwd_kernel), dR1 after
+  // the q|k|v GEMM (its latency under the attention)
+  f32x4 Xn[NT][3];
+  {
+    long rn[3];
+    const bool okn = unit_rows<H>(u0, u1, npairs, j, rn);
+    load_tiles<NT>(Xn, a.x, F::DP, rn, okn, g);
+  }
 #pragma unroll 1
   for (long u = u0; u < u1; ++u) {
-    const long p = u * 16 + j;
-    const bool ok = p < npairs;
     long row[3];
-#pragma unroll
-    for (int w = 0; w < 3; ++w) row[w] = ok ? tf_row<H>(p, w) : 0;
+    const bool ok = unit_rows<H>(u, u1, npairs, j, row);
     f32x4 QKV[F::NQ][3];
-    {
-      f32x4 X[NT][3];
-      load_tiles<NT>(X, a.x, F::DP, row, ok, g);
-      init_bias<F::NQ>(QKV, par + Q::BIN, g);
-      tf_gemm<F::NQ, F::KS>(QKV, sm + L::W_IN, [&](int s, int w) { return X[s >> 2][w][s & 3]; }, lane);
-    }
-    float Pr[2][3][3];
     f32x4 O[NT][3], dR1[NT][3];
+    TF_ST(1);
+    init_bias<F::NQ>(QKV, par + Q::BIN, g);
+    tf_gemm<F::NQ, F::KS>(QKV, sm + L::W_IN, [&](int s, int w) { return Xn[s >> 2][w][s & 3]; }, lane);
+    TF_ST(2);
+    float Pr[2][3][3];
     tf_attn_fwd<H>(QKV, Pr, O, g);
+    TF_ST(3);
     load_tiles<NT>(dR1, a.in, F::DP, row, ok, g);
+    TF_ST(4);
     // dWo += dR1 (x) attention output, dbo += sum dR1
 #pragma unroll
     for (int w = 0; w < 3; ++w) {
@@ -847,12 +1061,14 @@ __global__ __launch_bounds__(kTfWaves * 64, 1) void tf_bwd_att_kernel(TfArgs a) 
       stage<NT>(O, w, sb, g, j);
       dw_step<NT, NT>(dWo, bos, sa, sb, g, j);
     }
+    TF_ST(5);
     // dO = Wo^T dR1
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
       for (int w = 0; w < 3; ++w) O[t][w] = zero4();
     tf_gemm<NT, F::KS>(O, sm + L::W_OT, [&](int s, int w) { return dR1[s >> 2][w][s & 3]; }, lane);
+    TF_ST(6);
     // attention backward (pgp_tune.hip attn_bwd_kernel, per lane)
     float dS[2][3][3];
 #pragma unroll
@@ -915,47 +1131,43 @@ __global__ __launch_bounds__(kTfWaves * 64, 1) void tf_bwd_att_kernel(TfArgs a) 
           QKV[2 * NT + t][w][r] = dv[w];
         }
       }
-    // dQKV rows to HBM ([M][Q3P], q | k | v natural) for in_proj's weight gradient
-    if (ok) {
+    TF_ST(7);
+    TF_ST(8);
+    // dX = Win^T dQKV + dR1 (the residual); the dQKV rows go to HBM ([M + 1][3][DP]:
+    // q | k | v, each zero-padded) for in_proj's weight gradient, one tile per
+    // fragment group
+    // and the next unit's input X is loaded
+    long rn[3];
+    const bool okn = unit_rows<H>(u + 1, u1, npairs, j, rn);
+    constexpr int NS = 3 * F::NQ, NL = 3 * NT, NG = F::NT * F::KGQ, PER = (NS + NL + NG - 1) / NG;
+    long srow[3];
 #pragma unroll
-      for (int part = 0; part < 3; ++part)
-#pragma unroll
-        for (int t = 0; t < NT; ++t) {
-          const int c0 = 16 * t + 4 * g;
-#pragma unroll
-          for (int w = 0; w < 3; ++w) {
-            float* dst = a.dqkv + row[w] * F::Q3P + part * H + c0;
-            const f32x4 v = QKV[part * NT + t][w];
-            if (c0 + 3 < H) {
-              *reinterpret_cast<f32x2*>(dst) = f32x2{v[0], v[1]};
-              *reinterpret_cast<f32x2*>(dst + 2) = f32x2{v[2], v[3]};
-            } else {
-#pragma unroll
-              for (int r = 0; r < 4; ++r)
-                if (c0 + r < H) dst[r] = v[r];
-            }
-          }
-        }
-    }
-    // dX = Win^T dQKV + dR1 (the residual)
-    tf_gemm<NT, F::KSQ>(dR1, sm + L::W_INT, [&](int s, int w) {
+    for (int w = 0; w < 3; ++w) srow[w] = (ok ? row[w] : spare) * (3 * F::DP) + 4 * g;
+    tf_gemm_side<NT, F::KSQ>(dR1, sm + L::W_INT, [&](int s, int w) {
       const int part = s / F::KS, sl = s - part * F::KS;
       return QKV[part * NT + (sl >> 2)][w][sl & 3];
-    }, lane);
-    store_tiles<NT>(dR1, a.out, F::DP, row, ok, g);
+    }, lane, [&](int i) {
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        const int c = i * PER + k;
+        if (c < NS)
+          st4(a.dqkv + srow[c % 3] + 16 * (c / 3), QKV[c / 3][c % 3]);
+        else if (c < NS + NL)
+          load_tile<NT>(Xn, a.x, F::DP, rn, okn, g, c - NS);
+      }
+    });
+    store_tiles<NT>(dR1, a.out, F::DP, row, ok, spare, g);
+    TF_ST(9);
   }
+  TF_ST(10);
+  __syncthreads();  // every wave is past its units: the weight area is free
+  float* reg = sm + wv * L::SLAB;
+  put_dw<NT, NT>(reg + L::S_WO, dWo, H, H, H, g, j);
+  put_bias<NT>(reg + L::S_BO, bos, H, g, j);
   __syncthreads();
-  float* slab = sm;
-  slab_zero(slab, L::SLAB);
-  __syncthreads();
-  for (int k = 0; k < kTfWaves; ++k) {
-    if (wv == k) {
-      add_dw<NT, NT>(slab + L::S_WO, dWo, H, H, H, g, j);
-      add_bias<NT>(slab + L::S_BO, bos, H, g, j);
-    }
-    __syncthreads();
-  }
-  slab_out(slab, a.part + (long)blockIdx.x * L::SLAB, L::SLAB);
+  sum_regions(a.part + (long)blockIdx.x * L::SLAB, sm, L::SLAB, L::SLAB);
+  TF_ST(11);
+  TF_ST_END(3);
 }
 
 template <int H>
@@ -1016,6 +1228,18 @@ long tf_slab_floats(int H, int kind) {
 }
 
 int tf_grid() { return device_cus(); }
+
+#ifdef PGP_TF_STAMPS
+// profiling builds: copy out (host != null) or clear (host == null) the phase stamps
+extern "C" int pgp_debug_tf_stamps(unsigned long long* host) {
+  if (!host) {
+    static unsigned long long zero[4][kStWaves][kStPhases];
+    return hipMemcpyToSymbol(HIP_SYMBOL(tf_stamps), zero, sizeof(zero)) == hipSuccess ? 0 : -3;
+  }
+  if (hipDeviceSynchronize() != hipSuccess) return -3;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(tf_stamps), sizeof(tf_stamps)) == hipSuccess ? 0 : -3;
+}
+#endif
 
 hipError_t launch_tf(int H, int kind, const TfArgs& a, hipStream_t st) {
   const int grid = tf_grid();

@@ -54,7 +54,8 @@ struct TF {
   }
 };
 
-// arguments of the fused kernels (unused pointers may be null)
+// arguments of the fused kernels (unused pointers may be null); every [M][*]
+// buffer a fused kernel writes has a spare row M (lanes outside the batch)
 struct TfArgs {
   int layer, B;
   const float* P;      // master weights (natural blob)
@@ -65,7 +66,7 @@ struct TfArgs {
   const float* x;      // att bwd: the layer input X                                             [M][DP]
   float* xh1;          // norm1 x-hat [M][DP] (fwd writes, ffn bwd reads)
   float* rs1;          // norm1 rstd [M]
-  float* dqkv;         // att bwd: dQKV [M][Q3P] (q | k | v natural)
+  float* dqkv;         // att bwd: dQKV [M][3][DP] (q | k | v, each zero-padded)
   float* part;         // bwd: one weight-gradient slab per workgroup
 };
 

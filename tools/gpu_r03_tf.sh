@@ -6,8 +6,12 @@ OUT=gpurun_out/r03_tf${1:-}
 mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread -p no:cacheprovider \
-  tests/test_gpu_decide.py tests/test_gpu_train.py tests/test_gpu_tunedp.py tests/test_gpu_dist.py > $OUT/tests.log 2>&1
+  tests/test_gpu_train.py tests/test_gpu_tunedp.py tests/test_gpu_dist.py > $OUT/tests.log 2>&1
 rc=$?; grep -E "PASS|FAIL|Error|error" $OUT/tests.log | tail -60; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 120 python3 -u bench.py --config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline > $OUT/tune50.json 2> $OUT/tune50.err; rc=$?; cat $OUT/tune50.json; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 180 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 bench.py --config tune --hosts 50 --steps 20 --warmup 3 --no-cpu-baseline > $OUT/prof.log 2>&1; rc=$?; [ $rc -eq 0 ] || exit $rc
+
+if [ -f preganplus_amd/_lib/var/libpreganplus_st.so ]; then
+  PGP_LIB=preganplus_amd/_lib/var/libpreganplus_st.so timeout -k 10 120 python3 -u tools/tf_stamps.py 50 1030 > $OUT/stamps.txt 2>&1; rc=$?; [ $rc -eq 0 ] || exit $rc
+fi
 echo done
