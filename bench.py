@@ -13,6 +13,7 @@ stream the kernels run on.  cpu_baseline times the numpy oracle (a CPU port of
 the reference math) on a bounded sample, rank 0 at N=1 only.
 """
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -24,7 +25,10 @@ import torch
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+from preganplus_amd import _native  # noqa: E402
 from preganplus_amd import roofline as R  # noqa: E402
+
+R_ROOF = R
 from preganplus_amd import weights as W  # noqa: E402
 from preganplus_amd.model import DecisionModel, embedding, migrations  # noqa: E402
 
@@ -434,6 +438,38 @@ def bench_tune(args):
     el = _timed(world, device, lambda: step(*next(it)), args.steps)
     stage = np.array([[e[k].elapsed_time(e[k + 1]) for k in range(len(names))] for e in ev[:args.steps]]).mean(0)
     sub = np.array([[e[k].elapsed_time(e[k + 1]) for k in range(len(subs))] for e in sev[:args.steps]]).mean(0)
+    # roofline of the dominant kernels: the six fused encoder launches of the
+    # tuning forward + backward, timed live with HIP events recorded on their
+    # stream inside the library (pgp_tune_timing) over extra steps after the
+    # timed region; achieved = their executed MFMA flops (ISA-counted per unit,
+    # roofline.TUNE_MFMA_PER_UNIT) / the mean launch duration
+    RL = R_ROOF  # (R is the window count here)
+    L = _native.lib()
+    L.pgp_tune_timing.argtypes = [ctypes.c_int]
+    L.pgp_tune_fused_ms.argtypes = [ctypes.c_void_p]
+    _native.check(L.pgp_tune_timing(1), "pgp_tune_timing")
+    fused = []
+    ms6 = (ctypes.c_float * 6)()
+    for _ in range(max(3, min(args.steps, 10))):
+        step()
+        _native.check(L.pgp_tune_fused_ms(ms6), "pgp_tune_fused_ms")
+        fused.append(list(ms6))
+    _native.check(L.pgp_tune_timing(0), "pgp_tune_timing")
+    fused_ms = np.array(fused).mean(0)
+    flops = RL.tune_fused_flops(H, B)
+    roof = None
+    if flops is not None:
+        rates = [f / (t * 1e-3) / 1e12 for f, t in zip(flops, fused_ms)]
+        k = int(np.argmax(fused_ms))
+        roof = {"kernel": f"tf_*_kernel<{H}> ({RL.TUNE_FUSED_LAUNCHES[k]}, the longest fused launch)",
+                "bound": "mfma", "achieved": rates[k], "peak": RL.PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+                "frac": rates[k] / RL.PEAK_FP32_TFLOPS, "traffic": None,
+                "basis": "executed v_mfma_f32_16x16x4_f32 flops of the batch's units (ISA count per unit) / mean "
+                         "launch duration (HIP events on the launch stream)",
+                "fused_launches": {n: {"ms": float(t), "tflops": float(r), "frac": float(r / RL.PEAK_FP32_TFLOPS)}
+                                   for n, t, r in zip(RL.TUNE_FUSED_LAUNCHES, fused_ms, rates)},
+                "fused_total": {"ms": float(fused_ms.sum()),
+                                "frac": float(sum(flops) / (fused_ms.sum() * 1e-3) / 1e12 / RL.PEAK_FP32_TFLOPS)}}
     if rank == 0:
         res = {
             "metric": "tuning windows/sec (semi-supervised step: dataset + detect + train_gan + DP tune_model)",
@@ -449,6 +485,7 @@ def bench_tune(args):
             "stage_ms": {n: float(stage[k]) for k, n in enumerate(names)},
             "tune_model_ms": {n: float(sub[k]) for k, n in enumerate(subs)},
             "grad_all_reduce_ms": float(sub[subs.index("all_reduce")]),
+            "roofline": roof,
         }
         if world == 1 and not args.no_cpu_baseline:
             log("timing CPU baseline ...")

@@ -225,6 +225,14 @@ int pgp_tune_forward(int n_hosts, int batch, const float* windows, const float* 
  * into G (the caller zeroes G before the step). */
 int pgp_tune_backward(int n_hosts, int batch, const float* P, float* G, float* workspace, const float* logits,
                       const float* protos, const int* y, const float* mult, const float* tgt, void* stream);
+/* Profiling: with pgp_tune_timing(1), pgp_tune_forward / pgp_tune_backward
+ * record HIP events on their stream around each fused encoder launch
+ * (pgp_tunef.hip); pgp_tune_fused_ms(ms6) synchronises on them and returns the
+ * last forward + backward's six durations [fwd layer 0, fwd layer 1, ffn
+ * backward layer 1, attention backward layer 1, ffn backward layer 0,
+ * attention backward layer 0] in ms.  Off by default (not graph-capturable). */
+int pgp_tune_timing(int on);
+int pgp_tune_fused_ms(float* ms6);
 /* custom_loss / triplet_loss bookkeeping of ONE window (train.py:13-40,
  * replaces the host loop between `model(...)` and `loss.backward()` in
  * backprop, train.py:47-53), on the stream: reads the batch-1 forward's logits

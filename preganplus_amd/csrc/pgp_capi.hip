@@ -358,6 +358,19 @@ int pgp_tune_backward(int n_hosts, int batch, const float* P, float* G, float* w
   return PGP_OK;
 }
 
+int pgp_tune_timing(int on) {
+  HIPCHK(tune_timing(on != 0));
+  return PGP_OK;
+}
+
+int pgp_tune_fused_ms(float* ms6) {
+  if (!ms6) return fail(PGP_ERR_ARG, "NULL output");
+  const hipError_t e = tune_fused_ms(ms6);
+  if (e == hipErrorInvalidValue) return fail(PGP_ERR_STATE, "pgp_tune_timing(1) was never called");
+  HIPCHK(e);
+  return PGP_OK;
+}
+
 int pgp_tune_targets(int n_hosts, int n_protos, const float* logits, const float* protos, const int* y, const int* cls,
                      double* state, double update_min, double decay, float* mult, float* tgt, double* loss,
                      void* stream) {

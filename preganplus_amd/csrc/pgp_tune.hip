@@ -865,6 +865,17 @@ bool plan_h(int B, TunePlan* out) {
   return true;
 }
 
+// Live timing of the fused encoder launches (pgp_tune_timing): events around
+// each of the six per step, [fwd l0, fwd l1, ffn l1, att l1, ffn l0, att l0]
+struct TfTiming {
+  bool on = false, made = false;
+  hipEvent_t ev[12];
+  void mark(int k, hipStream_t st) {
+    if (on) (void)hipEventRecord(ev[k], st);
+  }
+};
+TfTiming g_tft;
+
 template <int H>
 hipError_t tune_fwd_h(const TunePlan& p, const float* win, const float* P, float* ws, float* latent, float* logits,
                       float* protos, hipStream_t st) {
@@ -886,7 +897,9 @@ hipError_t tune_fwd_h(const TunePlan& p, const float* win, const float* P, float
     t.x0 = ws + p.x[0];
     t.xh1 = ws + p.xh1[l];
     t.rs1 = ws + p.rs1[l];
+    g_tft.mark(2 * l, st);
     if ((e = launch_tf(H, 1, t, st)) != hipSuccess) return e;
+    g_tft.mark(2 * l + 1, st);
   }
   if ((e = launch_dec_fwd(H, B, p.dec_s, ws + p.x[2], ws + p.wp, ws + p.part, st)) != hipSuccess) return e;
   TCK((dec_fin_kernel<H><<<(int)(((long)B * 4 * H + 255) / 256), 256, 0, st>>>(B, p.dec_s, ws + p.part, P, logits,
@@ -931,7 +944,10 @@ hipError_t tune_bwd_h(const TunePlan& p, const float* P, float* Gd, float* ws, c
     t.xh1 = ws + p.xh1[l];
     t.rs1 = ws + p.rs1[l];
     t.part = ws + p.tfs[l][0];
+    const int tk = 4 + 4 * (1 - l);
+    g_tft.mark(tk, st);
     if ((e = launch_tf(H, 2, t, st)) != hipSuccess) return e;
+    g_tft.mark(tk + 1, st);
     {
       const long sl = tf_slab_floats(H, 2);
       const float* s0 = ws + p.tfs[l][0];
@@ -949,7 +965,9 @@ hipError_t tune_bwd_h(const TunePlan& p, const float* P, float* Gd, float* ws, c
     t.x = ws + p.x[l];
     t.dqkv = ws + p.dq;
     t.part = ws + p.tfs[l][1];
+    g_tft.mark(tk + 2, st);
     if ((e = launch_tf(H, 3, t, st)) != hipSuccess) return e;
+    g_tft.mark(tk + 3, st);
     if (!rb.add(ng, tf_slab_floats(H, 3), ws + p.tfs[l][1], H, H, H, Lg + G::L_OUT, H, H, (long)H * H,
                 Lg + G::L_OUTB))
       return hipErrorInvalidValue;
@@ -982,6 +1000,30 @@ hipError_t tune_bwd_h(const TunePlan& p, const float* P, float* Gd, float* ws, c
 }
 
 }  // namespace
+
+hipError_t tune_timing(bool on) {
+  if (on && !g_tft.made) {
+    for (auto& e : g_tft.ev)
+      if (hipEventCreate(&e) != hipSuccess) return hipErrorOutOfMemory;
+    g_tft.made = true;
+  }
+  g_tft.on = on;
+  return hipSuccess;
+}
+
+hipError_t tune_fused_ms(float* out) {
+  if (!g_tft.made) return hipErrorInvalidValue;
+  // every event: a forward records its pair twice per C3 step (detect, then tuning)
+  for (auto& ev : g_tft.ev) {
+    const hipError_t w = hipEventSynchronize(ev);
+    if (w != hipSuccess) return w;
+  }
+  for (int k = 0; k < 6; ++k) {
+    const hipError_t e = hipEventElapsedTime(&out[k], g_tft.ev[2 * k], g_tft.ev[2 * k + 1]);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
 
 bool tune_plan(int H, int B, TunePlan* p) {
   if (B < 1) return false;

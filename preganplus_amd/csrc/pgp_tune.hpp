@@ -45,6 +45,10 @@ struct TunePlan {
 };
 
 bool tune_plan(int H, int B, TunePlan* p);
+// live timing of the six fused encoder launches of a forward + backward
+// (pgp_tune_timing / pgp_tune_fused_ms)
+hipError_t tune_timing(bool on);
+hipError_t tune_fused_ms(float* out6);
 
 // decoder GEMMs (pgp_dec.hip): split-K forward into part[S][B][NOP] and the
 // backward into the encoder output's gradient [M][DP]

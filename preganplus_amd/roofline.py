@@ -61,6 +61,39 @@ def encoder_executed_flops_per_window(H: int):
     return None if n is None else n * 2048 * H / 16
 
 
+# Fused tuning encoder (pgp_tunef.hip): v_mfma_f32_16x16x4_f32 per unit of 16
+# (window, host) pairs, the static counts of the built ISA (tools/isa_count.py
+# tune_counts, held equal by tests/test_roofline_isa.py).  tf_fwd_kernel's count
+# includes layer 0's time encoder (tune_te_mfma), which layer 1 skips.
+TUNE_MFMA_PER_UNIT = {
+    16: {"tf_fwd_kernel": 156, "tf_bwd_ffn_kernel": 288, "tf_bwd_att_kernel": 96},
+    50: {"tf_fwd_kernel": 1200, "tf_bwd_ffn_kernel": 1104, "tf_bwd_att_kernel": 1368},
+}
+TUNE_FUSED_LAUNCHES = ("fwd layer 0", "fwd layer 1", "ffn bwd layer 1", "att bwd layer 1", "ffn bwd layer 0",
+                       "att bwd layer 0")
+
+
+def tune_te_mfma(H: int) -> int:
+    """Time-encoder MFMAs per unit: NT output tiles x KS k-steps x 3 window steps."""
+    nt = (H + 15) // 16
+    ks = 4 * (H // 16) + (min(H % 16, 4) if H % 16 else 0)
+    return nt * ks * 3
+
+
+def tune_fused_flops(H: int, B: int):
+    """Executed MFMA flops of each of the six fused launches of one tuning
+    forward + backward (TUNE_FUSED_LAUNCHES order) over the batch's units; the
+    FFN backward's zero rounds of waves past their units are not counted."""
+    c = TUNE_MFMA_PER_UNIT.get(H)
+    if c is None:
+        return None
+    units = (B * H + 15) // 16
+    fwd, te = c["tf_fwd_kernel"], tune_te_mfma(H)
+    per = [fwd, fwd - te, c["tf_bwd_ffn_kernel"], c["tf_bwd_att_kernel"], c["tf_bwd_ffn_kernel"],
+           c["tf_bwd_att_kernel"]]
+    return [units * n * 2048 for n in per]
+
+
 def encoder_io_bytes_per_window(H: int) -> int:
     """K2's own compulsory HBM I/O: the GAT output it reads (W x H x 3 aggregated
     raw features, fp32) and the latent it writes (3H^2 fp32) for K2b."""

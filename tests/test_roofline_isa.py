@@ -26,6 +26,23 @@ def test_encoder_mfma_count_matches_built_library():
         assert counts[H][0] == n, f"H={H}: built library issues {counts[H][0]} MFMAs per host, roofline says {n}"
 
 
+@pytest.mark.skipif(not os.path.exists(LIB) or not os.path.exists("/opt/rocm/lib/llvm/bin/llvm-objdump"),
+                    reason="built library / llvm-objdump absent")
+def test_tuning_kernel_mfma_counts_match_built_library():
+    import isa_count
+    counts = isa_count.tune_counts(tuple(R.TUNE_MFMA_PER_UNIT))
+    assert counts == R.TUNE_MFMA_PER_UNIT
+
+
+def test_tune_fused_flops_bookkeeping():
+    # layer 1's forward = the forward kernel's count minus layer 0's time encoder
+    f = R.tune_fused_flops(50, 1030)
+    units = (1030 * 50 + 15) // 16
+    assert f[0] - f[1] == units * R.tune_te_mfma(50) * 2048 == units * 4 * 14 * 3 * 2048
+    assert f[2] == f[4] and f[3] == f[5]
+    assert R.tune_te_mfma(16) == 1 * 4 * 3
+
+
 def test_executed_rate_cannot_exceed_peak_definition():
     # executed flops per window are what K2 issues; the reference formulation's
     # count is reported separately as an algorithmic rate

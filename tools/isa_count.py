@@ -4,7 +4,8 @@ preganplus_amd/_lib/libpreganplus.so (llvm-objdump --offloading, in a scratch
 directory) and disassembled.  The host loop is `#pragma unroll 1` and holds all
 of the kernel's MFMAs, so the kernel-wide v_mfma count is the per-host count.
 These counts are preganplus_amd/roofline.py ENC_MFMA_PER_HOST (bench.py's
-executed-work `frac`); tests/test_roofline_isa.py holds the two equal.
+executed-work `frac`); tests/test_roofline_isa.py holds the two equal.  The same
+holds for the fused tuning-encoder kernels' per-unit counts (TUNE_MFMA_PER_UNIT).
 usage: python tools/isa_count.py [H ...]"""
 import glob
 import os
@@ -19,8 +20,8 @@ LIB = os.path.join(ROOT, "preganplus_amd", "_lib", "libpreganplus.so")
 OBJDUMP = "/opt/rocm/lib/llvm/bin/llvm-objdump"
 
 
-def encoder_counts(Hs=(16, 50), lib=LIB):
-    """{H: (mfma, other_valu)} for encoder_kernel<H> in the built library."""
+def _disasm(lib, needle):
+    """Disassembly of the library's gfx950 code objects that mention `needle`."""
     with tempfile.TemporaryDirectory() as td:
         shutil.copy(lib, os.path.join(td, "lib.so"))
         subprocess.run([OBJDUMP, "--offloading", "lib.so"], cwd=td, check=True, capture_output=True)
@@ -28,8 +29,31 @@ def encoder_counts(Hs=(16, 50), lib=LIB):
         for co in sorted(glob.glob(os.path.join(td, "lib.so.*gfx950"))):
             d = subprocess.run([OBJDUMP, "-d", "--mcpu=gfx950", co], check=True, capture_output=True,
                                text=True).stdout
-            if "encoder_kernel" in d:
+            if needle in d:
                 asm += d
+    return asm
+
+
+def tune_counts(Hs=(16, 50), lib=LIB):
+    """{H: {kernel: mfma}} for the fused tuning-encoder kernels (pgp_tunef.hip):
+    the unit loop is `#pragma unroll 1` and holds every MFMA, so the static
+    count is the per-unit count (tf_fwd_kernel's includes layer 0's time
+    encoder, which layer 1 skips)."""
+    asm = _disasm(lib, "tf_fwd_kernel")
+    out = {}
+    for H in Hs:
+        out[H] = {}
+        for name in ("tf_fwd_kernel", "tf_bwd_ffn_kernel", "tf_bwd_att_kernel"):
+            m = re.search(rf"<_ZN3pgp12_GLOBAL__N_1\d+{name}ILi{H}EEEvNS_6TfArgsE>:\n(.*?)s_endpgm", asm, re.S)
+            if m is None:
+                raise RuntimeError(f"{name}<{H}> not found in {lib}")
+            out[H][name] = len(re.findall(r"^\s+v_mfma", m.group(1), re.M))
+    return out
+
+
+def encoder_counts(Hs=(16, 50), lib=LIB):
+    """{H: (mfma, other_valu)} for encoder_kernel<H> in the built library."""
+    asm = _disasm(lib, "encoder_kernel")
     out = {}
     for H in Hs:
         m = re.search(rf"<_ZN3pgp12_GLOBAL__N_114encoder_kernelILi{H}EEEvNS_7FwdArgsE>:\n(.*?)s_endpgm", asm, re.S)
@@ -46,3 +70,5 @@ if __name__ == "__main__":
     Hs = [int(h) for h in sys.argv[1:]] or [16, 50]
     for H, (mfma, valu) in encoder_counts(Hs).items():
         print(f"H={H}: {mfma} MFMA (16x16x4 f32), {valu} other VALU per host and wave")
+    for H, d in tune_counts(Hs).items():
+        print(f"H={H}: fused tuning kernels, MFMA per unit: {d}")
