@@ -63,6 +63,10 @@ struct GanGeo {
   static constexpr int mx(int x, int y) { return x > y ? x : y; }
   static constexpr int SLOT_G = mx(G::GE_G, mx(kQC * G::GS_G, CPC * G::GC_G));
   static constexpr int SLOT = SLOT_G * G::FQ;
+  // per-wave container targets (gen | final) as int16 [2][C][16 windows],
+  // flushed row-contiguous at the end (no scattered 4-byte stores in the loop)
+  static constexpr int TGT = 2 * G::C * 16;          // int16 per wave
+  static constexpr int LDS_BYTES = 2 * SLOT * 4 + kGanWaves * TGT * 2;
   // chunk k -> (global source, groups)
   PGP_DEV static void chunk(int k, const float* frags, const float** src, int* ng) {
     if (k == 0) {
@@ -83,7 +87,7 @@ template <int H>
 __global__ __launch_bounds__(kGanWaves * 64) void gan_kernel(FwdArgs a) {
   using G = Geo<H>;
   using GG = GanGeo<H>;
-  __shared__ __attribute__((aligned(16))) float smem[2 * GG::SLOT];
+  extern __shared__ __attribute__((aligned(16))) float smem[];  // ring [2][SLOT] | targets
   const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const long blk = (long)blockIdx.x * kGanWaves + wv;
@@ -93,6 +97,7 @@ __global__ __launch_bounds__(kGanWaves * 64) void gan_kernel(FwdArgs a) {
   const float* sw = a.sched + (valid ? b : 0) * G::H2;
   const float* ew = a.emb + (valid ? b : 0) * G::EP;
   const float* gt = a.gtab;
+  short* tg = reinterpret_cast<short*>(smem + 2 * GG::SLOT) + wv * GG::TGT;  // this wave's targets
 
   float* cur = smem;
   float* nxt = smem + GG::SLOT;
@@ -299,9 +304,9 @@ __global__ __launch_bounds__(kGanWaves * 64) void gan_kernel(FwdArgs a) {
         bs_i = osi;
       }
     }
-    if (valid && g == 0) {
-      a.gen_t[b * G::C + c] = bn_i;
-      a.final_t[b * G::C + c] = bs_i;
+    if (g == 0) {
+      tg[c * 16 + j] = (short)bn_i;
+      tg[(G::C + c) * 16 + j] = (short)bs_i;
     }
   };
   auto copy_row = [&](float (&d)[G::MT_N][4], const float (&sr)[G::MT_N][4]) {
@@ -325,6 +330,32 @@ __global__ __launch_bounds__(kGanWaves * 64) void gan_kernel(FwdArgs a) {
     finish(c, cw, ns, racc, sv);
     if ((c + 1) % GG::CPC == 0) advance();
     copy_row(sv, svn);
+  }
+
+  // the wave's targets: its windows' rows are contiguous in gen_t / final_t
+  // ([B][C]), written 4 ints per lane (the wave's own LDS region: no barrier)
+  {
+    const long base = blk * 16 * G::C;
+    const long n = (a.B - blk * 16 < 16 ? a.B - blk * 16 : 16) * (long)G::C;  // valid elements
+    for (int k = 4 * lane; k < 16 * G::C; k += 256) {
+#pragma unroll
+      for (int arr = 0; arr < 2; ++arr) {
+        int v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int idx = k + e, w = idx / G::C, c = idx - w * G::C;
+          v[e] = tg[(arr * G::C + c) * 16 + w];
+        }
+        int* dst = (arr ? a.final_t : a.gen_t) + base + k;
+        if (blk < nblk && k + 3 < n) {
+          *reinterpret_cast<int4*>(dst) = make_int4(v[0], v[1], v[2], v[3]);
+        } else if (blk < nblk) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (k + e < n) dst[e] = v[e];
+        }
+      }
+    }
   }
 
   // ---- Disc2 + softmax + gate (PreGANPlus.py:87) ----
@@ -353,9 +384,18 @@ __global__ __launch_bounds__(kGanWaves * 64) void gan_kernel(FwdArgs a) {
 
 template <int H>
 hipError_t launch(const FwdArgs& a, hipStream_t st) {
+  using GG = GanGeo<H>;
+  static_assert(GG::LDS_BYTES <= 160 * 1024, "K3 LDS");
+  static_assert(Geo<H>::C < 32768, "int16 targets");
+  static bool attr = [] {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gan_kernel<H>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, GG::LDS_BYTES);
+    return true;
+  }();
+  (void)attr;
   const long nblk = (a.B + 15) / 16;
   const int grid = (int)((nblk + kGanWaves - 1) / kGanWaves);
-  gan_kernel<H><<<grid, kGanWaves * 64, 0, st>>>(a);
+  gan_kernel<H><<<grid, kGanWaves * 64, GG::LDS_BYTES, st>>>(a);
   return hipGetLastError();
 }
 
