@@ -12,6 +12,8 @@
 //                                      hd += Wd1[:, H^2 + cH : H^2 + (c+1)H] . ns_c  (Disc1, new-schedule half)
 // so the new schedule never leaves registers.  Then Disc2 + softmax + gate.
 // LeakyReLU(True) in Gen/Disc has slope 1.0 (identity), so no activation is applied.
+#include <type_traits>
+
 #include "pgp_device.hpp"
 
 namespace pgp {
@@ -21,7 +23,15 @@ namespace {
 #define PGP_GAN_WAVES 16
 #endif
 constexpr int kGanWaves = PGP_GAN_WAVES;  // waves per workgroup (16 windows each)
-constexpr int kQC = 4;  // schedule k-blocks (16 columns each) per chunk
+// schedule k-blocks (16 columns each) per ring chunk, and the chunk size cap
+// (1-KiB groups) that sets the containers per phase-3 chunk: one barrier per chunk
+#ifndef PGP_GAN_QC
+#define PGP_GAN_QC 8
+#endif
+#ifndef PGP_GAN_CHUNK_G
+#define PGP_GAN_CHUNK_G 64
+#endif
+constexpr int kQC = PGP_GAN_QC;
 // per-container MFMA loops at wave priority 1, the tanh / argmax VALU at 0
 #ifndef PGP_GAN_PRIO
 #define PGP_GAN_PRIO 1
@@ -54,7 +64,7 @@ struct GanGeo {
   // container's chunk is 8 groups, 32 MFMAs per wave per barrier
   static constexpr int cpc() {
     int best = 1;
-    for (int c = 1; c * G::GC_G <= 32; ++c)
+    for (int c = 1; c * G::GC_G <= PGP_GAN_CHUNK_G; ++c)
       if (G::C % c == 0) best = c;
     return best;
   }
@@ -63,10 +73,12 @@ struct GanGeo {
   static constexpr int mx(int x, int y) { return x > y ? x : y; }
   static constexpr int SLOT_G = mx(G::GE_G, mx(kQC * G::GS_G, CPC * G::GC_G));
   static constexpr int SLOT = SLOT_G * G::FQ;
-  // per-wave container targets (gen | final) as int16 [2][C][16 windows],
-  // flushed row-contiguous at the end (no scattered 4-byte stores in the loop)
-  static constexpr int TGT = 2 * G::C * 16;          // int16 per wave
-  static constexpr int LDS_BYTES = 2 * SLOT * 4 + kGanWaves * TGT * 2;
+  // per-wave container targets (gen | final) as [2][C][16 windows] of int8
+  // (C < 128) or int16, flushed row-contiguous at the end (no scattered 4-byte
+  // stores in the loop)
+  using TgtT = typename std::conditional<(G::C < 128), signed char, short>::type;
+  static constexpr int TGT = 2 * G::C * 16;  // entries per wave
+  static constexpr int LDS_BYTES = 2 * SLOT * 4 + kGanWaves * TGT * (int)sizeof(TgtT);
   // chunk k -> (global source, groups)
   PGP_DEV static void chunk(int k, const float* frags, const float** src, int* ng) {
     if (k == 0) {
@@ -97,7 +109,8 @@ __global__ __launch_bounds__(kGanWaves * 64) void gan_kernel(FwdArgs a) {
   const float* sw = a.sched + (valid ? b : 0) * G::H2;
   const float* ew = a.emb + (valid ? b : 0) * G::EP;
   const float* gt = a.gtab;
-  short* tg = reinterpret_cast<short*>(smem + 2 * GG::SLOT) + wv * GG::TGT;  // this wave's targets
+  using TgtT = typename GG::TgtT;
+  TgtT* tg = reinterpret_cast<TgtT*>(smem + 2 * GG::SLOT) + wv * GG::TGT;  // this wave's targets
 
   float* cur = smem;
   float* nxt = smem + GG::SLOT;
@@ -305,8 +318,8 @@ __global__ __launch_bounds__(kGanWaves * 64) void gan_kernel(FwdArgs a) {
       }
     }
     if (g == 0) {
-      tg[c * 16 + j] = (short)bn_i;
-      tg[(G::C + c) * 16 + j] = (short)bs_i;
+      tg[c * 16 + j] = (TgtT)bn_i;
+      tg[(G::C + c) * 16 + j] = (TgtT)bs_i;
     }
   };
   auto copy_row = [&](float (&d)[G::MT_N][4], const float (&sr)[G::MT_N][4]) {
@@ -386,7 +399,7 @@ template <int H>
 hipError_t launch(const FwdArgs& a, hipStream_t st) {
   using GG = GanGeo<H>;
   static_assert(GG::LDS_BYTES <= 160 * 1024, "K3 LDS");
-  static_assert(Geo<H>::C < 32768, "int16 targets");
+  static_assert(Geo<H>::C < 32768, "int8 / int16 targets");
   static bool attr = [] {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gan_kernel<H>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, GG::LDS_BYTES);
