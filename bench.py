@@ -418,25 +418,40 @@ def bench_tune(args):
     subs = TR.DPTuner.SUBSTAGES
     ev = [[torch.cuda.Event(enable_timing=True) for _ in range(len(names) + 1)] for _ in range(max(args.steps, 1))]
     sev = [[torch.cuda.Event(enable_timing=True) for _ in range(len(subs) + 1)] for _ in range(max(args.steps, 1))]
+    # train_gan and tune_model share no data (run_model calls them back to
+    # back, PreGANPlus.py:133-134: the GAN step reads the embedding and writes
+    # the GAN's weights; the tuning step reads the dataset and writes the
+    # Transformer's), so the GAN step runs on a second stream beside the
+    # tuning step; the step ends when both have (results are unchanged:
+    # tests/test_gpu_dist.py and test_gpu_tunedp.py run them in either order)
+    main = torch.cuda.current_stream(device)
+    side = torch.cuda.Stream(device)
 
     def step(e=None, se=None):
-        rec = (lambda k: e[k].record()) if e is not None else (lambda k: None)
+        rec = (lambda k: e[k].record(main)) if e is not None else (lambda k: None)
         rec(0)
         wins, y, cls, inf = TR.tune_dataset(tr, series, tmax, out=bufs)
         rec(1)
         logits, protos = tr.tune_forward(inf)
         emb = embedding(logits, protos, out=emb_buf)   # PreGANPlus.py:129
         rec(2)
-        TR.train_gan_batched(tr, sim, envs, emb, s, out=sim_out, target=gan_target, all_reduce=True)
-        rec(3)
-        tun.step(wins, y, cls, mark=(lambda k: se[k].record()) if se is not None else None)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            TR.train_gan_batched(tr, sim, envs, emb, s, out=sim_out, target=gan_target, all_reduce=True)
+            if e is not None:
+                e[3].record(side)
+        tun.step(wins, y, cls, mark=(lambda k: se[k].record(main)) if se is not None else None)
+        main.wait_stream(side)
         rec(4)
 
     for _ in range(args.warmup):
         step()
     it = iter(zip(ev, sev))
     el = _timed(world, device, lambda: step(*next(it)), args.steps)
-    stage = np.array([[e[k].elapsed_time(e[k + 1]) for k in range(len(names))] for e in ev[:args.steps]]).mean(0)
+    # train_gan (side stream, from the embedding to its last kernel) and
+    # tune_model (main stream, its first sub-stage mark to its last) overlap
+    stage = np.array([[e[0].elapsed_time(e[1]), e[1].elapsed_time(e[2]), e[2].elapsed_time(e[3]),
+                       s_[0].elapsed_time(s_[len(subs)])] for e, s_ in zip(ev[:args.steps], sev[:args.steps])]).mean(0)
     sub = np.array([[e[k].elapsed_time(e[k + 1]) for k in range(len(subs))] for e in sev[:args.steps]]).mean(0)
     # roofline of the dominant kernels: the six fused encoder launches of the
     # tuning forward + backward, timed live with HIP events recorded on their
@@ -483,6 +498,7 @@ def bench_tune(args):
                                    f"= {B} tuning windows per GPU", "hosts": H, "environments_per_gpu": E,
                        "windows_per_gpu": B, "parallelism": f"dp{world} + RCCL all-reduce (grads, state)"},
             "stage_ms": {n: float(stage[k]) for k, n in enumerate(names)},
+            "streams": "train_gan on a second stream, concurrent with tune_model (no shared data)",
             "tune_model_ms": {n: float(sub[k]) for k, n in enumerate(subs)},
             "grad_all_reduce_ms": float(sub[subs.index("all_reduce")]),
             "roofline": roof,
@@ -791,6 +807,8 @@ def bench_loop(args):
     names = ("gobi", "encode_classify", "gan_step", "tune_step", "weight_sync", "gan_decide_moves")
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(len(names) + 1)]
     acc = np.zeros(len(names))
+    main = torch.cuda.current_stream(device)
+    side = torch.cuda.Stream(device)
 
     def interval(timed=False):
         if timed:
@@ -804,12 +822,17 @@ def bench_loop(args):
         emb = embedding(out["logits"], out["protos"], out=emb_buf)   # PreGANPlus.py:129
         if timed:
             ev[2].record()
-        TR.train_gan_batched(tr, sim, envs, emb, sched, out=sim_out, target=gan_target)
-        if timed:
-            ev[3].record()
+        # the GAN step on a second stream beside the tuning step (no shared
+        # data, see bench_tune); the repack reads both sections of the master
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            TR.train_gan_batched(tr, sim, envs, emb, sched, out=sim_out, target=gan_target)
+            if timed:
+                ev[3].record(side)
         tun.step(x, y, cls)
         if timed:
-            ev[4].record()
+            ev[4].record(main)
+        main.wait_stream(side)
         model.repack_master(tr.P, tun.state[:2 * K])
         if timed:
             ev[5].record()
@@ -826,7 +849,8 @@ def bench_loop(args):
         interval(True)
         torch.cuda.synchronize()
         for k in range(len(names)):
-            acc[k] += ev[k].elapsed_time(ev[k + 1])
+            # gan_step (side stream) and tune_step both start at ev[2]
+            acc[k] += ev[2 if k == 3 else k].elapsed_time(ev[k + 1])
 
     el = _timed(world, device, timed_interval, steps)
     if rank == 0:
@@ -839,7 +863,8 @@ def bench_loop(args):
                     "and tuning labels; shipped H=16 weights",
             "config": {"workload": f"online interval, {E} independent 16-host cells per GPU", "hosts": H,
                        "cells_per_gpu": E, "parallelism": f"dp{world}"},
-            "stage_ms": {n: float(acc[k] / steps) for k, n in enumerate(names)}}
+            "stage_ms": {n: float(acc[k] / steps) for k, n in enumerate(names)},
+            "streams": "gan_step on a second stream, concurrent with tune_step (no shared data)"}
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = loop_cpu_baseline(w, extra, inits_h, x.cpu().numpy(), envs_h,
                                                     y.cpu().numpy(), args.cpu_budget)
@@ -976,8 +1001,11 @@ def bench_plugin(args):
             return r
         return wrapper
 
-    for name in ("train_gan", "tune_model", "sync_inference_weights", "recover_decision"):
-        setattr(rec, name, timed(name, getattr(rec, name)))
+    # (this pass serialises the stages; run_model overlaps the tuning graph,
+    # launched by _tune_launch, with train_gan's host simulator call)
+    staged = ("train_gan", "_tune_launch", "_tune_finish", "sync_inference_weights", "recover_decision")
+    for name in staged:
+        setattr(rec, name, timed(name.lstrip("_"), getattr(rec, name)))
     rec._detect = timed("detect_forward", rec._detect)
     import preganplus_amd.train as TRm
     bp, ds = TRm.backprop, TRm.on_the_fly_dataset
@@ -987,7 +1015,7 @@ def bench_plugin(args):
             call(k)
     finally:
         TRm.backprop, TRm.on_the_fly_dataset = bp, ds
-        for name in ("train_gan", "tune_model", "sync_inference_weights", "recover_decision"):
+        for name in staged:
             delattr(rec, name)
         del rec._detect
     stage_ms = {k: float(np.median(v) * 1e3) for k, v in stages.items()}

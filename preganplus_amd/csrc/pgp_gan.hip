@@ -29,7 +29,7 @@ constexpr int kGanWaves = PGP_GAN_WAVES;  // waves per workgroup (16 windows eac
 #define PGP_GAN_QC 8
 #endif
 #ifndef PGP_GAN_CHUNK_G
-#define PGP_GAN_CHUNK_G 64
+#define PGP_GAN_CHUNK_G 65
 #endif
 constexpr int kQC = PGP_GAN_QC;
 // per-container MFMA loops at wave priority 1, the tanh / argmax VALU at 0
@@ -60,25 +60,31 @@ template <int H>
 struct GanGeo {
   using G = Geo<H>;
   static constexpr int NQC = cdiv(G::SQ, kQC);
-  // CPC containers per ring chunk (up to 32 groups; CPC divides C): at H = 16 a
-  // container's chunk is 8 groups, 32 MFMAs per wave per barrier
+  // CPC containers per ring chunk (CPC divides C), their weight groups plus one
+  // group holding their Gen2 biases (copied from the GAN table: the bias is the
+  // accumulator's initial value, so an LDS read instead of a global load that
+  // the first MFMA would wait for, together with the prefetched schedule row)
+  static constexpr int BIAS_F = G::MT_N * 16;  // bias floats per container
+  static constexpr int mx(int x, int y) { return x > y ? x : y; }
+  using TgtT = typename std::conditional<(G::C < 128), signed char, short>::type;
+  static constexpr int TGT = 2 * G::C * 16;  // target entries per wave
+  static constexpr int lds_bytes(int cpc) {
+    return 2 * mx(G::GE_G, mx(kQC * G::GS_G, cpc * G::GC_G + 1)) * G::FQ * 4 + kGanWaves * TGT * (int)sizeof(TgtT);
+  }
   static constexpr int cpc() {
     int best = 1;
-    for (int c = 1; c * G::GC_G <= PGP_GAN_CHUNK_G; ++c)
-      if (G::C % c == 0) best = c;
+    for (int c = 1; c * G::GC_G + 1 <= PGP_GAN_CHUNK_G; ++c)
+      if (G::C % c == 0 && c * BIAS_F <= 256 && lds_bytes(c) <= 160 * 1024) best = c;
     return best;
   }
   static constexpr int CPC = cpc();
   static constexpr int NCHUNK = 1 + NQC + G::C / CPC;
-  static constexpr int mx(int x, int y) { return x > y ? x : y; }
-  static constexpr int SLOT_G = mx(G::GE_G, mx(kQC * G::GS_G, CPC * G::GC_G));
+  static constexpr int SLOT_G = mx(G::GE_G, mx(kQC * G::GS_G, CPC * G::GC_G + 1));
   static constexpr int SLOT = SLOT_G * G::FQ;
-  // per-wave container targets (gen | final) as [2][C][16 windows] of int8
-  // (C < 128) or int16, flushed row-contiguous at the end (no scattered 4-byte
-  // stores in the loop)
-  using TgtT = typename std::conditional<(G::C < 128), signed char, short>::type;
-  static constexpr int TGT = 2 * G::C * 16;  // entries per wave
-  static constexpr int LDS_BYTES = 2 * SLOT * 4 + kGanWaves * TGT * (int)sizeof(TgtT);
+  // per-wave container targets (gen | final) as [2][C][16 windows] of TgtT:
+  // int8 (C < 128) or int16, flushed row-contiguous at the end (no scattered
+  // 4-byte stores in the loop)
+  static constexpr int LDS_BYTES = lds_bytes(CPC);
   // chunk k -> (global source, groups)
   PGP_DEV static void chunk(int k, const float* frags, const float** src, int* ng) {
     if (k == 0) {
@@ -94,6 +100,8 @@ struct GanGeo {
     }
   }
 };
+
+__device__ __attribute__((aligned(8))) float k3_zero_pair[2];  // never written
 
 template <int H>
 __global__ __launch_bounds__(kGanWaves * 64) void gan_kernel(FwdArgs a) {
@@ -127,6 +135,9 @@ __global__ __launch_bounds__(kGanWaves * 64) void gan_kernel(FwdArgs a) {
       int ng;
       GG::chunk(next, a.frags, &src, &ng);
       dma_groups(src, nxt, ng, wv, kGanWaves, lane);
+      if (next > GG::NQC)  // a container chunk: its biases after its groups (G_SIZE pads the last)
+        dma_groups(gt + G::G_B2 + (long)(next - 1 - GG::NQC) * GG::CPC * GG::BIAS_F, nxt + ng * 256, 1,
+                   (wv + ng) % kGanWaves, kGanWaves, lane);
     }
   };
   auto advance = [&]() {
@@ -205,14 +216,16 @@ __global__ __launch_bounds__(kGanWaves * 64) void gan_kernel(FwdArgs a) {
   // a lane's 4 row values 16t+4g+{0..3} as two 8-byte loads (H even: every pair is
   // aligned and lies wholly inside or wholly past the row)
   static_assert(H % 2 == 0, "row pairs");
+  // (branch-free: the address is selected, a zero pair outside the row, so the
+  // loaded values are not touched, nor waited for, until the next container)
   auto load_row = [&](int c, float (&v)[G::MT_N][4]) {
 #pragma unroll
     for (int t = 0; t < G::MT_N; ++t)
 #pragma unroll
       for (int r = 0; r < 4; r += 2) {
         const int hh = 16 * t + 4 * g + r;
-        float2 p = make_float2(0.f, 0.f);
-        if (valid && hh < H && c < G::C) p = *reinterpret_cast<const float2*>(sw + c * H + hh);
+        const float* src = (valid && hh < H && c < G::C) ? sw + c * H + hh : k3_zero_pair;
+        const float2 p = *reinterpret_cast<const float2*>(src);
         v[t][r] = p.x;
         v[t][r + 1] = p.y;
       }
@@ -228,8 +241,9 @@ __global__ __launch_bounds__(kGanWaves * 64) void gan_kernel(FwdArgs a) {
   // Gen2 of container c from its chunk groups cw: ns = b2[c] + W2[c] . hg (the
   // VALU tail rows into racc)
   auto gen2 = [&](int c, const float* cw, f32x4 (&ns)[G::MT_N], float (&racc)[kTailMax]) {
+    const float* bias = cur + GG::CPC * G::GC_G * G::FQ + (c % GG::CPC) * GG::BIAS_F;
 #pragma unroll
-    for (int t = 0; t < G::MT_N; ++t) ns[t] = ld4(gt + G::G_B2 + c * G::MT_N * 16 + 16 * t + 4 * g);
+    for (int t = 0; t < G::MT_N; ++t) ns[t] = ld4(bias + 16 * t + 4 * g);
 #pragma unroll
     for (int r = 0; r < kTailMax; ++r) racc[r] = 0.f;
     gan_prio<1>();

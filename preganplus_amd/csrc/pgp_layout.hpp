@@ -190,7 +190,9 @@ struct Geo {
   static constexpr int G_WD2 = G_BD1 + 64;        // [2][64]
   static constexpr int G_BD2 = G_WD2 + 128;       // [4] (2 used)
   static constexpr int G_B2 = G_BD2 + 4;          // [C][MT_N*16] gen output bias
-  static constexpr int G_SIZE = G_B2 + C * MT_N * 16;
+  // + one 1-KiB group of zero padding: K3 copies a ring chunk's biases to LDS
+  // as a whole group (global_load_lds), which may run past the last container
+  static constexpr int G_SIZE = G_B2 + C * MT_N * 16 + 256;
 };
 
 // PreGAN's FPE_16 encoder (models.py:10-115), folded table of K4 (pgp_fpe.hip).

@@ -158,18 +158,23 @@ PGP_DEV long tf_row(long p, int w) {
 // N-layout tiles <-> token-major [M][ld] rows (16-byte row groups).  Loads and
 // stores are unconditional (no branches, so the compiler's memory-counter waits
 // stay exact and a load issued a unit ahead is not waited for together with the
-// stores after it): a lane outside the batch reads row 0 (row[] is 0 there) and
-// selects zeros, and writes the spare row M of the destination (plan: M + 1 rows).
+// stores after it): a lane outside the batch reads a row of zeros (the ADDRESS
+// is selected, so the loaded value is not touched until its first use: a select
+// on the value made the compiler wait for each prefetch right after issuing it)
+// and writes the spare row M of the destination (plan: M + 1 rows).
+__device__ __attribute__((aligned(16))) float tf_zero_row[64];  // never written (DP <= 64)
+PGP_DEV const float* row_ptr(const float* __restrict__ base, long row, int ld, bool ok) {
+  return ok ? base + row * ld : tf_zero_row;
+}
 template <int NTL>
 PGP_DEV void load_tiles(f32x4 (&v)[NTL][3], const float* __restrict__ base, int ld, const long (&row)[3], bool ok,
                         int g) {
 #pragma unroll
-  for (int w = 0; w < 3; ++w)
+  for (int w = 0; w < 3; ++w) {
+    const float* p = row_ptr(base, row[w], ld, ok);
 #pragma unroll
-    for (int t = 0; t < NTL; ++t) {
-      const f32x4 x = ld4(base + row[w] * ld + 16 * t + 4 * g);
-      v[t][w] = ok ? x : zero4();
-    }
+    for (int t = 0; t < NTL; ++t) v[t][w] = ld4(p + 16 * t + 4 * g);
+  }
 }
 template <int NTL>
 PGP_DEV void store_tiles(const f32x4 (&v)[NTL][3], float* __restrict__ base, int ld, const long (&row)[3], bool ok,
@@ -186,8 +191,7 @@ PGP_DEV void store_tiles(const f32x4 (&v)[NTL][3], float* __restrict__ base, int
 template <int NTL>
 PGP_DEV void load_tile(f32x4 (&v)[NTL][3], const float* __restrict__ base, int ld, const long (&row)[3], bool ok,
                        int g, int c) {
-  const f32x4 x = ld4(base + row[c % 3] * ld + 16 * (c / 3) + 4 * g);
-  v[c / 3][c % 3] = ok ? x : zero4();
+  v[c / 3][c % 3] = ld4(row_ptr(base, row[c % 3], ld, ok) + 16 * (c / 3) + 4 * g);
 }
 
 // acc[o][w] += A . B over KSn k-steps; A = NO tiles of fragment groups in LDS
@@ -633,8 +637,7 @@ __global__ __launch_bounds__(kTfWaves * 64, 1) void tf_fwd_kernel(TfArgs a) {
                              for (int k = 0; k < PER; ++k) {
                                const int c = i * PER + k;
                                if (c < NS) {
-                                 const f32x4 v = ld4(tile_at(const_cast<float*>(a.in), rn[c % 3]) + 16 * (c / 3));
-                                 Xn[c / 3][c % 3] = okn ? v : zero4();
+                                 Xn[c / 3][c % 3] = ld4(row_ptr(a.in, rn[c % 3], F::DP, okn) + 16 * (c / 3) + 4 * g);
                                }
                              }
                            });
@@ -1247,6 +1250,7 @@ hipError_t launch_tf(int H, int kind, const TfArgs& a, hipStream_t st) {
 #define CASE(h)                                                                          \
   case h: {                                                                              \
     static_assert(FwdL<h>::TOTAL * 4 <= 160 * 1024, "forward LDS");                      \
+    static_assert(TF<h>::DP <= 64, "tf_zero_row covers a row");                          \
     static_assert(BffL<h>::TOTAL * 4 <= 160 * 1024, "ffn backward LDS");                 \
     static_assert(BatL<h>::TOTAL * 4 <= 160 * 1024, "attention backward LDS");           \
     static bool attr = [] {                                                              \

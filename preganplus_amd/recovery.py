@@ -158,11 +158,26 @@ class PreGANPlusRecovery(Recovery):
 
     # -- PreGANPlus.py:51-58 --
     def tune_model(self):
+        return self._tune_finish(self._tune_launch())
+
+    def _tune_launch(self):
+        """tune_model up to its device work: the on-the-fly dataset, then
+        backprop + accuracy (PreGANPlus.py:55-56) as one device graph launched
+        on the plugin's tuning stream, ordered after everything already issued
+        on the current stream (the detect forward read the weights it updates)."""
         wins, _, anom, cls = TR.on_the_fly_dataset(self.env.stats.time_series, self.env.stats.schedule_series,
                                                    self.train_time_data)
-        # backprop + accuracy (PreGANPlus.py:55-56) in one device graph
-        losses, (anomaly_score, class_score) = TR.backprop(self.trainer, self.tune_state, wins, anom, cls,
-                                                           score=True)
+        cur = torch.cuda.current_stream(self.trainer.device)
+        if getattr(self, "_tune_stream", None) is None:
+            self._tune_stream = torch.cuda.Stream(self.trainer.device)
+        self._tune_stream.wait_stream(cur)
+        return TR.backprop(self.trainer, self.tune_state, wins, anom, cls, score=True, stream=self._tune_stream,
+                           defer=True)
+
+    def _tune_finish(self, finish):
+        # later work on the current stream (weight sync, repack, the next detect) follows the graph
+        torch.cuda.current_stream(self.trainer.device).wait_stream(self._tune_stream)
+        losses, (anomaly_score, class_score) = finish()
         loss = float(np.mean([a for a, _ in losses]) + np.mean([t for _, t in losses]))   # train.py:56-57
         factor = self.tune_state.factor + TR.PROTO_UPDATE_MIN
         self.accuracy_list.append((loss, factor, anomaly_score, class_score))                  # :58
@@ -263,10 +278,28 @@ class PreGANPlusRecovery(Recovery):
         embedding = np.where(anom[:, None], out["protos"][0], 0.0)
         self.classes = out["cls"][0].tolist()
         self._final_target = out["final_target"][0].tolist()
+        # train_gan then tune_model (PreGANPlus.py:133-134).  They share no data
+        # (the GAN step reads the embedding and writes the GAN; the tuning step
+        # reads the time series and writes the Transformer and prototypes), so
+        # the tuning graph is launched first on its own stream and runs while
+        # train_gan waits for the host simulator; its host bookkeeping and
+        # accuracy_list entry still come after train_gan's, in the reference's
+        # order.  (If train_gan raises, the already launched tuning step is still
+        # completed and recorded, where the reference would not have run it.)
+        pending = launch_err = None
         try:
+            try:
+                pending = self._tune_launch()
+            except Exception as e:   # raised after train_gan, in the reference's order
+                launch_err = e
             self.train_gan(embedding, schedule_data)
-            self.tune_model()
+            if launch_err is not None:
+                raise launch_err
+            fin, pending = pending, None
+            self._tune_finish(fin)
         finally:
+            if pending is not None:
+                self._tune_finish(pending)
             # the master moved even if tune_model raised (accuracy() divides by zero
             # without a positive label, as the reference's does): K1-K3 follow it
             self.sync_inference_weights()

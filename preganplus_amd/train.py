@@ -812,21 +812,35 @@ class _TuneGraph:
                     self.dout[o:o + 2 * n * H].copy_(lg.reshape(-1))
                     self.dout[o + 2 * n * H:o + 4 * n * H].copy_(pr.reshape(-1))
 
-    def run(self, tr, wins, anom, cls, state_vec, tab):
+    def launch(self, tr, wins, anom, cls, state_vec, tab, stream=None):
+        """Upload, replay and download on ``stream`` (default: the current
+        one) without waiting; ``wait()`` returns the gathered outputs."""
         hv = self.hviews
         hv["W"][...] = wins
         hv["Y"][...] = anom
         hv["C"][...] = cls
         hv["sched"][...] = tab
         hv["state"][...] = state_vec
-        self.din.copy_(self.hin, non_blocking=True)
-        self.graph.replay()
-        self.hout.copy_(self.dout, non_blocking=True)
-        torch.cuda.current_stream(tr.device).synchronize()
+        st = stream if stream is not None else torch.cuda.current_stream(tr.device)
+        with torch.cuda.stream(st):
+            self.din.copy_(self.hin, non_blocking=True)
+            self.graph.replay()
+            self.hout.copy_(self.dout, non_blocking=True)
+        if getattr(self, "done", None) is None:
+            self.done = torch.cuda.Event()
+        self.done.record(st)
+
+    def wait(self):
+        self.done.synchronize()
         return self.hout.numpy()
 
+    def run(self, tr, wins, anom, cls, state_vec, tab):
+        self.launch(tr, wins, anom, cls, state_vec, tab)
+        return self.wait()
 
-def backprop(tr: Trainer, st: TuneState, wins, anom, cls, fused: bool | None = None, score: bool = False):
+
+def backprop(tr: Trainer, st: TuneState, wins, anom, cls, fused: bool | None = None, score: bool = False,
+             stream=None, defer: bool = False):
     """train.py:42-57: sequential batch-1 steps (forward, custom_loss, backward,
     AdamW).  Returns the per-window (aloss, tloss); with ``score`` also
     accuracy()'s (AScore, CScore) of the updated model on the same windows
@@ -839,12 +853,18 @@ def backprop(tr: Trainer, st: TuneState, wins, anom, cls, fused: bool | None = N
     replay as one captured HIP graph (``_TuneGraph``, cached per shape).  The
     host uploads the inputs and reads back the results once per call.
     ``loss_targets`` is the same bookkeeping in numpy (the tests restate with
-    it)."""
+    it).
+
+    With ``defer`` the graph is launched on ``stream`` (default: the current
+    one) and a function is returned that waits for it and returns what
+    backprop would (the plugin overlaps the tuning graph with train_gan's host
+    simulation this way); the host state ``st`` is updated when it is called."""
     st.num_zero, st.num_ones = 1, 1
     wins = np.asarray(wins)
     n, H = wins.shape[0], tr.H
     if n == 0:
-        return ([], None) if score else []
+        res = ([], None) if score else []
+        return (lambda: res) if defer else res
     anom = np.asarray(anom).reshape(n, H)
     cls = np.asarray(cls).reshape(n, H)
     bad = (anom > 0) & ((cls < 0) | (cls > 2))
@@ -860,16 +880,21 @@ def backprop(tr: Trainer, st: TuneState, wins, anom, cls, fused: bool | None = N
         tr._graphs[key] = g
     positive = np.any(anom > 0, axis=1)
     tab = tr.adam_schedule_np("transformer", positive, ("prototype_decoder.0.weight", "prototype_decoder.0.bias"))
-    out = g.run(tr, wins, anom, cls, st.vector(), tab)
-    tr.tune_state_dev = g.state     # the updated state, on the device (prototypes first: the device repack)
-    st.from_vector(out[2 * n:2 * n + 2 * K + 3])
-    losses = [tuple(r) for r in out[:2 * n].reshape(n, 2).tolist()]
-    if not score:
-        return losses
-    o = 2 * n + 2 * K + 3
-    lg = out[o:o + 2 * n * H].reshape(n, H, 2)
-    pr = out[o + 2 * n * H:o + 4 * n * H].reshape(n, H, 2)
-    return losses, accuracy_scores(lg, pr, anom, cls, st.protos)
+    g.launch(tr, wins, anom, cls, st.vector(), tab, stream)
+
+    def finish():
+        out = g.wait()
+        tr.tune_state_dev = g.state     # the updated state, on the device (prototypes first: the device repack)
+        st.from_vector(out[2 * n:2 * n + 2 * K + 3])
+        losses = [tuple(r) for r in out[:2 * n].reshape(n, 2).tolist()]
+        if not score:
+            return losses
+        o = 2 * n + 2 * K + 3
+        lg = out[o:o + 2 * n * H].reshape(n, H, 2)
+        pr = out[o + 2 * n * H:o + 4 * n * H].reshape(n, H, 2)
+        return losses, accuracy_scores(lg, pr, anom, cls, st.protos)
+
+    return finish if defer else finish()
 
 
 def bce_target(new_score, orig_score):

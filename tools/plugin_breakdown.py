@@ -31,7 +31,7 @@ def timed(name, fn):
     return wrap
 
 
-for name in ("train_gan", "tune_model", "sync_inference_weights", "recover_decision", "input_window"):
+for name in ("train_gan", "_tune_launch", "_tune_finish", "sync_inference_weights", "recover_decision", "input_window"):
     setattr(rec, name, timed(name, getattr(rec, name)))
 rec.infer.forward = timed("forward", rec.infer.forward)
 N = 40
