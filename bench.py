@@ -436,11 +436,13 @@ def bench_tune(args):
         emb = embedding(logits, protos, out=emb_buf)   # PreGANPlus.py:129
         rec(2)
         side.wait_stream(main)
+        # the tuning step (the longer chain) is issued first: the host's ~40 GAN
+        # launches would otherwise leave the device's main stream idle meanwhile
+        tun.step(wins, y, cls, mark=(lambda k: se[k].record(main)) if se is not None else None)
         with torch.cuda.stream(side):
             TR.train_gan_batched(tr, sim, envs, emb, s, out=sim_out, target=gan_target, all_reduce=True)
             if e is not None:
                 e[3].record(side)
-        tun.step(wins, y, cls, mark=(lambda k: se[k].record(main)) if se is not None else None)
         main.wait_stream(side)
         rec(4)
 
@@ -825,13 +827,13 @@ def bench_loop(args):
         # the GAN step on a second stream beside the tuning step (no shared
         # data, see bench_tune); the repack reads both sections of the master
         side.wait_stream(main)
+        tun.step(x, y, cls)          # issued first (see bench_tune)
+        if timed:
+            ev[4].record(main)
         with torch.cuda.stream(side):
             TR.train_gan_batched(tr, sim, envs, emb, sched, out=sim_out, target=gan_target)
             if timed:
                 ev[3].record(side)
-        tun.step(x, y, cls)
-        if timed:
-            ev[4].record(main)
         main.wait_stream(side)
         model.repack_master(tr.P, tun.state[:2 * K])
         if timed:

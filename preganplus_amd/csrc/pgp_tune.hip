@@ -21,6 +21,8 @@
 // (dlutils.py:326-329); the result is the same function, rounded once in fp32.
 #include <hip/hip_runtime.h>
 
+#include <mutex>
+
 #include <algorithm>
 
 #include "pgp_device.hpp"
@@ -813,7 +815,9 @@ bool plan_h(int B, TunePlan* out) {
   }
   q.da = take(M1 * Q::DP);
   q.db = take(M1 * Q::DP);
-  q.dq = take(M1 * 3 * Q::DP);
+  // one dQKV buffer per layer: layer 1's in_proj weight gradient reads its
+  // buffer on the side stream while layer 0's attention backward writes the other
+  for (int l = 0; l < 2; ++l) q.dq[l] = take(M1 * 3 * Q::DP);
   q.gsx = take(3L * B * 8);
   q.dpre = take((long)B * Q::NOP);
   q.wp = take((long)Q::NOP * Q::KD);
@@ -876,13 +880,64 @@ struct TfTiming {
 };
 TfTiming g_tft;
 
+// The backward's second stream: work off the critical path (the decoder's and
+// in_proj's weight gradients) runs beside the chain loss -> dX -> fused layer
+// backwards -> time encoder -> GAT, on the CUs the fused launches leave idle
+// in their last unit round (tf_unit_range packs the waves with an extra unit
+// into the first workgroups).  One non-blocking stream per device at low
+// priority; fork / join by events.  While the caller's stream is being
+// captured into a graph the work stays on it (serial, same results).
+struct SideStream {
+  hipStream_t s = nullptr;
+  hipEvent_t ev[8] = {};
+  unsigned next = 0;
+  bool ok = false;
+};
+SideStream* side_stream() {
+  static SideStream ss[16];
+  static std::mutex mu;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return nullptr;
+  std::lock_guard<std::mutex> lk(mu);
+  SideStream& x = ss[dev];
+  if (!x.s) {
+    int lo = 0, hi = 0;
+    (void)hipDeviceGetStreamPriorityRange(&lo, &hi);  // lo: the least urgent
+    x.ok = hipStreamCreateWithPriority(&x.s, hipStreamNonBlocking, lo) == hipSuccess;
+    for (auto& e : x.ev) x.ok = x.ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
+  }
+  return x.ok ? &x : nullptr;
+}
+struct Fork {
+  hipStream_t main, side;
+  SideStream* ss = nullptr;
+  explicit Fork(hipStream_t st) : main(st), side(st) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return;
+    ss = side_stream();
+    if (ss) side = ss->s;
+  }
+  // `to` waits for everything issued on `from` so far
+  hipError_t order(hipStream_t from, hipStream_t to) {
+    if (!ss || from == to) return hipSuccess;
+    hipEvent_t e = ss->ev[ss->next++ % 8];
+    hipError_t r = hipEventRecord(e, from);
+    return r != hipSuccess ? r : hipStreamWaitEvent(to, e, 0);
+  }
+  hipError_t fork() { return order(main, side); }
+  hipError_t join() { return order(side, main); }
+};
+
 template <int H>
 hipError_t tune_fwd_h(const TunePlan& p, const float* win, const float* P, float* ws, float* latent, float* logits,
                       float* protos, hipStream_t st) {
   using Q = TuneGeo<H>;
   const int B = p.B;
   hipError_t e;
-  TCK((dec_pack_kernel<H><<<(int)((Q::NOP * Q::KD + 255) / 256), 256, 0, st>>>(P, ws + p.wp, ws + p.wpt)));
+  // side: the decoder weights permuted for this step's forward and backward
+  Fork fk(st);
+  if ((e = fk.fork()) != hipSuccess) return e;
+  TCK((dec_pack_kernel<H><<<(int)((Q::NOP * Q::KD + 255) / 256), 256, 0, fk.side>>>(P, ws + p.wp, ws + p.wpt)));
   TCK((gat_fwd_kernel<H><<<(3 * B + 3) / 4, 256, 0, st>>>(B, win, P, ws + p.win, ws + p.g, ws + p.xb, ws + p.gs)));
   // the encoder: fragments packed from P, then one fused launch per layer
   TfArgs t{};
@@ -901,6 +956,7 @@ hipError_t tune_fwd_h(const TunePlan& p, const float* win, const float* P, float
     if ((e = launch_tf(H, 1, t, st)) != hipSuccess) return e;
     g_tft.mark(2 * l + 1, st);
   }
+  if ((e = fk.join()) != hipSuccess) return e;
   if ((e = launch_dec_fwd(H, B, p.dec_s, ws + p.x[2], ws + p.wp, ws + p.part, st)) != hipSuccess) return e;
   TCK((dec_fin_kernel<H><<<(int)(((long)B * 4 * H + 255) / 256), 256, 0, st>>>(B, p.dec_s, ws + p.part, P, logits,
                                                                                 protos)));
@@ -919,13 +975,11 @@ hipError_t tune_bwd_h(const TunePlan& p, const float* P, float* Gd, float* ws, c
   const long M = p.M;
   hipError_t e;
   RedBatch rb{ws + p.pool, p.pool_len};
+  Fork fk(st);
+  const hipStream_t sd = fk.side;
   TCK((tune_loss_kernel<<<(int)(((long)B * H + 255) / 256), 256, 0, st>>>(B, H, Q::NOP, logits, protos, y, mult,
                                                                            tgt, ws + p.dpre)));
-  TCK((dec_dw_kernel<H><<<dim3(Q::T, 2, p.dec_dws), 256, 0, st>>>(B, ws + p.dpre, ws + p.x[2], Gd, ws + p.part)));
-  if (p.dec_dws > 1) {
-    const long nw = 4L * H * G::L + 4 * H;
-    TCK((dec_dw_sum_kernel<H><<<(int)((nw + 255) / 256), 256, 0, st>>>(p.dec_dws, ws + p.part, Gd)));
-  }
+
   // grad of the encoder output = dpre . Wp (token layout, pgp_dec.hip)
   if ((e = launch_dec_dx(H, B, ws + p.dpre, ws + p.wpt, ws + p.da, st)) != hipSuccess) return e;
   // the encoder layers, fused per unit (pgp_tunef.hip); their weight-gradient
@@ -959,11 +1013,11 @@ hipError_t tune_bwd_h(const TunePlan& p, const float* P, float* Gd, float* ws, c
       ok = ok && rb.add(ng, sl, s0 + oG2, 1, H, 0, Lg + G::L_N2W, 0, H, H, Lg + G::L_N2B);
       if (!ok) return hipErrorInvalidValue;
     }
-    // attention block: dR1 (p.db), X_l -> dX_l (p.da), dQKV (p.dq)
+    // attention block: dR1 (p.db), X_l -> dX_l (p.da), dQKV (p.dq[l])
     t.in = ws + p.db;
     t.out = ws + p.da;
     t.x = ws + p.x[l];
-    t.dqkv = ws + p.dq;
+    t.dqkv = ws + p.dq[l];
     t.part = ws + p.tfs[l][1];
     g_tft.mark(tk + 2, st);
     if ((e = launch_tf(H, 3, t, st)) != hipSuccess) return e;
@@ -971,17 +1025,30 @@ hipError_t tune_bwd_h(const TunePlan& p, const float* P, float* Gd, float* ws, c
     if (!rb.add(ng, tf_slab_floats(H, 3), ws + p.tfs[l][1], H, H, H, Lg + G::L_OUT, H, H, (long)H * H,
                 Lg + G::L_OUTB))
       return hipErrorInvalidValue;
-    {  // in_proj: dQKV [M][3][DP] (x) X -> three [H][H] blocks of L_IN (+ bias)
-      constexpr int NP = 3 * DP;
-      const long pstride = (long)NP * DP + NP;
-      float* part = rb.take((long)p.dw_grid * pstride);
-      DwArgs a{M, ws + p.dq, NP, ws + p.x[l], DP, 0, part};
-      TCK((dw_kernel<NP, DP><<<p.dw_grid, 256, 0, st>>>(a)));
-      for (int q = 0; q < 3; ++q)
-        if (!rb.add(p.dw_grid, pstride, part + (long)q * DP * DP, H, H, DP, Lg + G::L_IN + (long)q * H * H, H, H,
-                    (long)NP * DP + q * DP - (long)q * DP * DP, Lg + G::L_INB + q * H))
-          return hipErrorInvalidValue;
-    }
+  }
+  // side, beside the serial tail below (time encoder, GAT): the weight
+  // gradients nothing on the critical path reads — the decoders' (dpre,
+  // encoder output -> G) and both layers' in_proj (dQKV [M][3][DP] (x) X ->
+  // three [H][H] blocks of L_IN + bias).  (Beside the fused launches they
+  // only slowed them: those take whole CUs, and a long side workgroup on a
+  // CU delays the next fused launch's workgroup there.)
+  if ((e = fk.fork()) != hipSuccess) return e;
+  TCK((dec_dw_kernel<H><<<dim3(Q::T, 2, p.dec_dws), 256, 0, sd>>>(B, ws + p.dpre, ws + p.x[2], Gd, ws + p.part)));
+  if (p.dec_dws > 1) {
+    const long nw = 4L * H * G::L + 4 * H;
+    TCK((dec_dw_sum_kernel<H><<<(int)((nw + 255) / 256), 256, 0, sd>>>(p.dec_dws, ws + p.part, Gd)));
+  }
+  for (int l = 1; l >= 0; --l) {
+    float* Lg = Gd + G::LAY0 + l * G::L_SIZE;
+    constexpr int NP = 3 * DP;
+    const long pstride = (long)NP * DP + NP;
+    float* part = rb.take((long)p.dw_grid * pstride);
+    DwArgs a{M, ws + p.dq[l], NP, ws + p.x[l], DP, 0, part};
+    TCK((dw_kernel<NP, DP><<<p.dw_grid, 256, 0, sd>>>(a)));
+    for (int q = 0; q < 3; ++q)
+      if (!rb.add(p.dw_grid, pstride, part + (long)q * DP * DP, H, H, DP, Lg + G::L_IN + (long)q * H * H, H, H,
+                  (long)NP * DP + q * DP - (long)q * DP * DP, Lg + G::L_INB + q * H))
+        return hipErrorInvalidValue;
   }
   // time encoder: p.da = grad of X0
   if ((e = dw<DP, DP>(p, rb, ws + p.da, DP, ws + p.g, DP, 0, H, H, Gd + G::W_TE, Gd + G::B_TE, st)) != hipSuccess)
@@ -996,6 +1063,7 @@ hipError_t tune_bwd_h(const TunePlan& p, const float* P, float* Gd, float* ws, c
       hipSuccess)
     return e;
   TCK((gat_param_kernel<H><<<1, 256, 0, st>>>(3 * B, ws + p.gsx, P, Gd)));
+  if ((e = fk.join()) != hipSuccess) return e;  // the side stream's partials and G writes
   return rb.flush(st);  // every deferred weight-gradient reduction: 2 launches
 }
 

@@ -36,7 +36,7 @@ struct TunePlan {
   long g = 0, xb = 0, gs = 0;                            // GAT out [M][DP], x-bar [M][16], (max, Z) [3B][4]
   long x[3] = {0, 0, 0};                                 // layer inputs; x[2] = encoder output [M][DP]
   long xh1[2] = {0, 0}, rs1[2] = {0, 0};                 // norm1 x-hat [M][DP], rstd [M] (checkpoints)
-  long da = 0, db = 0, dq = 0;                           // backward temporaries ([M][DP], [M][DP], [M][Q3P])
+  long da = 0, db = 0, dq[2] = {0, 0};                   // backward temporaries ([M][DP], [M][DP], 2 x [M][3][DP])
   long gsx = 0, dpre = 0, wp = 0, wpt = 0, part = 0, total = 0;  // wp: Wp [NOP][KD], wpt: WpT [T][DP][NOP]
   long tff = 0;                                          // fused-kernel weight fragments (pgp_tunef.hpp)
   long tfs[2][2] = {{0, 0}, {0, 0}};                     // [layer][ffn | attention] weight-gradient slabs

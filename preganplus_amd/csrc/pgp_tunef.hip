@@ -202,11 +202,16 @@ PGP_DEV void load_tile(f32x4 (&v)[NTL][3], const float* __restrict__ base, int l
 template <int NO, int KSn, class BF, class SIDE>
 PGP_DEV void tf_gemm_side(f32x4 (&acc)[NO][3], const float* A, BF bsrc, int lane, SIDE side) {
   constexpr int KGn = (KSn + 3) / 4;
+  // the A fragment group of the next 12 MFMAs is read one group ahead, so its
+  // LDS latency hides under the current group's MFMAs (one wave per SIMD: no
+  // other wave covers it), across output tiles too
+  f32x4 an = ld4(A + lane * 4);
 #pragma unroll
   for (int o = 0; o < NO; ++o) {
 #pragma unroll
     for (int q = 0; q < KGn; ++q) {
-      const f32x4 a = ld4(A + ((o * KGn + q) * 64 + lane) * 4);
+      const f32x4 a = an;
+      if (o * KGn + q + 1 < NO * KGn) an = ld4(A + ((o * KGn + q + 1) * 64 + lane) * 4);
 #pragma unroll
       for (int e = 0; e < 4; ++e)
         if (4 * q + e < KSn) {
@@ -443,12 +448,17 @@ PGP_DEV bool unit_rows(long u, long u1, long npairs, int j, long (&row)[3]) {
   return ok;
 }
 
-// unit range of one wave (contiguous, balanced over all waves of the grid)
+// unit range of one wave (contiguous, balanced over all waves of the grid):
+// floor(nu / waves) units each, and the nu % waves extra units to the FIRST
+// waves, so the waves that run one unit longer fill the first workgroups and
+// every other workgroup frees its CU a unit round early (the tuning step's
+// side stream runs there, pgp_tune.hip Fork)
 PGP_DEV void unit_range(long nu, long& u0, long& u1) {
   const long nw = (long)gridDim.x * kTfWaves;
   const long wv = (long)blockIdx.x * kTfWaves + (threadIdx.x >> 6);
-  u0 = nu * wv / nw;
-  u1 = nu * (wv + 1) / nw;
+  const long q = nu / nw, r = nu - q * nw;
+  u0 = wv * q + (wv < r ? wv : r);
+  u1 = u0 + q + (wv < r ? 1 : 0);
 }
 
 // LDS parameter block of a layer (natural rows, zero-padded)
