@@ -48,3 +48,17 @@ def test_executed_rate_cannot_exceed_peak_definition():
     # count is reported separately as an algorithmic rate
     for H in R.ENC_MFMA_PER_HOST:
         assert R.encoder_executed_flops_per_window(H) == R.ENC_MFMA_PER_HOST[H] * 2048 * H / 16
+
+
+@pytest.mark.skipif(not os.path.exists(LIB) or not os.path.exists("/opt/rocm/lib/llvm/bin/llvm-objdump"),
+                    reason="built library / llvm-objdump absent")
+def test_fused_tuning_prefetches_are_not_waited_for_at_once():
+    """The fused tuning kernels prefetch the next unit's 12 input tiles during
+    a GEMM; a value select right after the loads made the compiler wait for
+    them at once (0 MFMAs of cover).  Loads outside the batch select the
+    ADDRESS (pgp_tunef.hip row_ptr), so each prefetch has a GEMM's worth of
+    MFMAs before its wait in the built library."""
+    import isa_count
+    for name in ("tf_fwd_kernel", "tf_bwd_ffn_kernel", "tf_bwd_att_kernel"):
+        cover = isa_count.load_cover(name, 50)
+        assert sum(1 for c in cover if c >= 48) >= 12, (name, cover)

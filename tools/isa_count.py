@@ -72,3 +72,35 @@ if __name__ == "__main__":
         print(f"H={H}: {mfma} MFMA (16x16x4 f32), {valu} other VALU per host and wave")
     for H, d in tune_counts(Hs).items():
         print(f"H={H}: fused tuning kernels, MFMA per unit: {d}")
+
+
+def load_cover(name, H, lib=LIB):
+    """For each vector-memory load of kernel `name`<H> (program order), the
+    MFMAs issued between the load and the s_waitcnt that first requires it
+    (vmcnt counts loads and stores in order: `vmcnt(N)` requires all but the
+    newest N).  A prefetch whose value is selected right after the load shows
+    0 here (the compiler waits at once)."""
+    asm = _disasm(lib, name)
+    m = re.search(rf"<_ZN3pgp12_GLOBAL__N_1\d+{name}ILi{H}EE[^>]*>:\n(.*?)s_endpgm", asm, re.S)
+    if m is None:
+        raise RuntimeError(f"{name}<{H}> not found in {lib}")
+    pend, cover = [], []  # pend: [is_load, mfma_since]
+    for line in m.group(1).splitlines():
+        t = line.strip().split("//")[0].strip()
+        op = t.split(" ")[0] if t else ""
+        if op.startswith("v_mfma"):
+            for p in pend:
+                p[1] += 1
+        elif op.startswith(("global_load", "buffer_load")):
+            pend.append([True, 0])
+        elif op.startswith(("global_store", "buffer_store", "global_atomic")):
+            pend.append([False, 0])
+        elif op == "s_waitcnt":
+            w = re.search(r"vmcnt\((\d+)\)", t)
+            if w:
+                n = int(w.group(1))
+                while len(pend) > n:
+                    p = pend.pop(0)
+                    if p[0]:
+                        cover.append(p[1])
+    return cover
