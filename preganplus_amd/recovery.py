@@ -48,6 +48,7 @@ from . import weights as W
 from .model import DecisionModel, FPEDecisionModel, assemble_decision, migrations, to_numpy
 
 COEFF_ENERGY, COEFF_LATENCY = 0.8, 0.2  # constants.py:19-20
+NUM_EPOCHS = 50                          # constants.py:10 (offline training, train_model)
 MODEL_PLUS_FOLDER = "recovery/PreGANSrc/checkpointsplus"   # constants.py:3
 _DATA = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data")
 _AUTO = object()   # save_folder default: where load_models read the checkpoints
@@ -98,7 +99,10 @@ class PreGANPlusRecovery(Recovery):
             else:
                 packaged = os.path.join(_DATA, f"{self.env_name}_{self.hosts}.npz")
                 if not os.path.exists(packaged):
-                    raise FileNotFoundError(f"no checkpoint for {self.model_name} in {folder} or {packaged}")
+                    # no checkpoint at all: a new model trained offline, as the
+                    # reference's load_models does (PreGANPlus.py:26-28, 39-49)
+                    self._load_new_model(folder)
+                    return
                 weights, extra = W.load_npz(packaged)
                 # the GAN checkpoints save_gan keeps rewriting (load_gan, PreGANPlus.py:32-34)
                 gan = W.load_gan_checkpoints(folder, self.env_name, self.hosts)
@@ -123,6 +127,48 @@ class PreGANPlusRecovery(Recovery):
             self.train_time_data = np.asarray(self.extra["train_time_data"], dtype=np.float64)
         else:
             self.train_time_data = np.load(os.path.join("recovery/PreGANSrc/data", self.env_name, "time_series.npy"))
+
+    def _load_new_model(self, folder):
+        """load_model without a checkpoint (utils.py:76-78: epoch -1, fresh
+        parameters with torch's default initialisation, PGP_INIT_SEED seeds it)
+        and the GAN's (load_gan: its checkpoints, else new as well), then
+        train_model for num_epochs on the reference's data/<env>/time_series.npy."""
+        data = os.path.join("recovery/PreGANSrc/data", self.env_name, "time_series.npy")
+        if not os.path.exists(data):
+            raise FileNotFoundError(f"no checkpoint for {self.model_name} in {folder}, no packaged weights, and "
+                                    f"no training data {data} (utils.py:27-31)")
+        weights = W.synth_weights(self.hosts, seed=int(os.environ.get("PGP_INIT_SEED", 0)))
+        extra = {"meta/transformer/epoch": np.array(-1), "train_time_data": np.load(data)}
+        gan = W.load_gan_checkpoints(folder, self.env_name, self.hosts)
+        if gan is not None:
+            weights = dict(weights, **gan[0])
+            extra.update(gan[1])
+        self.load_models(weights=weights, extra=extra)
+        self.model_accuracy_list = []
+        self.train_model(NUM_EPOCHS)
+
+    # -- PreGANPlus.py:39-49 (offline training; the plotter is out of scope) --
+    def train_model(self, num_epochs=None, time_data=None):
+        """num_epochs epochs of backprop + accuracy over the whole training
+        series (load_dataset, utils.py:36-42), each appending (loss, factor,
+        AScore, CScore) to the Transformer's accuracy_list and, with a save
+        folder, rewriting its checkpoint (save_model, utils.py:49-58).  One
+        epoch is one backprop() graph of sequential batch-1 steps, the same
+        device path tune_model takes."""
+        wins, anom, cls = TR.load_dataset(self.train_time_data if time_data is None else time_data)
+        for _ in range(NUM_EPOCHS if num_epochs is None else num_epochs):
+            self.model_epoch += 1
+            losses, (anomaly_score, class_score) = TR.backprop(self.trainer, self.tune_state, wins, anom, cls,
+                                                               score=True)
+            loss = float(np.mean([a for a, _ in losses]) + np.mean([t for _, t in losses]))   # train.py:56-57
+            factor = self.tune_state.factor + TR.PROTO_UPDATE_MIN
+            self.model_accuracy_list.append((loss, factor, anomaly_score, class_score))
+            if self.save_folder is not None:
+                self.flush_checkpoints()
+                save_checkpoints(self.trainer, self.save_folder, self.env_name, self.model_epoch,
+                                 self.model_accuracy_list,
+                                 [("transformer", self.model_name, self.tune_state.protos)])
+        self.sync_inference_weights()
 
     # -- PreGANPlus.py:107-113 --
     def input_window(self):

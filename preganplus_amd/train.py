@@ -732,6 +732,22 @@ def form_test_dataset(data):
     return anydim + 0, which
 
 
+def normalize_time_data(time_data):
+    """utils.py:91-92: each column over its own maximum."""
+    d = np.asarray(time_data, dtype=np.float64)
+    return d / (np.max(d, axis=0) + 1e-8)
+
+
+def load_dataset(time_data):
+    """utils.py:36-42 (the offline training set of train_model) from the series
+    the reference reads from data/<env>/time_series.npy: normalised over its
+    own maxima, windows of every row, labels from the normalised series.  (The
+    schedules it also loads do not enter the Transformer's backprop.)"""
+    td = normalize_time_data(time_data)
+    anom, cls = form_test_dataset(td)
+    return convert_to_windows(td), anom, cls
+
+
 def on_the_fly_dataset(time_series, schedule_series, train_time_data):
     """utils.py:40-47: the last 10 rows, normalised; windows and labels."""
     td = normalize_test_time_data(np.asarray(time_series)[-LATEST_WINDOW_SIZE:], train_time_data)
