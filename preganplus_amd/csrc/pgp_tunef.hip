@@ -43,7 +43,7 @@ constexpr int kTfWaves = 4;  // one wave per SIMD (the backward needs > 256 regi
 // shader-clock cycles between consecutive TF_ST(k) marks to phase k of its slot
 // in tf_stamps[kind][wave] (vector stores by lane 0; one writer per slot).
 #ifdef PGP_TF_STAMPS
-constexpr int kStPhases = 16, kStWaves = 1024;
+constexpr int kStPhases = 16, kStWaves = 2048;
 __device__ unsigned long long tf_stamps[4][kStWaves][kStPhases];
 #define TF_ST_INIT()                                              \
   unsigned long long st_acc[kStPhases];                           \
@@ -59,7 +59,7 @@ __device__ unsigned long long tf_stamps[4][kStWaves][kStPhases];
   } while (0)
 #define TF_ST_END(kind)                                                                    \
   do {                                                                                     \
-    const int _w = (int)blockIdx.x * kTfWaves + (int)(threadIdx.x >> 6);                   \
+    const int _w = (int)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));                 \
     if ((threadIdx.x & 63) == 0 && _w < kStWaves)                                          \
       for (int _k = 0; _k < kStPhases; ++_k) tf_stamps[kind][_w][_k] += st_acc[_k];         \
   } while (0)
@@ -449,16 +449,19 @@ PGP_DEV bool unit_rows(long u, long u1, long npairs, int j, long (&row)[3]) {
 }
 
 // unit range of one wave (contiguous, balanced over all waves of the grid):
-// floor(nu / waves) units each, and the nu % waves extra units to the FIRST
-// waves, so the waves that run one unit longer fill the first workgroups and
-// every other workgroup frees its CU a unit round early (the tuning step's
-// side stream runs there, pgp_tune.hip Fork)
-PGP_DEV void unit_range(long nu, long& u0, long& u1) {
-  const long nw = (long)gridDim.x * kTfWaves;
-  const long wv = (long)blockIdx.x * kTfWaves + (threadIdx.x >> 6);
+// floor(nu / waves) units each, and the nu % waves extra units in rank order:
+// the first wave of every SIMD of every workgroup, then the second wave of
+// every SIMD, ... (waves w and w + 4 of a workgroup share SIMD w % 4), so the
+// units per SIMD stay balanced whatever the batch (a small batch gets one unit
+// per SIMD, not two on half of them); with one wave per SIMD the extras fill
+// the first workgroups, which free the others' CUs a unit round early
+PGP_DEV void unit_range(long nu, long& u0, long& u1, int waves = kTfWaves) {
+  const long nw = (long)gridDim.x * waves;
+  const int w = threadIdx.x >> 6;
+  const long rank = (long)(w / 4) * gridDim.x * 4 + (long)blockIdx.x * 4 + (w % 4);
   const long q = nu / nw, r = nu - q * nw;
-  u0 = wv * q + (wv < r ? wv : r);
-  u1 = u0 + q + (wv < r ? 1 : 0);
+  u0 = rank * q + (rank < r ? rank : r);
+  u1 = u0 + q + (rank < r ? 1 : 0);
 }
 
 // LDS parameter block of a layer (natural rows, zero-padded)
@@ -511,8 +514,60 @@ struct FwdL {
                        TOTAL = PAR + TfPar<H>::SIZE;
 };
 
+// attention scores of both heads from the q | k tiles -> probabilities
+// P[head][query w][key w2] (softmax over the 3 keys, lane-local)
 template <int H>
-__global__ __launch_bounds__(kTfWaves * 64, 1) void tf_fwd_kernel(TfArgs a) {
+PGP_DEV void tf_attn_probs(const f32x4 (&QK)[2 * TF<H>::NT][3], float (&P)[2][3][3], int g) {
+  using F = TF<H>;
+  constexpr int NT = F::NT;
+  float s[2][3][3];
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+    for (int w = 0; w < 3; ++w)
+#pragma unroll
+      for (int w2 = 0; w2 < 3; ++w2) s[hh][w][w2] = 0.f;
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int c = 16 * t + 4 * g + r;
+      const bool h0 = c < F::HD, h1 = c >= F::HD && c < H;
+#pragma unroll
+      for (int w = 0; w < 3; ++w)
+#pragma unroll
+        for (int w2 = 0; w2 < 3; ++w2) {
+          const float pr = QK[t][w][r] * QK[NT + t][w2][r];
+          s[0][w][w2] += h0 ? pr : 0.f;
+          s[1][w][w2] += h1 ? pr : 0.f;
+        }
+    }
+  float* f = &s[0][0][0];
+#pragma unroll
+  for (int i = 0; i < 18; i += 2) xsum2(f[i], f[i + 1]);
+  const float scale = 1.0f / sqrtf((float)F::HD);
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+    for (int w = 0; w < 3; ++w) {
+      const float a0 = s[hh][w][0] * scale, a1 = s[hh][w][1] * scale, a2 = s[hh][w][2] * scale;
+      const float mx = fmaxf(a0, fmaxf(a1, a2));
+      const float e0 = expf(a0 - mx), e1 = expf(a1 - mx), e2 = expf(a2 - mx);
+      const float inv = 1.0f / (e0 + e1 + e2);
+      P[hh][w][0] = e0 * inv;
+      P[hh][w][1] = e1 * inv;
+      P[hh][w][2] = e2 * inv;
+    }
+}
+
+// the forward runs TWO waves per SIMD (8 per workgroup, <= 256 registers per
+// wave): each wave's latencies (LDS fragments, the softmax / LayerNorm chains,
+// prefetch waits) are covered by the other wave's MFMAs.  q | k and v are
+// separate GEMMs (96 + 48 accumulator registers instead of 144 at once).
+constexpr int kTfFwdWaves = 8;
+
+template <int H>
+__global__ __launch_bounds__(kTfFwdWaves * 64, 1) void tf_fwd_kernel(TfArgs a) {
   using F = TF<H>;
   using L = FwdL<H>;
   using Q = TfPar<H>;
@@ -521,8 +576,8 @@ __global__ __launch_bounds__(kTfWaves * 64, 1) void tf_fwd_kernel(TfArgs a) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, g = lane >> 4, j = lane & 15;
   const int layer = a.layer;
   const float* fr = a.frags + F::layer_off(layer);
-  if (layer == 0) dma_groups(a.frags + F::TE_OFF, sm + L::W_TE, F::G_TE, wv, kTfWaves, lane);
-  dma_groups(fr + F::OFF_IN, sm + L::W_IN, F::G_IN + F::G_O + F::G_F1 + F::G_F2, wv, kTfWaves, lane);
+  if (layer == 0) dma_groups(a.frags + F::TE_OFF, sm + L::W_TE, F::G_TE, wv, kTfFwdWaves, lane);
+  dma_groups(fr + F::OFF_IN, sm + L::W_IN, F::G_IN + F::G_O + F::G_F1 + F::G_F2, wv, kTfFwdWaves, lane);
   load_params<H>(sm + L::PAR, a.P, layer);
   TF_ST_INIT();
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -531,18 +586,11 @@ __global__ __launch_bounds__(kTfWaves * 64, 1) void tf_fwd_kernel(TfArgs a) {
   const float* par = sm + L::PAR;
   const long npairs = (long)a.B * H, nu = (npairs + 15) / 16, spare = 3 * npairs;
   long u0, u1;
-  unit_range(nu, u0, u1);
-  // Memory traffic rides on the GEMMs (tf_gemm_side), one instruction per
-  // fragment group: the unit's input (layer 0: the GAT output) is loaded one
-  // unit ahead during the previous unit's linear2; x0 is stored during q|k|v,
-  // norm1's x-hat / rstd during linear1, and the layer output during the next
-  // unit's q|k|v (the last one after the loop).
-  f32x4 Xn[NT][3], Rp[NT][3];
-  long prow[3] = {spare, spare, spare};  // rows of the output held in Rp
-#pragma unroll
-  for (int t = 0; t < NT; ++t)
-#pragma unroll
-    for (int w = 0; w < 3; ++w) Rp[t][w] = zero4();
+  unit_range(nu, u0, u1, kTfFwdWaves);
+  // the unit's input (layer 0: the GAT output) is loaded one unit ahead during
+  // the previous unit's linear2; x0 is stored during q|k, norm1's x-hat / rstd
+  // during linear1, the layer output at the end of the unit
+  f32x4 Xn[NT][3];
   {
     long rn[3];
     const bool okn = unit_rows<H>(u0, u1, npairs, j, rn);
@@ -572,28 +620,42 @@ __global__ __launch_bounds__(kTfWaves * 64, 1) void tf_fwd_kernel(TfArgs a) {
         for (int w = 0; w < 3; ++w) X[t][w] = Xn[t][w];
       TF_ST(1);
     }
-    f32x4 QKV[F::NQ][3];
-    init_bias<F::NQ>(QKV, par + Q::BIN, g);
-    {  // side work: the previous unit's output, then (layer 0) this unit's x0
-      constexpr int NS = 3 * NT, NG = F::NQ * F::KG, PER = (2 * NS + NG - 1) / NG;
-      tf_gemm_side<F::NQ, F::KS>(QKV, sm + L::W_IN, [&](int s, int w) { return X[s >> 2][w][s & 3]; }, lane,
-                                 [&](int i) {
-#pragma unroll
-                                   for (int k = 0; k < PER; ++k) {
-                                     const int c = i * PER + k;
-                                     if (c < NS) {
-                                       st4(tile_at(a.out, prow[c % 3]) + 16 * (c / 3), Rp[c / 3][c % 3]);
-                                     } else if (c < 2 * NS && layer == 0) {
-                                       const int d = c - NS;
-                                       st4(tile_at(a.x0, srow[d % 3]) + 16 * (d / 3), X[d / 3][d % 3]);
-                                     }
-                                   }
-                                 });
-    }
-    TF_ST(3);
     float Pr[2][3][3];
+    {  // q | k (side work: layer 0's x0) -> the attention probabilities
+      f32x4 QK[2 * NT][3];
+      init_bias<2 * NT>(QK, par + Q::BIN, g);
+      constexpr int NS = 3 * NT, NG = 2 * NT * F::KG, PER = (NS + NG - 1) / NG;
+      tf_gemm_side<2 * NT, F::KS>(QK, sm + L::W_IN, [&](int s, int w) { return X[s >> 2][w][s & 3]; }, lane,
+                                  [&](int i) {
+#pragma unroll
+                                    for (int k = 0; k < PER; ++k) {
+                                      const int c = i * PER + k;
+                                      if (c < NS && layer == 0)
+                                        st4(tile_at(a.x0, srow[c % 3]) + 16 * (c / 3), X[c / 3][c % 3]);
+                                    }
+                                  });
+      TF_ST(3);
+      tf_attn_probs<H>(QK, Pr, g);
+    }
     f32x4 O[NT][3];
-    tf_attn_fwd<H>(QKV, Pr, O, g);
+    {  // v, then O = P . v per head
+      f32x4 V[NT][3];
+      init_bias<NT>(V, par + Q::BIN + 2 * NT * 16, g);
+      tf_gemm<NT, F::KS>(V, sm + L::W_IN + 2 * NT * F::KG * 256, [&](int s, int w) { return X[s >> 2][w][s & 3]; },
+                         lane);
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int hh = (16 * t + 4 * g + r) < F::HD ? 0 : 1;
+#pragma unroll
+          for (int w = 0; w < 3; ++w) {
+            const float p0 = hh ? Pr[1][w][0] : Pr[0][w][0], p1 = hh ? Pr[1][w][1] : Pr[0][w][1],
+                        p2 = hh ? Pr[1][w][2] : Pr[0][w][2];
+            O[t][w][r] = fmaf(p0, V[t][0][r], fmaf(p1, V[t][1][r], p2 * V[t][2][r]));
+          }
+        }
+    }
     TF_ST(4);
     f32x4 R[NT][3];
     init_bias<NT>(R, par + Q::BO, g);
@@ -646,9 +708,8 @@ __global__ __launch_bounds__(kTfWaves * 64, 1) void tf_fwd_kernel(TfArgs a) {
 #pragma unroll
                              for (int k = 0; k < PER; ++k) {
                                const int c = i * PER + k;
-                               if (c < NS) {
+                               if (c < NS)
                                  Xn[c / 3][c % 3] = ld4(row_ptr(a.in, rn[c % 3], F::DP, okn) + 16 * (c / 3) + 4 * g);
-                               }
                              }
                            });
     }
@@ -662,17 +723,14 @@ __global__ __launch_bounds__(kTfWaves * 64, 1) void tf_fwd_kernel(TfArgs a) {
     for (int t = 0; t < NT; ++t) {
       const f32x4 ga = ld4(par + Q::N2W + 16 * t + 4 * g), be = ld4(par + Q::N2B + 16 * t + 4 * g);
 #pragma unroll
-      for (int w = 0; w < 3; ++w) Rp[t][w] = R[t][w] * ga + be;
+      for (int w = 0; w < 3; ++w) R[t][w] = R[t][w] * ga + be;
     }
 #pragma unroll
-    for (int w = 0; w < 3; ++w) prow[w] = srow[w];
+    for (int w = 0; w < 3; ++w)
+#pragma unroll
+      for (int t = 0; t < NT; ++t) st4(tile_at(a.out, srow[w]) + 16 * t, R[t][w]);
     TF_ST(9);
   }
-  // the last unit's output
-#pragma unroll
-  for (int w = 0; w < 3; ++w)
-#pragma unroll
-    for (int t = 0; t < NT; ++t) st4(tile_at(a.out, prow[w]) + 16 * t, Rp[t][w]);
   TF_ST(10);
   TF_ST_END(layer);
 }
@@ -1194,7 +1252,7 @@ hipError_t tf_launch(int kind, const TfArgs& a, int grid, hipStream_t st) {
     }
     case 1: {
       const size_t lds = (size_t)FwdL<H>::TOTAL * 4;
-      tf_fwd_kernel<H><<<grid, kTfWaves * 64, lds, st>>>(a);
+      tf_fwd_kernel<H><<<grid, kTfFwdWaves * 64, lds, st>>>(a);
       return hipGetLastError();
     }
     case 2: {

@@ -45,7 +45,7 @@ def main(H=50, B=1030):
     tr.tune_forward(x)
     tr.tune_backward(B, y, mult, tgt)
     torch.cuda.synchronize()
-    buf = np.zeros((4, 1024, 16), dtype=np.uint64)
+    buf = np.zeros((4, 2048, 16), dtype=np.uint64)
     assert L.pgp_debug_tf_stamps(buf.ctypes.data) == 0
     names = list(PHASES)
     for k, name in enumerate(names):
