@@ -21,45 +21,28 @@
 namespace pgp {
 namespace {
 
-// Tail mode, layer 0: attention scores as bilinear forms of the 3 raw features
-// per step (q, k affine in them; pgp_pack.cpp T_F0S): lane-local FMAs instead of
-// q / k tiles, partial dot products and cross-lane sums
-#ifndef PGP_ENC_BILIN
-#define PGP_ENC_BILIN 1
-#endif
+// Launch geometry (the alternatives were A/B-timed and are recorded in
+// DESIGN.md §12; they are not kept as build switches):
+//  * tail mode, layer 0: attention scores as bilinear forms of the 3 raw
+//    features per step (q, k affine in them; pgp_pack.cpp T_F0S): lane-local
+//    FMAs instead of q / k tiles, partial dot products and cross-lane sums;
+//  * H <= 16 (weights LDS-resident): kEnc16Waves waves per workgroup share one
+//    LDS copy, kEnc16EU waves per SIMD requested from the register allocator,
+//    one 16-window block per wave (unit ranges measured slower there).
 constexpr int kEncWaves = 4;
-// H <= 16 (weights LDS-resident): ENC16_WAVES waves per workgroup share one LDS
-// copy, and ENC16_EU waves per SIMD are requested from the register allocator
-#ifndef PGP_ENC16_WAVES
-#define PGP_ENC16_WAVES 4
-#endif
-#ifndef PGP_ENC16_EU
-#define PGP_ENC16_EU 2
-#endif
-#ifndef PGP_ENC_UNITS16
-#define PGP_ENC_UNITS16 0
-#endif
+constexpr int kEnc16Waves = 4, kEnc16EU = 2;
 // Tail mode (H = 50) resident: the weight groups the tail path reads (layer 0's
 // stage 2 — its q/k/v and out_proj are folded onto the raw features — and all
 // of layer 1: 104 KB at H = 50) stay in LDS for the whole launch, one 8-wave
 // workgroup per CU (2 waves per SIMD as before); no ring barriers or DMAs in the
 // host loop, and one copy per workgroup instead of one per host
-#ifndef PGP_ENC_TAIL_RES
-#define PGP_ENC_TAIL_RES 1
-#endif
 template <int H>
-constexpr bool tail_res() { return PGP_ENC_TAIL_RES && Geo<H>::TAIL && PGP_ENC_BILIN; }
+constexpr bool tail_res() { return Geo<H>::TAIL; }
 // waves per tail-resident workgroup (one workgroup per CU): 8 = 2 waves per
 // SIMD, 12 = 3 (the register allocator then has 168 VGPRs + AGPRs per wave)
-// tail mode: the feed-forward hidden state formed and consumed 16 rows at a time
-#ifndef PGP_ENC_FFN_CHUNK
-#define PGP_ENC_FFN_CHUNK 1
-#endif
-#ifndef PGP_ENC_TAIL_WAVES
-#define PGP_ENC_TAIL_WAVES 8
-#endif
+constexpr int kEncTailWaves = 8;
 template <int H>
-constexpr int enc_waves() { return H <= 16 ? PGP_ENC16_WAVES : tail_res<H>() ? PGP_ENC_TAIL_WAVES : kEncWaves; }
+constexpr int enc_waves() { return H <= 16 ? kEnc16Waves : tail_res<H>() ? kEncTailWaves : kEncWaves; }
 template <int H>
 constexpr int NW_STAGE() { return enc_waves<H>(); }
 
@@ -69,17 +52,16 @@ constexpr int NW_STAGE() { return enc_waves<H>(); }
 template <int H>
 struct EncLds {
   static constexpr bool TRES = tail_res<H>();
-  // resident modes have no barrier in the host loop: waves can take (block,
-  // host) unit ranges and prefetch through an LDS slot.  At H <= 16 that
-  // measured slower (fleet 1.97 -> 2.00 ms), so PGP_ENC_UNITS16 defaults to 0
-  // there (one block per wave)
+  // the tail-resident mode has no barrier in the host loop: waves take
+  // (block, host) unit ranges and prefetch through an LDS slot (at H <= 16,
+  // also resident, that measured slower: fleet 1.97 -> 2.00 ms)
   static constexpr int RES0 = TRES ? Geo<H>::st_begin(Geo<H>::NST - 1) : 0;  // layer 0 stage 2
   static constexpr int STREAM = (kLayers * Geo<H>::LAYER_G - RES0) * Geo<H>::FQ;  // floats
   static constexpr bool RESIDENT = TRES || STREAM * 4 <= 32 * 1024;
   static constexpr int SLOT = Geo<H>::SLOT_G * Geo<H>::FQ;
   static constexpr int TAB = Geo<H>::t_size(kMaxProtos);
   static constexpr int TOTAL = (RESIDENT ? STREAM : 2 * SLOT) + TAB;
-  static constexpr bool UNITS = TRES || (RESIDENT && PGP_ENC_UNITS16);
+  static constexpr bool UNITS = TRES;
 };
 
 // ReLU as one integer max on the bit pattern (negative floats have negative
@@ -97,16 +79,9 @@ PGP_DEV float relu_enc(float x) {
 
 // MFMA phases run at wave priority 1, VALU phases (softmax, LayerNorm) at 0: the
 // co-resident wave of the other workgroup on the SIMD then gets its MFMA issue
-// slots ahead of a VALU stream (PGP_ENC_PRIO=0 disables)
-#ifndef PGP_ENC_PRIO
-#define PGP_ENC_PRIO 1
-#endif
-PGP_DEV void prio_mfma() {
-  if (PGP_ENC_PRIO) __builtin_amdgcn_s_setprio(1);
-}
-PGP_DEV void prio_valu() {
-  if (PGP_ENC_PRIO) __builtin_amdgcn_s_setprio(0);
-}
+// slots ahead of a VALU stream
+PGP_DEV void prio_mfma() { __builtin_amdgcn_s_setprio(1); }
+PGP_DEV void prio_valu() { __builtin_amdgcn_s_setprio(0); }
 
 // acc[m][w] += A[m] . B for the first NM of NMA accumulator tiles, A = NM tiles
 // x KQ groups in LDS, B k-step s = Bx[s/4][w][s%4]
@@ -372,21 +347,10 @@ PGP_DEV void encoder_layer_tail(f32x4 (&X)[Geo<H>::MT_D][3], Ring<H>& ring, cons
   constexpr int TQ = G::TQ, SR = G::SR, HF = G::HF;
   const int g = lane >> 4;
   // [S0] q and k of both heads
-  constexpr bool BIL = F0 && PGP_ENC_BILIN;
+  constexpr bool BIL = F0;  // layer 0's scores as bilinear forms (the q / k fold is not needed)
   f32x4 QK[BIL ? 1 : 2 * TQ][3];
   float qr[SR][3], kr[SR][3];
   if constexpr (BIL) {
-  } else if constexpr (F0) {
-    qkv_fold<H, 2 * TQ>(QK, 0, 2 * TQ, tab, ba, lane, g);
-#pragma unroll
-    for (int n = 0; n < SR; ++n)
-#pragma unroll
-      for (int w = 0; w < 3; ++w) {
-        float q = row_fold_part<H>(0, n, w, tab, ba, g), k = row_fold_part<H>(1, n, w, tab, ba, g);
-        xsum2(q, k);
-        qr[n][w] = q + row_fold_bias<H>(0, n, w, tab);
-        kr[n][w] = k + row_fold_bias<H>(1, n, w, tab);
-      }
   } else {
 #pragma unroll
     for (int m = 0; m < 2 * TQ; ++m) {
@@ -569,7 +533,6 @@ PGP_DEV void encoder_layer_tail(f32x4 (&X)[Geo<H>::MT_D][3], Ring<H>& ring, cons
   }  // F0
   ring.advance();
   // [S2] relu(W1 x + b1), W2 . h + b2 + x, norm2
-#if PGP_ENC_FFN_CHUNK
   // hidden tile by hidden tile: tile c of relu(W1 x + b1) is k-group c of the
   // W2 contraction, consumed as soon as it is formed (12 hidden-state VGPRs
   // live instead of 48; same accumulation order as the unchunked form)
@@ -617,36 +580,6 @@ PGP_DEV void encoder_layer_tail(f32x4 (&X)[Geo<H>::MT_D][3], Ring<H>& ring, cons
 #pragma unroll
     for (int w = 0; w < 3; ++w) acc[G::MT_X][w][0] += rows_pick<G::XR>(rf, w);
   }
-#else
-  f32x4 F1[G::MT_F][3];
-#pragma unroll
-  for (int mt = 0; mt < G::MT_F; ++mt) {
-    const f32x4 b1 = ld4(TL + G::TL_B1 + 16 * mt + 4 * g);
-#pragma unroll
-    for (int w = 0; w < 3; ++w) F1[mt][w] = b1;
-  }
-  gemm3<G::MT_F, G::KQ_D, G::KS_D, G::MT_D>(F1, ring.cur, X, lane);
-#pragma unroll
-  for (int mt = 0; mt < G::MT_F; ++mt)
-#pragma unroll
-    for (int w = 0; w < 3; ++w)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) F1[mt][w][r] = relu_enc<H>(F1[mt][w][r]);
-#pragma unroll
-  for (int mt = 0; mt < G::MT_D; ++mt) {
-    const f32x4 b2 = ld4(TL + G::TL_B2 + 16 * mt + 4 * g), g1 = ld4(TL + G::TL_LN1G + 16 * mt + 4 * g);
-#pragma unroll
-    for (int w = 0; w < 3; ++w) acc[mt][w] = X[mt][w] * g1 + b2;  // residual gamma*x-hat + beta, + b2
-  }
-  {
-    float rf[G::XR][3];
-    zero_rows(rf);
-    gemm3_rows<G::MT_X, G::KQ_F, 16, G::MT_F, G::MT_D, G::XR>(acc, ring.cur + G::G_F1 * G::FQ, F1, lane, rf,
-                                                             TL + G::TL_RF, g);
-#pragma unroll
-    for (int w = 0; w < 3; ++w) acc[G::MT_X][w][0] += rows_pick<G::XR>(rf, w);
-  }
-#endif
   ring.advance();
   // both norm2s emit x-hat: layer 0's gamma / beta are folded into layer 1's
   // in_proj and residual, the last layer's into the decoders (which are linear
@@ -726,7 +659,7 @@ PGP_DEV void encoder_layer(f32x4 (&X)[Geo<H>::MT_D][3], Ring<H>& ring, const flo
 }
 
 template <int H>
-__global__ __launch_bounds__(enc_waves<H>() * 64, H <= 16 ? PGP_ENC16_EU : tail_res<H>() ? 1 : 2) void encoder_kernel(
+__global__ __launch_bounds__(enc_waves<H>() * 64, H <= 16 ? kEnc16EU : tail_res<H>() ? 1 : 2) void encoder_kernel(
     FwdArgs a) {
   using G = Geo<H>;
   using L = EncLds<H>;
@@ -771,7 +704,7 @@ __global__ __launch_bounds__(enc_waves<H>() * 64, H <= 16 ? PGP_ENC16_EU : tail_
 #pragma unroll
       for (int w = 0; w < 3; ++w) {
 #pragma unroll
-        for (int f = 0; f < 3; ++f) xv[w][f] = (G::TAIL && PGP_ENC_BILIN) ? pre[w * 48 + 16 * f + j] : 0.f;
+        for (int f = 0; f < 3; ++f) xv[w][f] = G::TAIL ? pre[w * 48 + 16 * f + j] : 0.f;
         const float v = pre[w * 48 + (lane < 48 ? lane : 47)];
         ba[w] = g < 3 ? v : 0.f;  // feature g of window j
       }
@@ -782,7 +715,7 @@ __global__ __launch_bounds__(enc_waves<H>() * 64, H <= 16 ? PGP_ENC16_EU : tail_
       for (int w = 0; w < 3; ++w)
 #pragma unroll
         for (int f = 0; f < 3; ++f)
-          xv[w][f] = (G::TAIL && PGP_ENC_BILIN && active) ? agg[(h * 3 + w) * 48 + 16 * f + j] : 0.f;
+          xv[w][f] = (G::TAIL && active) ? agg[(h * 3 + w) * 48 + 16 * f + j] : 0.f;
     }
     f32x4 X[G::MT_D][3];
 #pragma unroll

@@ -19,41 +19,24 @@
 namespace pgp {
 namespace {
 
-#ifndef PGP_GAN_WAVES
-#define PGP_GAN_WAVES 16
-#endif
-constexpr int kGanWaves = PGP_GAN_WAVES;  // waves per workgroup (16 windows each)
-// schedule k-blocks (16 columns each) per ring chunk, and the chunk size cap
-// (1-KiB groups) that sets the containers per phase-3 chunk: one barrier per chunk
-#ifndef PGP_GAN_QC
-#define PGP_GAN_QC 8
-#endif
-#ifndef PGP_GAN_CHUNK_G
-#define PGP_GAN_CHUNK_G 65
-#endif
-constexpr int kQC = PGP_GAN_QC;
-// per-container MFMA loops at wave priority 1, the tanh / argmax VALU at 0
-#ifndef PGP_GAN_PRIO
-#define PGP_GAN_PRIO 1
-#endif
-// Disc1's new-schedule half: skip the MFMAs whose whole k slice is padding rows
-// (at H = 50 the last tile's e = 2, 3 steps: 8 of 128 MFMAs per container)
-#ifndef PGP_GAN_KSKIP
-#define PGP_GAN_KSKIP 1
-#endif
-// Gen2 tail rows: a last row tile with at most kTailMax real rows runs on VALU
-#ifndef PGP_GAN_TAIL
-#define PGP_GAN_TAIL 1
-#endif
+// Geometry and schedule (alternatives A/B-timed in DESIGN.md §12, not kept as
+// build switches): 16 waves per workgroup (16 windows each); kQC schedule
+// k-blocks (16 columns each) per ring chunk; kChunkG caps a phase-3 ring chunk
+// (1-KiB groups), which sets the containers per chunk (one barrier per chunk);
+// the per-container MFMA loops run at wave priority 1, the tanh / argmax VALU
+// at 0; Disc1's new-schedule half skips the MFMAs whose whole k slice is
+// padding rows (at H = 50 the last tile's e = 2, 3 steps: 8 of 128 MFMAs per
+// container); a Gen2 last row tile with at most kTailMax real rows runs on
+// VALU; with one container per chunk the second half of the waves starts each
+// container kGanSleep x 64 cycles late.
+constexpr int kGanWaves = 16;
+constexpr int kQC = 8;
+constexpr int kChunkG = 65;
 constexpr int kTailMax = 2;
-// start-of-container delay of the second half of the waves, in s_sleep units of
-// 64 cycles (0: off)
-#ifndef PGP_GAN_SLEEP
-#define PGP_GAN_SLEEP 24
-#endif
+constexpr int kGanSleep = 24;
 template <int P>
 __device__ __forceinline__ void gan_prio() {
-  if (PGP_GAN_PRIO) __builtin_amdgcn_s_setprio(P);
+  __builtin_amdgcn_s_setprio(P);
 }
 
 template <int H>
@@ -73,7 +56,7 @@ struct GanGeo {
   }
   static constexpr int cpc() {
     int best = 1;
-    for (int c = 1; c * G::GC_G + 1 <= PGP_GAN_CHUNK_G; ++c)
+    for (int c = 1; c * G::GC_G + 1 <= kChunkG; ++c)
       if (G::C % c == 0 && c * BIAS_F <= 256 && lds_bytes(c) <= 160 * 1024) best = c;
     return best;
   }
@@ -234,7 +217,7 @@ __global__ __launch_bounds__(kGanWaves * 64) void gan_kernel(FwdArgs a) {
   // dot products (k split over the lane groups, summed across them) issued in
   // the shadow of the other tiles' MFMAs, instead of 16 MFMAs per container
   constexpr int NTR = H - 16 * (G::MT_N - 1);
-  constexpr bool TAIL = PGP_GAN_TAIL && G::MT_N > 1 && NTR <= kTailMax;
+  constexpr bool TAIL = G::MT_N > 1 && NTR <= kTailMax;
   constexpr int MTM = TAIL ? G::MT_N - 1 : G::MT_N;  // Gen2 tiles on MFMA
   float sv[G::MT_N][4];
   load_row(0, sv);
@@ -313,7 +296,7 @@ __global__ __launch_bounds__(kGanWaves * 64) void gan_kernel(FwdArgs a) {
         for (int i = 0; i < 2; ++i) w[i] = ld4(cw + (G::GC_G2 + (m0 + i) * G::MT_N + q4) * 256 + lane * 4);
 #pragma unroll
         for (int e = 0; e < 4; ++e)
-          if (!PGP_GAN_KSKIP || 16 * q4 + e < H)  // k = 16 q4 + 4g + e: all lanes' rows >= H are zero
+          if (16 * q4 + e < H)  // k = 16 q4 + 4g + e: all lanes' rows >= H are zero
 #pragma unroll
             for (int i = 0; i < 2; ++i) hd[m0 + i] = mfma(w[i][e], ns[q4][e], hd[m0 + i]);
       }
@@ -352,7 +335,7 @@ __global__ __launch_bounds__(kGanWaves * 64) void gan_kernel(FwdArgs a) {
     // container interval late, so its tanh / argmax VALU phase meets the
     // first half's MFMAs instead of every wave reaching it together
     // (one container per chunk only: at H <= 32 it cost the fleet 0.3 %)
-    if (PGP_GAN_SLEEP > 0 && GG::CPC == 1 && wv >= kGanWaves / 2) __builtin_amdgcn_s_sleep(PGP_GAN_SLEEP);
+    if (GG::CPC == 1 && wv >= kGanWaves / 2) __builtin_amdgcn_s_sleep(kGanSleep);
     gen2(c, cw, ns, racc);
     finish(c, cw, ns, racc, sv);
     if ((c + 1) % GG::CPC == 0) advance();

@@ -35,13 +35,9 @@ __device__ __forceinline__ float lrelu001(float e) { return fmaxf(e, 0.01f * e);
 // 16-B stores (scattered 4-B stores amplified the HBM writes 6x:
 // profiles/r01/pmc_r01pmc2_summary.txt).
 // one-item-per-wave mode (H > 32): load the next item's features one item
-// ahead (PGP_GAT_PF), and the edge loop's independent accumulation chains
-#ifndef PGP_GAT_PF
-#define PGP_GAT_PF 1
-#endif
-#ifndef PGP_GAT_CHAINS
-#define PGP_GAT_CHAINS 2
-#endif
+// ahead (kGatPf), and the edge loop's independent accumulation chains (kGatChains)
+constexpr bool kGatPf = true;
+constexpr int kGatChains = 2;
 constexpr int seg_lanes(int h) { return h <= 8 ? 8 : h <= 16 ? 16 : h <= 32 ? 32 : 64; }
 
 template <int H>
@@ -62,7 +58,7 @@ __global__ __launch_bounds__(256) void gat_agg_kernel(int B, const float* __rest
   __syncthreads();
   // P == 1 (H > 32): the next item's features are loaded one item ahead, from a
   // clamped address (unconditional loads, zeroed when out of range)
-  constexpr bool PF1 = P == 1 && PGP_GAT_PF;
+  constexpr bool PF1 = P == 1 && kGatPf;
   auto ldx = [&](int i0, float& x0, float& x1, float& x2) {
     const int it = i0 + seg;
     const long b = blk * 16 + it / 3;
@@ -109,14 +105,14 @@ __global__ __launch_bounds__(256) void gat_agg_kernel(int B, const float* __rest
     if constexpr (P == 1) {
       // one item per wave (H > 32): the edge loop is latency-bound on its
       // accumulation chains, so packed f32 (one v_pk_mul for both branch
-      // products, a max, two v_pk_fma for (a0, a1) and (a2, S)) over PGP_GAT_CHAINS
+      // products, a max, two v_pk_fma for (a0, a1) and (a2, S)) over kGatChains
       // interleaved chains (source i -> chain i mod NC) summed at the end
       sx[wv][base + hl] = f32x4{Ap, An, x0, x1};
       sy[wv][base + hl] = f32x2{x2, 1.f};
       __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes landed
       __builtin_amdgcn_wave_barrier();
       const f32x2 Bpn = {Bp, Bn};
-      constexpr int NC = PGP_GAT_CHAINS;
+      constexpr int NC = kGatChains;
       f32x2 a01[NC], a2s[NC];
 #pragma unroll
       for (int c = 0; c < NC; ++c) a01[c] = a2s[c] = f32x2{0.f, 0.f};

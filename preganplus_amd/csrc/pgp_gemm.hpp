@@ -110,10 +110,7 @@ PGP_DEV float lrelu(float x) { return x > 0.f ? x : 0.01f * x; }
 // fragment read hit disjoint banks.
 // ============================================================================
 constexpr int lds_stride(int n) { return n + ((16 - n % 64) % 64 + 64) % 64; }
-#ifndef PGP_DW_ROWS
-#define PGP_DW_ROWS 32
-#endif
-constexpr int kDwRows = PGP_DW_ROWS;  // rows per LDS-staged chunk of the weight-gradient contractions
+constexpr int kDwRows = 32;  // rows per LDS-staged chunk of the weight-gradient contractions
 
 template <int NP, int KP, int NTW>
 PGP_DEV void dw_accumulate(long r0, long r1, const float* __restrict__ Y, long ldy, const float* __restrict__ X,

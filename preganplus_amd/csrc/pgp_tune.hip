@@ -32,16 +32,12 @@
 #include "pgp_tunef.hpp"
 #include "pgp_tunetargets.hpp"
 
-// workgroups of the token-major GEMMs / weight-gradient kernels (grid-stride loops)
-#ifndef PGP_LIN_CAP
-#define PGP_LIN_CAP 512
-#endif
-#ifndef PGP_DW_CAP
-#define PGP_DW_CAP 512
-#endif
 
 namespace pgp {
 namespace {
+
+// workgroups of the token-major GEMMs / weight-gradient kernels (grid-stride loops)
+constexpr int kLinCap = 512, kDwCap = 512;
 
 enum : int { EPI_STORE = 0 };
 
@@ -827,12 +823,12 @@ bool plan_h(int B, TunePlan* out) {
   for (int l = 0; l < 2; ++l)
     for (int k = 0; k < 2; ++k) q.tfs[l][k] = take((long)q.tf_grid * tf_slab_floats(H, 2 + k));
   const long nrb = (M + 15) / 16;
-  q.lin_grid = (int)std::min<long>(PGP_LIN_CAP, std::max<long>(1, (nrb + 3) / 4));
-  q.dw_grid = (int)std::min<long>(PGP_DW_CAP, std::max<long>(1, (nrb + 7) / 8));
+  q.lin_grid = (int)std::min<long>(kLinCap, std::max<long>(1, (nrb + 3) / 4));
+  q.dw_grid = (int)std::min<long>(kDwCap, std::max<long>(1, (nrb + 7) / 8));
   q.dec_s = dec_fwd_splits(H, B);
   // partial slabs; every bound grows with B, so a workspace sized for B_max serves any B <= B_max
   const long np_max = std::max(Q::Q3P, 64);
-  long part = (long)PGP_DW_CAP * (np_max * 64 + np_max);                  // dW slabs
+  long part = (long)kDwCap * (np_max * 64 + np_max);                  // dW slabs
   part = std::max(part, (long)q.dec_s * B * Q::NOP);                    // decoder split-K
   // decoder weight gradient: windows split over up to 4 parts of >= 8 chunks
   q.dec_dws = (int)std::max<long>(1, std::min<long>(4, (B + kDwRows - 1) / kDwRows / 8));
