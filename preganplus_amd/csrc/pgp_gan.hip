@@ -335,7 +335,11 @@ __global__ __launch_bounds__(kGanWaves * 64) void gan_kernel(FwdArgs a) {
     // container interval late, so its tanh / argmax VALU phase meets the
     // first half's MFMAs instead of every wave reaching it together
     // (one container per chunk only: at H <= 32 it cost the fleet 0.3 %)
+    #ifdef PGP_XSTG
+    if (GG::CPC <= 2 && wv >= kGanWaves / 2 && (PGP_XSTG_ALL || c % GG::CPC == 0)) __builtin_amdgcn_s_sleep(PGP_XSTG);
+#else
     if (GG::CPC == 1 && wv >= kGanWaves / 2) __builtin_amdgcn_s_sleep(kGanSleep);
+#endif
     gen2(c, cw, ns, racc);
     finish(c, cw, ns, racc, sv);
     if ((c + 1) % GG::CPC == 0) advance();
