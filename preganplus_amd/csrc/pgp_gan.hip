@@ -27,8 +27,10 @@ namespace {
 // at 0; Disc1's new-schedule half skips the MFMAs whose whole k slice is
 // padding rows (at H = 50 the last tile's e = 2, 3 steps: 8 of 128 MFMAs per
 // container); a Gen2 last row tile with at most kTailMax real rows runs on
-// VALU; with one container per chunk the second half of the waves starts each
-// container kGanSleep x 64 cycles late.
+// VALU; with one or two containers per chunk the second half of the waves
+// starts each chunk kGanSleep x CPC x 64 cycles late (A/B at H = 50, two
+// containers per chunk: 24 / 48 / 96 / 127 units 0.788 / 0.788 / 0.793 /
+// 0.798 ms against 0.800 without; profiles/r03/c2ab/k3_stagger2.txt).
 constexpr int kGanWaves = 16;
 constexpr int kQC = 8;
 constexpr int kChunkG = 65;
@@ -331,15 +333,11 @@ __global__ __launch_bounds__(kGanWaves * 64) void gan_kernel(FwdArgs a) {
     const float* cw = cur + (c % GG::CPC) * G::GC_G * G::FQ;  // this container's groups
     float svn[G::MT_N][4];
     load_row(c + 1, svn);
-    // stagger: the second half of the waves (two per SIMD) starts each
-    // container interval late, so its tanh / argmax VALU phase meets the
-    // first half's MFMAs instead of every wave reaching it together
-    // (one container per chunk only: at H <= 32 it cost the fleet 0.3 %)
-    #ifdef PGP_XSTG
-    if (GG::CPC <= 2 && wv >= kGanWaves / 2 && (PGP_XSTG_ALL || c % GG::CPC == 0)) __builtin_amdgcn_s_sleep(PGP_XSTG);
-#else
-    if (GG::CPC == 1 && wv >= kGanWaves / 2) __builtin_amdgcn_s_sleep(kGanSleep);
-#endif
+    // stagger: the second half of the waves (two per SIMD) starts each chunk
+    // interval late, so its tanh / argmax VALU phases meet the first half's
+    // MFMAs instead of every wave reaching them together (at most two
+    // containers per chunk: with 4-8, at H <= 32, it cost the fleet 0.3 %)
+    if (GG::CPC <= 2 && c % GG::CPC == 0 && wv >= kGanWaves / 2) __builtin_amdgcn_s_sleep(kGanSleep * GG::CPC);
     gen2(c, cw, ns, racc);
     finish(c, cw, ns, racc, sv);
     if ((c + 1) % GG::CPC == 0) advance();
