@@ -12,8 +12,8 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 PHASES = {
-    "fwd l0": ["prologue", "load", "te gemm+store", "qkv gemm", "attention", "o gemm+res", "ln1+store",
-               "f1 gemm+relu", "f2 gemm+res", "ln2+store", "tail"],
+    "fwd l0": ["prologue", "load", "te gemm", "qk gemm (+x0 store)", "probs + v gemm + P.v", "o gemm+res", "ln1",
+               "f1 gemm+relu (+x-hat store)", "f2 gemm+res (+prefetch)", "ln2+store", "tail"],
     "fwd l1": None,
     "bwd ffn": ["prologue", "load", "f1 gemm", "f2 gemm", "ln2+ln2 bwd", "dW2 contraction", "dW2 lds add",
                 "dF gemm+mask", "dW1 contraction", "dW1 lds add", "dy1 gemm", "ln1 bwd+store", "tail", "epilogue"],
