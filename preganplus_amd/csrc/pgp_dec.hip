@@ -96,15 +96,9 @@ __global__ __launch_bounds__(kDecWaves * 64) void dec_fwd2_kernel(int B, int S, 
   }
 }
 
-// Backward into the encoder output: workgroup (x: kDxNB b-tiles per wave, y:
-// token) computes dX2[b][tok][0..DP) = sum_n dpre[b][n] WpT[tok][c][n]; A =
-// WpT[tok] (DP x NOP, 52 KiB in LDS), B = the wave's dpre rows (registers):
-// every A fragment read from LDS feeds kDxNB MFMAs (one per b-tile), and one
-// LDS copy of WpT[tok] serves 8 kDxNB b-tiles.  Pad columns come out 0.
-#ifndef PGP_XDXNB
-#define PGP_XDXNB 2
-#endif
-constexpr int kDxNB = PGP_XDXNB;
+// Backward into the encoder output: workgroup (x: 8 b-tiles, y: token) computes
+// dX2[b][tok][0..DP) = sum_n dpre[b][n] WpT[tok][c][n]; A = WpT[tok] (DP x NOP,
+// 52 KiB in LDS), B = the wave's dpre rows (registers).  Pad columns come out 0.
 template <int H>
 __global__ __launch_bounds__(kDecWaves * 64) void dec_dx_kernel(int B, const float* __restrict__ dpre,
                                                                 const float* __restrict__ WpT,
@@ -114,30 +108,25 @@ __global__ __launch_bounds__(kDecWaves * 64) void dec_dx_kernel(int B, const flo
   extern __shared__ __attribute__((aligned(16))) float lds[];  // [PCS][256]
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, g = lane >> 4, j = lane & 15;
   const int tok = blockIdx.y;
-  const long bt0 = ((long)blockIdx.x * kDecWaves + wv) * kDxNB;  // the wave's first b-tile
+  const long b = ((long)blockIdx.x * kDecWaves + wv) * 16 + j;
+  const bool okb = b < B;
   for (int pc = wv; pc < PCS; pc += kDecWaves) {
     const int ct = pc / QG, q = pc - ct * QG;
     dma_piece(WpT + ((long)tok * Q::DP + 16 * ct + j) * Q::NOP + 16 * q + 4 * g, lds + pc * 256);
   }
-  f32x4 x[kDxNB][QG];
+  f32x4 x[QG];
+  const float* dr = dpre + (okb ? b : 0) * Q::NOP + 4 * g;
 #pragma unroll
-  for (int i = 0; i < kDxNB; ++i) {
-    const long b = (bt0 + i) * 16 + j;
-    const float* dr = dpre + (b < B ? b : 0) * Q::NOP + 4 * g;
-#pragma unroll
-    for (int q = 0; q < QG; ++q) {
-      const f32x4 v = ld4(dr + 16 * q);
-      x[i][q] = b < B ? v : zero4();
-    }
+  for (int q = 0; q < QG; ++q) {
+    const f32x4 v = ld4(dr + 16 * q);
+    x[q] = okb ? v : zero4();
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (bt0 * 16 >= B) return;  // every b-tile of the wave past the batch (after the barrier)
-  f32x4 acc[kDxNB][CT];
+  if ((long)((long)blockIdx.x * kDecWaves + wv) * 16 >= B) return;  // a b-tile past the batch (after the barrier)
+  f32x4 acc[CT];
 #pragma unroll
-  for (int i = 0; i < kDxNB; ++i)
-#pragma unroll
-    for (int ct = 0; ct < CT; ++ct) acc[i][ct] = zero4();
+  for (int ct = 0; ct < CT; ++ct) acc[ct] = zero4();
   const float* L = lds + lane * 4;
 #pragma unroll
   for (int ct = 0; ct < CT; ++ct)
@@ -145,17 +134,11 @@ __global__ __launch_bounds__(kDecWaves * 64) void dec_dx_kernel(int B, const flo
     for (int q = 0; q < QG; ++q) {
       const f32x4 a = ld4(L + (ct * QG + q) * 256);
 #pragma unroll
-      for (int e = 0; e < 4; ++e)
-#pragma unroll
-        for (int i = 0; i < kDxNB; ++i) acc[i][ct] = mfma(a[e], x[i][q][e], acc[i][ct]);
+      for (int e = 0; e < 4; ++e) acc[ct] = mfma(a[e], x[q][e], acc[ct]);
     }
+  if (okb) {
 #pragma unroll
-  for (int i = 0; i < kDxNB; ++i) {
-    const long b = (bt0 + i) * 16 + j;
-    if (b < B) {
-#pragma unroll
-      for (int ct = 0; ct < CT; ++ct) st4(dX + (b * Q::T + tok) * Q::DP + 16 * ct + 4 * g, acc[i][ct]);
-    }
+    for (int ct = 0; ct < CT; ++ct) st4(dX + ((long)b * Q::T + tok) * Q::DP + 16 * ct + 4 * g, acc[ct]);
   }
 }
 
@@ -188,7 +171,7 @@ hipError_t dec_dx_h(int B, const float* dpre, const float* WpT, float* dX, hipSt
     return true;
   }();
   (void)attr;
-  const int bg = (B + 16 * kDecWaves * kDxNB - 1) / (16 * kDecWaves * kDxNB);
+  const int bg = (B + 16 * kDecWaves - 1) / (16 * kDecWaves);
   dec_dx_kernel<H><<<dim3(bg, Q::T), kDecWaves * 64, lds, st>>>(B, dpre, WpT, dX);
   return hipGetLastError();
 }
