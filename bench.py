@@ -271,6 +271,13 @@ def _dist_setup():
     if world != _GPUS_REQUESTED:
         raise SystemExit(f"bench.py: world size {world} != --gpus {_GPUS_REQUESTED}")
     dev_env = os.environ.get("PGP_DEVICE", os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and "PGP_DEVICE" in os.environ:
+        # a rehearsal with every rank on ONE device: one stream per rank (the
+        # GAN / tuning overlap and the library's side stream multiply the
+        # processes' hardware queues on that device and time-slice them; the
+        # driver's runs, one GPU per rank, keep both)
+        os.environ["PGP_BENCH_ONE_STREAM"] = "1"
+        os.environ["PGP_TUNE_SIDE_STREAM"] = "0"
     if dev_env == "cpu":
         device = torch.device("cpu")
     else:
@@ -425,7 +432,7 @@ def bench_tune(args):
     # tuning step; the step ends when both have (results are unchanged:
     # tests/test_gpu_dist.py and test_gpu_tunedp.py run them in either order)
     main = torch.cuda.current_stream(device)
-    side = torch.cuda.Stream(device)
+    side = main if os.environ.get("PGP_BENCH_ONE_STREAM") == "1" else torch.cuda.Stream(device)
 
     def step(e=None, se=None):
         rec = (lambda k: e[k].record(main)) if e is not None else (lambda k: None)
@@ -810,7 +817,7 @@ def bench_loop(args):
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(len(names) + 1)]
     acc = np.zeros(len(names))
     main = torch.cuda.current_stream(device)
-    side = torch.cuda.Stream(device)
+    side = main if os.environ.get("PGP_BENCH_ONE_STREAM") == "1" else torch.cuda.Stream(device)
 
     def interval(timed=False):
         if timed:

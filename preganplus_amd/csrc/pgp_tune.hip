@@ -21,6 +21,7 @@
 // (dlutils.py:326-329); the result is the same function, rounded once in fp32.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <mutex>
 
 #include <algorithm>
@@ -908,6 +909,11 @@ struct Fork {
   hipStream_t main, side;
   SideStream* ss = nullptr;
   explicit Fork(hipStream_t st) : main(st), side(st) {
+    static const bool off = [] {
+      const char* v = getenv("PGP_TUNE_SIDE_STREAM");
+      return v && v[0] == '0';
+    }();
+    if (off) return;  // PGP_TUNE_SIDE_STREAM=0: everything on the caller's stream
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return;
     ss = side_stream();
