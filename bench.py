@@ -423,7 +423,7 @@ def bench_tune(args):
     emb_buf = torch.empty((E, H, 2), dtype=torch.float32, device=device)
     names = ("dataset", "detect", "train_gan", "tune_model")
     subs = TR.DPTuner.SUBSTAGES
-    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(len(names) + 1)] for _ in range(max(args.steps, 1))]
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(len(names) + 2)] for _ in range(max(args.steps, 1))]
     sev = [[torch.cuda.Event(enable_timing=True) for _ in range(len(subs) + 1)] for _ in range(max(args.steps, 1))]
     # train_gan and tune_model share no data (run_model calls them back to
     # back, PreGANPlus.py:133-134: the GAN step reads the embedding and writes
@@ -434,18 +434,30 @@ def bench_tune(args):
     main = torch.cuda.current_stream(device)
     side = main if os.environ.get("PGP_BENCH_ONE_STREAM") == "1" else torch.cuda.Stream(device)
 
+    # detect reads the step-start weights and feeds only the GAN step, so it
+    # runs on the second stream too, with a workspace of its own; the tuning
+    # step's weight update waits for it (before_update)
+    det_ctx = tr.forward_context(E) if side is not main else None
+    det_done = torch.cuda.Event()
+
     def step(e=None, se=None):
         rec = (lambda k: e[k].record(main)) if e is not None else (lambda k: None)
         rec(0)
         wins, y, cls, inf = TR.tune_dataset(tr, series, tmax, out=bufs)
         rec(1)
-        logits, protos = tr.tune_forward(inf)
-        emb = embedding(logits, protos, out=emb_buf)   # PreGANPlus.py:129
-        rec(2)
         side.wait_stream(main)
-        # the tuning step (the longer chain) is issued first: the host's ~40 GAN
-        # launches would otherwise leave the device's main stream idle meanwhile
-        tun.step(wins, y, cls, mark=(lambda k: se[k].record(main)) if se is not None else None)
+        with torch.cuda.stream(side):
+            if e is not None:
+                e[5].record(side)
+            logits, protos = tr.tune_forward(inf, ctx=det_ctx)
+            emb = embedding(logits, protos, out=emb_buf)   # PreGANPlus.py:129
+            det_done.record(side)
+            if e is not None:
+                e[2].record(side)
+        # the tuning step (the longer chain) is issued before the GAN step: the
+        # host's ~40 GAN launches would otherwise leave the main stream idle
+        tun.step(wins, y, cls, mark=(lambda k: se[k].record(main)) if se is not None else None,
+                 before_update=det_done)
         with torch.cuda.stream(side):
             TR.train_gan_batched(tr, sim, envs, emb, s, out=sim_out, target=gan_target, all_reduce=True)
             if e is not None:
@@ -459,7 +471,9 @@ def bench_tune(args):
     el = _timed(world, device, lambda: step(*next(it)), args.steps)
     # train_gan (side stream, from the embedding to its last kernel) and
     # tune_model (main stream, its first sub-stage mark to its last) overlap
-    stage = np.array([[e[0].elapsed_time(e[1]), e[1].elapsed_time(e[2]), e[2].elapsed_time(e[3]),
+    # detect (second stream: its start e[5] to the embedding e[2]), train_gan
+    # (second stream, after detect) and tune_model (main stream) overlap
+    stage = np.array([[e[0].elapsed_time(e[1]), e[5].elapsed_time(e[2]), e[2].elapsed_time(e[3]),
                        s_[0].elapsed_time(s_[len(subs)])] for e, s_ in zip(ev[:args.steps], sev[:args.steps])]).mean(0)
     sub = np.array([[e[k].elapsed_time(e[k + 1]) for k in range(len(subs))] for e in sev[:args.steps]]).mean(0)
     # roofline of the dominant kernels: the six fused encoder launches of the
@@ -507,7 +521,8 @@ def bench_tune(args):
                                    f"= {B} tuning windows per GPU", "hosts": H, "environments_per_gpu": E,
                        "windows_per_gpu": B, "parallelism": f"dp{world} + RCCL all-reduce (grads, state)"},
             "stage_ms": {n: float(stage[k]) for k, n in enumerate(names)},
-            "streams": "train_gan on a second stream, concurrent with tune_model (no shared data)",
+            "streams": "detect + train_gan on a second stream, concurrent with tune_model (no shared data; the "
+                       "tuning step's weight update waits for detect)",
             "tune_model_ms": {n: float(sub[k]) for k, n in enumerate(subs)},
             "grad_all_reduce_ms": float(sub[subs.index("all_reduce")]),
             "roofline": roof,

@@ -17,6 +17,8 @@ from __future__ import annotations
 import ctypes
 import math
 
+import types
+
 import numpy as np
 import torch
 
@@ -169,18 +171,37 @@ class Trainer:
     def zero_grad(self, section: str):
         self.G[self.sec_off[section]:self.sec_end[section]].zero_()
 
-    def tune_forward(self, windows: torch.Tensor, latent: torch.Tensor | None = None):
+    def forward_context(self, B):
+        """A workspace and outputs of their own for a forward that runs beside
+        the tuning step (the C3 detect on a second stream): tune_forward(...,
+        ctx=) leaves the tuning step's activations alone."""
+        L, dev, f32 = self._L, self.device, torch.float32
+        return types.SimpleNamespace(
+            cap=B, ws=torch.zeros((L.pgp_tune_workspace_len(self.H, B),), dtype=f32, device=dev),
+            logits=torch.zeros((B, self.H, 2), dtype=f32, device=dev),
+            protos=torch.zeros((B, self.H, 2), dtype=f32, device=dev))
+
+    def tune_forward(self, windows: torch.Tensor, latent: torch.Tensor | None = None, ctx=None):
         """Transformer forward of a batch of windows [B,3,3H], activations kept
-        in the workspace for tune_backward; optional latent tap [B,3H^2]."""
+        in the workspace for tune_backward; optional latent tap [B,3H^2].  With
+        ``ctx`` (forward_context) the workspace and outputs are the context's
+        (no tune_backward may follow from them)."""
         B = windows.shape[0]
-        self._ensure(B)
+        if ctx is None:
+            self._ensure(B)
+            ws, lg, pr = self.ws, self.logits, self.protos
+        else:
+            if B > ctx.cap:
+                raise ValueError(f"batch {B} > forward context capacity {ctx.cap}")
+            ws, lg, pr = ctx.ws, ctx.logits, ctx.protos
         windows = windows.to(self.device, torch.float32).contiguous()
         _native.check(self._L.pgp_tune_forward(
-            self.H, B, windows.data_ptr(), self.P.data_ptr(), self.ws.data_ptr(),
+            self.H, B, windows.data_ptr(), self.P.data_ptr(), ws.data_ptr(),
             None if latent is None else latent.data_ptr(),
-            self.logits.data_ptr(), self.protos.data_ptr(), self._stream()), "pgp_tune_forward")
-        self._fwd_batch = B
-        return self.logits[:B], self.protos[:B]
+            lg.data_ptr(), pr.data_ptr(), self._stream()), "pgp_tune_forward")
+        if ctx is None:
+            self._fwd_batch = B
+        return lg[:B], pr[:B]
 
     def tune_backward(self, B, y, mult, tgt):
         """y [B,H] int, mult [B,H], tgt [B,H,2] (host arrays or tensors); B must
@@ -628,11 +649,14 @@ class DPTuner:
 
     SUBSTAGES = ("forward", "targets", "backward", "all_reduce", "apply_adamw")
 
-    def step(self, wins: torch.Tensor, y: torch.Tensor, cls: torch.Tensor, mark=None):
+    def step(self, wins: torch.Tensor, y: torch.Tensor, cls: torch.Tensor, mark=None, before_update=None):
         """wins [B,3,3H] fp32, y / cls [B,H] int32, all on the device.
         Returns the per-window (aloss, tloss) [B,2] fp64 device view.
         ``mark(k)``, if given, is called before sub-stage k of SUBSTAGES and
-        once more at the end (the bench records HIP events there)."""
+        once more at the end (the bench records HIP events there).
+        ``before_update``, if given, is an event the step's stream waits for
+        before the state update and AdamW (work on another stream that still
+        reads the step-start weights)."""
         mark = mark or (lambda k: None)
         import torch.distributed as dist
         tr, L = self.tr, self.tr._L
@@ -659,6 +683,8 @@ class DPTuner:
         if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
             dist.all_reduce(self.inc, group=self.group)
         mark(4)
+        if before_update is not None:
+            torch.cuda.current_stream(tr.device).wait_event(before_update)
         row = self.table[i]
         _native.check(L.pgp_tune_state_apply(
             self.K, self.state.data_ptr(), self.inc.data_ptr(), PROTO_FACTOR_DECAY, len(self.cond), self.cond_rows,
