@@ -656,7 +656,9 @@ class DPTuner:
         once more at the end (the bench records HIP events there).
         ``before_update``, if given, is an event the step's stream waits for
         before the state update and AdamW (work on another stream that still
-        reads the step-start weights)."""
+        reads the step-start weights), or a callable returning one, called at
+        that point of the host's issue order (so the work it issues elsewhere
+        is queued after this step's forward and backward)."""
         mark = mark or (lambda k: None)
         import torch.distributed as dist
         tr, L = self.tr, self.tr._L
@@ -684,7 +686,8 @@ class DPTuner:
             dist.all_reduce(self.inc, group=self.group)
         mark(4)
         if before_update is not None:
-            torch.cuda.current_stream(tr.device).wait_event(before_update)
+            ev = before_update() if callable(before_update) else before_update
+            torch.cuda.current_stream(tr.device).wait_event(ev)
         row = self.table[i]
         _native.check(L.pgp_tune_state_apply(
             self.K, self.state.data_ptr(), self.inc.data_ptr(), PROTO_FACTOR_DECAY, len(self.cond), self.cond_rows,
