@@ -298,9 +298,16 @@ def _dist_setup():
     return world, rank, device
 
 
+_HOST_ISSUE_S = None
+
+
 def emit(res):
-    """Rank 0's one JSON line, with the rendezvous count."""
+    """Rank 0's one JSON line, with the rendezvous count (and, for the timed
+    loop, the host's own time to issue the steps: a line whose host_issue_ms
+    approaches ms_per_step is bound by the launches, not the device)."""
     res["ranks_seen"] = _RANKS_SEEN
+    if _HOST_ISSUE_S is not None and res.get("steps"):
+        res["host_issue_ms_per_step"] = _HOST_ISSUE_S / res["steps"] * 1e3
     print(json.dumps(res), flush=True)
 
 
@@ -321,6 +328,8 @@ def _timed(world, device, fn, steps):
     t0 = time.perf_counter()
     for _ in range(steps):
         fn()
+    global _HOST_ISSUE_S
+    _HOST_ISSUE_S = time.perf_counter() - t0   # host time to issue the K steps (no sync inside)
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
