@@ -225,6 +225,13 @@ int pgp_tune_forward(int n_hosts, int batch, const float* windows, const float* 
  * into G (the caller zeroes G before the step). */
 int pgp_tune_backward(int n_hosts, int batch, const float* P, float* G, float* workspace, const float* logits,
                       const float* protos, const int* y, const float* mult, const float* tgt, void* stream);
+/* Streams: both calls may run part of their work (the decoder weight packing;
+ * the decoders' and in_proj's weight gradients) on a library-owned,
+ * low-priority stream of the current device, forked from `stream` by an event
+ * and joined back into it before the call's last launch, so every result is
+ * ordered on `stream` as if all of it ran there.  While `stream` is being
+ * captured into a graph, or with PGP_TUNE_SIDE_STREAM=0 in the environment,
+ * everything stays on `stream`. */
 /* Profiling: with pgp_tune_timing(1), pgp_tune_forward / pgp_tune_backward
  * record HIP events on their stream around each fused encoder launch
  * (pgp_tunef.hip); pgp_tune_fused_ms(ms6) synchronises on them and returns the
