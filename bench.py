@@ -577,7 +577,7 @@ def tune_cpu_baseline(w, series, tmax, sched, envs, H, per_repeat=2, repeats=5):
             n += 1
         if rep:
             rates.append(per_repeat * 10 / (time.perf_counter() - t0))
-    return {"value": float(np.median(rates)), "unit": "windows/s", "cores": threads, "kind": "port",
+    return {"value": float(np.median(rates)), "unit": "windows/s", "cores": threads, "kind": "port", "threads_note": CB.THREADS_NOTE,
             "sample": f"{per_repeat} environments x 10 tuning windows per repeat, median of {repeats}: detect, "
                       f"train_gan (runSimulation restatement), sequential batch-1 backprop; fp64 torch-CPU "
                       f"(the reference's algorithm, H={H})",
@@ -587,8 +587,9 @@ def tune_cpu_baseline(w, series, tmax, sched, envs, H, per_repeat=2, repeats=5):
 def fpe_cpu_baseline(weights, budget_s=12.0, max_threads=16):
     """numpy fp64 FPE oracle on the host cores, bounded sample (C4)."""
     from threadpoolctl import threadpool_limits
+    from oracle import cpu_baseline as CB  # CPU baseline leg only
     from oracle import pregan_oracle as O  # CPU baseline leg only
-    threads = min(max_threads, os.cpu_count() or 1)
+    threads = min(max_threads, CB.host_threads())
     rng = np.random.Generator(np.random.PCG64(98))
     nb, H = 256, 16
     x = rng.uniform(0, 0.6, size=(nb, 3, 3 * H))
@@ -603,7 +604,7 @@ def fpe_cpu_baseline(weights, budget_s=12.0, max_threads=16):
             O.forward_fpe(weights, x, h0, s)
             done += nb
     dt = time.perf_counter() - t0
-    return {"value": done * H / dt, "unit": "host-windows/s", "cores": threads, "kind": "port",
+    return {"value": done * H / dt, "unit": "host-windows/s", "cores": threads, "kind": "port", "threads_note": CB.THREADS_NOTE,
             "sample": f"{done} windows (H=16, batches of {nb}), numpy fp64 FPE oracle, {dt:.1f}s"}
 
 
@@ -724,7 +725,7 @@ def bench_gobi(args):
                 GO.opt(sd, z["inits"][n % z["inits"].shape[0]])
                 n += 1
             dt = time.perf_counter() - t0
-            res["cpu_baseline"] = {"value": n / dt, "unit": "schedules/s", "cores": 1, "kind": "port",
+            res["cpu_baseline"] = {"value": n / dt, "unit": "schedules/s", "cores": 1, "kind": "port", "threads_note": "sequential per-environment restatement (the reference's one-call-at-a-time loop over small tensors, below torch's intra-op parallel grain): 1 thread",
                                    "sample": f"{n} opt() runs of the torch-CPU restatement (bit-identical to the "
                                              f"reference's), 1 thread, {dt:.1f}s"}
         emit(res)
@@ -780,7 +781,7 @@ def bench_sim(args):
                 SO.simulate_batch(envs_h[i:i + 1], new_h[i:i + 1], orig_h[i:i + 1], H)
                 n += 1
             dt = time.perf_counter() - t0
-            res["cpu_baseline"] = {"value": n / dt, "unit": "environments/s", "cores": 1, "kind": "port",
+            res["cpu_baseline"] = {"value": n / dt, "unit": "environments/s", "cores": 1, "kind": "port", "threads_note": "sequential per-environment restatement (the reference's one-call-at-a-time loop over small tensors, below torch's intra-op parallel grain): 1 thread",
                                    "sample": f"{n} environments through the Python restatement (bit-identical to "
                                              f"the reference's runSimulation), 1 thread, {dt:.1f}s"}
         emit(res)
@@ -936,7 +937,7 @@ def loop_cpu_baseline(w, extra, inits, wins, envs, y, budget_s):
             TO.disc_t(P.dw, s[None], ns)
         n += 1
     dt = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "cell-intervals/s", "cores": 1, "kind": "port",
+    return {"value": n / dt, "unit": "cell-intervals/s", "cores": 1, "kind": "port", "threads_note": "sequential per-environment restatement (the reference's one-call-at-a-time loop over small tensors, below torch's intra-op parallel grain): 1 thread",
             "sample": f"{n} cell-intervals through the CPU restatements (GOBI opt, encode/classify, train_gan with "
                       f"runSimulation labels, one tuning window, Gen/Disc), 1 thread, {dt:.1f}s"}
 
@@ -1088,7 +1089,7 @@ def bench_plugin(args):
                 po.run_model(_plugin_env(z, step, tr_time), [tuple(x) for x in z[f"s{step}/decision_in"]])
                 n += 1
             dt = time.perf_counter() - t0
-            res["cpu_baseline"] = {"value": n / dt, "unit": "calls/s", "cores": 1, "kind": "port",
+            res["cpu_baseline"] = {"value": n / dt, "unit": "calls/s", "cores": 1, "kind": "port", "threads_note": "sequential per-environment restatement (the reference's one-call-at-a-time loop over small tensors, below torch's intra-op parallel grain): 1 thread",
                                    "sample": f"{n} run_model calls of the torch-fp64 plugin restatement "
                                              f"(pinned to the reference's outputs), 1 thread, {dt:.1f}s"}
         emit(res)

@@ -41,6 +41,10 @@ def cpu_model() -> str:
     return "unknown"
 
 
+THREADS_NOTE = ("BASELINE.md §4 asks for os.cpu_count() threads; that counts the whole host, while this process's "
+                "CPU share is OMP_NUM_THREADS (16 on the GPU box), so the baseline runs on that share")
+
+
 def host_threads() -> int:
     n = os.cpu_count() or 1
     env = os.environ.get("OMP_NUM_THREADS")
@@ -134,4 +138,5 @@ def measure(weights, windows, sched, per_window_n=32, batch_n=1024, repeats=5):
                   "batched_fp32": {"value": bf, "windows_per_repeat": batch_n,
                                    "repeats": [float(v) for v in bt]}},
         "cpu_model": cpu_model(), "host_cpus": os.cpu_count(), "threads": threads,
+        "threads_note": THREADS_NOTE,
     }
