@@ -21,6 +21,7 @@
 // (dlutils.py:326-329); the result is the same function, rounded once in fp32.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdlib>
 #include <mutex>
 
@@ -887,7 +888,7 @@ TfTiming g_tft;
 struct SideStream {
   hipStream_t s = nullptr;
   hipEvent_t ev[8] = {};
-  unsigned next = 0;
+  std::atomic<unsigned> next{0};  // event rotation (callers on several host threads)
   bool ok = false;
 };
 SideStream* side_stream() {
@@ -922,7 +923,7 @@ struct Fork {
   // `to` waits for everything issued on `from` so far
   hipError_t order(hipStream_t from, hipStream_t to) {
     if (!ss || from == to) return hipSuccess;
-    hipEvent_t e = ss->ev[ss->next++ % 8];
+    hipEvent_t e = ss->ev[ss->next.fetch_add(1, std::memory_order_relaxed) % 8];
     hipError_t r = hipEventRecord(e, from);
     return r != hipSuccess ? r : hipStreamWaitEvent(to, e, 0);
   }
