@@ -455,22 +455,28 @@ def bench_tune(args):
         wins, y, cls, inf = TR.tune_dataset(tr, series, tmax, out=bufs)
         rec(1)
         side.wait_stream(main)
-        with torch.cuda.stream(side):
-            if e is not None:
-                e[5].record(side)
-            logits, protos = tr.tune_forward(inf, ctx=det_ctx)
-            emb = embedding(logits, protos, out=emb_buf)   # PreGANPlus.py:129
-            det_done.record(side)
-            if e is not None:
-                e[2].record(side)
+
+        def detect():
+            with torch.cuda.stream(side):
+                if e is not None:
+                    e[5].record(side)
+                logits, protos = tr.tune_forward(inf, ctx=det_ctx)
+                embedding(logits, protos, out=emb_buf)   # PreGANPlus.py:129
+                det_done.record(side)
+                if e is not None:
+                    e[2].record(side)
         # the tuning step (the longer chain) is issued before the GAN step: the
-        # host's ~40 GAN launches would otherwise leave the main stream idle
+        # host's ~40 GAN launches would otherwise leave the main stream idle;
+        # detect's launches are issued once the tuning forward's are queued
+        def gan():
+            with torch.cuda.stream(side):
+                TR.train_gan_batched(tr, sim, envs, emb_buf, s, out=sim_out, target=gan_target, all_reduce=True)
+                if e is not None:
+                    e[3].record(side)
+
         tun.step(wins, y, cls, mark=(lambda k: se[k].record(main)) if se is not None else None,
-                 before_update=det_done)
-        with torch.cuda.stream(side):
-            TR.train_gan_batched(tr, sim, envs, emb, s, out=sim_out, target=gan_target, all_reduce=True)
-            if e is not None:
-                e[3].record(side)
+                 before_update=det_done, after_forward=detect)
+        gan()   # (issued with detect, before the backward: no faster, profiles/r03/s3/)
         main.wait_stream(side)
         rec(4)
 

@@ -52,12 +52,23 @@ __global__ __launch_bounds__(kDecWaves * 64) void dec_fwd2_kernel(int B, int S, 
                 lds + (buf * PCS + pc) * 256);
     }
   };
+  // a lane past the batch reads window 0 (clamped address) into its own
+  // column, which is not stored; no select on the loaded value, so the next
+  // token's loads are not waited for before this token's MFMAs
   const float* xr = X2 + (okb ? b : 0) * Q::T * Q::DP + 4 * g;
+  // (the last k-block reads only its ELAST live features: a dead half of a
+  // float4 would let the compiler reuse its registers right after the load,
+  // which makes it wait for the prefetch before this token's MFMAs)
   auto xload = [&](int tok, f32x4 (&x)[KB]) {
 #pragma unroll
     for (int kb = 0; kb < KB; ++kb) {
-      const f32x4 v = ld4(xr + (long)tok * Q::DP + 16 * kb);
-      x[kb] = okb ? v : zero4();
+      const float* p = xr + (long)tok * Q::DP + 16 * kb;
+      if (kb == KB - 1 && ELAST <= 2) {
+        const float2 v = *reinterpret_cast<const float2*>(p);
+        x[kb] = f32x4{v.x, v.y, 0.f, 0.f};
+      } else {
+        x[kb] = ld4(p);
+      }
     }
   };
   f32x4 acc[NT];

@@ -110,6 +110,7 @@ PGP_DEV float lrelu(float x) { return x > 0.f ? x : 0.01f * x; }
 // fragment read hit disjoint banks.
 // ============================================================================
 constexpr int lds_stride(int n) { return n + ((16 - n % 64) % 64 + 64) % 64; }
+static __device__ __attribute__((aligned(16))) float dw_zero4[4];  // zero, read by masked-off lanes
 constexpr int kDwRows = 32;  // rows per LDS-staged chunk of the weight-gradient contractions
 
 template <int NP, int KP, int NTW>
@@ -118,21 +119,28 @@ PGP_DEV void dw_accumulate(long r0, long r1, const float* __restrict__ Y, long l
                            f32x4 (&acc)[NTW][KP / 16], float (&pb)[NTW], int ny = NP, int nx = KP) {
   constexpr int NT = NP / 16, KT = KP / 16, YS = lds_stride(NP), XS = lds_stride(KP);
   constexpr int NY = (kDwRows * NP / 4 + 255) / 256, NX = (kDwRows * KP / 4 + 255) / 256;  // float4 per thread
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, g = lane >> 4, i = lane & 15;
+  const int lane = threadIdx.x & 63, g = lane >> 4, i = lane & 15;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int tq[NTW];  // this wave's n-tiles (clamped; see below)
+#pragma unroll
+  for (int q = 0; q < NTW; ++q) tq[q] = min(tbase + wv + tstride * q, NT - 1);
   f32x4 ry[NY], rx[NX];
-  // software pipeline: chunk c+1 is loaded into registers while chunk c is computed from LDS
+  // software pipeline: chunk c+1 is loaded into registers while chunk c is
+  // computed from LDS.  Rows past the range read a zero float4 (the ADDRESS
+  // is selected: a select on the loaded value would make the compiler wait for
+  // the prefetch at once, before the chunk's MFMAs)
   auto fetch = [&](long c0) {
 #pragma unroll
     for (int k = 0; k < NY; ++k) {
       const int idx = threadIdx.x + 256 * k, row = idx / (NP / 4), c4 = idx - row * (NP / 4);
       const long m = c0 + row;
-      ry[k] = (idx < kDwRows * NP / 4 && m < r1 && 4 * c4 < ny) ? ld4(Y + m * ldy + 4 * c4) : zero4();
+      ry[k] = ld4((idx < kDwRows * NP / 4 && m < r1 && 4 * c4 < ny) ? Y + m * ldy + 4 * c4 : dw_zero4);
     }
 #pragma unroll
     for (int k = 0; k < NX; ++k) {
       const int idx = threadIdx.x + 256 * k, row = idx / (KP / 4), c4 = idx - row * (KP / 4);
       const long m = c0 + row;
-      rx[k] = (idx < kDwRows * KP / 4 && m < r1 && 4 * c4 < nx) ? ld4(X + m * ldx + 4 * c4) : zero4();
+      rx[k] = ld4((idx < kDwRows * KP / 4 && m < r1 && 4 * c4 < nx) ? X + m * ldx + 4 * c4 : dw_zero4);
     }
   };
   if (r0 < r1) fetch(r0);
@@ -155,7 +163,10 @@ PGP_DEV void dw_accumulate(long r0, long r1, const float* __restrict__ Y, long l
     }
     __syncthreads();
     if (c0 + kDwRows < r1) fetch(c0 + kDwRows);
-#pragma unroll 2
+    // the chunk's 8 row groups, fully unrolled and branch-free: a wave whose
+    // tile q is past NT computes tile NT - 1 again and never stores it, so the
+    // compiler can issue the next group's LDS reads under this group's MFMAs
+#pragma unroll
     for (int s = 0; s < kDwRows / 4; ++s) {
       const int row = 4 * s + g;
       float bv[KT];
@@ -163,13 +174,10 @@ PGP_DEV void dw_accumulate(long r0, long r1, const float* __restrict__ Y, long l
       for (int u = 0; u < KT; ++u) bv[u] = xs[row * XS + 16 * u + i];
 #pragma unroll
       for (int q = 0; q < NTW; ++q) {
-        const int t = tbase + wv + tstride * q;
-        if (t < NT) {
-          const float av = ys[row * YS + 16 * t + i];
-          pb[q] += av;
+        const float av = ys[row * YS + 16 * tq[q] + i];
+        pb[q] += av;
 #pragma unroll
-          for (int u = 0; u < KT; ++u) acc[q][u] = mfma(av, bv[u], acc[q][u]);
-        }
+        for (int u = 0; u < KT; ++u) acc[q][u] = mfma(av, bv[u], acc[q][u]);
       }
     }
   }

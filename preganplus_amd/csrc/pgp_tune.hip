@@ -96,10 +96,12 @@ __global__ __launch_bounds__(256, 2) void linear_kernel(LinArgs a) {
   constexpr int PF = NT > 4 ? (KB < 2 ? KB : 2) : (KB < 4 ? KB : 4);
   const long rstep = (long)gridDim.x * 4;
   f32x4 xq[PF];
+  // rows past M read row 0 (the address is clamped: a select on the loaded
+  // value would wait for the prefetch at once); their columns are not stored
   {
     const long m0 = ((long)blockIdx.x * 4 + wv) * 16 + mi;
 #pragma unroll
-    for (int j = 0; j < PF; ++j) xq[j] = m0 < a.M ? ld4(a.X + m0 * a.ldx + 4 * g + 16 * j) : zero4();
+    for (int j = 0; j < PF; ++j) xq[j] = ld4(a.X + (m0 < a.M ? m0 : 0) * a.ldx + 4 * g + 16 * j);
   }
   for (long rb = (long)blockIdx.x * 4 + wv; rb < nrb; rb += rstep) {
     const long m = rb * 16 + mi;
@@ -107,12 +109,12 @@ __global__ __launch_bounds__(256, 2) void linear_kernel(LinArgs a) {
     f32x4 acc[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[t] = *reinterpret_cast<const f32x4*>(&cb[16 * t + 4 * g]);
-    const float* xr = a.X + m * a.ldx + 4 * g;
+    const float* xr = a.X + (ok ? m : 0) * a.ldx + 4 * g;
     f32x4 xn[PF];
     {
       const long mn = m + rstep * 16;
 #pragma unroll
-      for (int j = 0; j < PF; ++j) xn[j] = mn < a.M ? ld4(a.X + mn * a.ldx + 4 * g + 16 * j) : zero4();
+      for (int j = 0; j < PF; ++j) xn[j] = ld4(a.X + (mn < a.M ? mn : 0) * a.ldx + 4 * g + 16 * j);
     }
 #pragma unroll 1
     for (int j0 = 0; j0 < KB; j0 += PF) {
@@ -121,7 +123,7 @@ __global__ __launch_bounds__(256, 2) void linear_kernel(LinArgs a) {
         const int j = j0 + jj;
         if (j < KB) {
           f32x4 xv = xq[jj];
-          if (j + PF < KB) xq[jj] = ok ? ld4(xr + 16 * (j + PF)) : zero4();
+          if (j + PF < KB) xq[jj] = ld4(xr + 16 * (j + PF));
           if (a.relu_x) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) xv[r] = fmaxf(xv[r], 0.f);
@@ -370,18 +372,23 @@ __global__ __launch_bounds__(256) void gat_fwd_kernel(int B, const float* __rest
   }
 }
 
-// GAT backward from dG (grad of the GAT output): the fc gradient through the
-// aggregation is a dW GEMM over (dG, x-bar); this kernel back-propagates into
-// the edge softmax and writes, per (window, step), Xs = sum_i ds_i x_i and
+// GAT backward from dX0, the gradient of the time encoder's output: the time
+// encoder X0 = G W_TE^T + b is linear, so the gradient of the aggregated raw
+// features x-bar_j = fc^T dG_j = fc^T W_TE^T dX0_j = Mt^T dX0_j with
+// Mt = W_TE fc ([64][3], gat_mt_kernel in the forward); no dG round trip.  This
+// kernel back-propagates into the edge softmax and writes, per workgroup (its
+// 4 (window, step) graphs summed in wave order), Xs = sum_i ds_i x_i and
 // Xt = sum_j dt_j x_j (ds, dt: grads of the per-node source / destination
-// scores), from which gat_param_kernel forms the attn_fc and remaining fc grads.
+// scores), from which gat_param_kernel forms the attn_fc and fc grads.
+// Workgroup 0 also clears `fcd` (the tokens' dX0 (x) x-bar sum, reduced after
+// this kernel; gat_param_kernel maps it through W_TE into the fc gradient).
 template <int H>
 __global__ __launch_bounds__(256) void gat_bwd_kernel(int B, const float* __restrict__ wcopy,
-                                                      const float* __restrict__ P, const float* __restrict__ dG,
-                                                      const float* __restrict__ GS, float* __restrict__ GSX) {
+                                                      const float* __restrict__ P, const float* __restrict__ dX0,
+                                                      const float* __restrict__ GS, const float* __restrict__ Mt,
+                                                      float* __restrict__ GSX, float* __restrict__ fcd) {
   using Q = TuneGeo<H>;
-  using G = TGeo<H>;
-  __shared__ float ss[4][64], st[4][64], sx[4][64][3], sdx[4][64][3];
+  __shared__ float ss[4][64], st[4][64], sx[4][64][3], sdx[4][64][3], smt[64][3], sred[4][6];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const long pw = (long)blockIdx.x * 4 + wv;
   const bool okw = pw < 3L * B;
@@ -389,6 +396,8 @@ __global__ __launch_bounds__(256) void gat_bwd_kernel(int B, const float* __rest
   const int w = okw ? (int)(pw - b * 3) : 0;
   const int j = lane;
   const bool okj = okw && j < H;
+  if (blockIdx.x == 0 && threadIdx.x < 64 * 3) fcd[threadIdx.x] = 0.f;
+  if (threadIdx.x < 64 * 3) smt[threadIdx.x / 3][threadIdx.x % 3] = Mt[threadIdx.x];
   const GatFold<H> fo = gat_fold<H>(P);
   float x[3];
 #pragma unroll
@@ -400,16 +409,17 @@ __global__ __launch_bounds__(256) void gat_bwd_kernel(int B, const float* __rest
   st[wv][j] = t;
 #pragma unroll
   for (int k = 0; k < 3; ++k) sx[wv][j][k] = x[k];
-  // grad of x-bar_j = fc^T dG_j, the dG rows read coalesced: lane (rr, q) takes
-  // features 4q .. 4q+3 of rows rr, rr+4, ...; the 16 lanes of a row are summed
+  __syncthreads();
+  // grad of x-bar_j = Mt^T dX0_j, the dX0 rows read coalesced: lane (rr, q)
+  // takes features 4q .. 4q+3 of rows rr, rr+4, ...; the 16 lanes of a row are summed
   {
     const int q = lane & 15, rr = lane >> 4;
-    float fc[4][3];
+    float mt[4][3];
 #pragma unroll
     for (int e = 0; e < 4; ++e)
 #pragma unroll
-      for (int k = 0; k < 3; ++k) fc[e][k] = 4 * q + e < H ? P[G::W_FC + (4 * q + e) * 3 + k] : 0.f;
-    const float* g0 = dG + (b * Q::T + (long)w * H) * Q::DP + 4 * q;
+      for (int k = 0; k < 3; ++k) mt[e][k] = 4 * q + e < Q::DP ? smt[4 * q + e][k] : 0.f;
+    const float* g0 = dX0 + (b * Q::T + (long)w * H) * Q::DP + 4 * q;
     for (int r0 = 0; r0 < H; r0 += 4) {  // uniform trip count: the row sums are cross-lane
       const int r = r0 + rr;
       const bool okr = okw && r < H && 4 * q < Q::DP;
@@ -417,7 +427,7 @@ __global__ __launch_bounds__(256) void gat_bwd_kernel(int B, const float* __rest
       float d[3];
 #pragma unroll
       for (int k = 0; k < 3; ++k)
-        d[k] = row16_sum(fmaf(fc[0][k], v[0], fmaf(fc[1][k], v[1], fmaf(fc[2][k], v[2], fc[3][k] * v[3]))));
+        d[k] = row16_sum(fmaf(mt[0][k], v[0], fmaf(mt[1][k], v[1], fmaf(mt[2][k], v[2], mt[3][k] * v[3]))));
       if (okr && q == 0) {
 #pragma unroll
         for (int k = 0; k < 3; ++k) sdx[wv][r][k] = d[k];
@@ -459,21 +469,42 @@ __global__ __launch_bounds__(256) void gat_bwd_kernel(int B, const float* __rest
     xs[k] = wave_sum(ds * x[k]);
     xt[k] = wave_sum(dt * x[k]);
   }
-  if (okw && lane == 0) {
+  if (lane == 0) {
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-      GSX[pw * 8 + k] = xs[k];
-      GSX[pw * 8 + 3 + k] = xt[k];
+      sred[wv][k] = okw ? xs[k] : 0.f;
+      sred[wv][3 + k] = okw ? xt[k] : 0.f;
     }
+  }
+  __syncthreads();
+  if (threadIdx.x < 6) {
+    const int k = threadIdx.x;
+    GSX[(long)blockIdx.x * 8 + k] = (sred[0][k] + sred[1][k]) + (sred[2][k] + sred[3][k]);
   }
 }
 
+// Mt[c][k] = sum_f W_TE[c][f] fc[f][k] (rows past H are 0): the time
+// encoder folded into the GAT backward's first contraction (gat_bwd_kernel).
+template <int H>
+__global__ __launch_bounds__(256) void gat_mt_kernel(const float* __restrict__ P, float* __restrict__ Mt) {
+  using G = TGeo<H>;
+  const int c = threadIdx.x / 3, k = threadIdx.x - 3 * c;
+  if (c >= 64) return;
+  float m = 0.f;
+  if (c < H)
+    for (int f = 0; f < H; ++f) m = fmaf(P[G::W_TE + c * H + f], P[G::W_FC + f * 3 + k], m);
+  Mt[threadIdx.x] = m;
+}
+
 // attn_fc and the score part of the fc gradient: s_i = a_1 . fc x_i, so
-// d a_1 = fc Xs, d fc += a_1 Xs^T (and likewise a_2, Xt), summed over all
-// (window, step) in a fixed order.
+// d a_1 = fc Xs, d fc += a_1 Xs^T (and likewise a_2, Xt), summed over the
+// gat_bwd workgroups in a fixed order; plus the aggregation part of the fc
+// gradient, sum_tokens dG (x) x-bar = W_TE^T fcd.  Runs after the deferred
+// reductions (fcd is one of them).
 template <int H>
 __global__ __launch_bounds__(256) void gat_param_kernel(int n, const float* __restrict__ GSX,
-                                                        const float* __restrict__ P, float* __restrict__ Gd) {
+                                                        const float* __restrict__ P, const float* __restrict__ fcd,
+                                                        float* __restrict__ Gd) {
   using G = TGeo<H>;
   __shared__ float red[256][7];
   float acc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -494,8 +525,14 @@ __global__ __launch_bounds__(256) void gat_param_kernel(int n, const float* __re
   for (int c = threadIdx.x; c < H; c += 256) {
     const float* fc = P + G::W_FC + c * 3;
     const float a1 = P[G::W_ATT + c], a2 = P[G::W_ATT + H + c];
+    float agg[3] = {0.f, 0.f, 0.f};
+    for (int r = 0; r < H; ++r) {
+      const float wt = P[G::W_TE + r * H + c];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) Gd[G::W_FC + c * 3 + k] += a1 * xs[k] + a2 * xt[k];
+      for (int k = 0; k < 3; ++k) agg[k] = fmaf(wt, fcd[r * 3 + k], agg[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) Gd[G::W_FC + c * 3 + k] += agg[k] + (a1 * xs[k] + a2 * xt[k]);
     Gd[G::W_ATT + c] += fc[0] * xs[0] + fc[1] * xs[1] + fc[2] * xs[2];
     Gd[G::W_ATT + H + c] += fc[0] * xt[0] + fc[1] * xt[1] + fc[2] * xt[2];
   }
@@ -816,7 +853,9 @@ bool plan_h(int B, TunePlan* out) {
   // one dQKV buffer per layer: layer 1's in_proj weight gradient reads its
   // buffer on the side stream while layer 0's attention backward writes the other
   for (int l = 0; l < 2; ++l) q.dq[l] = take(M1 * 3 * Q::DP);
-  q.gsx = take(3L * B * 8);
+  q.gsx = take(((3L * B + 3) / 4) * 8);
+  q.fcd = take(64 * 3);
+  q.mt = take(64 * 3);
   q.dpre = take((long)B * Q::NOP);
   q.wp = take((long)Q::NOP * Q::KD);
   q.wpt = take((long)Q::NOP * Q::KD);
@@ -941,6 +980,7 @@ hipError_t tune_fwd_h(const TunePlan& p, const float* win, const float* P, float
   Fork fk(st);
   if ((e = fk.fork()) != hipSuccess) return e;
   TCK((dec_pack_kernel<H><<<(int)((Q::NOP * Q::KD + 255) / 256), 256, 0, fk.side>>>(P, ws + p.wp, ws + p.wpt)));
+  TCK((gat_mt_kernel<H><<<1, 192, 0, fk.side>>>(P, ws + p.mt)));  // for the backward's GAT (gat_bwd_kernel)
   TCK((gat_fwd_kernel<H><<<(3 * B + 3) / 4, 256, 0, st>>>(B, win, P, ws + p.win, ws + p.g, ws + p.xb, ws + p.gs)));
   // the encoder: fragments packed from P, then one fused launch per layer
   TfArgs t{};
@@ -982,6 +1022,30 @@ hipError_t tune_bwd_h(const TunePlan& p, const float* P, float* Gd, float* ws, c
   const hipStream_t sd = fk.side;
   TCK((tune_loss_kernel<<<(int)(((long)B * H + 255) / 256), 256, 0, st>>>(B, H, Q::NOP, logits, protos, y, mult,
                                                                            tgt, ws + p.dpre)));
+  // side work: the decoders' weight gradients (dpre, encoder output -> G)
+  // and each layer's in_proj weight gradient (dQKV [M][3][DP] (x) X -> three
+  // [H][H] blocks of L_IN + bias); nothing on the critical path reads them
+  auto side_dec = [&]() -> hipError_t {
+    TCK((dec_dw_kernel<H><<<dim3(Q::T, 2, p.dec_dws), 256, 0, sd>>>(B, ws + p.dpre, ws + p.x[2], Gd, ws + p.part)));
+    if (p.dec_dws > 1) {
+      const long nw = 4L * H * G::L + 4 * H;
+      TCK((dec_dw_sum_kernel<H><<<(int)((nw + 255) / 256), 256, 0, sd>>>(p.dec_dws, ws + p.part, Gd)));
+    }
+    return hipSuccess;
+  };
+  auto in_proj_dw = [&](int l, hipStream_t ss) -> hipError_t {
+    float* Lg = Gd + G::LAY0 + l * G::L_SIZE;
+    constexpr int NP = 3 * DP;
+    const long pstride = (long)NP * DP + NP;
+    float* part = rb.take((long)p.dw_grid * pstride);
+    DwArgs a{M, ws + p.dq[l], NP, ws + p.x[l], DP, 0, part};
+    TCK((dw_kernel<NP, DP><<<p.dw_grid, 256, 0, ss>>>(a)));
+    for (int q = 0; q < 3; ++q)
+      if (!rb.add(p.dw_grid, pstride, part + (long)q * DP * DP, H, H, DP, Lg + G::L_IN + (long)q * H * H, H, H,
+                  (long)NP * DP + q * DP - (long)q * DP * DP, Lg + G::L_INB + q * H))
+        return hipErrorInvalidValue;
+    return hipSuccess;
+  };
 
   // grad of the encoder output = dpre . Wp (token layout, pgp_dec.hip)
   if ((e = launch_dec_dx(H, B, ws + p.dpre, ws + p.wpt, ws + p.da, st)) != hipSuccess) return e;
@@ -1029,45 +1093,31 @@ hipError_t tune_bwd_h(const TunePlan& p, const float* P, float* Gd, float* ws, c
                 Lg + G::L_OUTB))
       return hipErrorInvalidValue;
   }
-  // side, beside the serial tail below (time encoder, GAT): the weight
-  // gradients nothing on the critical path reads — the decoders' (dpre,
-  // encoder output -> G) and both layers' in_proj (dQKV [M][3][DP] (x) X ->
-  // three [H][H] blocks of L_IN + bias).  (Beside the fused launches they
-  // only slowed them: those take whole CUs, and a long side workgroup on a
-  // CU delays the next fused launch's workgroup there.)
+  // side, beside the serial tail below (time encoder, GAT): weight gradients
+  // nothing on the critical path reads — the decoders' and layer 1's in_proj.
+  // (Beside the fused launches they only slowed them: those take whole CUs,
+  // and a long side workgroup on a CU delays the next fused launch's
+  // workgroup there; measured again in round 3, profiles/r03/s3/side_ab.txt.)
   if ((e = fk.fork()) != hipSuccess) return e;
-  TCK((dec_dw_kernel<H><<<dim3(Q::T, 2, p.dec_dws), 256, 0, sd>>>(B, ws + p.dpre, ws + p.x[2], Gd, ws + p.part)));
-  if (p.dec_dws > 1) {
-    const long nw = 4L * H * G::L + 4 * H;
-    TCK((dec_dw_sum_kernel<H><<<(int)((nw + 255) / 256), 256, 0, sd>>>(p.dec_dws, ws + p.part, Gd)));
-  }
-  for (int l = 1; l >= 0; --l) {
-    float* Lg = Gd + G::LAY0 + l * G::L_SIZE;
-    constexpr int NP = 3 * DP;
-    const long pstride = (long)NP * DP + NP;
-    float* part = rb.take((long)p.dw_grid * pstride);
-    DwArgs a{M, ws + p.dq[l], NP, ws + p.x[l], DP, 0, part};
-    TCK((dw_kernel<NP, DP><<<p.dw_grid, 256, 0, sd>>>(a)));
-    for (int q = 0; q < 3; ++q)
-      if (!rb.add(p.dw_grid, pstride, part + (long)q * DP * DP, H, H, DP, Lg + G::L_IN + (long)q * H * H, H, H,
-                  (long)NP * DP + q * DP - (long)q * DP * DP, Lg + G::L_INB + q * H))
-        return hipErrorInvalidValue;
-  }
-  // time encoder: p.da = grad of X0
+  if ((e = side_dec()) != hipSuccess) return e;
+  if ((e = in_proj_dw(1, sd)) != hipSuccess) return e;
+  // time encoder: p.da = grad of X0 (weight gradient: dX0 (x) G)
   if ((e = dw<DP, DP>(p, rb, ws + p.da, DP, ws + p.g, DP, 0, H, H, Gd + G::W_TE, Gd + G::B_TE, st)) != hipSuccess)
     return e;
-  {
-    LinArgs a = lin_args(M, ws + p.da, DP, P + G::W_TE, H, H, H, 1, nullptr, ws + p.db, DP);
-    if ((e = lin<DP, DP, EPI_STORE>(p, a, st)) != hipSuccess) return e;
-  }
-  // GAT: db = grad of the GAT output
-  TCK((gat_bwd_kernel<H><<<(3 * B + 3) / 4, 256, 0, st>>>(B, ws + p.win, P, ws + p.db, ws + p.gs, ws + p.gsx)));
-  if ((e = dw<DP, Q::XBP>(p, rb, ws + p.db, DP, ws + p.xb, Q::XBP, 0, H, 3, Gd + G::W_FC, nullptr, st)) !=
-      hipSuccess)
+  // GAT, straight from dX0 (the time encoder's input gradient folded in,
+  // gat_bwd_kernel); the fc gradient's aggregation part: fcd = dX0 (x) x-bar
+  const int gat_wg = (3 * B + 3) / 4;
+  TCK((gat_bwd_kernel<H><<<gat_wg, 256, 0, st>>>(B, ws + p.win, P, ws + p.da, ws + p.gs, ws + p.mt, ws + p.gsx,
+                                                  ws + p.fcd)));
+  if ((e = dw<DP, Q::XBP>(p, rb, ws + p.da, DP, ws + p.xb, Q::XBP, 0, H, 3, ws + p.fcd, nullptr, st)) != hipSuccess)
     return e;
-  TCK((gat_param_kernel<H><<<1, 256, 0, st>>>(3 * B, ws + p.gsx, P, Gd)));
+  // layer 0's in_proj weight gradient closes the main stream's share (the two
+  // streams' tails are then about equal: kernel trace, profiles/r03/s3/)
+  if ((e = in_proj_dw(0, st)) != hipSuccess) return e;
   if ((e = fk.join()) != hipSuccess) return e;  // the side stream's partials and G writes
-  return rb.flush(st);  // every deferred weight-gradient reduction: 2 launches
+  if ((e = rb.flush(st)) != hipSuccess) return e;  // every deferred weight-gradient reduction: 2 launches
+  TCK((gat_param_kernel<H><<<1, 256, 0, st>>>(gat_wg, ws + p.gsx, P, ws + p.fcd, Gd)));
+  return hipSuccess;
 }
 
 }  // namespace

@@ -649,7 +649,8 @@ class DPTuner:
 
     SUBSTAGES = ("forward", "targets", "backward", "all_reduce", "apply_adamw")
 
-    def step(self, wins: torch.Tensor, y: torch.Tensor, cls: torch.Tensor, mark=None, before_update=None):
+    def step(self, wins: torch.Tensor, y: torch.Tensor, cls: torch.Tensor, mark=None, before_update=None,
+             after_forward=None):
         """wins [B,3,3H] fp32, y / cls [B,H] int32, all on the device.
         Returns the per-window (aloss, tloss) [B,2] fp64 device view.
         ``mark(k)``, if given, is called before sub-stage k of SUBSTAGES and
@@ -658,7 +659,10 @@ class DPTuner:
         before the state update and AdamW (work on another stream that still
         reads the step-start weights), or a callable returning one, called at
         that point of the host's issue order (so the work it issues elsewhere
-        is queued after this step's forward and backward)."""
+        is queued after this step's forward and backward).  ``after_forward``,
+        if given, is called once the forward is issued (work for another stream
+        that should queue behind the forward's launches but ahead of the
+        backward's)."""
         mark = mark or (lambda k: None)
         import torch.distributed as dist
         tr, L = self.tr, self.tr._L
@@ -674,6 +678,8 @@ class DPTuner:
         mark(0)
         tr.tune_forward(wins)
         mark(1)
+        if after_forward is not None:
+            after_forward()
         _native.check(L.pgp_tune_targets_dp(
             tr.H, self.K, B, tr.logits.data_ptr(), tr.protos.data_ptr(), y.data_ptr(), cls.data_ptr(),
             self.state.data_ptr(), PROTO_UPDATE_MIN, self.mult.data_ptr(), self.tgt.data_ptr(), self.loss.data_ptr(),

@@ -62,3 +62,19 @@ def test_fused_tuning_prefetches_are_not_waited_for_at_once():
     for name in ("tf_fwd_kernel", "tf_bwd_ffn_kernel", "tf_bwd_att_kernel"):
         cover = isa_count.load_cover(name, 50)
         assert sum(1 for c in cover if c >= 48) >= 12, (name, cover)
+
+
+def test_weight_gradient_and_decoder_prefetches_are_covered():
+    """The token-major weight-gradient contraction (dw_accumulate: in_proj,
+    time encoder, GAT fc, decoders) prefetches the next 32-row chunk while the
+    current one is contracted from LDS, and the decoder forward loads the next
+    token's rows under this token's MFMAs.  Zeros for rows past the range come
+    from a selected ADDRESS (pgp_gemm.hpp dw_zero4), the chunk loop is
+    branch-free, and dec_fwd2 reads only the live features of its last
+    k-block, so no prefetch is waited for before the MFMAs it should hide
+    behind (before: 24 / 16 / 0 MFMAs of cover)."""
+    import isa_count
+    for name, tag, need, n in (("dw_kernel", "192ELi64", 96, 8), ("dec_dw_kernel", "50", 64, 9),
+                               ("dec_fwd2_kernel", "50", 128, 4)):
+        cover = isa_count.load_cover(name, tag)
+        assert sum(1 for c in cover if c >= need) >= n, (name, cover)

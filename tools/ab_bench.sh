@@ -7,7 +7,7 @@ cd "$ROOT"
 TAG=$1; ARGS=$2; shift 2
 OUT=$ROOT/gpurun_out/$TAG
 mkdir -p "$OUT"
-for rep in 1 2; do
+for rep in 1 2 3; do
   for v in base "$@"; do
     if [ "$v" = base ]; then lib=$ROOT/preganplus_amd/_lib/libpreganplus.so; else lib=$ROOT/preganplus_amd/_lib/var/libpreganplus_$v.so; fi
     PGP_LIB=$lib timeout -k 10 300 python bench.py $ARGS --no-cpu-baseline >"$OUT/$v.$rep.json" 2>"$OUT/$v.$rep.err" || { tail "$OUT/$v.$rep.err"; exit 1; }
