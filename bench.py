@@ -49,7 +49,7 @@ def synth_inputs(B, H, device, seed):
     return x.contiguous(), s.contiguous()
 
 
-def cpu_baseline(weights, x, s, per_window_n=32, batch_n=1024):
+def cpu_baseline(weights, x, s, per_window_n=256, batch_n=1024):
     """the CPU restatement timed on this box's host cores, on the
     GPU run's own first windows (same C2 inputs, spikes included), in two modes
     (reference-faithful per-window fp64; batched fp32 torch-CPU), median of 5."""
@@ -61,15 +61,36 @@ def cpu_baseline(weights, x, s, per_window_n=32, batch_n=1024):
 def load_traffic(H, B, kernel="encoder"):
     """HBM bytes per launch of one kernel from the committed rocprofv3 --pmc
     FETCH_SIZE / WRITE_SIZE passes (profiles/pmc_<kernel>_h<H>.json, corrected
-    per MI355X_MICROARCH.md §HBM), or None when absent / another batch."""
-    p = os.path.join(ROOT, "profiles", f"pmc_{kernel}_h{H}.json")
+    per MI355X_MICROARCH.md §HBM, tools/pmc_traffic.py), or None when absent,
+    taken at another batch, or taken with a different build of that kernel
+    (the file's isa_sha256 against the loaded library's instructions: a
+    stale counter pass is never reported as this build's traffic)."""
+    d = traffic_record(H, B, kernel)
+    return None if d is None else d.get("hbm_bytes_per_launch")
+
+
+def traffic_record(H, B, kernel, path=None):
+    p = path or os.path.join(ROOT, "profiles", f"pmc_{kernel}_h{H}.json")
     if not os.path.exists(p):
         return None
     try:
         d = json.load(open(p))
         if int(d.get("batch", -1)) != B:
             return None
-        return d.get("hbm_bytes_per_launch")
+        if d.get("isa_sha256") is None or d["isa_sha256"] != loaded_isa_hash(kernel + "_kernel", H):
+            return None
+        return d
+    except Exception:
+        return None
+
+
+def loaded_isa_hash(name, H):
+    """sha256 of kernel `name`<H> in the library this process loads (PGP_LIB or
+    the in-tree build), tools/isa_count.kernel_isa_hash; None without llvm-objdump."""
+    try:
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        import isa_count
+        return isa_count.kernel_isa_hash(name, H, lib=_native.LIB_PATH)
     except Exception:
         return None
 
@@ -275,9 +296,15 @@ def _dist_setup():
         # a rehearsal with every rank on ONE device: one stream per rank (the
         # GAN / tuning overlap and the library's side stream multiply the
         # processes' hardware queues on that device and time-slice them; the
-        # driver's runs, one GPU per rank, keep both)
+        # driver's runs, one GPU per rank, keep the GAN / tuning overlap)
         os.environ["PGP_BENCH_ONE_STREAM"] = "1"
         os.environ["PGP_TUNE_SIDE_STREAM"] = "0"
+    elif world > 1:
+        # one GPU per rank: main + GAN stream + the two communicators' internal
+        # streams (tuning, GAN) = the 4 hardware queues a process gets
+        # (GPU_MAX_HW_QUEUES); the library's low-priority side stream would be a
+        # fifth, sharing a queue with one of them, so it is off
+        os.environ.setdefault("PGP_TUNE_SIDE_STREAM", "0")
     if dev_env == "cpu":
         device = torch.device("cpu")
     else:
@@ -299,6 +326,16 @@ def _dist_setup():
 
 
 _HOST_ISSUE_S = None
+
+
+def _backend_label():
+    """The collective backend the ranks actually use (RCCL is torch's "nccl"
+    backend on ROCm; gloo in CPU / shared-device rehearsals)."""
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()):
+        return "none"
+    b = dist.get_backend()
+    return "RCCL" if b == "nccl" else b
 
 
 def emit(res):
@@ -343,7 +380,9 @@ def bench_fleet(args):
     """BASELINE config 5: a 1024-host fleet as 64 independent 16-host cells
     (SURVEY §8d), 1M windows per cell = 64M cell-windows sharded over the GPUs.
     One step = one launch sequence over a chunk of cell-windows resident in HBM;
-    the per-GPU share is covered in ceil(share / chunk) steps."""
+    the per-GPU share is covered in ceil(share / chunk) steps.  The roofline is
+    the dominant kernel's (K2 encoder_kernel<16>, executed MFMA flops over its
+    HIP-event time, recorded around each stage on the kernels' stream)."""
     world, rank, device = _dist_setup()
     w, _ = W.load_npz(os.path.join(ROOT, "preganplus_amd/data/simulator_16.npz"))
     H, B = 16, args.batch if args.batch != 65536 else 262144
@@ -354,11 +393,29 @@ def bench_fleet(args):
     total = 64 * 1_000_000
     share = total // world
     steps = -(-share // B) if args.steps <= 0 else args.steps
+    NK = 4   # K1 gat, K2 encoder, K2b decoder, K3 gan
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(NK + 1)] for _ in range(steps)]
+    it = iter(evs)
+
+    def step():
+        e = next(it)
+        for k in range(NK):
+            e[k].record()
+            model.forward(x, s, out=out, stage=k)
+        e[NK].record()
+
     for _ in range(args.warmup):
         model.forward(x, s, out=out)
-    el = _timed(world, device, lambda: model.forward(x, s, out=out), steps)
+    el = _timed(world, device, step, steps)
+    k_mean = np.array([[e[k].elapsed_time(e[k + 1]) for k in range(NK)] for e in evs]).mean(axis=0)
     if rank == 0:
         cw = B * steps * world
+        names = ("gat_agg", "encoder", "decoder", "gan")
+        dom = int(np.argmax(k_mean))
+        exe = R.encoder_executed_flops_per_window(H)
+        ach = exe * B / (k_mean[1] * 1e-3) / 1e12
+        k_traffic = {k: load_traffic(H, B, k) for k in names}
+        path_bytes = R.path_bytes_per_window(H) * B
         res = {
             "metric": "host-windows/sec (detect+diagnose+generate), fleet", "value": cw * H / el,
             "unit": "host-windows/s", "n_gpus": world, "steps": steps, "warmup": args.warmup,
@@ -366,10 +423,30 @@ def bench_fleet(args):
             "vs_baseline": None, "dtype": "fp32", "data": "synthetic (C2 distribution), shipped H=16 weights",
             "config": {"workload": "C5: 1024-host fleet = 64 x 16-host cells, cell-windows sharded over GPUs",
                        "hosts_per_cell": H, "cells": 64, "cell_windows_per_step_per_gpu": B,
-                       "cell_windows_total": cw, "parallelism": f"dp{world}"}}
+                       "cell_windows_total": cw, "parallelism": f"dp{world}"},
+            "kernel_ms": {n: float(k_mean[k]) for k, n in enumerate(names)},
+            "roofline": {"kernel": "encoder_kernel<16> (K2)" + ("" if dom == 1 else
+                                                                 f" (the longest stage is {names[dom]})"),
+                         "bound": "mfma", "achieved": ach, "peak": R.PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+                         "frac": ach / R.PEAK_FP32_TFLOPS,
+                         "basis": "executed MFMA flops per launch (ISA count, tools/isa_count.py) / HIP-event kernel "
+                                  "time on the kernels' stream",
+                         "executed_flops_per_window": exe,
+                         "traffic": k_traffic["encoder"],
+                         "traffic_ratio": (None if k_traffic["encoder"] is None else
+                                           k_traffic["encoder"] / (R.encoder_io_bytes_per_window(H) * B))},
+            "path_roofline": {
+                "hbm_algorithmic_gbs": path_bytes / (k_mean.sum() * 1e-3) / 1e9,
+                "traffic_per_step": (None if None in k_traffic.values() else sum(k_traffic.values())),
+                "traffic_ratio": (None if None in k_traffic.values() else sum(k_traffic.values()) / path_bytes),
+                "traffic_by_kernel": k_traffic,
+                "kernel_tflops": {"encoder": ach,
+                                  "decoder": R.decoder_flops_per_window(H) * B / (k_mean[2] * 1e-3) / 1e12,
+                                  "gan": R.gan_flops_per_window(H) * B / (k_mean[3] * 1e-3) / 1e12}},
+        }
         if world == 1 and not args.no_cpu_baseline:
             log("timing CPU baseline ...")
-            res["cpu_baseline"] = cpu_baseline(w, x, s, per_window_n=64, batch_n=4096)
+            res["cpu_baseline"] = cpu_baseline(w, x, s, per_window_n=256, batch_n=4096)
         emit(res)
     if world > 1:
         torch.distributed.destroy_process_group()
@@ -417,7 +494,8 @@ def bench_tune(args):
     w = W.synth_weights(H, seed=0)
     tr = TR.Trainer(H, w, device=device, max_batch=B)
     st = TR.TuneState(w["prototypes"])
-    tun = TR.DPTuner(tr, st, B)
+    tune_group, gan_group = TR.dp_groups()    # the GAN step's collectives on a communicator of their own
+    tun = TR.DPTuner(tr, st, B, group=tune_group)
     series_h, tmax_h = synth_series(E, H, 5 + rank, R)
     series = torch.tensor(series_h, device=device)
     tmax = torch.tensor(tmax_h, device=device)
@@ -445,8 +523,10 @@ def bench_tune(args):
 
     # detect reads the step-start weights and feeds only the GAN step, so it
     # runs on the second stream too, with a workspace of its own; the tuning
-    # step's weight update waits for it (before_update)
-    det_ctx = tr.forward_context(E) if side is not main else None
+    # step's weight update waits for it (before_update).  The workspace is its
+    # own in single-stream mode as well: detect is issued between the tuning
+    # forward and its targets / backward, which read the trainer's workspace
+    det_ctx = tr.forward_context(E)
     det_done = torch.cuda.Event()
 
     def step(e=None, se=None):
@@ -470,7 +550,8 @@ def bench_tune(args):
         # detect's launches are issued once the tuning forward's are queued
         def gan():
             with torch.cuda.stream(side):
-                TR.train_gan_batched(tr, sim, envs, emb_buf, s, out=sim_out, target=gan_target, all_reduce=True)
+                TR.train_gan_batched(tr, sim, envs, emb_buf, s, out=sim_out, target=gan_target, all_reduce=True,
+                                     group=gan_group)
                 if e is not None:
                     e[3].record(side)
 
@@ -534,13 +615,30 @@ def bench_tune(args):
                     "environment records; GAN labels simulated; seeded H-architecture weights",
             "config": {"workload": f"C3: semi-supervised tuning step, {H} hosts, {E} environments x {R} windows "
                                    f"= {B} tuning windows per GPU", "hosts": H, "environments_per_gpu": E,
-                       "windows_per_gpu": B, "parallelism": f"dp{world} + RCCL all-reduce (grads, state)"},
+                       "windows_per_gpu": B, "parallelism": f"dp{world}" + (f" + {_backend_label()} all-reduce "
+                                                                           "(grads, state; GAN on its own group)"
+                                                                           if world > 1 else "")},
             "stage_ms": {n: float(stage[k]) for k, n in enumerate(names)},
             "streams": "detect + train_gan on a second stream, concurrent with tune_model (no shared data; the "
                        "tuning step's weight update waits for detect)",
             "tune_model_ms": {n: float(sub[k]) for k, n in enumerate(subs)},
             "grad_all_reduce_ms": float(sub[subs.index("all_reduce")]),
             "roofline": roof,
+            # the two training stages as a whole, on the reference formulation's
+            # flops (algorithmic, not executed) over the stage's HIP-event span;
+            # train_gan runs on the second stream beside tune_model, so its span
+            # includes the time its launches wait for CUs the tuning kernels hold
+            "stage_roofline": {
+                n: {"ms": float(ms), "achieved": fl / (ms * 1e-3) / 1e12, "peak": RL.PEAK_FP32_TFLOPS,
+                    "unit": "TFLOP/s", "frac": fl / (ms * 1e-3) / 1e12 / RL.PEAK_FP32_TFLOPS, "flops": fl,
+                    "basis": basis}
+                for n, ms, fl, basis in (
+                    ("tune_model", stage[3], RL.tune_step_flops_per_window(H) * B,
+                     f"{RL.tune_step_flops_per_window(H) / 1e6:.2f} MFLOP per tuning window (3 x the Transformer "
+                     f"forward: input and weight gradients) x {B} windows"),
+                    ("train_gan", stage[2], RL.gan_step_flops_per_env(H) * E,
+                     f"{RL.gan_step_flops_per_env(H) / 1e6:.2f} MFLOP per environment (Gen + Disc forward, Disc "
+                     f"step, Gen step through the updated Disc) x {E} environments"))},
         }
         if world == 1 and not args.no_cpu_baseline:
             log("timing CPU baseline ...")
@@ -550,7 +648,7 @@ def bench_tune(args):
         torch.distributed.destroy_process_group()
 
 
-def tune_cpu_baseline(w, series, tmax, sched, envs, H, per_repeat=2, repeats=5):
+def tune_cpu_baseline(w, series, tmax, sched, envs, H, per_repeat=8, repeats=5):
     """The same per-environment work through the CPU restatements, as the
     reference runs it (CPU baseline leg only): run_encoder window -> detect ->
     train_gan with runSimulation labels (bit-identical restatement) ->
@@ -583,11 +681,11 @@ def tune_cpu_baseline(w, series, tmax, sched, envs, H, per_repeat=2, repeats=5):
             n += 1
         if rep:
             rates.append(per_repeat * 10 / (time.perf_counter() - t0))
-    return {"value": float(np.median(rates)), "unit": "windows/s", "cores": threads, "kind": "port", "threads_note": CB.THREADS_NOTE,
+    return {"value": float(np.median(rates)), "unit": "windows/s", "cores": threads, "kind": "port", **CB.thread_report(),
             "sample": f"{per_repeat} environments x 10 tuning windows per repeat, median of {repeats}: detect, "
                       f"train_gan (runSimulation restatement), sequential batch-1 backprop; fp64 torch-CPU "
                       f"(the reference's algorithm, H={H})",
-            "repeats": rates, "cpu_model": CB.cpu_model(), "host_cpus": os.cpu_count()}
+            "repeats": rates, "cpu_model": CB.cpu_model()}
 
 
 def fpe_cpu_baseline(weights, budget_s=12.0, max_threads=16):
@@ -610,7 +708,7 @@ def fpe_cpu_baseline(weights, budget_s=12.0, max_threads=16):
             O.forward_fpe(weights, x, h0, s)
             done += nb
     dt = time.perf_counter() - t0
-    return {"value": done * H / dt, "unit": "host-windows/s", "cores": threads, "kind": "port", "threads_note": CB.THREADS_NOTE,
+    return {"value": done * H / dt, "unit": "host-windows/s", "cores": threads, "kind": "port", **CB.thread_report(),
             "sample": f"{done} windows (H=16, batches of {nb}), numpy fp64 FPE oracle, {dt:.1f}s"}
 
 
@@ -835,7 +933,8 @@ def bench_loop(args):
     g = torch.Generator(device=device).manual_seed(19 + rank)
     y = (torch.rand((E, H), generator=g, device=device) < 0.1).to(torch.int32)
     cls = torch.randint(0, 3, (E, H), generator=g, device=device, dtype=torch.int32)
-    tun = TR.DPTuner(tr, TR.TuneState(np.asarray(model.prototypes, dtype=np.float64)), E)
+    tune_group, gan_group = TR.dp_groups()
+    tun = TR.DPTuner(tr, TR.TuneState(np.asarray(model.prototypes, dtype=np.float64)), E, group=tune_group)
     K = model.K
     gout = (torch.empty_like(inits), torch.empty(E, dtype=torch.int32, device=device),
             torch.empty(E, dtype=torch.float32, device=device))
@@ -869,7 +968,8 @@ def bench_loop(args):
         if timed:
             ev[4].record(main)
         with torch.cuda.stream(side):
-            TR.train_gan_batched(tr, sim, envs, emb, sched, out=sim_out, target=gan_target)
+            TR.train_gan_batched(tr, sim, envs, emb, sched, out=sim_out, target=gan_target, all_reduce=True,
+                                 group=gan_group)
             if timed:
                 ev[3].record(side)
         main.wait_stream(side)

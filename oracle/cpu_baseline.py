@@ -16,8 +16,9 @@ asks:
 2. ``batched_fp32``: the same math batched over windows in fp32 torch-CPU
    (oracle/pregan_train_oracle.py's forward pieces).
 
-Threads: the host's CPU share (``OMP_NUM_THREADS`` when set — 16 on the GPU
-box — else ``os.cpu_count()``), warm-up, median of 5 repeats.
+Threads: the CPUs this process may run on (``os.sched_getaffinity``), capped by
+``OMP_NUM_THREADS`` when set (16 on the GPU box: the box's CPU share per GPU);
+both are reported beside the count used.  Warm-up, median of 5 repeats.
 """
 from __future__ import annotations
 
@@ -41,14 +42,28 @@ def cpu_model() -> str:
     return "unknown"
 
 
-THREADS_NOTE = ("BASELINE.md §4 asks for os.cpu_count() threads; that counts the whole host, while this process's "
-                "CPU share is OMP_NUM_THREADS (16 on the GPU box), so the baseline runs on that share")
+THREADS_NOTE = ("threads = the CPUs in this process's affinity mask (os.sched_getaffinity), capped by "
+                "OMP_NUM_THREADS when set (the box's CPU share per GPU); os.cpu_count() counts the whole host")
+
+
+def affinity_cpus() -> int:
+    try:
+        return len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        return os.cpu_count() or 1
 
 
 def host_threads() -> int:
-    n = os.cpu_count() or 1
+    n = affinity_cpus()
     env = os.environ.get("OMP_NUM_THREADS")
     return min(n, int(env)) if env and env.isdigit() and int(env) > 0 else n
+
+
+def thread_report() -> dict:
+    """What the thread count was derived from (reported in every cpu_baseline)."""
+    return {"threads": host_threads(), "affinity_cpus": affinity_cpus(),
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS"), "host_cpus": os.cpu_count(),
+            "threads_note": THREADS_NOTE}
 
 
 def _tensors(weights, dtype):
@@ -97,7 +112,7 @@ def batched_fp32(tw, gw, dw, P, win, s):
         return cls, probs[:, 0] > probs[:, 1], s.argmax(-1), ns.argmax(-1)
 
 
-def measure(weights, windows, sched, per_window_n=32, batch_n=1024, repeats=5):
+def measure(weights, windows, sched, per_window_n=256, batch_n=1024, repeats=5):
     """windows [N,3,3H], sched [N,H,H] (numpy, the GPU run's own inputs; N >=
     batch_n).  Returns the cpu_baseline object for bench.py (host-windows/s)."""
     H = windows.shape[2] // 3
@@ -137,6 +152,5 @@ def measure(weights, windows, sched, per_window_n=32, batch_n=1024, repeats=5):
                                               "repeats": [float(v) for v in pw]},
                   "batched_fp32": {"value": bf, "windows_per_repeat": batch_n,
                                    "repeats": [float(v) for v in bt]}},
-        "cpu_model": cpu_model(), "host_cpus": os.cpu_count(), "threads": threads,
-        "threads_note": THREADS_NOTE,
+        "cpu_model": cpu_model(), **thread_report(),
     }

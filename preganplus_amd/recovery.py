@@ -39,6 +39,8 @@ from __future__ import annotations
 import atexit
 import os
 import threading
+import warnings
+import weakref
 
 import numpy as np
 import torch
@@ -70,7 +72,32 @@ class Recovery:
         return original_decision
 
 
-class PreGANPlusRecovery(Recovery):
+class _SaveGan:
+    """save_gan after every train_gan (utils.py:86-88) through one
+    _GanCheckpointWriter per plugin, created on first use; the plugin's
+    finalizer (or ``close()``) ends the writer's thread."""
+
+    _writer = None
+
+    def _post_gan_checkpoint(self):
+        if self._writer is None:
+            self._writer = _GanCheckpointWriter(self.trainer, self.gen_name, self.disc_name)
+            self._writer_fin = weakref.finalize(self, _close_writer, self._writer)
+        self._writer.post(self.save_folder, self.env_name, self.epoch, self.accuracy_list)
+
+    def flush_checkpoints(self):
+        """Wait until the last posted Gen / Disc checkpoint is on disk."""
+        if self._writer is not None:
+            self._writer.flush()
+
+    def close(self):
+        """Write the queued checkpoint and end the writer thread."""
+        if self._writer is not None:
+            self._writer_fin()
+            self._writer = None
+
+
+class PreGANPlusRecovery(_SaveGan, Recovery):
     def __init__(self, hosts, env, training=False, device=None, model_folder=None, save_folder=_AUTO,
                  weights=None, extra=None):
         super().__init__()
@@ -130,15 +157,17 @@ class PreGANPlusRecovery(Recovery):
 
     def _load_new_model(self, folder):
         """load_model without a checkpoint (utils.py:76-78: epoch -1, fresh
-        parameters with torch's default initialisation, PGP_INIT_SEED seeds it)
-        and the GAN's (load_gan: its checkpoints, else new as well), then
+        parameters drawn from the distributions torch's module constructors use,
+        ``weights.torch_default_weights``, PGP_INIT_SEED seeds it) and the GAN's
+        (load_gan: its checkpoints, else new as well, Gen epoch -1), then
         train_model for num_epochs on the reference's data/<env>/time_series.npy."""
         data = os.path.join("recovery/PreGANSrc/data", self.env_name, "time_series.npy")
         if not os.path.exists(data):
             raise FileNotFoundError(f"no checkpoint for {self.model_name} in {folder}, no packaged weights, and "
                                     f"no training data {data} (utils.py:27-31)")
-        weights = W.synth_weights(self.hosts, seed=int(os.environ.get("PGP_INIT_SEED", 0)))
-        extra = {"meta/transformer/epoch": np.array(-1), "train_time_data": np.load(data)}
+        weights = W.torch_default_weights(self.hosts, seed=int(os.environ.get("PGP_INIT_SEED", 0)))
+        extra = {"meta/transformer/epoch": np.array(-1), "meta/gen/epoch": np.array(-1),
+                 "train_time_data": np.load(data)}
         gan = W.load_gan_checkpoints(folder, self.env_name, self.hosts)
         if gan is not None:
             weights = dict(weights, **gan[0])
@@ -192,15 +221,8 @@ class PreGANPlusRecovery(Recovery):
         self.epoch += 1
         self.accuracy_list.append((gen_loss, disc_loss))
         if self.save_gan:
-            if self._writer is None:
-                self._writer = _GanCheckpointWriter(self)
-            self._writer.post()
+            self._post_gan_checkpoint()
         return ns
-
-    def flush_checkpoints(self):
-        """Wait until the last posted Gen / Disc checkpoint is on disk."""
-        if self._writer is not None:
-            self._writer.flush()
 
     # -- PreGANPlus.py:51-58 --
     def tune_model(self):
@@ -332,7 +354,7 @@ class PreGANPlusRecovery(Recovery):
         # accuracy_list entry still come after train_gan's, in the reference's
         # order.  (If train_gan raises, the already launched tuning step is still
         # completed and recorded, where the reference would not have run it.)
-        pending = launch_err = None
+        pending = launch_err = first = None
         try:
             try:
                 pending = self._tune_launch()
@@ -343,9 +365,18 @@ class PreGANPlusRecovery(Recovery):
                 raise launch_err
             fin, pending = pending, None
             self._tune_finish(fin)
+        except BaseException as e:
+            first = e
+            raise
         finally:
             if pending is not None:
-                self._tune_finish(pending)
+                try:
+                    self._tune_finish(pending)
+                except Exception as e2:
+                    if first is None:
+                        raise
+                    # train_gan's error propagates; the launched tuning step's own is reported beside it
+                    warnings.warn(f"tune_model after a failed train_gan also failed: {e2!r}", RuntimeWarning)
             # the master moved even if tune_model raised (accuracy() divides by zero
             # without a positive label, as the reference's does): K1-K3 follow it
             self.sync_inference_weights()
@@ -411,6 +442,21 @@ def save_checkpoints(trainer, folder, env_name, epoch, accuracy_list, entries):
                      os.path.join(folder, f"{env_name}_{name}.ckpt"))
 
 
+_LIVE_WRITERS = weakref.WeakSet()
+
+
+@atexit.register
+def _flush_live_writers():
+    """At exit, every writer still alive writes its newest snapshot (one
+    handler for all of them: a per-writer atexit entry would keep each writer,
+    its Trainer and its device buffers alive for the whole process)."""
+    for w in list(_LIVE_WRITERS):
+        try:
+            w.flush()
+        except Exception:
+            pass
+
+
 class _GanCheckpointWriter:
     """save_gan (utils.py:86-88) after every train_gan, off the critical path.
     ``post()`` snapshots the Gen / Disc master weights and AdamW moments into a
@@ -421,16 +467,20 @@ class _GanCheckpointWriter:
     (0, []), atomic renames).  Snapshots still queued when a newer one is posted
     are superseded (the files on disk always end at the newest call, as the
     reference's do).  ``fence()`` makes the caller's stream wait for the last
-    snapshot copy before the next GAN update; ``flush()`` waits for the disk.
+    snapshot copy before the next GAN update; ``flush()`` waits for the disk;
+    ``close()`` flushes and ends the thread.
     Pickling a checkpoint holds the GIL for milliseconds, so after each write the
     writer pauses ``min_interval`` seconds (PGP_SAVE_GAN_INTERVAL, default 0.05)
     before taking the newest snapshot: calls that come faster than that do not
     wait on the GIL; the files then lag the plugin by at most one pause, and
-    ``flush()`` (also at exit) writes the newest state at once."""
+    ``flush()`` (also at exit) writes the newest state at once.
+    The writer holds the Trainer and the two model names, never the plugin, so
+    a plugin that goes out of scope is collected and its finalizer closes the
+    writer (the thread then releases the Trainer too)."""
 
-    def __init__(self, rec, min_interval=None):
-        tr = rec.trainer
-        self.rec, self.tr = rec, tr
+    def __init__(self, trainer, gen_name, disc_name, min_interval=None):
+        tr = trainer
+        self.tr, self.gen_name, self.disc_name = tr, gen_name, disc_name
         self.lo, self.hi = tr.sec_off["gen"], tr.sec_end["disc"]
         n = self.hi - self.lo
         self.bufs = [torch.empty((3, n), dtype=torch.float32).pin_memory() for _ in range(2)]
@@ -444,18 +494,21 @@ class _GanCheckpointWriter:
         self.writing = False
         self.error = None
         self.urgent = False
+        self.stopping = False
         self.min_interval = float(os.environ.get("PGP_SAVE_GAN_INTERVAL", 0.05) if min_interval is None
                                   else min_interval)
         self.thread = threading.Thread(target=self._run, daemon=True, name="pgp-save-gan")
         self.thread.start()
-        atexit.register(self.flush)
+        _LIVE_WRITERS.add(self)
 
     def fence(self):
         if self.last_event is not None:
             torch.cuda.current_stream(self.tr.device).wait_event(self.last_event)
 
-    def post(self):
-        rec, tr = self.rec, self.tr
+    def post(self, folder, env_name, epoch, accuracy_list):
+        tr = self.tr
+        if self.stopping:
+            raise RuntimeError("save_gan writer is closed")
         with self.cv:
             while self.busy[self.next]:
                 self.cv.wait()
@@ -471,7 +524,7 @@ class _GanCheckpointWriter:
             self.events[k].record(self.stream)
         self.last_event = self.events[k]
         # accuracy_list only grows (append): the writer slices the first n entries itself
-        job = (k, rec.save_folder, rec.env_name, rec.epoch, (rec.accuracy_list, len(rec.accuracy_list)),
+        job = (k, folder, env_name, epoch, (accuracy_list, len(accuracy_list)),
                {t["name"] + "@" + t["section"]: t["step"] for t in tr.tensors if t["section"] in ("gen", "disc")})
         with self.cv:
             if self.job is not None:          # superseded, never written
@@ -484,36 +537,41 @@ class _GanCheckpointWriter:
     def _run(self):
         while True:
             with self.cv:
-                while self.job is None:
+                while self.job is None and not self.stopping:
                     self.cv.wait()
+                if self.job is None:      # stopping, nothing queued
+                    return
                 k, folder, env_name, epoch, acc, steps = self.job
                 self.job = None
                 self.writing = True
+            released = False   # buffer k handed back (after its host copy): post() may take it again
             try:
                 self.events[k].synchronize()
                 host = self.bufs[k].numpy().copy()
                 with self.cv:
                     self.busy[k] = False
+                    released = True
                     self.cv.notify_all()
                 self._write(host, folder, env_name, epoch, acc, steps)
             except Exception as e:  # surfaced on the next post()
                 self.error = e
             finally:
                 with self.cv:
-                    self.busy[k] = False
+                    if not released:   # failed before the copy: free the buffer here, never a re-taken one
+                        self.busy[k] = False
                     self.writing = False
                     self.cv.notify_all()
                     # pause before the next write unless a flush is waiting
-                    if self.min_interval > 0 and not self.urgent:
-                        self.cv.wait_for(lambda: self.urgent, timeout=self.min_interval)
+                    if self.min_interval > 0 and not self.urgent and not self.stopping:
+                        self.cv.wait_for(lambda: self.urgent or self.stopping, timeout=self.min_interval)
 
     def _write(self, host, folder, env_name, epoch, acc, steps):
-        tr, rec = self.tr, self.rec
+        tr = self.tr
         os.makedirs(folder, exist_ok=True)
         p, m, v = host
         shapes = {(sec, name): shp for sec, name, shp in W.blob_layout(tr.H)[:-1]}
         acc = acc[0][:acc[1]]
-        for sec, name, ep, al in (("gen", rec.gen_name, epoch, acc), ("disc", rec.disc_name, 0, [])):
+        for sec, name, ep, al in (("gen", self.gen_name, epoch, acc), ("disc", self.disc_name, 0, [])):
             wsec = {t["name"]: p[t["offset"] - self.lo:t["offset"] - self.lo + t["n"]].reshape(shapes[(sec, t["name"])])
                     for t in tr.tensors if t["section"] == sec}
             st = {t["name"]: steps[t["name"] + "@" + sec] for t in tr.tensors if t["section"] == sec}
@@ -529,6 +587,27 @@ class _GanCheckpointWriter:
             self.urgent = False
         if self.error is not None:
             raise RuntimeError("save_gan writer failed") from self.error
+
+    def close(self):
+        """Write what is queued, end the thread (idempotent)."""
+        if self.stopping:
+            return
+        try:
+            self.flush()
+        finally:
+            with self.cv:
+                self.stopping = True
+                self.cv.notify_all()
+            if self.thread is not threading.current_thread():
+                self.thread.join()
+            _LIVE_WRITERS.discard(self)
+
+
+def _close_writer(writer):
+    try:
+        writer.close()
+    except Exception:
+        pass
 
 
 class _RecoverIO:
@@ -576,10 +655,18 @@ def _recover(env, hosts, schedule_data, original_decision, keep_original, device
     return assemble_decision(original_decision, moves, cur), [int(v) for v in hosts_from]
 
 
-class PreGANRecovery(Recovery):
-    """recovery/PreGAN.py:11-126 on MI355X."""
+MODEL_FOLDER = "recovery/PreGANSrc/checkpoints"   # constants.py:2 (PreGAN's model_folder)
 
-    def __init__(self, hosts, env, training=False, device=None, model_folder=None, save_folder=None,
+
+class PreGANRecovery(_SaveGan, Recovery):
+    """recovery/PreGAN.py:11-126 on MI355X.  As the reference's train_gan does
+    (PreGAN.py:66-71), every GAN step rewrites the Gen / Disc checkpoints
+    (save_gan, utils.py:86-88: Disc with epoch 0 and []) into the folder the
+    models were loaded from, on the same writer thread as PreGANPlusRecovery;
+    a plugin built from injected ``weights=`` (tests, benches) writes only when
+    ``save_folder`` is given."""
+
+    def __init__(self, hosts, env, training=False, device=None, model_folder=None, save_folder=_AUTO,
                  weights=None, extra=None):
         super().__init__()
         self.model_name = f"FPE_{hosts}"
@@ -588,15 +675,19 @@ class PreGANRecovery(Recovery):
         self.hosts = hosts
         self.env_name = "simulator" if env == "" else "framework"
         self.training = training
+        if save_folder is _AUTO:   # the reference's save_gan call in train_gan (PreGAN.py:70-71)
+            save_folder = None if weights is not None else (model_folder or MODEL_FOLDER)
         self.save_folder = save_folder
+        self.save_gan = save_folder is not None
         self.device = torch.device(device or "cuda")
         self.load_models(model_folder, weights, extra)
 
     # -- PreGAN.py:22-37 (the encoder is frozen; no encoder training path: a
-    #    missing FPE checkpoint is an error, not a 30-epoch training run) --
+    #    missing FPE checkpoint falls back to the packaged FPE_16 weights, and
+    #    the GAN checkpoints save_gan keeps rewriting are loaded over them) --
     def load_models(self, model_folder=None, weights=None, extra=None):
         if weights is None:
-            folder = model_folder or "recovery/PreGANSrc/checkpoints"
+            folder = model_folder or MODEL_FOLDER
             ck = os.path.join(folder, f"{self.env_name}_{self.model_name}.ckpt")
             if os.path.exists(ck):
                 weights, state = W.load_reference_checkpoints(folder, self.env_name, self.hosts, encoder="FPE",
@@ -607,6 +698,12 @@ class PreGANRecovery(Recovery):
                 if not os.path.exists(packaged):
                     raise FileNotFoundError(f"no checkpoint for {self.model_name} in {folder} or {packaged}")
                 weights, extra = W.load_npz(packaged)
+                gan = W.load_gan_checkpoints(folder, self.env_name, self.hosts)   # load_gan (PreGAN.py:31-33)
+                if gan is not None:
+                    weights = dict(weights, **gan[0])
+                    extra = {k: v for k, v in extra.items()
+                             if not k.startswith(("opt/gen/", "opt/disc/", "meta/gen/", "meta/disc/"))}
+                    extra.update(gan[1])
         self.weights = weights
         self.extra = extra or {}
         self.model = FPEDecisionModel(self.hosts, weights, device=self.device)
@@ -641,16 +738,16 @@ class PreGANRecovery(Recovery):
 
     # -- PreGAN.py:51-71 --
     def train_gan(self, embedding, schedule_data):
+        if self._writer is not None:
+            self._writer.fence()   # the previous call's snapshot copy precedes this update
         _, _, _, gen_loss, disc_loss = TR.train_gan(self.trainer, embedding, schedule_data, self._score)
         self.epoch += 1
         self.accuracy_list.append((gen_loss, disc_loss))                          # PreGAN.py:67
         w = self.trainer.weights_numpy()
         self.weights = dict(self.weights, gen=w["gen"], disc=w["disc"])
         self.model.load_weights(self.weights)     # keep K3's packed GAN in step with the master
-        if self.save_folder is not None:           # save_gan (utils.py:86-88): Disc with epoch 0, []
-            save_checkpoints(self.trainer, self.save_folder, self.env_name, self.epoch, self.accuracy_list,
-                             [("gen", self.gen_name, None)])
-            save_checkpoints(self.trainer, self.save_folder, self.env_name, 0, [], [("disc", self.disc_name, None)])
+        if self.save_gan:                          # save_gan (utils.py:86-88): Disc with epoch 0, []
+            self._post_gan_checkpoint()
 
     # -- PreGAN.py:73-95 --
     def recover_decision(self, embedding, schedule_data, original_decision):

@@ -136,3 +136,30 @@ def fpe_bytes_per_window(H: int = 16) -> int:
     """K4's compulsory HBM I/O: window 36H + h0 12 in; scores 8H, protos 8H,
     class 4H, any 4, masked embedding 8H (to K3) out."""
     return 36 * H + 12 + 8 * H + 8 * H + 4 * H + 4 + 8 * H
+
+
+def tune_step_flops_per_window(H: int) -> int:
+    """One window of the tuning step (train.py:42-57): the Transformer's forward
+    (GAT, time encoder, 2 encoder layers, both decoders) and its backward, which
+    for every dense product forms the input gradient and the weight gradient
+    (2 x the forward's MACs): 3 x the forward's flops (the GAN is not trained
+    by tune_model)."""
+    f = flops_per_window(H)
+    return 3 * (f["gat"] + f["time_encoder"] + f["encoder_layers"] + f["decoders"])
+
+
+def gan_step_macs_per_env(H: int, hidden: int = GAN_HIDDEN) -> int:
+    """One environment of train_gan (PreGANPlus.py:60-75) on the reference's
+    formulation: Gen forward (Gen1 over [e; s], Gen2), Disc forward on [s; ns]
+    (Disc1, head); Disc step: head and Disc1 weight gradients; Gen step: the
+    updated Disc's forward again, d ns = Disc1[:, ns]^T dDD, Gen2's weight
+    gradient, dHg = Gen2^T dY, Gen1's weight gradient."""
+    gin, hh = 2 * H + H * H, H * H
+    fwd = hidden * gin + hh * hidden + hidden * 2 * hh + 2 * hidden
+    disc_step = 2 * hidden + 2 * hidden + hidden * 2 * hh            # head dW, dDD, Disc1 dW
+    gen_step = hidden * 2 * hh + 2 * hidden + 2 * hidden + 3 * hh * hidden + hidden * gin
+    return fwd + disc_step + gen_step
+
+
+def gan_step_flops_per_env(H: int) -> int:
+    return 2 * gan_step_macs_per_env(H)

@@ -1143,6 +1143,23 @@ def accuracy_scores(lg, pr, anom, cls, P):
     return anomaly_correct / n, class_correct / class_total
 
 
+def dp_groups():
+    """Process groups of the data-parallel C3 step: (tuning group,
+    GAN group).  At world size > 1 the GAN step's gradient all-reduces get a
+    communicator of their own: the GAN step runs on a second stream beside the
+    tuning step, and collectives that share one communicator run in issue
+    order on its one internal stream, so the GAN's Disc all-reduce would wait
+    for the tuning backward and its gradient all-reduce (the two streams'
+    overlap would collapse).  With two communicators each chain waits only for
+    its own peers.  Both groups span all ranks and are created in the same
+    order on every rank (torch.distributed.new_group is collective).
+    (None, None) without a process group or at world size 1."""
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return None, None
+    return None, dist.new_group(ranks=list(range(dist.get_world_size())))
+
+
 def train_gan_batched(tr: Trainer, sim, envs, emb, sched, out=None, target=None, all_reduce=False, group=None):
     """PreGANPlus.py:60-75 for a batch of environments with the label simulated
     on the device (``simulate.Simulation`` -> ``pgp_simulate``):

@@ -192,6 +192,55 @@ def synth_weights(H, seed=0):
     return w
 
 
+def torch_default_weights(H, seed=0):
+    """A new model as the reference's constructors initialise it (load_model
+    without a checkpoint, utils.py:76-78): nn.Linear weights and biases
+    U(+-1/sqrt(fan_in)) (kaiming_uniform(a=sqrt(5)) and its bias rule);
+    LayerNorm gamma 1, beta 0; nn.MultiheadAttention in_proj xavier_uniform
+    (bound sqrt(6 / (d + 3d))), in_proj_bias and out_proj.bias 0, out_proj.weight
+    the Linear rule; TransformerEncoder deep-copies its layer, so every layer
+    starts from layer 0's values; prototypes U(0,1) (torch.rand, models.py:373).
+    The distributions are torch's; the draws are numpy's (seeded), so the values
+    are not torch's own (parity unpinned: only the offline-training fallback
+    uses them).  fp32-representable doubles, as synth_weights."""
+    if H % 2:
+        raise ValueError("H must be even (d_model = H is split over 2 heads)")
+    rng = np.random.Generator(np.random.PCG64(seed))
+
+    def lin(shapes, name):
+        shp = shapes[name]
+        fan_in = shp[1] if len(shp) == 2 else shapes[name.replace("bias", "weight")][1]
+        b = 1.0 / np.sqrt(fan_in)
+        return rng.uniform(-b, b, size=shp)
+
+    def fill(shapes):
+        out = {}
+        for name, shp in shapes.items():
+            if name == "pos_encoder.pe":
+                out[name] = positional_encoding(H, shp[0])
+                continue
+            if ".layers." in name and not name.startswith("transformer_encoder.layers.0."):
+                continue   # cloned below
+            if name.endswith(("norm1.weight", "norm2.weight")):
+                a = np.ones(shp)
+            elif name.endswith(("norm1.bias", "norm2.bias", "in_proj_bias", "out_proj.bias")):
+                a = np.zeros(shp)
+            elif name.endswith("in_proj_weight"):
+                b = np.sqrt(6.0 / (shp[0] + shp[1]))
+                a = rng.uniform(-b, b, size=shp)
+            else:
+                a = lin(shapes, name)
+            out[name] = np.asarray(a, dtype=np.float32).astype(np.float64)
+        for name in shapes:
+            if ".layers." in name and name not in out:
+                out[name] = out["transformer_encoder.layers.0." + name.split(".", 3)[3]].copy()
+        return {k: out[k] for k in shapes}
+
+    w = {"transformer": fill(transformer_shapes(H)), "gen": fill(gen_shapes(H)), "disc": fill(disc_shapes(H))}
+    w["prototypes"] = rng.uniform(0, 1, size=(H, PROTO_DIM)).astype(np.float32).astype(np.float64)
+    return w
+
+
 def weights_checksum(weights):
     h = 0.0
     for sec in ("transformer", "gen", "disc"):

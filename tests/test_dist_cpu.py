@@ -169,3 +169,77 @@ def test_dp_state_single_window_is_reference_update():
     assert not np.array_equal(st2.protos, base)
     assert a2[0] == pytest.approx(a1, rel=1e-14) and l2[0] == pytest.approx(l1, rel=1e-14, abs=1e-15)
     assert st2.factor == pytest.approx(st1.factor) and (st2.num_zero, st2.num_ones) == (st1.num_zero, st1.num_ones)
+
+
+# ---- the C3 step's two communicators (tuning, GAN) ----
+class _FakeGanTrainer:
+    """Records the groups train_gan_batched hands to all_reduce_grads."""
+
+    def __init__(self):
+        self.calls = []
+        self._gan_in = (None, None)
+
+    def gan_forward(self, emb, sched):
+        return torch.zeros((2, 1)), None
+
+    def gan_disc_backward(self, target):
+        pass
+
+    def gan_gen_backward(self, B):
+        pass
+
+    def adam_step(self, section):
+        pass
+
+    def all_reduce_grads(self, section, group=None):
+        self.calls.append((section, group))
+
+
+class _FakeSim:
+    def score(self, envs, ns, orig, out=None, target=None):
+        return out, target
+
+
+def _groups_worker(rank, world, port, q):
+    from preganplus_amd import train as TR
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    tune_g, gan_g = TR.dp_groups()
+    # the GAN group is a communicator of its own over every rank
+    own = gan_g is not None and gan_g is not dist.group.WORLD
+    t = torch.tensor([float(rank + 1)])
+    dist.all_reduce(t, group=gan_g)
+    ranks = dist.get_process_group_ranks(gan_g)
+    # train_gan_batched sends both of its all-reduces to that group
+    fake = _FakeGanTrainer()
+    TR.train_gan_batched(fake, _FakeSim(), None, None, None, all_reduce=True, group=gan_g)
+    q.put((rank, own, tune_g is None, float(t.item()), ranks,
+           [(s, g is gan_g) for s, g in fake.calls]))
+    dist.destroy_process_group()
+
+
+def test_gan_collectives_use_their_own_group():
+    """at world size > 1 the C3 step's GAN
+    all-reduces go to a second process group (communicator), so they do not
+    queue behind the tuning step's gradient all-reduce on one communicator's
+    stream; the tuning step keeps the default group."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 31500 + os.getpid() % 1000
+    procs = [ctx.Process(target=_groups_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    for rank, own, tune_default, tsum, ranks, calls in res:
+        assert own and tune_default
+        assert tsum == 3.0 and ranks == [0, 1]
+        assert calls == [("disc", True), ("gen", True)]
+
+
+def test_dp_groups_single_process():
+    from preganplus_amd import train as TR
+    assert TR.dp_groups() == (None, None)

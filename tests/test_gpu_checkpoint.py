@@ -118,3 +118,75 @@ def test_plugin_save_gan_every_call_resumes(tmp_path):
     assert torch.equal(tr_b.P[t0:lo], fresh.trainer.P[t0:lo])
     ck = torch.load(tmp_path / "simulator_Disc_16.ckpt", weights_only=True)
     assert ck["epoch"] == 0 and ck["accuracy_list"] == []
+
+
+def test_pregan_save_gan_every_call_resumes(tmp_path):
+    """PreGANRecovery rewrites the Gen / Disc checkpoints after every GAN step
+    as the reference's train_gan does (PreGAN.py:66-71, save_gan utils.py:86-88),
+    by default into the folder it loaded from; a second plugin on that folder
+    (packaged FPE_16 weights, no FPE checkpoint there) resumes the first's GAN
+    weights, AdamW moments and step counts, epoch and accuracy_list."""
+    from preganplus_amd.recovery import PreGANRecovery
+    from tests.test_train_oracle_golden import fake_env
+    _, extra = W.load_npz("preganplus_amd/data/pregan_simulator_16.npz")
+    z = np.load("tests/golden/pregan_plugin_h16.npz")
+    a = PreGANRecovery(16, "", training=True, model_folder=str(tmp_path))
+    assert a.save_gan and a.save_folder == str(tmp_path)
+    e0 = a.epoch
+    for step in range(3):
+        a.setEnvironment(fake_env(z, step, extra["train_time_data"], z["schedule_series"]))
+        torch.manual_seed(2000 + step)
+        a.run_model(None, [tuple(x) for x in z[f"s{step}/decision_in"]])
+    assert a.epoch == e0 + 3
+    a.flush_checkpoints()
+    for name in ("Gen", "Disc"):
+        assert os.path.exists(tmp_path / f"simulator_{name}_16.ckpt")
+    assert not os.path.exists(tmp_path / "simulator_FPE_16.ckpt")    # the encoder is frozen, never saved
+    b = PreGANRecovery(16, "", training=True, model_folder=str(tmp_path))
+    assert b.epoch == a.epoch and b.accuracy_list == a.accuracy_list
+    lo, hi = a.trainer.sec_off["gen"], a.trainer.sec_end["disc"]
+    torch.cuda.synchronize()
+    assert torch.equal(a.trainer.P[lo:hi], b.trainer.P[lo:hi])
+    assert torch.equal(a.trainer.m[lo:hi], b.trainer.m[lo:hi]) and torch.equal(a.trainer.v[lo:hi], b.trainer.v[lo:hi])
+    sa = [t["step"] for t in a.trainer.tensors if t["section"] in ("gen", "disc")]
+    assert sa == [t["step"] for t in b.trainer.tensors if t["section"] in ("gen", "disc")]
+    ck = torch.load(tmp_path / "simulator_Disc_16.ckpt", weights_only=True)
+    assert ck["epoch"] == 0 and ck["accuracy_list"] == []
+    # injected weights (tests, benches): no save unless a folder is given
+    w, ex = W.load_npz("preganplus_amd/data/pregan_simulator_16.npz")
+    assert not PreGANRecovery(16, "", training=True, weights=w, extra=ex).save_gan
+    a.close()
+    b.close()
+    assert a._writer is None
+
+
+def test_writer_snapshots_are_never_torn(tmp_path):
+    """posting as fast as possible (no pause between writes) must
+    never hand the writer a buffer that a later post() is refilling: every
+    snapshot it writes holds one post's weights and moments throughout."""
+    from preganplus_amd import recovery as RC
+    w, _ = W.load_npz("preganplus_amd/data/simulator_16.npz")
+    tr = TR.Trainer(16, w, max_batch=1)
+    lo, hi = tr.sec_off["gen"], tr.sec_end["disc"]
+    seen = []
+
+    class Checking(RC._GanCheckpointWriter):
+        def _write(self, host, folder, env_name, epoch, acc, steps):
+            p, m, v = host
+            seen.append(epoch)
+            assert p.min() == p.max() == m.min() == m.max() == v.min() == v.max() == float(epoch), epoch
+
+    wr = Checking(tr, "Gen_16", "Disc_16", min_interval=0.0)
+    try:
+        for k in range(200):
+            wr.fence()
+            tr.P[lo:hi].fill_(float(k))
+            tr.m[lo:hi].fill_(float(k))
+            tr.v[lo:hi].fill_(float(k))
+            wr.post(str(tmp_path), "simulator", k, [])
+        wr.flush()
+    finally:
+        wr.close()
+    assert wr.error is None, wr.error
+    assert seen and seen[-1] == 199 and seen == sorted(seen)
+    assert not wr.thread.is_alive()

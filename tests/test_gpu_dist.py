@@ -3,7 +3,8 @@ the box (gloo process group: RCCL refuses two ranks on one device; the driver's
 multi-GPU runs use RCCL with one rank per GPU).
 
 Each rank runs train.dp_tune_step (device bookkeeping, gradient and state
-all-reduces) and train.train_gan_batched(all_reduce=True) on its half of the
+all-reduces, the default group) and train.train_gan_batched(all_reduce=True)
+with its all-reduces on the GAN's own group (train.dp_groups) on its half of the
 windows / environments; the result must equal one process on the
 concatenated batch (SURVEY §8e parity rule): gradients and parameters to fp32
 reduction tolerance, prototypes / counters / factor to fp64 rounding."""
@@ -45,10 +46,11 @@ def _run(sl_w, sl_e, group_init=None):
     x, y, c, emb, s = _inputs()
     tr = TR.Trainer(H, w, max_batch=B)
     st = _state0()
-    TR.dp_tune_step(tr, st, x[sl_w], y[sl_w], c[sl_w])
+    tune_group, gan_group = TR.dp_groups()   # the bench's two-communicator design
+    TR.dp_tune_step(tr, st, x[sl_w], y[sl_w], c[sl_w], group=tune_group)
     envs = SIM.synth_envs(E, H, seed=3)[sl_e]
     sim = SIM.Simulation(H, device=tr.device)
-    out, target = TR.train_gan_batched(tr, sim, envs, emb[sl_e], s[sl_e], all_reduce=True)
+    out, target = TR.train_gan_batched(tr, sim, envs, emb[sl_e], s[sl_e], all_reduce=True, group=gan_group)
     torch.cuda.synchronize()
     return (tr.G.cpu().numpy(), tr.P.cpu().numpy(), st.protos.copy(), st.num_zero, st.num_ones, st.factor,
             target.cpu().numpy())

@@ -23,8 +23,8 @@ def _series(rows=40, seed=3):
 @pytest.mark.gpu
 def test_train_model_epochs_match_backprop_loop(tmp_path):
     series = _series()
-    a = RC.PreGANPlusRecovery(16, "", save_folder=str(tmp_path))
-    b = RC.PreGANPlusRecovery(16, "", save_folder=None)
+    a = RC.PreGANPlusRecovery(16, "", model_folder=str(tmp_path / "in"), save_folder=str(tmp_path))
+    b = RC.PreGANPlusRecovery(16, "", model_folder=str(tmp_path / "in"), save_folder=None)
     e0 = a.model_epoch
     a.train_model(num_epochs=2, time_data=series)
     # the same two epochs by hand on an identical plugin

@@ -78,3 +78,44 @@ def test_weight_gradient_and_decoder_prefetches_are_covered():
                                ("dec_fwd2_kernel", "50", 128, 4)):
         cover = isa_count.load_cover(name, tag)
         assert sum(1 for c in cover if c >= need) >= n, (name, cover)
+
+
+def _pmc_files():
+    import glob
+    return sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*_h*.json")))
+
+
+@pytest.mark.skipif(not os.path.exists(LIB) or not os.path.exists("/opt/rocm/lib/llvm/bin/llvm-objdump"),
+                    reason="built library / llvm-objdump absent")
+def test_committed_pmc_traffic_matches_built_library():
+    """Every committed PMC traffic file (profiles/pmc_<kernel>_h<H>.json, the
+    source of bench.py's `traffic` fields) was taken with the kernel as it is
+    built now: its isa_sha256 equals the built library's instructions of that
+    kernel.  A kernel change without a new counter pass fails here (VERDICT r3
+    item 1: stale r02 counters were reported as r03 traffic)."""
+    import json
+    import re
+    import isa_count
+    files = _pmc_files()
+    assert files
+    for f in files:
+        d = json.load(open(f))
+        m = re.match(r"pmc_(\w+)_h(\d+)\.json", os.path.basename(f))
+        want = isa_count.kernel_isa_hash(m.group(1) + "_kernel", int(m.group(2)))
+        assert d.get("isa_sha256") == want, f"{os.path.basename(f)} is stale (taken with another build)"
+
+
+def test_bench_traffic_ignores_other_builds(tmp_path):
+    """bench.py reports a PMC file's traffic only for the batch it was taken at
+    and only when its isa_sha256 matches the loaded library's kernel."""
+    import json
+    import bench
+    p = tmp_path / "pmc.json"
+    rec = {"hbm_bytes_per_launch": 123.0, "batch": 64, "isa_sha256": "0" * 64}
+    p.write_text(json.dumps(rec))
+    assert bench.traffic_record(50, 64, "encoder", path=str(p)) is None       # another build
+    rec["isa_sha256"] = bench.loaded_isa_hash("encoder_kernel", 50)
+    if rec["isa_sha256"] is not None:
+        p.write_text(json.dumps(rec))
+        assert bench.traffic_record(50, 64, "encoder", path=str(p))["hbm_bytes_per_launch"] == 123.0
+        assert bench.traffic_record(50, 65, "encoder", path=str(p)) is None   # another batch

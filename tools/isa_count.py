@@ -66,6 +66,39 @@ def encoder_counts(Hs=(16, 50), lib=LIB):
     return out
 
 
+_ASM_CACHE = {}
+
+
+def _all_asm(lib):
+    """Disassembly of every gfx950 code object of `lib` (cached per path and mtime)."""
+    key = (os.path.abspath(lib), os.path.getmtime(lib))
+    if key not in _ASM_CACHE:
+        _ASM_CACHE[key] = _disasm(lib, "")
+    return _ASM_CACHE[key]
+
+
+def kernel_isa_hash(name, H=None, lib=LIB):
+    """sha256 of kernel `name` (template argument H if given) as BUILT in `lib`:
+    its instruction text with addresses and encodings stripped, so it changes
+    when that kernel's code changes and not when another kernel moves it.  The
+    PMC traffic files (profiles/pmc_*.json) carry it; bench.py reports a
+    file's traffic only while the loaded library's kernel still hashes the
+    same.  None when the kernel is not found."""
+    import hashlib
+    asm = _all_asm(lib)
+    targ = rf"ILi{H}E" if H is not None else ""
+    m = re.search(rf"^[0-9a-f]+ <(_ZN3pgp12_GLOBAL__N_1\d+{name}{targ}[^>]*)>:\n(.*?)(?=^[0-9a-f]+ <|\Z)", asm,
+                  re.S | re.M)
+    if m is None:
+        return None
+    lines = []
+    for line in m.group(2).splitlines():
+        t = line.split("//")[0].strip()
+        if t:
+            lines.append(re.sub(r"\s+", " ", t))
+    return hashlib.sha256("\n".join(lines).encode()).hexdigest()
+
+
 if __name__ == "__main__":
     Hs = [int(h) for h in sys.argv[1:]] or [16, 50]
     for H, (mfma, valu) in encoder_counts(Hs).items():

@@ -3,30 +3,56 @@
 Correction (MI355X_MICROARCH.md §HBM): on gfx950 FETCH_SIZE reports 1/2 of
 the bytes of a wide (16 B/lane) coalesced read; WRITE_SIZE is exact for
 16-B-per-lane stores.  We report both the raw counters and the corrected figure
-(2 x FETCH + WRITE), in bytes per launch, averaged over the timed dispatches.
-usage: python tools/pmc_traffic.py gpurun_out/<tag> BATCH [H]
-"""
-import csv, glob, json, re, sys, collections
+(2 x FETCH + WRITE), in bytes per launch, averaged over the dispatches.
 
-root, batch = sys.argv[1], int(sys.argv[2])
-H = int(sys.argv[3]) if len(sys.argv) > 3 else 50
-vals = collections.defaultdict(lambda: collections.defaultdict(list))
-for f in glob.glob(f"{root}/pmc*/run_counter_collection.csv"):
-    for row in csv.DictReader(open(f)):
-        name = re.sub(r"\(.*$", "", row["Kernel_Name"].replace("void pgp::(anonymous namespace)::", ""))
-        vals[name][row["Counter_Name"]].append(float(row["Counter_Value"]))
-out = {}
-for k, d in vals.items():
-    if "FETCH_SIZE" not in d or "WRITE_SIZE" not in d:
-        continue
-    fe = sum(d["FETCH_SIZE"]) / len(d["FETCH_SIZE"]) * 1024
-    wr = sum(d["WRITE_SIZE"]) / len(d["WRITE_SIZE"]) * 1024
-    out[k] = {"fetch_bytes_raw": fe, "write_bytes": wr, "hbm_bytes_per_launch": 2 * fe + wr}
-    print(f"{k:28s} FETCH {fe/1e6:10.1f} MB  WRITE {wr/1e6:10.1f} MB  corrected {(2*fe+wr)/1e6:10.1f} MB")
-for k, v in out.items():
-    m = re.match(r"(\w+?)_kernel<(\d+)>", k)
-    if m and int(m.group(2)) == H:
-        v.update({"batch": batch, "kernel": k,
-                  "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; "
-                            "hbm = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 wide-read correction)"})
-        json.dump(v, open(f"profiles/pmc_{m.group(1)}_h{H}.json", "w"), indent=1)
+Each kernel<H> of the run is written to profiles/pmc_<kernel>_h<H>.json,
+stamped with the batch, the run it came from and the sha256 of that kernel's
+instructions in the library the counters were taken with
+(tools/isa_count.kernel_isa_hash; run this right after the GPU call, against
+the same in-tree build): bench.py reports the traffic only while the loaded
+library's kernel hashes the same, and tests/test_roofline_isa.py fails when a
+committed file is stale.
+usage: python tools/pmc_traffic.py gpurun_out/<tag> BATCH H [kernel ...]
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import re
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import isa_count  # noqa: E402
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def main():
+    root, batch, H = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
+    only = set(sys.argv[4:])
+    vals = collections.defaultdict(lambda: collections.defaultdict(list))
+    for f in glob.glob(f"{root}/pmc*/run_counter_collection.csv"):
+        for row in csv.DictReader(open(f)):
+            name = re.sub(r"\(.*$", "", row["Kernel_Name"].replace("void pgp::(anonymous namespace)::", ""))
+            vals[name][row["Counter_Name"]].append(float(row["Counter_Value"]))
+    for k, d in sorted(vals.items()):
+        if "FETCH_SIZE" not in d or "WRITE_SIZE" not in d:
+            continue
+        fe = sum(d["FETCH_SIZE"]) / len(d["FETCH_SIZE"]) * 1024
+        wr = sum(d["WRITE_SIZE"]) / len(d["WRITE_SIZE"]) * 1024
+        print(f"{k:28s} FETCH {fe / 1e6:10.1f} MB  WRITE {wr / 1e6:10.1f} MB  corrected {(2 * fe + wr) / 1e6:10.1f} MB"
+              f"  (n={len(d['FETCH_SIZE'])})")
+        m = re.match(r"(\w+?)_kernel<(\d+)>", k)
+        if not m or int(m.group(2)) != H or (only and m.group(1) not in only):
+            continue
+        h = isa_count.kernel_isa_hash(m.group(1) + "_kernel", H)
+        out = {"fetch_bytes_raw": fe, "write_bytes": wr, "hbm_bytes_per_launch": 2 * fe + wr, "batch": batch,
+               "kernel": k, "dispatches": len(d["FETCH_SIZE"]), "isa_sha256": h, "source": os.path.relpath(root, ROOT),
+               "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; "
+                         "hbm = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 wide-read correction)"}
+        json.dump(out, open(os.path.join(ROOT, "profiles", f"pmc_{m.group(1)}_h{H}.json"), "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
