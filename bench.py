@@ -299,12 +299,7 @@ def _dist_setup():
         # driver's runs, one GPU per rank, keep the GAN / tuning overlap)
         os.environ["PGP_BENCH_ONE_STREAM"] = "1"
         os.environ["PGP_TUNE_SIDE_STREAM"] = "0"
-    elif world > 1:
-        # one GPU per rank: main + GAN stream + the two communicators' internal
-        # streams (tuning, GAN) = the 4 hardware queues a process gets
-        # (GPU_MAX_HW_QUEUES); the library's low-priority side stream would be a
-        # fifth, sharing a queue with one of them, so it is off
-        os.environ.setdefault("PGP_TUNE_SIDE_STREAM", "0")
+
     if dev_env == "cpu":
         device = torch.device("cpu")
     else:
@@ -326,6 +321,35 @@ def _dist_setup():
 
 
 _HOST_ISSUE_S = None
+
+
+GAN_RESERVED_CUS = 8   # CUs the fused tuning launches leave to the GAN step beside them (pgp_tune_reserve_cus)
+
+
+def _reserve_cus(main, side):
+    """With the GAN step on a second stream beside the tuning step, the fused
+    tuning launches leave GAN_RESERVED_CUS CUs to it: they hold whole CUs and
+    deal their units statically, so a CU taken by a GAN workgroup would hold
+    back the whole launch (and the GAN workgroups would wait for CUs the fused
+    launches hold).  Returns the count set."""
+    n = GAN_RESERVED_CUS if side is not main else 0
+    L = _native.lib()
+    L.pgp_tune_reserve_cus.argtypes = [ctypes.c_int]
+    L.pgp_tune_reserve_cus.restype = ctypes.c_int
+    _native.check(L.pgp_tune_reserve_cus(n), "pgp_tune_reserve_cus")
+    return n
+
+
+def _share_side_stream(world, main, side):
+    """At world size > 1 with a second stream: make it the tuning backward's
+    side stream too (see bench_tune); returns whether it did."""
+    if world == 1 or side is main:
+        return False
+    L = _native.lib()
+    L.pgp_tune_set_side_stream.argtypes = [ctypes.c_void_p]
+    L.pgp_tune_set_side_stream.restype = ctypes.c_int
+    _native.check(L.pgp_tune_set_side_stream(ctypes.c_void_p(side.cuda_stream)), "pgp_tune_set_side_stream")
+    return True
 
 
 def _backend_label():
@@ -520,6 +544,14 @@ def bench_tune(args):
     # tests/test_gpu_dist.py and test_gpu_tunedp.py run them in either order)
     main = torch.cuda.current_stream(device)
     side = main if os.environ.get("PGP_BENCH_ONE_STREAM") == "1" else torch.cuda.Stream(device)
+    # world > 1, one GPU per rank: main + this second stream + the two
+    # communicators' streams are the 4 hardware queues a process gets
+    # (GPU_MAX_HW_QUEUES), so the tuning backward's side work (decoder and
+    # in_proj weight gradients) runs on this same second stream instead of a
+    # fifth (pgp_tune_set_side_stream), and the GAN step is issued right after
+    # detect, ahead of that side work
+    shared_side = _share_side_stream(world, main, side)
+    reserved = _reserve_cus(main, side)
 
     # detect reads the step-start weights and feeds only the GAN step, so it
     # runs on the second stream too, with a workspace of its own; the tuning
@@ -555,9 +587,16 @@ def bench_tune(args):
                 if e is not None:
                     e[3].record(side)
 
-        tun.step(wins, y, cls, mark=(lambda k: se[k].record(main)) if se is not None else None,
-                 before_update=det_done, after_forward=detect)
-        gan()   # (issued with detect, before the backward: no faster, profiles/r03/s3/)
+        if shared_side:
+            def detect_gan():
+                detect()
+                gan()
+            tun.step(wins, y, cls, mark=(lambda k: se[k].record(main)) if se is not None else None,
+                     before_update=det_done, after_forward=detect_gan)
+        else:
+            tun.step(wins, y, cls, mark=(lambda k: se[k].record(main)) if se is not None else None,
+                     before_update=det_done, after_forward=detect)
+            gan()   # (issued with detect, before the backward: no faster at N=1, profiles/r03/s3/)
         main.wait_stream(side)
         rec(4)
 
@@ -620,7 +659,8 @@ def bench_tune(args):
                                                                            if world > 1 else "")},
             "stage_ms": {n: float(stage[k]) for k, n in enumerate(names)},
             "streams": "detect + train_gan on a second stream, concurrent with tune_model (no shared data; the "
-                       "tuning step's weight update waits for detect)",
+                       "tuning step's weight update waits for detect)" if side is not main else "one stream",
+            "reserved_cus": reserved,
             "tune_model_ms": {n: float(sub[k]) for k, n in enumerate(subs)},
             "grad_all_reduce_ms": float(sub[subs.index("all_reduce")]),
             "roofline": roof,
@@ -948,6 +988,8 @@ def bench_loop(args):
     acc = np.zeros(len(names))
     main = torch.cuda.current_stream(device)
     side = main if os.environ.get("PGP_BENCH_ONE_STREAM") == "1" else torch.cuda.Stream(device)
+    shared_side = _share_side_stream(world, main, side)   # see bench_tune
+    _reserve_cus(main, side)
 
     def interval(timed=False):
         if timed:
@@ -964,14 +1006,20 @@ def bench_loop(args):
         # the GAN step on a second stream beside the tuning step (no shared
         # data, see bench_tune); the repack reads both sections of the master
         side.wait_stream(main)
-        tun.step(x, y, cls)          # issued first (see bench_tune)
+
+        def gan_step():
+            with torch.cuda.stream(side):
+                TR.train_gan_batched(tr, sim, envs, emb, sched, out=sim_out, target=gan_target, all_reduce=True,
+                                     group=gan_group)
+                if timed:
+                    ev[3].record(side)
+        if shared_side:              # ahead of the tuning backward's side work on the shared stream
+            gan_step()
+        tun.step(x, y, cls)          # issued first at N = 1 (see bench_tune)
         if timed:
             ev[4].record(main)
-        with torch.cuda.stream(side):
-            TR.train_gan_batched(tr, sim, envs, emb, sched, out=sim_out, target=gan_target, all_reduce=True,
-                                 group=gan_group)
-            if timed:
-                ev[3].record(side)
+        if not shared_side:
+            gan_step()
         main.wait_stream(side)
         model.repack_master(tr.P, tun.state[:2 * K])
         if timed:

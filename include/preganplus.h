@@ -199,9 +199,10 @@ int pgp_forward_fpe_stage(pgp_model* m, int stage, int batch, const float* windo
  *                      and arrives as y, mult, tgt) + backward into G
  *                      (loss.backward(), train.py:53)
  *   pgp_gan_forward    Gen + Disc forward (PreGANPlus.py:62-63)
- *   pgp_gan_disc_backward  BCE(probs, target) backward into the Disc grads (:66-67)
+ *   pgp_gan_disc_backward  BCE(probs, target) backward; the Disc grads are
+ *                      WRITTEN (not accumulated) into G's disc section (:66-67)
  *   pgp_gan_gen_backward   Disc forward with the updated Disc, BCE toward [0,1],
- *                      backward into the Gen grads (:69-74)
+ *                      backward; the Gen grads are written into G's gen section (:69-74)
  *   pgp_adamw          torch.optim.AdamW.step (utils.py:65)
  * ---------------------------------------------------------------------- */
 size_t pgp_master_len(int n_hosts);               /* floats in P / G            */
@@ -209,8 +210,8 @@ size_t pgp_master_len(int n_hosts);               /* floats in P / G            
  * the backward, token-major, plus split-K / weight-gradient partial slabs).
  * Sizes grow with batch: a workspace for B_max serves every batch <= B_max. */
 size_t pgp_tune_workspace_len(int n_hosts, int batch);
-/* floats of GAN-step workspace for a batch (per-window activation rows, split-K
- * partials, weight transposes); grows with batch like the tuning workspace. */
+/* floats of GAN-step workspace for a batch (one activation row per
+ * environment); grows with batch like the tuning workspace. */
 size_t pgp_gan_workspace_len(int n_hosts, int batch);
 size_t pgp_master_offset(int n_hosts, int section); /* 0 transformer, 1 gen, 2 disc */
 
@@ -231,7 +232,20 @@ int pgp_tune_backward(int n_hosts, int batch, const float* P, float* G, float* w
  * and joined back into it before the call's last launch, so every result is
  * ordered on `stream` as if all of it ran there.  While `stream` is being
  * captured into a graph, or with PGP_TUNE_SIDE_STREAM=0 in the environment,
- * everything stays on `stream`. */
+ * everything stays on `stream`.
+ * pgp_tune_set_side_stream(s): use the caller's stream `s` as that side stream
+ * on the current device from now on (NULL: the library's own again).  A
+ * data-parallel caller that already runs a second stream (the GAN step) and two
+ * communicators keeps its streams within the hardware queues this way. */
+int pgp_tune_set_side_stream(void* stream);
+/* pgp_tune_reserve_cus(n): the fused encoder launches of pgp_tune_forward /
+ * pgp_tune_backward use at most (CUs - n) workgroups (one per CU; at most half
+ * the CUs are reserved), leaving n CUs free for a concurrent stream (the GAN
+ * step beside the tuning step): a fused launch deals its units to its waves
+ * statically, so a CU held by another stream's workgroup would hold back the
+ * whole launch.  Default 0.  Results do not depend on it beyond fp32 summation
+ * grouping of the weight gradients (one slab per workgroup). */
+int pgp_tune_reserve_cus(int n);
 /* Profiling: with pgp_tune_timing(1), pgp_tune_forward / pgp_tune_backward
  * record HIP events on their stream around each fused encoder launch
  * (pgp_tunef.hip); pgp_tune_fused_ms(ms6) synchronises on them and returns the

@@ -13,6 +13,7 @@
 #include "pgp_repack.hpp"
 #include "pgp_train.hpp"
 #include "pgp_tune.hpp"
+#include "pgp_tunef.hpp"
 #include "pgp_tunedp.hpp"
 
 #include <vector>
@@ -355,6 +356,17 @@ int pgp_tune_backward(int n_hosts, int batch, const float* P, float* G, float* w
   tune_plan(n_hosts, batch, &p);
   HIPCHK(launch_tune_backward(p, P, G, workspace, logits, protos, y, mult, tgt,
                               reinterpret_cast<hipStream_t>(stream)));
+  return PGP_OK;
+}
+
+int pgp_tune_reserve_cus(int n) {
+  if (n < 0) return fail(PGP_ERR_ARG, "negative CU count");
+  tf_reserve_cus(n);
+  return PGP_OK;
+}
+
+int pgp_tune_set_side_stream(void* stream) {
+  HIPCHK(tune_set_side_stream(reinterpret_cast<hipStream_t>(stream)));
   return PGP_OK;
 }
 

@@ -1,19 +1,37 @@
 // pgp_gantrain.hip — the GAN step (PreGANPlus.py:60-81) over a batch of
-// windows as fp32 MFMA GEMMs: Gen + Disc forward (models.py:118-151,
-// 258-291), Disc BCE backward, then Gen BCE backward through the updated Disc.
+// environments: Gen + Disc forward (models.py:118-151, 258-291), Disc BCE
+// backward, then Gen BCE backward through the updated Disc — in five launches
+// (plus the simulator between forward and Disc step, pgp_sim.hip):
 //
-// Layout: one scratch row per window (row stride GS_SIZE, pgp_train.hpp) holds
-// that window's activations, every segment 16-byte aligned, so the batch's
-// rows of one segment form a strided [B][width] matrix:
-//   X  = [emb; s] (GIN = 2H + H^2), Z = [s; ns] (DIN = 2H^2), Hg (64), T = tanh
-//   (H^2), DD (64), P (2), dOut (2), dDD (64), dY (H^2), dHg (64).
-// Products with a long contraction (Gen1 over GIN, Disc1 over DIN, dHg over H^2)
-// are split-K GEMMs (gemm_nt_kernel, partial slabs summed in a fixed order by
-// the epilogue kernel); the wide ones (Gen2, dZ over H^2 outputs) tile the
-// outputs.  Weight gradients sum over the batch's windows with the LDS-staged
-// MFMA core shared with the tuning step (dw_accumulate): one workgroup per
-// 64x64 output block, written once into G (deterministic).  The 2-way Disc
-// head, its softmax and the BCE gradient are one wave per window.
+//   gan_fwd_kernel     per 16-environment block: Gen1 over [e; s] and Disc1's
+//                      schedule half in one pass over the input, Gen2 + tanh +
+//                      ns = s + 4 tanh tile by tile with Disc1's ns half
+//                      accumulated from each tile as it is produced, the head
+//                      and softmax;
+//   disc_head_kernel   BCE gradient toward the simulated label -> dOut, dDD;
+//   outer_kernel       the Disc's weight / bias gradients (sums over the batch
+//                      of outer products, written into G);
+//   gan_gen_kernel     per block: Disc1 with the UPDATED Disc, head, BCE toward
+//                      [0, 1] -> dDD', then tile by tile d ns = Disc1[:, ns]^T dDD',
+//                      dY = 4 d ns (1 - tanh^2) and dHg = Gen2^T dY accumulated
+//                      from each tile;
+//   outer_kernel       the Gen's weight / bias gradients.
+//
+// A block is 16 environments on the lane columns of v_mfma_f32_16x16x4_f32
+// (column j = lane & 15); its 8 waves split the contraction of each product
+// (Gen1 / Disc1 chunks of 16 inputs, Gen2 / d ns output tiles of 16 rows) and
+// combine their partial accumulators through LDS in wave order (deterministic).
+// Accumulator registers feed the next product directly: a Gen2 tile (rows =
+// schedule entries n, columns = environments) is the B operand of Disc1's ns
+// half, a dY tile that of Gen2^T, so neither ns nor dY is re-read.  Weights are
+// A operands read straight from the master P (L2-resident, 2.6 MB at H = 50).
+// The weight gradients contract over the environments: each wave owns a 64 x 64
+// block of one gradient matrix, one MFMA k-step per 4 environments, written
+// once (no zero-fill, no split slabs).
+//
+// Per-environment scratch rows (TGeo::GS_*, one row of GS_SIZE floats each) keep
+// what the later launches read: emb (GS_X), [s; ns] (GS_Z), Hg, tanh, DD, the
+// probabilities, dOut, dDD, dY, dHg.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -25,93 +43,207 @@
 namespace pgp {
 namespace {
 
-// part[s][m][n0 + n] = sum over k in split s of X[m][k] W[n0 + n][k], n < 64 of
-// output group blockIdx.y; 4 waves x 16 rows; K a multiple of 4.
-__global__ __launch_bounds__(256) void gemm_nt_kernel(int M, int N, int K, const float* __restrict__ X, long ldx,
-                                                      const float* __restrict__ W, long ldw, int S, int ldp,
-                                                      float* __restrict__ part) {
-  constexpr int NT = 4;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, g = lane >> 4, i = lane & 15;
-  const long m = ((long)blockIdx.x * 4 + wv) * 16 + i;
-  const bool ok = m < M;
-  const int n0 = blockIdx.y * 64, s = blockIdx.z;
-  const int kbt = (K + 15) / 16;
-  const int kb0 = (int)((long)kbt * s / S), kb1 = (int)((long)kbt * (s + 1) / S);
-  f32x4 acc[NT];
+constexpr int kGW = 8;     // waves per block workgroup (2 per SIMD)
+constexpr int kHP = 68;    // LDS pitch of a [env][64] hidden array (bank spread)
+
+// masked 16-byte loads select this ADDRESS (never written), so a prefetched
+// value is not waited for at the select
+__device__ __attribute__((aligned(16))) float gk_zero[16];
+
+template <int H>
+struct GanK {
+  using G = TGeo<H>;
+  static constexpr int HH = H * H, E2 = 2 * H, GIN = G::GIN, DIN = G::DIN;
+  static constexpr int KE = (E2 + 15) / 16;   // emb chunks of 16 inputs
+  static constexpr int KS = (HH + 15) / 16;   // schedule chunks = Gen2 / d ns output tiles
+  static constexpr int KZ = (DIN + 15) / 16;  // [s; ns] chunks
+  static_assert(HH % 4 == 0 && E2 % 4 == 0, "16-byte groups never straddle the end of a segment");
+};
+
+// the kGW waves' partial accumulators acc[4] (per lane) -> their sum in wave
+// order, as out[tile t][lane][r] (row 16t + 4g + r, column lane & 15); red holds
+// kGW * 4 * 256 floats; ends with a barrier
+PGP_DEV void reduce4(float* red, const f32x4 (&acc)[4], int wv, int lane) {
 #pragma unroll
-  for (int t = 0; t < NT; ++t) acc[t] = zero4();
-  const float* xr = X + m * ldx + 4 * g;
-  bool nok[NT];
-  const float* wr[NT];
+  for (int t = 0; t < 4; ++t)
+    *reinterpret_cast<f32x4*>(red + ((wv * 4 + t) * 64 + lane) * 4) = acc[t];
+  __syncthreads();
+  for (int k = threadIdx.x; k < 4 * 256; k += blockDim.x) {
+    float v = red[k];
 #pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    nok[t] = n0 + 16 * t + i < N;
-    wr[t] = W + (long)(n0 + 16 * t + i) * ldw + 4 * g;
+    for (int w = 1; w < kGW; ++w) v += red[w * 1024 + k];
+    red[k] = v;
   }
-  for (int kb = kb0; kb < kb1; ++kb) {
-    const bool kok = 16 * kb + 4 * g < K;
-    const f32x4 xv = (ok && kok) ? ld4(xr + 16 * kb) : zero4();
+  __syncthreads();
+}
+// element k of reduce4's result -> (hidden row h, column j)
+PGP_DEV void red_index(int k, int& h, int& j) {
+  const int t = k >> 8, l = (k >> 2) & 63, r = k & 3;
+  h = 16 * t + 4 * (l >> 4) + r;
+  j = l & 15;
+}
+
+// the 2-way Disc head (models.py:146-151: Linear(64, 2), Softmax) of the block's
+// 16 environments from DD in LDS (ddl[env][h]); p -> pl[env][2].  Thread-serial
+// 64-term dot products.
+PGP_DEV void head16(const float* ddl, const float* __restrict__ Pd2, const float* __restrict__ db2, float* zl,
+                    float* pl) {
+  const int t = threadIdx.x;
+  if (t < 32) {
+    const int j = t >> 1, o = t & 1;
+    float z = 0.f;
+    for (int h = 0; h < 64; ++h) z = fmaf(Pd2[o * 64 + h], ddl[j * kHP + h], z);
+    zl[t] = z + db2[o];
+  }
+  __syncthreads();
+  if (t < 16) {
+    const float z0 = zl[2 * t], z1 = zl[2 * t + 1];
+    const float mx = fmaxf(z0, z1), e0 = expf(z0 - mx), e1 = expf(z1 - mx);
+    pl[2 * t] = e0 / (e0 + e1);
+    pl[2 * t + 1] = e1 / (e0 + e1);
+  }
+  __syncthreads();
+}
+
+// ---------------------------------------------------------------------------
+// Gen + Disc forward of a block of 16 environments
+// ---------------------------------------------------------------------------
+template <int H>
+__global__ __launch_bounds__(kGW * 64) void gan_fwd_kernel(int B, const float* __restrict__ emb,
+                                                           const float* __restrict__ sched,
+                                                           const float* __restrict__ Pg, const float* __restrict__ Pd,
+                                                           float* __restrict__ rows, float* __restrict__ ns_out,
+                                                           float* __restrict__ probs) {
+  using K = GanK<H>;
+  using G = TGeo<H>;
+  constexpr int HH = K::HH, E2 = K::E2, GIN = K::GIN, DIN = K::DIN;
+  __shared__ __attribute__((aligned(16))) float red[kGW * 4 * 256];
+  __shared__ __attribute__((aligned(16))) float hgl[16 * kHP];   // Hg [env][hidden]
+  __shared__ __attribute__((aligned(16))) float dsl[16 * kHP];   // Disc1's schedule half, then DD
+  __shared__ float zl[32], pl[32];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, g = lane >> 4, i = lane & 15;
+  const long env = (long)blockIdx.x * 16 + i;
+  const bool eok = env < B;
+  float* row = rows + (eok ? env : 0) * G::GS_SIZE;
+  const float* W1 = Pg + G::G_W1;
+  const float* D1 = Pd + G::D_W1;
+
+  // 1. Gen1 = W1 [e; s] and Disc1's schedule half D1[:, :HH] s, one pass over
+  //    the input chunks (16 inputs each, k-step r <-> input 16c + 4g + r)
+  f32x4 aG[4], aD[4];
 #pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      const f32x4 wf = (nok[t] && kok) ? ld4(wr[t] + 16 * kb) : zero4();
-      acc[t] = mfma(wf[0], xv[0], acc[t]);
-      acc[t] = mfma(wf[1], xv[1], acc[t]);
-      acc[t] = mfma(wf[2], xv[2], acc[t]);
-      acc[t] = mfma(wf[3], xv[3], acc[t]);
+  for (int t = 0; t < 4; ++t) aG[t] = aD[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int c = wv; c < K::KE; c += kGW) {  // embedding chunks
+    const int f = 16 * c + 4 * g;
+    const bool fok = f < E2;
+    const f32x4 bv = ld4(fok && eok ? emb + env * E2 + f : gk_zero);
+    f32x4 wa[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) wa[t] = ld4(fok ? W1 + (long)(16 * t + i) * GIN + f : gk_zero);
+    if (fok && eok) st4(row + G::GS_X + f, bv);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) aG[t] = mfma(wa[t][r], bv[r], aG[t]);
+  }
+  for (int c = wv; c < K::KS; c += kGW) {  // schedule chunks
+    const int f = 16 * c + 4 * g;
+    const bool fok = f < HH;
+    const f32x4 bv = ld4(fok && eok ? sched + env * HH + f : gk_zero);
+    f32x4 wa[4], wd[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      wa[t] = ld4(fok ? W1 + (long)(16 * t + i) * GIN + E2 + f : gk_zero);
+      wd[t] = ld4(fok ? D1 + (long)(16 * t + i) * DIN + f : gk_zero);
+    }
+    if (fok && eok) st4(row + G::GS_Z + f, bv);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        aG[t] = mfma(wa[t][r], bv[r], aG[t]);
+        aD[t] = mfma(wd[t][r], bv[r], aD[t]);
+      }
+  }
+  // Hg = W1 [e; s] + b1 (LeakyReLU(True): slope 1, the identity, models.py:127)
+  reduce4(red, aG, wv, lane);
+  for (int k = threadIdx.x; k < 1024; k += blockDim.x) {
+    int h, j;
+    red_index(k, h, j);
+    const float v = red[k] + Pg[G::G_B1 + h];
+    hgl[j * kHP + h] = v;
+    if ((long)blockIdx.x * 16 + j < B) rows[((long)blockIdx.x * 16 + j) * G::GS_SIZE + G::GS_H + h] = v;
+  }
+  __syncthreads();
+  reduce4(red, aD, wv, lane);
+  for (int k = threadIdx.x; k < 1024; k += blockDim.x) {
+    int h, j;
+    red_index(k, h, j);
+    dsl[j * kHP + h] = red[k];
+  }
+  __syncthreads();
+
+  // 2. Gen2 tiles: T = tanh(W2 Hg + b2), ns = s + 4 T (models.py:128-133);
+  //    Disc1's ns half accumulated from each tile (the tile is its B operand)
+  f32x4 hb[4];  // Hg as the B operand of the 16 hidden k-steps
+#pragma unroll
+  for (int q = 0; q < 4; ++q) hb[q] = ld4(hgl + i * kHP + 16 * q + 4 * g);
+  const float* W2 = Pg + G::G_W2;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) aD[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int c = wv; c < K::KS; c += kGW) {
+    const int n0 = 16 * c, n = n0 + 4 * g;  // this lane's output rows n .. n + 3
+    const bool nok = n < HH, rok = n0 + i < HH;
+    f32x4 acc = ld4(nok ? Pg + G::G_B2 + n : gk_zero);
+    f32x4 wa[4], wd[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) wa[q] = ld4(rok ? W2 + (long)(n0 + i) * 64 + 16 * q + 4 * g : gk_zero);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) wd[t] = ld4(nok ? D1 + (long)(16 * t + i) * DIN + HH + n : gk_zero);
+    const f32x4 s4 = ld4(nok && eok ? sched + env * HH + n : gk_zero);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc = mfma(wa[q][r], hb[q][r], acc);
+    f32x4 tv, nv;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      tv[r] = tanhf(acc[r]);
+      nv[r] = s4[r] + 4.0f * tv[r];
+    }
+    if (nok && eok) {
+      st4(row + G::GS_T + n, tv);
+      st4(row + G::GS_Z + HH + n, nv);
+      st4(ns_out + env * HH + n, nv);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) aD[t] = mfma(wd[t][r], nv[r], aD[t]);
+  }
+  // DD = Disc1 [s; ns] + db1 (LeakyReLU(True) = identity, models.py:145)
+  reduce4(red, aD, wv, lane);
+  for (int k = threadIdx.x; k < 1024; k += blockDim.x) {
+    int h, j;
+    red_index(k, h, j);
+    const float v = (red[k] + dsl[j * kHP + h]) + Pd[G::D_B1 + h];
+    dsl[j * kHP + h] = v;
+    if ((long)blockIdx.x * 16 + j < B) rows[((long)blockIdx.x * 16 + j) * G::GS_SIZE + G::GS_DD + h] = v;
+  }
+  __syncthreads();
+  head16(dsl, Pd + G::D_W2, Pd + G::D_B2, zl, pl);
+  if (threadIdx.x < 32) {
+    const long e = (long)blockIdx.x * 16 + (threadIdx.x >> 1);
+    if (e < B) {
+      rows[e * G::GS_SIZE + G::GS_P + (threadIdx.x & 1)] = pl[threadIdx.x];
+      if (probs) probs[2 * e + (threadIdx.x & 1)] = pl[threadIdx.x];
     }
   }
-  if (ok) {
-#pragma unroll
-    for (int t = 0; t < NT; ++t) st4(part + ((long)s * M + m) * ldp + n0 + 16 * t + 4 * g, acc[t]);
-  }
 }
 
-enum : int { GE_BIAS = 0, GE_TANH = 1, GE_DY = 2 };
-
-// epilogue of a split GEMM: v = sum_s part[s][m][n] (+ bias[n]), n < N, then
-//   GE_BIAS: out[m*ldo + n] = v
-//   GE_TANH: t = tanh(v) -> out (T);  ns = sched + 4 t -> out2 (Z's ns half) and ns_out
-//   GE_DY:   out = 4 v (1 - T^2), T read from aux
-__global__ __launch_bounds__(256) void gemm_epi_kernel(int mode, int M, int N, int S, int ldp,
-                                                       const float* __restrict__ part, const float* __restrict__ bias,
-                                                       float* __restrict__ out, long ldo, const float* __restrict__ aux,
-                                                       float* __restrict__ out2, float* __restrict__ ns_out) {
-  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
-  if (idx >= (long)M * N) return;
-  const long m = idx / N;
-  const int n = (int)(idx - m * N);
-  // the S split partials in split order, loads issued 8 at a time (one
-  // dependent round trip per split made this latency-bound at S = 128)
-  const float* pp = part + m * ldp + n;
-  const long ss = (long)M * ldp;
-  float v = 0.f;
-  int s = 0;
-  for (; s + 8 <= S; s += 8) {
-    float q[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) q[j] = pp[(s + j) * ss];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v += q[j];
-  }
-  for (; s < S; ++s) v += pp[s * ss];
-  if (bias) v += bias[n];  // LeakyReLU(True) = identity (models.py:127,145)
-  if (mode == GE_BIAS) {
-    out[m * ldo + n] = v;
-  } else if (mode == GE_TANH) {
-    const float t = tanhf(v);
-    out[m * ldo + n] = t;
-    const float nv = aux[m * ldo + n] + 4.0f * t;  // aux: the schedule half of Z
-    out2[m * ldo + n] = nv;
-    ns_out[m * N + n] = nv;
-  } else {
-    const float t = aux[m * ldo + n];
-    out[m * ldo + n] = 4.0f * v * (1.f - t * t);
-  }
-}
-
-// one wave per window: the Disc head (models.py:146-151: Linear(64,2), Softmax),
-// then (mode >= 1) nn.BCELoss's gradient toward the target (mean over the 2
-// probabilities, PreGANPlus.py:66-67,72-73) back through the softmax and the
+// one wave per environment: the Disc head (models.py:146-151) from DD in the
+// row, then (mode >= 1) nn.BCELoss's gradient toward the target (mean over the
+// 2 probabilities, PreGANPlus.py:66-67,72-73) back through the softmax and the
 // head: dOut (2) and dDD = D2^T dOut (64).  mode 1: target from tgt[b]; mode 2: [0,1].
 template <int H>
 __global__ __launch_bounds__(256) void disc_head_kernel(int B, int mode, const float* __restrict__ Pd,
@@ -149,95 +281,206 @@ __global__ __launch_bounds__(256) void disc_head_kernel(int B, int mode, const f
   S[G::GS_DDD + lane] = Pd[G::D_W2 + lane] * do0 + Pd[G::D_W2 + 64 + lane] * do1;
 }
 
-// write the Gen input [emb; s] and Z's schedule half
+// ---------------------------------------------------------------------------
+// Gen backward of a block through the updated Disc
+// ---------------------------------------------------------------------------
 template <int H>
-__global__ __launch_bounds__(256) void gan_in_kernel(int B, const float* __restrict__ emb,
-                                                     const float* __restrict__ sched, float* __restrict__ scr) {
+__global__ __launch_bounds__(kGW * 64) void gan_gen_kernel(int B, const float* __restrict__ Pg,
+                                                           const float* __restrict__ Pd, float* __restrict__ rows) {
+  using K = GanK<H>;
   using G = TGeo<H>;
-  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
-  if (idx >= (long)B * G::GIN) return;
-  const long b = idx / G::GIN;
-  const int k = (int)(idx - b * G::GIN);
-  float* S = scr + b * G::GS_SIZE;
-  if (k < 2 * H) {
-    S[G::GS_X + k] = emb[b * 2 * H + k];
-  } else {
-    const float s = sched[b * H * H + k - 2 * H];
-    S[G::GS_X + k] = s;
-    S[G::GS_Z + k - 2 * H] = s;
-  }
-}
-
-// out[c][r] = in[r*ldi + c] for r < R, c < C (small weight transposes)
-__global__ __launch_bounds__(256) void transpose_kernel(int R, int C, const float* __restrict__ in, long ldi,
-                                                        float* __restrict__ out) {
-  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
-  if (idx >= (long)R * C) return;
-  const int c = (int)(idx / R), r = (int)(idx - (long)c * R);
-  out[idx] = in[(long)r * ldi + c];
-}
-
-// dW[n][k] += sum_b Y[b][n] X[b][k] for the 64x64 block (blockIdx.y, blockIdx.x);
-// db[n] += sum_b Y[b][n] by the blockIdx.x == 0 blocks.  With gridDim.z > 1 the
-// batch is split: split z sums its rows into part[z] ([N][K] then [N]) and
-// dw_part_reduce adds the splits in order.
-__global__ __launch_bounds__(256) void dw_block_kernel(int B, int N, int K, const float* __restrict__ Y, long ldy,
-                                                       const float* __restrict__ X, long ldx, float* __restrict__ dW,
-                                                       float* __restrict__ db, float* __restrict__ part) {
-  constexpr int NP = 64, KP = 64, KT = 4, NTW = 1;
-  __shared__ __attribute__((aligned(16))) float ys[kDwRows * lds_stride(NP)];
-  __shared__ __attribute__((aligned(16))) float xs[kDwRows * lds_stride(KP)];
+  constexpr int HH = K::HH, DIN = K::DIN;
+  __shared__ __attribute__((aligned(16))) float red[kGW * 4 * 256];
+  __shared__ __attribute__((aligned(16))) float ddl[16 * kHP];  // DD', then dDD' [env][hidden]
+  __shared__ float zl[32], pl[32];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, g = lane >> 4, i = lane & 15;
-  const int k0 = blockIdx.x * 64, n0 = blockIdx.y * 64;
-  f32x4 acc[NTW][KT];
-  float pb[NTW] = {0.f};
+  const long env = (long)blockIdx.x * 16 + i;
+  const bool eok = env < B;
+  float* row = rows + (eok ? env : 0) * G::GS_SIZE;
+  const float* D1 = Pd + G::D_W1;
+
+  // 1. DD' = Disc1' [s; ns] + db1' (the row's Z holds [s; ns] contiguously)
+  f32x4 a[4];
 #pragma unroll
-  for (int u = 0; u < KT; ++u) acc[0][u] = zero4();
-  const int S = gridDim.z, z = blockIdx.z;
-  const long nch = (B + kDwRows - 1) / kDwRows;
-  const long r0 = nch * z / S * kDwRows, r1 = std::min<long>(B, nch * (z + 1) / S * kDwRows);
-  dw_accumulate<NP, KP, NTW>(r0, r1, Y + n0, ldy, X + k0, ldx, 0, 0, 4, ys, xs, acc, pb, std::min(NP, N - n0),
-                             std::min(KP, K - k0));
-  float* oW = S > 1 ? part + (long)z * ((long)N * K + N) : dW;
-  float* ob = S > 1 ? part + (long)z * ((long)N * K + N) + (long)N * K : db;
-  const int t = wv;  // n-tile of this wave
+  for (int t = 0; t < 4; ++t) a[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int c = wv; c < K::KZ; c += kGW) {
+    const int f = 16 * c + 4 * g;
+    const bool fok = f < DIN;
+    const f32x4 bv = ld4(fok && eok ? row + G::GS_Z + f : gk_zero);
+    f32x4 wd[4];
 #pragma unroll
-  for (int u = 0; u < KT; ++u)
+    for (int t = 0; t < 4; ++t) wd[t] = ld4(fok ? D1 + (long)(16 * t + i) * DIN + f : gk_zero);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int n = n0 + 16 * t + 4 * g + r, k = k0 + 16 * u + i;
-      if (n < N && k < K) {
-        if (S > 1)
-          oW[(long)n * K + k] = acc[0][u][r];
-        else
-          oW[(long)n * K + k] += acc[0][u][r];
-      }
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) a[t] = mfma(wd[t][r], bv[r], a[t]);
+  }
+  reduce4(red, a, wv, lane);
+  for (int k = threadIdx.x; k < 1024; k += blockDim.x) {
+    int h, j;
+    red_index(k, h, j);
+    ddl[j * kHP + h] = red[k] + Pd[G::D_B1 + h];
+  }
+  __syncthreads();
+  // 2. head, BCE toward [0, 1] (PreGANPlus.py:69-73) -> dOut', dDD' = D2'^T dOut'
+  head16(ddl, Pd + G::D_W2, Pd + G::D_B2, zl, pl);
+  if (threadIdx.x < 16) {
+    const int j = threadIdx.x;
+    const float p0 = pl[2 * j], p1 = pl[2 * j + 1];
+    const float dp0 = p0 / fmaxf(p0 * (1.f - p0), 1e-12f) * 0.5f;
+    const float dp1 = (p1 - 1.f) / fmaxf(p1 * (1.f - p1), 1e-12f) * 0.5f;
+    const float sd = p0 * dp0 + p1 * dp1;
+    zl[2 * j] = p0 * (dp0 - sd);
+    zl[2 * j + 1] = p1 * (dp1 - sd);
+    const long e = (long)blockIdx.x * 16 + j;
+    if (e < B) {
+      rows[e * G::GS_SIZE + G::GS_P] = p0;  // gen_loss's probabilities (pgp_gan_probs)
+      rows[e * G::GS_SIZE + G::GS_P + 1] = p1;
+      rows[e * G::GS_SIZE + G::GS_DO] = zl[2 * j];
+      rows[e * G::GS_SIZE + G::GS_DO + 1] = zl[2 * j + 1];
     }
-  if (db && blockIdx.x == 0) {
-    const float s = xsum(pb[0], true);
-    const int n = n0 + 16 * t + i;
-    if (g == 0 && n < N) {
-      if (S > 1)
-        ob[n] = s;
-      else
-        ob[n] += s;
-    }
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < 16 * 64; k += blockDim.x) {
+    const int j = k >> 6, h = k & 63;
+    ddl[j * kHP + h] = Pd[G::D_W2 + h] * zl[2 * j] + Pd[G::D_W2 + 64 + h] * zl[2 * j + 1];
+  }
+  __syncthreads();
+  // 3. per tile of 16 schedule entries n: d ns = Disc1'[:, HH + n]^T dDD',
+  //    dY = 4 d ns (1 - T^2) (models.py:128-133), dHg += W2[n, :]^T dY
+  f32x4 db[4];  // dDD' as the B operand of the 16 hidden k-steps
+#pragma unroll
+  for (int q = 0; q < 4; ++q) db[q] = ld4(ddl + i * kHP + 16 * q + 4 * g);
+  const float* W2 = Pg + G::G_W2;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) a[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int c = wv; c < K::KS; c += kGW) {
+    const int n0 = 16 * c, n = n0 + 4 * g;
+    const bool nok = n < HH, rok = n0 + i < HH;
+    // A[i][k]: Disc1'[hidden 16q + 4g + r][HH + n0 + i] (k-step (q, r))
+    float da[4][4], wa[4][4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) da[q][r] = *(rok ? D1 + (long)(16 * q + 4 * g + r) * DIN + HH + n0 + i : gk_zero);
+    // A[i][k]: W2[n0 + 4g + r][16t + i] (k-step r of the dY tile)
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) wa[t][r] = *(nok ? W2 + (long)(n + r) * 64 + 16 * t + i : gk_zero);
+    const f32x4 tv = ld4(nok && eok ? row + G::GS_T + n : gk_zero);
+    f32x4 dn = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) dn = mfma(da[q][r], db[q][r], dn);
+    f32x4 dy;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) dy[r] = 4.0f * dn[r] * (1.f - tv[r] * tv[r]);
+    if (nok && eok) st4(row + G::GS_DY + n, dy);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) a[t] = mfma(wa[t][r], dy[r], a[t]);
+  }
+  reduce4(red, a, wv, lane);
+  for (int k = threadIdx.x; k < 1024; k += blockDim.x) {
+    int h, j;
+    red_index(k, h, j);
+    if ((long)blockIdx.x * 16 + j < B) rows[((long)blockIdx.x * 16 + j) * G::GS_SIZE + G::GS_DH + h] = red[k];
   }
 }
 
-// dW[o] += sum_z part[z][o] (o < N*K), db[n] += sum_z part[z][N*K + n], z ascending
-__global__ __launch_bounds__(256) void dw_part_reduce(int S, int N, int K, const float* __restrict__ part,
-                                                      float* __restrict__ dW, float* __restrict__ db) {
-  const long o = (long)blockIdx.x * 256 + threadIdx.x;
-  const long nk = (long)N * K, stride = nk + N;
-  if (o < nk) {
-    float s = 0.f;
-    for (int z = 0; z < S; ++z) s += part[z * stride + o];
-    dW[o] += s;
-  } else if (db && o < nk + N) {
-    float s = 0.f;
-    for (int z = 0; z < S; ++z) s += part[z * stride + o];
-    db[o - nk] += s;
+// ---------------------------------------------------------------------------
+// weight gradients: dW[n][k] = sum_b Y[b][n] X[b][k] (= into G), db[n] = sum_b Y[b][n]
+// ---------------------------------------------------------------------------
+struct OuterProd {
+  const float* Y;  // Y[b][n] at Y + b * ld_rows, n < N
+  const float* X;  // X[b][k] at X + b * ld_rows, k < K
+  float* dW;       // dW[n][k] at dW + n * ldw + k
+  float* db;       // optional: db[n]
+  int N, K, ldw;
+  int nbk;    // 64-column blocks of k
+  int first;  // index of this product's first 64 x 64 block
+};
+struct OuterArgs {
+  int B;
+  long ld_rows;
+  int nprod;
+  OuterProd p[4];
+};
+
+// one wave per 64 x 64 block of one product: 4 x 4 MFMA tiles, one k-step per
+// 4 environments (k = lane group), the next step's 8 values loaded ahead
+__global__ __launch_bounds__(256) void outer_kernel(OuterArgs a) {
+  const int lane = threadIdx.x & 63, g = lane >> 4, i = lane & 15;
+  const int blk = blockIdx.x * 4 + (threadIdx.x >> 6);
+  int pi = -1;
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (k < a.nprod && blk >= a.p[k].first) pi = k;
+  if (pi < 0) return;
+  const OuterProd p = a.p[pi];
+  const int lb = blk - p.first;
+  const int nb = lb / p.nbk, kb = lb - nb * p.nbk;
+  if (nb * 64 >= p.N) return;  // past the product (the grid rounds up)
+  const int n0 = nb * 64, k0 = kb * 64;
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc[t][u] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float bs[4] = {0.f, 0.f, 0.f, 0.f};
+  bool nok[4], kok[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    nok[t] = n0 + 16 * t + i < p.N;
+    kok[t] = k0 + 16 * t + i < p.K;
+  }
+  const int steps = (a.B + 3) / 4;
+  auto load = [&](int s, float (&y)[4], float (&x)[4]) {
+    const long e = 4L * s + g;
+    const bool ok = e < a.B;
+    const float* yr = p.Y + e * a.ld_rows + n0 + i;
+    const float* xr = p.X + e * a.ld_rows + k0 + i;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      y[t] = *(ok && nok[t] ? yr + 16 * t : gk_zero);
+      x[t] = *(ok && kok[t] ? xr + 16 * t : gk_zero);
+    }
+  };
+  float y[4], x[4];
+  load(0, y, x);
+  for (int s = 0; s < steps; ++s) {
+    float yn[4], xn[4];
+    load(s + 1 < steps ? s + 1 : s, yn, xn);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      bs[t] += y[t];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc[t][u] = mfma(y[t], x[u], acc[t][u]);
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      y[t] = yn[t];
+      x[t] = xn[t];
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = n0 + 16 * t + 4 * g + r, k = k0 + 16 * u + i;
+        if (n < p.N && k < p.K) p.dW[(long)n * p.ldw + k] = acc[t][u][r];
+      }
+  if (p.db && kb == 0) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const float sum = xsum(bs[t], true);
+      if (g == 0 && nok[t]) p.db[n0 + 16 * t + i] = sum;
+    }
   }
 }
 
@@ -251,137 +494,59 @@ __global__ __launch_bounds__(256) void dw_part_reduce(int S, int N, int K, const
     if (e_ != hipSuccess) return e_;         \
   } while (0)
 
-struct GanPlan {
-  long rows = 0;   // [B][GS_SIZE] window rows
-  long part = 0;   // split-K partial slabs
-  long tr = 0;     // weight transposes (D1's ns half, W2)
-  long total = 0;
-};
-
-template <int H>
-GanPlan gan_plan_h(int B) {
-  using G = TGeo<H>;
-  GanPlan p;
-  long off = 0;
-  auto take = [&](long n) {
-    const long o = off;
-    off += (n + 63) / 64 * 64;
-    return o;
-  };
-  p.rows = take((long)B * G::GS_SIZE);
-  const long wide = (long)B * round_up(H * H, 64);  // S = 1 GEMMs over H^2 outputs
-  // split GEMMs: S * ceil(B/64)*64 <= 256*64 rows x 64; weight-gradient splits <= 8 x the largest [N][K] + [N]
-  const long dwmax = 8L * (std::max({64L * G::DIN, (long)H * H * 64, 64L * G::GIN}) + (long)H * H);
-  p.part = take(std::max({256L * 64 * 64, wide, dwmax}));
-  p.tr = take(2L * H * H * 64);
-  p.total = off;
-  return p;
-}
-
-// split factor for an M x 64 output over K: ~256 workgroups
-inline int split_for(int M, int K) {
-  const int mb = (M + 63) / 64, kbt = (K + 15) / 16;
-  return std::max(1, std::min(kbt, 256 / mb));
-}
-
-// out (row stride ldo) <- X[M][K] . W[N][K]^T (+ bias) through the epilogue
-hipError_t gemm(int M, int N, int K, const float* X, long ldx, const float* W, long ldw, int S, float* part, int mode,
-                const float* bias, float* out, long ldo, const float* aux, float* out2, float* ns_out,
-                hipStream_t st) {
-  const int ng = (N + 63) / 64, ldp = ng * 64;
-  GCK((gemm_nt_kernel<<<dim3((M + 63) / 64, ng, S), 256, 0, st>>>(M, N, K, X, ldx, W, ldw, S, ldp, part)));
-  GCK((gemm_epi_kernel<<<(int)(((long)M * N + 255) / 256), 256, 0, st>>>(mode, M, N, S, ldp, part, bias, out, ldo,
-                                                                           aux, out2, ns_out)));
-  return hipSuccess;
-}
-
-hipError_t dw_blocks(int B, int N, int K, const float* Y, long ldy, const float* X, long ldx, float* dW, float* db,
-                     float* part, hipStream_t st) {
-  const int nb = ((K + 63) / 64) * ((N + 63) / 64);
-  const int S = std::max(1, std::min({8, 256 / nb, (B + kDwRows - 1) / kDwRows}));
-  GCK((dw_block_kernel<<<dim3((K + 63) / 64, (N + 63) / 64, S), 256, 0, st>>>(B, N, K, Y, ldy, X, ldx, dW, db,
-                                                                                part)));
-  if (S > 1) {
-    const long n = (long)N * K + N;
-    GCK((dw_part_reduce<<<(int)((n + 255) / 256), 256, 0, st>>>(S, N, K, part, dW, db)));
+hipError_t outer(const OuterArgs& a0, hipStream_t st) {
+  OuterArgs a = a0;
+  int blocks = 0;
+  for (int k = 0; k < a.nprod; ++k) {
+    OuterProd& p = a.p[k];
+    p.nbk = (p.K + 63) / 64;
+    p.first = blocks;
+    blocks += ((p.N + 63) / 64) * p.nbk;
   }
+  GCK((outer_kernel<<<(blocks + 3) / 4, 256, 0, st>>>(a)));
   return hipSuccess;
-}
-
-// Disc1 hidden: DD = Z . D1^T + db1
-template <int H>
-hipError_t disc_hidden(int B, const float* Pd, float* ws, const GanPlan& gp, hipStream_t st) {
-  using G = TGeo<H>;
-  float* R = ws + gp.rows;
-  return gemm(B, 64, G::DIN, R + G::GS_Z, G::GS_SIZE, Pd + G::D_W1, G::DIN, split_for(B, G::DIN), ws + gp.part,
-              GE_BIAS, Pd + G::D_B1, R + G::GS_DD, G::GS_SIZE, nullptr, nullptr, nullptr, st);
 }
 
 template <int H>
 hipError_t gan_fwd_h(int B, const float* emb, const float* sched, const float* Pg, const float* Pd, float* ws,
                      float* ns_out, float* probs, hipStream_t st) {
-  using G = TGeo<H>;
-  const GanPlan gp = gan_plan_h<H>(B);
-  float* R = ws + gp.rows;
-  hipError_t e;
-  GCK((gan_in_kernel<H><<<(int)(((long)B * G::GIN + 255) / 256), 256, 0, st>>>(B, emb, sched, R)));
-  // Gen1 (models.py:124-127): Hg = W1 [emb; s] + b1
-  if ((e = gemm(B, 64, G::GIN, R + G::GS_X, G::GS_SIZE, Pg + G::G_W1, G::GIN, split_for(B, G::GIN), ws + gp.part,
-                GE_BIAS, Pg + G::G_B1, R + G::GS_H, G::GS_SIZE, nullptr, nullptr, nullptr, st)) != hipSuccess)
-    return e;
-  // Gen2 + tanh, ns = s + 4 tanh(.) (models.py:128-133)
-  if ((e = gemm(B, H * H, 64, R + G::GS_H, G::GS_SIZE, Pg + G::G_W2, 64, 1, ws + gp.part, GE_TANH, Pg + G::G_B2,
-                R + G::GS_T, G::GS_SIZE, R + G::GS_Z, R + G::GS_Z + H * H, ns_out, st)) != hipSuccess)
-    return e;
-  if ((e = disc_hidden<H>(B, Pd, ws, gp, st)) != hipSuccess) return e;
-  GCK((disc_head_kernel<H><<<(B + 3) / 4, 256, 0, st>>>(B, 0, Pd, R, nullptr, probs)));
+  GCK((gan_fwd_kernel<H><<<(B + 15) / 16, kGW * 64, 0, st>>>(B, emb, sched, Pg, Pd, ws, ns_out, probs)));
   return hipSuccess;
 }
 
 template <int H>
 hipError_t gan_disc_bwd_h(int B, const float* target, const float* Pd, float* Gdd, float* ws, hipStream_t st) {
   using G = TGeo<H>;
-  const GanPlan gp = gan_plan_h<H>(B);
-  float* R = ws + gp.rows;
-  hipError_t e;
-  GCK((disc_head_kernel<H><<<(B + 3) / 4, 256, 0, st>>>(B, 1, Pd, R, target, nullptr)));
-  if ((e = dw_blocks(B, 2, 64, R + G::GS_DO, G::GS_SIZE, R + G::GS_DD, G::GS_SIZE, Gdd + G::D_W2, Gdd + G::D_B2,
-                     ws + gp.part, st)) != hipSuccess)
-    return e;
-  return dw_blocks(B, 64, G::DIN, R + G::GS_DDD, G::GS_SIZE, R + G::GS_Z, G::GS_SIZE, Gdd + G::D_W1, Gdd + G::D_B1,
-                   ws + gp.part, st);
+  GCK((disc_head_kernel<H><<<(B + 3) / 4, 256, 0, st>>>(B, 1, Pd, ws, target, nullptr)));
+  OuterArgs a{};
+  a.B = B;
+  a.ld_rows = G::GS_SIZE;
+  a.nprod = 2;
+  // Disc1: dD1 = sum_b dDD_b [s; ns]_b^T, db1 = sum_b dDD_b
+  a.p[0] = OuterProd{ws + G::GS_DDD, ws + G::GS_Z, Gdd + G::D_W1, Gdd + G::D_B1, 64, G::DIN, G::DIN, 0, 0};
+  // head: dD2 = sum_b dOut_b DD_b^T, db2 = sum_b dOut_b
+  a.p[1] = OuterProd{ws + G::GS_DO, ws + G::GS_DD, Gdd + G::D_W2, Gdd + G::D_B2, 2, 64, 64, 0, 0};
+  return outer(a, st);
 }
 
 template <int H>
 hipError_t gan_gen_bwd_h(int B, const float* Pg, const float* Pd, float* Gdg, float* ws, hipStream_t st) {
   using G = TGeo<H>;
   constexpr int HH = H * H;
-  const GanPlan gp = gan_plan_h<H>(B);
-  float* R = ws + gp.rows;
-  float* D1nsT = ws + gp.tr;        // [H^2][64] = D1[:, H^2:]^T
-  float* W2T = ws + gp.tr + HH * 64;  // [64][H^2] = W2^T
-  hipError_t e;
-  // Disc forward with the updated Disc, BCE toward [0,1] (PreGANPlus.py:69-73)
-  if ((e = disc_hidden<H>(B, Pd, ws, gp, st)) != hipSuccess) return e;
-  GCK((disc_head_kernel<H><<<(B + 3) / 4, 256, 0, st>>>(B, 2, Pd, R, nullptr, nullptr)));
-  // d ns = D1[:, H^2:]^T dDD; through 4 tanh: dY = 4 dns (1 - T^2)
-  GCK((transpose_kernel<<<(int)((64L * HH + 255) / 256), 256, 0, st>>>(64, HH, Pd + G::D_W1 + HH, G::DIN, D1nsT)));
-  if ((e = gemm(B, HH, 64, R + G::GS_DDD, G::GS_SIZE, D1nsT, 64, 1, ws + gp.part, GE_DY, nullptr, R + G::GS_DY,
-                G::GS_SIZE, R + G::GS_T, nullptr, nullptr, st)) != hipSuccess)
-    return e;
-  if ((e = dw_blocks(B, HH, 64, R + G::GS_DY, G::GS_SIZE, R + G::GS_H, G::GS_SIZE, Gdg + G::G_W2, Gdg + G::G_B2,
-                     ws + gp.part, st)) != hipSuccess)
-    return e;
-  // dHg = W2^T dY, then Gen1's gradients
-  GCK((transpose_kernel<<<(int)((64L * HH + 255) / 256), 256, 0, st>>>(HH, 64, Pg + G::G_W2, 64, W2T)));
-  if ((e = gemm(B, 64, HH, R + G::GS_DY, G::GS_SIZE, W2T, HH, split_for(B, HH), ws + gp.part, GE_BIAS, nullptr,
-                R + G::GS_DH, G::GS_SIZE, nullptr, nullptr, nullptr, st)) != hipSuccess)
-    return e;
-  return dw_blocks(B, 64, G::GIN, R + G::GS_DH, G::GS_SIZE, R + G::GS_X, G::GS_SIZE, Gdg + G::G_W1, Gdg + G::G_B1,
-                   ws + gp.part, st);
+  GCK((gan_gen_kernel<H><<<(B + 15) / 16, kGW * 64, 0, st>>>(B, Pg, Pd, ws)));
+  OuterArgs a{};
+  a.B = B;
+  a.ld_rows = G::GS_SIZE;
+  a.nprod = 3;
+  // Gen2: dW2 = sum_b dY_b Hg_b^T, db2 = sum_b dY_b
+  a.p[0] = OuterProd{ws + G::GS_DY, ws + G::GS_H, Gdg + G::G_W2, Gdg + G::G_B2, HH, 64, 64, 0, 0};
+  // Gen1 over [e; s]: dW1[:, :2H] = sum_b dHg_b e_b^T (+ db1), dW1[:, 2H:] = sum_b dHg_b s_b^T
+  a.p[1] = OuterProd{ws + G::GS_DH, ws + G::GS_X, Gdg + G::G_W1, Gdg + G::G_B1, 64, 2 * H, G::GIN, 0, 0};
+  a.p[2] = OuterProd{ws + G::GS_DH, ws + G::GS_Z, Gdg + G::G_W1 + 2 * H, nullptr, 64, HH, G::GIN, 0, 0};
+  return outer(a, st);
 }
 
-// the Disc probabilities the last disc_head_kernel left in the window rows (after
+// the Disc probabilities the last head evaluation left in the rows (after
 // pgp_gan_gen_backward: the updated Disc's, i.e. gen_loss's, PreGANPlus.py:71-73)
 template <int H>
 __global__ void gan_probs_kernel(int B, const float* __restrict__ scr, float* __restrict__ probs) {
@@ -394,8 +559,7 @@ __global__ void gan_probs_kernel(int B, const float* __restrict__ scr, float* __
 
 template <int H>
 hipError_t gan_probs_h(int B, const float* ws, float* probs, hipStream_t st) {
-  const GanPlan gp = gan_plan_h<H>(B);
-  GCK((gan_probs_kernel<H><<<(B + 255) / 256, 256, 0, st>>>(B, ws + gp.rows, probs)));
+  GCK((gan_probs_kernel<H><<<(B + 255) / 256, 256, 0, st>>>(B, ws, probs)));
   return hipSuccess;
 }
 
@@ -412,12 +576,13 @@ hipError_t launch_gan_probs(int H, int B, const float* ws, float* probs, hipStre
   return hipErrorInvalidValue;
 }
 
+// one row of GS_SIZE floats per environment
 long gan_workspace_floats(int H, int B) {
   if (B < 1) return 0;
   switch (H) {
 #define CASE(h) \
   case h:       \
-    return gan_plan_h<h>(B).total;
+    return (long)B * TGeo<h>::GS_SIZE;
     PGP_FOR_EACH_H(CASE)
 #undef CASE
   }

@@ -860,9 +860,9 @@ bool plan_h(int B, TunePlan* out) {
   q.wp = take((long)Q::NOP * Q::KD);
   q.wpt = take((long)Q::NOP * Q::KD);
   q.tff = take(tf_frag_floats(H));
-  q.tf_grid = tf_grid();
+  q.tf_grid = tf_bwd_grid(H, B);   // this call's backward launches (slabs); sized below for the most
   for (int l = 0; l < 2; ++l)
-    for (int k = 0; k < 2; ++k) q.tfs[l][k] = take((long)q.tf_grid * tf_slab_floats(H, 2 + k));
+    for (int k = 0; k < 2; ++k) q.tfs[l][k] = take((long)tf_max_grid() * tf_slab_floats(H, 2 + k));
   const long nrb = (M + 15) / 16;
   q.lin_grid = (int)std::min<long>(kLinCap, std::max<long>(1, (nrb + 3) / 4));
   q.dw_grid = (int)std::min<long>(kDwCap, std::max<long>(1, (nrb + 7) / 8));
@@ -896,7 +896,7 @@ bool plan_h(int B, TunePlan* out) {
     dwr(DPl, DPl, Hl, Hl, true);           // time encoder
     dwr(DPl, Q::XBP, Hl, 3, false);        // GAT fc
     // level-2 regions of the fused slabs (more than 256 workgroups)
-    const long ns = (q.tf_grid + 255) / 256;
+    const long ns = (tf_max_grid() + 255) / 256;
     if (ns > 1) pool += 2 * ns * r64(tf_slab_floats(H, 2) + tf_slab_floats(H, 3)) * 2;
     q.pool = take(pool);
     q.pool_len = pool;
@@ -945,6 +945,9 @@ SideStream* side_stream() {
   }
   return x.ok ? &x : nullptr;
 }
+// a caller-owned stream to use as the side stream (pgp_tune_set_side_stream),
+// per device; null: the library's own
+std::atomic<hipStream_t> g_side_override[16];
 struct Fork {
   hipStream_t main, side;
   SideStream* ss = nullptr;
@@ -957,7 +960,12 @@ struct Fork {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return;
     ss = side_stream();
-    if (ss) side = ss->s;
+    if (!ss) return;
+    int dev = 0;
+    const hipStream_t o = (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 16)
+                              ? g_side_override[dev].load(std::memory_order_relaxed)
+                              : nullptr;
+    side = o ? o : ss->s;
   }
   // `to` waits for everything issued on `from` so far
   hipError_t order(hipStream_t from, hipStream_t to) {
@@ -1121,6 +1129,13 @@ hipError_t tune_bwd_h(const TunePlan& p, const float* P, float* Gd, float* ws, c
 }
 
 }  // namespace
+
+hipError_t tune_set_side_stream(hipStream_t s) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return hipErrorInvalidDevice;
+  g_side_override[dev].store(s, std::memory_order_relaxed);
+  return hipSuccess;
+}
 
 hipError_t tune_timing(bool on) {
   if (on && !g_tft.made) {

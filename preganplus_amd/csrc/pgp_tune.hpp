@@ -50,6 +50,9 @@ bool tune_plan(int H, int B, TunePlan* p);
 // live timing of the six fused encoder launches of a forward + backward
 // (pgp_tune_timing / pgp_tune_fused_ms)
 hipError_t tune_timing(bool on);
+// the tuning backward's side stream on the current device: `s`, or the
+// library's own low-priority stream when null (pgp_tune_set_side_stream)
+hipError_t tune_set_side_stream(hipStream_t s);
 hipError_t tune_fused_ms(float* out6);
 
 // decoder GEMMs (pgp_dec.hip): split-K forward into part[S][B][NOP] and the

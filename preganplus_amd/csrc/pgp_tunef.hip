@@ -1298,7 +1298,24 @@ long tf_slab_floats(int H, int kind) {
   return 0;
 }
 
-int tf_grid() { return device_cus(); }
+// CUs left to other streams (pgp_tune_reserve_cus): a fused launch holds whole
+// CUs (one workgroup per CU, its registers and LDS) and deals its units to the
+// waves statically, so one CU taken by a concurrent stream's long workgroup
+// (the GAN step beside the tuning step) holds back the whole launch; with a
+// few CUs reserved the two streams stop blocking each other
+std::atomic<int> g_tf_reserve{0};
+
+int tf_grid_for(long nu, int waves) {
+  const int cus = device_cus();
+  const int r = std::max(0, std::min(g_tf_reserve.load(std::memory_order_relaxed), cus / 2));
+  return (int)std::max<long>(1, std::min<long>(cus - r, (nu + waves - 1) / waves));
+}
+
+int tf_max_grid() { return device_cus(); }
+
+int tf_bwd_grid(int H, int B) { return tf_grid_for(((long)B * H + 15) / 16, kTfWaves); }
+
+void tf_reserve_cus(int n) { g_tf_reserve.store(n < 0 ? 0 : n, std::memory_order_relaxed); }
 
 #ifdef PGP_TF_STAMPS
 // profiling builds: copy out (host != null) or clear (host == null) the phase stamps
@@ -1313,7 +1330,8 @@ extern "C" int pgp_debug_tf_stamps(unsigned long long* host) {
 #endif
 
 hipError_t launch_tf(int H, int kind, const TfArgs& a, hipStream_t st) {
-  const int grid = tf_grid();
+  const long nu = ((long)a.B * H + 15) / 16;
+  const int grid = tf_grid_for(nu, kind == 1 ? kTfFwdWaves : kTfWaves);
   switch (H) {
 #define CASE(h)                                                                          \
   case h: {                                                                              \

@@ -72,7 +72,9 @@ struct TfArgs {
 
 long tf_frag_floats(int H);
 long tf_slab_floats(int H, int kind);  // kind 2: ffn backward, 3: attention backward
-int tf_grid();                          // workgroups per fused launch (one per CU)
+int tf_max_grid();                      // the most workgroups a fused launch uses (one per CU)
+int tf_bwd_grid(int H, int B);          // workgroups (= weight-gradient slabs) of a backward launch
+void tf_reserve_cus(int n);             // CUs the fused launches leave to other streams
 // kind 0: pack fragments from P; 1: forward of a.layer; 2: ffn backward; 3: attention backward
 hipError_t launch_tf(int H, int kind, const TfArgs& a, hipStream_t st);
 

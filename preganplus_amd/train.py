@@ -302,15 +302,17 @@ class Trainer:
             self.gscr.data_ptr(), probs_gen.data_ptr(), probs_after.data_ptr(), self._stream()), "pgp_gan_step1")
 
     def gan_disc_backward(self, target):
+        """The Disc's BCE gradients toward target [B,2], WRITTEN into G's disc
+        section (every element: no zero-fill needed)."""
         target = self._dev(target, torch.float32)
         B = target.shape[0]
-        self.zero_grad("disc")
         _native.check(self._L.pgp_gan_disc_backward(
             self.H, B, target.data_ptr(), self.P.data_ptr(), self.G.data_ptr(), self.gscr.data_ptr(),
             self._stream()), "pgp_gan_disc_backward")
 
     def gan_gen_backward(self, B):
-        self.zero_grad("gen")
+        """The Gen's BCE gradients toward [0,1] through the current Disc, WRITTEN
+        into G's gen section."""
         _native.check(self._L.pgp_gan_gen_backward(
             self.H, B, self.P.data_ptr(), self.G.data_ptr(), self.gscr.data_ptr(), self._stream()),
             "pgp_gan_gen_backward")

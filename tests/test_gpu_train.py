@@ -554,3 +554,39 @@ def test_gan_step_b1024_h50_matches_reference():
         if sec:
             D.check(z, f"{sec}/{t['name']}", g[t["offset"]:t["offset"] + t["n"]].reshape(
                 w[t["section"]][t["name"]].shape), _dclose(1e-3, 1e-4), sum_rel=1e-4, key=t["name"])
+
+
+@pytest.mark.parametrize("H", [16, 50])
+def test_reserved_cus_same_gradients(H):
+    """pgp_tune_reserve_cus (the C3 bench leaves 8 CUs to the GAN stream): the
+    fused launches then run on fewer workgroups, so units are dealt differently
+    and the weight gradients are summed in other fp32 groupings; the gradients
+    agree with the full-grid step to fp32 summation tolerance, and two reserved
+    steps are bit-identical (still one fixed slab per workgroup)."""
+    import ctypes
+    from preganplus_amd import _native
+    from preganplus_amd import train as TR
+    B = 1030
+    w, x, y, mult, tgt = _batched_case(H, B, seed=9)
+    tr = TR.Trainer(H, w, max_batch=B)
+    xs = torch.tensor(x, dtype=torch.float32)
+    L = _native.lib()
+    L.pgp_tune_reserve_cus.argtypes = [ctypes.c_int]
+
+    def grads(n):
+        _native.check(L.pgp_tune_reserve_cus(n), "pgp_tune_reserve_cus")
+        tr.tune_forward(xs)
+        tr.tune_backward(B, y, mult, tgt)
+        return tr.G.cpu().numpy().copy()
+    try:
+        g0 = grads(0)
+        g8, g8b = grads(8), grads(8)
+        g128 = grads(200)      # clamped to half the CUs
+    finally:
+        _native.check(L.pgp_tune_reserve_cus(0), "pgp_tune_reserve_cus")
+    assert np.array_equal(g8, g8b)
+    for g in (g8, g128):
+        for t in tr.tensors:
+            if t["section"] == "transformer" and t["trainable"]:
+                sl = slice(t["offset"], t["offset"] + t["n"])
+                close(g[sl], g0[sl], rel=1e-4, abs_scale=1e-5, what=f"reserved {t['name']}")

@@ -36,13 +36,17 @@ pmc() {  # pmc NAME COUNTERS BENCH_ARGS...
   if [ $rc -ne 0 ]; then tail -5 $OUT/$name.log; exit $rc; fi
 }
 STALL1="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_MFMA"
-STALL2="SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU"
+STALL2="SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE"
 for step in "$@"; do
   case $step in
     tests)
       run gpu_tests 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread
       tail -2 $OUT/gpu_tests.out
       run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+      ;;
+    ttrain)
+      run t_train 600 python -u -m pytest tests/test_gpu_train.py tests/test_gpu_bench_modes.py tests/test_gpu_dist.py -x -v -p no:cacheprovider --timeout 300 --timeout-method thread
+      tail -2 $OUT/t_train.out
       ;;
     c2)
       run c2 400 python3 -u bench.py

@@ -32,7 +32,7 @@ def main():
     root, batch, H = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
     only = set(sys.argv[4:])
     vals = collections.defaultdict(lambda: collections.defaultdict(list))
-    for f in glob.glob(f"{root}/pmc*/run_counter_collection.csv"):
+    for f in glob.glob(f"{root}/*pmc*/run_counter_collection.csv"):
         for row in csv.DictReader(open(f)):
             name = re.sub(r"\(.*$", "", row["Kernel_Name"].replace("void pgp::(anonymous namespace)::", ""))
             vals[name][row["Counter_Name"]].append(float(row["Counter_Value"]))
