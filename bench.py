@@ -566,7 +566,6 @@ def bench_tune(args):
         rec(0)
         wins, y, cls, inf = TR.tune_dataset(tr, series, tmax, out=bufs)
         rec(1)
-        side.wait_stream(main)
 
         def detect():
             with torch.cuda.stream(side):
@@ -577,9 +576,6 @@ def bench_tune(args):
                 det_done.record(side)
                 if e is not None:
                     e[2].record(side)
-        # the tuning step (the longer chain) is issued before the GAN step: the
-        # host's ~40 GAN launches would otherwise leave the main stream idle;
-        # detect's launches are issued once the tuning forward's are queued
         def gan():
             with torch.cuda.stream(side):
                 TR.train_gan_batched(tr, sim, envs, emb_buf, s, out=sim_out, target=gan_target, all_reduce=True,
@@ -587,16 +583,17 @@ def bench_tune(args):
                 if e is not None:
                     e[3].record(side)
 
-        if shared_side:
-            def detect_gan():
-                detect()
-                gan()
-            tun.step(wins, y, cls, mark=(lambda k: se[k].record(main)) if se is not None else None,
-                     before_update=det_done, after_forward=detect_gan)
-        else:
-            tun.step(wins, y, cls, mark=(lambda k: se[k].record(main)) if se is not None else None,
-                     before_update=det_done, after_forward=detect)
-            gan()   # (issued with detect, before the backward: no faster at N=1, profiles/r03/s3/)
+        # detect + the GAN step start with the tuning BACKWARD (the second
+        # stream waits for the tuning step's targets): its fused launches leave
+        # GAN_RESERVED_CUS CUs free, while the forward's would be slowed by a
+        # concurrent detect forward (round 4: detect beside the forward cost the
+        # tuning forward ~55 us, profiles/r04/)
+        def detect_gan():
+            side.wait_stream(main)
+            detect()
+            gan()
+        tun.step(wins, y, cls, mark=(lambda k: se[k].record(main)) if se is not None else None,
+                 before_update=det_done, before_backward=detect_gan)
         main.wait_stream(side)
         rec(4)
 
@@ -658,8 +655,8 @@ def bench_tune(args):
                                                                            "(grads, state; GAN on its own group)"
                                                                            if world > 1 else "")},
             "stage_ms": {n: float(stage[k]) for k, n in enumerate(names)},
-            "streams": "detect + train_gan on a second stream, concurrent with tune_model (no shared data; the "
-                       "tuning step's weight update waits for detect)" if side is not main else "one stream",
+            "streams": "detect + train_gan on a second stream, concurrent with tune_model's backward (no shared "
+                       "data; the tuning step's weight update waits for detect)" if side is not main else "one stream",
             "reserved_cus": reserved,
             "tune_model_ms": {n: float(sub[k]) for k, n in enumerate(subs)},
             "grad_all_reduce_ms": float(sub[subs.index("all_reduce")]),

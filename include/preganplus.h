@@ -386,6 +386,26 @@ int pgp_gan_step1(int n_hosts, const float* target, float* P, float* G, float* e
                   const pgp_adam_tensor* gen_tensors, int n_gen, const float* gen_sched, float* workspace,
                   float* probs_gen, float* probs_after, void* stream);
 
+/* ---------------------------------------------------------------------------
+ * Offline training of PreGAN's FPE_16 (PreGAN.py:26-27, 39-49: a new FPE is
+ * trained when no checkpoint exists, train.py:42-57).  P / G: the FPE's
+ * parameters, natural fp32 blob in state_dict order (pgp_fpe_param_len(16) =
+ * 11401 floats).
+ * pgp_fpe_train_step: one sequential batch-1 step of backprop: FPE forward of
+ *   window [3,48] with GRU state h0 [3] (the reference's torch.randn draw,
+ *   models.py:70), custom_loss / triplet_loss bookkeeping on state [2K+3]
+ *   fp64 (prototypes [K][2], factor, num_zero, num_ones; as pgp_tune_targets),
+ *   loss [2] fp64 = (aloss, tloss), and the gradient WRITTEN into G.  The
+ *   AdamW step that follows is pgp_adamw / pgp_adamw_table over P, G.
+ * pgp_fpe_forward_many: n independent forwards (accuracy(), train.py:94-109):
+ *   windows [n,3,48], h0 [n,3] -> probs / protos [n,16,2] fp64. */
+size_t pgp_fpe_param_len(int n_hosts);
+int pgp_fpe_train_step(int n_hosts, int n_protos, const float* window, const float* h0, const int* y, const int* cls,
+                       const float* P, float* G, double* state, double update_min, double decay, double* loss,
+                       void* stream);
+int pgp_fpe_forward_many(int n_hosts, int n, const float* windows, const float* h0, const float* P, double* probs,
+                         double* protos, void* stream);
+
 /* Rebuild the inference layouts from device master weights P (natural fp32)
  * and prototypes [K,2] (host, fp64): the sync after an optimizer step, via the
  * host packer (a device-to-host copy of P, pack, upload; synchronous). */

@@ -93,6 +93,45 @@ def disc_t(dw, s, ns):
     return T.softmax(z, dim=-1)
 
 
+def fpe_t(fw, win, h0):
+    """PreGAN's FPE_16 forward (models.py:65-115) in torch, batched: win [B,3,3H],
+    h0 [B,3] (the GRU state models.py:70 draws) -> per-host anomaly softmax
+    probabilities [B,H,2] and sigmoid prototypes [B,H,2].  Same math as
+    pregan_oracle.fpe_forward (pinned to the reference's fixtures), with
+    autograd: the offline-training restatement (PreGAN.py:39-49)."""
+    B, Wn, F = win.shape
+    H = F // 3
+    h = h0.reshape(B, 3)
+    Wih, Whh, bih, bhh = fw["gru.weight_ih_l0"], fw["gru.weight_hh_l0"], fw["gru.bias_ih_l0"], fw["gru.bias_hh_l0"]
+    gru = []
+    for w in range(Wn):
+        gi = _lin(win[:, w], Wih, bih)
+        gh = _lin(h, Whh, bhh)
+        r = T.sigmoid(gi[:, 0:3] + gh[:, 0:3])
+        z = T.sigmoid(gi[:, 3:6] + gh[:, 3:6])
+        n = T.tanh(gi[:, 6:9] + r * gh[:, 6:9])
+        h = (1 - z) * n + z * h
+        gru.append(h)
+    gru = T.stack(gru, 1)                                                         # [B,3,3]
+    fc, at = fw["gat.layer1.heads.0.fc.weight"], fw["gat.layer1.heads.0.attn_fc.weight"]
+    x = win.reshape(B, Wn, H, 3)
+    z = x @ fc.T                                                                  # [B,W,H,d]
+    d = fc.shape[0]
+    e = T.nn.functional.leaky_relu((z @ at[0, :d])[..., :, None] + (z @ at[0, d:])[..., None, :], 0.01)
+    a = T.softmax(e.reshape(B, Wn, H * H), dim=-1).reshape(B, Wn, H, H)       # graph-wise (all edges)
+    g = T.einsum("bwij,bwid->bwjd", a, z).mean(dim=2)                            # node mean [B,W,d]
+    c = T.cat([gru, g], 2)
+    E = c.shape[2]
+    qkv = _lin(c, fw["mha.in_proj_weight"], fw["mha.in_proj_bias"])
+    q, k, v = qkv[..., :E], qkv[..., E:2 * E], qkv[..., 2 * E:]
+    p = T.softmax(T.einsum("bse,bte->bst", q, k) / math.sqrt(E), dim=-1)
+    o = _lin(T.einsum("bst,bte->bse", p, v), fw["mha.out_proj.weight"], fw["mha.out_proj.bias"])
+    lat = _lin(o.reshape(B, -1), fw["encoder.0.weight"], fw["encoder.0.bias"]).reshape(B, H, -1)
+    probs = T.softmax(_lin(lat, fw["anomaly_decoder.0.weight"], fw["anomaly_decoder.0.bias"]), dim=-1)
+    protos = T.sigmoid(_lin(lat, fw["prototype_decoder.0.weight"], fw["prototype_decoder.0.bias"]))
+    return probs, protos
+
+
 # ---------------------------------------------------------------------------
 # AdamW exactly as torch.optim.AdamW (single-tensor path)
 # ---------------------------------------------------------------------------
@@ -212,6 +251,24 @@ def backprop(tw: dict, opt: AdamW, st: TuneState, wins, sched, anom, cls, record
         opt.apply()
         if record is not None and i == 0:
             record["p1"] = {n: q.detach().numpy().copy() for n, q in tw.items()}
+        losses.append((float(aloss), float(tloss)))
+    return losses
+
+
+def fpe_backprop(fw: dict, opt: AdamW, st: TuneState, wins, h0s, anom, cls):
+    """train.py:42-57 for PreGAN's FPE_16 (PreGAN.py:39-49, train_model): the
+    same sequential batch-1 loop and custom_loss as the Transformer's, on the
+    FPE's outputs (its anomaly decoder ends in a Softmax, so CrossEntropyLoss
+    sees probabilities, models.py:49-52); h0s [n,3]: the GRU state each
+    forward drew.  Returns the per-window (aloss, tloss)."""
+    st.num_zero, st.num_ones = 1, 1
+    losses = []
+    for i in range(wins.shape[0]):
+        probs, protos = fpe_t(fw, T.tensor(wins[i:i + 1]), T.tensor(h0s[i:i + 1]))
+        aloss, tloss = custom_loss(probs[0], protos[0], anom[i], cls[i], st)
+        opt.zero_grad()
+        (aloss + tloss).backward()
+        opt.apply()
         losses.append((float(aloss), float(tloss)))
     return losses
 

@@ -359,6 +359,28 @@ int pgp_tune_backward(int n_hosts, int batch, const float* P, float* G, float* w
   return PGP_OK;
 }
 
+size_t pgp_fpe_param_len(int n_hosts) { return n_hosts == 16 ? (size_t)fpe_param_count() : 0; }
+
+int pgp_fpe_train_step(int n_hosts, int n_protos, const float* window, const float* h0, const int* y, const int* cls,
+                       const float* P, float* G, double* state, double update_min, double decay, double* loss,
+                       void* stream) {
+  if (n_hosts != 16) return fail(PGP_ERR_UNSUPPORTED, "FPE training: n_hosts 16 only (FPE_16)");
+  if (n_protos < 3 || n_protos > kMaxProtos) return fail(PGP_ERR_ARG, "n_protos");
+  if (!window || !h0 || !y || !cls || !P || !G || !state || !loss) return fail(PGP_ERR_ARG, "NULL argument");
+  HIPCHK(launch_fpe_step(window, h0, y, cls, P, G, n_protos, state, update_min, decay, loss,
+                         reinterpret_cast<hipStream_t>(stream)));
+  return PGP_OK;
+}
+
+int pgp_fpe_forward_many(int n_hosts, int n, const float* windows, const float* h0, const float* P, double* probs,
+                         double* protos, void* stream) {
+  if (n_hosts != 16) return fail(PGP_ERR_UNSUPPORTED, "FPE training: n_hosts 16 only (FPE_16)");
+  if (n < 0 || (n > 0 && (!windows || !h0 || !P || !probs || !protos))) return fail(PGP_ERR_ARG, "bad arguments");
+  if (n == 0) return PGP_OK;
+  HIPCHK(launch_fpe_forward_many(n, windows, h0, P, probs, protos, reinterpret_cast<hipStream_t>(stream)));
+  return PGP_OK;
+}
+
 int pgp_tune_reserve_cus(int n) {
   if (n < 0) return fail(PGP_ERR_ARG, "negative CU count");
   tf_reserve_cus(n);

@@ -65,6 +65,12 @@ struct FpeArgs {
   float* emb;            // workspace [B][EP] -> K3
 };
 hipError_t launch_fpe(int H, const FpeArgs& a, hipStream_t st);
+// offline FPE_16 training (pgp_fpetrain.hip): one batch-1 step / n forwards
+int fpe_param_count();
+hipError_t launch_fpe_step(const float* win, const float* h0, const int* y, const int* cls, const float* P, float* G,
+                           int K, double* state, double update_min, double decay, double* loss, hipStream_t st);
+hipError_t launch_fpe_forward_many(int n, const float* wins, const float* h0s, const float* P, double* probs,
+                                   double* protos, hipStream_t st);
 
 // recover_decision's per-container moves (pgp_decide.hip)
 hipError_t launch_decide(int B, int C, const int* keep, const int* target, const int* cur, int* moves,

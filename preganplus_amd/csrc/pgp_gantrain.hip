@@ -146,24 +146,43 @@ __global__ __launch_bounds__(kGW * 64) void gan_fwd_kernel(int B, const float* _
 #pragma unroll
       for (int t = 0; t < 4; ++t) aG[t] = mfma(wa[t][r], bv[r], aG[t]);
   }
-  for (int c = wv; c < K::KS; c += kGW) {  // schedule chunks
-    const int f = 16 * c + 4 * g;
-    const bool fok = f < HH;
-    const f32x4 bv = ld4(fok && eok ? sched + env * HH + f : gk_zero);
-    f32x4 wa[4], wd[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      wa[t] = ld4(fok ? W1 + (long)(16 * t + i) * GIN + E2 + f : gk_zero);
-      wd[t] = ld4(fok ? D1 + (long)(16 * t + i) * DIN + f : gk_zero);
-    }
-    if (fok && eok) st4(row + G::GS_Z + f, bv);
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
+  {  // schedule chunks, software-pipelined: chunk c + kGW's operands are loaded
+     // before chunk c's MFMAs (one latency per wave, not one per chunk)
+    struct Ops {
+      f32x4 bv, wa[4], wd[4];
+    };
+    auto load = [&](int c, Ops& o) {
+      const int f = 16 * c + 4 * g;
+      const bool fok = f < HH;
+      o.bv = ld4(fok && eok ? sched + env * HH + f : gk_zero);
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
-        aG[t] = mfma(wa[t][r], bv[r], aG[t]);
-        aD[t] = mfma(wd[t][r], bv[r], aD[t]);
+        o.wa[t] = ld4(fok ? W1 + (long)(16 * t + i) * GIN + E2 + f : gk_zero);
+        o.wd[t] = ld4(fok ? D1 + (long)(16 * t + i) * DIN + f : gk_zero);
       }
+    };
+    // ping-pong buffers, no loop-carried copy (a copy would make the compiler
+    // wait for the prefetch at once)
+    Ops A, B;
+    auto step = [&](int c, const Ops& cur) {
+      const int f = 16 * c + 4 * g;
+      if (f < HH && eok) st4(row + G::GS_Z + f, cur.bv);
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          aG[t] = mfma(cur.wa[t][r], cur.bv[r], aG[t]);
+          aD[t] = mfma(cur.wd[t][r], cur.bv[r], aD[t]);
+        }
+    };
+    if (wv < K::KS) load(wv, A);
+    for (int c = wv; c < K::KS; c += 2 * kGW) {
+      load(c + kGW < K::KS ? c + kGW : c, B);
+      step(c, A);
+      if (c + kGW >= K::KS) break;
+      load(c + 2 * kGW < K::KS ? c + 2 * kGW : c + kGW, A);
+      step(c + kGW, B);
+    }
   }
   // Hg = W1 [e; s] + b1 (LeakyReLU(True): slope 1, the identity, models.py:127)
   reduce4(red, aG, wv, lane);
@@ -191,35 +210,55 @@ __global__ __launch_bounds__(kGW * 64) void gan_fwd_kernel(int B, const float* _
   const float* W2 = Pg + G::G_W2;
 #pragma unroll
   for (int t = 0; t < 4; ++t) aD[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int c = wv; c < K::KS; c += kGW) {
-    const int n0 = 16 * c, n = n0 + 4 * g;  // this lane's output rows n .. n + 3
-    const bool nok = n < HH, rok = n0 + i < HH;
-    f32x4 acc = ld4(nok ? Pg + G::G_B2 + n : gk_zero);
-    f32x4 wa[4], wd[4];
+  {  // software-pipelined as phase 1
+    struct Ops {
+      f32x4 bias, wa[4], wd[4], s4;
+    };
+    auto load = [&](int c, Ops& o) {
+      const int n0 = 16 * c, n = n0 + 4 * g;  // this lane's output rows n .. n + 3
+      const bool nok = n < HH, rok = n0 + i < HH;
+      o.bias = ld4(nok ? Pg + G::G_B2 + n : gk_zero);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) wa[q] = ld4(rok ? W2 + (long)(n0 + i) * 64 + 16 * q + 4 * g : gk_zero);
+      for (int q = 0; q < 4; ++q) o.wa[q] = ld4(rok ? W2 + (long)(n0 + i) * 64 + 16 * q + 4 * g : gk_zero);
 #pragma unroll
-    for (int t = 0; t < 4; ++t) wd[t] = ld4(nok ? D1 + (long)(16 * t + i) * DIN + HH + n : gk_zero);
-    const f32x4 s4 = ld4(nok && eok ? sched + env * HH + n : gk_zero);
+      for (int t = 0; t < 4; ++t) o.wd[t] = ld4(nok ? D1 + (long)(16 * t + i) * DIN + HH + n : gk_zero);
+      o.s4 = ld4(nok && eok ? sched + env * HH + n : gk_zero);
+    };
+    // ping-pong buffers, no loop-carried copy (a copy would make the compiler
+    // wait for the prefetch at once)
+    Ops A, B;
+    auto step = [&](int c, const Ops& cur) {
+      const int n = 16 * c + 4 * g;
+      const bool nok = n < HH;
+      f32x4 acc = cur.bias;
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
+      for (int q = 0; q < 4; ++q)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) acc = mfma(wa[q][r], hb[q][r], acc);
-    f32x4 tv, nv;
+        for (int r = 0; r < 4; ++r) acc = mfma(cur.wa[q][r], hb[q][r], acc);
+      f32x4 tv, nv;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      tv[r] = tanhf(acc[r]);
-      nv[r] = s4[r] + 4.0f * tv[r];
+      for (int r = 0; r < 4; ++r) {
+        tv[r] = tanhf(acc[r]);
+        nv[r] = cur.s4[r] + 4.0f * tv[r];
+      }
+      if (nok && eok) {
+        st4(row + G::GS_T + n, tv);
+        st4(row + G::GS_Z + HH + n, nv);
+        st4(ns_out + env * HH + n, nv);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) aD[t] = mfma(cur.wd[t][r], nv[r], aD[t]);
+    };
+    if (wv < K::KS) load(wv, A);
+    for (int c = wv; c < K::KS; c += 2 * kGW) {
+      load(c + kGW < K::KS ? c + kGW : c, B);
+      step(c, A);
+      if (c + kGW >= K::KS) break;
+      load(c + 2 * kGW < K::KS ? c + 2 * kGW : c + kGW, A);
+      step(c + kGW, B);
     }
-    if (nok && eok) {
-      st4(row + G::GS_T + n, tv);
-      st4(row + G::GS_Z + HH + n, nv);
-      st4(ns_out + env * HH + n, nv);
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-#pragma unroll
-      for (int t = 0; t < 4; ++t) aD[t] = mfma(wd[t][r], nv[r], aD[t]);
   }
   // DD = Disc1 [s; ns] + db1 (LeakyReLU(True) = identity, models.py:145)
   reduce4(red, aD, wv, lane);
@@ -303,17 +342,34 @@ __global__ __launch_bounds__(kGW * 64) void gan_gen_kernel(int B, const float* _
   f32x4 a[4];
 #pragma unroll
   for (int t = 0; t < 4; ++t) a[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int c = wv; c < K::KZ; c += kGW) {
-    const int f = 16 * c + 4 * g;
-    const bool fok = f < DIN;
-    const f32x4 bv = ld4(fok && eok ? row + G::GS_Z + f : gk_zero);
-    f32x4 wd[4];
+  {  // software-pipelined: chunk c + kGW loaded before chunk c's MFMAs
+    struct Ops {
+      f32x4 bv, wd[4];
+    };
+    auto load = [&](int c, Ops& o) {
+      const int f = 16 * c + 4 * g;
+      const bool fok = f < DIN;
+      o.bv = ld4(fok && eok ? row + G::GS_Z + f : gk_zero);
 #pragma unroll
-    for (int t = 0; t < 4; ++t) wd[t] = ld4(fok ? D1 + (long)(16 * t + i) * DIN + f : gk_zero);
+      for (int t = 0; t < 4; ++t) o.wd[t] = ld4(fok ? D1 + (long)(16 * t + i) * DIN + f : gk_zero);
+    };
+    // ping-pong buffers, no loop-carried copy (a copy would make the compiler
+    // wait for the prefetch at once)
+    Ops A, B;
+    auto step = [&](int c, const Ops& cur) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
+      for (int r = 0; r < 4; ++r)
 #pragma unroll
-      for (int t = 0; t < 4; ++t) a[t] = mfma(wd[t][r], bv[r], a[t]);
+        for (int t = 0; t < 4; ++t) a[t] = mfma(cur.wd[t][r], cur.bv[r], a[t]);
+    };
+    if (wv < K::KZ) load(wv, A);
+    for (int c = wv; c < K::KZ; c += 2 * kGW) {
+      load(c + kGW < K::KZ ? c + kGW : c, B);
+      step(c, A);
+      if (c + kGW >= K::KZ) break;
+      load(c + 2 * kGW < K::KZ ? c + 2 * kGW : c + kGW, A);
+      step(c + kGW, B);
+    }
   }
   reduce4(red, a, wv, lane);
   for (int k = threadIdx.x; k < 1024; k += blockDim.x) {
@@ -354,34 +410,55 @@ __global__ __launch_bounds__(kGW * 64) void gan_gen_kernel(int B, const float* _
   const float* W2 = Pg + G::G_W2;
 #pragma unroll
   for (int t = 0; t < 4; ++t) a[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int c = wv; c < K::KS; c += kGW) {
-    const int n0 = 16 * c, n = n0 + 4 * g;
-    const bool nok = n < HH, rok = n0 + i < HH;
-    // A[i][k]: Disc1'[hidden 16q + 4g + r][HH + n0 + i] (k-step (q, r))
-    float da[4][4], wa[4][4];
+  {  // software-pipelined: tile c + kGW's operands loaded before tile c's MFMAs
+    struct Ops {
+      float da[4][4], wa[4][4];
+      f32x4 tv;
+    };
+    auto load = [&](int c, Ops& o) {
+      const int n0 = 16 * c, n = n0 + 4 * g;
+      const bool nok = n < HH, rok = n0 + i < HH;
+      // A[i][k]: Disc1'[hidden 16q + 4g + r][HH + n0 + i] (k-step (q, r))
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
+      for (int q = 0; q < 4; ++q)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) da[q][r] = *(rok ? D1 + (long)(16 * q + 4 * g + r) * DIN + HH + n0 + i : gk_zero);
-    // A[i][k]: W2[n0 + 4g + r][16t + i] (k-step r of the dY tile)
+        for (int r = 0; r < 4; ++r)
+          o.da[q][r] = *(rok ? D1 + (long)(16 * q + 4 * g + r) * DIN + HH + n0 + i : gk_zero);
+      // A[i][k]: W2[n0 + 4g + r][16t + i] (k-step r of the dY tile)
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
+      for (int t = 0; t < 4; ++t)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) wa[t][r] = *(nok ? W2 + (long)(n + r) * 64 + 16 * t + i : gk_zero);
-    const f32x4 tv = ld4(nok && eok ? row + G::GS_T + n : gk_zero);
-    f32x4 dn = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int r = 0; r < 4; ++r) o.wa[t][r] = *(nok ? W2 + (long)(n + r) * 64 + 16 * t + i : gk_zero);
+      o.tv = ld4(nok && eok ? row + G::GS_T + n : gk_zero);
+    };
+    // ping-pong buffers, no loop-carried copy (a copy would make the compiler
+    // wait for the prefetch at once)
+    Ops A, B;
+    auto step = [&](int c, const Ops& cur) {
+      const int n = 16 * c + 4 * g;
+      const bool nok = n < HH;
+      f32x4 dn = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
+      for (int q = 0; q < 4; ++q)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) dn = mfma(da[q][r], db[q][r], dn);
-    f32x4 dy;
+        for (int r = 0; r < 4; ++r) dn = mfma(cur.da[q][r], db[q][r], dn);
+      f32x4 dy;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) dy[r] = 4.0f * dn[r] * (1.f - tv[r] * tv[r]);
-    if (nok && eok) st4(row + G::GS_DY + n, dy);
+      for (int r = 0; r < 4; ++r) dy[r] = 4.0f * dn[r] * (1.f - cur.tv[r] * cur.tv[r]);
+      if (nok && eok) st4(row + G::GS_DY + n, dy);
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
+      for (int r = 0; r < 4; ++r)
 #pragma unroll
-      for (int t = 0; t < 4; ++t) a[t] = mfma(wa[t][r], dy[r], a[t]);
+        for (int t = 0; t < 4; ++t) a[t] = mfma(cur.wa[t][r], dy[r], a[t]);
+    };
+    if (wv < K::KS) load(wv, A);
+    for (int c = wv; c < K::KS; c += 2 * kGW) {
+      load(c + kGW < K::KS ? c + kGW : c, B);
+      step(c, A);
+      if (c + kGW >= K::KS) break;
+      load(c + 2 * kGW < K::KS ? c + 2 * kGW : c + kGW, A);
+      step(c + kGW, B);
+    }
   }
   reduce4(red, a, wv, lane);
   for (int k = threadIdx.x; k < 1024; k += blockDim.x) {
@@ -449,11 +526,13 @@ __global__ __launch_bounds__(256) void outer_kernel(OuterArgs a) {
       x[t] = *(ok && kok[t] ? xr + 16 * t : gk_zero);
     }
   };
-  float y[4], x[4];
+  // three steps in flight: step s + 2's values are loaded before step s's MFMAs
+  float y[4], x[4], y1[4], x1[4];
   load(0, y, x);
+  load(steps > 1 ? 1 : 0, y1, x1);
   for (int s = 0; s < steps; ++s) {
     float yn[4], xn[4];
-    load(s + 1 < steps ? s + 1 : s, yn, xn);
+    load(s + 2 < steps ? s + 2 : s, yn, xn);
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       bs[t] += y[t];
@@ -462,8 +541,10 @@ __global__ __launch_bounds__(256) void outer_kernel(OuterArgs a) {
     }
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      y[t] = yn[t];
-      x[t] = xn[t];
+      y[t] = y1[t];
+      x[t] = x1[t];
+      y1[t] = yn[t];
+      x1[t] = xn[t];
     }
   }
 #pragma unroll

@@ -696,7 +696,10 @@ class PreGANRecovery(_SaveGan, Recovery):
             else:
                 packaged = os.path.join(_DATA, f"pregan_{self.env_name}_{self.hosts}.npz")
                 if not os.path.exists(packaged):
-                    raise FileNotFoundError(f"no checkpoint for {self.model_name} in {folder} or {packaged}")
+                    # no checkpoint at all: a new FPE trained offline, as the
+                    # reference's load_models does (PreGAN.py:24-27, 39-49)
+                    self._load_new_model(folder)
+                    return
                 weights, extra = W.load_npz(packaged)
                 gan = W.load_gan_checkpoints(folder, self.env_name, self.hosts)   # load_gan (PreGAN.py:31-33)
                 if gan is not None:
@@ -723,6 +726,58 @@ class PreGANRecovery(_SaveGan, Recovery):
     def _score(self, schedule):
         e, r = self.env.stats.runSimulation(torch.tensor(schedule))  # utils.py:97-100
         return COEFF_ENERGY * e + COEFF_LATENCY * r
+
+    def _load_new_model(self, folder):
+        """load_model without a checkpoint (utils.py:76-78: epoch -1, a new
+        FPE_16 with torch's module initialisation distributions,
+        weights.torch_default_fpe_weights, PGP_INIT_SEED seeds it), train_model
+        (PreGAN.py:39-49: num_epochs epochs of backprop + accuracy over
+        load_dataset's whole data/<env>/time_series.npy, the FPE checkpoint
+        rewritten after every epoch into the model folder), then the frozen
+        encoder with load_gan's GAN (its checkpoints, else new: epoch -1)."""
+        data = os.path.join("recovery/PreGANSrc/data", self.env_name, "time_series.npy")
+        if not os.path.exists(data):
+            raise FileNotFoundError(f"no checkpoint for {self.model_name} in {folder}, no packaged weights, and "
+                                    f"no training data {data} (utils.py:27-31)")
+        init = W.torch_default_fpe_weights(self.hosts, seed=int(os.environ.get("PGP_INIT_SEED", 0)))
+        series = np.load(data)
+        self.fpe_epoch, self.fpe_accuracy_list = -1, []
+        fpe, protos = self.train_model(init["fpe"], init["prototypes"], series, folder)
+        weights = {"fpe": fpe, "gen": init["gen"], "disc": init["disc"], "prototypes": protos}
+        extra = {"meta/gen/epoch": np.array(-1), "train_time_data": series}
+        gan = W.load_gan_checkpoints(folder, self.env_name, self.hosts)   # load_gan (PreGAN.py:31-33)
+        if gan is not None:
+            weights = dict(weights, **gan[0])
+            extra.update(gan[1])
+        self.load_models(weights=weights, extra=extra)
+
+    # -- PreGAN.py:39-49 (offline training; the plotter is out of scope) --
+    def train_model(self, fpe, prototypes, time_data, folder=None, num_epochs=None, generator=None):
+        """num_epochs epochs of backprop + accuracy of the FPE on the device
+        (preganplus_amd.fpetrain) over load_dataset(time_data) (utils.py:36-42),
+        each appending (loss, factor, AScore, CScore) to the FPE's accuracy_list
+        and, with a folder, rewriting {env}_FPE_{H}.ckpt (save_model,
+        utils.py:49-58).  The GRU states are drawn as the reference's forwards
+        draw them (torch.randn, models.py:70), backprop's then accuracy's.
+        Returns the trained FPE weights (fp64 dict) and prototypes."""
+        from . import fpetrain as FT
+        wins, anom, cls = TR.load_dataset(time_data)
+        n = len(wins)
+        ft = FT.FPETrainer(fpe, device=self.device, H=self.hosts)
+        st = TR.TuneState(prototypes)
+        for _ in range(NUM_EPOCHS if num_epochs is None else num_epochs):
+            self.fpe_epoch += 1
+            losses = ft.backprop(st, wins, FT.draw_h0(n, generator), anom, cls)
+            loss = float(np.mean([a for a, _ in losses]) + np.mean([t for _, t in losses]))   # train.py:56-57
+            factor = st.factor + TR.PROTO_UPDATE_MIN
+            asc, csc = ft.accuracy(st, wins, FT.draw_h0(n, generator), anom, cls)
+            self.fpe_accuracy_list.append((loss, factor, asc, csc))
+            if folder is not None:
+                os.makedirs(folder, exist_ok=True)
+                _save_atomic(ft.checkpoint(self.fpe_epoch, self.fpe_accuracy_list, st.protos),
+                             os.path.join(folder, f"{self.env_name}_{self.model_name}.ckpt"))
+        self.fpe_trainer, self.fpe_state = ft, st
+        return ft.weights_numpy(), st.protos.copy()
 
     # -- PreGAN.py:97-103 --
     def run_encoder(self, schedule_data):

@@ -652,7 +652,7 @@ class DPTuner:
     SUBSTAGES = ("forward", "targets", "backward", "all_reduce", "apply_adamw")
 
     def step(self, wins: torch.Tensor, y: torch.Tensor, cls: torch.Tensor, mark=None, before_update=None,
-             after_forward=None):
+             after_forward=None, before_backward=None):
         """wins [B,3,3H] fp32, y / cls [B,H] int32, all on the device.
         Returns the per-window (aloss, tloss) [B,2] fp64 device view.
         ``mark(k)``, if given, is called before sub-stage k of SUBSTAGES and
@@ -664,7 +664,9 @@ class DPTuner:
         is queued after this step's forward and backward).  ``after_forward``,
         if given, is called once the forward is issued (work for another stream
         that should queue behind the forward's launches but ahead of the
-        backward's)."""
+        backward's); ``before_backward``, if given, once the targets are issued,
+        right before the backward (work for another stream that should start
+        with the backward: the caller makes its stream wait for this one)."""
         mark = mark or (lambda k: None)
         import torch.distributed as dist
         tr, L = self.tr, self.tr._L
@@ -687,6 +689,8 @@ class DPTuner:
             self.state.data_ptr(), PROTO_UPDATE_MIN, self.mult.data_ptr(), self.tgt.data_ptr(), self.loss.data_ptr(),
             self.inc.data_ptr(), self.ws.data_ptr(), s), "pgp_tune_targets_dp")
         mark(2)
+        if before_backward is not None:
+            before_backward()
         tr.tune_backward(B, y, self.mult[:B], self.tgt[:B])
         mark(3)
         tr.all_reduce_grads("transformer", self.group)

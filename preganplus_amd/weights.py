@@ -241,6 +241,33 @@ def torch_default_weights(H, seed=0):
     return w
 
 
+def torch_default_fpe_weights(H=16, seed=0):
+    """A new PreGAN model as its constructors initialise it (load_model without
+    a checkpoint): nn.GRU every parameter U(+-1/sqrt(hidden = 3)); nn.Linear
+    U(+-1/sqrt(fan_in)) for weights and biases (GAT fc / attn_fc have no bias,
+    dlutils.py:300-301); nn.MultiheadAttention in_proj xavier_uniform, in_proj
+    and out_proj biases 0, out_proj.weight the Linear rule; prototypes U(0,1)
+    (torch.rand, models.py:62); Gen / Disc nn.Linear.  torch's distributions,
+    numpy's draws (parity unpinned for the values themselves)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    out = {"fpe": {}, "gen": {}, "disc": {}}
+    for sec, shapes in (("fpe", fpe_shapes(H)), ("gen", gen_shapes(H)), ("disc", disc_shapes(H))):
+        for name, shp in shapes.items():
+            if name.startswith("gru."):
+                a = rng.uniform(-1, 1, size=shp) / np.sqrt(3.0)
+            elif name.endswith(("in_proj_bias", "out_proj.bias")):
+                a = np.zeros(shp)
+            elif name.endswith("in_proj_weight"):
+                b = np.sqrt(6.0 / (shp[0] + shp[1]))
+                a = rng.uniform(-b, b, size=shp)
+            else:
+                fan_in = shp[1] if len(shp) == 2 else shapes[name.replace("bias", "weight")][1]
+                a = rng.uniform(-1, 1, size=shp) / np.sqrt(fan_in)
+            out[sec][name] = np.asarray(a, dtype=np.float32).astype(np.float64)
+    out["prototypes"] = rng.uniform(0, 1, size=(FPE_PROTOS, PROTO_DIM)).astype(np.float32).astype(np.float64)
+    return out
+
+
 def weights_checksum(weights):
     h = 0.0
     for sec in ("transformer", "gen", "disc"):

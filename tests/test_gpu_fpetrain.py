@@ -1,0 +1,121 @@
+"""PreGAN's offline FPE_16 training on the device (PreGAN.py:26-27, 39-49;
+preganplus_amd/fpetrain.py, csrc/pgp_fpetrain.hip) against the reference's own
+modules: tests/golden/fpe_train_h16.npz (make_golden_fpetrain.py) holds a new
+FPE_16, two epochs of train.backprop + accuracy over 24 windows of the
+framework series, and every GRU state the forwards drew.  fp32 device training
+vs the fp64 reference: parameters after each epoch within fp32 tolerance (the
+AdamW rule of the tuning tests: entries whose gradient is rounding noise take
+an lr-sized step of either sign), prototypes / factor / counters / scores from
+the same bookkeeping."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import pregan_oracle as O
+from oracle import pregan_train_oracle as TO
+
+pytestmark = pytest.mark.gpu
+
+
+def _fixture():
+    z = np.load("tests/golden/fpe_train_h16.npz")
+    init = {k[len("init/"):]: z[k] for k in z.files if k.startswith("init/") and k != "init/prototypes"}
+    return z, init
+
+
+def test_fpe_step_gradient_matches_autograd():
+    """One device step (forward, bookkeeping, backward) == torch autograd of
+    the FPE restatement (pinned to the reference), from the same weights, h0
+    and state: losses, the gradient of every parameter, the updated state."""
+    from preganplus_amd import fpetrain as FT
+    from preganplus_amd import train as TR
+    z, init = _fixture()
+    ft = FT.FPETrainer(init)
+    wins, anom, cls = z["wins"], z["anom"], z["cls"]
+    i = int(np.argmax(anom.sum(1) > 0))            # a window with a positive label
+    h0 = z["ep0/h0_backprop"][i:i + 1]
+    st = TR.TuneState(z["init/prototypes"], 0.2)
+    st.num_zero, st.num_ones = 7, 3
+    state = torch.tensor(st.vector(), dtype=torch.float64, device="cuda")
+    dev = lambda a, dt: torch.as_tensor(np.asarray(a), dtype=dt).cuda().contiguous()
+    w, h = dev(wins[i], torch.float32), dev(h0, torch.float32)
+    y, c = dev(anom[i], torch.int32), dev(np.clip(cls[i], 0, 2), torch.int32)
+    loss = torch.zeros(2, dtype=torch.float64, device="cuda")
+    ft._L.pgp_fpe_train_step(16, 3, w.data_ptr(), h.data_ptr(), y.data_ptr(), c.data_ptr(), ft.P.data_ptr(),
+                             ft.G.data_ptr(), state.data_ptr(), TR.PROTO_UPDATE_MIN, TR.PROTO_FACTOR_DECAY,
+                             loss.data_ptr(), ft._stream())
+    torch.cuda.synchronize()
+    fw = TO.leaf_params(init, skip=())
+    sto = TO.TuneState(z["init/prototypes"], 0.2)
+    sto.num_zero, sto.num_ones = 7, 3
+    probs, protos = TO.fpe_t(fw, torch.tensor(wins[i:i + 1]), torch.tensor(h0))
+    aloss, tloss = TO.custom_loss(probs[0], protos[0], anom[i], cls[i], sto)
+    (aloss + tloss).backward()
+    lo = loss.cpu().numpy()
+    assert lo[0] == pytest.approx(float(aloss), rel=1e-4) and lo[1] == pytest.approx(float(tloss), rel=1e-3, abs=1e-6)
+    g = ft.G.cpu().numpy()
+    for t in ft.tensors:
+        want = fw[t["name"]].grad
+        want = np.zeros(t["n"]) if want is None else want.numpy().reshape(-1)
+        got = g[t["offset"]:t["offset"] + t["n"]]
+        tol = 1e-3 * np.abs(want) + 1e-4 * (np.abs(want).max() + 1e-30)
+        assert np.all(np.abs(got - want) <= tol), (t["name"], np.abs(got - want).max(), np.abs(want).max())
+    sv = state.cpu().numpy()
+    np.testing.assert_allclose(sv[:6].reshape(3, 2), np.stack([p.numpy() for p in sto.protos]), rtol=1e-6)
+    assert sv[6] == pytest.approx(sto.factor, rel=1e-15) and (sv[7], sv[8]) == (sto.num_zero, sto.num_ones)
+
+
+def test_fpe_offline_training_epochs_match_reference():
+    from preganplus_amd import fpetrain as FT
+    from preganplus_amd import train as TR
+    z, init = _fixture()
+    ft = FT.FPETrainer(init)
+    st = TR.TuneState(z["init/prototypes"], 0.2)
+    wins, anom, cls = z["wins"], z["anom"], z["cls"]
+    for ep in range(2):
+        losses = ft.backprop(st, wins, z[f"ep{ep}/h0_backprop"], anom, cls)
+        loss = np.mean([a for a, _ in losses]) + np.mean([t for _, t in losses])
+        assert loss == pytest.approx(float(z[f"ep{ep}/loss"]), rel=1e-4)
+        assert st.factor + O.PROTO_UPDATE_MIN == pytest.approx(float(z[f"ep{ep}/factor"]), rel=1e-14)
+        assert (st.num_zero, st.num_ones) == (z[f"ep{ep}/num_zero"], z[f"ep{ep}/num_ones"])
+        np.testing.assert_allclose(st.protos, z[f"ep{ep}/prototypes"], rtol=1e-4, atol=1e-6)
+        pw = ft.weights_numpy()
+        lr = FT.FPE_LR
+        for t in ft.tensors:
+            want = z[f"ep{ep}/p/{t['name']}"].reshape(-1)
+            got = pw[t["name"]].reshape(-1)
+            # fp32 tolerance for all but entries whose gradient is rounding noise: those take
+            # AdamW steps of arbitrary sign on both sides, at most 2 lr apart per step
+            tol = 1e-4 * np.abs(want) + 1e-5 * np.abs(want).max()
+            bad = np.abs(got - want) > tol
+            assert bad.mean() < 0.01, (t["name"], bad.sum(), np.abs(got - want).max())
+            assert np.all(np.abs(got - want) <= 2 * lr * 24 * (ep + 1)), t["name"]
+            assert t["step"] == float(z[f"ep{ep}/step/{t['name']}"]), t["name"]
+        asc, csc = ft.accuracy(st, wins, z[f"ep{ep}/h0_accuracy"], anom, cls)
+        assert asc == pytest.approx(float(z[f"ep{ep}/ascore"]), abs=1.0 / (16 * 24) + 1e-12)
+        assert csc == pytest.approx(float(z[f"ep{ep}/cscore"]), abs=0.05)
+
+
+def test_pregan_new_model_trains_offline(tmp_path, monkeypatch):
+    """No FPE checkpoint, no packaged weights (the framework environment):
+    PreGANRecovery trains a new FPE for num_epochs (here 2, on 30 rows of the
+    framework series), rewriting {env}_FPE_16.ckpt each epoch in the
+    reference's format, then runs the plugin on the trained encoder."""
+    from preganplus_amd import recovery as RC
+    from preganplus_amd import weights as W
+    rng = np.random.default_rng(4)
+    d = tmp_path / "recovery" / "PreGANSrc" / "data" / "framework"
+    d.mkdir(parents=True)
+    np.save(d / "time_series.npy", rng.uniform(0, 100, size=(30, 48)))
+    monkeypatch.chdir(tmp_path)
+    monkeypatch.setattr(RC, "NUM_EPOCHS", 2)
+    torch.manual_seed(5)
+    rec = RC.PreGANRecovery(16, "framework", training=False, model_folder=str(tmp_path / "ck"))
+    assert rec.fpe_epoch == 1 and len(rec.fpe_accuracy_list) == 2
+    ck = W._safe_load(str(tmp_path / "ck" / "framework_FPE_16.ckpt"))
+    assert int(ck["epoch"]) == 1 and len(ck["accuracy_list"]) == 2 and len(ck["model_prototypes"]) == 3
+    fw = rec.fpe_trainer.weights_numpy()
+    for k, v in ck["model_state_dict"].items():
+        np.testing.assert_array_equal(np.asarray(v), fw[k])
+    assert rec.epoch == -1            # a new GAN (load_gan without checkpoints)
+    np.testing.assert_array_equal(rec.weights["fpe"]["encoder.0.weight"], fw["encoder.0.weight"])

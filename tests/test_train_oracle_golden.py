@@ -198,3 +198,41 @@ def test_dp_batch_h50_matches_reference():
     for k in w["transformer"]:
         if k != "pos_encoder.pe":
             D.check(z, f"grad/{k}", tw[k].grad.numpy(), _close(1e-8, 1e-9), sum_rel=1e-8, key=k)
+
+
+def fpe_train_fixture():
+    z = np.load("tests/golden/fpe_train_h16.npz")
+    init = {k[len("init/"):]: z[k] for k in z.files if k.startswith("init/") and k != "init/prototypes"}
+    return z, init
+
+
+def test_fpe_offline_training_matches_reference():
+    """The torch restatement of PreGAN's offline FPE training (fpe_backprop,
+    PreGAN.py:39-49 / train.py:42-57 on FPE_16) against the reference's own
+    modules (tests/golden/make_golden_fpetrain.py): two epochs over 24 windows
+    of the framework series with the recorded GRU states; parameters, AdamW
+    moments, prototypes, factor, counters after each epoch, and accuracy()'s
+    scores (train.py:94-109) from the same forwards."""
+    from preganplus_amd import train as TR
+    z, init = fpe_train_fixture()
+    fw = TO.leaf_params(init, skip=())
+    opt = TO.AdamW(fw, 1e-4)
+    st = TO.TuneState(z["init/prototypes"], 0.2)
+    wins, anom, cls = z["wins"], z["anom"], z["cls"]
+    for ep in range(2):
+        losses = TO.fpe_backprop(fw, opt, st, wins, z[f"ep{ep}/h0_backprop"], anom, cls)
+        loss = np.mean([a for a, _ in losses]) + np.mean([t for _, t in losses])
+        assert loss == pytest.approx(float(z[f"ep{ep}/loss"]), rel=1e-12)
+        assert st.factor + O.PROTO_UPDATE_MIN == pytest.approx(float(z[f"ep{ep}/factor"]), rel=1e-14)
+        assert (st.num_zero, st.num_ones) == (z[f"ep{ep}/num_zero"], z[f"ep{ep}/num_ones"])
+        for k, q in fw.items():
+            np.testing.assert_allclose(q.detach().numpy(), z[f"ep{ep}/p/{k}"], rtol=1e-10, atol=1e-13, err_msg=k)
+            np.testing.assert_allclose(opt.m[k].numpy(), z[f"ep{ep}/m/{k}"], rtol=1e-9, atol=1e-14, err_msg=k)
+            assert opt.step[k] == float(z[f"ep{ep}/step/{k}"])
+        np.testing.assert_allclose(np.stack([p.numpy() for p in st.protos]), z[f"ep{ep}/prototypes"], rtol=1e-12)
+        with torch.no_grad():
+            probs, protos = TO.fpe_t(fw, torch.tensor(wins), torch.tensor(z[f"ep{ep}/h0_accuracy"]))
+        asc, csc = TR.accuracy_scores(probs.numpy(), protos.numpy(), anom, cls,
+                                      np.stack([p.numpy() for p in st.protos]))
+        assert asc == pytest.approx(float(z[f"ep{ep}/ascore"]), rel=1e-12)
+        assert csc == pytest.approx(float(z[f"ep{ep}/cscore"]), rel=1e-12)

@@ -69,6 +69,7 @@ for step in "$@"; do
       run tune50 400 python3 -u bench.py --config tune --hosts 50 --steps 50 --warmup 5
       run tune16 400 python3 -u bench.py --config tune --hosts 16 --steps 50 --warmup 5
       run prof_tune 240 rocprofv3 --kernel-trace --stats -d $OUT/prof_tune -o tune --output-format csv -- python3 bench.py --config tune --hosts 50 --steps 60 --warmup 10 --no-cpu-baseline
+      run prof_tune16 240 rocprofv3 --kernel-trace --stats -d $OUT/prof_tune16 -o tune --output-format csv -- python3 bench.py --config tune --hosts 16 --steps 60 --warmup 10 --no-cpu-baseline
       ;;
     tunepmc)
       pmc tunestall1 "$STALL1" --config tune --hosts 50 --steps 3 --warmup 1 --no-cpu-baseline
