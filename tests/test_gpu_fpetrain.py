@@ -81,16 +81,28 @@ def test_fpe_offline_training_epochs_match_reference():
         np.testing.assert_allclose(st.protos, z[f"ep{ep}/prototypes"], rtol=1e-4, atol=1e-6)
         pw = ft.weights_numpy()
         lr = FT.FPE_LR
+        fails = []
         for t in ft.tensors:
             want = z[f"ep{ep}/p/{t['name']}"].reshape(-1)
             got = pw[t["name"]].reshape(-1)
             # fp32 tolerance for all but entries whose gradient is rounding noise: those take
-            # AdamW steps of arbitrary sign on both sides, at most 2 lr apart per step
+            # AdamW steps of arbitrary sign on both sides, at most 2 lr apart per step.  The
+            # attention's key bias (in_proj_bias[E:2E]) is such an entry everywhere: its exact
+            # gradient is zero (softmax is invariant to a shift of all scores of a query), as
+            # in the tuning tests (DESIGN §8 "Parity")
+            noise = np.zeros(t["n"], dtype=bool)
+            if t["name"] == "mha.in_proj_bias":
+                E = t["n"] // 3
+                noise[E:2 * E] = True
             tol = 1e-4 * np.abs(want) + 1e-5 * np.abs(want).max()
-            bad = np.abs(got - want) > tol
-            assert bad.mean() < 0.01, (t["name"], bad.sum(), np.abs(got - want).max())
-            assert np.all(np.abs(got - want) <= 2 * lr * 24 * (ep + 1)), t["name"]
-            assert t["step"] == float(z[f"ep{ep}/step/{t['name']}"]), t["name"]
+            bad = (np.abs(got - want) > tol) & ~noise
+            if bad.mean() >= 0.01:
+                fails.append((t["name"], int(bad.sum()), float(np.abs(got - want).max())))
+            if not np.all(np.abs(got - want) <= 2 * lr * 24 * (ep + 1)):
+                fails.append((t["name"], "beyond the lr bound", float(np.abs(got - want).max())))
+            if t["step"] != float(z[f"ep{ep}/step/{t['name']}"]):
+                fails.append((t["name"], "step", t["step"]))
+        assert not fails, (ep, fails)
         asc, csc = ft.accuracy(st, wins, z[f"ep{ep}/h0_accuracy"], anom, cls)
         assert asc == pytest.approx(float(z[f"ep{ep}/ascore"]), abs=1.0 / (16 * 24) + 1e-12)
         assert csc == pytest.approx(float(z[f"ep{ep}/cscore"]), abs=0.05)

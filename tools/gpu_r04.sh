@@ -7,6 +7,7 @@
 #   fleet   C5 line + FETCH / WRITE passes at its batch
 #   tune    C3 lines (H=50, H=16) + rocprofv3 kernel stats of H=50
 #   tunepmc C3 stall passes (H=50)
+#   graphc  HIP graph branch concurrency / launch-cost probe
 #   others  C4, C1, loop lines
 # every GPU step runs under its own timeout; the script stops at the first failure
 set -u
@@ -48,6 +49,10 @@ for step in "$@"; do
       run t_train 600 python -u -m pytest tests/test_gpu_train.py tests/test_gpu_bench_modes.py tests/test_gpu_dist.py -x -v -p no:cacheprovider --timeout 300 --timeout-method thread
       tail -2 $OUT/t_train.out
       ;;
+    tfpe)
+      run t_fpe 600 python -u -m pytest tests/test_gpu_fpetrain.py tests/test_gpu_checkpoint.py -v -p no:cacheprovider --timeout 300 --timeout-method thread
+      tail -2 $OUT/t_fpe.out
+      ;;
     c2)
       run c2 400 python3 -u bench.py
       run prof_c2 240 rocprofv3 --kernel-trace --stats -d $OUT/prof_c2 -o c2 --output-format csv -- python3 bench.py --steps 60 --warmup 10 --no-cpu-baseline
@@ -74,6 +79,10 @@ for step in "$@"; do
     tunepmc)
       pmc tunestall1 "$STALL1" --config tune --hosts 50 --steps 3 --warmup 1 --no-cpu-baseline
       pmc tunestall2 "$STALL2" --config tune --hosts 50 --steps 3 --warmup 1 --no-cpu-baseline
+      ;;
+    graphc)
+      run graphc 120 python3 -u tools/graph_concurrency.py
+      cat $OUT/graphc.out
       ;;
     others)
       run fpe 300 python3 -u bench.py --config fpe --steps 100 --warmup 5
