@@ -497,7 +497,8 @@ def bench_tune(args):
       1. tune_model's on-the-fly dataset (utils.py:40-47): each environment's
          last 10 rows -> 10 windows + 98th-percentile labels and classes
          (pgp_tune_dataset), and run_encoder's window of the same rows
-      2. detect (PreGANPlus.py:107-131): encoder forward of that window ->
+      2. detect (PreGANPlus.py:107-131): encoder forward of that window (the
+         last E rows of the tuning forward's batch: same step-start weights) ->
          masked prototype embedding
       3. train_gan (PreGANPlus.py:60-81): Gen + Disc forward, the label from
          two runSimulation scores on the device (pgp_simulate),
@@ -507,7 +508,8 @@ def bench_tune(args):
          step-start state (pgp_tune_targets_dp), backward, one RCCL gradient
          all-reduce + one all-reduce of the state increments, state update and
          AdamW from device tables (DPTuner)
-    No fixed labels, CE weights or targets, and no host round trip."""
+    No fixed labels, CE weights or targets, and no host round trip
+    (TR.OnlineTrainStep; the timed steps replay it as a captured HIP graph)."""
     from preganplus_amd import simulate as SIM
     from preganplus_amd import train as TR
     world, rank, device = _dist_setup()
@@ -516,103 +518,61 @@ def bench_tune(args):
     R = 10                                             # LATEST_WINDOW_SIZE (constants.py:16)
     B = E * R
     w = W.synth_weights(H, seed=0)
-    tr = TR.Trainer(H, w, device=device, max_batch=B)
+    tr = TR.Trainer(H, w, device=device, max_batch=B + E)   # the tuning windows + run_encoder's, one forward
     st = TR.TuneState(w["prototypes"])
-    tune_group, gan_group = TR.dp_groups()    # the GAN step's collectives on a communicator of their own
-    tun = TR.DPTuner(tr, st, B, group=tune_group)
     series_h, tmax_h = synth_series(E, H, 5 + rank, R)
-    series = torch.tensor(series_h, device=device)
-    tmax = torch.tensor(tmax_h, device=device)
     g = torch.Generator(device=device).manual_seed(17 + rank)
     s = torch.zeros((E, H, H), device=device)
     s.scatter_(2, torch.randint(0, H, (E, H, 1), generator=g, device=device), 1.0)
-    envs = torch.tensor(SIM.synth_envs(E, H, seed=5 + rank), device=device)
+    envs = SIM.synth_envs(E, H, seed=5 + rank)
     sim = SIM.Simulation(H, device=device)
-    sim_out = torch.empty((E, 4), dtype=torch.float64, device=device)
-    gan_target = torch.empty((E, 2), dtype=torch.float32, device=device)
-    bufs = TR.dataset_buffers(tr, E, R)
-    emb_buf = torch.empty((E, H, 2), dtype=torch.float32, device=device)
     names = ("dataset", "detect", "train_gan", "tune_model")
     subs = TR.DPTuner.SUBSTAGES
     ev = [[torch.cuda.Event(enable_timing=True) for _ in range(len(names) + 2)] for _ in range(max(args.steps, 1))]
     sev = [[torch.cuda.Event(enable_timing=True) for _ in range(len(subs) + 1)] for _ in range(max(args.steps, 1))]
-    # train_gan and tune_model share no data (run_model calls them back to
-    # back, PreGANPlus.py:133-134: the GAN step reads the embedding and writes
-    # the GAN's weights; the tuning step reads the dataset and writes the
-    # Transformer's), so the GAN step runs on a second stream beside the
-    # tuning step; the step ends when both have (results are unchanged:
-    # tests/test_gpu_dist.py and test_gpu_tunedp.py run them in either order)
-    main = torch.cuda.current_stream(device)
+    # the step's streams (TR.OnlineTrainStep): the GAN step runs on a second
+    # stream beside the tuning step (no shared data, PreGANPlus.py:133-134);
+    # the main stream is not the default one, which a HIP graph cannot capture
+    main = torch.cuda.Stream(device)
+    torch.cuda.set_stream(main)
     side = main if os.environ.get("PGP_BENCH_ONE_STREAM") == "1" else torch.cuda.Stream(device)
     # world > 1, one GPU per rank: main + this second stream + the two
     # communicators' streams are the 4 hardware queues a process gets
     # (GPU_MAX_HW_QUEUES), so the tuning backward's side work (decoder and
     # in_proj weight gradients) runs on this same second stream instead of a
-    # fifth (pgp_tune_set_side_stream), and the GAN step is issued right after
-    # detect, ahead of that side work
-    shared_side = _share_side_stream(world, main, side)
+    # fifth (pgp_tune_set_side_stream), and the GAN step is issued ahead of
+    # that side work
+    _share_side_stream(world, main, side)
     reserved = _reserve_cus(main, side)
-
-    # detect reads the step-start weights and feeds only the GAN step, so it
-    # runs on the second stream too, with a workspace of its own; the tuning
-    # step's weight update waits for it (before_update).  The workspace is its
-    # own in single-stream mode as well: detect is issued between the tuning
-    # forward and its targets / backward, which read the trainer's workspace
-    det_ctx = tr.forward_context(E)
-    det_done = torch.cuda.Event()
-
-    def step(e=None, se=None):
-        rec = (lambda k: e[k].record(main)) if e is not None else (lambda k: None)
-        rec(0)
-        wins, y, cls, inf = TR.tune_dataset(tr, series, tmax, out=bufs)
-        rec(1)
-
-        def detect():
-            with torch.cuda.stream(side):
-                if e is not None:
-                    e[5].record(side)
-                logits, protos = tr.tune_forward(inf, ctx=det_ctx)
-                embedding(logits, protos, out=emb_buf)   # PreGANPlus.py:129
-                det_done.record(side)
-                if e is not None:
-                    e[2].record(side)
-        def gan():
-            with torch.cuda.stream(side):
-                TR.train_gan_batched(tr, sim, envs, emb_buf, s, out=sim_out, target=gan_target, all_reduce=True,
-                                     group=gan_group)
-                if e is not None:
-                    e[3].record(side)
-
-        # detect + the GAN step start with the tuning BACKWARD (the second
-        # stream waits for the tuning step's targets): its fused launches leave
-        # GAN_RESERVED_CUS CUs free, while the forward's would be slowed by a
-        # concurrent detect forward (round 4: detect beside the forward cost the
-        # tuning forward ~55 us, profiles/r04/)
-        def detect_gan():
-            side.wait_stream(main)
-            detect()
-            gan()
-        tun.step(wins, y, cls, mark=(lambda k: se[k].record(main)) if se is not None else None,
-                 before_update=det_done, before_backward=detect_gan)
-        main.wait_stream(side)
-        rec(4)
-
+    step = TR.OnlineTrainStep(tr, st, sim, series_h, tmax_h, s, envs, R=R, side=side, groups=TR.dp_groups())
     for _ in range(args.warmup):
-        step()
-    it = iter(zip(ev, sev))
-    el = _timed(world, device, lambda: step(*next(it)), args.steps)
-    # train_gan (side stream, from the embedding to its last kernel) and
-    # tune_model (main stream, its first sub-stage mark to its last) overlap
-    # detect (second stream: its start e[5] to the embedding e[2]), train_gan
-    # (second stream, after detect) and tune_model (main stream) overlap
+        step.run()
+    # the timed steps: the step captured once as a HIP graph and replayed (the
+    # host issues ~70 launches per step otherwise: at 16 hosts the eager step is
+    # bound by that issue rate).  World > 1 keeps eager issue (RCCL calls).
+    graphed = world == 1 and os.environ.get("PGP_BENCH_GRAPH", "1") != "0"
+    if graphed:
+        step.capture()
+    el = _timed(world, device, step.run, args.steps)
+    # stage spans: the same step issued eagerly with HIP events (a captured
+    # step cannot record timing events)
+    n_ev = min(args.steps, len(ev))
+    for k in range(n_ev):
+        step.prep()
+        step.issue(ev[k], sev[k])
+    torch.cuda.synchronize()
+    # dataset (main stream), detect's embedding (second stream: its start e[5]
+    # to e[2]), train_gan (second stream, after it) and tune_model (main
+    # stream, its first sub-stage mark to its last); the last three overlap
     stage = np.array([[e[0].elapsed_time(e[1]), e[5].elapsed_time(e[2]), e[2].elapsed_time(e[3]),
-                       s_[0].elapsed_time(s_[len(subs)])] for e, s_ in zip(ev[:args.steps], sev[:args.steps])]).mean(0)
-    sub = np.array([[e[k].elapsed_time(e[k + 1]) for k in range(len(subs))] for e in sev[:args.steps]]).mean(0)
+                       s_[0].elapsed_time(s_[len(subs)])] for e, s_ in zip(ev[:n_ev], sev[:n_ev])]).mean(0)
+    sub = np.array([[e[k].elapsed_time(e[k + 1]) for k in range(len(subs))] for e in sev[:n_ev]]).mean(0)
+    eager_ms = float(np.mean([e[0].elapsed_time(e[4]) for e in ev[:n_ev]]))
     # roofline of the dominant kernels: the six fused encoder launches of the
     # tuning forward + backward, timed live with HIP events recorded on their
-    # stream inside the library (pgp_tune_timing) over extra steps after the
-    # timed region; achieved = their executed MFMA flops (ISA-counted per unit,
-    # roofline.TUNE_MFMA_PER_UNIT) / the mean launch duration
+    # stream inside the library (pgp_tune_timing) over extra eager steps after
+    # the timed region; achieved = their executed MFMA flops (ISA-counted per
+    # unit, roofline.TUNE_MFMA_PER_UNIT) / the mean launch duration
     RL = R_ROOF  # (R is the window count here)
     L = _native.lib()
     L.pgp_tune_timing.argtypes = [ctypes.c_int]
@@ -621,12 +581,13 @@ def bench_tune(args):
     fused = []
     ms6 = (ctypes.c_float * 6)()
     for _ in range(max(3, min(args.steps, 10))):
-        step()
+        step.prep()
+        step.issue()
         _native.check(L.pgp_tune_fused_ms(ms6), "pgp_tune_fused_ms")
         fused.append(list(ms6))
     _native.check(L.pgp_tune_timing(0), "pgp_tune_timing")
     fused_ms = np.array(fused).mean(0)
-    flops = RL.tune_fused_flops(H, B)
+    flops = RL.tune_fused_flops(H, B, B + E)
     roof = None
     if flops is not None:
         rates = [f / (t * 1e-3) / 1e12 for f, t in zip(flops, fused_ms)]
@@ -654,9 +615,14 @@ def bench_tune(args):
                        "windows_per_gpu": B, "parallelism": f"dp{world}" + (f" + {_backend_label()} all-reduce "
                                                                            "(grads, state; GAN on its own group)"
                                                                            if world > 1 else "")},
+            "timed": ("the step captured once as a HIP graph and replayed (AdamW scalars from device rows "
+                      "written before each replay)" if graphed else "eager issue"),
+            "eager_ms_per_step": eager_ms,
             "stage_ms": {n: float(stage[k]) for k, n in enumerate(names)},
-            "streams": "detect + train_gan on a second stream, concurrent with tune_model's backward (no shared "
-                       "data; the tuning step's weight update waits for detect)" if side is not main else "one stream",
+            "stage_note": ("eager steps with HIP events; detect = run_encoder's windows as the last E rows of the "
+                           "tuning forward (same step-start weights), then their embedding on the second stream"),
+            "streams": "detect's embedding + train_gan on a second stream, concurrent with tune_model's backward "
+                       "(no shared data)" if side is not main else "one stream",
             "reserved_cus": reserved,
             "tune_model_ms": {n: float(sub[k]) for k, n in enumerate(subs)},
             "grad_all_reduce_ms": float(sub[subs.index("all_reduce")]),
@@ -670,9 +636,10 @@ def bench_tune(args):
                     "unit": "TFLOP/s", "frac": fl / (ms * 1e-3) / 1e12 / RL.PEAK_FP32_TFLOPS, "flops": fl,
                     "basis": basis}
                 for n, ms, fl, basis in (
-                    ("tune_model", stage[3], RL.tune_step_flops_per_window(H) * B,
+                    ("tune_model", stage[3], RL.tune_step_flops_per_window(H) * (B + E / 3),
                      f"{RL.tune_step_flops_per_window(H) / 1e6:.2f} MFLOP per tuning window (3 x the Transformer "
-                     f"forward: input and weight gradients) x {B} windows"),
+                     f"forward: input and weight gradients) x {B} windows + 1/3 of it (the forward) x {E} detect "
+                     f"windows"),
                     ("train_gan", stage[2], RL.gan_step_flops_per_env(H) * E,
                      f"{RL.gan_step_flops_per_env(H) / 1e6:.2f} MFLOP per environment (Gen + Disc forward, Disc "
                      f"step, Gen step through the updated Disc) x {E} environments"))},

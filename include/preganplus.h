@@ -226,13 +226,23 @@ int pgp_tune_forward(int n_hosts, int batch, const float* windows, const float* 
  * into G (the caller zeroes G before the step). */
 int pgp_tune_backward(int n_hosts, int batch, const float* P, float* G, float* workspace, const float* logits,
                       const float* protos, const int* y, const float* mult, const float* tgt, void* stream);
+/* The same backward over the FIRST `batch` windows of a pgp_tune_forward of
+ * fwd_batch >= batch windows (same workspace; logits / protos / y / mult / tgt
+ * of those windows): a caller that appends inference windows to the tuning
+ * batch (the C3 detect: run_encoder's windows, PreGANPlus.py:107-113, read the
+ * same step-start weights) runs one forward for both and differentiates only
+ * the tuning windows.  pgp_tune_backward(B) == pgp_tune_backward_prefix(B, B). */
+int pgp_tune_backward_prefix(int n_hosts, int fwd_batch, int batch, const float* P, float* G, float* workspace,
+                             const float* logits, const float* protos, const int* y, const float* mult,
+                             const float* tgt, void* stream);
 /* Streams: both calls may run part of their work (the decoder weight packing;
  * the decoders' and in_proj's weight gradients) on a library-owned,
  * low-priority stream of the current device, forked from `stream` by an event
  * and joined back into it before the call's last launch, so every result is
  * ordered on `stream` as if all of it ran there.  While `stream` is being
- * captured into a graph, or with PGP_TUNE_SIDE_STREAM=0 in the environment,
- * everything stays on `stream`.
+ * captured into a graph the fork / join are captured too (the graph holds the
+ * two branches); with PGP_TUNE_SIDE_STREAM=0 in the environment everything
+ * stays on `stream`.
  * pgp_tune_set_side_stream(s): use the caller's stream `s` as that side stream
  * on the current device from now on (NULL: the library's own again).  A
  * data-parallel caller that already runs a second stream (the GAN step) and two

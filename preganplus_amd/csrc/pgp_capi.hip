@@ -359,6 +359,21 @@ int pgp_tune_backward(int n_hosts, int batch, const float* P, float* G, float* w
   return PGP_OK;
 }
 
+int pgp_tune_backward_prefix(int n_hosts, int fwd_batch, int batch, const float* P, float* G, float* workspace,
+                             const float* logits, const float* protos, const int* y, const float* mult,
+                             const float* tgt, void* stream) {
+  if (!supported(n_hosts)) return fail(PGP_ERR_UNSUPPORTED, "host count");
+  if (batch < 0 || batch > fwd_batch ||
+      (batch > 0 && (!P || !G || !workspace || !logits || !protos || !y || !mult || !tgt)))
+    return fail(PGP_ERR_ARG, "bad tune_backward_prefix arguments");
+  if (batch == 0) return PGP_OK;
+  TunePlan p;
+  if (!tune_plan_prefix(n_hosts, fwd_batch, batch, &p)) return fail(PGP_ERR_ARG, "tune_backward_prefix plan");
+  HIPCHK(launch_tune_backward(p, P, G, workspace, logits, protos, y, mult, tgt,
+                              reinterpret_cast<hipStream_t>(stream)));
+  return PGP_OK;
+}
+
 size_t pgp_fpe_param_len(int n_hosts) { return n_hosts == 16 ? (size_t)fpe_param_count() : 0; }
 
 int pgp_fpe_train_step(int n_hosts, int n_protos, const float* window, const float* h0, const int* y, const int* cls,

@@ -923,7 +923,7 @@ TfTiming g_tft;
 // in their last unit round (tf_unit_range packs the waves with an extra unit
 // into the first workgroups).  One non-blocking stream per device at low
 // priority; fork / join by events.  While the caller's stream is being
-// captured into a graph the work stays on it (serial, same results).
+// captured into a graph the events become the graph's edges (two branches).
 struct SideStream {
   hipStream_t s = nullptr;
   hipEvent_t ev[8] = {};
@@ -957,8 +957,13 @@ struct Fork {
       return v && v[0] == '0';
     }();
     if (off) return;  // PGP_TUNE_SIDE_STREAM=0: everything on the caller's stream
+    // while `st` is being captured into a graph the fork / join events become
+    // the graph's edges: the side stream joins the capture at the fork's wait
+    // and leaves it at the join, so the graph keeps the two branches (a
+    // replayed graph runs independent branches concurrently, measured:
+    // profiles/r04/s3/graph_concurrency.txt)
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return;
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs == hipStreamCaptureStatusInvalidated) return;
     ss = side_stream();
     if (!ss) return;
     int dev = 0;
@@ -1171,6 +1176,28 @@ bool tune_plan(int H, int B, TunePlan* p) {
 #undef CASE
   }
   return false;
+}
+
+// The plan of a backward over the first B windows of a forward of B_fwd: the
+// regions stay where the forward's plan put them (its activations are read in
+// place; rows are window-major, so the first B windows are the first B*3H
+// rows), the launch geometry is B's.  Every bound that sized a region grows
+// with the batch, so B's grids fit B_fwd's regions.  The spare row M of the
+// backward's outputs is then a row of window B: the backward only writes
+// temporaries (da, db, dQKV) there, never a forward activation.
+bool tune_plan_prefix(int H, int B_fwd, int B, TunePlan* p) {
+  if (B < 1 || B > B_fwd || !tune_plan(H, B_fwd, p)) return false;
+  if (B == B_fwd) return true;
+  TunePlan n;
+  if (!tune_plan(H, B, &n)) return false;
+  p->B = B;
+  p->M = n.M;
+  p->tf_grid = n.tf_grid;
+  p->lin_grid = n.lin_grid;
+  p->dw_grid = n.dw_grid;
+  p->dec_s = n.dec_s;
+  p->dec_dws = n.dec_dws;
+  return true;
 }
 
 hipError_t launch_tune_forward(const TunePlan& p, const float* windows, const float* P, float* ws, float* latent,

@@ -47,6 +47,8 @@ struct TunePlan {
 };
 
 bool tune_plan(int H, int B, TunePlan* p);
+// a backward over the first B windows of a forward of B_fwd (same workspace)
+bool tune_plan_prefix(int H, int B_fwd, int B, TunePlan* p);
 // live timing of the six fused encoder launches of a forward + backward
 // (pgp_tune_timing / pgp_tune_fused_ms)
 hipError_t tune_timing(bool on);

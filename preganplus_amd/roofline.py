@@ -80,18 +80,21 @@ def tune_te_mfma(H: int) -> int:
     return nt * ks * 3
 
 
-def tune_fused_flops(H: int, B: int):
+def tune_fused_flops(H: int, B: int, B_fwd: int | None = None):
     """Executed MFMA flops of each of the six fused launches of one tuning
     forward + backward (TUNE_FUSED_LAUNCHES order) over the batch's units; the
-    FFN backward's zero rounds of waves past their units are not counted."""
+    FFN backward's zero rounds of waves past their units are not counted.
+    B_fwd (default B): the forward's batch when it also carries inference
+    windows (C3's detect) that the backward does not."""
     c = TUNE_MFMA_PER_UNIT.get(H)
     if c is None:
         return None
     units = (B * H + 15) // 16
+    ufwd = ((B if B_fwd is None else B_fwd) * H + 15) // 16
     fwd, te = c["tf_fwd_kernel"], tune_te_mfma(H)
-    per = [fwd, fwd - te, c["tf_bwd_ffn_kernel"], c["tf_bwd_att_kernel"], c["tf_bwd_ffn_kernel"],
-           c["tf_bwd_att_kernel"]]
-    return [units * n * 2048 for n in per]
+    return ([ufwd * fwd * 2048, ufwd * (fwd - te) * 2048]
+            + [units * n * 2048 for n in (c["tf_bwd_ffn_kernel"], c["tf_bwd_att_kernel"], c["tf_bwd_ffn_kernel"],
+                                          c["tf_bwd_att_kernel"])])
 
 
 def encoder_io_bytes_per_window(H: int) -> int:

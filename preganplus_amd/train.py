@@ -109,6 +109,7 @@ class Trainer:
         L.pgp_gan_workspace_len.restype = sz
         L.pgp_tune_forward.argtypes = [i32, i32] + [vp] * 6 + [vp]
         L.pgp_tune_backward.argtypes = [i32, i32] + [vp] * 8 + [vp]
+        L.pgp_tune_backward_prefix.argtypes = [i32, i32, i32] + [vp] * 8 + [vp]
         L.pgp_gan_forward.argtypes = [i32, i32] + [vp] * 6 + [vp]
         L.pgp_gan_disc_backward.argtypes = [i32, i32] + [vp] * 4 + [vp]
         L.pgp_gan_gen_backward.argtypes = [i32, i32] + [vp] * 3 + [vp]
@@ -132,7 +133,7 @@ class Trainer:
         L.pgp_tune_targets_dp.argtypes = [i32, i32, i32] + [vp] * 5 + [dbl] + [vp] * 5 + [vp]
         L.pgp_tune_state_apply.argtypes = [i32, vp, vp, dbl, i32, ctypes.POINTER(ctypes.c_int), vp, vp,
                                            dbl, dbl, dbl, vp]
-        for f in ("pgp_tune_forward", "pgp_tune_backward", "pgp_gan_forward", "pgp_gan_disc_backward",
+        for f in ("pgp_tune_forward", "pgp_tune_backward", "pgp_tune_backward_prefix", "pgp_gan_forward", "pgp_gan_disc_backward",
                   "pgp_gan_gen_backward", "pgp_adamw", "pgp_load_weights_master", "pgp_tune_targets",
                   "pgp_adamw_table", "pgp_tune_dataset", "pgp_tune_targets_dp", "pgp_tune_state_apply",
                   "pgp_gan_probs", "pgp_tune_step1", "pgp_forward1", "pgp_tune_forward_many",
@@ -204,18 +205,26 @@ class Trainer:
         return lg[:B], pr[:B]
 
     def tune_backward(self, B, y, mult, tgt):
-        """y [B,H] int, mult [B,H], tgt [B,H,2] (host arrays or tensors); B must
-        be the batch of the preceding tune_forward."""
-        if B != self._fwd_batch:
-            raise ValueError(f"tune_backward batch {B} != tune_forward batch {self._fwd_batch}")
+        """y [B,H] int, mult [B,H], tgt [B,H,2] (host arrays or tensors).  B is
+        the batch of the preceding tune_forward, or fewer: then the gradient is
+        of its FIRST B windows' losses (``pgp_tune_backward_prefix``; the rest
+        were inference windows sharing the forward, e.g. C3's detect)."""
+        if not 0 < B <= self._fwd_batch:
+            raise ValueError(f"tune_backward batch {B} not in 1..{self._fwd_batch} (the tune_forward batch)")
         y = self._dev(y, torch.int32)
         mult = self._dev(mult, torch.float32)
         tgt = self._dev(tgt, torch.float32)
         self.zero_grad("transformer")
-        _native.check(self._L.pgp_tune_backward(
-            self.H, B, self.P.data_ptr(), self.G.data_ptr(), self.ws.data_ptr(),
-            self.logits.data_ptr(), self.protos.data_ptr(), y.data_ptr(), mult.data_ptr(), tgt.data_ptr(),
-            self._stream()), "pgp_tune_backward")
+        if B == self._fwd_batch:
+            _native.check(self._L.pgp_tune_backward(
+                self.H, B, self.P.data_ptr(), self.G.data_ptr(), self.ws.data_ptr(),
+                self.logits.data_ptr(), self.protos.data_ptr(), y.data_ptr(), mult.data_ptr(), tgt.data_ptr(),
+                self._stream()), "pgp_tune_backward")
+        else:
+            _native.check(self._L.pgp_tune_backward_prefix(
+                self.H, self._fwd_batch, B, self.P.data_ptr(), self.G.data_ptr(), self.ws.data_ptr(),
+                self.logits.data_ptr(), self.protos.data_ptr(), y.data_ptr(), mult.data_ptr(), tgt.data_ptr(),
+                self._stream()), "pgp_tune_backward_prefix")
 
     def tune_targets(self, y, cls, state, mult, tgt, loss):
         """custom_loss / triplet_loss bookkeeping of the preceding batch-1
@@ -568,9 +577,16 @@ def dp_state_update(st: TuneState, inc: TuneIncrements, group=None):
     return tot
 
 
-def dataset_buffers(tr: "Trainer", E: int, R: int = LATEST_WINDOW_SIZE):
-    """Preallocated outputs of tune_dataset for E environments of R rows."""
+def dataset_buffers(tr: "Trainer", E: int, R: int = LATEST_WINDOW_SIZE, joint: bool = False):
+    """Preallocated outputs of tune_dataset for E environments of R rows.
+    With ``joint`` the tuning windows and run_encoder's windows are views of
+    ONE [E*R + E, 3, 3H] buffer (returned fifth), so a single forward covers
+    both (``DPTuner.step`` trains on the first E*R)."""
     H, dev = tr.H, tr.device
+    if joint:
+        allw = torch.empty((E * R + E, 3, 3 * H), dtype=torch.float32, device=dev)
+        return (allw[:E * R], torch.empty((E * R, H), dtype=torch.int32, device=dev),
+                torch.empty((E * R, H), dtype=torch.int32, device=dev), allw[E * R:], allw)
     return (torch.empty((E * R, 3, 3 * H), dtype=torch.float32, device=dev),
             torch.empty((E * R, H), dtype=torch.int32, device=dev),
             torch.empty((E * R, H), dtype=torch.int32, device=dev),
@@ -590,7 +606,7 @@ def tune_dataset(tr: "Trainer", series, train_max, infer: bool = True, out=None)
     H = tr.H
     if F != 3 * H:
         raise ValueError(f"series must be [E,R,{3 * H}]")
-    wins, y, cls, inf = out if out is not None else dataset_buffers(tr, E, R)
+    wins, y, cls, inf = out[:4] if out is not None else dataset_buffers(tr, E, R)
     if tuple(wins.shape) != (E * R, 3, F) or tuple(y.shape) != (E * R, H) or tuple(inf.shape) != (E, 3, F):
         raise ValueError("tune_dataset: output buffers do not match the series")
     inf = inf if infer else None
@@ -651,10 +667,30 @@ class DPTuner:
 
     SUBSTAGES = ("forward", "targets", "backward", "all_reduce", "apply_adamw")
 
+    def next_row(self, out: torch.Tensor | None = None):
+        """The AdamW table row of the next step (host bookkeeping: the table is
+        refilled every CHUNK steps).  With ``out`` (a fixed [T,3] device buffer
+        that a captured step reads, ``step(row=out)``) the row is copied there
+        on the current stream: call it before each replay."""
+        i = self.n % self.CHUNK
+        if i == 0:
+            self._fill_table()
+        self.n += 1
+        row = self.table[i]
+        if out is None:
+            return row
+        out.copy_(row)
+        return out
+
     def step(self, wins: torch.Tensor, y: torch.Tensor, cls: torch.Tensor, mark=None, before_update=None,
-             after_forward=None, before_backward=None):
-        """wins [B,3,3H] fp32, y / cls [B,H] int32, all on the device.
+             after_forward=None, before_backward=None, row: torch.Tensor | None = None):
+        """wins [B',3,3H] fp32, y / cls [B,H] int32, all on the device, B <= B':
+        the forward runs over all B' windows and the step trains on the first
+        B (windows B.. are inference windows sharing the forward, e.g. C3's
+        detect: their logits / protos are ``tr.logits[B:B']`` afterwards).
         Returns the per-window (aloss, tloss) [B,2] fp64 device view.
+        ``row``: the AdamW row buffer ``next_row(out=row)`` filled for this
+        step (graph capture); by default the step takes ``next_row()`` itself.
         ``mark(k)``, if given, is called before sub-stage k of SUBSTAGES and
         once more at the end (the bench records HIP events there).
         ``before_update``, if given, is an event the step's stream waits for
@@ -670,14 +706,13 @@ class DPTuner:
         mark = mark or (lambda k: None)
         import torch.distributed as dist
         tr, L = self.tr, self.tr._L
-        B = wins.shape[0]
-        if B > self.cap:
-            raise ValueError(f"batch {B} > DPTuner capacity {self.cap}")
+        B = y.shape[0]
+        if B > self.cap or B > wins.shape[0] or cls.shape[0] != B:
+            raise ValueError(f"batch {B} (labels) vs windows {wins.shape[0]} / DPTuner capacity {self.cap}")
         if y.dtype != torch.int32 or cls.dtype != torch.int32 or y.device != tr.device or cls.device != tr.device:
             raise ValueError("y / cls must be int32 device tensors")
-        i = self.n % self.CHUNK
-        if i == 0:
-            self._fill_table()
+        if row is None:
+            row = self.next_row()
         s = tr._stream()
         mark(0)
         tr.tune_forward(wins)
@@ -700,14 +735,12 @@ class DPTuner:
         if before_update is not None:
             ev = before_update() if callable(before_update) else before_update
             torch.cuda.current_stream(tr.device).wait_event(ev)
-        row = self.table[i]
         _native.check(L.pgp_tune_state_apply(
             self.K, self.state.data_ptr(), self.inc.data_ptr(), PROTO_FACTOR_DECAY, len(self.cond), self.cond_rows,
             self.cond_steps.data_ptr(), row.data_ptr(), tr.lrs["transformer"], tr.b1, tr.b2, s),
             "pgp_tune_state_apply")
         tr.adam_step_table("transformer", self.sel, row)
         mark(5)
-        self.n += 1
         return self.loss[:B]
 
     def sync(self, st: TuneState):
@@ -1166,22 +1199,162 @@ def dp_groups():
     return None, dist.new_group(ranks=list(range(dist.get_world_size())))
 
 
-def train_gan_batched(tr: Trainer, sim, envs, emb, sched, out=None, target=None, all_reduce=False, group=None):
+class SectionRows:
+    """AdamW's per-step scalars for a section whose tensors all step on every
+    call (the GAN's Gen and Disc: both sections get a gradient each
+    train_gan), for a captured step: ``next_row(out)`` (host, before each
+    replay) writes the next step's row into the fixed buffer the graph's
+    ``adam_step_table`` reads and advances the host step counts as
+    ``adam_step`` would.  A table of CHUNK rows is filled ahead on the host and
+    uploaded once per CHUNK steps (same values as adam_step)."""
+
+    CHUNK = 64
+
+    def __init__(self, tr: Trainer, section: str):
+        self.tr, self.section = tr, section
+        self.sel = [t for t in tr.tensors if t["section"] == section and t["trainable"]]
+        self.table = torch.zeros((self.CHUNK, len(self.sel), 3), dtype=torch.float32, device=tr.device)
+        self.i = 0
+
+    def buffer(self):
+        return torch.zeros((len(self.sel), 3), dtype=torch.float32, device=self.tr.device)
+
+    def next_row(self, out: torch.Tensor):
+        if self.i % self.CHUNK == 0:
+            tab = self.tr.adam_schedule_np(self.section, np.ones(self.CHUNK, dtype=bool), ())
+            for t in self.sel:            # adam_schedule_np advanced the counts by CHUNK; one step at a time here
+                t["step"] -= self.CHUNK
+            self.table.copy_(torch.from_numpy(tab).pin_memory(), non_blocking=True)
+        out.copy_(self.table[self.i % self.CHUNK])
+        self.i += 1
+        for t in self.sel:
+            t["step"] += 1
+        return out
+
+
+def train_gan_batched(tr: Trainer, sim, envs, emb, sched, out=None, target=None, all_reduce=False, group=None,
+                      rows=None):
     """PreGANPlus.py:60-75 for a batch of environments with the label simulated
     on the device (``simulate.Simulation`` -> ``pgp_simulate``):
     Gen + Disc forward, both schedules scored, Disc BCE step on the label, Gen
     BCE step toward [0, 1] — no host round trip.  envs [B, env_len(H)] fp64
     records (``simulate.pack_env``).  With ``all_reduce`` each section's
     gradients are summed over ranks before its AdamW step (data parallel).
+    ``rows`` = (disc row, gen row): AdamW reads its per-step scalars from
+    these device buffers (``SectionRows.next_row``, graph capture) instead of
+    kernel arguments.
     Returns (out [B,4] energy/score of new and original, target [B,2])."""
     ns, _ = tr.gan_forward(emb, sched)
     out, target = sim.score(envs, ns, tr._gan_in[1], out=out, target=target)
     tr.gan_disc_backward(target)
     if all_reduce:
         tr.all_reduce_grads("disc", group)
-    tr.adam_step("disc")
+    if rows is None:
+        tr.adam_step("disc")
+    else:
+        tr.adam_step_table("disc", [t for t in tr.tensors if t["section"] == "disc" and t["trainable"]], rows[0])
     tr.gan_gen_backward(ns.shape[0])
     if all_reduce:
         tr.all_reduce_grads("gen", group)
-    tr.adam_step("gen")
+    if rows is None:
+        tr.adam_step("gen")
+    else:
+        tr.adam_step_table("gen", [t for t in tr.tensors if t["section"] == "gen" and t["trainable"]], rows[1])
     return out, target
+
+class OnlineTrainStep:
+    """run_model's semi-supervised training (PreGANPlus.py:115-136, all but the
+    decision) for E environments on this rank, data parallel,
+    as one launch-only step on the device:
+      1. tune_model's on-the-fly dataset (utils.py:40-47, ``pgp_tune_dataset``):
+         each environment's last R rows -> R tuning windows with labels and
+         classes, and run_encoder's window (PreGANPlus.py:107-112) — the latter
+         as the last E rows of the same window buffer;
+      2. ONE Transformer forward over the R*E + E windows (the tuning windows
+         and detect's read the same step-start weights), then the tuning
+         bookkeeping over the first R*E (``DPTuner``);
+      3. on the second stream ``side``: detect's masked embedding
+         (PreGANPlus.py:129) and train_gan (PreGANPlus.py:60-81, ``
+         train_gan_batched``: device-simulated label, Disc step, Gen step);
+      4. the tuning backward over the R*E windows, gradient / state all-reduce,
+         state update and AdamW (``DPTuner``).
+    The GAN and tuning steps share no data, so 3 runs beside 4.  AdamW's
+    per-step scalars are read from fixed device rows written by ``prep()``
+    before each step, so every step issues the same launches: ``capture()``
+    records the step once as a HIP graph and ``run()`` replays it (world size
+    1; collectives stay eager).  ``issue()`` is the eager step (optional
+    ``stage`` / ``sub`` HIP-event lists as bench.py records them)."""
+
+    def __init__(self, tr: "Trainer", st: "TuneState", sim, series, train_max, sched, envs, R: int = 10,
+                 side=None, groups=(None, None), out=None):
+        self.tr, self.sim = tr, sim
+        self.series, self.tmax = tr._dev(series, torch.float64), tr._dev(train_max, torch.float64)
+        E = self.series.shape[0]
+        self.E, self.R, self.B = E, R, E * R
+        H, dev = tr.H, tr.device
+        tr._ensure(self.B + E)
+        self.tun = DPTuner(tr, st, self.B, group=groups[0])
+        self.gan_group = groups[1]
+        self.sched = tr._dev(sched, torch.float32)
+        self.envs = tr._dev(envs, torch.float64)
+        self.bufs = dataset_buffers(tr, E, R, joint=True)
+        self.emb = torch.zeros((E, H, 2), dtype=torch.float32, device=dev)
+        self.sim_out = torch.zeros((E, 4), dtype=torch.float64, device=dev)
+        self.target = torch.zeros((E, 2), dtype=torch.float32, device=dev)
+        self.side = side
+        self.rowT = torch.zeros_like(self.tun.table[0])
+        self.rows_d, self.rows_g = SectionRows(tr, "disc"), SectionRows(tr, "gen")
+        self.rowD, self.rowG = self.rows_d.buffer(), self.rows_g.buffer()
+        self.graph = None
+
+    def prep(self):
+        """Host bookkeeping of the next step (AdamW rows), on the current stream."""
+        self.tun.next_row(out=self.rowT)
+        self.rows_d.next_row(self.rowD)
+        self.rows_g.next_row(self.rowG)
+
+    def issue(self, stage=None, sub=None):
+        from .model import embedding
+        tr, B, E = self.tr, self.B, self.E
+        main = torch.cuda.current_stream(tr.device)
+        side = self.side if self.side is not None else main
+        rec = (lambda k: stage[k].record(main)) if stage is not None else (lambda k: None)
+        rec(0)
+        _, y, cls, _ = tune_dataset(tr, self.series, self.tmax, out=self.bufs)
+        rec(1)
+
+        def detect_gan():   # once the targets are issued: beside the tuning backward
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                if stage is not None:
+                    stage[5].record(side)
+                embedding(tr.logits[B:B + E], tr.protos[B:B + E], out=self.emb)
+                if stage is not None:
+                    stage[2].record(side)
+                train_gan_batched(tr, self.sim, self.envs, self.emb, self.sched, out=self.sim_out,
+                                  target=self.target, all_reduce=True, group=self.gan_group,
+                                  rows=(self.rowD, self.rowG))
+                if stage is not None:
+                    stage[3].record(side)
+
+        self.tun.step(self.bufs[4], y, cls, mark=(lambda k: sub[k].record(main)) if sub is not None else None,
+                      before_backward=detect_gan, row=self.rowT)
+        main.wait_stream(side)
+        rec(4)
+
+    def capture(self):
+        """Record one step as a HIP graph on the current (non-default) stream."""
+        main = torch.cuda.current_stream(self.tr.device)
+        torch.cuda.synchronize(self.tr.device)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=main):
+            self.issue()
+        torch.cuda.synchronize(self.tr.device)
+        self.graph = g
+
+    def run(self):
+        self.prep()
+        if self.graph is not None:
+            self.graph.replay()
+        else:
+            self.issue()

@@ -1,0 +1,104 @@
+"""The C3 step's composition (train.OnlineTrainStep): detect's windows share
+the tuning forward (pgp_tune_backward_prefix differentiates only the tuning
+windows), AdamW's scalars come from device rows, and the step replays as a
+captured HIP graph with the same results as eager issue."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("H", [16, 50])
+def test_prefix_backward_equals_backward_of_the_prefix(H):
+    """Forward over B + E windows, backward over the first B == forward and
+    backward over the B windows alone (the forward's decoder split-K grouping
+    depends on the batch: fp32 rounding apart)."""
+    from preganplus_amd import train as TR
+    from preganplus_amd import weights as W
+    rng = np.random.default_rng(3)
+    B, E = 24, 7
+    w = W.synth_weights(H, seed=1)
+    wins = torch.tensor(rng.uniform(0, 1, size=(B + E, 3, 3 * H)), dtype=torch.float32, device="cuda")
+    y = torch.tensor(rng.integers(0, 2, size=(B, H)), dtype=torch.int32, device="cuda")
+    mult = torch.tensor(rng.uniform(0.5, 2, size=(B, H)), dtype=torch.float32, device="cuda")
+    tgt = torch.tensor(rng.uniform(0, 1, size=(B, H, 2)), dtype=torch.float32, device="cuda")
+    a = TR.Trainer(H, w, device="cuda", max_batch=B + E)
+    lg_a, _ = a.tune_forward(wins)
+    a.tune_backward(B, y, mult, tgt)
+    b = TR.Trainer(H, w, device="cuda", max_batch=B)
+    lg_b, _ = b.tune_forward(wins[:B].contiguous())
+    b.tune_backward(B, y, mult, tgt)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(lg_a[:B].cpu().numpy(), lg_b.cpu().numpy(), rtol=1e-5, atol=1e-6)
+    ga = a.G[a.sec_off["transformer"]:a.sec_end["transformer"]].cpu().numpy()
+    gb = b.G[b.sec_off["transformer"]:b.sec_end["transformer"]].cpu().numpy()
+    np.testing.assert_allclose(ga, gb, rtol=1e-4, atol=1e-5 * np.abs(gb).max())
+    with pytest.raises(ValueError):
+        a.tune_backward(B + E + 1, y, mult, tgt)
+
+
+def _online(H, E, seed=5):
+    from preganplus_amd import simulate as SIM
+    from preganplus_amd import train as TR
+    from preganplus_amd import weights as W
+    import bench
+    w = W.synth_weights(H, seed=0)
+    tr = TR.Trainer(H, w, device="cuda", max_batch=11 * E)
+    st = TR.TuneState(w["prototypes"])
+    series, tmax = bench.synth_series(E, H, seed, 10)
+    rng = np.random.default_rng(seed)
+    s = np.zeros((E, H, H), dtype=np.float32)
+    s[np.arange(E)[:, None], np.arange(H)[None, :], rng.integers(0, H, size=(E, H))] = 1.0
+    envs = SIM.synth_envs(E, H, seed=seed)
+    side = torch.cuda.Stream()
+    step = TR.OnlineTrainStep(tr, st, SIM.Simulation(H, device="cuda"), series, tmax, s, envs, side=side)
+    return tr, step
+
+
+@pytest.mark.parametrize("H", [16, 50])
+def test_online_step_graph_replay_equals_eager(H):
+    """Three steps issued eagerly == one eager step + two replays of the
+    captured step: every weight, AdamW moment, the tuning state and the GAN
+    label outcome are identical (same kernels, same order)."""
+    main = torch.cuda.Stream()
+    with torch.cuda.stream(main):
+        tr_a, sa = _online(H, 6)
+        for _ in range(3):
+            sa.run()
+        tr_b, sb = _online(H, 6)
+        sb.run()
+        sb.capture()
+        for _ in range(2):
+            sb.run()
+        torch.cuda.synchronize()
+    for x, y in ((tr_a.P, tr_b.P), (tr_a.m, tr_b.m), (tr_a.v, tr_b.v), (sa.tun.state, sb.tun.state),
+                 (sa.target, sb.target), (sa.sim_out, sb.sim_out)):
+        np.testing.assert_array_equal(x.cpu().numpy(), y.cpu().numpy())
+    assert sa.tun.n == sb.tun.n == 3
+    for t_a, t_b in zip(tr_a.tensors, tr_b.tensors):
+        assert t_a["step"] == t_b["step"], t_a["name"]
+    # the GAN sections stepped three times, as adam_step would have counted
+    assert {t["step"] for t in tr_a.tensors if t["section"] in ("gen", "disc") and t["trainable"]} == {3.0}
+
+
+def test_section_rows_match_adam_step():
+    """SectionRows' device rows drive AdamW to the same weights as adam_step."""
+    from preganplus_amd import train as TR
+    from preganplus_amd import weights as W
+    w = W.synth_weights(16, seed=2)
+    a = TR.Trainer(16, w, device="cuda", max_batch=1)
+    b = TR.Trainer(16, w, device="cuda", max_batch=1)
+    g = torch.randn_like(a.G)
+    rows = TR.SectionRows(b, "gen")
+    row = rows.buffer()
+    sel = [t for t in b.tensors if t["section"] == "gen" and t["trainable"]]
+    for _ in range(3):
+        a.G.copy_(g)
+        b.G.copy_(g)
+        a.adam_step("gen")
+        rows.next_row(row)
+        b.adam_step_table("gen", sel, row)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(a.P.cpu().numpy(), b.P.cpu().numpy(), rtol=1e-6, atol=1e-7)
+    assert [t["step"] for t in a.tensors] == [t["step"] for t in b.tensors]

@@ -49,6 +49,10 @@ for step in "$@"; do
       run t_train 600 python -u -m pytest tests/test_gpu_train.py tests/test_gpu_bench_modes.py tests/test_gpu_dist.py -x -v -p no:cacheprovider --timeout 300 --timeout-method thread
       tail -2 $OUT/t_train.out
       ;;
+    tc3)
+      run t_c3 600 python -u -m pytest tests/test_gpu_c3step.py tests/test_gpu_tunedp.py tests/test_gpu_dist.py tests/test_gpu_plugin_graphs.py tests/test_gpu_train.py -x -v -p no:cacheprovider --timeout 300 --timeout-method thread
+      tail -2 $OUT/t_c3.out
+      ;;
     tfpe)
       run t_fpe 600 python -u -m pytest tests/test_gpu_fpetrain.py tests/test_gpu_checkpoint.py -v -p no:cacheprovider --timeout 300 --timeout-method thread
       tail -2 $OUT/t_fpe.out
