@@ -323,7 +323,8 @@ def _dist_setup():
 _HOST_ISSUE_S = None
 
 
-GAN_RESERVED_CUS = 8   # CUs the fused tuning launches leave to the GAN step beside them (pgp_tune_reserve_cus)
+GAN_RESERVED_CUS = int(os.environ.get("PGP_GAN_RESERVED_CUS", "8"))   # CUs the fused tuning launches leave to
+# the GAN step beside them (pgp_tune_reserve_cus); the variable is for A/B runs
 
 
 def _reserve_cus(main, side):
@@ -547,10 +548,11 @@ def bench_tune(args):
     step = TR.OnlineTrainStep(tr, st, sim, series_h, tmax_h, s, envs, R=R, side=side, groups=TR.dp_groups())
     for _ in range(args.warmup):
         step.run()
-    # the timed steps: the step captured once as a HIP graph and replayed (the
-    # host issues ~70 launches per step otherwise: at 16 hosts the eager step is
-    # bound by that issue rate).  World > 1 keeps eager issue (RCCL calls).
-    graphed = world == 1 and os.environ.get("PGP_BENCH_GRAPH", "1") != "0"
+    # the timed steps: eager issue.  PGP_BENCH_GRAPH=1 replays the step
+    # captured once as a HIP graph instead (world size 1); on one box that was
+    # slower than eager issue at both H (16: 0.313 vs 0.302 ms, 50: 1.301-1.314
+    # vs 1.297 ms; profiles/r04/s5/ab_tune*_graph_eager.txt)
+    graphed = world == 1 and os.environ.get("PGP_BENCH_GRAPH", "0") == "1"
     if graphed:
         step.capture()
     el = _timed(world, device, step.run, args.steps)

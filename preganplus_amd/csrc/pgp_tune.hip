@@ -948,15 +948,20 @@ SideStream* side_stream() {
 // a caller-owned stream to use as the side stream (pgp_tune_set_side_stream),
 // per device; null: the library's own
 std::atomic<hipStream_t> g_side_override[16];
+// Below kSideMinTokens tokens (B * 3H) the side work is a few microseconds per
+// launch and the fork / join events cost more than the overlap returns (A/B on
+// one box, C3 at 1,030 windows: H = 16 (49 k tokens) 0.362 -> 0.302 ms per step
+// without the fork, H = 50 (154 k tokens) 1.297 -> 1.340 ms; profiles/r04/s5/)
+constexpr long kSideMinTokens = 65536;
 struct Fork {
   hipStream_t main, side;
   SideStream* ss = nullptr;
-  explicit Fork(hipStream_t st) : main(st), side(st) {
+  Fork(hipStream_t st, long tokens) : main(st), side(st) {
     static const bool off = [] {
       const char* v = getenv("PGP_TUNE_SIDE_STREAM");
       return v && v[0] == '0';
     }();
-    if (off) return;  // PGP_TUNE_SIDE_STREAM=0: everything on the caller's stream
+    if (off || tokens < kSideMinTokens) return;  // PGP_TUNE_SIDE_STREAM=0: everything on the caller's stream
     // while `st` is being captured into a graph the fork / join events become
     // the graph's edges: the side stream joins the capture at the fork's wait
     // and leaves it at the join, so the graph keeps the two branches (a
@@ -990,7 +995,7 @@ hipError_t tune_fwd_h(const TunePlan& p, const float* win, const float* P, float
   const int B = p.B;
   hipError_t e;
   // side: the decoder weights permuted for this step's forward and backward
-  Fork fk(st);
+  Fork fk(st, p.M);
   if ((e = fk.fork()) != hipSuccess) return e;
   TCK((dec_pack_kernel<H><<<(int)((Q::NOP * Q::KD + 255) / 256), 256, 0, fk.side>>>(P, ws + p.wp, ws + p.wpt)));
   TCK((gat_mt_kernel<H><<<1, 192, 0, fk.side>>>(P, ws + p.mt)));  // for the backward's GAT (gat_bwd_kernel)
@@ -1031,7 +1036,7 @@ hipError_t tune_bwd_h(const TunePlan& p, const float* P, float* Gd, float* ws, c
   const long M = p.M;
   hipError_t e;
   RedBatch rb{ws + p.pool, p.pool_len};
-  Fork fk(st);
+  Fork fk(st, p.M);
   const hipStream_t sd = fk.side;
   TCK((tune_loss_kernel<<<(int)(((long)B * H + 255) / 256), 256, 0, st>>>(B, H, Q::NOP, logits, protos, y, mult,
                                                                            tgt, ws + p.dpre)));
