@@ -182,10 +182,18 @@ PGP_DEV float xsum_rows(const float (&v)[NR]) {
 // workgroup's waves (group g by wave g % nwaves).  LDS destination is the
 // wave-uniform base + lane*16 (global_load_lds_dwordx4), so a group's 64
 // lane-consecutive float4 land contiguously, exactly as packed.
+// The lane's byte offset is re-derived at each use (opaque to the optimiser):
+// otherwise the compiler keeps a 64-bit per-lane pointer per call site live
+// across the kernel's loops, and in K3 (127 VGPRs at H = 50) it spilled them,
+// each reload followed by an s_waitcnt vmcnt(0) that also drained the wave's
+// prefetches.  With the offset fresh, the load takes the scalar base and a
+// 32-bit vector offset.
 PGP_DEV void dma_groups(const float* __restrict__ src, float* dst, int ngroups, int wv, int nwaves, int lane) {
   for (int g = wv; g < ngroups; g += nwaves) {
+    unsigned off = (unsigned)lane * 16u;
+    asm volatile("" : "+v"(off));
     __builtin_amdgcn_global_load_lds(
-        (const __attribute__((address_space(1))) void*)(src + (long)g * 256 + lane * 4),
+        (const __attribute__((address_space(1))) void*)(reinterpret_cast<const char*>(src + (long)g * 256) + off),
         (__attribute__((address_space(3))) void*)(dst + g * 256), 16, 0, 0);
   }
 }

@@ -88,6 +88,22 @@ for step in "$@"; do
       run graphc 120 python3 -u tools/graph_concurrency.py
       cat $OUT/graphc.out
       ;;
+    abtune)
+      run ab16 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 16 --steps 100 --warmup 10 --no-cpu-baseline" base= side0=PGP_TUNE_SIDE_STREAM=0 eager=PGP_BENCH_GRAPH=0 res16=PGP_GAN_RESERVED_CUS=16
+      grep median $OUT/ab16.out
+      run ab50 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" base= side0=PGP_TUNE_SIDE_STREAM=0 eager=PGP_BENCH_GRAPH=0 res16=PGP_GAN_RESERVED_CUS=16 res4=PGP_GAN_RESERVED_CUS=4
+      grep median $OUT/ab50.out
+      ;;
+    abtune2)
+      run ab16b 600 python3 -u tools/ab_bench.py --rounds 4 --args "--config tune --hosts 16 --steps 100 --warmup 10 --no-cpu-baseline" graph= graph_side0=PGP_TUNE_SIDE_STREAM=0 eager=PGP_BENCH_GRAPH=0 eager_side0=PGP_BENCH_GRAPH=0,PGP_TUNE_SIDE_STREAM=0
+      grep median $OUT/ab16b.out
+      run ab50b 600 python3 -u tools/ab_bench.py --rounds 4 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" graph= graph_side0=PGP_TUNE_SIDE_STREAM=0 eager=PGP_BENCH_GRAPH=0 eager_side0=PGP_BENCH_GRAPH=0,PGP_TUNE_SIDE_STREAM=0
+      grep median $OUT/ab50b.out
+      ;;
+    abdma)
+      run abc2 600 python3 -u tools/ab_bench.py --rounds 3 --args "--steps 100 --warmup 10 --no-cpu-baseline" new= old=PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_olddma.so
+      grep median $OUT/abc2.out
+      ;;
     others)
       run fpe 300 python3 -u bench.py --config fpe --steps 100 --warmup 5
       run plugin 300 python3 -u bench.py --config plugin --steps 50 --warmup 5
