@@ -113,12 +113,12 @@ constexpr int lds_stride(int n) { return n + ((16 - n % 64) % 64 + 64) % 64; }
 static __device__ __attribute__((aligned(16))) float dw_zero4[4];  // zero, read by masked-off lanes
 constexpr int kDwRows = 32;  // rows per LDS-staged chunk of the weight-gradient contractions
 
-template <int NP, int KP, int NTW>
+template <int NP, int KP, int NTW, int ROWS = kDwRows>
 PGP_DEV void dw_accumulate(long r0, long r1, const float* __restrict__ Y, long ldy, const float* __restrict__ X,
                            long ldx, int relu_x, int tbase, int tstride, float* ys, float* xs,
                            f32x4 (&acc)[NTW][KP / 16], float (&pb)[NTW], int ny = NP, int nx = KP) {
   constexpr int NT = NP / 16, KT = KP / 16, YS = lds_stride(NP), XS = lds_stride(KP);
-  constexpr int NY = (kDwRows * NP / 4 + 255) / 256, NX = (kDwRows * KP / 4 + 255) / 256;  // float4 per thread
+  constexpr int NY = (ROWS * NP / 4 + 255) / 256, NX = (ROWS * KP / 4 + 255) / 256;  // float4 per thread
   const int lane = threadIdx.x & 63, g = lane >> 4, i = lane & 15;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   int tq[NTW];  // this wave's n-tiles (clamped; see below)
@@ -134,22 +134,22 @@ PGP_DEV void dw_accumulate(long r0, long r1, const float* __restrict__ Y, long l
     for (int k = 0; k < NY; ++k) {
       const int idx = threadIdx.x + 256 * k, row = idx / (NP / 4), c4 = idx - row * (NP / 4);
       const long m = c0 + row;
-      ry[k] = ld4((idx < kDwRows * NP / 4 && m < r1 && 4 * c4 < ny) ? Y + m * ldy + 4 * c4 : dw_zero4);
+      ry[k] = ld4((idx < ROWS * NP / 4 && m < r1 && 4 * c4 < ny) ? Y + m * ldy + 4 * c4 : dw_zero4);
     }
 #pragma unroll
     for (int k = 0; k < NX; ++k) {
       const int idx = threadIdx.x + 256 * k, row = idx / (KP / 4), c4 = idx - row * (KP / 4);
       const long m = c0 + row;
-      rx[k] = ld4((idx < kDwRows * KP / 4 && m < r1 && 4 * c4 < nx) ? X + m * ldx + 4 * c4 : dw_zero4);
+      rx[k] = ld4((idx < ROWS * KP / 4 && m < r1 && 4 * c4 < nx) ? X + m * ldx + 4 * c4 : dw_zero4);
     }
   };
   if (r0 < r1) fetch(r0);
-  for (long c0 = r0; c0 < r1; c0 += kDwRows) {
+  for (long c0 = r0; c0 < r1; c0 += ROWS) {
     __syncthreads();  // the previous chunk has been consumed
 #pragma unroll
     for (int k = 0; k < NY; ++k) {
       const int idx = threadIdx.x + 256 * k, row = idx / (NP / 4), c4 = idx - row * (NP / 4);
-      if (idx < kDwRows * NP / 4) st4(ys + row * YS + 4 * c4, ry[k]);
+      if (idx < ROWS * NP / 4) st4(ys + row * YS + 4 * c4, ry[k]);
     }
 #pragma unroll
     for (int k = 0; k < NX; ++k) {
@@ -159,15 +159,15 @@ PGP_DEV void dw_accumulate(long r0, long r1, const float* __restrict__ Y, long l
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
       }
-      if (idx < kDwRows * KP / 4) st4(xs + row * XS + 4 * c4, v);
+      if (idx < ROWS * KP / 4) st4(xs + row * XS + 4 * c4, v);
     }
     __syncthreads();
-    if (c0 + kDwRows < r1) fetch(c0 + kDwRows);
+    if (c0 + ROWS < r1) fetch(c0 + ROWS);
     // the chunk's 8 row groups, fully unrolled and branch-free: a wave whose
     // tile q is past NT computes tile NT - 1 again and never stores it, so the
     // compiler can issue the next group's LDS reads under this group's MFMAs
 #pragma unroll
-    for (int s = 0; s < kDwRows / 4; ++s) {
+    for (int s = 0; s < ROWS / 4; ++s) {
       const int row = 4 * s + g;
       float bv[KT];
 #pragma unroll

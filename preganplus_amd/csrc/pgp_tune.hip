@@ -159,11 +159,15 @@ struct DwArgs {
   float* part;
 };
 
+// rows per staged chunk: 64-row chunks (one barrier pair per 64 rows, twice
+// the registers in flight) were slower for every shape (A/B at H = 50: C3
+// 1.287 -> 1.307-1.312 ms, in_proj dW 53 -> 85 us; profiles/r04/dw_rows/)
+constexpr int dw_rows(int) { return kDwRows; }
 template <int NP, int KP>
 __global__ __launch_bounds__(256) void dw_kernel(DwArgs a) {
-  constexpr int NT = NP / 16, KT = KP / 16, NTW = (NT + 3) / 4;
-  __shared__ __attribute__((aligned(16))) float ys[kDwRows * lds_stride(NP)];
-  __shared__ __attribute__((aligned(16))) float xs[kDwRows * lds_stride(KP)];
+  constexpr int NT = NP / 16, KT = KP / 16, NTW = (NT + 3) / 4, ROWS = dw_rows(NP);
+  __shared__ __attribute__((aligned(16))) float ys[ROWS * lds_stride(NP)];
+  __shared__ __attribute__((aligned(16))) float xs[ROWS * lds_stride(KP)];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, g = lane >> 4, i = lane & 15;
   f32x4 acc[NTW][KT];
   float pb[NTW];
@@ -173,10 +177,10 @@ __global__ __launch_bounds__(256) void dw_kernel(DwArgs a) {
 #pragma unroll
     for (int u = 0; u < KT; ++u) acc[q][u] = zero4();
   }
-  const long nch = (a.M + kDwRows - 1) / kDwRows;
-  const long r0 = nch * blockIdx.x / gridDim.x * kDwRows;
-  const long r1 = std::min<long>(a.M, nch * (blockIdx.x + 1) / gridDim.x * kDwRows);
-  dw_accumulate<NP, KP, NTW>(r0, r1, a.Y, a.ldy, a.X, a.ldx, a.relu_x, 0, 4, ys, xs, acc, pb);
+  const long nch = (a.M + ROWS - 1) / ROWS;
+  const long r0 = nch * blockIdx.x / gridDim.x * ROWS;
+  const long r1 = std::min<long>(a.M, nch * (blockIdx.x + 1) / gridDim.x * ROWS);
+  dw_accumulate<NP, KP, NTW, ROWS>(r0, r1, a.Y, a.ldy, a.X, a.ldx, a.relu_x, 0, 4, ys, xs, acc, pb);
   float* P = a.part + (long)blockIdx.x * (NP * KP + NP);
 #pragma unroll
   for (int q = 0; q < NTW; ++q) {
@@ -280,18 +284,25 @@ template <int H>
 struct GatFold {
   float u[3], v[3];  // u = fc^T a_src, v = fc^T a_dst
 };
+// Each wave forms the fold itself: lane c loads row c of fc and both attn_fc
+// weights (one round of loads for the whole wave) and the six sums are wave
+// butterflies.  (A serial loop over c issued 50 dependent rounds of loads per
+// wave: most of gat_fwd's and gat_bwd's time at H = 50.)  The same function in
+// the forward and the backward, so both see the same u, v.
 template <int H>
 PGP_DEV GatFold<H> gat_fold(const float* P) {
   using G = TGeo<H>;
+  static_assert(H <= 64, "one host per lane");
+  const int c = threadIdx.x & 63;
+  const bool ok = c < H;
+  const float a_s = ok ? P[G::W_ATT + c] : 0.f, a_d = ok ? P[G::W_ATT + H + c] : 0.f;
   GatFold<H> f;
 #pragma unroll
-  for (int k = 0; k < 3; ++k) f.u[k] = f.v[k] = 0.f;
-  for (int c = 0; c < H; ++c)
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      f.u[k] = fmaf(P[G::W_ATT + c], P[G::W_FC + c * 3 + k], f.u[k]);
-      f.v[k] = fmaf(P[G::W_ATT + H + c], P[G::W_FC + c * 3 + k], f.v[k]);
-    }
+  for (int k = 0; k < 3; ++k) {
+    const float fc = ok ? P[G::W_FC + c * 3 + k] : 0.f;
+    f.u[k] = wave_sum(a_s * fc);
+    f.v[k] = wave_sum(a_d * fc);
+  }
   return f;
 }
 
@@ -328,6 +339,7 @@ __global__ __launch_bounds__(256) void gat_fwd_kernel(int B, const float* __rest
   __syncthreads();
   float sum = 0.f, xb[3] = {0.f, 0.f, 0.f};
   if (okj)
+#pragma unroll 10
     for (int i = 0; i < H; ++i) {
       const float p = expf(lrelu(ss[wv][i] + t) - mx);  // graph-wise softmax_edges (dlutils.py:335)
       sum += p;
@@ -420,6 +432,9 @@ __global__ __launch_bounds__(256) void gat_bwd_kernel(int B, const float* __rest
 #pragma unroll
       for (int k = 0; k < 3; ++k) mt[e][k] = 4 * q + e < Q::DP ? smt[4 * q + e][k] : 0.f;
     const float* g0 = dX0 + (b * Q::T + (long)w * H) * Q::DP + 4 * q;
+    // unrolled: the ceil(H/4) row loads are all in flight before the first sum
+    // (a rolled loop waited for each load in turn)
+#pragma unroll
     for (int r0 = 0; r0 < H; r0 += 4) {  // uniform trip count: the row sums are cross-lane
       const int r = r0 + rr;
       const bool okr = okw && r < H && 4 * q < Q::DP;
@@ -443,6 +458,7 @@ __global__ __launch_bounds__(256) void gat_bwd_kernel(int B, const float* __rest
   // in the same pass as sum a da lrelu' - dot * sum a lrelu'
   float part = 0.f, s1 = 0.f, s2 = 0.f;
   if (okj)
+#pragma unroll 10
     for (int i = 0; i < H; ++i) {
       const float pre = ss[wv][i] + t;
       const float a = expf(lrelu(pre) - mx) * iz;
@@ -456,6 +472,7 @@ __global__ __launch_bounds__(256) void gat_bwd_kernel(int B, const float* __rest
   float dt = 0.f, ds = 0.f;
   if (okj) {
     dt = fmaf(-dot, s2, s1);
+#pragma unroll 10
     for (int jj = 0; jj < H; ++jj) {  // this lane as source
       const float pre = s + st[wv][jj];
       const float a = expf(lrelu(pre) - mx) * iz;

@@ -1219,16 +1219,20 @@ class SectionRows:
     def buffer(self):
         return torch.zeros((len(self.sel), 3), dtype=torch.float32, device=self.tr.device)
 
-    def next_row(self, out: torch.Tensor):
+    def next_row(self, out: torch.Tensor | None = None):
+        """The next step's row: a view of the table, or copied into ``out``."""
         if self.i % self.CHUNK == 0:
             tab = self.tr.adam_schedule_np(self.section, np.ones(self.CHUNK, dtype=bool), ())
             for t in self.sel:            # adam_schedule_np advanced the counts by CHUNK; one step at a time here
                 t["step"] -= self.CHUNK
             self.table.copy_(torch.from_numpy(tab).pin_memory(), non_blocking=True)
-        out.copy_(self.table[self.i % self.CHUNK])
+        row = self.table[self.i % self.CHUNK]
         self.i += 1
         for t in self.sel:
             t["step"] += 1
+        if out is None:
+            return row
+        out.copy_(row)
         return out
 
 
@@ -1305,13 +1309,18 @@ class OnlineTrainStep:
         self.rowT = torch.zeros_like(self.tun.table[0])
         self.rows_d, self.rows_g = SectionRows(tr, "disc"), SectionRows(tr, "gen")
         self.rowD, self.rowG = self.rows_d.buffer(), self.rows_g.buffer()
+        self._rows = (self.rowT, self.rowD, self.rowG)
         self.graph = None
 
     def prep(self):
-        """Host bookkeeping of the next step (AdamW rows), on the current stream."""
-        self.tun.next_row(out=self.rowT)
-        self.rows_d.next_row(self.rowD)
-        self.rows_g.next_row(self.rowG)
+        """Host bookkeeping of the next step (AdamW rows).  Eager steps read
+        the rows straight from the tables; a captured step reads the fixed
+        buffers, so the rows are copied there (on the current stream)."""
+        if self.graph is None:
+            self._rows = (self.tun.next_row(), self.rows_d.next_row(), self.rows_g.next_row())
+        else:
+            self._rows = (self.tun.next_row(out=self.rowT), self.rows_d.next_row(self.rowD),
+                          self.rows_g.next_row(self.rowG))
 
     def issue(self, stage=None, sub=None):
         from .model import embedding
@@ -1333,12 +1342,12 @@ class OnlineTrainStep:
                     stage[2].record(side)
                 train_gan_batched(tr, self.sim, self.envs, self.emb, self.sched, out=self.sim_out,
                                   target=self.target, all_reduce=True, group=self.gan_group,
-                                  rows=(self.rowD, self.rowG))
+                                  rows=self._rows[1:])
                 if stage is not None:
                     stage[3].record(side)
 
         self.tun.step(self.bufs[4], y, cls, mark=(lambda k: sub[k].record(main)) if sub is not None else None,
-                      before_backward=detect_gan, row=self.rowT)
+                      before_backward=detect_gan, row=self._rows[0])
         main.wait_stream(side)
         rec(4)
 
@@ -1347,6 +1356,7 @@ class OnlineTrainStep:
         main = torch.cuda.current_stream(self.tr.device)
         torch.cuda.synchronize(self.tr.device)
         g = torch.cuda.CUDAGraph()
+        self._rows = (self.rowT, self.rowD, self.rowG)
         with torch.cuda.graph(g, stream=main):
             self.issue()
         torch.cuda.synchronize(self.tr.device)

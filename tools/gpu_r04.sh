@@ -104,6 +104,12 @@ for step in "$@"; do
       run abc2 600 python3 -u tools/ab_bench.py --rounds 3 --args "--steps 100 --warmup 10 --no-cpu-baseline" new= old=PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_olddma.so
       grep median $OUT/abc2.out
       ;;
+    abdw)
+      run abdw 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" base= dw64=PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_dw64.so dw64a=PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_dw64a.so
+      grep median $OUT/abdw.out
+      run prof_dw 240 rocprofv3 --kernel-trace --stats -d $OUT/prof_dw -o tune --output-format csv -- python3 bench.py --config tune --hosts 50 --steps 30 --warmup 5 --no-cpu-baseline
+      PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_dw64a.so run prof_dw64a 240 rocprofv3 --kernel-trace --stats -d $OUT/prof_dw64a -o tune --output-format csv -- python3 bench.py --config tune --hosts 50 --steps 30 --warmup 5 --no-cpu-baseline
+      ;;
     others)
       run fpe 300 python3 -u bench.py --config fpe --steps 100 --warmup 5
       run plugin 300 python3 -u bench.py --config plugin --steps 50 --warmup 5
