@@ -789,50 +789,39 @@ struct BffL {
                        W_F1T = W_F2T + F::G_F2T * 256, PAR = W_F1T + F::G_F1T * 256,
                        SCR = PAR + TfPar<H>::SIZE,
                        SCR_A = Scr<4>::SIZE, SCR_B = Scr<4>::SIZE,  // both operands <= 64 rows
-                       ACC = SCR + kTfWaves * (SCR_A + SCR_B),     // dW2 | dW1 accumulator tiles
-                       NTILE = 2 * F::NT * 4,                     // [NT][4] + [4][NT] tiles of 256 floats
-                       TOTAL = ACC + NTILE * 256;
+                       TOTAL = SCR + kTfWaves * (SCR_A + SCR_B),
+                       NTW = F::NT * 4;                           // dW2 [NT][4] (and dW1 [4][NT]) tiles of 256 floats
   static constexpr int S_W2 = 0, S_B2 = S_W2 + H * 64, S_W1 = S_B2 + H, S_B1 = S_W1 + 64 * H,
                        S_G1 = S_B1 + 64, S_BT1 = S_G1 + H, S_G2 = S_BT1 + H, S_BT2 = S_G2 + H,
                        SLAB = S_BT2 + H;
   static constexpr int NV = 5 * H + 64;  // per-wave vector partials in the epilogue
 };
 
-// Add a unit's dW tiles (registers) into the workgroup's LDS accumulators
-// (tile-major, per-lane f32x4) in kTfWaves rounds separated by barriers: in
-// round k wave w adds the tiles of set (w + k) % kTfWaves, so every tile
-// receives the waves' contributions in one fixed order (deterministic) and the
-// waves never write the same tile at once.
+// The waves' register tiles d[T][U] summed in wave order into dst (row
+// 16T+4g+r, column 16U+j per lane; rows < rows, cols < cols, pitch ld): each
+// wave stores its tiles to a region of its own, then wave k sums tiles k, k + W, ...
+// over the regions and writes them.  Ends with a barrier (the LDS is reusable).
 template <int NA, int NB>
-PGP_DEV void lds_acc_add(float* acc, const f32x4 (&d)[NA][NB], int wv, int lane) {
-#pragma unroll
-  for (int k = 0; k < kTfWaves; ++k) {
-    const int set = (wv + k) % kTfWaves;
-#pragma unroll
-    for (int T = 0; T < NA; ++T)
-#pragma unroll
-      for (int U = 0; U < NB; ++U)
-        if ((T * NB + U) % kTfWaves == set) {
-          float* pa = acc + ((T * NB + U) * 64 + lane) * 4;
-          st4(pa, ld4(pa) + d[T][U]);
-        }
-    __syncthreads();
-  }
-}
-// LDS accumulator tile (row 16T+4g+r, column 16U+j per lane) -> dst (global)
-template <int NA, int NB>
-PGP_DEV void put_dw_lds(float* dst, const float* acc, int rows, int cols, int ld, int g, int j, int lane) {
+PGP_DEV void sum_tiles(float* dst, const f32x4 (&d)[NA][NB], float* lds, int rows, int cols, int ld, int wv, int g,
+                       int j, int lane) {
+  constexpr int NTL = NA * NB;
 #pragma unroll
   for (int T = 0; T < NA; ++T)
 #pragma unroll
-    for (int U = 0; U < NB; ++U) {
-      const f32x4 v = ld4(acc + ((T * NB + U) * 64 + lane) * 4);
+    for (int U = 0; U < NB; ++U) st4(lds + ((wv * NTL + T * NB + U) * 64 + lane) * 4, d[T][U]);
+  __syncthreads();
+  for (int k = wv; k < NTL; k += kTfWaves) {
+    f32x4 v = ld4(lds + (k * 64 + lane) * 4);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int n = 16 * T + 4 * g + r, c = 16 * U + j;
-        if (n < rows && c < cols) dst[n * ld + c] = v[r];
-      }
+    for (int w = 1; w < kTfWaves; ++w) v += ld4(lds + ((w * NTL + k) * 64 + lane) * 4);
+    const int T = k / NB, U = k - T * NB;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int n = 16 * T + 4 * g + r, c = 16 * U + j;
+      if (n < rows && c < cols) dst[n * ld + c] = v[r];
     }
+  }
+  __syncthreads();
 }
 
 template <int H>
@@ -842,48 +831,38 @@ __global__ __launch_bounds__(kTfWaves * 64, 1) void tf_bwd_ffn_kernel(TfArgs a) 
   using Q = TfPar<H>;
   constexpr int NT = F::NT;
   static_assert(kTfWaves * L::NV <= L::SCR, "epilogue partials fit the LDS they reuse");
+  static_assert(kTfWaves * L::NTW * 256 <= L::TOTAL, "epilogue dW regions fit the LDS they reuse");
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, g = lane >> 4, j = lane & 15;
   const int layer = a.layer;
   dma_groups(a.frags + F::layer_off(layer) + F::OFF_F1, sm + L::W_F1, F::G_F1 + F::G_F2 + F::G_F2T + F::G_F1T, wv,
              kTfWaves, lane);
   load_params<H>(sm + L::PAR, a.P, layer);
-  for (int k = threadIdx.x; k < L::NTILE * 256; k += blockDim.x) sm[L::ACC + k] = 0.f;
   TF_ST_INIT();
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   TF_ST(0);
   float* sa = sm + L::SCR + wv * (L::SCR_A + L::SCR_B);
   float* sb = sa + L::SCR_A;
-  float* accW2 = sm + L::ACC;
-  float* accW1 = accW2 + NT * 4 * 256;
+  // dW2 / dW1 accumulate in registers over all of the wave's units (no
+  // per-unit LDS accumulation: the waves run their units without barriers);
+  // the waves' sums are combined in wave order at the end
+  f32x4 dW2[NT][4], dW1[4][NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int U = 0; U < 4; ++U) dW2[t][U] = dW1[U][t] = zero4();
   float b2s[NT], b1s[4];
   float ag1 = 0.f, ab1 = 0.f, ag2 = 0.f, ab2 = 0.f;  // LayerNorm gamma / beta sums (compressed rows)
 #pragma unroll
   for (int t = 0; t < NT; ++t) b2s[t] = 0.f;
 #pragma unroll
   for (int U = 0; U < 4; ++U) b1s[U] = 0.f;
-  // every wave runs the same number of rounds (the LDS accumulation joins
-  // barriers); a wave past its units computes on zeros, which adds exactly 0
   const long npairs = (long)a.B * H, nu = (npairs + 15) / 16, spare = 3 * npairs;
   long u0, u1;
   unit_range(nu, u0, u1);
-  const long nwav = (long)gridDim.x * kTfWaves, rounds = (nu + nwav - 1) / nwav;
-  // LN1's x-hat and rstd of the unit are loaded one unit ahead (see tf_fwd_kernel)
-  f32x4 Yn[NT][3];
-  float rsn[3];
-  {
-    long rn[3];
-    const bool okn = unit_rows<H>(u0, u1, npairs, j, rn);
-    load_tiles<NT>(Yn, a.xh1, F::DP, rn, okn, g);
-#pragma unroll
-    for (int w = 0; w < 3; ++w) {
-      const float r = a.rs1[rn[w]];
-      rsn[w] = okn ? r : 0.f;
-    }
-  }
 #pragma unroll 1
-  for (long it = 0; it < rounds; ++it) {
+  for (long u = u0; u < u1; ++u) {
     // loop-variant view of the LDS base: keeps LICM from hoisting the
     // loop-invariant parameter / weight reads out of the unit loop (hundreds of
     // registers held across it)
@@ -891,7 +870,6 @@ __global__ __launch_bounds__(kTfWaves * 64, 1) void tf_bwd_ffn_kernel(TfArgs a) 
     asm volatile("" : "+s"(z));
     float* smz = sm + z;
     const float* par = smz + L::PAR;
-    const long u = u0 + it;
     // y1 = gamma1 x-hat1 + beta1, tile t of step w
     auto y1 = [&](const f32x4 (&xh)[NT][3], int t, int w) {
       return xh[t][w] * ld4(par + Q::N1W + 16 * t + 4 * g) + ld4(par + Q::N1B + 16 * t + 4 * g);
@@ -900,16 +878,18 @@ __global__ __launch_bounds__(kTfWaves * 64, 1) void tf_bwd_ffn_kernel(TfArgs a) 
     const bool ok = unit_rows<H>(u, u1, npairs, j, row);
     f32x4 dY[NT][3], Fh[4][3];
     float rs1[3], rs2[3];
-#pragma unroll
-    for (int w = 0; w < 3; ++w) rs1[w] = rsn[w];
     {  // recompute the FFN (pre-activation F) and norm2's x-hat
       f32x4 X2[NT][3];
       {
+        // LN1's x-hat and rstd of the unit (not prefetched a unit ahead: with
+        // the dW accumulators in registers that prefetch spilled)
         f32x4 Y1[NT][3];
+        load_tiles<NT>(Y1, a.xh1, F::DP, row, ok, g);
 #pragma unroll
-        for (int t = 0; t < NT; ++t)
-#pragma unroll
-          for (int w = 0; w < 3; ++w) Y1[t][w] = Yn[t][w];
+        for (int w = 0; w < 3; ++w) {
+          const float r = a.rs1[row[w]];
+          rs1[w] = ok ? r : 0.f;
+        }
         TF_ST(1);
 #pragma unroll
         for (int t = 0; t < NT; ++t)
@@ -947,19 +927,13 @@ __global__ __launch_bounds__(kTfWaves * 64, 1) void tf_bwd_ffn_kernel(TfArgs a) 
     TF_ST(4);
     __builtin_amdgcn_sched_barrier(0);
     {  // dW2 += dR2 (x) relu(F), db2 += sum dR2
-      f32x4 dW[NT][4];
-#pragma unroll
-      for (int t = 0; t < NT; ++t)
-#pragma unroll
-        for (int U = 0; U < 4; ++U) dW[t][U] = zero4();
 #pragma unroll
       for (int w = 0; w < 3; ++w) {
         stage<NT>(dY, w, sa, g, j);
         stage<4>(Fh, w, sb, g, j);
-        dw_step<NT, 4>(dW, b2s, sa, sb, g, j);
+        dw_step<NT, 4>(dW2, b2s, sa, sb, g, j);
       }
       TF_ST(5);
-      lds_acc_add<NT, 4>(accW2, dW, wv, lane);
       TF_ST(6);
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -989,41 +963,18 @@ __global__ __launch_bounds__(kTfWaves * 64, 1) void tf_bwd_ffn_kernel(TfArgs a) 
       __builtin_amdgcn_sched_barrier(0);
       TF_ST(7);
       {  // dW1 += dF (x) y1, db1 += sum dF
-        f32x4 dW[4][NT];
-#pragma unroll
-        for (int U = 0; U < 4; ++U)
-#pragma unroll
-          for (int t = 0; t < NT; ++t) dW[U][t] = zero4();
 #pragma unroll
         for (int w = 0; w < 3; ++w) {
           stage<4>(dF, w, sa, g, j);
           stage_fn<NT>([&](int t) { return y1(XH1, t, w); }, sb, g, j);
-          dw_step<4, NT>(dW, b1s, sa, sb, g, j);
+          dw_step<4, NT>(dW1, b1s, sa, sb, g, j);
         }
         TF_ST(8);
-        lds_acc_add<4, NT>(accW1, dW, wv, lane);
         TF_ST(9);
       }
       __builtin_amdgcn_sched_barrier(0);
       // dy1 = W1^T dF + dR2 (residual)
-      {  // side work: the next unit's norm1 x-hat and rstd
-        long rn[3];
-        const bool okn = unit_rows<H>(u + 1, u1, npairs, j, rn);
-        constexpr int NS = 3 * NT + 3, NG = NT * F::KGF, PER = (NS + NG - 1) / NG;
-        tf_gemm_side<NT, 16>(dY, smz + L::W_F1T, [&](int s, int w) { return dF[s >> 2][w][s & 3]; }, lane,
-                             [&](int i) {
-#pragma unroll
-                               for (int k = 0; k < PER; ++k) {
-                                 const int c = i * PER + k;
-                                 if (c < 3 * NT) {
-                                   load_tile<NT>(Yn, a.xh1, F::DP, rn, okn, g, c);
-                                 } else if (c < NS) {
-                                   const float r = a.rs1[rn[c - 3 * NT]];
-                                   rsn[c - 3 * NT] = okn ? r : 0.f;
-                                 }
-                               }
-                             });
-      }
+      tf_gemm<NT, 16>(dY, smz + L::W_F1T, [&](int s, int w) { return dF[s >> 2][w][s & 3]; }, lane);
     }
     __builtin_amdgcn_sched_barrier(0);
     TF_ST(10);
@@ -1032,14 +983,12 @@ __global__ __launch_bounds__(kTfWaves * 64, 1) void tf_bwd_ffn_kernel(TfArgs a) 
     TF_ST(11);
   }
   TF_ST(12);
-  // one slab per workgroup: the LDS dW tiles (already summed over the waves in
-  // a fixed order), then the waves' vector partials summed in wave order
+  // one slab per workgroup: the waves' dW tiles summed in wave order (two
+  // passes through the LDS the weights held), then their vector partials
   float* slab = a.part + (long)blockIdx.x * L::SLAB;
-  if (wv == 0) {
-    put_dw_lds<NT, 4>(slab + L::S_W2, accW2, H, 64, 64, g, j, lane);
-    put_dw_lds<4, NT>(slab + L::S_W1, accW1, 64, H, H, g, j, lane);
-  }
   __syncthreads();   // every wave is past its units: the weight area is free
+  sum_tiles<NT, 4>(slab + L::S_W2, dW2, sm, H, 64, 64, wv, g, j, lane);
+  sum_tiles<4, NT>(slab + L::S_W1, dW1, sm, 64, H, H, wv, g, j, lane);
   float* vr = sm + wv * L::NV;  // this wave's vector partials: b2 | b1 | g1 | bt1 | g2 | bt2
   put_bias<NT>(vr, b2s, H, g, j);
   put_bias<4>(vr + H, b1s, 64, g, j);
