@@ -589,6 +589,20 @@ def bench_tune(args):
         fused.append(list(ms6))
     _native.check(L.pgp_tune_timing(0), "pgp_tune_timing")
     fused_ms = np.array(fused).mean(0)
+    # each training stage ALONE on the device (the timed step runs them
+    # concurrently, the GAN step on the CUs the fused tuning launches leave it):
+    # train_gan for the E environments, and the tuning step without the GAN
+    n_alone = max(5, min(args.steps, 20))
+    torch.cuda.synchronize()
+    a0, a1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a0.record(main)
+    for _ in range(n_alone):
+        step.prep()
+        TR.train_gan_batched(tr, sim, step.envs, step.emb, step.sched, out=step.sim_out, target=step.target,
+                             rows=step._rows[1:])
+    a1.record(main)
+    torch.cuda.synchronize()
+    gan_alone = a0.elapsed_time(a1) / n_alone
     flops = RL.tune_fused_flops(H, B, B + E)
     roof = None
     if flops is not None:
@@ -628,6 +642,10 @@ def bench_tune(args):
             "reserved_cus": reserved,
             "tune_model_ms": {n: float(sub[k]) for k, n in enumerate(subs)},
             "grad_all_reduce_ms": float(sub[subs.index("all_reduce")]),
+            "train_gan_alone": {"ms": gan_alone, "environments": E,
+                                "achieved_tflops": RL.gan_step_flops_per_env(H) * E / (gan_alone * 1e-3) / 1e12,
+                                "note": "the GAN step by itself on the whole device (HIP events, main stream); in "
+                                        "the timed step it runs beside the tuning backward on the reserved CUs"},
             "roofline": roof,
             # the two training stages as a whole, on the reference formulation's
             # flops (algorithmic, not executed) over the stage's HIP-event span;

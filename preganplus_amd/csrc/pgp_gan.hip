@@ -36,6 +36,10 @@ constexpr int kQC = 8;
 constexpr int kChunkG = 65;
 constexpr int kTailMax = 2;
 constexpr int kGanSleep = 24;
+#ifndef PGP_GAN_PINGPONG
+#define PGP_GAN_PINGPONG 0
+#endif
+constexpr bool kGanPingPong = PGP_GAN_PINGPONG;
 template <int P>
 __device__ __forceinline__ void gan_prio() {
   __builtin_amdgcn_s_setprio(P);
@@ -225,8 +229,8 @@ __global__ __launch_bounds__(kGanWaves * 64) void gan_kernel(FwdArgs a) {
   load_row(0, sv);
   // Gen2 of container c from its chunk groups cw: ns = b2[c] + W2[c] . hg (the
   // VALU tail rows into racc)
-  auto gen2 = [&](int c, const float* cw, f32x4 (&ns)[G::MT_N], float (&racc)[kTailMax]) {
-    const float* bias = cur + GG::CPC * G::GC_G * G::FQ + (c % GG::CPC) * GG::BIAS_F;
+  auto gen2 = [&](int c, const float* cw, const float* chunk, f32x4 (&ns)[G::MT_N], float (&racc)[kTailMax]) {
+    const float* bias = chunk + GG::CPC * G::GC_G * G::FQ + (c % GG::CPC) * GG::BIAS_F;
 #pragma unroll
     for (int t = 0; t < G::MT_N; ++t) ns[t] = ld4(bias + 16 * t + 4 * g);
 #pragma unroll
@@ -259,14 +263,19 @@ __global__ __launch_bounds__(kGanWaves * 64) void gan_kernel(FwdArgs a) {
   };
   // the rest of container c: tanh / new schedule / both first-argmaxes against
   // the schedule row sv, Disc1's new-schedule half, the targets
-  auto finish = [&](int c, const float* cw, f32x4 (&ns)[G::MT_N], float (&racc)[kTailMax],
-                    const float (&sv)[G::MT_N][4]) {
+  // the rest of container c in three parts: v1 (tanh / new schedule / the
+  // lane-local first-argmaxes against the schedule row sv), m2 (Disc1's
+  // new-schedule half), v2 (the cross-lane argmaxes and the targets)
+  struct Arg {
+    float bn_v, bs_v;
+    int bn_i, bs_i;
+  };
+  auto finish_v1 = [&](f32x4 (&ns)[G::MT_N], float (&racc)[kTailMax], const float (&sv)[G::MT_N][4]) {
     if (TAIL) {  // lanes g = 0 hold rows 16 MTM + r; the other groups' rows are >= H
 #pragma unroll
       for (int r = 0; r < NTR; ++r) ns[MTM][r] += xsum(racc[r], true);
     }
-    float bn_v = -INFINITY, bs_v = -INFINITY;
-    int bn_i = 0, bs_i = 0;
+    Arg x{-INFINITY, -INFINITY, 0, 0};
 #pragma unroll
     for (int t = 0; t < G::MT_N; ++t)
 #pragma unroll
@@ -276,18 +285,21 @@ __global__ __launch_bounds__(kGanWaves * 64) void gan_kernel(FwdArgs a) {
           const float s0 = sv[t][r];
           const float nv = s0 + 4.0f * tanh_fast(ns[t][r]);
           ns[t][r] = nv;
-          if (nv > bn_v) {  // strict: first maximum wins (list.index(max(...)))
-            bn_v = nv;
-            bn_i = hh;
+          if (nv > x.bn_v) {  // strict: first maximum wins (list.index(max(...)))
+            x.bn_v = nv;
+            x.bn_i = hh;
           }
-          if (s0 > bs_v) {
-            bs_v = s0;
-            bs_i = hh;
+          if (s0 > x.bs_v) {
+            x.bs_v = s0;
+            x.bs_i = hh;
           }
         } else {
           ns[t][r] = 0.f;
         }
       }
+    return x;
+  };
+  auto finish_m2 = [&](const float* cw, const f32x4 (&ns)[G::MT_N]) {
     gan_prio<1>();
 #pragma unroll
     for (int q4 = 0; q4 < G::MT_N; ++q4)
@@ -303,6 +315,10 @@ __global__ __launch_bounds__(kGanWaves * 64) void gan_kernel(FwdArgs a) {
             for (int i = 0; i < 2; ++i) hd[m0 + i] = mfma(w[i][e], ns[q4][e], hd[m0 + i]);
       }
     gan_prio<0>();
+  };
+  auto finish_v2 = [&](int c, Arg x) {
+    float bn_v = x.bn_v, bs_v = x.bs_v;
+    int bn_i = x.bn_i, bs_i = x.bs_i;
 #pragma unroll
     for (int off = 16; off <= 32; off <<= 1) {
       const float ov = __shfl_xor(bn_v, off), os = __shfl_xor(bs_v, off);
@@ -329,6 +345,53 @@ __global__ __launch_bounds__(kGanWaves * 64) void gan_kernel(FwdArgs a) {
   };
   f32x4 ns[G::MT_N];
   float racc[kTailMax];
+  if constexpr (kGanPingPong) {
+    // Ping-pong: a workgroup barrier between the container's four phases
+    // (MFMA Gen2, VALU tanh / argmax, MFMA Disc1, VALU argmax / targets) with
+    // the second half of the waves one phase behind the first, so the two
+    // halves' MFMA and VALU phases alternate on every SIMD.  The ring: a
+    // chunk's slot is rewritten only after the lagging half's last read of it
+    // (its Disc1 of the chunk's last container); every wave waits for its DMA
+    // share of the next chunk (vmcnt(0)) at the same barrier, the first half
+    // after that container's targets, the second after its Disc1.
+    const bool lag = wv >= kGanWaves / 2;
+    float* slot0 = cur;  // container chunk 0 (loaded); chunk 1 is in flight into `nxt`
+    float* slot1 = nxt;
+    auto bar = [&]() {
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    // chunk k's slot is free: every wave has its DMA share of chunk k + 1
+    // landed (vmcnt(0), then the barrier makes all of it visible) and issues
+    // its share of chunk k + 2 into the slot
+    auto chunk_end = [&](int k) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      bar();
+      next = GG::NQC + 1 + (k + 2);
+      nxt = (k & 1) ? slot1 : slot0;
+      issue();
+    };
+    if (lag) bar();
+    for (int c = 0; c < G::C; ++c) {
+      const int k = c / GG::CPC;
+      const float* chunk = (k & 1) ? slot1 : slot0;
+      const float* cw = chunk + (c % GG::CPC) * G::GC_G * G::FQ;
+      const bool last = (c + 1) % GG::CPC == 0;
+      float svn[G::MT_N][4];
+      load_row(c + 1, svn);
+      gen2(c, cw, chunk, ns, racc);
+      bar();
+      const Arg x = finish_v1(ns, racc, sv);
+      bar();
+      finish_m2(cw, ns);
+      if (last && lag) chunk_end(k); else bar();
+      finish_v2(c, x);
+      if (last && !lag) chunk_end(k); else bar();
+      copy_row(sv, svn);
+    }
+    if (!lag) bar();
+  } else {
   for (int c = 0; c < G::C; ++c) {
     const float* cw = cur + (c % GG::CPC) * G::GC_G * G::FQ;  // this container's groups
     float svn[G::MT_N][4];
@@ -338,10 +401,13 @@ __global__ __launch_bounds__(kGanWaves * 64) void gan_kernel(FwdArgs a) {
     // MFMAs instead of every wave reaching them together (at most two
     // containers per chunk: with 4-8, at H <= 32, it cost the fleet 0.3 %)
     if (GG::CPC <= 2 && c % GG::CPC == 0 && wv >= kGanWaves / 2) __builtin_amdgcn_s_sleep(kGanSleep * GG::CPC);
-    gen2(c, cw, ns, racc);
-    finish(c, cw, ns, racc, sv);
+    gen2(c, cw, cur, ns, racc);
+    const Arg x = finish_v1(ns, racc, sv);
+    finish_m2(cw, ns);
+    finish_v2(c, x);
     if ((c + 1) % GG::CPC == 0) advance();
     copy_row(sv, svn);
+  }
   }
 
   // the wave's targets: its windows' rows are contiguous in gen_t / final_t

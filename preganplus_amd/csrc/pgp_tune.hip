@@ -306,6 +306,24 @@ PGP_DEV GatFold<H> gat_fold(const float* P) {
   return f;
 }
 
+// node factors of the factorised edge exponentials: for source i (s) and
+// destination j (t), exp(lrelu(s_i + t_j) - mx) = max(a_i * b_j, an_i * bn_j)
+// (exp is monotone and lrelu(e) = max(e, 0.01 e)); with smax = max_i s_i and
+// mx = lrelu(smax + tmax) every factor is <= 1, so none overflows and an
+// underflow only drops an edge below 1e-38 of the largest.  4 exponentials per
+// node instead of H per edge row.
+struct GatEdge {
+  float a, an, b, bn;
+};
+PGP_DEV GatEdge gat_edge(float s, float t, float smax, float mx) {
+  GatEdge e;
+  e.a = expf(s - smax);
+  e.an = expf(0.01f * (s - smax));
+  e.b = expf(t + smax - mx);
+  e.bn = expf(0.01f * (t + smax) - mx);
+  return e;
+}
+
 template <int H>
 __global__ __launch_bounds__(256) void gat_fwd_kernel(int B, const float* __restrict__ win,
                                                       const float* __restrict__ P, float* __restrict__ wcopy,
@@ -313,7 +331,7 @@ __global__ __launch_bounds__(256) void gat_fwd_kernel(int B, const float* __rest
                                                       float* __restrict__ GS) {
   using Q = TuneGeo<H>;
   using G = TGeo<H>;
-  __shared__ float ss[4][64], sx[4][64][3], sxb[4][64][4];
+  __shared__ float sa[4][64][2], sx[4][64][3], sxb[4][64][4];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const long pw = (long)blockIdx.x * 4 + wv;  // (window, step)
   const bool okw = pw < 3L * B;
@@ -333,7 +351,11 @@ __global__ __launch_bounds__(256) void gat_fwd_kernel(int B, const float* __rest
   const float t = fo.v[0] * x[0] + fo.v[1] * x[1] + fo.v[2] * x[2];
   const float smax = wave_max(okj ? s : -INFINITY), tmax = wave_max(okj ? t : -INFINITY);
   const float mx = lrelu(smax + tmax);  // max over all H^2 edges (leaky_relu is monotone)
-  ss[wv][j] = s;
+  // the H^2 edge exponentials factorise (as K1's, pgp_gat.hip):
+  // exp(lrelu(s_i + t_j) - mx) = max(A_i B_j, A'_i B'_j), every factor <= 1
+  const GatEdge ge = gat_edge(s, t, smax, mx);
+  sa[wv][j][0] = ge.a;
+  sa[wv][j][1] = ge.an;
 #pragma unroll
   for (int k = 0; k < 3; ++k) sx[wv][j][k] = x[k];
   __syncthreads();
@@ -341,7 +363,7 @@ __global__ __launch_bounds__(256) void gat_fwd_kernel(int B, const float* __rest
   if (okj)
 #pragma unroll 10
     for (int i = 0; i < H; ++i) {
-      const float p = expf(lrelu(ss[wv][i] + t) - mx);  // graph-wise softmax_edges (dlutils.py:335)
+      const float p = fmaxf(sa[wv][i][0] * ge.b, sa[wv][i][1] * ge.bn);  // graph-wise softmax_edges (dlutils.py:335)
       sum += p;
 #pragma unroll
       for (int k = 0; k < 3; ++k) xb[k] = fmaf(p, sx[wv][i][k], xb[k]);
@@ -400,7 +422,7 @@ __global__ __launch_bounds__(256) void gat_bwd_kernel(int B, const float* __rest
                                                       const float* __restrict__ GS, const float* __restrict__ Mt,
                                                       float* __restrict__ GSX, float* __restrict__ fcd) {
   using Q = TuneGeo<H>;
-  __shared__ float ss[4][64], st[4][64], sx[4][64][3], sdx[4][64][3], smt[64][3], sred[4][6];
+  __shared__ float ss[4][64], st[4][64], sx[4][64][3], sdx[4][64][3], smt[64][3], sred[4][6], sab[4][64][4];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const long pw = (long)blockIdx.x * 4 + wv;
   const bool okw = pw < 3L * B;
@@ -417,8 +439,14 @@ __global__ __launch_bounds__(256) void gat_bwd_kernel(int B, const float* __rest
   const float s = fo.u[0] * x[0] + fo.u[1] * x[1] + fo.u[2] * x[2];
   const float t = fo.v[0] * x[0] + fo.v[1] * x[1] + fo.v[2] * x[2];
   const float mx = okw ? GS[pw * 4] : 0.f, iz = okw ? 1.0f / GS[pw * 4 + 1] : 0.f;
+  const float smax = wave_max(okj ? s : -INFINITY);
+  const GatEdge ge = gat_edge(s, t, smax, mx);  // the forward's factorised edge weights (gat_fwd_kernel)
   ss[wv][j] = s;
   st[wv][j] = t;
+  sab[wv][j][0] = ge.a;
+  sab[wv][j][1] = ge.an;
+  sab[wv][j][2] = ge.b;
+  sab[wv][j][3] = ge.bn;
 #pragma unroll
   for (int k = 0; k < 3; ++k) sx[wv][j][k] = x[k];
   __syncthreads();
@@ -461,7 +489,7 @@ __global__ __launch_bounds__(256) void gat_bwd_kernel(int B, const float* __rest
 #pragma unroll 10
     for (int i = 0; i < H; ++i) {
       const float pre = ss[wv][i] + t;
-      const float a = expf(lrelu(pre) - mx) * iz;
+      const float a = fmaxf(sab[wv][i][0] * ge.b, sab[wv][i][1] * ge.bn) * iz;
       const float da = dxb[0] * sx[wv][i][0] + dxb[1] * sx[wv][i][1] + dxb[2] * sx[wv][i][2];
       const float sl = pre > 0.f ? a : 0.01f * a;
       part = fmaf(a, da, part);
@@ -475,7 +503,7 @@ __global__ __launch_bounds__(256) void gat_bwd_kernel(int B, const float* __rest
 #pragma unroll 10
     for (int jj = 0; jj < H; ++jj) {  // this lane as source
       const float pre = s + st[wv][jj];
-      const float a = expf(lrelu(pre) - mx) * iz;
+      const float a = fmaxf(ge.a * sab[wv][jj][2], ge.an * sab[wv][jj][3]) * iz;
       const float da = sdx[wv][jj][0] * x[0] + sdx[wv][jj][1] * x[1] + sdx[wv][jj][2] * x[2];
       ds = fmaf(a * (da - dot), pre > 0.f ? 1.f : 0.01f, ds);
     }

@@ -116,6 +116,17 @@ for step in "$@"; do
       run abp16 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 16 --steps 100 --warmup 10 --no-cpu-baseline" new= prev=PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_prev.so
       grep median $OUT/abp16.out
       ;;
+    abpp)
+      run pp_quick_base 180 python -u -m pytest tests/test_gpu_parity.py -k "not census" -x -q -p no:cacheprovider --timeout 120 --timeout-method thread
+      PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_k2pp.so run pp_quick 180 python -u -m pytest tests/test_gpu_parity.py -k "not census" -x -q -p no:cacheprovider --timeout 120 --timeout-method thread
+      PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_k3pp.so run pp_quick_k3 180 python -u -m pytest tests/test_gpu_parity.py -k "not census" -x -q -p no:cacheprovider --timeout 120 --timeout-method thread
+      tail -2 $OUT/pp_quick.out
+      run abpp 600 python3 -u tools/ab_bench.py --rounds 3 --args "--steps 100 --warmup 10 --no-cpu-baseline" base= k2pp=PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_k2pp.so k3pp=PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_k3pp.so
+      grep median $OUT/abpp.out
+      python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); [print(k, [{kk: round(vv, 4) for kk, vv in e['kernel_ms'].items()} for e in v]) for k, v in d['extra'].items()]" $OUT/abpp.out
+      run abtfpp 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" base= tfpp=PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_tfpp.so
+      grep median $OUT/abtfpp.out
+      ;;
     others)
       run fpe 300 python3 -u bench.py --config fpe --steps 100 --warmup 5
       run plugin 300 python3 -u bench.py --config plugin --steps 50 --warmup 5
