@@ -77,29 +77,6 @@ PGP_DEV float relu_enc(float x) {
     return fmaxf(x, 0.f);
 }
 
-// Ping-pong (tail-resident mode): the two waves of a SIMD come from the two
-// halves of the 8-wave workgroup, and a workgroup barrier at every boundary
-// between an MFMA-heavy and a VALU-heavy phase of the host chain keeps the
-// second half one phase behind the first, so while one wave of a SIMD runs a
-// GEMM the other runs a LayerNorm / softmax phase (8 phases per unit: VALU
-// [LN2 + store + layer 0 scores / fold / LN1], MFMA [layer 0 FFN], VALU [LN2],
-// MFMA [q | k], VALU [scores], MFMA [v, P.v, out_proj], VALU [LN1], MFMA [FFN]).
-// Every wave of the workgroup executes 8 x (the most units of any wave) + 1
-// barriers: the second half one before its first unit, the first half one
-// after its last, waves with fewer units the difference at the end.
-#ifndef PGP_ENC_PINGPONG
-#define PGP_ENC_PINGPONG 0
-#endif
-constexpr bool kEncPingPong = PGP_ENC_PINGPONG;
-template <bool PP>
-PGP_DEV void pp_sync() {
-  if constexpr (PP) {
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-  }
-}
-
 // MFMA phases run at wave priority 1, VALU phases (softmax, LayerNorm) at 0: the
 // co-resident wave of the other workgroup on the SIMD then gets its MFMA issue
 // slots ahead of a VALU stream
@@ -363,13 +340,12 @@ PGP_DEV float row_fold_bias(int m, int n, int w, const float* tab) {
 // Tail-mode layer (Geo<H>::TAIL, H = 50): stages [qk] [v o] [f1 f2].
 // F0: layer 0, q/k/v from the folded raw-feature product (the ring's q/k/v
 // stages are then unused).
-template <int H, bool F0, bool PP>
+template <int H, bool F0>
 PGP_DEV void encoder_layer_tail(f32x4 (&X)[Geo<H>::MT_D][3], Ring<H>& ring, const float* TL, int lane,
                                 const float* tab, const float (&ba)[3], const float (&xv)[3][3]) {
   using G = Geo<H>;
   constexpr int TQ = G::TQ, SR = G::SR, HF = G::HF;
   const int g = lane >> 4;
-  if constexpr (!F0) pp_sync<PP>();  // VALU [layer 0's LN2] | MFMA [q | k]
   // [S0] q and k of both heads
   constexpr bool BIL = F0;  // layer 0's scores as bilinear forms (the q / k fold is not needed)
   f32x4 QK[BIL ? 1 : 2 * TQ][3];
@@ -393,7 +369,6 @@ PGP_DEV void encoder_layer_tail(f32x4 (&X)[Geo<H>::MT_D][3], Ring<H>& ring, cons
         qr[n][w] = qkr[n][w] + TL[G::TL_RQB + n];
         kr[n][w] = qkr[SR + n][w] + TL[G::TL_RQB + SR + n];
       }
-    pp_sync<PP>();  // MFMA [q | k] | VALU [scores, softmax]
   }
   ring.advance();
   // scores of both heads; the shared tile's slot 4r+g belongs to head 0 below HT
@@ -470,7 +445,6 @@ PGP_DEV void encoder_layer_tail(f32x4 (&X)[Geo<H>::MT_D][3], Ring<H>& ring, cons
     P1[w][1] = e11 * i1;
     P1[w][2] = e12 * i1;
   }
-  if constexpr (!F0) pp_sync<PP>();  // VALU [scores, softmax] | MFMA [v, P.v, out_proj]
   f32x4 acc[G::MT_D][3];
 #pragma unroll
   for (int mt = 0; mt < G::MT_D; ++mt) {
@@ -555,10 +529,8 @@ PGP_DEV void encoder_layer_tail(f32x4 (&X)[Geo<H>::MT_D][3], Ring<H>& ring, cons
 #pragma unroll
     for (int w = 0; w < 3; ++w) acc[G::MT_X][w][0] += rows_pick<G::XR>(ro, w);
   }
-  pp_sync<PP>();  // MFMA [v, P.v, out_proj] | VALU [LN1]
   layer_norm_tiles<H, false>(acc, X, TL + G::TL_LN1G, TL + G::TL_LN1B, g);
   }  // F0
-  pp_sync<PP>();  // VALU [LN1] | MFMA [FFN]
   ring.advance();
   // [S2] relu(W1 x + b1), W2 . h + b2 + x, norm2
   // hidden tile by hidden tile: tile c of relu(W1 x + b1) is k-group c of the
@@ -608,7 +580,6 @@ PGP_DEV void encoder_layer_tail(f32x4 (&X)[Geo<H>::MT_D][3], Ring<H>& ring, cons
 #pragma unroll
     for (int w = 0; w < 3; ++w) acc[G::MT_X][w][0] += rows_pick<G::XR>(rf, w);
   }
-  pp_sync<PP>();  // MFMA [FFN] | VALU [LN2]
   ring.advance();
   // both norm2s emit x-hat: layer 0's gamma / beta are folded into layer 1's
   // in_proj and residual, the last layer's into the decoders (which are linear
@@ -702,8 +673,6 @@ __global__ __launch_bounds__(enc_waves<H>() * 64, H <= 16 ? kEnc16EU : tail_res<
   const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   constexpr int NW = enc_waves<H>();
-  constexpr bool PP = kEncPingPong && L::UNITS && G::TAIL && NW == 8;
-  constexpr int kPhases = 8;  // pp_sync calls per unit (encoder_layer_tail: 2 in layer 0, 6 in layer 1)
   const long nblk = (a.B + 15) / 16;
 
   Ring<H> ring{smem, smem + L::SLOT, a.frags + G::OFF_ENC, 0, H * kLayers * G::NST, wv, lane};
@@ -757,8 +726,8 @@ __global__ __launch_bounds__(enc_waves<H>() * 64, H <= 16 ? kEnc16EU : tail_res<
     }
     static_assert(kLayers == 2, "layer 0 (folded q/k/v) + layer 1");
     if constexpr (G::TAIL) {
-      encoder_layer_tail<H, true, PP>(X, ring, tab + G::T_L0, lane, tab, ba, xv);
-      encoder_layer_tail<H, false, PP>(X, ring, tab + G::T_L0 + G::TL_SIZE, lane, tab, ba, xv);
+      encoder_layer_tail<H, true>(X, ring, tab + G::T_L0, lane, tab, ba, xv);
+      encoder_layer_tail<H, false>(X, ring, tab + G::T_L0 + G::TL_SIZE, lane, tab, ba, xv);
     } else {
       encoder_layer<H, true>(X, ring, tab + G::T_L0, lane, tab, ba);
       encoder_layer<H, false>(X, ring, tab + G::T_L0 + G::TL_SIZE, lane, tab, ba);
@@ -823,21 +792,12 @@ __global__ __launch_bounds__(enc_waves<H>() * 64, H <= 16 ? kEnc16EU : tail_res<
       load_x(u0);
       stage_x();
     }
-    const bool lag = wv >= NW / 2;  // ping-pong: the second half runs one phase behind
-    if (PP && lag) pp_sync<PP>();
 #pragma unroll 1
     for (long u = u0; u < u1; ++u) {
       load_x(u + 1 < u1 ? u + 1 : u);
       const long blk = u / H;
       unit(blk, (int)(u - blk * H), true, slot);
       stage_x();
-    }
-    if constexpr (PP) {
-      // every wave: kPhases x (the most units of any wave) + 1 barriers in all
-      const long most = (U + NWT - 1) / NWT;
-#pragma unroll 1
-      for (long k = (u1 - u0) * kPhases; k < most * kPhases; ++k) pp_sync<PP>();
-      if (!lag) pp_sync<PP>();
     }
   } else {
     const long blk = (long)blockIdx.x * NW + wv;

@@ -36,10 +36,7 @@ constexpr int kQC = 8;
 constexpr int kChunkG = 65;
 constexpr int kTailMax = 2;
 constexpr int kGanSleep = 24;
-#ifndef PGP_GAN_PINGPONG
-#define PGP_GAN_PINGPONG 0
-#endif
-constexpr bool kGanPingPong = PGP_GAN_PINGPONG;
+
 template <int P>
 __device__ __forceinline__ void gan_prio() {
   __builtin_amdgcn_s_setprio(P);
@@ -345,53 +342,6 @@ __global__ __launch_bounds__(kGanWaves * 64) void gan_kernel(FwdArgs a) {
   };
   f32x4 ns[G::MT_N];
   float racc[kTailMax];
-  if constexpr (kGanPingPong) {
-    // Ping-pong: a workgroup barrier between the container's four phases
-    // (MFMA Gen2, VALU tanh / argmax, MFMA Disc1, VALU argmax / targets) with
-    // the second half of the waves one phase behind the first, so the two
-    // halves' MFMA and VALU phases alternate on every SIMD.  The ring: a
-    // chunk's slot is rewritten only after the lagging half's last read of it
-    // (its Disc1 of the chunk's last container); every wave waits for its DMA
-    // share of the next chunk (vmcnt(0)) at the same barrier, the first half
-    // after that container's targets, the second after its Disc1.
-    const bool lag = wv >= kGanWaves / 2;
-    float* slot0 = cur;  // container chunk 0 (loaded); chunk 1 is in flight into `nxt`
-    float* slot1 = nxt;
-    auto bar = [&]() {
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-    };
-    // chunk k's slot is free: every wave has its DMA share of chunk k + 1
-    // landed (vmcnt(0), then the barrier makes all of it visible) and issues
-    // its share of chunk k + 2 into the slot
-    auto chunk_end = [&](int k) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      bar();
-      next = GG::NQC + 1 + (k + 2);
-      nxt = (k & 1) ? slot1 : slot0;
-      issue();
-    };
-    if (lag) bar();
-    for (int c = 0; c < G::C; ++c) {
-      const int k = c / GG::CPC;
-      const float* chunk = (k & 1) ? slot1 : slot0;
-      const float* cw = chunk + (c % GG::CPC) * G::GC_G * G::FQ;
-      const bool last = (c + 1) % GG::CPC == 0;
-      float svn[G::MT_N][4];
-      load_row(c + 1, svn);
-      gen2(c, cw, chunk, ns, racc);
-      bar();
-      const Arg x = finish_v1(ns, racc, sv);
-      bar();
-      finish_m2(cw, ns);
-      if (last && lag) chunk_end(k); else bar();
-      finish_v2(c, x);
-      if (last && !lag) chunk_end(k); else bar();
-      copy_row(sv, svn);
-    }
-    if (!lag) bar();
-  } else {
   for (int c = 0; c < G::C; ++c) {
     const float* cw = cur + (c % GG::CPC) * G::GC_G * G::FQ;  // this container's groups
     float svn[G::MT_N][4];
@@ -407,7 +357,6 @@ __global__ __launch_bounds__(kGanWaves * 64) void gan_kernel(FwdArgs a) {
     finish_v2(c, x);
     if ((c + 1) % GG::CPC == 0) advance();
     copy_row(sv, svn);
-  }
   }
 
   // the wave's targets: its windows' rows are contiguous in gen_t / final_t

@@ -565,23 +565,6 @@ PGP_DEV void tf_attn_probs(const f32x4 (&QK)[2 * TF<H>::NT][3], float (&P)[2][3]
 // prefetch waits) are covered by the other wave's MFMAs.  q | k and v are
 // separate GEMMs (96 + 48 accumulator registers instead of 144 at once).
 constexpr int kTfFwdWaves = 8;
-// Ping-pong (as K2, pgp_encoder.hip): a workgroup barrier at every boundary
-// between the unit's MFMA and VALU phases, the second half of the waves one
-// phase behind the first, so the two waves of a SIMD alternate GEMM and
-// LayerNorm / softmax phases.  8 phases per unit: [TE +] q|k, probabilities,
-// v, P.v, out_proj, LN1, FFN, LN2 + store.
-#ifndef PGP_TF_PINGPONG
-#define PGP_TF_PINGPONG 0
-#endif
-constexpr bool kTfPingPong = PGP_TF_PINGPONG;
-template <bool PP>
-PGP_DEV void tf_pp_sync() {
-  if constexpr (PP) {
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-  }
-}
 
 template <int H>
 __global__ __launch_bounds__(kTfFwdWaves * 64, 1) void tf_fwd_kernel(TfArgs a) {
@@ -604,10 +587,6 @@ __global__ __launch_bounds__(kTfFwdWaves * 64, 1) void tf_fwd_kernel(TfArgs a) {
   const long npairs = (long)a.B * H, nu = (npairs + 15) / 16, spare = 3 * npairs;
   long u0, u1;
   unit_range(nu, u0, u1, kTfFwdWaves);
-  constexpr bool PP = kTfPingPong;
-  constexpr int kPhases = 8;  // tf_pp_sync calls per unit
-  const bool lag = (threadIdx.x >> 6) >= kTfFwdWaves / 2;
-  if (PP && lag) tf_pp_sync<PP>();
   // the unit's input (layer 0: the GAT output) is loaded one unit ahead during
   // the previous unit's linear2; x0 is stored during q|k, norm1's x-hat / rstd
   // during linear1, the layer output at the end of the unit
@@ -656,17 +635,14 @@ __global__ __launch_bounds__(kTfFwdWaves * 64, 1) void tf_fwd_kernel(TfArgs a) {
                                     }
                                   });
       TF_ST(3);
-      tf_pp_sync<PP>();  // MFMA [q | k] | VALU [probabilities]
       tf_attn_probs<H>(QK, Pr, g);
     }
     f32x4 O[NT][3];
     {  // v, then O = P . v per head
       f32x4 V[NT][3];
-      tf_pp_sync<PP>();  // VALU [probabilities] | MFMA [v]
       init_bias<NT>(V, par + Q::BIN + 2 * NT * 16, g);
       tf_gemm<NT, F::KS>(V, sm + L::W_IN + 2 * NT * F::KG * 256, [&](int s, int w) { return X[s >> 2][w][s & 3]; },
                          lane);
-      tf_pp_sync<PP>();  // MFMA [v] | VALU [P . v]
 #pragma unroll
       for (int t = 0; t < NT; ++t)
 #pragma unroll
@@ -682,10 +658,8 @@ __global__ __launch_bounds__(kTfFwdWaves * 64, 1) void tf_fwd_kernel(TfArgs a) {
     }
     TF_ST(4);
     f32x4 R[NT][3];
-    tf_pp_sync<PP>();  // VALU [P . v] | MFMA [out_proj]
     init_bias<NT>(R, par + Q::BO, g);
     tf_gemm<NT, F::KS>(R, sm + L::W_O, [&](int s, int w) { return O[s >> 2][w][s & 3]; }, lane);
-    tf_pp_sync<PP>();  // MFMA [out_proj] | VALU [LN1]
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
@@ -702,7 +676,6 @@ __global__ __launch_bounds__(kTfFwdWaves * 64, 1) void tf_fwd_kernel(TfArgs a) {
       for (int w = 0; w < 3; ++w) X[t][w] = R[t][w] * ga + be;
     }
     f32x4 Fh[4][3];
-    tf_pp_sync<PP>();  // VALU [LN1] | MFMA [FFN]
     init_bias<4>(Fh, par + Q::B1, g);
     {  // side work: norm1's x-hat tiles and rstd (every lane group: the same value)
       constexpr int NS = 3 * NT + 3, NG = 4 * F::KG, PER = (NS + NG - 1) / NG;
@@ -740,7 +713,6 @@ __global__ __launch_bounds__(kTfFwdWaves * 64, 1) void tf_fwd_kernel(TfArgs a) {
                              }
                            });
     }
-    tf_pp_sync<PP>();  // MFMA [FFN] | VALU [LN2, store]
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
@@ -758,14 +730,6 @@ __global__ __launch_bounds__(kTfFwdWaves * 64, 1) void tf_fwd_kernel(TfArgs a) {
 #pragma unroll
       for (int t = 0; t < NT; ++t) st4(tile_at(a.out, srow[w]) + 16 * t, R[t][w]);
     TF_ST(9);
-    tf_pp_sync<PP>();  // VALU [LN2, store] | MFMA [the next unit's (TE +) q | k]
-  }
-  if constexpr (PP) {
-    // every wave: kPhases x (the most units of any wave) + 1 barriers in all
-    const long most = (nu + (long)gridDim.x * kTfFwdWaves - 1) / ((long)gridDim.x * kTfFwdWaves);
-#pragma unroll 1
-    for (long k = (u1 - u0) * kPhases; k < most * kPhases; ++k) tf_pp_sync<PP>();
-    if (!lag) tf_pp_sync<PP>();
   }
   TF_ST(10);
   TF_ST_END(layer);
