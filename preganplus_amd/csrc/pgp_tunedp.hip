@@ -41,28 +41,35 @@ namespace {
 constexpr int kWin = 3;  // models.py:320 n_window
 
 // ---------------------------------------------------------------------------
-// dataset: one thread per (environment, host)
+// dataset: one thread per (environment, host, column): wave c of a 3-wave
+// workgroup holds column c of 64 (environment, host) pairs, so the per-value
+// fp64 work (the division by the column max, the rank search of the
+// percentile) runs 3 ways parallel; the labels, which need all three columns,
+// are formed by wave 0 from LDS.  (One thread per pair held 30 fp64 divisions
+// and 300 comparisons in one chain: 25 us for C3's 103 environments.)
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void tune_dataset_kernel(int H, int E, int R, const double* __restrict__ series,
-                                                           const double* __restrict__ train_max,
-                                                           float* __restrict__ windows, int* __restrict__ y,
-                                                           int* __restrict__ cls, float* __restrict__ infer) {
+constexpr int kDsPairs = 64;
+__global__ __launch_bounds__(3 * kDsPairs) void tune_dataset_kernel(int H, int E, int R,
+                                                                   const double* __restrict__ series,
+                                                                   const double* __restrict__ train_max,
+                                                                   float* __restrict__ windows, int* __restrict__ y,
+                                                                   int* __restrict__ cls, float* __restrict__ infer) {
 #pragma clang fp contract(off)
-  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= (long)E * H) return;
-  const int e = (int)(t / H), h = (int)(t % H);
+  __shared__ double sv[3][kMaxTuneRows][kDsPairs], sthr[3][kDsPairs];
+  const int c = threadIdx.x / kDsPairs, q = threadIdx.x % kDsPairs;  // column (wave-uniform), pair slot
+  const long t = (long)blockIdx.x * kDsPairs + q;
+  const bool ok = t < (long)E * H;
+  const int e = ok ? (int)(t / H) : 0, h = ok ? (int)(t % H) : 0;
   const int F = 3 * H;
   // every loop runs to kMaxTuneRows with an r < R guard, so all indices are
   // compile-time and the rows stay in registers
-  double v[kMaxTuneRows][3];  // normalised rows x the host's 3 columns
-#pragma unroll
-  for (int c = 0; c < 3; ++c) {
+  double v[kMaxTuneRows];  // this column's normalised rows
+  {
     const double den = train_max[3 * h + c] + 1e-8;  // np.max(train, axis=0) + 1e-8
 #pragma unroll
-    for (int r = 0; r < kMaxTuneRows; ++r)
-      v[r][c] = r < R ? series[((long)e * R + r) * F + 3 * h + c] / den : 0.0;
+    for (int r = 0; r < kMaxTuneRows; ++r) v[r] = (ok && r < R) ? series[((long)e * R + r) * F + 3 * h + c] / den : 0.0;
   }
-  // 98th percentile per column, numpy 'linear': virtual index (R-1)*0.98,
+  // 98th percentile of the column, numpy 'linear': virtual index (R-1)*0.98,
   // gamma = frac, lerp(a, b, g) = g >= 0.5 ? b - (b-a)(1-g) : a + (b-a) g.
   // The order statistics ilo, ihi are found by stable rank (the element with
   // rank p is sorted[p]) instead of sorting.
@@ -70,57 +77,68 @@ __global__ __launch_bounds__(256) void tune_dataset_kernel(int H, int E, int R, 
   const double lo = floor(vi);
   const double gm = vi - lo;
   const int ilo = (int)lo, ihi = ilo + 1 < R ? ilo + 1 : R - 1;
-  double thr[3];
-#pragma unroll
-  for (int c = 0; c < 3; ++c) {
+  double thr;
+  {
     double a = 0.0, b = 0.0;
 #pragma unroll
     for (int r = 0; r < kMaxTuneRows; ++r) {
       int rank = 0;
 #pragma unroll
       for (int j = 0; j < kMaxTuneRows; ++j)
-        if (j != r && j < R) rank += (v[j][c] < v[r][c] || (j < r && v[j][c] == v[r][c])) ? 1 : 0;
-      if (r < R && rank == ilo) a = v[r][c];
-      if (r < R && rank == ihi) b = v[r][c];
+        if (j != r && j < R) rank += (v[j] < v[r] || (j < r && v[j] == v[r])) ? 1 : 0;
+      if (r < R && rank == ilo) a = v[r];
+      if (r < R && rank == ihi) b = v[r];
     }
     const double d = b - a;
-    thr[c] = gm >= 0.5 ? b - d * (1.0 - gm) : a + d * gm;
+    thr = gm >= 0.5 ? b - d * (1.0 - gm) : a + d * gm;
   }
 #pragma unroll
-  for (int r = 0; r < kMaxTuneRows; ++r) {
-    if (r < R) {
-      const bool an = v[r][0] > thr[0] || v[r][1] > thr[1] || v[r][2] > thr[2];
-      int am = 0;  // np.argmax: first maximum
-      if (v[r][1] > v[r][am]) am = 1;
-      if (v[r][2] > v[r][am]) am = 2;
-      y[((long)e * R + r) * H + h] = an ? 1 : 0;
-      cls[((long)e * R + r) * H + h] = am;
-      // convert_to_windows: window r = rows r-3..r-1, row 0 repeated for r < 3
+  for (int r = 0; r < kMaxTuneRows; ++r) sv[c][r][q] = v[r];
+  sthr[c][q] = thr;
+  if (ok) {
 #pragma unroll
-      for (int w = 0; w < kWin; ++w) {
-        const int src = r >= kWin ? r - kWin + w : (w < kWin - r ? 0 : w - (kWin - r));
-        float* o = windows + (((long)e * R + r) * kWin + w) * F + 3 * h;
+    for (int r = 0; r < kMaxTuneRows; ++r) {
+      if (r < R) {
+        // convert_to_windows: window r = rows r-3..r-1, row 0 repeated for r < 3
 #pragma unroll
-        for (int c = 0; c < 3; ++c) o[c] = (float)v[src][c];
+        for (int w = 0; w < kWin; ++w) {
+          const int src = r >= kWin ? r - kWin + w : (w < kWin - r ? 0 : w - (kWin - r));
+          windows[(((long)e * R + r) * kWin + w) * F + 3 * h + c] = (float)v[src];
+        }
       }
     }
-  }
-  if (infer) {  // run_encoder: last 3 rows -> convert_to_windows(...)[-1] = [R-3, R-3, R-2];
-                // a shorter series (R = 1, 2: the first intervals) keeps all its rows and
-                // its last window is row 0 three times
-    const int ra = R >= kWin ? R - 3 : 0, rb = R >= kWin ? R - 2 : 0;
-    double u[2][3] = {};
+    if (infer) {  // run_encoder: last 3 rows -> convert_to_windows(...)[-1] = [R-3, R-3, R-2];
+                  // a shorter series (R = 1, 2: the first intervals) keeps all its rows and
+                  // its last window is row 0 three times
+      const int ra = R >= kWin ? R - 3 : 0, rb = R >= kWin ? R - 2 : 0;
+      double u0 = 0.0, u1 = 0.0;
 #pragma unroll
-    for (int r = 0; r < kMaxTuneRows; ++r)
-#pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        if (r == ra) u[0][c] = v[r][c];
-        if (r == rb) u[1][c] = v[r][c];
+      for (int r = 0; r < kMaxTuneRows; ++r) {
+        if (r == ra) u0 = v[r];
+        if (r == rb) u1 = v[r];
       }
 #pragma unroll
-    for (int w = 0; w < kWin; ++w)
+      for (int w = 0; w < kWin; ++w) infer[((long)e * kWin + w) * F + 3 * h + c] = (float)(w < 2 ? u0 : u1);
+    }
+  }
+  __syncthreads();
+  if (c == 0 && ok) {  // labels: all three columns of the pair
 #pragma unroll
-      for (int c = 0; c < 3; ++c) infer[((long)e * kWin + w) * F + 3 * h + c] = (float)u[w < 2 ? 0 : 1][c];
+    for (int r = 0; r < kMaxTuneRows; ++r) {
+      if (r < R) {
+        const double x0 = sv[0][r][q], x1 = sv[1][r][q], x2 = sv[2][r][q];
+        const bool an = x0 > sthr[0][q] || x1 > sthr[1][q] || x2 > sthr[2][q];
+        int am = 0;  // np.argmax: first maximum
+        double best = x0;
+        if (x1 > best) {
+          am = 1;
+          best = x1;
+        }
+        if (x2 > best) am = 2;
+        y[((long)e * R + r) * H + h] = an ? 1 : 0;
+        cls[((long)e * R + r) * H + h] = am;
+      }
+    }
   }
 }
 
@@ -282,7 +300,8 @@ __global__ void tune_state_apply_kernel(int K, double* __restrict__ state, const
 hipError_t launch_tune_dataset(int H, int E, int R, const double* series, const double* train_max, float* windows,
                                int* y, int* cls, float* infer, hipStream_t st) {
   const long n = (long)E * H;
-  tune_dataset_kernel<<<(int)((n + 255) / 256), 256, 0, st>>>(H, E, R, series, train_max, windows, y, cls, infer);
+  tune_dataset_kernel<<<(int)((n + kDsPairs - 1) / kDsPairs), 3 * kDsPairs, 0, st>>>(H, E, R, series, train_max,
+                                                                                     windows, y, cls, infer);
   return hipGetLastError();
 }
 

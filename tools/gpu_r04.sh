@@ -127,6 +127,13 @@ for step in "$@"; do
       run abtfpp 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" base= tfpp=PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_tfpp.so
       grep median $OUT/abtfpp.out
       ;;
+    abfull)
+      run abfull50 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" base= fullreg=PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_fullreg.so
+      grep median $OUT/abfull50.out
+      run abfull16 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 16 --steps 100 --warmup 10 --no-cpu-baseline" base= fullreg=PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_fullreg.so
+      grep median $OUT/abfull16.out
+      PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_fullreg.so run prof_full 240 rocprofv3 --kernel-trace --stats -d $OUT/prof_full -o tune --output-format csv -- python3 bench.py --config tune --hosts 50 --steps 30 --warmup 5 --no-cpu-baseline
+      ;;
     others)
       run fpe 300 python3 -u bench.py --config fpe --steps 100 --warmup 5
       run plugin 300 python3 -u bench.py --config plugin --steps 50 --warmup 5
