@@ -37,9 +37,6 @@ namespace pgp {
 namespace {
 
 constexpr int kTfWaves = 4;  // one wave per SIMD (the backward needs > 256 registers)
-#ifndef PGP_TF_FULLREG
-#define PGP_TF_FULLREG 0
-#endif
 
 // Phase attribution (profiling builds only: make variant NAME=st
 // VFLAGS=-DPGP_TF_STAMPS, read by tools/tf_stamps.py): each wave adds the
@@ -575,7 +572,6 @@ __global__ __launch_bounds__(kTfFwdWaves * 64, 1) void tf_fwd_kernel(TfArgs a) {
   using L = FwdL<H>;
   using Q = TfPar<H>;
   constexpr int NT = F::NT;
-  if constexpr (PGP_TF_FULLREG) asm volatile("" ::: "v255");
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, g = lane >> 4, j = lane & 15;
   const int layer = a.layer;
@@ -836,7 +832,6 @@ __global__ __launch_bounds__(kTfWaves * 64, 1) void tf_bwd_ffn_kernel(TfArgs a) 
   constexpr int NT = F::NT;
   static_assert(kTfWaves * L::NV <= L::SCR, "epilogue partials fit the LDS they reuse");
   static_assert(kTfWaves * L::NTW * 256 <= L::TOTAL, "epilogue dW regions fit the LDS they reuse");
-  if constexpr (PGP_TF_FULLREG) asm volatile("" ::: "a255");
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, g = lane >> 4, j = lane & 15;
   const int layer = a.layer;

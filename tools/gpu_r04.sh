@@ -134,6 +134,10 @@ for step in "$@"; do
       grep median $OUT/abfull16.out
       PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_fullreg.so run prof_full 240 rocprofv3 --kernel-trace --stats -d $OUT/prof_full -o tune --output-format csv -- python3 bench.py --config tune --hosts 50 --steps 30 --warmup 5 --no-cpu-baseline
       ;;
+    abloop)
+      run abloop 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config loop --steps 20 --warmup 3 --no-cpu-baseline" base= res0=PGP_GAN_RESERVED_CUS=0 res32=PGP_GAN_RESERVED_CUS=32 one=PGP_BENCH_ONE_STREAM=1
+      grep median $OUT/abloop.out
+      ;;
     others)
       run fpe 300 python3 -u bench.py --config fpe --steps 100 --warmup 5
       run plugin 300 python3 -u bench.py --config plugin --steps 50 --warmup 5
