@@ -487,20 +487,26 @@ struct OuterArgs {
   OuterProd p[4];
 };
 
-// one wave per 64 x 64 block of one product: 4 x 4 MFMA tiles, one k-step per
-// 4 environments (k = lane group), the next step's 8 values loaded ahead
-__global__ __launch_bounds__(256) void outer_kernel(OuterArgs a) {
-  const int lane = threadIdx.x & 63, g = lane >> 4, i = lane & 15;
-  const int blk = blockIdx.x * 4 + (threadIdx.x >> 6);
+// one workgroup per 64 x 64 block of one product: 4 x 4 MFMA tiles, one
+// k-step per 4 environments (k = lane group); its kOW waves take contiguous
+// eighths of the batch (three steps in flight each) and their partial tiles
+// are summed in wave order through LDS (deterministic).  One wave per block
+// ran a B/4-step chain: 55 us at the online loop's 1,024 environments.
+constexpr int kOW = 8;
+__global__ __launch_bounds__(kOW * 64) void outer_kernel(OuterArgs a) {
+  __shared__ __attribute__((aligned(16))) float red[(kOW - 1) * 16 * 256];
+  __shared__ float bred[(kOW - 1) * 4 * 64];
+  const int lane = threadIdx.x & 63, g = lane >> 4, i = lane & 15, wv = threadIdx.x >> 6;
+  const int blk = blockIdx.x;
   int pi = -1;
 #pragma unroll
   for (int k = 0; k < 4; ++k)
     if (k < a.nprod && blk >= a.p[k].first) pi = k;
-  if (pi < 0) return;
+  if (pi < 0) return;  // (workgroup-uniform)
   const OuterProd p = a.p[pi];
   const int lb = blk - p.first;
   const int nb = lb / p.nbk, kb = lb - nb * p.nbk;
-  if (nb * 64 >= p.N) return;  // past the product (the grid rounds up)
+  if (nb * 64 >= p.N) return;  // past the product (workgroup-uniform)
   const int n0 = nb * 64, k0 = kb * 64;
   f32x4 acc[4][4];
 #pragma unroll
@@ -515,9 +521,10 @@ __global__ __launch_bounds__(256) void outer_kernel(OuterArgs a) {
     kok[t] = k0 + 16 * t + i < p.K;
   }
   const int steps = (a.B + 3) / 4;
+  const int s0 = (int)((long)steps * wv / kOW), s1 = (int)((long)steps * (wv + 1) / kOW);
   auto load = [&](int s, float (&y)[4], float (&x)[4]) {
     const long e = 4L * s + g;
-    const bool ok = e < a.B;
+    const bool ok = s < s1 && e < a.B;
     const float* yr = p.Y + e * a.ld_rows + n0 + i;
     const float* xr = p.X + e * a.ld_rows + k0 + i;
 #pragma unroll
@@ -528,11 +535,11 @@ __global__ __launch_bounds__(256) void outer_kernel(OuterArgs a) {
   };
   // three steps in flight: step s + 2's values are loaded before step s's MFMAs
   float y[4], x[4], y1[4], x1[4];
-  load(0, y, x);
-  load(steps > 1 ? 1 : 0, y1, x1);
-  for (int s = 0; s < steps; ++s) {
+  load(s0, y, x);
+  load(s0 + 1, y1, x1);
+  for (int s = s0; s < s1; ++s) {
     float yn[4], xn[4];
-    load(s + 2 < steps ? s + 2 : s, yn, xn);
+    load(s + 2, yn, xn);
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       bs[t] += y[t];
@@ -547,6 +554,24 @@ __global__ __launch_bounds__(256) void outer_kernel(OuterArgs a) {
       x1[t] = xn[t];
     }
   }
+  if (wv > 0) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) st4(red + (((wv - 1) * 16 + t * 4 + u) * 64 + lane) * 4, acc[t][u]);
+      bred[((wv - 1) * 4 + t) * 64 + lane] = bs[t];
+    }
+  }
+  __syncthreads();
+  if (wv != 0) return;
+#pragma unroll 1
+  for (int w = 1; w < kOW; ++w)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc[t][u] += ld4(red + (((w - 1) * 16 + t * 4 + u) * 64 + lane) * 4);
+      bs[t] += bred[((w - 1) * 4 + t) * 64 + lane];
+    }
 #pragma unroll
   for (int t = 0; t < 4; ++t)
 #pragma unroll
@@ -584,7 +609,7 @@ hipError_t outer(const OuterArgs& a0, hipStream_t st) {
     p.first = blocks;
     blocks += ((p.N + 63) / 64) * p.nbk;
   }
-  GCK((outer_kernel<<<(blocks + 3) / 4, 256, 0, st>>>(a)));
+  GCK((outer_kernel<<<blocks, kOW * 64, 0, st>>>(a)));
   return hipSuccess;
 }
 

@@ -138,6 +138,13 @@ for step in "$@"; do
       run abloop 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config loop --steps 20 --warmup 3 --no-cpu-baseline" base= res0=PGP_GAN_RESERVED_CUS=0 res32=PGP_GAN_RESERVED_CUS=32 one=PGP_BENCH_ONE_STREAM=1
       grep median $OUT/abloop.out
       ;;
+    profloop)
+      run prof_loop 240 rocprofv3 --kernel-trace --stats -d $OUT/prof_loop -o loop --output-format csv -- python3 bench.py --config loop --steps 20 --warmup 3 --no-cpu-baseline
+      PGP_BENCH_ONE_STREAM=1 run prof_loop1 240 rocprofv3 --kernel-trace --stats -d $OUT/prof_loop1 -o loop --output-format csv -- python3 bench.py --config loop --steps 20 --warmup 3 --no-cpu-baseline
+      ;;
+    loop)
+      run loop 300 python3 -u bench.py --config loop --steps 20 --warmup 3
+      ;;
     others)
       run fpe 300 python3 -u bench.py --config fpe --steps 100 --warmup 5
       run plugin 300 python3 -u bench.py --config plugin --steps 50 --warmup 5
