@@ -145,6 +145,19 @@ for step in "$@"; do
     loop)
       run loop 300 python3 -u bench.py --config loop --steps 20 --warmup 3
       ;;
+    abgraph)
+      run abg16 600 python3 -u tools/ab_bench.py --rounds 4 --args "--config tune --hosts 16 --steps 100 --warmup 10 --no-cpu-baseline" eager= graph=PGP_BENCH_GRAPH=1
+      grep median $OUT/abg16.out
+      run abg50 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" eager= graph=PGP_BENCH_GRAPH=1
+      grep median $OUT/abg50.out
+      ;;
+    gobi)
+      run tgobi 300 python3 -u -m pytest tests/test_gpu_gobi.py -x -v --timeout 120 --timeout-method thread -m gpu
+      run gobi1 120 python3 -u bench.py --config gobi --steps 50 --warmup 5 --no-cpu-baseline
+      run gobi2 120 python3 -u bench.py --config gobi --steps 50 --warmup 5 --no-cpu-baseline
+      run loopg 300 python3 -u bench.py --config loop --steps 20 --warmup 3 --no-cpu-baseline
+      grep -h -o '"ms_per_step": [0-9.]*\|"mean_iterations": [0-9.]*' $OUT/gobi1.out $OUT/gobi2.out $OUT/loopg.out
+      ;;
     others)
       run fpe 300 python3 -u bench.py --config fpe --steps 100 --warmup 5
       run plugin 300 python3 -u bench.py --config plugin --steps 50 --warmup 5
