@@ -27,6 +27,8 @@
 // fixed order by the tuning step's deferred reduction: deterministic.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "pgp_device.hpp"
 #include "pgp_gemm.hpp"
 #include "pgp_train.hpp"
@@ -1254,10 +1256,24 @@ long tf_slab_floats(int H, int kind) {
 // few CUs reserved the two streams stop blocking each other
 std::atomic<int> g_tf_reserve{0};
 
+// The launch takes the FEWEST workgroups that keep its longest wave as short
+// as on the whole budget: units are whole 16-pair tiles, so the kernel lasts
+// max-units-per-wave unit rounds, and at H = 50 (3,200 units, 248 workgroups x
+// 4 waves) a quarter of the waves carry 4 units and the rest 3 -- 200
+// workgroups of 4-unit waves finish in the same 4 rounds and leave 56 CUs to
+// the GAN stream and the side work instead of sharing CUs with them.
+// PGP_TF_SPREAD=1 restores the spread over the whole budget (A/B).
 int tf_grid_for(long nu, int waves) {
   const int cus = device_cus();
   const int r = std::max(0, std::min(g_tf_reserve.load(std::memory_order_relaxed), cus / 2));
-  return (int)std::max<long>(1, std::min<long>(cus - r, (nu + waves - 1) / waves));
+  const long gmax = std::max<long>(1, std::min<long>(cus - r, (nu + waves - 1) / waves));
+  static const bool spread = [] {
+    const char* e = std::getenv("PGP_TF_SPREAD");
+    return e && e[0] == '1';
+  }();
+  if (spread) return (int)gmax;
+  const long m = (nu + waves * gmax - 1) / (waves * gmax);  // units of the longest wave
+  return (int)std::max<long>(1, (nu + waves * m - 1) / (waves * m));
 }
 
 int tf_max_grid() { return device_cus(); }

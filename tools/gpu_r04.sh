@@ -158,6 +158,15 @@ for step in "$@"; do
       run loopg 300 python3 -u bench.py --config loop --steps 20 --warmup 3 --no-cpu-baseline
       grep -h -o '"ms_per_step": [0-9.]*\|"mean_iterations": [0-9.]*' $OUT/gobi1.out $OUT/gobi2.out $OUT/loopg.out
       ;;
+    abspread)
+      run tbal 600 python3 -u -m pytest tests/test_gpu_c3step.py tests/test_gpu_tunedp.py tests/test_gpu_train.py -x -q --timeout 120 --timeout-method thread -m gpu
+      run abs50 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" balanced= spread=PGP_TF_SPREAD=1
+      grep median $OUT/abs50.out
+      run abs16 600 python3 -u tools/ab_bench.py --rounds 4 --args "--config tune --hosts 16 --steps 100 --warmup 10 --no-cpu-baseline" balanced= spread=PGP_TF_SPREAD=1
+      grep median $OUT/abs16.out
+      run absloop 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config loop --steps 20 --warmup 3 --no-cpu-baseline" balanced= spread=PGP_TF_SPREAD=1
+      grep median $OUT/absloop.out
+      ;;
     others)
       run fpe 300 python3 -u bench.py --config fpe --steps 100 --warmup 5
       run plugin 300 python3 -u bench.py --config plugin --steps 50 --warmup 5
