@@ -1085,6 +1085,17 @@ hipError_t tune_bwd_h(const TunePlan& p, const float* P, float* Gd, float* ws, c
   const hipStream_t sd = fk.side;
   TCK((tune_loss_kernel<<<(int)(((long)B * H + 255) / 256), 256, 0, st>>>(B, H, Q::NOP, logits, protos, y, mult,
                                                                            tgt, ws + p.dpre)));
+  // Side work issued as soon as its inputs exist: the decoders' weight
+  // gradient right here (bit 2), layer 1's in_proj weight gradient right after
+  // layer 1's attention backward (bit 1).  They run beside the fused launches
+  // on the CUs those leave free (tf_grid_for takes the fewest workgroups with
+  // the same longest wave): C3 at H = 50 1.171 -> 1.131 ms
+  // (profiles/r04/side_early/).  PGP_TUNE_SIDE_EARLY=0 issues both after the
+  // encoder backward (A/B).
+  static const int early = [] {
+    const char* v = getenv("PGP_TUNE_SIDE_EARLY");
+    return v ? atoi(v) : 3;
+  }();
   // side work: the decoders' weight gradients (dpre, encoder output -> G)
   // and each layer's in_proj weight gradient (dQKV [M][3][DP] (x) X -> three
   // [H][H] blocks of L_IN + bias); nothing on the critical path reads them
@@ -1110,6 +1121,10 @@ hipError_t tune_bwd_h(const TunePlan& p, const float* P, float* Gd, float* ws, c
     return hipSuccess;
   };
 
+  if (early & 2) {
+    if ((e = fk.fork()) != hipSuccess) return e;
+    if ((e = side_dec()) != hipSuccess) return e;
+  }
   // grad of the encoder output = dpre . Wp (token layout, pgp_dec.hip)
   if ((e = launch_dec_dx(H, B, ws + p.dpre, ws + p.wpt, ws + p.da, st)) != hipSuccess) return e;
   // the encoder layers, fused per unit (pgp_tunef.hip); their weight-gradient
@@ -1155,15 +1170,19 @@ hipError_t tune_bwd_h(const TunePlan& p, const float* P, float* Gd, float* ws, c
     if (!rb.add(ng, tf_slab_floats(H, 3), ws + p.tfs[l][1], H, H, H, Lg + G::L_OUT, H, H, (long)H * H,
                 Lg + G::L_OUTB))
       return hipErrorInvalidValue;
+    if (l == 1 && (early & 1)) {
+      if ((e = fk.fork()) != hipSuccess) return e;
+      if ((e = in_proj_dw(1, sd)) != hipSuccess) return e;
+    }
   }
-  // side, beside the serial tail below (time encoder, GAT): weight gradients
-  // nothing on the critical path reads — the decoders' and layer 1's in_proj.
-  // (Beside the fused launches they only slowed them: those take whole CUs,
-  // and a long side workgroup on a CU delays the next fused launch's
-  // workgroup there; measured again in round 3, profiles/r03/s3/side_ab.txt.)
+  // side, beside the serial tail below (time encoder, GAT), unless issued
+  // early: weight gradients nothing on the critical path reads — the
+  // decoders' and layer 1's in_proj.  (While the fused launches spread over
+  // every CU, side work beside them only slowed them: a long side workgroup on
+  // a CU delays the next fused launch's workgroup there; profiles/r03/s3/.)
   if ((e = fk.fork()) != hipSuccess) return e;
-  if ((e = side_dec()) != hipSuccess) return e;
-  if ((e = in_proj_dw(1, sd)) != hipSuccess) return e;
+  if (!(early & 2) && (e = side_dec()) != hipSuccess) return e;
+  if (!(early & 1) && (e = in_proj_dw(1, sd)) != hipSuccess) return e;
   // time encoder: p.da = grad of X0 (weight gradient: dX0 (x) G)
   if ((e = dw<DP, DP>(p, rb, ws + p.da, DP, ws + p.g, DP, 0, H, H, Gd + G::W_TE, Gd + G::B_TE, st)) != hipSuccess)
     return e;

@@ -167,6 +167,19 @@ for step in "$@"; do
       run absloop 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config loop --steps 20 --warmup 3 --no-cpu-baseline" balanced= spread=PGP_TF_SPREAD=1
       grep median $OUT/absloop.out
       ;;
+    abearly)
+      PGP_TUNE_SIDE_EARLY=3 run tearly 600 python3 -u -m pytest tests/test_gpu_c3step.py tests/test_gpu_tunedp.py -x -q --timeout 120 --timeout-method thread -m gpu
+      run abe50 900 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" base= e1=PGP_TUNE_SIDE_EARLY=1 e2=PGP_TUNE_SIDE_EARLY=2 e3=PGP_TUNE_SIDE_EARLY=3
+      grep median $OUT/abe50.out
+      ;;
+    abres)
+      run abr16 600 python3 -u tools/ab_bench.py --rounds 4 --args "--config tune --hosts 16 --steps 100 --warmup 10 --no-cpu-baseline" r8= r0=PGP_GAN_RESERVED_CUS=0
+      grep median $OUT/abr16.out
+      run abr50 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" r8= r0=PGP_GAN_RESERVED_CUS=0
+      grep median $OUT/abr50.out
+      run abrloop 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config loop --steps 20 --warmup 3 --no-cpu-baseline" r8= r0=PGP_GAN_RESERVED_CUS=0
+      grep median $OUT/abrloop.out
+      ;;
     others)
       run fpe 300 python3 -u bench.py --config fpe --steps 100 --warmup 5
       run plugin 300 python3 -u bench.py --config plugin --steps 50 --warmup 5
