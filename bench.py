@@ -324,16 +324,19 @@ _HOST_ISSUE_S = None
 
 
 GAN_RESERVED_CUS = int(os.environ.get("PGP_GAN_RESERVED_CUS", "8"))   # CUs the fused tuning launches leave to
-# the GAN step beside them (pgp_tune_reserve_cus); the variable is for A/B runs
+# the GAN step beside them (pgp_tune_reserve_cus); the variable is for A/B runs.
+# The online loop (H = 16 cells, GOBI beside) measured better with none
+# (1.616 -> 1.599 ms, profiles/r04/reserve_ab/); C3 keeps 8 (H = 16: 0.290 -> 0.273 ms)
+LOOP_RESERVED_CUS = int(os.environ.get("PGP_LOOP_RESERVED_CUS", "0"))
 
 
-def _reserve_cus(main, side):
+def _reserve_cus(main, side, count=None):
     """With the GAN step on a second stream beside the tuning step, the fused
     tuning launches leave GAN_RESERVED_CUS CUs to it: they hold whole CUs and
     deal their units statically, so a CU taken by a GAN workgroup would hold
     back the whole launch (and the GAN workgroups would wait for CUs the fused
     launches hold).  Returns the count set."""
-    n = GAN_RESERVED_CUS if side is not main else 0
+    n = (GAN_RESERVED_CUS if count is None else count) if side is not main else 0
     L = _native.lib()
     L.pgp_tune_reserve_cus.argtypes = [ctypes.c_int]
     L.pgp_tune_reserve_cus.restype = ctypes.c_int
@@ -973,7 +976,7 @@ def bench_loop(args):
     main = torch.cuda.current_stream(device)
     side = main if os.environ.get("PGP_BENCH_ONE_STREAM") == "1" else torch.cuda.Stream(device)
     shared_side = _share_side_stream(world, main, side)   # see bench_tune
-    _reserve_cus(main, side)
+    _reserve_cus(main, side, LOOP_RESERVED_CUS)
 
     def interval(timed=False):
         if timed:

@@ -1090,11 +1090,13 @@ hipError_t tune_bwd_h(const TunePlan& p, const float* P, float* Gd, float* ws, c
   // layer 1's attention backward (bit 1).  They run beside the fused launches
   // on the CUs those leave free (tf_grid_for takes the fewest workgroups with
   // the same longest wave): C3 at H = 50 1.171 -> 1.131 ms
-  // (profiles/r04/side_early/).  PGP_TUNE_SIDE_EARLY=0 issues both after the
-  // encoder backward (A/B).
+  // (profiles/r04/side_early/).  Bit 4: layer 0's in_proj weight gradient on
+  // the side stream beside the time encoder / GAT tail, 1.137 -> 1.126 ms;
+  // bit 8 (the time encoder's too) measured neutral.  PGP_TUNE_SIDE_EARLY=0
+  // is round 3's placement (A/B).
   static const int early = [] {
     const char* v = getenv("PGP_TUNE_SIDE_EARLY");
-    return v ? atoi(v) : 3;
+    return v ? atoi(v) : 7;
   }();
   // side work: the decoders' weight gradients (dpre, encoder output -> G)
   // and each layer's in_proj weight gradient (dQKV [M][3][DP] (x) X -> three
@@ -1183,8 +1185,12 @@ hipError_t tune_bwd_h(const TunePlan& p, const float* P, float* Gd, float* ws, c
   if ((e = fk.fork()) != hipSuccess) return e;
   if (!(early & 2) && (e = side_dec()) != hipSuccess) return e;
   if (!(early & 1) && (e = in_proj_dw(1, sd)) != hipSuccess) return e;
+  // bits 4 / 8: layer 0's in_proj and the time encoder's weight gradients on
+  // the side stream too
+  if ((early & 4) && (e = in_proj_dw(0, sd)) != hipSuccess) return e;
   // time encoder: p.da = grad of X0 (weight gradient: dX0 (x) G)
-  if ((e = dw<DP, DP>(p, rb, ws + p.da, DP, ws + p.g, DP, 0, H, H, Gd + G::W_TE, Gd + G::B_TE, st)) != hipSuccess)
+  if ((e = dw<DP, DP>(p, rb, ws + p.da, DP, ws + p.g, DP, 0, H, H, Gd + G::W_TE, Gd + G::B_TE,
+                      (early & 8) ? sd : st)) != hipSuccess)
     return e;
   // GAT, straight from dX0 (the time encoder's input gradient folded in,
   // gat_bwd_kernel); the fc gradient's aggregation part: fcd = dX0 (x) x-bar
@@ -1193,9 +1199,8 @@ hipError_t tune_bwd_h(const TunePlan& p, const float* P, float* Gd, float* ws, c
                                                   ws + p.fcd)));
   if ((e = dw<DP, Q::XBP>(p, rb, ws + p.da, DP, ws + p.xb, Q::XBP, 0, H, 3, ws + p.fcd, nullptr, st)) != hipSuccess)
     return e;
-  // layer 0's in_proj weight gradient closes the main stream's share (the two
-  // streams' tails are then about equal: kernel trace, profiles/r03/s3/)
-  if ((e = in_proj_dw(0, st)) != hipSuccess) return e;
+  // without bit 4, layer 0's in_proj weight gradient closes the main stream's share
+  if (!(early & 4) && (e = in_proj_dw(0, st)) != hipSuccess) return e;
   if ((e = fk.join()) != hipSuccess) return e;  // the side stream's partials and G writes
   if ((e = rb.flush(st)) != hipSuccess) return e;  // every deferred weight-gradient reduction: 2 launches
   TCK((gat_param_kernel<H><<<1, 256, 0, st>>>(gat_wg, ws + p.gsx, P, ws + p.fcd, Gd)));

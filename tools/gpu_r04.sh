@@ -180,6 +180,11 @@ for step in "$@"; do
       run abrloop 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config loop --steps 20 --warmup 3 --no-cpu-baseline" r8= r0=PGP_GAN_RESERVED_CUS=0
       grep median $OUT/abrloop.out
       ;;
+    abside2)
+      PGP_TUNE_SIDE_EARLY=15 run tside2 600 python3 -u -m pytest tests/test_gpu_c3step.py tests/test_gpu_tunedp.py -x -q --timeout 120 --timeout-method thread -m gpu
+      run abe2 900 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" e3= e7=PGP_TUNE_SIDE_EARLY=7 e11=PGP_TUNE_SIDE_EARLY=11 e15=PGP_TUNE_SIDE_EARLY=15
+      grep median $OUT/abe2.out
+      ;;
     others)
       run fpe 300 python3 -u bench.py --config fpe --steps 100 --warmup 5
       run plugin 300 python3 -u bench.py --config plugin --steps 50 --warmup 5
