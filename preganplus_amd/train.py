@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 
 import types
 
@@ -30,6 +31,11 @@ PROTO_UPDATE_MIN = 0.02     # constants.py:14
 PROTO_FACTOR_DECAY = 0.995  # constants.py:15
 LATEST_WINDOW_SIZE = 10     # constants.py:16
 PERCENTILES = 98            # constants.py:11
+
+
+# the current stream's raw handle by device index (torch's C++ accessor; None
+# if this torch lacks it, then Trainer._stream takes the public API)
+_RAW_STREAM = getattr(torch._C, "_cuda_getCurrentRawStream", None)
 
 
 class _AdamTensor(ctypes.Structure):
@@ -59,6 +65,7 @@ class Trainer:
         L = _native.lib()
         self._L = L
         self._bind()
+        self._desc_cache = {}
         n = L.pgp_master_len(self.H)
         if n == 0:
             raise ValueError(f"H={H} not compiled in")
@@ -162,11 +169,39 @@ class Trainer:
             self._alloc(B)
 
     def _dev(self, a, dtype):
+        if torch.is_tensor(a) and a.dtype == dtype and a.device == self.device and a.is_contiguous():
+            return a   # already in place: no dispatcher round trip (host issue time, C3 at H = 16)
         t = a if torch.is_tensor(a) else torch.as_tensor(np.asarray(a))
         return t.to(self.device, dtype).contiguous()
 
     def _stream(self):
+        # the current stream's raw handle straight from the C++ side:
+        # torch.cuda.current_stream(device) costs ~4 us of argument parsing, and
+        # a C3 step asks ~20 times (cProfile, profiles/r04/host_issue/)
+        idx = self.device.index
+        if idx is not None and _RAW_STREAM is not None:
+            return ctypes.c_void_p(_RAW_STREAM(idx))
         return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def trainable(self, section: str) -> list:
+        """The section's trainable tensor records (one list object per section,
+        so its AdamW descriptor is built once)."""
+        c = self._desc_cache.get(("sel", section))
+        if c is None:
+            c = [t for t in self.tensors if t["section"] == section and t["trainable"]]
+            self._desc_cache[("sel", section)] = c
+        return c
+
+    def _adam_desc(self, sel):
+        """ctypes descriptor array of an AdamW selection, built once per list
+        object (the selections are fixed lists held by their callers, or
+        ``trainable(section)``; the cache keeps each list alive, so no id is
+        reused)."""
+        c = self._desc_cache.get(id(sel))
+        if c is None or c[0] is not sel:
+            c = (sel, (_AdamTensor * len(sel))(*[_AdamTensor(t["offset"], t["n"], 1, 0.0, 0.0) for t in sel]))
+            self._desc_cache[id(sel)] = c
+        return c[1]
 
     # ---------------- ops ----------------
     def zero_grad(self, section: str):
@@ -396,7 +431,7 @@ class Trainer:
     def adam_step_table(self, section: str, sel, sched):
         """AdamW over `sel` with the per-step scalars in the device row `sched`
         [T,3] (``pgp_adamw_table``): fixed kernel arguments, graph-capturable."""
-        desc = (_AdamTensor * len(sel))(*[_AdamTensor(t["offset"], t["n"], 1, 0.0, 0.0) for t in sel])
+        desc = self._adam_desc(sel)
         _native.check(self._L.pgp_adamw_table(
             ctypes.c_void_p(self.P.data_ptr()), ctypes.c_void_p(self.G.data_ptr()),
             ctypes.c_void_p(self.m.data_ptr()), ctypes.c_void_p(self.v.data_ptr()),
@@ -683,7 +718,7 @@ class DPTuner:
         return out
 
     def step(self, wins: torch.Tensor, y: torch.Tensor, cls: torch.Tensor, mark=None, before_update=None,
-             after_forward=None, before_backward=None, row: torch.Tensor | None = None):
+             after_forward=None, before_backward=None, row: torch.Tensor | None = None, after_backward=None):
         """wins [B',3,3H] fp32, y / cls [B,H] int32, all on the device, B <= B':
         the forward runs over all B' windows and the step trains on the first
         B (windows B.. are inference windows sharing the forward, e.g. C3's
@@ -702,7 +737,9 @@ class DPTuner:
         that should queue behind the forward's launches but ahead of the
         backward's); ``before_backward``, if given, once the targets are issued,
         right before the backward (work for another stream that should start
-        with the backward: the caller makes its stream wait for this one)."""
+        with the backward: the caller makes its stream wait for this one);
+        ``after_backward``, if given, once the backward is issued (the same,
+        issued after the backward's launches)."""
         mark = mark or (lambda k: None)
         import torch.distributed as dist
         tr, L = self.tr, self.tr._L
@@ -727,6 +764,8 @@ class DPTuner:
         if before_backward is not None:
             before_backward()
         tr.tune_backward(B, y, self.mult[:B], self.tgt[:B])
+        if after_backward is not None:
+            after_backward()
         mark(3)
         tr.all_reduce_grads("transformer", self.group)
         if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
@@ -1256,15 +1295,20 @@ def train_gan_batched(tr: Trainer, sim, envs, emb, sched, out=None, target=None,
     if rows is None:
         tr.adam_step("disc")
     else:
-        tr.adam_step_table("disc", [t for t in tr.tensors if t["section"] == "disc" and t["trainable"]], rows[0])
+        tr.adam_step_table("disc", tr.trainable("disc"), rows[0])
     tr.gan_gen_backward(ns.shape[0])
     if all_reduce:
         tr.all_reduce_grads("gen", group)
     if rows is None:
         tr.adam_step("gen")
     else:
-        tr.adam_step_table("gen", [t for t in tr.tensors if t["section"] == "gen" and t["trainable"]], rows[1])
+        tr.adam_step_table("gen", tr.trainable("gen"), rows[1])
     return out, target
+
+# C3 issue order (A/B): the GAN step's launches after the tuning backward's
+# instead of before them (PGP_C3_GAN_LATE=1)
+_GAN_AFTER_BACKWARD = os.environ.get("PGP_C3_GAN_LATE", "0") == "1"
+
 
 class OnlineTrainStep:
     """run_model's semi-supervised training (PreGANPlus.py:115-136, all but the
@@ -1311,6 +1355,7 @@ class OnlineTrainStep:
         self.rowD, self.rowG = self.rows_d.buffer(), self.rows_g.buffer()
         self._rows = (self.rowT, self.rowD, self.rowG)
         self.graph = None
+        self._gate = torch.cuda.Event()   # the targets are issued: the GAN stream may start
 
     def prep(self):
         """Host bookkeeping of the next step (AdamW rows).  Eager steps read
@@ -1332,8 +1377,10 @@ class OnlineTrainStep:
         _, y, cls, _ = tune_dataset(tr, self.series, self.tmax, out=self.bufs)
         rec(1)
 
+        gate = self._gate
+
         def detect_gan():   # once the targets are issued: beside the tuning backward
-            side.wait_stream(main)
+            side.wait_event(gate)
             with torch.cuda.stream(side):
                 if stage is not None:
                     stage[5].record(side)
@@ -1346,8 +1393,16 @@ class OnlineTrainStep:
                 if stage is not None:
                     stage[3].record(side)
 
+        late = _GAN_AFTER_BACKWARD
+
+        def targets_issued():
+            gate.record(main)
+            if not late:
+                detect_gan()
+
         self.tun.step(self.bufs[4], y, cls, mark=(lambda k: sub[k].record(main)) if sub is not None else None,
-                      before_backward=detect_gan, row=self._rows[0])
+                      before_backward=targets_issued, after_backward=detect_gan if late else None,
+                      row=self._rows[0])
         main.wait_stream(side)
         rec(4)
 

@@ -185,6 +185,29 @@ for step in "$@"; do
       run abe2 900 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" e3= e7=PGP_TUNE_SIDE_EARLY=7 e11=PGP_TUNE_SIDE_EARLY=11 e15=PGP_TUNE_SIDE_EARLY=15
       grep median $OUT/abe2.out
       ;;
+    cprof)
+      run cprof16 300 python3 -u -m cProfile -o $OUT/cprof16.pstats bench.py --config tune --hosts 16 --steps 400 --warmup 10 --no-cpu-baseline
+      python3 -c "import pstats; p=pstats.Stats('$OUT/cprof16.pstats'); p.sort_stats('tottime').print_stats(40)" > $OUT/cprof16_tottime.txt
+      python3 -c "import pstats; p=pstats.Stats('$OUT/cprof16.pstats'); p.sort_stats('cumtime').print_stats(60)" > $OUT/cprof16_cumtime.txt
+      ;;
+    host)
+      run thost 600 python3 -u -m pytest tests/test_gpu_c3step.py tests/test_gpu_tunedp.py tests/test_gpu_train.py tests/test_gpu_bench_modes.py -x -q --timeout 120 --timeout-method thread -m gpu
+      run h16a 120 python3 -u bench.py --config tune --hosts 16 --steps 200 --warmup 10 --no-cpu-baseline
+      run h16b 120 python3 -u bench.py --config tune --hosts 16 --steps 200 --warmup 10 --no-cpu-baseline
+      run h50a 120 python3 -u bench.py --config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline
+      run hloop 300 python3 -u bench.py --config loop --steps 20 --warmup 3 --no-cpu-baseline
+      grep -h -o '"ms_per_step": [0-9.]*\|"host_issue_ms_per_step": [0-9.]*' $OUT/h16a.out $OUT/h16b.out $OUT/h50a.out $OUT/hloop.out
+      ;;
+    late)
+      PGP_C3_GAN_LATE=1 run tlate 600 python3 -u -m pytest tests/test_gpu_c3step.py tests/test_gpu_bench_modes.py -x -q --timeout 120 --timeout-method thread -m gpu
+      run abl16 600 python3 -u tools/ab_bench.py --rounds 4 --args "--config tune --hosts 16 --steps 100 --warmup 10 --no-cpu-baseline" early= late=PGP_C3_GAN_LATE=1
+      grep median $OUT/abl16.out
+      run abl50 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" early= late=PGP_C3_GAN_LATE=1
+      grep median $OUT/abl50.out
+      run cprofloop 300 python3 -u -m cProfile -o $OUT/cprofloop.pstats bench.py --config loop --steps 40 --warmup 3 --no-cpu-baseline
+      python3 -c "import pstats; p=pstats.Stats('$OUT/cprofloop.pstats'); p.sort_stats('tottime').print_stats(50)" > $OUT/cprofloop_tottime.txt
+      python3 -c "import pstats; p=pstats.Stats('$OUT/cprofloop.pstats'); p.sort_stats('cumtime').print_stats('preganplus_amd|bench', 60)" > $OUT/cprofloop_cumtime.txt
+      ;;
     others)
       run fpe 300 python3 -u bench.py --config fpe --steps 100 --warmup 5
       run plugin 300 python3 -u bench.py --config plugin --steps 50 --warmup 5
