@@ -1305,9 +1305,12 @@ def train_gan_batched(tr: Trainer, sim, envs, emb, sched, out=None, target=None,
         tr.adam_step_table("gen", tr.trainable("gen"), rows[1])
     return out, target
 
-# C3 issue order (A/B): the GAN step's launches after the tuning backward's
-# instead of before them (PGP_C3_GAN_LATE=1)
-_GAN_AFTER_BACKWARD = os.environ.get("PGP_C3_GAN_LATE", "0") == "1"
+# C3 issue order: the GAN step's launches are issued after the tuning
+# backward's (its stream still starts at the targets, gated by an event), so
+# the main stream has the backward queued while the host issues the GAN step:
+# H = 16 0.274 -> 0.263 ms, H = 50 neutral (A/B, profiles/r04/issue_order/).
+# PGP_C3_GAN_LATE=0 issues them before the backward (round 4's first order).
+_GAN_AFTER_BACKWARD = os.environ.get("PGP_C3_GAN_LATE", "1") == "1"
 
 
 class OnlineTrainStep:
