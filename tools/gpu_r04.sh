@@ -208,6 +208,14 @@ for step in "$@"; do
       python3 -c "import pstats; p=pstats.Stats('$OUT/cprofloop.pstats'); p.sort_stats('tottime').print_stats(50)" > $OUT/cprofloop_tottime.txt
       python3 -c "import pstats; p=pstats.Stats('$OUT/cprofloop.pstats'); p.sort_stats('cumtime').print_stats('preganplus_amd|bench', 60)" > $OUT/cprofloop_cumtime.txt
       ;;
+    abdec)
+      run tdec 600 python3 -u -m pytest tests/test_gpu_c3step.py tests/test_gpu_tunedp.py tests/test_gpu_tune1.py tests/test_gpu_train_model.py -x -q --timeout 120 --timeout-method thread -m gpu
+      run abd50 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" new= prev=PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_prevdec.so
+      grep median $OUT/abd50.out
+      run abd16 600 python3 -u tools/ab_bench.py --rounds 4 --args "--config tune --hosts 16 --steps 100 --warmup 10 --no-cpu-baseline" new= prev=PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_prevdec.so
+      grep median $OUT/abd16.out
+      run prof_dec 240 rocprofv3 --kernel-trace --stats -d $OUT/prof_dec -o tune --output-format csv -- python3 bench.py --config tune --hosts 50 --steps 30 --warmup 5 --no-cpu-baseline
+      ;;
     others)
       run fpe 300 python3 -u bench.py --config fpe --steps 100 --warmup 5
       run plugin 300 python3 -u bench.py --config plugin --steps 50 --warmup 5
