@@ -1006,7 +1006,11 @@ struct Fork {
       const char* v = getenv("PGP_TUNE_SIDE_STREAM");
       return v && v[0] == '0';
     }();
-    if (off || tokens < kSideMinTokens) return;  // PGP_TUNE_SIDE_STREAM=0: everything on the caller's stream
+    static const long min_tokens = [] {  // PGP_TUNE_SIDE_MIN_TOKENS: A/B of the threshold
+      const char* v = getenv("PGP_TUNE_SIDE_MIN_TOKENS");
+      return v ? atol(v) : kSideMinTokens;
+    }();
+    if (off || tokens < min_tokens) return;  // PGP_TUNE_SIDE_STREAM=0: everything on the caller's stream
     // while `st` is being captured into a graph the fork / join events become
     // the graph's edges: the side stream joins the capture at the fork's wait
     // and leaves it at the join, so the graph keeps the two branches (a

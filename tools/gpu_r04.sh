@@ -216,6 +216,17 @@ for step in "$@"; do
       grep median $OUT/abd16.out
       run prof_dec 240 rocprofv3 --kernel-trace --stats -d $OUT/prof_dec -o tune --output-format csv -- python3 bench.py --config tune --hosts 50 --steps 30 --warmup 5 --no-cpu-baseline
       ;;
+    abzero)
+      run tzero 600 python3 -u -m pytest tests/test_gpu_c3step.py tests/test_gpu_bench_modes.py tests/test_gpu_dist.py -x -q --timeout 120 --timeout-method thread -m gpu
+      run abz16 600 python3 -u tools/ab_bench.py --rounds 4 --args "--config tune --hosts 16 --steps 100 --warmup 10 --no-cpu-baseline" zside= zmain=PGP_C3_ZERO_SIDE=0
+      grep median $OUT/abz16.out
+      run abz50 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" zside= zmain=PGP_C3_ZERO_SIDE=0
+      grep median $OUT/abz50.out
+      ;;
+    abmin)
+      run abm16 600 python3 -u tools/ab_bench.py --rounds 4 --args "--config tune --hosts 16 --steps 100 --warmup 10 --no-cpu-baseline" nofork= fork=PGP_TUNE_SIDE_MIN_TOKENS=1
+      grep median $OUT/abm16.out
+      ;;
     others)
       run fpe 300 python3 -u bench.py --config fpe --steps 100 --warmup 5
       run plugin 300 python3 -u bench.py --config plugin --steps 50 --warmup 5
