@@ -917,7 +917,11 @@ bool plan_h(int B, TunePlan* out) {
   long part = (long)kDwCap * (np_max * 64 + np_max);                  // dW slabs
   part = std::max(part, (long)q.dec_s * B * Q::NOP);                    // decoder split-K
   // decoder weight gradient: windows split over up to 4 parts of >= 8 chunks
-  q.dec_dws = (int)std::max<long>(1, std::min<long>(4, (B + kDwRows - 1) / kDwRows / 8));
+  static const long dws_max = [] {  // PGP_TUNE_DEC_DWS: A/B of the part count
+    const char* v = getenv("PGP_TUNE_DEC_DWS");
+    return v ? std::max(1L, atol(v)) : 4L;
+  }();
+  q.dec_dws = (int)std::max<long>(1, std::min<long>(dws_max, (B + kDwRows - 1) / kDwRows / 8));
   if (q.dec_dws > 1) part = std::max(part, (long)q.dec_dws * (Q::T * Q::NOP * Q::DP + Q::NOP));
   q.part = take(part);
   // the backward's deferred reductions (RedBatch): each dW partial region plus

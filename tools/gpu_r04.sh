@@ -227,6 +227,11 @@ for step in "$@"; do
       run abm16 600 python3 -u tools/ab_bench.py --rounds 4 --args "--config tune --hosts 16 --steps 100 --warmup 10 --no-cpu-baseline" nofork= fork=PGP_TUNE_SIDE_MIN_TOKENS=1
       grep median $OUT/abm16.out
       ;;
+    abdws)
+      PGP_TUNE_DEC_DWS=1 run tdws 600 python3 -u -m pytest tests/test_gpu_c3step.py tests/test_gpu_tunedp.py -x -q --timeout 120 --timeout-method thread -m gpu
+      run abdws50 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" p4= p2=PGP_TUNE_DEC_DWS=2 p1=PGP_TUNE_DEC_DWS=1
+      grep median $OUT/abdws50.out
+      ;;
     others)
       run fpe 300 python3 -u bench.py --config fpe --steps 100 --warmup 5
       run plugin 300 python3 -u bench.py --config plugin --steps 50 --warmup 5
