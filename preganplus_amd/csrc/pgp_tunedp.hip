@@ -39,6 +39,9 @@ namespace pgp {
 namespace {
 
 constexpr int kWin = 3;  // models.py:320 n_window
+// state apply lane map: prototypes 0..K-1 (K <= kMaxProtos = 64), the counters /
+// factor on thread 64, the conditional AdamW rows' lanes from thread 66 (wave 1)
+constexpr int kStateCountLane = 64, kStateCondLane0 = 66, kStateThreads = 128;
 
 // ---------------------------------------------------------------------------
 // dataset: one thread per (environment, host, column): wave c of a 3-wave
@@ -269,29 +272,43 @@ __global__ __launch_bounds__(kTB) void tune_dp_finish_kernel(int H, int B, int K
   }
 }
 
+// One lane per independent value (K prototypes, the counters / factor, and
+// each conditional AdamW row's two bias corrections), each computed exactly as
+// the single-thread version did: the fp64 pow calls run side by side instead
+// of one after another (13 -> a few us on the C3 step's critical path).
+// A row's two lanes are in one wave: its step count is read by both before
+// the even lane writes it back.
 __global__ void tune_state_apply_kernel(int K, double* __restrict__ state, const double* __restrict__ inc, double decay,
                                         CondRows cr, double* __restrict__ dsteps, float* __restrict__ table, double lr,
                                         double b1, double b2) {
 #pragma clang fp contract(off)
-  if (threadIdx.x != 0) return;
-  for (int c = 0; c < K; ++c) {
-    const double n = inc[2 * K + c];
-    if (n > 0) {
-      state[2 * c] += inc[2 * c] / n;
-      state[2 * c + 1] += inc[2 * c + 1] / n;
-    }
-  }
-  state[2 * K + 1] += inc[3 * K];
-  state[2 * K + 2] += inc[3 * K + 1];
-  state[2 * K] *= pow(decay, inc[3 * K + 2]);
+  const int t = threadIdx.x;
   const bool active = inc[3 * K + 1] > 0;  // a positive label somewhere in the global batch
-  for (int i = 0; i < cr.n; ++i) {
-    if (active) dsteps[i] += 1.0;
-    const double s = dsteps[i] > 1.0 ? dsteps[i] : 1.0;
+  if (t < K) {
+    const double n = inc[2 * K + t];
+    if (n > 0) {
+      state[2 * t] += inc[2 * t] / n;
+      state[2 * t + 1] += inc[2 * t + 1] / n;
+    }
+  } else if (t == kStateCountLane) {
+    state[2 * K + 1] += inc[3 * K];
+    state[2 * K + 2] += inc[3 * K + 1];
+    state[2 * K] *= pow(decay, inc[3 * K + 2]);
+  }
+  const int u = t - kStateCondLane0;  // threads kStateCondLane0.. : row u / 2, bias correction u % 2
+  if (u >= 0 && u < 2 * cr.n) {
+    const int i = u >> 1;
+    const double ds = active ? dsteps[i] + 1.0 : dsteps[i];
+    const double s = ds > 1.0 ? ds : 1.0;
     float* r = table + 3 * cr.row[i];
-    r[0] = active ? 1.f : 0.f;
-    r[1] = (float)(lr / (1.0 - pow(b1, s)));
-    r[2] = (float)sqrt(1.0 - pow(b2, s));
+    if ((u & 1) == 0) {
+      r[0] = active ? 1.f : 0.f;
+      r[1] = (float)(lr / (1.0 - pow(b1, s)));
+    } else {
+      r[2] = (float)sqrt(1.0 - pow(b2, s));
+    }
+    __builtin_amdgcn_wave_barrier();
+    if ((u & 1) == 0) dsteps[i] = ds;
   }
 }
 
@@ -320,7 +337,11 @@ hipError_t launch_tune_targets_dp(int H, int K, int B, const float* logits, cons
 
 hipError_t launch_tune_state_apply(int K, double* state, const double* inc, double decay, const CondRows& cr,
                                    double* dsteps, float* table, double lr, double b1, double b2, hipStream_t st) {
-  tune_state_apply_kernel<<<1, 64, 0, st>>>(K, state, inc, decay, cr, dsteps, table, lr, b1, b2);
+  static_assert(kMaxProtos <= kStateCountLane && kStateCondLane0 + 2 * kMaxCond <= kStateThreads &&
+                    kStateCondLane0 / 64 == (kStateCondLane0 + 2 * kMaxCond - 1) / 64,
+                "state apply lane map (a row's two lanes in one wave)");
+  if (K < 0 || K > kMaxProtos || cr.n < 0 || cr.n > kMaxCond) return hipErrorInvalidValue;
+  tune_state_apply_kernel<<<1, kStateThreads, 0, st>>>(K, state, inc, decay, cr, dsteps, table, lr, b1, b2);
   return hipGetLastError();
 }
 

@@ -232,6 +232,13 @@ for step in "$@"; do
       run abdws50 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" p4= p2=PGP_TUNE_DEC_DWS=2 p1=PGP_TUNE_DEC_DWS=1
       grep median $OUT/abdws50.out
       ;;
+    state)
+      run tstate 600 python3 -u -m pytest tests/test_gpu_tunedp.py tests/test_gpu_c3step.py tests/test_gpu_train.py tests/test_gpu_dist.py tests/test_gpu_plugin_graphs.py -x -q --timeout 120 --timeout-method thread -m gpu
+      run st50 120 python3 -u bench.py --config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline
+      run st16 120 python3 -u bench.py --config tune --hosts 16 --steps 100 --warmup 10 --no-cpu-baseline
+      run prof_st 240 rocprofv3 --kernel-trace --stats -d $OUT/prof_st -o tune --output-format csv -- python3 bench.py --config tune --hosts 50 --steps 30 --warmup 5 --no-cpu-baseline
+      grep -h -o '"ms_per_step": [0-9.]*' $OUT/st50.out $OUT/st16.out
+      ;;
     others)
       run fpe 300 python3 -u bench.py --config fpe --steps 100 --warmup 5
       run plugin 300 python3 -u bench.py --config plugin --steps 50 --warmup 5
