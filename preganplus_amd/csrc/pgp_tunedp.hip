@@ -44,34 +44,36 @@ constexpr int kWin = 3;  // models.py:320 n_window
 constexpr int kStateCountLane = 64, kStateCondLane0 = 66, kStateThreads = 128;
 
 // ---------------------------------------------------------------------------
-// dataset: one thread per (environment, host, column): wave c of a 3-wave
-// workgroup holds column c of 64 (environment, host) pairs, so the per-value
-// fp64 work (the division by the column max, the rank search of the
-// percentile) runs 3 ways parallel; the labels, which need all three columns,
-// are formed by wave 0 from LDS.  (One thread per pair held 30 fp64 divisions
-// and 300 comparisons in one chain: 25 us for C3's 103 environments.)
+// dataset: one thread per (environment, host, column, row): a workgroup holds
+// kDsP (environment, host) pairs x 3 columns x kMaxTuneRows rows, lanes
+// ordered column-fastest so a row's loads are contiguous.  Each thread divides
+// its value by the column max and finds that value's stable rank among the
+// column's rows (LDS); the rows of rank ilo / ihi publish the order statistics
+// of the 98th percentile; then each thread writes its windows and the column-0
+// threads form the labels.  Every value goes through the same operations as
+// in the one-thread-per-column version (bit-identical outputs); the rows now
+// run side by side instead of in one thread's chain (C3: 81 workgroups of
+// dependent fp64 divisions and 256 comparisons per thread before).
 // ---------------------------------------------------------------------------
-constexpr int kDsPairs = 64;
-__global__ __launch_bounds__(3 * kDsPairs) void tune_dataset_kernel(int H, int E, int R,
-                                                                   const double* __restrict__ series,
-                                                                   const double* __restrict__ train_max,
-                                                                   float* __restrict__ windows, int* __restrict__ y,
-                                                                   int* __restrict__ cls, float* __restrict__ infer) {
+constexpr int kDsP = 16;                           // pairs per workgroup
+constexpr int kDsThreads = kDsP * 3 * kMaxTuneRows;  // 768
+__global__ __launch_bounds__(kDsThreads) void tune_dataset_kernel(int H, int E, int R,
+                                                                  const double* __restrict__ series,
+                                                                  const double* __restrict__ train_max,
+                                                                  float* __restrict__ windows, int* __restrict__ y,
+                                                                  int* __restrict__ cls, float* __restrict__ infer) {
 #pragma clang fp contract(off)
-  __shared__ double sv[3][kMaxTuneRows][kDsPairs], sthr[3][kDsPairs];
-  const int c = threadIdx.x / kDsPairs, q = threadIdx.x % kDsPairs;  // column (wave-uniform), pair slot
-  const long t = (long)blockIdx.x * kDsPairs + q;
+  __shared__ double sv[3][kMaxTuneRows][kDsP];  // normalised rows
+  __shared__ double sab[3][2][kDsP];            // the percentile's order statistics (ranks ilo, ihi)
+  const int c = threadIdx.x % 3, q = (threadIdx.x / 3) % kDsP, r = threadIdx.x / (3 * kDsP);
+  const long t = (long)blockIdx.x * kDsP + q;
   const bool ok = t < (long)E * H;
   const int e = ok ? (int)(t / H) : 0, h = ok ? (int)(t % H) : 0;
   const int F = 3 * H;
-  // every loop runs to kMaxTuneRows with an r < R guard, so all indices are
-  // compile-time and the rows stay in registers
-  double v[kMaxTuneRows];  // this column's normalised rows
-  {
-    const double den = train_max[3 * h + c] + 1e-8;  // np.max(train, axis=0) + 1e-8
-#pragma unroll
-    for (int r = 0; r < kMaxTuneRows; ++r) v[r] = (ok && r < R) ? series[((long)e * R + r) * F + 3 * h + c] / den : 0.0;
-  }
+  const bool live = ok && r < R;
+  const double den = train_max[3 * h + c] + 1e-8;  // np.max(train, axis=0) + 1e-8
+  const double v = live ? series[((long)e * R + r) * F + 3 * h + c] / den : 0.0;
+  sv[c][r][q] = v;
   // 98th percentile of the column, numpy 'linear': virtual index (R-1)*0.98,
   // gamma = frac, lerp(a, b, g) = g >= 0.5 ? b - (b-a)(1-g) : a + (b-a) g.
   // The order statistics ilo, ihi are found by stable rank (the element with
@@ -80,68 +82,50 @@ __global__ __launch_bounds__(3 * kDsPairs) void tune_dataset_kernel(int H, int E
   const double lo = floor(vi);
   const double gm = vi - lo;
   const int ilo = (int)lo, ihi = ilo + 1 < R ? ilo + 1 : R - 1;
-  double thr;
-  {
-    double a = 0.0, b = 0.0;
+  __syncthreads();
+  if (live) {
+    int rank = 0;
 #pragma unroll
-    for (int r = 0; r < kMaxTuneRows; ++r) {
-      int rank = 0;
-#pragma unroll
-      for (int j = 0; j < kMaxTuneRows; ++j)
-        if (j != r && j < R) rank += (v[j] < v[r] || (j < r && v[j] == v[r])) ? 1 : 0;
-      if (r < R && rank == ilo) a = v[r];
-      if (r < R && rank == ihi) b = v[r];
+    for (int j = 0; j < kMaxTuneRows; ++j) {
+      const double vj = sv[c][j][q];
+      if (j != r && j < R) rank += (vj < v || (j < r && vj == v)) ? 1 : 0;
     }
-    const double d = b - a;
-    thr = gm >= 0.5 ? b - d * (1.0 - gm) : a + d * gm;
-  }
-#pragma unroll
-  for (int r = 0; r < kMaxTuneRows; ++r) sv[c][r][q] = v[r];
-  sthr[c][q] = thr;
-  if (ok) {
-#pragma unroll
-    for (int r = 0; r < kMaxTuneRows; ++r) {
-      if (r < R) {
-        // convert_to_windows: window r = rows r-3..r-1, row 0 repeated for r < 3
-#pragma unroll
-        for (int w = 0; w < kWin; ++w) {
-          const int src = r >= kWin ? r - kWin + w : (w < kWin - r ? 0 : w - (kWin - r));
-          windows[(((long)e * R + r) * kWin + w) * F + 3 * h + c] = (float)v[src];
-        }
-      }
-    }
-    if (infer) {  // run_encoder: last 3 rows -> convert_to_windows(...)[-1] = [R-3, R-3, R-2];
-                  // a shorter series (R = 1, 2: the first intervals) keeps all its rows and
-                  // its last window is row 0 three times
-      const int ra = R >= kWin ? R - 3 : 0, rb = R >= kWin ? R - 2 : 0;
-      double u0 = 0.0, u1 = 0.0;
-#pragma unroll
-      for (int r = 0; r < kMaxTuneRows; ++r) {
-        if (r == ra) u0 = v[r];
-        if (r == rb) u1 = v[r];
-      }
-#pragma unroll
-      for (int w = 0; w < kWin; ++w) infer[((long)e * kWin + w) * F + 3 * h + c] = (float)(w < 2 ? u0 : u1);
-    }
+    if (rank == ilo) sab[c][0][q] = v;
+    if (rank == ihi) sab[c][1][q] = v;
   }
   __syncthreads();
-  if (c == 0 && ok) {  // labels: all three columns of the pair
+  auto thr_of = [&](int cc) {
+    const double a = sab[cc][0][q], b = sab[cc][1][q];
+    const double d = b - a;
+    return gm >= 0.5 ? b - d * (1.0 - gm) : a + d * gm;
+  };
+  if (!live) return;  // (no barrier below)
+  // convert_to_windows: window r = rows r-3..r-1, row 0 repeated for r < 3
 #pragma unroll
-    for (int r = 0; r < kMaxTuneRows; ++r) {
-      if (r < R) {
-        const double x0 = sv[0][r][q], x1 = sv[1][r][q], x2 = sv[2][r][q];
-        const bool an = x0 > sthr[0][q] || x1 > sthr[1][q] || x2 > sthr[2][q];
-        int am = 0;  // np.argmax: first maximum
-        double best = x0;
-        if (x1 > best) {
-          am = 1;
-          best = x1;
-        }
-        if (x2 > best) am = 2;
-        y[((long)e * R + r) * H + h] = an ? 1 : 0;
-        cls[((long)e * R + r) * H + h] = am;
-      }
+  for (int w = 0; w < kWin; ++w) {
+    const int src = r >= kWin ? r - kWin + w : (w < kWin - r ? 0 : w - (kWin - r));
+    windows[(((long)e * R + r) * kWin + w) * F + 3 * h + c] = (float)sv[c][src][q];
+  }
+  if (infer && r == 0) {  // run_encoder: last 3 rows -> convert_to_windows(...)[-1] = [R-3, R-3, R-2];
+                          // a shorter series (R = 1, 2: the first intervals) keeps all its rows and
+                          // its last window is row 0 three times
+    const int ra = R >= kWin ? R - 3 : 0, rb = R >= kWin ? R - 2 : 0;
+    const double u0 = sv[c][ra][q], u1 = sv[c][rb][q];
+#pragma unroll
+    for (int w = 0; w < kWin; ++w) infer[((long)e * kWin + w) * F + 3 * h + c] = (float)(w < 2 ? u0 : u1);
+  }
+  if (c == 0) {  // labels: all three columns of the row
+    const double x0 = sv[0][r][q], x1 = sv[1][r][q], x2 = sv[2][r][q];
+    const bool an = x0 > thr_of(0) || x1 > thr_of(1) || x2 > thr_of(2);
+    int am = 0;  // np.argmax: first maximum
+    double best = x0;
+    if (x1 > best) {
+      am = 1;
+      best = x1;
     }
+    if (x2 > best) am = 2;
+    y[((long)e * R + r) * H + h] = an ? 1 : 0;
+    cls[((long)e * R + r) * H + h] = am;
   }
 }
 
@@ -181,7 +165,10 @@ __global__ __launch_bounds__(kTB) void tune_targets_dp_kernel(int H, int B, cons
       mult[o] = (float)mu;
       const double l0 = logits[2 * o], l1 = logits[2 * o + 1];
       const double m = fmax(l0, l1);
-      s_ce[wv][lane] = (log(exp(l0 - m) + exp(l1 - m)) + m - (yi ? l1 : l0)) * mu;
+      // log(exp(l0 - m) + exp(l1 - m)): the larger logit's term is exp(0) = 1
+      // exactly, so one exp (the sum is the same either way round)
+      const double em = exp((l0 >= l1 ? l1 : l0) - m);
+      s_ce[wv][lane] = (log(1.0 + em) + m - (yi ? l1 : l0)) * mu;
       int code = -1;
       if (yi > 0) {
         const int cc = cls[o];
@@ -317,8 +304,8 @@ __global__ void tune_state_apply_kernel(int K, double* __restrict__ state, const
 hipError_t launch_tune_dataset(int H, int E, int R, const double* series, const double* train_max, float* windows,
                                int* y, int* cls, float* infer, hipStream_t st) {
   const long n = (long)E * H;
-  tune_dataset_kernel<<<(int)((n + kDsPairs - 1) / kDsPairs), 3 * kDsPairs, 0, st>>>(H, E, R, series, train_max,
-                                                                                     windows, y, cls, infer);
+  tune_dataset_kernel<<<(int)((n + kDsP - 1) / kDsP), kDsThreads, 0, st>>>(H, E, R, series, train_max, windows, y,
+                                                                           cls, infer);
   return hipGetLastError();
 }
 
