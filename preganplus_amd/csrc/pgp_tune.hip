@@ -849,6 +849,15 @@ struct RedBatch {
     if (l2.n) TCK((reduce_multi_kernel<<<gx2, 256, 0, st>>>(l2)));
     return hipSuccess;
   }
+  // reduce what is registered so far (on `st`, ordered after its partials) and
+  // start new lists; the pool regions already taken stay theirs
+  hipError_t flush_now(hipStream_t st) {
+    const hipError_t e = flush(st);
+    l1.n = l2.n = 0;
+    gx1 = gx2 = 0;
+    ny1 = 1;
+    return e;
+  }
 };
 
 // dW[N][K] (row stride K) += sum_m Y[m][n] X[m][k];  db[N] += sum_m Y[m][n]
@@ -1183,6 +1192,13 @@ hipError_t tune_bwd_h(const TunePlan& p, const float* P, float* Gd, float* ws, c
     if (l == 1 && (early & 1)) {
       if ((e = fk.fork()) != hipSuccess) return e;
       if ((e = in_proj_dw(1, sd)) != hipSuccess) return e;
+      // layer 1's reductions (its fused slabs, in_proj) on the side stream
+      // beside layer 0's backward, not in the final flush (PGP_TUNE_EARLY_FLUSH=0: A/B)
+      static const bool early_flush = [] {
+        const char* v = getenv("PGP_TUNE_EARLY_FLUSH");
+        return !(v && v[0] == '0');
+      }();
+      if (early_flush && sd != st && (e = rb.flush_now(sd)) != hipSuccess) return e;
     }
   }
   // side, beside the serial tail below (time encoder, GAT), unless issued

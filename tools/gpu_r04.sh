@@ -247,6 +247,11 @@ for step in "$@"; do
       run prof_ds16 240 rocprofv3 --kernel-trace --stats -d $OUT/prof_ds16 -o tune --output-format csv -- python3 bench.py --config tune --hosts 16 --steps 30 --warmup 5 --no-cpu-baseline
       grep -h -o '"ms_per_step": [0-9.]*' $OUT/ds50.out $OUT/ds16.out
       ;;
+    abflush)
+      run tflush 600 python3 -u -m pytest tests/test_gpu_c3step.py tests/test_gpu_tunedp.py tests/test_gpu_train.py -x -q --timeout 120 --timeout-method thread -m gpu
+      run abf50 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" early= late=PGP_TUNE_EARLY_FLUSH=0
+      grep median $OUT/abf50.out
+      ;;
     others)
       run fpe 300 python3 -u bench.py --config fpe --steps 100 --warmup 5
       run plugin 300 python3 -u bench.py --config plugin --steps 50 --warmup 5
