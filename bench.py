@@ -620,6 +620,18 @@ def bench_tune(args):
                                    for n, t, r in zip(RL.TUNE_FUSED_LAUNCHES, fused_ms, rates)},
                 "fused_total": {"ms": float(fused_ms.sum()),
                                 "frac": float(sum(flops) / (fused_ms.sum() * 1e-3) / 1e12 / RL.PEAK_FP32_TFLOPS)}}
+        try:   # the CUs each launch holds (it takes the fewest that keep its longest wave)
+            cus = torch.cuda.get_device_properties(device).multi_processor_count
+            grids = RL.tune_fused_grids(H, B, B + E, cus, reserved)
+            for (n, d), g in zip(roof["fused_launches"].items(), grids):
+                d["cus"] = int(g)
+                d["frac_of_its_cus"] = float(d["frac"] * cus / g)
+            roof["cus"] = int(grids[k])
+            roof["frac_of_its_cus"] = float(roof["frac"] * cus / grids[k])
+            roof["cus_note"] = (f"each fused launch holds one CU per workgroup; the rest ({cus} CUs in all) run "
+                                "the GAN step and the side weight gradients beside it")
+        except Exception as exc:   # reporting only: never lose the line
+            roof["cus_note"] = f"CU count unavailable: {exc}"
     if rank == 0:
         res = {
             "metric": "tuning windows/sec (semi-supervised step: dataset + detect + train_gan + DP tune_model)",

@@ -73,6 +73,26 @@ TUNE_FUSED_LAUNCHES = ("fwd layer 0", "fwd layer 1", "ffn bwd layer 1", "att bwd
                        "att bwd layer 0")
 
 
+def tf_grid(units: int, waves: int, cus: int, reserve: int = 0) -> int:
+    """Workgroups of one fused tuning launch (mirrors pgp_tunef.hip
+    tf_grid_for): the fewest workgroups whose longest wave has as many units
+    as on the whole budget (cus - reserve, reserve capped at cus / 2)."""
+    r = max(0, min(reserve, cus // 2))
+    gmax = max(1, min(cus - r, (units + waves - 1) // waves))
+    m = (units + waves * gmax - 1) // (waves * gmax)
+    return max(1, (units + waves * m - 1) // (waves * m))
+
+
+def tune_fused_grids(H: int, B: int, B_fwd: int | None, cus: int, reserve: int = 0):
+    """Workgroups (= CUs held, one per CU) of the six fused launches, in
+    TUNE_FUSED_LAUNCHES order: the forward's 8-wave workgroups over the
+    forward batch's units, the backward's 4-wave ones over the backward's."""
+    units = (B * H + 15) // 16
+    ufwd = ((B if B_fwd is None else B_fwd) * H + 15) // 16
+    gf, gb = tf_grid(ufwd, 8, cus, reserve), tf_grid(units, 4, cus, reserve)
+    return [gf, gf, gb, gb, gb, gb]
+
+
 def tune_te_mfma(H: int) -> int:
     """Time-encoder MFMAs per unit: NT output tiles x KS k-steps x 3 window steps."""
     nt = (H + 15) // 16

@@ -252,6 +252,10 @@ for step in "$@"; do
       run abf50 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" early= late=PGP_TUNE_EARLY_FLUSH=0
       grep median $OUT/abf50.out
       ;;
+    abe15)
+      run abe15 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" e7= e15=PGP_TUNE_SIDE_EARLY=15
+      grep median $OUT/abe15.out
+      ;;
     others)
       run fpe 300 python3 -u bench.py --config fpe --steps 100 --warmup 5
       run plugin 300 python3 -u bench.py --config plugin --steps 50 --warmup 5
