@@ -253,7 +253,10 @@ int pgp_tune_set_side_stream(void* stream);
  * the CUs are reserved), leaving n CUs free for a concurrent stream (the GAN
  * step beside the tuning step): a fused launch deals its units to its waves
  * statically, so a CU held by another stream's workgroup would hold back the
- * whole launch.  Default 0.  Results do not depend on it beyond fp32 summation
+ * whole launch.  Within that budget a launch takes the fewest workgroups whose
+ * longest wave has as many units as on the whole budget (units are whole
+ * 16-pair tiles), so it ends as early and leaves the rest of the CUs to other
+ * streams too.  Default 0.  Results do not depend on it beyond fp32 summation
  * grouping of the weight gradients (one slab per workgroup). */
 int pgp_tune_reserve_cus(int n);
 /* Profiling: with pgp_tune_timing(1), pgp_tune_forward / pgp_tune_backward

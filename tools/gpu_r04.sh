@@ -256,6 +256,11 @@ for step in "$@"; do
       run abe15 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" e7= e15=PGP_TUNE_SIDE_EARLY=15
       grep median $OUT/abe15.out
       ;;
+    roofchk)
+      run rc50 120 python3 -u bench.py --config tune --hosts 50 --steps 20 --warmup 3 --no-cpu-baseline
+      run rc16 120 python3 -u bench.py --config tune --hosts 16 --steps 50 --warmup 5 --no-cpu-baseline
+      python3 -c "import json; [print(json.dumps({k: v for k, v in json.loads(open('$OUT/' + f + '.out').read().strip().splitlines()[-1])['roofline'].items() if k != 'basis'})) for f in ('rc50', 'rc16')]"
+      ;;
     others)
       run fpe 300 python3 -u bench.py --config fpe --steps 100 --warmup 5
       run plugin 300 python3 -u bench.py --config plugin --steps 50 --warmup 5
