@@ -620,6 +620,11 @@ def bench_tune(args):
                                    for n, t, r in zip(RL.TUNE_FUSED_LAUNCHES, fused_ms, rates)},
                 "fused_total": {"ms": float(fused_ms.sum()),
                                 "frac": float(sum(flops) / (fused_ms.sum() * 1e-3) / 1e12 / RL.PEAK_FP32_TFLOPS)}}
+        # HBM bytes per launch of the dominant launch's kernel (both layers'
+        # launches averaged) from the committed, ISA-stamped counter pass
+        kname = {0: "tf_fwd", 1: "tf_fwd", 2: "tf_bwd_ffn", 3: "tf_bwd_att", 4: "tf_bwd_ffn", 5: "tf_bwd_att"}[k]
+        roof["traffic"] = load_traffic(H, B, kname)
+        roof["traffic_kernel"] = kname + "_kernel (mean over its two layer launches per step)"
         try:   # the CUs each launch holds (it takes the fewest that keep its longest wave)
             cus = torch.cuda.get_device_properties(device).multi_processor_count
             grids = RL.tune_fused_grids(H, B, B + E, cus, reserved)

@@ -261,6 +261,10 @@ for step in "$@"; do
       run rc16 120 python3 -u bench.py --config tune --hosts 16 --steps 50 --warmup 5 --no-cpu-baseline
       python3 -c "import json; [print(json.dumps({k: v for k, v in json.loads(open('$OUT/' + f + '.out').read().strip().splitlines()[-1])['roofline'].items() if k != 'basis'})) for f in ('rc50', 'rc16')]"
       ;;
+    tunetraffic)
+      pmc tunepmcf FETCH_SIZE --config tune --hosts 50 --steps 3 --warmup 1 --no-cpu-baseline
+      pmc tunepmcw WRITE_SIZE --config tune --hosts 50 --steps 3 --warmup 1 --no-cpu-baseline
+      ;;
     others)
       run fpe 300 python3 -u bench.py --config fpe --steps 100 --warmup 5
       run plugin 300 python3 -u bench.py --config plugin --steps 50 --warmup 5
