@@ -551,22 +551,25 @@ __global__ __launch_bounds__(256) void gat_param_kernel(int n, const float* __re
                                                         const float* __restrict__ P, const float* __restrict__ fcd,
                                                         float* __restrict__ Gd) {
   using G = TGeo<H>;
-  __shared__ float red[256][7];
+  // the workgroups' partials: strided per thread, a butterfly per wave, the
+  // four waves in order (one barrier; the 8-level LDS tree took 9)
+  __shared__ float wred[4][6];
+  __shared__ float tot[6];
   float acc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   for (int p = threadIdx.x; p < n; p += 256)
 #pragma unroll
     for (int k = 0; k < 6; ++k) acc[k] += GSX[(long)p * 8 + k];
 #pragma unroll
-  for (int k = 0; k < 6; ++k) red[threadIdx.x][k] = acc[k];
-  __syncthreads();
-  for (int s = 128; s >= 1; s >>= 1) {
-    if (threadIdx.x < s)
+  for (int k = 0; k < 6; ++k) acc[k] = wave_sum(acc[k]);
+  if ((threadIdx.x & 63) == 0)
 #pragma unroll
-      for (int k = 0; k < 6; ++k) red[threadIdx.x][k] += red[threadIdx.x + s][k];
-    __syncthreads();
-  }
-  const float* xs = red[0];
-  const float* xt = red[0] + 3;
+    for (int k = 0; k < 6; ++k) wred[threadIdx.x >> 6][k] = acc[k];
+  __syncthreads();
+  if (threadIdx.x < 6) tot[threadIdx.x] = ((wred[0][threadIdx.x] + wred[1][threadIdx.x]) + wred[2][threadIdx.x]) +
+                                         wred[3][threadIdx.x];
+  __syncthreads();
+  const float* xs = tot;
+  const float* xt = tot + 3;
   for (int c = threadIdx.x; c < H; c += 256) {
     const float* fc = P + G::W_FC + c * 3;
     const float a1 = P[G::W_ATT + c], a2 = P[G::W_ATT + H + c];

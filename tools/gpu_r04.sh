@@ -265,6 +265,13 @@ for step in "$@"; do
       pmc tunepmcf FETCH_SIZE --config tune --hosts 50 --steps 3 --warmup 1 --no-cpu-baseline
       pmc tunepmcw WRITE_SIZE --config tune --hosts 50 --steps 3 --warmup 1 --no-cpu-baseline
       ;;
+    gp)
+      run tgp 600 python3 -u -m pytest tests/test_gpu_tunedp.py tests/test_gpu_c3step.py tests/test_gpu_train.py tests/test_gpu_dist.py tests/test_gpu_plugin_graphs.py tests/test_gpu_tune1.py tests/test_gpu_train_model.py tests/test_gpu_bench_modes.py -x -q --timeout 120 --timeout-method thread -m gpu
+      run gp50 120 python3 -u bench.py --config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline
+      run gp16 120 python3 -u bench.py --config tune --hosts 16 --steps 100 --warmup 10 --no-cpu-baseline
+      run prof_gp 240 rocprofv3 --kernel-trace --stats -d $OUT/prof_gp -o tune --output-format csv -- python3 bench.py --config tune --hosts 50 --steps 30 --warmup 5 --no-cpu-baseline
+      grep -h -o '"ms_per_step": [0-9.]*' $OUT/gp50.out $OUT/gp16.out
+      ;;
     others)
       run fpe 300 python3 -u bench.py --config fpe --steps 100 --warmup 5
       run plugin 300 python3 -u bench.py --config plugin --steps 50 --warmup 5
