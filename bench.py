@@ -269,6 +269,13 @@ def main():
             res["cpu_baseline"] = cpu_baseline(weights, x, s)
         else:
             res["cpu_baseline"] = None
+    # sub-records (every rank takes part; rank 0 reports them in the line)
+    sub = {}
+    if "c3_dp" in c2_subrecords(world):
+        del out, mv_out, model
+        sub["c3_dp"] = c3_dp_record(world, rank, device)
+    if rank == 0:
+        res.update(sub)
         emit(res)
     if world > 1:
         torch.distributed.destroy_process_group()
@@ -387,15 +394,16 @@ def bench_ranks(args):
 
 
 def _timed(world, device, fn, steps):
+    sync = torch.cuda.synchronize if device.type == "cuda" else (lambda: None)
     if world > 1:
         torch.distributed.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for _ in range(steps):
         fn()
     global _HOST_ISSUE_S
     _HOST_ISSUE_S = time.perf_counter() - t0   # host time to issue the K steps (no sync inside)
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         torch.distributed.barrier()
     el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=device)
@@ -493,6 +501,91 @@ def synth_series(E, H, seed, R=10):
     return x, train_max
 
 
+def _build_c3_step(H, E, R, world, rank, device):
+    """The C3 step of one rank (TR.OnlineTrainStep, native): seeded
+    H-architecture weights, synthetic series / one-hot schedules /
+    environment records of E environments, the step's two streams (the GAN
+    step on a second stream beside the tuning step: no shared data,
+    PreGANPlus.py:133-134) and, at world > 1, the two process groups."""
+    import types
+    from preganplus_amd import simulate as SIM
+    from preganplus_amd import train as TR
+    B = E * R
+    w = W.synth_weights(H, seed=0)
+    tr = TR.Trainer(H, w, device=device, max_batch=B + E)   # the tuning windows + run_encoder's, one forward
+    st = TR.TuneState(w["prototypes"])
+    series_h, tmax_h = synth_series(E, H, 5 + rank, R)
+    g = torch.Generator(device=device).manual_seed(17 + rank)
+    s = torch.zeros((E, H, H), device=device)
+    s.scatter_(2, torch.randint(0, H, (E, H, 1), generator=g, device=device), 1.0)
+    envs = SIM.synth_envs(E, H, seed=5 + rank)
+    sim = SIM.Simulation(H, device=device)
+    main = torch.cuda.Stream(device)
+    torch.cuda.set_stream(main)
+    side = main if os.environ.get("PGP_BENCH_ONE_STREAM") == "1" else torch.cuda.Stream(device)
+    # world > 1, one GPU per rank: main + this second stream + the two
+    # communicators' streams are the 4 hardware queues a process gets
+    # (GPU_MAX_HW_QUEUES), so the tuning backward's side work (decoder and
+    # in_proj weight gradients) runs on this same second stream instead of a
+    # fifth (pgp_tune_set_side_stream); the GAN step is issued ahead of that
+    # side work (pgp_online_step issues it right after the forward, DESIGN §6)
+    _share_side_stream(world, main, side)
+    reserved = _reserve_cus(main, side)
+    step = TR.OnlineTrainStep(tr, st, sim, series_h, tmax_h, s, envs, R=R, side=side, groups=TR.dp_groups())
+    return types.SimpleNamespace(tr=tr, w=w, series=series_h, tmax=tmax_h, s=s, sim=sim, step=step, main=main,
+                                 side=side, reserved=reserved)
+
+
+def c2_subrecords(world):
+    """Sub-records the default (c2) line carries besides its headline value:
+    at world > 1 the data-parallel C3 step over the ranks' collective backend
+    (the one exchange step north_star names: the tuning gradient all-reduce),
+    so the driver's multi-GPU run of the default config measures it too."""
+    return ("c3_dp",) if world > 1 else ()
+
+
+def c3_dp_record(world, rank, device, steps=20, warmup=3, hosts=50, envs_per_gpu=103, make_step=None):
+    """The C3 data-parallel step (H = 50, 103 environments x 10 windows per
+    rank: OnlineTrainStep over the ranks' groups) timed like every line
+    (barrier + synchronize around `steps` steps, max over ranks), with the
+    main stream's exchange span (the tuning gradient + state all-reduces) from
+    the library's HIP events.  ``make_step(hosts, envs, rank, device)`` ->
+    (run, exchange_ms) replaces the real step (the CPU test's gloo stand-in).
+    Returns the sub-record (every rank; rank 0 emits it)."""
+    global _HOST_ISSUE_S
+    R = 10
+    if make_step is None:
+        def make_step(H, E, rk, dev):
+            c3 = _build_c3_step(H, E, R, world, rk, dev)
+
+            def exchange_ms(n=5):
+                c3.step.timing(True)
+                v = []
+                for _ in range(n):
+                    c3.step.run()
+                    v.append(c3.step.stage_ms()["exchange"])
+                c3.step.timing(False)
+                return float(np.mean(v))
+            return c3.step.run, exchange_ms
+    run, exchange_ms = make_step(hosts, envs_per_gpu, rank, device)
+    saved = _HOST_ISSUE_S
+    for _ in range(warmup):
+        run()
+    el = _timed(world, device, run, steps)
+    _HOST_ISSUE_S = saved
+    ar = exchange_ms()
+    ar_t = torch.tensor([ar], dtype=torch.float64, device=device)
+    if world > 1:
+        torch.distributed.all_reduce(ar_t, op=torch.distributed.ReduceOp.MAX)
+    B = envs_per_gpu * R
+    return {"workload": f"C3: semi-supervised tuning step, {hosts} hosts, {envs_per_gpu} environments x {R} windows "
+                        f"per GPU, data parallel", "n_gpus": world, "steps": steps, "warmup": warmup,
+            "ms_per_step": el / steps * 1e3, "windows_per_s": B * world * steps / el,
+            "all_reduce_ms": float(ar_t.item()), "backend": _backend_label(),
+            "all_reduce_note": "main stream span of the tuning gradient + state-increment all-reduces (the GAN "
+                               "step's two all-reduces run on its own group and stream beside the backward)"}
+
+
 def bench_tune(args):
     """BASELINE config 3: the semi-supervised training of run_model
     (PreGANPlus.py:115-136, everything but the decision) for a batch of
@@ -512,67 +605,39 @@ def bench_tune(args):
          step-start state (pgp_tune_targets_dp), backward, one RCCL gradient
          all-reduce + one all-reduce of the state increments, state update and
          AdamW from device tables (DPTuner)
-    No fixed labels, CE weights or targets, and no host round trip
-    (TR.OnlineTrainStep; the timed steps replay it as a captured HIP graph)."""
-    from preganplus_amd import simulate as SIM
+    No fixed labels, CE weights or targets, and no host round trip: each step
+    is ONE C-ABI call (TR.OnlineTrainStep -> pgp_online_step, which issues
+    every launch of both streams from C++; the collectives call back into
+    torch.distributed)."""
     from preganplus_amd import train as TR
     world, rank, device = _dist_setup()
     H = args.hosts
     E = args.batch if args.batch != 65536 else 103     # 103 environments x 10 windows ~ SURVEY's 1,024
     R = 10                                             # LATEST_WINDOW_SIZE (constants.py:16)
     B = E * R
-    w = W.synth_weights(H, seed=0)
-    tr = TR.Trainer(H, w, device=device, max_batch=B + E)   # the tuning windows + run_encoder's, one forward
-    st = TR.TuneState(w["prototypes"])
-    series_h, tmax_h = synth_series(E, H, 5 + rank, R)
-    g = torch.Generator(device=device).manual_seed(17 + rank)
-    s = torch.zeros((E, H, H), device=device)
-    s.scatter_(2, torch.randint(0, H, (E, H, 1), generator=g, device=device), 1.0)
-    envs = SIM.synth_envs(E, H, seed=5 + rank)
-    sim = SIM.Simulation(H, device=device)
+    c3 = _build_c3_step(H, E, R, world, rank, device)
+    tr, w, series_h, tmax_h, s, sim, step = c3.tr, c3.w, c3.series, c3.tmax, c3.s, c3.sim, c3.step
+    main, side, reserved = c3.main, c3.side, c3.reserved
     names = ("dataset", "detect", "train_gan", "tune_model")
     subs = TR.DPTuner.SUBSTAGES
-    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(len(names) + 2)] for _ in range(max(args.steps, 1))]
-    sev = [[torch.cuda.Event(enable_timing=True) for _ in range(len(subs) + 1)] for _ in range(max(args.steps, 1))]
-    # the step's streams (TR.OnlineTrainStep): the GAN step runs on a second
-    # stream beside the tuning step (no shared data, PreGANPlus.py:133-134);
-    # the main stream is not the default one, which a HIP graph cannot capture
-    main = torch.cuda.Stream(device)
-    torch.cuda.set_stream(main)
-    side = main if os.environ.get("PGP_BENCH_ONE_STREAM") == "1" else torch.cuda.Stream(device)
-    # world > 1, one GPU per rank: main + this second stream + the two
-    # communicators' streams are the 4 hardware queues a process gets
-    # (GPU_MAX_HW_QUEUES), so the tuning backward's side work (decoder and
-    # in_proj weight gradients) runs on this same second stream instead of a
-    # fifth (pgp_tune_set_side_stream), and the GAN step is issued ahead of
-    # that side work (DESIGN §6)
-    _share_side_stream(world, main, side)
-    reserved = _reserve_cus(main, side)
-    step = TR.OnlineTrainStep(tr, st, sim, series_h, tmax_h, s, envs, R=R, side=side, groups=TR.dp_groups())
     for _ in range(args.warmup):
         step.run()
-    # the timed steps: eager issue.  PGP_BENCH_GRAPH=1 replays the step
-    # captured once as a HIP graph instead (world size 1); on one box that was
-    # slower than eager issue at both H (16: 0.313 vs 0.302 ms, 50: 1.301-1.314
-    # vs 1.297 ms; profiles/r04/s5/ab_tune*_graph_eager.txt)
-    graphed = world == 1 and os.environ.get("PGP_BENCH_GRAPH", "0") == "1"
-    if graphed:
-        step.capture()
     el = _timed(world, device, step.run, args.steps)
-    # stage spans: the same step issued eagerly with HIP events (a captured
-    # step cannot record timing events)
-    n_ev = min(args.steps, len(ev))
-    for k in range(n_ev):
-        step.prep()
-        step.issue(ev[k], sev[k])
-    torch.cuda.synchronize()
-    # dataset (main stream), detect's embedding (second stream: its start e[5]
-    # to e[2]), train_gan (second stream, after it) and tune_model (main
-    # stream, its first sub-stage mark to its last); the last three overlap
-    stage = np.array([[e[0].elapsed_time(e[1]), e[5].elapsed_time(e[2]), e[2].elapsed_time(e[3]),
-                       s_[0].elapsed_time(s_[len(subs)])] for e, s_ in zip(ev[:n_ev], sev[:n_ev])]).mean(0)
-    sub = np.array([[e[k].elapsed_time(e[k + 1]) for k in range(len(subs))] for e in sev[:n_ev]]).mean(0)
-    eager_ms = float(np.mean([e[0].elapsed_time(e[4]) for e in ev[:n_ev]]))
+    # stage spans: more steps with the library's HIP events on (dataset on
+    # the main stream; the embedding and train_gan on the GAN stream;
+    # tune_model = the main stream from the forward to AdamW, with its
+    # sub-stages); the GAN stream overlaps the targets and the backward
+    n_ev = max(3, min(args.steps, 20))
+    step.timing(True)
+    spans = []
+    for _ in range(n_ev):
+        step.run()
+        spans.append(step.stage_ms())
+    step.timing(False)
+    mean = lambda k: float(np.mean([d[k] for d in spans]))
+    stage = np.array([mean("dataset"), mean("embedding"), mean("train_gan"), mean("tune_model")])
+    sub = np.array([mean(k) for k in ("forward", "targets", "backward", "exchange", "apply_adamw")])
+    eager_ms = mean("main")
     # roofline of the dominant kernels: the six fused encoder launches of the
     # tuning forward + backward, timed live with HIP events recorded on their
     # stream inside the library (pgp_tune_timing) over extra eager steps after
@@ -586,8 +651,7 @@ def bench_tune(args):
     fused = []
     ms6 = (ctypes.c_float * 6)()
     for _ in range(max(3, min(args.steps, 10))):
-        step.prep()
-        step.issue()
+        step.run()
         _native.check(L.pgp_tune_fused_ms(ms6), "pgp_tune_fused_ms")
         fused.append(list(ms6))
     _native.check(L.pgp_tune_timing(0), "pgp_tune_timing")
@@ -600,9 +664,7 @@ def bench_tune(args):
     a0, a1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     a0.record(main)
     for _ in range(n_alone):
-        step.prep()
-        TR.train_gan_batched(tr, sim, step.envs, step.emb, step.sched, out=step.sim_out, target=step.target,
-                             rows=step._rows[1:])
+        TR.train_gan_batched(tr, sim, step.envs, step.emb, step.sched, out=step.sim_out, target=step.target)
     a1.record(main)
     torch.cuda.synchronize()
     gan_alone = a0.elapsed_time(a1) / n_alone
@@ -651,12 +713,12 @@ def bench_tune(args):
                        "windows_per_gpu": B, "parallelism": f"dp{world}" + (f" + {_backend_label()} all-reduce "
                                                                            "(grads, state; GAN on its own group)"
                                                                            if world > 1 else "")},
-            "timed": ("the step captured once as a HIP graph and replayed (AdamW scalars from device rows "
-                      "written before each replay)" if graphed else "eager issue"),
-            "eager_ms_per_step": eager_ms,
+            "timed": "one pgp_online_step C-ABI call per step (every launch issued from C++)",
+            "timed_with_events_ms_per_step": eager_ms,
             "stage_ms": {n: float(stage[k]) for k, n in enumerate(names)},
-            "stage_note": ("eager steps with HIP events; detect = run_encoder's windows as the last E rows of the "
-                           "tuning forward (same step-start weights), then their embedding on the second stream"),
+            "stage_note": ("steps with the library's HIP events; detect = run_encoder's windows as the last E rows "
+                           "of the tuning forward (same step-start weights), then their embedding on the second "
+                           "stream"),
             "streams": "detect's embedding + train_gan on a second stream, concurrent with tune_model's backward "
                        "(no shared data)" if side is not main else "one stream",
             "reserved_cus": reserved,

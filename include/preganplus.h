@@ -400,6 +400,90 @@ int pgp_gan_step1(int n_hosts, const float* target, float* P, float* G, float* e
                   float* probs_gen, float* probs_after, void* stream);
 
 /* ---------------------------------------------------------------------------
+ * The whole online training step of run_model in ONE call (BASELINE config
+ * C3; replaces, per interval and for a batch of E environments, the sequence
+ * PreGANPlus.py:115-136 minus the decision: run_encoder + detect/embed
+ * (:107-131), train_gan (:60-81 -> utils.py:97-100 runSimulation), tune_model
+ * (:51-58 -> utils.py:40-47 load_on_the_fly_dataset, train.py:42-57 backprop in
+ * the data-parallel form of SURVEY §8e), i.e. the composition of
+ * pgp_tune_dataset, pgp_tune_forward, pgp_embedding, pgp_gan_forward,
+ * pgp_simulate, pgp_gan_disc_backward, pgp_adamw, pgp_gan_gen_backward,
+ * pgp_tune_targets_dp, pgp_tune_backward_prefix, pgp_tune_state_apply).
+ * pgp_online_create takes every buffer once (caller-owned device memory):
+ *   series [E,R,3H] f64, train_max [3H] f64, sched [E,H,H] f32 (the original
+ *   schedules), envs [E, pgp_sim_env_len(H)] f64 (simulation records);
+ *   P / G / exp_avg / exp_avg_sq: the master (pgp_master_len(H) floats);
+ *   tune_ws: pgp_tune_workspace_len(H, E*R + E) floats; logits / protos
+ *   [E*R+E, H, 2]; windows [E*R+E, 3, 3H] (the tuning windows, then detect's);
+ *   y / cls [E*R, H] int32; state [2K+3] f64 (prototypes, factor, num_zero,
+ *   num_ones: updated in place); mult [E*R,H]; tgt [E*R,H,2]; loss [E*R,2] f64;
+ *   inc [3K+3] f64; dp_ws pgp_tune_targets_dp_workspace_len(E*R) doubles;
+ *   adam_rows [n_tensors of section 0][3] f32 (the conditional rows,
+ *   written on the device); cond_steps [n_cond] f64 (their step counts);
+ *   gan_ws pgp_gan_workspace_len(H, E) floats; ns [E,H,H]; probs [E,2];
+ *   emb [E,H,2]; sim_out [E,4] f64; target [E,2] f32.
+ *   tensors: every trainable tensor of the three sections (0 Transformer,
+ *   1 Gen, 2 Disc) in blob order, with its AdamW step count so far; `cond`
+ *   marks the prototype decoder's (no gradient when the global batch has no
+ *   positive label: their activity and step counts live on the device).
+ * pgp_online_step issues one step on main_stream (tuning) and gan_stream (the
+ * GAN step, beside it; NULL: main_stream), the main stream waiting for the GAN
+ * stream at the end.  AdamW's per-step scalars are the host's (double, rounded
+ * to fp32 as torch's AdamW computes them per step).  `cb` (NULL at world size
+ * 1) performs the data-parallel exchange in place, ordered on `stream`:
+ * PGP_COLL_DISC_GRAD / PGP_COLL_GEN_GRAD (the Disc / Gen sections of G, on the
+ * GAN stream), PGP_COLL_TUNE_GRAD (the Transformer section of G) and
+ * PGP_COLL_TUNE_STATE (inc), on the main stream; the same order on every rank.
+ * pgp_online_timing(h, 1) records HIP events in later steps;
+ * pgp_online_stage_ms(h, ms[PGP_ONLINE_NSTAGE]) returns the last step's spans:
+ * dataset, embedding, train_gan, tune_model, forward, targets, backward,
+ * exchange, state + AdamW, whole main stream.  pgp_online_steps returns the
+ * host step counts (in `tensors` order; -1 for the conditional tensors). */
+typedef struct {
+  long long offset;  /* first element in P/G/m/v */
+  int n;
+  int section;       /* 0 Transformer, 1 Gen, 2 Disc */
+  int cond;          /* prototype decoder (device-side activity) */
+  double step;       /* AdamW steps taken so far */
+} pgp_online_tensor;
+typedef struct {
+  int n_hosts, n_env, n_rows, n_protos;
+  const double* series;
+  const double* train_max;
+  const float* sched;
+  const double* envs;
+  float *P, *G, *exp_avg, *exp_avg_sq;
+  float* tune_ws;
+  float *logits, *protos, *windows;
+  int *y, *cls;
+  double* state;
+  float *mult, *tgt;
+  double *loss, *inc, *dp_ws;
+  float* adam_rows;
+  double* cond_steps;
+  float *gan_ws, *ns, *probs, *emb;
+  double* sim_out;
+  float* target;
+  const pgp_online_tensor* tensors;
+  int n_tensors, n_cond;
+  double lr[3]; /* per section */
+  double weight_decay, beta1, beta2, eps, update_min, decay;
+} pgp_online_desc;
+typedef struct pgp_online pgp_online;
+typedef int (*pgp_collective_fn)(void* user, int which, void* stream);
+#define PGP_COLL_DISC_GRAD 0
+#define PGP_COLL_GEN_GRAD 1
+#define PGP_COLL_TUNE_GRAD 2
+#define PGP_COLL_TUNE_STATE 3
+#define PGP_ONLINE_NSTAGE 10
+int pgp_online_create(const pgp_online_desc* desc, pgp_online** out);
+int pgp_online_destroy(pgp_online* h);
+int pgp_online_step(pgp_online* h, void* main_stream, void* gan_stream, pgp_collective_fn cb, void* user);
+int pgp_online_timing(pgp_online* h, int on);
+int pgp_online_stage_ms(pgp_online* h, float* ms);
+int pgp_online_steps(const pgp_online* h, double* steps, int n);
+
+/* ---------------------------------------------------------------------------
  * Offline training of PreGAN's FPE_16 (PreGAN.py:26-27, 39-49: a new FPE is
  * trained when no checkpoint exists, train.py:42-57).  P / G: the FPE's
  * parameters, natural fp32 blob in state_dict order (pgp_fpe_param_len(16) =

@@ -653,7 +653,7 @@ int pgp_adamw_table(float* P, const float* G, float* exp_avg, float* exp_avg_sq,
   for (int i = 0; i < ntensors; ++i) {
     a.t[i].off = (long)tensors[i].offset;
     a.t[i].n = tensors[i].n;
-    a.t[i].active = tensors[i].active;
+    a.t[i].active = kAdamFromTable;  // every row from the table
     a.t[i].step_size = tensors[i].step_size;
     a.t[i].bc2_sqrt = tensors[i].bc2_sqrt;
   }

@@ -103,6 +103,9 @@ hipError_t launch_gan_disc_bwd(int H, int B, const float* target, const float* P
 hipError_t launch_gan_gen_bwd(int H, int B, const float* Pg, const float* Pd, float* Gdg, float* ws,
                               hipStream_t st);
 hipError_t launch_gan_probs(int H, int B, const float* ws, float* probs, hipStream_t st);
+// GAN labels (pgp_sim.hip, pgp_simulate's kernel): 1 <= H <= 64
+hipError_t launch_simulate(int H, int E, const double* envs, const float* new_sched, const float* orig_sched,
+                           double* out, float* target, hipStream_t st);
 
 #ifdef __HIP_DEVICE_COMPILE__
 #define PGP_DEV __device__ __forceinline__

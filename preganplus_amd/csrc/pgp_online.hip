@@ -1,0 +1,297 @@
+// pgp_online.hip — run_model's semi-supervised training (PreGANPlus.py:115-136,
+// all but the decision; BASELINE config C3) for a batch of environments,
+// issued from ONE C-ABI call (pgp_online_step) instead of ~40 host calls:
+//
+//   main stream  dataset (load_on_the_fly_dataset utils.py:40-47 + run_encoder's
+//                window PreGANPlus.py:107-112) -> ONE tuning forward over the
+//                R*E tuning windows and the E detect windows (same step-start
+//                weights) -> custom_loss / triplet_loss bookkeeping against the
+//                step-start state (train.py:13-40, DP form) -> backward over
+//                the tuning windows -> [all-reduce grads, state increments] ->
+//                state update, AdamW (utils.py:65)
+//   GAN stream   (from the forward's end) detect's masked embedding
+//                (PreGANPlus.py:129) -> Gen + Disc forward -> both schedules
+//                simulated on the device (utils.py:97-100 -> Stats.py:154-177)
+//                -> Disc BCE step -> [all-reduce] -> AdamW -> Gen BCE step
+//                through the updated Disc -> [all-reduce] -> AdamW
+//                (train_gan, PreGANPlus.py:60-81)
+//
+// The GAN and tuning steps share no data (the GAN reads the embedding and
+// writes the Gen / Disc sections; the tuning step writes the Transformer
+// section), so they run side by side; the step ends with the main stream
+// waiting for the GAN stream.  AdamW's per-step scalars are computed here on
+// the host from the step counts this object keeps (lr / (1 - beta1^step),
+// sqrt(1 - beta2^step) in double, rounded to fp32: the values the Python
+// tables hold) and passed by value; the prototype decoder's rows, whose
+// activity depends on the global batch's labels, come from the device table
+// pgp_tune_state_apply writes.  The collectives of a data-parallel step are
+// the caller's (a callback at the four exchange points, on the stream it
+// names): this library has no communicator of its own.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <string>
+
+#include "../../include/preganplus.h"
+#include "pgp_device.hpp"
+#include "pgp_train.hpp"
+#include "pgp_tune.hpp"
+#include "pgp_tunedp.hpp"
+
+using namespace pgp;
+
+namespace {
+
+enum Sec { kTr = 0, kGen = 1, kDisc = 2 };
+// timing events: main stream 0..6, GAN stream 7..9
+enum Ev { kE0, kE1, kE2, kE3, kE4, kE5, kE6, kG0, kG1, kG2, kNumEv };
+
+}  // namespace
+
+struct pgp_online {
+  pgp_online_desc d{};
+  int H = 0, E = 0, R = 0, B = 0, K = 0;
+  TunePlan fwd{}, bwd{};
+  AdamArgs adam[3]{};
+  double step[3][kMaxTensors] = {};  // host step counts (the prototype decoder's live on the device)
+  int cond_local[kMaxTensors] = {};  // transformer selection index -> cond flag
+  CondRows cr{};
+  long sec_lo[3] = {0, 0, 0};
+  hipEvent_t gate = nullptr, gan_done = nullptr;
+  bool timing = false, timed = false;
+  hipEvent_t tev[kNumEv] = {};
+};
+
+namespace {
+
+thread_local std::string g_oerr;
+int ofail(int code, const std::string& msg) {
+  set_error(code, msg);
+  g_oerr = msg;
+  return code;
+}
+#define OCHK(x)                                                                                     \
+  do {                                                                                              \
+    hipError_t e_ = (x);                                                                            \
+    if (e_ != hipSuccess) return ofail(PGP_ERR_HIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+#define OCALL(x)               \
+  do {                         \
+    const int r_ = (x);        \
+    if (r_ != PGP_OK) return r_; \
+  } while (0)
+
+// the next step's AdamW scalars of a section's always-active tensors
+void next_scalars(pgp_online* o, int sec) {
+  AdamArgs& a = o->adam[sec];
+  const double lr = o->d.lr[sec], b1 = o->d.beta1, b2 = o->d.beta2;
+  for (int i = 0; i < a.ntensors; ++i) {
+    if (a.t[i].active & kAdamFromTable) continue;
+    o->step[sec][i] += 1.0;
+    const double st = o->step[sec][i] > 1.0 ? o->step[sec][i] : 1.0;
+    a.t[i].step_size = (float)(lr / (1.0 - std::pow(b1, st)));
+    a.t[i].bc2_sqrt = (float)std::sqrt(1.0 - std::pow(b2, st));
+  }
+}
+
+void mark(pgp_online* o, int k, hipStream_t s) {
+  if (o->timing) (void)hipEventRecord(o->tev[k], s);
+}
+
+int collective(pgp_collective_fn cb, void* user, int which, hipStream_t s) {
+  if (!cb) return PGP_OK;
+  const int r = cb(user, which, reinterpret_cast<void*>(s));
+  return r == 0 ? PGP_OK : ofail(PGP_ERR_STATE, "collective callback failed (which = " + std::to_string(which) + ")");
+}
+
+}  // namespace
+
+extern "C" {
+
+int pgp_online_create(const pgp_online_desc* desc, pgp_online** out) {
+  if (!desc || !out) return ofail(PGP_ERR_ARG, "pgp_online_create: NULL argument");
+  *out = nullptr;
+  const pgp_online_desc& d = *desc;
+  const int H = d.n_hosts, E = d.n_env, R = d.n_rows, K = d.n_protos;
+  if (E < 1 || R < 1 || R > kMaxTuneRows) return ofail(PGP_ERR_ARG, "pgp_online_create: 1 <= n_env, 1 <= n_rows <= 16");
+  if (K < 3 || K > kMaxProtos) return ofail(PGP_ERR_ARG, "pgp_online_create: n_protos");
+  const size_t olen = pgp_master_len(H);
+  if (olen == 0) return ofail(PGP_ERR_UNSUPPORTED, "pgp_online_create: host count not compiled in");
+  const void* need[] = {d.series, d.train_max, d.sched, d.envs, d.P, d.G, d.exp_avg, d.exp_avg_sq, d.tune_ws,
+                        d.logits, d.protos, d.windows, d.y, d.cls, d.state, d.mult, d.tgt, d.loss, d.inc, d.dp_ws,
+                        d.adam_rows, d.gan_ws, d.ns, d.probs, d.emb, d.sim_out, d.target, d.tensors};
+  for (const void* p : need)
+    if (!p) return ofail(PGP_ERR_ARG, "pgp_online_create: NULL buffer in the descriptor");
+  if ((d.n_cond > 0 && !d.cond_steps) || d.n_tensors < 1 || d.n_tensors > 3 * kMaxTensors)
+    return ofail(PGP_ERR_ARG, "pgp_online_create: tensors / cond_steps");
+  auto* o = new pgp_online;
+  o->d = d;
+  o->H = H;
+  o->E = E;
+  o->R = R;
+  o->B = E * R;
+  o->K = K;
+  const int B = o->B;
+  if (!tune_plan(H, B + E, &o->fwd) || !tune_plan_prefix(H, B + E, B, &o->bwd)) {
+    delete o;
+    return ofail(PGP_ERR_ARG, "pgp_online_create: tuning plan");
+  }
+  o->sec_lo[kTr] = (long)pgp_master_offset(H, 0);
+  o->sec_lo[kGen] = (long)pgp_master_offset(H, 1);
+  o->sec_lo[kDisc] = (long)pgp_master_offset(H, 2);
+  const long sec_hi[3] = {o->sec_lo[kGen], o->sec_lo[kDisc], (long)olen};
+  for (int s = 0; s < 3; ++s) {
+    AdamArgs& a = o->adam[s];
+    a.param = d.P;
+    a.grad = d.G;
+    a.m = d.exp_avg;
+    a.v = d.exp_avg_sq;
+    a.lr_wd = (float)d.lr[s] * (float)d.weight_decay;  // pgp_adamw_table's (float lr) * (float wd)
+    a.b1 = (float)d.beta1;
+    a.b2 = (float)d.beta2;
+    a.eps = (float)d.eps;
+    a.ntensors = 0;
+    a.sched = s == kTr ? d.adam_rows : nullptr;
+  }
+  int ncond = 0;
+  for (int i = 0; i < d.n_tensors; ++i) {
+    const pgp_online_tensor& t = d.tensors[i];
+    if (t.section < 0 || t.section > 2) {
+      delete o;
+      return ofail(PGP_ERR_ARG, "pgp_online_create: tensor section");
+    }
+    AdamArgs& a = o->adam[t.section];
+    if (a.ntensors >= kMaxTensors || t.offset < o->sec_lo[t.section] || t.n < 0 ||
+        (long)t.offset + t.n > sec_hi[t.section] || (t.cond && t.section != kTr)) {
+      delete o;
+      return ofail(PGP_ERR_ARG, "pgp_online_create: tensor outside its section (or a conditional GAN tensor)");
+    }
+    const int j = a.ntensors++;
+    a.t[j].off = (long)t.offset;
+    a.t[j].n = t.n;
+    a.t[j].active = t.cond ? kAdamFromTable : 1;
+    o->step[t.section][j] = t.step;
+    if (t.cond) {
+      if (ncond >= kMaxCond) {
+        delete o;
+        return ofail(PGP_ERR_ARG, "pgp_online_create: too many conditional tensors");
+      }
+      o->cr.row[ncond++] = j;
+    }
+  }
+  if (ncond != d.n_cond) {
+    delete o;
+    return ofail(PGP_ERR_ARG, "pgp_online_create: n_cond does not match the tensors flagged cond");
+  }
+  o->cr.n = ncond;
+  if (hipEventCreateWithFlags(&o->gate, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&o->gan_done, hipEventDisableTiming) != hipSuccess) {
+    delete o;
+    return ofail(PGP_ERR_HIP, "pgp_online_create: events");
+  }
+  *out = o;
+  return PGP_OK;
+}
+
+int pgp_online_destroy(pgp_online* o) {
+  if (!o) return PGP_OK;
+  if (o->gate) (void)hipEventDestroy(o->gate);
+  if (o->gan_done) (void)hipEventDestroy(o->gan_done);
+  for (auto& e : o->tev)
+    if (e) (void)hipEventDestroy(e);
+  delete o;
+  return PGP_OK;
+}
+
+int pgp_online_step(pgp_online* o, void* main_stream, void* gan_stream, pgp_collective_fn cb, void* user) {
+  if (!o) return ofail(PGP_ERR_ARG, "pgp_online_step: NULL handle");
+  const pgp_online_desc& d = o->d;
+  const int H = o->H, E = o->E, R = o->R, B = o->B, K = o->K;
+  const hipStream_t sm = reinterpret_cast<hipStream_t>(main_stream);
+  const hipStream_t sg = gan_stream ? reinterpret_cast<hipStream_t>(gan_stream) : sm;
+  const long go = o->sec_lo[kGen], dof = o->sec_lo[kDisc];
+  o->timed = o->timing;
+  // 1. the dataset: R tuning windows per environment, then the E detect windows
+  mark(o, kE0, sm);
+  float* detect_win = d.windows + (long)B * 9 * H;
+  OCHK(launch_tune_dataset(H, E, R, d.series, d.train_max, d.windows, d.y, d.cls, detect_win, sm));
+  mark(o, kE1, sm);
+  // 2. ONE forward over the B + E windows (step-start weights)
+  OCHK(launch_tune_forward(o->fwd, d.windows, d.P, d.tune_ws, nullptr, d.logits, d.protos, sm));
+  mark(o, kE2, sm);
+  // 3. the GAN stream starts at the forward's end: embedding, Gen + Disc
+  //    forward, the simulated label, the Disc gradient
+  if (sg != sm) {
+    OCHK(hipEventRecord(o->gate, sm));
+    OCHK(hipStreamWaitEvent(sg, o->gate, 0));
+  }
+  mark(o, kG0, sg);
+  OCHK(launch_embed((long)E * H, d.logits + (long)B * H * 2, d.protos + (long)B * H * 2, d.emb, sg));
+  mark(o, kG1, sg);
+  OCHK(launch_gan_fwd(H, E, d.emb, d.sched, d.P + go, d.P + dof, d.gan_ws, d.ns, d.probs, sg));
+  OCHK(launch_simulate(H, E, d.envs, d.ns, d.sched, d.sim_out, d.target, sg));
+  OCHK(launch_gan_disc_bwd(H, E, d.target, d.P + dof, d.G + dof, d.gan_ws, sg));
+  // 4. main: bookkeeping against the step-start state, then the backward
+  //    (the decoders' input gradient dpre written by the same launch)
+  OCHK(launch_tune_targets_dp(H, K, B, d.logits, d.protos, d.y, d.cls, d.state, d.update_min, d.mult, d.tgt, d.loss,
+                              d.inc, d.dp_ws, sm, d.tune_ws + o->bwd.dpre, o->bwd.NOP));
+  mark(o, kE3, sm);
+  OCHK(hipMemsetAsync(d.G + o->sec_lo[kTr], 0, (size_t)(go - o->sec_lo[kTr]) * sizeof(float), sm));
+  OCHK(launch_tune_backward(o->bwd, d.P, d.G, d.tune_ws, d.logits, d.protos, d.y, d.mult, d.tgt, sm, true));
+  mark(o, kE4, sm);
+  // 5. the GAN's updates (its collectives on the GAN stream)
+  OCALL(collective(cb, user, PGP_COLL_DISC_GRAD, sg));
+  next_scalars(o, kDisc);
+  OCHK(launch_adamw(o->adam[kDisc], sg));
+  OCHK(launch_gan_gen_bwd(H, E, d.P + go, d.P + dof, d.G + go, d.gan_ws, sg));
+  OCALL(collective(cb, user, PGP_COLL_GEN_GRAD, sg));
+  next_scalars(o, kGen);
+  OCHK(launch_adamw(o->adam[kGen], sg));
+  mark(o, kG2, sg);
+  // 6. the tuning step's exchange, state update and AdamW
+  OCALL(collective(cb, user, PGP_COLL_TUNE_GRAD, sm));
+  OCALL(collective(cb, user, PGP_COLL_TUNE_STATE, sm));
+  mark(o, kE5, sm);
+  OCHK(launch_tune_state_apply(K, d.state, d.inc, d.decay, o->cr, d.cond_steps, d.adam_rows, d.lr[kTr], d.beta1,
+                               d.beta2, sm));
+  next_scalars(o, kTr);
+  OCHK(launch_adamw(o->adam[kTr], sm));
+  mark(o, kE6, sm);
+  if (sg != sm) {
+    OCHK(hipEventRecord(o->gan_done, sg));
+    OCHK(hipStreamWaitEvent(sm, o->gan_done, 0));
+  }
+  (void)R;
+  return PGP_OK;
+}
+
+int pgp_online_timing(pgp_online* o, int on) {
+  if (!o) return ofail(PGP_ERR_ARG, "pgp_online_timing: NULL handle");
+  if (on && !o->tev[0])
+    for (auto& e : o->tev) OCHK(hipEventCreate(&e));
+  o->timing = on != 0;
+  return PGP_OK;
+}
+
+int pgp_online_stage_ms(pgp_online* o, float* ms) {
+  if (!o || !ms) return ofail(PGP_ERR_ARG, "pgp_online_stage_ms: NULL argument");
+  if (!o->timed) return ofail(PGP_ERR_STATE, "pgp_online_stage_ms: the last step was not timed (pgp_online_timing)");
+  for (auto& e : o->tev) OCHK(hipEventSynchronize(e));
+  const int pairs[PGP_ONLINE_NSTAGE][2] = {{kE0, kE1}, {kG0, kG1}, {kG1, kG2}, {kE1, kE6}, {kE1, kE2},
+                                           {kE2, kE3}, {kE3, kE4}, {kE4, kE5}, {kE5, kE6}, {kE0, kE6}};
+  for (int k = 0; k < PGP_ONLINE_NSTAGE; ++k) OCHK(hipEventElapsedTime(&ms[k], o->tev[pairs[k][0]], o->tev[pairs[k][1]]));
+  return PGP_OK;
+}
+
+int pgp_online_steps(const pgp_online* o, double* steps, int n) {
+  if (!o || !steps || n != o->d.n_tensors) return ofail(PGP_ERR_ARG, "pgp_online_steps: arguments");
+  int cnt[3] = {0, 0, 0};
+  for (int i = 0; i < n; ++i) {
+    const pgp_online_tensor& t = o->d.tensors[i];
+    const int j = cnt[t.section]++;
+    steps[i] = t.cond ? -1.0 : o->step[t.section][j];
+  }
+  return PGP_OK;
+}
+
+}  // extern "C"

@@ -174,6 +174,15 @@ __global__ __launch_bounds__(128) void simulate_kernel(int H, int E, const doubl
 }
 
 }  // namespace
+
+hipError_t launch_simulate(int H, int E, const double* envs, const float* new_sched, const float* orig_sched,
+                           double* out, float* target, hipStream_t st) {
+  if (H < 1 || H > kMaxH || E < 0) return hipErrorInvalidValue;
+  if (E == 0) return hipSuccess;
+  simulate_kernel<<<E, 128, sim_lds_bytes(H), st>>>(H, E, envs, new_sched, orig_sched, out, target);
+  return hipGetLastError();
+}
+
 }  // namespace pgp
 
 using namespace pgp;

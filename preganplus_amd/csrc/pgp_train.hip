@@ -29,7 +29,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(AdamArgs a, AdamGrid g) {
   }
   const AdamTensor& t = a.t[lo];
   float step_size = t.step_size, bc2_sqrt = t.bc2_sqrt;
-  if (a.sched) {  // per-step scalars from the device (graph-captured loops)
+  if (a.sched && (t.active & kAdamFromTable)) {  // per-step scalars from the device (graph-captured loops)
     const float* r = a.sched + 3 * lo;
     if (r[0] == 0.f) return;
     step_size = r[1];

@@ -56,10 +56,12 @@ struct TGeo {
 
 // AdamW descriptor: one per parameter tensor in the natural blob
 constexpr int kMaxTensors = 48;
+constexpr int kAdamFromTable = 2;
 struct AdamTensor {
   long off;       // offset in the master buffer (floats)
   int n;          // elements
-  int active;     // got a gradient this step (torch skips params whose grad is None)
+  int active;     // got a gradient this step (torch skips params whose grad is None); with
+                  // kAdamFromTable set, (active, step_size, bc2_sqrt) come from AdamArgs::sched's row
   float step_size;  // lr / (1 - b1^step)
   float bc2_sqrt;   // sqrt(1 - b2^step)
 };

@@ -31,6 +31,7 @@
 #include "pgp_gemm.hpp"
 #include "pgp_train.hpp"
 #include "pgp_tune.hpp"
+#include "pgp_tunedp.hpp"
 #include "pgp_tunef.hpp"
 #include "pgp_tunetargets.hpp"
 
@@ -667,19 +668,9 @@ __global__ __launch_bounds__(256) void tune_loss_kernel(int B, int H, int NOP, c
   if (idx >= (long)B * H) return;
   const long b = idx / H;
   const int h = (int)(idx - b * H);
-  const float l0 = logits[b * 2 * H + 2 * h], l1 = logits[b * 2 * H + 2 * h + 1];
-  const float m = fmaxf(l0, l1), e0 = expf(l0 - m), e1 = expf(l1 - m), inv = 1.0f / (e0 + e1);
-  const int yy = y[idx];
-  const float mu = mult[idx];
   float* d = dpre + b * NOP;
-  d[2 * h] = mu * (e0 * inv - (yy == 0 ? 1.f : 0.f));
-  d[2 * h + 1] = mu * (e1 * inv - (yy == 1 ? 1.f : 0.f));
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const float p = protos[b * 2 * H + 2 * h + k];
-    const float gk = yy > 0 ? (p - tgt[idx * 2 + k]) : 0.f;  // d/dp mean_k (p - t)^2
-    d[2 * H + 2 * h + k] = gk * p * (1.f - p);                // through the sigmoid
-  }
+  dpre_host(logits[2 * idx], logits[2 * idx + 1], y[idx], mult[idx], protos[2 * idx], protos[2 * idx + 1],
+            tgt[2 * idx], tgt[2 * idx + 1], d + 2 * h, d + 2 * H + 2 * h);
 }
 
 // decoder weight / bias gradients straight into G (natural layout): one
@@ -1093,7 +1084,8 @@ hipError_t tune_fwd_h(const TunePlan& p, const float* win, const float* P, float
 
 template <int H>
 hipError_t tune_bwd_h(const TunePlan& p, const float* P, float* Gd, float* ws, const float* logits,
-                      const float* protos, const int* y, const float* mult, const float* tgt, hipStream_t st) {
+                      const float* protos, const int* y, const float* mult, const float* tgt, hipStream_t st,
+                      bool dpre_ready) {
   using Q = TuneGeo<H>;
   using G = TGeo<H>;
   constexpr int DP = Q::DP;
@@ -1103,8 +1095,9 @@ hipError_t tune_bwd_h(const TunePlan& p, const float* P, float* Gd, float* ws, c
   RedBatch rb{ws + p.pool, p.pool_len};
   Fork fk(st, p.M);
   const hipStream_t sd = fk.side;
-  TCK((tune_loss_kernel<<<(int)(((long)B * H + 255) / 256), 256, 0, st>>>(B, H, Q::NOP, logits, protos, y, mult,
-                                                                           tgt, ws + p.dpre)));
+  if (!dpre_ready)  // (pgp_online_step: written by the targets kernel)
+    TCK((tune_loss_kernel<<<(int)(((long)B * H + 255) / 256), 256, 0, st>>>(B, H, Q::NOP, logits, protos, y, mult,
+                                                                             tgt, ws + p.dpre)));
   // Side work issued as soon as its inputs exist: the decoders' weight
   // gradient right here (bit 2), layer 1's in_proj weight gradient right after
   // layer 1's attention backward (bit 1).  They run beside the fused launches
@@ -1315,11 +1308,11 @@ hipError_t launch_tune_forward(const TunePlan& p, const float* windows, const fl
 
 hipError_t launch_tune_backward(const TunePlan& p, const float* P, float* G, float* ws, const float* logits,
                                 const float* protos, const int* y, const float* mult, const float* tgt,
-                                hipStream_t st) {
+                                hipStream_t st, bool dpre_ready) {
   switch (p.H) {
 #define CASE(h) \
   case h:       \
-    return tune_bwd_h<h>(p, P, G, ws, logits, protos, y, mult, tgt, st);
+    return tune_bwd_h<h>(p, P, G, ws, logits, protos, y, mult, tgt, st, dpre_ready);
     PGP_FOR_EACH_H(CASE)
 #undef CASE
   }

@@ -65,9 +65,11 @@ hipError_t launch_dec_dx(int H, int B, const float* dpre, const float* WpT, floa
 
 hipError_t launch_tune_forward(const TunePlan& p, const float* windows, const float* P, float* ws, float* latent,
                                float* logits, float* protos, hipStream_t st);
+// dpre_ready: the decoder pre-activation gradient [B][NOP] at ws + p.dpre was
+// already written (launch_tune_targets_dp with dpre), so the loss kernel is skipped
 hipError_t launch_tune_backward(const TunePlan& p, const float* P, float* G, float* ws, const float* logits,
                                 const float* protos, const int* y, const float* mult, const float* tgt,
-                                hipStream_t st);
+                                hipStream_t st, bool dpre_ready = false);
 hipError_t launch_tune_targets(int H, int K, const float* logits, const float* protos, const int* y, const int* cls,
                                double* state, double update_min, double decay, float* mult, float* tgt, double* loss,
                                hipStream_t st);

@@ -18,8 +18,9 @@
 //                           weights, positive targets, per-window losses and the
 //                           state increments (prototype-EMA deltas f(a - P[c]) and
 //                           counts, num_zero / num_ones, windows)
-//   tune_dp_finish_kernel   the increments summed over the batch in a fixed order
-//                           (deterministic; the rank's buffer for the all-reduce)
+//                           summed over the batch in a fixed order by its last
+//                           workgroup (deterministic; the rank's buffer for the
+//                           all-reduce)
 //   tune_state_apply_kernel train.dp_state_update after the all-reduce: each
 //                           prototype moves by the mean of its deltas, counters
 //                           add, the factor decays once per window; and the AdamW
@@ -135,15 +136,52 @@ __global__ __launch_bounds__(kDsThreads) void tune_dataset_kernel(int H, int E, 
 // the lanes; lane 0 then folds them in host order, so each window's losses and
 // increments are summed exactly as the one-thread-per-window loop would
 // (train.loss_targets_dp's per-window order); windows are combined in a fixed
-// tree per workgroup and the workgroups in index order by the finish kernel.
+// tree per workgroup, and the LAST workgroup to finish (a device-scope
+// counter in the workspace, reset by it) sums the workgroups' partials in
+// index order into inc: the former tune_dp_finish_kernel's order, bit for bit,
+// one launch fewer on the C3 step's critical path.  With dpre != nullptr each
+// lane also writes its host's decoder pre-activation gradient [B][nop] (the
+// former tune_loss_kernel of pgp_tune.hip, same fp32 expressions, from the
+// mult / tgt values it has just written): CE(logits, y) * mult
+// (train.py:28-36) and the positive triplet MSE toward tgt through the
+// sigmoid (train.py:15-21; the negative terms are detached there).
 // ---------------------------------------------------------------------------
 constexpr int kWpb = 4, kTB = 64 * kWpb;
+__device__ __forceinline__ void dp_finish(int tid, int H, int B, int K, int nblk, const double* part, double* inc) {
+#pragma clang fp contract(off)
+  __shared__ double red[kDpInc][kTB];
+  const int t = tid;
+  double v[kDpInc] = {};
+  for (int i = t; i < nblk; i += kTB)
+    for (int k = 0; k < kDpInc; ++k)  // other workgroups' rows: coherent loads past this XCD's L2
+      v[k] += __hip_atomic_load(part + (long)i * kDpInc + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (int k = 0; k < kDpInc; ++k) red[k][t] = v[k];
+  __syncthreads();
+  for (int s = kTB / 2; s > 0; s >>= 1) {
+    if (t < s)
+      for (int k = 0; k < kDpInc; ++k) red[k][t] += red[k][t + s];
+    __syncthreads();
+  }
+  for (int k = t; k < 3 * K + 3; k += kTB) {
+    int src = -1;
+    if (k < 6) src = k;                                           // delta rows 0-2 (triplet classes)
+    else if (k >= 2 * K && k < 2 * K + 3) src = 6 + (k - 2 * K);  // counts 0-2
+    else if (k == 3 * K + 1) src = 9;                             // num_ones
+    double x = src >= 0 ? red[src][0] : 0.0;
+    if (k == 3 * K) x = (double)H * (double)B;  // num_zero: every host counts (train.py:31)
+    if (k == 3 * K + 2) x = (double)B;          // windows
+    inc[k] = x;
+  }
+}
+
 __global__ __launch_bounds__(kTB) void tune_targets_dp_kernel(int H, int B, const float* __restrict__ logits,
                                                               const float* __restrict__ protos,
                                                               const int* __restrict__ y, const int* __restrict__ cls,
                                                               const double* __restrict__ state, int K, double update_min,
                                                               float* __restrict__ mult, float* __restrict__ tgt,
-                                                              double* __restrict__ loss, double* __restrict__ part) {
+                                                              double* __restrict__ loss, double* __restrict__ part,
+                                                              unsigned* __restrict__ counter, double* __restrict__ inc,
+                                                              float* __restrict__ dpre, int nop) {
 #pragma clang fp contract(off)
   __shared__ double s_ce[kWpb][64], s_tl[kWpb][64], s_d0[kWpb][64], s_d1[kWpb][64];
   __shared__ int s_code[kWpb][64];  // -1: negative label; 0-2: class, +4 when the window's prototype moves
@@ -194,6 +232,12 @@ __global__ __launch_bounds__(kTB) void tune_targets_dp_kernel(int H, int B, cons
         tgt[2 * o + 1] = 0.f;
       }
       s_code[wv][lane] = code;
+      if (dpre) {  // tune_loss's function on the values just written (mult, tgt)
+        float* d = dpre + (long)b * nop;
+        const int cc = yi > 0 ? cls[o] : 0;
+        dpre_host(logits[2 * o], logits[2 * o + 1], yi, (float)mu, protos[2 * o], protos[2 * o + 1],
+                  yi > 0 ? (float)P[2 * cc] : 0.f, yi > 0 ? (float)P[2 * cc + 1] : 0.f, d + 2 * i, d + 2 * H + 2 * i);
+      }
     }
     __syncthreads();
     if (live && lane == 0) {  // host order, as the per-window loop
@@ -224,39 +268,22 @@ __global__ __launch_bounds__(kTB) void tune_targets_dp_kernel(int H, int B, cons
   __syncthreads();
   if (threadIdx.x < kDpInc) {  // fixed tree over the workgroup's windows
     const int k = threadIdx.x;
-    part[(long)blockIdx.x * kDpInc + k] = (red[0][k] + red[1][k]) + (red[2][k] + red[3][k]);
+    __hip_atomic_store(part + (long)blockIdx.x * kDpInc + k, (red[0][k] + red[1][k]) + (red[2][k] + red[3][k]),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-}
-
-// increments [3K+3] = delta [K][2], count [K], num_zero, num_ones, windows.
-// One workgroup: thread t sums the partials t, t+256, ... in order, then a
-// fixed tree over the threads (deterministic for a given B).
-__global__ __launch_bounds__(kTB) void tune_dp_finish_kernel(int H, int B, int K, int nblk,
-                                                             const double* __restrict__ part,
-                                                             double* __restrict__ inc) {
-#pragma clang fp contract(off)
-  __shared__ double red[kDpInc][kTB];
-  const int t = threadIdx.x;
-  double v[kDpInc] = {};
-  for (int i = t; i < nblk; i += kTB)
-    for (int k = 0; k < kDpInc; ++k) v[k] += part[(long)i * kDpInc + k];
-  for (int k = 0; k < kDpInc; ++k) red[k][t] = v[k];
+  // the last workgroup sums every workgroup's partials (release: this
+  // workgroup's row before its count; acquire: every row after the count)
+  __shared__ int s_last;
   __syncthreads();
-  for (int s = kTB / 2; s > 0; s >>= 1) {
-    if (t < s)
-      for (int k = 0; k < kDpInc; ++k) red[k][t] += red[k][t + s];
-    __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned nblk = gridDim.x;
+    const unsigned done = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = done == nblk - 1;
   }
-  for (int k = t; k < 3 * K + 3; k += kTB) {
-    int src = -1;
-    if (k < 6) src = k;                                           // delta rows 0-2 (triplet classes)
-    else if (k >= 2 * K && k < 2 * K + 3) src = 6 + (k - 2 * K);  // counts 0-2
-    else if (k == 3 * K + 1) src = 9;                             // num_ones
-    double x = src >= 0 ? red[src][0] : 0.0;
-    if (k == 3 * K) x = (double)H * (double)B;  // num_zero: every host counts (train.py:31)
-    if (k == 3 * K + 2) x = (double)B;          // windows
-    inc[k] = x;
-  }
+  __syncthreads();
+  if (!s_last) return;
+  dp_finish(threadIdx.x, H, B, K, (int)gridDim.x, part, inc);
+  if (threadIdx.x == 0) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
 }
 
 // One lane per independent value (K prototypes, the counters / factor, and
@@ -309,16 +336,17 @@ hipError_t launch_tune_dataset(int H, int E, int R, const double* series, const 
   return hipGetLastError();
 }
 
-long tune_dp_workspace_doubles(int B) { return (long)((B + kWpb - 1) / kWpb) * kDpInc; }
+// the finishing counter (slot 0: zero in a fresh workspace, reset by the last
+// workgroup of every launch), then the partials [nblk][kDpInc]
+long tune_dp_workspace_doubles(int B) { return (long)((B + kWpb - 1) / kWpb) * kDpInc + 1; }
 
 hipError_t launch_tune_targets_dp(int H, int K, int B, const float* logits, const float* protos, const int* y,
                                   const int* cls, const double* state, double update_min, float* mult, float* tgt,
-                                  double* loss, double* inc, double* ws, hipStream_t st) {
+                                  double* loss, double* inc, double* ws, hipStream_t st, float* dpre, int nop) {
   const int nblk = (B + kWpb - 1) / kWpb;
-  tune_targets_dp_kernel<<<nblk, kTB, 0, st>>>(H, B, logits, protos, y, cls, state, K, update_min, mult, tgt, loss, ws);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  tune_dp_finish_kernel<<<1, kTB, 0, st>>>(H, B, K, nblk, ws, inc);
+  unsigned* counter = reinterpret_cast<unsigned*>(ws);   // slot 0 (any batch), the partials after it
+  tune_targets_dp_kernel<<<nblk, kTB, 0, st>>>(H, B, logits, protos, y, cls, state, K, update_min, mult, tgt, loss,
+                                               ws + 1, counter, inc, dpre, nop);
   return hipGetLastError();
 }
 

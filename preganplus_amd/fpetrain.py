@@ -65,10 +65,10 @@ class FPETrainer:
         self.G = torch.zeros_like(self.P)
         self.m = torch.zeros_like(self.P)
         self.v = torch.zeros_like(self.P)
-        if state:   # AdamW state per parameter (a checkpoint's optimizer_state_dict)
-            m, v = self.m.cpu().numpy(), self.v.cpu().numpy()
-            for t in self.tensors:
-                s = state.get(t["name"])
+        if state:   # AdamW state per parameter INDEX: a checkpoint's optimizer_state_dict["state"]
+            m, v = self.m.cpu().numpy(), self.v.cpu().numpy()   # (torch's keys, as checkpoint() writes them)
+            for idx, t in enumerate(self.tensors):
+                s = state.get(idx)
                 if s:
                     m[t["offset"]:t["offset"] + t["n"]] = np.asarray(s["exp_avg"]).reshape(-1)
                     v[t["offset"]:t["offset"] + t["n"]] = np.asarray(s["exp_avg_sq"]).reshape(-1)

@@ -121,7 +121,9 @@ class PreGANPlusRecovery(_SaveGan, Recovery):
             folder = model_folder or "recovery/PreGANSrc/checkpointsplus"
             ck = os.path.join(folder, f"{self.env_name}_{self.model_name}.ckpt")
             if os.path.exists(ck):   # load_model + load_gan (utils.py:60-84): weights AND training state
-                weights, state = W.load_reference_checkpoints(folder, self.env_name, self.hosts, with_state=True)
+                fresh = lambda: W.torch_default_weights(self.hosts, seed=int(os.environ.get("PGP_INIT_SEED", 0)))
+                weights, state = W.load_reference_checkpoints(folder, self.env_name, self.hosts, with_state=True,
+                                                              gan_fresh=fresh)
                 extra = dict(state, **(extra or {}))
             else:
                 packaged = os.path.join(_DATA, f"{self.env_name}_{self.hosts}.npz")
@@ -592,13 +594,18 @@ class _GanCheckpointWriter:
         """Write what is queued, end the thread (idempotent)."""
         if self.stopping:
             return
+        on_writer = self.thread is threading.current_thread()
         try:
-            self.flush()
+            # on the writer thread itself (the plugin collected by a GC pass that
+            # runs there, e.g. while _write pickles): flush() would wait for this
+            # very thread; the loop writes what is queued before it sees stopping
+            if not on_writer:
+                self.flush()
         finally:
             with self.cv:
                 self.stopping = True
                 self.cv.notify_all()
-            if self.thread is not threading.current_thread():
+            if not on_writer:
                 self.thread.join()
             _LIVE_WRITERS.discard(self)
 
@@ -690,8 +697,11 @@ class PreGANRecovery(_SaveGan, Recovery):
             folder = model_folder or MODEL_FOLDER
             ck = os.path.join(folder, f"{self.env_name}_{self.model_name}.ckpt")
             if os.path.exists(ck):
+                # load_gan creates a new Gen / Disc for an absent file (utils.py:81-84): a folder
+                # holding only the FPE checkpoint (offline training, before the first train_gan)
+                fresh = lambda: W.torch_default_fpe_weights(self.hosts, seed=int(os.environ.get("PGP_INIT_SEED", 0)))
                 weights, state = W.load_reference_checkpoints(folder, self.env_name, self.hosts, encoder="FPE",
-                                                              with_state=True)
+                                                              with_state=True, gan_fresh=fresh)
                 extra = dict(state, **(extra or {}))
             else:
                 packaged = os.path.join(_DATA, f"pregan_{self.env_name}_{self.hosts}.npz")

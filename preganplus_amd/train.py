@@ -193,15 +193,15 @@ class Trainer:
         return c
 
     def _adam_desc(self, sel):
-        """ctypes descriptor array of an AdamW selection, built once per list
-        object (the selections are fixed lists held by their callers, or
-        ``trainable(section)``; the cache keeps each list alive, so no id is
-        reused)."""
-        c = self._desc_cache.get(id(sel))
-        if c is None or c[0] is not sel:
-            c = (sel, (_AdamTensor * len(sel))(*[_AdamTensor(t["offset"], t["n"], 1, 0.0, 0.0) for t in sel]))
-            self._desc_cache[id(sel)] = c
-        return c[1]
+        """ctypes descriptor array of an AdamW selection, cached by its
+        (offset, n) ranges: the same tensors give the same descriptor whatever
+        list object names them, and a list mutated in place gets a new one."""
+        key = ("desc",) + tuple((t["offset"], t["n"]) for t in sel)
+        c = self._desc_cache.get(key)
+        if c is None:
+            c = (_AdamTensor * len(sel))(*[_AdamTensor(t["offset"], t["n"], 1, 0.0, 0.0) for t in sel])
+            self._desc_cache[key] = c
+        return c
 
     # ---------------- ops ----------------
     def zero_grad(self, section: str):
@@ -1305,12 +1305,51 @@ def train_gan_batched(tr: Trainer, sim, envs, emb, sched, out=None, target=None,
         tr.adam_step_table("gen", tr.trainable("gen"), rows[1])
     return out, target
 
-# C3 issue order: the GAN step's launches are issued after the tuning
-# backward's (its stream still starts at the targets, gated by an event), so
-# the main stream has the backward queued while the host issues the GAN step:
-# H = 16 0.274 -> 0.263 ms, H = 50 neutral (A/B, profiles/r04/issue_order/).
-# PGP_C3_GAN_LATE=0 issues them before the backward (round 4's first order).
-_GAN_AFTER_BACKWARD = os.environ.get("PGP_C3_GAN_LATE", "1") == "1"
+class _OnlineTensor(ctypes.Structure):
+    _fields_ = [("offset", ctypes.c_longlong), ("n", ctypes.c_int), ("section", ctypes.c_int),
+                ("cond", ctypes.c_int), ("step", ctypes.c_double)]
+
+
+_vp, _dp = ctypes.c_void_p, ctypes.c_double
+
+
+class _OnlineDesc(ctypes.Structure):
+    """pgp_online_desc (include/preganplus.h)."""
+    _fields_ = ([(n, ctypes.c_int) for n in ("n_hosts", "n_env", "n_rows", "n_protos")]
+                + [(n, _vp) for n in ("series", "train_max", "sched", "envs", "P", "G", "exp_avg", "exp_avg_sq",
+                                      "tune_ws", "logits", "protos", "windows", "y", "cls", "state", "mult", "tgt",
+                                      "loss", "inc", "dp_ws", "adam_rows", "cond_steps", "gan_ws", "ns", "probs",
+                                      "emb", "sim_out", "target")]
+                + [("tensors", ctypes.POINTER(_OnlineTensor)), ("n_tensors", ctypes.c_int), ("n_cond", ctypes.c_int),
+                   ("lr", _dp * 3)]
+                + [(n, _dp) for n in ("weight_decay", "beta1", "beta2", "eps", "update_min", "decay")])
+
+
+_COLL_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p)
+ONLINE_STAGES = ("dataset", "embedding", "train_gan", "tune_model", "forward", "targets", "backward", "exchange",
+                 "apply_adamw", "main")
+
+
+def _bind_online(L):
+    if getattr(L, "_pgp_online_bound", False):
+        return
+    L.pgp_online_create.argtypes = [ctypes.POINTER(_OnlineDesc), ctypes.POINTER(ctypes.c_void_p)]
+    L.pgp_online_destroy.argtypes = [ctypes.c_void_p]
+    L.pgp_online_step.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, _COLL_FN, ctypes.c_void_p]
+    L.pgp_online_timing.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    L.pgp_online_stage_ms.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    L.pgp_online_steps.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+    for f in ("pgp_online_create", "pgp_online_destroy", "pgp_online_step", "pgp_online_timing",
+              "pgp_online_stage_ms", "pgp_online_steps"):
+        getattr(L, f).restype = ctypes.c_int
+    L._pgp_online_bound = True
+
+
+def _destroy_online(L, h):
+    try:
+        L.pgp_online_destroy(h)
+    except Exception:
+        pass
 
 
 class OnlineTrainStep:
@@ -1329,15 +1368,23 @@ class OnlineTrainStep:
          train_gan_batched``: device-simulated label, Disc step, Gen step);
       4. the tuning backward over the R*E windows, gradient / state all-reduce,
          state update and AdamW (``DPTuner``).
-    The GAN and tuning steps share no data, so 3 runs beside 4.  AdamW's
-    per-step scalars are read from fixed device rows written by ``prep()``
-    before each step, so every step issues the same launches: ``capture()``
-    records the step once as a HIP graph and ``run()`` replays it (world size
-    1; collectives stay eager).  ``issue()`` is the eager step (optional
-    ``stage`` / ``sub`` HIP-event lists as bench.py records them)."""
+    The GAN and tuning steps share no data, so 3 runs beside 4.
+
+    ``native`` (default): ``run()`` issues the whole step from ONE C-ABI call
+    (``pgp_online_step``, csrc/pgp_online.hip): the launches, the stream
+    fork / join and AdamW's per-step scalars (from step counts the library
+    keeps, ``sync()`` copies them back to the Trainer) come from C++, and the
+    data-parallel exchange calls back into ``_collective`` (torch.distributed
+    on the step's streams and groups) at its four points.
+    ``native=False``: the same step composed from the per-op calls in Python
+    (``issue()``; AdamW's scalars from fixed device rows written by
+    ``prep()``, so ``capture()`` can record it once as a HIP graph that
+    ``run()`` replays at world size 1) — the reference composition the native
+    step is tested against.  ``issue()`` takes optional ``stage`` / ``sub``
+    HIP-event lists as bench.py records them."""
 
     def __init__(self, tr: "Trainer", st: "TuneState", sim, series, train_max, sched, envs, R: int = 10,
-                 side=None, groups=(None, None), out=None):
+                 side=None, groups=(None, None), out=None, native: bool = True):
         self.tr, self.sim = tr, sim
         self.series, self.tmax = tr._dev(series, torch.float64), tr._dev(train_max, torch.float64)
         E = self.series.shape[0]
@@ -1358,7 +1405,103 @@ class OnlineTrainStep:
         self.rowD, self.rowG = self.rows_d.buffer(), self.rows_g.buffer()
         self._rows = (self.rowT, self.rowD, self.rowG)
         self.graph = None
-        self._gate = torch.cuda.Event()   # the targets are issued: the GAN stream may start
+        self._gate = torch.cuda.Event()   # the forward is issued: the GAN stream may start
+        self.native = bool(native)
+        self._h = None
+        if self.native:
+            self._create_native(sim)
+
+    # -- the native step (pgp_online_*) --
+    def _create_native(self, sim):
+        tr, tun, L = self.tr, self.tun, self.tr._L
+        _bind_online(L)
+        H, E, R, B = tr.H, self.E, self.R, self.B
+        wins, y, cls, _, allw = self.bufs
+        sel = [t for t in tr.tensors if t["trainable"]]
+        secs = {"transformer": 0, "gen": 1, "disc": 2}
+        self._tensors = (_OnlineTensor * len(sel))(*[
+            _OnlineTensor(t["offset"], t["n"], secs[t["section"]], int(t["name"] in DPTuner.COND and
+                                                                       t["section"] == "transformer"), t["step"])
+            for t in sel])
+        self._sel = sel
+        self.ns = torch.zeros((E, H, H), dtype=torch.float32, device=tr.device)
+        self.probs = torch.zeros((E, 2), dtype=torch.float32, device=tr.device)
+        self.gscr = torch.zeros((L.pgp_gan_workspace_len(H, E),), dtype=torch.float32, device=tr.device)
+        ptr = lambda t: ctypes.c_void_p(t.data_ptr())
+        d = _OnlineDesc()
+        d.n_hosts, d.n_env, d.n_rows, d.n_protos = H, E, R, tun.K
+        for name, t in (("series", self.series), ("train_max", self.tmax), ("sched", self.sched), ("envs", self.envs),
+                        ("P", tr.P), ("G", tr.G), ("exp_avg", tr.m), ("exp_avg_sq", tr.v), ("tune_ws", tr.ws),
+                        ("logits", tr.logits), ("protos", tr.protos), ("windows", allw), ("y", y), ("cls", cls),
+                        ("state", tun.state), ("mult", tun.mult), ("tgt", tun.tgt), ("loss", tun.loss),
+                        ("inc", tun.inc), ("dp_ws", tun.ws), ("adam_rows", self.rowT),
+                        ("cond_steps", tun.cond_steps), ("gan_ws", self.gscr), ("ns", self.ns),
+                        ("probs", self.probs), ("emb", self.emb), ("sim_out", self.sim_out),
+                        ("target", self.target)):
+            setattr(d, name, ptr(t))
+        d.tensors = self._tensors
+        d.n_tensors = len(sel)
+        d.n_cond = len(tun.cond)
+        d.lr = (_dp * 3)(tr.lrs["transformer"], tr.lrs["gen"], tr.lrs["disc"])
+        d.weight_decay, d.beta1, d.beta2, d.eps = tr.wd, tr.b1, tr.b2, tr.eps
+        d.update_min, d.decay = PROTO_UPDATE_MIN, PROTO_FACTOR_DECAY
+        if tr.cap < B + E or L.pgp_tune_workspace_len(H, B + E) > tr.ws.numel():
+            raise ValueError("trainer workspace smaller than the step's batch")
+        h = ctypes.c_void_p()
+        _native.check(L.pgp_online_create(ctypes.byref(d), ctypes.byref(h)), "pgp_online_create")
+        self._desc, self._h = d, h
+        self._fin = __import__("weakref").finalize(self, _destroy_online, L, h)
+        self._err = None
+        import torch.distributed as dist
+        multi = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+        self._cb = _COLL_FN(self._collective) if multi else _COLL_FN()
+        self._timing = False
+
+    def _collective(self, user, which, stream):
+        """pgp_online_step's exchange points (include/preganplus.h
+        PGP_COLL_*): the section's gradients (Disc, Gen: the GAN group, on the
+        GAN stream; Transformer: the tuning group, on the main stream) or the
+        state increments, summed over ranks in place."""
+        import torch.distributed as dist
+        try:
+            tr, tun = self.tr, self.tun
+            if which in (0, 1):
+                sec, grp, st = ("disc" if which == 0 else "gen"), self.gan_group, self._streams[1]
+                buf = tr.G[tr.sec_off[sec]:tr.sec_end[sec]]
+            else:
+                grp, st = tun.group, self._streams[0]
+                buf = tr.G[tr.sec_off["transformer"]:tr.sec_end["transformer"]] if which == 2 else tun.inc
+            with torch.cuda.stream(st):
+                dist.all_reduce(buf, group=grp)
+            return 0
+        except BaseException as e:   # surfaced by run() after the C call returns
+            self._err = e
+            return -1
+
+    def timing(self, on: bool):
+        """Record HIP events in the native steps that follow (stage_ms())."""
+        _native.check(self.tr._L.pgp_online_timing(self._h, int(on)), "pgp_online_timing")
+        self._timing = bool(on)
+
+    def stage_ms(self) -> dict:
+        """The last native step's spans in ms (ONLINE_STAGES)."""
+        ms = (ctypes.c_float * len(ONLINE_STAGES))()
+        _native.check(self.tr._L.pgp_online_stage_ms(self._h, ms), "pgp_online_stage_ms")
+        return dict(zip(ONLINE_STAGES, list(ms)))
+
+    def sync(self):
+        """The native step's AdamW step counts back into the Trainer's tensor
+        records (the prototype decoder's from the device), the tuning state
+        into the TuneState the step was built with."""
+        if not self.native:
+            return
+        n = len(self._sel)
+        out = (ctypes.c_double * n)()
+        _native.check(self.tr._L.pgp_online_steps(self._h, out, n), "pgp_online_steps")
+        cs = self.tun.cond_steps.cpu().numpy()
+        tsel = self.tun.sel
+        for t, v in zip(self._sel, out):
+            t["step"] = float(cs[self.tun.cond.index(tsel.index(t))]) if v < 0 else float(v)
 
     def prep(self):
         """Host bookkeeping of the next step (AdamW rows).  Eager steps read
@@ -1371,6 +1514,9 @@ class OnlineTrainStep:
                           self.rows_g.next_row(self.rowG))
 
     def issue(self, stage=None, sub=None):
+        if self.native:
+            raise RuntimeError("native OnlineTrainStep: run() issues the step (construct with native=False "
+                               "for the Python composition)")
         from .model import embedding
         tr, B, E = self.tr, self.B, self.E
         main = torch.cuda.current_stream(tr.device)
@@ -1382,7 +1528,8 @@ class OnlineTrainStep:
 
         gate = self._gate
 
-        def detect_gan():   # once the targets are issued: beside the tuning backward
+        def detect_gan():   # once the forward is issued: beside the targets and the tuning backward
+            gate.record(main)
             side.wait_event(gate)
             with torch.cuda.stream(side):
                 if stage is not None:
@@ -1396,21 +1543,16 @@ class OnlineTrainStep:
                 if stage is not None:
                     stage[3].record(side)
 
-        late = _GAN_AFTER_BACKWARD
-
-        def targets_issued():
-            gate.record(main)
-            if not late:
-                detect_gan()
-
         self.tun.step(self.bufs[4], y, cls, mark=(lambda k: sub[k].record(main)) if sub is not None else None,
-                      before_backward=targets_issued, after_backward=detect_gan if late else None,
-                      row=self._rows[0])
+                      after_forward=detect_gan, row=self._rows[0])
         main.wait_stream(side)
         rec(4)
 
     def capture(self):
-        """Record one step as a HIP graph on the current (non-default) stream."""
+        """Record one step (the Python composition) as a HIP graph on the
+        current (non-default) stream."""
+        if self.native:
+            raise RuntimeError("capture() records the Python composition (native=False)")
         main = torch.cuda.current_stream(self.tr.device)
         torch.cuda.synchronize(self.tr.device)
         g = torch.cuda.CUDAGraph()
@@ -1421,6 +1563,17 @@ class OnlineTrainStep:
         self.graph = g
 
     def run(self):
+        if self.native:
+            main = torch.cuda.current_stream(self.tr.device)
+            side = self.side if self.side is not None else main
+            self._streams = (main, side)
+            rc = self.tr._L.pgp_online_step(self._h, ctypes.c_void_p(main.cuda_stream),
+                                            ctypes.c_void_p(side.cuda_stream), self._cb, None)
+            if self._err is not None:
+                e, self._err = self._err, None
+                raise RuntimeError("pgp_online_step: collective failed") from e
+            _native.check(rc, "pgp_online_step")
+            return
         self.prep()
         if self.graph is not None:
             self.graph.replay()

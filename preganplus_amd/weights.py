@@ -280,7 +280,8 @@ def weights_checksum(weights):
 _BUFFERS = {"transformer": ("pos_encoder.pe",), "fpe": (), "gen": (), "disc": ()}   # state_dict entries that are not parameters
 
 
-def load_reference_checkpoints(model_dir, env_name="simulator", H=16, encoder="Transformer", with_state=False):
+def load_reference_checkpoints(model_dir, env_name="simulator", H=16, encoder="Transformer", with_state=False,
+                               gan_fresh=None):
     """Read ``{env}_Transformer_{H}.ckpt``/``Gen``/``Disc`` from a COSCO tree
     (``checkpointsplus/``; format ``utils.py:53-58``) with the safe loader.
 
@@ -291,16 +292,29 @@ def load_reference_checkpoints(model_dir, env_name="simulator", H=16, encoder="T
     order = the state_dict order without buffers), ``meta/{sec}/epoch`` and the
     Gen checkpoint's ``accuracy_list`` (the one PreGANPlusRecovery keeps,
     ``PreGANPlus.py:32-34``) as ``meta/gen/accuracy_list`` (flat) +
-    ``meta/gen/accuracy_list_lens``."""
-    def ld(name):
-        return _safe_load(os.path.join(model_dir, f"{env_name}_{name}_{H}.ckpt"))
+    ``meta/gen/accuracy_list_lens``.
 
-    t, g, d = ld(encoder), ld("Gen"), ld("Disc")
+    ``gan_fresh`` ({"gen": ..., "disc": ...} weights of a new GAN, or a
+    callable returning them, called only when needed): a Gen or
+    Disc checkpoint that is absent is replaced by that new model, as
+    ``load_gan`` -> ``load_model`` creates one (utils.py:76-78, 81-84: Gen
+    epoch -1 and an empty accuracy_list, no optimizer state); without it an
+    absent file raises."""
+    def path(name):
+        return os.path.join(model_dir, f"{env_name}_{name}_{H}.ckpt")
+
+    t = _safe_load(path(encoder))
+    new_model = {"epoch": -1, "accuracy_list": [], "model_state_dict": None}
+    g, d = ({**new_model, "fresh": n} if gan_fresh is not None and not os.path.exists(path(n)) else _safe_load(path(n))
+            for n in ("Gen", "Disc"))
     tsec = "fpe" if encoder == "FPE" else "transformer"
+    if g.get("fresh") or d.get("fresh"):
+        gan_fresh = gan_fresh() if callable(gan_fresh) else gan_fresh
+    sd = lambda ck, sec: (dict(gan_fresh[sec]) if ck.get("fresh") else _conv_sd(ck["model_state_dict"]))
     weights = {
         tsec: _conv_sd(t["model_state_dict"]),
-        "gen": _conv_sd(g["model_state_dict"]),
-        "disc": _conv_sd(d["model_state_dict"]),
+        "gen": sd(g, "gen"),
+        "disc": sd(d, "disc"),
         "prototypes": np.stack([p.detach().cpu().numpy() for p in t["model_prototypes"]]),
         "meta": {"epoch": t["epoch"], "gan_epoch": g["epoch"]},
     }
@@ -308,7 +322,7 @@ def load_reference_checkpoints(model_dir, env_name="simulator", H=16, encoder="T
         return weights
     extra = {}
     for sec, ck in ((tsec, t), ("gen", g), ("disc", d)):
-        extra.update(_ck_state(sec, ck))
+        extra.update({f"meta/{sec}/epoch": np.int64(-1)} if ck.get("fresh") else _ck_state(sec, ck))
     extra.update(accuracy_list_to_arrays(g["accuracy_list"], "meta/gen/accuracy_list"))
     # the encoder checkpoint's own accuracy_list (train_model's, PreGANPlus.py:41-49): kept
     # apart so an explicit full save writes the encoder checkpoint as load_model read it

@@ -42,3 +42,59 @@ def test_world_size_mismatch_fails():
     p = _run(["--config", "ranks", "--gpus", "3"], {"WORLD_SIZE": "2", "RANK": "0"})
     assert p.returncode != 0
     assert "world size 2 != --gpus 3" in p.stderr
+
+
+def _c3dp_rank(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    sys.path.insert(0, ROOT)
+    import bench
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        buf = torch.ones(4096)
+        calls = []
+
+        def make_step(H, E, rk, dev):   # the exchange pattern of a step, on CPU tensors
+            def run():
+                dist.all_reduce(buf)
+                calls.append(1)
+
+            def exchange_ms():
+                import time
+                t0 = time.perf_counter()
+                dist.all_reduce(buf)
+                return (time.perf_counter() - t0) * 1e3
+            return run, exchange_ms
+        rec = bench.c3_dp_record(world, rank, torch.device("cpu"), steps=4, warmup=1, make_step=make_step)
+        q.put((rank, rec, len(calls)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_c2_line_carries_c3_dp_at_world_gt_1():
+    """At world > 1 the default (c2) line gets the data-parallel C3 sub-record
+    (the tuning all-reduce north_star names; c2 itself has no data-path
+    collective); at world 1 it does not.  The record's timing / exchange /
+    backend logic runs over two gloo ranks with a stand-in step."""
+    import multiprocessing as mp
+    sys.path.insert(0, ROOT)
+    import bench
+    assert bench.c2_subrecords(1) == () and bench.c2_subrecords(2) == ("c3_dp",)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 32500 + os.getpid() % 1000
+    procs = [ctx.Process(target=_c3dp_rank, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=120) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    for rank, rec, ncalls in got:
+        assert ncalls == 1 + 4                      # warmup + timed steps, on every rank
+        assert rec["backend"] == "gloo" and rec["n_gpus"] == 2 and rec["steps"] == 4
+        assert rec["ms_per_step"] > 0 and rec["all_reduce_ms"] > 0 and rec["windows_per_s"] > 0
+    # the timing is the max over ranks: both ranks report the same numbers
+    assert got[0][1]["ms_per_step"] == got[1][1]["ms_per_step"]

@@ -38,7 +38,7 @@ def test_prefix_backward_equals_backward_of_the_prefix(H):
         a.tune_backward(B + E + 1, y, mult, tgt)
 
 
-def _online(H, E, seed=5):
+def _online(H, E, seed=5, native=False):
     from preganplus_amd import simulate as SIM
     from preganplus_amd import train as TR
     from preganplus_amd import weights as W
@@ -52,7 +52,8 @@ def _online(H, E, seed=5):
     s[np.arange(E)[:, None], np.arange(H)[None, :], rng.integers(0, H, size=(E, H))] = 1.0
     envs = SIM.synth_envs(E, H, seed=seed)
     side = torch.cuda.Stream()
-    step = TR.OnlineTrainStep(tr, st, SIM.Simulation(H, device="cuda"), series, tmax, s, envs, side=side)
+    step = TR.OnlineTrainStep(tr, st, SIM.Simulation(H, device="cuda"), series, tmax, s, envs, side=side,
+                              native=native)
     return tr, step
 
 
@@ -80,6 +81,51 @@ def test_online_step_graph_replay_equals_eager(H):
         assert t_a["step"] == t_b["step"], t_a["name"]
     # the GAN sections stepped three times, as adam_step would have counted
     assert {t["step"] for t in tr_a.tensors if t["section"] in ("gen", "disc") and t["trainable"]} == {3.0}
+
+
+@pytest.mark.parametrize("H", [16, 50])
+def test_native_step_equals_python_composition(H):
+    """pgp_online_step (the whole step issued from C++, AdamW's scalars from
+    the library's step counts) == the step composed from the per-op C-ABI
+    calls in Python (AdamW's scalars from the host tables), three steps each:
+    every weight, AdamW moment, the tuning state, the GAN labels and scores,
+    the per-window losses and the step counts identical."""
+    main = torch.cuda.Stream()
+    with torch.cuda.stream(main):
+        tr_a, sa = _online(H, 6, native=False)
+        tr_b, sb = _online(H, 6, native=True)
+        for _ in range(3):
+            sa.run()
+            sb.run()
+        torch.cuda.synchronize()
+    for x, y in ((tr_a.P, tr_b.P), (tr_a.m, tr_b.m), (tr_a.v, tr_b.v), (sa.tun.state, sb.tun.state),
+                 (sa.target, sb.target), (sa.sim_out, sb.sim_out), (sa.tun.loss, sb.tun.loss),
+                 (sa.tun.cond_steps, sb.tun.cond_steps), (sa.emb, sb.emb)):
+        np.testing.assert_array_equal(x.cpu().numpy(), y.cpu().numpy())
+    sa.tun.sync(__import__("preganplus_amd.train", fromlist=["x"]).TuneState(np.zeros((H, 2))))
+    sb.sync()
+    for t_a, t_b in zip(tr_a.tensors, tr_b.tensors):
+        assert t_a["step"] == t_b["step"], t_a["name"]
+    assert {t["step"] for t in tr_b.tensors if t["section"] in ("gen", "disc") and t["trainable"]} == {3.0}
+
+
+def test_native_step_stage_timing():
+    """pgp_online_timing / pgp_online_stage_ms: every span is non-negative and
+    the main stream's span covers its stages."""
+    from preganplus_amd import train as TR
+    main = torch.cuda.Stream()
+    with torch.cuda.stream(main):
+        _, sb = _online(16, 4, native=True)
+        sb.run()
+        sb.timing(True)
+        sb.run()
+        ms = sb.stage_ms()
+        sb.timing(False)
+    assert set(ms) == set(TR.ONLINE_STAGES)
+    assert all(v >= 0 for v in ms.values())
+    assert ms["main"] + 1e-3 >= ms["dataset"] + ms["tune_model"] - 1e-2
+    with pytest.raises(RuntimeError):
+        sb.issue()
 
 
 def test_section_rows_match_adam_step():

@@ -107,3 +107,120 @@ def test_two_rank_dp_steps_equal_full_batch():
         assert np.all(np.abs(P2[sl][noise] - P1[sl][noise]) <= 2 * lr)
     np.testing.assert_allclose(pr2, pr1, rtol=1e-13, atol=1e-15)
     assert (nz2, no2) == (nz1, no1) and abs(f2 - f1) <= 1e-15
+
+
+# ---------------------------------------------------------------------------
+# The C3 step itself at world size 2: OnlineTrainStep (native: pgp_online_step
+# with the collectives called back into torch.distributed), two streams per
+# rank, the GAN stream shared as the tuning backward's side stream
+# (pgp_tune_set_side_stream, as bench.py does at world > 1) and the two
+# process groups (train.dp_groups).  H = 50 with 48 environments per rank: 72 k
+# tokens, above the side stream's threshold, so the backward's side work
+# really runs on the shared stream.  One step on each half == one process on
+# the concatenated batch.
+# ---------------------------------------------------------------------------
+HS, ES = 50, 96
+
+
+def _c3_inputs():
+    import bench
+    from preganplus_amd import simulate as SIM
+    series, tmax = bench.synth_series(ES, HS, 21, 10)
+    rng = np.random.default_rng(21)
+    s = np.zeros((ES, HS, HS), np.float32)
+    s[np.arange(ES)[:, None], np.arange(HS)[None, :], rng.integers(0, HS, size=(ES, HS))] = 1.0
+    return series, tmax, s, SIM.synth_envs(ES, HS, seed=21)
+
+
+def _c3_run(sl, world):
+    from preganplus_amd import _native
+    from preganplus_amd import simulate as SIM
+    from preganplus_amd import train as TR
+    from preganplus_amd import weights as W
+    import ctypes
+    series, tmax, s, envs = _c3_inputs()
+    w = W.synth_weights(HS, seed=4)
+    E = len(range(ES)[sl])
+    main = torch.cuda.Stream()
+    side = torch.cuda.Stream()
+    L = _native.lib()
+    L.pgp_tune_set_side_stream.argtypes = [ctypes.c_void_p]
+    if world > 1:
+        _native.check(L.pgp_tune_set_side_stream(ctypes.c_void_p(side.cuda_stream)), "pgp_tune_set_side_stream")
+    try:
+        with torch.cuda.stream(main):
+            tr = TR.Trainer(HS, w, max_batch=11 * E)
+            st = TR.TuneState(w["prototypes"])
+            step = TR.OnlineTrainStep(tr, st, SIM.Simulation(HS, device=tr.device), series[sl], tmax, s[sl], envs[sl],
+                                      side=side, groups=TR.dp_groups())
+            step.run()
+            torch.cuda.synchronize()
+            step.sync()
+            return (tr.P.cpu().numpy(), step.tun.state.cpu().numpy(), step.target.cpu().numpy(),
+                    step.sim_out.cpu().numpy(), [t["step"] for t in tr.tensors])
+    finally:
+        L.pgp_tune_set_side_stream(None)
+
+
+def _c3_rank(rank, world, port, q):
+    import sys
+    import torch.distributed as dist
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    try:
+        per = ES // world
+        P, state, target, sim_out, steps = _c3_run(slice(rank * per, (rank + 1) * per), world)
+        got = [None] * world
+        dist.all_gather_object(got, (target, sim_out))
+        if rank == 0:
+            q.put((P, state, np.concatenate([g[0] for g in got]), np.concatenate([g[1] for g in got]), steps))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_online_step_two_ranks_equal_full_batch():
+    import torch.multiprocessing as mp
+    from preganplus_amd import train as TR
+    from preganplus_amd import weights as W
+    from tests.test_gpu_train import key_bias_mask
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 33500 + os.getpid() % 1000
+    procs = [ctx.Process(target=_c3_rank, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        P2, st2, tg2, so2, steps2 = q.get(timeout=240)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    P1, st1, tg1, so1, steps1 = _c3_run(slice(0, ES), 1)
+    # the GAN labels and scores of every environment: the step-start GAN, per environment
+    np.testing.assert_array_equal(tg2, tg1)
+    np.testing.assert_array_equal(so2, so1)
+    assert steps2 == steps1
+    K = (st1.size - 3) // 2
+    # prototypes: the deltas f (a - P) come from the forward's prototype outputs a, whose
+    # decoder split-K grouping depends on the batch (fp32 rounding apart, as the gradients)
+    np.testing.assert_allclose(st2[:2 * K], st1[:2 * K], rtol=1e-7, atol=1e-9)
+    assert st2[2 * K + 1] == st1[2 * K + 1] and st2[2 * K + 2] == st1[2 * K + 2]      # num_zero, num_ones
+    assert abs(st2[2 * K] - st1[2 * K]) <= 1e-15                                       # factor
+    tr = TR.Trainer(HS, W.synth_weights(HS, seed=4))
+    for t in tr.tensors:
+        if not t["trainable"]:
+            continue
+        sl = slice(t["offset"], t["offset"] + t["n"])
+        lr = tr.lrs[t["section"]]
+        d = np.abs(P2[sl] - P1[sl])
+        # one AdamW step from zero moments moves each entry by ~lr * sign(g): the
+        # two runs' gradients differ by fp32 summation grouping only, so the
+        # entries agree to rounding except where g is rounding noise (<= 2 lr)
+        assert np.all(d <= 2 * lr + 1e-6), (t["name"], float(d.max()))
+        noise = key_bias_mask(t["name"], t["n"], HS)    # exact gradient 0: rounding noise on both sides
+        assert np.mean((d <= 1e-6 + 1e-5 * np.abs(P1[sl]))[~noise]) >= 0.99, t["name"]

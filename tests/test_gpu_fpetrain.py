@@ -105,7 +105,81 @@ def test_fpe_offline_training_epochs_match_reference():
         assert not fails, (ep, fails)
         asc, csc = ft.accuracy(st, wins, z[f"ep{ep}/h0_accuracy"], anom, cls)
         assert asc == pytest.approx(float(z[f"ep{ep}/ascore"]), abs=1.0 / (16 * 24) + 1e-12)
-        assert csc == pytest.approx(float(z[f"ep{ep}/cscore"]), abs=0.05)
+        _cscore_within_decision_bounds(ft, st, z, ep, wins, anom, cls, csc)
+
+
+def _cscore_within_decision_bounds(ft, st, z, ep, wins, anom, cls, csc):
+    """class_accuracy (train.py:75-92) counts, per positive host, whether its
+    prototype output is closest to its own class.  The device model is the
+    reference's up to fp32 training, so a host's verdict may differ only where
+    the reference's own distance margin is inside what that difference can
+    move: |d_k(a') - d_k(a)| <= |a' - a|_inf * (|a - P_k|_1 + |a' - a|_1 / 2)
+    per distance (d_k = mean over the 2 dims of (a - P_k)^2), plus the device
+    prototypes' deviation from the reference's.  The reference's forward is
+    restated in fp64 (oracle, pinned) on ITS epoch-end weights and the recorded
+    GRU states; its CScore must equal the fixture's, and the device CScore must
+    equal the reference's with exactly the in-bound flips applied."""
+    from preganplus_amd import train as TR
+    n, H = wins.shape[0], 16
+    fw = {k[len(f"ep{ep}/p/"):]: torch.tensor(z[k]) for k in z.files if k.startswith(f"ep{ep}/p/")}
+    h0 = z[f"ep{ep}/h0_accuracy"]
+    with torch.no_grad():
+        rp, rq = TO.fpe_t(fw, torch.tensor(wins), torch.tensor(h0))
+    rp, rq = rp.numpy().reshape(n, H, 2), rq.numpy().reshape(n, H, 2)
+    Pref = np.asarray(z[f"ep{ep}/prototypes"], dtype=np.float64)[:3]
+    _, csc_ref = TR.accuracy_scores(rp, rq, anom, cls, Pref)
+    assert csc_ref == pytest.approx(float(z[f"ep{ep}/cscore"]), rel=1e-12, abs=1e-12)
+    _, dq = ft.forward_many(wins, h0)
+    P = np.asarray(st.protos, dtype=np.float64)[:3]
+
+    def hits(q, PP):
+        d = np.mean((q[:, :, None, :] - PP[None, None]) ** 2, axis=-1)       # [n,H,3]
+        c = np.clip(cls, 0, 2)
+        pos = np.take_along_axis(d, c[..., None], -1)[..., 0]
+        negs = np.where(np.arange(3)[None, None] == c[..., None], np.inf, d).min(-1)
+        return (anom > 0) & (pos <= negs), negs - pos, d
+
+    h_ref, margin, d_ref = hits(rq, Pref)
+    h_dev, _, _ = hits(dq, P)
+    da = np.abs(dq - rq).max(-1)                                                # per host, inf-norm
+    dP = np.abs(P - Pref).max()
+    span = np.abs(rq[:, :, None, :] - Pref[None, None]).sum(-1).max(-1)        # max_k |a - P_k|_1
+    bound = 2 * ((da + dP) * (span + (da + dP)))                               # pos and neg both move
+    flip = h_ref != h_dev
+    assert np.all(np.abs(margin[flip]) <= bound[flip]), (np.abs(margin[flip]), bound[flip])
+    # the device score is the reference's with those flips: the count is exact
+    cc, tot = 0.0, 0
+    for i in range(n):
+        npos = int(np.sum(anom[i] > 0))
+        if npos:
+            tot += 1
+            cc += int(np.sum(h_dev[i])) / (1e-4 + npos)
+    assert csc == pytest.approx(cc / tot, rel=1e-12)
+    assert int(flip.sum()) <= max(2, int((np.abs(margin) <= bound).sum()))
+
+
+def test_fpe_optimizer_state_round_trip():
+    """FPETrainer(state=...) restores the AdamW moments and step counts that
+    checkpoint() writes (torch's optimizer_state_dict: keyed by parameter
+    index): a restored trainer's next step equals the original's."""
+    from preganplus_amd import fpetrain as FT
+    from preganplus_amd import train as TR
+    z, init = _fixture()
+    wins, anom, cls = z["wins"][:6], z["anom"][:6], z["cls"][:6]
+    h0 = z["ep0/h0_backprop"][:6]
+    a = FT.FPETrainer(init)
+    st = TR.TuneState(z["init/prototypes"], 0.2)
+    a.backprop(st, wins[:4], h0[:4], anom[:4], cls[:4])
+    ck = a.checkpoint(0, [], st.protos)
+    b = FT.FPETrainer({k: np.asarray(v) for k, v in ck["model_state_dict"].items()},
+                      state=ck["optimizer_state_dict"]["state"])
+    assert [t["step"] for t in b.tensors] == [t["step"] for t in a.tensors] and a.tensors[0]["step"] > 0
+    np.testing.assert_array_equal(b.m.cpu().numpy(), a.m.cpu().numpy())
+    np.testing.assert_array_equal(b.v.cpu().numpy(), a.v.cpu().numpy())
+    st2 = TR.TuneState(st.protos, st.factor)
+    a.backprop(st, wins[4:], h0[4:], anom[4:], cls[4:])
+    b.backprop(st2, wins[4:], h0[4:], anom[4:], cls[4:])
+    np.testing.assert_array_equal(b.P.cpu().numpy(), a.P.cpu().numpy())
 
 
 def test_pregan_new_model_trains_offline(tmp_path, monkeypatch):
@@ -131,3 +205,10 @@ def test_pregan_new_model_trains_offline(tmp_path, monkeypatch):
         np.testing.assert_array_equal(np.asarray(v), fw[k])
     assert rec.epoch == -1            # a new GAN (load_gan without checkpoints)
     np.testing.assert_array_equal(rec.weights["fpe"]["encoder.0.weight"], fw["encoder.0.weight"])
+    # the folder now holds the FPE checkpoint and no GAN ones (training=False never saves
+    # them): a second plugin loads the trained FPE and, as load_gan does for absent files
+    # (utils.py:81-84), a new GAN at epoch -1
+    rec2 = RC.PreGANRecovery(16, "framework", training=True, model_folder=str(tmp_path / "ck"))
+    assert rec2.epoch == -1 and rec2.accuracy_list == []
+    np.testing.assert_array_equal(rec2.weights["fpe"]["encoder.0.weight"], fw["encoder.0.weight"])
+    np.testing.assert_array_equal(rec2.weights["gen"]["delta.0.weight"], rec.weights["gen"]["delta.0.weight"])

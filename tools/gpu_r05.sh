@@ -1,0 +1,303 @@
+#!/bin/bash
+# Round-5 GPU session steps.  usage: tools/gpu_r05.sh TAG STEP...
+#   tests   GPU suite (+ smoke)
+#   c2      C2 line (CPU baseline included) + rocprofv3 kernel stats
+#   c2pmc   C2 FETCH_SIZE / WRITE_SIZE passes (traffic of K1, K2, K2b, K3)
+#   c2stall C2 stall / MFMA-busy passes (K2, K3)
+#   fleet   C5 line + FETCH / WRITE passes at its batch
+#   tune    C3 lines (H=50, H=16) + rocprofv3 kernel stats of H=50
+#   tunepmc C3 stall passes (H=50)
+#   graphc  HIP graph branch concurrency / launch-cost probe
+#   others  C4, C1, loop lines
+# every GPU step runs under its own timeout; the script stops at the first failure
+set -u
+cd "$GRAFT_REPO_ROOT"
+T=${1:?tag}
+shift
+OUT=gpurun_out/$T
+mkdir -p $OUT
+export TMPDIR=/tmp
+run() {  # run NAME SECONDS CMD...
+  local name=$1 secs=$2
+  shift 2
+  echo "[$name] $(date +%T) start"
+  timeout -k 10 $secs "$@" > $OUT/$name.out 2> $OUT/$name.err
+  local rc=$?
+  echo "[$name] $(date +%T) rc=$rc"
+  if [ $rc -ne 0 ]; then tail -20 $OUT/$name.err; tail -5 $OUT/$name.out; exit $rc; fi
+}
+pmc() {  # pmc NAME COUNTERS BENCH_ARGS...
+  local name=$1 ctr=$2
+  shift 2
+  echo "[$name] $(date +%T) start"
+  timeout -s KILL 120 rocprofv3 --pmc $ctr -d $OUT/$name -o run --output-format csv -- python3 bench.py "$@" \
+    > $OUT/$name.log 2>&1
+  local rc=$?
+  echo "[$name] $(date +%T) rc=$rc"
+  if [ $rc -ne 0 ]; then tail -5 $OUT/$name.log; exit $rc; fi
+}
+STALL1="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_MFMA"
+STALL2="SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE"
+for step in "$@"; do
+  case $step in
+    tests)
+      run gpu_tests 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread
+      tail -2 $OUT/gpu_tests.out
+      run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+      ;;
+    ttrain)
+      run t_train 600 python -u -m pytest tests/test_gpu_train.py tests/test_gpu_bench_modes.py tests/test_gpu_dist.py -x -v -p no:cacheprovider --timeout 300 --timeout-method thread
+      tail -2 $OUT/t_train.out
+      ;;
+    tc3)
+      run t_c3 600 python -u -m pytest tests/test_gpu_c3step.py tests/test_gpu_tunedp.py tests/test_gpu_dist.py tests/test_gpu_plugin_graphs.py tests/test_gpu_train.py -x -v -p no:cacheprovider --timeout 300 --timeout-method thread
+      tail -2 $OUT/t_c3.out
+      ;;
+    tfpe)
+      run t_fpe 600 python -u -m pytest tests/test_gpu_fpetrain.py tests/test_gpu_checkpoint.py -v -p no:cacheprovider --timeout 300 --timeout-method thread
+      tail -2 $OUT/t_fpe.out
+      ;;
+    c2)
+      run c2 400 python3 -u bench.py
+      run prof_c2 240 rocprofv3 --kernel-trace --stats -d $OUT/prof_c2 -o c2 --output-format csv -- python3 bench.py --steps 60 --warmup 10 --no-cpu-baseline
+      ;;
+    c2pmc)
+      pmc c2pmc1 FETCH_SIZE --steps 3 --warmup 1 --no-cpu-baseline
+      pmc c2pmc2 WRITE_SIZE --steps 3 --warmup 1 --no-cpu-baseline
+      ;;
+    c2stall)
+      pmc c2stall1 "$STALL1" --steps 3 --warmup 1 --no-cpu-baseline
+      pmc c2stall2 "$STALL2" --steps 3 --warmup 1 --no-cpu-baseline
+      ;;
+    fleet)
+      run fleet 400 python3 -u bench.py --config fleet --steps 100 --warmup 5
+      pmc fleetpmc1 FETCH_SIZE --config fleet --steps 3 --warmup 1 --no-cpu-baseline
+      pmc fleetpmc2 WRITE_SIZE --config fleet --steps 3 --warmup 1 --no-cpu-baseline
+      ;;
+    tune)
+      run tune50 400 python3 -u bench.py --config tune --hosts 50 --steps 50 --warmup 5
+      run tune16 400 python3 -u bench.py --config tune --hosts 16 --steps 50 --warmup 5
+      run prof_tune 240 rocprofv3 --kernel-trace --stats -d $OUT/prof_tune -o tune --output-format csv -- python3 bench.py --config tune --hosts 50 --steps 60 --warmup 10 --no-cpu-baseline
+      run prof_tune16 240 rocprofv3 --kernel-trace --stats -d $OUT/prof_tune16 -o tune --output-format csv -- python3 bench.py --config tune --hosts 16 --steps 60 --warmup 10 --no-cpu-baseline
+      ;;
+    tunepmc)
+      pmc tunestall1 "$STALL1" --config tune --hosts 50 --steps 3 --warmup 1 --no-cpu-baseline
+      pmc tunestall2 "$STALL2" --config tune --hosts 50 --steps 3 --warmup 1 --no-cpu-baseline
+      ;;
+    graphc)
+      run graphc 120 python3 -u tools/graph_concurrency.py
+      cat $OUT/graphc.out
+      ;;
+    abtune)
+      run ab16 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 16 --steps 100 --warmup 10 --no-cpu-baseline" base= side0=PGP_TUNE_SIDE_STREAM=0 eager=PGP_BENCH_GRAPH=0 res16=PGP_GAN_RESERVED_CUS=16
+      grep median $OUT/ab16.out
+      run ab50 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" base= side0=PGP_TUNE_SIDE_STREAM=0 eager=PGP_BENCH_GRAPH=0 res16=PGP_GAN_RESERVED_CUS=16 res4=PGP_GAN_RESERVED_CUS=4
+      grep median $OUT/ab50.out
+      ;;
+    abtune2)
+      run ab16b 600 python3 -u tools/ab_bench.py --rounds 4 --args "--config tune --hosts 16 --steps 100 --warmup 10 --no-cpu-baseline" graph= graph_side0=PGP_TUNE_SIDE_STREAM=0 eager=PGP_BENCH_GRAPH=0 eager_side0=PGP_BENCH_GRAPH=0,PGP_TUNE_SIDE_STREAM=0
+      grep median $OUT/ab16b.out
+      run ab50b 600 python3 -u tools/ab_bench.py --rounds 4 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" graph= graph_side0=PGP_TUNE_SIDE_STREAM=0 eager=PGP_BENCH_GRAPH=0 eager_side0=PGP_BENCH_GRAPH=0,PGP_TUNE_SIDE_STREAM=0
+      grep median $OUT/ab50b.out
+      ;;
+    abdma)
+      run abc2 600 python3 -u tools/ab_bench.py --rounds 3 --args "--steps 100 --warmup 10 --no-cpu-baseline" new= old=PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_olddma.so
+      grep median $OUT/abc2.out
+      ;;
+    abdw)
+      run abdw 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" base= dw64=PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_dw64.so dw64a=PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_dw64a.so
+      grep median $OUT/abdw.out
+      run prof_dw 240 rocprofv3 --kernel-trace --stats -d $OUT/prof_dw -o tune --output-format csv -- python3 bench.py --config tune --hosts 50 --steps 30 --warmup 5 --no-cpu-baseline
+      PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_dw64a.so run prof_dw64a 240 rocprofv3 --kernel-trace --stats -d $OUT/prof_dw64a -o tune --output-format csv -- python3 bench.py --config tune --hosts 50 --steps 30 --warmup 5 --no-cpu-baseline
+      ;;
+    abprev)
+      run abp50 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" new= prev=PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_prev.so
+      grep median $OUT/abp50.out
+      run abp16 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 16 --steps 100 --warmup 10 --no-cpu-baseline" new= prev=PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_prev.so
+      grep median $OUT/abp16.out
+      ;;
+    abpp)
+      run pp_quick_base 180 python -u -m pytest tests/test_gpu_parity.py -k "not census" -x -q -p no:cacheprovider --timeout 120 --timeout-method thread
+      PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_k2pp.so run pp_quick 180 python -u -m pytest tests/test_gpu_parity.py -k "not census" -x -q -p no:cacheprovider --timeout 120 --timeout-method thread
+      PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_k3pp.so run pp_quick_k3 180 python -u -m pytest tests/test_gpu_parity.py -k "not census" -x -q -p no:cacheprovider --timeout 120 --timeout-method thread
+      tail -2 $OUT/pp_quick.out
+      run abpp 600 python3 -u tools/ab_bench.py --rounds 3 --args "--steps 100 --warmup 10 --no-cpu-baseline" base= k2pp=PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_k2pp.so k3pp=PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_k3pp.so
+      grep median $OUT/abpp.out
+      python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); [print(k, [{kk: round(vv, 4) for kk, vv in e['kernel_ms'].items()} for e in v]) for k, v in d['extra'].items()]" $OUT/abpp.out
+      run abtfpp 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" base= tfpp=PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_tfpp.so
+      grep median $OUT/abtfpp.out
+      ;;
+    abfull)
+      run abfull50 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" base= fullreg=PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_fullreg.so
+      grep median $OUT/abfull50.out
+      run abfull16 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 16 --steps 100 --warmup 10 --no-cpu-baseline" base= fullreg=PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_fullreg.so
+      grep median $OUT/abfull16.out
+      PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_fullreg.so run prof_full 240 rocprofv3 --kernel-trace --stats -d $OUT/prof_full -o tune --output-format csv -- python3 bench.py --config tune --hosts 50 --steps 30 --warmup 5 --no-cpu-baseline
+      ;;
+    abloop)
+      run abloop 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config loop --steps 20 --warmup 3 --no-cpu-baseline" base= res0=PGP_GAN_RESERVED_CUS=0 res32=PGP_GAN_RESERVED_CUS=32 one=PGP_BENCH_ONE_STREAM=1
+      grep median $OUT/abloop.out
+      ;;
+    profloop)
+      run prof_loop 240 rocprofv3 --kernel-trace --stats -d $OUT/prof_loop -o loop --output-format csv -- python3 bench.py --config loop --steps 20 --warmup 3 --no-cpu-baseline
+      PGP_BENCH_ONE_STREAM=1 run prof_loop1 240 rocprofv3 --kernel-trace --stats -d $OUT/prof_loop1 -o loop --output-format csv -- python3 bench.py --config loop --steps 20 --warmup 3 --no-cpu-baseline
+      ;;
+    loop)
+      run loop 300 python3 -u bench.py --config loop --steps 20 --warmup 3
+      ;;
+    abgraph)
+      run abg16 600 python3 -u tools/ab_bench.py --rounds 4 --args "--config tune --hosts 16 --steps 100 --warmup 10 --no-cpu-baseline" eager= graph=PGP_BENCH_GRAPH=1
+      grep median $OUT/abg16.out
+      run abg50 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" eager= graph=PGP_BENCH_GRAPH=1
+      grep median $OUT/abg50.out
+      ;;
+    gobi)
+      run tgobi 300 python3 -u -m pytest tests/test_gpu_gobi.py -x -v --timeout 120 --timeout-method thread -m gpu
+      run gobi1 120 python3 -u bench.py --config gobi --steps 50 --warmup 5 --no-cpu-baseline
+      run gobi2 120 python3 -u bench.py --config gobi --steps 50 --warmup 5 --no-cpu-baseline
+      run loopg 300 python3 -u bench.py --config loop --steps 20 --warmup 3 --no-cpu-baseline
+      grep -h -o '"ms_per_step": [0-9.]*\|"mean_iterations": [0-9.]*' $OUT/gobi1.out $OUT/gobi2.out $OUT/loopg.out
+      ;;
+    abspread)
+      run tbal 600 python3 -u -m pytest tests/test_gpu_c3step.py tests/test_gpu_tunedp.py tests/test_gpu_train.py -x -q --timeout 120 --timeout-method thread -m gpu
+      run abs50 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" balanced= spread=PGP_TF_SPREAD=1
+      grep median $OUT/abs50.out
+      run abs16 600 python3 -u tools/ab_bench.py --rounds 4 --args "--config tune --hosts 16 --steps 100 --warmup 10 --no-cpu-baseline" balanced= spread=PGP_TF_SPREAD=1
+      grep median $OUT/abs16.out
+      run absloop 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config loop --steps 20 --warmup 3 --no-cpu-baseline" balanced= spread=PGP_TF_SPREAD=1
+      grep median $OUT/absloop.out
+      ;;
+    abearly)
+      PGP_TUNE_SIDE_EARLY=3 run tearly 600 python3 -u -m pytest tests/test_gpu_c3step.py tests/test_gpu_tunedp.py -x -q --timeout 120 --timeout-method thread -m gpu
+      run abe50 900 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" base= e1=PGP_TUNE_SIDE_EARLY=1 e2=PGP_TUNE_SIDE_EARLY=2 e3=PGP_TUNE_SIDE_EARLY=3
+      grep median $OUT/abe50.out
+      ;;
+    abres)
+      run abr16 600 python3 -u tools/ab_bench.py --rounds 4 --args "--config tune --hosts 16 --steps 100 --warmup 10 --no-cpu-baseline" r8= r0=PGP_GAN_RESERVED_CUS=0
+      grep median $OUT/abr16.out
+      run abr50 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" r8= r0=PGP_GAN_RESERVED_CUS=0
+      grep median $OUT/abr50.out
+      run abrloop 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config loop --steps 20 --warmup 3 --no-cpu-baseline" r8= r0=PGP_GAN_RESERVED_CUS=0
+      grep median $OUT/abrloop.out
+      ;;
+    abside2)
+      PGP_TUNE_SIDE_EARLY=15 run tside2 600 python3 -u -m pytest tests/test_gpu_c3step.py tests/test_gpu_tunedp.py -x -q --timeout 120 --timeout-method thread -m gpu
+      run abe2 900 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" e3= e7=PGP_TUNE_SIDE_EARLY=7 e11=PGP_TUNE_SIDE_EARLY=11 e15=PGP_TUNE_SIDE_EARLY=15
+      grep median $OUT/abe2.out
+      ;;
+    cprof)
+      run cprof16 300 python3 -u -m cProfile -o $OUT/cprof16.pstats bench.py --config tune --hosts 16 --steps 400 --warmup 10 --no-cpu-baseline
+      python3 -c "import pstats; p=pstats.Stats('$OUT/cprof16.pstats'); p.sort_stats('tottime').print_stats(40)" > $OUT/cprof16_tottime.txt
+      python3 -c "import pstats; p=pstats.Stats('$OUT/cprof16.pstats'); p.sort_stats('cumtime').print_stats(60)" > $OUT/cprof16_cumtime.txt
+      ;;
+    host)
+      run thost 600 python3 -u -m pytest tests/test_gpu_c3step.py tests/test_gpu_tunedp.py tests/test_gpu_train.py tests/test_gpu_bench_modes.py -x -q --timeout 120 --timeout-method thread -m gpu
+      run h16a 120 python3 -u bench.py --config tune --hosts 16 --steps 200 --warmup 10 --no-cpu-baseline
+      run h16b 120 python3 -u bench.py --config tune --hosts 16 --steps 200 --warmup 10 --no-cpu-baseline
+      run h50a 120 python3 -u bench.py --config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline
+      run hloop 300 python3 -u bench.py --config loop --steps 20 --warmup 3 --no-cpu-baseline
+      grep -h -o '"ms_per_step": [0-9.]*\|"host_issue_ms_per_step": [0-9.]*' $OUT/h16a.out $OUT/h16b.out $OUT/h50a.out $OUT/hloop.out
+      ;;
+    late)
+      PGP_C3_GAN_LATE=1 run tlate 600 python3 -u -m pytest tests/test_gpu_c3step.py tests/test_gpu_bench_modes.py -x -q --timeout 120 --timeout-method thread -m gpu
+      run abl16 600 python3 -u tools/ab_bench.py --rounds 4 --args "--config tune --hosts 16 --steps 100 --warmup 10 --no-cpu-baseline" early= late=PGP_C3_GAN_LATE=1
+      grep median $OUT/abl16.out
+      run abl50 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" early= late=PGP_C3_GAN_LATE=1
+      grep median $OUT/abl50.out
+      run cprofloop 300 python3 -u -m cProfile -o $OUT/cprofloop.pstats bench.py --config loop --steps 40 --warmup 3 --no-cpu-baseline
+      python3 -c "import pstats; p=pstats.Stats('$OUT/cprofloop.pstats'); p.sort_stats('tottime').print_stats(50)" > $OUT/cprofloop_tottime.txt
+      python3 -c "import pstats; p=pstats.Stats('$OUT/cprofloop.pstats'); p.sort_stats('cumtime').print_stats('preganplus_amd|bench', 60)" > $OUT/cprofloop_cumtime.txt
+      ;;
+    abdec)
+      run tdec 600 python3 -u -m pytest tests/test_gpu_c3step.py tests/test_gpu_tunedp.py tests/test_gpu_tune1.py tests/test_gpu_train_model.py -x -q --timeout 120 --timeout-method thread -m gpu
+      run abd50 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" new= prev=PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_prevdec.so
+      grep median $OUT/abd50.out
+      run abd16 600 python3 -u tools/ab_bench.py --rounds 4 --args "--config tune --hosts 16 --steps 100 --warmup 10 --no-cpu-baseline" new= prev=PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_prevdec.so
+      grep median $OUT/abd16.out
+      run prof_dec 240 rocprofv3 --kernel-trace --stats -d $OUT/prof_dec -o tune --output-format csv -- python3 bench.py --config tune --hosts 50 --steps 30 --warmup 5 --no-cpu-baseline
+      ;;
+    abzero)
+      run tzero 600 python3 -u -m pytest tests/test_gpu_c3step.py tests/test_gpu_bench_modes.py tests/test_gpu_dist.py -x -q --timeout 120 --timeout-method thread -m gpu
+      run abz16 600 python3 -u tools/ab_bench.py --rounds 4 --args "--config tune --hosts 16 --steps 100 --warmup 10 --no-cpu-baseline" zside= zmain=PGP_C3_ZERO_SIDE=0
+      grep median $OUT/abz16.out
+      run abz50 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" zside= zmain=PGP_C3_ZERO_SIDE=0
+      grep median $OUT/abz50.out
+      ;;
+    abmin)
+      run abm16 600 python3 -u tools/ab_bench.py --rounds 4 --args "--config tune --hosts 16 --steps 100 --warmup 10 --no-cpu-baseline" nofork= fork=PGP_TUNE_SIDE_MIN_TOKENS=1
+      grep median $OUT/abm16.out
+      ;;
+    abdws)
+      PGP_TUNE_DEC_DWS=1 run tdws 600 python3 -u -m pytest tests/test_gpu_c3step.py tests/test_gpu_tunedp.py -x -q --timeout 120 --timeout-method thread -m gpu
+      run abdws50 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" p4= p2=PGP_TUNE_DEC_DWS=2 p1=PGP_TUNE_DEC_DWS=1
+      grep median $OUT/abdws50.out
+      ;;
+    state)
+      run tstate 600 python3 -u -m pytest tests/test_gpu_tunedp.py tests/test_gpu_c3step.py tests/test_gpu_train.py tests/test_gpu_dist.py tests/test_gpu_plugin_graphs.py -x -q --timeout 120 --timeout-method thread -m gpu
+      run st50 120 python3 -u bench.py --config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline
+      run st16 120 python3 -u bench.py --config tune --hosts 16 --steps 100 --warmup 10 --no-cpu-baseline
+      run prof_st 240 rocprofv3 --kernel-trace --stats -d $OUT/prof_st -o tune --output-format csv -- python3 bench.py --config tune --hosts 50 --steps 30 --warmup 5 --no-cpu-baseline
+      grep -h -o '"ms_per_step": [0-9.]*' $OUT/st50.out $OUT/st16.out
+      ;;
+    ds)
+      run tds 600 python3 -u -m pytest tests/test_gpu_tunedp.py tests/test_gpu_c3step.py tests/test_gpu_train.py tests/test_gpu_plugin_graphs.py -x -q --timeout 120 --timeout-method thread -m gpu
+      run ds50 120 python3 -u bench.py --config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline
+      run ds16 120 python3 -u bench.py --config tune --hosts 16 --steps 100 --warmup 10 --no-cpu-baseline
+      run prof_ds 240 rocprofv3 --kernel-trace --stats -d $OUT/prof_ds -o tune --output-format csv -- python3 bench.py --config tune --hosts 50 --steps 30 --warmup 5 --no-cpu-baseline
+      run prof_ds16 240 rocprofv3 --kernel-trace --stats -d $OUT/prof_ds16 -o tune --output-format csv -- python3 bench.py --config tune --hosts 16 --steps 30 --warmup 5 --no-cpu-baseline
+      grep -h -o '"ms_per_step": [0-9.]*' $OUT/ds50.out $OUT/ds16.out
+      ;;
+    abflush)
+      run tflush 600 python3 -u -m pytest tests/test_gpu_c3step.py tests/test_gpu_tunedp.py tests/test_gpu_train.py -x -q --timeout 120 --timeout-method thread -m gpu
+      run abf50 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" early= late=PGP_TUNE_EARLY_FLUSH=0
+      grep median $OUT/abf50.out
+      ;;
+    abe15)
+      run abe15 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" e7= e15=PGP_TUNE_SIDE_EARLY=15
+      grep median $OUT/abe15.out
+      ;;
+    roofchk)
+      run rc50 120 python3 -u bench.py --config tune --hosts 50 --steps 20 --warmup 3 --no-cpu-baseline
+      run rc16 120 python3 -u bench.py --config tune --hosts 16 --steps 50 --warmup 5 --no-cpu-baseline
+      python3 -c "import json; [print(json.dumps({k: v for k, v in json.loads(open('$OUT/' + f + '.out').read().strip().splitlines()[-1])['roofline'].items() if k != 'basis'})) for f in ('rc50', 'rc16')]"
+      ;;
+    tunetraffic)
+      pmc tunepmcf FETCH_SIZE --config tune --hosts 50 --steps 3 --warmup 1 --no-cpu-baseline
+      pmc tunepmcw WRITE_SIZE --config tune --hosts 50 --steps 3 --warmup 1 --no-cpu-baseline
+      ;;
+    gp)
+      run tgp 600 python3 -u -m pytest tests/test_gpu_tunedp.py tests/test_gpu_c3step.py tests/test_gpu_train.py tests/test_gpu_dist.py tests/test_gpu_plugin_graphs.py tests/test_gpu_tune1.py tests/test_gpu_train_model.py tests/test_gpu_bench_modes.py -x -q --timeout 120 --timeout-method thread -m gpu
+      run gp50 120 python3 -u bench.py --config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline
+      run gp16 120 python3 -u bench.py --config tune --hosts 16 --steps 100 --warmup 10 --no-cpu-baseline
+      run prof_gp 240 rocprofv3 --kernel-trace --stats -d $OUT/prof_gp -o tune --output-format csv -- python3 bench.py --config tune --hosts 50 --steps 30 --warmup 5 --no-cpu-baseline
+      grep -h -o '"ms_per_step": [0-9.]*' $OUT/gp50.out $OUT/gp16.out
+      ;;
+    tc3q)
+      run tc3q 600 python3 -u -m pytest tests/test_gpu_c3step.py tests/test_gpu_tunedp.py tests/test_gpu_train.py tests/test_gpu_dist.py tests/test_gpu_plugin_graphs.py tests/test_gpu_bench_modes.py -x -q --timeout 120 --timeout-method thread -m gpu -p no:cacheprovider
+      tail -2 $OUT/tc3q.out
+      run q16 120 python3 -u bench.py --config tune --hosts 16 --steps 200 --warmup 10 --no-cpu-baseline
+      run q50 120 python3 -u bench.py --config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline
+      grep -h -o '"ms_per_step": [0-9.]*\|"host_issue_ms_per_step": [0-9.]*' $OUT/q16.out $OUT/q50.out
+      ;;
+    native)
+      run tnat 600 python3 -u -m pytest tests/test_gpu_c3step.py tests/test_gpu_dist.py -x -v --timeout 120 --timeout-method thread -m gpu -p no:cacheprovider
+      run n16 120 python3 -u bench.py --config tune --hosts 16 --steps 200 --warmup 10 --no-cpu-baseline
+      run n50 120 python3 -u bench.py --config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline
+      grep -h -o '"ms_per_step": [0-9.]*\|"host_issue_ms_per_step": [0-9.]*' $OUT/n16.out $OUT/n50.out
+      run prof_n16 240 rocprofv3 --kernel-trace --stats -d $OUT/prof_n16 -o tune --output-format csv -- python3 bench.py --config tune --hosts 16 --steps 60 --warmup 10 --no-cpu-baseline
+      ;;
+    base)
+      run b16 120 python3 -u bench.py --config tune --hosts 16 --steps 200 --warmup 10 --no-cpu-baseline
+      run b50 120 python3 -u bench.py --config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline
+      run bc2 200 python3 -u bench.py --steps 100 --warmup 10 --no-cpu-baseline
+      grep -h -o '"ms_per_step": [0-9.]*\|"host_issue_ms_per_step": [0-9.]*' $OUT/b16.out $OUT/b50.out $OUT/bc2.out
+      ;;
+    others)
+      run fpe 300 python3 -u bench.py --config fpe --steps 100 --warmup 5
+      run plugin 300 python3 -u bench.py --config plugin --steps 50 --warmup 5
+      run loop 300 python3 -u bench.py --config loop --steps 20 --warmup 3
+      ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo done
