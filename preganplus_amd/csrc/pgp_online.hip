@@ -217,7 +217,9 @@ int pgp_online_step(pgp_online* o, void* main_stream, void* gan_stream, pgp_coll
   OCHK(launch_tune_dataset(H, E, R, d.series, d.train_max, d.windows, d.y, d.cls, detect_win, sm));
   mark(o, kE1, sm);
   // 2. ONE forward over the B + E windows (step-start weights)
-  OCHK(launch_tune_forward(o->fwd, d.windows, d.P, d.tune_ws, nullptr, d.logits, d.protos, sm));
+  //    (and the Transformer section of G zeroed for the backward, in its packing launch)
+  OCHK(launch_tune_forward(o->fwd, d.windows, d.P, d.tune_ws, nullptr, d.logits, d.protos, sm, d.G + o->sec_lo[kTr],
+                           o->sec_lo[kGen] - o->sec_lo[kTr]));
   mark(o, kE2, sm);
   // 3. the GAN stream starts at the forward's end: embedding, Gen + Disc
   //    forward, the simulated label, the Disc gradient
@@ -236,7 +238,6 @@ int pgp_online_step(pgp_online* o, void* main_stream, void* gan_stream, pgp_coll
   OCHK(launch_tune_targets_dp(H, K, B, d.logits, d.protos, d.y, d.cls, d.state, d.update_min, d.mult, d.tgt, d.loss,
                               d.inc, d.dp_ws, sm, d.tune_ws + o->bwd.dpre, o->bwd.NOP));
   mark(o, kE3, sm);
-  OCHK(hipMemsetAsync(d.G + o->sec_lo[kTr], 0, (size_t)(go - o->sec_lo[kTr]) * sizeof(float), sm));
   OCHK(launch_tune_backward(o->bwd, d.P, d.G, d.tune_ws, d.logits, d.protos, d.y, d.mult, d.tgt, sm, true));
   mark(o, kE4, sm);
   // 5. the GAN's updates (its collectives on the GAN stream)

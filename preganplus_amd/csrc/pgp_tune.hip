@@ -203,7 +203,10 @@ __global__ __launch_bounds__(256) void dw_kernel(DwArgs a) {
 // p in [y*pc, (y+1)*pc) of this block's split y — 4 lane groups x 4 independent
 // chains, a fixed order — and adds into the destination (one split) or writes
 // lvl2[y][o] for a second pass.
-constexpr int kRedChunk = 256;
+// parts per split of one reduction: the step's dW slabs (<= kDwCap = 512) and the
+// fused launches' slabs (<= one per CU) reduce in ONE level (one launch of
+// reduce_multi_kernel, not two)
+constexpr int kRedChunk = 512;
 struct RedArgs {
   int nparts, pc;
   long pstride;
@@ -615,6 +618,62 @@ __global__ __launch_bounds__(256) void dec_pack_kernel(const float* __restrict__
   WpT[((long)tok * Q::DP + c) * Q::NOP + n] = v;
 }
 
+// The step's per-step packing as ONE launch when it all runs on the caller's
+// stream (below the side-stream threshold, e.g. C3 at H = 16): blocks
+// [0, nb_dec) dec_pack_kernel's elements, then one block of gat_mt_kernel,
+// then tf_pack_kernel's elements (pgp_tunef.hpp tf_pack_elem), then (zero !=
+// nullptr) the zero-fill of nzero floats (the transformer section of G before a
+// backward that accumulates into it).  Each element is computed as by its own
+// kernel: the same bits.
+template <int H>
+__global__ __launch_bounds__(256) void tune_pack_kernel(const float* __restrict__ P, float* __restrict__ Wp,
+                                                        float* __restrict__ WpT, float* __restrict__ Mt,
+                                                        float* __restrict__ frags, float* __restrict__ zero,
+                                                        long nzero, int nb_dec, int nb_tf) {
+  using Q = TuneGeo<H>;
+  using G = TGeo<H>;
+  int bx = blockIdx.x;
+  const int t = threadIdx.x;
+  if (bx < nb_dec) {
+    const long idx = (long)bx * 256 + t;
+    if (idx >= (long)Q::NOP * Q::KD) return;
+    const int n = (int)(idx / Q::KD);
+    const long k = idx - (long)n * Q::KD;
+    const int tok = (int)(k / Q::DP), c = (int)(k - (long)tok * Q::DP);
+    const int w = tok / H, h = tok - w * H;
+    float v = 0.f;
+    if (n < 4 * H && c < H) {
+      const long col = (long)h * 3 * H + w * H + c;
+      v = n < 2 * H ? P[G::W_AN + (long)n * G::L + col] : P[G::W_PR + (long)(n - 2 * H) * G::L + col];
+    }
+    Wp[idx] = v;
+    WpT[((long)tok * Q::DP + c) * Q::NOP + n] = v;
+    return;
+  }
+  bx -= nb_dec;
+  if (bx == 0) {
+    const int c = t / 3, k = t - 3 * c;
+    if (c >= 64) return;
+    float m = 0.f;
+    if (c < H)
+      for (int f = 0; f < H; ++f) m = fmaf(P[G::W_TE + c * H + f], P[G::W_FC + f * 3 + k], m);
+    Mt[t] = m;
+    return;
+  }
+  bx -= 1;
+  if (bx < nb_tf) {
+    tf_pack_elem<H>(P, frags, (long)bx * 256 + t);
+    return;
+  }
+  bx -= nb_tf;
+  const long i = ((long)bx * 256 + t) * 4;
+  if (i + 3 < nzero) {
+    *reinterpret_cast<float4*>(zero + i) = float4{0.f, 0.f, 0.f, 0.f};
+  } else {
+    for (long j = i; j < nzero; ++j) zero[j] = 0.f;
+  }
+}
+
 template <int H>
 __global__ __launch_bounds__(256) void dec_fin_kernel(int B, int S, const float* __restrict__ part,
                                                       const float* __restrict__ P, float* __restrict__ logits,
@@ -935,20 +994,20 @@ bool plan_h(int B, TunePlan* out) {
     auto r64 = [](long n) { return (n + 63) / 64 * 64; };
     auto red = [&](long nparts, long slab, long nout) {
       pool += r64(nparts * slab);
-      const long ns = (nparts + 255) / 256;
+      const long ns = (nparts + kRedChunk - 1) / kRedChunk;
       if (ns > 1) pool += r64(ns * nout);
     };
     auto dwr = [&](long np, long kp, long n, long k, bool bias) { red(q.dw_grid, np * kp + np, n * k + (bias ? n : 0)); };
     const long DPl = Q::DP, Hl = H;
     for (int l = 1; l >= 0; --l) {  // in_proj: one dW launch over [q|k|v] x DP rows, three reductions
       pool += r64((long)q.dw_grid * (3 * DPl * DPl + 3 * DPl));
-      const long ns2 = (q.dw_grid + 255) / 256;
+      const long ns2 = (q.dw_grid + kRedChunk - 1) / kRedChunk;
       if (ns2 > 1) pool += 3 * r64(ns2 * (Hl * Hl + Hl));
     }
     dwr(DPl, DPl, Hl, Hl, true);           // time encoder
     dwr(DPl, Q::XBP, Hl, 3, false);        // GAT fc
     // level-2 regions of the fused slabs (more than 256 workgroups)
-    const long ns = (tf_max_grid() + 255) / 256;
+    const long ns = (tf_max_grid() + kRedChunk - 1) / kRedChunk;
     if (ns > 1) pool += 2 * ns * r64(tf_slab_floats(H, 2) + tf_slab_floats(H, 3)) * 2;
     q.pool = take(pool);
     q.pool_len = pool;
@@ -1046,22 +1105,31 @@ struct Fork {
 
 template <int H>
 hipError_t tune_fwd_h(const TunePlan& p, const float* win, const float* P, float* ws, float* latent, float* logits,
-                      float* protos, hipStream_t st) {
+                      float* protos, hipStream_t st, float* zero, long nzero) {
   using Q = TuneGeo<H>;
   const int B = p.B;
   hipError_t e;
   // side: the decoder weights permuted for this step's forward and backward
   Fork fk(st, p.M);
-  if ((e = fk.fork()) != hipSuccess) return e;
-  TCK((dec_pack_kernel<H><<<(int)((Q::NOP * Q::KD + 255) / 256), 256, 0, fk.side>>>(P, ws + p.wp, ws + p.wpt)));
-  TCK((gat_mt_kernel<H><<<1, 192, 0, fk.side>>>(P, ws + p.mt)));  // for the backward's GAT (gat_bwd_kernel)
-  TCK((gat_fwd_kernel<H><<<(3 * B + 3) / 4, 256, 0, st>>>(B, win, P, ws + p.win, ws + p.g, ws + p.xb, ws + p.gs)));
-  // the encoder: fragments packed from P, then one fused launch per layer
   TfArgs t{};
   t.B = B;
   t.P = P;
   t.frags = ws + p.tff;
-  if ((e = launch_tf(H, 0, t, st)) != hipSuccess) return e;
+  if (fk.side == st) {  // all on the caller's stream: every packing (and the zero-fill) in ONE launch
+    const int nb_dec = (int)((Q::NOP * Q::KD + 255) / 256), nb_tf = (int)((tf_frag_floats(H) + 255) / 256);
+    const int nb_zero = zero ? (int)((nzero + 1023) / 1024) : 0;
+    TCK((tune_pack_kernel<H><<<nb_dec + 1 + nb_tf + nb_zero, 256, 0, st>>>(P, ws + p.wp, ws + p.wpt, ws + p.mt,
+                                                                            ws + p.tff, zero, nzero, nb_dec, nb_tf)));
+    TCK((gat_fwd_kernel<H><<<(3 * B + 3) / 4, 256, 0, st>>>(B, win, P, ws + p.win, ws + p.g, ws + p.xb, ws + p.gs)));
+  } else {
+    if ((e = fk.fork()) != hipSuccess) return e;
+    TCK((dec_pack_kernel<H><<<(int)((Q::NOP * Q::KD + 255) / 256), 256, 0, fk.side>>>(P, ws + p.wp, ws + p.wpt)));
+    TCK((gat_mt_kernel<H><<<1, 192, 0, fk.side>>>(P, ws + p.mt)));  // for the backward's GAT (gat_bwd_kernel)
+    if (zero && (e = hipMemsetAsync(zero, 0, (size_t)nzero * sizeof(float), fk.side)) != hipSuccess) return e;
+    TCK((gat_fwd_kernel<H><<<(3 * B + 3) / 4, 256, 0, st>>>(B, win, P, ws + p.win, ws + p.g, ws + p.xb, ws + p.gs)));
+    // the encoder: fragments packed from P, then one fused launch per layer
+    if ((e = launch_tf(H, 0, t, st)) != hipSuccess) return e;
+  }
   for (int l = 0; l < 2; ++l) {
     t.layer = l;
     t.in = ws + (l == 0 ? p.g : p.x[1]);
@@ -1295,11 +1363,11 @@ bool tune_plan_prefix(int H, int B_fwd, int B, TunePlan* p) {
 }
 
 hipError_t launch_tune_forward(const TunePlan& p, const float* windows, const float* P, float* ws, float* latent,
-                               float* logits, float* protos, hipStream_t st) {
+                               float* logits, float* protos, hipStream_t st, float* zero, long nzero) {
   switch (p.H) {
 #define CASE(h) \
   case h:       \
-    return tune_fwd_h<h>(p, windows, P, ws, latent, logits, protos, st);
+    return tune_fwd_h<h>(p, windows, P, ws, latent, logits, protos, st, zero, nzero);
     PGP_FOR_EACH_H(CASE)
 #undef CASE
   }

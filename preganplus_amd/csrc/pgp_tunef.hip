@@ -77,76 +77,9 @@ __device__ unsigned long long tf_stamps[4][kStWaves][kStPhases];
   } while (0)
 #endif
 
-// fragment group of matrix `mat`: float offset ((tile * KG + q) * 64 + lane) * 4 + e
-// holds A[i = lane & 15][k = lane >> 4] of k-step 4q + e of output tile `tile`
-template <int H>
-PGP_DEV float tf_frag_value(const float* __restrict__ P, int layer, int mat, int tile, int ks, int lane) {
-  using F = TF<H>;
-  using G = TGeo<H>;
-  const int i = lane & 15, g = lane >> 4;
-  const float* L = P + G::LAY0 + (long)layer * G::L_SIZE;
-  auto dfeat = [&](int s) { return 16 * (s >> 2) + 4 * g + (s & 3); };  // d-space k-step -> feature
-  switch (mat) {
-    case TFM_TE: {  // out d, in d
-      if (ks >= F::KS) return 0.f;
-      const int n = 16 * tile + i, c = dfeat(ks);
-      return (n < H && c < H) ? P[G::W_TE + n * H + c] : 0.f;
-    }
-    case TFM_IN: {  // out q|k|v tiles, in d
-      if (ks >= F::KS) return 0.f;
-      const int part = tile / F::NT, n = 16 * (tile - part * F::NT) + i, c = dfeat(ks);
-      return (n < H && c < H) ? L[G::L_IN + (long)(part * H + n) * H + c] : 0.f;
-    }
-    case TFM_O: {  // out d, in d
-      if (ks >= F::KS) return 0.f;
-      const int n = 16 * tile + i, c = dfeat(ks);
-      return (n < H && c < H) ? L[G::L_OUT + n * H + c] : 0.f;
-    }
-    case TFM_F1: {  // out hidden, in d
-      if (ks >= F::KS) return 0.f;
-      const int u = 16 * tile + i, c = dfeat(ks);
-      return c < H ? L[G::L_W1 + u * H + c] : 0.f;
-    }
-    case TFM_F2: {  // out d, in hidden
-      const int n = 16 * tile + i, u = dfeat(ks);
-      return n < H ? L[G::L_W2 + n * 64 + u] : 0.f;
-    }
-    case TFM_F2T: {  // out hidden, in d: W2^T
-      if (ks >= F::KS) return 0.f;
-      const int u = 16 * tile + i, n = dfeat(ks);
-      return n < H ? L[G::L_W2 + n * 64 + u] : 0.f;
-    }
-    case TFM_F1T: {  // out d, in hidden: W1^T
-      const int c = 16 * tile + i, u = dfeat(ks);
-      return c < H ? L[G::L_W1 + u * H + c] : 0.f;
-    }
-    case TFM_INT: {  // out d, in q|k|v rows: Win^T
-      if (ks >= F::KSQ) return 0.f;
-      const int part = ks / F::KS, s = ks - part * F::KS, n = dfeat(s), c = 16 * tile + i;
-      return (n < H && c < H) ? L[G::L_IN + (long)(part * H + n) * H + c] : 0.f;
-    }
-    case TFM_OT: {  // out d (attention output feature), in d (dR1 feature): Wo^T
-      if (ks >= F::KS) return 0.f;
-      const int c = 16 * tile + i, n = dfeat(ks);
-      return (n < H && c < H) ? L[G::L_OUT + n * H + c] : 0.f;
-    }
-  }
-  return 0.f;
-}
-
 template <int H>
 __global__ __launch_bounds__(256) void tf_pack_kernel(const float* __restrict__ P, float* __restrict__ frags) {
-  using F = TF<H>;
-  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
-  if (idx >= F::TOTAL_FLOATS) return;
-  const int e = (int)(idx & 3), lane = (int)((idx >> 2) & 63);
-  const long grp = idx >> 8;  // 1-KiB group
-  int layer, mat;
-  long gi;
-  F::locate(grp, layer, mat, gi);
-  const int kg = F::mat_kg(mat);
-  const int tile = (int)(gi / kg), q = (int)(gi - (long)tile * kg);
-  frags[idx] = tf_frag_value<H>(P, layer < 0 ? 0 : layer, mat, tile, 4 * q + e, lane);
+  tf_pack_elem<H>(P, frags, (long)blockIdx.x * 256 + threadIdx.x);
 }
 
 // ---------------------------------------------------------------------------
