@@ -222,8 +222,10 @@ int pgp_tune_forward(int n_hosts, int batch, const float* windows, const float* 
                      float* latent, float* logits, float* protos, void* stream);
 /* After pgp_tune_forward with the same batch and workspace: y [B,H] int
  * labels, mult [B,H] CE weights, tgt [B,H,2] positive prototypes (only rows
- * with y>0 used).  Accumulates the gradient of the summed per-window losses
- * into G (the caller zeroes G before the step). */
+ * with y>0 used).  WRITES the gradient of the summed per-window losses into
+ * the transformer section of G (every trainable entry is written exactly once
+ * by the call's reductions: no zeroing needed; the non-trainable positional
+ * encoding's entries are left as they are). */
 int pgp_tune_backward(int n_hosts, int batch, const float* P, float* G, float* workspace, const float* logits,
                       const float* protos, const int* y, const float* mult, const float* tgt, void* stream);
 /* The same backward over the FIRST `batch` windows of a pgp_tune_forward of

@@ -217,9 +217,7 @@ int pgp_online_step(pgp_online* o, void* main_stream, void* gan_stream, pgp_coll
   OCHK(launch_tune_dataset(H, E, R, d.series, d.train_max, d.windows, d.y, d.cls, detect_win, sm));
   mark(o, kE1, sm);
   // 2. ONE forward over the B + E windows (step-start weights)
-  //    (and the Transformer section of G zeroed for the backward, in its packing launch)
-  OCHK(launch_tune_forward(o->fwd, d.windows, d.P, d.tune_ws, nullptr, d.logits, d.protos, sm, d.G + o->sec_lo[kTr],
-                           o->sec_lo[kGen] - o->sec_lo[kTr]));
+  OCHK(launch_tune_forward(o->fwd, d.windows, d.P, d.tune_ws, nullptr, d.logits, d.protos, sm));
   mark(o, kE2, sm);
   // 3. the GAN stream starts at the forward's end: embedding, Gen + Disc
   //    forward, the simulated label, the Disc gradient

@@ -253,9 +253,9 @@ PGP_DEV void reduce_block(const RedArgs& a, int bx, int by) {
       a.lvl2[by * nout + o] = t;
     } else if (o < na) {
       const int i = (int)(o / a.cols), j = (int)(o - (long)i * a.cols);
-      a.outA[(long)i * a.ldo + j] += t;
+      a.outA[(long)i * a.ldo + j] = t;
     } else {
-      a.outB[o - na] += t;
+      a.outB[o - na] = t;
     }
   }
 }
@@ -584,9 +584,9 @@ __global__ __launch_bounds__(256) void gat_param_kernel(int n, const float* __re
       for (int k = 0; k < 3; ++k) agg[k] = fmaf(wt, fcd[r * 3 + k], agg[k]);
     }
 #pragma unroll
-    for (int k = 0; k < 3; ++k) Gd[G::W_FC + c * 3 + k] += agg[k] + (a1 * xs[k] + a2 * xt[k]);
-    Gd[G::W_ATT + c] += fc[0] * xs[0] + fc[1] * xs[1] + fc[2] * xs[2];
-    Gd[G::W_ATT + H + c] += fc[0] * xt[0] + fc[1] * xt[1] + fc[2] * xt[2];
+    for (int k = 0; k < 3; ++k) Gd[G::W_FC + c * 3 + k] = agg[k] + (a1 * xs[k] + a2 * xt[k]);
+    Gd[G::W_ATT + c] = fc[0] * xs[0] + fc[1] * xs[1] + fc[2] * xs[2];
+    Gd[G::W_ATT + H + c] = fc[0] * xt[0] + fc[1] * xt[1] + fc[2] * xt[2];
   }
 }
 
@@ -621,15 +621,12 @@ __global__ __launch_bounds__(256) void dec_pack_kernel(const float* __restrict__
 // The step's per-step packing as ONE launch when it all runs on the caller's
 // stream (below the side-stream threshold, e.g. C3 at H = 16): blocks
 // [0, nb_dec) dec_pack_kernel's elements, then one block of gat_mt_kernel,
-// then tf_pack_kernel's elements (pgp_tunef.hpp tf_pack_elem), then (zero !=
-// nullptr) the zero-fill of nzero floats (the transformer section of G before a
-// backward that accumulates into it).  Each element is computed as by its own
-// kernel: the same bits.
+// then tf_pack_kernel's elements (pgp_tunef.hpp tf_pack_elem).  Each element is
+// computed as by its own kernel: the same bits.
 template <int H>
 __global__ __launch_bounds__(256) void tune_pack_kernel(const float* __restrict__ P, float* __restrict__ Wp,
                                                         float* __restrict__ WpT, float* __restrict__ Mt,
-                                                        float* __restrict__ frags, float* __restrict__ zero,
-                                                        long nzero, int nb_dec, int nb_tf) {
+                                                        float* __restrict__ frags, int nb_dec, int nb_tf) {
   using Q = TuneGeo<H>;
   using G = TGeo<H>;
   int bx = blockIdx.x;
@@ -661,17 +658,7 @@ __global__ __launch_bounds__(256) void tune_pack_kernel(const float* __restrict_
     return;
   }
   bx -= 1;
-  if (bx < nb_tf) {
-    tf_pack_elem<H>(P, frags, (long)bx * 256 + t);
-    return;
-  }
-  bx -= nb_tf;
-  const long i = ((long)bx * 256 + t) * 4;
-  if (i + 3 < nzero) {
-    *reinterpret_cast<float4*>(zero + i) = float4{0.f, 0.f, 0.f, 0.f};
-  } else {
-    for (long j = i; j < nzero; ++j) zero[j] = 0.f;
-  }
+  tf_pack_elem<H>(P, frags, (long)bx * 256 + t);
 }
 
 template <int H>
@@ -779,7 +766,7 @@ __global__ __launch_bounds__(256) void dec_dw_kernel(int B, const float* __restr
             ps[n * KP + c] = acc[q][u][r];
           } else if (n < 4 * H && c < H) {
             const long col = (long)h * 3 * H + w * H + c;
-            Gd[(n < 2 * H ? G::W_AN + (long)n * G::L : G::W_PR + (long)(n - 2 * H) * G::L) + col] += acc[q][u][r];
+            Gd[(n < 2 * H ? G::W_AN + (long)n * G::L : G::W_PR + (long)(n - 2 * H) * G::L) + col] = acc[q][u][r];
           }
         }
       if (tok == 0) {
@@ -788,7 +775,7 @@ __global__ __launch_bounds__(256) void dec_dw_kernel(int B, const float* __restr
         if (S > 1) {
           if (g == 0) pbias[n] = sb;
         } else if (g == 0 && n < 4 * H) {
-          Gd[n < 2 * H ? G::B_AN + n : G::B_PR + n - 2 * H] += sb;
+          Gd[n < 2 * H ? G::B_AN + n : G::B_PR + n - 2 * H] = sb;
         }
       }
     }
@@ -812,13 +799,13 @@ __global__ __launch_bounds__(256) void dec_dw_sum_kernel(int S, const float* __r
     const float* src = part + ((long)tok * NP + n) * KP + c;
     float v = 0.f;
     for (int z = 0; z < S; ++z) v += src[(long)z * Q::T * NP * KP];
-    Gd[(n < 2 * H ? G::W_AN + (long)n * G::L : G::W_PR + (long)(n - 2 * H) * G::L) + col] += v;
+    Gd[(n < 2 * H ? G::W_AN + (long)n * G::L : G::W_PR + (long)(n - 2 * H) * G::L) + col] = v;
   } else if (idx < NW + 4 * H) {
     const int n = (int)(idx - NW);
     const float* src = part + (long)S * Q::T * NP * KP + n;
     float v = 0.f;
     for (int z = 0; z < S; ++z) v += src[(long)z * NP];
-    Gd[n < 2 * H ? G::B_AN + n : G::B_PR + n - 2 * H] += v;
+    Gd[n < 2 * H ? G::B_AN + n : G::B_PR + n - 2 * H] = v;
   }
 }
 
@@ -1105,7 +1092,7 @@ struct Fork {
 
 template <int H>
 hipError_t tune_fwd_h(const TunePlan& p, const float* win, const float* P, float* ws, float* latent, float* logits,
-                      float* protos, hipStream_t st, float* zero, long nzero) {
+                      float* protos, hipStream_t st) {
   using Q = TuneGeo<H>;
   const int B = p.B;
   hipError_t e;
@@ -1115,17 +1102,15 @@ hipError_t tune_fwd_h(const TunePlan& p, const float* win, const float* P, float
   t.B = B;
   t.P = P;
   t.frags = ws + p.tff;
-  if (fk.side == st) {  // all on the caller's stream: every packing (and the zero-fill) in ONE launch
+  if (fk.side == st) {  // all on the caller's stream: every packing in ONE launch
     const int nb_dec = (int)((Q::NOP * Q::KD + 255) / 256), nb_tf = (int)((tf_frag_floats(H) + 255) / 256);
-    const int nb_zero = zero ? (int)((nzero + 1023) / 1024) : 0;
-    TCK((tune_pack_kernel<H><<<nb_dec + 1 + nb_tf + nb_zero, 256, 0, st>>>(P, ws + p.wp, ws + p.wpt, ws + p.mt,
-                                                                            ws + p.tff, zero, nzero, nb_dec, nb_tf)));
+    TCK((tune_pack_kernel<H><<<nb_dec + 1 + nb_tf, 256, 0, st>>>(P, ws + p.wp, ws + p.wpt, ws + p.mt, ws + p.tff,
+                                                                  nb_dec, nb_tf)));
     TCK((gat_fwd_kernel<H><<<(3 * B + 3) / 4, 256, 0, st>>>(B, win, P, ws + p.win, ws + p.g, ws + p.xb, ws + p.gs)));
   } else {
     if ((e = fk.fork()) != hipSuccess) return e;
     TCK((dec_pack_kernel<H><<<(int)((Q::NOP * Q::KD + 255) / 256), 256, 0, fk.side>>>(P, ws + p.wp, ws + p.wpt)));
     TCK((gat_mt_kernel<H><<<1, 192, 0, fk.side>>>(P, ws + p.mt)));  // for the backward's GAT (gat_bwd_kernel)
-    if (zero && (e = hipMemsetAsync(zero, 0, (size_t)nzero * sizeof(float), fk.side)) != hipSuccess) return e;
     TCK((gat_fwd_kernel<H><<<(3 * B + 3) / 4, 256, 0, st>>>(B, win, P, ws + p.win, ws + p.g, ws + p.xb, ws + p.gs)));
     // the encoder: fragments packed from P, then one fused launch per layer
     if ((e = launch_tf(H, 0, t, st)) != hipSuccess) return e;
@@ -1363,11 +1348,11 @@ bool tune_plan_prefix(int H, int B_fwd, int B, TunePlan* p) {
 }
 
 hipError_t launch_tune_forward(const TunePlan& p, const float* windows, const float* P, float* ws, float* latent,
-                               float* logits, float* protos, hipStream_t st, float* zero, long nzero) {
+                               float* logits, float* protos, hipStream_t st) {
   switch (p.H) {
 #define CASE(h) \
   case h:       \
-    return tune_fwd_h<h>(p, windows, P, ws, latent, logits, protos, st, zero, nzero);
+    return tune_fwd_h<h>(p, windows, P, ws, latent, logits, protos, st);
     PGP_FOR_EACH_H(CASE)
 #undef CASE
   }

@@ -63,10 +63,8 @@ int dec_fwd_splits(int H, int B);
 hipError_t launch_dec_fwd(int H, int B, int S, const float* X2, const float* Wp, float* part, hipStream_t st);
 hipError_t launch_dec_dx(int H, int B, const float* dpre, const float* WpT, float* dX, hipStream_t st);
 
-// zero != nullptr: also zero-fill nzero floats there, ordered before the
-// call's end (the gradient section a following backward accumulates into)
 hipError_t launch_tune_forward(const TunePlan& p, const float* windows, const float* P, float* ws, float* latent,
-                               float* logits, float* protos, hipStream_t st, float* zero = nullptr, long nzero = 0);
+                               float* logits, float* protos, hipStream_t st);
 // dpre_ready: the decoder pre-activation gradient [B][NOP] at ws + p.dpre was
 // already written (launch_tune_targets_dp with dpre), so the loss kernel is skipped
 hipError_t launch_tune_backward(const TunePlan& p, const float* P, float* G, float* ws, const float* logits,

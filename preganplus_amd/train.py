@@ -249,7 +249,7 @@ class Trainer:
         y = self._dev(y, torch.int32)
         mult = self._dev(mult, torch.float32)
         tgt = self._dev(tgt, torch.float32)
-        self.zero_grad("transformer")
+        # (the backward writes every trainable entry of the section: no zero_grad)
         if B == self._fwd_batch:
             _native.check(self._L.pgp_tune_backward(
                 self.H, B, self.P.data_ptr(), self.G.data_ptr(), self.ws.data_ptr(),

@@ -284,6 +284,9 @@ for step in "$@"; do
       PGP_BENCH_ONE_STREAM=1 run one16 120 python3 -u bench.py --config tune --hosts 16 --steps 200 --warmup 10 --no-cpu-baseline
       grep -h -o '"ms_per_step": [0-9.]*\|"host_issue_ms_per_step": [0-9.]*' $OUT/one16.out
       ;;
+    prof50)
+      run prof50 240 rocprofv3 --kernel-trace --stats -d $OUT/prof50 -o tune --output-format csv -- python3 bench.py --config tune --hosts 50 --steps 40 --warmup 5 --no-cpu-baseline
+      ;;
     native)
       run tnat 600 python3 -u -m pytest tests/test_gpu_c3step.py tests/test_gpu_dist.py -x -v --timeout 120 --timeout-method thread -m gpu -p no:cacheprovider
       run n16 120 python3 -u bench.py --config tune --hosts 16 --steps 200 --warmup 10 --no-cpu-baseline
