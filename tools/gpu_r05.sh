@@ -285,7 +285,14 @@ for step in "$@"; do
       grep -h -o '"ms_per_step": [0-9.]*\|"host_issue_ms_per_step": [0-9.]*' $OUT/one16.out
       ;;
     prof50)
+      run p50b 120 python3 -u bench.py --config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline
+      grep -h -o '"ms_per_step": [0-9.]*' $OUT/p50b.out
       run prof50 240 rocprofv3 --kernel-trace --stats -d $OUT/prof50 -o tune --output-format csv -- python3 bench.py --config tune --hosts 50 --steps 40 --warmup 5 --no-cpu-baseline
+      ;;
+    ffn8)
+      PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_ffn8.so run ffn8 120 python3 -u bench.py --config tune --hosts 50 --steps 30 --warmup 5 --no-cpu-baseline
+      run ffn4 120 python3 -u bench.py --config tune --hosts 50 --steps 30 --warmup 5 --no-cpu-baseline
+      python3 -c "import json; [print(f, json.dumps({k: round(v['ms'],4) for k, v in json.loads(open('$OUT/' + f + '.out').read().strip().splitlines()[-1])['roofline']['fused_launches'].items()})) for f in ('ffn8', 'ffn4')]"
       ;;
     native)
       run tnat 600 python3 -u -m pytest tests/test_gpu_c3step.py tests/test_gpu_dist.py -x -v --timeout 120 --timeout-method thread -m gpu -p no:cacheprovider
