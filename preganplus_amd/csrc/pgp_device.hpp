@@ -96,10 +96,15 @@ hipError_t launch_gan1_step(int H, const float* target, float* Pg, float* Pd, fl
                             hipStream_t st);
 
 // GAN step (pgp_gantrain.hip); ws = gan_workspace_floats(H, B) floats
+// logits != nullptr: the embedding is run_model's mask of logits / protos
+// [B][H][2] (PreGANPlus.py:129), formed in the launch and written to emb_out
+// (emb unused); probs may be nullptr (the Disc step evaluates the head itself)
 hipError_t launch_gan_fwd(int H, int B, const float* emb, const float* sched, const float* Pg, const float* Pd,
-                          float* ws, float* ns_out, float* probs, hipStream_t st);
+                          float* ws, float* ns_out, float* probs, hipStream_t st, const float* logits = nullptr,
+                          const float* protos = nullptr, float* emb_out = nullptr);
+// probs (may be nullptr): the Disc probabilities of the step's forward
 hipError_t launch_gan_disc_bwd(int H, int B, const float* target, const float* Pd, float* Gdd, float* ws,
-                               hipStream_t st);
+                               hipStream_t st, float* probs = nullptr);
 hipError_t launch_gan_gen_bwd(int H, int B, const float* Pg, const float* Pd, float* Gdg, float* ws,
                               hipStream_t st);
 hipError_t launch_gan_probs(int H, int B, const float* ws, float* probs, hipStream_t st);

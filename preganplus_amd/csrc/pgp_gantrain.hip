@@ -108,12 +108,37 @@ PGP_DEV void head16(const float* ddl, const float* __restrict__ Pd2, const float
 // ---------------------------------------------------------------------------
 // Gen + Disc forward of a block of 16 environments
 // ---------------------------------------------------------------------------
-template <int H>
-__global__ __launch_bounds__(kGW * 64) void gan_fwd_kernel(int B, const float* __restrict__ emb,
-                                                           const float* __restrict__ sched,
-                                                           const float* __restrict__ Pg, const float* __restrict__ Pd,
-                                                           float* __restrict__ rows, float* __restrict__ ns_out,
-                                                           float* __restrict__ probs) {
+// Arguments of the batched forward.  Embedding: `emb` [B][2H] is read, or,
+// with `logits` set, run_model's masked embedding (PreGANPlus.py:129, the rule
+// of embed_kernel) is formed from the detect forward's logits / protos [B][H][2]
+// on the fly and written to `emb` (one launch fewer).  The split form's
+// partials live after the rows in the workspace (gan_split_offsets).
+struct GanFwdArgs {
+  int B;
+  const float* emb_in;
+  float* emb_out;
+  const float* logits;
+  const float* protos;
+  const float* sched;
+  const float* Pg;
+  const float* Pd;
+  float* rows;
+  float* ns_out;
+  float* probs;
+  float* part1;  // [nblk][S][2][1024]: phase-1 Gen1 | Disc1-schedule partials (PH 1)
+  float* part2;  // [nblk][S][1024]: Disc1-ns partials (PH 2)
+  float* dsum;   // [nblk][1024]: Disc1's schedule half (PH 2, slice 0)
+};
+
+// The forward of a block of 16 environments.  PH 0: the whole forward in one
+// workgroup (8 waves splitting each contraction's chunks); PH 1 / PH 2: the
+// same two contraction phases split over gridDim.y workgroups ("slices") per
+// block, chunk c to wave (c mod S*kGW) of slice (c / kGW mod S), the slices'
+// partials summed in slice order by the next launch (phase 1 -> PH 2's start;
+// phase 2 -> gan_dd_head_kernel): at C3's 103 environments (7 blocks) one
+// workgroup per block left most of the chip idle for the whole GAN step.
+template <int H, int PH>
+__global__ __launch_bounds__(kGW * 64) void gan_fwd_kernel(GanFwdArgs a) {
   using K = GanK<H>;
   using G = TGeo<H>;
   constexpr int HH = K::HH, E2 = K::E2, GIN = K::GIN, DIN = K::DIN;
@@ -121,22 +146,39 @@ __global__ __launch_bounds__(kGW * 64) void gan_fwd_kernel(int B, const float* _
   __shared__ __attribute__((aligned(16))) float hgl[16 * kHP];   // Hg [env][hidden]
   __shared__ __attribute__((aligned(16))) float dsl[16 * kHP];   // Disc1's schedule half, then DD
   __shared__ float zl[32], pl[32];
+  const int B = a.B;
+  const float* __restrict__ sched = a.sched;
+  const float* __restrict__ Pg = a.Pg;
+  const float* __restrict__ Pd = a.Pd;
+  float* __restrict__ rows = a.rows;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, g = lane >> 4, i = lane & 15;
-  const long env = (long)blockIdx.x * 16 + i;
+  const int blk = blockIdx.x, sl = blockIdx.y, S = gridDim.y;
+  const int c0 = sl * kGW + wv, cs = S * kGW;  // this wave's chunks: c0, c0 + cs, ...
+  const long env = (long)blk * 16 + i;
   const bool eok = env < B;
   float* row = rows + (eok ? env : 0) * G::GS_SIZE;
   const float* W1 = Pg + G::G_W1;
   const float* D1 = Pd + G::D_W1;
 
-  // 1. Gen1 = W1 [e; s] and Disc1's schedule half D1[:, :HH] s, one pass over
-  //    the input chunks (16 inputs each, k-step r <-> input 16c + 4g + r)
   f32x4 aG[4], aD[4];
 #pragma unroll
   for (int t = 0; t < 4; ++t) aG[t] = aD[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int c = wv; c < K::KE; c += kGW) {  // embedding chunks
+  if constexpr (PH != 2) {
+  // 1. Gen1 = W1 [e; s] and Disc1's schedule half D1[:, :HH] s, one pass over
+  //    the input chunks (16 inputs each, k-step r <-> input 16c + 4g + r)
+  for (int c = c0; c < K::KE; c += cs) {  // embedding chunks
     const int f = 16 * c + 4 * g;
     const bool fok = f < E2;
-    const f32x4 bv = ld4(fok && eok ? emb + env * E2 + f : gk_zero);
+    f32x4 bv;
+    if (a.logits) {  // PreGANPlus.py:129: a host's prototype pair where its logits' argmax is 1
+      const f32x4 l = ld4(fok && eok ? a.logits + env * E2 + f : gk_zero);
+      const f32x4 pr = ld4(fok && eok ? a.protos + env * E2 + f : gk_zero);
+      const bool k0 = l[1] > l[0], k1 = l[3] > l[2];
+      bv = f32x4{k0 ? pr[0] : 0.f, k0 ? pr[1] : 0.f, k1 ? pr[2] : 0.f, k1 ? pr[3] : 0.f};
+      if (fok && eok) st4(a.emb_out + env * E2 + f, bv);
+    } else {
+      bv = ld4(fok && eok ? a.emb_in + env * E2 + f : gk_zero);
+    }
     f32x4 wa[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) wa[t] = ld4(fok ? W1 + (long)(16 * t + i) * GIN + f : gk_zero);
@@ -146,7 +188,7 @@ __global__ __launch_bounds__(kGW * 64) void gan_fwd_kernel(int B, const float* _
 #pragma unroll
       for (int t = 0; t < 4; ++t) aG[t] = mfma(wa[t][r], bv[r], aG[t]);
   }
-  {  // schedule chunks, software-pipelined: chunk c + kGW's operands are loaded
+  {  // schedule chunks, software-pipelined: chunk c + cs's operands are loaded
      // before chunk c's MFMAs (one latency per wave, not one per chunk)
     struct Ops {
       f32x4 bv, wa[4], wd[4];
@@ -175,15 +217,43 @@ __global__ __launch_bounds__(kGW * 64) void gan_fwd_kernel(int B, const float* _
           aD[t] = mfma(cur.wd[t][r], cur.bv[r], aD[t]);
         }
     };
-    if (wv < K::KS) load(wv, A);
-    for (int c = wv; c < K::KS; c += 2 * kGW) {
-      load(c + kGW < K::KS ? c + kGW : c, B);
+    if (c0 < K::KS) load(c0, A);
+    for (int c = c0; c < K::KS; c += 2 * cs) {
+      load(c + cs < K::KS ? c + cs : c, B);
       step(c, A);
-      if (c + kGW >= K::KS) break;
-      load(c + 2 * kGW < K::KS ? c + 2 * kGW : c + kGW, A);
-      step(c + kGW, B);
+      if (c + cs >= K::KS) break;
+      load(c + 2 * cs < K::KS ? c + 2 * cs : c + cs, A);
+      step(c + cs, B);
     }
   }
+  }
+  if constexpr (PH == 1) {  // the slice's partials, in wave order
+    float* out = a.part1 + ((long)blk * S + sl) * 2048;
+    reduce4(red, aG, wv, lane);
+    for (int k = threadIdx.x; k < 1024; k += blockDim.x) out[k] = red[k];
+    __syncthreads();  // red is read before the next reduction overwrites it
+    reduce4(red, aD, wv, lane);
+    for (int k = threadIdx.x; k < 1024; k += blockDim.x) out[1024 + k] = red[k];
+    return;
+  } else if constexpr (PH == 2) {  // phase 1's slices summed in slice order
+    const float* in = a.part1 + (long)blk * S * 2048;
+    for (int k = threadIdx.x; k < 1024; k += blockDim.x) {
+      int h, j;
+      red_index(k, h, j);
+      float v = in[k], d = in[1024 + k];
+      for (int q = 1; q < S; ++q) {
+        v += in[(long)q * 2048 + k];
+        d += in[(long)q * 2048 + 1024 + k];
+      }
+      v += Pg[G::G_B1 + h];
+      hgl[j * kHP + h] = v;
+      if (sl == 0) {
+        if ((long)blk * 16 + j < B) rows[((long)blk * 16 + j) * G::GS_SIZE + G::GS_H + h] = v;
+        a.dsum[(long)blk * 1024 + k] = d;
+      }
+    }
+    __syncthreads();
+  } else {
   // Hg = W1 [e; s] + b1 (LeakyReLU(True): slope 1, the identity, models.py:127)
   reduce4(red, aG, wv, lane);
   for (int k = threadIdx.x; k < 1024; k += blockDim.x) {
@@ -191,7 +261,7 @@ __global__ __launch_bounds__(kGW * 64) void gan_fwd_kernel(int B, const float* _
     red_index(k, h, j);
     const float v = red[k] + Pg[G::G_B1 + h];
     hgl[j * kHP + h] = v;
-    if ((long)blockIdx.x * 16 + j < B) rows[((long)blockIdx.x * 16 + j) * G::GS_SIZE + G::GS_H + h] = v;
+    if ((long)blk * 16 + j < B) rows[((long)blk * 16 + j) * G::GS_SIZE + G::GS_H + h] = v;
   }
   __syncthreads();
   reduce4(red, aD, wv, lane);
@@ -201,6 +271,7 @@ __global__ __launch_bounds__(kGW * 64) void gan_fwd_kernel(int B, const float* _
     dsl[j * kHP + h] = red[k];
   }
   __syncthreads();
+  }
 
   // 2. Gen2 tiles: T = tanh(W2 Hg + b2), ns = s + 4 T (models.py:128-133);
   //    Disc1's ns half accumulated from each tile (the tile is its B operand)
@@ -244,22 +315,28 @@ __global__ __launch_bounds__(kGW * 64) void gan_fwd_kernel(int B, const float* _
       if (nok && eok) {
         st4(row + G::GS_T + n, tv);
         st4(row + G::GS_Z + HH + n, nv);
-        st4(ns_out + env * HH + n, nv);
+        st4(a.ns_out + env * HH + n, nv);
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r)
 #pragma unroll
         for (int t = 0; t < 4; ++t) aD[t] = mfma(cur.wd[t][r], nv[r], aD[t]);
     };
-    if (wv < K::KS) load(wv, A);
-    for (int c = wv; c < K::KS; c += 2 * kGW) {
-      load(c + kGW < K::KS ? c + kGW : c, B);
+    if (c0 < K::KS) load(c0, A);
+    for (int c = c0; c < K::KS; c += 2 * cs) {
+      load(c + cs < K::KS ? c + cs : c, B);
       step(c, A);
-      if (c + kGW >= K::KS) break;
-      load(c + 2 * kGW < K::KS ? c + 2 * kGW : c + kGW, A);
-      step(c + kGW, B);
+      if (c + cs >= K::KS) break;
+      load(c + 2 * cs < K::KS ? c + 2 * cs : c + cs, A);
+      step(c + cs, B);
     }
   }
+  if constexpr (PH == 2) {  // the slice's Disc1-ns partial (gan_dd_head_kernel sums the slices)
+    float* out = a.part2 + ((long)blk * S + sl) * 1024;
+    reduce4(red, aD, wv, lane);
+    for (int k = threadIdx.x; k < 1024; k += blockDim.x) out[k] = red[k];
+    return;
+  } else {
   // DD = Disc1 [s; ns] + db1 (LeakyReLU(True) = identity, models.py:145)
   reduce4(red, aD, wv, lane);
   for (int k = threadIdx.x; k < 1024; k += blockDim.x) {
@@ -267,16 +344,74 @@ __global__ __launch_bounds__(kGW * 64) void gan_fwd_kernel(int B, const float* _
     red_index(k, h, j);
     const float v = (red[k] + dsl[j * kHP + h]) + Pd[G::D_B1 + h];
     dsl[j * kHP + h] = v;
-    if ((long)blockIdx.x * 16 + j < B) rows[((long)blockIdx.x * 16 + j) * G::GS_SIZE + G::GS_DD + h] = v;
+    if ((long)blk * 16 + j < B) rows[((long)blk * 16 + j) * G::GS_SIZE + G::GS_DD + h] = v;
   }
   __syncthreads();
   head16(dsl, Pd + G::D_W2, Pd + G::D_B2, zl, pl);
   if (threadIdx.x < 32) {
-    const long e = (long)blockIdx.x * 16 + (threadIdx.x >> 1);
+    const long e = (long)blk * 16 + (threadIdx.x >> 1);
+    if (e < B) {
+      rows[e * G::GS_SIZE + G::GS_P + (threadIdx.x & 1)] = pl[threadIdx.x];
+      if (a.probs) a.probs[2 * e + (threadIdx.x & 1)] = pl[threadIdx.x];
+    }
+  }
+  }
+}
+
+// The split forward's end, per block, after the simulator: DD = the slices'
+// Disc1-ns partials (slice order) + Disc1's schedule half + db1 -> rows; the
+// head and softmax (head16) -> rows' probabilities (and probs); mode 1: the BCE
+// gradient toward the simulated label tgt (PreGANPlus.py:66-67) back through
+// the softmax and the head -> dOut, dDD (disc_head_kernel's mode 1).
+template <int H>
+__global__ __launch_bounds__(256) void gan_dd_head_kernel(int B, int S, int mode, const float* __restrict__ Pd,
+                                                          float* __restrict__ rows, const float* __restrict__ part2,
+                                                          const float* __restrict__ dsum, const float* __restrict__ tgt,
+                                                          float* __restrict__ probs) {
+  using G = TGeo<H>;
+  __shared__ __attribute__((aligned(16))) float ddl[16 * kHP];
+  __shared__ float zl[32], pl[32];
+  const int blk = blockIdx.x;
+  const float* in = part2 + (long)blk * S * 1024;
+  for (int k = threadIdx.x; k < 1024; k += blockDim.x) {
+    int h, j;
+    red_index(k, h, j);
+    float v = in[k];
+    for (int q = 1; q < S; ++q) v += in[(long)q * 1024 + k];
+    v = (v + dsum[(long)blk * 1024 + k]) + Pd[G::D_B1 + h];
+    ddl[j * kHP + h] = v;
+    if ((long)blk * 16 + j < B) rows[((long)blk * 16 + j) * G::GS_SIZE + G::GS_DD + h] = v;
+  }
+  __syncthreads();
+  head16(ddl, Pd + G::D_W2, Pd + G::D_B2, zl, pl);
+  if (threadIdx.x < 32) {
+    const long e = (long)blk * 16 + (threadIdx.x >> 1);
     if (e < B) {
       rows[e * G::GS_SIZE + G::GS_P + (threadIdx.x & 1)] = pl[threadIdx.x];
       if (probs) probs[2 * e + (threadIdx.x & 1)] = pl[threadIdx.x];
     }
+  }
+  if (mode == 0) return;
+  if (threadIdx.x < 16) {  // torch BCE grad (p - t) / max(p (1 - p), 1e-12) / N, through the softmax
+    const int j = threadIdx.x;
+    const long e = (long)blk * 16 + j;
+    const float p0 = pl[2 * j], p1 = pl[2 * j + 1];
+    const float t0 = e < B ? tgt[2 * e] : 0.f, t1 = e < B ? tgt[2 * e + 1] : 0.f;
+    const float dp0 = (p0 - t0) / fmaxf(p0 * (1.f - p0), 1e-12f) * 0.5f;
+    const float dp1 = (p1 - t1) / fmaxf(p1 * (1.f - p1), 1e-12f) * 0.5f;
+    const float sd = p0 * dp0 + p1 * dp1;
+    zl[2 * j] = p0 * (dp0 - sd);
+    zl[2 * j + 1] = p1 * (dp1 - sd);
+    if (e < B) {
+      rows[e * G::GS_SIZE + G::GS_DO] = zl[2 * j];
+      rows[e * G::GS_SIZE + G::GS_DO + 1] = zl[2 * j + 1];
+    }
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < 16 * 64; k += blockDim.x) {
+    const int j = k >> 6, h = k & 63;
+    const long e = (long)blk * 16 + j;
+    if (e < B) rows[e * G::GS_SIZE + G::GS_DDD + h] = Pd[G::D_W2 + h] * zl[2 * j] + Pd[G::D_W2 + 64 + h] * zl[2 * j + 1];
   }
 }
 
@@ -323,17 +458,38 @@ __global__ __launch_bounds__(256) void disc_head_kernel(int B, int mode, const f
 // ---------------------------------------------------------------------------
 // Gen backward of a block through the updated Disc
 // ---------------------------------------------------------------------------
-template <int H>
-__global__ __launch_bounds__(kGW * 64) void gan_gen_kernel(int B, const float* __restrict__ Pg,
-                                                           const float* __restrict__ Pd, float* __restrict__ rows) {
+// Gen backward of a block.  PH 0: one workgroup per block; PH 1 / PH 2: phase
+// 1 (Disc1' over [s; ns]) and phase 3 (the tiles) split over gridDim.y slices
+// as the forward: PH 1 writes the slices' DD' partials (part3), PH 2 sums them,
+// evaluates the head / BCE / dDD' (every slice; slice 0 writes the rows), runs
+// its tiles and writes its dHg partial (part4); the last slice of the block to
+// finish (a device-scope counter per block, reset by it) sums the partials in
+// slice order into the rows.
+struct GanGenArgs {
+  int B;
+  const float* Pg;
+  const float* Pd;
+  float* rows;
+  float* part3;        // [nblk][S][1024]
+  float* part4;        // [nblk][S][1024]
+  unsigned* counter;   // [nblk], zero between launches
+};
+template <int H, int PH>
+__global__ __launch_bounds__(kGW * 64) void gan_gen_kernel(GanGenArgs ga) {
   using K = GanK<H>;
   using G = TGeo<H>;
   constexpr int HH = K::HH, DIN = K::DIN;
   __shared__ __attribute__((aligned(16))) float red[kGW * 4 * 256];
   __shared__ __attribute__((aligned(16))) float ddl[16 * kHP];  // DD', then dDD' [env][hidden]
   __shared__ float zl[32], pl[32];
+  const int B = ga.B;
+  const float* __restrict__ Pg = ga.Pg;
+  const float* __restrict__ Pd = ga.Pd;
+  float* __restrict__ rows = ga.rows;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, g = lane >> 4, i = lane & 15;
-  const long env = (long)blockIdx.x * 16 + i;
+  const int blk = blockIdx.x, sl = blockIdx.y, S = gridDim.y;
+  const int c0 = sl * kGW + wv, cs = S * kGW;
+  const long env = (long)blk * 16 + i;
   const bool eok = env < B;
   float* row = rows + (eok ? env : 0) * G::GS_SIZE;
   const float* D1 = Pd + G::D_W1;
@@ -342,7 +498,7 @@ __global__ __launch_bounds__(kGW * 64) void gan_gen_kernel(int B, const float* _
   f32x4 a[4];
 #pragma unroll
   for (int t = 0; t < 4; ++t) a[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  {  // software-pipelined: chunk c + kGW loaded before chunk c's MFMAs
+  if constexpr (PH != 2) {  // software-pipelined: chunk c + cs loaded before chunk c's MFMAs
     struct Ops {
       f32x4 bv, wd[4];
     };
@@ -362,15 +518,31 @@ __global__ __launch_bounds__(kGW * 64) void gan_gen_kernel(int B, const float* _
 #pragma unroll
         for (int t = 0; t < 4; ++t) a[t] = mfma(cur.wd[t][r], cur.bv[r], a[t]);
     };
-    if (wv < K::KZ) load(wv, A);
-    for (int c = wv; c < K::KZ; c += 2 * kGW) {
-      load(c + kGW < K::KZ ? c + kGW : c, B);
+    if (c0 < K::KZ) load(c0, A);
+    for (int c = c0; c < K::KZ; c += 2 * cs) {
+      load(c + cs < K::KZ ? c + cs : c, B);
       step(c, A);
-      if (c + kGW >= K::KZ) break;
-      load(c + 2 * kGW < K::KZ ? c + 2 * kGW : c + kGW, A);
-      step(c + kGW, B);
+      if (c + cs >= K::KZ) break;
+      load(c + 2 * cs < K::KZ ? c + 2 * cs : c + cs, A);
+      step(c + cs, B);
     }
   }
+  if constexpr (PH == 1) {
+    float* out = ga.part3 + ((long)blk * S + sl) * 1024;
+    reduce4(red, a, wv, lane);
+    for (int k = threadIdx.x; k < 1024; k += blockDim.x) out[k] = red[k];
+    return;
+  } else if constexpr (PH == 2) {
+    const float* in = ga.part3 + (long)blk * S * 1024;
+    for (int k = threadIdx.x; k < 1024; k += blockDim.x) {
+      int h, j;
+      red_index(k, h, j);
+      float v = in[k];
+      for (int q = 1; q < S; ++q) v += in[(long)q * 1024 + k];
+      ddl[j * kHP + h] = v + Pd[G::D_B1 + h];
+    }
+    __syncthreads();
+  } else {
   reduce4(red, a, wv, lane);
   for (int k = threadIdx.x; k < 1024; k += blockDim.x) {
     int h, j;
@@ -378,6 +550,7 @@ __global__ __launch_bounds__(kGW * 64) void gan_gen_kernel(int B, const float* _
     ddl[j * kHP + h] = red[k] + Pd[G::D_B1 + h];
   }
   __syncthreads();
+  }
   // 2. head, BCE toward [0, 1] (PreGANPlus.py:69-73) -> dOut', dDD' = D2'^T dOut'
   head16(ddl, Pd + G::D_W2, Pd + G::D_B2, zl, pl);
   if (threadIdx.x < 16) {
@@ -388,8 +561,8 @@ __global__ __launch_bounds__(kGW * 64) void gan_gen_kernel(int B, const float* _
     const float sd = p0 * dp0 + p1 * dp1;
     zl[2 * j] = p0 * (dp0 - sd);
     zl[2 * j + 1] = p1 * (dp1 - sd);
-    const long e = (long)blockIdx.x * 16 + j;
-    if (e < B) {
+    const long e = (long)blk * 16 + j;
+    if (e < B && sl == 0) {
       rows[e * G::GS_SIZE + G::GS_P] = p0;  // gen_loss's probabilities (pgp_gan_probs)
       rows[e * G::GS_SIZE + G::GS_P + 1] = p1;
       rows[e * G::GS_SIZE + G::GS_DO] = zl[2 * j];
@@ -451,20 +624,44 @@ __global__ __launch_bounds__(kGW * 64) void gan_gen_kernel(int B, const float* _
 #pragma unroll
         for (int t = 0; t < 4; ++t) a[t] = mfma(cur.wa[t][r], dy[r], a[t]);
     };
-    if (wv < K::KS) load(wv, A);
-    for (int c = wv; c < K::KS; c += 2 * kGW) {
-      load(c + kGW < K::KS ? c + kGW : c, B);
+    if (c0 < K::KS) load(c0, A);
+    for (int c = c0; c < K::KS; c += 2 * cs) {
+      load(c + cs < K::KS ? c + cs : c, B);
       step(c, A);
-      if (c + kGW >= K::KS) break;
-      load(c + 2 * kGW < K::KS ? c + 2 * kGW : c + kGW, A);
-      step(c + kGW, B);
+      if (c + cs >= K::KS) break;
+      load(c + 2 * cs < K::KS ? c + 2 * cs : c + cs, A);
+      step(c + cs, B);
     }
   }
   reduce4(red, a, wv, lane);
+  if constexpr (PH == 2) {
+    // this slice's dHg partial; the block's last slice sums them (release:
+    // the partial before the count; acquire: every partial after it)
+    float* base = ga.part4 + (long)blk * S * 1024;
+    for (int k = threadIdx.x; k < 1024; k += blockDim.x)
+      __hip_atomic_store(base + (long)sl * 1024 + k, red[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __shared__ int s_last;
+    __syncthreads();
+    if (threadIdx.x == 0)
+      s_last = __hip_atomic_fetch_add(ga.counter + blk, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
+               (unsigned)(S - 1);
+    __syncthreads();
+    if (!s_last) return;
+    for (int k = threadIdx.x; k < 1024; k += blockDim.x) {
+      int h, j;
+      red_index(k, h, j);
+      float v = __hip_atomic_load(base + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int q = 1; q < S; ++q)
+        v += __hip_atomic_load(base + (long)q * 1024 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if ((long)blk * 16 + j < B) rows[((long)blk * 16 + j) * G::GS_SIZE + G::GS_DH + h] = v;
+    }
+    if (threadIdx.x == 0) __hip_atomic_store(ga.counter + blk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
   for (int k = threadIdx.x; k < 1024; k += blockDim.x) {
     int h, j;
     red_index(k, h, j);
-    if ((long)blockIdx.x * 16 + j < B) rows[((long)blockIdx.x * 16 + j) * G::GS_SIZE + G::GS_DH + h] = red[k];
+    if ((long)blk * 16 + j < B) rows[((long)blk * 16 + j) * G::GS_SIZE + G::GS_DH + h] = red[k];
+  }
   }
 }
 
@@ -613,17 +810,67 @@ hipError_t outer(const OuterArgs& a0, hipStream_t st) {
   return hipSuccess;
 }
 
+// Slices per 16-environment block: the split form when the blocks alone leave
+// the chip mostly idle and each wave still gets a chunk (at C3's 103
+// environments, H = 50: 7 blocks -> 7 x 16 workgroups); one workgroup per
+// block otherwise (H <= 16: 16 chunks are 2 per wave already; large batches).
+constexpr int kGanMaxSlices = 16;
 template <int H>
-hipError_t gan_fwd_h(int B, const float* emb, const float* sched, const float* Pg, const float* Pd, float* ws,
-                     float* ns_out, float* probs, hipStream_t st) {
-  GCK((gan_fwd_kernel<H><<<(B + 15) / 16, kGW * 64, 0, st>>>(B, emb, sched, Pg, Pd, ws, ns_out, probs)));
+int gan_slices(int B) {
+  using K = GanK<H>;
+  const int nblk = (B + 15) / 16;
+  const int cap = std::min(kGanMaxSlices, K::KS / kGW);
+  const int s = std::min(cap, (256 + nblk - 1) / nblk);
+  return s >= 4 ? s : 1;
+}
+// the split form's regions after the rows (floats)
+struct GanSplit {
+  long part1, part2, dsum, part3, part4, counter, total;
+};
+template <int H>
+GanSplit gan_split_offsets(int B) {
+  const long nblk = (B + 15) / 16, S = kGanMaxSlices;
+  GanSplit o{};
+  o.part1 = (long)B * TGeo<H>::GS_SIZE;
+  o.part2 = o.part1 + nblk * S * 2048;
+  o.dsum = o.part2 + nblk * S * 1024;
+  o.part3 = o.dsum + nblk * 1024;
+  o.part4 = o.part3 + nblk * S * 1024;
+  o.counter = o.part4 + nblk * S * 1024;
+  o.total = o.counter + nblk;
+  return o;
+}
+
+template <int H>
+hipError_t gan_fwd_h(int B, const float* emb, const float* logits, const float* protos, float* emb_out,
+                     const float* sched, const float* Pg, const float* Pd, float* ws, float* ns_out, float* probs,
+                     hipStream_t st) {
+  const int nblk = (B + 15) / 16, S = gan_slices<H>(B);
+  const GanSplit o = gan_split_offsets<H>(B);
+  GanFwdArgs a{B, emb, emb_out, logits, protos, sched, Pg, Pd, ws, ns_out, probs, ws + o.part1, ws + o.part2,
+               ws + o.dsum};
+  if (S == 1) {
+    GCK((gan_fwd_kernel<H, 0><<<nblk, kGW * 64, 0, st>>>(a)));
+    return hipSuccess;
+  }
+  GCK((gan_fwd_kernel<H, 1><<<dim3(nblk, S), kGW * 64, 0, st>>>(a)));
+  GCK((gan_fwd_kernel<H, 2><<<dim3(nblk, S), kGW * 64, 0, st>>>(a)));
+  if (probs)  // the forward's Disc probabilities (the Disc step re-evaluates the head itself)
+    GCK((gan_dd_head_kernel<H><<<nblk, 256, 0, st>>>(B, S, 0, Pd, ws, ws + o.part2, ws + o.dsum, nullptr, probs)));
   return hipSuccess;
 }
 
 template <int H>
-hipError_t gan_disc_bwd_h(int B, const float* target, const float* Pd, float* Gdd, float* ws, hipStream_t st) {
+hipError_t gan_disc_bwd_h(int B, const float* target, const float* Pd, float* Gdd, float* ws, float* probs,
+                          hipStream_t st) {
   using G = TGeo<H>;
-  GCK((disc_head_kernel<H><<<(B + 3) / 4, 256, 0, st>>>(B, 1, Pd, ws, target, nullptr)));
+  const int nblk = (B + 15) / 16, S = gan_slices<H>(B);
+  if (S == 1) {
+    GCK((disc_head_kernel<H><<<(B + 3) / 4, 256, 0, st>>>(B, 1, Pd, ws, target, probs)));
+  } else {
+    const GanSplit o = gan_split_offsets<H>(B);
+    GCK((gan_dd_head_kernel<H><<<nblk, 256, 0, st>>>(B, S, 1, Pd, ws, ws + o.part2, ws + o.dsum, target, probs)));
+  }
   OuterArgs a{};
   a.B = B;
   a.ld_rows = G::GS_SIZE;
@@ -639,7 +886,15 @@ template <int H>
 hipError_t gan_gen_bwd_h(int B, const float* Pg, const float* Pd, float* Gdg, float* ws, hipStream_t st) {
   using G = TGeo<H>;
   constexpr int HH = H * H;
-  GCK((gan_gen_kernel<H><<<(B + 15) / 16, kGW * 64, 0, st>>>(B, Pg, Pd, ws)));
+  const int nblk = (B + 15) / 16, S = gan_slices<H>(B);
+  const GanSplit o = gan_split_offsets<H>(B);
+  GanGenArgs ga{B, Pg, Pd, ws, ws + o.part3, ws + o.part4, reinterpret_cast<unsigned*>(ws + o.counter)};
+  if (S == 1) {
+    GCK((gan_gen_kernel<H, 0><<<nblk, kGW * 64, 0, st>>>(ga)));
+  } else {
+    GCK((gan_gen_kernel<H, 1><<<dim3(nblk, S), kGW * 64, 0, st>>>(ga)));
+    GCK((gan_gen_kernel<H, 2><<<dim3(nblk, S), kGW * 64, 0, st>>>(ga)));
+  }
   OuterArgs a{};
   a.B = B;
   a.ld_rows = G::GS_SIZE;
@@ -682,13 +937,14 @@ hipError_t launch_gan_probs(int H, int B, const float* ws, float* probs, hipStre
   return hipErrorInvalidValue;
 }
 
-// one row of GS_SIZE floats per environment
+// one row of GS_SIZE floats per environment, then the split form's partials
+// and per-block counters (zero in a fresh workspace; reset after each use)
 long gan_workspace_floats(int H, int B) {
   if (B < 1) return 0;
   switch (H) {
 #define CASE(h) \
   case h:       \
-    return (long)B * TGeo<h>::GS_SIZE;
+    return gan_split_offsets<h>(B).total;
     PGP_FOR_EACH_H(CASE)
 #undef CASE
   }
@@ -696,11 +952,12 @@ long gan_workspace_floats(int H, int B) {
 }
 
 hipError_t launch_gan_fwd(int H, int B, const float* emb, const float* sched, const float* Pg, const float* Pd,
-                          float* ws, float* ns_out, float* probs, hipStream_t st) {
+                          float* ws, float* ns_out, float* probs, hipStream_t st, const float* logits,
+                          const float* protos, float* emb_out) {
   switch (H) {
 #define CASE(h) \
   case h:       \
-    return gan_fwd_h<h>(B, emb, sched, Pg, Pd, ws, ns_out, probs, st);
+    return gan_fwd_h<h>(B, emb, logits, protos, emb_out, sched, Pg, Pd, ws, ns_out, probs, st);
     PGP_FOR_EACH_H(CASE)
 #undef CASE
   }
@@ -708,11 +965,11 @@ hipError_t launch_gan_fwd(int H, int B, const float* emb, const float* sched, co
 }
 
 hipError_t launch_gan_disc_bwd(int H, int B, const float* target, const float* Pd, float* Gdd, float* ws,
-                               hipStream_t st) {
+                               hipStream_t st, float* probs) {
   switch (H) {
 #define CASE(h) \
   case h:       \
-    return gan_disc_bwd_h<h>(B, target, Pd, Gdd, ws, st);
+    return gan_disc_bwd_h<h>(B, target, Pd, Gdd, ws, probs, st);
     PGP_FOR_EACH_H(CASE)
 #undef CASE
   }

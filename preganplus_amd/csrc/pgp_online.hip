@@ -226,11 +226,12 @@ int pgp_online_step(pgp_online* o, void* main_stream, void* gan_stream, pgp_coll
     OCHK(hipStreamWaitEvent(sg, o->gate, 0));
   }
   mark(o, kG0, sg);
-  OCHK(launch_embed((long)E * H, d.logits + (long)B * H * 2, d.protos + (long)B * H * 2, d.emb, sg));
   mark(o, kG1, sg);
-  OCHK(launch_gan_fwd(H, E, d.emb, d.sched, d.P + go, d.P + dof, d.gan_ws, d.ns, d.probs, sg));
+  //    (the embedding, PreGANPlus.py:129, formed inside the GAN forward's first launch)
+  OCHK(launch_gan_fwd(H, E, nullptr, d.sched, d.P + go, d.P + dof, d.gan_ws, d.ns, nullptr, sg,
+                      d.logits + (long)B * H * 2, d.protos + (long)B * H * 2, d.emb));
   OCHK(launch_simulate(H, E, d.envs, d.ns, d.sched, d.sim_out, d.target, sg));
-  OCHK(launch_gan_disc_bwd(H, E, d.target, d.P + dof, d.G + dof, d.gan_ws, sg));
+  OCHK(launch_gan_disc_bwd(H, E, d.target, d.P + dof, d.G + dof, d.gan_ws, sg, d.probs));
   // 4. main: bookkeeping against the step-start state, then the backward
   //    (the decoders' input gradient dpre written by the same launch)
   OCHK(launch_tune_targets_dp(H, K, B, d.logits, d.protos, d.y, d.cls, d.state, d.update_min, d.mult, d.tgt, d.loss,

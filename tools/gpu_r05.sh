@@ -278,6 +278,7 @@ for step in "$@"; do
       run q16 120 python3 -u bench.py --config tune --hosts 16 --steps 200 --warmup 10 --no-cpu-baseline
       run q50 120 python3 -u bench.py --config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline
       grep -h -o '"ms_per_step": [0-9.]*\|"host_issue_ms_per_step": [0-9.]*' $OUT/q16.out $OUT/q50.out
+      python3 -c "import json; [print(f, json.loads(open('$OUT/' + f + '.out').read().strip().splitlines()[-1])['train_gan_alone']['ms']) for f in ('q16', 'q50')]"
       ;;
     prof16)
       run prof16 240 rocprofv3 --kernel-trace --stats -d $OUT/prof16 -o tune --output-format csv -- python3 bench.py --config tune --hosts 16 --steps 60 --warmup 10 --no-cpu-baseline
