@@ -664,7 +664,7 @@ def bench_tune(args):
     a0, a1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     a0.record(main)
     for _ in range(n_alone):
-        TR.train_gan_batched(tr, sim, step.envs, step.emb, step.sched, out=step.sim_out, target=step.target)
+        step.gan_step()
     a1.record(main)
     torch.cuda.synchronize()
     gan_alone = a0.elapsed_time(a1) / n_alone
@@ -726,8 +726,8 @@ def bench_tune(args):
             "grad_all_reduce_ms": float(sub[subs.index("all_reduce")]),
             "train_gan_alone": {"ms": gan_alone, "environments": E,
                                 "achieved_tflops": RL.gan_step_flops_per_env(H) * E / (gan_alone * 1e-3) / 1e12,
-                                "note": "the GAN step by itself on the whole device (HIP events, main stream); in "
-                                        "the timed step it runs beside the tuning backward on the reserved CUs"},
+                                "note": "the step's GAN part by itself on the whole device (pgp_online_gan_step, "
+                                        "HIP events); in the timed step it runs beside the tuning step on its stream"},
             "roofline": roof,
             # the two training stages as a whole, on the reference formulation's
             # flops (algorithmic, not executed) over the stage's HIP-event span;

@@ -484,6 +484,11 @@ int pgp_online_step(pgp_online* h, void* main_stream, void* gan_stream, pgp_coll
 int pgp_online_timing(pgp_online* h, int on);
 int pgp_online_stage_ms(pgp_online* h, float* ms);
 int pgp_online_steps(const pgp_online* h, double* steps, int n);
+/* The step's GAN part alone (train_gan, PreGANPlus.py:60-81, for the E
+ * environments, from the detect rows of the last step's forward), on `stream`,
+ * world size 1: what pgp_online_step runs on its GAN stream (a measurement
+ * entry: it advances the GAN's AdamW step counts like a step). */
+int pgp_online_gan_step(pgp_online* h, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Offline training of PreGAN's FPE_16 (PreGAN.py:26-27, 39-49: a new FPE is

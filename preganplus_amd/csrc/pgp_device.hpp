@@ -85,6 +85,7 @@ hipError_t launch_gan(const FwdArgs& a, hipStream_t st);
 
 // training ops (pgp_train.hip)
 struct AdamArgs;
+struct AdamFuse;
 long gan_workspace_floats(int H, int B);
 hipError_t launch_adamw(const AdamArgs& a, hipStream_t st);
 // fused batch-1 GAN step (pgp_gan1.hip), H in {8, 16}
@@ -102,11 +103,12 @@ hipError_t launch_gan1_step(int H, const float* target, float* Pg, float* Pd, fl
 hipError_t launch_gan_fwd(int H, int B, const float* emb, const float* sched, const float* Pg, const float* Pd,
                           float* ws, float* ns_out, float* probs, hipStream_t st, const float* logits = nullptr,
                           const float* protos = nullptr, float* emb_out = nullptr);
-// probs (may be nullptr): the Disc probabilities of the step's forward
+// probs (may be nullptr): the Disc probabilities of the step's forward; af
+// (may be nullptr): the section's AdamW applied as its gradients are written
 hipError_t launch_gan_disc_bwd(int H, int B, const float* target, const float* Pd, float* Gdd, float* ws,
-                               hipStream_t st, float* probs = nullptr);
+                               hipStream_t st, float* probs = nullptr, const AdamFuse* af = nullptr);
 hipError_t launch_gan_gen_bwd(int H, int B, const float* Pg, const float* Pd, float* Gdg, float* ws,
-                              hipStream_t st);
+                              hipStream_t st, const AdamFuse* af = nullptr);
 hipError_t launch_gan_probs(int H, int B, const float* ws, float* probs, hipStream_t st);
 // GAN labels (pgp_sim.hip, pgp_simulate's kernel): 1 <= H <= 64
 hipError_t launch_simulate(int H, int E, const double* envs, const float* new_sched, const float* orig_sched,

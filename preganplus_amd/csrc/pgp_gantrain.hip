@@ -682,6 +682,7 @@ struct OuterArgs {
   long ld_rows;
   int nprod;
   OuterProd p[4];
+  AdamFuse adam;  // the section's AdamW applied as each gradient element is written (P == nullptr: not)
 };
 
 // one workgroup per 64 x 64 block of one product: 4 x 4 MFMA tiles, one
@@ -691,8 +692,8 @@ struct OuterArgs {
 // ran a B/4-step chain: 55 us at the online loop's 1,024 environments.
 constexpr int kOW = 8;
 __global__ __launch_bounds__(kOW * 64) void outer_kernel(OuterArgs a) {
-  __shared__ __attribute__((aligned(16))) float red[(kOW - 1) * 16 * 256];
-  __shared__ float bred[(kOW - 1) * 4 * 64];
+  __shared__ __attribute__((aligned(16))) float red[kOW * 16 * 256];
+  __shared__ float bred[kOW * 4 * 64];
   const int lane = threadIdx.x & 63, g = lane >> 4, i = lane & 15, wv = threadIdx.x >> 6;
   const int blk = blockIdx.x;
   int pi = -1;
@@ -751,38 +752,43 @@ __global__ __launch_bounds__(kOW * 64) void outer_kernel(OuterArgs a) {
       x1[t] = xn[t];
     }
   }
-  if (wv > 0) {
+  // every wave's tiles to LDS, then wave w sums tiles 2w, 2w+1 over the waves
+  // in wave order (the same association as one wave accumulating them) and
+  // writes them (with the section's AdamW when fused): the epilogue spread over
+  // the 8 waves
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
+  for (int t = 0; t < 4; ++t) {
 #pragma unroll
-      for (int u = 0; u < 4; ++u) st4(red + (((wv - 1) * 16 + t * 4 + u) * 64 + lane) * 4, acc[t][u]);
-      bred[((wv - 1) * 4 + t) * 64 + lane] = bs[t];
-    }
+    for (int u = 0; u < 4; ++u) st4(red + ((wv * 16 + t * 4 + u) * 64 + lane) * 4, acc[t][u]);
+    bred[(wv * 4 + t) * 64 + lane] = bs[t];
   }
   __syncthreads();
-  if (wv != 0) return;
-#pragma unroll 1
-  for (int w = 1; w < kOW; ++w)
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
+  for (int q = 0; q < 2; ++q) {
+    const int tu = 2 * wv + q, t = tu >> 2, u = tu & 3;
+    f32x4 v = ld4(red + ((0 * 16 + tu) * 64 + lane) * 4);
 #pragma unroll
-      for (int u = 0; u < 4; ++u) acc[t][u] += ld4(red + (((w - 1) * 16 + t * 4 + u) * 64 + lane) * 4);
-      bs[t] += bred[((w - 1) * 4 + t) * 64 + lane];
-    }
+    for (int w = 1; w < kOW; ++w) v += ld4(red + ((w * 16 + tu) * 64 + lane) * 4);
 #pragma unroll
-  for (int t = 0; t < 4; ++t)
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int n = n0 + 16 * t + 4 * g + r, k = k0 + 16 * u + i;
-        if (n < p.N && k < p.K) p.dW[(long)n * p.ldw + k] = acc[t][u][r];
+    for (int r = 0; r < 4; ++r) {
+      const int n = n0 + 16 * t + 4 * g + r, k = k0 + 16 * u + i;
+      if (n < p.N && k < p.K) {
+        float* gp = p.dW + (long)n * p.ldw + k;
+        *gp = v[r];
+        adamw_fused(a.adam, gp, v[r]);
       }
-  if (p.db && kb == 0) {
+    }
+  }
+  if (p.db && kb == 0 && wv < 4) {  // bias tile t = wv
+    const int t = wv;
+    float b = bred[(0 * 4 + t) * 64 + lane];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const float sum = xsum(bs[t], true);
-      if (g == 0 && nok[t]) p.db[n0 + 16 * t + i] = sum;
+    for (int w = 1; w < kOW; ++w) b += bred[(w * 4 + t) * 64 + lane];
+    const float sum = xsum(b, true);
+    if (g == 0 && nok[t]) {
+      float* gp = p.db + n0 + 16 * t + i;
+      *gp = sum;
+      adamw_fused(a.adam, gp, sum);
     }
   }
 }
@@ -862,7 +868,7 @@ hipError_t gan_fwd_h(int B, const float* emb, const float* logits, const float* 
 
 template <int H>
 hipError_t gan_disc_bwd_h(int B, const float* target, const float* Pd, float* Gdd, float* ws, float* probs,
-                          hipStream_t st) {
+                          const AdamFuse* af, hipStream_t st) {
   using G = TGeo<H>;
   const int nblk = (B + 15) / 16, S = gan_slices<H>(B);
   if (S == 1) {
@@ -879,11 +885,13 @@ hipError_t gan_disc_bwd_h(int B, const float* target, const float* Pd, float* Gd
   a.p[0] = OuterProd{ws + G::GS_DDD, ws + G::GS_Z, Gdd + G::D_W1, Gdd + G::D_B1, 64, G::DIN, G::DIN, 0, 0};
   // head: dD2 = sum_b dOut_b DD_b^T, db2 = sum_b dOut_b
   a.p[1] = OuterProd{ws + G::GS_DO, ws + G::GS_DD, Gdd + G::D_W2, Gdd + G::D_B2, 2, 64, 64, 0, 0};
+  if (af) a.adam = *af;
   return outer(a, st);
 }
 
 template <int H>
-hipError_t gan_gen_bwd_h(int B, const float* Pg, const float* Pd, float* Gdg, float* ws, hipStream_t st) {
+hipError_t gan_gen_bwd_h(int B, const float* Pg, const float* Pd, float* Gdg, float* ws, const AdamFuse* af,
+                         hipStream_t st) {
   using G = TGeo<H>;
   constexpr int HH = H * H;
   const int nblk = (B + 15) / 16, S = gan_slices<H>(B);
@@ -904,6 +912,7 @@ hipError_t gan_gen_bwd_h(int B, const float* Pg, const float* Pd, float* Gdg, fl
   // Gen1 over [e; s]: dW1[:, :2H] = sum_b dHg_b e_b^T (+ db1), dW1[:, 2H:] = sum_b dHg_b s_b^T
   a.p[1] = OuterProd{ws + G::GS_DH, ws + G::GS_X, Gdg + G::G_W1, Gdg + G::G_B1, 64, 2 * H, G::GIN, 0, 0};
   a.p[2] = OuterProd{ws + G::GS_DH, ws + G::GS_Z, Gdg + G::G_W1 + 2 * H, nullptr, 64, HH, G::GIN, 0, 0};
+  if (af) a.adam = *af;
   return outer(a, st);
 }
 
@@ -965,11 +974,11 @@ hipError_t launch_gan_fwd(int H, int B, const float* emb, const float* sched, co
 }
 
 hipError_t launch_gan_disc_bwd(int H, int B, const float* target, const float* Pd, float* Gdd, float* ws,
-                               hipStream_t st, float* probs) {
+                               hipStream_t st, float* probs, const AdamFuse* af) {
   switch (H) {
 #define CASE(h) \
   case h:       \
-    return gan_disc_bwd_h<h>(B, target, Pd, Gdd, ws, probs, st);
+    return gan_disc_bwd_h<h>(B, target, Pd, Gdd, ws, probs, af, st);
     PGP_FOR_EACH_H(CASE)
 #undef CASE
   }
@@ -977,11 +986,11 @@ hipError_t launch_gan_disc_bwd(int H, int B, const float* target, const float* P
 }
 
 hipError_t launch_gan_gen_bwd(int H, int B, const float* Pg, const float* Pd, float* Gdg, float* ws,
-                              hipStream_t st) {
+                              hipStream_t st, const AdamFuse* af) {
   switch (H) {
 #define CASE(h) \
   case h:       \
-    return gan_gen_bwd_h<h>(B, Pg, Pd, Gdg, ws, st);
+    return gan_gen_bwd_h<h>(B, Pg, Pd, Gdg, ws, af, st);
     PGP_FOR_EACH_H(CASE)
 #undef CASE
   }

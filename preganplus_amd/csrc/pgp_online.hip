@@ -98,10 +98,75 @@ void mark(pgp_online* o, int k, hipStream_t s) {
   if (o->timing) (void)hipEventRecord(o->tev[k], s);
 }
 
+// A section's AdamW fused into its weight-gradient kernel (world size 1: no
+// exchange between gradient and update), when every tensor of the section
+// takes the same per-step scalars (all GAN tensors step together); the next
+// step's scalars must have been computed (next_scalars).
+bool fuse_adam(const pgp_online* o, int sec, AdamFuse* f) {
+  const AdamArgs& a = o->adam[sec];
+  if (a.ntensors == 0) return false;
+  for (int i = 1; i < a.ntensors; ++i)
+    if (a.t[i].step_size != a.t[0].step_size || a.t[i].bc2_sqrt != a.t[0].bc2_sqrt ||
+        (a.t[i].active & kAdamFromTable))
+      return false;
+  *f = AdamFuse{a.param, a.m, a.v, a.grad, a.lr_wd, a.b1, a.b2, a.eps, a.t[0].step_size, a.t[0].bc2_sqrt};
+  return true;
+}
+
 int collective(pgp_collective_fn cb, void* user, int which, hipStream_t s) {
   if (!cb) return PGP_OK;
   const int r = cb(user, which, reinterpret_cast<void*>(s));
   return r == 0 ? PGP_OK : ofail(PGP_ERR_STATE, "collective callback failed (which = " + std::to_string(which) + ")");
+}
+
+}  // namespace
+
+namespace {
+// train_gan up to the Disc gradient: the embedding (PreGANPlus.py:129, formed
+// inside the GAN forward's first launch from detect's logits / protos, the
+// forward's last E rows), Gen + Disc forward, the simulated label, the Disc
+// BCE gradient (with its AdamW when fused)
+int gan_part_a(pgp_online* o, hipStream_t sg, bool fused) {
+  const pgp_online_desc& d = o->d;
+  const int H = o->H, E = o->E, B = o->B;
+  const long go = o->sec_lo[kGen], dof = o->sec_lo[kDisc];
+  OCHK(launch_gan_fwd(H, E, nullptr, d.sched, d.P + go, d.P + dof, d.gan_ws, d.ns, nullptr, sg,
+                      d.logits + (long)B * H * 2, d.protos + (long)B * H * 2, d.emb));
+  OCHK(launch_simulate(H, E, d.envs, d.ns, d.sched, d.sim_out, d.target, sg));
+  AdamFuse f{};
+  bool fz = false;
+  if (fused) {
+    next_scalars(o, kDisc);
+    fz = fuse_adam(o, kDisc, &f);
+  }
+  OCHK(launch_gan_disc_bwd(H, E, d.target, d.P + dof, d.G + dof, d.gan_ws, sg, d.probs, fz ? &f : nullptr));
+  if (fused && !fz) OCHK(launch_adamw(o->adam[kDisc], sg));
+  return PGP_OK;
+}
+// the rest: [exchange] Disc AdamW, the Gen step through the updated Disc,
+// [exchange] Gen AdamW
+int gan_part_b(pgp_online* o, hipStream_t sg, bool fused, pgp_collective_fn cb, void* user) {
+  const pgp_online_desc& d = o->d;
+  const int H = o->H, E = o->E;
+  const long go = o->sec_lo[kGen], dof = o->sec_lo[kDisc];
+  if (!fused) {
+    OCALL(collective(cb, user, PGP_COLL_DISC_GRAD, sg));
+    next_scalars(o, kDisc);
+    OCHK(launch_adamw(o->adam[kDisc], sg));
+  }
+  AdamFuse f{};
+  bool fz = false;
+  if (fused) {
+    next_scalars(o, kGen);
+    fz = fuse_adam(o, kGen, &f);
+  }
+  OCHK(launch_gan_gen_bwd(H, E, d.P + go, d.P + dof, d.G + go, d.gan_ws, sg, fz ? &f : nullptr));
+  if (!fused) {
+    OCALL(collective(cb, user, PGP_COLL_GEN_GRAD, sg));
+    next_scalars(o, kGen);
+  }
+  if (!fz) OCHK(launch_adamw(o->adam[kGen], sg));
+  return PGP_OK;
 }
 
 }  // namespace
@@ -227,11 +292,8 @@ int pgp_online_step(pgp_online* o, void* main_stream, void* gan_stream, pgp_coll
   }
   mark(o, kG0, sg);
   mark(o, kG1, sg);
-  //    (the embedding, PreGANPlus.py:129, formed inside the GAN forward's first launch)
-  OCHK(launch_gan_fwd(H, E, nullptr, d.sched, d.P + go, d.P + dof, d.gan_ws, d.ns, nullptr, sg,
-                      d.logits + (long)B * H * 2, d.protos + (long)B * H * 2, d.emb));
-  OCHK(launch_simulate(H, E, d.envs, d.ns, d.sched, d.sim_out, d.target, sg));
-  OCHK(launch_gan_disc_bwd(H, E, d.target, d.P + dof, d.G + dof, d.gan_ws, sg, d.probs));
+  const bool fused = cb == nullptr;  // world size 1: each GAN AdamW inside its gradient kernel
+  OCALL(gan_part_a(o, sg, fused));
   // 4. main: bookkeeping against the step-start state, then the backward
   //    (the decoders' input gradient dpre written by the same launch)
   OCHK(launch_tune_targets_dp(H, K, B, d.logits, d.protos, d.y, d.cls, d.state, d.update_min, d.mult, d.tgt, d.loss,
@@ -240,13 +302,7 @@ int pgp_online_step(pgp_online* o, void* main_stream, void* gan_stream, pgp_coll
   OCHK(launch_tune_backward(o->bwd, d.P, d.G, d.tune_ws, d.logits, d.protos, d.y, d.mult, d.tgt, sm, true));
   mark(o, kE4, sm);
   // 5. the GAN's updates (its collectives on the GAN stream)
-  OCALL(collective(cb, user, PGP_COLL_DISC_GRAD, sg));
-  next_scalars(o, kDisc);
-  OCHK(launch_adamw(o->adam[kDisc], sg));
-  OCHK(launch_gan_gen_bwd(H, E, d.P + go, d.P + dof, d.G + go, d.gan_ws, sg));
-  OCALL(collective(cb, user, PGP_COLL_GEN_GRAD, sg));
-  next_scalars(o, kGen);
-  OCHK(launch_adamw(o->adam[kGen], sg));
+  OCALL(gan_part_b(o, sg, fused, cb, user));
   mark(o, kG2, sg);
   // 6. the tuning step's exchange, state update and AdamW
   OCALL(collective(cb, user, PGP_COLL_TUNE_GRAD, sm));
@@ -281,6 +337,13 @@ int pgp_online_stage_ms(pgp_online* o, float* ms) {
                                            {kE2, kE3}, {kE3, kE4}, {kE4, kE5}, {kE5, kE6}, {kE0, kE6}};
   for (int k = 0; k < PGP_ONLINE_NSTAGE; ++k) OCHK(hipEventElapsedTime(&ms[k], o->tev[pairs[k][0]], o->tev[pairs[k][1]]));
   return PGP_OK;
+}
+
+int pgp_online_gan_step(pgp_online* o, void* stream) {
+  if (!o) return ofail(PGP_ERR_ARG, "pgp_online_gan_step: NULL handle");
+  const hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  OCALL(gan_part_a(o, s, true));
+  return gan_part_b(o, s, true, nullptr, nullptr);
 }
 
 int pgp_online_steps(const pgp_online* o, double* steps, int n) {

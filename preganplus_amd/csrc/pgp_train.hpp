@@ -81,16 +81,34 @@ struct AdamArgs {
 // p *= 1 - lr*wd; m = lerp(m, g, 1-b1); v = b2 v + (1-b2) g^2;
 // p -= lr/bc1 * m / (sqrt(v)/sqrt(bc2) + eps).  Shared by the batched kernel
 // (pgp_train.hip) and the fused batch-1 GAN step (pgp_gan1.hip).
+// One section's AdamW fused into the kernel that writes its gradients (the
+// batched GAN step's weight-gradient kernel, world size 1: no all-reduce
+// between gradient and update): every tensor of the section with the same
+// per-step scalars.  P == nullptr: no update.
+struct AdamFuse {
+  float* P;
+  float* m;
+  float* v;
+  const float* G;  // the gradient buffer the kernel writes (element o of G updates P[o])
+  float lr_wd, b1, b2, eps, step_size, bc2_sqrt;
+};
 #ifdef __HIP__
+__device__ __forceinline__ void adamw_update(float* __restrict__ P, float* __restrict__ M, float* __restrict__ V,
+                                             long o, float g, float lr_wd, float b1, float b2, float eps,
+                                             float step_size, float bc2_sqrt) {
+  float p = P[o] * (1.0f - lr_wd);
+  const float m = M[o] + (1.0f - b1) * (g - M[o]);
+  const float v = b2 * V[o] + (1.0f - b2) * g * g;
+  p -= step_size * m / (sqrtf(v) / bc2_sqrt + eps);
+  P[o] = p;
+  M[o] = m;
+  V[o] = v;
+}
 __device__ __forceinline__ void adamw_elem(const AdamArgs& a, long o, float step_size, float bc2_sqrt) {
-  const float g = a.grad[o];
-  float p = a.param[o] * (1.0f - a.lr_wd);
-  const float m = a.m[o] + (1.0f - a.b1) * (g - a.m[o]);
-  const float v = a.b2 * a.v[o] + (1.0f - a.b2) * g * g;
-  p -= step_size * m / (sqrtf(v) / bc2_sqrt + a.eps);
-  a.param[o] = p;
-  a.m[o] = m;
-  a.v[o] = v;
+  adamw_update(a.param, a.m, a.v, o, a.grad[o], a.lr_wd, a.b1, a.b2, a.eps, step_size, bc2_sqrt);
+}
+__device__ __forceinline__ void adamw_fused(const AdamFuse& f, const float* g_at, float g) {
+  if (f.P) adamw_update(f.P, f.m, f.v, g_at - f.G, g, f.lr_wd, f.b1, f.b2, f.eps, f.step_size, f.bc2_sqrt);
 }
 #endif
 

@@ -1339,8 +1339,9 @@ def _bind_online(L):
     L.pgp_online_timing.argtypes = [ctypes.c_void_p, ctypes.c_int]
     L.pgp_online_stage_ms.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
     L.pgp_online_steps.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+    L.pgp_online_gan_step.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
     for f in ("pgp_online_create", "pgp_online_destroy", "pgp_online_step", "pgp_online_timing",
-              "pgp_online_stage_ms", "pgp_online_steps"):
+              "pgp_online_stage_ms", "pgp_online_steps", "pgp_online_gan_step"):
         getattr(L, f).restype = ctypes.c_int
     L._pgp_online_bound = True
 
@@ -1488,6 +1489,14 @@ class OnlineTrainStep:
         ms = (ctypes.c_float * len(ONLINE_STAGES))()
         _native.check(self.tr._L.pgp_online_stage_ms(self._h, ms), "pgp_online_stage_ms")
         return dict(zip(ONLINE_STAGES, list(ms)))
+
+    def gan_step(self):
+        """The step's GAN part alone on the current stream (pgp_online_gan_step:
+        train_gan for the E environments from the last forward's detect rows,
+        world size 1), as the native step runs it on its GAN stream."""
+        st = torch.cuda.current_stream(self.tr.device)
+        _native.check(self.tr._L.pgp_online_gan_step(self._h, ctypes.c_void_p(st.cuda_stream)),
+                      "pgp_online_gan_step")
 
     def sync(self):
         """The native step's AdamW step counts back into the Trainer's tensor
