@@ -76,6 +76,25 @@ PGP_DEV void reduce4(float* red, const f32x4 (&acc)[4], int wv, int lane) {
   }
   __syncthreads();
 }
+// sum over the S <= kGanMaxSlices slices' partials p[q * stride] in slice
+// order, every load issued before the first add (a loop of load-then-add
+// waited one memory latency per slice); slices past S read nothing and add 0
+template <bool ATOMIC = false>
+PGP_DEV float slice_sum(const float* p, long stride, int S) {
+  float t[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    if (ATOMIC)
+      t[q] = q < S ? __hip_atomic_load(p + q * stride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.f;
+    else
+      t[q] = q < S ? p[q * stride] : 0.f;
+  }
+  float v = t[0];
+#pragma unroll
+  for (int q = 1; q < 16; ++q)
+    if (q < S) v += t[q];
+  return v;
+}
 // element k of reduce4's result -> (hidden row h, column j)
 PGP_DEV void red_index(int k, int& h, int& j) {
   const int t = k >> 8, l = (k >> 2) & 63, r = k & 3;
@@ -240,11 +259,8 @@ __global__ __launch_bounds__(kGW * 64) void gan_fwd_kernel(GanFwdArgs a) {
     for (int k = threadIdx.x; k < 1024; k += blockDim.x) {
       int h, j;
       red_index(k, h, j);
-      float v = in[k], d = in[1024 + k];
-      for (int q = 1; q < S; ++q) {
-        v += in[(long)q * 2048 + k];
-        d += in[(long)q * 2048 + 1024 + k];
-      }
+      float v = slice_sum(in + k, 2048, S);
+      const float d = slice_sum(in + 1024 + k, 2048, S);
       v += Pg[G::G_B1 + h];
       hgl[j * kHP + h] = v;
       if (sl == 0) {
@@ -376,8 +392,7 @@ __global__ __launch_bounds__(256) void gan_dd_head_kernel(int B, int S, int mode
   for (int k = threadIdx.x; k < 1024; k += blockDim.x) {
     int h, j;
     red_index(k, h, j);
-    float v = in[k];
-    for (int q = 1; q < S; ++q) v += in[(long)q * 1024 + k];
+    float v = slice_sum(in + k, 1024, S);
     v = (v + dsum[(long)blk * 1024 + k]) + Pd[G::D_B1 + h];
     ddl[j * kHP + h] = v;
     if ((long)blk * 16 + j < B) rows[((long)blk * 16 + j) * G::GS_SIZE + G::GS_DD + h] = v;
@@ -537,8 +552,7 @@ __global__ __launch_bounds__(kGW * 64) void gan_gen_kernel(GanGenArgs ga) {
     for (int k = threadIdx.x; k < 1024; k += blockDim.x) {
       int h, j;
       red_index(k, h, j);
-      float v = in[k];
-      for (int q = 1; q < S; ++q) v += in[(long)q * 1024 + k];
+      const float v = slice_sum(in + k, 1024, S);
       ddl[j * kHP + h] = v + Pd[G::D_B1 + h];
     }
     __syncthreads();
@@ -650,9 +664,7 @@ __global__ __launch_bounds__(kGW * 64) void gan_gen_kernel(GanGenArgs ga) {
     for (int k = threadIdx.x; k < 1024; k += blockDim.x) {
       int h, j;
       red_index(k, h, j);
-      float v = __hip_atomic_load(base + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      for (int q = 1; q < S; ++q)
-        v += __hip_atomic_load(base + (long)q * 1024 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const float v = slice_sum<true>(base + k, 1024, S);
       if ((long)blk * 16 + j < B) rows[((long)blk * 16 + j) * G::GS_SIZE + G::GS_DH + h] = v;
     }
     if (threadIdx.x == 0) __hip_atomic_store(ga.counter + blk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
