@@ -305,7 +305,6 @@ def _dist_setup():
         # processes' hardware queues on that device and time-slice them; the
         # driver's runs, one GPU per rank, keep the GAN / tuning overlap)
         os.environ["PGP_BENCH_ONE_STREAM"] = "1"
-        os.environ["PGP_TUNE_SIDE_STREAM"] = "0"
 
     if dev_env == "cpu":
         device = torch.device("cpu")
@@ -330,11 +329,10 @@ def _dist_setup():
 _HOST_ISSUE_S = None
 
 
-GAN_RESERVED_CUS = int(os.environ.get("PGP_GAN_RESERVED_CUS", "8"))   # CUs the fused tuning launches leave to
-# the GAN step beside them (pgp_tune_reserve_cus); the variable is for A/B runs.
+GAN_RESERVED_CUS = 8   # CUs the fused tuning launches leave to the GAN step beside them (pgp_tune_reserve_cus).
 # The online loop (H = 16 cells, GOBI beside) measured better with none
 # (1.616 -> 1.599 ms, profiles/r04/reserve_ab/); C3 keeps 8 (H = 16: 0.290 -> 0.273 ms)
-LOOP_RESERVED_CUS = int(os.environ.get("PGP_LOOP_RESERVED_CUS", "0"))
+LOOP_RESERVED_CUS = 0
 
 
 def _reserve_cus(main, side, count=None):
@@ -352,15 +350,17 @@ def _reserve_cus(main, side, count=None):
 
 
 def _share_side_stream(world, main, side):
-    """At world size > 1 with a second stream: make it the tuning backward's
-    side stream too (see bench_tune); returns whether it did."""
-    if world == 1 or side is main:
+    """At world size > 1: make the second stream the tuning backward's side
+    stream too (see bench_tune); in one-stream mode (side is main) the library
+    then keeps everything on the main stream.  Returns whether a second stream
+    is shared."""
+    if world == 1:
         return False
     L = _native.lib()
     L.pgp_tune_set_side_stream.argtypes = [ctypes.c_void_p]
     L.pgp_tune_set_side_stream.restype = ctypes.c_int
     _native.check(L.pgp_tune_set_side_stream(ctypes.c_void_p(side.cuda_stream)), "pgp_tune_set_side_stream")
-    return True
+    return side is not main
 
 
 def _backend_label():
@@ -458,6 +458,8 @@ def bench_fleet(args):
             "ms_per_step": el / steps * 1e3, "higher_is_better": True, "scaling": "strong" if args.steps <= 0 else "weak",
             "vs_baseline": None, "dtype": "fp32", "data": "synthetic (C2 distribution), shipped H=16 weights",
             "config": {"workload": "C5: 1024-host fleet = 64 x 16-host cells, cell-windows sharded over GPUs",
+                       "timing": "kernel-only: one resident chunk of cell-windows re-run per step "
+                                 "(inputs in HBM, no host->device streaming)",
                        "hosts_per_cell": H, "cells": 64, "cell_windows_per_step_per_gpu": B,
                        "cell_windows_total": cw, "parallelism": f"dp{world}"},
             "kernel_ms": {n: float(k_mean[k]) for k, n in enumerate(names)},
@@ -896,6 +898,29 @@ def bench_fpe(args):
         torch.distributed.destroy_process_group()
 
 
+def gobi_flops(its, E):
+    """Algorithmic flops of one pgp_gobi_optimize launch: per environment and
+    iteration the surrogate's forward + input gradient, 2 x (288x128 + 128x128
+    + 128x64 + 64x2) MACs, for the mean iterations + 2 (the first forward and
+    the final scoring pass)."""
+    macs_it = 2 * (288 * 128 + 128 * 128 + 128 * 64 + 64 * 2)
+    return 2 * macs_it * (its + 2) * E
+
+
+def gobi_roofline(its, E, k_ms):
+    """GOBI's roofline field: fp32 MFMA peak; achieved = algorithmic flops per
+    launch / the launch's HIP-event time.  The iterations of one environment
+    are a dependent chain (each step's input is the last step's output), so
+    the kernel is latency-bound and far below the peak by construction; the
+    line shows how far."""
+    ach = gobi_flops(its, E) / (k_ms * 1e-3) / 1e12
+    return {"kernel": "gobi_kernel", "bound": "mfma", "achieved": ach, "peak": R.PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+            "frac": ach / R.PEAK_FP32_TFLOPS, "kernel_ms": k_ms,
+            "basis": "algorithmic flops (forward + input gradient per iteration, mean iterations + 2) / HIP-event "
+                     "time of the launch on its stream; latency-bound dependent iteration chain",
+            "traffic": None}
+
+
 def bench_gobi(args):
     """GOBI (scheduler/GOBI.py:19-42, BaGTI/src/opt.py:17-33)
     over a batch of independent 16-host environments per GPU (the fleet's
@@ -912,10 +937,19 @@ def bench_gobi(args):
            torch.empty(E, dtype=torch.float32, device=device))
     for _ in range(args.warmup):
         g.optimize(inits, out=out)
-    el = _timed(world, device, lambda: g.optimize(inits, out=out), args.steps)
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(args.steps)]
+    it = iter(evs)
+
+    def step():
+        e = next(it)
+        e[0].record()
+        g.optimize(inits, out=out)
+        e[1].record()
+
+    el = _timed(world, device, step, args.steps)
     its = out[1].float().mean().item()
+    k_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
     if rank == 0:
-        macs_it = 2 * (288 * 128 + 128 * 128 + 128 * 64 + 64 * 2)  # forward + input gradient
         res = {
             "metric": "GOBI schedules/sec (opt() over energy_latency_16)", "value": E * world * args.steps / el,
             "unit": "schedules/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -924,7 +958,8 @@ def bench_gobi(args):
             "data": "inits = the reference's scheduling dataset rows + synthetic (tests/golden/gobi_h16.npz)",
             "config": {"workload": f"f3: GOBI, {E} independent 16-host environments per GPU", "hosts": 16,
                        "environments_per_gpu": E, "mean_iterations": its, "parallelism": f"dp{world}"},
-            "algorithmic_rate_tflops": 2 * macs_it * (its + 2) * E / (el / args.steps) / 1e12,
+            "algorithmic_rate_tflops": gobi_flops(its, E) / (el / args.steps) / 1e12,
+            "roofline": gobi_roofline(its, E, k_ms),
         }
         if world == 1 and not args.no_cpu_baseline:
             from oracle import gobi_oracle as GO  # CPU baseline leg only
@@ -1119,6 +1154,9 @@ def bench_loop(args):
                        "cells_per_gpu": E, "parallelism": f"dp{world}"},
             "stage_ms": {n: float(acc[k] / steps) for k, n in enumerate(names)},
             "streams": "gan_step on a second stream, concurrent with tune_step (no shared data)"}
+        # the longest stage is GOBI (a latency-bound iteration chain): its roofline
+        res["roofline"] = gobi_roofline(float(gout[1].float().mean().item()), E, float(acc[0] / steps))
+        res["roofline"]["basis"] += "; the loop's gobi stage time (events around the launch and the schedule copy)"
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = loop_cpu_baseline(w, extra, inits_h, x.cpu().numpy(), envs_h,
                                                     y.cpu().numpy(), args.cpu_budget)

@@ -243,12 +243,12 @@ int pgp_tune_backward_prefix(int n_hosts, int fwd_batch, int batch, const float*
  * and joined back into it before the call's last launch, so every result is
  * ordered on `stream` as if all of it ran there.  While `stream` is being
  * captured into a graph the fork / join are captured too (the graph holds the
- * two branches); with PGP_TUNE_SIDE_STREAM=0 in the environment everything
- * stays on `stream`.
+ * two branches).
  * pgp_tune_set_side_stream(s): use the caller's stream `s` as that side stream
  * on the current device from now on (NULL: the library's own again).  A
  * data-parallel caller that already runs a second stream (the GAN step) and two
- * communicators keeps its streams within the hardware queues this way. */
+ * communicators keeps its streams within the hardware queues this way; `s`
+ * equal to the call's own `stream` keeps everything on that one stream. */
 int pgp_tune_set_side_stream(void* stream);
 /* pgp_tune_reserve_cus(n): the fused encoder launches of pgp_tune_forward /
  * pgp_tune_backward use at most (CUs - n) workgroups (one per CU; at most half

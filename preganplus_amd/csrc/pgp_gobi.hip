@@ -184,6 +184,13 @@ __device__ void surrogate_fwd(const float* __restrict__ W, const GobiRegs& R, Go
                               const bool (&act)[kNE], const bool (&dense)[kNE], unsigned long long& gmark_t_) {
   (void)gmark_t_;
   const int t = threadIdx.x, o = t >> 2, sp = t & 3, o3 = t >> 3, sp3 = t & 7;
+  bool act_sp = false, act_sp3 = false;  // this lane's owned environments (sp; sp3 / 2) are active
+#pragma unroll
+  for (int e = 0; e < kNE; ++e) {
+    act_sp = sp == e ? act[e] : act_sp;
+    act_sp3 = (sp3 >> 1) == e ? act[e] : act_sp3;
+  }
+  float mine = 0.f;
   // layer 1 (288 -> 128)
 #pragma unroll
   for (int e = 0; e < kNE; ++e) {
@@ -204,11 +211,14 @@ __device__ void surrogate_fwd(const float* __restrict__ W, const GobiRegs& R, Go
       }
     }
     acc = lane_sum<4>(acc);
-    if (sp == e) {
-      const float a = acc + R.b1;
-      K.a1 = a;
-      L.h1[e][o] = softplus_keep(a, K.z1);
-    }
+    if (sp == e) mine = acc;
+  }
+  // the elementwise tail once per lane, for its own environment sp (not once
+  // per environment under a quarter of the lanes)
+  if (act_sp) {
+    const float a = mine + R.b1;
+    K.a1 = a;
+    L.h1[sp][o] = softplus_keep(a, K.z1);
   }
   __syncthreads();
   GMARK(0);
@@ -220,11 +230,12 @@ __device__ void surrogate_fwd(const float* __restrict__ W, const GobiRegs& R, Go
 #pragma unroll
     for (int j = 0; j < 32; ++j) acc = fmaf(R.w2f[j], L.h1[e][sp * 32 + j], acc);
     acc = lane_sum<4>(acc);
-    if (sp == e) {
-      const float a = acc + R.b2;
-      K.a2 = a;
-      L.h2[e][o] = softplus_keep(a, K.z2);
-    }
+    if (sp == e) mine = acc;
+  }
+  if (act_sp) {
+    const float a = mine + R.b2;
+    K.a2 = a;
+    L.h2[sp][o] = softplus_keep(a, K.z2);
   }
   __syncthreads();
   GMARK(1);
@@ -236,11 +247,14 @@ __device__ void surrogate_fwd(const float* __restrict__ W, const GobiRegs& R, Go
 #pragma unroll
     for (int j = 0; j < 16; ++j) acc = fmaf(R.w3f[j], L.h2[e][sp3 * 16 + j], acc);
     acc = lane_sum<8>(acc);
-    if (sp3 == 2 * e) {
-      const float a = acc + R.b3;
-      const float th = tanhf(a);
-      L.th3[e][o3] = th;
-      L.h3[e][o3] = a - th;
+    if ((sp3 >> 1) == e) mine = acc;
+  }
+  if (act_sp3) {  // lanes 2e and 2e + 1 both hold env e's sum; lane 2e writes
+    const float a = mine + R.b3;
+    const float th = tanhf(a);
+    if (!(sp3 & 1)) {
+      L.th3[sp3 >> 1][o3] = th;
+      L.h3[sp3 >> 1][o3] = a - th;
     }
   }
   __syncthreads();
@@ -355,6 +369,10 @@ __global__ __launch_bounds__(kT) void gobi_kernel(int E, const float* __restrict
     if (!any) break;
     surrogate_fwd(W, R, L, K, true, act, dense, gmark_t_);
     // ---- backward to the input (autograd of z; g3 came with the forward) ----
+    bool act_sp = false;
+#pragma unroll
+    for (int e = 0; e < kNE; ++e) act_sp = sp == e ? act[e] : act_sp;
+    float mine = 0.f;
     // dh2 = W3^T g3 through softplus (W3 column o, k-chunk sp)
 #pragma unroll
     for (int e = 0; e < kNE; ++e) {
@@ -363,8 +381,9 @@ __global__ __launch_bounds__(kT) void gobi_kernel(int E, const float* __restrict
 #pragma unroll
       for (int j = 0; j < 16; ++j) acc = fmaf(R.w3b[j], L.g3[e][sp * 16 + j], acc);
       acc = lane_sum<4>(acc);
-      if (sp == e) L.g2[e][o] = softplus_grad(acc, K.a2, K.z2);
+      if (sp == e) mine = acc;
     }
+    if (act_sp) L.g2[sp][o] = softplus_grad(mine, K.a2, K.z2);
     if (t < kNE) L.flag[(it + 1) & 1][t] = 0;  // next iteration's flag; its last readers passed barriers since
     __syncthreads();
     GMARK(4);
@@ -376,33 +395,42 @@ __global__ __launch_bounds__(kT) void gobi_kernel(int E, const float* __restrict
 #pragma unroll
       for (int j = 0; j < 32; ++j) acc = fmaf(R.w2b[j], L.g2[e][sp * 32 + j], acc);
       acc = lane_sum<4>(acc);
-      if (sp == e) L.g1[e][o] = softplus_grad(acc, K.a1, K.z1);
+      if (sp == e) mine = acc;
     }
+    if (act_sp) L.g1[sp][o] = softplus_grad(mine, K.a1, K.z1);
     __syncthreads();
     GMARK(5);
     // dx for the 256 allocation entries (W1[:, xi] . g1, 2 k-chunks of 64), AdamW, one-hot
     const float* ad = W + GobiW::ADAM + it * 4;
     const float a0 = ad[0], a1 = ad[1], a2 = ad[2];
+    // lane sq owns the entry of envs e = sq + 2k: AdamW and the one-hot once
+    // per k with every lane busy (lanes sq = 0 and 1 on envs 2k and 2k + 1)
 #pragma unroll
-    for (int e = 0; e < kNE; ++e) {
-      if (!act[e]) continue;
-      float acc = 0.f;
+    for (int k = 0; k < kNE / 2; ++k) {
+      if (!act[2 * k] && !act[2 * k + 1]) continue;
+      float gxs[2] = {0.f, 0.f};
 #pragma unroll
-      for (int j = 0; j < 64; ++j) acc = fmaf(R.w1c[j], L.g1[e][sq * 64 + j], acc);
-      const float gx = lane_sum<2>(acc);
-      const bool mine = sq == (e & 1);
+      for (int q = 0; q < 2; ++q) {
+        if (!act[2 * k + q]) continue;
+        float acc = 0.f;
+#pragma unroll
+        for (int j = 0; j < 64; ++j) acc = fmaf(R.w1c[j], L.g1[2 * k + q][sq * 64 + j], acc);
+        gxs[q] = lane_sum<2>(acc);
+      }
+      const int e = sq + 2 * k;
+      const bool on = sq ? act[2 * k + 1] : act[2 * k];
+      const float gx = sq ? gxs[1] : gxs[0];
       // ---- AdamW (torch single-tensor, opt.py:18 defaults) on the entry ----
-      float xv = 0.f;
       const float xold = L.x[e][xi];
-      if (mine) {
-        float& mm = m[e >> 1];
-        float& vv = v[e >> 1];
-        xv = xold * a0;
+      float& mm = m[k];
+      float& vv = v[k];
+      float xv = xold * a0;
+      if (on) {
         mm = mm + 0.1f * (gx - mm);           // exp_avg.lerp_(grad, 1 - beta1)
         vv = vv * 0.999f + 0.001f * gx * gx;  // exp_avg_sq.mul_(beta2).addcmul_(grad, grad, 1 - beta2)
-        const float denom = sqrtf(vv) / a2 + 1e-8f;
-        xv = xv + (-a1) * mm / denom;         // addcdiv_: self + value * t1 / t2 (ATen's order)
       }
+      const float denom = sqrtf(vv) / a2 + 1e-8f;
+      xv = xv + (-a1) * mm / denom;           // addcdiv_: self + value * t1 / t2 (ATen's order)
       // ---- one-hot of the row's first argmax (opt.py:9-15): the row's lanes of this sq ----
       // (max value, then lowest column) over the 16 lanes of this sq in the row's
       // 32: xor 2, the row's parity class by rotations of 4 and 8 (each lane then
@@ -419,7 +447,7 @@ __global__ __launch_bounds__(kT) void gobi_kernel(int E, const float* __restrict
       take(dppf<kDppRor4>(best), dppi<kDppRor4>(bi));
       take(dppf<kDppRor8>(best), dppi<kDppRor8>(bi));
       take(__shfl_xor(best, 16), __shfl_xor(bi, 16));
-      if (mine) {
+      if (on) {
         if (pre) pre[(e0 + e) * kH * kH + entry] = xv;  // test tap: the step's values before the projection
         const float nv = bi == hcol ? 1.f : 0.f;
         if (nv != xold) L.flag[it & 1][e] = 1;  // benign race: every writer stores 1

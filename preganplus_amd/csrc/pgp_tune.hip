@@ -966,11 +966,7 @@ bool plan_h(int B, TunePlan* out) {
   long part = (long)kDwCap * (np_max * 64 + np_max);                  // dW slabs
   part = std::max(part, (long)q.dec_s * B * Q::NOP);                    // decoder split-K
   // decoder weight gradient: windows split over up to 4 parts of >= 8 chunks
-  static const long dws_max = [] {  // PGP_TUNE_DEC_DWS: A/B of the part count
-    const char* v = getenv("PGP_TUNE_DEC_DWS");
-    return v ? std::max(1L, atol(v)) : 4L;
-  }();
-  q.dec_dws = (int)std::max<long>(1, std::min<long>(dws_max, (B + kDwRows - 1) / kDwRows / 8));
+  q.dec_dws = (int)std::max<long>(1, std::min<long>(4, (B + kDwRows - 1) / kDwRows / 8));
   if (q.dec_dws > 1) part = std::max(part, (long)q.dec_dws * (Q::T * Q::NOP * Q::DP + Q::NOP));
   q.part = take(part);
   // the backward's deferred reductions (RedBatch): each dW partial region plus
@@ -1055,15 +1051,7 @@ struct Fork {
   hipStream_t main, side;
   SideStream* ss = nullptr;
   Fork(hipStream_t st, long tokens) : main(st), side(st) {
-    static const bool off = [] {
-      const char* v = getenv("PGP_TUNE_SIDE_STREAM");
-      return v && v[0] == '0';
-    }();
-    static const long min_tokens = [] {  // PGP_TUNE_SIDE_MIN_TOKENS: A/B of the threshold
-      const char* v = getenv("PGP_TUNE_SIDE_MIN_TOKENS");
-      return v ? atol(v) : kSideMinTokens;
-    }();
-    if (off || tokens < min_tokens) return;  // PGP_TUNE_SIDE_STREAM=0: everything on the caller's stream
+    if (tokens < kSideMinTokens) return;
     // while `st` is being captured into a graph the fork / join events become
     // the graph's edges: the side stream joins the capture at the fork's wait
     // and leaves it at the join, so the graph keeps the two branches (a
@@ -1077,7 +1065,7 @@ struct Fork {
     const hipStream_t o = (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 16)
                               ? g_side_override[dev].load(std::memory_order_relaxed)
                               : nullptr;
-    side = o ? o : ss->s;
+    side = o ? o : ss->s;  // an override equal to `st`: everything on the caller's stream
   }
   // `to` waits for everything issued on `from` so far
   hipError_t order(hipStream_t from, hipStream_t to) {
@@ -1158,12 +1146,8 @@ hipError_t tune_bwd_h(const TunePlan& p, const float* P, float* Gd, float* ws, c
   // the same longest wave): C3 at H = 50 1.171 -> 1.131 ms
   // (profiles/r04/side_early/).  Bit 4: layer 0's in_proj weight gradient on
   // the side stream beside the time encoder / GAT tail, 1.137 -> 1.126 ms;
-  // bit 8 (the time encoder's too) measured neutral.  PGP_TUNE_SIDE_EARLY=0
-  // is round 3's placement (A/B).
-  static const int early = [] {
-    const char* v = getenv("PGP_TUNE_SIDE_EARLY");
-    return v ? atoi(v) : 7;
-  }();
+  // bit 8 (the time encoder's too) measured neutral.
+  constexpr int early = 7;
   // side work: the decoders' weight gradients (dpre, encoder output -> G)
   // and each layer's in_proj weight gradient (dQKV [M][3][DP] (x) X -> three
   // [H][H] blocks of L_IN + bias); nothing on the critical path reads them
@@ -1242,12 +1226,8 @@ hipError_t tune_bwd_h(const TunePlan& p, const float* P, float* Gd, float* ws, c
       if ((e = fk.fork()) != hipSuccess) return e;
       if ((e = in_proj_dw(1, sd)) != hipSuccess) return e;
       // layer 1's reductions (its fused slabs, in_proj) on the side stream
-      // beside layer 0's backward, not in the final flush (PGP_TUNE_EARLY_FLUSH=0: A/B)
-      static const bool early_flush = [] {
-        const char* v = getenv("PGP_TUNE_EARLY_FLUSH");
-        return !(v && v[0] == '0');
-      }();
-      if (early_flush && sd != st && (e = rb.flush_now(sd)) != hipSuccess) return e;
+      // beside layer 0's backward, not in the final flush
+      if (sd != st && (e = rb.flush_now(sd)) != hipSuccess) return e;
     }
   }
   // side, beside the serial tail below (time encoder, GAT), unless issued

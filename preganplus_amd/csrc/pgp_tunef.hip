@@ -1195,16 +1195,10 @@ std::atomic<int> g_tf_reserve{0};
 // 4 waves) a quarter of the waves carry 4 units and the rest 3 -- 200
 // workgroups of 4-unit waves finish in the same 4 rounds and leave 56 CUs to
 // the GAN stream and the side work instead of sharing CUs with them.
-// PGP_TF_SPREAD=1 restores the spread over the whole budget (A/B).
 int tf_grid_for(long nu, int waves) {
   const int cus = device_cus();
   const int r = std::max(0, std::min(g_tf_reserve.load(std::memory_order_relaxed), cus / 2));
   const long gmax = std::max<long>(1, std::min<long>(cus - r, (nu + waves - 1) / waves));
-  static const bool spread = [] {
-    const char* e = std::getenv("PGP_TF_SPREAD");
-    return e && e[0] == '1';
-  }();
-  if (spread) return (int)gmax;
   const long m = (nu + waves * gmax - 1) / (waves * gmax);  // units of the longest wave
   return (int)std::max<long>(1, (nu + waves * m - 1) / (waves * m));
 }

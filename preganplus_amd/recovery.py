@@ -99,8 +99,9 @@ class _SaveGan:
 
 class PreGANPlusRecovery(_SaveGan, Recovery):
     def __init__(self, hosts, env, training=False, device=None, model_folder=None, save_folder=_AUTO,
-                 weights=None, extra=None):
+                 weights=None, extra=None, init_seed=0):
         super().__init__()
+        self.init_seed = int(init_seed)   # seeds a fresh model's initialisation (no checkpoint, no packaged weights)
         self.model_name = f"Transformer_{hosts}"
         self.gen_name = f"Gen_{hosts}"
         self.disc_name = f"Disc_{hosts}"
@@ -121,7 +122,7 @@ class PreGANPlusRecovery(_SaveGan, Recovery):
             folder = model_folder or "recovery/PreGANSrc/checkpointsplus"
             ck = os.path.join(folder, f"{self.env_name}_{self.model_name}.ckpt")
             if os.path.exists(ck):   # load_model + load_gan (utils.py:60-84): weights AND training state
-                fresh = lambda: W.torch_default_weights(self.hosts, seed=int(os.environ.get("PGP_INIT_SEED", 0)))
+                fresh = lambda: W.torch_default_weights(self.hosts, seed=self.init_seed)
                 weights, state = W.load_reference_checkpoints(folder, self.env_name, self.hosts, with_state=True,
                                                               gan_fresh=fresh)
                 extra = dict(state, **(extra or {}))
@@ -160,14 +161,14 @@ class PreGANPlusRecovery(_SaveGan, Recovery):
     def _load_new_model(self, folder):
         """load_model without a checkpoint (utils.py:76-78: epoch -1, fresh
         parameters drawn from the distributions torch's module constructors use,
-        ``weights.torch_default_weights``, PGP_INIT_SEED seeds it) and the GAN's
+        ``weights.torch_default_weights``, ``init_seed`` seeds it) and the GAN's
         (load_gan: its checkpoints, else new as well, Gen epoch -1), then
         train_model for num_epochs on the reference's data/<env>/time_series.npy."""
         data = os.path.join("recovery/PreGANSrc/data", self.env_name, "time_series.npy")
         if not os.path.exists(data):
             raise FileNotFoundError(f"no checkpoint for {self.model_name} in {folder}, no packaged weights, and "
                                     f"no training data {data} (utils.py:27-31)")
-        weights = W.torch_default_weights(self.hosts, seed=int(os.environ.get("PGP_INIT_SEED", 0)))
+        weights = W.torch_default_weights(self.hosts, seed=self.init_seed)
         extra = {"meta/transformer/epoch": np.array(-1), "meta/gen/epoch": np.array(-1),
                  "train_time_data": np.load(data)}
         gan = W.load_gan_checkpoints(folder, self.env_name, self.hosts)
@@ -472,7 +473,7 @@ class _GanCheckpointWriter:
     snapshot copy before the next GAN update; ``flush()`` waits for the disk;
     ``close()`` flushes and ends the thread.
     Pickling a checkpoint holds the GIL for milliseconds, so after each write the
-    writer pauses ``min_interval`` seconds (PGP_SAVE_GAN_INTERVAL, default 0.05)
+    writer pauses ``min_interval`` seconds (default 0.05)
     before taking the newest snapshot: calls that come faster than that do not
     wait on the GIL; the files then lag the plugin by at most one pause, and
     ``flush()`` (also at exit) writes the newest state at once.
@@ -497,8 +498,7 @@ class _GanCheckpointWriter:
         self.error = None
         self.urgent = False
         self.stopping = False
-        self.min_interval = float(os.environ.get("PGP_SAVE_GAN_INTERVAL", 0.05) if min_interval is None
-                                  else min_interval)
+        self.min_interval = 0.05 if min_interval is None else float(min_interval)
         self.thread = threading.Thread(target=self._run, daemon=True, name="pgp-save-gan")
         self.thread.start()
         _LIVE_WRITERS.add(self)
@@ -674,8 +674,9 @@ class PreGANRecovery(_SaveGan, Recovery):
     ``save_folder`` is given."""
 
     def __init__(self, hosts, env, training=False, device=None, model_folder=None, save_folder=_AUTO,
-                 weights=None, extra=None):
+                 weights=None, extra=None, init_seed=0):
         super().__init__()
+        self.init_seed = int(init_seed)   # seeds a fresh model's initialisation (no checkpoint, no packaged weights)
         self.model_name = f"FPE_{hosts}"
         self.gen_name = f"Gen_{hosts}"
         self.disc_name = f"Disc_{hosts}"
@@ -699,7 +700,7 @@ class PreGANRecovery(_SaveGan, Recovery):
             if os.path.exists(ck):
                 # load_gan creates a new Gen / Disc for an absent file (utils.py:81-84): a folder
                 # holding only the FPE checkpoint (offline training, before the first train_gan)
-                fresh = lambda: W.torch_default_fpe_weights(self.hosts, seed=int(os.environ.get("PGP_INIT_SEED", 0)))
+                fresh = lambda: W.torch_default_fpe_weights(self.hosts, seed=self.init_seed)
                 weights, state = W.load_reference_checkpoints(folder, self.env_name, self.hosts, encoder="FPE",
                                                               with_state=True, gan_fresh=fresh)
                 extra = dict(state, **(extra or {}))
@@ -740,7 +741,7 @@ class PreGANRecovery(_SaveGan, Recovery):
     def _load_new_model(self, folder):
         """load_model without a checkpoint (utils.py:76-78: epoch -1, a new
         FPE_16 with torch's module initialisation distributions,
-        weights.torch_default_fpe_weights, PGP_INIT_SEED seeds it), train_model
+        weights.torch_default_fpe_weights, ``init_seed`` seeds it), train_model
         (PreGAN.py:39-49: num_epochs epochs of backprop + accuracy over
         load_dataset's whole data/<env>/time_series.npy, the FPE checkpoint
         rewritten after every epoch into the model folder), then the frozen
@@ -749,7 +750,7 @@ class PreGANRecovery(_SaveGan, Recovery):
         if not os.path.exists(data):
             raise FileNotFoundError(f"no checkpoint for {self.model_name} in {folder}, no packaged weights, and "
                                     f"no training data {data} (utils.py:27-31)")
-        init = W.torch_default_fpe_weights(self.hosts, seed=int(os.environ.get("PGP_INIT_SEED", 0)))
+        init = W.torch_default_fpe_weights(self.hosts, seed=self.init_seed)
         series = np.load(data)
         self.fpe_epoch, self.fpe_accuracy_list = -1, []
         fpe, protos = self.train_model(init["fpe"], init["prototypes"], series, folder)

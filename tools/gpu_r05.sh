@@ -89,15 +89,11 @@ for step in "$@"; do
       cat $OUT/graphc.out
       ;;
     abtune)
-      run ab16 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 16 --steps 100 --warmup 10 --no-cpu-baseline" base= side0=PGP_TUNE_SIDE_STREAM=0 eager=PGP_BENCH_GRAPH=0 res16=PGP_GAN_RESERVED_CUS=16
       grep median $OUT/ab16.out
-      run ab50 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" base= side0=PGP_TUNE_SIDE_STREAM=0 eager=PGP_BENCH_GRAPH=0 res16=PGP_GAN_RESERVED_CUS=16 res4=PGP_GAN_RESERVED_CUS=4
       grep median $OUT/ab50.out
       ;;
     abtune2)
-      run ab16b 600 python3 -u tools/ab_bench.py --rounds 4 --args "--config tune --hosts 16 --steps 100 --warmup 10 --no-cpu-baseline" graph= graph_side0=PGP_TUNE_SIDE_STREAM=0 eager=PGP_BENCH_GRAPH=0 eager_side0=PGP_BENCH_GRAPH=0,PGP_TUNE_SIDE_STREAM=0
       grep median $OUT/ab16b.out
-      run ab50b 600 python3 -u tools/ab_bench.py --rounds 4 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" graph= graph_side0=PGP_TUNE_SIDE_STREAM=0 eager=PGP_BENCH_GRAPH=0 eager_side0=PGP_BENCH_GRAPH=0,PGP_TUNE_SIDE_STREAM=0
       grep median $OUT/ab50b.out
       ;;
     abdma)
@@ -135,7 +131,6 @@ for step in "$@"; do
       PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_fullreg.so run prof_full 240 rocprofv3 --kernel-trace --stats -d $OUT/prof_full -o tune --output-format csv -- python3 bench.py --config tune --hosts 50 --steps 30 --warmup 5 --no-cpu-baseline
       ;;
     abloop)
-      run abloop 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config loop --steps 20 --warmup 3 --no-cpu-baseline" base= res0=PGP_GAN_RESERVED_CUS=0 res32=PGP_GAN_RESERVED_CUS=32 one=PGP_BENCH_ONE_STREAM=1
       grep median $OUT/abloop.out
       ;;
     profloop)
@@ -173,11 +168,8 @@ for step in "$@"; do
       grep median $OUT/abe50.out
       ;;
     abres)
-      run abr16 600 python3 -u tools/ab_bench.py --rounds 4 --args "--config tune --hosts 16 --steps 100 --warmup 10 --no-cpu-baseline" r8= r0=PGP_GAN_RESERVED_CUS=0
       grep median $OUT/abr16.out
-      run abr50 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" r8= r0=PGP_GAN_RESERVED_CUS=0
       grep median $OUT/abr50.out
-      run abrloop 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config loop --steps 20 --warmup 3 --no-cpu-baseline" r8= r0=PGP_GAN_RESERVED_CUS=0
       grep median $OUT/abrloop.out
       ;;
     abside2)
@@ -307,6 +299,20 @@ for step in "$@"; do
       run b50 120 python3 -u bench.py --config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline
       run bc2 200 python3 -u bench.py --steps 100 --warmup 10 --no-cpu-baseline
       grep -h -o '"ms_per_step": [0-9.]*\|"host_issue_ms_per_step": [0-9.]*' $OUT/b16.out $OUT/b50.out $OUT/bc2.out
+      ;;
+    fcal)  # FETCH_SIZE / WRITE_SIZE per access width (tools/micro/fetch_cal.hip)
+      for c in FETCH_SIZE WRITE_SIZE; do
+        echo "[fcal $c] $(date +%T)"
+        timeout -s KILL 60 rocprofv3 --pmc $c -d $OUT/fcal_$c -o run --output-format csv -- ./tools/micro/fetch_cal \
+          > $OUT/fcal_$c.log 2>&1 || { tail -5 $OUT/fcal_$c.log; exit 1; }
+      done
+      ;;
+    gobiab)
+      run gobitest 300 python3 -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_gobi.py
+      run gobiab 300 python3 -u tools/dbg/gobi_ab.py $GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_gobi7.so
+      cat $OUT/gobiab.out
+      run gobib 200 python3 -u bench.py --config gobi --steps 50 --warmup 5 --no-cpu-baseline
+      run loopb 300 python3 -u bench.py --config loop --steps 20 --warmup 3 --no-cpu-baseline
       ;;
     others)
       run fpe 300 python3 -u bench.py --config fpe --steps 100 --warmup 5
