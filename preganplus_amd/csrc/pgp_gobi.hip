@@ -74,6 +74,8 @@ __device__ unsigned long long g_gobi_prof[16];
 #endif
 
 constexpr int kA = kH * kH;  // allocation entries
+__host__ __device__ constexpr int kp(int k) { return k + (k >> 4); }  // padded k-major row
+constexpr int kP1 = kp(kN1), kP3 = kp(kN3);
 constexpr int kSA = kA + 1;  // LDS row stride of layer 1's allocation columns (257 = 1 mod 64)
 
 // Layer 1's allocation columns (the forward's one-hot column gather) and the
@@ -81,8 +83,12 @@ constexpr int kSA = kA + 1;  // LDS row stride of layer 1's allocation columns (
 struct GobiLds {
   float w1a[kN1 * kSA];  // W1[o][c*18 + 2 + h] at [o][c*16 + h]
   float x[kNE][kIn];
-  float h1[kNE][kN1], h2[kNE][kN2], h3[kNE][kN3], th3[kNE][kN3];
-  float g1[kNE][kN1], g2[kNE][kN2], g3[kNE][kN3];
+  // the dot products' inputs k-major ([k][env]: one 16-byte read gives the
+  // four environments' k-th value), one pad row after every 16 (kp(k)) so the
+  // lanes' chunks (16 or 32 rows each) start in different banks; the head's
+  // and the input gradient's inputs per environment
+  alignas(16) float h1[kP1][kNE], h2[kP1][kNE], g2[kP1][kNE], g3[kP3][kNE];
+  float h3[kNE][kN3], th3[kNE][kN3], g1[kNE][kN1];
   float o[kNE][4];
   int hs[kNE][kH];   // each container's host (the one-hot column of its allocation row)
   int dense[kNE];    // the init's allocation is not one-hot (iteration 0 takes the dense layer 1)
@@ -165,6 +171,55 @@ __device__ __forceinline__ float lane_sum(float v) {
   return v;
 }
 
+// the four environments' partial dot products over this lane's N-k chunk:
+// w[j] times h[kp(j)][e] (h at the chunk's first row, a multiple of 16), one
+// 16-byte LDS read per k feeding four independent fmaf chains (one per
+// environment, each in k order as before).  The reads go in groups of 2 k,
+// the next group's issued before this group's FMAs; the scheduling barriers
+// keep the compiler from hoisting every read of the chunk (it would spill the
+// weight registers to hold them)
+template <int N>
+__device__ __forceinline__ void dot4(const float* w, const float (*h)[kNE], float (&r)[kNE]) {
+  constexpr int G = 2;
+  static_assert(N % G == 0, "chunk of whole groups");
+  auto ld = [&](int j) { return *reinterpret_cast<const float4*>(h[kp(j)]); };
+#pragma unroll
+  for (int e = 0; e < kNE; ++e) r[e] = 0.f;
+  float4 cur[G], nxt[G];
+#pragma unroll
+  for (int q = 0; q < G; ++q) cur[q] = ld(q);
+#pragma unroll
+  for (int g = 0; g < N / G; ++g) {
+    if (g + 1 < N / G) {
+#pragma unroll
+      for (int q = 0; q < G; ++q) nxt[q] = ld((g + 1) * G + q);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int q = 0; q < G; ++q) {
+      const float wj = w[g * G + q];
+      r[0] = fmaf(wj, cur[q].x, r[0]);
+      r[1] = fmaf(wj, cur[q].y, r[1]);
+      r[2] = fmaf(wj, cur[q].z, r[2]);
+      r[3] = fmaf(wj, cur[q].w, r[3]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int q = 0; q < G; ++q) cur[q] = nxt[q];
+  }
+}
+// the lane-group sums of the four environments' partials; the one of env `mine_e`
+template <int G>
+__device__ __forceinline__ float sum_pick(float (&r)[kNE], int mine_e) {
+  float m = 0.f;
+#pragma unroll
+  for (int e = 0; e < kNE; ++e) {
+    r[e] = lane_sum<G>(r[e]);
+    m = mine_e == e ? r[e] : m;
+  }
+  return m;
+}
+
 // pre-activations (and their exp) of the activations this lane owns
 struct FwdKeep {
   float a1, z1, a2, z2;
@@ -218,37 +273,24 @@ __device__ void surrogate_fwd(const float* __restrict__ W, const GobiRegs& R, Go
   if (act_sp) {
     const float a = mine + R.b1;
     K.a1 = a;
-    L.h1[sp][o] = softplus_keep(a, K.z1);
+    L.h1[kp(o)][sp] = softplus_keep(a, K.z1);
   }
   __syncthreads();
   GMARK(0);
+  float r[kNE];
   // layer 2 (128 -> 128): W2 row o, k-chunk sp
-#pragma unroll
-  for (int e = 0; e < kNE; ++e) {
-    if (!act[e]) continue;
-    float acc = 0.f;
-#pragma unroll
-    for (int j = 0; j < 32; ++j) acc = fmaf(R.w2f[j], L.h1[e][sp * 32 + j], acc);
-    acc = lane_sum<4>(acc);
-    if (sp == e) mine = acc;
-  }
+  dot4<32>(R.w2f, &L.h1[kp(sp * 32)], r);
+  mine = sum_pick<4>(r, sp);
   if (act_sp) {
     const float a = mine + R.b2;
     K.a2 = a;
-    L.h2[sp][o] = softplus_keep(a, K.z2);
+    L.h2[kp(o)][sp] = softplus_keep(a, K.z2);
   }
   __syncthreads();
   GMARK(1);
   // layer 3 (128 -> 64), Tanhshrink: W3 row o3, k-chunk sp3
-#pragma unroll
-  for (int e = 0; e < kNE; ++e) {
-    if (!act[e]) continue;
-    float acc = 0.f;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) acc = fmaf(R.w3f[j], L.h2[e][sp3 * 16 + j], acc);
-    acc = lane_sum<8>(acc);
-    if ((sp3 >> 1) == e) mine = acc;
-  }
+  dot4<16>(R.w3f, &L.h2[kp(sp3 * 16)], r);
+  mine = sum_pick<8>(r, sp3 >> 1);
   if (act_sp3) {  // lanes 2e and 2e + 1 both hold env e's sum; lane 2e writes
     const float a = mine + R.b3;
     const float th = tanhf(a);
@@ -294,7 +336,7 @@ __device__ void surrogate_fwd(const float* __restrict__ W, const GobiRegs& R, Go
         const float d0 = 0.8f * (1.f - o0) * o0, d1 = 0.2f * (1.f - o1) * o1;
         const float gh = R.w40 * d0 + R.w41 * d1;
         const float th = L.th3[e][l];
-        L.g3[e][l] = gh - gh * (1.f - th * th);
+        L.g3[kp(l)][e] = gh - gh * (1.f - th * th);
       }
     }
   }
@@ -374,29 +416,16 @@ __global__ __launch_bounds__(kT) void gobi_kernel(int E, const float* __restrict
     for (int e = 0; e < kNE; ++e) act_sp = sp == e ? act[e] : act_sp;
     float mine = 0.f;
     // dh2 = W3^T g3 through softplus (W3 column o, k-chunk sp)
-#pragma unroll
-    for (int e = 0; e < kNE; ++e) {
-      if (!act[e]) continue;
-      float acc = 0.f;
-#pragma unroll
-      for (int j = 0; j < 16; ++j) acc = fmaf(R.w3b[j], L.g3[e][sp * 16 + j], acc);
-      acc = lane_sum<4>(acc);
-      if (sp == e) mine = acc;
-    }
-    if (act_sp) L.g2[sp][o] = softplus_grad(mine, K.a2, K.z2);
+    float r[kNE];
+    dot4<16>(R.w3b, &L.g3[kp(sp * 16)], r);
+    mine = sum_pick<4>(r, sp);
+    if (act_sp) L.g2[kp(o)][sp] = softplus_grad(mine, K.a2, K.z2);
     if (t < kNE) L.flag[(it + 1) & 1][t] = 0;  // next iteration's flag; its last readers passed barriers since
     __syncthreads();
     GMARK(4);
     // dh1 = W2^T g2 through softplus (W2 column o, k-chunk sp)
-#pragma unroll
-    for (int e = 0; e < kNE; ++e) {
-      if (!act[e]) continue;
-      float acc = 0.f;
-#pragma unroll
-      for (int j = 0; j < 32; ++j) acc = fmaf(R.w2b[j], L.g2[e][sp * 32 + j], acc);
-      acc = lane_sum<4>(acc);
-      if (sp == e) mine = acc;
-    }
+    dot4<32>(R.w2b, &L.g2[kp(sp * 32)], r);
+    mine = sum_pick<4>(r, sp);
     if (act_sp) L.g1[sp][o] = softplus_grad(mine, K.a1, K.z1);
     __syncthreads();
     GMARK(5);

@@ -311,6 +311,8 @@ for step in "$@"; do
       run gobitest 300 python3 -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_gobi.py
       run gobiab 300 python3 -u tools/dbg/gobi_ab.py $GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_gobi7.so
       cat $OUT/gobiab.out
+      PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_gprof.so run gphase 120 python3 -u tools/gobi_phases.py
+      cat $OUT/gphase.out
       run gobib 200 python3 -u bench.py --config gobi --steps 50 --warmup 5 --no-cpu-baseline
       run loopb 300 python3 -u bench.py --config loop --steps 20 --warmup 3 --no-cpu-baseline
       ;;
