@@ -208,10 +208,14 @@ int pgp_forward_fpe_stage(pgp_model* m, int stage, int batch, const float* windo
 size_t pgp_master_len(int n_hosts);               /* floats in P / G            */
 /* floats of tuning workspace for a batch (activations saved by the forward for
  * the backward, token-major, plus split-K / weight-gradient partial slabs).
- * Sizes grow with batch: a workspace for B_max serves every batch <= B_max. */
+ * Sizes grow with batch: a workspace for B_max serves every batch <= B_max.
+ * Zero-fill it once before its first use: its head holds device counters
+ * (last-part finishes of the backward's reductions) that every call leaves at
+ * zero. */
 size_t pgp_tune_workspace_len(int n_hosts, int batch);
 /* floats of GAN-step workspace for a batch (one activation row per
- * environment); grows with batch like the tuning workspace. */
+ * environment); grows with batch like the tuning workspace; zero-filled once
+ * before first use (per-block counters of the split form, left at zero). */
 size_t pgp_gan_workspace_len(int n_hosts, int batch);
 size_t pgp_master_offset(int n_hosts, int section); /* 0 transformer, 1 gen, 2 disc */
 
@@ -322,7 +326,8 @@ int pgp_forward1(int n_hosts, int n_protos, const float* window, const float* sc
  * rows (PreGANPlus.py:107-112: [R-3, R-3, R-2]) infer [E,3,3H]. */
 int pgp_tune_dataset(int n_hosts, int n_env, int n_rows, const double* series, const double* train_max,
                      float* windows, int* y, int* cls, float* infer, void* stream);
-/* doubles of workspace pgp_tune_targets_dp needs for a batch */
+/* doubles of workspace pgp_tune_targets_dp needs for a batch (zero-filled
+ * once before first use: slot 0 is the finishing counter, left at zero) */
 size_t pgp_tune_targets_dp_workspace_len(int batch);
 /* custom_loss / triplet_loss (train.py:13-40) for a batch in the data-parallel
  * form (train.loss_targets_dp; replaces its B x H host loop): every window is

@@ -489,8 +489,9 @@ int pgp_tune_targets_dp(int n_hosts, int n_protos, int batch, const float* logit
   if (n_protos < 3 || n_protos > kMaxProtos) return fail(PGP_ERR_ARG, "triplet_loss needs prototypes 0-2");
   if (batch <= 0 || !logits || !protos || !y || !cls || !state || !mult || !tgt || !loss || !inc || !workspace)
     return fail(PGP_ERR_ARG, "bad tune_targets_dp arguments");
-  HIPCHK(launch_tune_targets_dp(n_hosts, n_protos, batch, logits, protos, y, cls, state, update_min, mult, tgt, loss,
-                                inc, workspace, reinterpret_cast<hipStream_t>(stream)));
+  // state is only read here (no fused state update)
+  HIPCHK(launch_tune_targets_dp(n_hosts, n_protos, batch, logits, protos, y, cls, const_cast<double*>(state),
+                                update_min, mult, tgt, loss, inc, workspace, reinterpret_cast<hipStream_t>(stream)));
   return PGP_OK;
 }
 

@@ -121,6 +121,31 @@ hipError_t launch_simulate(int H, int E, const double* envs, const float* new_sc
 #endif
 
 PGP_DEV f32x4 mfma(float a, float b, f32x4 c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
+// In-launch last-arriver finish (cdna_hip_programming.md, split-K recipe, the
+// write-through form): every partial the other workgroups read was stored
+// write-through (__hip_atomic_store relaxed / agent = sc1 stores), so no
+// release fence: every wave drains its stores, the workgroup counts itself in
+// with ONE relaxed agent-scope add, and the workgroup that came last takes an
+// agent-scope acquire (then plain loads of the partials are current) and
+// resets the counter for the next launch.  Returns whether this workgroup is
+// the last of n (every thread; flag: one __shared__ int of the caller's).
+PGP_DEV bool arrive_last(unsigned* ctr, unsigned n, int* flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const bool last = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == n - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    *flag = last;
+  }
+  __syncthreads();
+  return *flag != 0;
+}
+// a write-through store (sc1) of a partial another workgroup of the launch reads
+PGP_DEV void store_wt(float* p, float v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 PGP_DEV f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 // Sum over lane groups: v + v[lane ^ 16] (+ the same across lane ^ 32), with
 // the gfx950 half-row swaps instead of ds_bpermute round trips.

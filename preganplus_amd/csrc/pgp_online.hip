@@ -274,7 +274,6 @@ int pgp_online_step(pgp_online* o, void* main_stream, void* gan_stream, pgp_coll
   const int H = o->H, E = o->E, R = o->R, B = o->B, K = o->K;
   const hipStream_t sm = reinterpret_cast<hipStream_t>(main_stream);
   const hipStream_t sg = gan_stream ? reinterpret_cast<hipStream_t>(gan_stream) : sm;
-  const long go = o->sec_lo[kGen], dof = o->sec_lo[kDisc];
   o->timed = o->timing;
   // 1. the dataset: R tuning windows per environment, then the E detect windows
   mark(o, kE0, sm);
@@ -290,15 +289,21 @@ int pgp_online_step(pgp_online* o, void* main_stream, void* gan_stream, pgp_coll
     OCHK(hipEventRecord(o->gate, sm));
     OCHK(hipStreamWaitEvent(sg, o->gate, 0));
   }
+  // 4. main: bookkeeping against the step-start state (the decoders' input
+  //    gradient dpre written by the same launch), issued before the GAN part so
+  //    the main stream has work while the host issues the GAN launches
+  //    (H = 16: the main stream sat idle ≈30 µs here)
+  // world size 1 (no exchange of the increments): the state update by the
+  // same launch's last workgroup
+  const StateApplyArgs sa{1, d.decay, o->cr, d.cond_steps, d.adam_rows, d.lr[kTr], d.beta1, d.beta2};
+  OCHK(launch_tune_targets_dp(H, K, B, d.logits, d.protos, d.y, d.cls, d.state, d.update_min, d.mult, d.tgt, d.loss,
+                              d.inc, d.dp_ws, sm, d.tune_ws + o->bwd.dpre, o->bwd.NOP, cb ? nullptr : &sa));
+  mark(o, kE3, sm);
   mark(o, kG0, sg);
   mark(o, kG1, sg);
   const bool fused = cb == nullptr;  // world size 1: each GAN AdamW inside its gradient kernel
   OCALL(gan_part_a(o, sg, fused));
-  // 4. main: bookkeeping against the step-start state, then the backward
-  //    (the decoders' input gradient dpre written by the same launch)
-  OCHK(launch_tune_targets_dp(H, K, B, d.logits, d.protos, d.y, d.cls, d.state, d.update_min, d.mult, d.tgt, d.loss,
-                              d.inc, d.dp_ws, sm, d.tune_ws + o->bwd.dpre, o->bwd.NOP));
-  mark(o, kE3, sm);
+  // then the backward
   OCHK(launch_tune_backward(o->bwd, d.P, d.G, d.tune_ws, d.logits, d.protos, d.y, d.mult, d.tgt, sm, true));
   mark(o, kE4, sm);
   // 5. the GAN's updates (its collectives on the GAN stream)
@@ -308,8 +313,9 @@ int pgp_online_step(pgp_online* o, void* main_stream, void* gan_stream, pgp_coll
   OCALL(collective(cb, user, PGP_COLL_TUNE_GRAD, sm));
   OCALL(collective(cb, user, PGP_COLL_TUNE_STATE, sm));
   mark(o, kE5, sm);
-  OCHK(launch_tune_state_apply(K, d.state, d.inc, d.decay, o->cr, d.cond_steps, d.adam_rows, d.lr[kTr], d.beta1,
-                               d.beta2, sm));
+  if (cb)
+    OCHK(launch_tune_state_apply(K, d.state, d.inc, d.decay, o->cr, d.cond_steps, d.adam_rows, d.lr[kTr], d.beta1,
+                                 d.beta2, sm));
   next_scalars(o, kTr);
   OCHK(launch_adamw(o->adam[kTr], sm));
   mark(o, kE6, sm);

@@ -164,11 +164,10 @@ struct DwArgs {
 // the registers in flight) were slower for every shape (A/B at H = 50: C3
 // 1.287 -> 1.307-1.312 ms, in_proj dW 53 -> 85 us; profiles/r04/dw_rows/)
 constexpr int dw_rows(int) { return kDwRows; }
+// block bx of nbx (the rows split evenly over the blocks), LDS staging ys / xs
 template <int NP, int KP>
-__global__ __launch_bounds__(256) void dw_kernel(DwArgs a) {
+PGP_DEV void dw_block(const DwArgs& a, int bx, int nbx, float* ys, float* xs) {
   constexpr int NT = NP / 16, KT = KP / 16, NTW = (NT + 3) / 4, ROWS = dw_rows(NP);
-  __shared__ __attribute__((aligned(16))) float ys[ROWS * lds_stride(NP)];
-  __shared__ __attribute__((aligned(16))) float xs[ROWS * lds_stride(KP)];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, g = lane >> 4, i = lane & 15;
   f32x4 acc[NTW][KT];
   float pb[NTW];
@@ -179,10 +178,10 @@ __global__ __launch_bounds__(256) void dw_kernel(DwArgs a) {
     for (int u = 0; u < KT; ++u) acc[q][u] = zero4();
   }
   const long nch = (a.M + ROWS - 1) / ROWS;
-  const long r0 = nch * blockIdx.x / gridDim.x * ROWS;
-  const long r1 = std::min<long>(a.M, nch * (blockIdx.x + 1) / gridDim.x * ROWS);
+  const long r0 = nch * bx / nbx * ROWS;
+  const long r1 = std::min<long>(a.M, nch * (bx + 1) / nbx * ROWS);
   dw_accumulate<NP, KP, NTW, ROWS>(r0, r1, a.Y, a.ldy, a.X, a.ldx, a.relu_x, 0, 4, ys, xs, acc, pb);
-  float* P = a.part + (long)blockIdx.x * (NP * KP + NP);
+  float* P = a.part + (long)bx * (NP * KP + NP);
 #pragma unroll
   for (int q = 0; q < NTW; ++q) {
     const int t = wv + 4 * q;
@@ -194,6 +193,38 @@ __global__ __launch_bounds__(256) void dw_kernel(DwArgs a) {
       const float sb = xsum(pb[q], true);
       if (g == 0) P[NP * KP + 16 * t + i] = sb;
     }
+  }
+}
+template <int NP, int KP>
+__global__ __launch_bounds__(256) void dw_kernel(DwArgs a) {
+  constexpr int ROWS = dw_rows(NP);
+  __shared__ __attribute__((aligned(16))) float ys[ROWS * lds_stride(NP)];
+  __shared__ __attribute__((aligned(16))) float xs[ROWS * lds_stride(KP)];
+  dw_block<NP, KP>(a, blockIdx.x, gridDim.x, ys, xs);
+}
+// Several weight gradients in ONE launch (the backward's without a side
+// stream: in_proj of both layers, the time encoder, the GAT fc aggregation):
+// segment s takes blocks [s * nbx, (s + 1) * nbx), each block exactly as its
+// own dw_kernel launch would run it (same rows, same slab), so the partials
+// are bit-identical.  Shapes: kind 0 = <3 DP, DP>, 1 = <DP, DP>, 2 = <DP, XBP>.
+constexpr int kMaxDwSeg = 4;
+struct DwMulti {
+  int n, nbx;
+  int kind[kMaxDwSeg];
+  DwArgs seg[kMaxDwSeg];
+};
+template <int DP, int XBP>
+__global__ __launch_bounds__(256) void dw_multi_kernel(DwMulti m) {
+  constexpr int ROWS = dw_rows(0);
+  constexpr int SY = ROWS * lds_stride(3 * DP), SX = ROWS * lds_stride(DP > XBP ? DP : XBP);
+  __shared__ __attribute__((aligned(16))) float ys[SY];
+  __shared__ __attribute__((aligned(16))) float xs[SX];
+  const int s = blockIdx.x / m.nbx, bx = blockIdx.x - s * m.nbx;
+  if (s >= m.n) return;
+  switch (m.kind[s]) {
+    case 0: dw_block<3 * DP, DP>(m.seg[s], bx, m.nbx, ys, xs); break;
+    case 1: dw_block<DP, DP>(m.seg[s], bx, m.nbx, ys, xs); break;
+    default: dw_block<DP, XBP>(m.seg[s], bx, m.nbx, ys, xs); break;
   }
 }
 
@@ -216,6 +247,7 @@ struct RedArgs {
   float* outA;
   float* outB;
   float* lvl2;
+  int wt = 0;  // outputs stored write-through (read by the launch's last workgroup)
 };
 PGP_DEV void reduce_block(const RedArgs& a, int bx, int by) {
   __shared__ float red[4][65];
@@ -237,6 +269,21 @@ PGP_DEV void reduce_block(const RedArgs& a, int bx, int by) {
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
   if (ok) {
     int p = p0 + pg;
+    // 16 loads in flight per lane, then their adds in the same order as the
+    // loop below (a part count of hundreds was otherwise ~25 dependent memory
+    // rounds of 4 loads: reduce_multi 13 us per C3 step at H = 16)
+    for (; p + 60 < p1; p += 64) {
+      float v[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) v[q] = sp[(long)(p + 4 * q) * a.pstride];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        s0 += v[4 * q];
+        s1 += v[4 * q + 1];
+        s2 += v[4 * q + 2];
+        s3 += v[4 * q + 3];
+      }
+    }
     for (; p + 12 < p1; p += 16) {
       s0 += sp[p * a.pstride];
       s1 += sp[(p + 4) * a.pstride];
@@ -249,14 +296,19 @@ PGP_DEV void reduce_block(const RedArgs& a, int bx, int by) {
   __syncthreads();
   if (pg == 0 && ok) {
     const float t = (red[0][jl] + red[1][jl]) + (red[2][jl] + red[3][jl]);
+    float* dst;
     if (a.lvl2) {
-      a.lvl2[by * nout + o] = t;
+      dst = a.lvl2 + by * nout + o;
     } else if (o < na) {
       const int i = (int)(o / a.cols), j = (int)(o - (long)i * a.cols);
-      a.outA[(long)i * a.ldo + j] = t;
+      dst = a.outA + (long)i * a.ldo + j;
     } else {
-      a.outB[o - na] = t;
+      dst = a.outB + (o - na);
     }
+    if (a.wt)
+      store_wt(dst, t);
+    else
+      *dst = t;
   }
 }
 __global__ __launch_bounds__(256) void reduce_kernel(RedArgs a) { reduce_block(a, blockIdx.x, blockIdx.y); }
@@ -417,9 +469,9 @@ __global__ __launch_bounds__(256) void gat_fwd_kernel(int B, const float* __rest
 // kernel back-propagates into the edge softmax and writes, per workgroup (its
 // 4 (window, step) graphs summed in wave order), Xs = sum_i ds_i x_i and
 // Xt = sum_j dt_j x_j (ds, dt: grads of the per-node source / destination
-// scores), from which gat_param_kernel forms the attn_fc and fc grads.
+// scores), from which gat_param_body forms the attn_fc and fc grads.
 // Workgroup 0 also clears `fcd` (the tokens' dX0 (x) x-bar sum, reduced after
-// this kernel; gat_param_kernel maps it through W_TE into the fc gradient).
+// this kernel; gat_param_body maps it through W_TE into the fc gradient).
 template <int H>
 __global__ __launch_bounds__(256) void gat_bwd_kernel(int B, const float* __restrict__ wcopy,
                                                       const float* __restrict__ P, const float* __restrict__ dX0,
@@ -550,10 +602,12 @@ __global__ __launch_bounds__(256) void gat_mt_kernel(const float* __restrict__ P
 // gat_bwd workgroups in a fixed order; plus the aggregation part of the fc
 // gradient, sum_tokens dG (x) x-bar = W_TE^T fcd.  Runs after the deferred
 // reductions (fcd is one of them).
+// (run by the last workgroup of the backward's final reduction, after its
+// agent-scope acquire on the launch's counter: fcd, just written by other
+// workgroups, is read with plain loads)
 template <int H>
-__global__ __launch_bounds__(256) void gat_param_kernel(int n, const float* __restrict__ GSX,
-                                                        const float* __restrict__ P, const float* __restrict__ fcd,
-                                                        float* __restrict__ Gd) {
+PGP_DEV void gat_param_body(int n, const float* __restrict__ GSX, const float* __restrict__ P,
+                            const float* __restrict__ fcd, float* __restrict__ Gd) {
   using G = TGeo<H>;
   // the workgroups' partials: strided per thread, a butterfly per wave, the
   // four waves in order (one barrier; the 8-level LDS tree took 9)
@@ -588,6 +642,27 @@ __global__ __launch_bounds__(256) void gat_param_kernel(int n, const float* __re
     Gd[G::W_ATT + c] = fc[0] * xs[0] + fc[1] * xs[1] + fc[2] * xs[2];
     Gd[G::W_ATT + H + c] = fc[0] * xt[0] + fc[1] * xt[1] + fc[2] * xt[2];
   }
+}
+// the backward's last reduction launch with the GAT parameter gradient as its
+// tail: the launch's last workgroup (device counter at the workspace head)
+// runs gat_param_body once every reduction, fcd's included, is written
+struct GatTail {
+  int n;
+  const float* gsx;
+  const float* P;
+  const float* fcd;
+  float* Gd;
+  unsigned* counter;
+};
+template <int H>
+__global__ __launch_bounds__(256) void reduce_multi_gat_kernel(RedTable t, GatTail g) {
+  const int bx = blockIdx.x;
+  int s = 0;
+  while (s + 1 < t.n && bx >= t.bx0[s + 1]) ++s;
+  if ((int)blockIdx.y < t.nsplit[s]) reduce_block(t.seg[s], bx - t.bx0[s], blockIdx.y);
+  __shared__ int s_last;
+  if (!arrive_last(g.counter, gridDim.x * gridDim.y, &s_last)) return;
+  gat_param_body<H>(g.n, g.gsx, g.P, g.fcd, g.Gd);
 }
 
 // ============================================================================
@@ -725,12 +800,14 @@ __global__ __launch_bounds__(256) void tune_loss_kernel(int B, int H, int NOP, c
 // Decoder weight gradient: for token tok (grid.x) and output-tile half y,
 // sum over windows of dpre[b] (x) X2[b][tok].  The windows are split over
 // grid.z = S parts (latency: one part is a short chain of LDS-staged chunks);
-// S = 1 adds straight into G, otherwise each part writes its [NOP][DP] slab
-// (and tok 0 its bias column) to `part` and dec_dw_sum adds them in part order.
+// S = 1 writes straight into G, otherwise each part writes its [NOP][DP] slab
+// (and tok 0 its bias column) to `part` and the last part of each (token,
+// half) adds them into G in part order (a device counter per (token, half) at
+// the workspace head).
 template <int H>
 __global__ __launch_bounds__(256) void dec_dw_kernel(int B, const float* __restrict__ dpre,
                                                      const float* __restrict__ X2, float* __restrict__ Gd,
-                                                     float* __restrict__ part) {
+                                                     float* __restrict__ part, unsigned* __restrict__ counter) {
   using Q = TuneGeo<H>;
   using G = TGeo<H>;
   constexpr int NP = Q::NOP, KP = Q::DP, NT = NP / 16, NTW = (NT + 7) / 8, KT = KP / 16;
@@ -753,6 +830,44 @@ __global__ __launch_bounds__(256) void dec_dw_kernel(int B, const float* __restr
   const int w = tok / H, h = tok - w * H;
   float* ps = part + ((long)z * Q::T + tok) * NP * KP;
   float* pbias = part + (long)S * Q::T * NP * KP + (long)z * NP;
+  float sbs[NTW];
+#pragma unroll
+  for (int q = 0; q < NTW; ++q) {
+    const int t = 4 * y + wv + 8 * q;
+    sbs[q] = 0.f;
+    if (t < NT) {
+#pragma unroll
+      for (int u = 0; u < KT; ++u)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int n = 16 * t + 4 * g + r, c = 16 * u + i;
+          if (S > 1) {
+            store_wt(ps + n * KP + c, acc[q][u][r]);
+          } else if (n < 4 * H && c < H) {
+            const long col = (long)h * 3 * H + w * H + c;
+            Gd[(n < 2 * H ? G::W_AN + (long)n * G::L : G::W_PR + (long)(n - 2 * H) * G::L) + col] = acc[q][u][r];
+          }
+        }
+      if (tok == 0) {
+        const float sb = xsum(pb[q], true);
+        sbs[q] = sb;
+        const int n = 16 * t + i;
+        if (S > 1) {
+          if (g == 0) store_wt(pbias + n, sb);
+        } else if (g == 0 && n < 4 * H) {
+          Gd[n < 2 * H ? G::B_AN + n : G::B_PR + n - 2 * H] = sb;
+        }
+      }
+    }
+  }
+  if (S == 1) return;
+  // the last of the S parts of this (token, half) sums them in part order
+  // into G (what dec_dw_sum_kernel did: one launch fewer); its own part from
+  // registers, the others' with plain loads after the agent-scope acquire
+  __shared__ int s_last;
+  if (!arrive_last(counter + 2 * tok + y, (unsigned)S, &s_last)) return;
+  const long zstride = (long)Q::T * NP * KP;
+  const float* p0 = part + (long)tok * NP * KP;
 #pragma unroll
   for (int q = 0; q < NTW; ++q) {
     const int t = 4 * y + wv + 8 * q;
@@ -762,50 +877,35 @@ __global__ __launch_bounds__(256) void dec_dw_kernel(int B, const float* __restr
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int n = 16 * t + 4 * g + r, c = 16 * u + i;
-          if (S > 1) {
-            ps[n * KP + c] = acc[q][u][r];
-          } else if (n < 4 * H && c < H) {
+          if (n < 4 * H && c < H) {
+            // every part loaded (its own too, stored above) before the sum: a
+            // per-part "register or load" choice would wait once per load
+            float pv[kMaxDecDws];
+#pragma unroll
+            for (int zz = 0; zz < kMaxDecDws; ++zz) pv[zz] = zz < S ? p0[zz * zstride + n * KP + c] : 0.f;
+            float v = 0.f;
+#pragma unroll
+            for (int zz = 0; zz < kMaxDecDws; ++zz)
+              if (zz < S) v += pv[zz];
             const long col = (long)h * 3 * H + w * H + c;
-            Gd[(n < 2 * H ? G::W_AN + (long)n * G::L : G::W_PR + (long)(n - 2 * H) * G::L) + col] = acc[q][u][r];
+            Gd[(n < 2 * H ? G::W_AN + (long)n * G::L : G::W_PR + (long)(n - 2 * H) * G::L) + col] = v;
           }
         }
-      if (tok == 0) {
-        const float sb = xsum(pb[q], true);
+      if (tok == 0 && g == 0) {
         const int n = 16 * t + i;
-        if (S > 1) {
-          if (g == 0) pbias[n] = sb;
-        } else if (g == 0 && n < 4 * H) {
-          Gd[n < 2 * H ? G::B_AN + n : G::B_PR + n - 2 * H] = sb;
+        if (n < 4 * H) {
+          const float* pb0 = part + (long)S * Q::T * NP * KP + n;
+          float pv[kMaxDecDws];
+#pragma unroll
+          for (int zz = 0; zz < kMaxDecDws; ++zz) pv[zz] = zz < S ? pb0[(long)zz * NP] : 0.f;
+          float v = 0.f;
+#pragma unroll
+          for (int zz = 0; zz < kMaxDecDws; ++zz)
+            if (zz < S) v += pv[zz];
+          Gd[n < 2 * H ? G::B_AN + n : G::B_PR + n - 2 * H] = v;
         }
       }
     }
-  }
-}
-
-// G += the S parts of dec_dw_kernel, summed in part order (one thread per
-// decoder weight in G's own layout, so the adds into G are coalesced)
-template <int H>
-__global__ __launch_bounds__(256) void dec_dw_sum_kernel(int S, const float* __restrict__ part, float* __restrict__ Gd) {
-  using Q = TuneGeo<H>;
-  using G = TGeo<H>;
-  constexpr int NP = Q::NOP, KP = Q::DP;
-  constexpr long NW = 4L * H * G::L;  // anomaly rows then prototype rows, each [2H][L]
-  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
-  if (idx < NW) {
-    const int n = (int)(idx / G::L);
-    const long col = idx - (long)n * G::L;  // h*3H + w*H + c
-    const int h = (int)(col / (3 * H)), rem = (int)(col - (long)h * 3 * H), w = rem / H, c = rem - w * H;
-    const int tok = w * H + h;
-    const float* src = part + ((long)tok * NP + n) * KP + c;
-    float v = 0.f;
-    for (int z = 0; z < S; ++z) v += src[(long)z * Q::T * NP * KP];
-    Gd[(n < 2 * H ? G::W_AN + (long)n * G::L : G::W_PR + (long)(n - 2 * H) * G::L) + col] = v;
-  } else if (idx < NW + 4 * H) {
-    const int n = (int)(idx - NW);
-    const float* src = part + (long)S * Q::T * NP * KP + n;
-    float v = 0.f;
-    for (int z = 0; z < S; ++z) v += src[(long)z * NP];
-    Gd[n < 2 * H ? G::B_AN + n : G::B_PR + n - 2 * H] = v;
   }
 }
 
@@ -889,6 +989,30 @@ struct RedBatch {
     if (l2.n) TCK((reduce_multi_kernel<<<gx2, 256, 0, st>>>(l2)));
     return hipSuccess;
   }
+  // the last registered reduction's final outputs stored write-through (the
+  // flush's last workgroup reads them: flush_gat)
+  void mark_last_wt() {
+    RedArgs& a = l1.seg[l1.n - 1];
+    if (a.lvl2)
+      l2.seg[l2.n - 1].wt = 1;
+    else
+      a.wt = 1;
+  }
+  // the same, the last launch carrying the GAT parameter gradient as its tail
+  template <int H>
+  hipError_t flush_gat(hipStream_t st, const GatTail& g) {
+    if (used > cap) return hipErrorInvalidValue;
+    l1.bx0[l1.n] = gx1;
+    l2.bx0[l2.n] = gx2;
+    if (!l1.n) return hipErrorInvalidValue;  // the backward always has reductions
+    if (l2.n) {
+      TCK((reduce_multi_kernel<<<dim3(gx1, ny1), 256, 0, st>>>(l1)));
+      TCK((reduce_multi_gat_kernel<H><<<gx2, 256, 0, st>>>(l2, g)));
+    } else {
+      TCK((reduce_multi_gat_kernel<H><<<dim3(gx1, ny1), 256, 0, st>>>(l1, g)));
+    }
+    return hipSuccess;
+  }
   // reduce what is registered so far (on `st`, ordered after its partials) and
   // start new lists; the pool regions already taken stay theirs
   hipError_t flush_now(hipStream_t st) {
@@ -902,13 +1026,21 @@ struct RedBatch {
 
 // dW[N][K] (row stride K) += sum_m Y[m][n] X[m][k];  db[N] += sum_m Y[m][n]
 // (partial slabs from the pool; the reduction is deferred to rb.flush)
+// (dm != nullptr: the launch is deferred into that multi-segment launch as
+// segment kind `kind`, dw_multi_kernel)
 template <int NP, int KP>
 hipError_t dw(const TunePlan& p, RedBatch& rb, const float* Y, int ldy, const float* X, int ldx, int relu, int N,
-              int K, float* gW, float* gb, hipStream_t st) {
+              int K, float* gW, float* gb, hipStream_t st, DwMulti* dm = nullptr, int kind = 0) {
   const long pstride = (long)NP * KP + NP;
   float* part = rb.take((long)p.dw_grid * pstride);
   DwArgs a{p.M, Y, ldy, X, ldx, relu, part};
-  TCK((dw_kernel<NP, KP><<<p.dw_grid, 256, 0, st>>>(a)));
+  if (dm) {
+    if (dm->n >= kMaxDwSeg) return hipErrorInvalidValue;
+    dm->kind[dm->n] = kind;
+    dm->seg[dm->n++] = a;
+  } else {
+    TCK((dw_kernel<NP, KP><<<p.dw_grid, 256, 0, st>>>(a)));
+  }
   return rb.add(p.dw_grid, pstride, part, N, K, KP, gW, K, gb ? N : 0, (long)NP * KP, gb) ? hipSuccess
                                                                                           : hipErrorInvalidValue;
 }
@@ -924,7 +1056,7 @@ bool plan_h(int B, TunePlan* out) {
   q.Q3P = Q::Q3P;
   q.NOP = Q::NOP;
   q.KD = Q::KD;
-  long off = 0;
+  long off = kTuneCounters;  // the head: device counters (zero in a fresh workspace, reset by their users)
   auto take = [&](long n) {
     const long o = off;
     off += (n + 63) / 64 * 64;
@@ -966,7 +1098,7 @@ bool plan_h(int B, TunePlan* out) {
   long part = (long)kDwCap * (np_max * 64 + np_max);                  // dW slabs
   part = std::max(part, (long)q.dec_s * B * Q::NOP);                    // decoder split-K
   // decoder weight gradient: windows split over up to 4 parts of >= 8 chunks
-  q.dec_dws = (int)std::max<long>(1, std::min<long>(4, (B + kDwRows - 1) / kDwRows / 8));
+  q.dec_dws = (int)std::max<long>(1, std::min<long>(kMaxDecDws, (B + kDwRows - 1) / kDwRows / 8));
   if (q.dec_dws > 1) part = std::max(part, (long)q.dec_dws * (Q::T * Q::NOP * Q::DP + Q::NOP));
   q.part = take(part);
   // the backward's deferred reductions (RedBatch): each dW partial region plus
@@ -1148,15 +1280,20 @@ hipError_t tune_bwd_h(const TunePlan& p, const float* P, float* Gd, float* ws, c
   // the side stream beside the time encoder / GAT tail, 1.137 -> 1.126 ms;
   // bit 8 (the time encoder's too) measured neutral.
   constexpr int early = 7;
+  // without a side stream every weight-gradient launch that nothing on the
+  // chain reads (in_proj of both layers, the time encoder, the GAT fc
+  // aggregation) waits for ONE multi-segment launch before the reductions:
+  // their inputs stay untouched until then (per-layer dQKV / X regions, dX0
+  // is read-only after the time encoder)
+  const bool defer = sd == st;
+  DwMulti dm{};
+  dm.nbx = p.dw_grid;
   // side work: the decoders' weight gradients (dpre, encoder output -> G)
   // and each layer's in_proj weight gradient (dQKV [M][3][DP] (x) X -> three
   // [H][H] blocks of L_IN + bias); nothing on the critical path reads them
   auto side_dec = [&]() -> hipError_t {
-    TCK((dec_dw_kernel<H><<<dim3(Q::T, 2, p.dec_dws), 256, 0, sd>>>(B, ws + p.dpre, ws + p.x[2], Gd, ws + p.part)));
-    if (p.dec_dws > 1) {
-      const long nw = 4L * H * G::L + 4 * H;
-      TCK((dec_dw_sum_kernel<H><<<(int)((nw + 255) / 256), 256, 0, sd>>>(p.dec_dws, ws + p.part, Gd)));
-    }
+    TCK((dec_dw_kernel<H><<<dim3(Q::T, 2, p.dec_dws), 256, 0, sd>>>(B, ws + p.dpre, ws + p.x[2], Gd, ws + p.part,
+                                                                     reinterpret_cast<unsigned*>(ws))));
     return hipSuccess;
   };
   auto in_proj_dw = [&](int l, hipStream_t ss) -> hipError_t {
@@ -1165,7 +1302,13 @@ hipError_t tune_bwd_h(const TunePlan& p, const float* P, float* Gd, float* ws, c
     const long pstride = (long)NP * DP + NP;
     float* part = rb.take((long)p.dw_grid * pstride);
     DwArgs a{M, ws + p.dq[l], NP, ws + p.x[l], DP, 0, part};
-    TCK((dw_kernel<NP, DP><<<p.dw_grid, 256, 0, ss>>>(a)));
+    if (defer && ss == st) {
+      if (dm.n >= kMaxDwSeg) return hipErrorInvalidValue;
+      dm.kind[dm.n] = 0;
+      dm.seg[dm.n++] = a;
+    } else {
+      TCK((dw_kernel<NP, DP><<<p.dw_grid, 256, 0, ss>>>(a)));
+    }
     for (int q = 0; q < 3; ++q)
       if (!rb.add(p.dw_grid, pstride, part + (long)q * DP * DP, H, H, DP, Lg + G::L_IN + (long)q * H * H, H, H,
                   (long)NP * DP + q * DP - (long)q * DP * DP, Lg + G::L_INB + q * H))
@@ -1243,20 +1386,25 @@ hipError_t tune_bwd_h(const TunePlan& p, const float* P, float* Gd, float* ws, c
   if ((early & 4) && (e = in_proj_dw(0, sd)) != hipSuccess) return e;
   // time encoder: p.da = grad of X0 (weight gradient: dX0 (x) G)
   if ((e = dw<DP, DP>(p, rb, ws + p.da, DP, ws + p.g, DP, 0, H, H, Gd + G::W_TE, Gd + G::B_TE,
-                      (early & 8) ? sd : st)) != hipSuccess)
+                      (early & 8) ? sd : st, defer ? &dm : nullptr, 1)) != hipSuccess)
     return e;
   // GAT, straight from dX0 (the time encoder's input gradient folded in,
   // gat_bwd_kernel); the fc gradient's aggregation part: fcd = dX0 (x) x-bar
   const int gat_wg = (3 * B + 3) / 4;
   TCK((gat_bwd_kernel<H><<<gat_wg, 256, 0, st>>>(B, ws + p.win, P, ws + p.da, ws + p.gs, ws + p.mt, ws + p.gsx,
                                                   ws + p.fcd)));
-  if ((e = dw<DP, Q::XBP>(p, rb, ws + p.da, DP, ws + p.xb, Q::XBP, 0, H, 3, ws + p.fcd, nullptr, st)) != hipSuccess)
+  if ((e = dw<DP, Q::XBP>(p, rb, ws + p.da, DP, ws + p.xb, Q::XBP, 0, H, 3, ws + p.fcd, nullptr, st,
+                          defer ? &dm : nullptr, 2)) != hipSuccess)
     return e;
+  rb.mark_last_wt();  // fcd: read by the final reduction launch's last workgroup (gat_param_body)
   // without bit 4, layer 0's in_proj weight gradient closes the main stream's share
   if (!(early & 4) && (e = in_proj_dw(0, st)) != hipSuccess) return e;
+  if (dm.n) TCK((dw_multi_kernel<DP, Q::XBP><<<dm.n * dm.nbx, 256, 0, st>>>(dm)));
   if ((e = fk.join()) != hipSuccess) return e;  // the side stream's partials and G writes
-  if ((e = rb.flush(st)) != hipSuccess) return e;  // every deferred weight-gradient reduction: 2 launches
-  TCK((gat_param_kernel<H><<<1, 256, 0, st>>>(gat_wg, ws + p.gsx, P, ws + p.fcd, Gd)));
+  // every deferred weight-gradient reduction, then (the same launch's last
+  // workgroup) the GAT parameter gradient, which needs fcd's reduction
+  const GatTail gt{gat_wg, ws + p.gsx, P, ws + p.fcd, Gd, reinterpret_cast<unsigned*>(ws) + kCtrGatTail};
+  if ((e = rb.flush_gat<H>(st, gt)) != hipSuccess) return e;
   return hipSuccess;
 }
 

@@ -25,6 +25,12 @@ struct TuneGeo {
   static constexpr int XBP = 16;                               // GAT aggregated raw features, padded
 };
 
+// The workspace starts with kTuneCounters floats of device counters (the
+// last-part finishes of the backward's reductions; zero in a fresh workspace,
+// each left at zero by the launch that uses it), then the regions below.
+constexpr long kTuneCounters = 1024;
+constexpr int kCtrGatTail = 1000;
+constexpr int kMaxDecDws = 4;  // decoder weight-gradient parts (windows split over up to 4)  // [0, 2 * 3H): the decoder weight gradient's per-(token, half) counters
 // Workspace regions (float offsets) for one (H, B); region-major, so the same
 // (H, B) must be used by the forward and the backward of one step.
 struct TunePlan {

@@ -147,14 +147,20 @@ __global__ __launch_bounds__(kDsThreads) void tune_dataset_kernel(int H, int E, 
 // sigmoid (train.py:15-21; the negative terms are detached there).
 // ---------------------------------------------------------------------------
 constexpr int kWpb = 4, kTB = 64 * kWpb;
-__device__ __forceinline__ void dp_finish(int tid, int H, int B, int K, int nblk, const double* part, double* inc) {
+// (the caller's last workgroup, after its agent-scope acquire on the counter:
+// the other workgroups' rows are read with plain loads; sh != nullptr also
+// keeps the finished increments in LDS for the fused state update)
+__device__ __forceinline__ void dp_finish(int tid, int H, int B, int K, int nblk, const double* part, double* inc,
+                                          double* sh = nullptr) {
 #pragma clang fp contract(off)
   __shared__ double red[kDpInc][kTB];
   const int t = tid;
   double v[kDpInc] = {};
-  for (int i = t; i < nblk; i += kTB)
-    for (int k = 0; k < kDpInc; ++k)  // other workgroups' rows: coherent loads past this XCD's L2
-      v[k] += __hip_atomic_load(part + (long)i * kDpInc + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (int i = t; i < nblk; i += kTB) {
+    double r[kDpInc];
+    for (int k = 0; k < kDpInc; ++k) r[k] = part[(long)i * kDpInc + k];  // all of the row's loads in flight
+    for (int k = 0; k < kDpInc; ++k) v[k] += r[k];
+  }
   for (int k = 0; k < kDpInc; ++k) red[k][t] = v[k];
   __syncthreads();
   for (int s = kTB / 2; s > 0; s >>= 1) {
@@ -171,17 +177,58 @@ __device__ __forceinline__ void dp_finish(int tid, int H, int B, int K, int nblk
     if (k == 3 * K) x = (double)H * (double)B;  // num_zero: every host counts (train.py:31)
     if (k == 3 * K + 2) x = (double)B;          // windows
     inc[k] = x;
+    if (sh) sh[k] = x;
   }
 }
 
+// One lane per independent value (K prototypes, the counters / factor, and
+// each conditional AdamW row's two bias corrections), each computed exactly as
+// the single-thread version did: the fp64 pow calls run side by side instead
+// of one after another (13 -> a few us on the C3 step's critical path).
+// A row's two lanes are in one wave: its step count is read by both before
+// the even lane writes it back.
+// (inc: global, or the finishing workgroup's LDS copy)
+__device__ __forceinline__ void state_apply_body(int t, int K, double* state, const double* inc,
+                                                 const StateApplyArgs& sa) {
+#pragma clang fp contract(off)
+  auto in = [&](int k) { return inc[k]; };
+  const CondRows& cr = sa.cr;
+  const bool active = in(3 * K + 1) > 0;  // a positive label somewhere in the global batch
+  if (t < K) {
+    const double n = in(2 * K + t);
+    if (n > 0) {
+      state[2 * t] += in(2 * t) / n;
+      state[2 * t + 1] += in(2 * t + 1) / n;
+    }
+  } else if (t == kStateCountLane) {
+    state[2 * K + 1] += in(3 * K);
+    state[2 * K + 2] += in(3 * K + 1);
+    state[2 * K] *= pow(sa.decay, in(3 * K + 2));
+  }
+  const int u = t - kStateCondLane0;  // threads kStateCondLane0.. : row u / 2, bias correction u % 2
+  if (u >= 0 && u < 2 * cr.n) {
+    const int i = u >> 1;
+    const double ds = active ? sa.dsteps[i] + 1.0 : sa.dsteps[i];
+    const double s = ds > 1.0 ? ds : 1.0;
+    float* r = sa.table + 3 * cr.row[i];
+    if ((u & 1) == 0) {
+      r[0] = active ? 1.f : 0.f;
+      r[1] = (float)(sa.lr / (1.0 - pow(sa.b1, s)));
+    } else {
+      r[2] = (float)sqrt(1.0 - pow(sa.b2, s));
+    }
+    __builtin_amdgcn_wave_barrier();
+    if ((u & 1) == 0) sa.dsteps[i] = ds;
+  }
+}
 __global__ __launch_bounds__(kTB) void tune_targets_dp_kernel(int H, int B, const float* __restrict__ logits,
                                                               const float* __restrict__ protos,
                                                               const int* __restrict__ y, const int* __restrict__ cls,
-                                                              const double* __restrict__ state, int K, double update_min,
+                                                              double* state, int K, double update_min,
                                                               float* __restrict__ mult, float* __restrict__ tgt,
                                                               double* __restrict__ loss, double* __restrict__ part,
                                                               unsigned* __restrict__ counter, double* __restrict__ inc,
-                                                              float* __restrict__ dpre, int nop) {
+                                                              float* __restrict__ dpre, int nop, StateApplyArgs sa) {
 #pragma clang fp contract(off)
   __shared__ double s_ce[kWpb][64], s_tl[kWpb][64], s_d0[kWpb][64], s_d1[kWpb][64];
   __shared__ int s_code[kWpb][64];  // -1: negative label; 0-2: class, +4 when the window's prototype moves
@@ -271,59 +318,24 @@ __global__ __launch_bounds__(kTB) void tune_targets_dp_kernel(int H, int B, cons
     __hip_atomic_store(part + (long)blockIdx.x * kDpInc + k, (red[0][k] + red[1][k]) + (red[2][k] + red[3][k]),
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  // the last workgroup sums every workgroup's partials (release: this
-  // workgroup's row before its count; acquire: every row after the count)
+  // the last workgroup sums every workgroup's partials (rows stored
+  // write-through above; arrive_last resets the counter)
   __shared__ int s_last;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned nblk = gridDim.x;
-    const unsigned done = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    s_last = done == nblk - 1;
+  if (!arrive_last(counter, gridDim.x, &s_last)) return;
+  __shared__ double s_inc[3 * kMaxProtos + 3];
+  dp_finish(threadIdx.x, H, B, K, (int)gridDim.x, part, inc, s_inc);
+  if (sa.on) {
+    // world size 1: the state update right here (every other workgroup read
+    // the step-start state before it counted itself done), one launch fewer;
+    // the increments from this workgroup's LDS copy
+    __syncthreads();
+    if (threadIdx.x < kStateThreads) state_apply_body(threadIdx.x, K, state, s_inc, sa);
   }
-  __syncthreads();
-  if (!s_last) return;
-  dp_finish(threadIdx.x, H, B, K, (int)gridDim.x, part, inc);
-  if (threadIdx.x == 0) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
 }
 
-// One lane per independent value (K prototypes, the counters / factor, and
-// each conditional AdamW row's two bias corrections), each computed exactly as
-// the single-thread version did: the fp64 pow calls run side by side instead
-// of one after another (13 -> a few us on the C3 step's critical path).
-// A row's two lanes are in one wave: its step count is read by both before
-// the even lane writes it back.
-__global__ void tune_state_apply_kernel(int K, double* __restrict__ state, const double* __restrict__ inc, double decay,
-                                        CondRows cr, double* __restrict__ dsteps, float* __restrict__ table, double lr,
-                                        double b1, double b2) {
-#pragma clang fp contract(off)
-  const int t = threadIdx.x;
-  const bool active = inc[3 * K + 1] > 0;  // a positive label somewhere in the global batch
-  if (t < K) {
-    const double n = inc[2 * K + t];
-    if (n > 0) {
-      state[2 * t] += inc[2 * t] / n;
-      state[2 * t + 1] += inc[2 * t + 1] / n;
-    }
-  } else if (t == kStateCountLane) {
-    state[2 * K + 1] += inc[3 * K];
-    state[2 * K + 2] += inc[3 * K + 1];
-    state[2 * K] *= pow(decay, inc[3 * K + 2]);
-  }
-  const int u = t - kStateCondLane0;  // threads kStateCondLane0.. : row u / 2, bias correction u % 2
-  if (u >= 0 && u < 2 * cr.n) {
-    const int i = u >> 1;
-    const double ds = active ? dsteps[i] + 1.0 : dsteps[i];
-    const double s = ds > 1.0 ? ds : 1.0;
-    float* r = table + 3 * cr.row[i];
-    if ((u & 1) == 0) {
-      r[0] = active ? 1.f : 0.f;
-      r[1] = (float)(lr / (1.0 - pow(b1, s)));
-    } else {
-      r[2] = (float)sqrt(1.0 - pow(b2, s));
-    }
-    __builtin_amdgcn_wave_barrier();
-    if ((u & 1) == 0) dsteps[i] = ds;
-  }
+__global__ void tune_state_apply_kernel(int K, double* __restrict__ state, const double* __restrict__ inc,
+                                        StateApplyArgs sa) {
+  state_apply_body(threadIdx.x, K, state, inc, sa);
 }
 
 }  // namespace
@@ -341,22 +353,31 @@ hipError_t launch_tune_dataset(int H, int E, int R, const double* series, const 
 long tune_dp_workspace_doubles(int B) { return (long)((B + kWpb - 1) / kWpb) * kDpInc + 1; }
 
 hipError_t launch_tune_targets_dp(int H, int K, int B, const float* logits, const float* protos, const int* y,
-                                  const int* cls, const double* state, double update_min, float* mult, float* tgt,
-                                  double* loss, double* inc, double* ws, hipStream_t st, float* dpre, int nop) {
+                                  const int* cls, double* state, double update_min, float* mult, float* tgt,
+                                  double* loss, double* inc, double* ws, hipStream_t st, float* dpre, int nop,
+                                  const StateApplyArgs* apply) {
   const int nblk = (B + kWpb - 1) / kWpb;
   unsigned* counter = reinterpret_cast<unsigned*>(ws);   // slot 0 (any batch), the partials after it
+  StateApplyArgs sa{};
+  if (apply) {
+    if (K < 0 || K > kMaxProtos || apply->cr.n < 0 || apply->cr.n > kMaxCond) return hipErrorInvalidValue;
+    sa = *apply;
+    sa.on = 1;
+  }
   tune_targets_dp_kernel<<<nblk, kTB, 0, st>>>(H, B, logits, protos, y, cls, state, K, update_min, mult, tgt, loss,
-                                               ws + 1, counter, inc, dpre, nop);
+                                               ws + 1, counter, inc, dpre, nop, sa);
   return hipGetLastError();
 }
 
 hipError_t launch_tune_state_apply(int K, double* state, const double* inc, double decay, const CondRows& cr,
                                    double* dsteps, float* table, double lr, double b1, double b2, hipStream_t st) {
   static_assert(kMaxProtos <= kStateCountLane && kStateCondLane0 + 2 * kMaxCond <= kStateThreads &&
+                    kStateThreads <= kTB &&
                     kStateCondLane0 / 64 == (kStateCondLane0 + 2 * kMaxCond - 1) / 64,
                 "state apply lane map (a row's two lanes in one wave)");
   if (K < 0 || K > kMaxProtos || cr.n < 0 || cr.n > kMaxCond) return hipErrorInvalidValue;
-  tune_state_apply_kernel<<<1, kStateThreads, 0, st>>>(K, state, inc, decay, cr, dsteps, table, lr, b1, b2);
+  tune_state_apply_kernel<<<1, kStateThreads, 0, st>>>(K, state, inc,
+                                                       StateApplyArgs{1, decay, cr, dsteps, table, lr, b1, b2});
   return hipGetLastError();
 }
 

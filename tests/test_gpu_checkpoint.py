@@ -190,3 +190,65 @@ def test_writer_snapshots_are_never_torn(tmp_path):
     assert wr.error is None, wr.error
     assert seen and seen[-1] == 199 and seen == sorted(seen)
     assert not wr.thread.is_alive()
+
+
+def test_checkpoint_folder_without_gan_files_starts_a_new_gan(tmp_path):
+    """load_gan creates a new Gen / Disc when their files are absent
+    (utils.py:76-78, 81-84): a folder holding only the encoder checkpoint (an
+    offline-trained model before its first train_gan) loads the encoder and a
+    fresh GAN (Gen epoch -1, no optimizer state) instead of failing."""
+    from preganplus_amd.recovery import PreGANPlusRecovery
+    H, B = 16, 4
+    w, _ = W.load_npz("preganplus_amd/data/simulator_16.npz")
+    tr = TR.Trainer(H, w, max_batch=B)
+    protos = np.asarray(w["prototypes"])
+    save_checkpoints(tr, str(tmp_path), "simulator", 3, [], [("transformer", f"Transformer_{H}", protos)])
+    assert not os.path.exists(tmp_path / f"simulator_Gen_{H}.ckpt")
+    with pytest.raises(Exception):
+        W.load_reference_checkpoints(str(tmp_path), "simulator", H)   # no fallback given: an absent file raises
+    fresh = W.torch_default_weights(H, seed=5)
+    back, extra = W.load_reference_checkpoints(str(tmp_path), "simulator", H, with_state=True,
+                                               gan_fresh=lambda: fresh)
+    cur = tr.weights_numpy()
+    for k, v in cur["transformer"].items():
+        assert np.array_equal(back["transformer"][k], v), k
+    for sec in ("gen", "disc"):
+        for k, v in fresh[sec].items():
+            assert np.array_equal(np.asarray(back[sec][k]), np.asarray(v)), (sec, k)
+    assert back["meta"]["gan_epoch"] == -1
+    assert not any(k.startswith("opt/gen/") or k.startswith("opt/disc/") for k in extra)
+    # the plugin's checkpoint branch takes the same path (init_seed seeds the new GAN)
+    _, extra0 = W.load_npz("preganplus_amd/data/simulator_16.npz")
+    plug = PreGANPlusRecovery(H, "", model_folder=str(tmp_path), save_folder=None, init_seed=5,
+                              extra={"train_time_data": extra0["train_time_data"]})
+    got = plug.trainer.weights_numpy()
+    for k, v in cur["transformer"].items():
+        assert np.array_equal(got["transformer"][k], v), k
+    for k, v in fresh["gen"].items():
+        assert np.array_equal(got["gen"][k], np.asarray(v, dtype=np.float32)), k
+
+
+def test_writer_close_on_its_own_thread_returns(tmp_path):
+    """close() called on the writer thread itself (a plugin collected by a GC
+    pass that runs there) must not wait for that very thread: it returns, and
+    the thread ends after the write in progress."""
+    import threading
+    from preganplus_amd.recovery import _GanCheckpointWriter
+    H = 16
+    w, _ = W.load_npz("preganplus_amd/data/simulator_16.npz")
+    tr = TR.Trainer(H, w, max_batch=4)
+    wr = _GanCheckpointWriter(tr, f"Gen_{H}", f"Disc_{H}", min_interval=0.0)
+    done = threading.Event()
+    real_write = wr._write
+
+    def write_then_close(*a):
+        real_write(*a)
+        wr.close()            # on the writer thread
+        done.set()
+
+    wr._write = write_then_close
+    wr.post(str(tmp_path), "simulator", 1, [])
+    assert done.wait(60), "close() on the writer thread did not return"
+    wr.thread.join(60)
+    assert not wr.thread.is_alive()
+    assert os.path.exists(tmp_path / f"simulator_Gen_{H}.ckpt")

@@ -300,6 +300,10 @@ for step in "$@"; do
       run bc2 200 python3 -u bench.py --steps 100 --warmup 10 --no-cpu-baseline
       grep -h -o '"ms_per_step": [0-9.]*\|"host_issue_ms_per_step": [0-9.]*' $OUT/b16.out $OUT/b50.out $OUT/bc2.out
       ;;
+    ckpt)
+      run ckpt 300 python3 -u -m pytest tests/test_gpu_checkpoint.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider
+      tail -3 $OUT/ckpt.out
+      ;;
     fcal)  # FETCH_SIZE / WRITE_SIZE per access width (tools/micro/fetch_cal.hip)
       for c in FETCH_SIZE WRITE_SIZE; do
         echo "[fcal $c] $(date +%T)"
