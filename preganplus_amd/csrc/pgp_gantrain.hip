@@ -78,17 +78,14 @@ PGP_DEV void reduce4(float* red, const f32x4 (&acc)[4], int wv, int lane) {
 }
 // sum over the S <= kGanMaxSlices slices' partials p[q * stride] in slice
 // order, every load issued before the first add (a loop of load-then-add
-// waited one memory latency per slice); slices past S read nothing and add 0
-template <bool ATOMIC = false>
+// waited one memory latency per slice); slices past S add nothing
 PGP_DEV float slice_sum(const float* p, long stride, int S) {
   float t[16];
+  // unconditional loads (slices past S re-read slice S - 1, unused): a
+  // "load or 0" select per slice would branch around each load and wait once
+  // per slice
 #pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    if (ATOMIC)
-      t[q] = q < S ? __hip_atomic_load(p + q * stride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.f;
-    else
-      t[q] = q < S ? p[q * stride] : 0.f;
-  }
+  for (int q = 0; q < 16; ++q) t[q] = p[(q < S ? q : S - 1) * stride];
   float v = t[0];
 #pragma unroll
   for (int q = 1; q < 16; ++q)
@@ -649,25 +646,18 @@ __global__ __launch_bounds__(kGW * 64) void gan_gen_kernel(GanGenArgs ga) {
   }
   reduce4(red, a, wv, lane);
   if constexpr (PH == 2) {
-    // this slice's dHg partial; the block's last slice sums them (release:
-    // the partial before the count; acquire: every partial after it)
+    // this slice's dHg partial (stored write-through); the block's last slice
+    // sums them in slice order (arrive_last: drain, count, acquire, reset)
     float* base = ga.part4 + (long)blk * S * 1024;
-    for (int k = threadIdx.x; k < 1024; k += blockDim.x)
-      __hip_atomic_store(base + (long)sl * 1024 + k, red[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int k = threadIdx.x; k < 1024; k += blockDim.x) store_wt(base + (long)sl * 1024 + k, red[k]);
     __shared__ int s_last;
-    __syncthreads();
-    if (threadIdx.x == 0)
-      s_last = __hip_atomic_fetch_add(ga.counter + blk, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
-               (unsigned)(S - 1);
-    __syncthreads();
-    if (!s_last) return;
+    if (!arrive_last(ga.counter + blk, (unsigned)S, &s_last)) return;
     for (int k = threadIdx.x; k < 1024; k += blockDim.x) {
       int h, j;
       red_index(k, h, j);
-      const float v = slice_sum<true>(base + k, 1024, S);
+      const float v = slice_sum(base + k, 1024, S);
       if ((long)blk * 16 + j < B) rows[((long)blk * 16 + j) * G::GS_SIZE + G::GS_DH + h] = v;
     }
-    if (threadIdx.x == 0) __hip_atomic_store(ga.counter + blk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   } else {
   for (int k = threadIdx.x; k < 1024; k += blockDim.x) {
     int h, j;

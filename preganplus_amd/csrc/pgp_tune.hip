@@ -878,11 +878,12 @@ __global__ __launch_bounds__(256) void dec_dw_kernel(int B, const float* __restr
         for (int r = 0; r < 4; ++r) {
           const int n = 16 * t + 4 * g + r, c = 16 * u + i;
           if (n < 4 * H && c < H) {
-            // every part loaded (its own too, stored above) before the sum: a
-            // per-part "register or load" choice would wait once per load
+            // every part loaded (its own too, stored above; parts past S
+            // re-read part S - 1, unused) before the sum: a per-part
+            // "register or load" choice would wait once per load
             float pv[kMaxDecDws];
 #pragma unroll
-            for (int zz = 0; zz < kMaxDecDws; ++zz) pv[zz] = zz < S ? p0[zz * zstride + n * KP + c] : 0.f;
+            for (int zz = 0; zz < kMaxDecDws; ++zz) pv[zz] = p0[(zz < S ? zz : S - 1) * zstride + n * KP + c];
             float v = 0.f;
 #pragma unroll
             for (int zz = 0; zz < kMaxDecDws; ++zz)
@@ -897,7 +898,7 @@ __global__ __launch_bounds__(256) void dec_dw_kernel(int B, const float* __restr
           const float* pb0 = part + (long)S * Q::T * NP * KP + n;
           float pv[kMaxDecDws];
 #pragma unroll
-          for (int zz = 0; zz < kMaxDecDws; ++zz) pv[zz] = zz < S ? pb0[(long)zz * NP] : 0.f;
+          for (int zz = 0; zz < kMaxDecDws; ++zz) pv[zz] = pb0[(long)(zz < S ? zz : S - 1) * NP];
           float v = 0.f;
 #pragma unroll
           for (int zz = 0; zz < kMaxDecDws; ++zz)
@@ -1279,7 +1280,7 @@ hipError_t tune_bwd_h(const TunePlan& p, const float* P, float* Gd, float* ws, c
   // (profiles/r04/side_early/).  Bit 4: layer 0's in_proj weight gradient on
   // the side stream beside the time encoder / GAT tail, 1.137 -> 1.126 ms;
   // bit 8 (the time encoder's too) measured neutral.
-  constexpr int early = 7;
+  constexpr int early = 7;  // round 5 A/B (H = 50): 5 1.102, 13 1.118, 15 1.090, 7 1.092 ms (profiles/r05/side_early_ab.txt)
   // without a side stream every weight-gradient launch that nothing on the
   // chain reads (in_proj of both layers, the time encoder, the GAT fc
   // aggregation) waits for ONE multi-segment launch before the reductions:

@@ -162,11 +162,6 @@ for step in "$@"; do
       run absloop 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config loop --steps 20 --warmup 3 --no-cpu-baseline" balanced= spread=PGP_TF_SPREAD=1
       grep median $OUT/absloop.out
       ;;
-    abearly)
-      PGP_TUNE_SIDE_EARLY=3 run tearly 600 python3 -u -m pytest tests/test_gpu_c3step.py tests/test_gpu_tunedp.py -x -q --timeout 120 --timeout-method thread -m gpu
-      run abe50 900 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" base= e1=PGP_TUNE_SIDE_EARLY=1 e2=PGP_TUNE_SIDE_EARLY=2 e3=PGP_TUNE_SIDE_EARLY=3
-      grep median $OUT/abe50.out
-      ;;
     abres)
       grep median $OUT/abr16.out
       grep median $OUT/abr50.out
@@ -303,6 +298,11 @@ for step in "$@"; do
     ckpt)
       run ckpt 300 python3 -u -m pytest tests/test_gpu_checkpoint.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider
       tail -3 $OUT/ckpt.out
+      ;;
+    abearly)
+      L=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var
+      run abearly 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" base= e5=PGP_LIB=$L/libpreganplus_e5.so e13=PGP_LIB=$L/libpreganplus_e13.so e15=PGP_LIB=$L/libpreganplus_e15.so
+      tail -6 $OUT/abearly.out
       ;;
     fcal)  # FETCH_SIZE / WRITE_SIZE per access width (tools/micro/fetch_cal.hip)
       for c in FETCH_SIZE WRITE_SIZE; do
