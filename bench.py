@@ -538,6 +538,11 @@ def _build_c3_step(H, E, R, world, rank, device):
                                  side=side, reserved=reserved)
 
 
+def _sim_envs(E, H, seed):
+    from preganplus_amd import simulate as SIM
+    return SIM.synth_envs(E, H, seed=seed)
+
+
 def c2_subrecords(world):
     """Sub-records the default (c2) line carries besides its headline value:
     at world > 1 the data-parallel C3 step over the ranks' collective backend
@@ -750,7 +755,7 @@ def bench_tune(args):
         }
         if world == 1 and not args.no_cpu_baseline:
             log("timing CPU baseline ...")
-            res["cpu_baseline"] = tune_cpu_baseline(w, series_h, tmax_h, s.cpu().numpy(), SIM.synth_envs(4, H, 5), H)
+            res["cpu_baseline"] = tune_cpu_baseline(w, series_h, tmax_h, s.cpu().numpy(), _sim_envs(4, H, 5), H)
         emit(res)
     if world > 1:
         torch.distributed.destroy_process_group()

@@ -324,6 +324,7 @@ for step in "$@"; do
       run fpe 300 python3 -u bench.py --config fpe --steps 100 --warmup 5
       run plugin 300 python3 -u bench.py --config plugin --steps 50 --warmup 5
       run loop 300 python3 -u bench.py --config loop --steps 20 --warmup 3
+      run gobi 300 python3 -u bench.py --config gobi --steps 50 --warmup 5
       ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
