@@ -1180,9 +1180,13 @@ std::atomic<hipStream_t> g_side_override[16];
 // one box, C3 at 1,030 windows: H = 16 (49 k tokens) 0.362 -> 0.302 ms per step
 // without the fork, H = 50 (154 k tokens) 1.297 -> 1.340 ms; profiles/r04/s5/)
 constexpr long kSideMinTokens = 65536;
+}  // namespace
+bool tune_side_active(long tokens) { return tokens >= kSideMinTokens; }
+namespace {
 struct Fork {
   hipStream_t main, side;
   SideStream* ss = nullptr;
+  bool capturing = false;
   Fork(hipStream_t st, long tokens) : main(st), side(st) {
     if (tokens < kSideMinTokens) return;
     // while `st` is being captured into a graph the fork / join events become
@@ -1192,6 +1196,7 @@ struct Fork {
     // profiles/r04/s3/graph_concurrency.txt)
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs == hipStreamCaptureStatusInvalidated) return;
+    capturing = cs == hipStreamCaptureStatusActive;
     ss = side_stream();
     if (!ss) return;
     int dev = 0;
@@ -1209,11 +1214,27 @@ struct Fork {
   }
   hipError_t fork() { return order(main, side); }
   hipError_t join() { return order(side, main); }
+  // An event for the NEXT launch on the main stream to signal at its end
+  // (hipExtLaunchKernel's stop event) for a fork right after it: no marker
+  // packet on the main stream.  A hipEventRecord costs the recording stream
+  // ~4.9 us of device time, a stop event ~1.4 (tools/micro/fork_cost.hip,
+  // profiles/r05/fork_cost/).  nullptr (no side stream, or a graph capture:
+  // fork_on records as before).
+  hipEvent_t launch_event() {
+    if (!ss || side == main || capturing) return nullptr;
+    return ss->ev[ss->next.fetch_add(1, std::memory_order_relaxed) % 8];
+  }
+  // fork after the launch that signals `e` (launch_event or the caller's own
+  // stop event); e == nullptr: an ordinary fork
+  hipError_t fork_on(hipEvent_t e) {
+    if (!ss || side == main) return hipSuccess;
+    return e ? hipStreamWaitEvent(side, e, 0) : fork();
+  }
 };
 
 template <int H>
 hipError_t tune_fwd_h(const TunePlan& p, const float* win, const float* P, float* ws, float* latent, float* logits,
-                      float* protos, hipStream_t st) {
+                      float* protos, hipStream_t st, hipEvent_t pre) {
   using Q = TuneGeo<H>;
   const int B = p.B;
   hipError_t e;
@@ -1229,7 +1250,7 @@ hipError_t tune_fwd_h(const TunePlan& p, const float* win, const float* P, float
                                                                   nb_dec, nb_tf)));
     TCK((gat_fwd_kernel<H><<<(3 * B + 3) / 4, 256, 0, st>>>(B, win, P, ws + p.win, ws + p.g, ws + p.xb, ws + p.gs)));
   } else {
-    if ((e = fk.fork()) != hipSuccess) return e;
+    if ((e = fk.fork_on(pre)) != hipSuccess) return e;
     TCK((dec_pack_kernel<H><<<(int)((Q::NOP * Q::KD + 255) / 256), 256, 0, fk.side>>>(P, ws + p.wp, ws + p.wpt)));
     TCK((gat_mt_kernel<H><<<1, 192, 0, fk.side>>>(P, ws + p.mt)));  // for the backward's GAT (gat_bwd_kernel)
     TCK((gat_fwd_kernel<H><<<(3 * B + 3) / 4, 256, 0, st>>>(B, win, P, ws + p.win, ws + p.g, ws + p.xb, ws + p.gs)));
@@ -1259,7 +1280,7 @@ hipError_t tune_fwd_h(const TunePlan& p, const float* win, const float* P, float
 template <int H>
 hipError_t tune_bwd_h(const TunePlan& p, const float* P, float* Gd, float* ws, const float* logits,
                       const float* protos, const int* y, const float* mult, const float* tgt, hipStream_t st,
-                      bool dpre_ready) {
+                      bool dpre_ready, hipEvent_t pre) {
   using Q = TuneGeo<H>;
   using G = TGeo<H>;
   constexpr int DP = Q::DP;
@@ -1318,7 +1339,9 @@ hipError_t tune_bwd_h(const TunePlan& p, const float* P, float* Gd, float* ws, c
   };
 
   if (early & 2) {
-    if ((e = fk.fork()) != hipSuccess) return e;
+    // after the targets (pre: the caller's launch of them signals it; the
+    // loss kernel above when dpre was not ready)
+    if ((e = fk.fork_on(dpre_ready ? pre : nullptr)) != hipSuccess) return e;
     if ((e = side_dec()) != hipSuccess) return e;
   }
   // grad of the encoder output = dpre . Wp (token layout, pgp_dec.hip)
@@ -1326,6 +1349,7 @@ hipError_t tune_bwd_h(const TunePlan& p, const float* P, float* Gd, float* ws, c
   // the encoder layers, fused per unit (pgp_tunef.hip); their weight-gradient
   // slabs (one per workgroup) join the deferred reductions
   const int ng = p.tf_grid;
+  hipEvent_t tail_fork = nullptr;
   for (int l = 1; l >= 0; --l) {
     float* Lg = Gd + G::LAY0 + l * G::L_SIZE;
     TfArgs t{};
@@ -1361,13 +1385,17 @@ hipError_t tune_bwd_h(const TunePlan& p, const float* P, float* Gd, float* ws, c
     t.dqkv = ws + p.dq[l];
     t.part = ws + p.tfs[l][1];
     g_tft.mark(tk + 2, st);
-    if ((e = launch_tf(H, 3, t, st)) != hipSuccess) return e;
+    // its end forks the side work (layer 1: in_proj dW and the early flush;
+    // layer 0: the tail's side work)
+    hipEvent_t att_end = g_tft.on ? nullptr : fk.launch_event();
+    if ((e = launch_tf(H, 3, t, st, att_end)) != hipSuccess) return e;
     g_tft.mark(tk + 3, st);
     if (!rb.add(ng, tf_slab_floats(H, 3), ws + p.tfs[l][1], H, H, H, Lg + G::L_OUT, H, H, (long)H * H,
                 Lg + G::L_OUTB))
       return hipErrorInvalidValue;
+    if (l == 0) tail_fork = att_end;
     if (l == 1 && (early & 1)) {
-      if ((e = fk.fork()) != hipSuccess) return e;
+      if ((e = fk.fork_on(att_end)) != hipSuccess) return e;
       if ((e = in_proj_dw(1, sd)) != hipSuccess) return e;
       // layer 1's reductions (its fused slabs, in_proj) on the side stream
       // beside layer 0's backward, not in the final flush
@@ -1379,7 +1407,7 @@ hipError_t tune_bwd_h(const TunePlan& p, const float* P, float* Gd, float* ws, c
   // decoders' and layer 1's in_proj.  (While the fused launches spread over
   // every CU, side work beside them only slowed them: a long side workgroup on
   // a CU delays the next fused launch's workgroup there; profiles/r03/s3/.)
-  if ((e = fk.fork()) != hipSuccess) return e;
+  if ((e = fk.fork_on(tail_fork)) != hipSuccess) return e;
   if (!(early & 2) && (e = side_dec()) != hipSuccess) return e;
   if (!(early & 1) && (e = in_proj_dw(1, sd)) != hipSuccess) return e;
   // bits 4 / 8: layer 0's in_proj and the time encoder's weight gradients on
@@ -1477,11 +1505,11 @@ bool tune_plan_prefix(int H, int B_fwd, int B, TunePlan* p) {
 }
 
 hipError_t launch_tune_forward(const TunePlan& p, const float* windows, const float* P, float* ws, float* latent,
-                               float* logits, float* protos, hipStream_t st) {
+                               float* logits, float* protos, hipStream_t st, hipEvent_t pre) {
   switch (p.H) {
 #define CASE(h) \
   case h:       \
-    return tune_fwd_h<h>(p, windows, P, ws, latent, logits, protos, st);
+    return tune_fwd_h<h>(p, windows, P, ws, latent, logits, protos, st, pre);
     PGP_FOR_EACH_H(CASE)
 #undef CASE
   }
@@ -1490,11 +1518,11 @@ hipError_t launch_tune_forward(const TunePlan& p, const float* windows, const fl
 
 hipError_t launch_tune_backward(const TunePlan& p, const float* P, float* G, float* ws, const float* logits,
                                 const float* protos, const int* y, const float* mult, const float* tgt,
-                                hipStream_t st, bool dpre_ready) {
+                                hipStream_t st, bool dpre_ready, hipEvent_t pre) {
   switch (p.H) {
 #define CASE(h) \
   case h:       \
-    return tune_bwd_h<h>(p, P, G, ws, logits, protos, y, mult, tgt, st, dpre_ready);
+    return tune_bwd_h<h>(p, P, G, ws, logits, protos, y, mult, tgt, st, dpre_ready, pre);
     PGP_FOR_EACH_H(CASE)
 #undef CASE
   }

@@ -61,6 +61,9 @@ hipError_t tune_timing(bool on);
 // the tuning backward's side stream on the current device: `s`, or the
 // library's own low-priority stream when null (pgp_tune_set_side_stream)
 hipError_t tune_set_side_stream(hipStream_t s);
+// whether a step of that many tokens forks side work (a capture, or a side
+// stream override equal to the step's stream, can still keep it on one stream)
+bool tune_side_active(long tokens);
 hipError_t tune_fused_ms(float* out6);
 
 // decoder GEMMs (pgp_dec.hip): split-K forward into part[S][B][NOP] and the
@@ -69,13 +72,18 @@ int dec_fwd_splits(int H, int B);
 hipError_t launch_dec_fwd(int H, int B, int S, const float* X2, const float* Wp, float* part, hipStream_t st);
 hipError_t launch_dec_dx(int H, int B, const float* dpre, const float* WpT, float* dX, hipStream_t st);
 
+// pre: an event the caller's last launch on `st` signals at its end (the side
+// stream's decoder packing forks on it instead of an event recorded here)
 hipError_t launch_tune_forward(const TunePlan& p, const float* windows, const float* P, float* ws, float* latent,
-                               float* logits, float* protos, hipStream_t st);
+                               float* logits, float* protos, hipStream_t st, hipEvent_t pre = nullptr);
 // dpre_ready: the decoder pre-activation gradient [B][NOP] at ws + p.dpre was
-// already written (launch_tune_targets_dp with dpre), so the loss kernel is skipped
+// already written (launch_tune_targets_dp with dpre), so the loss kernel is
+// skipped; pre (with dpre_ready): an event the caller's last launch on `st`
+// signals at its end, which the first fork of the side work waits on instead
+// of an event recorded here
 hipError_t launch_tune_backward(const TunePlan& p, const float* P, float* G, float* ws, const float* logits,
                                 const float* protos, const int* y, const float* mult, const float* tgt,
-                                hipStream_t st, bool dpre_ready = false);
+                                hipStream_t st, bool dpre_ready = false, hipEvent_t pre = nullptr);
 hipError_t launch_tune_targets(int H, int K, const float* logits, const float* protos, const int* y, const int* cls,
                                double* state, double update_min, double decay, float* mult, float* tgt, double* loss,
                                hipStream_t st);

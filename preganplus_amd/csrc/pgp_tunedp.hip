@@ -31,6 +31,7 @@
 // All fp64 with FMA contraction off, in the numpy restatement's operation order
 // per value (labels and CE weights bit-identical to it; sums over the batch are
 // tree-ordered, equal to fp64 rounding).
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include "pgp_device.hpp"
@@ -341,10 +342,15 @@ __global__ void tune_state_apply_kernel(int K, double* __restrict__ state, const
 }  // namespace
 
 hipError_t launch_tune_dataset(int H, int E, int R, const double* series, const double* train_max, float* windows,
-                               int* y, int* cls, float* infer, hipStream_t st) {
+                               int* y, int* cls, float* infer, hipStream_t st, hipEvent_t stop) {
   const long n = (long)E * H;
-  tune_dataset_kernel<<<(int)((n + kDsP - 1) / kDsP), kDsThreads, 0, st>>>(H, E, R, series, train_max, windows, y,
-                                                                           cls, infer);
+  const int grid = (int)((n + kDsP - 1) / kDsP);
+  if (stop) {  // the launch signals `stop` at its end (a fork right after it)
+    void* args[] = {&H, &E, &R, &series, &train_max, &windows, &y, &cls, &infer};
+    return hipExtLaunchKernel(reinterpret_cast<const void*>(tune_dataset_kernel), dim3(grid), dim3(kDsThreads), args,
+                              0, st, nullptr, stop, 0);
+  }
+  tune_dataset_kernel<<<grid, kDsThreads, 0, st>>>(H, E, R, series, train_max, windows, y, cls, infer);
   return hipGetLastError();
 }
 
@@ -355,7 +361,7 @@ long tune_dp_workspace_doubles(int B) { return (long)((B + kWpb - 1) / kWpb) * k
 hipError_t launch_tune_targets_dp(int H, int K, int B, const float* logits, const float* protos, const int* y,
                                   const int* cls, double* state, double update_min, float* mult, float* tgt,
                                   double* loss, double* inc, double* ws, hipStream_t st, float* dpre, int nop,
-                                  const StateApplyArgs* apply) {
+                                  const StateApplyArgs* apply, hipEvent_t stop) {
   const int nblk = (B + kWpb - 1) / kWpb;
   unsigned* counter = reinterpret_cast<unsigned*>(ws);   // slot 0 (any batch), the partials after it
   StateApplyArgs sa{};
@@ -363,6 +369,13 @@ hipError_t launch_tune_targets_dp(int H, int K, int B, const float* logits, cons
     if (K < 0 || K > kMaxProtos || apply->cr.n < 0 || apply->cr.n > kMaxCond) return hipErrorInvalidValue;
     sa = *apply;
     sa.on = 1;
+  }
+  if (stop) {  // the launch signals `stop` at its end (a fork right after it)
+    double* part = ws + 1;
+    void* args[] = {&H, &B, &logits, &protos, &y, &cls, &state, &K, &update_min, &mult, &tgt, &loss, &part,
+                    &counter, &inc, &dpre, &nop, &sa};
+    return hipExtLaunchKernel(reinterpret_cast<const void*>(tune_targets_dp_kernel), dim3(nblk), dim3(kTB), args, 0,
+                              st, nullptr, stop, 0);
   }
   tune_targets_dp_kernel<<<nblk, kTB, 0, st>>>(H, B, logits, protos, y, cls, state, K, update_min, mult, tgt, loss,
                                                ws + 1, counter, inc, dpre, nop, sa);

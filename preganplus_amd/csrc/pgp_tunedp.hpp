@@ -33,7 +33,7 @@ __device__ __forceinline__ void dpre_host(float l0, float l1, int yy, float mu, 
 #endif
 
 hipError_t launch_tune_dataset(int H, int E, int R, const double* series, const double* train_max, float* windows,
-                               int* y, int* cls, float* infer, hipStream_t st);
+                               int* y, int* cls, float* infer, hipStream_t st, hipEvent_t stop = nullptr);
 long tune_dp_workspace_doubles(int B);
 // the state update (pgp_tune_state_apply) done by the targets kernel's last
 // workgroup, when the step has no exchange between the two (world size 1)
@@ -48,7 +48,7 @@ struct StateApplyArgs {
 hipError_t launch_tune_targets_dp(int H, int K, int B, const float* logits, const float* protos, const int* y,
                                   const int* cls, double* state, double update_min, float* mult, float* tgt,
                                   double* loss, double* inc, double* ws, hipStream_t st, float* dpre = nullptr,
-                                  int nop = 0, const StateApplyArgs* apply = nullptr);
+                                  int nop = 0, const StateApplyArgs* apply = nullptr, hipEvent_t stop = nullptr);
 hipError_t launch_tune_state_apply(int K, double* state, const double* inc, double decay, const CondRows& cr,
                                    double* dsteps, float* table, double lr, double b1, double b2, hipStream_t st);
 

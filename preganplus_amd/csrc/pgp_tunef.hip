@@ -25,6 +25,7 @@
 // one k-step per register).  The waves of a workgroup combine their registers
 // in a fixed order at the end, one partial slab per workgroup, reduced in a
 // fixed order by the tuning step's deferred reduction: deterministic.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
@@ -1126,8 +1127,17 @@ __global__ __launch_bounds__(kTfWaves * 64, 1) void tf_bwd_att_kernel(TfArgs a) 
 }
 
 template <int H>
-hipError_t tf_launch(int kind, const TfArgs& a, int grid, hipStream_t st) {
+hipError_t tf_launch(int kind, const TfArgs& a, int grid, hipStream_t st, hipEvent_t stop) {
   using F = TF<H>;
+  if (stop && kind != 0) {  // the fused launches with a stop event (a fork right after them)
+    void* args[] = {const_cast<TfArgs*>(&a)};
+    const void* fn = kind == 1 ? reinterpret_cast<const void*>(tf_fwd_kernel<H>)
+                     : kind == 2 ? reinterpret_cast<const void*>(tf_bwd_ffn_kernel<H>)
+                                 : reinterpret_cast<const void*>(tf_bwd_att_kernel<H>);
+    const size_t lds = (size_t)(kind == 1 ? FwdL<H>::TOTAL : kind == 2 ? BffL<H>::TOTAL : BatL<H>::TOTAL) * 4;
+    const int threads = (kind == 1 ? kTfFwdWaves : kTfWaves) * 64;
+    return hipExtLaunchKernel(fn, dim3(grid), dim3(threads), args, lds, st, nullptr, stop, 0);
+  }
   switch (kind) {
     case 0: {
       const long n = F::TOTAL_FLOATS;
@@ -1221,7 +1231,7 @@ extern "C" int pgp_debug_tf_stamps(unsigned long long* host) {
 }
 #endif
 
-hipError_t launch_tf(int H, int kind, const TfArgs& a, hipStream_t st) {
+hipError_t launch_tf(int H, int kind, const TfArgs& a, hipStream_t st, hipEvent_t stop) {
   const long nu = ((long)a.B * H + 15) / 16;
   const int grid = tf_grid_for(nu, kind == 1 ? kTfFwdWaves : kTfWaves);
   switch (H) {
@@ -1241,7 +1251,7 @@ hipError_t launch_tf(int H, int kind, const TfArgs& a, hipStream_t st) {
       return true;                                                                       \
     }();                                                                                 \
     (void)attr;                                                                          \
-    return tf_launch<h>(kind, a, grid, st);                                              \
+    return tf_launch<h>(kind, a, grid, st, stop);                                        \
   }
     PGP_FOR_EACH_H(CASE)
 #undef CASE

@@ -153,6 +153,7 @@ int tf_max_grid();                      // the most workgroups a fused launch us
 int tf_bwd_grid(int H, int B);          // workgroups (= weight-gradient slabs) of a backward launch
 void tf_reserve_cus(int n);             // CUs the fused launches leave to other streams
 // kind 0: pack fragments from P; 1: forward of a.layer; 2: ffn backward; 3: attention backward
-hipError_t launch_tf(int H, int kind, const TfArgs& a, hipStream_t st);
+// stop != nullptr: the launch signals that event at its end (hipExtLaunchKernel)
+hipError_t launch_tf(int H, int kind, const TfArgs& a, hipStream_t st, hipEvent_t stop = nullptr);
 
 }  // namespace pgp
