@@ -1127,6 +1127,8 @@ __global__ __launch_bounds__(kTfWaves * 64, 1) void tf_bwd_att_kernel(TfArgs a) 
 }
 
 template <int H>
+constexpr size_t bff_lds() { return (size_t)BffL<H>::TOTAL * 4; }  // the FFN backward's dynamic LDS
+template <int H>
 hipError_t tf_launch(int kind, const TfArgs& a, int grid, hipStream_t st, hipEvent_t stop) {
   using F = TF<H>;
   if (stop && kind != 0) {  // the fused launches with a stop event (a fork right after them)
@@ -1134,7 +1136,7 @@ hipError_t tf_launch(int kind, const TfArgs& a, int grid, hipStream_t st, hipEve
     const void* fn = kind == 1 ? reinterpret_cast<const void*>(tf_fwd_kernel<H>)
                      : kind == 2 ? reinterpret_cast<const void*>(tf_bwd_ffn_kernel<H>)
                                  : reinterpret_cast<const void*>(tf_bwd_att_kernel<H>);
-    const size_t lds = (size_t)(kind == 1 ? FwdL<H>::TOTAL : kind == 2 ? BffL<H>::TOTAL : BatL<H>::TOTAL) * 4;
+    const size_t lds = kind == 2 ? bff_lds<H>() : (size_t)(kind == 1 ? FwdL<H>::TOTAL : BatL<H>::TOTAL) * 4;
     const int threads = (kind == 1 ? kTfFwdWaves : kTfWaves) * 64;
     return hipExtLaunchKernel(fn, dim3(grid), dim3(threads), args, lds, st, nullptr, stop, 0);
   }
@@ -1150,7 +1152,7 @@ hipError_t tf_launch(int kind, const TfArgs& a, int grid, hipStream_t st, hipEve
       return hipGetLastError();
     }
     case 2: {
-      const size_t lds = (size_t)BffL<H>::TOTAL * 4;
+      const size_t lds = bff_lds<H>();
       tf_bwd_ffn_kernel<H><<<grid, kTfWaves * 64, lds, st>>>(a);
       return hipGetLastError();
     }
@@ -1245,7 +1247,7 @@ hipError_t launch_tf(int H, int kind, const TfArgs& a, hipStream_t st, hipEvent_
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(tf_fwd_kernel<h>),         \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, FwdL<h>::TOTAL * 4); \
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(tf_bwd_ffn_kernel<h>),     \
-                                hipFuncAttributeMaxDynamicSharedMemorySize, BffL<h>::TOTAL * 4); \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)bff_lds<h>()); \
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(tf_bwd_att_kernel<h>),     \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, BatL<h>::TOTAL * 4); \
       return true;                                                                       \

@@ -304,6 +304,12 @@ for step in "$@"; do
       run abearly 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" base= e5=PGP_LIB=$L/libpreganplus_e5.so e13=PGP_LIB=$L/libpreganplus_e13.so e15=PGP_LIB=$L/libpreganplus_e15.so
       tail -6 $OUT/abearly.out
       ;;
+    abffn)
+      L=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var
+      run abffn50 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" base= f124=PGP_LIB=$L/libpreganplus_ffn124.so f132=PGP_LIB=$L/libpreganplus_ffn132.so
+      run abffn16 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 16 --steps 100 --warmup 10 --no-cpu-baseline" base= f124=PGP_LIB=$L/libpreganplus_ffn124.so f132=PGP_LIB=$L/libpreganplus_ffn132.so
+      grep median $OUT/abffn50.out $OUT/abffn16.out
+      ;;
     fcal)  # FETCH_SIZE / WRITE_SIZE per access width (tools/micro/fetch_cal.hip)
       for c in FETCH_SIZE WRITE_SIZE; do
         echo "[fcal $c] $(date +%T)"
