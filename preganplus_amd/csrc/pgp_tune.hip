@@ -212,21 +212,8 @@ struct DwMulti {
   int n, nbx;
   int kind[kMaxDwSeg];
   DwArgs seg[kMaxDwSeg];
+  int gat_nb;  // leading blocks running the GAT backward (0: none)
 };
-template <int DP, int XBP>
-__global__ __launch_bounds__(256) void dw_multi_kernel(DwMulti m) {
-  constexpr int ROWS = dw_rows(0);
-  constexpr int SY = ROWS * lds_stride(3 * DP), SX = ROWS * lds_stride(DP > XBP ? DP : XBP);
-  __shared__ __attribute__((aligned(16))) float ys[SY];
-  __shared__ __attribute__((aligned(16))) float xs[SX];
-  const int s = blockIdx.x / m.nbx, bx = blockIdx.x - s * m.nbx;
-  if (s >= m.n) return;
-  switch (m.kind[s]) {
-    case 0: dw_block<3 * DP, DP>(m.seg[s], bx, m.nbx, ys, xs); break;
-    case 1: dw_block<DP, DP>(m.seg[s], bx, m.nbx, ys, xs); break;
-    default: dw_block<DP, XBP>(m.seg[s], bx, m.nbx, ys, xs); break;
-  }
-}
 
 // Deterministic reduction of partial slabs.  Outputs: segment A, rows x cols
 // (source i*ldp + j, destination outA[i*ldo + j]) then segment B, nb values
@@ -380,16 +367,20 @@ PGP_DEV GatEdge gat_edge(float s, float t, float smax, float mx) {
   return e;
 }
 
+struct GatFwdIn {
+  int B;
+  const float* win;
+  float *wcopy, *Gout, *XB, *GS;
+};
 template <int H>
-__global__ __launch_bounds__(256) void gat_fwd_kernel(int B, const float* __restrict__ win,
-                                                      const float* __restrict__ P, float* __restrict__ wcopy,
-                                                      float* __restrict__ Gout, float* __restrict__ XB,
-                                                      float* __restrict__ GS) {
+PGP_DEV void gat_fwd_block(int bx, int B, const float* __restrict__ win, const float* __restrict__ P,
+                           float* __restrict__ wcopy, float* __restrict__ Gout, float* __restrict__ XB,
+                           float* __restrict__ GS) {
   using Q = TuneGeo<H>;
   using G = TGeo<H>;
   __shared__ float sa[4][64][2], sx[4][64][3], sxb[4][64][4];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const long pw = (long)blockIdx.x * 4 + wv;  // (window, step)
+  const long pw = (long)bx * 4 + wv;  // (window, step)
   const bool okw = pw < 3L * B;
   const long b = okw ? pw / 3 : 0;
   const int w = okw ? (int)(pw - b * 3) : 0;
@@ -470,23 +461,44 @@ __global__ __launch_bounds__(256) void gat_fwd_kernel(int B, const float* __rest
 // 4 (window, step) graphs summed in wave order), Xs = sum_i ds_i x_i and
 // Xt = sum_j dt_j x_j (ds, dt: grads of the per-node source / destination
 // scores), from which gat_param_body forms the attn_fc and fc grads.
-// Workgroup 0 also clears `fcd` (the tokens' dX0 (x) x-bar sum, reduced after
-// this kernel; gat_param_body maps it through W_TE into the fc gradient).
+// (fcd, the tokens' dX0 (x) x-bar sum that gat_param_body maps through W_TE
+// into the fc gradient, is a weight-gradient reduction of its own.)  Runs as
+// the first segment of the backward's multi-segment tail launch.
+struct GatBwdArgs {
+  int B;
+  const float* wcopy;
+  const float* P;
+  const float* dX0;
+  const float* GS;
+  const float* Mt;
+  float* GSX;
+};
+// workgroup bx (4 (window, step) graphs) of the GAT backward
 template <int H>
-__global__ __launch_bounds__(256) void gat_bwd_kernel(int B, const float* __restrict__ wcopy,
-                                                      const float* __restrict__ P, const float* __restrict__ dX0,
-                                                      const float* __restrict__ GS, const float* __restrict__ Mt,
-                                                      float* __restrict__ GSX, float* __restrict__ fcd) {
+__global__ __launch_bounds__(256) void gat_fwd_kernel(int B, const float* __restrict__ win,
+                                                      const float* __restrict__ P, float* __restrict__ wcopy,
+                                                      float* __restrict__ Gout, float* __restrict__ XB,
+                                                      float* __restrict__ GS) {
+  gat_fwd_block<H>(blockIdx.x, B, win, P, wcopy, Gout, XB, GS);
+}
+template <int H>
+PGP_DEV void gat_bwd_block(const GatBwdArgs& ga, int bx) {
   using Q = TuneGeo<H>;
+  const int B = ga.B;
+  const float* __restrict__ wcopy = ga.wcopy;
+  const float* __restrict__ P = ga.P;
+  const float* __restrict__ dX0 = ga.dX0;
+  const float* __restrict__ GS = ga.GS;
+  const float* __restrict__ Mt = ga.Mt;
+  float* __restrict__ GSX = ga.GSX;
   __shared__ float ss[4][64], st[4][64], sx[4][64][3], sdx[4][64][3], smt[64][3], sred[4][6], sab[4][64][4];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const long pw = (long)blockIdx.x * 4 + wv;
+  const long pw = (long)bx * 4 + wv;
   const bool okw = pw < 3L * B;
   const long b = okw ? pw / 3 : 0;
   const int w = okw ? (int)(pw - b * 3) : 0;
   const int j = lane;
   const bool okj = okw && j < H;
-  if (blockIdx.x == 0 && threadIdx.x < 64 * 3) fcd[threadIdx.x] = 0.f;
   if (threadIdx.x < 64 * 3) smt[threadIdx.x / 3][threadIdx.x % 3] = Mt[threadIdx.x];
   const GatFold<H> fo = gat_fold<H>(P);
   float x[3];
@@ -580,7 +592,38 @@ __global__ __launch_bounds__(256) void gat_bwd_kernel(int B, const float* __rest
   __syncthreads();
   if (threadIdx.x < 6) {
     const int k = threadIdx.x;
-    GSX[(long)blockIdx.x * 8 + k] = (sred[0][k] + sred[1][k]) + (sred[2][k] + sred[3][k]);
+    GSX[(long)bx * 8 + k] = (sred[0][k] + sred[1][k]) + (sred[2][k] + sred[3][k]);
+  }
+}
+
+template <int H>
+__global__ __launch_bounds__(256) void gat_bwd_kernel(GatBwdArgs ga) {
+  gat_bwd_block<H>(ga, blockIdx.x);
+}
+// The backward's tail in ONE launch: the GAT backward (leading gat_nb
+// blocks, gat_bwd_block) and the weight gradients that do not wait for it
+// (segments: each block exactly as its own dw_kernel launch would run it, so
+// the partials are bit-identical).  Shapes: kind 0 = <3 DP, DP> (in_proj),
+// 1 = <DP, DP> (time encoder), 2 = <DP, XBP> (GAT fc aggregation).
+template <int H>
+__global__ __launch_bounds__(256) void dw_multi_kernel(DwMulti m, GatBwdArgs ga) {
+  using Q = TuneGeo<H>;
+  constexpr int DP = Q::DP, XBP = Q::XBP;
+  constexpr int ROWS = dw_rows(0);
+  constexpr int SY = ROWS * lds_stride(3 * DP), SX = ROWS * lds_stride(DP > XBP ? DP : XBP);
+  if ((int)blockIdx.x < m.gat_nb) {
+    gat_bwd_block<H>(ga, blockIdx.x);
+    return;
+  }
+  __shared__ __attribute__((aligned(16))) float ys[SY];
+  __shared__ __attribute__((aligned(16))) float xs[SX];
+  const int b = blockIdx.x - m.gat_nb;
+  const int s = b / m.nbx, bx = b - s * m.nbx;
+  if (s >= m.n) return;
+  switch (m.kind[s]) {
+    case 0: dw_block<3 * DP, DP>(m.seg[s], bx, m.nbx, ys, xs); break;
+    case 1: dw_block<DP, DP>(m.seg[s], bx, m.nbx, ys, xs); break;
+    default: dw_block<DP, XBP>(m.seg[s], bx, m.nbx, ys, xs); break;
   }
 }
 
@@ -701,10 +744,17 @@ __global__ __launch_bounds__(256) void dec_pack_kernel(const float* __restrict__
 template <int H>
 __global__ __launch_bounds__(256) void tune_pack_kernel(const float* __restrict__ P, float* __restrict__ Wp,
                                                         float* __restrict__ WpT, float* __restrict__ Mt,
-                                                        float* __restrict__ frags, int nb_dec, int nb_tf) {
+                                                        float* __restrict__ frags, int nb_dec, int nb_tf,
+                                                        GatFwdIn g) {
   using Q = TuneGeo<H>;
   using G = TGeo<H>;
   int bx = blockIdx.x;
+  // the blocks after the packings: the GAT forward (it reads P and the
+  // windows only), one launch fewer on the step's chain
+  if (bx >= nb_dec + 1 + nb_tf) {
+    gat_fwd_block<H>(bx - (nb_dec + 1 + nb_tf), g.B, g.win, P, g.wcopy, g.Gout, g.XB, g.GS);
+    return;
+  }
   const int t = threadIdx.x;
   if (bx < nb_dec) {
     const long idx = (long)bx * 256 + t;
@@ -1246,9 +1296,10 @@ hipError_t tune_fwd_h(const TunePlan& p, const float* win, const float* P, float
   t.frags = ws + p.tff;
   if (fk.side == st) {  // all on the caller's stream: every packing in ONE launch
     const int nb_dec = (int)((Q::NOP * Q::KD + 255) / 256), nb_tf = (int)((tf_frag_floats(H) + 255) / 256);
-    TCK((tune_pack_kernel<H><<<nb_dec + 1 + nb_tf, 256, 0, st>>>(P, ws + p.wp, ws + p.wpt, ws + p.mt, ws + p.tff,
-                                                                  nb_dec, nb_tf)));
-    TCK((gat_fwd_kernel<H><<<(3 * B + 3) / 4, 256, 0, st>>>(B, win, P, ws + p.win, ws + p.g, ws + p.xb, ws + p.gs)));
+    // ... and the GAT forward in the same launch
+    const GatFwdIn g{B, win, ws + p.win, ws + p.g, ws + p.xb, ws + p.gs};
+    TCK((tune_pack_kernel<H><<<nb_dec + 1 + nb_tf + (3 * B + 3) / 4, 256, 0, st>>>(
+        P, ws + p.wp, ws + p.wpt, ws + p.mt, ws + p.tff, nb_dec, nb_tf, g)));
   } else {
     if ((e = fk.fork_on(pre)) != hipSuccess) return e;
     TCK((dec_pack_kernel<H><<<(int)((Q::NOP * Q::KD + 255) / 256), 256, 0, fk.side>>>(P, ws + p.wp, ws + p.wpt)));
@@ -1302,11 +1353,16 @@ hipError_t tune_bwd_h(const TunePlan& p, const float* P, float* Gd, float* ws, c
   // the side stream beside the time encoder / GAT tail, 1.137 -> 1.126 ms;
   // bit 8 (the time encoder's too) measured neutral.
   constexpr int early = 7;  // round 5 A/B (H = 50): 5 1.102, 13 1.118, 15 1.090, 7 1.092 ms (profiles/r05/side_early_ab.txt)
-  // without a side stream every weight-gradient launch that nothing on the
-  // chain reads (in_proj of both layers, the time encoder, the GAT fc
-  // aggregation) waits for ONE multi-segment launch before the reductions:
-  // their inputs stay untouched until then (per-layer dQKV / X regions, dX0
-  // is read-only after the time encoder)
+  // Without a side stream the tail's weight gradients that nothing on the
+  // chain reads (in_proj of both layers, the time encoder's, the GAT fc
+  // aggregation's) join the GAT backward in ONE multi-segment launch before
+  // the reductions: their inputs stay untouched until then (per-layer dQKV /
+  // X regions; dX0 is read-only after the attention backward).  H = 16:
+  // 0.207 -> 0.202 ms.  With a side stream (H = 50) the same merge of the GAT
+  // backward and the two main-stream weight gradients ran as long as the
+  // three launches in turn (82 vs 85 us: their blocks are throughput-bound)
+  // and slowed the side stream's in_proj weight gradient beside it (50 -> 93
+  // us): C3 1.080 -> 1.100 ms, so there they stay separate launches.
   const bool defer = sd == st;
   DwMulti dm{};
   dm.nbx = p.dw_grid;
@@ -1420,15 +1476,18 @@ hipError_t tune_bwd_h(const TunePlan& p, const float* P, float* Gd, float* ws, c
   // GAT, straight from dX0 (the time encoder's input gradient folded in,
   // gat_bwd_kernel); the fc gradient's aggregation part: fcd = dX0 (x) x-bar
   const int gat_wg = (3 * B + 3) / 4;
-  TCK((gat_bwd_kernel<H><<<gat_wg, 256, 0, st>>>(B, ws + p.win, P, ws + p.da, ws + p.gs, ws + p.mt, ws + p.gsx,
-                                                  ws + p.fcd)));
+  const GatBwdArgs gba{B, ws + p.win, P, ws + p.da, ws + p.gs, ws + p.mt, ws + p.gsx};
+  if (defer)
+    dm.gat_nb = gat_wg;
+  else
+    TCK((gat_bwd_kernel<H><<<gat_wg, 256, 0, st>>>(gba)));
   if ((e = dw<DP, Q::XBP>(p, rb, ws + p.da, DP, ws + p.xb, Q::XBP, 0, H, 3, ws + p.fcd, nullptr, st,
                           defer ? &dm : nullptr, 2)) != hipSuccess)
     return e;
   rb.mark_last_wt();  // fcd: read by the final reduction launch's last workgroup (gat_param_body)
   // without bit 4, layer 0's in_proj weight gradient closes the main stream's share
   if (!(early & 4) && (e = in_proj_dw(0, st)) != hipSuccess) return e;
-  if (dm.n) TCK((dw_multi_kernel<DP, Q::XBP><<<dm.n * dm.nbx, 256, 0, st>>>(dm)));
+  if (defer) TCK((dw_multi_kernel<H><<<dm.gat_nb + dm.n * dm.nbx, 256, 0, st>>>(dm, gba)));
   if ((e = fk.join()) != hipSuccess) return e;  // the side stream's partials and G writes
   // every deferred weight-gradient reduction, then (the same launch's last
   // workgroup) the GAT parameter gradient, which needs fcd's reduction
