@@ -57,7 +57,7 @@ struct pgp_online {
   int cond_local[kMaxTensors] = {};  // transformer selection index -> cond flag
   CondRows cr{};
   long sec_lo[3] = {0, 0, 0};
-  hipEvent_t gate = nullptr, gan_done = nullptr, fwd_fork = nullptr;
+  hipEvent_t gate = nullptr, gan_done = nullptr, fwd_fork = nullptr, tgt_end = nullptr;
   bool timing = false, timed = false;
   hipEvent_t tev[kNumEv] = {};
 };
@@ -251,7 +251,8 @@ int pgp_online_create(const pgp_online_desc* desc, pgp_online** out) {
   o->cr.n = ncond;
   if (hipEventCreateWithFlags(&o->gate, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&o->gan_done, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&o->fwd_fork, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&o->fwd_fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&o->tgt_end, hipEventDisableTiming) != hipSuccess) {
     delete o;
     return ofail(PGP_ERR_HIP, "pgp_online_create: events");
   }
@@ -264,6 +265,7 @@ int pgp_online_destroy(pgp_online* o) {
   if (o->gate) (void)hipEventDestroy(o->gate);
   if (o->gan_done) (void)hipEventDestroy(o->gan_done);
   if (o->fwd_fork) (void)hipEventDestroy(o->fwd_fork);
+  if (o->tgt_end) (void)hipEventDestroy(o->tgt_end);
   for (auto& e : o->tev)
     if (e) (void)hipEventDestroy(e);
   delete o;
@@ -285,7 +287,10 @@ int pgp_online_step(pgp_online* o, void* main_stream, void* gan_stream, pgp_coll
   OCHK(launch_tune_dataset(H, E, R, d.series, d.train_max, d.windows, d.y, d.cls, detect_win, sm, ff));
   mark(o, kE1, sm);
   // 2. ONE forward over the B + E windows (step-start weights)
-  OCHK(launch_tune_forward(o->fwd, d.windows, d.P, d.tune_ws, nullptr, d.logits, d.protos, sm, ff));
+  // its end (the stop event of its last launch) starts the GAN stream: the
+  // GAN forward runs beside the targets
+  hipEvent_t gate = (sg != sm && !o->timed) ? o->gate : nullptr;
+  OCHK(launch_tune_forward(o->fwd, d.windows, d.P, d.tune_ws, nullptr, d.logits, d.protos, sm, ff, gate));
   mark(o, kE2, sm);
   // 3. main: bookkeeping against the step-start state (the decoders' input
   //    gradient dpre written by the same launch), issued before the GAN part so
@@ -293,14 +298,15 @@ int pgp_online_step(pgp_online* o, void* main_stream, void* gan_stream, pgp_coll
   //    (H = 16: the main stream sat idle ≈30 µs here); at world size 1 (no
   //    exchange of the increments) the state update by the same launch's last
   //    workgroup.  Its end (the launch's stop event, no marker packet on the
-  //    main stream) starts the GAN stream and the backward's side work.
+  //    main stream) starts the backward's side work.
   const StateApplyArgs sa{1, d.decay, o->cr, d.cond_steps, d.adam_rows, d.lr[kTr], d.beta1, d.beta2};
-  hipEvent_t gate = (sg != sm && !o->timed) ? o->gate : nullptr;
+  hipEvent_t tgt_end = (!o->timed && tune_side_active(o->bwd.M)) ? o->tgt_end : nullptr;
   OCHK(launch_tune_targets_dp(H, K, B, d.logits, d.protos, d.y, d.cls, d.state, d.update_min, d.mult, d.tgt, d.loss,
-                              d.inc, d.dp_ws, sm, d.tune_ws + o->bwd.dpre, o->bwd.NOP, cb ? nullptr : &sa, gate));
+                              d.inc, d.dp_ws, sm, d.tune_ws + o->bwd.dpre, o->bwd.NOP, cb ? nullptr : &sa,
+                              tgt_end));
   mark(o, kE3, sm);
-  // 4. the GAN stream: Gen + Disc forward (the embedding formed inside), the
-  //    simulated label, the Disc gradient
+  // 4. the GAN stream, from the forward's end: Gen + Disc forward (the
+  //    embedding formed inside), the simulated label, the Disc gradient
   if (sg != sm) {
     if (!gate) OCHK(hipEventRecord(o->gate, sm));
     OCHK(hipStreamWaitEvent(sg, o->gate, 0));
@@ -311,7 +317,7 @@ int pgp_online_step(pgp_online* o, void* main_stream, void* gan_stream, pgp_coll
   OCALL(gan_part_a(o, sg, fused));
   // then the backward
   OCHK(launch_tune_backward(o->bwd, d.P, d.G, d.tune_ws, d.logits, d.protos, d.y, d.mult, d.tgt, sm, true,
-                            gate));
+                            tgt_end));
   mark(o, kE4, sm);
   // 5. the GAN's updates (its collectives on the GAN stream)
   OCALL(gan_part_b(o, sg, fused, cb, user));

@@ -475,13 +475,6 @@ struct GatBwdArgs {
 };
 // workgroup bx (4 (window, step) graphs) of the GAT backward
 template <int H>
-__global__ __launch_bounds__(256) void gat_fwd_kernel(int B, const float* __restrict__ win,
-                                                      const float* __restrict__ P, float* __restrict__ wcopy,
-                                                      float* __restrict__ Gout, float* __restrict__ XB,
-                                                      float* __restrict__ GS) {
-  gat_fwd_block<H>(blockIdx.x, B, win, P, wcopy, Gout, XB, GS);
-}
-template <int H>
 PGP_DEV void gat_bwd_block(const GatBwdArgs& ga, int bx) {
   using Q = TuneGeo<H>;
   const int B = ga.B;
@@ -508,7 +501,7 @@ PGP_DEV void gat_bwd_block(const GatBwdArgs& ga, int bx) {
   const float t = fo.v[0] * x[0] + fo.v[1] * x[1] + fo.v[2] * x[2];
   const float mx = okw ? GS[pw * 4] : 0.f, iz = okw ? 1.0f / GS[pw * 4 + 1] : 0.f;
   const float smax = wave_max(okj ? s : -INFINITY);
-  const GatEdge ge = gat_edge(s, t, smax, mx);  // the forward's factorised edge weights (gat_fwd_kernel)
+  const GatEdge ge = gat_edge(s, t, smax, mx);  // the forward's factorised edge weights (gat_fwd_block)
   ss[wv][j] = s;
   st[wv][j] = t;
   sab[wv][j][0] = ge.a;
@@ -773,9 +766,9 @@ __global__ __launch_bounds__(256) void tune_pack_kernel(const float* __restrict_
     return;
   }
   bx -= nb_dec;
-  if (bx == 0) {
+  if (bx == 0) {  // (Mt == nullptr: formed elsewhere, gat_mt_kernel on the side stream)
     const int c = t / 3, k = t - 3 * c;
-    if (c >= 64) return;
+    if (c >= 64 || !Mt) return;
     float m = 0.f;
     if (c < H)
       for (int f = 0; f < H; ++f) m = fmaf(P[G::W_TE + c * H + f], P[G::W_FC + f * 3 + k], m);
@@ -1284,7 +1277,7 @@ struct Fork {
 
 template <int H>
 hipError_t tune_fwd_h(const TunePlan& p, const float* win, const float* P, float* ws, float* latent, float* logits,
-                      float* protos, hipStream_t st, hipEvent_t pre) {
+                      float* protos, hipStream_t st, hipEvent_t pre, hipEvent_t post) {
   using Q = TuneGeo<H>;
   const int B = p.B;
   hipError_t e;
@@ -1304,9 +1297,12 @@ hipError_t tune_fwd_h(const TunePlan& p, const float* win, const float* P, float
     if ((e = fk.fork_on(pre)) != hipSuccess) return e;
     TCK((dec_pack_kernel<H><<<(int)((Q::NOP * Q::KD + 255) / 256), 256, 0, fk.side>>>(P, ws + p.wp, ws + p.wpt)));
     TCK((gat_mt_kernel<H><<<1, 192, 0, fk.side>>>(P, ws + p.mt)));  // for the backward's GAT (gat_bwd_kernel)
-    TCK((gat_fwd_kernel<H><<<(3 * B + 3) / 4, 256, 0, st>>>(B, win, P, ws + p.win, ws + p.g, ws + p.xb, ws + p.gs)));
-    // the encoder: fragments packed from P, then one fused launch per layer
-    if ((e = launch_tf(H, 0, t, st)) != hipSuccess) return e;
+    // main: the encoder's fragments packed from P and the GAT forward in ONE
+    // launch (the packing kernel's tf blocks, then the GAT blocks)
+    const int nb_tf = (int)((tf_frag_floats(H) + 255) / 256);
+    const GatFwdIn g{B, win, ws + p.win, ws + p.g, ws + p.xb, ws + p.gs};
+    TCK((tune_pack_kernel<H><<<1 + nb_tf + (3 * B + 3) / 4, 256, 0, st>>>(P, nullptr, nullptr, nullptr, ws + p.tff, 0,
+                                                                           nb_tf, g)));
   }
   for (int l = 0; l < 2; ++l) {
     t.layer = l;
@@ -1321,8 +1317,17 @@ hipError_t tune_fwd_h(const TunePlan& p, const float* win, const float* P, float
   }
   if ((e = fk.join()) != hipSuccess) return e;
   if ((e = launch_dec_fwd(H, B, p.dec_s, ws + p.x[2], ws + p.wp, ws + p.part, st)) != hipSuccess) return e;
-  TCK((dec_fin_kernel<H><<<(int)(((long)B * 4 * H + 255) / 256), 256, 0, st>>>(B, p.dec_s, ws + p.part, P, logits,
-                                                                                protos)));
+  const int nfin = (int)(((long)B * 4 * H + 255) / 256);
+  if (post && !latent) {  // the forward's last launch signals `post` at its end
+    int Bv = B, S = p.dec_s;
+    const float* partc = ws + p.part;
+    void* args[] = {&Bv, &S, &partc, &P, &logits, &protos};
+    TCK((void)hipExtLaunchKernel(reinterpret_cast<const void*>(dec_fin_kernel<H>), dim3(nfin), dim3(256), args, 0, st,
+                                 nullptr, post, 0));
+  } else {
+    TCK((dec_fin_kernel<H><<<nfin, 256, 0, st>>>(B, p.dec_s, ws + p.part, P, logits, protos)));
+    if (post) TCK((void)hipEventRecord(post, st));
+  }
   if (latent)
     TCK((latent_kernel<H><<<(int)(((long)B * 3 * H * H + 255) / 256), 256, 0, st>>>(B, ws + p.x[2], latent)));
   return hipSuccess;
@@ -1564,11 +1569,11 @@ bool tune_plan_prefix(int H, int B_fwd, int B, TunePlan* p) {
 }
 
 hipError_t launch_tune_forward(const TunePlan& p, const float* windows, const float* P, float* ws, float* latent,
-                               float* logits, float* protos, hipStream_t st, hipEvent_t pre) {
+                               float* logits, float* protos, hipStream_t st, hipEvent_t pre, hipEvent_t post) {
   switch (p.H) {
 #define CASE(h) \
   case h:       \
-    return tune_fwd_h<h>(p, windows, P, ws, latent, logits, protos, st, pre);
+    return tune_fwd_h<h>(p, windows, P, ws, latent, logits, protos, st, pre, post);
     PGP_FOR_EACH_H(CASE)
 #undef CASE
   }
