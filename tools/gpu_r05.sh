@@ -304,6 +304,13 @@ for step in "$@"; do
       run abearly 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" base= e5=PGP_LIB=$L/libpreganplus_e5.so e13=PGP_LIB=$L/libpreganplus_e13.so e15=PGP_LIB=$L/libpreganplus_e15.so
       tail -6 $OUT/abearly.out
       ;;
+    gobidx)
+      L=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var
+      run gdx1 300 python3 -u tools/dbg/gobi_ab.py $L/libpreganplus_dxbase.so
+      run gdx2 300 python3 -u tools/dbg/gobi_ab.py $L/libpreganplus_dxpref.so
+      run gdx3 300 python3 -u tools/dbg/gobi_ab.py $L/libpreganplus_gobi7.so
+      cat $OUT/gdx1.out $OUT/gdx2.out $OUT/gdx3.out
+      ;;
     abffn)
       L=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var
       run abffn50 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" base= f124=PGP_LIB=$L/libpreganplus_ffn124.so f132=PGP_LIB=$L/libpreganplus_ffn132.so
