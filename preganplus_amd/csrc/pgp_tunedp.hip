@@ -289,18 +289,44 @@ __global__ __launch_bounds__(kTB) void tune_targets_dp_kernel(int H, int B, cons
     }
     __syncthreads();
     if (live && lane == 0) {  // host order, as the per-window loop
+      // 8 hosts' LDS values read together (clamped index: no branch around a
+      // read), then their adds in host order: one LDS round trip per 8 hosts
+      // instead of two dependent ones per host (the loop was LDS-latency-bound:
+      // the kernel 22.6 us at H = 50)
       const int n = H - i0 < 64 ? H - i0 : 64;
-      for (int j = 0; j < n; ++j) {
-        const int code = s_code[wv][j];
-        aloss += s_ce[wv][j];
-        acc[9] += code >= 0 ? 1.0 : 0.0;
-        if (code >= 0) {
-          tloss += s_tl[wv][j];
-          if (code >= 4) {
-            const int cc = code - 4;
-            acc[2 * cc] += s_d0[wv][j];
-            acc[2 * cc + 1] += s_d1[wv][j];
-            acc[6 + cc] += 1.0;
+      for (int j0 = 0; j0 < n; j0 += 8) {
+        int cd[8];
+        double ce[8], tl[8], e0[8], e1[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int jj = j0 + q < n ? j0 + q : n - 1;
+          cd[q] = s_code[wv][jj];
+          ce[q] = s_ce[wv][jj];
+          tl[q] = s_tl[wv][jj];
+          e0[q] = s_d0[wv][jj];
+          e1[q] = s_d1[wv][jj];
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          if (j0 + q >= n) break;
+          const int code = cd[q];
+          aloss += ce[q];
+          acc[9] += code >= 0 ? 1.0 : 0.0;
+          if (code >= 0) {
+            tloss += tl[q];
+            if (code == 4) {
+              acc[0] += e0[q];
+              acc[1] += e1[q];
+              acc[6] += 1.0;
+            } else if (code == 5) {
+              acc[2] += e0[q];
+              acc[3] += e1[q];
+              acc[7] += 1.0;
+            } else if (code == 6) {
+              acc[4] += e0[q];
+              acc[5] += e1[q];
+              acc[8] += 1.0;
+            }
           }
         }
       }
