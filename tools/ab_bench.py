@@ -42,7 +42,7 @@ def main():
             line = [ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1]
             d = json.loads(line)
             res[name].append(d["ms_per_step"])
-            extra[name].append({k: d[k] for k in ("eager_ms_per_step", "stage_ms", "kernel_ms") if k in d})
+            extra[name].append({k: d[k] for k in ("eager_ms_per_step", "stage_ms", "kernel_ms", "train_gan_alone") if k in d})
             print(f"round {r} {name:10s} {d['ms_per_step']:.4f} ms", flush=True)
     for name, _ in variants:
         print(f"{name:10s} median {statistics.median(res[name]):.4f} ms  rounds {[round(x, 4) for x in res[name]]}")

@@ -311,6 +311,12 @@ for step in "$@"; do
       run gdx3 300 python3 -u tools/dbg/gobi_ab.py $L/libpreganplus_gobi7.so
       cat $OUT/gdx1.out $OUT/gdx2.out $OUT/gdx3.out
       ;;
+    abgs2)
+      L=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var
+      run abgs16 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 16 --steps 100 --warmup 10 --no-cpu-baseline" base= gs2=PGP_LIB=$L/libpreganplus_gs2.so
+      grep median $OUT/abgs16.out
+      python3 -c "import json; d=json.loads(open('$OUT/abgs16.out').read().strip().splitlines()[-1]); print({k: [x.get('train_gan_alone') for x in v] for k, v in d.get('extra', {}).items()})"
+      ;;
     abffn)
       L=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var
       run abffn50 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" base= f124=PGP_LIB=$L/libpreganplus_ffn124.so f132=PGP_LIB=$L/libpreganplus_ffn132.so
