@@ -317,6 +317,12 @@ for step in "$@"; do
       grep median $OUT/abgs16.out
       python3 -c "import json; d=json.loads(open('$OUT/abgs16.out').read().strip().splitlines()[-1]); print({k: [x.get('train_gan_alone') for x in v] for k, v in d.get('extra', {}).items()})"
       ;;
+    abdx)
+      L=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var
+      run abdec50 600 python3 -u tools/ab_bench.py --rounds 4 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" new= old=PGP_LIB=$L/libpreganplus_decold.so
+      run abdec16 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 16 --steps 100 --warmup 10 --no-cpu-baseline" new= old=PGP_LIB=$L/libpreganplus_decold.so
+      grep median $OUT/abdec50.out $OUT/abdec16.out
+      ;;
     abffn)
       L=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var
       run abffn50 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" base= f124=PGP_LIB=$L/libpreganplus_ffn124.so f132=PGP_LIB=$L/libpreganplus_ffn132.so
