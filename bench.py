@@ -1097,21 +1097,40 @@ def bench_loop(args):
     shared_side = _share_side_stream(world, main, side)   # see bench_tune
     _reserve_cus(main, side, LOOP_RESERVED_CUS)
 
+    emb_ready = torch.cuda.Event()
+
     def interval(timed=False):
         if timed:
             ev[0].record()
-        res, _, _ = gobi.optimize(inits, out=gout)
-        sched.copy_(res[:, :, 2:])
-        if timed:
-            ev[1].record()
+        if shared_side:
+            # world > 1 sharing the second stream with the tuning backward's
+            # side work: GOBI first on the main stream (its 0.8 ms would hold
+            # that side work back)
+            res, _, _ = gobi.optimize(inits, out=gout)
+            sched.copy_(res[:, :, 2:])
+            if timed:
+                ev[1].record()
+        else:
+            # GOBI on the second stream: only the GAN step and K3 read its
+            # schedule, so the encoder stages and the tuning step run beside it
+            # on the main stream, on the CUs its finished workgroups leave
+            # (its time is its slowest workgroup's iteration chain)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                res, _, _ = gobi.optimize(inits, out=gout)
+                sched.copy_(res[:, :, 2:])
+                if timed:
+                    ev[1].record(side)
         for st in (0, 1, 2):
             model.forward(x, sched, out=out, stage=st)
         emb = embedding(out["logits"], out["protos"], out=emb_buf)   # PreGANPlus.py:129
         if timed:
             ev[2].record()
-        # the GAN step on a second stream beside the tuning step (no shared
-        # data, see bench_tune); the repack reads both sections of the master
-        side.wait_stream(main)
+        # the GAN step on the second stream beside the tuning step (no shared
+        # data, see bench_tune), after GOBI and the embedding; the repack
+        # reads both sections of the master
+        emb_ready.record(main)
+        side.wait_event(emb_ready)
 
         def gan_step():
             with torch.cuda.stream(side):
@@ -1139,12 +1158,17 @@ def bench_loop(args):
         interval()
     steps = args.steps
 
+    # stage spans: gobi ev0 -> ev1 (second stream at N = 1), encode_classify
+    # ev0 -> ev2 (beside GOBI), gan_step from the later of GOBI's end and the
+    # embedding to ev3, tune_step ev2 -> ev4, weight_sync ev4 -> ev5 (with the
+    # wait for the GAN step), gan_decide_moves ev5 -> ev6
     def timed_interval():
         interval(True)
         torch.cuda.synchronize()
+        t = [ev[0].elapsed_time(e) for e in ev]   # ms from the interval's start
+        spans = (t[1], t[2], t[3] - max(t[1], t[2]), t[4] - t[2], t[5] - t[4], t[6] - t[5])
         for k in range(len(names)):
-            # gan_step (side stream) and tune_step both start at ev[2]
-            acc[k] += ev[2 if k == 3 else k].elapsed_time(ev[k + 1])
+            acc[k] += spans[k]
 
     el = _timed(world, device, timed_interval, steps)
     if rank == 0:
@@ -1158,7 +1182,9 @@ def bench_loop(args):
             "config": {"workload": f"online interval, {E} independent 16-host cells per GPU", "hosts": H,
                        "cells_per_gpu": E, "parallelism": f"dp{world}"},
             "stage_ms": {n: float(acc[k] / steps) for k, n in enumerate(names)},
-            "streams": "gan_step on a second stream, concurrent with tune_step (no shared data)"}
+            "streams": "GOBI on a second stream beside the encoder stages and the tuning step (only the GAN "
+                       "step and K3 read its schedule); the GAN step on that stream after GOBI and the "
+                       "embedding, concurrent with the tuning step (no shared data)"}
         # the longest stage is GOBI (a latency-bound iteration chain): its roofline
         res["roofline"] = gobi_roofline(float(gout[1].float().mean().item()), E, float(acc[0] / steps))
         res["roofline"]["basis"] += "; the loop's gobi stage time (events around the launch and the schedule copy)"
