@@ -323,6 +323,10 @@ for step in "$@"; do
       run abdec16 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 16 --steps 100 --warmup 10 --no-cpu-baseline" new= old=PGP_LIB=$L/libpreganplus_decold.so
       grep median $OUT/abdec50.out $OUT/abdec16.out
       ;;
+    dist2)  # the driver's N > 1 path rehearsed with two gloo ranks on the one GPU (c3_dp sub-record included)
+      PGP_DIST_BACKEND=gloo PGP_DEVICE=0 run dist2 600 python3 -u bench.py --gpus 2 --steps 20 --warmup 3
+      python3 -c "import json; d=json.loads(open('$OUT/dist2.out').read().strip().splitlines()[-1]); print(d['n_gpus'], d['ranks_seen'], d['ms_per_step'], {k: (v.get('ms_per_step'), v.get('ranks_seen')) for k, v in d.get('sub_records', d.get('sub', {})).items()} if isinstance(d.get('sub_records', d.get('sub', {})), dict) else list(d.keys()))"
+      ;;
     abffn)
       L=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var
       run abffn50 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" base= f124=PGP_LIB=$L/libpreganplus_ffn124.so f132=PGP_LIB=$L/libpreganplus_ffn132.so
