@@ -89,15 +89,19 @@ __global__ __launch_bounds__(kDecWaves * 64) void dec_fwd2_kernel(int B, int S, 
       xload(tok + 1, xn);
     }
     const float* L = lds + buf * PCS * 256 + lane * 4;
+    // k-block outer, output tile inner: consecutive MFMAs go to different
+    // accumulators (a tile's 16 MFMAs in a row waited on each other)
 #pragma unroll
-    for (int t = 0; t < NT; ++t)
+    for (int kb = 0; kb < KB; ++kb) {
+      f32x4 a[NT];
 #pragma unroll
-      for (int kb = 0; kb < KB; ++kb) {
-        const f32x4 a = ld4(L + (t * KB + kb) * 256);
+      for (int t = 0; t < NT; ++t) a[t] = ld4(L + (t * KB + kb) * 256);
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if (kb < KB - 1 || e < ELAST) acc[t] = mfma(a[e], xc[kb][e], acc[t]);
-      }
+      for (int e = 0; e < 4; ++e)
+        if (kb < KB - 1 || e < ELAST)
+#pragma unroll
+          for (int t = 0; t < NT; ++t) acc[t] = mfma(a[t][e], xc[kb][e], acc[t]);
+    }
 #pragma unroll
     for (int kb = 0; kb < KB; ++kb) xc[kb] = xn[kb];
   }
