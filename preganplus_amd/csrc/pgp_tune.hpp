@@ -29,8 +29,10 @@ struct TuneGeo {
 // last-part finishes of the backward's reductions; zero in a fresh workspace,
 // each left at zero by the launch that uses it), then the regions below.
 constexpr long kTuneCounters = 1024;
+// counters [0, 2 * 3H): the decoder weight gradient's per-(token, half) parts;
+// kCtrGatTail: the GAT parameter tail of the fused reduction
 constexpr int kCtrGatTail = 1000;
-constexpr int kMaxDecDws = 4;  // decoder weight-gradient parts (windows split over up to 4)  // [0, 2 * 3H): the decoder weight gradient's per-(token, half) counters
+constexpr int kMaxDecDws = 4;  // decoder weight-gradient parts (windows split over up to 4)
 // Workspace regions (float offsets) for one (H, B); region-major, so the same
 // (H, B) must be used by the forward and the backward of one step.
 struct TunePlan {
