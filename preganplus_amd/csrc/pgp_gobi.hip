@@ -58,12 +58,15 @@ constexpr int kNE = 4;   // environments per workgroup: they share the weight re
 // workgroup 0, the wall clock of each barrier-delimited phase over the run;
 // pgp_gobi_prof_read copies the sums out
 #ifdef PGP_GOBI_PROF
-__device__ unsigned long long g_gobi_prof[16];
+constexpr int kProfWG = 256, kProfSlots = 32;
+__device__ unsigned long long g_gobi_prof[kProfWG][kProfSlots];
 #define GMARK(i)                                                        \
   do {                                                                  \
-    if (blockIdx.x == 0 && threadIdx.x == 0) {                          \
+    if (blockIdx.x < kProfWG && threadIdx.x == 0) {                     \
       const unsigned long long now_ = wall_clock64();                   \
-      g_gobi_prof[i] += now_ - gmark_t_;                                \
+      g_gobi_prof[blockIdx.x][i] += now_ - gmark_t_;                    \
+      if ((i) < 7 && act[0] + act[1] + act[2] + act[3] == 1)            \
+        g_gobi_prof[blockIdx.x][16 + (i)] += now_ - gmark_t_;           \
       gmark_t_ = now_;                                                  \
     }                                                                   \
   } while (0)
@@ -87,8 +90,8 @@ struct GobiLds {
   // four environments' k-th value), one pad row after every 16 (kp(k)) so the
   // lanes' chunks (16 or 32 rows each) start in different banks; the head's
   // and the input gradient's inputs per environment
-  alignas(16) float h1[kP1][kNE], h2[kP1][kNE], g2[kP1][kNE], g3[kP3][kNE];
-  float h3[kNE][kN3], th3[kNE][kN3], g1[kNE][kN1];
+  alignas(16) float h1[kP1][kNE], h2[kP1][kNE], g2[kP1][kNE], g3[kP3][kNE], g1[kP1][kNE];
+  float h3[kNE][kN3], th3[kNE][kN3];
   float o[kNE][4];
   int hs[kNE][kH];   // each container's host (the one-hot column of its allocation row)
   int dense[kNE];    // the init's allocation is not one-hot (iteration 0 takes the dense layer 1)
@@ -96,15 +99,16 @@ struct GobiLds {
 };
 
 // Thread roles (fixed for the whole run; every weight slice is loaded once):
-//   128-output layers (1, 2 and the backward's dh2, dh1): o = t >> 2, k-chunk
-//     sp = t & 3; an xor butterfly over the 4 lanes sums the chunks (every
-//     lane holds the same bits) and lane sp == e owns env e's activation and
-//     keeps its pre-activation for the backward;
+//   128-output layers (1, 2 and the backward's dh2, dh1): wave w, row r, row
+//     lane i: o = 16w + i, k-chunk sp = r; the rows' sums (row_sum4: the bits
+//     of the 4-lane butterfly) in every lane, and row sp == e owns env e's
+//     activation and keeps its pre-activation for the backward;
 //   layer 3 (64 outputs): o3 = t >> 3, k-chunk sp3 = t & 7, owner lane 2e;
 //   the head: wave e (t < 256), lane = o3;
-//   allocation entries: entry = t >> 1 (a container row = 32 lanes), k-chunk
-//     sq = t & 1 of the input gradient; lane sq owns the entry of envs
-//     e = sq, sq + 2 (their AdamW moments).
+//   allocation entries: a DPP row of 16 lanes (row r of wave w) is container
+//     c = 2w + (r >> 1), lane = host, k-chunk sq = r & 1 of the input gradient
+//     (the chunk pair of an entry in lanes l and l ^ 16); the lane owns the
+//     entry of envs e = sq, sq + 2 (their AdamW moments).
 struct GobiRegs {
   float w2f[32], w2b[32], w3f[16], w3b[16], w1c[64];
   float w1x[8];  // layer 1's cpu / ips weights of this lane's 4 containers
@@ -112,8 +116,8 @@ struct GobiRegs {
 };
 
 __device__ void load_regs(const float* __restrict__ W, GobiRegs& R) {
-  const int t = threadIdx.x, o = t >> 2, sp = t & 3, o3 = t >> 3, sp3 = t & 7;
-  const int entry = t >> 1, sq = t & 1, xi = (entry >> 4) * kF + 2 + (entry & 15);
+  const int t = threadIdx.x, o = (t >> 6) * 16 + (t & 15), sp = (t >> 4) & 3, o3 = t >> 3, sp3 = t & 7;
+  const int sq = (t >> 4) & 1, xi = ((t >> 6) * 2 + ((t >> 5) & 1)) * kF + 2 + (t & 15);
 #pragma unroll
   for (int j = 0; j < 64; ++j) R.w1c[j] = W[GobiW::W1T + xi * kN1 + sq * 64 + j];  // W1[k][xi]
 #pragma unroll
@@ -208,6 +212,111 @@ __device__ __forceinline__ void dot4(const float* w, const float (*h)[kNE], floa
     for (int q = 0; q < G; ++q) cur[q] = nxt[q];
   }
 }
+// the k-chunk dot products of the 128-output layers for the four environments:
+// row r of the wave holds chunk sp = r; its N inputs x 4 envs (k-major rows h,
+// from the chunk's first) are spread over the row's 16 lanes, P = N / 16
+// consecutive k each (P 16-byte reads), and k = J is broadcast from row lane
+// J / P (component J % P) into each environment's fmaf chain, in k order as
+// dot4's.  All four active: the chains side by side; otherwise only the
+// active environments' chains run (the others' sums are left at 0, unused).
+// Each multiply-add is one v_fmac_f32 with a row_newbcast source (the builtin
+// form costs a separate v_mov_b32_dpp).  A DPP instruction reads its swizzled
+// source as of 2 wait states back, and inline asm hides it from the compiler's
+// hazard check.  The sources here are LDS loads (no VALU writes them), and
+// tools/dpp_hazard_check.py checks the BUILT kernel for any VALU write of a
+// DPP source within 2 wait states (tests/test_roofline_isa.py runs it on the
+// library, so a compiler-inserted copy fails the CPU suite).  A tied s_nop
+// before the chains instead made the loads complete before the first FMA
+// (0.731 -> 0.756 ms).
+// acc += (row lane L's g) * w
+template <int L>
+__device__ __forceinline__ void fmac_bcast(float& acc, float g, float w) {
+  asm("v_fmac_f32_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(g), "v"(w), "i"(L));
+}
+// chain1: one environment's chain (k = J)
+template <int P, int E, int J, int N>
+__device__ __forceinline__ void chain1(const float4 (&gq)[P], const float* w, float& a) {
+  const float4 g = gq[J % P];
+  fmac_bcast<J / P>(a, E == 0 ? g.x : E == 1 ? g.y : E == 2 ? g.z : g.w, w[J]);
+  if constexpr (J + 1 < N) chain1<P, E, J + 1, N>(gq, w, a);
+}
+// chain4: the four chains side by side
+template <int P, int J, int N>
+__device__ __forceinline__ void chain4(const float4 (&gq)[P], const float* w, float (&a)[kNE]) {
+  const float4 g = gq[J % P];
+  fmac_bcast<J / P>(a[0], g.x, w[J]);
+  fmac_bcast<J / P>(a[1], g.y, w[J]);
+  fmac_bcast<J / P>(a[2], g.z, w[J]);
+  fmac_bcast<J / P>(a[3], g.w, w[J]);
+  if constexpr (J + 1 < N) chain4<P, J + 1, N>(gq, w, a);
+}
+template <int N, int P>
+__device__ __forceinline__ void dotb_regs(const float4 (&gq)[P], const float* w, const bool (&act)[kNE],
+                                          float (&r)[kNE]) {
+  static_assert(P == N / 16, "P inputs per row lane");
+#pragma unroll
+  for (int e = 0; e < kNE; ++e) r[e] = 0.f;
+  if (act[0] && act[1] && act[2] && act[3]) {
+    chain4<P, 0, N>(gq, w, r);
+  } else {
+    if (act[0]) chain1<P, 0, 0, N>(gq, w, r[0]);
+    if (act[1]) chain1<P, 1, 0, N>(gq, w, r[1]);
+    if (act[2]) chain1<P, 2, 0, N>(gq, w, r[2]);
+    if (act[3]) chain1<P, 3, 0, N>(gq, w, r[3]);
+  }
+}
+template <int N>
+__device__ __forceinline__ void dotb(const float (*h)[kNE], const float* w, const bool (&act)[kNE], float (&r)[kNE]) {
+  constexpr int P = N / 16;
+  const int lane = threadIdx.x & 15;
+  float4 gq[P];
+#pragma unroll
+  for (int q = 0; q < P; ++q) gq[q] = *reinterpret_cast<const float4*>(h[kp(P * lane + q)]);
+  dotb_regs<N, P>(gq, w, act, r);
+}
+// sum over the wave's 4 rows (lanes l ^ 16, then l ^ 32) by permlane swaps:
+// every lane gets (c0 + c1) + (c2 + c3), the bits of the 4-lane butterfly
+__device__ __forceinline__ float row_sum4(float v) {
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+// the row sums of the active environments' partials (all four: side by side,
+// no branch); the one of env `mine_e`
+__device__ __forceinline__ float sum_rows(float (&r)[kNE], const bool (&act)[kNE], int mine_e) {
+  float m = 0.f;
+  if (act[0] && act[1] && act[2] && act[3]) {
+#pragma unroll
+    for (int e = 0; e < kNE; ++e) {
+      r[e] = row_sum4(r[e]);
+      m = mine_e == e ? r[e] : m;
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < kNE; ++e) {
+      if (!act[e]) continue;
+      r[e] = row_sum4(r[e]);
+      m = mine_e == e ? r[e] : m;
+    }
+  }
+  return m;
+}
+// the same for the chunk pair of rows 2m, 2m + 1 (c0 + c1 in both)
+__device__ __forceinline__ float pair_sum(float v) {
+  const auto pr = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(pr[0]) + __uint_as_float(pr[1]);
+}
+__device__ __forceinline__ void sum_pairs(float (&r)[kNE], const bool (&act)[kNE]) {
+  if (act[0] && act[1] && act[2] && act[3]) {
+#pragma unroll
+    for (int e = 0; e < kNE; ++e) r[e] = pair_sum(r[e]);
+  } else {
+#pragma unroll
+    for (int e = 0; e < kNE; ++e)
+      if (act[e]) r[e] = pair_sum(r[e]);
+  }
+}
 // the lane-group sums of the four environments' partials; the one of env `mine_e`
 template <int G>
 __device__ __forceinline__ float sum_pick(float (&r)[kNE], int mine_e) {
@@ -238,7 +347,7 @@ __device__ __forceinline__ float softplus_grad(float g, float a, float z) {  // 
 __device__ void surrogate_fwd(const float* __restrict__ W, const GobiRegs& R, GobiLds& L, FwdKeep& K, bool grad,
                               const bool (&act)[kNE], const bool (&dense)[kNE], unsigned long long& gmark_t_) {
   (void)gmark_t_;
-  const int t = threadIdx.x, o = t >> 2, sp = t & 3, o3 = t >> 3, sp3 = t & 7;
+  const int t = threadIdx.x, o = (t >> 6) * 16 + (t & 15), sp = (t >> 4) & 3, o3 = t >> 3, sp3 = t & 7;
   bool act_sp = false, act_sp3 = false;  // this lane's owned environments (sp; sp3 / 2) are active
 #pragma unroll
   for (int e = 0; e < kNE; ++e) {
@@ -247,6 +356,7 @@ __device__ void surrogate_fwd(const float* __restrict__ W, const GobiRegs& R, Go
   }
   float mine = 0.f;
   // layer 1 (288 -> 128)
+  float l1[kNE] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int e = 0; e < kNE; ++e) {
     if (!act[e]) continue;
@@ -265,9 +375,9 @@ __device__ void surrogate_fwd(const float* __restrict__ W, const GobiRegs& R, Go
         acc = acc + L.w1a[o * kSA + c * kH + L.hs[e][c]];  // w * 1.0; the other columns multiply 0
       }
     }
-    acc = lane_sum<4>(acc);
-    if (sp == e) mine = acc;
+    l1[e] = acc;
   }
+  mine = sum_rows(l1, act, sp);
   // the elementwise tail once per lane, for its own environment sp (not once
   // per environment under a quarter of the lanes)
   if (act_sp) {
@@ -279,8 +389,8 @@ __device__ void surrogate_fwd(const float* __restrict__ W, const GobiRegs& R, Go
   GMARK(0);
   float r[kNE];
   // layer 2 (128 -> 128): W2 row o, k-chunk sp
-  dot4<32>(R.w2f, &L.h1[kp(sp * 32)], r);
-  mine = sum_pick<4>(r, sp);
+  dotb<32>(&L.h1[kp(sp * 32)], R.w2f, act, r);
+  mine = sum_rows(r, act, sp);
   if (act_sp) {
     const float a = mine + R.b2;
     K.a2 = a;
@@ -354,8 +464,8 @@ __global__ __launch_bounds__(kT) void gobi_kernel(int E, const float* __restrict
 #ifdef PGP_GOBI_PROF
   gmark_t_ = wall_clock64();
 #endif
-  const int t = threadIdx.x, o = t >> 2, sp = t & 3;
-  const int entry = t >> 1, sq = t & 1, c = entry >> 4, hcol = entry & 15;
+  const int t = threadIdx.x, o = (t >> 6) * 16 + (t & 15), sp = (t >> 4) & 3;
+  const int c = (t >> 6) * 2 + ((t >> 5) & 1), sq = (t >> 4) & 1, hcol = t & 15, entry = c * kH + hcol;
   const int xi = c * kF + 2 + hcol;  // this thread's allocation entry in the flattened input
   const long e0 = (long)blockIdx.x * kNE;
   for (int k = t; k < kN1 * kA; k += kT) {
@@ -389,7 +499,12 @@ __global__ __launch_bounds__(kT) void gobi_kernel(int E, const float* __restrict
     if (ones != 1 || other) L.dense[e] = 1;  // benign race: every writer stores 1
   }
   __syncthreads();
-  GMARK(7);
+#ifdef PGP_GOBI_PROF
+  {
+    const bool act[kNE] = {false, false, false, false};  // the prologue's mark
+    GMARK(7);
+  }
+#endif
   float m[kNE / 2], v[kNE / 2];  // AdamW moments of this lane's entries (envs sq, sq + 2)
 #pragma unroll
   for (int k = 0; k < kNE / 2; ++k) m[k] = v[k] = 0.f;
@@ -409,6 +524,12 @@ __global__ __launch_bounds__(kT) void gobi_kernel(int E, const float* __restrict
 #pragma unroll
     for (int e = 0; e < kNE; ++e) any |= act[e];
     if (!any) break;
+#ifdef PGP_GOBI_PROF
+    int nact_ = 0;
+#pragma unroll
+    for (int e = 0; e < kNE; ++e) nact_ += act[e];
+    const unsigned long long it_t0_ = wall_clock64();
+#endif
     surrogate_fwd(W, R, L, K, true, act, dense, gmark_t_);
     // ---- backward to the input (autograd of z; g3 came with the forward) ----
     bool act_sp = false;
@@ -417,38 +538,36 @@ __global__ __launch_bounds__(kT) void gobi_kernel(int E, const float* __restrict
     float mine = 0.f;
     // dh2 = W3^T g3 through softplus (W3 column o, k-chunk sp)
     float r[kNE];
-    dot4<16>(R.w3b, &L.g3[kp(sp * 16)], r);
-    mine = sum_pick<4>(r, sp);
+    dotb<16>(&L.g3[kp(sp * 16)], R.w3b, act, r);
+    mine = sum_rows(r, act, sp);
     if (act_sp) L.g2[kp(o)][sp] = softplus_grad(mine, K.a2, K.z2);
     if (t < kNE) L.flag[(it + 1) & 1][t] = 0;  // next iteration's flag; its last readers passed barriers since
     __syncthreads();
     GMARK(4);
     // dh1 = W2^T g2 through softplus (W2 column o, k-chunk sp)
-    dot4<32>(R.w2b, &L.g2[kp(sp * 32)], r);
-    mine = sum_pick<4>(r, sp);
-    if (act_sp) L.g1[sp][o] = softplus_grad(mine, K.a1, K.z1);
+    dotb<32>(&L.g2[kp(sp * 32)], R.w2b, act, r);
+    mine = sum_rows(r, act, sp);
+    if (act_sp) L.g1[kp(o)][sp] = softplus_grad(mine, K.a1, K.z1);
     __syncthreads();
     GMARK(5);
     // dx for the 256 allocation entries (W1[:, xi] . g1, 2 k-chunks of 64), AdamW, one-hot
     const float* ad = W + GobiW::ADAM + it * 4;
     const float a0 = ad[0], a1 = ad[1], a2 = ad[2];
+    // the row's chunk of g1 (64 k x 4 envs) spread over its 16 lanes (four
+    // 16-byte reads instead of 64), every k broadcast into the active
+    // environments' chains (dotb), then the chunk pair of rows 2m, 2m + 1
+    // (c0 + c1 in both) by a permlane swap
+    float gxa[kNE];
+    dotb<64>(&L.g1[kp(sq * 64)], R.w1c, act, gxa);
+    sum_pairs(gxa, act);
     // lane sq owns the entry of envs e = sq + 2k: AdamW and the one-hot once
-    // per k with every lane busy (lanes sq = 0 and 1 on envs 2k and 2k + 1)
+    // per k with every lane busy (rows sq = 0 and 1 on envs 2k and 2k + 1)
 #pragma unroll
     for (int k = 0; k < kNE / 2; ++k) {
       if (!act[2 * k] && !act[2 * k + 1]) continue;
-      float gxs[2] = {0.f, 0.f};
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        if (!act[2 * k + q]) continue;
-        float acc = 0.f;
-#pragma unroll
-        for (int j = 0; j < 64; ++j) acc = fmaf(R.w1c[j], L.g1[2 * k + q][sq * 64 + j], acc);
-        gxs[q] = lane_sum<2>(acc);
-      }
       const int e = sq + 2 * k;
       const bool on = sq ? act[2 * k + 1] : act[2 * k];
-      const float gx = sq ? gxs[1] : gxs[0];
+      const float gx = sq ? gxa[2 * k + 1] : gxa[2 * k];
       // ---- AdamW (torch single-tensor, opt.py:18 defaults) on the entry ----
       const float xold = L.x[e][xi];
       float& mm = m[k];
@@ -461,21 +580,19 @@ __global__ __launch_bounds__(kT) void gobi_kernel(int E, const float* __restrict
       const float denom = sqrtf(vv) / a2 + 1e-8f;
       xv = xv + (-a1) * mm / denom;           // addcdiv_: self + value * t1 / t2 (ATen's order)
       // ---- one-hot of the row's first argmax (opt.py:9-15): the row's lanes of this sq ----
-      // (max value, then lowest column) over the 16 lanes of this sq in the row's
-      // 32: xor 2, the row's parity class by rotations of 4 and 8 (each lane then
-      // holds the same winner), then xor 16
+      // (max value, then lowest column) over the row's 16 lanes: xor 1, xor 2,
+      // then the quads by rotations of 4 and 8 (each lane then holds the winner)
       float best = xv;
       int bi = hcol;
       auto take = [&](float ov, int oi) {
-        if (ov > best || (ov == best && oi < bi)) {
-          best = ov;
-          bi = oi;
-        }
+        const bool b = ov > best || (ov == best && oi < bi);
+        best = b ? ov : best;
+        bi = b ? oi : bi;
       };
+      take(dppf<kDppX1>(best), dppi<kDppX1>(bi));
       take(dppf<kDppX2>(best), dppi<kDppX2>(bi));
       take(dppf<kDppRor4>(best), dppi<kDppRor4>(bi));
       take(dppf<kDppRor8>(best), dppi<kDppRor8>(bi));
-      take(__shfl_xor(best, 16), __shfl_xor(bi, 16));
       if (on) {
         if (pre) pre[(e0 + e) * kH * kH + entry] = xv;  // test tap: the step's values before the projection
         const float nv = bi == hcol ? 1.f : 0.f;
@@ -497,6 +614,12 @@ __global__ __launch_bounds__(kT) void gobi_kernel(int E, const float* __restrict
         act[e] = false;
       }
     }
+#ifdef PGP_GOBI_PROF
+    if (blockIdx.x < kProfWG && t == 0) {  // iteration time and count by active environments
+      g_gobi_prof[blockIdx.x][7 + nact_] += wall_clock64() - it_t0_;
+      g_gobi_prof[blockIdx.x][11 + nact_] += 1;
+    }
+#endif
     ++it;
   }
   // final fitness of every real environment
@@ -515,7 +638,7 @@ __global__ __launch_bounds__(kT) void gobi_kernel(int E, const float* __restrict
     fitness[e0 + t] = L.o[t][2];
   }
 #ifdef PGP_GOBI_PROF
-  if (blockIdx.x == 0 && t == 0) g_gobi_prof[15] = (unsigned long long)it;
+  if (blockIdx.x < kProfWG && t == 0) g_gobi_prof[blockIdx.x][31] = (unsigned long long)it;
 #endif
 }
 
@@ -628,7 +751,7 @@ int pgp_gobi_prof_read(unsigned long long* out) {  // phase sums of workgroup 0 
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_gobi_prof), sizeof(g_gobi_prof)) == hipSuccess ? 0 : -1;
 }
 int pgp_gobi_prof_reset(void) {
-  static const unsigned long long z[16] = {};
+  static const unsigned long long z[kProfWG * kProfSlots] = {};
   return hipMemcpyToSymbol(HIP_SYMBOL(g_gobi_prof), z, sizeof(z)) == hipSuccess ? 0 : -1;
 }
 #endif

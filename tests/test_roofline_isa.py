@@ -119,3 +119,21 @@ def test_bench_traffic_ignores_other_builds(tmp_path):
         p.write_text(json.dumps(rec))
         assert bench.traffic_record(50, 64, "encoder", path=str(p))["hbm_bytes_per_launch"] == 123.0
         assert bench.traffic_record(50, 65, "encoder", path=str(p)) is None   # another batch
+
+
+@pytest.mark.skipif(not os.path.exists(LIB) or not os.path.exists("/opt/rocm/lib/llvm/bin/llvm-objdump"),
+                    reason="built library / llvm-objdump absent")
+def test_gobi_dpp_sources_clear_of_valu_writes():
+    """GOBI's row_newbcast multiply-adds are inline asm, outside the compiler's
+    hazard check: in the built gobi_kernel no VALU write of a DPP source sits
+    within the 2 wait states the hardware needs (tools/dpp_hazard_check.py)."""
+    import re
+    import dpp_hazard_check
+    import isa_count
+    asm = isa_count._disasm(LIB, "gobi_kernel")
+    m = re.search(r"^[0-9a-f]+ <_ZN3pgp12_GLOBAL__N_1\d+gobi_kernel[^>]*>:\n(.*?)(?=^[0-9a-f]+ <|\Z)", asm, re.S | re.M)
+    assert m is not None, "gobi_kernel not found in the built library"
+    insts = dpp_hazard_check.parse(m.group(1).split("\n"))
+    n, found = dpp_hazard_check.check_insts(insts)
+    assert n > 100, f"only {n} DPP instructions: the row_newbcast chains are gone?"
+    assert not found, found[:5]

@@ -349,6 +349,30 @@ for step in "$@"; do
       run gobib 200 python3 -u bench.py --config gobi --steps 50 --warmup 5 --no-cpu-baseline
       run loopb 300 python3 -u bench.py --config loop --steps 20 --warmup 3 --no-cpu-baseline
       ;;
+    gobi8ab)  # the in-tree GOBI against the round-5 v8 build (bit-identical results and timing), phases
+      run gobitest 300 python3 -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_gobi.py
+      run gobiab 300 python3 -u tools/dbg/gobi_ab.py $GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_gobi8.so
+      cat $OUT/gobiab.out
+      PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_gprof.so run gphase 120 python3 -u tools/gobi_phases.py
+      cat $OUT/gphase.out
+      ;;
+    gobivs)  # the in-tree GOBI against variant $GOBI_VS (bit-identical results and timing)
+      run gobivs 300 python3 -u tools/dbg/gobi_ab.py $GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_$GOBI_VS.so
+      cat $OUT/gobivs.out
+      ;;
+    ginv)  # GOBI batch invariance probe, in-tree and variant $GOBI_VS
+      run ginv 120 python3 -u tools/dbg/gobi_inv.py
+      PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_$GOBI_VS.so run ginvvs 120 python3 -u tools/dbg/gobi_inv.py
+      cat $OUT/ginv.out $OUT/ginvvs.out
+      ;;
+    gphase)
+      PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_gprof.so run gphase 120 python3 -u tools/gobi_phases.py
+      cat $OUT/gphase.out
+      ;;
+    gphase8)  # the same for the round-5 v8 kernel (variant gprof8)
+      PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_gprof8.so run gphase8 120 python3 -u tools/gobi_phases.py
+      cat $OUT/gphase8.out
+      ;;
     others)
       run fpe 300 python3 -u bench.py --config fpe --steps 100 --warmup 5
       run plugin 300 python3 -u bench.py --config plugin --steps 50 --warmup 5
