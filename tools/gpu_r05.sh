@@ -365,6 +365,13 @@ for step in "$@"; do
       PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_$GOBI_VS.so run ginvvs 120 python3 -u tools/dbg/gobi_inv.py
       cat $OUT/ginv.out $OUT/ginvvs.out
       ;;
+    abk3)  # C2 A/B: in-tree vs variant k3old, then the census parity tests
+      L=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var
+      run abk3 600 python3 -u tools/ab_bench.py --rounds 4 --args "--steps 100 --warmup 10 --no-cpu-baseline" new= old=PGP_LIB=$L/libpreganplus_k3old.so
+      grep median $OUT/abk3.out
+      run k3par 300 python3 -u -m pytest -x -q --timeout 240 --timeout-method thread tests/test_gpu_parity.py tests/test_gpu_decide.py
+      tail -2 $OUT/k3par.out
+      ;;
     gphase)
       PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_gprof.so run gphase 120 python3 -u tools/gobi_phases.py
       cat $OUT/gphase.out
