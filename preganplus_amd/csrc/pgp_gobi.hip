@@ -60,13 +60,16 @@ constexpr int kNE = 4;   // environments per workgroup: they share the weight re
 #ifdef PGP_GOBI_PROF
 constexpr int kProfWG = 256, kProfSlots = 32;
 __device__ unsigned long long g_gobi_prof[kProfWG][kProfSlots];
+// (summed in the workgroup's LDS, L.prof, and added to g_gobi_prof once at
+// the end: a global read-modify-write per mark stalled wave 0 for a memory
+// round trip that the next barrier then charged to every phase)
 #define GMARK(i)                                                        \
   do {                                                                  \
-    if (blockIdx.x < kProfWG && threadIdx.x == 0) {                     \
+    if (threadIdx.x == 0) {                                             \
       const unsigned long long now_ = wall_clock64();                   \
-      g_gobi_prof[blockIdx.x][i] += now_ - gmark_t_;                    \
+      L.prof[i] += now_ - gmark_t_;                                     \
       if ((i) < 7 && act[0] + act[1] + act[2] + act[3] == 1)            \
-        g_gobi_prof[blockIdx.x][16 + (i)] += now_ - gmark_t_;           \
+        L.prof[16 + (i)] += now_ - gmark_t_;                            \
       gmark_t_ = now_;                                                  \
     }                                                                   \
   } while (0)
@@ -95,7 +98,10 @@ struct GobiLds {
   float o[kNE][4];
   int hs[kNE][kH];   // each container's host (the one-hot column of its allocation row)
   int dense[kNE];    // the init's allocation is not one-hot (iteration 0 takes the dense layer 1)
-  int flag[2][kNE];  // "some entry changed" of the current / next iteration
+  alignas(16) int flag[2][kNE];  // "some entry changed" of the current / next iteration (one 16-byte read)
+#ifdef PGP_GOBI_PROF
+  unsigned long long prof[kProfSlots];
+#endif
 };
 
 // Thread roles (fixed for the whole run; every weight slice is loaded once):
@@ -421,12 +427,19 @@ __device__ void surrogate_fwd(const float* __restrict__ W, const GobiRegs& R, Go
       const float h3 = L.h3[e][l];
       float p0 = R.w40 * h3, p1 = R.w41 * h3;
       // 64-lane xor butterfly, offsets 32, 16, 8, 4, 2, 1 (the same bits in every
-      // lane): 32 and 16 by ds_bpermute, 8 = row_ror 8, 4 = two bank-masked row
-      // shifts, 2 and 1 = quad_perm
-#pragma unroll
-      for (int off = 32; off >= 16; off >>= 1) {
-        p0 += __shfl_xor(p0, off);
-        p1 += __shfl_xor(p1, off);
+      // lane): 32 and 16 by permlane swaps instead of ds_bpermute round trips,
+      // 8 = row_ror 8, 4 = two bank-masked row shifts, 2 and 1 = quad_perm.
+      // The first step keeps the form the compiler gave the shuffle version:
+      // the lane's own product fused into the add, fma(w, h3, partner's
+      // rounded product)
+      {
+        const bool hi = (l & 32) != 0;
+        const auto a0 = __builtin_amdgcn_permlane32_swap(__float_as_uint(p0), __float_as_uint(p0), false, false);
+        const auto a1 = __builtin_amdgcn_permlane32_swap(__float_as_uint(p1), __float_as_uint(p1), false, false);
+        p0 = fmaf(R.w40, h3, __uint_as_float(hi ? a0[0] : a0[1]));
+        p1 = fmaf(R.w41, h3, __uint_as_float(hi ? a1[0] : a1[1]));
+        p0 = pair_sum(p0);
+        p1 = pair_sum(p1);
       }
       p0 += dppf<kDppRor8>(p0);
       p1 += dppf<kDppRor8>(p1);
@@ -480,6 +493,9 @@ __global__ __launch_bounds__(kT) void gobi_kernel(int E, const float* __restrict
     L.dense[t] = 0;
     L.flag[0][t] = L.flag[1][t] = 0;
   }
+#ifdef PGP_GOBI_PROF
+  if (t < kProfSlots) L.prof[t] = 0;
+#endif
   GobiRegs R;
   load_regs(W, R);
   __syncthreads();
@@ -524,6 +540,10 @@ __global__ __launch_bounds__(kT) void gobi_kernel(int E, const float* __restrict
 #pragma unroll
     for (int e = 0; e < kNE; ++e) any |= act[e];
     if (!any) break;
+    // this iteration's AdamW scalars, requested here (scalar loads) so that the
+    // input-gradient phase does not wait for them
+    const float* ad = W + GobiW::ADAM + it * 4;
+    const float a0 = ad[0], a1 = ad[1], a2 = ad[2];
 #ifdef PGP_GOBI_PROF
     int nact_ = 0;
 #pragma unroll
@@ -551,8 +571,6 @@ __global__ __launch_bounds__(kT) void gobi_kernel(int E, const float* __restrict
     __syncthreads();
     GMARK(5);
     // dx for the 256 allocation entries (W1[:, xi] . g1, 2 k-chunks of 64), AdamW, one-hot
-    const float* ad = W + GobiW::ADAM + it * 4;
-    const float a0 = ad[0], a1 = ad[1], a2 = ad[2];
     // the row's chunk of g1 (64 k x 4 envs) spread over its 16 lanes (four
     // 16-byte reads instead of 64), every k broadcast into the active
     // environments' chains (dotb), then the chunk pair of rows 2m, 2m + 1
@@ -604,11 +622,14 @@ __global__ __launch_bounds__(kT) void gobi_kernel(int E, const float* __restrict
     __syncthreads();
     GMARK(6);
     // convergence (opt.py:28-31), per environment, in every thread's registers
+    // (the four flags in one 16-byte read)
+    const int4 fl = *reinterpret_cast<const int4*>(L.flag[it & 1]);
+    const int flv[kNE] = {fl.x, fl.y, fl.z, fl.w};
 #pragma unroll
     for (int e = 0; e < kNE; ++e) {
       dense[e] = false;  // one-hot from here on
       if (!act[e]) continue;
-      equal[e] = __builtin_amdgcn_readfirstlane(L.flag[it & 1][e]) ? 0 : equal[e] + 1;
+      equal[e] = __builtin_amdgcn_readfirstlane(flv[e]) ? 0 : equal[e] + 1;
       if (equal[e] > kPatience) {
         its[e] = it;
         act[e] = false;
@@ -616,8 +637,8 @@ __global__ __launch_bounds__(kT) void gobi_kernel(int E, const float* __restrict
     }
 #ifdef PGP_GOBI_PROF
     if (blockIdx.x < kProfWG && t == 0) {  // iteration time and count by active environments
-      g_gobi_prof[blockIdx.x][7 + nact_] += wall_clock64() - it_t0_;
-      g_gobi_prof[blockIdx.x][11 + nact_] += 1;
+      L.prof[7 + nact_] += wall_clock64() - it_t0_;
+      L.prof[11 + nact_] += 1;
     }
 #endif
     ++it;
@@ -638,7 +659,10 @@ __global__ __launch_bounds__(kT) void gobi_kernel(int E, const float* __restrict
     fitness[e0 + t] = L.o[t][2];
   }
 #ifdef PGP_GOBI_PROF
-  if (blockIdx.x < kProfWG && t == 0) g_gobi_prof[blockIdx.x][31] = (unsigned long long)it;
+  if (blockIdx.x < kProfWG && t == 0) {
+    for (int i = 0; i < 31; ++i) g_gobi_prof[blockIdx.x][i] += L.prof[i];
+    g_gobi_prof[blockIdx.x][31] = (unsigned long long)it;
+  }
 #endif
 }
 
