@@ -208,11 +208,25 @@ __global__ __launch_bounds__(256) void dw_kernel(DwArgs a) {
 // own dw_kernel launch would run it (same rows, same slab), so the partials
 // are bit-identical.  Shapes: kind 0 = <3 DP, DP>, 1 = <DP, DP>, 2 = <DP, XBP>.
 constexpr int kMaxDwSeg = 4;
+// the decoders' weight gradient (dec_dw_block): windows split over S parts,
+// one block per (token, n-half, part)
+struct DecDwArgs {
+  int B, S;
+  const float* dpre;
+  const float* X2;
+  float* Gd;
+  float* part;
+  unsigned* counter;
+};
+template <int H>
+PGP_DEV void dec_dw_block(const DecDwArgs& d, int tok, int y, int z, float* ys, float* xs);
 struct DwMulti {
   int n, nbx;
   int kind[kMaxDwSeg];
   DwArgs seg[kMaxDwSeg];
   int gat_nb;  // leading blocks running the GAT backward (0: none)
+  int dec_nb;  // then blocks running the decoders' weight gradient (0: none)
+  DecDwArgs dec;
 };
 
 // Deterministic reduction of partial slabs.  Outputs: segment A, rows x cols
@@ -603,14 +617,21 @@ __global__ __launch_bounds__(256) void dw_multi_kernel(DwMulti m, GatBwdArgs ga)
   using Q = TuneGeo<H>;
   constexpr int DP = Q::DP, XBP = Q::XBP;
   constexpr int ROWS = dw_rows(0);
-  constexpr int SY = ROWS * lds_stride(3 * DP), SX = ROWS * lds_stride(DP > XBP ? DP : XBP);
+  constexpr int SY0 = ROWS * lds_stride(3 * DP), SX0 = ROWS * lds_stride(DP > XBP ? DP : XBP);
+  constexpr int SYD = kDwRows * lds_stride(Q::NOP), SXD = kDwRows * lds_stride(DP);
+  constexpr int SY = SY0 > SYD ? SY0 : SYD, SX = SX0 > SXD ? SX0 : SXD;
   if ((int)blockIdx.x < m.gat_nb) {
     gat_bwd_block<H>(ga, blockIdx.x);
     return;
   }
   __shared__ __attribute__((aligned(16))) float ys[SY];
   __shared__ __attribute__((aligned(16))) float xs[SX];
-  const int b = blockIdx.x - m.gat_nb;
+  if ((int)blockIdx.x < m.gat_nb + m.dec_nb) {  // (token, half, part) = blocks in dec_dw_kernel's grid order
+    const int q = blockIdx.x - m.gat_nb, T = Q::T;
+    dec_dw_block<H>(m.dec, q % T, (q / T) % 2, q / (2 * T), ys, xs);
+    return;
+  }
+  const int b = blockIdx.x - m.gat_nb - m.dec_nb;
   const int s = b / m.nbx, bx = b - s * m.nbx;
   if (s >= m.n) return;
   switch (m.kind[s]) {
@@ -848,16 +869,17 @@ __global__ __launch_bounds__(256) void tune_loss_kernel(int B, int H, int NOP, c
 // half) adds them into G in part order (a device counter per (token, half) at
 // the workspace head).
 template <int H>
-__global__ __launch_bounds__(256) void dec_dw_kernel(int B, const float* __restrict__ dpre,
-                                                     const float* __restrict__ X2, float* __restrict__ Gd,
-                                                     float* __restrict__ part, unsigned* __restrict__ counter) {
+PGP_DEV void dec_dw_block(const DecDwArgs& d, int tok, int y, int z, float* ys, float* xs) {
   using Q = TuneGeo<H>;
   using G = TGeo<H>;
   constexpr int NP = Q::NOP, KP = Q::DP, NT = NP / 16, NTW = (NT + 7) / 8, KT = KP / 16;
-  __shared__ __attribute__((aligned(16))) float ys[kDwRows * lds_stride(NP)];
-  __shared__ __attribute__((aligned(16))) float xs[kDwRows * lds_stride(KP)];
+  const int B = d.B, S = d.S;
+  const float* __restrict__ dpre = d.dpre;
+  const float* __restrict__ X2 = d.X2;
+  float* __restrict__ Gd = d.Gd;
+  float* __restrict__ part = d.part;
+  unsigned* __restrict__ counter = d.counter;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, g = lane >> 4, i = lane & 15;
-  const int tok = blockIdx.x, y = blockIdx.y, z = blockIdx.z, S = gridDim.z;
   f32x4 acc[NTW][KT];
   float pb[NTW];
 #pragma unroll
@@ -951,6 +973,13 @@ __global__ __launch_bounds__(256) void dec_dw_kernel(int B, const float* __restr
       }
     }
   }
+}
+template <int H>
+__global__ __launch_bounds__(256) void dec_dw_kernel(DecDwArgs d) {
+  using Q = TuneGeo<H>;
+  __shared__ __attribute__((aligned(16))) float ys[kDwRows * lds_stride(Q::NOP)];
+  __shared__ __attribute__((aligned(16))) float xs[kDwRows * lds_stride(Q::DP)];
+  dec_dw_block<H>(d, blockIdx.x, blockIdx.y, blockIdx.z, ys, xs);
 }
 
 // ============================================================================
@@ -1375,8 +1404,13 @@ hipError_t tune_bwd_h(const TunePlan& p, const float* P, float* Gd, float* ws, c
   // and each layer's in_proj weight gradient (dQKV [M][3][DP] (x) X -> three
   // [H][H] blocks of L_IN + bias); nothing on the critical path reads them
   auto side_dec = [&]() -> hipError_t {
-    TCK((dec_dw_kernel<H><<<dim3(Q::T, 2, p.dec_dws), 256, 0, sd>>>(B, ws + p.dpre, ws + p.x[2], Gd, ws + p.part,
-                                                                     reinterpret_cast<unsigned*>(ws))));
+    const DecDwArgs da{B, p.dec_dws, ws + p.dpre, ws + p.x[2], Gd, ws + p.part, reinterpret_cast<unsigned*>(ws)};
+    if (defer) {  // no side stream: its blocks join the tail's multi-segment launch
+      dm.dec = da;
+      dm.dec_nb = Q::T * 2 * p.dec_dws;
+      return hipSuccess;
+    }
+    TCK((dec_dw_kernel<H><<<dim3(Q::T, 2, p.dec_dws), 256, 0, sd>>>(da)));
     return hipSuccess;
   };
   auto in_proj_dw = [&](int l, hipStream_t ss) -> hipError_t {
@@ -1492,7 +1526,7 @@ hipError_t tune_bwd_h(const TunePlan& p, const float* P, float* Gd, float* ws, c
   rb.mark_last_wt();  // fcd: read by the final reduction launch's last workgroup (gat_param_body)
   // without bit 4, layer 0's in_proj weight gradient closes the main stream's share
   if (!(early & 4) && (e = in_proj_dw(0, st)) != hipSuccess) return e;
-  if (defer) TCK((dw_multi_kernel<H><<<dm.gat_nb + dm.n * dm.nbx, 256, 0, st>>>(dm, gba)));
+  if (defer) TCK((dw_multi_kernel<H><<<dm.gat_nb + dm.dec_nb + dm.n * dm.nbx, 256, 0, st>>>(dm, gba)));
   if ((e = fk.join()) != hipSuccess) return e;  // the side stream's partials and G writes
   // every deferred weight-gradient reduction, then (the same launch's last
   // workgroup) the GAT parameter gradient, which needs fcd's reduction

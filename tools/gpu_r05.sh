@@ -372,6 +372,14 @@ for step in "$@"; do
       run k3par 300 python3 -u -m pytest -x -q --timeout 240 --timeout-method thread tests/test_gpu_parity.py tests/test_gpu_decide.py
       tail -2 $OUT/k3par.out
       ;;
+    abt)  # C3 A/B, H = 16 and 50: in-tree vs variant $TV, then the C3 parity tests
+      L=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var
+      run abt16 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 16 --steps 100 --warmup 10 --no-cpu-baseline" new= old=PGP_LIB=$L/libpreganplus_$TV.so
+      run abt50 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" new= old=PGP_LIB=$L/libpreganplus_$TV.so
+      grep median $OUT/abt16.out $OUT/abt50.out
+      run tc3par 600 python3 -u -m pytest -x -q --timeout 240 --timeout-method thread tests/test_gpu_c3step.py tests/test_gpu_tunedp.py tests/test_gpu_train.py
+      tail -2 $OUT/tc3par.out
+      ;;
     gphase)
       PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_gprof.so run gphase 120 python3 -u tools/gobi_phases.py
       cat $OUT/gphase.out
