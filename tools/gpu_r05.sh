@@ -380,6 +380,15 @@ for step in "$@"; do
       run tc3par 600 python3 -u -m pytest -x -q --timeout 240 --timeout-method thread tests/test_gpu_c3step.py tests/test_gpu_tunedp.py tests/test_gpu_train.py
       tail -2 $OUT/tc3par.out
       ;;
+    stalls)  # one PMC pass per config with tools/pmc_stalls.py's counter set: C3 H = 50 and C2
+      SC="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"
+      pmc stall_tune50 "$SC" --config tune --hosts 50 --steps 3 --warmup 1 --no-cpu-baseline
+      pmc stall_c2 "$SC" --steps 3 --warmup 1 --no-cpu-baseline
+      for n in stall_tune50 stall_c2; do
+        f=$(find $OUT/$n -name "*counter_collection.csv" | head -1)
+        python3 tools/pmc_stalls.py "$f" > $OUT/$n.txt && cat $OUT/$n.txt
+      done
+      ;;
     gphase)
       PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_gprof.so run gphase 120 python3 -u tools/gobi_phases.py
       cat $OUT/gphase.out
