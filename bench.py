@@ -1143,10 +1143,14 @@ def bench_loop(args):
         tun.step(x, y, cls)          # issued first at N = 1 (see bench_tune)
         if timed:
             ev[4].record(main)
+        # the weight sync in two parts (pgp_repack_master_sections): the
+        # PreGAN+ part as soon as the tuning step has updated its section,
+        # beside the GAN step; after it only the GAN part
+        model.repack_master(tr.P, tun.state[:2 * K], sections=1)
         if not shared_side:
             gan_step()
         main.wait_stream(side)
-        model.repack_master(tr.P, tun.state[:2 * K])
+        model.repack_master(tr.P, tun.state[:2 * K], sections=2)
         if timed:
             ev[5].record()
         model.forward(x, sched, out=out, stage=3)

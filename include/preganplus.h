@@ -528,6 +528,14 @@ int pgp_load_weights_master(pgp_model* m, const float* P_device, const double* p
  * PreGANPlus.py:115-136 runs the next interval on the updated model).  The
  * model must have been loaded once (pgp_load_weights). */
 int pgp_repack_master(pgp_model* m, const float* P_device, const double* prototypes_device, void* stream);
+/* One part of that rebuild: sections bit 0 = the PreGAN+ encoder / decoders
+ * (the transformer section of P and the prototypes: three launches), bit 1 =
+ * the GAN (Gen / Disc sections: one launch); 3 = pgp_repack_master.  Either
+ * part may run as soon as its section of P is final (the online interval
+ * repacks the PreGAN+ part after the tuning step while the GAN step runs,
+ * then only the GAN part after it); the two write disjoint packed regions. */
+int pgp_repack_master_sections(pgp_model* m, const float* P_device, const double* prototypes_device, int sections,
+                               void* stream);
 
 /* ------------------------------------------------------------------------
  * GOBI, the schedule producer: replaces

@@ -663,14 +663,20 @@ int pgp_adamw_table(float* P, const float* G, float* exp_avg, float* exp_avg_sq,
 }
 
 int pgp_repack_master(pgp_model* m, const float* P_device, const double* prototypes_device, void* stream) {
+  return pgp_repack_master_sections(m, P_device, prototypes_device, 3, stream);
+}
+
+int pgp_repack_master_sections(pgp_model* m, const float* P_device, const double* prototypes_device, int sections,
+                               void* stream) {
   if (!m || !P_device || !prototypes_device) return fail(PGP_ERR_ARG, "NULL argument");
+  if (sections < 1 || sections > 3) return fail(PGP_ERR_ARG, "sections: 1 (PreGAN+), 2 (GAN) or 3 (both)");
   if (m->fpe) return fail(PGP_ERR_STATE, "FPE model: master-layout reload covers the PreGAN+ model only");
   if (!m->loaded) return fail(PGP_ERR_STATE, "weights not loaded (the first load packs on the host)");
   long tr, go, dof, all;
   if (!master_offsets(m->H, &tr, &go, &dof, &all)) return fail(PGP_ERR_UNSUPPORTED, "host count");
   if (repack_blob_protos_offset(m->H, m->K) != all) return fail(PGP_ERR_STATE, "master / blob layout mismatch");
   if (!m->d_pscr) HIPCHK(hipMalloc(&m->d_pscr, repack_scratch_len(m->H) * sizeof(double)));
-  RepackArgs a{m->K, P_device, all, prototypes_device, m->d_pscr, m->d_frags, m->d_tab, m->d_gtab, m->d_gat};
+  RepackArgs a{m->K, P_device, all, prototypes_device, m->d_pscr, m->d_frags, m->d_tab, m->d_gtab, m->d_gat, sections};
   HIPCHK(launch_repack(m->H, a, reinterpret_cast<hipStream_t>(stream)));
   return PGP_OK;
 }

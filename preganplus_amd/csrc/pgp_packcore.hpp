@@ -360,16 +360,21 @@ PGP_HD void pack_phase1(int K, const Src& src, const Ex& ex, double scale, doubl
   });
 }
 
-// phase 2: everything else
+// phase 2: everything else.  sections: bit 0 the PreGAN+ encoder / decoder
+// layouts (which read phases 0 / 1's scratch), bit 1 the GAN's (pack_gan, from
+// its own weights only); independent outputs, so either order
 template <int H, class Src, class Ex>
 PGP_HD void pack_phase2(int K, const Src& src, const Ex& ex, double scale, const double* scr, float* F, float* T,
-                        float* GT) {
+                        float* GT, int sections = 3) {
   using G = Geo<H>;
   using Ly = typename BlobOff<H>::Ly;
   constexpr int d = H;
   constexpr long L = 3L * H * H;
   const BlobOff<H> B(K);
   auto V = [&](long o) { return View<Src>{src, o}; };
+  if (sections & 2)
+    pack_gan<H>(V(B.g0W), V(B.g0B), V(B.g2W), V(B.g2B), V(B.d0W), V(B.d0B), V(B.d2W), V(B.d2B), ex, F, GT);
+  if (!(sections & 1)) return;
   const View<Src> teB = V(B.teB), pe = V(B.pe);
   const double* A = scr + Scratch<H>::A;
   const double* FT = scr + Scratch<H>::FOLD;
@@ -584,8 +589,6 @@ PGP_HD void pack_phase2(int K, const Src& src, const Ex& ex, double scale, const
   });
   const View<Src> protos = V(B.protos);
   ex.par(2L * K, [&](long k) { T[G::T_PROTO + k] = (float)protos[k]; });
-
-  pack_gan<H>(V(B.g0W), V(B.g0B), V(B.g2W), V(B.g2B), V(B.d0W), V(B.d0B), V(B.d2W), V(B.d2B), ex, F, GT);
 }
 
 }  // namespace packcore

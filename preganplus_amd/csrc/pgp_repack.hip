@@ -38,14 +38,14 @@ struct DevEx {
 
 template <int H>
 __global__ __launch_bounds__(256) void repack_kernel(int phase, int K, DevSrc src, double scale, double* scr,
-                                                     float* F, float* T, float* GT, float* gatc) {
+                                                     float* F, float* T, float* GT, float* gatc, int sections) {
   const DevEx ex{(long)blockIdx.x * blockDim.x + threadIdx.x, (long)gridDim.x * blockDim.x};
   if (phase == 0)
     packcore::pack_phase0<H>(K, src, ex, scr, gatc);
   else if (phase == 1)
     packcore::pack_phase1<H>(K, src, ex, scale, scr);
   else
-    packcore::pack_phase2<H>(K, src, ex, scale, scr, F, T, GT);
+    packcore::pack_phase2<H>(K, src, ex, scale, scr, F, T, GT, sections);
 }
 
 template <int H>
@@ -56,11 +56,16 @@ hipError_t repack_h(const RepackArgs& a, hipStream_t st) {
   // the largest loop is the decoders' (H * 3 * DEC_G groups of 256 floats)
   const long big = (long)H * 3 * G::DEC_G * 256;
   const int grid2 = (int)std::min<long>(2048, (big + 255) / 256);
-  repack_kernel<H><<<1, 256, 0, st>>>(0, a.K, src, scale, a.scr, a.frags, a.tab, a.gtab, a.gat);
-  // phase 1 also sums the decoder weights per (row, feature, step): MT_O*16*H*3 items
-  const int grid1 = (int)std::min<long>(256, ((long)G::MT_O * 16 * H * 3 + 255) / 256);
-  repack_kernel<H><<<grid1, 256, 0, st>>>(1, a.K, src, scale, a.scr, a.frags, a.tab, a.gtab, a.gat);
-  repack_kernel<H><<<grid2, 256, 0, st>>>(2, a.K, src, scale, a.scr, a.frags, a.tab, a.gtab, a.gat);
+  if (a.sections & 1) {  // phases 0 / 1 feed the encoder / decoder part of phase 2 only
+    repack_kernel<H><<<1, 256, 0, st>>>(0, a.K, src, scale, a.scr, a.frags, a.tab, a.gtab, a.gat, a.sections);
+    // phase 1 also sums the decoder weights per (row, feature, step): MT_O*16*H*3 items
+    const int grid1 = (int)std::min<long>(256, ((long)G::MT_O * 16 * H * 3 + 255) / 256);
+    repack_kernel<H><<<grid1, 256, 0, st>>>(1, a.K, src, scale, a.scr, a.frags, a.tab, a.gtab, a.gat, a.sections);
+  }
+  // the GAN alone: its largest loop is the per-container groups (C * GC_G groups of 256)
+  const int gridg = (int)std::min<long>(2048, ((long)G::C * G::GC_G * 256 + 255) / 256);
+  repack_kernel<H><<<(a.sections & 1) ? grid2 : gridg, 256, 0, st>>>(2, a.K, src, scale, a.scr, a.frags, a.tab,
+                                                                       a.gtab, a.gat, a.sections);
   return hipGetLastError();
 }
 

@@ -14,6 +14,7 @@ struct RepackArgs {
   float* tab;          // Geo<H>::t_size(K)
   float* gtab;         // Geo<H>::G_SIZE
   float* gat;          // [8] GAT constants u[4] | v[4]
+  int sections = 3;    // bit 0: the PreGAN+ encoder / decoders (phases 0-2), bit 1: the GAN (pack_gan)
 };
 
 long repack_scratch_len(int H);

@@ -62,19 +62,22 @@ class DecisionModel:
                       "pgp_load_weights_master")
         self.prototypes = pr.copy()
 
-    def repack_master(self, P: torch.Tensor, protos_dev: torch.Tensor, prototypes_host=None, stream=None):
+    def repack_master(self, P: torch.Tensor, protos_dev: torch.Tensor, prototypes_host=None, stream=None,
+                      sections: int = 3):
         """Rebuild the packed inference weights ON THE DEVICE (``pgp_repack_master``)
         from device master weights P (natural fp32) and device prototypes
         protos_dev [K,2] fp64: three launches on the stream, no host round trip,
         the same bits as load_master.  prototypes_host (optional) updates the
-        host-side copy of the prototypes."""
+        host-side copy of the prototypes.  sections (``pgp_repack_master_sections``):
+        1 the PreGAN+ encoder / decoders only, 2 the GAN only, 3 both."""
         if protos_dev.dtype != torch.float64 or protos_dev.numel() != 2 * self.K or not protos_dev.is_contiguous():
             raise ValueError(f"protos_dev must be contiguous float64 [{self.K},2] on the device")
         L = self._L
-        L.pgp_repack_master.argtypes = [ctypes.c_void_p] * 4
+        L.pgp_repack_master_sections.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int, ctypes.c_void_p]
         st = stream if stream is not None else torch.cuda.current_stream(self.device)
-        _native.check(L.pgp_repack_master(self._h, ctypes.c_void_p(P.data_ptr()), ctypes.c_void_p(protos_dev.data_ptr()),
-                                          ctypes.c_void_p(st.cuda_stream)), "pgp_repack_master")
+        _native.check(L.pgp_repack_master_sections(self._h, ctypes.c_void_p(P.data_ptr()),
+                                                   ctypes.c_void_p(protos_dev.data_ptr()), int(sections),
+                                                   ctypes.c_void_p(st.cuda_stream)), "pgp_repack_master_sections")
         if prototypes_host is not None:
             self.prototypes = np.array(prototypes_host, dtype=np.float64)
 

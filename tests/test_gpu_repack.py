@@ -45,6 +45,40 @@ def test_device_repack_equals_host_pack(H):
     assert not torch.equal(base["logits"], b["logits"])
 
 
+@pytest.mark.parametrize("H", [16, 50])
+def test_repack_sections_equal_full_repack(H):
+    """pgp_repack_master_sections: the PreGAN+ part (1) then the GAN part (2),
+    or the other way round, give the same packed model as one full repack
+    (bit-identical forward outputs), and each part alone changes only its own
+    outputs (the GAN part leaves the logits as they were)."""
+    from preganplus_amd import train as TR
+    from preganplus_amd.model import DecisionModel
+    rng = np.random.default_rng(7 + H)
+    w = W.synth_weights(H, seed=H + 1)
+    tr = TR.Trainer(H, w, max_batch=1)
+    tr.P.add_(torch.randn_like(tr.P) * 1e-2)
+    protos = rng.uniform(0, 1, (H, 2))
+    pd = torch.tensor(protos, dtype=torch.float64, device=tr.device)
+    B = 40
+    x = torch.tensor(rng.uniform(0, 1, (B, 3, 3 * H)), dtype=torch.float32, device=tr.device)
+    s = torch.tensor(rng.uniform(0, 1, (B, H, H)), dtype=torch.float32, device=tr.device)
+    full, a, b, gan_only = (DecisionModel(H, w) for _ in range(4))
+    full.repack_master(tr.P, pd, protos)
+    a.repack_master(tr.P, pd, protos, sections=1)
+    a.repack_master(tr.P, pd, protos, sections=2)
+    b.repack_master(tr.P, pd, protos, sections=2)
+    b.repack_master(tr.P, pd, protos, sections=1)
+    ref = _outputs(full, x, s)
+    for m in (a, b):
+        o = _outputs(m, x, s)
+        for k in ref:
+            assert torch.equal(ref[k], o[k]), k
+    gan_only.repack_master(tr.P, pd, protos, sections=2)
+    base, g = _outputs(DecisionModel(H, w), x, s), _outputs(gan_only, x, s)
+    assert torch.equal(base["logits"], g["logits"])
+    assert not torch.equal(base["probs"], g["probs"])
+
+
 def test_plugin_sync_uses_device_state():
     """PreGANPlusRecovery.sync_inference_weights after tune_model rebuilds from
     the tuning graph's device state: same outputs as the host repack."""

@@ -389,6 +389,12 @@ for step in "$@"; do
         python3 tools/pmc_stalls.py "$f" > $OUT/$n.txt && cat $OUT/$n.txt
       done
       ;;
+    trepack)  # the repack tests, then the loop line
+      run trepack 300 python3 -u -m pytest -x -q --timeout 240 --timeout-method thread tests/test_gpu_repack.py tests/test_gpu_loop.py
+      tail -2 $OUT/trepack.out
+      run loopb 300 python3 -u bench.py --config loop --steps 20 --warmup 3 --no-cpu-baseline
+      python3 -c "import json; d=json.loads(open('$OUT/loopb.out').read().strip().splitlines()[-1]); print(d['ms_per_step'], d.get('stage_ms'))"
+      ;;
     gphase)
       PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_gprof.so run gphase 120 python3 -u tools/gobi_phases.py
       cat $OUT/gphase.out
