@@ -31,18 +31,23 @@ namespace {
 // starts each chunk kGanSleep x CPC x 64 cycles late (A/B at H = 50, two
 // containers per chunk: 24 / 48 / 96 / 127 units 0.788 / 0.788 / 0.793 /
 // 0.798 ms against 0.800 without; profiles/r03/c2ab/k3_stagger2.txt).
-constexpr int kGanWaves = 16;
+constexpr int kGanWaves = 16;  // waves per workgroup at large batches (kGanWavesSmall below)
 constexpr int kQC = 8;
 constexpr int kChunkG = 65;
 constexpr int kTailMax = 2;
 constexpr int kGanSleep = 24;
+#ifndef PGP_K3_SMALL_WAVES
+#define PGP_K3_SMALL_WAVES 4
+#endif
+constexpr int kGanWavesSmall = PGP_K3_SMALL_WAVES;
+constexpr long kGanSmallBlocks = 16L * 256;  // below 64 K windows (16 x 256 blocks of 16), kGanWavesSmall
 
 template <int P>
 __device__ __forceinline__ void gan_prio() {
   __builtin_amdgcn_s_setprio(P);
 }
 
-template <int H>
+template <int H, int NW = kGanWaves>
 struct GanGeo {
   using G = Geo<H>;
   static constexpr int NQC = cdiv(G::SQ, kQC);
@@ -55,7 +60,7 @@ struct GanGeo {
   using TgtT = typename std::conditional<(G::C < 128), signed char, short>::type;
   static constexpr int TGT = 2 * G::C * 16;  // target entries per wave
   static constexpr int lds_bytes(int cpc) {
-    return 2 * mx(G::GE_G, mx(kQC * G::GS_G, cpc * G::GC_G + 1)) * G::FQ * 4 + kGanWaves * TGT * (int)sizeof(TgtT);
+    return 2 * mx(G::GE_G, mx(kQC * G::GS_G, cpc * G::GC_G + 1)) * G::FQ * 4 + NW * TGT * (int)sizeof(TgtT);
   }
   static constexpr int cpc() {
     int best = 1;
@@ -89,14 +94,14 @@ struct GanGeo {
 
 __device__ __attribute__((aligned(8))) float k3_zero_pair[2];  // never written
 
-template <int H>
-__global__ __launch_bounds__(kGanWaves * 64) void gan_kernel(FwdArgs a) {
+template <int H, int NW>
+__global__ __launch_bounds__(NW * 64) void gan_kernel(FwdArgs a) {
   using G = Geo<H>;
-  using GG = GanGeo<H>;
+  using GG = GanGeo<H, NW>;
   extern __shared__ __attribute__((aligned(16))) float smem[];  // ring [2][SLOT] | targets
   const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const long blk = (long)blockIdx.x * kGanWaves + wv;
+  const long blk = (long)blockIdx.x * NW + wv;
   const long nblk = (a.B + 15) / 16;
   const long b = blk * 16 + j;
   const bool valid = blk < nblk && b < a.B;
@@ -113,17 +118,17 @@ __global__ __launch_bounds__(kGanWaves * 64) void gan_kernel(FwdArgs a) {
     const float* src;
     int ng;
     GG::chunk(0, a.frags, &src, &ng);
-    dma_groups(src, cur, ng, wv, kGanWaves, lane);
+    dma_groups(src, cur, ng, wv, NW, lane);
   }
   auto issue = [&]() {
     if (next < GG::NCHUNK) {
       const float* src;
       int ng;
       GG::chunk(next, a.frags, &src, &ng);
-      dma_groups(src, nxt, ng, wv, kGanWaves, lane);
+      dma_groups(src, nxt, ng, wv, NW, lane);
       if (next > GG::NQC)  // a container chunk: its biases after its groups (G_SIZE pads the last)
         dma_groups(gt + G::G_B2 + (long)(next - 1 - GG::NQC) * GG::CPC * GG::BIAS_F, nxt + ng * 256, 1,
-                   (wv + ng) % kGanWaves, kGanWaves, lane);
+                   (wv + ng) % NW, NW, lane);
     }
   };
   auto advance = [&]() {
@@ -350,7 +355,7 @@ __global__ __launch_bounds__(kGanWaves * 64) void gan_kernel(FwdArgs a) {
     // interval late, so its tanh / argmax VALU phases meet the first half's
     // MFMAs instead of every wave reaching them together (at most two
     // containers per chunk: with 4-8, at H <= 32, it cost the fleet 0.3 %)
-    if (GG::CPC <= 2 && c % GG::CPC == 0 && wv >= kGanWaves / 2) __builtin_amdgcn_s_sleep(kGanSleep * GG::CPC);
+    if (NW > 1 && GG::CPC <= 2 && c % GG::CPC == 0 && wv >= NW / 2) __builtin_amdgcn_s_sleep(kGanSleep * GG::CPC);
     gen2(c, cw, cur, ns, racc);
     const Arg x = finish_v1(ns, racc, sv);
     finish_m2(cw, ns);
@@ -409,21 +414,32 @@ __global__ __launch_bounds__(kGanWaves * 64) void gan_kernel(FwdArgs a) {
   }
 }
 
-template <int H>
-hipError_t launch(const FwdArgs& a, hipStream_t st) {
-  using GG = GanGeo<H>;
+template <int H, int NW>
+hipError_t launch_nw(const FwdArgs& a, hipStream_t st) {
+  using GG = GanGeo<H, NW>;
   static_assert(GG::LDS_BYTES <= 160 * 1024, "K3 LDS");
   static_assert(Geo<H>::C < 32768, "int8 / int16 targets");
   static bool attr = [] {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gan_kernel<H>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gan_kernel<H, NW>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, GG::LDS_BYTES);
     return true;
   }();
   (void)attr;
   const long nblk = (a.B + 15) / 16;
-  const int grid = (int)((nblk + kGanWaves - 1) / kGanWaves);
-  gan_kernel<H><<<grid, kGanWaves * 64, GG::LDS_BYTES, st>>>(a);
+  const int grid = (int)((nblk + NW - 1) / NW);
+  gan_kernel<H, NW><<<grid, NW * 64, GG::LDS_BYTES, st>>>(a);
   return hipGetLastError();
+}
+// Small batches: 16 waves per workgroup put 256 windows on ONE CU (1,024
+// windows: 4 CUs); kGanWavesSmall waves per workgroup spread them over more
+// CUs, each workgroup streaming the weights through its own LDS ring.  Every
+// wave computes its 16 windows exactly as before (same operands, same MFMA
+// order): the outputs are the same bits.
+template <int H>
+hipError_t launch(const FwdArgs& a, hipStream_t st) {
+  const long nblk = (a.B + 15) / 16;
+  if (nblk < kGanSmallBlocks) return launch_nw<H, kGanWavesSmall>(a, st);
+  return launch_nw<H, kGanWaves>(a, st);
 }
 
 }  // namespace

@@ -395,6 +395,13 @@ for step in "$@"; do
       run loopb 300 python3 -u bench.py --config loop --steps 20 --warmup 3 --no-cpu-baseline
       python3 -c "import json; d=json.loads(open('$OUT/loopb.out').read().strip().splitlines()[-1]); print(d['ms_per_step'], d.get('stage_ms'))"
       ;;
+    abk3w)  # K3 waves per workgroup at small batches: the loop line (1,024 windows) and the K3 tests
+      L=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var
+      run k3wpar 300 python3 -u -m pytest -x -q --timeout 240 --timeout-method thread tests/test_gpu_parity.py tests/test_gpu_decide.py tests/test_gpu_loop.py
+      tail -2 $OUT/k3wpar.out
+      run abk3w 900 python3 -u tools/ab_bench.py --rounds 3 --args "--config loop --steps 20 --warmup 3 --no-cpu-baseline" w4= w1=PGP_LIB=$L/libpreganplus_k3w1.so w2=PGP_LIB=$L/libpreganplus_k3w2.so w8=PGP_LIB=$L/libpreganplus_k3w8.so w16=PGP_LIB=$L/libpreganplus_k3w16.so
+      grep median $OUT/abk3w.out
+      ;;
     gphase)
       PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_gprof.so run gphase 120 python3 -u tools/gobi_phases.py
       cat $OUT/gphase.out
