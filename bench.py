@@ -77,20 +77,22 @@ def traffic_record(H, B, kernel, path=None):
         d = json.load(open(p))
         if int(d.get("batch", -1)) != B:
             return None
-        if d.get("isa_sha256") is None or d["isa_sha256"] != loaded_isa_hash(kernel + "_kernel", H):
+        if d.get("isa_sha256") is None or d["isa_sha256"] != loaded_isa_hash(kernel + "_kernel", H,
+                                                                             d.get("template_args")):
             return None
         return d
     except Exception:
         return None
 
 
-def loaded_isa_hash(name, H):
-    """sha256 of kernel `name`<H> in the library this process loads (PGP_LIB or
-    the in-tree build), tools/isa_count.kernel_isa_hash; None without llvm-objdump."""
+def loaded_isa_hash(name, H, targs=None):
+    """sha256 of kernel `name`<H> (or `name`<targs...>) in the library this
+    process loads (PGP_LIB or the in-tree build), tools/isa_count.kernel_isa_hash;
+    None without llvm-objdump."""
     try:
         sys.path.insert(0, os.path.join(ROOT, "tools"))
         import isa_count
-        return isa_count.kernel_isa_hash(name, H, lib=_native.LIB_PATH)
+        return isa_count.kernel_isa_hash(name, H, lib=_native.LIB_PATH, targs=targs)
     except Exception:
         return None
 

@@ -101,7 +101,7 @@ def test_committed_pmc_traffic_matches_built_library():
     for f in files:
         d = json.load(open(f))
         m = re.match(r"pmc_(\w+)_h(\d+)\.json", os.path.basename(f))
-        want = isa_count.kernel_isa_hash(m.group(1) + "_kernel", int(m.group(2)))
+        want = isa_count.kernel_isa_hash(m.group(1) + "_kernel", int(m.group(2)), targs=d.get("template_args"))
         assert d.get("isa_sha256") == want, f"{os.path.basename(f)} is stale (taken with another build)"
 
 

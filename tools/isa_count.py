@@ -77,7 +77,7 @@ def _all_asm(lib):
     return _ASM_CACHE[key]
 
 
-def kernel_isa_hash(name, H=None, lib=LIB):
+def kernel_isa_hash(name, H=None, lib=LIB, targs=None):
     """sha256 of kernel `name` (template argument H if given) as BUILT in `lib`:
     its instruction text with addresses and encodings stripped, so it changes
     when that kernel's code changes and not when another kernel moves it.  The
@@ -86,7 +86,12 @@ def kernel_isa_hash(name, H=None, lib=LIB):
     same.  None when the kernel is not found."""
     import hashlib
     asm = _all_asm(lib)
-    targ = rf"ILi{H}E" if H is not None else ""
+    # targs: every integer template argument (e.g. gan_kernel<16, 16>: the same
+    # H has several instantiations); otherwise the first whose first is H
+    if targs:
+        targ = "I" + "".join(f"Li{int(t)}E" for t in targs) + "E"
+    else:
+        targ = rf"ILi{H}E" if H is not None else ""
     m = re.search(rf"^[0-9a-f]+ <(_ZN3pgp12_GLOBAL__N_1\d+{name}{targ}[^>]*)>:\n(.*?)(?=^[0-9a-f]+ <|\Z)", asm,
                   re.S | re.M)
     if m is None:
