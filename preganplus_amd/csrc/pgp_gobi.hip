@@ -3,20 +3,24 @@
 // the energy_latency_16 surrogate (scheduler/BaGTI/src/models.py:8-27), for a
 // batch of independent environments.
 //
-// One 1024-thread workgroup per environment runs the whole optimisation
-// in-kernel (the reference's loop: up to 200 AdamW steps on the input matrix,
-// one-hot projection after each, stop after 31 unchanged steps).  Thread t < 256
-// owns allocation entry t = (container t/16, host t%16): its AdamW moments live
-// in registers, and a row's first-argmax is a 16-lane reduction inside one wave.
-// The MLP (288-128-128-64-2) and its input gradient are VALU dot products split
-// 4-16 ways over the threads; layer 1 (60% of the work, used in both
-// directions) sits in LDS as one copy with a 289-float row stride, so row reads
-// (forward) and column reads (input gradient) are both bank-conflict-free;
-// layers 2-3 are read from L2, forward from transposed copies, backward from
-// the natural rows, both coalesced.  Elementwise semantics follow torch's
-// CPU kernels (softplus threshold 20, tanhshrink = x - tanh x composite,
-// sigmoid backward g(1-y)y, AdamW single-tensor op order); per-iteration AdamW
-// scalars (cosine lr) are computed on the host in double, as torch does.
+// One 512-thread workgroup (8 waves, 2 per SIMD) runs the whole optimisation
+// of kNE = 4 environments in-kernel (the reference's loop: up to 200 AdamW
+// steps on the input matrix, one-hot projection after each, stop after 31
+// unchanged steps); the four share the weight registers and every barrier,
+// and the launch lasts as long as its slowest workgroup's iteration chain.
+// The MLP (288-128-128-64-2) and its input gradient are VALU dot products
+// split over the threads in fixed k-chunks whose association every variant
+// keeps (the trajectories are bit-identical to round 2's v7): the 128-output
+// layers and the input gradient on DPP rows (a row's chunk inputs spread over
+// its 16 lanes and broadcast by v_fmac_f32_dpp row_newbcast, the chunk sums by
+// permlane swaps), layer 3 and the head on lane groups (DPP butterflies).
+// Layer 1's allocation columns sit in LDS (the forward's one-hot column
+// gather); the other weights live in registers.  Once some environments of a
+// workgroup have converged, only the active ones' chains run.  Elementwise
+// semantics follow torch's CPU kernels (softplus threshold 20, tanhshrink =
+// x - tanh x composite, sigmoid backward g(1-y)y, AdamW single-tensor op
+// order); per-iteration AdamW scalars (cosine lr) are computed on the host in
+// double, as torch does.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
