@@ -402,6 +402,12 @@ for step in "$@"; do
       run abk3w 900 python3 -u tools/ab_bench.py --rounds 3 --args "--config loop --steps 20 --warmup 3 --no-cpu-baseline" w4= w1=PGP_LIB=$L/libpreganplus_k3w1.so w2=PGP_LIB=$L/libpreganplus_k3w2.so w8=PGP_LIB=$L/libpreganplus_k3w8.so w16=PGP_LIB=$L/libpreganplus_k3w16.so
       grep median $OUT/abk3w.out
       ;;
+    abdws2)  # the decoder weight gradient's window split S: in-tree (4) vs 1 and 2
+      L=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var
+      run abdws50 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" s4= s1=PGP_LIB=$L/libpreganplus_dws1.so s2=PGP_LIB=$L/libpreganplus_dws2.so
+      run abdws16 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 16 --steps 100 --warmup 10 --no-cpu-baseline" s4= s1=PGP_LIB=$L/libpreganplus_dws1.so s2=PGP_LIB=$L/libpreganplus_dws2.so
+      grep median $OUT/abdws50.out $OUT/abdws16.out
+      ;;
     gphase)
       PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_gprof.so run gphase 120 python3 -u tools/gobi_phases.py
       cat $OUT/gphase.out
