@@ -36,10 +36,9 @@ constexpr int kQC = 8;
 constexpr int kChunkG = 65;
 constexpr int kTailMax = 2;
 constexpr int kGanSleep = 24;
-#ifndef PGP_K3_SMALL_WAVES
-#define PGP_K3_SMALL_WAVES 4
-#endif
-constexpr int kGanWavesSmall = PGP_K3_SMALL_WAVES;
+// (A/B on the online interval's 1,024 windows, 1 / 2 / 4 / 8 / 16 waves:
+// 1.031 / 1.034 / 1.026 / 1.043 / 1.089 ms, profiles/r05/k3_small/)
+constexpr int kGanWavesSmall = 4;
 constexpr long kGanSmallBlocks = 16L * 256;  // below 64 K windows (16 x 256 blocks of 16), kGanWavesSmall
 
 template <int P>
