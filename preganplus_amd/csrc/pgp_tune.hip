@@ -1379,8 +1379,9 @@ hipError_t tune_bwd_h(const TunePlan& p, const float* P, float* Gd, float* ws, c
     TCK((tune_loss_kernel<<<(int)(((long)B * H + 255) / 256), 256, 0, st>>>(B, H, Q::NOP, logits, protos, y, mult,
                                                                              tgt, ws + p.dpre)));
   // Side work issued as soon as its inputs exist: the decoders' weight
-  // gradient right here (bit 2), layer 1's in_proj weight gradient right after
-  // layer 1's attention backward (bit 1).  They run beside the fused launches
+  // gradient early (bit 2: after the first fused launch, dec_late below),
+  // layer 1's in_proj weight gradient right after layer 1's attention backward
+  // (bit 1).  They run beside the fused launches
   // on the CUs those leave free (tf_grid_for takes the fewest workgroups with
   // the same longest wave): C3 at H = 50 1.171 -> 1.131 ms
   // (profiles/r04/side_early/).  Bit 4: layer 0's in_proj weight gradient on
@@ -1433,7 +1434,13 @@ hipError_t tune_bwd_h(const TunePlan& p, const float* P, float* Gd, float* ws, c
     return hipSuccess;
   };
 
-  if (early & 2) {
+  // With a side stream the decoders' weight gradient forks at the end of the
+  // first fused launch (layer 1's feed-forward backward), so it runs beside
+  // layer 1's attention backward, where the side stream was idle, instead of
+  // beside that first launch, which the GAN stream already shares: C3 at
+  // H = 50 1.067 -> 1.049 ms (A/B, profiles/r05/dec_late/)
+  const bool dec_late = (early & 2) && !defer;
+  if ((early & 2) && !dec_late) {
     // after the targets (pre: the caller's launch of them signals it; the
     // loss kernel above when dpre was not ready)
     if ((e = fk.fork_on(dpre_ready ? pre : nullptr)) != hipSuccess) return e;
@@ -1460,8 +1467,13 @@ hipError_t tune_bwd_h(const TunePlan& p, const float* P, float* Gd, float* ws, c
     t.part = ws + p.tfs[l][0];
     const int tk = 4 + 4 * (1 - l);
     g_tft.mark(tk, st);
-    if ((e = launch_tf(H, 2, t, st)) != hipSuccess) return e;
+    hipEvent_t ffn_end = (dec_late && l == 1 && !g_tft.on) ? fk.launch_event() : nullptr;
+    if ((e = launch_tf(H, 2, t, st, ffn_end)) != hipSuccess) return e;
     g_tft.mark(tk + 1, st);
+    if (dec_late && l == 1) {
+      if ((e = fk.fork_on(ffn_end)) != hipSuccess) return e;
+      if ((e = side_dec()) != hipSuccess) return e;
+    }
     {
       const long sl = tf_slab_floats(H, 2);
       const float* s0 = ws + p.tfs[l][0];

@@ -408,6 +408,11 @@ for step in "$@"; do
       run abdws16 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 16 --steps 100 --warmup 10 --no-cpu-baseline" s4= s1=PGP_LIB=$L/libpreganplus_dws1.so s2=PGP_LIB=$L/libpreganplus_dws2.so
       grep median $OUT/abdws50.out $OUT/abdws16.out
       ;;
+    abdeclate)  # the decoders' weight gradient forked after layer 1's FFN backward (variant declate) vs after the targets
+      L=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var
+      run abdl50 600 python3 -u tools/ab_bench.py --rounds 4 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" base= late=PGP_LIB=$L/libpreganplus_declate.so
+      grep median $OUT/abdl50.out
+      ;;
     gphase)
       PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_gprof.so run gphase 120 python3 -u tools/gobi_phases.py
       cat $OUT/gphase.out
