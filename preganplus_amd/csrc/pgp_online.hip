@@ -57,7 +57,7 @@ struct pgp_online {
   int cond_local[kMaxTensors] = {};  // transformer selection index -> cond flag
   CondRows cr{};
   long sec_lo[3] = {0, 0, 0};
-  hipEvent_t gate = nullptr, gan_done = nullptr, fwd_fork = nullptr, tgt_end = nullptr;
+  hipEvent_t gate = nullptr, gan_done = nullptr, tgt_end = nullptr;
   bool timing = false, timed = false;
   hipEvent_t tev[kNumEv] = {};
 };
@@ -251,7 +251,6 @@ int pgp_online_create(const pgp_online_desc* desc, pgp_online** out) {
   o->cr.n = ncond;
   if (hipEventCreateWithFlags(&o->gate, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&o->gan_done, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&o->fwd_fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&o->tgt_end, hipEventDisableTiming) != hipSuccess) {
     delete o;
     return ofail(PGP_ERR_HIP, "pgp_online_create: events");
@@ -264,7 +263,6 @@ int pgp_online_destroy(pgp_online* o) {
   if (!o) return PGP_OK;
   if (o->gate) (void)hipEventDestroy(o->gate);
   if (o->gan_done) (void)hipEventDestroy(o->gan_done);
-  if (o->fwd_fork) (void)hipEventDestroy(o->fwd_fork);
   if (o->tgt_end) (void)hipEventDestroy(o->tgt_end);
   for (auto& e : o->tev)
     if (e) (void)hipEventDestroy(e);
@@ -282,15 +280,13 @@ int pgp_online_step(pgp_online* o, void* main_stream, void* gan_stream, pgp_coll
   // 1. the dataset: R tuning windows per environment, then the E detect windows
   mark(o, kE0, sm);
   float* detect_win = d.windows + (long)B * 9 * H;
-  // (its end signals the forward's side-stream fork, when the forward forks)
-  hipEvent_t ff = (!o->timed && tune_side_active(o->fwd.M)) ? o->fwd_fork : nullptr;
-  OCHK(launch_tune_dataset(H, E, R, d.series, d.train_max, d.windows, d.y, d.cls, detect_win, sm, ff));
+  OCHK(launch_tune_dataset(H, E, R, d.series, d.train_max, d.windows, d.y, d.cls, detect_win, sm));
   mark(o, kE1, sm);
   // 2. ONE forward over the B + E windows (step-start weights)
   // its end (the stop event of its last launch) starts the GAN stream: the
   // GAN forward runs beside the targets
   hipEvent_t gate = (sg != sm && !o->timed) ? o->gate : nullptr;
-  OCHK(launch_tune_forward(o->fwd, d.windows, d.P, d.tune_ws, nullptr, d.logits, d.protos, sm, ff, gate));
+  OCHK(launch_tune_forward(o->fwd, d.windows, d.P, d.tune_ws, nullptr, d.logits, d.protos, sm, gate));
   mark(o, kE2, sm);
   // 3. main: bookkeeping against the step-start state (the decoders' input
   //    gradient dpre written by the same launch), issued before the GAN part so

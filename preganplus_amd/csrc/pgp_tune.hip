@@ -1306,11 +1306,10 @@ struct Fork {
 
 template <int H>
 hipError_t tune_fwd_h(const TunePlan& p, const float* win, const float* P, float* ws, float* latent, float* logits,
-                      float* protos, hipStream_t st, hipEvent_t pre, hipEvent_t post) {
+                      float* protos, hipStream_t st, hipEvent_t post) {
   using Q = TuneGeo<H>;
   const int B = p.B;
   hipError_t e;
-  // side: the decoder weights permuted for this step's forward and backward
   Fork fk(st, p.M);
   TfArgs t{};
   t.B = B;
@@ -1323,9 +1322,6 @@ hipError_t tune_fwd_h(const TunePlan& p, const float* win, const float* P, float
     TCK((tune_pack_kernel<H><<<nb_dec + 1 + nb_tf + (3 * B + 3) / 4, 256, 0, st>>>(
         P, ws + p.wp, ws + p.wpt, ws + p.mt, ws + p.tff, nb_dec, nb_tf, g)));
   } else {
-    if ((e = fk.fork_on(pre)) != hipSuccess) return e;
-    TCK((dec_pack_kernel<H><<<(int)((Q::NOP * Q::KD + 255) / 256), 256, 0, fk.side>>>(P, ws + p.wp, ws + p.wpt)));
-    TCK((gat_mt_kernel<H><<<1, 192, 0, fk.side>>>(P, ws + p.mt)));  // for the backward's GAT (gat_bwd_kernel)
     // main: the encoder's fragments packed from P and the GAT forward in ONE
     // launch (the packing kernel's tf blocks, then the GAT blocks)
     const int nb_tf = (int)((tf_frag_floats(H) + 255) / 256);
@@ -1341,8 +1337,20 @@ hipError_t tune_fwd_h(const TunePlan& p, const float* win, const float* P, float
     t.xh1 = ws + p.xh1[l];
     t.rs1 = ws + p.rs1[l];
     g_tft.mark(2 * l, st);
-    if ((e = launch_tf(H, 1, t, st)) != hipSuccess) return e;
+    // side: the decoder weights permuted for this step's decoder forward and
+    // backward, and the GAT's Mt for the backward, forked at the end of the
+    // layer-0 launch: beside layer 1's forward, not beside layer 0's (which
+    // also runs the time encoder / GAT input): C3 at H = 50 1.050 -> 1.043 ms
+    // (A/B, profiles/r05/pack_late/)
+    const bool pack_here = fk.side != st && l == 0;
+    hipEvent_t f0 = (pack_here && !g_tft.on) ? fk.launch_event() : nullptr;
+    if ((e = launch_tf(H, 1, t, st, f0)) != hipSuccess) return e;
     g_tft.mark(2 * l + 1, st);
+    if (pack_here) {
+      if ((e = fk.fork_on(f0)) != hipSuccess) return e;
+      TCK((dec_pack_kernel<H><<<(int)((Q::NOP * Q::KD + 255) / 256), 256, 0, fk.side>>>(P, ws + p.wp, ws + p.wpt)));
+      TCK((gat_mt_kernel<H><<<1, 192, 0, fk.side>>>(P, ws + p.mt)));  // for the backward's GAT (gat_bwd_kernel)
+    }
   }
   if ((e = fk.join()) != hipSuccess) return e;
   if ((e = launch_dec_fwd(H, B, p.dec_s, ws + p.x[2], ws + p.wp, ws + p.part, st)) != hipSuccess) return e;
@@ -1615,11 +1623,11 @@ bool tune_plan_prefix(int H, int B_fwd, int B, TunePlan* p) {
 }
 
 hipError_t launch_tune_forward(const TunePlan& p, const float* windows, const float* P, float* ws, float* latent,
-                               float* logits, float* protos, hipStream_t st, hipEvent_t pre, hipEvent_t post) {
+                               float* logits, float* protos, hipStream_t st, hipEvent_t post) {
   switch (p.H) {
 #define CASE(h) \
   case h:       \
-    return tune_fwd_h<h>(p, windows, P, ws, latent, logits, protos, st, pre, post);
+    return tune_fwd_h<h>(p, windows, P, ws, latent, logits, protos, st, post);
     PGP_FOR_EACH_H(CASE)
 #undef CASE
   }

@@ -74,13 +74,10 @@ int dec_fwd_splits(int H, int B);
 hipError_t launch_dec_fwd(int H, int B, int S, const float* X2, const float* Wp, float* part, hipStream_t st);
 hipError_t launch_dec_dx(int H, int B, const float* dpre, const float* WpT, float* dX, hipStream_t st);
 
-// pre: an event the caller's last launch on `st` signals at its end (the side
-// stream's decoder packing forks on it instead of an event recorded here);
 // post: signalled when the logits / prototypes are written (the forward's last
 // launch's stop event)
 hipError_t launch_tune_forward(const TunePlan& p, const float* windows, const float* P, float* ws, float* latent,
-                               float* logits, float* protos, hipStream_t st, hipEvent_t pre = nullptr,
-                               hipEvent_t post = nullptr);
+                               float* logits, float* protos, hipStream_t st, hipEvent_t post = nullptr);
 // dpre_ready: the decoder pre-activation gradient [B][NOP] at ws + p.dpre was
 // already written (launch_tune_targets_dp with dpre), so the loss kernel is
 // skipped; pre (with dpre_ready): an event the caller's last launch on `st`

@@ -413,6 +413,11 @@ for step in "$@"; do
       run abdl50 600 python3 -u tools/ab_bench.py --rounds 4 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" base= late=PGP_LIB=$L/libpreganplus_declate.so
       grep median $OUT/abdl50.out
       ;;
+    abpack)  # the decoder weight packing forked after the layer-0 forward (variant packlate) vs after the dataset
+      L=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var
+      run abpk50 600 python3 -u tools/ab_bench.py --rounds 4 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" base= late=PGP_LIB=$L/libpreganplus_packlate.so
+      grep median $OUT/abpk50.out
+      ;;
     gphase)
       PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_gprof.so run gphase 120 python3 -u tools/gobi_phases.py
       cat $OUT/gphase.out
