@@ -470,7 +470,7 @@ PGP_DEV void gat_fwd_block(int bx, int B, const float* __restrict__ win, const f
 // GAT backward from dX0, the gradient of the time encoder's output: the time
 // encoder X0 = G W_TE^T + b is linear, so the gradient of the aggregated raw
 // features x-bar_j = fc^T dG_j = fc^T W_TE^T dX0_j = Mt^T dX0_j with
-// Mt = W_TE fc ([64][3], gat_mt_kernel in the forward); no dG round trip.  This
+// Mt = W_TE fc ([64][3], formed by the forward's packing launch); no dG round trip.  This
 // kernel back-propagates into the edge softmax and writes, per workgroup (its
 // 4 (window, step) graphs summed in wave order), Xs = sum_i ds_i x_i and
 // Xt = sum_j dt_j x_j (ds, dt: grads of the per-node source / destination
@@ -641,19 +641,6 @@ __global__ __launch_bounds__(256) void dw_multi_kernel(DwMulti m, GatBwdArgs ga)
   }
 }
 
-// Mt[c][k] = sum_f W_TE[c][f] fc[f][k] (rows past H are 0): the time
-// encoder folded into the GAT backward's first contraction (gat_bwd_kernel).
-template <int H>
-__global__ __launch_bounds__(256) void gat_mt_kernel(const float* __restrict__ P, float* __restrict__ Mt) {
-  using G = TGeo<H>;
-  const int c = threadIdx.x / 3, k = threadIdx.x - 3 * c;
-  if (c >= 64) return;
-  float m = 0.f;
-  if (c < H)
-    for (int f = 0; f < H; ++f) m = fmaf(P[G::W_TE + c * H + f], P[G::W_FC + f * 3 + k], m);
-  Mt[threadIdx.x] = m;
-}
-
 // attn_fc and the score part of the fc gradient: s_i = a_1 . fc x_i, so
 // d a_1 = fc Xs, d fc += a_1 Xs^T (and likewise a_2, Xt), summed over the
 // gat_bwd workgroups in a fixed order; plus the aggregation part of the fc
@@ -752,7 +739,7 @@ __global__ __launch_bounds__(256) void dec_pack_kernel(const float* __restrict__
 
 // The step's per-step packing as ONE launch when it all runs on the caller's
 // stream (below the side-stream threshold, e.g. C3 at H = 16): blocks
-// [0, nb_dec) dec_pack_kernel's elements, then one block of gat_mt_kernel,
+// [0, nb_dec) dec_pack_kernel's elements (none with a side stream), then one block forming Mt,
 // then tf_pack_kernel's elements (pgp_tunef.hpp tf_pack_elem).  Each element is
 // computed as by its own kernel: the same bits.
 template <int H>
@@ -787,7 +774,8 @@ __global__ __launch_bounds__(256) void tune_pack_kernel(const float* __restrict_
     return;
   }
   bx -= nb_dec;
-  if (bx == 0) {  // (Mt == nullptr: formed elsewhere, gat_mt_kernel on the side stream)
+  if (bx == 0) {  // Mt[c][k] = sum_f W_TE[c][f] fc[f][k] (rows past H are 0): the time encoder
+                  // folded into the GAT backward's first contraction (gat_bwd_kernel)
     const int c = t / 3, k = t - 3 * c;
     if (c >= 64 || !Mt) return;
     float m = 0.f;
@@ -1326,7 +1314,9 @@ hipError_t tune_fwd_h(const TunePlan& p, const float* win, const float* P, float
     // launch (the packing kernel's tf blocks, then the GAT blocks)
     const int nb_tf = (int)((tf_frag_floats(H) + 255) / 256);
     const GatFwdIn g{B, win, ws + p.win, ws + p.g, ws + p.xb, ws + p.gs};
-    TCK((tune_pack_kernel<H><<<1 + nb_tf + (3 * B + 3) / 4, 256, 0, st>>>(P, nullptr, nullptr, nullptr, ws + p.tff, 0,
+    // (and the GAT's Mt for the backward: its block, not a side-stream
+    // launch the forward's join would wait for)
+    TCK((tune_pack_kernel<H><<<1 + nb_tf + (3 * B + 3) / 4, 256, 0, st>>>(P, nullptr, nullptr, ws + p.mt, ws + p.tff, 0,
                                                                            nb_tf, g)));
   }
   for (int l = 0; l < 2; ++l) {
@@ -1338,8 +1328,7 @@ hipError_t tune_fwd_h(const TunePlan& p, const float* win, const float* P, float
     t.rs1 = ws + p.rs1[l];
     g_tft.mark(2 * l, st);
     // side: the decoder weights permuted for this step's decoder forward and
-    // backward, and the GAT's Mt for the backward, forked at the end of the
-    // layer-0 launch: beside layer 1's forward, not beside layer 0's (which
+    // backward, forked at the end of the layer-0 launch: beside layer 1's forward, not beside layer 0's (which
     // also runs the time encoder / GAT input): C3 at H = 50 1.050 -> 1.043 ms
     // (A/B, profiles/r05/pack_late/)
     const bool pack_here = fk.side != st && l == 0;
@@ -1349,7 +1338,6 @@ hipError_t tune_fwd_h(const TunePlan& p, const float* win, const float* P, float
     if (pack_here) {
       if ((e = fk.fork_on(f0)) != hipSuccess) return e;
       TCK((dec_pack_kernel<H><<<(int)((Q::NOP * Q::KD + 255) / 256), 256, 0, fk.side>>>(P, ws + p.wp, ws + p.wpt)));
-      TCK((gat_mt_kernel<H><<<1, 192, 0, fk.side>>>(P, ws + p.mt)));  // for the backward's GAT (gat_bwd_kernel)
     }
   }
   if ((e = fk.join()) != hipSuccess) return e;

@@ -47,7 +47,7 @@ struct TunePlan {
   long da = 0, db = 0, dq[2] = {0, 0};                   // backward temporaries ([M][DP], [M][DP], 2 x [M][3][DP])
   long gsx = 0, dpre = 0, wp = 0, wpt = 0, part = 0, total = 0;  // wp: Wp [NOP][KD], wpt: WpT [T][DP][NOP]
   long fcd = 0;  // sum over tokens of dX0 (x) x-bar [H][3] (the fc gradient before W_TE, gat_param_kernel)
-  long mt = 0;   // W_TE fc [64][3] (gat_mt_kernel, read by gat_bwd_kernel)
+  long mt = 0;   // W_TE fc [64][3] (the forward's packing launch, read by gat_bwd_kernel)
   long tff = 0;                                          // fused-kernel weight fragments (pgp_tunef.hpp)
   long tfs[2][2] = {{0, 0}, {0, 0}};                     // [layer][ffn | attention] weight-gradient slabs
   long pool = 0, pool_len = 0;  // the backward's deferred-reduction regions (RedBatch)
