@@ -418,6 +418,11 @@ for step in "$@"; do
       run abpk50 600 python3 -u tools/ab_bench.py --rounds 4 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" base= late=PGP_LIB=$L/libpreganplus_packlate.so
       grep median $OUT/abpk50.out
       ;;
+    abearly2)  # the side-work mask after the round-5 moves: 7 (in-tree) vs 15 and 3
+      L=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var
+      run abe2 600 python3 -u tools/ab_bench.py --rounds 4 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" e7= e15=PGP_LIB=$L/libpreganplus_e15.so e3=PGP_LIB=$L/libpreganplus_e3.so
+      grep median $OUT/abe2.out
+      ;;
     gphase)
       PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_gprof.so run gphase 120 python3 -u tools/gobi_phases.py
       cat $OUT/gphase.out
