@@ -29,6 +29,9 @@
  *       recover_decision's container loop PreGANPlus.py:90-105 (PreGAN.py:80-95)
  *   pgp_embedding
  *       run_model's masked prototype embedding PreGANPlus.py:129
+ *   pgp_schedule_onehot
+ *       result_cache rows from GOBI's one-hot placement (opt.py:9-15), for
+ *       streamed fleet chunks
  *   pgp_create_fpe / pgp_forward_fpe
  *       PreGAN: PreGANRecovery.run_encoder + detect/embed/get_classes + the
  *       GAN gate, recovery/PreGAN.py:97-126 over FPE_16.forward models.py:65-115
@@ -152,6 +155,14 @@ int pgp_migrations(int n_hosts, int batch, const int* keep_orig, const int* fina
 /* run_model's embedding (PreGANPlus.py:129): emb[b,h,:] = protos[b,h,:] where
  * argmax(logits[b,h,:]) == 1 (ties -> 0), else 0.  fp32 device [B,H,2] each. */
 int pgp_embedding(int n_hosts, int batch, const float* logits, const float* protos, float* emb, void* stream);
+/* The dense schedule pgp_forward reads, from per-container host indices: a
+ * GOBI result_cache row is one-hot (scheduler/BaGTI/src/opt.py:9-15), so a
+ * streamed fleet chunk (bench.py --config fleet, preganplus_amd/fleet.py)
+ * carries one byte per container over PCIe instead of H floats.
+ *   in  idx   [B,C] uint8 host of container c; >= n_hosts: an all-zero row
+ *   out sched [B,C,H] fp32 device, sched[b,c,h] = (idx[b,c] == h)
+ * C = H; n_hosts <= 255. */
+int pgp_schedule_onehot(int n_hosts, int batch, const unsigned char* idx, float* sched, void* stream);
 
 /* ------------------------------------------------------------------------
  * PreGAN (FPE) variant — BASELINE config C4, SURVEY.md §8 a14.

@@ -18,6 +18,22 @@ _ERRS = {-1: "PGP_ERR_ARG", -2: "PGP_ERR_UNSUPPORTED", -3: "PGP_ERR_HIP", -4: "P
 
 _lib = None
 
+# A/B switches removed in round 5: the library and the
+# Python host read none of them any more.  Setting one warns instead of
+# silently measuring the default; PGP_INIT_SEED became the recoveries'
+# ``init_seed`` argument.
+REMOVED_ENV = ("PGP_TUNE_SIDE_STREAM", "PGP_TUNE_SIDE_MIN_TOKENS", "PGP_TUNE_DEC_DWS", "PGP_TUNE_SIDE_EARLY",
+               "PGP_TUNE_EARLY_FLUSH", "PGP_TF_SPREAD", "PGP_C3_GAN_LATE", "PGP_INIT_SEED", "PGP_SAVE_GAN_INTERVAL")
+
+
+def _warn_removed_env():
+    import warnings
+    for k in REMOVED_ENV:
+        if k in os.environ:
+            hint = " (use the init_seed argument)" if k == "PGP_INIT_SEED" else ""
+            warnings.warn(f"{k} is no longer read by preganplus_amd{hint}; it has no effect", RuntimeWarning,
+                          stacklevel=3)
+
 
 class NativeError(RuntimeError):
     pass
@@ -28,6 +44,7 @@ def lib():
     global _lib
     if _lib is not None:
         return _lib
+    _warn_removed_env()
     if not os.path.exists(LIB_PATH):
         raise ImportError(
             f"HIP library not found at {LIB_PATH}; build it with `make` "
@@ -69,6 +86,8 @@ def lib():
     L.pgp_migrations.restype = c_int
     L.pgp_embedding.argtypes = [c_int, c_int] + [fp] * 3 + [vp]
     L.pgp_embedding.restype = c_int
+    L.pgp_schedule_onehot.argtypes = [c_int, c_int, fp, fp, vp]
+    L.pgp_schedule_onehot.restype = c_int
     _lib = L
     return L
 

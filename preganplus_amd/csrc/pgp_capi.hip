@@ -297,6 +297,14 @@ int pgp_embedding(int n_hosts, int batch, const float* logits, const float* prot
   return PGP_OK;
 }
 
+int pgp_schedule_onehot(int n_hosts, int batch, const unsigned char* idx, float* sched, void* stream) {
+  if (n_hosts < 1 || n_hosts > 255 || batch < 0) return fail(PGP_ERR_ARG, "bad schedule_onehot arguments");
+  if (batch == 0) return PGP_OK;
+  if (!idx || !sched) return fail(PGP_ERR_ARG, "NULL input/output pointer");
+  HIPCHK(launch_onehot(n_hosts, (long)batch * n_hosts, idx, sched, reinterpret_cast<hipStream_t>(stream)));
+  return PGP_OK;
+}
+
 // ---------------------------------------------------------------------------
 // training ops
 // ---------------------------------------------------------------------------

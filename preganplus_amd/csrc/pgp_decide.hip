@@ -42,7 +42,23 @@ __global__ __launch_bounds__(256) void zero_kernel(long n, int* __restrict__ p) 
   if (i < n) p[i] = 0;
 }
 
+// one-hot schedule rows from per-container host indices: one lane per
+// output float, consecutive lanes consecutive floats of a row (coalesced)
+__global__ __launch_bounds__(256) void onehot_kernel(long n, int H, const unsigned char* __restrict__ idx,
+                                                     float* __restrict__ sched) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const long row = i / H;
+  sched[i] = (int)idx[row] == (int)(i - row * H) ? 1.f : 0.f;
+}
+
 }  // namespace
+
+hipError_t launch_onehot(int H, long rows, const unsigned char* idx, float* sched, hipStream_t st) {
+  const long n = rows * H;
+  if (n > 0) onehot_kernel<<<(int)((n + 255) / 256), 256, 0, st>>>(n, H, idx, sched);
+  return hipGetLastError();
+}
 
 hipError_t launch_decide(int B, int C, const int* keep, const int* target, const int* cur, int* moves,
                          int* hosts_from, hipStream_t st) {

@@ -77,6 +77,8 @@ hipError_t launch_decide(int B, int C, const int* keep, const int* target, const
                          int* hosts_from, hipStream_t st);
 // run_model's masked embedding over n (window, host) pairs (pgp_decide.hip)
 hipError_t launch_embed(long n, const float* logits, const float* protos, float* emb, hipStream_t st);
+// dense one-hot schedule rows [rows][H] from host indices (pgp_decide.hip)
+hipError_t launch_onehot(int H, long rows, const unsigned char* idx, float* sched, hipStream_t st);
 
 hipError_t launch_gat(const FwdArgs& a, hipStream_t st);
 hipError_t launch_encoder(const FwdArgs& a, hipStream_t st);
@@ -114,11 +116,7 @@ hipError_t launch_gan_probs(int H, int B, const float* ws, float* probs, hipStre
 hipError_t launch_simulate(int H, int E, const double* envs, const float* new_sched, const float* orig_sched,
                            double* out, float* target, hipStream_t st);
 
-#ifdef __HIP_DEVICE_COMPILE__
 #define PGP_DEV __device__ __forceinline__
-#else
-#define PGP_DEV __device__ __forceinline__
-#endif
 
 PGP_DEV f32x4 mfma(float a, float b, f32x4 c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
 // In-launch last-arriver finish (cdna_hip_programming.md, split-K recipe, the

@@ -1,19 +1,27 @@
 // pgp_fpe.hip — K4: PreGAN's FPE_16 encoder, decoders and diagnosis, one
-// window per lane (BASELINE config C4; reference recovery/PreGANSrc/src/models.py:10-115,
-// recovery/PreGAN.py:97-120).
+// window per lane, for H = 16 (shipped FPE_16) and H = 50 (the same reference
+// code at n_hosts = 50, BASELINE config C4; reference
+// recovery/PreGANSrc/src/models.py:10-115, recovery/PreGAN.py:97-120).
 //
-// Per window the whole model is ~10k multiply-adds over a 576-byte input: far too
-// little per window to amortise an MFMA tiling's operand shuffles, so each lane
-// owns one window and the folded weights (pgp_pack.cpp, FpeGeo) are read at
-// wave-uniform addresses (scalar loads, shared by the 64 windows of a wave).
+// Per window the work after the GAT is tiny once folded (pgp_pack.cpp,
+// FpeGeo): the GAT node mean has rank 3, so every MHA token is P u_w with
+// u_w = [GRU state; r-weighted raw features] (6 floats) and the MHA, V,
+// out_proj, encoder and both decoders collapse to a 6x6 score form and one
+// [4H x 18] affine map.  The GAT's graph-wise edge softmax is the only H^2
+// term; it stays on the VALU (an indicator-weighted sum, not a GEMM), one
+// window per lane, weights at wave-uniform addresses (scalar loads).
 //   GRU(3H -> 3), 3 steps, torch gate order (r, z, n), h0 supplied by the caller
 //   GAT node mean: r_i = sum_j softmax_ij over all H^2 edges; the edge term
-//     exp(lrelu(s_i + t_j) - m) factorises per branch into node exponentials,
-//     so a step costs 4H exp2 and H^2 compare/selects instead of H^2 exp
-//   MHA (1 head, E = 3 + H) as scores c_s^T M c_t + beta.c_t, softmax over t
-//   one [4H x 3E] matrix (V, out_proj, encoder, decoders folded) -> per host
-//   {a0, a1, p0, p1}: softmax / sigmoid, detect (argmax, ties -> 0), embed,
-//   nearest of K = 3 prototypes (utils.py get_classes), any-anomaly flag.
+//     exp(lrelu(s_i + t_j) - m) factorises per branch into node exponentials
+//     A_j = 2^(t_j - tmax), C_j = 2^(0.01 (t_j - tmax)):
+//       r_i = E1_i sum_{j: s_i + t_j > 0} A_j + E2_i (sum_j C_j - sum_{j: s_i + t_j > 0} C_j)
+//     so an edge costs one add with output clamp (the 0/1 branch indicator:
+//     2^64 (s_i + t_j) clamped to [0, 1]) and one packed FMA into {SA, SC}.
+//     r_i >= E2_i sum_j C_j, so the subtraction loses no relative accuracy.
+//   MHA (1 head) as scores u_s^T M6 u_t + beta6.u_t, softmax over t
+//   [4H x 18] map -> per host {a0, a1, p0, p1}: softmax / sigmoid, detect
+//   (argmax, ties -> 0), embed, nearest of K = 3 prototypes (utils.py
+//   get_classes), any-anomaly flag.
 // The embedding goes to the workspace row K3 (pgp_gan.hip) reads.
 #include "pgp_device.hpp"
 
@@ -21,148 +29,180 @@ namespace pgp {
 namespace {
 
 constexpr int kFpeThreads = 64;
+// 2^64: (s + t) * 2^64 >= 1 for every positive sum the scores produce (|s|,
+// |t| < 2^60); a positive sum below 2^-64 gets a fraction, i.e. a convex
+// combination of two edge values that agree to ~2^-64 there
+constexpr float kBig = 18446744073709551616.0f;
 
 PGP_DEV float sigm(float x) { return 1.0f / (1.0f + __expf(-x)); }
 
 template <int H>
 __global__ __launch_bounds__(kFpeThreads) void fpe_kernel(FpeArgs a) {
   using F = FpeGeo<H>;
-  constexpr int E = F::E, NIN = F::NIN;
+  constexpr int NIN = F::NIN;
   const float* __restrict__ T = a.tab;
   const long b = (long)blockIdx.x * kFpeThreads + threadIdx.x;
   if (b >= a.B) return;
-  const float* __restrict__ xw = a.windows + b * 3 * NIN;
+  const float* __restrict__ xb = a.windows + b * 3 * NIN;
 
   float hs[3];
 #pragma unroll
   for (int k = 0; k < 3; ++k) hs[k] = a.h0[b * 3 + k];
-  float c[3][E];
+  float u[3][6] = {};  // per step: GRU state after the step, r-weighted raw features
 
-#pragma unroll
   for (int w = 0; w < 3; ++w) {
-    float x[NIN];
+    const float* __restrict__ xw = xb + w * NIN;
+    // ---- pass 1: GRU input product, node scores s / t (log2e-scaled) ----
+    float gi[9];
 #pragma unroll
-    for (int q = 0; q < NIN / 4; ++q) {
-      const f32x4 v = ld4(xw + w * NIN + 4 * q);
-      x[4 * q] = v[0];
-      x[4 * q + 1] = v[1];
-      x[4 * q + 2] = v[2];
-      x[4 * q + 3] = v[3];
-    }
-    // ---- GRU cell (torch.nn.GRU, gates r, z, n) ----
-    float gi[9], gh[9];
-#pragma unroll
-    for (int i = 0; i < 9; ++i) {
-      float acc = 0.f;
-#pragma unroll
-      for (int k = 0; k < NIN; ++k) acc = fmaf(T[F::F_WIH + i * NIN + k], x[k], acc);
-      gi[i] = acc;
-      gh[i] = fmaf(T[F::F_WHH + 3 * i], hs[0], fmaf(T[F::F_WHH + 3 * i + 1], hs[1], T[F::F_WHH + 3 * i + 2] * hs[2]));
-    }
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      const float r = sigm(gi[k] + gh[k] + T[F::F_BRZ + k]);
-      const float z = sigm(gi[3 + k] + gh[3 + k] + T[F::F_BRZ + 3 + k]);
-      const float n = tanhf(gi[6 + k] + T[F::F_BIN + k] + r * (gh[6 + k] + T[F::F_BHN + k]));
-      hs[k] = (1.f - z) * n + z * hs[k];
-    }
-    // ---- GAT, mean over nodes (log2e-scaled scores) ----
-    float s[H], t[H];
+    for (int i = 0; i < 9; ++i) gi[i] = 0.f;
+    float t[H];
     float smax = -INFINITY, tmax = -INFINITY;
 #pragma unroll
     for (int i = 0; i < H; ++i) {
-      s[i] = fmaf(T[F::F_UV], x[3 * i], fmaf(T[F::F_UV + 1], x[3 * i + 1], T[F::F_UV + 2] * x[3 * i + 2]));
-      t[i] = fmaf(T[F::F_UV + 4], x[3 * i], fmaf(T[F::F_UV + 5], x[3 * i + 1], T[F::F_UV + 6] * x[3 * i + 2]));
-      smax = fmaxf(smax, s[i]);
+      const float x0 = xw[3 * i], x1 = xw[3 * i + 1], x2 = xw[3 * i + 2];
+#pragma unroll
+      for (int g = 0; g < 9; ++g)
+        gi[g] = fmaf(T[F::F_WIH + g * NIN + 3 * i + 2], x2,
+                     fmaf(T[F::F_WIH + g * NIN + 3 * i + 1], x1, fmaf(T[F::F_WIH + g * NIN + 3 * i], x0, gi[g])));
+      const float s = fmaf(T[F::F_UV], x0, fmaf(T[F::F_UV + 1], x1, T[F::F_UV + 2] * x2));
+      t[i] = fmaf(T[F::F_UV + 4], x0, fmaf(T[F::F_UV + 5], x1, T[F::F_UV + 6] * x2));
+      smax = fmaxf(smax, s);
       tmax = fmaxf(tmax, t[i]);
     }
+    // ---- GRU cell (torch.nn.GRU, gates r, z, n) ----
+    {
+      float gh[9];
+#pragma unroll
+      for (int i = 0; i < 9; ++i)
+        gh[i] = fmaf(T[F::F_WHH + 3 * i], hs[0], fmaf(T[F::F_WHH + 3 * i + 1], hs[1], T[F::F_WHH + 3 * i + 2] * hs[2]));
+      float hn[3];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const float r = sigm(gi[k] + gh[k] + T[F::F_BRZ + k]);
+        const float z = sigm(gi[3 + k] + gh[3 + k] + T[F::F_BRZ + 3 + k]);
+        const float n = tanhf(gi[6 + k] + T[F::F_BIN + k] + r * (gh[6 + k] + T[F::F_BHN + k]));
+        hn[k] = (1.f - z) * n + z * hs[k];
+      }
+#pragma unroll
+      for (int k = 0; k < 3; ++k) hs[k] = hn[k];
+    }
+    // ---- GAT, mean over nodes ----
     const float mraw = smax + tmax;
     const float m = fmaxf(mraw, 0.01f * mraw);  // max over edges of lrelu(s_i + t_j)
     const float k1 = __builtin_amdgcn_exp2f(mraw - m);
     const float k2 = __builtin_amdgcn_exp2f(0.01f * mraw - m);
-    float A[H], C[H];
+    f32x2 ac[H];
+    float ctot = 0.f;
 #pragma unroll
     for (int j = 0; j < H; ++j) {
-      A[j] = __builtin_amdgcn_exp2f(t[j] - tmax);
-      C[j] = __builtin_amdgcn_exp2f(0.01f * (t[j] - tmax));
+      ac[j] = f32x2{__builtin_amdgcn_exp2f(t[j] - tmax), __builtin_amdgcn_exp2f(0.01f * (t[j] - tmax))};
+      ctot += ac[j][1];
+      t[j] *= kBig;
     }
     float Z = 0.f, g0 = 0.f, g1 = 0.f, g2 = 0.f;
+    const float us0 = T[F::F_UV], us1 = T[F::F_UV + 1], us2 = T[F::F_UV + 2];
+    // two source nodes per trip: their feature loads (L1/L2 hits; with one
+    // window per lane no other wave on the SIMD hides them) share one wait
+    static_assert(H % 2 == 0, "node pairs");
+#pragma unroll 1
+    for (int i = 0; i < H; i += 2) {
+      float xs[2][3], sv[2];
+      f32x2 pa[2], pb[2];
 #pragma unroll
-    for (int i = 0; i < H; ++i) {
-      float sa = 0.f, scn = 0.f;
-      const float ns = -s[i];
-#pragma unroll
-      for (int j = 0; j < H; ++j) {
-        const bool pos = t[j] > ns;
-        sa += pos ? A[j] : 0.f;
-        scn += pos ? 0.f : C[j];
+      for (int q = 0; q < 2; ++q) {
+        xs[q][0] = xw[3 * (i + q)];
+        xs[q][1] = xw[3 * (i + q) + 1];
+        xs[q][2] = xw[3 * (i + q) + 2];
       }
-      const float r = __builtin_amdgcn_exp2f(s[i] - smax) * k1 * sa +
-                      __builtin_amdgcn_exp2f(0.01f * (s[i] - smax)) * k2 * scn;
-      Z += r;
-      g0 = fmaf(r, x[3 * i], g0);
-      g1 = fmaf(r, x[3 * i + 1], g1);
-      g2 = fmaf(r, x[3 * i + 2], g2);
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        sv[q] = fmaf(us0, xs[q][0], fmaf(us1, xs[q][1], us2 * xs[q][2]));
+        pa[q] = f32x2{0.f, 0.f};
+        pb[q] = f32x2{0.f, 0.f};
+      }
+#pragma unroll
+      for (int j = 0; j < H; j += 2) {
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const float m0 = __builtin_amdgcn_fmed3f(sv[q] * kBig + t[j], 0.f, 1.f);
+          pa[q] = __builtin_elementwise_fma(f32x2{m0, m0}, ac[j], pa[q]);
+          const float m1 = __builtin_amdgcn_fmed3f(sv[q] * kBig + t[j + 1], 0.f, 1.f);
+          pb[q] = __builtin_elementwise_fma(f32x2{m1, m1}, ac[j + 1], pb[q]);
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const f32x2 p = pa[q] + pb[q];
+        const float s = sv[q];
+        const float r = __builtin_amdgcn_exp2f(s - smax) * k1 * p[0] +
+                        __builtin_amdgcn_exp2f(0.01f * (s - smax)) * k2 * (ctot - p[1]);
+        Z += r;
+        g0 = fmaf(r, xs[q][0], g0);
+        g1 = fmaf(r, xs[q][1], g1);
+        g2 = fmaf(r, xs[q][2], g2);
+      }
     }
     const float iz = 1.0f / Z;
-    g0 *= iz;
-    g1 *= iz;
-    g2 *= iz;
-    c[w][0] = hs[0];
-    c[w][1] = hs[1];
-    c[w][2] = hs[2];
+    // shift register over the steps (static indices)
 #pragma unroll
-    for (int dd = 0; dd < H; ++dd)
-      c[w][3 + dd] = fmaf(T[F::F_FC + 3 * dd], g0, fmaf(T[F::F_FC + 3 * dd + 1], g1, T[F::F_FC + 3 * dd + 2] * g2));
+    for (int k = 0; k < 6; ++k) {
+      u[0][k] = u[1][k];
+      u[1][k] = u[2][k];
+    }
+    u[2][0] = hs[0];
+    u[2][1] = hs[1];
+    u[2][2] = hs[2];
+    u[2][3] = g0 * iz;
+    u[2][4] = g1 * iz;
+    u[2][5] = g2 * iz;
   }
 
-  // ---- single-head attention over the 3 steps ----
-  float sc[3][3];
+  // ---- single-head attention over the 3 steps, in u-space ----
+  float ub[3][6];
   {
-    float mt[3][E], bt[3];
+    float mt[3][6], bt[3];
 #pragma unroll
     for (int tt = 0; tt < 3; ++tt) {
       float bb = 0.f;
 #pragma unroll
-      for (int e = 0; e < E; ++e) {
+      for (int e = 0; e < 6; ++e) {
         float acc = 0.f;
 #pragma unroll
-        for (int f = 0; f < E; ++f) acc = fmaf(T[F::F_M + e * E + f], c[tt][f], acc);
+        for (int f = 0; f < 6; ++f) acc = fmaf(T[F::F_M6 + e * 6 + f], u[tt][f], acc);
         mt[tt][e] = acc;
-        bb = fmaf(T[F::F_BETA + e], c[tt][e], bb);
+        bb = fmaf(T[F::F_BETA6 + e], u[tt][e], bb);
       }
       bt[tt] = bb;
     }
 #pragma unroll
-    for (int ss = 0; ss < 3; ++ss)
+    for (int ss = 0; ss < 3; ++ss) {
+      float sc[3];
 #pragma unroll
       for (int tt = 0; tt < 3; ++tt) {
         float acc = bt[tt];
 #pragma unroll
-        for (int e = 0; e < E; ++e) acc = fmaf(c[ss][e], mt[tt][e], acc);
-        sc[ss][tt] = acc;
+        for (int e = 0; e < 6; ++e) acc = fmaf(u[ss][e], mt[tt][e], acc);
+        sc[tt] = acc;
       }
-  }
-  float ch[3][E];
+      const float mx = fmaxf(sc[0], fmaxf(sc[1], sc[2]));
+      float p[3], ps = 0.f;
 #pragma unroll
-  for (int ss = 0; ss < 3; ++ss) {
-    const float mx = fmaxf(sc[ss][0], fmaxf(sc[ss][1], sc[ss][2]));
-    float p[3], ps = 0.f;
+      for (int tt = 0; tt < 3; ++tt) {
+        p[tt] = __builtin_amdgcn_exp2f(sc[tt] - mx);
+        ps += p[tt];
+      }
+      const float ip = 1.0f / ps;
 #pragma unroll
-    for (int tt = 0; tt < 3; ++tt) {
-      p[tt] = __builtin_amdgcn_exp2f(sc[ss][tt] - mx);
-      ps += p[tt];
+      for (int e = 0; e < 6; ++e) ub[ss][e] = (p[0] * u[0][e] + p[1] * u[1][e] + p[2] * u[2][e]) * ip;
     }
-    const float ip = 1.0f / ps;
-#pragma unroll
-    for (int e = 0; e < E; ++e) ch[ss][e] = (p[0] * c[0][e] + p[1] * c[1][e] + p[2] * c[2][e]) * ip;
   }
 
   // ---- folded encoder + decoders, softmax / sigmoid, detect, diagnose ----
   const float* P = T + F::F_PROTO;
   int anyf = 0;
   float* emb = a.emb + b * Geo<H>::EP;
-#pragma unroll
+#pragma unroll 2
   for (int h = 0; h < H; ++h) {
     float o[4];
 #pragma unroll
@@ -172,7 +212,7 @@ __global__ __launch_bounds__(kFpeThreads) void fpe_kernel(FpeArgs a) {
 #pragma unroll
       for (int ss = 0; ss < 3; ++ss)
 #pragma unroll
-        for (int e = 0; e < E; ++e) acc = fmaf(T[F::F_W2 + n * F::KC + ss * E + e], ch[ss][e], acc);
+        for (int e = 0; e < 6; ++e) acc = fmaf(T[F::F_W6 + n * F::KU + ss * 6 + e], ub[ss][e], acc);
       o[q] = acc;
     }
     const float mx = fmaxf(o[0], o[1]);

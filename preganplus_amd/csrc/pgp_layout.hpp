@@ -196,9 +196,11 @@ struct Geo {
 };
 
 // PreGAN's FPE_16 encoder (models.py:10-115), folded table of K4 (pgp_fpe.hip).
-// Only H = 16 is instantiated: the reference defines FPE_16 alone
-// (FPE_50 is not constructible there).
-#define PGP_FOR_EACH_FPE_H(X) X(16)
+// FPE_16's encode/forward are host-count generic (every shape comes from
+// n_hosts); H = 50 is that code at n_hosts = 50 (tests/golden/make_golden_fpe50.py),
+// an extrapolation of the FPE_16 architecture: the reference's own FPE_50
+// (models.py:156-210) raises in its GAT call (dlutils.py:306).
+#define PGP_FOR_EACH_FPE_H(X) X(16) X(50)
 template <int H>
 struct FpeGeo {
   static constexpr int W = 3;          // window rows = GRU steps = GRU state size
@@ -207,17 +209,22 @@ struct FpeGeo {
   static constexpr int KC = W * E;     // flattened attention output (encoder input)
   static constexpr int NO = 4 * H;     // outputs per window: per host {a0, a1, p0, p1}
   static constexpr int K = 3;          // prototypes (models.py:62)
+  // The GAT node mean is Wfc (sum_i r_i x_i) / (H Z): rank 3.  So each MHA
+  // token c_w = P u_w with u_w = [GRU state (3); node-weighted raw features
+  // g_w (3)] and P = blockdiag(I3, Wfc / H): every map after the GAT acts on
+  // the 6-vector u_w (pgp_pack.cpp pack_fpe_t).
+  static constexpr int U = 6;
+  static constexpr int KU = W * U;     // 18: the attention output in u-space
   static constexpr int F_WIH = 0;                                 // [9][NIN] GRU input weights (r,z,n)
   static constexpr int F_WHH = F_WIH + round_up(9 * NIN, 4);      // [9][3]
   static constexpr int F_BRZ = F_WHH + round_up(27, 4);           // [6] b_ih + b_hh for r, z
   static constexpr int F_BIN = F_BRZ + 8;                         // [3] b_ih of n
   static constexpr int F_BHN = F_BIN + 4;                         // [3] b_hh of n
   static constexpr int F_UV = F_BHN + 4;                          // u[3] (+pad), v[3] (+pad), log2e-scaled
-  static constexpr int F_FC = F_UV + 8;                           // [H][3] GAT fc / H (node mean)
-  static constexpr int F_M = F_FC + round_up(3 * H, 4);           // [E][E] log2e Wq^T Wk / sqrt(E)
-  static constexpr int F_BETA = F_M + round_up(E * E, 4);         // [E]    log2e Wk^T bq / sqrt(E)
-  static constexpr int F_W2 = F_BETA + round_up(E, 4);            // [NO][KC] Dec . Wenc . Wout . Wv
-  static constexpr int F_B2 = F_W2 + round_up(NO * KC, 4);        // [NO]
+  static constexpr int F_M6 = F_UV + 8;                           // [6][6] log2e P^T Wq^T Wk P / sqrt(E)
+  static constexpr int F_BETA6 = F_M6 + 36;                       // [6]    log2e P^T Wk^T bq / sqrt(E)
+  static constexpr int F_W6 = F_BETA6 + 8;                        // [NO][KU] Dec . Wenc . (Wout Wv P)_s
+  static constexpr int F_B2 = F_W6 + round_up(NO * KU, 4);        // [NO]
   static constexpr int F_PROTO = F_B2 + round_up(NO, 4);          // [K][2]
   static constexpr int F_SIZE = F_PROTO + round_up(2 * K, 4);
   static constexpr size_t blob_len() {

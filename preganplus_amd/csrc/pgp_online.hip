@@ -54,6 +54,7 @@ struct pgp_online {
   TunePlan fwd{}, bwd{};
   AdamArgs adam[3]{};
   double step[3][kMaxTensors] = {};  // host step counts (the prototype decoder's live on the device)
+  bool pending[3] = {false, false, false};  // scalars of step + 1 issued; counted once the step is issued
   int cond_local[kMaxTensors] = {};  // transformer selection index -> cond flag
   CondRows cr{};
   long sec_lo[3] = {0, 0, 0};
@@ -81,18 +82,44 @@ int ofail(int code, const std::string& msg) {
     if (r_ != PGP_OK) return r_; \
   } while (0)
 
-// the next step's AdamW scalars of a section's always-active tensors
+// the next step's AdamW scalars of a section's always-active tensors (step + 1);
+// the counts themselves advance in commit_steps, once the whole step is issued
 void next_scalars(pgp_online* o, int sec) {
   AdamArgs& a = o->adam[sec];
   const double lr = o->d.lr[sec], b1 = o->d.beta1, b2 = o->d.beta2;
   for (int i = 0; i < a.ntensors; ++i) {
     if (a.t[i].active & kAdamFromTable) continue;
-    o->step[sec][i] += 1.0;
-    const double st = o->step[sec][i] > 1.0 ? o->step[sec][i] : 1.0;
+    const double nx = o->step[sec][i] + 1.0;
+    const double st = nx > 1.0 ? nx : 1.0;
     a.t[i].step_size = (float)(lr / (1.0 - std::pow(b1, st)));
     a.t[i].bc2_sqrt = (float)std::sqrt(1.0 - std::pow(b2, st));
   }
+  o->pending[sec] = true;
 }
+
+void commit_steps(pgp_online* o) {
+  for (int sec = 0; sec < 3; ++sec) {
+    if (!o->pending[sec]) continue;
+    const AdamArgs& a = o->adam[sec];
+    for (int i = 0; i < a.ntensors; ++i)
+      if (!(a.t[i].active & kAdamFromTable)) o->step[sec][i] += 1.0;
+    o->pending[sec] = false;
+  }
+}
+
+// After the GAN stream forks off the main stream, every exit joins it back:
+// on an error path the main stream still waits for the GAN work already queued
+// (the caller's next use of the weights must not race it).
+struct GanJoin {
+  pgp_online* o;
+  hipStream_t sm, sg;
+  bool armed = false;
+  ~GanJoin() {
+    if (!armed) return;
+    (void)hipEventRecord(o->gan_done, sg);
+    (void)hipStreamWaitEvent(sm, o->gan_done, 0);
+  }
+};
 
 void mark(pgp_online* o, int k, hipStream_t s) {
   if (o->timing) (void)hipEventRecord(o->tev[k], s);
@@ -277,6 +304,7 @@ int pgp_online_step(pgp_online* o, void* main_stream, void* gan_stream, pgp_coll
   const hipStream_t sm = reinterpret_cast<hipStream_t>(main_stream);
   const hipStream_t sg = gan_stream ? reinterpret_cast<hipStream_t>(gan_stream) : sm;
   o->timed = o->timing;
+  o->pending[0] = o->pending[1] = o->pending[2] = false;
   // 1. the dataset: R tuning windows per environment, then the E detect windows
   mark(o, kE0, sm);
   float* detect_win = d.windows + (long)B * 9 * H;
@@ -303,9 +331,11 @@ int pgp_online_step(pgp_online* o, void* main_stream, void* gan_stream, pgp_coll
   mark(o, kE3, sm);
   // 4. the GAN stream, from the forward's end: Gen + Disc forward (the
   //    embedding formed inside), the simulated label, the Disc gradient
+  GanJoin join{o, sm, sg};
   if (sg != sm) {
     if (!gate) OCHK(hipEventRecord(o->gate, sm));
     OCHK(hipStreamWaitEvent(sg, o->gate, 0));
+    join.armed = true;
   }
   mark(o, kG0, sg);
   mark(o, kG1, sg);
@@ -329,9 +359,11 @@ int pgp_online_step(pgp_online* o, void* main_stream, void* gan_stream, pgp_coll
   OCHK(launch_adamw(o->adam[kTr], sm));
   mark(o, kE6, sm);
   if (sg != sm) {
+    join.armed = false;
     OCHK(hipEventRecord(o->gan_done, sg));
     OCHK(hipStreamWaitEvent(sm, o->gan_done, 0));
   }
+  commit_steps(o);
   (void)R;
   return PGP_OK;
 }
@@ -357,8 +389,11 @@ int pgp_online_stage_ms(pgp_online* o, float* ms) {
 int pgp_online_gan_step(pgp_online* o, void* stream) {
   if (!o) return ofail(PGP_ERR_ARG, "pgp_online_gan_step: NULL handle");
   const hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  o->pending[0] = o->pending[1] = o->pending[2] = false;
   OCALL(gan_part_a(o, s, true));
-  return gan_part_b(o, s, true, nullptr, nullptr);
+  OCALL(gan_part_b(o, s, true, nullptr, nullptr));
+  commit_steps(o);
+  return PGP_OK;
 }
 
 int pgp_online_steps(const pgp_online* o, double* steps, int n) {

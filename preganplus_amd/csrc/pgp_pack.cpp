@@ -80,14 +80,17 @@ std::string pack_t(int K, const double* blob, size_t len, Packed* P) {
 
 // ---------------------------------------------------------------------------
 // PreGAN FPE_16 variant (models.py:10-115).  Folds, all in fp64:
-//   GAT node mean: mean_j sum_i a_ij Wfc x_i = (Wfc / H) sum_i r_i x_i, r_i = sum_j a_ij
+//   GAT node mean: mean_j sum_i a_ij Wfc x_i = (Wfc / H) sum_i r_i x_i, r_i = sum_j a_ij,
+//     so each MHA token is c_w = P u_w, u_w = [h_w; g_w] (GRU state, r-weighted
+//     raw features / Z), P = blockdiag(I3, Wfc / H) [E x 6]
 //   edge scores as above (u, v), pre-scaled by log2(e)
 //   MHA scores: q_s.k_t = c_s^T (Wq^T Wk) c_t + (Wk^T bq).c_t + (terms constant in t,
-//     which cancel in the softmax over t); 1/sqrt(E) and log2(e) folded in
+//     which cancel in the softmax over t) = u_s^T M6 u_t + beta6.u_t with
+//     M6 = P^T Wq^T Wk P, beta6 = P^T Wk^T bq; 1/sqrt(E) and log2(e) folded in
 //   V, out_proj, encoder Linear (identity LeakyReLU(True)) and both decoders are
 //     affine maps applied after a convex combination (sum_t p_st = 1), so
-//     [a0 a1 p0 p1]_host = W2 . [sum_t p_st c_t]_s + b2 with
-//     W2 = Dec . Wenc . blockdiag_s(Wout Wv), b2 = Dec (Wenc (Wout bv + bout)_s + benc) + bdec
+//     [a0 a1 p0 p1]_host = W6 . [sum_t p_st u_t]_s + b2 with
+//     W6 = Dec . Wenc . blockdiag_s(Wout Wv P), b2 = Dec (Wenc (Wout bv + bout)_s + benc) + bdec
 // ---------------------------------------------------------------------------
 template <int H>
 std::string pack_fpe_t(const double* blob, size_t len, Packed* P) {
@@ -147,44 +150,76 @@ std::string pack_fpe_t(const double* blob, size_t len, Packed* P) {
     T[FG::F_UV + f] = (float)(u * log2e);
     T[FG::F_UV + 4 + f] = (float)(v * log2e);
   }
-  for (int i = 0; i < 3 * d; ++i) T[FG::F_FC + i] = (float)(fcW[i] / d);
+  // P [E][6]: rows 0-2 the identity on the GRU state, rows 3.. Wfc / H
+  std::vector<double> Pm((size_t)E * 6, 0.0);
+  for (int k = 0; k < 3; ++k) Pm[(size_t)k * 6 + k] = 1.0;
+  for (int dd = 0; dd < d; ++dd)
+    for (int f = 0; f < 3; ++f) Pm[(size_t)(3 + dd) * 6 + 3 + f] = fcW[dd * 3 + f] / d;
   const double* Wq = inW;
   const double* Wk = inW + E * E;
   const double* Wv = inW + 2 * E * E;
   const double* bq = inB;
   const double* bv = inB + 2 * E;
   const double sc = log2e / std::sqrt((double)E);
+  std::vector<double> M((size_t)E * E), beta(E);  // Wq^T Wk, Wk^T bq
   for (int a = 0; a < E; ++a) {
     for (int b = 0; b < E; ++b) {
       double m = 0;
       for (int e = 0; e < E; ++e) m += Wq[e * E + a] * Wk[e * E + b];
-      T[FG::F_M + a * E + b] = (float)(m * sc);
+      M[(size_t)a * E + b] = m;
     }
-    double beta = 0;
-    for (int e = 0; e < E; ++e) beta += Wk[e * E + a] * bq[e];
-    T[FG::F_BETA + a] = (float)(beta * sc);
+    double bb = 0;
+    for (int e = 0; e < E; ++e) bb += Wk[e * E + a] * bq[e];
+    beta[a] = bb;
   }
-  std::vector<double> A((size_t)E * E), a0(E);  // A = Wout Wv, a0 = Wout bv + bout
-  for (int f = 0; f < E; ++f) {
-    double acc0 = outB[f];
-    for (int g = 0; g < E; ++g) acc0 += outW[f * E + g] * bv[g];
-    a0[f] = acc0;
-    for (int e = 0; e < E; ++e) {
+  std::vector<double> MP((size_t)E * 6, 0.0);  // M P
+  for (int a = 0; a < E; ++a)
+    for (int k = 0; k < 6; ++k) {
       double acc = 0;
-      for (int g = 0; g < E; ++g) acc += outW[f * E + g] * Wv[g * E + e];
-      A[(size_t)f * E + e] = acc;
+      for (int b = 0; b < E; ++b) acc += M[(size_t)a * E + b] * Pm[(size_t)b * 6 + k];
+      MP[(size_t)a * 6 + k] = acc;
     }
+  for (int j = 0; j < 6; ++j) {
+    for (int k = 0; k < 6; ++k) {
+      double acc = 0;
+      for (int a = 0; a < E; ++a) acc += Pm[(size_t)a * 6 + j] * MP[(size_t)a * 6 + k];
+      T[FG::F_M6 + j * 6 + k] = (float)(acc * sc);
+    }
+    double bb = 0;
+    for (int a = 0; a < E; ++a) bb += Pm[(size_t)a * 6 + j] * beta[a];
+    T[FG::F_BETA6 + j] = (float)(bb * sc);
   }
-  // encoder rows composed with A:  WA[row][s*E+e] = sum_f Wenc[row][s*E+f] A[f][e]
-  std::vector<double> WA((size_t)L * d * KC), bA((size_t)L * d);
+  std::vector<double> A((size_t)E * 6), a0(E);  // A = Wout Wv P, a0 = Wout bv + bout
+  {
+    std::vector<double> OV((size_t)E * E);
+    for (int f = 0; f < E; ++f) {
+      double acc0 = outB[f];
+      for (int g = 0; g < E; ++g) acc0 += outW[f * E + g] * bv[g];
+      a0[f] = acc0;
+      for (int e = 0; e < E; ++e) {
+        double acc = 0;
+        for (int g = 0; g < E; ++g) acc += outW[f * E + g] * Wv[g * E + e];
+        OV[(size_t)f * E + e] = acc;
+      }
+    }
+    for (int f = 0; f < E; ++f)
+      for (int k = 0; k < 6; ++k) {
+        double acc = 0;
+        for (int e = 0; e < E; ++e) acc += OV[(size_t)f * E + e] * Pm[(size_t)e * 6 + k];
+        A[(size_t)f * 6 + k] = acc;
+      }
+  }
+  // encoder rows composed with A:  WA[row][s*6+k] = sum_f Wenc[row][s*E+f] A[f][k]
+  const int KU = FG::KU;
+  std::vector<double> WA((size_t)L * d * KU), bA((size_t)L * d);
   for (int row = 0; row < L * d; ++row) {
     double bb = encB[row];
     for (int s = 0; s < 3; ++s) {
       for (int f = 0; f < E; ++f) bb += encW[(size_t)row * KC + s * E + f] * a0[f];
-      for (int e = 0; e < E; ++e) {
+      for (int k = 0; k < 6; ++k) {
         double acc = 0;
-        for (int f = 0; f < E; ++f) acc += encW[(size_t)row * KC + s * E + f] * A[(size_t)f * E + e];
-        WA[(size_t)row * KC + s * E + e] = acc;
+        for (int f = 0; f < E; ++f) acc += encW[(size_t)row * KC + s * E + f] * A[(size_t)f * 6 + k];
+        WA[(size_t)row * KU + s * 6 + k] = acc;
       }
     }
     bA[row] = bb;
@@ -195,10 +230,10 @@ std::string pack_fpe_t(const double* blob, size_t len, Packed* P) {
       double bb = q < 2 ? anB[q] : prB[q - 2];
       for (int l = 0; l < L; ++l) bb += dw[l] * bA[h * L + l];
       T[FG::F_B2 + 4 * h + q] = (float)bb;
-      for (int k = 0; k < KC; ++k) {
+      for (int k = 0; k < KU; ++k) {
         double acc = 0;
-        for (int l = 0; l < L; ++l) acc += dw[l] * WA[(size_t)(h * L + l) * KC + k];
-        T[FG::F_W2 + (4 * h + q) * KC + k] = (float)acc;
+        for (int l = 0; l < L; ++l) acc += dw[l] * WA[(size_t)(h * L + l) * KU + k];
+        T[FG::F_W6 + (4 * h + q) * KU + k] = (float)acc;
       }
     }
   for (int k = 0; k < 2 * FG::K; ++k) T[FG::F_PROTO + k] = (float)protos[k];

@@ -32,6 +32,10 @@ constexpr long kTuneCounters = 1024;
 // counters [0, 2 * 3H): the decoder weight gradient's per-(token, half) parts;
 // kCtrGatTail: the GAT parameter tail of the fused reduction
 constexpr int kCtrGatTail = 1000;
+static_assert(kCtrGatTail < kTuneCounters, "GAT tail counter inside the counter head");
+#define PGP_CTR_FITS(h) static_assert(2 * 3 * (h) <= kCtrGatTail, "decoder dW counters reach kCtrGatTail");
+PGP_FOR_EACH_H(PGP_CTR_FITS)
+#undef PGP_CTR_FITS
 constexpr int kMaxDecDws = 4;  // decoder weight-gradient parts (windows split over up to 4)
 // Workspace regions (float offsets) for one (H, B); region-major, so the same
 // (H, B) must be used by the forward and the backward of one step.

@@ -155,6 +155,25 @@ def fpe_flops_per_window(H: int = 16) -> int:
     return 2 * fpe_macs_per_window(H)
 
 
+def fpe_executed_flops_per_window(H: int = 16) -> int:
+    """Flops K4 (pgp_fpe.hip) executes per window, an FMA counted as 2 (a
+    v_pk_fma_f32 as 4): per step the GRU input product (27 FMAs per node) and
+    the node scores s, t (6), the GRU cell's hidden product (27), then per
+    edge (i, j) one v_fma_f32 with output clamp (the branch indicator) and one
+    v_pk_fma_f32 into {SA, SC}, per source node s_i (3 FMAs), its weight r_i
+    and the r-weighted features (3); after the steps the 6x6 score form over
+    3x3 token pairs and the [4H x 18] map.  Exponentials, compares and
+    stores are not counted.  The reference's formulation (fpe_flops_per_window:
+    H^3 GAT aggregation, E = H+3 MHA, 3E -> 10H encoder) is far larger; the
+    kernel's algebra (rank-3 node mean, per-branch factorised edge softmax)
+    removes that work, so the executed figure is the one priced against the
+    VALU peak."""
+    per_step = H * (27 + 6) * 2 + 27 * 2 + H * H * (2 + 4) + H * (3 + 3 + 2) * 2
+    mha = 3 * (36 + 6) * 2 + 9 * 6 * 2 + 3 * 3 * 6 * 2
+    out = 4 * H * 18 * 2
+    return 3 * per_step + mha + out
+
+
 def fpe_bytes_per_window(H: int = 16) -> int:
     """K4's compulsory HBM I/O: window 36H + h0 12 in; scores 8H, protos 8H,
     class 4H, any 4, masked embedding 8H (to K3) out."""

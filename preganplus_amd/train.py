@@ -1386,7 +1386,7 @@ class OnlineTrainStep:
 
     def __init__(self, tr: "Trainer", st: "TuneState", sim, series, train_max, sched, envs, R: int = 10,
                  side=None, groups=(None, None), out=None, native: bool = True):
-        self.tr, self.sim = tr, sim
+        self.tr, self.sim, self.st = tr, sim, st
         self.series, self.tmax = tr._dev(series, torch.float64), tr._dev(train_max, torch.float64)
         E = self.series.shape[0]
         self.E, self.R, self.B = E, R, E * R
@@ -1499,18 +1499,27 @@ class OnlineTrainStep:
                       "pgp_online_gan_step")
 
     def sync(self):
-        """The native step's AdamW step counts back into the Trainer's tensor
-        records (the prototype decoder's from the device), the tuning state
-        into the TuneState the step was built with."""
+        """The step's AdamW step counts back into the Trainer's tensor records
+        (native: from the library's counts, the prototype decoder's from the
+        device) and the tuning state (prototypes, factor, counters) into the
+        TuneState the step was built with.  Native steps do not advance the
+        DPTuner's host bookkeeping, so its base is re-anchored at the synced
+        counts: a later ``tun.sync(st)`` or Python-composed step continues from
+        them instead of resetting them."""
+        tun = self.tun
         if not self.native:
+            tun.sync(self.st)
             return
         n = len(self._sel)
         out = (ctypes.c_double * n)()
         _native.check(self.tr._L.pgp_online_steps(self._h, out, n), "pgp_online_steps")
-        cs = self.tun.cond_steps.cpu().numpy()
-        tsel = self.tun.sel
+        cs = tun.cond_steps.cpu().numpy()
+        tsel = tun.sel
         for t, v in zip(self._sel, out):
-            t["step"] = float(cs[self.tun.cond.index(tsel.index(t))]) if v < 0 else float(v)
+            t["step"] = float(cs[tun.cond.index(tsel.index(t))]) if v < 0 else float(v)
+        self.st.from_device(tun.state)
+        tun.base = [t["step"] for t in tun.sel]
+        tun.n = 0
 
     def prep(self):
         """Host bookkeeping of the next step (AdamW rows).  Eager steps read

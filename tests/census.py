@@ -55,18 +55,46 @@ def _chunk(task):
     return st, err
 
 
-def run(weights, x32, sidx, got, workers=None, chunk=2048, log=None):
+def _chunk_fpe(task):
+    """One chunk of the PreGAN (FPE) variant: the anomaly softmax plays the
+    detect logits' role, the discriminator probs are 'probs'."""
+    x32, h0, sidx, got = task
+    B, H = sidx.shape
+    s = np.zeros((B, H, H))
+    s[np.arange(B)[:, None], np.arange(H)[None, :], sidx] = 1.0
+    r = O.forward_fpe(_W, x32.astype(np.float64), h0.astype(np.float64), s)
+    ref = dict(r, logits=r["probs"], probs=r["gprobs"])
+    st = DB.compare(got, ref, _W, s)
+    lr = ref["logits"]
+    ok = ((got["logits"][..., 1] > got["logits"][..., 0]) == (lr[..., 1] > lr[..., 0])).all(axis=1)
+    err = {"logits": _envelope_ratio(got["logits"], lr, DB.ATOL_PROB),
+           "protos": _envelope_ratio(got["protos"], ref["protos"], DB.ATOL_PROB),
+           "probs": _envelope_ratio(got["probs"], ref["probs"], DB.ATOL_PROB, ok),
+           "logits_max_abs": float(np.abs(got["logits"] - lr).max()),
+           "logits_max_rel": float((np.abs(got["logits"] - lr) / np.maximum(np.abs(lr), 1e-3)).max())}
+    return st, err
+
+
+def run(weights, x32, sidx, got, workers=None, chunk=2048, log=None, h0=None):
     """x32 [B,3,3H] float32 windows, sidx [B,C] int one-hot schedule columns,
-    got: HIP outputs (numpy, full launch).  Returns (census, worst error ratios)."""
+    got: HIP outputs (numpy, full launch).  h0 [B,3]: the PreGAN (FPE)
+    variant's GRU states (got['logits'] = its anomaly softmax).  Returns
+    (census, worst error ratios)."""
     B = x32.shape[0]
     workers = workers or min(16, os.cpu_count() or 1)
     keys = ("logits", "protos", "probs", "cls", "any", "keep", "final_target", "gen_target")
-    tasks = [(x32[i:i + chunk], sidx[i:i + chunk], {k: got[k][i:i + chunk] for k in keys})
-             for i in range(0, B, chunk)]
+    if h0 is None:
+        fn = _chunk
+        tasks = [(x32[i:i + chunk], sidx[i:i + chunk], {k: got[k][i:i + chunk] for k in keys})
+                 for i in range(0, B, chunk)]
+    else:
+        fn = _chunk_fpe
+        tasks = [(x32[i:i + chunk], h0[i:i + chunk], sidx[i:i + chunk], {k: got[k][i:i + chunk] for k in keys})
+                 for i in range(0, B, chunk)]
     stats, errs = [], []
     ctx = mp.get_context("spawn")
     with ctx.Pool(workers, initializer=_init, initargs=(weights,)) as pool:
-        for i, (st, err) in enumerate(pool.imap(_chunk, tasks)):
+        for i, (st, err) in enumerate(pool.imap(fn, tasks)):
             stats.append(st)
             errs.append(err)
             if log is not None and (i + 1) % 8 == 0:

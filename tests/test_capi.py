@@ -82,9 +82,13 @@ def test_fpe_variant_abi():
     L = _native.lib()
     w, _ = W.load_npz("preganplus_amd/data/pregan_simulator_16.npz")
     assert W.pack_blob(w, 16).size == L.pgp_fpe_weight_blob_len(16)
-    assert L.pgp_fpe_weight_blob_len(50) == 0           # FPE_50 not defined by the reference
+    # 50 hosts: the FPE_16 code at n_hosts=50 (make_golden_fpe50.py), not the crashing FPE_50
+    assert W.pack_blob(W.synth_fpe_weights(50, 0), 50).size == L.pgp_fpe_weight_blob_len(50)
+    assert L.pgp_fpe_weight_blob_len(32) == 0
     h = ctypes.c_void_p()
-    assert L.pgp_create_fpe(50, ctypes.byref(h)) == -2
+    assert L.pgp_create_fpe(32, ctypes.byref(h)) == -2
+    assert L.pgp_create_fpe(50, ctypes.byref(h)) == 0
+    assert L.pgp_destroy(h) == 0
     assert L.pgp_create_fpe(16, ctypes.byref(h)) == 0
     blob = np.zeros(10)
     assert L.pgp_load_weights(h, blob.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), 10) == -1

@@ -109,6 +109,29 @@ def test_native_step_equals_python_composition(H):
     assert {t["step"] for t in tr_b.tensors if t["section"] in ("gen", "disc") and t["trainable"]} == {3.0}
 
 
+def test_native_sync_updates_tune_state_and_dptuner():
+    """after native steps, sync() writes the tuning state into the
+    TuneState the step was built with and re-anchors the DPTuner's host step
+    bookkeeping, so a following tun.sync(st) keeps the native counts (it used
+    to reset them to base + 0) and the Python composition continues from them."""
+    from preganplus_amd import train as TR
+    main = torch.cuda.Stream()
+    with torch.cuda.stream(main):
+        tr, sb = _online(16, 4, native=True)
+        for _ in range(3):
+            sb.run()
+        torch.cuda.synchronize()
+        sb.sync()
+    dev = TR.TuneState(np.zeros_like(st0))
+    dev.from_device(sb.tun.state)
+    np.testing.assert_array_equal(sb.st.protos, dev.protos)
+    assert sb.st.factor < TR.PROTO_UPDATE_FACTOR   # decayed on the device, now on the host
+    steps = {t["name"] + t["section"]: t["step"] for t in tr.tensors}
+    assert {t["step"] for t in sb.tun.sel if t["name"] not in TR.DPTuner.COND} == {3.0}
+    sb.tun.sync(sb.st)
+    assert {t["name"] + t["section"]: t["step"] for t in tr.tensors} == steps
+
+
 def test_native_step_stage_timing():
     """pgp_online_timing / pgp_online_stage_ms: every span is non-negative and
     the main stream's span covers its stages."""

@@ -18,10 +18,10 @@ pytestmark = pytest.mark.gpu
 _models = {}
 
 
-def model(key, w):
+def model(key, w, H=16):
     from preganplus_amd.model import FPEDecisionModel
     if key not in _models:
-        _models[key] = FPEDecisionModel(16, w)
+        _models[key] = FPEDecisionModel(H, w)
     return _models[key]
 
 
@@ -58,15 +58,34 @@ def test_fpe_reference_fixtures():
         assert np.array_equal(got[k], ref[k]), k
 
 
-@pytest.mark.parametrize("B", [1, 63, 64, 65, 1000])
-def test_fpe_synthetic_vs_oracle(B):
-    w = W.synth_fpe_weights(16, seed=11)
+@pytest.mark.parametrize("part", ["", "b/"])
+def test_fpe50_reference_fixtures(part):
+    """C4 at 50 hosts: the reference FPE_16 class instantiated at n_hosts=50
+    with Gen_50/Disc_50 (tests/golden/make_golden_fpe50.py).  Set "b/" (anomaly
+    bias shifted) holds windows without any flagged host; every decision must
+    match the reference exactly."""
+    from tests.test_oracle_golden import fpe50_weights
+    z = np.load("tests/golden/fpe_h50.npz")
+    ref = {k[len(part):]: z[k] for k in z.files if k.startswith(part) and (part or "/" not in k)}
+    w = fpe50_weights(z, part)
+    got = run(model("fix50" + part, w, 50), ref["windows"], ref["h0"], ref["sched"])
+    g, r = as_parity(got, ref)
+    assert_parity(g, r, w, ref["sched"], check_latent=False, exact=True)
+    for k in ("cls", "any", "keep", "gen_target", "final_target"):
+        assert np.array_equal(got[k], ref[k]), k
+    if part:
+        assert 0 < got["any"].sum() < got["any"].size
+
+
+@pytest.mark.parametrize("H,B", [(16, 1), (16, 63), (16, 64), (16, 65), (16, 1000), (50, 1), (50, 65), (50, 700)])
+def test_fpe_synthetic_vs_oracle(H, B):
+    w = W.synth_fpe_weights(H, seed=11)
     rng = np.random.Generator(np.random.PCG64(B))
-    x = rng.uniform(0, 1.2, size=(B, 3, 48)).astype(np.float32)
+    x = rng.uniform(0, 1.2, size=(B, 3, 3 * H)).astype(np.float32)
     h0 = rng.standard_normal((B, 3)).astype(np.float32)
-    sched = rng.uniform(0, 1, size=(B, 16, 16)).astype(np.float32)
+    sched = rng.uniform(0, 1, size=(B, H, H)).astype(np.float32)
     ref = O.forward_fpe(w, x.astype(np.float64), h0.astype(np.float64), sched.astype(np.float64))
-    got = run(model("syn", w), x, h0, sched)
+    got = run(model(f"syn{H}", w, H), x, h0, sched)
     g, r = as_parity(got, ref)
     r["sched32"] = sched
     assert_parity(g, r, w, sched, check_latent=False)
@@ -88,6 +107,84 @@ def test_fpe_edge_inputs():
     g, r = as_parity(got, ref)
     r["sched32"] = sched
     assert_parity(g, r, w, sched, check_latent=False)
+
+
+def test_fpe50_edge_inputs_and_batch_invariance():
+    """H=50: zeros (every edge score equal), constant rows, large and negative
+    loads; then a 4,099-window launch vs its ragged tail run alone."""
+    w = W.synth_fpe_weights(50, seed=0)
+    m = model("edge50", w, 50)
+    B = 4
+    x = np.zeros((B, 3, 150), np.float32)
+    x[1] = 0.5
+    x[2] = np.linspace(0, 40, 450).reshape(3, 150)
+    x[3] = -np.linspace(0, 3, 450).reshape(3, 150)
+    h0 = np.array([[0, 0, 0], [1, -1, 0.5], [5, 5, 5], [-5, 2, -3]], np.float32)
+    sched = np.tile(np.eye(50, dtype=np.float32), (B, 1, 1))
+    ref = O.forward_fpe(w, x.astype(np.float64), h0.astype(np.float64), sched.astype(np.float64))
+    got = run(m, x, h0, sched)
+    g, r = as_parity(got, ref)
+    assert_parity(g, r, w, sched, check_latent=False)
+    rng = np.random.Generator(np.random.PCG64(9))
+    B = 4099
+    x = rng.uniform(0, 1, size=(B, 3, 150)).astype(np.float32)
+    h0 = rng.standard_normal((B, 3)).astype(np.float32)
+    sched = rng.uniform(0, 1, size=(B, 50, 50)).astype(np.float32)
+    big = run(m, x, h0, sched)
+    small = run(m, x[-37:], h0[-37:], sched[-37:])
+    for k in small:
+        assert np.array_equal(big[k][-37:], small[k]), k
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("seed_off", [0, 970])
+def test_fpe50_full_size_census(seed_off):
+    """BASELINE C4 at its full size: 65,536 windows at 50 hosts through K4 + K3,
+    every window compared with the fp64 FPE oracle (tests/census.py): scores /
+    protos / probs within the north-star tolerance, every decision equal
+    unless its fp64 margin lies inside its derived fp32 bound."""
+    import json
+    import os
+
+    from preganplus_amd.model import to_numpy
+    from tests import census as CE
+    from tests import decision_bounds as DB
+    from tests.test_gpu_parity import _c2_torch
+    H, B = 50, 65536
+    w = W.synth_fpe_weights(H, seed=0)
+    m = model("census50", w, H)
+    seed = 77 + seed_off
+    x, s = _c2_torch(B, H, seed=seed)
+    g = torch.Generator(device="cuda").manual_seed(seed + 1)
+    h0 = torch.randn((B, 3), generator=g, device="cuda")
+    full = to_numpy(m.forward(x, h0, s))
+    torch.cuda.synchronize()
+    for lo, hi in ((0, 64), (B // 2 - 7, B // 2 + 50), (B - 45, B)):
+        part = to_numpy(m.forward(x[lo:hi].contiguous(), h0[lo:hi].contiguous(), s[lo:hi].contiguous()))
+        torch.cuda.synchronize()
+        for k in part:
+            assert np.array_equal(full[k][lo:hi], part[k]), (k, lo, hi)
+    got = dict(full, logits=full["scores"])
+    anom = got["logits"][..., 1] > got["logits"][..., 0]
+    assert np.array_equal(full["any"], anom.any(axis=1))
+    assert np.array_equal(full["cls"] < 0, ~anom)
+    x32, h32 = x.cpu().numpy(), h0.cpu().numpy()
+    sidx = s.argmax(dim=-1).cpu().numpy()
+    del x, s, h0
+    st, worst = CE.run(w, x32, sidx, got, log=print, h0=h32)
+    res = {"variant": "fpe", "H": H, "windows": B, "seed": seed, "census": st, "worst_error_over_tolerance": worst}
+    print("CENSUS", json.dumps(res))
+    os.makedirs("gpurun_out", exist_ok=True)
+    with open(f"gpurun_out/census_fpe_h{H}_b{B}_s{seed}.json", "w") as f:
+        json.dump(res, f, indent=1)
+    assert worst["logits"] <= 1.0 and worst["protos"] <= 1.0 and worst["probs"] <= 1.0, worst
+    assert not DB.violations(st), st
+    assert st["windows"] == B
+    for kind in ("anomaly", "class", "keep", "gen"):
+        assert st[kind]["in_band"] <= 1e-3 * max(st[kind]["n"], 1), (kind, st[kind])
+    for kind in ("any", "class", "keep", "final"):
+        assert st[kind]["mismatch"] == 0, (kind, st[kind])
+    assert st["anomaly"]["mismatch"] <= 8 and st["gen"]["mismatch"] <= 8, st
 
 
 def test_fpe_batch_invariance_and_errors():

@@ -98,3 +98,32 @@ def test_fpe_blob_layout():
     assert blob.size == sum(int(np.prod(s)) for _, _, s in W.fpe_blob_layout(16))
     ws = W.synth_fpe_weights(16, 1)
     assert W.pack_blob(ws, 16).size == blob.size
+
+
+def fpe50_weights(z, part=""):
+    """Weights of tests/golden/fpe_h50.npz (make_golden_fpe50.py): seeded
+    synth_fpe_weights(50), set "b/" with the anomaly bias moved by +-shift."""
+    w = W.synth_fpe_weights(50, int(z["weights_seed"]))
+    if part:
+        sh = float(z[f"{part}bias_shift"])
+        w["fpe"]["anomaly_decoder.0.bias"] = w["fpe"]["anomaly_decoder.0.bias"] + np.array([sh, -sh])
+    return w
+
+
+@pytest.mark.parametrize("part", ["", "b/"])
+def test_fpe50_oracle_matches_reference(part):
+    """C4 at 50 hosts: the reference FPE_16 class instantiated at n_hosts=50
+    (make_golden_fpe50.py; FPE_50 itself raises in the reference) with
+    Gen_50/Disc_50.  Set "b/" holds windows without any flagged host."""
+    z = np.load(f"{GOLD}/fpe_h50.npz")
+    w = fpe50_weights(z, part)
+    out = O.forward_fpe(w, z[f"{part}windows"], z[f"{part}h0"], z[f"{part}sched"])
+    for k in ["probs", "protos", "emb", "new_sched", "gprobs"]:
+        np.testing.assert_allclose(out[k], z[f"{part}{k}"], rtol=0, atol=1e-12, err_msg=k)
+    for k in ["cls", "any", "keep", "final_target", "gen_target"]:
+        np.testing.assert_array_equal(out[k], z[f"{part}{k}"], err_msg=k)
+    out32 = O.forward_fpe(w, z[f"{part}windows"], z[f"{part}h0"], z[f"{part}sched"], dtype=np.float32)
+    np.testing.assert_allclose(out32["probs"], z[f"{part}probs"], rtol=1e-4, atol=1e-6)
+    np.testing.assert_array_equal(out32["cls"], z[f"{part}cls"])
+    if part:
+        assert 0 < z["b/any"].sum() < z["b/any"].size   # both run_model branches (PreGAN.py:112-113)

@@ -4,7 +4,11 @@ box hits all variants alike.  Prints per variant the ms_per_step of each round
 and the median.
 
   python3 tools/ab_bench.py --rounds 3 --args "--config tune --hosts 16 --steps 50 --warmup 5 --no-cpu-baseline" \
-      base= side0=PGP_TUNE_SIDE_STREAM=0 eager=PGP_BENCH_GRAPH=0
+      base= eager=PGP_BENCH_GRAPH=0 prev=PGP_LIB=preganplus_amd/_lib/var/libpreganplus_prev.so
+
+The library reads no tuning switches from the environment (round 5 removed
+them, _native.REMOVED_ENV): a variant is another build (PGP_LIB) or a
+bench.py switch.
 """
 import argparse
 import json

@@ -1,0 +1,88 @@
+#!/bin/bash
+# Round-6 GPU session steps.  usage: tools/gpu_r06.sh TAG STEP...
+#   tests   GPU suite (+ smoke)
+#   tfpe4   C4 GPU tests only (H=16 and H=50 fixtures, oracle, census)
+#   fpe     C4 lines (H=50, H=16) + rocprofv3 kernel stats of both
+#   fpepmc  K4 stall / VALU passes (H=50)
+#   c2      C2 line (CPU baseline included) + rocprofv3 kernel stats
+#   c2stall C2 stall / MFMA-busy passes (K2, K3)
+#   tune    C3 lines (H=50, H=16) + rocprofv3 kernel stats
+#   fleet   C5 lines (resident and streamed)
+# every GPU step runs under its own timeout; the script stops at the first failure
+set -u
+cd "$GRAFT_REPO_ROOT"
+T=${1:?tag}
+shift
+OUT=gpurun_out/$T
+mkdir -p $OUT
+export TMPDIR=/tmp
+run() {  # run NAME SECONDS CMD...
+  local name=$1 secs=$2
+  shift 2
+  echo "[$name] $(date +%T) start"
+  timeout -k 10 $secs "$@" > $OUT/$name.out 2> $OUT/$name.err
+  local rc=$?
+  echo "[$name] $(date +%T) rc=$rc"
+  if [ $rc -ne 0 ]; then tail -20 $OUT/$name.err; tail -5 $OUT/$name.out; exit $rc; fi
+}
+pmc() {  # pmc NAME COUNTERS BENCH_ARGS...
+  local name=$1 ctr=$2
+  shift 2
+  echo "[$name] $(date +%T) start"
+  timeout -s KILL 120 rocprofv3 --pmc $ctr -d $OUT/$name -o run --output-format csv -- python3 bench.py "$@" \
+    > $OUT/$name.log 2>&1
+  local rc=$?
+  echo "[$name] $(date +%T) rc=$rc"
+  if [ $rc -ne 0 ]; then tail -5 $OUT/$name.log; exit $rc; fi
+}
+STALL1="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_MFMA"
+STALL2="SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE"
+PYT="python -u -m pytest -x -v -p no:cacheprovider --timeout 300 --timeout-method thread"
+for step in "$@"; do
+  case $step in
+    tests)
+      run gpu_tests 1100 $PYT tests -m gpu
+      tail -2 $OUT/gpu_tests.out
+      run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+      ;;
+    micro)
+      run bf16split 120 tools/micro/bf16_split 256 7680
+      cat $OUT/bf16split.out
+      ;;
+    tfpe4)
+      run t_fpe4 900 $PYT tests/test_gpu_fpe.py -m gpu
+      tail -2 $OUT/t_fpe4.out
+      ;;
+    fpe)
+      run fpe50 400 python3 -u bench.py --config fpe --hosts 50 --steps 100 --warmup 5
+      run fpe16 400 python3 -u bench.py --config fpe --hosts 16 --steps 100 --warmup 5
+      run prof_fpe50 240 rocprofv3 --kernel-trace --stats -d $OUT/prof_fpe50 -o fpe --output-format csv -- python3 bench.py --config fpe --hosts 50 --steps 60 --warmup 10 --no-cpu-baseline
+      run prof_fpe16 240 rocprofv3 --kernel-trace --stats -d $OUT/prof_fpe16 -o fpe --output-format csv -- python3 bench.py --config fpe --hosts 16 --steps 60 --warmup 10 --no-cpu-baseline
+      ;;
+    fpepmc)
+      pmc fpestall1 "$STALL1" --config fpe --hosts 50 --steps 3 --warmup 1 --no-cpu-baseline
+      pmc fpestall2 "$STALL2" --config fpe --hosts 50 --steps 3 --warmup 1 --no-cpu-baseline
+      ;;
+    c2)
+      run c2 400 python3 -u bench.py
+      run prof_c2 240 rocprofv3 --kernel-trace --stats -d $OUT/prof_c2 -o c2 --output-format csv -- python3 bench.py --steps 60 --warmup 10 --no-cpu-baseline
+      ;;
+    c2stall)
+      pmc c2stall1 "$STALL1" --steps 3 --warmup 1 --no-cpu-baseline
+      pmc c2stall2 "$STALL2" --steps 3 --warmup 1 --no-cpu-baseline
+      ;;
+    tune)
+      run tune50 400 python3 -u bench.py --config tune --hosts 50 --steps 50 --warmup 5
+      run tune16 400 python3 -u bench.py --config tune --hosts 16 --steps 50 --warmup 5
+      run prof_tune 240 rocprofv3 --kernel-trace --stats -d $OUT/prof_tune -o tune --output-format csv -- python3 bench.py --config tune --hosts 50 --steps 60 --warmup 10 --no-cpu-baseline
+      run prof_tune16 240 rocprofv3 --kernel-trace --stats -d $OUT/prof_tune16 -o tune --output-format csv -- python3 bench.py --config tune --hosts 16 --steps 60 --warmup 10 --no-cpu-baseline
+      ;;
+    fleet)
+      run fleet 400 python3 -u bench.py --config fleet --steps 100 --warmup 5
+      ;;
+    *)
+      echo "unknown step $step"; exit 2
+      ;;
+  esac
+done
+echo DONE
