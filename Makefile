@@ -4,7 +4,7 @@ ARCH ?= gfx950
 LIBDIR := preganplus_amd/_lib
 LIB := $(LIBDIR)/libpreganplus.so
 CSRC := preganplus_amd/csrc
-KSRCS := $(CSRC)/pgp_tunef.hip $(CSRC)/pgp_dec.hip $(CSRC)/pgp_gat.hip $(CSRC)/pgp_encoder.hip $(CSRC)/pgp_decoder.hip $(CSRC)/pgp_gan.hip $(CSRC)/pgp_train.hip $(CSRC)/pgp_tune.hip $(CSRC)/pgp_tune1.hip $(CSRC)/pgp_gan1.hip $(CSRC)/pgp_tunedp.hip $(CSRC)/pgp_gantrain.hip $(CSRC)/pgp_gobi.hip $(CSRC)/pgp_sim.hip $(CSRC)/pgp_fpe.hip $(CSRC)/pgp_fpetrain.hip $(CSRC)/pgp_decide.hip $(CSRC)/pgp_repack.hip $(CSRC)/pgp_online.hip $(CSRC)/pgp_capi.hip
+KSRCS := $(CSRC)/pgp_tunef.hip $(CSRC)/pgp_dec.hip $(CSRC)/pgp_gat.hip $(CSRC)/pgp_encoder.hip $(CSRC)/pgp_decoder.hip $(CSRC)/pgp_gan.hip $(CSRC)/pgp_gansplit.hip $(CSRC)/pgp_train.hip $(CSRC)/pgp_tune.hip $(CSRC)/pgp_tune1.hip $(CSRC)/pgp_gan1.hip $(CSRC)/pgp_tunedp.hip $(CSRC)/pgp_gantrain.hip $(CSRC)/pgp_gobi.hip $(CSRC)/pgp_sim.hip $(CSRC)/pgp_fpe.hip $(CSRC)/pgp_fpetrain.hip $(CSRC)/pgp_decide.hip $(CSRC)/pgp_repack.hip $(CSRC)/pgp_online.hip $(CSRC)/pgp_capi.hip
 SRCS := $(KSRCS) $(CSRC)/pgp_pack.cpp
 OBJDIR := build/obj
 OBJS := $(patsubst $(CSRC)/%,$(OBJDIR)/%.o,$(SRCS))

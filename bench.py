@@ -126,6 +126,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-gan", action="store_true", help="tune config: Transformer tuning step only")
+    ap.add_argument("--fp32-decoder", action="store_true", help="c2: K2b on the fp32 MFMA instead of the "
+                                                                 "split-bf16 form (A/B)")
+    ap.add_argument("--fp32-gan", action="store_true", help="c2: K3 on the fp32 MFMA instead of the split-bf16 "
+                                                             "form (A/B)")
     ap.add_argument("--stream", action="store_true", help="fleet config: the streamed (PCIe-inclusive) rate as "
                                                           "the line's value, kernel-only beside it")
     ap.add_argument("--config", choices=["c2", "fleet", "tune", "fpe", "gobi", "sim", "loop", "plugin", "ranks"],
@@ -189,24 +193,24 @@ def main():
         migrations(out["keep"], out["final_target"], cur, out=mv_out)
         evs[NK].record()
 
+    if args.fp32_decoder:
+        model.decoder_split(False)
+    if args.fp32_gan:
+        model.gan_split(False)
+    split = R.decoder_split(H) and not args.fp32_decoder
+    gsplit = R.gan_split(H) and not args.fp32_gan
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(NK + 1)] for _ in range(args.steps)]
-    if world > 1:
-        torch.distributed.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
+    # the timed loop: events at its ends only (barrier + sync on both sides)
+    elapsed = _timed(world, device, step, args.steps)
+    # per-stage HIP events in a separate pass right after (same inputs, same
+    # process): kernel times and the roofline's launch duration
+    n_prof = min(args.steps, 40)
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(NK + 1)] for _ in range(n_prof)]
+    for i in range(n_prof):
         step(evs[i])
     torch.cuda.synchronize()
-    if world > 1:
-        torch.distributed.barrier()
-    t1 = time.perf_counter()
-    el = torch.tensor([t1 - t0], dtype=torch.float64, device=device)
-    if world > 1:
-        torch.distributed.all_reduce(el, op=torch.distributed.ReduceOp.MAX)
-    elapsed = float(el.item())
     k_ms = np.array([[e[k].elapsed_time(e[k + 1]) for k in range(NK)] for e in evs])  # [steps, NK]
     k_mean = k_ms.mean(axis=0)
 
@@ -244,6 +248,17 @@ def main():
                 "encoder": achieved,
                 "decoder": R.decoder_flops_per_window(H) * B / (k_mean[2] * 1e-3) / 1e12,
                 "gan": R.gan_flops_per_window(H) * B / (k_mean[3] * 1e-3) / 1e12},
+            "kernel_timing": f"per-stage HIP events over {n_prof} steps after the timed loop",
+            "decoder_form": ({"form": "split-bf16: each fp32 operand split exactly into 3 bf16 parts, 6 "
+                                      "v_mfma_f32_16x16x32_bf16 per fp32 product (terms below 2^-26 dropped), fp32 "
+                                      "accumulation; K2b's fp32-equivalent rate above may exceed the fp32 peak",
+                              "executed_bf16_tflops": R.decoder_split_flops_per_window(H) * B / (k_mean[2] * 1e-3)
+                              / 1e12, "bf16_dense_peak_tflops": R.PEAK_BF16_TFLOPS,
+                              "frac_of_bf16_peak": R.decoder_split_flops_per_window(H) * B / (k_mean[2] * 1e-3)
+                              / 1e12 / R.PEAK_BF16_TFLOPS}
+                             if split else {"form": "fp32 MFMA (v_mfma_f32_16x16x4_f32)"}),
+            "gan_form": ("split-bf16 (6 v_mfma_f32_16x16x32_bf16 per fp32 product; schedule blocks exact in "
+                         "bf16, e.g. one-hot, in 3)" if gsplit else "fp32 MFMA (v_mfma_f32_16x16x4_f32)"),
             "roofline": {"kernel": "encoder_kernel (K2)", "bound": "mfma", "achieved": achieved,
                          "peak": R.PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                          "frac": achieved / R.PEAK_FP32_TFLOPS,

@@ -155,6 +155,17 @@ int pgp_migrations(int n_hosts, int batch, const int* keep_orig, const int* fina
 /* run_model's embedding (PreGANPlus.py:129): emb[b,h,:] = protos[b,h,:] where
  * argmax(logits[b,h,:]) == 1 (ties -> 0), else 0.  fp32 device [B,H,2] each. */
 int pgp_embedding(int n_hosts, int batch, const float* logits, const float* protos, float* emb, void* stream);
+/* K2b's contraction form.  on = 1 (the default where compiled: H = 32, 50):
+ * the decoder GEMM as six split-bf16 MFMAs per fp32 product (every operand
+ * split exactly into three bf16 parts; error at the fp32 MFMA's level,
+ * tools/micro/bf16_split.hip); on = 0: v_mfma_f32_16x16x4_f32.  Returns
+ * PGP_ERR_UNSUPPORTED for on = 1 where the split form is not compiled. */
+int pgp_decoder_split(pgp_model* m, int on);
+/* K3's contraction form, likewise (the default where compiled: H = 50; also
+ * the FPE variant's K3): Gen1, Disc1 and Gen2 as split-bf16 MFMAs, a schedule
+ * block exactly representable in bf16 (one-hot GOBI rows) in three products
+ * instead of six (the other three add exact zeros). */
+int pgp_gan_split(pgp_model* m, int on);
 /* The dense schedule pgp_forward reads, from per-container host indices: a
  * GOBI result_cache row is one-hot (scheduler/BaGTI/src/opt.py:9-15), so a
  * streamed fleet chunk (bench.py --config fleet, preganplus_amd/fleet.py)

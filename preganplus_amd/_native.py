@@ -86,6 +86,10 @@ def lib():
     L.pgp_migrations.restype = c_int
     L.pgp_embedding.argtypes = [c_int, c_int] + [fp] * 3 + [vp]
     L.pgp_embedding.restype = c_int
+    L.pgp_decoder_split.argtypes = [vp, c_int]
+    L.pgp_decoder_split.restype = c_int
+    L.pgp_gan_split.argtypes = [vp, c_int]
+    L.pgp_gan_split.restype = c_int
     L.pgp_schedule_onehot.argtypes = [c_int, c_int, fp, fp, vp]
     L.pgp_schedule_onehot.restype = c_int
     _lib = L

@@ -25,6 +25,10 @@ struct pgp_model {
   bool fpe = false;  // PreGAN FPE_16 variant (pgp_create_fpe)
   bool loaded = false;
   float* d_frags = nullptr;
+  float* d_decb = nullptr;   // split-bf16 decoder planes (derived from d_frags on the device)
+  bool dec_split = true;     // K2b on the split-bf16 planes where compiled (pgp_decoder_split)
+  float* d_ganb = nullptr;   // split-bf16 GAN planes (derived from d_frags on the device)
+  bool gan_split = true;     // K3 on the split-bf16 planes where compiled (pgp_gan_split)
   float* d_tab = nullptr;
   float* d_gtab = nullptr;
   float* d_gat = nullptr;    // GAT constants u[4] | v[4] (K1 reads them on the device)
@@ -142,7 +146,7 @@ int pgp_create_fpe(int n_hosts, pgp_model** out) {
 
 int pgp_destroy(pgp_model* m) {
   if (!m) return PGP_OK;
-  for (float* p : {m->d_frags, m->d_tab, m->d_gtab, m->d_agg, m->d_lat, m->d_emb, m->d_gat})
+  for (float* p : {m->d_frags, m->d_decb, m->d_ganb, m->d_tab, m->d_gtab, m->d_agg, m->d_lat, m->d_emb, m->d_gat})
     if (p) (void)hipFree(p);
   if (m->d_pscr) (void)hipFree(m->d_pscr);
   delete m;
@@ -162,6 +166,16 @@ int pgp_load_weights(pgp_model* m, const double* blob, size_t len) {
   HIPCHK(hipMemcpy(m->d_gtab, P.gan_tab.data(), P.gan_tab.size() * sizeof(float), hipMemcpyHostToDevice));
   if (!m->d_gat) HIPCHK(hipMalloc(&m->d_gat, sizeof(GatConst)));
   HIPCHK(hipMemcpy(m->d_gat, &P.gat, sizeof(GatConst), hipMemcpyHostToDevice));
+  if (!m->fpe && decoder_split_floats(m->H) > 0) {
+    if (!m->d_decb) HIPCHK(hipMalloc(&m->d_decb, decoder_split_floats(m->H) * sizeof(float)));
+    HIPCHK(launch_decoder_split(m->H, m->d_frags, m->d_decb, nullptr));
+    HIPCHK(hipStreamSynchronize(nullptr));
+  }
+  if (gan_split_floats(m->H) > 0) {
+    if (!m->d_ganb) HIPCHK(hipMalloc(&m->d_ganb, gan_split_floats(m->H) * sizeof(float)));
+    HIPCHK(launch_gan_split_derive(m->H, m->d_frags, m->d_ganb, nullptr));
+    HIPCHK(hipStreamSynchronize(nullptr));
+  }
   m->loaded = true;
   return PGP_OK;
 }
@@ -199,6 +213,8 @@ int pgp_forward_stage(pgp_model* m, int stage, int batch, const float* windows, 
   a.lat = m->d_lat;
   a.emb = m->d_emb;
   a.frags = m->d_frags;
+  a.decb = m->dec_split ? m->d_decb : nullptr;
+  a.ganb = m->gan_split ? m->d_ganb : nullptr;
   a.tab = m->d_tab;
   a.gtab = m->d_gtab;
   a.gat = m->d_gat;
@@ -262,6 +278,7 @@ int pgp_forward_fpe_stage(pgp_model* m, int stage, int batch, const float* windo
   a.sched = sched;
   a.emb = m->d_emb;
   a.frags = m->d_frags;
+  a.ganb = m->gan_split ? m->d_ganb : nullptr;
   a.gtab = m->d_gtab;
   a.probs = probs;
   a.keep = keep_orig;
@@ -294,6 +311,22 @@ int pgp_embedding(int n_hosts, int batch, const float* logits, const float* prot
   if (batch == 0) return PGP_OK;
   if (!logits || !protos || !emb) return fail(PGP_ERR_ARG, "NULL input/output pointer");
   HIPCHK(launch_embed((long)batch * n_hosts, logits, protos, emb, reinterpret_cast<hipStream_t>(stream)));
+  return PGP_OK;
+}
+
+int pgp_decoder_split(pgp_model* m, int on) {
+  if (!m) return fail(PGP_ERR_ARG, "NULL model");
+  if (m->fpe || decoder_split_floats(m->H) == 0)
+    return on ? fail(PGP_ERR_UNSUPPORTED, "split-bf16 decoder not compiled for this model / host count") : PGP_OK;
+  m->dec_split = on != 0;
+  return PGP_OK;
+}
+
+int pgp_gan_split(pgp_model* m, int on) {
+  if (!m) return fail(PGP_ERR_ARG, "NULL model");
+  if (gan_split_floats(m->H) == 0)
+    return on ? fail(PGP_ERR_UNSUPPORTED, "split-bf16 GAN kernel not compiled for this host count") : PGP_OK;
+  m->gan_split = on != 0;
   return PGP_OK;
 }
 
@@ -686,6 +719,10 @@ int pgp_repack_master_sections(pgp_model* m, const float* P_device, const double
   if (!m->d_pscr) HIPCHK(hipMalloc(&m->d_pscr, repack_scratch_len(m->H) * sizeof(double)));
   RepackArgs a{m->K, P_device, all, prototypes_device, m->d_pscr, m->d_frags, m->d_tab, m->d_gtab, m->d_gat, sections};
   HIPCHK(launch_repack(m->H, a, reinterpret_cast<hipStream_t>(stream)));
+  if ((sections & 1) && m->d_decb)
+    HIPCHK(launch_decoder_split(m->H, m->d_frags, m->d_decb, reinterpret_cast<hipStream_t>(stream)));
+  if ((sections & 2) && m->d_ganb)
+    HIPCHK(launch_gan_split_derive(m->H, m->d_frags, m->d_ganb, reinterpret_cast<hipStream_t>(stream)));
   return PGP_OK;
 }
 

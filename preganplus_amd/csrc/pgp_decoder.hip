@@ -174,12 +174,197 @@ __global__ __launch_bounds__(kDecWaves * 64, H <= 16 ? 8 : 1) void decoder_kerne
   if (valid && g == 0) a.any_anom[bw] = anyf;
 }
 
+// ---------------------------------------------------------------------------
+// Split-bf16 form (H = 32, 50): the same GEMM on v_mfma_f32_16x16x32_bf16.
+// Every fp32 operand is split exactly into three bf16 parts, x = x0 + x1 + x2
+// (x0 = bf16(x), x1 = bf16(x - x0), x2 = bf16(x - x0 - x1); each residual is
+// exact in fp32), and w . x = sum over i + j <= 2 of w_i . x_j: six bf16 MFMAs
+// whose products are exact in fp32 and accumulate in fp32; the dropped terms
+// are below 2^-26 of |w x| (tools/micro/bf16_split.hip measures the result
+// against fp64 beside the fp32 MFMA).  A bf16 MFMA does 16x the fp32 one's
+// flops per cycle, so six of them cost 3/8 of the fp32 contraction.
+// The weights' three planes are derived once per weight load from the fp32
+// fragments (dec_split_kernel, lane-local: a lane's 8 k-steps of a 16x16x32
+// fragment are its two fp32 groups of 4); the latent is split in registers as
+// it is loaded (VALU, shared by all MT_O output tiles).
+template <int H>
+struct DecB {
+  using G = Geo<H>;
+  static constexpr int NB = cdiv(G::KQ_D, 2);    // 8-k-step blocks per (host, step) chunk
+  static constexpr int FRC = NB * G::MT_O * 3;   // 1-KiB fragments per chunk: [blk][mt][plane]
+  static constexpr long SIZE = (long)H * kWindow * FRC * 256;  // floats (bf16 pairs)
+  static constexpr int SLOT = FRC * 256;         // one chunk per LDS slot
+  static constexpr int TOTAL = 2 * SLOT + G::MT_O * 16 + 2 * kMaxProtos;
+};
+template <int H>
+constexpr bool dec_split() {
+  return H >= 32 && DecB<H>::TOTAL * 4 <= 160 * 1024;
+}
+
+// fp32 decoder fragments -> bf16 planes [chunk][blk][mt][plane][lane][8]
+template <int H>
+__global__ __launch_bounds__(256) void dec_split_kernel(const float* __restrict__ wdec, float* __restrict__ out) {
+  using G = Geo<H>;
+  using D = DecB<H>;
+  const long f = (long)blockIdx.x * 4 + (threadIdx.x >> 6);  // over [chunk][blk][mt]
+  const int lane = threadIdx.x & 63;
+  if (f >= (long)H * kWindow * D::NB * G::MT_O) return;
+  const int mt = (int)(f % G::MT_O);
+  const long r = f / G::MT_O;
+  const int blk = (int)(r % D::NB);
+  const long c = r / D::NB;
+  float v[8];
+#pragma unroll
+  for (int hq = 0; hq < 2; ++hq) {
+    const int q4 = 2 * blk + hq;
+    const f32x4 t = q4 < G::KQ_D ? ld4(wdec + ((c * G::DEC_G) + mt * G::KQ_D + q4) * 256 + lane * 4)
+                                 : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[4 * hq + e] = t[e];
+  }
+  u32x4 p[3];
+  split8(v, p);
+#pragma unroll
+  for (int k = 0; k < 3; ++k) *reinterpret_cast<u32x4*>(out + (f * 3 + k) * 256 + lane * 4) = p[k];
+}
+
+template <int H>
+__global__ __launch_bounds__(kDecWaves * 64, 1) void decoder_split_kernel(FwdArgs a) {
+  using G = Geo<H>;
+  using D = DecB<H>;
+  __shared__ __attribute__((aligned(16))) float smem[D::TOTAL];
+  float* tdec = smem + 2 * D::SLOT;  // decoder bias [MT_O * 16]
+  float* P = tdec + G::MT_O * 16;    // prototypes [K][2]
+  for (int i = threadIdx.x; i < G::MT_O * 16; i += blockDim.x) tdec[i] = a.tab[G::T_DEC + i];
+  for (int i = threadIdx.x; i < 2 * a.K; i += blockDim.x) P[i] = a.tab[G::T_PROTO + i];
+
+  const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const long blk = (long)blockIdx.x * kDecWaves + wv;
+  const long nblk = (a.B + 15) / 16;
+  const bool active = blk < nblk;
+  const float* lat = a.lat + (active ? blk : 0) * G::LAT_BLK;
+  constexpr int NCH = H * kWindow;
+  auto load_b = [&](int c, bool ok, float (&v)[G::KS_D]) {
+    const float* lc = lat + (long)c * G::KS_D * 64;
+#pragma unroll
+    for (int q = 0; q < G::LAT_FG; ++q) {
+      const f32x4 t = ok ? ld4(lc + q * 256 + lane * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[4 * q + e] = t[e];
+    }
+#pragma unroll
+    for (int r = 0; r < G::KS_D % 4; ++r) v[4 * G::LAT_FG + r] = ok ? lc[G::LAT_FG * 256 + r * 64 + lane] : 0.f;
+  };
+  float* cur = smem;
+  float* nxt = smem + D::SLOT;
+  dma_groups(a.decb, cur, D::FRC, wv, kDecWaves, lane);
+  float b[G::KS_D];
+  load_b(0, active, b);
+  __syncthreads();
+  if (NCH > 1) dma_groups(a.decb + (long)D::SLOT, nxt, D::FRC, wv, kDecWaves, lane);
+
+  f32x4 acc[G::MT_O];
+#pragma unroll
+  for (int mt = 0; mt < G::MT_O; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll 1
+  for (int c = 0; c < NCH; ++c) {
+    float bn[G::KS_D];
+    load_b(c + 1, active && c + 1 < NCH, bn);
+#pragma unroll
+    for (int kb = 0; kb < D::NB; ++kb) {
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = 8 * kb + e < G::KS_D ? b[8 * kb + e] : 0.f;
+      u32x4 x[3];
+      split8(v, x);
+#pragma unroll
+      for (int mt = 0; mt < G::MT_O; ++mt) {
+        const float* F = cur + ((kb * G::MT_O + mt) * 3) * 256 + lane * 4;
+        const u32x4 w[3] = {*reinterpret_cast<const u32x4*>(F), *reinterpret_cast<const u32x4*>(F + 256),
+                            *reinterpret_cast<const u32x4*>(F + 512)};
+        acc[mt] = mfma_bf6(w, x, acc[mt]);
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < G::KS_D; ++s) b[s] = bn[s];
+    __syncthreads();
+    float* t = cur;
+    cur = nxt;
+    nxt = t;
+    if (c + 2 < NCH) dma_groups(a.decb + (long)(c + 2) * D::SLOT, nxt, D::FRC, wv, kDecWaves, lane);
+  }
+
+  // ---- epilogue: bias, sigmoid, detect, embed, classify (as decoder_kernel) ----
+  const long bw = blk * 16 + j;
+  const bool valid = active && bw < a.B;
+  int anyf = 0;
+#pragma unroll
+  for (int mt = 0; mt < G::MT_O; ++mt) {
+    const int host = 4 * mt + g;
+    const f32x4 v = acc[mt] + ld4(tdec + 16 * mt + 4 * g);
+    if (host < H) {
+      const float l0 = v[0], l1 = v[1];
+      const float p0 = __builtin_amdgcn_rcpf(1.0f + __expf(-v[2])), p1 = __builtin_amdgcn_rcpf(1.0f + __expf(-v[3]));
+      const bool an = l1 > l0;  // torch.argmax: ties -> index 0
+      const float e0 = an ? p0 : 0.f, e1 = an ? p1 : 0.f;
+      int cl = -1;
+      if (!(e0 == 0.f && e1 == 0.f)) {
+        float best = INFINITY;
+        for (int k = 0; k < a.K; ++k) {
+          const float d0 = e0 - P[2 * k], d1 = e1 - P[2 * k + 1];
+          const float dist = (d0 * d0 + d1 * d1) * 0.5f;  // torch.mean over PROTO_DIM = 2
+          if (dist < best) {                              // np.argmin: first minimum
+            best = dist;
+            cl = k;
+          }
+        }
+      }
+      anyf |= an ? 1 : 0;
+      if (valid) {
+        const long o = (bw * H + host) * 2;
+        a.logits[o] = l0;
+        a.logits[o + 1] = l1;
+        a.protos[o] = p0;
+        a.protos[o + 1] = p1;
+        a.cls[bw * H + host] = cl;
+        a.emb[bw * G::EP + 2 * host] = e0;
+        a.emb[bw * G::EP + 2 * host + 1] = e1;
+      }
+    }
+  }
+  {
+    const auto r = __builtin_amdgcn_permlane16_swap((unsigned)anyf, (unsigned)anyf, false, false);
+    const int a16 = (int)(r[0] | r[1]);
+    const auto q = __builtin_amdgcn_permlane32_swap((unsigned)a16, (unsigned)a16, false, false);
+    anyf = (int)(q[0] | q[1]);
+  }
+  if (valid && g == 0) a.any_anom[bw] = anyf;
+}
+
 template <int H>
 hipError_t launch(const FwdArgs& a, hipStream_t st) {
   const long nblk = (a.B + 15) / 16;
   const int grid = (int)((nblk + kDecWaves - 1) / kDecWaves);
+  if constexpr (dec_split<H>()) {
+    if (a.decb != nullptr) {
+      decoder_split_kernel<H><<<grid, kDecWaves * 64, 0, st>>>(a);
+      return hipGetLastError();
+    }
+  }
   decoder_kernel<H><<<grid, kDecWaves * 64, 0, st>>>(a);
   return hipGetLastError();
+}
+
+template <int H>
+hipError_t launch_split(const float* frags, float* decb, hipStream_t st) {
+  if constexpr (dec_split<H>()) {
+    const long nf = (long)H * kWindow * DecB<H>::NB * Geo<H>::MT_O;
+    dec_split_kernel<H><<<(int)((nf + 3) / 4), 256, 0, st>>>(frags + Geo<H>::OFF_DEC, decb);
+    return hipGetLastError();
+  }
+  return hipErrorInvalidValue;
 }
 
 }  // namespace
@@ -189,6 +374,28 @@ hipError_t launch_decoder(const FwdArgs& a, hipStream_t st) {
 #define CASE(h) \
   case h:       \
     return launch<h>(a, st);
+    PGP_FOR_EACH_H(CASE)
+#undef CASE
+  }
+  return hipErrorInvalidValue;
+}
+
+long decoder_split_floats(int H) {
+  switch (H) {
+#define CASE(h) \
+  case h:       \
+    return dec_split<h>() ? DecB<h>::SIZE : 0;
+    PGP_FOR_EACH_H(CASE)
+#undef CASE
+  }
+  return 0;
+}
+
+hipError_t launch_decoder_split(int H, const float* frags, float* decb, hipStream_t st) {
+  switch (H) {
+#define CASE(h) \
+  case h:       \
+    return launch_split<h>(frags, decb, st);
     PGP_FOR_EACH_H(CASE)
 #undef CASE
   }

@@ -38,6 +38,8 @@ struct FwdArgs {
   float* lat;            // workspace: encoder output tiles, [blk][H][3][KS_D][64]
   float* emb;            // workspace: masked embeddings [B][EP]
   const float* frags;    // device weight fragments (Geo<H> offsets)
+  const float* decb;     // split-bf16 decoder weight planes (pgp_decoder.hip DecB), or nullptr
+  const float* ganb;     // split-bf16 GAN weight planes (pgp_gansplit.hip GanS), or nullptr
   const float* tab;      // encoder/decoder tables (LDS-staged)
   const float* gtab;     // GAN tables
   const float* gat;      // GAT constants u[4] | v[4] (device)
@@ -83,7 +85,16 @@ hipError_t launch_onehot(int H, long rows, const unsigned char* idx, float* sche
 hipError_t launch_gat(const FwdArgs& a, hipStream_t st);
 hipError_t launch_encoder(const FwdArgs& a, hipStream_t st);
 hipError_t launch_decoder(const FwdArgs& a, hipStream_t st);
+// split-bf16 decoder weights (pgp_decoder.hip): floats of the planes (0: the
+// fp32 decoder runs at this H) and their derivation from the fp32 fragments
+long decoder_split_floats(int H);
+hipError_t launch_decoder_split(int H, const float* frags, float* decb, hipStream_t st);
 hipError_t launch_gan(const FwdArgs& a, hipStream_t st);
+// K3 on split-bf16 MFMAs (pgp_gansplit.hip): plane floats (0: not compiled at
+// this H), their derivation from the fp32 fragments, the launch
+long gan_split_floats(int H);
+hipError_t launch_gan_split_derive(int H, const float* frags, float* planes, hipStream_t st);
+hipError_t launch_gan_split(const FwdArgs& a, hipStream_t st);
 
 // training ops (pgp_train.hip)
 struct AdamArgs;
@@ -119,6 +130,53 @@ hipError_t launch_simulate(int H, int E, const double* envs, const float* new_sc
 #define PGP_DEV __device__ __forceinline__
 
 PGP_DEV f32x4 mfma(float a, float b, f32x4 c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
+// ---- split-bf16 contraction (K2b, K3): x = x0 + x1 + x2 exactly, each a bf16 ----
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+PGP_DEV unsigned bf16_bits(float x) {  // round to nearest even (finite inputs)
+  const unsigned u = __float_as_uint(x);
+  return (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
+}
+PGP_DEV float bf16_val(unsigned h) { return __uint_as_float(h << 16); }
+// 8 floats -> their three bf16 planes, packed as 4 dwords each (element 2d in
+// the low half of dword d, 2d + 1 in the high half): one 16x16x32 operand each
+PGP_DEV void split8(const float (&v)[8], u32x4 (&p)[3]) {
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    unsigned h[3][2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const float x = v[2 * d + q];
+      h[0][q] = bf16_bits(x);
+      const float r1 = x - bf16_val(h[0][q]);
+      h[1][q] = bf16_bits(r1);
+      h[2][q] = bf16_bits(r1 - bf16_val(h[1][q]));
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) p[k][d] = h[k][0] | (h[k][1] << 16);
+  }
+}
+PGP_DEV f32x4 mfma_bf(u32x4 a, u32x4 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0,
+                                                 0, 0);
+}
+// w . x over one 32-k block as the six products with i + j <= 2, smallest first
+PGP_DEV f32x4 mfma_bf6(const u32x4 (&w)[3], const u32x4 (&x)[3], f32x4 c) {
+  c = mfma_bf(w[2], x[0], c);
+  c = mfma_bf(w[1], x[1], c);
+  c = mfma_bf(w[0], x[2], c);
+  c = mfma_bf(w[1], x[0], c);
+  c = mfma_bf(w[0], x[1], c);
+  return mfma_bf(w[0], x[0], c);
+}
+// the same when x is exactly a bf16 (x1 = x2 = 0, e.g. a one-hot schedule): three
+// products, the same sums as mfma_bf6 (its other three add exact zeros)
+PGP_DEV f32x4 mfma_bf3(const u32x4 (&w)[3], const u32x4 (&x)[3], f32x4 c) {
+  c = mfma_bf(w[2], x[0], c);
+  c = mfma_bf(w[1], x[0], c);
+  return mfma_bf(w[0], x[0], c);
+}
+
 // In-launch last-arriver finish (cdna_hip_programming.md, split-K recipe, the
 // write-through form): every partial the other workgroups read was stored
 // write-through (__hip_atomic_store relaxed / agent = sc1 stores), so no

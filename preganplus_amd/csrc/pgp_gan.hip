@@ -444,6 +444,7 @@ hipError_t launch(const FwdArgs& a, hipStream_t st) {
 }  // namespace
 
 hipError_t launch_gan(const FwdArgs& a, hipStream_t st) {
+  if (a.ganb != nullptr && gan_split_floats(a.H) > 0) return launch_gan_split(a, st);
   switch (a.H) {
 #define CASE(h) \
   case h:       \

@@ -84,6 +84,16 @@ class DecisionModel:
     def reserve(self, max_batch: int):
         _native.check(self._L.pgp_reserve(self._h, int(max_batch)), "pgp_reserve")
 
+    def gan_split(self, on: bool):
+        """K3 on split-bf16 MFMAs (True: the default where compiled, H = 50) or
+        on the fp32 MFMA (False); ``pgp_gan_split``."""
+        _native.check(self._L.pgp_gan_split(self._h, int(bool(on))), "pgp_gan_split")
+
+    def decoder_split(self, on: bool):
+        """K2b on split-bf16 MFMAs (True: the default where compiled, H = 32 and
+        50) or on the fp32 MFMA (False); ``pgp_decoder_split``."""
+        _native.check(self._L.pgp_decoder_split(self._h, int(bool(on))), "pgp_decoder_split")
+
     def alloc_outputs(self, B: int, latent: bool = False, packed: bool = False):
         """Output tensors of forward().  packed=True places them all in one
         device buffer (every output is 4-byte) with a pinned host twin, so

@@ -10,6 +10,7 @@ from __future__ import annotations
 
 PEAK_FP32_TFLOPS = 157.3   # MI355X dense fp32 (VALU = f32 MFMA), MI355X_MICROARCH.md
 PEAK_HBM_GBS = 8000.0      # MI355X HBM3E spec
+PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (no sparsity), MI355X_MICROARCH.md
 
 W = 3
 FF = 64
@@ -126,6 +127,28 @@ def encoder_io_bytes_per_window(H: int) -> int:
 def decoder_flops_per_window(H: int) -> int:
     """K2b (decoder_kernel): anomaly + prototype decoders."""
     return flops_per_window(H)["decoders"]
+
+
+def decoder_split(H: int) -> bool:
+    """K2b runs the split-bf16 form at these H (pgp_decoder.hip dec_split: the
+    LDS ring of one (host, step) chunk's three weight planes fits)."""
+    return H in (32, 50)
+
+
+def gan_split(H: int) -> bool:
+    """K3 runs the split-bf16 form (pgp_gansplit.hip) at these H."""
+    return H == 50
+
+
+def decoder_split_flops_per_window(H: int) -> int:
+    """bf16 MFMA flops K2b's split form executes per window: per (host, step)
+    chunk ceil(KS/8) blocks of 8 k-steps (KS = ceil(H/4) k-steps of 4), per
+    16-row output tile (ceil(4H/16)) 6 v_mfma_f32_16x16x32_bf16 of
+    16 x 16 x 32 x 2 flops, shared by the 16 windows of a wave."""
+    ks = (H + 3) // 4
+    nb = ((ks + 3) // 4 + 1) // 2
+    mt = (4 * H + 15) // 16
+    return H * W * nb * mt * 6 * 16 * 16 * 32 * 2 // 16
 
 
 def gan_flops_per_window(H: int) -> int:

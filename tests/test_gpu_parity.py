@@ -59,6 +59,23 @@ def test_reference_fixtures(H):
     assert np.array_equal(got["keep"], ref["keep"])
 
 
+def test_reference_fixture_both_branches_h16():
+    """H=16 windows on both sides of run_model's gates (no flagged host / some;
+    discriminator keeps / overrides; make_golden_branches16.py): every decision
+    exactly the reference's."""
+    from tests.test_oracle_golden import branches16_weights
+    z = np.load(f"{GOLD}/fwd_h16_branches.npz")
+    w = branches16_weights(z)
+    ref = {k: z[k] for k in z.files}
+    ref["sched32"] = z["sched"].astype(np.float32)
+    m = get_model(16, w, "branches16")
+    got = run(m, ref["windows"], ref["sched"], latent=True)
+    assert_parity(got, ref, w, ref["sched"], exact=True)
+    for k in ("any", "keep", "cls", "gen_target", "final_target"):
+        assert np.array_equal(got[k], ref[k]), k
+    assert 0 < got["any"].sum() < got["any"].size and 0 < got["keep"].sum() < got["keep"].size
+
+
 @pytest.mark.parametrize("H", [16, 50])
 def test_stage_split_equals_fused_call(H):
     w, ref = fixture(H)
@@ -91,6 +108,73 @@ def test_synthetic_vs_oracle_ragged_batch(H):
     m = get_model(H, w, f"syn{H}")
     got = run(m, x, s, latent=True)
     assert_parity(got, ref, w, s)
+
+
+@pytest.mark.parametrize("H", [32, 50])
+def test_split_bf16_decoder_vs_fp32_decoder(H):
+    """K2b's split-bf16 form (the default at H = 32, 50: six bf16 MFMAs per fp32
+    product, pgp_decoder.hip) and its fp32-MFMA form on the same latent: both
+    within the north-star tolerance of the fp64 oracle, their logits within a
+    few fp32 ulps of the contraction's magnitude of each other, and every
+    decision equal (on these inputs no decision sits in band)."""
+    rng = np.random.Generator(np.random.PCG64(300 + H))
+    w = W.synth_weights(H, seed=3)
+    x, s = c2(rng, 517, H, dense=9)
+    ref = O.forward(w, x, s)
+    ref["sched32"] = s.astype(np.float32)
+    m = get_model(H, w, f"dsplit{H}")
+    m.decoder_split(True)
+    a = run(m, x, s)
+    m.decoder_split(False)
+    b = run(m, x, s)
+    m.decoder_split(True)
+    assert_parity(a, ref, w, s)
+    assert_parity(b, ref, w, s)
+    # the split form is no less accurate than the fp32 MFMA (tools/micro/bf16_split.hip:
+    # the same error level): its worst logit / proto error against the fp64 oracle
+    # within twice the fp32 form's (both far inside the north-star tolerance)
+    for k in ("logits", "protos"):
+        ea = np.abs(a[k].astype(np.float64) - ref[k]).max()
+        eb = np.abs(b[k].astype(np.float64) - ref[k]).max()
+        assert ea <= 2 * eb + 1e-7, (k, ea, eb)
+    for k in ("cls", "any", "keep", "final_target", "gen_target"):
+        assert np.array_equal(a[k], b[k]), k
+    assert not np.array_equal(a["logits"], b["logits"])   # the two forms really ran
+
+
+@pytest.mark.parametrize("dense", [0, 40])
+def test_split_bf16_gan_vs_fp32_gan(dense):
+    """K3's split-bf16 form (the default at H = 50, pgp_gansplit.hip; one-hot
+    schedule blocks in three products, dense ones in six) and its fp32-MFMA
+    form: both within tolerance of the fp64 oracle, probabilities within fp32
+    rounding of each other, every decision equal, and the one-hot shortcut
+    bitwise equal to the six-product form (its other products add exact zeros:
+    here checked by a batch whose dense windows take the six-product path in
+    the same launch)."""
+    H = 50
+    rng = np.random.Generator(np.random.PCG64(77 + dense))
+    w = W.synth_weights(H, seed=5)
+    x, s = c2(rng, 300, H, dense=dense)
+    ref = O.forward(w, x, s)
+    ref["sched32"] = s.astype(np.float32)
+    m = get_model(H, w, "gsplit50")
+    m.gan_split(True)
+    a = run(m, x, s)
+    m.gan_split(False)
+    b = run(m, x, s)
+    m.gan_split(True)
+    assert_parity(a, ref, w, s)
+    assert_parity(b, ref, w, s)
+    ea = np.abs(a["probs"].astype(np.float64) - ref["probs"]).max()
+    eb = np.abs(b["probs"].astype(np.float64) - ref["probs"]).max()
+    assert ea <= 2 * eb + 1e-7, (ea, eb)
+    for k in ("keep", "final_target", "gen_target", "any", "cls"):
+        assert np.array_equal(a[k], b[k]), k
+    # a window's outputs do not depend on the other windows of its wave (the
+    # one-hot shortcut is chosen per wave): the first 16 alone give the same bits
+    c = run(m, x[:16], s[:16])
+    for k in a:
+        assert np.array_equal(a[k][:16], c[k]), k
 
 
 def test_edge_inputs_h16():

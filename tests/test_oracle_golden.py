@@ -127,3 +127,33 @@ def test_fpe50_oracle_matches_reference(part):
     np.testing.assert_array_equal(out32["cls"], z[f"{part}cls"])
     if part:
         assert 0 < z["b/any"].sum() < z["b/any"].size   # both run_model branches (PreGAN.py:112-113)
+
+
+def branches16_weights(z):
+    """tests/golden/fwd_h16_branches.npz's weights: the shipped H=16 checkpoints
+    with the stored anomaly-decoder and discriminator bias offsets."""
+    import copy
+    w, _ = W.load_npz("preganplus_amd/data/simulator_16.npz")
+    w = copy.deepcopy(w)
+    b = np.array(w["transformer"]["anomaly_decoder.0.bias"], dtype=np.float64)
+    b[1::2] -= z["anomaly_bias_shift"]
+    w["transformer"]["anomaly_decoder.0.bias"] = b
+    db = np.array(w["disc"]["probs.2.bias"], dtype=np.float64)
+    db[0] += float(z["disc_bias_shift"])
+    w["disc"]["probs.2.bias"] = db
+    return w
+
+
+def test_oracle_matches_reference_both_branches_h16():
+    """Both gates of run_model at H=16 (make_golden_branches16.py): windows that
+    flag no host (the early return, PreGANPlus.py:125-127) and windows whose
+    discriminator keeps the original decision (:87-88), from the reference's
+    own modules on the shipped weights with stored bias offsets."""
+    z = np.load(f"{GOLD}/fwd_h16_branches.npz")
+    w = branches16_weights(z)
+    assert 0 < z["any"].sum() < z["any"].size and 0 < z["keep"].sum() < z["keep"].size
+    out = O.forward(w, z["windows"], z["sched"])
+    for k in ["logits", "protos", "emb", "new_sched", "probs"]:
+        np.testing.assert_allclose(out[k], z[k], rtol=0, atol=1e-12, err_msg=k)
+    for k in ["cls", "any", "keep", "final_target", "gen_target"]:
+        np.testing.assert_array_equal(out[k], z[k], err_msg=k)

@@ -49,6 +49,30 @@ for step in "$@"; do
       run bf16split 120 tools/micro/bf16_split 256 7680
       cat $OUT/bf16split.out
       ;;
+    tdec)
+      run t_dec 900 $PYT tests/test_gpu_parity.py -m gpu -k "split or reference_fixtures or ragged or stage_split or census"
+      tail -2 $OUT/t_dec.out
+      ;;
+    c2ab)
+      run c2split 300 python3 -u bench.py --steps 100 --warmup 5 --no-cpu-baseline
+      run c2fp32 300 python3 -u bench.py --steps 100 --warmup 5 --no-cpu-baseline --fp32-decoder --fp32-gan
+      run c2fp32g 300 python3 -u bench.py --steps 100 --warmup 5 --no-cpu-baseline --fp32-gan
+      grep -h -o "\"ms_per_step\": [0-9.]*\|\"decoder\": [0-9.]*\|\"gan\": [0-9.]*" $OUT/c2split.out $OUT/c2fp32.out $OUT/c2fp32g.out
+      ;;
+    tfleet)
+      run t_fleet 600 $PYT tests/test_gpu_fleet_stream.py -m gpu
+      tail -2 $OUT/t_fleet.out
+      run fleet 400 python3 -u bench.py --config fleet --steps 100 --warmup 5 --no-cpu-baseline
+      ;;
+    abbwd)
+      PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_bwdfirst.so run t_bwd 600 $PYT tests/test_gpu_c3step.py -m gpu
+      run abb16 600 python3 -u tools/ab_bench.py --rounds 4 --args "--config tune --hosts 16 --steps 100 --warmup 10 --no-cpu-baseline" base= bwd=PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_bwdfirst.so
+      grep median $OUT/abb16.out
+      ;;
+    ttrain)
+      run t_train 900 $PYT tests/test_gpu_train.py tests/test_gpu_c3step.py tests/test_gpu_dist.py -m gpu
+      tail -2 $OUT/t_train.out
+      ;;
     tfpe4)
       run t_fpe4 900 $PYT tests/test_gpu_fpe.py -m gpu
       tail -2 $OUT/t_fpe4.out
