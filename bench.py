@@ -951,6 +951,17 @@ def bench_fpe(args):
                     "reference_formulation_flops_per_window": R.fpe_flops_per_window(H),
                     "hbm_gbs": fpe_bytes / (k[0] * 1e-3) / 1e9,
                     "hbm_frac": fpe_bytes / (k[0] * 1e-3) / 1e9 / R.PEAK_HBM_GBS}
+        elif R.gan_split(H):
+            # K3 on split-bf16 MFMAs (pgp_gansplit.hip): priced on the bf16 flops it executes
+            # (one-hot schedules: their blocks take 3 products) against the dense bf16 peak
+            exe = R.gan_split_flops_per_window(H, onehot=True)
+            ach = exe * B / (k[1] * 1e-3) / 1e12
+            roof = {"kernel": f"gan_split_kernel<{H}> (K3, split-bf16)", "bound": "mfma", "achieved": ach,
+                    "peak": R.PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": ach / R.PEAK_BF16_TFLOPS,
+                    "traffic": None, "basis": "executed v_mfma_f32_16x16x32_bf16 flops (roofline."
+                                              "gan_split_flops_per_window) / HIP-event launch time",
+                    "flops_per_window": exe,
+                    "fp32_equivalent_tflops": gan_fl / (k[1] * 1e-3) / 1e12}
         else:
             ach = gan_fl / (k[1] * 1e-3) / 1e12
             roof = {"kernel": "gan_kernel (K3)", "bound": "mfma", "achieved": ach, "peak": R.PEAK_FP32_TFLOPS,

@@ -228,10 +228,18 @@ __global__ __launch_bounds__(256) void dec_split_kernel(const float* __restrict_
   for (int k = 0; k < 3; ++k) *reinterpret_cast<u32x4*>(out + (f * 3 + k) * 256 + lane * 4) = p[k];
 }
 
-template <int H>
-__global__ __launch_bounds__(kDecWaves * 64, 1) void decoder_split_kernel(FwdArgs a) {
+// TW window tiles (16 windows each) per wave, 16 / TW waves per workgroup (256
+// windows, as decoder_kernel): each weight plane read from LDS feeds TW MFMAs
+#ifndef PGP_DEC_TW
+#define PGP_DEC_TW 1
+#endif
+constexpr int kDecTW = PGP_DEC_TW;
+
+template <int H, int TW>
+__global__ __launch_bounds__(kDecWaves / TW * 64, 1) void decoder_split_kernel(FwdArgs a) {
   using G = Geo<H>;
   using D = DecB<H>;
+  constexpr int NWD = kDecWaves / TW;
   __shared__ __attribute__((aligned(16))) float smem[D::TOTAL];
   float* tdec = smem + 2 * D::SLOT;  // decoder bias [MT_O * 16]
   float* P = tdec + G::MT_O * 16;    // prototypes [K][2]
@@ -240,107 +248,121 @@ __global__ __launch_bounds__(kDecWaves * 64, 1) void decoder_split_kernel(FwdArg
 
   const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const long blk = (long)blockIdx.x * kDecWaves + wv;
+  const long blk0 = (long)blockIdx.x * kDecWaves + wv * TW;
   const long nblk = (a.B + 15) / 16;
-  const bool active = blk < nblk;
-  const float* lat = a.lat + (active ? blk : 0) * G::LAT_BLK;
   constexpr int NCH = H * kWindow;
-  auto load_b = [&](int c, bool ok, float (&v)[G::KS_D]) {
-    const float* lc = lat + (long)c * G::KS_D * 64;
+  auto load_b = [&](int t, int c, bool ok, float (&v)[G::KS_D]) {
+    const bool act = blk0 + t < nblk;
+    const float* lc = a.lat + (act ? blk0 + t : 0) * G::LAT_BLK + (long)c * G::KS_D * 64;
+    ok = ok && act;
 #pragma unroll
     for (int q = 0; q < G::LAT_FG; ++q) {
-      const f32x4 t = ok ? ld4(lc + q * 256 + lane * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+      const f32x4 u = ok ? ld4(lc + q * 256 + lane * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[4 * q + e] = t[e];
+      for (int e = 0; e < 4; ++e) v[4 * q + e] = u[e];
     }
 #pragma unroll
     for (int r = 0; r < G::KS_D % 4; ++r) v[4 * G::LAT_FG + r] = ok ? lc[G::LAT_FG * 256 + r * 64 + lane] : 0.f;
   };
   float* cur = smem;
   float* nxt = smem + D::SLOT;
-  dma_groups(a.decb, cur, D::FRC, wv, kDecWaves, lane);
-  float b[G::KS_D];
-  load_b(0, active, b);
-  __syncthreads();
-  if (NCH > 1) dma_groups(a.decb + (long)D::SLOT, nxt, D::FRC, wv, kDecWaves, lane);
-
-  f32x4 acc[G::MT_O];
+  dma_groups(a.decb, cur, D::FRC, wv, NWD, lane);
+  float b[TW][G::KS_D];
 #pragma unroll
-  for (int mt = 0; mt < G::MT_O; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int t = 0; t < TW; ++t) load_b(t, 0, true, b[t]);
+  __syncthreads();
+  if (NCH > 1) dma_groups(a.decb + (long)D::SLOT, nxt, D::FRC, wv, NWD, lane);
+
+  f32x4 acc[TW][G::MT_O];
+#pragma unroll
+  for (int t = 0; t < TW; ++t)
+#pragma unroll
+    for (int mt = 0; mt < G::MT_O; ++mt) acc[t][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
 #pragma unroll 1
   for (int c = 0; c < NCH; ++c) {
-    float bn[G::KS_D];
-    load_b(c + 1, active && c + 1 < NCH, bn);
+    float bn[TW][G::KS_D];
+#pragma unroll
+    for (int t = 0; t < TW; ++t) load_b(t, c + 1, c + 1 < NCH, bn[t]);
 #pragma unroll
     for (int kb = 0; kb < D::NB; ++kb) {
-      float v[8];
+      u32x4 x[TW][3];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = 8 * kb + e < G::KS_D ? b[8 * kb + e] : 0.f;
-      u32x4 x[3];
-      split8(v, x);
+      for (int t = 0; t < TW; ++t) {
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = 8 * kb + e < G::KS_D ? b[t][8 * kb + e] : 0.f;
+        split8(v, x[t]);
+      }
 #pragma unroll
       for (int mt = 0; mt < G::MT_O; ++mt) {
         const float* F = cur + ((kb * G::MT_O + mt) * 3) * 256 + lane * 4;
         const u32x4 w[3] = {*reinterpret_cast<const u32x4*>(F), *reinterpret_cast<const u32x4*>(F + 256),
                             *reinterpret_cast<const u32x4*>(F + 512)};
-        acc[mt] = mfma_bf6(w, x, acc[mt]);
+#pragma unroll
+        for (int t = 0; t < TW; ++t) acc[t][mt] = mfma_bf6(w, x[t], acc[t][mt]);
       }
     }
 #pragma unroll
-    for (int s = 0; s < G::KS_D; ++s) b[s] = bn[s];
+    for (int t = 0; t < TW; ++t)
+#pragma unroll
+      for (int s = 0; s < G::KS_D; ++s) b[t][s] = bn[t][s];
     __syncthreads();
-    float* t = cur;
+    float* tmp = cur;
     cur = nxt;
-    nxt = t;
-    if (c + 2 < NCH) dma_groups(a.decb + (long)(c + 2) * D::SLOT, nxt, D::FRC, wv, kDecWaves, lane);
+    nxt = tmp;
+    if (c + 2 < NCH) dma_groups(a.decb + (long)(c + 2) * D::SLOT, nxt, D::FRC, wv, NWD, lane);
   }
 
   // ---- epilogue: bias, sigmoid, detect, embed, classify (as decoder_kernel) ----
-  const long bw = blk * 16 + j;
-  const bool valid = active && bw < a.B;
-  int anyf = 0;
 #pragma unroll
-  for (int mt = 0; mt < G::MT_O; ++mt) {
-    const int host = 4 * mt + g;
-    const f32x4 v = acc[mt] + ld4(tdec + 16 * mt + 4 * g);
-    if (host < H) {
-      const float l0 = v[0], l1 = v[1];
-      const float p0 = __builtin_amdgcn_rcpf(1.0f + __expf(-v[2])), p1 = __builtin_amdgcn_rcpf(1.0f + __expf(-v[3]));
-      const bool an = l1 > l0;  // torch.argmax: ties -> index 0
-      const float e0 = an ? p0 : 0.f, e1 = an ? p1 : 0.f;
-      int cl = -1;
-      if (!(e0 == 0.f && e1 == 0.f)) {
-        float best = INFINITY;
-        for (int k = 0; k < a.K; ++k) {
-          const float d0 = e0 - P[2 * k], d1 = e1 - P[2 * k + 1];
-          const float dist = (d0 * d0 + d1 * d1) * 0.5f;  // torch.mean over PROTO_DIM = 2
-          if (dist < best) {                              // np.argmin: first minimum
-            best = dist;
-            cl = k;
+  for (int t = 0; t < TW; ++t) {
+    const long blk = blk0 + t;
+    const long bw = blk * 16 + j;
+    const bool valid = blk < nblk && bw < a.B;
+    int anyf = 0;
+#pragma unroll
+    for (int mt = 0; mt < G::MT_O; ++mt) {
+      const int host = 4 * mt + g;
+      const f32x4 v = acc[t][mt] + ld4(tdec + 16 * mt + 4 * g);
+      if (host < H) {
+        const float l0 = v[0], l1 = v[1];
+        const float p0 = __builtin_amdgcn_rcpf(1.0f + __expf(-v[2])), p1 = __builtin_amdgcn_rcpf(1.0f + __expf(-v[3]));
+        const bool an = l1 > l0;  // torch.argmax: ties -> index 0
+        const float e0 = an ? p0 : 0.f, e1 = an ? p1 : 0.f;
+        int cl = -1;
+        if (!(e0 == 0.f && e1 == 0.f)) {
+          float best = INFINITY;
+          for (int k = 0; k < a.K; ++k) {
+            const float d0 = e0 - P[2 * k], d1 = e1 - P[2 * k + 1];
+            const float dist = (d0 * d0 + d1 * d1) * 0.5f;  // torch.mean over PROTO_DIM = 2
+            if (dist < best) {                              // np.argmin: first minimum
+              best = dist;
+              cl = k;
+            }
           }
         }
-      }
-      anyf |= an ? 1 : 0;
-      if (valid) {
-        const long o = (bw * H + host) * 2;
-        a.logits[o] = l0;
-        a.logits[o + 1] = l1;
-        a.protos[o] = p0;
-        a.protos[o + 1] = p1;
-        a.cls[bw * H + host] = cl;
-        a.emb[bw * G::EP + 2 * host] = e0;
-        a.emb[bw * G::EP + 2 * host + 1] = e1;
+        anyf |= an ? 1 : 0;
+        if (valid) {
+          const long o = (bw * H + host) * 2;
+          a.logits[o] = l0;
+          a.logits[o + 1] = l1;
+          a.protos[o] = p0;
+          a.protos[o + 1] = p1;
+          a.cls[bw * H + host] = cl;
+          a.emb[bw * G::EP + 2 * host] = e0;
+          a.emb[bw * G::EP + 2 * host + 1] = e1;
+        }
       }
     }
+    {
+      const auto r = __builtin_amdgcn_permlane16_swap((unsigned)anyf, (unsigned)anyf, false, false);
+      const int a16 = (int)(r[0] | r[1]);
+      const auto q = __builtin_amdgcn_permlane32_swap((unsigned)a16, (unsigned)a16, false, false);
+      anyf = (int)(q[0] | q[1]);
+    }
+    if (valid && g == 0) a.any_anom[bw] = anyf;
   }
-  {
-    const auto r = __builtin_amdgcn_permlane16_swap((unsigned)anyf, (unsigned)anyf, false, false);
-    const int a16 = (int)(r[0] | r[1]);
-    const auto q = __builtin_amdgcn_permlane32_swap((unsigned)a16, (unsigned)a16, false, false);
-    anyf = (int)(q[0] | q[1]);
-  }
-  if (valid && g == 0) a.any_anom[bw] = anyf;
 }
 
 template <int H>
@@ -349,7 +371,7 @@ hipError_t launch(const FwdArgs& a, hipStream_t st) {
   const int grid = (int)((nblk + kDecWaves - 1) / kDecWaves);
   if constexpr (dec_split<H>()) {
     if (a.decb != nullptr) {
-      decoder_split_kernel<H><<<grid, kDecWaves * 64, 0, st>>>(a);
+      decoder_split_kernel<H, kDecTW><<<grid, kDecWaves / kDecTW * 64, 0, st>>>(a);
       return hipGetLastError();
     }
   }

@@ -236,11 +236,20 @@ __global__ __launch_bounds__(kSWaves * 64) void gan_split_kernel(FwdArgs a) {
       if (qc * kSQP + i < S::NPS) {
         float v[8];
         pair8(bq[i][0], bq[i][1], v);
+        // every value exactly a bf16 in every lane (one-hot rows: 0 / 1): the
+        // residual planes are zero and x0 is the values' high halves
+        unsigned low = 0u;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) low |= __float_as_uint(v[e]) & 0xFFFFu;
+        const bool exact = __builtin_amdgcn_ballot_w64(low != 0u) == 0ull;
         u32x4 x[3];
-        split8(v, x);
-        // exactly bf16 in every lane (one-hot rows): the residual planes are zero
-        const unsigned r = x[1][0] | x[1][1] | x[1][2] | x[1][3] | x[2][0] | x[2][1] | x[2][2] | x[2][3];
-        const bool exact = __builtin_amdgcn_ballot_w64(r != 0u) == 0ull;
+        if (exact) {
+#pragma unroll
+          for (int d = 0; d < 4; ++d)
+            x[0][d] = (__float_as_uint(v[2 * d]) >> 16) | (__float_as_uint(v[2 * d + 1]) & 0xFFFF0000u);
+        } else {
+          split8(v, x);
+        }
         const float* F = cur + i * S::FS * 256;
         if (exact) {
 #pragma unroll

@@ -140,6 +140,22 @@ def gan_split(H: int) -> bool:
     return H == 50
 
 
+def gan_split_flops_per_window(H: int, onehot: bool = True) -> int:
+    """bf16 MFMA flops K3's split form (pgp_gansplit.hip) executes per window:
+    v_mfma_f32_16x16x32_bf16 (16 x 16 x 32 x 2 flops for 16 windows) counted
+    per phase: Gen1 embedding pairs x 4 hidden tiles x 6; the schedule pass,
+    pairs of 16-column blocks x 8 tiles (Gen1 | Disc1) x 3 (one-hot rows are
+    exact in bf16) or 6; per container Gen2 (4 output tiles x 2 hidden pairs)
+    and Disc1's new half (4 tiles x its pairs), 6 each."""
+    ep = (2 * H + 15) // 16
+    npe = (ep + 1) // 2
+    nps = ((H * H + 15) // 16 + 1) // 2
+    mtn = (H + 15) // 16
+    npn = (mtn + 1) // 2
+    n = npe * 4 * 6 + nps * 8 * (3 if onehot else 6) + H * (mtn * 2 * 6 + 4 * npn * 6)
+    return n * 16 * 16 * 32 * 2 // 16
+
+
 def decoder_split_flops_per_window(H: int) -> int:
     """bf16 MFMA flops K2b's split form executes per window: per (host, step)
     chunk ceil(KS/8) blocks of 8 k-steps (KS = ceil(H/4) k-steps of 4), per

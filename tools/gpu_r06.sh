@@ -73,6 +73,15 @@ for step in "$@"; do
       run t_train 900 $PYT tests/test_gpu_train.py tests/test_gpu_c3step.py tests/test_gpu_dist.py -m gpu
       tail -2 $OUT/t_train.out
       ;;
+    abdec)
+      run abdec 900 python3 -u tools/ab_bench.py --rounds 5 --args "--steps 100 --warmup 5 --no-cpu-baseline" base= tw2=PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_dectw2.so
+      grep median $OUT/abdec.out
+      python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); [print(k, [{kk: round(vv, 4) for kk, vv in e['kernel_ms'].items()} for e in v]) for k, v in d['extra'].items()]" $OUT/abdec.out
+      ;;
+    tbr)
+      run t_br 600 $PYT tests/test_gpu_parity.py -m gpu -k "branches or split"
+      tail -2 $OUT/t_br.out
+      ;;
     tfpe4)
       run t_fpe4 900 $PYT tests/test_gpu_fpe.py -m gpu
       tail -2 $OUT/t_fpe4.out
