@@ -224,7 +224,9 @@ def main():
         alg = R.encoder_flops_per_window(H)
         achieved = (exe if exe is not None else alg) * B / k2_s / 1e12
         traffic = load_traffic(H, B)
-        k_traffic = {k: load_traffic(H, B, k) for k in ("gat_agg", "encoder", "decoder", "gan")}
+        kn = {"gat_agg": "gat_agg", "encoder": "encoder", "decoder": "decoder_split" if split else "decoder",
+              "gan": "gan_split" if gsplit else "gan"}
+        k_traffic = {k: load_traffic(H, B, v) for k, v in kn.items()}
         path_bytes = R.path_bytes_per_window(H) * B
         res = {
             "metric": "host-windows/sec (detect+diagnose+generate)",

@@ -230,10 +230,17 @@ __global__ __launch_bounds__(256) void dec_split_kernel(const float* __restrict_
 
 // TW window tiles (16 windows each) per wave, 16 / TW waves per workgroup (256
 // windows, as decoder_kernel): each weight plane read from LDS feeds TW MFMAs
+// (A/B, C2 at H = 50, 5 interleaved rounds: TW = 2 5.90 ms against TW = 1
+// 6.14 ms; profiles/r06/c2ab/abdec.txt)
 #ifndef PGP_DEC_TW
-#define PGP_DEC_TW 1
+#define PGP_DEC_TW 2
 #endif
 constexpr int kDecTW = PGP_DEC_TW;
+// latent chunks in flight ahead of the one being contracted (registers)
+#ifndef PGP_DEC_PF
+#define PGP_DEC_PF 1
+#endif
+constexpr int kDecPF = PGP_DEC_PF;
 
 template <int H, int TW>
 __global__ __launch_bounds__(kDecWaves / TW * 64, 1) void decoder_split_kernel(FwdArgs a) {
@@ -267,9 +274,13 @@ __global__ __launch_bounds__(kDecWaves / TW * 64, 1) void decoder_split_kernel(F
   float* cur = smem;
   float* nxt = smem + D::SLOT;
   dma_groups(a.decb, cur, D::FRC, wv, NWD, lane);
-  float b[TW][G::KS_D];
+  float b[TW][G::KS_D], b1[TW][G::KS_D];
 #pragma unroll
   for (int t = 0; t < TW; ++t) load_b(t, 0, true, b[t]);
+  if constexpr (kDecPF > 1) {
+#pragma unroll
+    for (int t = 0; t < TW; ++t) load_b(t, 1, NCH > 1, b1[t]);
+  }
   __syncthreads();
   if (NCH > 1) dma_groups(a.decb + (long)D::SLOT, nxt, D::FRC, wv, NWD, lane);
 
@@ -283,7 +294,7 @@ __global__ __launch_bounds__(kDecWaves / TW * 64, 1) void decoder_split_kernel(F
   for (int c = 0; c < NCH; ++c) {
     float bn[TW][G::KS_D];
 #pragma unroll
-    for (int t = 0; t < TW; ++t) load_b(t, c + 1, c + 1 < NCH, bn[t]);
+    for (int t = 0; t < TW; ++t) load_b(t, c + kDecPF, c + kDecPF < NCH, bn[t]);
 #pragma unroll
     for (int kb = 0; kb < D::NB; ++kb) {
       u32x4 x[TW][3];
@@ -306,7 +317,14 @@ __global__ __launch_bounds__(kDecWaves / TW * 64, 1) void decoder_split_kernel(F
 #pragma unroll
     for (int t = 0; t < TW; ++t)
 #pragma unroll
-      for (int s = 0; s < G::KS_D; ++s) b[t][s] = bn[t][s];
+      for (int s = 0; s < G::KS_D; ++s) {
+        if constexpr (kDecPF > 1) {
+          b[t][s] = b1[t][s];
+          b1[t][s] = bn[t][s];
+        } else {
+          b[t][s] = bn[t][s];
+        }
+      }
     __syncthreads();
     float* tmp = cur;
     cur = nxt;

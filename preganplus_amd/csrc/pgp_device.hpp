@@ -139,21 +139,23 @@ PGP_DEV unsigned bf16_bits(float x) {  // round to nearest even (finite inputs)
 }
 PGP_DEV float bf16_val(unsigned h) { return __uint_as_float(h << 16); }
 // 8 floats -> their three bf16 planes, packed as 4 dwords each (element 2d in
-// the low half of dword d, 2d + 1 in the high half): one 16x16x32 operand each
+// the low half of dword d, 2d + 1 in the high half): one 16x16x32 operand each.
+// Per pair: v_cvt_pk_bf16_f32 (round to nearest even, as bf16_bits), the part
+// back as two floats, a packed subtract for the exact residual; 9 VALU per pair
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+PGP_DEV unsigned bf16_pack(f32x2 x) { return __builtin_bit_cast(unsigned, __builtin_convertvector(x, bf16x2)); }
+PGP_DEV f32x2 bf16_unpack(unsigned h) { return f32x2{__uint_as_float(h << 16), __uint_as_float(h & 0xFFFF0000u)}; }
 PGP_DEV void split8(const float (&v)[8], u32x4 (&p)[3]) {
 #pragma unroll
   for (int d = 0; d < 4; ++d) {
-    unsigned h[3][2];
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const float x = v[2 * d + q];
-      h[0][q] = bf16_bits(x);
-      const float r1 = x - bf16_val(h[0][q]);
-      h[1][q] = bf16_bits(r1);
-      h[2][q] = bf16_bits(r1 - bf16_val(h[1][q]));
-    }
-#pragma unroll
-    for (int k = 0; k < 3; ++k) p[k][d] = h[k][0] | (h[k][1] << 16);
+    const f32x2 x = {v[2 * d], v[2 * d + 1]};
+    const unsigned h0 = bf16_pack(x);
+    const f32x2 r1 = x - bf16_unpack(h0);
+    const unsigned h1 = bf16_pack(r1);
+    const f32x2 r2 = r1 - bf16_unpack(h1);
+    p[0][d] = h0;
+    p[1][d] = h1;
+    p[2][d] = bf16_pack(r2);
   }
 }
 PGP_DEV f32x4 mfma_bf(u32x4 a, u32x4 b, f32x4 c) {

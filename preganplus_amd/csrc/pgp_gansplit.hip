@@ -303,11 +303,12 @@ __global__ __launch_bounds__(kSWaves * 64) void gan_split_kernel(FwdArgs a) {
     split8(v, hx[p]);
   }
   float sv[G::MT_N][4];
-  load_row(0, sv);
   for (int c = 0; c < G::C; ++c) {
     const float* cw = cur;  // CPC = 1: this container's planes
-    float svn[G::MT_N][4];
-    load_row(c + 1, svn);
+    // this container's schedule row, requested before Gen2's MFMAs (which
+    // cover its latency; a row prefetched a container ahead spilled at the
+    // 128-register budget of 4 waves per SIMD)
+    load_row(c, sv);
     // Gen2: ns = b2[c] + W2[c] . hg
     f32x4 ns[G::MT_N];
     const float* bias = cur + S::FC * 256;
@@ -382,10 +383,6 @@ __global__ __launch_bounds__(kSWaves * 64) void gan_split_kernel(FwdArgs a) {
       tg[(G::C + c) * 16 + j] = (signed char)bs_i;
     }
     advance();
-#pragma unroll
-    for (int t = 0; t < G::MT_N; ++t)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) sv[t][r] = svn[t][r];
   }
 
   // the wave's targets: its windows' rows are contiguous in gen_t / final_t

@@ -26,3 +26,21 @@ def test_tune_bench_single_and_two_streams(one_stream):
     assert len(lines) == 1
     res = json.loads(lines[0])
     assert res["value"] > 0 and res["n_gpus"] == 1
+
+
+@pytest.mark.timeout(240)
+def test_fleet_stream_line():
+    """bench.py --config fleet --stream: the PCIe-inclusive rate is the line's
+    value (the whole share streamed from pinned host memory), the kernel-only
+    rate beside it; both measured, the streamed one no faster than the
+    resident one (it does the same launches plus the copies)."""
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--config", "fleet", "--stream", "--batch",
+                        "65536", "--steps", "5", "--warmup", "1", "--no-cpu-baseline"], cwd=ROOT,
+                       capture_output=True, text=True, timeout=220)
+    assert p.returncode == 0, p.stderr[-3000:]
+    res = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    s, k = res["streamed"], res["kernel_only"]
+    assert res["value"] == s["value"] > 0 and k["value"] > 0
+    assert s["value"] <= 1.05 * k["value"]
+    assert s["chunks"] * s["chunk_windows"] >= 64 * 1_000_000 and s["h2d_gbs"] > 0
+    assert "streamed" in res["config"]["timing"]

@@ -122,7 +122,7 @@ def test_native_sync_updates_tune_state_and_dptuner():
             sb.run()
         torch.cuda.synchronize()
         sb.sync()
-    dev = TR.TuneState(np.zeros_like(st0))
+    dev = TR.TuneState(np.zeros_like(sb.st.protos))
     dev.from_device(sb.tun.state)
     np.testing.assert_array_equal(sb.st.protos, dev.protos)
     assert sb.st.factor < TR.PROTO_UPDATE_FACTOR   # decayed on the device, now on the host

@@ -92,6 +92,19 @@ for step in "$@"; do
       run prof_fpe50 240 rocprofv3 --kernel-trace --stats -d $OUT/prof_fpe50 -o fpe --output-format csv -- python3 bench.py --config fpe --hosts 50 --steps 60 --warmup 10 --no-cpu-baseline
       run prof_fpe16 240 rocprofv3 --kernel-trace --stats -d $OUT/prof_fpe16 -o fpe --output-format csv -- python3 bench.py --config fpe --hosts 16 --steps 60 --warmup 10 --no-cpu-baseline
       ;;
+    abpf)
+      run abpf 900 python3 -u tools/ab_bench.py --rounds 5 --args "--steps 100 --warmup 5 --no-cpu-baseline" base= pf2=PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_decpf2.so
+      grep median $OUT/abpf.out
+      python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); [print(k, [{kk: round(vv, 4) for kk, vv in e['kernel_ms'].items()} for e in v]) for k, v in d['extra'].items()]" $OUT/abpf.out
+      ;;
+    tmodes)
+      run t_modes 600 $PYT tests/test_gpu_bench_modes.py tests/test_gpu_parity.py -m gpu -k "stream or split or branches or reference or ragged"
+      tail -2 $OUT/t_modes.out
+      ;;
+    c2l2)
+      pmc c2l2 "TCC_HIT_sum TCC_MISS_sum" --steps 3 --warmup 1 --no-cpu-baseline
+      pmc c2fetch FETCH_SIZE --steps 3 --warmup 1 --no-cpu-baseline
+      ;;
     fpepmc)
       pmc fpestall1 "$STALL1" --config fpe --hosts 50 --steps 3 --warmup 1 --no-cpu-baseline
       pmc fpestall2 "$STALL2" --config fpe --hosts 50 --steps 3 --warmup 1 --no-cpu-baseline
