@@ -1005,13 +1005,15 @@ def gobi_flops(its, E):
 
 
 def gobi_roofline(its, E, k_ms):
-    """GOBI's roofline field: fp32 MFMA peak; achieved = algorithmic flops per
-    launch / the launch's HIP-event time.  The iterations of one environment
-    are a dependent chain (each step's input is the last step's output), so
-    the kernel is latency-bound and far below the peak by construction; the
-    line shows how far."""
+    """GOBI's roofline field: the fp32 VALU peak (the kernel's dot products
+    are VALU FMAs, not MFMAs; the same 157.3 TF); achieved = algorithmic flops
+    per launch / the launch's HIP-event time.  The iterations of one
+    environment are a dependent chain (each step's input is the last step's
+    output), so the kernel is latency-bound and far below the peak by
+    construction; the line shows how far."""
     ach = gobi_flops(its, E) / (k_ms * 1e-3) / 1e12
-    return {"kernel": "gobi_kernel", "bound": "mfma", "achieved": ach, "peak": R.PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+    return {"kernel": "gobi_kernel", "bound": "latency (dependent VALU chain; priced on the fp32 VALU peak)",
+            "achieved": ach, "peak": R.PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
             "frac": ach / R.PEAK_FP32_TFLOPS, "kernel_ms": k_ms,
             "basis": "algorithmic flops (forward + input gradient per iteration, mean iterations + 2) / HIP-event "
                      "time of the launch on its stream; latency-bound dependent iteration chain",

@@ -1,6 +1,7 @@
 // pgp_gansplit.hip — K3 (generator + discriminator + decision argmaxes,
 // models.py:118-151, 258-291; PreGANPlus.py:84-105; Stats.py:162-166) with its
-// contractions on split-bf16 MFMAs (v_mfma_f32_16x16x32_bf16), at H = 50.
+// contractions on split-bf16 MFMAs (v_mfma_f32_16x16x32_bf16), at H = 16 and 50
+// (batches of 64 K windows and more; smaller ones run gan_kernel).
 //
 // Same phases, ring and outputs as gan_kernel (pgp_gan.hip):
 //   1. Gen1, embedding columns        hg  = W1[:, :2H] . vec(emb)
@@ -29,6 +30,10 @@ namespace {
 
 constexpr int kSWaves = 16;
 constexpr int kSQP = 2;  // schedule pairs per ring chunk
+#ifndef PGP_K3_OH
+#define PGP_K3_OH 1
+#endif
+constexpr bool kK3OneHot = PGP_K3_OH != 0;  // phase 3 rebuilds one-hot rows from LDS (A/B: -DPGP_K3_OH=0)
 
 template <int H>
 struct GanS {
@@ -53,7 +58,8 @@ struct GanS {
   static constexpr int SLOT_G = mx(FE, mx(kSQP * FS, CPC * FC + 1));
   static constexpr int SLOT = SLOT_G * G::FQ;
   static constexpr int TGT = 2 * G::C * 16;  // int8 targets per wave
-  static constexpr int LDS_BYTES = 2 * SLOT * 4 + kSWaves * TGT;
+  static constexpr int OH = G::C * 16;       // int8 one-hot row index per (container, window) of a wave
+  static constexpr int LDS_BYTES = 2 * SLOT * 4 + kSWaves * (TGT + OH);
   PGP_DEV static void chunk(int k, const float* planes, const float** src, int* ng) {
     if (k == 0) {
       *src = planes + OFF_E * 256;
@@ -71,7 +77,7 @@ struct GanS {
 
 template <int H>
 constexpr bool gan_split() {
-  return H == 50 && GanS<H>::LDS_BYTES <= 160 * 1024 && Geo<H>::C < 128;
+  return (H == 16 || H == 50) && GanS<H>::LDS_BYTES <= 160 * 1024 && Geo<H>::C < 128;
 }
 
 // fp32 fragments -> planes.  One wave per destination fragment triple.
@@ -158,6 +164,17 @@ __global__ __launch_bounds__(kSWaves * 64) void gan_split_kernel(FwdArgs a) {
   const float* ew = a.emb + (valid ? b : 0) * G::EP;
   const float* gt = a.gtab;
   signed char* tg = reinterpret_cast<signed char*>(smem + 2 * S::SLOT) + wv * S::TGT;
+  // phase 2 records where each schedule row holds its 1.0 (a GOBI placement is
+  // one-hot, opt.py:9-15); phase 3 then rebuilds a row from it instead of
+  // reading the 4H-byte row from HBM again (the schedules are 2/3 of the
+  // kernel's traffic).  Rows proven one-hot only: per window exactly C nonzero
+  // values, all exactly 1.0, and every row recorded; otherwise the wave reads
+  // its rows as before.
+  signed char* oh = reinterpret_cast<signed char*>(smem + 2 * S::SLOT) + kSWaves * S::TGT + wv * S::OH;
+  if (kK3OneHot)
+    for (int i = lane; i < S::OH; i += 64) oh[i] = -1;
+  int n_one = 0, n_nz = 0;
+  bool oh_bad = false;  // wave-uniform
 
   float* cur = smem;
   float* nxt = smem + S::SLOT;
@@ -247,8 +264,31 @@ __global__ __launch_bounds__(kSWaves * 64) void gan_split_kernel(FwdArgs a) {
 #pragma unroll
           for (int d = 0; d < 4; ++d)
             x[0][d] = (__float_as_uint(v[2 * d]) >> 16) | (__float_as_uint(v[2 * d + 1]) & 0xFFFF0000u);
+          if (kK3OneHot) {
+            // bf16 halves: nonzero / exactly 1.0 (0x3F80), element e = half e
+            unsigned m_nz = 0u, m_one = 0u;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const unsigned hv = (x[0][e >> 1] >> (16 * (e & 1))) & 0xFFFFu;
+              m_nz |= ((hv & 0x7FFFu) != 0u ? 1u : 0u) << e;
+              m_one |= (hv == 0x3F80u ? 1u : 0u) << e;
+            }
+            n_nz += __builtin_popcount(m_nz);
+            n_one += __builtin_popcount(m_one);
+            if (m_one != 0u) {
+              // the lane's 8 values span at most two rows: record the lowest and
+              // the highest 1.0 (a row holding two is caught by the counts)
+              const int base = 32 * (qc * kSQP + i) + 4 * g;
+              const int elo = __builtin_ctz(m_one), ehi = 31 - __builtin_clz(m_one);
+              const int klo = base + 16 * (elo >> 2) + (elo & 3), khi = base + 16 * (ehi >> 2) + (ehi & 3);
+              const int clo = klo / H, chi = khi / H;  // flattened c * H + h
+              oh[clo * 16 + j] = (signed char)(klo - clo * H);
+              oh[chi * 16 + j] = (signed char)(khi - chi * H);
+            }
+          }
         } else {
           split8(v, x);
+          oh_bad = true;  // not all bf16: not one-hot
         }
         const float* F = cur + i * S::FS * 256;
         if (exact) {
@@ -303,12 +343,31 @@ __global__ __launch_bounds__(kSWaves * 64) void gan_split_kernel(FwdArgs a) {
     split8(v, hx[p]);
   }
   float sv[G::MT_N][4];
+  // the wave's rows are one-hot iff every window saw exactly C nonzero values,
+  // all 1.0, and every one of its C rows recorded a 1.0 (C ones over C rows,
+  // none empty: one per row)
+  bool ohw = kK3OneHot;
+  if (kK3OneHot) {
+    const float t1 = xsum((float)n_one, true), tn = xsum((float)n_nz, true);
+    bool bad = oh_bad || (valid && (t1 != (float)G::C || tn != (float)G::C));
+    for (int i = lane; i < S::OH; i += 64)
+      if (blk < nblk && blk * 16 + (i & 15) < a.B && oh[i] < 0) bad = true;
+    ohw = __builtin_amdgcn_ballot_w64(bad) == 0ull;
+  }
   for (int c = 0; c < G::C; ++c) {
     const float* cw = cur;  // CPC = 1: this container's planes
     // this container's schedule row, requested before Gen2's MFMAs (which
     // cover its latency; a row prefetched a container ahead spilled at the
     // 128-register budget of 4 waves per SIMD)
-    load_row(c, sv);
+    if (ohw) {
+      const int hc = oh[c * 16 + j];  // -1 for a window past B: a zero row, as load_row gives
+#pragma unroll
+      for (int t = 0; t < G::MT_N; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sv[t][r] = (16 * t + 4 * g + r == hc) ? 1.f : 0.f;
+    } else {
+      load_row(c, sv);
+    }
     // Gen2: ns = b2[c] + W2[c] . hg
     f32x4 ns[G::MT_N];
     const float* bias = cur + S::FC * 256;

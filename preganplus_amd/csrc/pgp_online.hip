@@ -340,16 +340,13 @@ int pgp_online_step(pgp_online* o, void* main_stream, void* gan_stream, pgp_coll
   mark(o, kG0, sg);
   mark(o, kG1, sg);
   const bool fused = cb == nullptr;  // world size 1: each GAN AdamW inside its gradient kernel
-#ifndef PGP_ONLINE_BWD_FIRST
-#define PGP_ONLINE_BWD_FIRST 0
-#endif
-  const bool bwd_first = PGP_ONLINE_BWD_FIRST && fused;
-  if (!bwd_first) OCALL(gan_part_a(o, sg, fused));
+  // (issuing the backward before the GAN part at world size 1 measured the same:
+  // 0.1851 vs 0.1853 ms at H = 16, profiles/r06/ab/abb16_bwdfirst.txt)
+  OCALL(gan_part_a(o, sg, fused));
   // then the backward
   OCHK(launch_tune_backward(o->bwd, d.P, d.G, d.tune_ws, d.logits, d.protos, d.y, d.mult, d.tgt, sm, true,
                             tgt_end));
   mark(o, kE4, sm);
-  if (bwd_first) OCALL(gan_part_a(o, sg, fused));
   // 5. the GAN's updates (its collectives on the GAN stream)
   OCALL(gan_part_b(o, sg, fused, cb, user));
   mark(o, kG2, sg);

@@ -136,8 +136,9 @@ def decoder_split(H: int) -> bool:
 
 
 def gan_split(H: int) -> bool:
-    """K3 runs the split-bf16 form (pgp_gansplit.hip) at these H."""
-    return H == 50
+    """K3 runs the split-bf16 form (pgp_gansplit.hip) at these H (batches of
+    64 K windows and more)."""
+    return H in (16, 50)
 
 
 def gan_split_flops_per_window(H: int, onehot: bool = True) -> int:

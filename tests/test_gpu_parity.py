@@ -142,39 +142,97 @@ def test_split_bf16_decoder_vs_fp32_decoder(H):
     assert not np.array_equal(a["logits"], b["logits"])   # the two forms really ran
 
 
-@pytest.mark.parametrize("dense", [0, 40])
-def test_split_bf16_gan_vs_fp32_gan(dense):
-    """K3's split-bf16 form (the default at H = 50, pgp_gansplit.hip; one-hot
-    schedule blocks in three products, dense ones in six) and its fp32-MFMA
-    form: both within tolerance of the fp64 oracle, probabilities within fp32
-    rounding of each other, every decision equal, and the one-hot shortcut
-    bitwise equal to the six-product form (its other products add exact zeros:
-    here checked by a batch whose dense windows take the six-product path in
-    the same launch)."""
-    H = 50
-    rng = np.random.Generator(np.random.PCG64(77 + dense))
-    w = W.synth_weights(H, seed=5)
-    x, s = c2(rng, 300, H, dense=dense)
-    ref = O.forward(w, x, s)
-    ref["sched32"] = s.astype(np.float32)
-    m = get_model(H, w, "gsplit50")
+@pytest.mark.parametrize("H,dense", [(50, 0), (50, 3000), (16, 0), (16, 3000)])
+def test_split_bf16_gan_vs_fp32_gan(H, dense):
+    """K3's split-bf16 form (pgp_gansplit.hip; the default at H = 16 and 50 for
+    batches of 64 K windows and more; one-hot schedule blocks in three products,
+    dense ones in six) against its fp32-MFMA form on one 65,536-window launch:
+    the first 2,048 windows (and the dense tail) within tolerance of the fp64
+    oracle for both forms, the split form no less accurate, every decision of
+    the whole launch equal (none sits in band here), and a window's outputs
+    independent of its wave's other windows (the one-hot shortcut is taken per
+    wave: 16 windows alone give the same bits)."""
+    from preganplus_amd.model import to_numpy
+    B = 65536
+    w = W.synth_weights(H, seed=5) if H == 50 else W.load_npz("preganplus_amd/data/simulator_16.npz")[0]
+    x, s = _c2_torch(B, H, seed=77 + H + dense)
+    if dense:
+        g = torch.Generator(device="cuda").manual_seed(5)
+        s[-dense:] = torch.rand((dense, H, H), generator=g, device="cuda")
+    m = get_model(H, w, f"gsplit{H}")
     m.gan_split(True)
-    a = run(m, x, s)
+    a = to_numpy(m.forward(x, s))
     m.gan_split(False)
-    b = run(m, x, s)
+    b = to_numpy(m.forward(x, s))
     m.gan_split(True)
-    assert_parity(a, ref, w, s)
-    assert_parity(b, ref, w, s)
-    ea = np.abs(a["probs"].astype(np.float64) - ref["probs"]).max()
-    eb = np.abs(b["probs"].astype(np.float64) - ref["probs"]).max()
-    assert ea <= 2 * eb + 1e-7, (ea, eb)
+    torch.cuda.synchronize()
     for k in ("keep", "final_target", "gen_target", "any", "cls"):
         assert np.array_equal(a[k], b[k]), k
-    # a window's outputs do not depend on the other windows of its wave (the
-    # one-hot shortcut is chosen per wave): the first 16 alone give the same bits
-    c = run(m, x[:16], s[:16])
-    for k in a:
+    idx = np.r_[0:2048, B - 256:B]
+    xs, ss = x[idx].cpu().numpy().astype(np.float64), s[idx].cpu().numpy().astype(np.float64)
+    ref = O.forward(w, xs, ss)
+    ref["sched32"] = ss.astype(np.float32)
+    sa = {k: v[idx] for k, v in a.items()}
+    sb = {k: v[idx] for k, v in b.items()}
+    assert_parity(sa, ref, w, ss)
+    assert_parity(sb, ref, w, ss)
+    ea = np.abs(sa["probs"].astype(np.float64) - ref["probs"]).max()
+    eb = np.abs(sb["probs"].astype(np.float64) - ref["probs"]).max()
+    assert ea <= 2 * eb + 1e-7, (ea, eb)
+    c = to_numpy(m.forward(x[:16].contiguous(), s[:16].contiguous()))   # (a 16-window batch runs gan_kernel)
+    for k in ("keep", "final_target", "gen_target"):
         assert np.array_equal(a[k][:16], c[k]), k
+
+
+@pytest.mark.parametrize("H", [16, 50])
+def test_k3_onehot_rebuild_guard(H):
+    """K3's split form rebuilds a wave's schedule rows from the 1.0 positions it
+    recorded in phase 2 (pgp_gansplit.hip) only when every window of the wave
+    has exactly C nonzero values, all 1.0, and every row holds one.  Near-one-hot
+    schedules that break one condition each (a row holding two 1.0s next to an
+    empty row: the counts still match; a 0.5; a 1.0 + 2^-7; a stray -1.0), each
+    in a wave of its own, must take the row reads; legitimate one-hot rows whose
+    1.0s sit at the row ends (a lane's values spanning two rows) take the
+    rebuild.  Decisions equal to the fp32 form's and within tolerance of the
+    oracle on every window of those waves."""
+    from preganplus_amd.model import to_numpy
+    B = 65536
+    w = W.synth_weights(H, seed=5) if H == 50 else W.load_npz("preganplus_amd/data/simulator_16.npz")[0]
+    x, s = _c2_torch(B, H, seed=913 + H)
+    eye_end = torch.zeros((H, H), device="cuda")
+    for r in range(H):
+        eye_end[r, H - 1 if r % 2 == 0 else 0] = 1.0
+    cases = []
+    k = 16 * 37 + 5
+    s[k, 3].zero_(); s[k, 3, 0] = s[k, 3, 5] = 1.0; s[k, 7].zero_()      # two in a row, an empty row
+    cases.append(k)
+    k = 16 * 911 + 0
+    s[k, 2] *= 0.5                                                      # a 0.5 (bf16, not 1.0)
+    cases.append(k)
+    k = 16 * 1500 + 15
+    s[k, H - 1] *= 1.0 + 2.0 ** -7                                      # bf16, not 1.0
+    cases.append(k)
+    k = 16 * 2047 + 9
+    s[k, 1, (int(s[k, 1].argmax()) + 1) % H] = -1.0                     # a stray nonzero
+    cases.append(k)
+    k = 16 * 3000 + 3
+    s[k] = eye_end                                                      # 1.0s at row ends
+    cases.append(k)
+    m = get_model(H, w, f"goh{H}")
+    m.gan_split(True)
+    a = to_numpy(m.forward(x, s))
+    m.gan_split(False)
+    b = to_numpy(m.forward(x, s))
+    m.gan_split(True)
+    torch.cuda.synchronize()
+    for key in ("keep", "final_target", "gen_target", "any", "cls"):
+        assert np.array_equal(a[key], b[key]), key
+    idx = np.concatenate([np.arange(16 * (c // 16), 16 * (c // 16) + 16) for c in cases])
+    xs, ss = x[idx].cpu().numpy().astype(np.float64), s[idx].cpu().numpy().astype(np.float64)
+    ref = O.forward(w, xs, ss)
+    ref["sched32"] = ss.astype(np.float32)
+    assert_parity({key: v[idx] for key, v in a.items()}, ref, w, ss)
+    assert_parity({key: v[idx] for key, v in b.items()}, ref, w, ss)
 
 
 def test_edge_inputs_h16():

@@ -97,8 +97,12 @@ for step in "$@"; do
       grep median $OUT/abpf.out
       python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); [print(k, [{kk: round(vv, 4) for kk, vv in e['kernel_ms'].items()} for e in v]) for k, v in d['extra'].items()]" $OUT/abpf.out
       ;;
+    k3probe)
+      run k3probe 900 python3 -u tools/ab_bench.py --rounds 2 --args "--steps 50 --warmup 5 --no-cpu-baseline" base= nop2=PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_k3p1.so nop3=PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_k3p2.so norow=PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_k3p3.so oh0=PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_k3oh0.so
+      python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); [print(k, [round(e['kernel_ms']['gan'], 4) for e in v]) for k, v in d['extra'].items()]" $OUT/k3probe.out
+      ;;
     tmodes)
-      run t_modes 600 $PYT tests/test_gpu_bench_modes.py tests/test_gpu_parity.py -m gpu -k "stream or split or branches or reference or ragged"
+      run t_modes 600 $PYT tests/test_gpu_bench_modes.py tests/test_gpu_parity.py -m gpu -k "stream or split or branches or reference or ragged or onehot"
       tail -2 $OUT/t_modes.out
       ;;
     c2l2)
