@@ -58,24 +58,28 @@ def cpu_baseline(weights, x, s, per_window_n=256, batch_n=1024):
     return CB.measure(weights, x[:n].cpu().numpy(), s[:n].cpu().numpy(), per_window_n, batch_n)
 
 
-def load_traffic(H, B, kernel="encoder"):
+def load_traffic(H, B, kernel="encoder", targs=None):
     """HBM bytes per launch of one kernel from the committed rocprofv3 --pmc
     FETCH_SIZE / WRITE_SIZE passes (profiles/pmc_<kernel>_h<H>.json, corrected
     per MI355X_MICROARCH.md §HBM, tools/pmc_traffic.py), or None when absent,
     taken at another batch, or taken with a different build of that kernel
     (the file's isa_sha256 against the loaded library's instructions: a
     stale counter pass is never reported as this build's traffic)."""
-    d = traffic_record(H, B, kernel)
+    d = traffic_record(H, B, kernel, targs=targs)
     return None if d is None else d.get("hbm_bytes_per_launch")
 
 
-def traffic_record(H, B, kernel, path=None):
+def traffic_record(H, B, kernel, path=None, targs=None):
+    """targs: the template arguments the file must have been taken with (a
+    kernel with several forms, e.g. encoder_kernel<50, split>)."""
     p = path or os.path.join(ROOT, "profiles", f"pmc_{kernel}_h{H}.json")
     if not os.path.exists(p):
         return None
     try:
         d = json.load(open(p))
         if int(d.get("batch", -1)) != B:
+            return None
+        if targs is not None and d.get("template_args") != list(targs):
             return None
         if d.get("isa_sha256") is None or d["isa_sha256"] != loaded_isa_hash(kernel + "_kernel", H,
                                                                              d.get("template_args")):
@@ -126,6 +130,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-gan", action="store_true", help="tune config: Transformer tuning step only")
+    ap.add_argument("--fp32-encoder", action="store_true", help="c2: K2's feed-forward on the fp32 MFMA instead of "
+                                                                 "the split-bf16 form (A/B)")
     ap.add_argument("--fp32-decoder", action="store_true", help="c2: K2b on the fp32 MFMA instead of the "
                                                                  "split-bf16 form (A/B)")
     ap.add_argument("--fp32-gan", action="store_true", help="c2: K3 on the fp32 MFMA instead of the split-bf16 "
@@ -193,11 +199,14 @@ def main():
         migrations(out["keep"], out["final_target"], cur, out=mv_out)
         evs[NK].record()
 
+    if args.fp32_encoder:
+        model.encoder_split(False)
     if args.fp32_decoder:
         model.decoder_split(False)
     if args.fp32_gan:
         model.gan_split(False)
     split = R.decoder_split(H) and not args.fp32_decoder
+    esplit = R.encoder_split(H) and not args.fp32_encoder
     gsplit = R.gan_split(H) and not args.fp32_gan
     for _ in range(args.warmup):
         step()
@@ -220,13 +229,21 @@ def main():
         k2_s = k_mean[1] * 1e-3
         # executed work: the MFMAs K2 issues (ISA count); the reference formulation's
         # flops are reported beside it (the layer-0 folds issue 0.67x of them)
-        exe = R.encoder_executed_flops_per_window(H)
         alg = R.encoder_flops_per_window(H)
+        if esplit:
+            # fp32 and bf16 MFMAs in one kernel: achieved = its MFMA work in
+            # fp32-MFMA-equivalent flops (the bf16 flops weighted by the peaks'
+            # ratio, 1/16), so achieved / the fp32 peak is the matrix pipe's
+            # busy fraction the ISA-counted work implies
+            ef, eb = R.encoder_split_executed_flops_per_window(H)
+            exe = ef + eb * R.PEAK_FP32_TFLOPS / R.PEAK_BF16_TFLOPS
+        else:
+            exe = R.encoder_executed_flops_per_window(H)
         achieved = (exe if exe is not None else alg) * B / k2_s / 1e12
-        traffic = load_traffic(H, B)
+        traffic = load_traffic(H, B, targs=[H, esplit])
         kn = {"gat_agg": "gat_agg", "encoder": "encoder", "decoder": "decoder_split" if split else "decoder",
               "gan": "gan_split" if gsplit else "gan"}
-        k_traffic = {k: load_traffic(H, B, v) for k, v in kn.items()}
+        k_traffic = {k: load_traffic(H, B, v, targs=[H, esplit] if k == "encoder" else None) for k, v in kn.items()}
         path_bytes = R.path_bytes_per_window(H) * B
         res = {
             "metric": "host-windows/sec (detect+diagnose+generate)",
@@ -259,13 +276,19 @@ def main():
                               "frac_of_bf16_peak": R.decoder_split_flops_per_window(H) * B / (k_mean[2] * 1e-3)
                               / 1e12 / R.PEAK_BF16_TFLOPS}
                              if split else {"form": "fp32 MFMA (v_mfma_f32_16x16x4_f32)"}),
+            "encoder_form": ({"form": "feed-forward (both layers' linear1 / linear2) split-bf16, 6 "
+                                      "v_mfma_f32_16x16x32_bf16 per fp32 product; attention projections fp32 MFMA",
+                              "executed_fp32_tflops": ef * B / k2_s / 1e12,
+                              "executed_bf16_tflops": eb * B / k2_s / 1e12}
+                             if esplit else {"form": "fp32 MFMA (v_mfma_f32_16x16x4_f32)"}),
             "gan_form": ("split-bf16 (6 v_mfma_f32_16x16x32_bf16 per fp32 product; schedule blocks exact in "
                          "bf16, e.g. one-hot, in 3)" if gsplit else "fp32 MFMA (v_mfma_f32_16x16x4_f32)"),
             "roofline": {"kernel": "encoder_kernel (K2)", "bound": "mfma", "achieved": achieved,
                          "peak": R.PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                          "frac": achieved / R.PEAK_FP32_TFLOPS,
-                         "basis": "executed MFMA flops per launch (ISA count, tools/isa_count.py) / HIP-event "
-                                  "kernel time",
+                         "basis": ("executed MFMA flops per launch (ISA count, tools/isa_count.py) / HIP-event "
+                                   "kernel time" + ("; the split feed-forward's bf16 flops counted at 1/16 (fp32 / "
+                                                    "bf16 dense peak): fp32-MFMA-equivalent work" if esplit else "")),
                          "executed_flops_per_window": exe,
                          "algorithmic_flops_per_window": alg,
                          "algorithmic_rate": alg * B / k2_s / 1e12,
@@ -601,6 +624,8 @@ def _build_c3_step(H, E, R, world, rank, device):
     _share_side_stream(world, main, side)
     reserved = _reserve_cus(main, side)
     step = TR.OnlineTrainStep(tr, st, sim, series_h, tmax_h, s, envs, R=R, side=side, groups=TR.dp_groups())
+    if step.native and os.environ.get("PGP_BENCH_SERIAL_ISSUE") == "1":
+        step.issue_worker(False)   # A/B: one host thread issues both streams
     return types.SimpleNamespace(tr=tr, w=w, series=series_h, tmax=tmax_h, s=s, sim=sim, step=step, main=main,
                                  side=side, reserved=reserved)
 

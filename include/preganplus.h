@@ -161,7 +161,12 @@ int pgp_embedding(int n_hosts, int batch, const float* logits, const float* prot
  * tools/micro/bf16_split.hip); on = 0: v_mfma_f32_16x16x4_f32.  Returns
  * PGP_ERR_UNSUPPORTED for on = 1 where the split form is not compiled. */
 int pgp_decoder_split(pgp_model* m, int on);
-/* K3's contraction form, likewise (the default where compiled: H = 50; also
+/* K2's feed-forward form, likewise (the default where compiled: H = 50, the
+ * tail-resident encoder): both layers' linear1 / linear2 as split-bf16 MFMAs
+ * (planes derived on the device at each weight load / repack); on = 0: the
+ * fp32 MFMA. */
+int pgp_encoder_split(pgp_model* m, int on);
+/* K3's contraction form, likewise (the default where compiled: H = 16, 50; also
  * the FPE variant's K3): Gen1, Disc1 and Gen2 as split-bf16 MFMAs, a schedule
  * block exactly representable in bf16 (one-hot GOBI rows) in three products
  * instead of six (the other three add exact zeros). */
@@ -509,6 +514,11 @@ int pgp_online_create(const pgp_online_desc* desc, pgp_online** out);
 int pgp_online_destroy(pgp_online* h);
 int pgp_online_step(pgp_online* h, void* main_stream, void* gan_stream, pgp_collective_fn cb, void* user);
 int pgp_online_timing(pgp_online* h, int on);
+/* pgp_online_issue_worker(h, on): at world size 1 with two streams, issue the
+ * GAN stream's launches from a second host thread of the library while the
+ * calling thread issues the tuning backward (default on; 0: one thread issues
+ * both, as under a callback or timing). */
+int pgp_online_issue_worker(pgp_online* h, int on);
 int pgp_online_stage_ms(pgp_online* h, float* ms);
 int pgp_online_steps(const pgp_online* h, double* steps, int n);
 /* The step's GAN part alone (train_gan, PreGANPlus.py:60-81, for the E

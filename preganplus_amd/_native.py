@@ -88,6 +88,8 @@ def lib():
     L.pgp_embedding.restype = c_int
     L.pgp_decoder_split.argtypes = [vp, c_int]
     L.pgp_decoder_split.restype = c_int
+    L.pgp_encoder_split.argtypes = [vp, c_int]
+    L.pgp_encoder_split.restype = c_int
     L.pgp_gan_split.argtypes = [vp, c_int]
     L.pgp_gan_split.restype = c_int
     L.pgp_schedule_onehot.argtypes = [c_int, c_int, fp, fp, vp]

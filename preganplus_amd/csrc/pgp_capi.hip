@@ -26,6 +26,8 @@ struct pgp_model {
   bool loaded = false;
   float* d_frags = nullptr;
   float* d_decb = nullptr;   // split-bf16 decoder planes (derived from d_frags on the device)
+  float* d_encb = nullptr;   // split-bf16 encoder LDS image (derived likewise)
+  bool enc_split = true;     // K2's feed-forward on the split-bf16 planes where compiled (pgp_encoder_split)
   bool dec_split = true;     // K2b on the split-bf16 planes where compiled (pgp_decoder_split)
   float* d_ganb = nullptr;   // split-bf16 GAN planes (derived from d_frags on the device)
   bool gan_split = true;     // K3 on the split-bf16 planes where compiled (pgp_gan_split)
@@ -146,7 +148,7 @@ int pgp_create_fpe(int n_hosts, pgp_model** out) {
 
 int pgp_destroy(pgp_model* m) {
   if (!m) return PGP_OK;
-  for (float* p : {m->d_frags, m->d_decb, m->d_ganb, m->d_tab, m->d_gtab, m->d_agg, m->d_lat, m->d_emb, m->d_gat})
+  for (float* p : {m->d_frags, m->d_decb, m->d_encb, m->d_ganb, m->d_tab, m->d_gtab, m->d_agg, m->d_lat, m->d_emb, m->d_gat})
     if (p) (void)hipFree(p);
   if (m->d_pscr) (void)hipFree(m->d_pscr);
   delete m;
@@ -169,6 +171,11 @@ int pgp_load_weights(pgp_model* m, const double* blob, size_t len) {
   if (!m->fpe && decoder_split_floats(m->H) > 0) {
     if (!m->d_decb) HIPCHK(hipMalloc(&m->d_decb, decoder_split_floats(m->H) * sizeof(float)));
     HIPCHK(launch_decoder_split(m->H, m->d_frags, m->d_decb, nullptr));
+    HIPCHK(hipStreamSynchronize(nullptr));
+  }
+  if (!m->fpe && encoder_split_floats(m->H) > 0) {
+    if (!m->d_encb) HIPCHK(hipMalloc(&m->d_encb, encoder_split_floats(m->H) * sizeof(float)));
+    HIPCHK(launch_encoder_split(m->H, m->d_frags, m->d_encb, nullptr));
     HIPCHK(hipStreamSynchronize(nullptr));
   }
   if (gan_split_floats(m->H) > 0) {
@@ -214,6 +221,7 @@ int pgp_forward_stage(pgp_model* m, int stage, int batch, const float* windows, 
   a.emb = m->d_emb;
   a.frags = m->d_frags;
   a.decb = m->dec_split ? m->d_decb : nullptr;
+  a.encb = m->enc_split ? m->d_encb : nullptr;
   a.ganb = m->gan_split ? m->d_ganb : nullptr;
   a.tab = m->d_tab;
   a.gtab = m->d_gtab;
@@ -319,6 +327,14 @@ int pgp_decoder_split(pgp_model* m, int on) {
   if (m->fpe || decoder_split_floats(m->H) == 0)
     return on ? fail(PGP_ERR_UNSUPPORTED, "split-bf16 decoder not compiled for this model / host count") : PGP_OK;
   m->dec_split = on != 0;
+  return PGP_OK;
+}
+
+int pgp_encoder_split(pgp_model* m, int on) {
+  if (!m) return fail(PGP_ERR_ARG, "NULL model");
+  if (m->fpe || encoder_split_floats(m->H) == 0)
+    return on ? fail(PGP_ERR_UNSUPPORTED, "split-bf16 encoder not compiled for this model / host count") : PGP_OK;
+  m->enc_split = on != 0;
   return PGP_OK;
 }
 
@@ -721,6 +737,8 @@ int pgp_repack_master_sections(pgp_model* m, const float* P_device, const double
   HIPCHK(launch_repack(m->H, a, reinterpret_cast<hipStream_t>(stream)));
   if ((sections & 1) && m->d_decb)
     HIPCHK(launch_decoder_split(m->H, m->d_frags, m->d_decb, reinterpret_cast<hipStream_t>(stream)));
+  if ((sections & 1) && m->d_encb)
+    HIPCHK(launch_encoder_split(m->H, m->d_frags, m->d_encb, reinterpret_cast<hipStream_t>(stream)));
   if ((sections & 2) && m->d_ganb)
     HIPCHK(launch_gan_split_derive(m->H, m->d_frags, m->d_ganb, reinterpret_cast<hipStream_t>(stream)));
   return PGP_OK;

@@ -40,6 +40,7 @@ struct FwdArgs {
   const float* frags;    // device weight fragments (Geo<H> offsets)
   const float* decb;     // split-bf16 decoder weight planes (pgp_decoder.hip DecB), or nullptr
   const float* ganb;     // split-bf16 GAN weight planes (pgp_gansplit.hip GanS), or nullptr
+  const float* encb;     // split-bf16 encoder LDS image (pgp_encoder.hip EncS), or nullptr
   const float* tab;      // encoder/decoder tables (LDS-staged)
   const float* gtab;     // GAN tables
   const float* gat;      // GAT constants u[4] | v[4] (device)
@@ -89,6 +90,8 @@ hipError_t launch_decoder(const FwdArgs& a, hipStream_t st);
 // fp32 decoder runs at this H) and their derivation from the fp32 fragments
 long decoder_split_floats(int H);
 hipError_t launch_decoder_split(int H, const float* frags, float* decb, hipStream_t st);
+long encoder_split_floats(int H);  // 0: no split-bf16 encoder at this H
+hipError_t launch_encoder_split(int H, const float* frags, float* encb, hipStream_t st);
 hipError_t launch_gan(const FwdArgs& a, hipStream_t st);
 // K3 on split-bf16 MFMAs (pgp_gansplit.hip): plane floats (0: not compiled at
 // this H), their derivation from the fp32 fragments, the launch

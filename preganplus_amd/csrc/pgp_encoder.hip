@@ -46,23 +46,113 @@ constexpr int enc_waves() { return H <= 16 ? kEnc16Waves : tail_res<H>() ? kEncT
 template <int H>
 constexpr int NW_STAGE() { return enc_waves<H>(); }
 
+// Split-bf16 feed-forward (tail-resident mode, H = 50): both layers' linear1
+// (K = d) and linear2 (K = 64) run as v_mfma_f32_16x16x32_bf16 over exact
+// three-part bf16 splits of both operands (the six products i + j <= 2, as K2b
+// and K3: pgp_device.hpp split8 / mfma_bf6), 96 MFMA cycles per 32-k block
+// against 256 for the fp32 MFMA; the FFN is 54% of K2's MFMA cycles.  A 32-k
+// block pairs two of the fp32 form's 4-k-step groups lane-locally (groups 2b,
+// 2b + 1: a lane's 8 values), for the weights (planes derived once per weight
+// load, enc_split_kernel) and the activations (split in registers).  The LDS
+// image (groups of 1 KiB, EncS): layer 0's FFN planes | layer 1's qk, v, o
+// (fp32, as in the stream) | layer 1's FFN planes: 132 KiB (fp32 form: 104).
+template <int H>
+struct EncS {
+  using G = Geo<H>;
+  static constexpr int NBD = cdiv(G::KQ_D, 2);  // 32-k blocks over d
+  static constexpr int NBF = G::KQ_F / 2;       // 32-k blocks over the hidden 64
+  static constexpr int F1S = G::MT_F * NBD * 3;  // linear1 planes [c][blk][plane]
+  static constexpr int F2S = G::MT_X * NBF * 3;  // linear2 planes [m][blk][plane]
+  static constexpr int FFN = F1S + F2S;
+  static constexpr int L0F = 0;                 // layer 0 FFN
+  static constexpr int L1A = FFN;               // layer 1 stages 0, 1 (fp32 groups [0, P_F1))
+  static constexpr int L1F = L1A + G::P_F1;     // layer 1 FFN
+  static constexpr int GROUPS = L1F + FFN;
+  static constexpr int STREAM = GROUPS * G::FQ;  // floats
+  static constexpr long SIZE = STREAM;           // the device image (floats)
+};
+
 // RESIDENT (H <= 16): both layers' weights (24 KB at H = 16) are loaded into LDS
 // once per workgroup; the host loop then runs with no ring barriers or DMAs.
-// Tail-resident: groups [RES0, 2*LAYER_G) of the stream (see tail_res).
-template <int H>
+// Tail-resident: groups [RES0, 2*LAYER_G) of the stream (see tail_res), or the
+// split image (EncS).
+template <int H, bool SPLIT = false>
 struct EncLds {
   static constexpr bool TRES = tail_res<H>();
   // the tail-resident mode has no barrier in the host loop: waves take
   // (block, host) unit ranges and prefetch through an LDS slot (at H <= 16,
   // also resident, that measured slower: fleet 1.97 -> 2.00 ms)
   static constexpr int RES0 = TRES ? Geo<H>::st_begin(Geo<H>::NST - 1) : 0;  // layer 0 stage 2
-  static constexpr int STREAM = (kLayers * Geo<H>::LAYER_G - RES0) * Geo<H>::FQ;  // floats
+  static constexpr int STREAM = SPLIT ? EncS<H>::STREAM : (kLayers * Geo<H>::LAYER_G - RES0) * Geo<H>::FQ;  // floats
   static constexpr bool RESIDENT = TRES || STREAM * 4 <= 32 * 1024;
   static constexpr int SLOT = Geo<H>::SLOT_G * Geo<H>::FQ;
   static constexpr int TAB = Geo<H>::t_size(kMaxProtos);
   static constexpr int TOTAL = (RESIDENT ? STREAM : 2 * SLOT) + TAB;
   static constexpr bool UNITS = TRES;
 };
+
+template <int H>
+constexpr bool enc_split() {
+  return tail_res<H>() && EncLds<H, true>::TOTAL * 4 + enc_waves<H>() * 144 * 4 <= 160 * 1024;
+}
+
+// fp32 stream -> the split image: one wave per FFN plane triple or fp32 group
+template <int H>
+__global__ __launch_bounds__(256) void enc_split_kernel(const float* __restrict__ enc, float* __restrict__ out) {
+  using G = Geo<H>;
+  using S = EncS<H>;
+  constexpr int T1 = G::MT_F * S::NBD, T2 = G::MT_X * S::NBF, TL = T1 + T2;  // triples per layer
+  const long f = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (f >= 2 * TL + G::P_F1) return;
+  if (f >= 2 * TL) {  // layer 1's attention groups, copied
+    const long i = f - 2 * TL;
+    *reinterpret_cast<f32x4*>(out + (S::L1A + i) * 256 + lane * 4) = ld4(enc + (G::LAYER_G + i) * 256 + lane * 4);
+    return;
+  }
+  const int l = (int)(f / TL), t = (int)(f % TL);
+  const float* src = enc + (long)(l * G::LAYER_G + G::P_F1) * 256;  // the layer's f1 | f2 groups
+  long q0, q1, dst;  // the two fp32 groups (-1: zero) and the first destination plane
+  const long base = l == 0 ? S::L0F : S::L1F;
+  if (t < T1) {  // linear1 tile c, d block b: groups [c][q4]
+    const int c = t / S::NBD, b = t % S::NBD;
+    q0 = c * G::KQ_D + 2 * b;
+    q1 = 2 * b + 1 < G::KQ_D ? q0 + 1 : -1;
+    dst = base + (long)t * 3;
+  } else {  // linear2 tile m, hidden block b: groups G_F1 + [m][q4]
+    const int u = t - T1, m = u / S::NBF, b = u % S::NBF;
+    q0 = G::G_F1 + m * G::KQ_F + 2 * b;
+    q1 = q0 + 1;
+    dst = base + S::F1S + (long)u * 3;
+  }
+  float v[8];
+  const f32x4 x0 = ld4(src + q0 * 256 + lane * 4);
+  const f32x4 x1 = q1 >= 0 ? ld4(src + q1 * 256 + lane * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    v[e] = x0[e];
+    v[4 + e] = x1[e];
+  }
+  u32x4 p[3];
+  split8(v, p);
+#pragma unroll
+  for (int k = 0; k < 3; ++k) *reinterpret_cast<u32x4*>(out + (dst + k) * 256 + lane * 4) = p[k];
+}
+
+// the lane's 8 values of 32-k block b of a [NT][3] activation (tiles 2b, 2b + 1
+// of step w; a tile past NT is zero)
+template <int NT>
+PGP_DEV void pair_tiles(const f32x4 (&T)[NT][3], int b, int w, float (&v)[8]) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    v[e] = 2 * b < NT ? T[2 * b][w][e] : 0.f;
+    v[4 + e] = 2 * b + 1 < NT ? T[2 * b + 1][w][e] : 0.f;
+  }
+}
+PGP_DEV void planes_lds(const float* F, int lane, u32x4 (&w)[3]) {
+#pragma unroll
+  for (int k = 0; k < 3; ++k) w[k] = *reinterpret_cast<const u32x4*>(F + k * 256 + lane * 4);
+}
 
 // ReLU as one integer max on the bit pattern (negative floats have negative
 // int patterns): fmaxf on an MFMA result costs a NaN-canonicalising v_max first,
@@ -215,10 +305,10 @@ PGP_DEV void layer_norm_tiles(f32x4 (&acc)[Geo<H>::MT_D][3], f32x4 (&X)[Geo<H>::
 // Ring state: `cur` holds the stage being computed, `nxt` is being filled.
 // Resident mode: `nxt` is the LDS copy of the whole stream and advance() only
 // moves `cur` to the next stage.
-template <int H>
+template <int H, bool SPLIT = false>
 struct Ring {
   using G = Geo<H>;
-  static constexpr bool RES = EncLds<H>::RESIDENT;
+  static constexpr bool RES = EncLds<H, SPLIT>::RESIDENT;
   float* cur;
   float* nxt;
   const float* enc;  // global encoder stream [layer][LAYER_G groups]
@@ -236,7 +326,11 @@ struct Ring {
   PGP_DEV void advance() {
     if constexpr (RES) {
       const int si = next % (kLayers * G::NST), l = si / G::NST, k = si % G::NST;
-      const int gi = l * G::LAYER_G + G::st_begin(k) - EncLds<H>::RES0;  // < 0: a stage tail mode never reads
+      int gi;
+      if constexpr (SPLIT)  // the split image (EncS); layer 0's stages 0, 1 are never read
+        gi = l == 0 ? EncS<H>::L0F : k == 2 ? EncS<H>::L1F : EncS<H>::L1A + G::st_begin(k);
+      else
+        gi = l * G::LAYER_G + G::st_begin(k) - EncLds<H>::RES0;  // < 0: a stage tail mode never reads
       cur = nxt + (gi > 0 ? gi : 0) * G::FQ;
       ++next;
       __builtin_amdgcn_sched_barrier(0);  // keep stages apart (no hoisting of later stages' LDS reads)
@@ -340,8 +434,8 @@ PGP_DEV float row_fold_bias(int m, int n, int w, const float* tab) {
 // Tail-mode layer (Geo<H>::TAIL, H = 50): stages [qk] [v o] [f1 f2].
 // F0: layer 0, q/k/v from the folded raw-feature product (the ring's q/k/v
 // stages are then unused).
-template <int H, bool F0>
-PGP_DEV void encoder_layer_tail(f32x4 (&X)[Geo<H>::MT_D][3], Ring<H>& ring, const float* TL, int lane,
+template <int H, bool F0, bool SPLIT>
+PGP_DEV void encoder_layer_tail(f32x4 (&X)[Geo<H>::MT_D][3], Ring<H, SPLIT>& ring, const float* TL, int lane,
                                 const float* tab, const float (&ba)[3], const float (&xv)[3][3]) {
   using G = Geo<H>;
   constexpr int TQ = G::TQ, SR = G::SR, HF = G::HF;
@@ -542,7 +636,75 @@ PGP_DEV void encoder_layer_tail(f32x4 (&X)[Geo<H>::MT_D][3], Ring<H>& ring, cons
 #pragma unroll
     for (int w = 0; w < 3; ++w) acc[mt][w] = X[mt][w] * g1 + b2;  // residual gamma*x-hat + beta, + b2
   }
-  {
+  if constexpr (SPLIT) {
+    // step by step: X's two 32-k blocks split (24 VGPRs), the four hidden tiles
+    // (4 independent MFMA chains), ReLU, the hidden pairs split, linear2 onto
+    // the residual accumulators; linear2's XR VALU rows as in the fp32 form
+    using S = EncS<H>;
+    static_assert(S::NBF * 2 == G::MT_F, "hidden pairs");
+    const float* A1 = ring.cur;
+    const float* A2 = ring.cur + S::F1S * G::FQ;
+#pragma unroll
+    for (int w = 0; w < 3; ++w) {
+      u32x4 xs[S::NBD][3];
+#pragma unroll
+      for (int b = 0; b < S::NBD; ++b) {
+        float v[8];
+        pair_tiles<G::MT_D>(X, b, w, v);
+        split8(v, xs[b]);
+      }
+      f32x4 F[G::MT_F];
+#pragma unroll
+      for (int c = 0; c < G::MT_F; ++c) F[c] = ld4(TL + G::TL_B1 + 16 * c + 4 * g);
+      prio_mfma();
+#pragma unroll
+      for (int b = 0; b < S::NBD; ++b)
+#pragma unroll
+        for (int c = 0; c < G::MT_F; ++c) {
+          u32x4 wp[3];
+          planes_lds(A1 + ((c * S::NBD + b) * 3) * 256, lane, wp);
+          F[c] = mfma_bf6(wp, xs[b], F[c]);
+        }
+      prio_valu();
+#pragma unroll
+      for (int c = 0; c < G::MT_F; ++c)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) F[c][r] = relu_enc<H>(F[c][r]);
+      float rf[G::XR];
+#pragma unroll
+      for (int n = 0; n < G::XR; ++n) rf[n] = 0.f;
+#pragma unroll
+      for (int c = 0; c < G::MT_F; ++c)
+#pragma unroll
+        for (int n = 0; n < G::XR; ++n) {
+          const f32x4 rw = ld4(TL + G::TL_RF + ((n * G::KQ_F + c) * 4 + g) * 4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) rf[n] = fmaf(rw[e], F[c][e], rf[n]);
+        }
+      u32x4 hs[S::NBF][3];
+#pragma unroll
+      for (int b = 0; b < S::NBF; ++b) {
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = F[2 * b][e];
+          v[4 + e] = F[2 * b + 1][e];
+        }
+        split8(v, hs[b]);
+      }
+      prio_mfma();
+#pragma unroll
+      for (int b = 0; b < S::NBF; ++b)
+#pragma unroll
+        for (int m = 0; m < G::MT_X; ++m) {
+          u32x4 wp[3];
+          planes_lds(A2 + ((m * S::NBF + b) * 3) * 256, lane, wp);
+          acc[m][w] = mfma_bf6(wp, hs[b], acc[m][w]);
+        }
+      prio_valu();
+      acc[G::MT_X][w][0] += xsum_rows<G::XR>(rf);  // row n's sum in lane group n
+    }
+  } else {
     static_assert(G::KQ_F == G::MT_F, "hidden tile c = W2 k-group c");
     float rf[G::XR][3];
     zero_rows(rf);
@@ -658,11 +820,11 @@ PGP_DEV void encoder_layer(f32x4 (&X)[Geo<H>::MT_D][3], Ring<H>& ring, const flo
   layer_norm_tiles<H, false>(acc, X, TL + G::TL_LN2G, TL + G::TL_LN2B, g);  // x-hat: both affines folded (see tail)
 }
 
-template <int H>
+template <int H, bool SPLIT>
 __global__ __launch_bounds__(enc_waves<H>() * 64, H <= 16 ? kEnc16EU : tail_res<H>() ? 1 : 2) void encoder_kernel(
     FwdArgs a) {
   using G = Geo<H>;
-  using L = EncLds<H>;
+  using L = EncLds<H, SPLIT>;
   __shared__ __attribute__((aligned(16))) float smem[L::TOTAL];
   // tail-resident mode: per-wave staging slot of the next unit's raw features
   __shared__ float xstage[L::UNITS ? NW_STAGE<H>() * 144 : 1];
@@ -675,8 +837,13 @@ __global__ __launch_bounds__(enc_waves<H>() * 64, H <= 16 ? kEnc16EU : tail_res<
   constexpr int NW = enc_waves<H>();
   const long nblk = (a.B + 15) / 16;
 
-  Ring<H> ring{smem, smem + L::SLOT, a.frags + G::OFF_ENC, 0, H * kLayers * G::NST, wv, lane};
-  if constexpr (L::RESIDENT) {
+  Ring<H, SPLIT> ring{smem, smem + L::SLOT, a.frags + G::OFF_ENC, 0, H * kLayers * G::NST, wv, lane};
+  if constexpr (SPLIT) {
+    dma_groups(a.encb, smem, EncS<H>::GROUPS, wv, NW, lane);
+    ring.nxt = smem;
+    ring.next = 1;
+    __syncthreads();
+  } else if constexpr (L::RESIDENT) {
     dma_groups(a.frags + G::OFF_ENC + (long)L::RES0 * G::FQ, smem, kLayers * G::LAYER_G - L::RES0, wv, NW, lane);
     ring.nxt = smem;
     ring.next = 1;
@@ -726,9 +893,9 @@ __global__ __launch_bounds__(enc_waves<H>() * 64, H <= 16 ? kEnc16EU : tail_res<
     }
     static_assert(kLayers == 2, "layer 0 (folded q/k/v) + layer 1");
     if constexpr (G::TAIL) {
-      encoder_layer_tail<H, true>(X, ring, tab + G::T_L0, lane, tab, ba, xv);
-      encoder_layer_tail<H, false>(X, ring, tab + G::T_L0 + G::TL_SIZE, lane, tab, ba, xv);
-    } else {
+      encoder_layer_tail<H, true, SPLIT>(X, ring, tab + G::T_L0, lane, tab, ba, xv);
+      encoder_layer_tail<H, false, SPLIT>(X, ring, tab + G::T_L0 + G::TL_SIZE, lane, tab, ba, xv);
+    } else if constexpr (!SPLIT) {
       encoder_layer<H, true>(X, ring, tab + G::T_L0, lane, tab, ba);
       encoder_layer<H, false>(X, ring, tab + G::T_L0 + G::TL_SIZE, lane, tab, ba);
     }
@@ -807,8 +974,8 @@ __global__ __launch_bounds__(enc_waves<H>() * 64, H <= 16 ? kEnc16EU : tail_res<
   }
 }
 
-template <int H>
-hipError_t launch(const FwdArgs& a, hipStream_t st) {
+template <int H, bool SPLIT>
+hipError_t launch_form(const FwdArgs& a, hipStream_t st) {
   const long nblk = (a.B + 15) / 16;
   constexpr int NW = enc_waves<H>();
   long grid = (nblk + NW - 1) / NW;
@@ -819,7 +986,7 @@ hipError_t launch(const FwdArgs& a, hipStream_t st) {
   static std::atomic<int> fits{-1};
   if (fits.load(std::memory_order_relaxed) < 0) {
     hipFuncAttributes fa{};
-    const bool ok = hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(encoder_kernel<H>)) == hipSuccess &&
+    const bool ok = hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(encoder_kernel<H, SPLIT>)) == hipSuccess &&
                     fa.maxThreadsPerBlock >= NW * 64;
     fits.store(ok ? 1 : 0, std::memory_order_relaxed);
   }
@@ -828,14 +995,33 @@ hipError_t launch(const FwdArgs& a, hipStream_t st) {
     static std::atomic<int> occ_cache{0};  // workgroups resident per CU (registers / LDS), queried once
     int occ = occ_cache.load(std::memory_order_relaxed);
     if (occ <= 0) {
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, encoder_kernel<H>, NW * 64, 0) != hipSuccess || occ <= 0)
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, encoder_kernel<H, SPLIT>, NW * 64, 0) != hipSuccess ||
+          occ <= 0)
         occ = 1;
       occ_cache.store(occ, std::memory_order_relaxed);
     }
     grid = std::min<long>((long)device_cus() * occ, (nblk * H + NW - 1) / NW);
   }
-  encoder_kernel<H><<<(int)grid, NW * 64, 0, st>>>(a);
+  encoder_kernel<H, SPLIT><<<(int)grid, NW * 64, 0, st>>>(a);
   return hipGetLastError();
+}
+
+template <int H>
+hipError_t launch(const FwdArgs& a, hipStream_t st) {
+  if constexpr (enc_split<H>())
+    if (a.encb != nullptr) return launch_form<H, true>(a, st);
+  return launch_form<H, false>(a, st);
+}
+
+template <int H>
+hipError_t launch_split(const float* frags, float* encb, hipStream_t st) {
+  if constexpr (enc_split<H>()) {
+    using G = Geo<H>;
+    constexpr long n = 2L * (G::MT_F * EncS<H>::NBD + G::MT_X * EncS<H>::NBF) + G::P_F1;
+    enc_split_kernel<H><<<(int)((n + 3) / 4), 256, 0, st>>>(frags + G::OFF_ENC, encb);
+    return hipGetLastError();
+  }
+  return hipErrorInvalidValue;
 }
 
 }  // namespace
@@ -845,6 +1031,28 @@ hipError_t launch_encoder(const FwdArgs& a, hipStream_t st) {
 #define CASE(h) \
   case h:       \
     return launch<h>(a, st);
+    PGP_FOR_EACH_H(CASE)
+#undef CASE
+  }
+  return hipErrorInvalidValue;
+}
+
+long encoder_split_floats(int H) {
+  switch (H) {
+#define CASE(h) \
+  case h:       \
+    return enc_split<h>() ? EncS<h>::SIZE : 0;
+    PGP_FOR_EACH_H(CASE)
+#undef CASE
+  }
+  return 0;
+}
+
+hipError_t launch_encoder_split(int H, const float* frags, float* encb, hipStream_t st) {
+  switch (H) {
+#define CASE(h) \
+  case h:       \
+    return launch_split<h>(frags, encb, st);
     PGP_FOR_EACH_H(CASE)
 #undef CASE
   }

@@ -29,8 +29,13 @@
 // names): this library has no communicator of its own.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cmath>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <string>
+#include <thread>
 
 #include "../../include/preganplus.h"
 #include "pgp_device.hpp"
@@ -45,6 +50,71 @@ namespace {
 enum Sec { kTr = 0, kGen = 1, kDisc = 2 };
 // timing events: main stream 0..6, GAN stream 7..9
 enum Ev { kE0, kE1, kE2, kE3, kE4, kE5, kE6, kG0, kG1, kG2, kNumEv };
+
+// A host thread that issues the GAN stream's launches while the calling thread
+// issues the tuning backward (world size 1).  Issuing ~20 launches costs the
+// host ~0.1 ms; serially, whichever stream is issued second waits for the
+// other's issue (H = 16: the main stream sat idle 46 us between the targets and
+// the backward while the GAN launches were issued; issuing the backward first
+// delays the GAN chain the same amount).  The worker spins a while between
+// jobs (back-to-back steps find it awake), then sleeps on a condition
+// variable.
+class IssueWorker {
+ public:
+  IssueWorker() : th_([this] { loop(); }) {}
+  ~IssueWorker() {
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      quit_ = true;
+    }
+    cv_.notify_one();
+    th_.join();
+  }
+  void post(std::function<int()> job) {
+    job_ = std::move(job);
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      posted_.store(posted_.load(std::memory_order_relaxed) + 1, std::memory_order_release);
+    }
+    cv_.notify_one();
+  }
+  // the posted job's return code (its error message in *err)
+  int wait(std::string* err) {
+    const unsigned long n = posted_.load(std::memory_order_relaxed);
+    while (done_.load(std::memory_order_acquire) != n) __builtin_ia32_pause();
+    *err = err_;
+    return rc_;
+  }
+
+ private:
+  void loop() {
+    unsigned long seen = 0;
+    for (;;) {
+      unsigned long n = 0;
+      for (long i = 0; i < kSpin && (n = posted_.load(std::memory_order_acquire)) == seen; ++i)
+        __builtin_ia32_pause();
+      if (n == seen) {
+        std::unique_lock<std::mutex> lk(m_);
+        cv_.wait(lk, [&] { return quit_ || posted_.load(std::memory_order_acquire) != seen; });
+        if (quit_) return;
+        n = posted_.load(std::memory_order_acquire);
+      }
+      rc_ = job_();
+      err_ = rc_ == PGP_OK ? std::string() : pgp_last_error();
+      seen = n;
+      done_.store(n, std::memory_order_release);
+    }
+  }
+  static constexpr long kSpin = 200000;  // ~2-5 ms of pause instructions
+  std::function<int()> job_;
+  int rc_ = PGP_OK;
+  std::string err_;
+  std::atomic<unsigned long> posted_{0}, done_{0};
+  bool quit_ = false;
+  std::mutex m_;
+  std::condition_variable cv_;
+  std::thread th_;
+};
 
 }  // namespace
 
@@ -61,6 +131,8 @@ struct pgp_online {
   hipEvent_t gate = nullptr, gan_done = nullptr, tgt_end = nullptr;
   bool timing = false, timed = false;
   hipEvent_t tev[kNumEv] = {};
+  bool issue_worker = true;  // world size 1, two streams: the GAN launches issued from a second host thread
+  IssueWorker* worker = nullptr;
 };
 
 namespace {
@@ -293,6 +365,7 @@ int pgp_online_destroy(pgp_online* o) {
   if (o->tgt_end) (void)hipEventDestroy(o->tgt_end);
   for (auto& e : o->tev)
     if (e) (void)hipEventDestroy(e);
+  delete o->worker;
   delete o;
   return PGP_OK;
 }
@@ -340,16 +413,43 @@ int pgp_online_step(pgp_online* o, void* main_stream, void* gan_stream, pgp_coll
   mark(o, kG0, sg);
   mark(o, kG1, sg);
   const bool fused = cb == nullptr;  // world size 1: each GAN AdamW inside its gradient kernel
-  // (issuing the backward before the GAN part at world size 1 measured the same:
-  // 0.1851 vs 0.1853 ms at H = 16, profiles/r06/ab/abb16_bwdfirst.txt)
-  OCALL(gan_part_a(o, sg, fused));
-  // then the backward
-  OCHK(launch_tune_backward(o->bwd, d.P, d.G, d.tune_ws, d.logits, d.protos, d.y, d.mult, d.tgt, sm, true,
-                            tgt_end));
-  mark(o, kE4, sm);
-  // 5. the GAN's updates (its collectives on the GAN stream)
-  OCALL(gan_part_b(o, sg, fused, cb, user));
-  mark(o, kG2, sg);
+  if (fused && sg != sm && !o->timed && o->issue_worker) {
+    // the whole GAN chain issued by the worker while this thread issues the
+    // backward (both parts: no exchange between them at world size 1)
+    if (!o->worker) o->worker = new IssueWorker;
+    struct Joined {  // every exit waits for the worker (its job refers to this frame)
+      IssueWorker* w;
+      bool waited = false;
+      int rc = PGP_OK;
+      std::string err;
+      int wait() {
+        if (!waited) {
+          rc = w->wait(&err);
+          waited = true;
+        }
+        return rc;
+      }
+      ~Joined() { wait(); }
+    } jw{o->worker};
+    o->worker->post([o, sg] {
+      OCALL(gan_part_a(o, sg, true));
+      return gan_part_b(o, sg, true, nullptr, nullptr);
+    });
+    OCHK(launch_tune_backward(o->bwd, d.P, d.G, d.tune_ws, d.logits, d.protos, d.y, d.mult, d.tgt, sm, true,
+                              tgt_end));
+    if (jw.wait() != PGP_OK) return ofail(jw.rc, jw.err);
+  } else {
+    // (issuing the backward before the GAN part at world size 1 measured the same:
+    // 0.1851 vs 0.1853 ms at H = 16, profiles/r06/ab/abb16_bwdfirst.txt)
+    OCALL(gan_part_a(o, sg, fused));
+    // then the backward
+    OCHK(launch_tune_backward(o->bwd, d.P, d.G, d.tune_ws, d.logits, d.protos, d.y, d.mult, d.tgt, sm, true,
+                              tgt_end));
+    mark(o, kE4, sm);
+    // 5. the GAN's updates (its collectives on the GAN stream)
+    OCALL(gan_part_b(o, sg, fused, cb, user));
+    mark(o, kG2, sg);
+  }
   // 6. the tuning step's exchange, state update and AdamW
   OCALL(collective(cb, user, PGP_COLL_TUNE_GRAD, sm));
   OCALL(collective(cb, user, PGP_COLL_TUNE_STATE, sm));
@@ -367,6 +467,12 @@ int pgp_online_step(pgp_online* o, void* main_stream, void* gan_stream, pgp_coll
   }
   commit_steps(o);
   (void)R;
+  return PGP_OK;
+}
+
+int pgp_online_issue_worker(pgp_online* o, int on) {
+  if (!o) return ofail(PGP_ERR_ARG, "pgp_online_issue_worker: NULL handle");
+  o->issue_worker = on != 0;
   return PGP_OK;
 }
 

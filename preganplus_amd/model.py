@@ -85,9 +85,14 @@ class DecisionModel:
         _native.check(self._L.pgp_reserve(self._h, int(max_batch)), "pgp_reserve")
 
     def gan_split(self, on: bool):
-        """K3 on split-bf16 MFMAs (True: the default where compiled, H = 50) or
+        """K3 on split-bf16 MFMAs (True: the default where compiled, H = 16, 50) or
         on the fp32 MFMA (False); ``pgp_gan_split``."""
         _native.check(self._L.pgp_gan_split(self._h, int(bool(on))), "pgp_gan_split")
+
+    def encoder_split(self, on: bool):
+        """K2's feed-forward on split-bf16 MFMAs (True: the default where
+        compiled, H = 50) or on the fp32 MFMA (False); ``pgp_encoder_split``."""
+        _native.check(self._L.pgp_encoder_split(self._h, int(bool(on))), "pgp_encoder_split")
 
     def decoder_split(self, on: bool):
         """K2b on split-bf16 MFMAs (True: the default where compiled, H = 32 and

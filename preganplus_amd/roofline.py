@@ -62,6 +62,23 @@ def encoder_executed_flops_per_window(H: int):
     return None if n is None else n * 2048 * H / 16
 
 
+# The split feed-forward form (pgp_encoder.hip EncS, encoder_kernel<H, true>):
+# (v_mfma_f32_16x16x4_f32, v_mfma_f32_16x16x32_bf16) per host and wave, ISA
+# counted likewise (tools/isa_count.py encoder_split_counts).
+ENC_SPLIT_MFMA_PER_HOST = {50: (516, 504)}
+
+
+def encoder_split(H: int) -> bool:
+    """K2 runs the split-bf16 feed-forward at these H (the tail-resident mode)."""
+    return H in ENC_SPLIT_MFMA_PER_HOST
+
+
+def encoder_split_executed_flops_per_window(H: int):
+    """(fp32 MFMA flops, bf16 MFMA flops) K2's split form executes per window."""
+    f32, bf = ENC_SPLIT_MFMA_PER_HOST[H]
+    return f32 * 2048 * H / 16, bf * 16 * 16 * 32 * 2 * H / 16
+
+
 # Fused tuning encoder (pgp_tunef.hip): v_mfma_f32_16x16x4_f32 per unit of 16
 # (window, host) pairs, the static counts of the built ISA (tools/isa_count.py
 # tune_counts, held equal by tests/test_roofline_isa.py).  tf_fwd_kernel's count

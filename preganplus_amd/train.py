@@ -1340,8 +1340,9 @@ def _bind_online(L):
     L.pgp_online_stage_ms.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
     L.pgp_online_steps.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
     L.pgp_online_gan_step.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    L.pgp_online_issue_worker.argtypes = [ctypes.c_void_p, ctypes.c_int]
     for f in ("pgp_online_create", "pgp_online_destroy", "pgp_online_step", "pgp_online_timing",
-              "pgp_online_stage_ms", "pgp_online_steps", "pgp_online_gan_step"):
+              "pgp_online_stage_ms", "pgp_online_steps", "pgp_online_gan_step", "pgp_online_issue_worker"):
         getattr(L, f).restype = ctypes.c_int
     L._pgp_online_bound = True
 
@@ -1478,6 +1479,12 @@ class OnlineTrainStep:
         except BaseException as e:   # surfaced by run() after the C call returns
             self._err = e
             return -1
+
+    def issue_worker(self, on: bool):
+        """World size 1, two streams: issue the GAN stream's launches from the
+        library's second host thread while this one issues the tuning backward
+        (the default; off: one thread issues both)."""
+        _native.check(self.tr._L.pgp_online_issue_worker(self._h, int(on)), "pgp_online_issue_worker")
 
     def timing(self, on: bool):
         """Record HIP events in the native steps that follow (stage_ms())."""

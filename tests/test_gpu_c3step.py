@@ -109,6 +109,36 @@ def test_native_step_equals_python_composition(H):
     assert {t["step"] for t in tr_b.tensors if t["section"] in ("gen", "disc") and t["trainable"]} == {3.0}
 
 
+@pytest.mark.parametrize("H", [16, 50])
+def test_native_step_issue_worker_equals_one_thread(H):
+    """pgp_online_issue_worker: the GAN stream's launches issued from the
+    library's second host thread (the default at world size 1) == one thread
+    issuing both streams, over five back-to-back steps (the worker spinning
+    between them) and a step after an idle pause (the worker asleep): every
+    weight, moment, the tuning state, the GAN labels and the step counts."""
+    import time
+    main = torch.cuda.Stream()
+    with torch.cuda.stream(main):
+        tr_a, sa = _online(H, 6, native=True)
+        tr_b, sb = _online(H, 6, native=True)
+        sb.issue_worker(False)
+        for s in (sa, sb):
+            for _ in range(5):
+                s.run()
+            torch.cuda.synchronize()
+            time.sleep(0.05)
+            s.run()
+        torch.cuda.synchronize()
+    for x, y in ((tr_a.P, tr_b.P), (tr_a.m, tr_b.m), (tr_a.v, tr_b.v), (sa.tun.state, sb.tun.state),
+                 (sa.target, sb.target), (sa.sim_out, sb.sim_out), (sa.tun.loss, sb.tun.loss), (sa.emb, sb.emb)):
+        np.testing.assert_array_equal(x.cpu().numpy(), y.cpu().numpy())
+    sa.sync()
+    sb.sync()
+    for t_a, t_b in zip(tr_a.tensors, tr_b.tensors):
+        assert t_a["step"] == t_b["step"], t_a["name"]
+    assert {t["step"] for t in tr_a.tensors if t["section"] in ("gen", "disc") and t["trainable"]} == {6.0}
+
+
 def test_native_sync_updates_tune_state_and_dptuner():
     """after native steps, sync() writes the tuning state into the
     TuneState the step was built with and re-anchors the DPTuner's host step

@@ -142,6 +142,39 @@ def test_split_bf16_decoder_vs_fp32_decoder(H):
     assert not np.array_equal(a["logits"], b["logits"])   # the two forms really ran
 
 
+def test_split_bf16_encoder_vs_fp32_encoder():
+    """K2's split-bf16 feed-forward (the default at H = 50: both layers' linear1
+    / linear2 as six bf16 MFMAs per fp32 product, pgp_encoder.hip EncS) and its
+    fp32-MFMA form: both within the north-star tolerance of the fp64 oracle
+    (latent included), the split form no less accurate (worst latent / logit /
+    proto error within twice the fp32 form's), every decision equal, and the
+    two forms really ran (different bits).  (A repack of the master re-derives
+    the split image: tests/test_gpu_repack.py, device repack == host pack at
+    H = 50.)"""
+    H = 50
+    rng = np.random.Generator(np.random.PCG64(350))
+    w = W.synth_weights(H, seed=4)
+    x, s = c2(rng, 517, H, dense=9)
+    ref = O.forward(w, x, s)
+    ref["sched32"] = s.astype(np.float32)
+    m = get_model(H, w, "esplit50")
+    m.encoder_split(True)
+    a = run(m, x, s, latent=True)
+    m.encoder_split(False)
+    b = run(m, x, s, latent=True)
+    m.encoder_split(True)
+    assert_parity(a, ref, w, s)
+    assert_parity(b, ref, w, s)
+    for k in ("latent", "logits", "protos"):
+        n = ref[k].shape[0]
+        ea = np.abs(a[k][:n].astype(np.float64) - ref[k]).max()
+        eb = np.abs(b[k][:n].astype(np.float64) - ref[k]).max()
+        assert ea <= 2 * eb + 1e-7, (k, ea, eb)
+    for k in ("cls", "any", "keep", "final_target", "gen_target"):
+        assert np.array_equal(a[k], b[k]), k
+    assert not np.array_equal(a["latent"], b["latent"])
+
+
 @pytest.mark.parametrize("H,dense", [(50, 0), (50, 3000), (16, 0), (16, 3000)])
 def test_split_bf16_gan_vs_fp32_gan(H, dense):
     """K3's split-bf16 form (pgp_gansplit.hip; the default at H = 16 and 50 for

@@ -28,6 +28,20 @@ def test_encoder_mfma_count_matches_built_library():
 
 @pytest.mark.skipif(not os.path.exists(LIB) or not os.path.exists("/opt/rocm/lib/llvm/bin/llvm-objdump"),
                     reason="built library / llvm-objdump absent")
+def test_encoder_split_mfma_counts_match_built_library():
+    """The split feed-forward form: its fp32 MFMAs are the fp32 form's minus the
+    feed-forward's (2 layers x (4 x 13 + 3 x 16) x 3 steps = 600), its bf16
+    MFMAs 6 per 32-k block (2 layers x (4 x 2 + 3 x 2) x 6 x 3 steps = 504)."""
+    import isa_count
+    counts = isa_count.encoder_split_counts(tuple(R.ENC_SPLIT_MFMA_PER_HOST))
+    for H, (f32, bf) in R.ENC_SPLIT_MFMA_PER_HOST.items():
+        assert counts[H][:2] == (f32, bf), (H, counts[H])
+    assert R.ENC_SPLIT_MFMA_PER_HOST[50][0] == R.ENC_MFMA_PER_HOST[50] - 2 * (4 * 13 + 3 * 16) * 3
+    assert R.ENC_SPLIT_MFMA_PER_HOST[50][1] == 2 * (4 * 2 + 3 * 2) * 6 * 3
+
+
+@pytest.mark.skipif(not os.path.exists(LIB) or not os.path.exists("/opt/rocm/lib/llvm/bin/llvm-objdump"),
+                    reason="built library / llvm-objdump absent")
 def test_tuning_kernel_mfma_counts_match_built_library():
     import isa_count
     counts = isa_count.tune_counts(tuple(R.TUNE_MFMA_PER_UNIT))

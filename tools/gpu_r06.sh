@@ -64,6 +64,13 @@ for step in "$@"; do
       tail -2 $OUT/t_fleet.out
       run fleet 400 python3 -u bench.py --config fleet --steps 100 --warmup 5 --no-cpu-baseline
       ;;
+    abissue)
+      run t_c3 600 $PYT tests/test_gpu_c3step.py -m gpu
+      run abi16 600 python3 -u tools/ab_bench.py --rounds 4 --args "--config tune --hosts 16 --steps 100 --warmup 10 --no-cpu-baseline" worker= serial=PGP_BENCH_SERIAL_ISSUE=1
+      grep median $OUT/abi16.out
+      run abi50 600 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" worker= serial=PGP_BENCH_SERIAL_ISSUE=1
+      grep median $OUT/abi50.out
+      ;;
     abbwd)
       PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_bwdfirst.so run t_bwd 600 $PYT tests/test_gpu_c3step.py -m gpu
       run abb16 600 python3 -u tools/ab_bench.py --rounds 4 --args "--config tune --hosts 16 --steps 100 --warmup 10 --no-cpu-baseline" base= bwd=PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_bwdfirst.so

@@ -51,18 +51,37 @@ def tune_counts(Hs=(16, 50), lib=LIB):
     return out
 
 
+def _encoder_body(asm, H, split, lib):
+    m = re.search(rf"<_ZN3pgp12_GLOBAL__N_114encoder_kernelILi{H}ELb{int(split)}EEEvNS_7FwdArgsE>:\n(.*?)s_endpgm",
+                  asm, re.S)
+    if m is None:
+        raise RuntimeError(f"encoder_kernel<{H}, {split}> not found in {lib}")
+    return m.group(1)
+
+
 def encoder_counts(Hs=(16, 50), lib=LIB):
-    """{H: (mfma, other_valu)} for encoder_kernel<H> in the built library."""
+    """{H: (mfma, other_valu)} for encoder_kernel<H> (the fp32 form) in the built library."""
     asm = _disasm(lib, "encoder_kernel")
     out = {}
     for H in Hs:
-        m = re.search(rf"<_ZN3pgp12_GLOBAL__N_114encoder_kernelILi{H}EEEvNS_7FwdArgsE>:\n(.*?)s_endpgm", asm, re.S)
-        if m is None:
-            raise RuntimeError(f"encoder_kernel<{H}> not found in {lib}")
-        body = m.group(1)
+        body = _encoder_body(asm, H, False, lib)
         mfma = len(re.findall(r"^\s+v_mfma", body, re.M))
         valu = len(re.findall(r"^\s+v_", body, re.M)) - mfma
         out[H] = (mfma, valu)
+    return out
+
+
+def encoder_split_counts(Hs=(50,), lib=LIB):
+    """{H: (f32 16x16x4 MFMAs, bf16 16x16x32 MFMAs, other VALU)} per host and
+    wave of the split-feed-forward form encoder_kernel<H, true>."""
+    asm = _disasm(lib, "encoder_kernel")
+    out = {}
+    for H in Hs:
+        body = _encoder_body(asm, H, True, lib)
+        f32 = len(re.findall(r"^\s+v_mfma_f32_16x16x4", body, re.M))
+        bf = len(re.findall(r"^\s+v_mfma_f32_16x16x32_bf16", body, re.M))
+        valu = len(re.findall(r"^\s+v_", body, re.M)) - len(re.findall(r"^\s+v_mfma", body, re.M))
+        out[H] = (f32, bf, valu)
     return out
 
 
@@ -89,7 +108,7 @@ def kernel_isa_hash(name, H=None, lib=LIB, targs=None):
     # targs: every integer template argument (e.g. gan_kernel<16, 16>: the same
     # H has several instantiations); otherwise the first whose first is H
     if targs:
-        targ = "I" + "".join(f"Li{int(t)}E" for t in targs) + "E"
+        targ = "I" + "".join(f"Lb{int(t)}E" if isinstance(t, bool) else f"Li{int(t)}E" for t in targs) + "E"
     else:
         targ = rf"ILi{H}E" if H is not None else ""
     m = re.search(rf"^[0-9a-f]+ <(_ZN3pgp12_GLOBAL__N_1\d+{name}{targ}[^>]*)>:\n(.*?)(?=^[0-9a-f]+ <|\Z)", asm,
@@ -108,6 +127,8 @@ if __name__ == "__main__":
     Hs = [int(h) for h in sys.argv[1:]] or [16, 50]
     for H, (mfma, valu) in encoder_counts(Hs).items():
         print(f"H={H}: {mfma} MFMA (16x16x4 f32), {valu} other VALU per host and wave")
+    for H, (f32, bf, valu) in encoder_split_counts([h for h in Hs if h == 50]).items():
+        print(f"H={H} split FFN: {f32} MFMA 16x16x4 f32 + {bf} MFMA 16x16x32 bf16, {valu} other VALU per host and wave")
     for H, d in tune_counts(Hs).items():
         print(f"H={H}: fused tuning kernels, MFMA per unit: {d}")
 

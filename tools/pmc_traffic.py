@@ -45,10 +45,12 @@ def main():
         wr = sum(d["WRITE_SIZE"]) / len(d["WRITE_SIZE"]) * 1024
         print(f"{k:28s} FETCH {fe / 1e6:10.1f} MB  WRITE {wr / 1e6:10.1f} MB  corrected {(2 * fe + wr) / 1e6:10.1f} MB"
               f"  (n={len(d['FETCH_SIZE'])})")
-        m = re.match(r"(\w+?)_kernel<(\d+)((?:, \d+)*)>", k)
+        m = re.match(r"(\w+?)_kernel<(\d+)((?:, (?:\d+|true|false))*)>", k)
         if not m or int(m.group(2)) != H or (only and m.group(1) not in only):
             continue
-        targs = [H] + [int(x) for x in m.group(3).split(",")[1:]] if m.group(3) else None
+        # integer and bool template arguments (encoder_kernel<50, true>: the split form)
+        targs = ([H] + [x.strip() == "true" if x.strip() in ("true", "false") else int(x)
+                        for x in m.group(3).split(",")[1:]] if m.group(3) else None)
         h = isa_count.kernel_isa_hash(m.group(1) + "_kernel", H, targs=targs)
         out = {"fetch_bytes_raw": fe, "write_bytes": wr, "hbm_bytes_per_launch": 2 * fe + wr, "batch": batch,
                "kernel": k, "dispatches": len(d["FETCH_SIZE"]), "isa_sha256": h, "template_args": targs,
