@@ -243,7 +243,8 @@ def main():
         traffic = load_traffic(H, B, targs=[H, esplit])
         kn = {"gat_agg": "gat_agg", "encoder": "encoder", "decoder": "decoder_split" if split else "decoder",
               "gan": "gan_split" if gsplit else "gan"}
-        k_traffic = {k: load_traffic(H, B, v, targs=[H, esplit] if k == "encoder" else None) for k, v in kn.items()}
+        ktargs = {"encoder": [H, esplit], "gan": [H, 16 if B >= 65536 else 4] if gsplit else None}
+        k_traffic = {k: load_traffic(H, B, v, targs=ktargs.get(k)) for k, v in kn.items()}
         path_bytes = R.path_bytes_per_window(H) * B
         res = {
             "metric": "host-windows/sec (detect+diagnose+generate)",

@@ -444,9 +444,9 @@ hipError_t launch(const FwdArgs& a, hipStream_t st) {
 }  // namespace
 
 hipError_t launch_gan(const FwdArgs& a, hipStream_t st) {
-  // the split form's 16-wave workgroups at large batches; below 64 K windows the
-  // fp32 kernel's 4-wave workgroups spread the batch over more CUs
-  if (a.ganb != nullptr && gan_split_floats(a.H) > 0 && (a.B + 15) / 16 >= kGanSmallBlocks)
+  // the split form at every batch (its own 4-wave workgroups below 64 K
+  // windows): a window's outputs do not depend on the batch it arrives in
+  if (a.ganb != nullptr && gan_split_floats(a.H) > 0)
     return launch_gan_split(a, st);
   switch (a.H) {
 #define CASE(h) \

@@ -1,7 +1,9 @@
 // pgp_gansplit.hip — K3 (generator + discriminator + decision argmaxes,
 // models.py:118-151, 258-291; PreGANPlus.py:84-105; Stats.py:162-166) with its
 // contractions on split-bf16 MFMAs (v_mfma_f32_16x16x32_bf16), at H = 16 and 50
-// (batches of 64 K windows and more; smaller ones run gan_kernel).
+// (16-wave workgroups from 64 K windows up, 4-wave ones below: every wave
+// computes its 16 windows the same way, so the outputs do not depend on the
+// batch a window arrives in).
 //
 // Same phases, ring and outputs as gan_kernel (pgp_gan.hip):
 //   1. Gen1, embedding columns        hg  = W1[:, :2H] . vec(emb)
@@ -28,7 +30,9 @@
 namespace pgp {
 namespace {
 
-constexpr int kSWaves = 16;
+constexpr int kSWaves = 16;      // waves per workgroup at large batches
+constexpr int kSWavesSmall = 4;  // below kSSmallBlocks blocks of 16 windows (spread over more CUs)
+constexpr long kSSmallBlocks = 16L * 256;
 constexpr int kSQP = 2;  // schedule pairs per ring chunk
 #ifndef PGP_K3_OH
 #define PGP_K3_OH 1
@@ -59,7 +63,8 @@ struct GanS {
   static constexpr int SLOT = SLOT_G * G::FQ;
   static constexpr int TGT = 2 * G::C * 16;  // int8 targets per wave
   static constexpr int OH = G::C * 16;       // int8 one-hot row index per (container, window) of a wave
-  static constexpr int LDS_BYTES = 2 * SLOT * 4 + kSWaves * (TGT + OH);
+  static constexpr int lds_bytes(int nw) { return 2 * SLOT * 4 + nw * (TGT + OH); }
+  static constexpr int LDS_BYTES = lds_bytes(kSWaves);
   PGP_DEV static void chunk(int k, const float* planes, const float** src, int* ng) {
     if (k == 0) {
       *src = planes + OFF_E * 256;
@@ -148,11 +153,10 @@ PGP_DEV void planes_at(const float* F, int lane, u32x4 (&w)[3]) {
 
 __device__ __attribute__((aligned(8))) float k3s_zero_pair[2];  // never written
 
-template <int H>
-__global__ __launch_bounds__(kSWaves * 64) void gan_split_kernel(FwdArgs a) {
+template <int H, int NW>
+__global__ __launch_bounds__(NW * 64) void gan_split_kernel(FwdArgs a) {
   using G = Geo<H>;
   using S = GanS<H>;
-  constexpr int NW = kSWaves;
   extern __shared__ __attribute__((aligned(16))) float smem[];  // ring [2][SLOT] | targets
   const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -170,7 +174,7 @@ __global__ __launch_bounds__(kSWaves * 64) void gan_split_kernel(FwdArgs a) {
   // kernel's traffic).  Rows proven one-hot only: per window exactly C nonzero
   // values, all exactly 1.0, and every row recorded; otherwise the wave reads
   // its rows as before.
-  signed char* oh = reinterpret_cast<signed char*>(smem + 2 * S::SLOT) + kSWaves * S::TGT + wv * S::OH;
+  signed char* oh = reinterpret_cast<signed char*>(smem + 2 * S::SLOT) + NW * S::TGT + wv * S::OH;
   if (kK3OneHot)
     for (int i = lane; i < S::OH; i += 64) oh[i] = -1;
   int n_one = 0, n_nz = 0;
@@ -493,20 +497,25 @@ __global__ __launch_bounds__(kSWaves * 64) void gan_split_kernel(FwdArgs a) {
   }
 }
 
+template <int H, int NW>
+hipError_t launch_nw(const FwdArgs& a, hipStream_t st) {
+  using S = GanS<H>;
+  static bool attr = [] {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gan_split_kernel<H, NW>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, S::lds_bytes(NW));
+    return true;
+  }();
+  (void)attr;
+  const long nblk = (a.B + 15) / 16;
+  const int grid = (int)((nblk + NW - 1) / NW);
+  gan_split_kernel<H, NW><<<grid, NW * 64, S::lds_bytes(NW), st>>>(a);
+  return hipGetLastError();
+}
 template <int H>
 hipError_t launch_t(const FwdArgs& a, hipStream_t st) {
   if constexpr (gan_split<H>()) {
-    using S = GanS<H>;
-    static bool attr = [] {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gan_split_kernel<H>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, S::LDS_BYTES);
-      return true;
-    }();
-    (void)attr;
-    const long nblk = (a.B + 15) / 16;
-    const int grid = (int)((nblk + kSWaves - 1) / kSWaves);
-    gan_split_kernel<H><<<grid, kSWaves * 64, S::LDS_BYTES, st>>>(a);
-    return hipGetLastError();
+    if ((a.B + 15) / 16 < kSSmallBlocks) return launch_nw<H, kSWavesSmall>(a, st);
+    return launch_nw<H, kSWaves>(a, st);
   }
   return hipErrorInvalidValue;
 }

@@ -177,14 +177,15 @@ def test_split_bf16_encoder_vs_fp32_encoder():
 
 @pytest.mark.parametrize("H,dense", [(50, 0), (50, 3000), (16, 0), (16, 3000)])
 def test_split_bf16_gan_vs_fp32_gan(H, dense):
-    """K3's split-bf16 form (pgp_gansplit.hip; the default at H = 16 and 50 for
-    batches of 64 K windows and more; one-hot schedule blocks in three products,
-    dense ones in six) against its fp32-MFMA form on one 65,536-window launch:
-    the first 2,048 windows (and the dense tail) within tolerance of the fp64
-    oracle for both forms, the split form no less accurate, every decision of
-    the whole launch equal (none sits in band here), and a window's outputs
-    independent of its wave's other windows (the one-hot shortcut is taken per
-    wave: 16 windows alone give the same bits)."""
+    """K3's split-bf16 form (pgp_gansplit.hip; the default at H = 16 and 50 at
+    every batch; one-hot schedule blocks in three products, dense ones in six)
+    against its fp32-MFMA form on one 65,536-window launch: the first 2,048
+    windows (and the dense tail) within tolerance of the fp64 oracle for both
+    forms, the split form no less accurate, every decision of the whole launch
+    equal except generator targets at fp32 near-ties (in band for both forms),
+    and a window's outputs independent of the batch and of its wave's other
+    windows (the one-hot shortcut is taken per wave: 16 windows alone and a
+    300-window batch on 4-wave workgroups give the same bits)."""
     from preganplus_amd.model import to_numpy
     B = 65536
     w = W.synth_weights(H, seed=5) if H == 50 else W.load_npz("preganplus_amd/data/simulator_16.npz")[0]
@@ -199,22 +200,34 @@ def test_split_bf16_gan_vs_fp32_gan(H, dense):
     b = to_numpy(m.forward(x, s))
     m.gan_split(True)
     torch.cuda.synchronize()
-    for k in ("keep", "final_target", "gen_target", "any", "cls"):
+    for k in ("keep", "final_target", "any", "cls"):
         assert np.array_equal(a[k], b[k]), k
+    # generator targets: a container whose two largest new-schedule values tie
+    # to within fp32 rounding (4 tanh(.) saturating at 1.0 in fp32 for two
+    # hosts, frequent with the shipped H = 16 weights) may break the tie either
+    # way in either form; every window where the forms differ must be in band
+    # against the fp64 oracle for BOTH forms (assert_parity below), and few
+    dw = np.nonzero((a["gen_target"] != b["gen_target"]).any(axis=1))[0]
+    assert dw.size <= 16, dw.size
     idx = np.r_[0:2048, B - 256:B]
+    idx = np.unique(np.r_[idx, dw])
     xs, ss = x[idx].cpu().numpy().astype(np.float64), s[idx].cpu().numpy().astype(np.float64)
     ref = O.forward(w, xs, ss)
     ref["sched32"] = ss.astype(np.float32)
     sa = {k: v[idx] for k, v in a.items()}
     sb = {k: v[idx] for k, v in b.items()}
-    assert_parity(sa, ref, w, ss)
-    assert_parity(sb, ref, w, ss)
+    sta = assert_parity(sa, ref, w, ss)
+    stb = assert_parity(sb, ref, w, ss)
+    assert sta["gen"]["mismatch"] <= dw.size and stb["gen"]["mismatch"] <= dw.size, (sta["gen"], stb["gen"])
     ea = np.abs(sa["probs"].astype(np.float64) - ref["probs"]).max()
     eb = np.abs(sb["probs"].astype(np.float64) - ref["probs"]).max()
     assert ea <= 2 * eb + 1e-7, (ea, eb)
-    c = to_numpy(m.forward(x[:16].contiguous(), s[:16].contiguous()))   # (a 16-window batch runs gan_kernel)
-    for k in ("keep", "final_target", "gen_target"):
-        assert np.array_equal(a[k][:16], c[k]), k
+    # the split form runs at every batch (4-wave workgroups below 64 K
+    # windows): a window's outputs do not depend on the batch it arrives in
+    for lo, hi in ((0, 16), (B // 2 - 5, B // 2 + 300)):
+        c = to_numpy(m.forward(x[lo:hi].contiguous(), s[lo:hi].contiguous()))
+        for k in ("keep", "final_target", "gen_target", "probs"):
+            assert np.array_equal(a[k][lo:hi], c[k]), (k, lo, hi)
 
 
 @pytest.mark.parametrize("H", [16, 50])
@@ -258,9 +271,13 @@ def test_k3_onehot_rebuild_guard(H):
     b = to_numpy(m.forward(x, s))
     m.gan_split(True)
     torch.cuda.synchronize()
-    for key in ("keep", "final_target", "gen_target", "any", "cls"):
+    for key in ("keep", "final_target", "any", "cls"):
         assert np.array_equal(a[key], b[key]), key
-    idx = np.concatenate([np.arange(16 * (c // 16), 16 * (c // 16) + 16) for c in cases])
+    # generator targets may differ only at fp32 near-ties (in band for both
+    # forms against the oracle: checked below on those windows)
+    dw = np.nonzero((a["gen_target"] != b["gen_target"]).any(axis=1))[0]
+    assert dw.size <= 16, dw.size
+    idx = np.concatenate([np.arange(16 * (c // 16), 16 * (c // 16) + 16) for c in cases] + [dw])
     xs, ss = x[idx].cpu().numpy().astype(np.float64), s[idx].cpu().numpy().astype(np.float64)
     ref = O.forward(w, xs, ss)
     ref["sched32"] = ss.astype(np.float32)

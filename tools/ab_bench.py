@@ -8,7 +8,7 @@ and the median.
 
 The library reads no tuning switches from the environment (round 5 removed
 them, _native.REMOVED_ENV): a variant is another build (PGP_LIB) or a
-bench.py switch.
+bench.py switch (ARGS=--flag in a variant appends that switch to --args).
 """
 import argparse
 import json
@@ -37,8 +37,10 @@ def main():
     extra = {n: [] for n, _ in variants}
     for r in range(a.rounds):
         for name, env in variants:
+            env = dict(env)
+            extra_args = env.pop("ARGS", "").split()
             e = dict(os.environ, **env)
-            out = subprocess.run([sys.executable, "bench.py"] + a.args.split(), env=e, capture_output=True, text=True,
+            out = subprocess.run([sys.executable, "bench.py"] + a.args.split() + extra_args, env=e, capture_output=True, text=True,
                                  timeout=a.timeout)
             if out.returncode != 0:
                 print(out.stderr[-2000:], flush=True)

@@ -59,6 +59,22 @@ for step in "$@"; do
       run c2fp32g 300 python3 -u bench.py --steps 100 --warmup 5 --no-cpu-baseline --fp32-gan
       grep -h -o "\"ms_per_step\": [0-9.]*\|\"decoder\": [0-9.]*\|\"gan\": [0-9.]*" $OUT/c2split.out $OUT/c2fp32.out $OUT/c2fp32g.out
       ;;
+    traffic)  # FETCH / WRITE passes of the C2 kernels at H=50 and 16 (tools/pmc_traffic.py gpurun_out/T/trH B H)
+      mkdir -p $OUT/tr50 $OUT/tr16
+      pmc tr50/pmc_fetch FETCH_SIZE --steps 3 --warmup 1 --no-cpu-baseline
+      pmc tr50/pmc_write WRITE_SIZE --steps 3 --warmup 1 --no-cpu-baseline
+      pmc tr16/pmc_fetch FETCH_SIZE --hosts 16 --steps 3 --warmup 1 --no-cpu-baseline
+      pmc tr16/pmc_write WRITE_SIZE --hosts 16 --steps 3 --warmup 1 --no-cpu-baseline
+      ;;
+    tline)  # C3 kernel traces (H=50, 16) -> per-step timelines
+      run tl50 240 rocprofv3 --kernel-trace --output-format csv -d $OUT/tl50 -o tl -- python3 bench.py --config tune --hosts 50 --steps 40 --warmup 5 --no-cpu-baseline
+      run tl16 240 rocprofv3 --kernel-trace --output-format csv -d $OUT/tl16 -o tl -- python3 bench.py --config tune --hosts 16 --steps 100 --warmup 10 --no-cpu-baseline
+      for h in 50 16; do python3 tools/tune_timeline.py $(find $OUT/tl$h -name "*kernel_trace.csv" | head -1) > $OUT/timeline$h.txt; head -3 $OUT/timeline$h.txt; done
+      ;;
+    abenc)
+      run abenc 900 python3 -u tools/ab_bench.py --rounds 4 --args "--steps 100 --warmup 5 --no-cpu-baseline" split= fp32enc=ARGS=--fp32-encoder
+      grep median $OUT/abenc.out
+      ;;
     tfleet)
       run t_fleet 600 $PYT tests/test_gpu_fleet_stream.py -m gpu
       tail -2 $OUT/t_fleet.out
