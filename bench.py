@@ -744,7 +744,7 @@ def bench_tune(args):
     # tuning forward + backward, timed live with HIP events recorded on their
     # stream inside the library (pgp_tune_timing) over extra eager steps after
     # the timed region; achieved = their executed MFMA flops (ISA-counted per
-    # unit, roofline.TUNE_MFMA_PER_UNIT) / the mean launch duration
+    # unit, roofline.TUNE_MFMA_PER_UNIT / TUNE_BF16_PER_UNIT) / the mean launch duration
     RL = R_ROOF  # (R is the window count here)
     L = _native.lib()
     L.pgp_tune_timing.argtypes = [ctypes.c_int]
@@ -778,8 +778,9 @@ def bench_tune(args):
         roof = {"kernel": f"tf_*_kernel<{H}> ({RL.TUNE_FUSED_LAUNCHES[k]}, the longest fused launch)",
                 "bound": "mfma", "achieved": rates[k], "peak": RL.PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                 "frac": rates[k] / RL.PEAK_FP32_TFLOPS, "traffic": None,
-                "basis": "executed v_mfma_f32_16x16x4_f32 flops of the batch's units (ISA count per unit) / mean "
-                         "launch duration (HIP events on the launch stream)",
+                "basis": "executed MFMA flops of the batch's units (ISA count per unit; the split-bf16 GEMMs' "
+                         "v_mfma_f32_16x16x32_bf16 counted at 1/16, the fp32 / bf16 dense-peak ratio: "
+                         "fp32-MFMA-equivalent work) / mean launch duration (HIP events on the launch stream)",
                 "fused_launches": {n: {"ms": float(t), "tflops": float(r), "frac": float(r / RL.PEAK_FP32_TFLOPS)}
                                    for n, t, r in zip(RL.TUNE_FUSED_LAUNCHES, fused_ms, rates)},
                 "fused_total": {"ms": float(fused_ms.sum()),

@@ -1304,7 +1304,7 @@ hipError_t tune_fwd_h(const TunePlan& p, const float* win, const float* P, float
   t.P = P;
   t.frags = ws + p.tff;
   if (fk.side == st) {  // all on the caller's stream: every packing in ONE launch
-    const int nb_dec = (int)((Q::NOP * Q::KD + 255) / 256), nb_tf = (int)((tf_frag_floats(H) + 255) / 256);
+    const int nb_dec = (int)((Q::NOP * Q::KD + 255) / 256), nb_tf = (int)((tf_pack_items(H) + 255) / 256);
     // ... and the GAT forward in the same launch
     const GatFwdIn g{B, win, ws + p.win, ws + p.g, ws + p.xb, ws + p.gs};
     TCK((tune_pack_kernel<H><<<nb_dec + 1 + nb_tf + (3 * B + 3) / 4, 256, 0, st>>>(
@@ -1312,7 +1312,7 @@ hipError_t tune_fwd_h(const TunePlan& p, const float* win, const float* P, float
   } else {
     // main: the encoder's fragments packed from P and the GAT forward in ONE
     // launch (the packing kernel's tf blocks, then the GAT blocks)
-    const int nb_tf = (int)((tf_frag_floats(H) + 255) / 256);
+    const int nb_tf = (int)((tf_pack_items(H) + 255) / 256);
     const GatFwdIn g{B, win, ws + p.win, ws + p.g, ws + p.xb, ws + p.gs};
     // (and the GAT's Mt for the backward: its block, not a side-stream
     // launch the forward's join would wait for)

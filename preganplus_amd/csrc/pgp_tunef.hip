@@ -166,6 +166,56 @@ PGP_DEV void tf_gemm(f32x4 (&acc)[NO][3], const float* A, BF bsrc, int lane) {
   tf_gemm_side<NO, KSn>(acc, A, bsrc, lane, [](int) {});
 }
 
+// The same product on split-bf16 planes (TF<H>::SPLIT): A = NO tiles x NB
+// 32-k blocks x 3 planes of 1-KiB fragments in LDS (tf_split_item), B's k-step
+// s of step w = bsrc(s, w), block b = k-steps 8b..8b+7 (zero past KSn) split in
+// registers per step; six v_mfma_f32_16x16x32_bf16 per block and tile
+// (mfma_bf6: the fp32 product to within 2^-26 of |w x|, fp32 accumulation).
+// Step by step, so only one step's split B operand (NB x 12 registers) is live;
+// the NO * KGn side slots are spread over the 3 * NO * NB blocks.
+template <int NO, int KSn, class BF, class SIDE>
+PGP_DEV void tf_gemm_split_side(f32x4 (&acc)[NO][3], const float* A, BF bsrc, int lane, SIDE side) {
+  constexpr int NB = (KSn + 7) / 8, KGn = (KSn + 3) / 4, NS = NO * KGn, NI = 3 * NO * NB;
+#pragma unroll
+  for (int w = 0; w < 3; ++w) {
+    u32x4 xs[NB][3];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = 8 * b + e < KSn ? bsrc(8 * b + e, w) : 0.f;
+      split8(v, xs[b]);
+    }
+#pragma unroll
+    for (int o = 0; o < NO; ++o) {
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        u32x4 wp[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+          wp[k] = *reinterpret_cast<const u32x4*>(A + ((o * NB + b) * 3 + k) * 256 + lane * 4);
+        acc[o][w] = mfma_bf6(wp, xs[b], acc[o][w]);
+        const int it = (w * NO + o) * NB + b;
+#pragma unroll
+        for (int i = it * NS / NI; i < (it + 1) * NS / NI; ++i) side(i);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+template <int NO, int KSn, class BF>
+PGP_DEV void tf_gemm_split(f32x4 (&acc)[NO][3], const float* A, BF bsrc, int lane) {
+  tf_gemm_split_side<NO, KSn>(acc, A, bsrc, lane, [](int) {});
+}
+// fp32 or split form by TF<H>::SPLIT (A: the matching LDS image)
+template <bool SPL, int NO, int KSn, class BF, class SIDE>
+PGP_DEV void tf_gemm_any(f32x4 (&acc)[NO][3], const float* A, BF bsrc, int lane, SIDE side) {
+  if constexpr (SPL)
+    tf_gemm_split_side<NO, KSn>(acc, A, bsrc, lane, side);
+  else
+    tf_gemm_side<NO, KSn>(acc, A, bsrc, lane, side);
+}
+
 // accumulators initialised with a per-row bias (LDS, natural rows)
 template <int NO>
 PGP_DEV void init_bias(f32x4 (&acc)[NO][3], const float* bias, int g) {
@@ -445,8 +495,11 @@ PGP_DEV void load_params(float* sp, const float* __restrict__ P, int layer) {
 template <int H>
 struct FwdL {
   using F = TF<H>;
+  // F1 / F2 as fp32 fragments or (SPLIT) split planes (the first P_F1 + P_F2
+  // fragments of the layer's plane block)
+  static constexpr int N_F1 = F::SPLIT ? F::P_F1 : F::G_F1, N_F2 = F::SPLIT ? F::P_F2 : F::G_F2;
   static constexpr int W_TE = 0, W_IN = W_TE + F::G_TE * 256, W_O = W_IN + F::G_IN * 256,
-                       W_F1 = W_O + F::G_O * 256, W_F2 = W_F1 + F::G_F1 * 256, PAR = W_F2 + F::G_F2 * 256,
+                       W_F1 = W_O + F::G_O * 256, W_F2 = W_F1 + N_F1 * 256, PAR = W_F2 + N_F2 * 256,
                        TOTAL = PAR + TfPar<H>::SIZE;
 };
 
@@ -513,7 +566,12 @@ __global__ __launch_bounds__(kTfFwdWaves * 64, 1) void tf_fwd_kernel(TfArgs a) {
   const int layer = a.layer;
   const float* fr = a.frags + F::layer_off(layer);
   if (layer == 0) dma_groups(a.frags + F::TE_OFF, sm + L::W_TE, F::G_TE, wv, kTfFwdWaves, lane);
-  dma_groups(fr + F::OFF_IN, sm + L::W_IN, F::G_IN + F::G_O + F::G_F1 + F::G_F2, wv, kTfFwdWaves, lane);
+  if constexpr (F::SPLIT) {
+    dma_groups(fr + F::OFF_IN, sm + L::W_IN, F::G_IN + F::G_O, wv, kTfFwdWaves, lane);
+    dma_groups(a.frags + F::pl_off(layer), sm + L::W_F1, F::P_F1 + F::P_F2, wv, kTfFwdWaves, lane);
+  } else {
+    dma_groups(fr + F::OFF_IN, sm + L::W_IN, F::G_IN + F::G_O + F::G_F1 + F::G_F2, wv, kTfFwdWaves, lane);
+  }
   load_params<H>(sm + L::PAR, a.P, layer);
   TF_ST_INIT();
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -615,7 +673,7 @@ __global__ __launch_bounds__(kTfFwdWaves * 64, 1) void tf_fwd_kernel(TfArgs a) {
     init_bias<4>(Fh, par + Q::B1, g);
     {  // side work: norm1's x-hat tiles and rstd (every lane group: the same value)
       constexpr int NS = 3 * NT + 3, NG = 4 * F::KG, PER = (NS + NG - 1) / NG;
-      tf_gemm_side<4, F::KS>(Fh, sm + L::W_F1, [&](int s, int w) { return X[s >> 2][w][s & 3]; }, lane,
+      tf_gemm_any<F::SPLIT, 4, F::KS>(Fh, sm + L::W_F1, [&](int s, int w) { return X[s >> 2][w][s & 3]; }, lane,
                              [&](int i) {
 #pragma unroll
                                for (int k = 0; k < PER; ++k) {
@@ -639,7 +697,7 @@ __global__ __launch_bounds__(kTfFwdWaves * 64, 1) void tf_fwd_kernel(TfArgs a) {
       long rn[3];
       const bool okn = unit_rows<H>(u + 1, u1, npairs, j, rn);
       constexpr int NS = 3 * NT, NG = NT * F::KGF, PER = (NS + NG - 1) / NG;
-      tf_gemm_side<NT, 16>(R, sm + L::W_F2, [&](int s, int w) { return Fh[s >> 2][w][s & 3]; }, lane,
+      tf_gemm_any<F::SPLIT, NT, 16>(R, sm + L::W_F2, [&](int s, int w) { return Fh[s >> 2][w][s & 3]; }, lane,
                            [&](int i) {
 #pragma unroll
                              for (int k = 0; k < PER; ++k) {
@@ -721,8 +779,12 @@ PGP_DEV void sum_regions(float* __restrict__ dst, const float* src, int pitch, i
 template <int H>
 struct BffL {
   using F = TF<H>;
-  static constexpr int W_F1 = 0, W_F2 = W_F1 + F::G_F1 * 256, W_F2T = W_F2 + F::G_F2 * 256,
-                       W_F1T = W_F2T + F::G_F2T * 256, PAR = W_F1T + F::G_F1T * 256,
+  // the four matrices as fp32 fragments or (SPLIT) split planes, in the
+  // fragment buffer's order (one DMA)
+  static constexpr int N_F1 = F::SPLIT ? F::P_F1 : F::G_F1, N_F2 = F::SPLIT ? F::P_F2 : F::G_F2,
+                       N_F2T = F::SPLIT ? F::P_F2T : F::G_F2T, N_F1T = F::SPLIT ? F::P_F1T : F::G_F1T;
+  static constexpr int W_F1 = 0, W_F2 = W_F1 + N_F1 * 256, W_F2T = W_F2 + N_F2 * 256,
+                       W_F1T = W_F2T + N_F2T * 256, PAR = W_F1T + N_F1T * 256,
                        SCR = PAR + TfPar<H>::SIZE,
                        SCR_A = Scr<4>::SIZE, SCR_B = Scr<4>::SIZE,  // both operands <= 64 rows
                        TOTAL = SCR + kTfWaves * (SCR_A + SCR_B),
@@ -771,8 +833,11 @@ __global__ __launch_bounds__(kTfWaves * 64, 1) void tf_bwd_ffn_kernel(TfArgs a) 
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, g = lane >> 4, j = lane & 15;
   const int layer = a.layer;
-  dma_groups(a.frags + F::layer_off(layer) + F::OFF_F1, sm + L::W_F1, F::G_F1 + F::G_F2 + F::G_F2T + F::G_F1T, wv,
-             kTfWaves, lane);
+  if constexpr (F::SPLIT)
+    dma_groups(a.frags + F::pl_off(layer), sm + L::W_F1, F::PO_OT, wv, kTfWaves, lane);
+  else
+    dma_groups(a.frags + F::layer_off(layer) + F::OFF_F1, sm + L::W_F1, F::G_F1 + F::G_F2 + F::G_F2T + F::G_F1T,
+               wv, kTfWaves, lane);
   load_params<H>(sm + L::PAR, a.P, layer);
   TF_ST_INIT();
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -832,7 +897,8 @@ __global__ __launch_bounds__(kTfWaves * 64, 1) void tf_bwd_ffn_kernel(TfArgs a) 
 #pragma unroll
           for (int w = 0; w < 3; ++w) Y1[t][w] = y1(Y1, t, w);
         init_bias<4>(Fh, par + Q::B1, g);
-        tf_gemm<4, F::KS>(Fh, smz + L::W_F1, [&](int s, int w) { return Y1[s >> 2][w][s & 3]; }, lane);
+        tf_gemm_any<F::SPLIT, 4, F::KS>(Fh, smz + L::W_F1, [&](int s, int w) { return Y1[s >> 2][w][s & 3]; }, lane,
+                                        [](int) {});
         init_bias<NT>(X2, par + Q::B2, g);
 #pragma unroll
         for (int t = 0; t < NT; ++t)
@@ -848,12 +914,12 @@ __global__ __launch_bounds__(kTfWaves * 64, 1) void tf_bwd_ffn_kernel(TfArgs a) 
       TF_ST(2);
       {  // side work: dOut of the unit
         constexpr int NS = 3 * NT, NG = NT * F::KGF, PER = (NS + NG - 1) / NG;
-        tf_gemm_side<NT, 16>(X2, smz + L::W_F2, [&](int s, int w) { return Fh[s >> 2][w][s & 3]; }, lane,
-                             [&](int i) {
+        tf_gemm_any<F::SPLIT, NT, 16>(X2, smz + L::W_F2, [&](int s, int w) { return Fh[s >> 2][w][s & 3]; }, lane,
+                                      [&](int i) {
 #pragma unroll
-                               for (int k = 0; k < PER; ++k)
-                                 if (i * PER + k < NS) load_tile<NT>(dY, a.in, F::DP, row, ok, g, i * PER + k);
-                             });
+                                        for (int k = 0; k < PER; ++k)
+                                          if (i * PER + k < NS) load_tile<NT>(dY, a.in, F::DP, row, ok, g, i * PER + k);
+                                      });
       }
       __builtin_amdgcn_sched_barrier(0);
       TF_ST(3);
@@ -883,12 +949,13 @@ __global__ __launch_bounds__(kTfWaves * 64, 1) void tf_bwd_ffn_kernel(TfArgs a) 
         for (int w = 0; w < 3; ++w) dF[t][w] = zero4();
       {  // side work: norm1's x-hat, reloaded (L2): not held through the phases above
         constexpr int NS = 3 * NT, NG = 4 * F::KG, PER = (NS + NG - 1) / NG;
-        tf_gemm_side<4, F::KS>(dF, smz + L::W_F2T, [&](int s, int w) { return dY[s >> 2][w][s & 3]; }, lane,
-                               [&](int i) {
+        tf_gemm_any<F::SPLIT, 4, F::KS>(dF, smz + L::W_F2T, [&](int s, int w) { return dY[s >> 2][w][s & 3]; }, lane,
+                                        [&](int i) {
 #pragma unroll
-                                 for (int k = 0; k < PER; ++k)
-                                   if (i * PER + k < NS) load_tile<NT>(XH1, a.xh1, F::DP, row, ok, g, i * PER + k);
-                               });
+                                          for (int k = 0; k < PER; ++k)
+                                            if (i * PER + k < NS)
+                                              load_tile<NT>(XH1, a.xh1, F::DP, row, ok, g, i * PER + k);
+                                        });
       }
 #pragma unroll
       for (int t = 0; t < 4; ++t)
@@ -910,7 +977,8 @@ __global__ __launch_bounds__(kTfWaves * 64, 1) void tf_bwd_ffn_kernel(TfArgs a) 
       }
       __builtin_amdgcn_sched_barrier(0);
       // dy1 = W1^T dF + dR2 (residual)
-      tf_gemm<NT, 16>(dY, smz + L::W_F1T, [&](int s, int w) { return dF[s >> 2][w][s & 3]; }, lane);
+      tf_gemm_any<F::SPLIT, NT, 16>(dY, smz + L::W_F1T, [&](int s, int w) { return dF[s >> 2][w][s & 3]; }, lane,
+                                    [](int) {});
     }
     __builtin_amdgcn_sched_barrier(0);
     TF_ST(10);
@@ -947,8 +1015,9 @@ __global__ __launch_bounds__(kTfWaves * 64, 1) void tf_bwd_ffn_kernel(TfArgs a) 
 template <int H>
 struct BatL {
   using F = TF<H>;
+  static constexpr int N_OT = F::SPLIT ? F::P_OT : F::G_OT;  // Wo^T as fp32 fragments or split planes
   static constexpr int W_IN = 0, W_INT = W_IN + F::G_IN * 256, W_OT = W_INT + F::G_INT * 256,
-                       PAR = W_OT + F::G_OT * 256, SCR = PAR + TfPar<H>::SIZE,
+                       PAR = W_OT + N_OT * 256, SCR = PAR + TfPar<H>::SIZE,
                        SCR_A = Scr<F::NT>::SIZE, SCR_B = Scr<F::NT>::SIZE,
                        TOTAL = SCR + kTfWaves * (SCR_A + SCR_B);
   static constexpr int S_WO = 0, S_BO = H * H, SLAB = S_BO + H;
@@ -966,7 +1035,12 @@ __global__ __launch_bounds__(kTfWaves * 64, 1) void tf_bwd_att_kernel(TfArgs a) 
   const int layer = a.layer;
   const float* fr = a.frags + F::layer_off(layer);
   dma_groups(fr + F::OFF_IN, sm + L::W_IN, F::G_IN, wv, kTfWaves, lane);
-  dma_groups(fr + F::OFF_INT, sm + L::W_INT, F::G_INT + F::G_OT, wv, kTfWaves, lane);
+  if constexpr (F::SPLIT) {
+    dma_groups(fr + F::OFF_INT, sm + L::W_INT, F::G_INT, wv, kTfWaves, lane);
+    dma_groups(a.frags + F::pl_off(layer) + F::PO_OT * 256L, sm + L::W_OT, F::P_OT, wv, kTfWaves, lane);
+  } else {
+    dma_groups(fr + F::OFF_INT, sm + L::W_INT, F::G_INT + F::G_OT, wv, kTfWaves, lane);
+  }
   load_params<H>(sm + L::PAR, a.P, layer);
   TF_ST_INIT();
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1023,7 +1097,8 @@ __global__ __launch_bounds__(kTfWaves * 64, 1) void tf_bwd_att_kernel(TfArgs a) 
     for (int t = 0; t < NT; ++t)
 #pragma unroll
       for (int w = 0; w < 3; ++w) O[t][w] = zero4();
-    tf_gemm<NT, F::KS>(O, sm + L::W_OT, [&](int s, int w) { return dR1[s >> 2][w][s & 3]; }, lane);
+    tf_gemm_any<F::SPLIT, NT, F::KS>(O, sm + L::W_OT, [&](int s, int w) { return dR1[s >> 2][w][s & 3]; }, lane,
+                                     [](int) {});
     TF_ST(6);
     // attention backward (pgp_tune.hip attn_bwd_kernel, per lane)
     float dS[2][3][3];
@@ -1142,7 +1217,7 @@ hipError_t tf_launch(int kind, const TfArgs& a, int grid, hipStream_t st, hipEve
   }
   switch (kind) {
     case 0: {
-      const long n = F::TOTAL_FLOATS;
+      const long n = F::PACK_ITEMS;
       tf_pack_kernel<H><<<(int)((n + 255) / 256), 256, 0, st>>>(a.P, a.frags);
       return hipGetLastError();
     }
@@ -1177,6 +1252,17 @@ long tf_frag_floats(int H) {
 #define CASE(h) \
   case h:       \
     return TF<h>::TOTAL_FLOATS;
+    PGP_FOR_EACH_H(CASE)
+#undef CASE
+  }
+  return 0;
+}
+
+long tf_pack_items(int H) {
+  switch (H) {
+#define CASE(h) \
+  case h:       \
+    return TF<h>::PACK_ITEMS;
     PGP_FOR_EACH_H(CASE)
 #undef CASE
   }

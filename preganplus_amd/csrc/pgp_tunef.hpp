@@ -7,6 +7,10 @@
 #include "pgp_layout.hpp"
 #include "pgp_train.hpp"
 
+#ifndef PGP_TF_SPLIT
+#define PGP_TF_SPLIT 1  // split-bf16 feed-forward GEMMs in the fused kernels at H = 50 (A/B: -DPGP_TF_SPLIT=0)
+#endif
+
 namespace pgp {
 
 // weight fragment matrices (A operands; "T" = transposed for the backward)
@@ -33,7 +37,23 @@ struct TF {
                         OFF_OT = OFF_INT + G_INT * 256L;
   static constexpr long TE_OFF = 0;
   static constexpr long layer_off(int l) { return (G_TE + (long)l * LG) * 256L; }
-  static constexpr long TOTAL_FLOATS = (G_TE + 2L * LG) * 256L;
+  static constexpr long FP32_FLOATS = (G_TE + 2L * LG) * 256L;
+  // Split-bf16 planes (SPLIT, H = 50): the feed-forward matrices F1 F2 F2T F1T
+  // and out_proj's transpose OT of each layer also as exact three-part bf16 splits (pgp_device.hpp split8)
+  // for v_mfma_f32_16x16x32_bf16: a 32-k block b pairs fragment groups 2b, 2b + 1
+  // lane-locally (element e of a lane's 8 <-> k-step 8b + e), 1-KiB fragments
+  // [tile][block][plane], after the fp32 fragments in the same buffer
+  static constexpr bool SPLIT = PGP_TF_SPLIT && H == 50;
+  static constexpr int NBD = (KS + 7) / 8;  // 32-k blocks over d
+  static constexpr int NBH = 2;             // over the hidden 64
+  static constexpr int P_F1 = 4 * NBD * 3, P_F2 = NT * NBH * 3, P_F2T = 4 * NBD * 3, P_F1T = NT * NBH * 3,
+                       P_OT = NT * NBD * 3;
+  static constexpr int PL = P_F1 + P_F2 + P_F2T + P_F1T + P_OT;  // per layer
+  static constexpr int PO_OT = P_F1 + P_F2 + P_F2T + P_F1T;      // OT's first fragment in the layer block
+  static constexpr long pl_off(int l) { return FP32_FLOATS + (long)l * PL * 256L; }
+  static constexpr long TRIPLES = SPLIT ? 2L * PL / 3 : 0;
+  static constexpr long TOTAL_FLOATS = FP32_FLOATS + TRIPLES * 768L;
+  static constexpr long PACK_ITEMS = FP32_FLOATS + TRIPLES * 64L;  // tf_pack_elem's index range
   static constexpr int mat_kg(int m) {
     return m == TFM_F2 || m == TFM_F1T ? KGF : m == TFM_INT ? KGQ : KG;
   }
@@ -130,12 +150,42 @@ PGP_DEV float tf_frag_value(const float* __restrict__ P, int layer, int mat, int
   return 0.f;
 }
 
+// one plane triple (SPLIT): item = triple * 64 + lane; the lane's 8 values of
+// fragment groups 2b, 2b + 1 split into three bf16 planes (u32x4 each)
+template <int H>
+PGP_DEV void tf_split_item(const float* __restrict__ P, float* __restrict__ frags, long item) {
+  using F = TF<H>;
+  const int lane = (int)(item & 63);
+  const long tr = item >> 6;
+  const int layer = (int)(tr / (F::PL / 3));
+  int t = (int)(tr - (long)layer * (F::PL / 3));
+  const int cnt[5] = {F::P_F1 / 3, F::P_F2 / 3, F::P_F2T / 3, F::P_F1T / 3, F::P_OT / 3};
+  const int mats[5] = {TFM_F1, TFM_F2, TFM_F2T, TFM_F1T, TFM_OT};
+  const int nbs[5] = {F::NBD, F::NBH, F::NBD, F::NBH, F::NBD};
+  int k = 0;
+  while (k < 4 && t >= cnt[k]) t -= cnt[k++];
+  const int tile = t / nbs[k], b = t - tile * nbs[k];
+  float v[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = tf_frag_value<H>(P, layer, mats[k], tile, 8 * b + e, lane);
+  u32x4 pl[3];
+  split8(v, pl);
+  u32x4* dst = reinterpret_cast<u32x4*>(frags + F::FP32_FLOATS + tr * 768L) + lane;
+#pragma unroll
+  for (int q = 0; q < 3; ++q) dst[q * 64] = pl[q];
+}
+
 // one element of the fragment buffer (tf_pack_kernel; the C3 step's merged
-// packing launch in pgp_tune.hip)
+// packing launch in pgp_tune.hip); indices past the fp32 fragments are plane
+// triple items (tf_split_item)
 template <int H>
 PGP_DEV void tf_pack_elem(const float* __restrict__ P, float* __restrict__ frags, long idx) {
   using F = TF<H>;
-  if (idx >= F::TOTAL_FLOATS) return;
+  if (idx >= F::PACK_ITEMS) return;
+  if (idx >= F::FP32_FLOATS) {
+    if constexpr (F::SPLIT) tf_split_item<H>(P, frags, idx - F::FP32_FLOATS);
+    return;
+  }
   const int e = (int)(idx & 3), lane = (int)((idx >> 2) & 63);
   const long grp = idx >> 8;  // 1-KiB group
   int layer, mat;
@@ -148,6 +198,7 @@ PGP_DEV void tf_pack_elem(const float* __restrict__ P, float* __restrict__ frags
 #endif
 
 long tf_frag_floats(int H);
+long tf_pack_items(int H);  // tf_pack_elem's index range (>= tf_frag_floats' fp32 part)
 long tf_slab_floats(int H, int kind);  // kind 2: ffn backward, 3: attention backward
 int tf_max_grid();                      // the most workgroups a fused launch uses (one per CU)
 int tf_bwd_grid(int H, int B);          // workgroups (= weight-gradient slabs) of a backward launch

@@ -82,10 +82,16 @@ def encoder_split_executed_flops_per_window(H: int):
 # Fused tuning encoder (pgp_tunef.hip): v_mfma_f32_16x16x4_f32 per unit of 16
 # (window, host) pairs, the static counts of the built ISA (tools/isa_count.py
 # tune_counts, held equal by tests/test_roofline_isa.py).  tf_fwd_kernel's count
-# includes layer 0's time encoder (tune_te_mfma), which layer 1 skips.
+# includes layer 0's time encoder (tune_te_mfma), which layer 1 skips.  At H = 50
+# the feed-forward GEMMs and out_proj's transpose run split-bf16
+# (TF<H>::SPLIT): their v_mfma_f32_16x16x32_bf16 per unit in TUNE_BF16_PER_UNIT.
 TUNE_MFMA_PER_UNIT = {
     16: {"tf_fwd_kernel": 156, "tf_bwd_ffn_kernel": 288, "tf_bwd_att_kernel": 96},
-    50: {"tf_fwd_kernel": 1200, "tf_bwd_ffn_kernel": 1104, "tf_bwd_att_kernel": 1368},
+    50: {"tf_fwd_kernel": 840, "tf_bwd_ffn_kernel": 384, "tf_bwd_att_kernel": 1200},
+}
+TUNE_BF16_PER_UNIT = {
+    16: {"tf_fwd_kernel": 0, "tf_bwd_ffn_kernel": 0, "tf_bwd_att_kernel": 0},
+    50: {"tf_fwd_kernel": 288, "tf_bwd_ffn_kernel": 576, "tf_bwd_att_kernel": 144},
 }
 TUNE_FUSED_LAUNCHES = ("fwd layer 0", "fwd layer 1", "ffn bwd layer 1", "att bwd layer 1", "ffn bwd layer 0",
                        "att bwd layer 0")
@@ -127,12 +133,17 @@ def tune_fused_flops(H: int, B: int, B_fwd: int | None = None):
     c = TUNE_MFMA_PER_UNIT.get(H)
     if c is None:
         return None
+    # fp32-MFMA-equivalent work: a bf16 16x16x32 (16,384 flops) counted at the
+    # fp32 / bf16 dense-peak ratio (1/16), so achieved / the fp32 peak is the
+    # matrix pipe's busy fraction the executed work implies
+    bf = TUNE_BF16_PER_UNIT.get(H, {})
+    eq = {k: n * 2048 + bf.get(k, 0) * 16 * 16 * 32 * 2 * PEAK_FP32_TFLOPS / PEAK_BF16_TFLOPS for k, n in c.items()}
     units = (B * H + 15) // 16
     ufwd = ((B if B_fwd is None else B_fwd) * H + 15) // 16
-    fwd, te = c["tf_fwd_kernel"], tune_te_mfma(H)
-    return ([ufwd * fwd * 2048, ufwd * (fwd - te) * 2048]
-            + [units * n * 2048 for n in (c["tf_bwd_ffn_kernel"], c["tf_bwd_att_kernel"], c["tf_bwd_ffn_kernel"],
-                                          c["tf_bwd_att_kernel"])])
+    fwd, te = eq["tf_fwd_kernel"], tune_te_mfma(H) * 2048
+    return ([ufwd * fwd, ufwd * (fwd - te)]
+            + [units * n for n in (eq["tf_bwd_ffn_kernel"], eq["tf_bwd_att_kernel"], eq["tf_bwd_ffn_kernel"],
+                                   eq["tf_bwd_att_kernel"])])
 
 
 def encoder_io_bytes_per_window(H: int) -> int:

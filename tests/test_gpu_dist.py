@@ -156,8 +156,10 @@ def _c3_run(sl, world):
             step.run()
             torch.cuda.synchronize()
             step.sync()
+            # the tuning loss's per-(window, host) weights and targets (tune_targets_dp_kernel)
+            lt = torch.cat([step.tun.mult[:step.B, :, None], step.tun.tgt[:step.B]], dim=2).cpu().numpy()
             return (tr.P.cpu().numpy(), step.tun.state.cpu().numpy(), step.target.cpu().numpy(),
-                    step.sim_out.cpu().numpy(), [t["step"] for t in tr.tensors], tr.G.cpu().numpy())
+                    step.sim_out.cpu().numpy(), [t["step"] for t in tr.tensors], tr.G.cpu().numpy(), lt)
     finally:
         L.pgp_tune_set_side_stream(None)
 
@@ -172,11 +174,12 @@ def _c3_rank(rank, world, port, q):
     torch.cuda.set_device(0)
     try:
         per = ES // world
-        P, state, target, sim_out, steps, G = _c3_run(slice(rank * per, (rank + 1) * per), world)
+        P, state, target, sim_out, steps, G, lt = _c3_run(slice(rank * per, (rank + 1) * per), world)
         got = [None] * world
-        dist.all_gather_object(got, (target, sim_out))
+        dist.all_gather_object(got, (target, sim_out, lt))
         if rank == 0:
-            q.put((P, state, np.concatenate([g[0] for g in got]), np.concatenate([g[1] for g in got]), steps, G))
+            q.put((P, state, np.concatenate([g[0] for g in got]), np.concatenate([g[1] for g in got]), steps, G,
+                   np.concatenate([g[2] for g in got])))
         dist.barrier()
     finally:
         dist.destroy_process_group()
@@ -195,12 +198,20 @@ def test_online_step_two_ranks_equal_full_batch():
     for p in procs:
         p.start()
     try:
-        P2, st2, tg2, so2, steps2, G2 = q.get(timeout=240)
+        P2, st2, tg2, so2, steps2, G2, lt2 = q.get(timeout=240)
     finally:
         for p in procs:
             p.join(timeout=60)
     assert all(p.exitcode == 0 for p in procs)
-    P1, st1, tg1, so1, steps1, G1 = _c3_run(slice(0, ES), 1)
+    P1, st1, tg1, so1, steps1, G1, lt1 = _c3_run(slice(0, ES), 1)
+    # the tuning loss's weights and targets: decisions on the forward's outputs,
+    # whose fp32 rounding depends on the batch (decoder split-K grouping), so a
+    # decision within rounding of a tie could flip between the two partitions
+    # and move the gradients by a whole window's share; this dataset has none
+    # (asserted first, so such a flip reads as what it is)
+    flip = np.argwhere(np.any(lt1 != lt2, axis=2))
+    assert flip.size == 0, ("tuning-target decisions differ at (row, host)", flip[:8].tolist(), lt1[tuple(flip[0])],
+                            lt2[tuple(flip[0])])
     # the GAN labels and scores of every environment: the step-start GAN, per environment
     np.testing.assert_array_equal(tg2, tg1)
     np.testing.assert_array_equal(so2, so1)
@@ -224,7 +235,10 @@ def test_online_step_two_ranks_equal_full_batch():
         # on both sides, so the two runs' parameters must differ by exactly what their
         # gradients (equal up to fp32 summation grouping) predict, every entry:
         #   P2 - P1 = -lr (f(g2) - f(g1)),  f(g) = g / (|g| + eps)
-        # up to the fp32 rounding of the two updates (a few ulps of |p| and of lr).
+        # up to the fp32 rounding of the two updates: each side's AdamW evaluation
+        # (m-hat, v-hat, sqrt, the division, the update) is within 8 ulps of |p| + lr
+        # of the exact formula on ITS gradient, and the two errors are independent
+        # where the gradients' bits differ, so their difference is within 16.
         if np.array_equal(P1[sl], P0[sl]):   # a tensor the step left alone (the prototype decoder's gate)
             assert np.array_equal(P2[sl], P0[sl]), t["name"]
             continue
@@ -233,11 +247,17 @@ def test_online_step_two_ranks_equal_full_batch():
         f = lambda g: g / (np.abs(g) + eps)
         pred = -lr * (f(g2) - f(g1))
         d = P2[sl].astype(np.float64) - P1[sl].astype(np.float64)
-        tol = 8 * u * (np.abs(P1[sl]).astype(np.float64) + lr)
-        bad = np.abs(d - pred) > tol
-        assert not bad.any(), (t["name"], int(bad.sum()), float(np.abs(d - pred).max()), float(tol.max()))
-        # and the gradients themselves agree to fp32 grouping where they are not
-        # rounding noise (exact zeros on both sides: key biases, key_bias_mask)
+        # The attention key biases' gradient is identically zero in exact
+        # arithmetic (key_bias_mask): both runs hold rounding noise there, which
+        # AdamW's g / (|g| + eps) turns into O(lr) steps where the formula's own
+        # rounding is not negligible against the noise; those entries are held
+        # to the step bound |d| <= 2 lr (each side moves by at most lr + lr wd |p|)
         noise = key_bias_mask(t["name"], t["n"], HS)
+        tol = 16 * u * (np.abs(P1[sl]).astype(np.float64) + lr)
+        bad = (np.abs(d - pred) > tol) & ~noise
+        assert not bad.any(), (t["name"], int(bad.sum()), float((np.abs(d - pred) / tol)[~noise].max()))
+        assert np.all(np.abs(d[noise]) <= 2 * lr * (1 + 1e-6)), t["name"] + " (key bias)"
+        # and the gradients themselves agree to fp32 grouping where they are not
+        # rounding noise (exact zeros on both sides: key biases)
         scale = np.abs(g1).max() + 1e-30
         np.testing.assert_allclose(g2[~noise], g1[~noise], rtol=1e-3, atol=1e-5 * scale, err_msg=t["name"])

@@ -46,6 +46,8 @@ def test_tuning_kernel_mfma_counts_match_built_library():
     import isa_count
     counts = isa_count.tune_counts(tuple(R.TUNE_MFMA_PER_UNIT))
     assert counts == R.TUNE_MFMA_PER_UNIT
+    bf = isa_count.tune_counts(tuple(R.TUNE_BF16_PER_UNIT), op="_f32_16x16x32_bf16")
+    assert bf == R.TUNE_BF16_PER_UNIT
 
 
 def test_tune_fused_flops_bookkeeping():

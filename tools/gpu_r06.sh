@@ -66,10 +66,20 @@ for step in "$@"; do
       pmc tr16/pmc_fetch FETCH_SIZE --hosts 16 --steps 3 --warmup 1 --no-cpu-baseline
       pmc tr16/pmc_write WRITE_SIZE --hosts 16 --steps 3 --warmup 1 --no-cpu-baseline
       ;;
+    trtune)  # FETCH / WRITE passes of the fused tuning kernels (tools/pmc_traffic.py gpurun_out/T/trt50 1030 50)
+      mkdir -p $OUT/trt50
+      pmc trt50/pmc_fetch FETCH_SIZE --config tune --hosts 50 --steps 3 --warmup 1 --no-cpu-baseline
+      pmc trt50/pmc_write WRITE_SIZE --config tune --hosts 50 --steps 3 --warmup 1 --no-cpu-baseline
+      ;;
     tline)  # C3 kernel traces (H=50, 16) -> per-step timelines
       run tl50 240 rocprofv3 --kernel-trace --output-format csv -d $OUT/tl50 -o tl -- python3 bench.py --config tune --hosts 50 --steps 40 --warmup 5 --no-cpu-baseline
       run tl16 240 rocprofv3 --kernel-trace --output-format csv -d $OUT/tl16 -o tl -- python3 bench.py --config tune --hosts 16 --steps 100 --warmup 10 --no-cpu-baseline
       for h in 50 16; do python3 tools/tune_timeline.py $(find $OUT/tl$h -name "*kernel_trace.csv" | head -1) > $OUT/timeline$h.txt; head -3 $OUT/timeline$h.txt; done
+      ;;
+    abtf)  # fused tuning kernels: split-bf16 (default build) vs fp32 (variant tfs0)
+      run abtf 900 python3 -u tools/ab_bench.py --rounds 4 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" split= fp32=PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_tfs0.so
+      grep median $OUT/abtf.out
+      python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); [print(k, [{kk: round(vv, 4) for kk, vv in e['stage_ms'].items()} for e in v]) for k, v in d['extra'].items()]" $OUT/abtf.out
       ;;
     abenc)
       run abenc 900 python3 -u tools/ab_bench.py --rounds 4 --args "--steps 100 --warmup 5 --no-cpu-baseline" split= fp32enc=ARGS=--fp32-encoder
@@ -91,6 +101,10 @@ for step in "$@"; do
       PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_bwdfirst.so run t_bwd 600 $PYT tests/test_gpu_c3step.py -m gpu
       run abb16 600 python3 -u tools/ab_bench.py --rounds 4 --args "--config tune --hosts 16 --steps 100 --warmup 10 --no-cpu-baseline" base= bwd=PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_bwdfirst.so
       grep median $OUT/abb16.out
+      ;;
+    tdist)
+      run t_dist 600 $PYT tests/test_gpu_dist.py -m gpu
+      tail -2 $OUT/t_dist.out
       ;;
     ttrain)
       run t_train 900 $PYT tests/test_gpu_train.py tests/test_gpu_c3step.py tests/test_gpu_dist.py -m gpu

@@ -34,8 +34,9 @@ def _disasm(lib, needle):
     return asm
 
 
-def tune_counts(Hs=(16, 50), lib=LIB):
-    """{H: {kernel: mfma}} for the fused tuning-encoder kernels (pgp_tunef.hip):
+def tune_counts(Hs=(16, 50), lib=LIB, op="_f32_16x16x4"):
+    """{H: {kernel: mfma}} for the fused tuning-encoder kernels (pgp_tunef.hip),
+    MFMAs of opcode suffix `op` (the split forms' bf16: "_f32_16x16x32_bf16"):
     the unit loop is `#pragma unroll 1` and holds every MFMA, so the static
     count is the per-unit count (tf_fwd_kernel's includes layer 0's time
     encoder, which layer 1 skips)."""
@@ -47,7 +48,7 @@ def tune_counts(Hs=(16, 50), lib=LIB):
             m = re.search(rf"<_ZN3pgp12_GLOBAL__N_1\d+{name}ILi{H}EEEvNS_6TfArgsE>:\n(.*?)s_endpgm", asm, re.S)
             if m is None:
                 raise RuntimeError(f"{name}<{H}> not found in {lib}")
-            out[H][name] = len(re.findall(r"^\s+v_mfma", m.group(1), re.M))
+            out[H][name] = len(re.findall(r"^\s+v_mfma" + op, m.group(1), re.M))
     return out
 
 
