@@ -470,8 +470,9 @@ int pgp_gan_step1(int n_hosts, const float* target, float* P, float* G, float* e
  * PGP_COLL_TUNE_STATE (inc), on the main stream; the same order on every rank.
  * pgp_online_timing(h, 1) records HIP events in later steps;
  * pgp_online_stage_ms(h, ms[PGP_ONLINE_NSTAGE]) returns the last step's spans:
- * dataset, embedding, train_gan, tune_model, forward, targets, backward,
- * exchange, state + AdamW, whole main stream.  pgp_online_steps returns the
+ * dataset, embedding (folded into the GAN forward's first launch since round 5:
+ * an empty span, kept so the array layout is stable), train_gan, tune_model,
+ * forward, targets, backward, exchange, state + AdamW, whole main stream.  pgp_online_steps returns the
  * host step counts (in `tensors` order; -1 for the conditional tensors). */
 typedef struct {
   long long offset;  /* first element in P/G/m/v */

@@ -166,6 +166,17 @@ for step in "$@"; do
       ;;
     fleet)
       run fleet 400 python3 -u bench.py --config fleet --steps 100 --warmup 5
+      run fleets 400 python3 -u bench.py --config fleet --stream --steps 20 --warmup 2 --no-cpu-baseline
+      ;;
+    tunestall)
+      pmc tstall1 "$STALL1" --config tune --hosts 50 --steps 3 --warmup 1 --no-cpu-baseline
+      pmc tstall2 "$STALL2" --config tune --hosts 50 --steps 3 --warmup 1 --no-cpu-baseline
+      ;;
+    lines)  # the other configs' lines: GOBI, the online loop, the plugin, the simulation
+      run gobi 400 python3 -u bench.py --config gobi --steps 20 --warmup 3
+      run loop 400 python3 -u bench.py --config loop --steps 50 --warmup 5
+      run plugin 400 python3 -u bench.py --config plugin --steps 20 --warmup 3
+      run sim 400 python3 -u bench.py --config sim --steps 50 --warmup 5
       ;;
     *)
       echo "unknown step $step"; exit 2
