@@ -71,6 +71,11 @@ for step in "$@"; do
       pmc trt50/pmc_fetch FETCH_SIZE --config tune --hosts 50 --steps 3 --warmup 1 --no-cpu-baseline
       pmc trt50/pmc_write WRITE_SIZE --config tune --hosts 50 --steps 3 --warmup 1 --no-cpu-baseline
       ;;
+    stamps)  # phase stamps of the fused tuning kernels (profiling build st)
+      PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_st.so run st50 300 python3 -u tools/tf_stamps.py 50 1030
+      PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_st.so run st16 300 python3 -u tools/tf_stamps.py 16 1030
+      cat $OUT/st16.out
+      ;;
     tline)  # C3 kernel traces (H=50, 16) -> per-step timelines
       run tl50 240 rocprofv3 --kernel-trace --output-format csv -d $OUT/tl50 -o tl -- python3 bench.py --config tune --hosts 50 --steps 40 --warmup 5 --no-cpu-baseline
       run tl16 240 rocprofv3 --kernel-trace --output-format csv -d $OUT/tl16 -o tl -- python3 bench.py --config tune --hosts 16 --steps 100 --warmup 10 --no-cpu-baseline
@@ -80,6 +85,10 @@ for step in "$@"; do
       run abtf 900 python3 -u tools/ab_bench.py --rounds 4 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" split= fp32=PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_tfs0.so
       grep median $OUT/abtf.out
       python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); [print(k, [{kk: round(vv, 4) for kk, vv in e['stage_ms'].items()} for e in v]) for k, v in d['extra'].items()]" $OUT/abtf.out
+      ;;
+    abatt)  # attention backward restructure (out_proj dW outside, Win^T split) vs the previous build (head)
+      run abatt 900 python3 -u tools/ab_bench.py --rounds 4 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" new= head=PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_head.so
+      grep median $OUT/abatt.out
       ;;
     abenc)
       run abenc 900 python3 -u tools/ab_bench.py --rounds 4 --args "--steps 100 --warmup 5 --no-cpu-baseline" split= fp32enc=ARGS=--fp32-encoder
