@@ -241,6 +241,13 @@ constexpr int kDecTW = PGP_DEC_TW;
 #define PGP_DEC_PF 1
 #endif
 constexpr int kDecPF = PGP_DEC_PF;
+// weight planes read PGP_DEC_PIPE (block, tile) steps ahead of their MFMAs
+// (0: where the compiler puts them; A/B, C2 at H = 50, 5 interleaved rounds:
+// K2b 1.035 -> 0.989 ms at 1, profiles/r06/c2/ab_decoder_pipe.txt)
+#ifndef PGP_DEC_PIPE
+#define PGP_DEC_PIPE 1
+#endif
+constexpr int kDecPipe = PGP_DEC_PIPE;
 
 template <int H, int TW>
 __global__ __launch_bounds__(kDecWaves / TW * 64, 1) void decoder_split_kernel(FwdArgs a) {
@@ -295,6 +302,22 @@ __global__ __launch_bounds__(kDecWaves / TW * 64, 1) void decoder_split_kernel(F
     float bn[TW][G::KS_D];
 #pragma unroll
     for (int t = 0; t < TW; ++t) load_b(t, c + kDecPF, c + kDecPF < NCH, bn[t]);
+    // the planes of the next (block, tile) are read while this one's MFMAs
+    // run (kDecPipe; without it the compiler waited for each read: one
+    // lgkmcnt(0) per tile)
+    auto planes = [&](int kb, int mt, u32x4 (&w)[3]) {
+      const float* F = cur + ((kb * G::MT_O + mt) * 3) * 256 + lane * 4;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) w[k] = *reinterpret_cast<const u32x4*>(F + k * 256);
+    };
+    constexpr int QN = D::NB * G::MT_O;  // (block, tile) steps of a chunk
+    constexpr int PD = kDecPipe > 0 ? kDecPipe : 1;
+    u32x4 wq[PD][3];
+    if constexpr (kDecPipe > 0) {
+#pragma unroll
+      for (int q = 0; q < PD; ++q)
+        if (q < QN) planes(q / G::MT_O, q % G::MT_O, wq[q]);
+    }
 #pragma unroll
     for (int kb = 0; kb < D::NB; ++kb) {
       u32x4 x[TW][3];
@@ -307,9 +330,18 @@ __global__ __launch_bounds__(kDecWaves / TW * 64, 1) void decoder_split_kernel(F
       }
 #pragma unroll
       for (int mt = 0; mt < G::MT_O; ++mt) {
-        const float* F = cur + ((kb * G::MT_O + mt) * 3) * 256 + lane * 4;
-        const u32x4 w[3] = {*reinterpret_cast<const u32x4*>(F), *reinterpret_cast<const u32x4*>(F + 256),
-                            *reinterpret_cast<const u32x4*>(F + 512)};
+        u32x4 w[3];
+        if constexpr (kDecPipe > 0) {
+          const int q = kb * G::MT_O + mt;
+#pragma unroll
+          for (int k = 0; k < 3; ++k) w[k] = wq[q % PD][k];
+          if (q + PD < QN) planes((q + PD) / G::MT_O, (q + PD) % G::MT_O, wq[q % PD]);
+          // keep the reads here, ahead of this tile's MFMAs (the scheduler
+          // otherwise sinks them next to their use)
+          __builtin_amdgcn_sched_barrier(0);
+        } else {
+          planes(kb, mt, w);
+        }
 #pragma unroll
         for (int t = 0; t < TW; ++t) acc[t][mt] = mfma_bf6(w, x[t], acc[t][mt]);
       }

@@ -100,6 +100,7 @@ struct GobiLds {
   alignas(16) float h1[kP1][kNE], h2[kP1][kNE], g2[kP1][kNE], g3[kP3][kNE], g1[kP1][kNE];
   float h3[kNE][kN3], th3[kNE][kN3];
   float o[kNE][4];
+  alignas(16) float adam[kMaxIt][4];  // the per-iteration AdamW scalars (GobiW::ADAM), read from LDS in the loop
   int hs[kNE][kH];   // each container's host (the one-hot column of its allocation row)
   int dense[kNE];    // the init's allocation is not one-hot (iteration 0 takes the dense layer 1)
   alignas(16) int flag[2][kNE];  // "some entry changed" of the current / next iteration (one 16-byte read)
@@ -455,9 +456,13 @@ __device__ void surrogate_fwd(const float* __restrict__ W, const GobiRegs& R, Go
       p1 += dppf<kDppX1>(p1);
       const float o0 = sigmoid_f(p0 + R.b40), o1 = sigmoid_f(p1 + R.b41);
       if (l == 0) {
-        L.o[e][0] = o0;
-        L.o[e][1] = o1;
-        L.o[e][2] = 0.8f * o0 + 0.2f * o1;
+        // the row address recomputed here (the compiler kept it in a scratch
+        // slot across the loop and reloaded it every iteration)
+        int ee = e;
+        asm volatile("" : "+v"(ee));
+        L.o[ee][0] = o0;
+        L.o[ee][1] = o1;
+        L.o[ee][2] = 0.8f * o0 + 0.2f * o1;
       }
       if (grad) {  // dz/do = (0.8, 0.2) through the sigmoids, dh3 = W4^T do, through Tanhshrink
         const float d0 = 0.8f * (1.f - o0) * o0, d1 = 0.2f * (1.f - o1) * o1;
@@ -493,6 +498,7 @@ __global__ __launch_bounds__(kT) void gobi_kernel(int E, const float* __restrict
     const int e = k / kIn;
     L.x[e][k - e * kIn] = e0 + e < E ? init[e0 * kIn + k] : 0.f;
   }
+  for (int k = t; k < kMaxIt * 4; k += kT) (&L.adam[0][0])[k] = W[GobiW::ADAM + k];
   if (t < kNE) {
     L.dense[t] = 0;
     L.flag[0][t] = L.flag[1][t] = 0;
@@ -544,10 +550,6 @@ __global__ __launch_bounds__(kT) void gobi_kernel(int E, const float* __restrict
 #pragma unroll
     for (int e = 0; e < kNE; ++e) any |= act[e];
     if (!any) break;
-    // this iteration's AdamW scalars, requested here (scalar loads) so that the
-    // input-gradient phase does not wait for them
-    const float* ad = W + GobiW::ADAM + it * 4;
-    const float a0 = ad[0], a1 = ad[1], a2 = ad[2];
 #ifdef PGP_GOBI_PROF
     int nact_ = 0;
 #pragma unroll
@@ -582,6 +584,11 @@ __global__ __launch_bounds__(kT) void gobi_kernel(int E, const float* __restrict
     float gxa[kNE];
     dotb<64>(&L.g1[kp(sq * 64)], R.w1c, act, gxa);
     sum_pairs(gxa, act);
+    // this iteration's AdamW scalars, from LDS (scalar loads from memory at the
+    // loop top made the first phase's LDS waits wait for them too: one lgkmcnt
+    // counts both; 0.714 -> see DESIGN §17)
+    const float4 ad = *reinterpret_cast<const float4*>(L.adam[it]);
+    const float a0 = ad.x, a1 = ad.y, a2 = ad.z;
     // lane sq owns the entry of envs e = sq + 2k: AdamW and the one-hot once
     // per k with every lane busy (rows sq = 0 and 1 on envs 2k and 2k + 1)
 #pragma unroll
@@ -589,7 +596,13 @@ __global__ __launch_bounds__(kT) void gobi_kernel(int E, const float* __restrict
       if (!act[2 * k] && !act[2 * k + 1]) continue;
       const int e = sq + 2 * k;
       const bool on = sq ? act[2 * k + 1] : act[2 * k];
-      const float gx = sq ? gxa[2 * k + 1] : gxa[2 * k];
+      // a lane select of two registers: written as `sq ? gxa[2k+1] : gxa[2k]`
+      // the compiler made it an indexed load of gxa[2k + sq], i.e. gxa stored
+      // to scratch and read back every iteration (4 stores + 2 loads in the
+      // AdamW chain); the opaque copies keep it a v_cndmask
+      float ga = gxa[2 * k], gb = gxa[2 * k + 1];
+      asm volatile("" : "+v"(ga), "+v"(gb));
+      const float gx = sq ? gb : ga;
       // ---- AdamW (torch single-tensor, opt.py:18 defaults) on the entry ----
       const float xold = L.x[e][xi];
       float& mm = m[k];

@@ -173,9 +173,53 @@ PGP_DEV void tf_gemm(f32x4 (&acc)[NO][3], const float* A, BF bsrc, int lane) {
 // (mfma_bf6: the fp32 product to within 2^-26 of |w x|, fp32 accumulation).
 // Step by step, so only one step's split B operand (NB x 12 registers) is live;
 // the NO * KGn side slots are spread over the 3 * NO * NB blocks.
-template <int NO, int KSn, class BF, class SIDE>
+template <int NO, int KSn, bool PF = false, class BF, class SIDE>
 PGP_DEV void tf_gemm_split_side(f32x4 (&acc)[NO][3], const float* A, BF bsrc, int lane, SIDE side) {
   constexpr int NB = (KSn + 7) / 8, KGn = (KSn + 3) / 4, NS = NO * KGn, NI = 3 * NO * NB;
+  auto planes = [&](int o, int b, u32x4 (&wp)[3]) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) wp[k] = *reinterpret_cast<const u32x4*>(A + ((o * NB + b) * 3 + k) * 256 + lane * 4);
+  };
+  if constexpr (PF) {
+    // as below, with the next (tile, block)'s planes read ahead of this one's
+    // MFMAs and pinned there (the forward: 2 waves per SIMD, registers to
+    // spare); the same MFMAs in the same order
+    constexpr int QN = NO * NB;
+    u32x4 wn[3];
+    planes(0, 0, wn);
+#pragma unroll
+    for (int w = 0; w < 3; ++w) {
+      u32x4 xs[NB][3];
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = 8 * b + e < KSn ? bsrc(8 * b + e, w) : 0.f;
+        split8(v, xs[b]);
+      }
+#pragma unroll
+      for (int o = 0; o < NO; ++o) {
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+          u32x4 wp[3];
+#pragma unroll
+          for (int k = 0; k < 3; ++k) wp[k] = wn[k];
+          const int q = o * NB + b + 1;  // the next (tile, block), wrapping to the next step's first
+          if (q < QN)
+            planes(q / NB, q % NB, wn);
+          else if (w + 1 < 3)
+            planes(0, 0, wn);
+          __builtin_amdgcn_sched_barrier(0);
+          acc[o][w] = mfma_bf6(wp, xs[b], acc[o][w]);
+          const int it = (w * NO + o) * NB + b;
+#pragma unroll
+          for (int i = it * NS / NI; i < (it + 1) * NS / NI; ++i) side(i);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    return;
+  }
 #pragma unroll
   for (int w = 0; w < 3; ++w) {
     u32x4 xs[NB][3];
@@ -208,10 +252,10 @@ PGP_DEV void tf_gemm_split(f32x4 (&acc)[NO][3], const float* A, BF bsrc, int lan
   tf_gemm_split_side<NO, KSn>(acc, A, bsrc, lane, [](int) {});
 }
 // fp32 or split form by TF<H>::SPLIT (A: the matching LDS image)
-template <bool SPL, int NO, int KSn, class BF, class SIDE>
+template <bool SPL, int NO, int KSn, bool PF = false, class BF, class SIDE>
 PGP_DEV void tf_gemm_any(f32x4 (&acc)[NO][3], const float* A, BF bsrc, int lane, SIDE side) {
   if constexpr (SPL)
-    tf_gemm_split_side<NO, KSn>(acc, A, bsrc, lane, side);
+    tf_gemm_split_side<NO, KSn, PF>(acc, A, bsrc, lane, side);
   else
     tf_gemm_side<NO, KSn>(acc, A, bsrc, lane, side);
 }
@@ -554,6 +598,13 @@ PGP_DEV void tf_attn_probs(const f32x4 (&QK)[2 * TF<H>::NT][3], float (&P)[2][3]
 // prefetch waits) are covered by the other wave's MFMAs.  q | k and v are
 // separate GEMMs (96 + 48 accumulator registers instead of 144 at once).
 constexpr int kTfFwdWaves = 8;
+// the forward's split GEMMs read each (tile, block)'s planes one ahead (A/B, C3
+// H = 50, 4 interleaved rounds: 1.0255 -> 1.0134 ms, profiles/r06/c3/ab_fwd_pf.txt;
+// 28 registers spill at the forward's 256, yet it is faster)
+#ifndef PGP_TF_FWD_PF
+#define PGP_TF_FWD_PF 1
+#endif
+constexpr bool kTfFwdPF = PGP_TF_FWD_PF != 0;
 
 template <int H>
 __global__ __launch_bounds__(kTfFwdWaves * 64, 1) void tf_fwd_kernel(TfArgs a) {
@@ -673,7 +724,7 @@ __global__ __launch_bounds__(kTfFwdWaves * 64, 1) void tf_fwd_kernel(TfArgs a) {
     init_bias<4>(Fh, par + Q::B1, g);
     {  // side work: norm1's x-hat tiles and rstd (every lane group: the same value)
       constexpr int NS = 3 * NT + 3, NG = 4 * F::KG, PER = (NS + NG - 1) / NG;
-      tf_gemm_any<F::SPLIT, 4, F::KS>(Fh, sm + L::W_F1, [&](int s, int w) { return X[s >> 2][w][s & 3]; }, lane,
+      tf_gemm_any<F::SPLIT, 4, F::KS, kTfFwdPF>(Fh, sm + L::W_F1, [&](int s, int w) { return X[s >> 2][w][s & 3]; }, lane,
                              [&](int i) {
 #pragma unroll
                                for (int k = 0; k < PER; ++k) {
@@ -697,7 +748,7 @@ __global__ __launch_bounds__(kTfFwdWaves * 64, 1) void tf_fwd_kernel(TfArgs a) {
       long rn[3];
       const bool okn = unit_rows<H>(u + 1, u1, npairs, j, rn);
       constexpr int NS = 3 * NT, NG = NT * F::KGF, PER = (NS + NG - 1) / NG;
-      tf_gemm_any<F::SPLIT, NT, 16>(R, sm + L::W_F2, [&](int s, int w) { return Fh[s >> 2][w][s & 3]; }, lane,
+      tf_gemm_any<F::SPLIT, NT, 16, kTfFwdPF>(R, sm + L::W_F2, [&](int s, int w) { return Fh[s >> 2][w][s & 3]; }, lane,
                            [&](int i) {
 #pragma unroll
                              for (int k = 0; k < PER; ++k) {

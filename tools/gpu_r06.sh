@@ -90,6 +90,35 @@ for step in "$@"; do
       run abatt 900 python3 -u tools/ab_bench.py --rounds 4 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" new= head=PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_head.so
       grep median $OUT/abatt.out
       ;;
+    abdecpipe)  # decoder plane reads pinned a tile ahead (variant decpipe) vs the default build
+      run abdp 900 python3 -u tools/ab_bench.py --rounds 5 --args "--steps 100 --warmup 5 --no-cpu-baseline" base= pipe=PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_decpipe.so
+      grep median $OUT/abdp.out
+      python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); [print(k, [round(e['kernel_ms']['decoder'], 4) for e in v]) for k, v in d['extra'].items()]" $OUT/abdp.out
+      ;;
+    abdepth)  # decoder plane-read depth: 1 (default build) vs 2, 3
+      run abdd 900 python3 -u tools/ab_bench.py --rounds 4 --args "--steps 100 --warmup 5 --no-cpu-baseline" d1= d2=PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_dp2.so d3=PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_dp3.so
+      grep median $OUT/abdd.out
+      python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); [print(k, [round(e['kernel_ms']['decoder'], 4) for e in v]) for k, v in d['extra'].items()]" $OUT/abdd.out
+      ;;
+    abdp0)  # decoder plane pipeline (default build) vs none (dp0); forward plane prefetch (fwdpf) on C3
+      run abd0 900 python3 -u tools/ab_bench.py --rounds 4 --args "--steps 100 --warmup 5 --no-cpu-baseline" pipe= none=PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_dp0.so
+      grep median $OUT/abd0.out
+      python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); [print(k, [round(e['kernel_ms']['decoder'], 4) for e in v]) for k, v in d['extra'].items()]" $OUT/abd0.out
+      run abfpf 900 python3 -u tools/ab_bench.py --rounds 4 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" base= fwdpf=PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_fwdpf.so
+      grep median $OUT/abfpf.out
+      ;;
+    gobiab)  # GOBI: bit-identical trajectories and kernel time against the previous build (gobi0); GPU tests; lines
+      run gobiab 600 python3 -u tools/dbg/gobi_ab.py $GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_gobi0.so
+      tail -5 $OUT/gobiab.out
+      run t_gobi 600 $PYT tests/test_gpu_gobi.py tests/test_gpu_loop.py -m gpu
+      tail -2 $OUT/t_gobi.out
+      run gobi 400 python3 -u bench.py --config gobi --steps 20 --warmup 3
+      run loop 400 python3 -u bench.py --config loop --steps 50 --warmup 5
+      ;;
+    gobiph)  # GOBI phase timing (profiling build gprof)
+      PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_gprof.so run gobiph 300 python3 -u tools/gobi_phases.py
+      cat $OUT/gobiph.out
+      ;;
     abenc)
       run abenc 900 python3 -u tools/ab_bench.py --rounds 4 --args "--steps 100 --warmup 5 --no-cpu-baseline" split= fp32enc=ARGS=--fp32-encoder
       grep median $OUT/abenc.out
