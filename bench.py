@@ -315,15 +315,27 @@ def main():
         else:
             res["cpu_baseline"] = None
     # sub-records (every rank takes part; rank 0 reports them in the line)
+    # The headline never waits on a sub-record: an exception in one is recorded
+    # in its place, and a sub-record still running after SUBRECORD_DEADLINE_S
+    # (a collective that never completes) ends every rank, rank 0 emitting the
+    # line first with the timeout recorded.
     sub = {}
     if "c3_dp" in c2_subrecords(world):
         del out, mv_out, model
-        sub["c3_dp"] = c3_dp_record(world, rank, device)
+
+        def on_timeout():
+            if rank == 0:
+                res["c3_dp"] = {"error": f"did not complete within {SUBRECORD_DEADLINE_S} s"}
+                emit(res)
+        try:
+            sub["c3_dp"] = with_deadline(lambda: c3_dp_record(world, rank, device), SUBRECORD_DEADLINE_S, on_timeout)
+        except Exception as e:  # noqa: BLE001 - recorded, the headline stands
+            sub["c3_dp"] = {"error": f"{type(e).__name__}: {e}"[:400]}
     if rank == 0:
         res.update(sub)
         emit(res)
     if world > 1:
-        torch.distributed.destroy_process_group()
+        with_deadline(torch.distributed.destroy_process_group, SUBRECORD_DEADLINE_S, lambda: None)
 
 
 _RANKS_SEEN = 1
@@ -416,6 +428,28 @@ def _backend_label():
         return "none"
     b = dist.get_backend()
     return "RCCL" if b == "nccl" else b
+
+
+SUBRECORD_DEADLINE_S = 180
+
+
+def with_deadline(fn, seconds, on_timeout):
+    """fn() on this thread; if it has not returned after `seconds`, a watchdog
+    thread calls on_timeout() and ends the process (os._exit(0): stdout
+    flushed first; exiting, not replacing the program)."""
+    import threading
+    done = threading.Event()
+
+    def watch():
+        if not done.wait(seconds):
+            on_timeout()
+            sys.stdout.flush()
+            os._exit(0)
+    threading.Thread(target=watch, daemon=True).start()
+    try:
+        return fn()
+    finally:
+        done.set()
 
 
 def emit(res):

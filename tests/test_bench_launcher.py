@@ -98,3 +98,23 @@ def test_c2_line_carries_c3_dp_at_world_gt_1():
         assert rec["ms_per_step"] > 0 and rec["all_reduce_ms"] > 0 and rec["windows_per_s"] > 0
     # the timing is the max over ranks: both ranks report the same numbers
     assert got[0][1]["ms_per_step"] == got[1][1]["ms_per_step"]
+
+
+def test_subrecord_deadline_emits_the_line_and_ends_the_process():
+    """bench.with_deadline: a sub-record that never returns (a collective that
+    never completes) ends the process after its deadline, on_timeout first
+    (rank 0 emits the headline there), exit status 0."""
+    code = ("import sys, time; sys.path.insert(0, %r); import bench\n"
+            "bench.with_deadline(lambda: time.sleep(60), 1, lambda: print('{\"emitted\": true}'))\n"
+            "print('not reached')\n") % ROOT
+    p = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True, timeout=120,
+                       env=dict(os.environ, PGP_DEVICE="cpu"))
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert json.loads(p.stdout.strip().splitlines()[-1]) == {"emitted": True}
+    assert "not reached" not in p.stdout
+
+
+def test_subrecord_deadline_returns_the_value_in_time():
+    sys.path.insert(0, ROOT)
+    import bench
+    assert bench.with_deadline(lambda: 7, 30, lambda: None) == 7
