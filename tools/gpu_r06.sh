@@ -119,6 +119,10 @@ for step in "$@"; do
       PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_gprof.so run gobiph 300 python3 -u tools/gobi_phases.py
       cat $OUT/gobiph.out
       ;;
+    dist2)  # N=2 rehearsal on one GPU: two gloo ranks, the C2 line with its c3_dp sub-record
+      PGP_DIST_BACKEND=gloo PGP_DEVICE=0 run dist2 600 python3 -u bench.py --gpus 2 --steps 20 --warmup 3 --no-cpu-baseline
+      grep "^{" $OUT/dist2.out | tail -1 | cut -c1-400
+      ;;
     abenc)
       run abenc 900 python3 -u tools/ab_bench.py --rounds 4 --args "--steps 100 --warmup 5 --no-cpu-baseline" split= fp32enc=ARGS=--fp32-encoder
       grep median $OUT/abenc.out
