@@ -46,6 +46,21 @@ constexpr int enc_waves() { return H <= 16 ? kEnc16Waves : tail_res<H>() ? kEncT
 template <int H>
 constexpr int NW_STAGE() { return enc_waves<H>(); }
 
+// the split feed-forward's planes read one (block, tile) ahead of their MFMAs
+// (A/B, C2 at H = 50, 5 interleaved rounds: K2 3.499 -> 3.370 ms, C2 5.160 ->
+// 5.025 ms, profiles/r06/c2/ab_encoder_pipe.txt)
+#ifndef PGP_ENC_PIPE
+#define PGP_ENC_PIPE 1
+#endif
+constexpr bool kEncPipe = PGP_ENC_PIPE != 0;
+// the fp32 GEMMs' A fragments likewise (A/B switch; measured within noise at
+// H = 50 (5.217 vs 5.206 ms) and H = 16 (fleet 1.8669 vs 1.8666 ms), 4
+// registers spilled at H = 50: off)
+#ifndef PGP_ENC_PIPE_F32
+#define PGP_ENC_PIPE_F32 0
+#endif
+constexpr bool kEncPipeF32 = PGP_ENC_PIPE_F32 != 0;
+
 // Split-bf16 feed-forward (tail-resident mode, H = 50): both layers' linear1
 // (K = d) and linear2 (K = 64) run as v_mfma_f32_16x16x32_bf16 over exact
 // three-part bf16 splits of both operands (the six products i + j <= 2, as K2b
@@ -203,11 +218,20 @@ PGP_DEV void gemm3_rows(f32x4 (&acc)[NMA][3], const float* A, const f32x4 (&Bx)[
                         float (&racc)[NR][3], const float* RW, int g) {
   static_assert(NM <= NMA, "accumulator tiles");
   prio_mfma();
+  // (kEncPipeF32) each A fragment read one (tile, group) ahead of its 12 MFMAs
+  f32x4 an = ld4(A + lane * 4);
 #pragma unroll
   for (int m = 0; m < NM; ++m)
 #pragma unroll
     for (int q4 = 0; q4 < KQ; ++q4) {
-      const f32x4 a = ld4(A + (m * KQ + q4) * 256 + lane * 4);
+      f32x4 a;
+      if constexpr (kEncPipeF32) {
+        a = an;
+        if (m * KQ + q4 + 1 < NM * KQ) an = ld4(A + (m * KQ + q4 + 1) * 256 + lane * 4);
+        __builtin_amdgcn_sched_barrier(0);
+      } else {
+        a = ld4(A + (m * KQ + q4) * 256 + lane * 4);
+      }
       f32x4 rw[NR];
       if (m == 0) {
 #pragma unroll
@@ -646,26 +670,57 @@ PGP_DEV void encoder_layer_tail(f32x4 (&X)[Geo<H>::MT_D][3], Ring<H, SPLIT>& rin
     const float* A2 = ring.cur + S::F1S * G::FQ;
 #pragma unroll
     for (int w = 0; w < 3; ++w) {
-      u32x4 xs[S::NBD][3];
-#pragma unroll
-      for (int b = 0; b < S::NBD; ++b) {
-        float v[8];
-        pair_tiles<G::MT_D>(X, b, w, v);
-        split8(v, xs[b]);
-      }
       f32x4 F[G::MT_F];
 #pragma unroll
       for (int c = 0; c < G::MT_F; ++c) F[c] = ld4(TL + G::TL_B1 + 16 * c + 4 * g);
-      prio_mfma();
+      if constexpr (kEncPipe) {
+        // block by block (one block's split X, 12 VGPRs, live at a time), the
+        // next (block, tile)'s planes read ahead of this one's MFMAs and pinned
+        // there (160 of the kernel's LDS reads were waited for right after
+        // issue); each F[c] takes its blocks in the same order as below
+        constexpr int QN = S::NBD * G::MT_F;
+        u32x4 wn[3];
+        planes_lds(A1, lane, wn);
 #pragma unroll
-      for (int b = 0; b < S::NBD; ++b)
+        for (int b = 0; b < S::NBD; ++b) {
+          u32x4 xb[3];
+          {
+            float v[8];
+            pair_tiles<G::MT_D>(X, b, w, v);
+            split8(v, xb);
+          }
+          prio_mfma();
 #pragma unroll
-        for (int c = 0; c < G::MT_F; ++c) {
-          u32x4 wp[3];
-          planes_lds(A1 + ((c * S::NBD + b) * 3) * 256, lane, wp);
-          F[c] = mfma_bf6(wp, xs[b], F[c]);
+          for (int c = 0; c < G::MT_F; ++c) {
+            u32x4 wp[3];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) wp[k] = wn[k];
+            const int q = b * G::MT_F + c + 1;
+            if (q < QN) planes_lds(A1 + (((q % G::MT_F) * S::NBD + q / G::MT_F) * 3) * 256, lane, wn);
+            __builtin_amdgcn_sched_barrier(0);
+            F[c] = mfma_bf6(wp, xb, F[c]);
+          }
+          prio_valu();
         }
-      prio_valu();
+      } else {
+        u32x4 xs[S::NBD][3];
+#pragma unroll
+        for (int b = 0; b < S::NBD; ++b) {
+          float v[8];
+          pair_tiles<G::MT_D>(X, b, w, v);
+          split8(v, xs[b]);
+        }
+        prio_mfma();
+#pragma unroll
+        for (int b = 0; b < S::NBD; ++b)
+#pragma unroll
+          for (int c = 0; c < G::MT_F; ++c) {
+            u32x4 wp[3];
+            planes_lds(A1 + ((c * S::NBD + b) * 3) * 256, lane, wp);
+            F[c] = mfma_bf6(wp, xs[b], F[c]);
+          }
+        prio_valu();
+      }
 #pragma unroll
       for (int c = 0; c < G::MT_F; ++c)
 #pragma unroll
@@ -681,27 +736,58 @@ PGP_DEV void encoder_layer_tail(f32x4 (&X)[Geo<H>::MT_D][3], Ring<H, SPLIT>& rin
 #pragma unroll
           for (int e = 0; e < 4; ++e) rf[n] = fmaf(rw[e], F[c][e], rf[n]);
         }
-      u32x4 hs[S::NBF][3];
+      if constexpr (kEncPipe) {
+        constexpr int QN = S::NBF * G::MT_X;
+        u32x4 wn[3];
+        planes_lds(A2, lane, wn);
 #pragma unroll
-      for (int b = 0; b < S::NBF; ++b) {
-        float v[8];
+        for (int b = 0; b < S::NBF; ++b) {
+          u32x4 hb[3];
+          {
+            float v[8];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          v[e] = F[2 * b][e];
-          v[4 + e] = F[2 * b + 1][e];
+            for (int e = 0; e < 4; ++e) {
+              v[e] = F[2 * b][e];
+              v[4 + e] = F[2 * b + 1][e];
+            }
+            split8(v, hb);
+          }
+          prio_mfma();
+#pragma unroll
+          for (int m = 0; m < G::MT_X; ++m) {
+            u32x4 wp[3];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) wp[k] = wn[k];
+            const int q = b * G::MT_X + m + 1;
+            if (q < QN) planes_lds(A2 + (((q % G::MT_X) * S::NBF + q / G::MT_X) * 3) * 256, lane, wn);
+            __builtin_amdgcn_sched_barrier(0);
+            acc[m][w] = mfma_bf6(wp, hb, acc[m][w]);
+          }
+          prio_valu();
         }
-        split8(v, hs[b]);
+      } else {
+        u32x4 hs[S::NBF][3];
+#pragma unroll
+        for (int b = 0; b < S::NBF; ++b) {
+          float v[8];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v[e] = F[2 * b][e];
+            v[4 + e] = F[2 * b + 1][e];
+          }
+          split8(v, hs[b]);
+        }
+        prio_mfma();
+#pragma unroll
+        for (int b = 0; b < S::NBF; ++b)
+#pragma unroll
+          for (int m = 0; m < G::MT_X; ++m) {
+            u32x4 wp[3];
+            planes_lds(A2 + ((m * S::NBF + b) * 3) * 256, lane, wp);
+            acc[m][w] = mfma_bf6(wp, hs[b], acc[m][w]);
+          }
+        prio_valu();
       }
-      prio_mfma();
-#pragma unroll
-      for (int b = 0; b < S::NBF; ++b)
-#pragma unroll
-        for (int m = 0; m < G::MT_X; ++m) {
-          u32x4 wp[3];
-          planes_lds(A2 + ((m * S::NBF + b) * 3) * 256, lane, wp);
-          acc[m][w] = mfma_bf6(wp, hs[b], acc[m][w]);
-        }
-      prio_valu();
       acc[G::MT_X][w][0] += xsum_rows<G::XR>(rf);  // row n's sum in lane group n
     }
   } else {

@@ -123,6 +123,18 @@ for step in "$@"; do
       PGP_DIST_BACKEND=gloo PGP_DEVICE=0 run dist2 600 python3 -u bench.py --gpus 2 --steps 20 --warmup 3 --no-cpu-baseline
       grep "^{" $OUT/dist2.out | tail -1 | cut -c1-400
       ;;
+    abencpipe)  # K2 split feed-forward planes pinned a (block, tile) ahead (variant encpipe)
+      run abep 900 python3 -u tools/ab_bench.py --rounds 5 --args "--steps 100 --warmup 5 --no-cpu-baseline" base= pipe=PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_encpipe.so
+      grep median $OUT/abep.out
+      python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); [print(k, [round(e['kernel_ms']['encoder'], 4) for e in v]) for k, v in d['extra'].items()]" $OUT/abep.out
+      ;;
+    abencf32)  # K2 fp32 GEMMs' A fragments one ahead (variant encf32): C2 (H=50) and fleet (H=16)
+      run abef 900 python3 -u tools/ab_bench.py --rounds 5 --args "--steps 100 --warmup 5 --no-cpu-baseline" base= f32pf=PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_encf32.so
+      grep median $OUT/abef.out
+      python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); [print(k, [round(e['kernel_ms']['encoder'], 4) for e in v]) for k, v in d['extra'].items()]" $OUT/abef.out
+      run abeff 900 python3 -u tools/ab_bench.py --rounds 4 --args "--config fleet --steps 50 --warmup 5 --no-cpu-baseline" base= f32pf=PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_encf32.so
+      grep median $OUT/abeff.out
+      ;;
     abenc)
       run abenc 900 python3 -u tools/ab_bench.py --rounds 4 --args "--steps 100 --warmup 5 --no-cpu-baseline" split= fp32enc=ARGS=--fp32-encoder
       grep median $OUT/abenc.out
