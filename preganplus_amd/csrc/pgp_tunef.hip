@@ -605,6 +605,12 @@ constexpr int kTfFwdWaves = 8;
 #define PGP_TF_FWD_PF 1
 #endif
 constexpr bool kTfFwdPF = PGP_TF_FWD_PF != 0;
+// the FFN backward's split GEMMs likewise (A/B, C3 H = 50, 5 interleaved rounds:
+// 1.0114 -> 1.0019 ms, no spills; profiles/r06/c3/ab_bff_pf.txt)
+#ifndef PGP_TF_BFF_PF
+#define PGP_TF_BFF_PF 1
+#endif
+constexpr bool kTfBffPF = PGP_TF_BFF_PF != 0;
 
 template <int H>
 __global__ __launch_bounds__(kTfFwdWaves * 64, 1) void tf_fwd_kernel(TfArgs a) {
@@ -948,7 +954,7 @@ __global__ __launch_bounds__(kTfWaves * 64, 1) void tf_bwd_ffn_kernel(TfArgs a) 
 #pragma unroll
           for (int w = 0; w < 3; ++w) Y1[t][w] = y1(Y1, t, w);
         init_bias<4>(Fh, par + Q::B1, g);
-        tf_gemm_any<F::SPLIT, 4, F::KS>(Fh, smz + L::W_F1, [&](int s, int w) { return Y1[s >> 2][w][s & 3]; }, lane,
+        tf_gemm_any<F::SPLIT, 4, F::KS, kTfBffPF>(Fh, smz + L::W_F1, [&](int s, int w) { return Y1[s >> 2][w][s & 3]; }, lane,
                                         [](int) {});
         init_bias<NT>(X2, par + Q::B2, g);
 #pragma unroll
@@ -965,7 +971,7 @@ __global__ __launch_bounds__(kTfWaves * 64, 1) void tf_bwd_ffn_kernel(TfArgs a) 
       TF_ST(2);
       {  // side work: dOut of the unit
         constexpr int NS = 3 * NT, NG = NT * F::KGF, PER = (NS + NG - 1) / NG;
-        tf_gemm_any<F::SPLIT, NT, 16>(X2, smz + L::W_F2, [&](int s, int w) { return Fh[s >> 2][w][s & 3]; }, lane,
+        tf_gemm_any<F::SPLIT, NT, 16, kTfBffPF>(X2, smz + L::W_F2, [&](int s, int w) { return Fh[s >> 2][w][s & 3]; }, lane,
                                       [&](int i) {
 #pragma unroll
                                         for (int k = 0; k < PER; ++k)
@@ -1000,7 +1006,7 @@ __global__ __launch_bounds__(kTfWaves * 64, 1) void tf_bwd_ffn_kernel(TfArgs a) 
         for (int w = 0; w < 3; ++w) dF[t][w] = zero4();
       {  // side work: norm1's x-hat, reloaded (L2): not held through the phases above
         constexpr int NS = 3 * NT, NG = 4 * F::KG, PER = (NS + NG - 1) / NG;
-        tf_gemm_any<F::SPLIT, 4, F::KS>(dF, smz + L::W_F2T, [&](int s, int w) { return dY[s >> 2][w][s & 3]; }, lane,
+        tf_gemm_any<F::SPLIT, 4, F::KS, kTfBffPF>(dF, smz + L::W_F2T, [&](int s, int w) { return dY[s >> 2][w][s & 3]; }, lane,
                                         [&](int i) {
 #pragma unroll
                                           for (int k = 0; k < PER; ++k)
@@ -1028,7 +1034,7 @@ __global__ __launch_bounds__(kTfWaves * 64, 1) void tf_bwd_ffn_kernel(TfArgs a) 
       }
       __builtin_amdgcn_sched_barrier(0);
       // dy1 = W1^T dF + dR2 (residual)
-      tf_gemm_any<F::SPLIT, NT, 16>(dY, smz + L::W_F1T, [&](int s, int w) { return dF[s >> 2][w][s & 3]; }, lane,
+      tf_gemm_any<F::SPLIT, NT, 16, kTfBffPF>(dY, smz + L::W_F1T, [&](int s, int w) { return dF[s >> 2][w][s & 3]; }, lane,
                                     [](int) {});
     }
     __builtin_amdgcn_sched_barrier(0);

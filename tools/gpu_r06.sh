@@ -135,6 +135,10 @@ for step in "$@"; do
       run abeff 900 python3 -u tools/ab_bench.py --rounds 4 --args "--config fleet --steps 50 --warmup 5 --no-cpu-baseline" base= f32pf=PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_encf32.so
       grep median $OUT/abeff.out
       ;;
+    abbff)  # FFN backward split GEMMs' planes one ahead (variant bffpf)
+      run abbff 900 python3 -u tools/ab_bench.py --rounds 5 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" base= bffpf=PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_bffpf.so
+      grep median $OUT/abbff.out
+      ;;
     abenc)
       run abenc 900 python3 -u tools/ab_bench.py --rounds 4 --args "--steps 100 --warmup 5 --no-cpu-baseline" split= fp32enc=ARGS=--fp32-encoder
       grep median $OUT/abenc.out
