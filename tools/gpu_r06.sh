@@ -139,6 +139,11 @@ for step in "$@"; do
       run abbff 900 python3 -u tools/ab_bench.py --rounds 5 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" base= bffpf=PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_bffpf.so
       grep median $OUT/abbff.out
       ;;
+    abtw)  # K3: two blocks of 16 windows per wave (default build) vs one (tw1)
+      run abtw 900 python3 -u tools/ab_bench.py --rounds 4 --args "--steps 100 --warmup 5 --no-cpu-baseline" tw2= tw1=PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_tw1.so
+      grep median $OUT/abtw.out
+      python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); [print(k, [round(e['kernel_ms']['gan'], 4) for e in v]) for k, v in d['extra'].items()]" $OUT/abtw.out
+      ;;
     abenc)
       run abenc 900 python3 -u tools/ab_bench.py --rounds 4 --args "--steps 100 --warmup 5 --no-cpu-baseline" split= fp32enc=ARGS=--fp32-encoder
       grep median $OUT/abenc.out
