@@ -38,6 +38,10 @@ constexpr int kSQP = 2;  // schedule pairs per ring chunk
 #define PGP_K3_OH 1
 #endif
 constexpr bool kK3OneHot = PGP_K3_OH != 0;  // phase 3 rebuilds one-hot rows from LDS (A/B: -DPGP_K3_OH=0)
+#ifndef PGP_K3_PF
+#define PGP_K3_PF 1
+#endif
+constexpr bool kK3PF = kK3OneHot && PGP_K3_PF != 0;  // one-hot containers: planes read a step ahead (A/B: -DPGP_K3_PF=0)
 
 template <int H>
 struct GanS {
@@ -146,12 +150,37 @@ PGP_DEV void pair8(const f32x4& a, const f32x4& b, float (&v)[8]) {
     v[4 + e] = b[e];
   }
 }
+// The planes' reads have landed here: the wait for them goes before whatever
+// follows (the next triple's reads), not after it with a drain of those too
+// (the compiler counts these waits as lgkmcnt(0) here)
+PGP_DEV void planes_ready(const u32x4 (&w)[3]) { asm volatile("" ::"v"(w[0]), "v"(w[1]), "v"(w[2])); }
 PGP_DEV void planes_at(const float* F, int lane, u32x4 (&w)[3]) {
 #pragma unroll
   for (int k = 0; k < 3; ++k) w[k] = *reinterpret_cast<const u32x4*>(F + k * 256 + lane * 4);
 }
 
+// The ring's DMA, issued where the compiler does not see it: a pending
+// global_load_lds (a VMEM op that writes) makes the compiler's wait for any
+// older load a full drain (vmcnt(0)), so each chunk's first use of its
+// schedule values also waited for the DMA and the next chunk's prefetch just
+// issued.  Its completion is waited for explicitly before every barrier
+// (k3_sync); the compiler's own waits stay correct, only stricter, with these
+// ops in flight (loads complete in order).
+PGP_DEV void k3_dma(const float* __restrict__ src, float* dst, int ngroups, int wv, int nwaves, int lane) {
+  for (int g = wv; g < ngroups; g += nwaves) {
+    const float* base = src + (long)g * 256;  // wave-uniform: the SGPR-base form, a 32-bit lane offset
+    const unsigned off = (unsigned)lane * 16u;
+    const unsigned m = (unsigned)(unsigned long)((__attribute__((address_space(3))) float*)(dst + g * 256));
+    asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(off), "s"(base), "s"(m) : "memory", "m0");
+  }
+}
+PGP_DEV void k3_sync() {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+}
+
 __device__ __attribute__((aligned(8))) float k3s_zero_pair[2];  // never written
+__device__ __attribute__((aligned(16))) float k3s_zero4[4];      // never written
 
 template <int H, int NW>
 __global__ __launch_bounds__(NW * 64) void gan_split_kernel(FwdArgs a) {
@@ -187,21 +216,21 @@ __global__ __launch_bounds__(NW * 64) void gan_split_kernel(FwdArgs a) {
     const float* src;
     int ng;
     S::chunk(0, a.ganb, &src, &ng);
-    dma_groups(src, cur, ng, wv, NW, lane);
+    k3_dma(src, cur, ng, wv, NW, lane);
   }
   auto issue = [&]() {
     if (next < S::NCHUNK) {
       const float* src;
       int ng;
       S::chunk(next, a.ganb, &src, &ng);
-      dma_groups(src, nxt, ng, wv, NW, lane);
+      k3_dma(src, nxt, ng, wv, NW, lane);
       if (next > S::NQC)  // a container chunk: its Gen2 biases after its planes
-        dma_groups(gt + G::G_B2 + (long)(next - 1 - S::NQC) * S::CPC * S::BIAS_F, nxt + ng * 256, 1,
+        k3_dma(gt + G::G_B2 + (long)(next - 1 - S::NQC) * S::CPC * S::BIAS_F, nxt + ng * 256, 1,
                    (wv + ng) % NW, NW, lane);
     }
   };
   auto advance = [&]() {
-    __syncthreads();
+    k3_sync();
     float* t = cur;
     cur = nxt;
     nxt = t;
@@ -216,7 +245,7 @@ __global__ __launch_bounds__(NW * 64) void gan_split_kernel(FwdArgs a) {
     hd[mt] = ld4(gt + G::G_BD1 + 16 * mt + 4 * g);
   }
   const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
-  __syncthreads();
+  k3_sync();
   issue();
 
   // ---- phase 1: Gen1, embedding columns ----
@@ -241,7 +270,10 @@ __global__ __launch_bounds__(NW * 64) void gan_split_kernel(FwdArgs a) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int idx = 16 * (2 * p + h) + 4 * g;
-      q[h] = (valid && p < S::NPS && idx < G::H2) ? ld4(sw + idx) : zero4;
+      // unconditional: a lane past the row reads zeros; a load behind a branch
+      // made the compiler wait for ALL loads at the next chunk's first use
+      // (vmcnt(0): the just-issued prefetch too, one HBM latency per chunk)
+      q[h] = ld4((valid && p < S::NPS && idx < G::H2) ? sw + idx : k3s_zero4);
     }
   };
   f32x4 bq[kSQP][2];
@@ -316,6 +348,10 @@ __global__ __launch_bounds__(NW * 64) void gan_split_kernel(FwdArgs a) {
         }
       }
     }
+    // the next chunk's values are taken here, before the barrier (which drains
+    // them anyway), so that the compiler's wait for them precedes the next DMA
+#pragma unroll
+    for (int i = 0; i < kSQP; ++i) asm volatile("" ::"v"(bn[i][0]), "v"(bn[i][1]));
     advance();
 #pragma unroll
     for (int i = 0; i < kSQP; ++i) {
@@ -358,8 +394,105 @@ __global__ __launch_bounds__(NW * 64) void gan_split_kernel(FwdArgs a) {
       if (blk < nblk && blk * 16 + (i & 15) < a.B && oh[i] < 0) bad = true;
     ohw = __builtin_amdgcn_ballot_w64(bad) == 0ull;
   }
+  // cross-group first-argmaxes of a container row, and its two targets
+  auto k3_targets = [&](int c, float bn_v, int bn_i, float bs_v, int bs_i) {
+#pragma unroll
+    for (int off = 16; off <= 32; off <<= 1) {
+      const float ov = __shfl_xor(bn_v, off), os = __shfl_xor(bs_v, off);
+      const int oi = __shfl_xor(bn_i, off), osi = __shfl_xor(bs_i, off);
+      if (ov > bn_v || (ov == bn_v && oi < bn_i)) {
+        bn_v = ov;
+        bn_i = oi;
+      }
+      if (os > bs_v || (os == bs_v && osi < bs_i)) {
+        bs_v = os;
+        bs_i = osi;
+      }
+    }
+    if (g == 0) {
+      tg[c * 16 + j] = (signed char)bn_i;
+      tg[(G::C + c) * 16 + j] = (signed char)bs_i;
+    }
+  };
+  // the 2 MT_N Gen2 and MT_G NPN Disc1 plane triples of a container, in use order
+  constexpr int NF = 2 * G::MT_N + S::NPN * G::MT_G;
+  auto pl_addr = [&](const float* cw, int f) -> const float* {
+    if (f < 2 * G::MT_N) return cw + (((f % G::MT_N) * 2 + f / G::MT_N) * 3) * 256;  // Gen2 (pair f / MT_N, tile f % MT_N)
+    const int q = f - 2 * G::MT_N;
+    return cw + (S::FC2 + ((q % G::MT_G) * S::NPN + q / G::MT_G) * 3) * 256;  // Disc1 (pair q / MT_G, tile q % MT_G)
+  };
   for (int c = 0; c < G::C; ++c) {
     const float* cw = cur;  // CPC = 1: this container's planes
+    if (kK3PF && ohw) {
+      // one-hot rows: the row is its 1.0's position (no registers for it), and
+      // each plane triple is read one step ahead of the MFMAs that use it,
+      // pinned there (the compiler otherwise reads it right before them and
+      // waits: 16 exposed LDS round trips per container)
+      const int hc = oh[c * 16 + j];  // -1 for a window past B: a zero row, as load_row gives
+      u32x4 wb[2][3];
+      planes_at(pl_addr(cw, 0), lane, wb[0]);
+      f32x4 ns[G::MT_N];
+      const float* bias = cur + S::FC * 256;
+#pragma unroll
+      for (int t = 0; t < G::MT_N; ++t) ns[t] = ld4(bias + 16 * t + 4 * g);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int p = 0; p < 2; ++p)
+#pragma unroll
+        for (int t = 0; t < G::MT_N; ++t) {
+          const int f = p * G::MT_N + t;
+          __builtin_amdgcn_sched_barrier(0);
+          planes_ready(wb[f & 1]);
+          planes_at(pl_addr(cw, f + 1), lane, wb[(f + 1) & 1]);
+          __builtin_amdgcn_sched_barrier(0);
+          ns[t] = mfma_bf6(wb[f & 1], hx[p], ns[t]);
+        }
+      __builtin_amdgcn_s_setprio(0);
+      float bn_v = -INFINITY, bs_v = -INFINITY;
+      int bn_i = 0, bs_i = 0;
+#pragma unroll
+      for (int t = 0; t < G::MT_N; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int hh = 16 * t + 4 * g + r;
+          if (hh < H) {
+            const float s0 = hh == hc ? 1.f : 0.f;
+            const float nv = s0 + 4.0f * tanh_fast(ns[t][r]);
+            ns[t][r] = nv;
+            if (nv > bn_v) {  // strict: first maximum wins (list.index(max(...)))
+              bn_v = nv;
+              bn_i = hh;
+            }
+            if (s0 > bs_v) {
+              bs_v = s0;
+              bs_i = hh;
+            }
+          } else {
+            ns[t][r] = 0.f;
+          }
+        }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int p = 0; p < S::NPN; ++p) {
+        float v[8];
+        pair8(ns[2 * p], 2 * p + 1 < G::MT_N ? ns[2 * p + 1] : zero4, v);
+        u32x4 x[3];
+        split8(v, x);
+#pragma unroll
+        for (int mt = 0; mt < G::MT_G; ++mt) {
+          const int f = 2 * G::MT_N + p * G::MT_G + mt;
+          __builtin_amdgcn_sched_barrier(0);
+          planes_ready(wb[f & 1]);
+          if (f + 1 < NF) planes_at(pl_addr(cw, f + 1), lane, wb[(f + 1) & 1]);
+          __builtin_amdgcn_sched_barrier(0);
+          hd[mt] = mfma_bf6(wb[f & 1], x, hd[mt]);
+        }
+      }
+      __builtin_amdgcn_s_setprio(0);
+      k3_targets(c, bn_v, bn_i, bs_v, bs_i);
+      advance();
+      continue;
+    }
     // this container's schedule row, requested before Gen2's MFMAs (which
     // cover its latency; a row prefetched a container ahead spilled at the
     // 128-register budget of 4 waves per SIMD)
@@ -427,24 +560,7 @@ __global__ __launch_bounds__(NW * 64) void gan_split_kernel(FwdArgs a) {
       }
     }
     __builtin_amdgcn_s_setprio(0);
-    // cross-group argmaxes and the targets
-#pragma unroll
-    for (int off = 16; off <= 32; off <<= 1) {
-      const float ov = __shfl_xor(bn_v, off), os = __shfl_xor(bs_v, off);
-      const int oi = __shfl_xor(bn_i, off), osi = __shfl_xor(bs_i, off);
-      if (ov > bn_v || (ov == bn_v && oi < bn_i)) {
-        bn_v = ov;
-        bn_i = oi;
-      }
-      if (os > bs_v || (os == bs_v && osi < bs_i)) {
-        bs_v = os;
-        bs_i = osi;
-      }
-    }
-    if (g == 0) {
-      tg[c * 16 + j] = (signed char)bn_i;
-      tg[(G::C + c) * 16 + j] = (signed char)bs_i;
-    }
+    k3_targets(c, bn_v, bn_i, bs_v, bs_i);
     advance();
   }
 

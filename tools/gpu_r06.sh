@@ -144,6 +144,13 @@ for step in "$@"; do
       grep median $OUT/abtw.out
       python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); [print(k, [round(e['kernel_ms']['gan'], 4) for e in v]) for k, v in d['extra'].items()]" $OUT/abtw.out
       ;;
+    abk3pf)  # K3 one-hot containers: planes read a step ahead (default build) vs not (pf0); C2 at H=50 and H=16
+      run abk3 900 python3 -u tools/ab_bench.py --rounds 4 --args "--steps 100 --warmup 5 --no-cpu-baseline" pf= pf0=PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_pf0.so
+      grep median $OUT/abk3.out
+      python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); [print(k, [round(e['kernel_ms']['gan'], 4) for e in v]) for k, v in d['extra'].items()]" $OUT/abk3.out
+      run abk316 900 python3 -u tools/ab_bench.py --rounds 3 --args "--hosts 16 --steps 100 --warmup 5 --no-cpu-baseline" pf= pf0=PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_pf0.so
+      python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); [print(k, [round(e['kernel_ms']['gan'], 4) for e in v]) for k, v in d['extra'].items()]" $OUT/abk316.out
+      ;;
     abenc)
       run abenc 900 python3 -u tools/ab_bench.py --rounds 4 --args "--steps 100 --warmup 5 --no-cpu-baseline" split= fp32enc=ARGS=--fp32-encoder
       grep median $OUT/abenc.out
