@@ -151,6 +151,12 @@ for step in "$@"; do
       run abk316 900 python3 -u tools/ab_bench.py --rounds 3 --args "--hosts 16 --steps 100 --warmup 5 --no-cpu-baseline" pf= pf0=PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_pf0.so
       python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); [print(k, [round(e['kernel_ms']['gan'], 4) for e in v]) for k, v in d['extra'].items()]" $OUT/abk316.out
       ;;
+    abtouch)  # C3: prefetched unit inputs taken before the unit's stores (default build) vs not (touch0)
+      run abtouch 900 python3 -u tools/ab_bench.py --rounds 4 --args "--config tune --hosts 50 --steps 50 --warmup 5 --no-cpu-baseline" touch= touch0=PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_touch0.so
+      grep median $OUT/abtouch.out
+      run abtouch16 900 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 16 --steps 100 --warmup 10 --no-cpu-baseline" touch= touch0=PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_touch0.so
+      grep median $OUT/abtouch16.out
+      ;;
     abenc)
       run abenc 900 python3 -u tools/ab_bench.py --rounds 4 --args "--steps 100 --warmup 5 --no-cpu-baseline" split= fp32enc=ARGS=--fp32-encoder
       grep median $OUT/abenc.out
