@@ -166,6 +166,10 @@ PGP_DEV f32x4 mfma_bf(u32x4 a, u32x4 b, f32x4 c) {
                                                  0, 0);
 }
 // w . x over one 32-k block as the six products with i + j <= 2, smallest first
+// A plane triple's reads have landed here: the compiler's wait for them goes
+// before whatever follows (the next triple's reads), not after it with a
+// drain of those too (its LDS waits in these loops are lgkmcnt(0))
+PGP_DEV void planes_ready(const u32x4 (&w)[3]) { asm volatile("" ::"v"(w[0]), "v"(w[1]), "v"(w[2])); }
 PGP_DEV f32x4 mfma_bf6(const u32x4 (&w)[3], const u32x4 (&x)[3], f32x4 c) {
   c = mfma_bf(w[2], x[0], c);
   c = mfma_bf(w[1], x[1], c);

@@ -150,10 +150,6 @@ PGP_DEV void pair8(const f32x4& a, const f32x4& b, float (&v)[8]) {
     v[4 + e] = b[e];
   }
 }
-// The planes' reads have landed here: the wait for them goes before whatever
-// follows (the next triple's reads), not after it with a drain of those too
-// (the compiler counts these waits as lgkmcnt(0) here)
-PGP_DEV void planes_ready(const u32x4 (&w)[3]) { asm volatile("" ::"v"(w[0]), "v"(w[1]), "v"(w[2])); }
 PGP_DEV void planes_at(const float* F, int lane, u32x4 (&w)[3]) {
 #pragma unroll
   for (int k = 0; k < 3; ++k) w[k] = *reinterpret_cast<const u32x4*>(F + k * 256 + lane * 4);

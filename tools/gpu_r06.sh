@@ -157,6 +157,11 @@ for step in "$@"; do
       run abtouch16 900 python3 -u tools/ab_bench.py --rounds 3 --args "--config tune --hosts 16 --steps 100 --warmup 10 --no-cpu-baseline" touch= touch0=PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_touch0.so
       grep median $OUT/abtouch16.out
       ;;
+    abdecready)  # K2b: each tile's planes waited for before the next tile's reads (default build) vs not (rd0); depth 2 (dp2)
+      run abdr 900 python3 -u tools/ab_bench.py --rounds 4 --args "--steps 100 --warmup 5 --no-cpu-baseline" ready= rd0=PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_rd0.so dp2=PGP_LIB=$GRAFT_REPO_ROOT/preganplus_amd/_lib/var/libpreganplus_dp2.so
+      grep median $OUT/abdr.out
+      python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); [print(k, [round(e['kernel_ms']['decoder'], 4) for e in v]) for k, v in d['extra'].items()]" $OUT/abdr.out
+      ;;
     abenc)
       run abenc 900 python3 -u tools/ab_bench.py --rounds 4 --args "--steps 100 --warmup 5 --no-cpu-baseline" split= fp32enc=ARGS=--fp32-encoder
       grep median $OUT/abenc.out
